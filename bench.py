@@ -1,0 +1,199 @@
+#!/usr/bin/env python3
+"""Benchmark: shuffled GB/s (partition+exchange) for BASELINE.json's workload.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]            (N=1 by default)
+  python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
+
+A step is one pass of the hot path over one batch: every rank partitions its own batch of
+16 B records resident in HBM (K1+K2 histogram, K3 decoupled-look-back scan, K4 stable
+scatter) and, for N > 1, pushes it to the reducer owners (counts all-gather +
+ncclAllToAllv over xGMI + K5 regroup).  Weak scaling: 2^28 records per GPU (config C1 at
+N=1; config C2's 2^31 total at N=8).  value = 16 B x records of all ranks / max-rank time.
+
+Also reported (rank 0): the roofline of the dominant kernel (K4 scatter) from HIP events
+on the engine's compute stream over the timed region, the stage breakdown, and the CPU
+baseline (the oracle's multi-threaded C restatement, timed on this host on a bounded
+sample of the same workload).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "shuffled GB/s (partition+exchange) at 1/2/4/8 GPUs; % of HBM/xGMI roofline"
+HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
+ALGO_BYTES_PER_REC = 32    # 16 B read + 16 B write per record
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--records", type=int, default=1 << 28, help="records per GPU")
+    ap.add_argument("--partitions", type=int, default=1024)
+    ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
+    ap.add_argument("--seed", type=int, default=0x5EEDC0DE)
+    ap.add_argument("--num-chunks", type=int, default=0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(args, n_total_hint):
+    """Oracle (C restatement, pthreads) on a bounded sample of the same workload."""
+    import numpy as np
+
+    import oracle
+
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        cores = os.cpu_count() or 1
+    cores = max(1, min(cores, 16))  # the GPU box's CPU share is 16
+    n = 1 << 24
+    recs = oracle.gen_uniform16(n, args.seed)
+    oracle.map_write(recs, args.partitions, nthreads=cores)  # warm-up (page faults)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        oracle.map_write(recs, args.partitions, nthreads=cores)
+        reps += 1
+        if time.perf_counter() - t0 >= args.cpu_baseline_seconds:
+            break
+    dt = time.perf_counter() - t0
+    del recs
+    return {"value": round(16.0 * n * reps / dt / 1e9, 3), "unit": "GB/s", "cores": cores, "kind": "port",
+            "sample": f"{reps} x map-side write of {n} uniform 16 B records, R={args.partitions} "
+                      f"(oracle/shuffle_oracle.c orc_map_write, {cores} threads, {dt:.1f} s)"}
+
+
+def load_traffic(config_key):
+    """HBM bytes per K4 launch from the committed rocprofv3 PMC summary (or None)."""
+    path = os.path.join(ROOT, "profiles", "pmc_scatter.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(config_key)
+        return None if e is None else e.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    import numpy as np
+    import torch
+
+    import sparkucx_amd as sgx
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local_rank)
+
+    n, R = args.records, args.partitions
+    eng = sgx.ShuffleEngine(device=local_rank, num_chunks=args.num_chunks)
+    if world > 1:
+        uid = [sgx.get_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(world, rank, uid[0])
+    buf = eng.alloc(n * 16)
+    if args.dist == "uniform":
+        eng.gen_uniform16(buf, n, args.seed + rank, value_base=rank * n)
+    else:
+        ranks = np.arange(1, (1 << 24) + 1, dtype=np.float64)
+        cdf = np.cumsum(ranks ** -1.1)
+        cdf /= cdf[-1]
+        eng.gen_zipf16(buf, n, args.seed + rank, cdf, value_base=rank * n)
+    sid = 1
+    eng.register_shuffle(sid, R)
+
+    def step(k):
+        mid = (k & 1) * world + rank  # two alternating map slots per rank
+        if world > 1:
+            eng.write_map(sid, mid, buf, n, 16)
+            eng.exchange(sid, mid)
+        else:
+            eng.write_map(sid, mid, buf, n, 16)
+
+    def barrier():
+        if dist is not None:
+            dist.barrier()
+        eng.sync()
+        torch.cuda.synchronize()
+
+    for k in range(args.warmup):
+        step(k)
+    barrier()
+    eng.stats_reset()
+    barrier()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    st = eng.stats()
+
+    verified = None
+    if not args.no_verify:
+        lens = eng.map_lengths(sid, rank, R)
+        verified = bool(lens.sum() == 16 * n)
+
+    if rank == 0:
+        ms_per_step = dt * 1e3 / args.steps
+        total_bytes = 16.0 * n * world * args.steps
+        value = total_bytes / dt / 1e9
+        sc_ms = st.ms["scatter"] / max(1, st.count["scatter"])
+        achieved = ALGO_BYTES_PER_REC * n / (sc_ms * 1e-3) / 1e9
+        traffic = load_traffic(f"uniform_n{n}_R{R}" if args.dist == "uniform" else f"zipf_n{n}_R{R}")
+        out = {
+            "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
+            "data": f"synthetic {args.dist} (Long,Long) 16 B records, splitmix64 seed {args.seed:#x}+rank",
+            "config": {"workload": "C1: 2^28 x 16 B, HashPartitioner R=1024, partition+scatter per GPU"
+                       if world == 1 else
+                       f"C2: {n} x 16 B per GPU ({n * world} total), R={R}, partition + RCCL alltoallv",
+                       "records_per_gpu": n, "partitions": R, "record_bytes": 16,
+                       "parallelism": f"dp{world} (map shards per GPU, reducers owned floor(r*P/R))"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                         "kernel": "k_scatter16 (K4)", "algo_bytes_per_record": ALGO_BYTES_PER_REC},
+            "stages_ms_per_step": {k: round(v / max(1, st.count[k]), 4) for k, v in st.ms.items() if st.count[k]},
+            "map_side_GBs_hist_scan_scatter": round(16.0 * n / ((st.ms["hist"] + st.ms["scan"] + st.ms["scatter"])
+                                                             / max(1, st.count["scatter"]) * 1e-3) / 1e9, 1),
+            "verified_lengths_sum": verified,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(args, n)
+        elif world == 1:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    eng.unregister_shuffle(sid)
+    buf.free()
+    eng.close()
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,174 @@
+/*
+ * sgx.h — C ABI of the MI355X-native shuffle engine (libsgx.so).
+ *
+ * This is the drop-in boundary behind SparkUCX's plugin API (ofirfarjun7/sparkucx,
+ * Spark 3.0 profile).  Plain C types only: no torch, no HIP types in signatures.  Each
+ * entry point names the reference interface it replaces (file:line relative to
+ * /root/reference/src/main/scala/org/apache/spark/).  The JNI glue a maintainer adds on
+ * the Scala side is shown in INTEGRATION.md.
+ *
+ * Conventions (mirror ShuffleTransport.scala:49-51,71 and the JVM exception mapping):
+ *   - every int-returning call returns SGX_OK (0) or a negative SGX_ERR_* code;
+ *     negative codes map to OperationStatus.FAILURE / a thrown exception on the JVM side;
+ *   - sgx_last_error() returns a thread-local message for the last failure on this thread;
+ *   - buffers passed in are caller-owned; map outputs and received blocks are engine-owned
+ *     and live in HBM until sgx_unregister_shuffle / sgx_destroy;
+ *   - one engine per GPU (= per executor); calls on one engine are serialised internally.
+ */
+#ifndef SGX_H
+#define SGX_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SGX_ABI_VERSION 1
+
+enum sgx_status {
+    SGX_OK = 0,
+    SGX_ERR_INVALID = -1,   /* IllegalArgumentException: bad argument / out-of-order use   */
+    SGX_ERR_STATE = -2,     /* IllegalStateException: not registered / not initialised     */
+    SGX_ERR_HIP = -3,       /* HIP runtime failure (RuntimeException)                      */
+    SGX_ERR_COMM = -4,      /* RCCL failure (TransportError)                               */
+    SGX_ERR_IO = -5,        /* IOException: index/data file commit                         */
+    SGX_ERR_NOMEM = -6,     /* device or host allocation failed                            */
+    SGX_ERR_NOT_FOUND = -7, /* block not registered (UcxShuffleTransport.scala:229-269)    */
+    SGX_ERR_UNSUPPORTED = -8,
+    SGX_ERR_TIMEOUT = -9    /* a bounded device spin gave up                               */
+};
+
+/* Partitioner kinds (the ShuffleDependency's partitioner). */
+enum sgx_partitioner {
+    SGX_PART_HASH = 0,          /* HashPartitioner: nonNegativeMod(Long.hashCode(k), R)    */
+    SGX_PART_RANGE_I64 = 1,     /* RangePartitioner over signed-long keys                  */
+    SGX_PART_RANGE_BYTES10 = 2  /* RangePartitioner over 10-byte unsigned keys (TeraSort)  */
+};
+
+/* Where a caller buffer lives. */
+enum sgx_mem_kind { SGX_MEM_HOST = 0, SGX_MEM_DEVICE = 1 };
+
+typedef struct sgx_engine sgx_engine;
+
+typedef struct sgx_config {
+    int32_t device;          /* HIP device ordinal for this executor                     */
+    int32_t num_chunks;      /* map-side work chunks per batch (0 = one per CU)           */
+    int32_t flags;           /* reserved, 0                                               */
+    int32_t reserved;
+} sgx_config;
+
+/* ---- engine lifetime: replaces CommonUcxShuffleManager.startUcxTransport
+ *      (shuffle/ucx/CommonUcxShuffleManager.scala:67-100) and stop() (:111-124) ---- */
+int sgx_create(const sgx_config *cfg, sgx_engine **out);
+void sgx_destroy(sgx_engine *e);
+const char *sgx_last_error(void);
+int32_t sgx_abi_version(void);
+
+/* ---- registerShuffle: SortShuffleManager.registerShuffle inherited at
+ *      shuffle/ucx/CommonUcxShuffleManager.scala:25; the partitioner of the dependency.
+ *      bounds: nbounds sorted keys (int64 for RANGE_I64, 10-byte rows for RANGE_BYTES10);
+ *      num_partitions must be nbounds+1 for range kinds. record_bytes: 16 (Long,Long) or
+ *      100 (TeraSort); the key is the first 8 (hash / range_i64) or 10 bytes. ---- */
+int sgx_register_shuffle(sgx_engine *e, int32_t shuffle_id, int32_t num_partitions,
+                         int32_t partitioner_kind, const void *bounds, int64_t nbounds,
+                         int32_t ascending, int32_t record_bytes);
+/* unregisterShuffle: CommonUcxShuffleManager.scala:103-106 -> removeShuffle
+ * (CommonUcxShuffleBlockResolver.scala:63-71). Frees the shuffle's HBM. */
+int sgx_unregister_shuffle(sgx_engine *e, int32_t shuffle_id);
+
+/* ---- getWriter(...).write(records) + ShuffleMapOutputWriter.commitAllPartitions
+ *      (spark_3_0/UcxShuffleManager.scala:32-53; ucx/NvkvShuffleMapOutputWriter.scala:
+ *      105-148): partition ids + histogram + scan + stable scatter on the GPU.  The map
+ *      output stays in HBM, engine-owned.  out_partition_lengths: caller-owned int64[R],
+ *      in BYTES (Spark's long[] lengths).  If NULL the call is asynchronous: lengths are
+ *      available from sgx_map_lengths after sgx_sync. ---- */
+int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records,
+                  int64_t nrecords, int32_t record_bytes, int32_t mem_kind,
+                  int64_t *out_partition_lengths);
+int sgx_map_lengths(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *out_lengths);
+/* Device pointer + byte size of a map output (partition-contiguous data). */
+int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, void **out_dev_ptr,
+                 int64_t *out_bytes);
+
+/* ---- IndexShuffleBlockResolver.writeIndexFileAndCommit (IndexShuffleBlockResolver.scala:
+ *      161-217): writes the map output as data file + index file ((R+1) big-endian int64
+ *      offsets), atomically via tmp+rename; an existing valid attempt wins and its lengths
+ *      are returned in out_lengths (may be NULL). ---- */
+int sgx_write_index(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const char *index_path,
+                    const char *data_path, int64_t *out_lengths);
+/* Host-only helpers (no GPU needed): checkIndexAndDataFile (:110-149) and the
+ * getBlockData offset lookup (:219-262). */
+int sgx_check_index_and_data(const char *index_path, const char *data_path, int32_t blocks,
+                             int64_t *out_lengths);
+int sgx_index_block_range(const char *index_path, int32_t start_reduce, int32_t end_reduce,
+                          int64_t *out_offset, int64_t *out_length);
+
+/* ---- reduce-side exchange: replaces the per-block UCX AM fetch path
+ *      (ucx/UcxWorkerWrapper.scala:96-186, spark_3_0/UcxShuffleClient.scala:17-91) with one
+ *      counts all-gather + ncclAllToAllv over xGMI + a regroup kernel.  Call
+ *      sgx_comm_init once per engine (the unique id travels over the host's control plane,
+ *      which replaces the ExecutorAdded/IntroduceAllExecutors RPC in the rpc/ package). ---- */
+int sgx_get_unique_id(uint8_t out_id[128]);
+int sgx_comm_init(sgx_engine *e, int32_t nranks, int32_t rank, const uint8_t id[128]);
+int sgx_comm_size(sgx_engine *e, int32_t *nranks, int32_t *rank);
+/* Push map `map_id` of `shuffle_id` to the reducer owners (reducer r lives on rank
+ * floor(r*P/R)); every rank calls it collectively with its own map.  Asynchronous on the
+ * engine's exchange stream; completes at sgx_sync. */
+int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id);
+
+/* ---- ShuffleTransport.fetchBlocksByBlockIds (ucx/ShuffleTransport.scala:154-156) /
+ *      BlockStoreClient.fetchBlocks (spark_3_0/UcxShuffleClient.scala:49-91): copy blocks
+ *      (map_ids[i], reduce_ids[i]) back to back into the caller-owned dst (dst_mem_kind).
+ *      out_lengths[i] = bytes of block i.  Blocks come from local map outputs or from data
+ *      received by sgx_exchange. Fails with SGX_ERR_NOT_FOUND for an unknown block and
+ *      SGX_ERR_INVALID if dst_cap is too small (nothing partial is reported as success). */
+int sgx_fetch_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids,
+                     const int32_t *reduce_ids, int64_t n, void *dst, int64_t dst_cap,
+                     int32_t dst_mem_kind, int64_t *out_lengths);
+
+/* ShuffleTransport.progress (ShuffleTransport.scala:158-165): non-blocking; returns 1 when
+ * all submitted work is complete, 0 while some is in flight. sgx_sync blocks until done. */
+int sgx_progress(sgx_engine *e);
+int sgx_sync(sgx_engine *e);
+
+/* ---- measurement: HIP-event times of the last write_map / exchange stages, and
+ *      accumulated per-stage sums since the last reset (index = enum sgx_stage). ---- */
+enum sgx_stage { SGX_STAGE_HIST = 0, SGX_STAGE_SCAN = 1, SGX_STAGE_SCATTER = 2,
+                 SGX_STAGE_ALLGATHER = 3, SGX_STAGE_ALLTOALL = 4, SGX_STAGE_REGROUP = 5,
+                 SGX_NUM_STAGES = 6 };
+int sgx_stats_reset(sgx_engine *e);
+/* out_ms[SGX_NUM_STAGES] summed milliseconds, out_count[SGX_NUM_STAGES] launches. */
+int sgx_stats_get(sgx_engine *e, double *out_ms, int64_t *out_count);
+
+/* ---- pure-host exchange planning (exported for tests of the multi-GPU logic) ----
+ * lengths_all: [P][R] per-rank partition lengths in bytes.  Writes, for `rank`:
+ * send_counts/send_displs[P] and recv_counts/recv_displs[P] in bytes, and the regroup
+ * copy list (src offset in the receive buffer, dst offset in the per-reducer output,
+ * bytes), ordered by reducer then source rank; *n_items in: capacity, out: count.
+ * item_bytes: max bytes per copy item (0 = unlimited). */
+int sgx_plan_exchange(const int64_t *lengths_all, int32_t P, int32_t R, int32_t rank,
+                      int64_t item_bytes, int64_t *send_counts, int64_t *send_displs,
+                      int64_t *recv_counts, int64_t *recv_displs, int64_t *items,
+                      int64_t *n_items);
+/* Apply a regroup copy list (items[n][3] host array, as produced by sgx_plan_exchange)
+ * from src_dev to dst_dev with the K5 kernel; synchronous. */
+int sgx_copy_items(sgx_engine *e, const void *src_dev, void *dst_dev, const int64_t *items,
+                   int64_t n_items, int32_t align);
+/* Reducer ownership: floor(r * P / R). */
+int32_t sgx_reducer_owner(int32_t reduce_id, int32_t num_partitions, int32_t nranks);
+
+/* ---- synthetic input generators (bench/test plumbing; the same definitions as the
+ *      oracle's). dst is device memory. ---- */
+int sgx_gen_uniform16(sgx_engine *e, void *dst_dev, int64_t n, uint64_t seed, int64_t value_base);
+int sgx_gen_zipf16(sgx_engine *e, void *dst_dev, int64_t n, uint64_t seed, int64_t value_base,
+                   const double *cdf_host, int64_t K);
+int sgx_gen_terasort100(sgx_engine *e, void *dst_dev, int64_t n, uint64_t seed, int64_t index_base);
+/* Device memory helpers for hosts without their own allocator (bench/tests). */
+int sgx_device_alloc(sgx_engine *e, int64_t bytes, void **out);
+int sgx_device_free(sgx_engine *e, void *p);
+int sgx_memcpy(sgx_engine *e, void *dst, const void *src, int64_t bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SGX_H */

@@ -1,0 +1,165 @@
+"""CPU oracle for the sparkucx_amd shuffle hot path.
+
+TEST INFRASTRUCTURE ONLY: ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg may import this package, and only as the checker (or, for the
+baseline, as the timed CPU restatement).  The product package ``sparkucx_amd`` never
+imports it and has no CPU fallback.
+
+Two independent restatements of Spark 3.0.1's map-side shuffle semantics live here:
+``spark_semantics.py`` (pure Python, small cases, fixture generation) and
+``shuffle_oracle.c`` (C99, wrapped below via ctypes; fast and multi-threaded).
+Parity is pinned by SURVEY.md §8(c)'s known-answer tests (the reference has no tests of
+its own).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+PART_HASH, PART_RANGE_I64, PART_RANGE_BYTES10 = 0, 1, 2
+
+
+def build() -> str:
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return _LIB_PATH
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        i32, i64, u64, vp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p
+        L.orc_java_long_hash.argtypes = [i64]
+        L.orc_java_long_hash.restype = i32
+        L.orc_non_negative_mod.argtypes = [i32, i32]
+        L.orc_non_negative_mod.restype = i32
+        L.orc_hash_partition.argtypes = [i64, i32]
+        L.orc_hash_partition.restype = i32
+        L.orc_range_partition_i64.argtypes = [i64, vp, i32, i32]
+        L.orc_range_partition_i64.restype = i32
+        L.orc_range_partition_bytes.argtypes = [vp, i32, vp, i32, i32]
+        L.orc_range_partition_bytes.restype = i32
+        L.orc_partition_ids.argtypes = [vp, i64, i32, i32, i32, vp, i32, i32, vp]
+        L.orc_partition_ids.restype = None
+        L.orc_stable_scatter.argtypes = [vp, i64, i32, vp, i32, vp, vp]
+        L.orc_stable_scatter.restype = None
+        L.orc_map_write.argtypes = [vp, i64, i32, i32, i32, vp, i32, i32, vp, vp, i32]
+        L.orc_map_write.restype = ctypes.c_int
+        L.orc_index_bytes.argtypes = [vp, i32, vp]
+        L.orc_index_bytes.restype = None
+        L.orc_check_index.argtypes = [vp, i64, i64, i32, vp]
+        L.orc_check_index.restype = ctypes.c_int
+        L.orc_splitmix64_at.argtypes = [u64, u64]
+        L.orc_splitmix64_at.restype = u64
+        L.orc_gen_uniform16.argtypes = [vp, i64, u64, i64]
+        L.orc_gen_uniform16.restype = None
+        L.orc_gen_terasort100.argtypes = [vp, i64, u64, i64]
+        L.orc_gen_terasort100.restype = None
+        L.orc_zipf_cdf.argtypes = [ctypes.c_double, i64, vp]
+        L.orc_zipf_cdf.restype = None
+        L.orc_gen_zipf16.argtypes = [vp, i64, u64, i64, vp, i64]
+        L.orc_gen_zipf16.restype = None
+        _lib = L
+    return _lib
+
+
+def _ptr(a: np.ndarray) -> int:
+    return a.ctypes.data
+
+
+# ---------------------------------------------------------------- generators ------
+def gen_uniform16(n: int, seed: int, value_base: int = 0) -> np.ndarray:
+    """n uniform 16-byte records as a (n, 16) uint8 array."""
+    out = np.empty((n, 16), dtype=np.uint8)
+    lib().orc_gen_uniform16(_ptr(out), n, seed & (2**64 - 1), value_base)
+    return out
+
+
+def gen_terasort100(n: int, seed: int, index_base: int = 0) -> np.ndarray:
+    out = np.empty((n, 100), dtype=np.uint8)
+    lib().orc_gen_terasort100(_ptr(out), n, seed & (2**64 - 1), index_base)
+    return out
+
+
+def zipf_cdf(s: float, K: int) -> np.ndarray:
+    cdf = np.empty(K, dtype=np.float64)
+    lib().orc_zipf_cdf(s, K, _ptr(cdf))
+    return cdf
+
+
+def gen_zipf16(n: int, seed: int, cdf: np.ndarray, value_base: int = 0) -> np.ndarray:
+    out = np.empty((n, 16), dtype=np.uint8)
+    lib().orc_gen_zipf16(_ptr(out), n, seed & (2**64 - 1), value_base, _ptr(cdf), len(cdf))
+    return out
+
+
+# ---------------------------------------------------------------- semantics -------
+def _bounds_arg(kind: int, bounds):
+    if bounds is None or kind == PART_HASH:
+        return None, 0
+    if kind == PART_RANGE_I64:
+        b = np.ascontiguousarray(bounds, dtype=np.int64)
+        return b, len(b)
+    b = np.ascontiguousarray(bounds, dtype=np.uint8).reshape(-1, 10)
+    return b, b.shape[0]
+
+
+def partition_ids(records: np.ndarray, num_partitions: int, kind: int = PART_HASH,
+                  bounds=None, ascending: bool = True) -> np.ndarray:
+    records = np.ascontiguousarray(records)
+    n, rb = records.shape
+    b, nb = _bounds_arg(kind, bounds)
+    pids = np.empty(n, dtype=np.int32)
+    lib().orc_partition_ids(_ptr(records), n, rb, kind, num_partitions,
+                            None if b is None else _ptr(b), nb, int(ascending), _ptr(pids))
+    return pids
+
+
+def map_write(records: np.ndarray, num_partitions: int, kind: int = PART_HASH, bounds=None,
+              ascending: bool = True, nthreads: int = 1):
+    """Map-side write: returns (partition-contiguous records, counts per partition)."""
+    records = np.ascontiguousarray(records)
+    n, rb = records.shape
+    b, nb = _bounds_arg(kind, bounds)
+    out = np.empty_like(records)
+    counts = np.empty(num_partitions, dtype=np.int64)
+    rc = lib().orc_map_write(_ptr(records), n, rb, kind, num_partitions,
+                             None if b is None else _ptr(b), nb, int(ascending), _ptr(out),
+                             _ptr(counts), nthreads)
+    if rc != 0:
+        raise MemoryError("orc_map_write failed")
+    return out, counts
+
+
+def index_bytes(lengths: np.ndarray) -> bytes:
+    lengths = np.ascontiguousarray(lengths, dtype=np.int64)
+    out = np.empty(8 * (len(lengths) + 1), dtype=np.uint8)
+    lib().orc_index_bytes(_ptr(lengths), len(lengths), _ptr(out))
+    return out.tobytes()
+
+
+def offsets(counts: np.ndarray) -> np.ndarray:
+    o = np.zeros(len(counts) + 1, dtype=np.int64)
+    np.cumsum(counts, out=o[1:])
+    return o
+
+
+def canonical_reducer_sequences(map_outputs, num_partitions: int, record_bytes: int):
+    """Per-reducer canonical sequences: for each reducer r, the concatenation over maps in
+    ascending map order of that map's block r (SURVEY.md §8(a) parity note).
+    ``map_outputs``: list of (data (n, rb) uint8, counts[R])."""
+    seqs = []
+    offs = [offsets(c) for _, c in map_outputs]
+    for r in range(num_partitions):
+        parts = [d[o[r]:o[r + 1]] for (d, _), o in zip(map_outputs, offs)]
+        seqs.append(np.concatenate(parts) if parts else np.empty((0, record_bytes), np.uint8))
+    return seqs

@@ -1,0 +1,257 @@
+"""Pure-Python restatement of the Spark 3.0.1 shuffle-write semantics on the hot path.
+
+TEST INFRASTRUCTURE ONLY.  This module is an oracle: only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import it,
+and only as the checker.  The product (``sparkucx_amd``) never imports it.
+
+PARITY STATUS: the reference (ofirfarjun7/sparkucx, Scala) ships no tests, no
+fixtures and no golden vectors for this path, and its arithmetic lives in the
+un-vendored dependency ``org.apache.spark:spark-core_2.12:3.0.1`` (pom.xml:80,90-95),
+which cannot be built or run here (no JVM).  This restatement is therefore pinned
+by the hand-verified known-answer tests of SURVEY.md §8(c) (Java semantics of
+``Long.hashCode`` / ``%`` / ``Utils.nonNegativeMod``) and cross-checked against the
+independent C restatement in ``oracle/shuffle_oracle.c``.  See DESIGN.md §Oracle.
+
+Each function names the reference call site / external algorithm it restates.
+Pure-Python loops: use only for small cases (fixtures, property checks).
+"""
+from __future__ import annotations
+
+import struct
+from typing import List, Optional, Sequence, Tuple
+
+MASK64 = (1 << 64) - 1
+MASK32 = (1 << 32) - 1
+
+# ----------------------------------------------------------------------------
+# Java integer semantics
+# ----------------------------------------------------------------------------
+
+
+def to_i32(x: int) -> int:
+    """Wrap an integer to Java ``int`` (two's complement, 32 bit)."""
+    x &= MASK32
+    return x - (1 << 32) if x & 0x80000000 else x
+
+
+def to_i64(x: int) -> int:
+    """Wrap an integer to Java ``long`` (two's complement, 64 bit)."""
+    x &= MASK64
+    return x - (1 << 64) if x & (1 << 63) else x
+
+
+def java_rem(a: int, b: int) -> int:
+    """Java ``%`` on ints: truncating remainder, sign follows the dividend."""
+    r = abs(a) % abs(b)
+    return -r if a < 0 else r
+
+
+def java_long_hash(k: int) -> int:
+    """``java.lang.Long.hashCode(long value)`` = ``(int)(value ^ (value >>> 32))``.
+
+    Spark's ``HashPartitioner.getPartition(key)`` calls ``key.hashCode`` on the boxed
+    ``java.lang.Long`` (spark-core 3.0.1 ``Partitioner.scala``; invoked by the
+    ``SortShuffleWriter`` built at ``spark_3_0/UcxShuffleManager.scala:50-51``).
+    NOTE: this is NOT Scala's ``##`` (which maps longs that fit an int to that int,
+    e.g. ``(-1L).## == -1`` whereas ``Long.hashCode(-1) == 0``).
+    """
+    u = k & MASK64
+    return to_i32(u ^ (u >> 32))
+
+
+def non_negative_mod(x: int, mod: int) -> int:
+    """``org.apache.spark.util.Utils.nonNegativeMod(x, mod)`` (spark-core 3.0.1)::
+
+        val rawMod = x % mod
+        rawMod + (if (rawMod < 0) mod else 0)
+    """
+    raw = java_rem(x, mod)
+    return raw + (mod if raw < 0 else 0)
+
+
+def hash_partition(key: int, num_partitions: int) -> int:
+    """``HashPartitioner.getPartition`` for a non-null ``java.lang.Long`` key.
+
+    ``case null => 0; case _ => Utils.nonNegativeMod(key.hashCode, numPartitions)``.
+    Primitive (Long, Long) records have no null keys.
+    """
+    return non_negative_mod(java_long_hash(key), num_partitions)
+
+
+# ----------------------------------------------------------------------------
+# RangePartitioner.getPartition (spark-core 3.0.1, Partitioner.scala)
+# ----------------------------------------------------------------------------
+
+
+def java_binary_search(a: Sequence, key, lt) -> int:
+    """``java.util.Arrays.binarySearch`` (JDK 8 ``binarySearch0``), generic form.
+
+    Returns the index of a match, else ``-(insertion point) - 1``.  Spark's
+    ``CollectionsUtils.makeBinarySearch`` dispatches ``Long`` keys to
+    ``Arrays.binarySearch(long[], long)`` and other keys to the Comparator form;
+    both run this exact loop.
+    """
+    low, high = 0, len(a) - 1
+    while low <= high:
+        mid = (low + high) >> 1  # (low + high) >>> 1
+        mv = a[mid]
+        if lt(mv, key):
+            low = mid + 1
+        elif lt(key, mv):
+            high = mid - 1
+        else:
+            return mid
+    return -(low + 1)
+
+
+def range_partition(key, bounds: Sequence, ascending: bool = True, lt=None) -> int:
+    """``RangePartitioner.getPartition``::
+
+        if (rangeBounds.length <= 128) {
+          while (partition < rangeBounds.length && ordering.gt(k, rangeBounds(partition)))
+            partition += 1
+        } else {
+          partition = binarySearch(rangeBounds, k)
+          if (partition < 0) partition = -partition-1
+          if (partition > rangeBounds.length) partition = rangeBounds.length
+        }
+        if (ascending) partition else rangeBounds.length - partition
+
+    ``numPartitions = rangeBounds.length + 1``.
+    """
+    if lt is None:
+        lt = lambda x, y: x < y  # noqa: E731
+    nb = len(bounds)
+    if nb <= 128:
+        p = 0
+        while p < nb and lt(bounds[p], key):  # ordering.gt(k, b) == lt(b, k)
+            p += 1
+    else:
+        p = java_binary_search(bounds, key, lt)
+        if p < 0:
+            p = -p - 1
+        if p > nb:
+            p = nb
+    return p if ascending else nb - p
+
+
+def bytes_lt(a: bytes, b: bytes) -> bool:
+    """Unsigned lexicographic order on byte keys (TeraSort's key comparator)."""
+    return a < b  # Python bytes compare unsigned-lexicographically
+
+
+# ----------------------------------------------------------------------------
+# Map-side grouping, index layout, block lookup
+# ----------------------------------------------------------------------------
+
+
+def stable_group_by_partition(pids: Sequence[int], num_partitions: int) -> Tuple[List[int], List[int]]:
+    """Stable group-by-partition of record indices.
+
+    Restates the ordering contract of ``ExternalSorter``/``PartitionedPairBuffer``
+    (TimSort with a partition comparator, stable) and ``ShuffleInMemorySorter``
+    (LSD radix on the partition id, stable): runs in increasing partition order,
+    map input order inside each run.  Returns ``(order, lengths_in_records)``.
+    """
+    buckets: List[List[int]] = [[] for _ in range(num_partitions)]
+    for i, p in enumerate(pids):
+        if not 0 <= p < num_partitions:
+            raise ValueError(f"partition id {p} out of range")
+        buckets[p].append(i)
+    order = [i for b in buckets for i in b]
+    return order, [len(b) for b in buckets]
+
+
+def index_offsets(lengths: Sequence[int]) -> List[int]:
+    """``IndexShuffleBlockResolver.writeIndexFileAndCommit`` offsets
+    (``IndexShuffleBlockResolver.scala:184-192``): ``[0, L0, L0+L1, ..., sum]``."""
+    out = [0]
+    for length in lengths:
+        out.append(to_i64(out[-1] + length))
+    return out
+
+
+def index_file_bytes(lengths: Sequence[int]) -> bytes:
+    """The index file: ``numPartitions + 1`` big-endian longs (``DataOutputStream.writeLong``)."""
+    return b"".join(struct.pack(">q", o) for o in index_offsets(lengths))
+
+
+def check_index_and_data(index_bytes: bytes, data_length: int, blocks: int) -> Optional[List[int]]:
+    """``IndexShuffleBlockResolver.checkIndexAndDataFile`` (``:110-149``).
+
+    Returns the partition lengths if index and data match, else ``None``.
+    """
+    if len(index_bytes) != (blocks + 1) * 8:
+        return None
+    offs = [struct.unpack_from(">q", index_bytes, 8 * i)[0] for i in range(blocks + 1)]
+    if offs[0] != 0:
+        return None
+    lengths = [offs[i + 1] - offs[i] for i in range(blocks)]
+    return lengths if data_length == sum(lengths) else None
+
+
+def block_range(index_bytes: bytes, start_reduce: int, end_reduce: int) -> Tuple[int, int]:
+    """``IndexShuffleBlockResolver.getBlockData`` (``:219-262``): the (offset, length)
+    of block ``(map, [start, end))`` read from the index at byte ``reduceId * 8``."""
+    start = struct.unpack_from(">q", index_bytes, start_reduce * 8)[0]
+    end = struct.unpack_from(">q", index_bytes, end_reduce * 8)[0]
+    return start, end - start
+
+
+def ucx_registered_blocks(lengths: Sequence[int]) -> List[Tuple[int, int, int]]:
+    """``CommonUcxShuffleBlockResolver.writeIndexFileAndCommitCommon`` (``:37-61``):
+    one ``(reduceId, fileOffset, size)`` per NON-EMPTY partition; offset is the
+    running sum of the lengths (equal to the index offsets)."""
+    out, off = [], 0
+    for r, length in enumerate(lengths):
+        if length > 0:
+            out.append((r, off, length))
+            off += length
+    return out
+
+
+def ucx_block_id_bytes(map_id: int, reduce_id: int) -> bytes:
+    """``UcxShuffleBlockId.serialize`` (``UcxShuffleTransport.scala:55-72``): 8 bytes
+    ``[mapId:i32][reduceId:i32]`` in ByteBuffer's default (big-endian) order;
+    shuffleId is dropped (decodes as 0)."""
+    return struct.pack(">ii", to_i32(map_id), to_i32(reduce_id))
+
+
+# ----------------------------------------------------------------------------
+# Synthetic inputs (the build's own definitions)
+# ----------------------------------------------------------------------------
+
+GOLDEN_GAMMA = 0x9E3779B97F4A7C15
+
+
+def splitmix64_at(seed: int, i: int) -> int:
+    """Counter-based splitmix64: the i-th output of the stream seeded by ``seed``."""
+    z = (seed + (i + 1) * GOLDEN_GAMMA) & MASK64
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & MASK64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & MASK64
+    return z ^ (z >> 31)
+
+
+def gen_uniform_records(n: int, seed: int, value_base: int = 0) -> List[Tuple[int, int]]:
+    """Uniform (Long, Long) records: key = splitmix64(seed, i) as signed i64,
+    value = value_base + i."""
+    return [(to_i64(splitmix64_at(seed, i)), value_base + i) for i in range(n)]
+
+
+def pack_records16(records: Sequence[Tuple[int, int]]) -> bytes:
+    """16-byte little-endian ``{i64 key, i64 value}`` record codec."""
+    return b"".join(struct.pack("<qq", k, v) for k, v in records)
+
+
+def map_side_shuffle(records: Sequence[Tuple[int, int]], num_partitions: int):
+    """Full map-side write for the fixed 16 B codec with a HashPartitioner:
+    returns ``(pids, data_bytes, lengths_in_bytes)``."""
+    pids = [hash_partition(k, num_partitions) for k, _ in records]
+    order, counts = stable_group_by_partition(pids, num_partitions)
+    data = pack_records16([records[i] for i in order])
+    return pids, data, [16 * c for c in counts]
+
+
+def reducer_owner(reduce_id: int, num_partitions: int, world: int) -> int:
+    """Contiguous reducer ownership used by the multi-GPU exchange: ``floor(r*P/R)``."""
+    return (reduce_id * world) // num_partitions

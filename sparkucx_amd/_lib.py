@@ -1,0 +1,142 @@
+"""ctypes binding of libsgx.so (the C ABI declared in include/sgx.h).
+
+There is no fallback: if the in-tree HIP library is missing or cannot be loaded, every
+entry point raises.  Negative return codes are mapped to the exception types the JVM side
+would throw (ShuffleTransport.scala:49-51,71 / the reference's IllegalArgument- and
+IllegalStateExceptions, NvkvShuffleMapOutputWriter.scala:108, DpuShuffleExecutorComponents
+.scala:28-30).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsgx.so")
+
+SGX_OK = 0
+SGX_ERR_INVALID, SGX_ERR_STATE, SGX_ERR_HIP, SGX_ERR_COMM = -1, -2, -3, -4
+SGX_ERR_IO, SGX_ERR_NOMEM, SGX_ERR_NOT_FOUND, SGX_ERR_UNSUPPORTED, SGX_ERR_TIMEOUT = -5, -6, -7, -8, -9
+PART_HASH, PART_RANGE_I64, PART_RANGE_BYTES10 = 0, 1, 2
+MEM_HOST, MEM_DEVICE = 0, 1
+STAGES = ("hist", "scan", "scatter", "allgather", "alltoall", "regroup")
+
+
+class ShuffleError(RuntimeError):
+    """Base of every error raised through the C ABI (OperationStatus.FAILURE)."""
+
+    code = -100
+
+
+class IllegalArgumentException(ShuffleError, ValueError):
+    code = SGX_ERR_INVALID
+
+
+class IllegalStateException(ShuffleError):
+    code = SGX_ERR_STATE
+
+
+class DeviceError(ShuffleError):
+    code = SGX_ERR_HIP
+
+
+class TransportError(ShuffleError):
+    code = SGX_ERR_COMM
+
+
+class ShuffleIOException(ShuffleError, IOError):
+    code = SGX_ERR_IO
+
+
+class DeviceOutOfMemory(ShuffleError, MemoryError):
+    code = SGX_ERR_NOMEM
+
+
+class BlockNotFoundException(ShuffleError, KeyError):
+    code = SGX_ERR_NOT_FOUND
+
+
+class UnsupportedOperationException(ShuffleError):
+    code = SGX_ERR_UNSUPPORTED
+
+
+class DeviceTimeout(ShuffleError):
+    code = SGX_ERR_TIMEOUT
+
+
+_BY_CODE = {c.code: c for c in (IllegalArgumentException, IllegalStateException, DeviceError,
+                                TransportError, ShuffleIOException, DeviceOutOfMemory,
+                                BlockNotFoundException, UnsupportedOperationException, DeviceTimeout)}
+
+_lib = None
+_lock = threading.Lock()
+
+_i32, _i64, _u64, _vp, _cp = ctypes.c_int32, ctypes.c_int64, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_char_p
+_P64, _P32 = ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)
+
+# name -> (restype, argtypes).  Must cover every function declared in include/sgx.h.
+SIGNATURES = {
+    "sgx_create": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
+    "sgx_destroy": (None, [_vp]),
+    "sgx_last_error": (_cp, []),
+    "sgx_abi_version": (_i32, []),
+    "sgx_register_shuffle": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _i64, _i32, _i32]),
+    "sgx_unregister_shuffle": (ctypes.c_int, [_vp, _i32]),
+    "sgx_write_map": (ctypes.c_int, [_vp, _i32, _i64, _vp, _i64, _i32, _i32, _vp]),
+    "sgx_map_lengths": (ctypes.c_int, [_vp, _i32, _i64, _vp]),
+    "sgx_map_data": (ctypes.c_int, [_vp, _i32, _i64, ctypes.POINTER(_vp), _P64]),
+    "sgx_write_index": (ctypes.c_int, [_vp, _i32, _i64, _cp, _cp, _vp]),
+    "sgx_check_index_and_data": (ctypes.c_int, [_cp, _cp, _i32, _vp]),
+    "sgx_index_block_range": (ctypes.c_int, [_cp, _i32, _i32, _P64, _P64]),
+    "sgx_get_unique_id": (ctypes.c_int, [_vp]),
+    "sgx_comm_init": (ctypes.c_int, [_vp, _i32, _i32, _vp]),
+    "sgx_comm_size": (ctypes.c_int, [_vp, _P32, _P32]),
+    "sgx_exchange": (ctypes.c_int, [_vp, _i32, _i64]),
+    "sgx_fetch_blocks": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i64, _vp, _i64, _i32, _vp]),
+    "sgx_progress": (ctypes.c_int, [_vp]),
+    "sgx_sync": (ctypes.c_int, [_vp]),
+    "sgx_stats_reset": (ctypes.c_int, [_vp]),
+    "sgx_stats_get": (ctypes.c_int, [_vp, _vp, _vp]),
+    "sgx_plan_exchange": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _P64]),
+    "sgx_copy_items": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i32]),
+    "sgx_reducer_owner": (_i32, [_i32, _i32, _i32]),
+    "sgx_gen_uniform16": (ctypes.c_int, [_vp, _vp, _i64, _u64, _i64]),
+    "sgx_gen_zipf16": (ctypes.c_int, [_vp, _vp, _i64, _u64, _i64, _vp, _i64]),
+    "sgx_gen_terasort100": (ctypes.c_int, [_vp, _vp, _i64, _u64, _i64]),
+    "sgx_device_alloc": (ctypes.c_int, [_vp, _i64, ctypes.POINTER(_vp)]),
+    "sgx_device_free": (ctypes.c_int, [_vp, _vp]),
+    "sgx_memcpy": (ctypes.c_int, [_vp, _vp, _vp, _i64]),
+}
+
+
+def lib() -> ctypes.CDLL:
+    """Load the in-tree libsgx.so (raises if it was not built: no CPU fallback)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"{LIB_PATH} is missing: build the HIP extension first "
+                    "(python -c 'import __graft_entry__ as g; g.build()'); "
+                    "sparkucx_amd has no CPU fallback")
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    msg = lib().sgx_last_error()
+    return msg.decode("utf-8", "replace") if msg else ""
+
+
+def check(rc: int, what: str = "") -> int:
+    """Raise the mapped exception for a negative return code."""
+    if rc >= 0:
+        return rc
+    cls = _BY_CODE.get(rc, ShuffleError)
+    raise cls(f"{what}: {last_error()} (code {rc})" if what else f"{last_error()} (code {rc})")

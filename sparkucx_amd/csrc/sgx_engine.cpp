@@ -1,0 +1,1011 @@
+// sgx_engine.cpp — the C-ABI engine behind include/sgx.h.
+//
+// One engine per GPU (= per Spark executor).  It replaces, on the hot path:
+//   * the map-output writer + NVKV storage (ucx/NvkvShuffleMapOutputWriter.scala:105-148,
+//     ucx/NvkvHandler.scala:213-265): map outputs are partitioned by HIP kernels and kept
+//     resident in HBM, engine-owned;
+//   * the index commit (IndexShuffleBlockResolver.scala:161-217) when a file is wanted;
+//   * the UCX fetch path (ucx/UcxWorkerWrapper.scala:96-186, spark_3_0/UcxShuffleClient.scala
+//     :17-91): one counts all-gather + ncclAllToAllv over xGMI + a regroup kernel, then
+//     block fetches are served from HBM.
+// There is no CPU fallback: every data-path call runs the HIP kernels or fails.
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <cerrno>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/sgx.h"
+#include "sgx_internal.h"
+
+using namespace sgx;
+
+// ------------------------------------------------------------------------------------
+// errors
+// ------------------------------------------------------------------------------------
+static thread_local std::string t_last_error;
+
+static int fail(int code, const char *fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess)                                                                  \
+            return fail(SGX_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e),    \
+                        __FILE__, __LINE__);                                                   \
+    } while (0)
+#define NCCL_TRY(expr)                                                                         \
+    do {                                                                                       \
+        ncclResult_t _r = (expr);                                                              \
+        if (_r != ncclSuccess)                                                                 \
+            return fail(SGX_ERR_COMM, "%s failed: %s", #expr, ncclGetErrorString(_r));          \
+    } while (0)
+#define SGX_TRY(expr)                                                                          \
+    do {                                                                                       \
+        int _c = (expr);                                                                       \
+        if (_c != SGX_OK) return _c;                                                           \
+    } while (0)
+
+// ------------------------------------------------------------------------------------
+// device buffers
+// ------------------------------------------------------------------------------------
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return SGX_OK;
+        release();
+        size_t want = bytes ? bytes : 16;
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(SGX_ERR_NOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+        }
+        cap = want;
+        return SGX_OK;
+    }
+};
+
+struct HostPinned {
+    void *p = nullptr;
+    size_t cap = 0;
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return SGX_OK;
+        release();
+        size_t want = bytes ? bytes : 16;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail(SGX_ERR_NOMEM, "hipHostMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+        }
+        cap = want;
+        return SGX_OK;
+    }
+};
+
+// ------------------------------------------------------------------------------------
+// registry
+// ------------------------------------------------------------------------------------
+struct MapOut {
+    DevBuf data;               // partition-contiguous records (engine-owned HBM)
+    int64_t nrec = 0;
+    int64_t bytes = 0;
+    HostPinned part_off;       // (R+1) u32 record offsets + 1 u32 error word, landed async
+    std::vector<int64_t> lengths;  // bytes per partition (valid once `ready`)
+    bool ready = false;
+    hipEvent_t done = nullptr;  // recorded on the compute stream after the scatter
+};
+
+// One exchange round: every rank pushed one map; this rank holds its reducers' blocks.
+struct Round {
+    std::vector<int64_t> map_ids;        // [P] the map pushed by each source rank
+    std::vector<int64_t> lens;           // [P][R] bytes
+    std::vector<int64_t> block_off;      // [P][nmine] byte offset in `data`
+    std::vector<int64_t> items;          // regroup copy list (kept alive for the async H2D)
+    int32_t r0 = 0, r1 = 0;              // my reducers [r0, r1)
+    DevBuf data;                          // regrouped: reducer-major, source-minor
+    const void *alias = nullptr;          // P == 1: the local map output itself
+    hipEvent_t done = nullptr;
+    const void *base() const { return alias ? alias : data.p; }
+};
+
+struct Shuffle {
+    int32_t R = 0, kind = 0, nb = 0, asc = 1, rb = 16;
+    DevBuf bounds;
+    PartParams pp{};
+    std::map<int64_t, std::unique_ptr<MapOut>> maps;
+    std::vector<std::unique_ptr<Round>> rounds;
+};
+
+struct PendingStage {
+    int stage;
+    hipEvent_t a, b;
+};
+
+struct sgx_engine {
+    std::mutex mu;
+    int device = 0;
+    int num_cus = 256;
+    int G = 256;
+    hipStream_t s_comp = nullptr, s_comm = nullptr;
+    // work buffers of the map-side pipeline
+    DevBuf counts, offs, status, part_off_dev, input_stage;
+    DevBuf ag_send, ag_recv, recv, items_dev;
+    HostPinned ag_host;
+    std::map<int32_t, Shuffle> shuffles;
+    // RCCL
+    ncclComm_t comm = nullptr;
+    int32_t nranks = 1, rank = 0;
+    // stats
+    std::vector<hipEvent_t> ev_free;
+    std::vector<PendingStage> pending;
+    double stage_ms[SGX_NUM_STAGES] = {0};
+    int64_t stage_n[SGX_NUM_STAGES] = {0};
+
+    hipEvent_t ev() {
+        if (!ev_free.empty()) {
+            hipEvent_t e = ev_free.back();
+            ev_free.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        (void)hipEventCreate(&e);
+        return e;
+    }
+    void resolve_stats() {
+        for (auto &p : pending) {
+            float ms = 0.f;
+            if (hipEventSynchronize(p.b) == hipSuccess && hipEventElapsedTime(&ms, p.a, p.b) == hipSuccess) {
+                stage_ms[p.stage] += ms;
+                stage_n[p.stage] += 1;
+            }
+            ev_free.push_back(p.a);
+            ev_free.push_back(p.b);
+        }
+        pending.clear();
+    }
+};
+
+static uint32_t bits_for(uint32_t R) {
+    uint32_t b = 0;
+    while ((1ull << b) < R) ++b;
+    return b ? b : 1;
+}
+
+static PartParams make_part_params(const Shuffle &s) {
+    PartParams pp{};
+    pp.kind = s.kind;
+    pp.R = (uint32_t)s.R;
+    pp.fm_M = UINT64_MAX / (uint64_t)s.R + 1;  // R == 1 wraps to 0 -> fastmod 0, as needed
+    pp.c31 = (uint32_t)((1ull << 31) % (uint64_t)s.R);
+    pp.nbits = bits_for((uint32_t)s.R);
+    pp.nb = s.nb;
+    pp.ascending = s.asc;
+    pp.bounds = s.bounds.p;
+    return pp;
+}
+
+// ------------------------------------------------------------------------------------
+// lifetime
+// ------------------------------------------------------------------------------------
+extern "C" const char *sgx_last_error(void) { return t_last_error.c_str(); }
+extern "C" int32_t sgx_abi_version(void) { return SGX_ABI_VERSION; }
+
+extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
+    if (!out) return fail(SGX_ERR_INVALID, "sgx_create: out is NULL");
+    *out = nullptr;
+    int dev = cfg ? cfg->device : 0;
+    int ndev = 0;
+    HIP_TRY(hipGetDeviceCount(&ndev));
+    if (dev < 0 || dev >= ndev) return fail(SGX_ERR_INVALID, "sgx_create: device %d of %d", dev, ndev);
+    HIP_TRY(hipSetDevice(dev));
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, dev));
+    std::unique_ptr<sgx_engine> e(new sgx_engine());
+    e->device = dev;
+    e->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    e->G = (cfg && cfg->num_chunks > 0) ? cfg->num_chunks : e->num_cus;
+    HIP_TRY(hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
+    *out = e.release();
+    return SGX_OK;
+}
+
+static void free_map(MapOut &m) {
+    m.data.release();
+    m.part_off.release();
+    if (m.done) (void)hipEventDestroy(m.done);
+    m.done = nullptr;
+}
+static void free_round(Round &r) {
+    r.data.release();
+    if (r.done) (void)hipEventDestroy(r.done);
+    r.done = nullptr;
+}
+
+extern "C" void sgx_destroy(sgx_engine *e) {
+    if (!e) return;
+    (void)hipSetDevice(e->device);
+    (void)hipDeviceSynchronize();
+    e->resolve_stats();
+    for (auto &kv : e->shuffles) {
+        for (auto &m : kv.second.maps) free_map(*m.second);
+        for (auto &r : kv.second.rounds) free_round(*r);
+        kv.second.bounds.release();
+    }
+    for (DevBuf *b : {&e->counts, &e->offs, &e->status, &e->part_off_dev, &e->input_stage, &e->ag_send,
+                      &e->ag_recv, &e->recv, &e->items_dev})
+        b->release();
+    e->ag_host.release();
+    for (hipEvent_t ev : e->ev_free) (void)hipEventDestroy(ev);
+    if (e->comm) (void)ncclCommDestroy(e->comm);
+    (void)hipStreamDestroy(e->s_comp);
+    (void)hipStreamDestroy(e->s_comm);
+    delete e;
+}
+
+// ------------------------------------------------------------------------------------
+// registerShuffle / unregisterShuffle
+// ------------------------------------------------------------------------------------
+static int max_partitions(int kind, int rb) {
+    (void)kind;
+    // LDS budget of the scatter kernels (sgx_kernels.hip scatter_geom*).
+    for (uint32_t R = 8192; R >= 1; R -= 1) {
+        ScatterGeom g = rb == 16 ? scatter_geom16(R) : scatter_geom_wide(R, rb);
+        if (g.items > 0) return (int)R;
+    }
+    return 0;
+}
+
+extern "C" int sgx_register_shuffle(sgx_engine *e, int32_t shuffle_id, int32_t R, int32_t kind,
+                                    const void *bounds, int64_t nbounds, int32_t ascending,
+                                    int32_t rb) {
+    if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (R < 1) return fail(SGX_ERR_INVALID, "numPartitions must be positive, got %d", R);
+    if (kind < SGX_PART_HASH || kind > SGX_PART_RANGE_BYTES10)
+        return fail(SGX_ERR_INVALID, "unknown partitioner kind %d", kind);
+    if (rb < 12 || (rb & 3) != 0)
+        return fail(SGX_ERR_INVALID, "record_bytes must be a multiple of 4 and >= 12, got %d", rb);
+    if (kind != SGX_PART_HASH && nbounds != (int64_t)R - 1)
+        return fail(SGX_ERR_INVALID, "RangePartitioner needs numPartitions == bounds+1 (%d vs %lld)",
+                    R, (long long)nbounds);
+    if (kind != SGX_PART_HASH && nbounds > 0 && !bounds)
+        return fail(SGX_ERR_INVALID, "range bounds pointer is NULL");
+    const int rmax = max_partitions(kind, rb);
+    if (R > rmax)
+        return fail(SGX_ERR_UNSUPPORTED, "numPartitions %d exceeds the single-pass LDS limit %d", R, rmax);
+    if (e->shuffles.count(shuffle_id))
+        return fail(SGX_ERR_STATE, "shuffle %d is already registered", shuffle_id);
+    HIP_TRY(hipSetDevice(e->device));
+    Shuffle &s = e->shuffles[shuffle_id];
+    s.R = R;
+    s.kind = kind;
+    s.nb = (int32_t)(kind == SGX_PART_HASH ? 0 : nbounds);
+    s.asc = ascending ? 1 : 0;
+    s.rb = rb;
+    if (kind == SGX_PART_RANGE_I64 && nbounds > 0) {
+        int rc = s.bounds.ensure((size_t)nbounds * 8);
+        if (rc) { e->shuffles.erase(shuffle_id); return rc; }
+        HIP_TRY(hipMemcpy(s.bounds.p, bounds, (size_t)nbounds * 8, hipMemcpyHostToDevice));
+    } else if (kind == SGX_PART_RANGE_BYTES10 && nbounds > 0) {
+        std::vector<Key10> k((size_t)nbounds);
+        const uint8_t *b = (const uint8_t *)bounds;
+        for (int64_t i = 0; i < nbounds; ++i) {
+            const uint8_t *q = b + 10 * i;
+            uint64_t hi = 0;
+            for (int j = 0; j < 8; ++j) hi = (hi << 8) | q[j];
+            k[(size_t)i] = Key10{hi, ((uint32_t)q[8] << 8) | q[9], 0};
+        }
+        int rc = s.bounds.ensure((size_t)nbounds * sizeof(Key10));
+        if (rc) { e->shuffles.erase(shuffle_id); return rc; }
+        HIP_TRY(hipMemcpy(s.bounds.p, k.data(), k.size() * sizeof(Key10), hipMemcpyHostToDevice));
+    }
+    s.pp = make_part_params(s);
+    return SGX_OK;
+}
+
+extern "C" int sgx_unregister_shuffle(sgx_engine *e, int32_t shuffle_id) {
+    if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    auto it = e->shuffles.find(shuffle_id);
+    if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->s_comp));
+    HIP_TRY(hipStreamSynchronize(e->s_comm));
+    for (auto &m : it->second.maps) free_map(*m.second);
+    for (auto &r : it->second.rounds) free_round(*r);
+    it->second.bounds.release();
+    e->shuffles.erase(it);
+    return SGX_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// map-side write: K1+K2 hist -> K3 scan -> K4 scatter (all on the compute stream)
+// ------------------------------------------------------------------------------------
+static int finish_lengths(Shuffle &s, MapOut &m) {
+    if (m.ready) return SGX_OK;
+    HIP_TRY(hipEventSynchronize(m.done));
+    const uint32_t *po = (const uint32_t *)m.part_off.p;
+    if (po[s.R + 1] != 0) return fail(SGX_ERR_TIMEOUT, "scan look-back spin gave up (device flag %u)", po[s.R + 1]);
+    if ((int64_t)po[s.R] != m.nrec)
+        return fail(SGX_ERR_HIP, "partition offsets do not sum to the record count (%u vs %lld)", po[s.R],
+                    (long long)m.nrec);
+    m.lengths.assign((size_t)s.R, 0);
+    for (int32_t p = 0; p < s.R; ++p) m.lengths[(size_t)p] = ((int64_t)po[p + 1] - (int64_t)po[p]) * s.rb;
+    m.ready = true;
+    return SGX_OK;
+}
+
+static void record_stage(sgx_engine *e, int stage, hipEvent_t a, hipEvent_t b) {
+    e->pending.push_back(PendingStage{stage, a, b});
+}
+
+extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records,
+                             int64_t n, int32_t rb, int32_t mem_kind, int64_t *out_lengths) {
+    if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    auto it = e->shuffles.find(shuffle_id);
+    if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
+    Shuffle &s = it->second;
+    if (rb != s.rb) return fail(SGX_ERR_INVALID, "record_bytes %d != registered %d", rb, s.rb);
+    if (n < 0 || n >= (int64_t)UINT32_MAX) return fail(SGX_ERR_INVALID, "nrecords %lld out of range", (long long)n);
+    if (n > 0 && !records) return fail(SGX_ERR_INVALID, "records is NULL");
+    if (mem_kind != SGX_MEM_HOST && mem_kind != SGX_MEM_DEVICE)
+        return fail(SGX_ERR_INVALID, "unknown mem_kind %d", mem_kind);
+    HIP_TRY(hipSetDevice(e->device));
+    hipStream_t st = e->s_comp;
+
+    std::unique_ptr<MapOut> &slot = s.maps[map_id];
+    if (!slot) slot.reset(new MapOut());
+    MapOut &m = *slot;
+    // A re-attempt of the same map replaces the previous output (the in-HBM analogue of the
+    // index commit; the file commit keeps "first valid attempt wins", sgx_write_index).
+    if (m.done) HIP_TRY(hipEventSynchronize(m.done));
+    m.ready = false;
+    m.nrec = n;
+    m.bytes = n * rb;
+    SGX_TRY(m.data.ensure((size_t)m.bytes));
+    SGX_TRY(m.part_off.ensure((size_t)(s.R + 2) * 4));
+    if (!m.done) HIP_TRY(hipEventCreateWithFlags(&m.done, hipEventDisableTiming));
+
+    const void *in = records;
+    if (mem_kind == SGX_MEM_HOST && n > 0) {
+        SGX_TRY(e->input_stage.ensure((size_t)m.bytes));
+        HIP_TRY(hipMemcpyAsync(e->input_stage.p, records, (size_t)m.bytes, hipMemcpyHostToDevice, st));
+        in = e->input_stage.p;
+    }
+
+    // chunking: G chunks, each a whole number of scatter tiles where possible
+    const int tile = rb == 16 ? scatter_geom16((uint32_t)s.R).tile : scatter_geom_wide((uint32_t)s.R, rb).tile;
+    int64_t chunk = n > 0 ? (n + e->G - 1) / e->G : 1;
+    chunk = (chunk + tile - 1) / tile * tile;
+    const int G = n > 0 ? (int)((n + chunk - 1) / chunk) : 1;
+    const int64_t len = (int64_t)s.R * G;
+    const int64_t tiles = scan_tiles(len);
+    SGX_TRY(e->counts.ensure((size_t)len * 4));
+    SGX_TRY(e->offs.ensure((size_t)len * 4));
+    SGX_TRY(e->status.ensure((size_t)(16 + tiles * 8)));
+    SGX_TRY(e->part_off_dev.ensure((size_t)(s.R + 2) * 4));
+    uint32_t *ticket_err = (uint32_t *)e->status.p;
+    uint64_t *status = (uint64_t *)((char *)e->status.p + 16);
+    HIP_TRY(hipMemsetAsync(e->status.p, 0, (size_t)(16 + tiles * 8), st));
+
+    hipEvent_t t0 = e->ev(), t1 = e->ev(), t2 = e->ev(), t3 = e->ev();
+    HIP_TRY(hipEventRecord(t0, st));
+    if (n > 0) {
+        HIP_TRY(launch_hist(in, n, rb, chunk, G, s.pp, (uint32_t *)e->counts.p, st));
+    } else {
+        HIP_TRY(hipMemsetAsync(e->counts.p, 0, (size_t)len * 4, st));
+    }
+    HIP_TRY(hipEventRecord(t1, st));
+    HIP_TRY(launch_scan((const uint32_t *)e->counts.p, (uint32_t *)e->offs.p, len, status, ticket_err,
+                        (uint32_t *)e->part_off_dev.p, G, s.R, st));
+    HIP_TRY(hipEventRecord(t2, st));
+    if (n > 0) HIP_TRY(launch_scatter(in, m.data.p, n, rb, chunk, G, s.pp, (const uint32_t *)e->offs.p, st));
+    HIP_TRY(hipEventRecord(t3, st));
+    // (R+1) offsets then the look-back give-up flag
+    HIP_TRY(hipMemcpyAsync((char *)e->part_off_dev.p + (size_t)(s.R + 1) * 4, ticket_err + 1, 4,
+                           hipMemcpyDeviceToDevice, st));
+    HIP_TRY(hipMemcpyAsync(m.part_off.p, e->part_off_dev.p, (size_t)(s.R + 2) * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(m.done, st));
+    record_stage(e, SGX_STAGE_HIST, t0, t1);
+    record_stage(e, SGX_STAGE_SCAN, t1, t2);
+    record_stage(e, SGX_STAGE_SCATTER, t2, t3);
+    if (out_lengths) {
+        SGX_TRY(finish_lengths(s, m));
+        std::memcpy(out_lengths, m.lengths.data(), sizeof(int64_t) * (size_t)s.R);
+    }
+    return SGX_OK;
+}
+
+static int find_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, Shuffle **ps, MapOut **pm) {
+    auto it = e->shuffles.find(shuffle_id);
+    if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
+    auto mt = it->second.maps.find(map_id);
+    if (mt == it->second.maps.end())
+        return fail(SGX_ERR_NOT_FOUND, "map %lld of shuffle %d was not written", (long long)map_id, shuffle_id);
+    *ps = &it->second;
+    *pm = mt->second.get();
+    return SGX_OK;
+}
+
+extern "C" int sgx_map_lengths(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *out) {
+    if (!e || !out) return fail(SGX_ERR_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    Shuffle *s;
+    MapOut *m;
+    SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
+    SGX_TRY(finish_lengths(*s, *m));
+    std::memcpy(out, m->lengths.data(), sizeof(int64_t) * (size_t)s->R);
+    return SGX_OK;
+}
+
+extern "C" int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, void **ptr, int64_t *bytes) {
+    if (!e || !ptr || !bytes) return fail(SGX_ERR_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    Shuffle *s;
+    MapOut *m;
+    SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
+    *ptr = m->data.p;
+    *bytes = m->bytes;
+    return SGX_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// IndexShuffleBlockResolver: index + data files (IndexShuffleBlockResolver.scala:56-262)
+// ------------------------------------------------------------------------------------
+static bool read_file(const char *path, std::vector<uint8_t> &out) {
+    FILE *f = fopen(path, "rb");
+    if (!f) return false;
+    out.clear();
+    uint8_t buf[1 << 16];
+    size_t k;
+    while ((k = fread(buf, 1, sizeof buf, f)) > 0) out.insert(out.end(), buf, buf + k);
+    fclose(f);
+    return true;
+}
+
+static int64_t file_size(const char *path) {
+    struct stat st;
+    if (stat(path, &st) != 0) return -1;
+    return (int64_t)st.st_size;
+}
+
+static int64_t load_be64(const uint8_t *p) {
+    uint64_t u = 0;
+    for (int i = 0; i < 8; ++i) u = (u << 8) | p[i];
+    return (int64_t)u;
+}
+
+// checkIndexAndDataFile (:110-149): lengths if index and data agree, else false.
+static bool check_index_and_data(const char *index_path, const char *data_path, int32_t blocks,
+                                 std::vector<int64_t> &lengths) {
+    const int64_t isz = file_size(index_path);
+    if (isz != ((int64_t)blocks + 1) * 8) return false;
+    std::vector<uint8_t> idx;
+    if (!read_file(index_path, idx) || (int64_t)idx.size() != isz) return false;
+    int64_t off = load_be64(idx.data());
+    if (off != 0) return false;
+    lengths.assign((size_t)blocks, 0);
+    int64_t sum = 0;
+    for (int32_t i = 0; i < blocks; ++i) {
+        const int64_t nx = load_be64(idx.data() + 8 * (size_t)(i + 1));
+        lengths[(size_t)i] = nx - off;
+        sum += nx - off;
+        off = nx;
+    }
+    const int64_t dsz = file_size(data_path);
+    return dsz >= 0 && dsz == sum;
+}
+
+extern "C" int sgx_check_index_and_data(const char *index_path, const char *data_path, int32_t blocks,
+                                        int64_t *out_lengths) {
+    if (!index_path || !data_path || blocks < 0) return fail(SGX_ERR_INVALID, "bad arguments");
+    std::vector<int64_t> l;
+    if (!check_index_and_data(index_path, data_path, blocks, l))
+        return fail(SGX_ERR_NOT_FOUND, "index %s and data %s do not match for %d blocks", index_path, data_path,
+                    blocks);
+    if (out_lengths) std::memcpy(out_lengths, l.data(), sizeof(int64_t) * l.size());
+    return SGX_OK;
+}
+
+extern "C" int sgx_index_block_range(const char *index_path, int32_t start, int32_t end, int64_t *off,
+                                     int64_t *len) {
+    if (!index_path || !off || !len || start < 0 || end < start)
+        return fail(SGX_ERR_INVALID, "bad arguments");
+    FILE *f = fopen(index_path, "rb");
+    if (!f) return fail(SGX_ERR_IO, "cannot open index %s: %s", index_path, strerror(errno));
+    uint8_t a[8], b[8];
+    bool ok = fseek(f, (long)start * 8, SEEK_SET) == 0 && fread(a, 1, 8, f) == 8 &&
+              fseek(f, (long)end * 8, SEEK_SET) == 0 && fread(b, 1, 8, f) == 8;
+    // SPARK-22982 position check: after reading end's long we must sit at end*8+8.
+    const bool pos_ok = ok && ftell(f) == (long)end * 8 + 8;
+    fclose(f);
+    if (!ok) return fail(SGX_ERR_IO, "index %s too short for reduce range [%d, %d)", index_path, start, end);
+    if (!pos_ok) return fail(SGX_ERR_IO, "SPARK-22982: incorrect channel position after index file reads");
+    *off = load_be64(a);
+    *len = load_be64(b) - *off;
+    return SGX_OK;
+}
+
+static int write_all(const char *path, const void *data, size_t n) {
+    int fd = open(path, O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) return fail(SGX_ERR_IO, "cannot create %s: %s", path, strerror(errno));
+    const char *p = (const char *)data;
+    while (n > 0) {
+        ssize_t k = write(fd, p, n);
+        if (k < 0) {
+            if (errno == EINTR) continue;
+            close(fd);
+            return fail(SGX_ERR_IO, "write %s: %s", path, strerror(errno));
+        }
+        p += k;
+        n -= (size_t)k;
+    }
+    if (close(fd) != 0) return fail(SGX_ERR_IO, "close %s: %s", path, strerror(errno));
+    return SGX_OK;
+}
+
+extern "C" int sgx_write_index(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const char *index_path,
+                               const char *data_path, int64_t *out_lengths) {
+    if (!e || !index_path || !data_path) return fail(SGX_ERR_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    Shuffle *s;
+    MapOut *m;
+    SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
+    SGX_TRY(finish_lengths(*s, *m));
+    HIP_TRY(hipSetDevice(e->device));
+    const std::string data_tmp = std::string(data_path) + ".sgx.tmp";
+    const std::string index_tmp = std::string(index_path) + ".sgx.tmp";
+    // map output -> data tmp (dataTmp of writeIndexFileAndCommit)
+    {
+        std::vector<uint8_t> host((size_t)m->bytes);
+        if (m->bytes) HIP_TRY(hipMemcpy(host.data(), m->data.p, (size_t)m->bytes, hipMemcpyDeviceToHost));
+        SGX_TRY(write_all(data_tmp.c_str(), host.data(), host.size()));
+    }
+    std::vector<int64_t> existing;
+    if (check_index_and_data(index_path, data_path, s->R, existing)) {
+        // another attempt already committed: use its lengths, drop our data
+        unlink(data_tmp.c_str());
+        if (out_lengths) std::memcpy(out_lengths, existing.data(), sizeof(int64_t) * existing.size());
+        return SGX_OK;
+    }
+    std::vector<uint8_t> idx((size_t)(s->R + 1) * 8);
+    int64_t off = 0;
+    for (int32_t i = 0; i <= s->R; ++i) {
+        if (i > 0) off += m->lengths[(size_t)i - 1];
+        uint64_t u = (uint64_t)off;
+        for (int b = 7; b >= 0; --b) { idx[(size_t)i * 8 + (size_t)b] = (uint8_t)(u & 0xFF); u >>= 8; }
+    }
+    int rc = write_all(index_tmp.c_str(), idx.data(), idx.size());
+    if (rc) { unlink(data_tmp.c_str()); return rc; }
+    unlink(index_path);
+    unlink(data_path);
+    if (rename(index_tmp.c_str(), index_path) != 0) {
+        unlink(index_tmp.c_str());
+        unlink(data_tmp.c_str());
+        return fail(SGX_ERR_IO, "fail to rename file %s to %s", index_tmp.c_str(), index_path);
+    }
+    if (rename(data_tmp.c_str(), data_path) != 0) {
+        unlink(data_tmp.c_str());
+        return fail(SGX_ERR_IO, "fail to rename file %s to %s", data_tmp.c_str(), data_path);
+    }
+    if (out_lengths) std::memcpy(out_lengths, m->lengths.data(), sizeof(int64_t) * (size_t)s->R);
+    return SGX_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// exchange planning (pure host)
+// ------------------------------------------------------------------------------------
+extern "C" int32_t sgx_reducer_owner(int32_t r, int32_t R, int32_t P) {
+    return (int32_t)(((int64_t)r * P) / R);
+}
+
+static void my_reducers(int32_t R, int32_t P, int32_t rank, int32_t *r0, int32_t *r1) {
+    // owner(r) = floor(r*P/R) is monotone: [r0, r1) = { r : owner(r) == rank }
+    int32_t lo = (int32_t)(((int64_t)rank * R + P - 1) / P);
+    int32_t hi = (int32_t)(((int64_t)(rank + 1) * R + P - 1) / P);
+    *r0 = std::min(lo, R);
+    *r1 = std::min(hi, R);
+}
+
+extern "C" int sgx_plan_exchange(const int64_t *L, int32_t P, int32_t R, int32_t rank, int64_t item_bytes,
+                                 int64_t *send_counts, int64_t *send_displs, int64_t *recv_counts,
+                                 int64_t *recv_displs, int64_t *items, int64_t *n_items) {
+    if (!L || P < 1 || R < 1 || rank < 0 || rank >= P || !send_counts || !send_displs || !recv_counts ||
+        !recv_displs || !n_items)
+        return fail(SGX_ERR_INVALID, "sgx_plan_exchange: bad arguments");
+    const int64_t *mine = L + (int64_t)rank * R;
+    for (int32_t j = 0; j < P; ++j) send_counts[j] = 0;
+    for (int32_t r = 0; r < R; ++r) send_counts[sgx_reducer_owner(r, R, P)] += mine[r];
+    int64_t run = 0;
+    for (int32_t j = 0; j < P; ++j) { send_displs[j] = run; run += send_counts[j]; }
+    int32_t r0, r1;
+    my_reducers(R, P, rank, &r0, &r1);
+    run = 0;
+    for (int32_t sidx = 0; sidx < P; ++sidx) {
+        int64_t c = 0;
+        for (int32_t r = r0; r < r1; ++r) c += L[(int64_t)sidx * R + r];
+        recv_counts[sidx] = c;
+        recv_displs[sidx] = run;
+        run += c;
+    }
+    const int64_t cap = *n_items;
+    int64_t cnt = 0, dst = 0;
+    std::vector<int64_t> src_run(recv_displs, recv_displs + P);
+    for (int32_t r = r0; r < r1; ++r) {
+        for (int32_t sidx = 0; sidx < P; ++sidx) {
+            int64_t len = L[(int64_t)sidx * R + r];
+            int64_t so = src_run[(size_t)sidx];
+            src_run[(size_t)sidx] += len;
+            while (len > 0) {
+                const int64_t piece = (item_bytes > 0 && len > item_bytes) ? item_bytes : len;
+                if (items && cnt < cap) {
+                    items[3 * cnt] = so;
+                    items[3 * cnt + 1] = dst;
+                    items[3 * cnt + 2] = piece;
+                }
+                ++cnt;
+                so += piece;
+                dst += piece;
+                len -= piece;
+            }
+        }
+    }
+    *n_items = cnt;
+    if (items && cnt > cap) return fail(SGX_ERR_INVALID, "item capacity %lld < %lld", (long long)cap, (long long)cnt);
+    return SGX_OK;
+}
+
+extern "C" int sgx_copy_items(sgx_engine *e, const void *src, void *dst, const int64_t *items,
+                              int64_t n_items, int32_t align) {
+    if (!e || n_items < 0 || (n_items > 0 && (!items || !src || !dst)) || (align != 4 && align != 16))
+        return fail(SGX_ERR_INVALID, "sgx_copy_items: bad arguments");
+    for (int64_t i = 0; i < n_items; ++i)
+        if (items[3 * i] % align || items[3 * i + 1] % align || items[3 * i + 2] % align || items[3 * i + 2] < 0)
+            return fail(SGX_ERR_INVALID, "sgx_copy_items: item %lld not %d-byte aligned", (long long)i, align);
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    if (n_items == 0) return SGX_OK;
+    DevBuf d;
+    SGX_TRY(d.ensure((size_t)n_items * 24));
+    HIP_TRY(hipMemcpyAsync(d.p, items, (size_t)n_items * 24, hipMemcpyHostToDevice, e->s_comp));
+    HIP_TRY(launch_copy_items(src, dst, (const int64_t *)d.p, n_items, align, e->s_comp));
+    HIP_TRY(hipStreamSynchronize(e->s_comp));
+    d.release();
+    return SGX_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// RCCL exchange
+// ------------------------------------------------------------------------------------
+extern "C" int sgx_get_unique_id(uint8_t out_id[128]) {
+    if (!out_id) return fail(SGX_ERR_INVALID, "NULL id");
+    ncclUniqueId id;
+    NCCL_TRY(ncclGetUniqueId(&id));
+    std::memcpy(out_id, id.internal, 128);
+    return SGX_OK;
+}
+
+extern "C" int sgx_comm_init(sgx_engine *e, int32_t nranks, int32_t rank, const uint8_t id[128]) {
+    if (!e || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail(SGX_ERR_INVALID, "bad arguments");
+    std::lock_guard<std::mutex> lk(e->mu);
+    if (e->comm) return fail(SGX_ERR_STATE, "communicator already initialised");
+    HIP_TRY(hipSetDevice(e->device));
+    ncclUniqueId uid;
+    std::memcpy(uid.internal, id, 128);
+    NCCL_TRY(ncclCommInitRank(&e->comm, nranks, uid, rank));
+    e->nranks = nranks;
+    e->rank = rank;
+    return SGX_OK;
+}
+
+extern "C" int sgx_comm_size(sgx_engine *e, int32_t *nranks, int32_t *rank) {
+    if (!e || !nranks || !rank) return fail(SGX_ERR_INVALID, "NULL argument");
+    *nranks = e->nranks;
+    *rank = e->rank;
+    return SGX_OK;
+}
+
+static constexpr int64_t ITEM_BYTES = 64 * 1024;
+
+extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
+    if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    Shuffle *s;
+    MapOut *m;
+    SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
+    HIP_TRY(hipSetDevice(e->device));
+    SGX_TRY(finish_lengths(*s, *m));
+    const int32_t P = e->nranks, R = s->R;
+    std::unique_ptr<Round> rd(new Round());
+    rd->map_ids.assign((size_t)P, 0);
+    rd->lens.assign((size_t)P * R, 0);
+    my_reducers(R, P, e->rank, &rd->r0, &rd->r1);
+    const int32_t nmine = rd->r1 - rd->r0;
+    HIP_TRY(hipEventCreateWithFlags(&rd->done, hipEventDisableTiming));
+    if (P == 1 && !e->comm) {
+        rd->map_ids[0] = map_id;
+        std::memcpy(rd->lens.data(), m->lengths.data(), sizeof(int64_t) * (size_t)R);
+        rd->block_off.assign((size_t)nmine, 0);
+        int64_t off = 0;
+        for (int32_t r = 0; r < R; ++r) { rd->block_off[(size_t)r] = off; off += m->lengths[(size_t)r]; }
+        rd->alias = m->data.p;
+        HIP_TRY(hipEventRecord(rd->done, e->s_comp));
+        for (auto it = s->rounds.begin(); it != s->rounds.end(); ++it)
+            if ((*it)->map_ids == rd->map_ids) { free_round(**it); s->rounds.erase(it); break; }
+        s->rounds.push_back(std::move(rd));
+        return SGX_OK;
+    }
+    if (!e->comm) return fail(SGX_ERR_STATE, "sgx_comm_init was not called (world of %d ranks)", P);
+    hipStream_t st = e->s_comm;
+    // (1) counts exchange: all-gather {map_id, lengths[R]}
+    const size_t row = (size_t)R + 1;
+    SGX_TRY(e->ag_host.ensure(row * 8 * (size_t)(P + 1)));
+    int64_t *agh = (int64_t *)e->ag_host.p;
+    agh[0] = map_id;
+    std::memcpy(agh + 1, m->lengths.data(), sizeof(int64_t) * (size_t)R);
+    SGX_TRY(e->ag_send.ensure(row * 8));
+    SGX_TRY(e->ag_recv.ensure(row * 8 * (size_t)P));
+    hipEvent_t a0 = e->ev(), a1 = e->ev(), a2 = e->ev(), a3 = e->ev();
+    HIP_TRY(hipEventRecord(a0, st));
+    HIP_TRY(hipMemcpyAsync(e->ag_send.p, agh, row * 8, hipMemcpyHostToDevice, st));
+    NCCL_TRY(ncclAllGather(e->ag_send.p, e->ag_recv.p, row, ncclInt64, e->comm, st));
+    HIP_TRY(hipMemcpyAsync(agh + row, e->ag_recv.p, row * 8 * (size_t)P, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipEventRecord(a1, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int32_t j = 0; j < P; ++j) {
+        rd->map_ids[(size_t)j] = agh[row * (size_t)(j + 1)];
+        std::memcpy(&rd->lens[(size_t)j * R], agh + row * (size_t)(j + 1) + 1, sizeof(int64_t) * (size_t)R);
+    }
+    // (2) plan
+    std::vector<int64_t> sc(P), sd(P), rc(P), rdp(P);
+    int64_t nitems = 0;
+    SGX_TRY(sgx_plan_exchange(rd->lens.data(), P, R, e->rank, ITEM_BYTES, sc.data(), sd.data(), rc.data(),
+                              rdp.data(), nullptr, &nitems));
+    rd->items.assign((size_t)(nitems > 0 ? nitems : 1) * 3, 0);
+    int64_t cap = nitems;
+    SGX_TRY(sgx_plan_exchange(rd->lens.data(), P, R, e->rank, ITEM_BYTES, sc.data(), sd.data(), rc.data(),
+                              rdp.data(), rd->items.data(), &cap));
+    int64_t total_recv = 0;
+    for (int32_t j = 0; j < P; ++j) total_recv += rc[(size_t)j];
+    rd->block_off.assign((size_t)P * nmine, 0);
+    {
+        int64_t off = 0;
+        for (int32_t r = rd->r0; r < rd->r1; ++r)
+            for (int32_t j = 0; j < P; ++j) {
+                rd->block_off[(size_t)j * nmine + (size_t)(r - rd->r0)] = off;
+                off += rd->lens[(size_t)j * R + r];
+            }
+    }
+    // A round with the same source maps replaces the previous one (a re-attempt): reuse
+    // its HBM once every reader of it has finished.
+    for (auto it = s->rounds.begin(); it != s->rounds.end(); ++it) {
+        if ((*it)->map_ids == rd->map_ids) {
+            if ((*it)->done) HIP_TRY(hipEventSynchronize((*it)->done));
+            std::swap(rd->data, (*it)->data);
+            free_round(**it);
+            s->rounds.erase(it);
+            break;
+        }
+    }
+    // (3) all-to-all of the partition-contiguous map output (already destination-grouped)
+    SGX_TRY(e->recv.ensure((size_t)total_recv));
+    SGX_TRY(rd->data.ensure((size_t)total_recv));
+    HIP_TRY(hipStreamWaitEvent(st, m->done, 0));
+    std::vector<size_t> scz(P), sdz(P), rcz(P), rdz(P);
+    for (int32_t j = 0; j < P; ++j) {
+        scz[(size_t)j] = (size_t)sc[(size_t)j];
+        sdz[(size_t)j] = (size_t)sd[(size_t)j];
+        rcz[(size_t)j] = (size_t)rc[(size_t)j];
+        rdz[(size_t)j] = (size_t)rdp[(size_t)j];
+    }
+    HIP_TRY(hipEventRecord(a2, st));
+    NCCL_TRY(ncclAllToAllv(m->data.p, scz.data(), sdz.data(), e->recv.p, rcz.data(), rdz.data(), ncclUint8,
+                           e->comm, st));
+    HIP_TRY(hipEventRecord(a3, st));
+    // (4) regroup (src, reducer) -> (reducer, src)
+    SGX_TRY(e->items_dev.ensure((size_t)(nitems > 0 ? nitems : 1) * 24));
+    hipEvent_t a3b = e->ev(), a4 = e->ev();
+    HIP_TRY(hipEventRecord(a3b, st));
+    if (nitems > 0) {
+        HIP_TRY(hipMemcpyAsync(e->items_dev.p, rd->items.data(), (size_t)nitems * 24, hipMemcpyHostToDevice, st));
+        HIP_TRY(launch_copy_items(e->recv.p, rd->data.p, (const int64_t *)e->items_dev.p, nitems,
+                                  (s->rb % 16 == 0) ? 16 : 4, st));
+    }
+    HIP_TRY(hipEventRecord(a4, st));
+    HIP_TRY(hipEventRecord(rd->done, st));
+    record_stage(e, SGX_STAGE_ALLGATHER, a0, a1);
+    record_stage(e, SGX_STAGE_ALLTOALL, a2, a3);
+    record_stage(e, SGX_STAGE_REGROUP, a3b, a4);
+    s->rounds.push_back(std::move(rd));
+    return SGX_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// fetchBlocksByBlockIds
+// ------------------------------------------------------------------------------------
+extern "C" int sgx_fetch_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids,
+                                const int32_t *reduce_ids, int64_t n, void *dst, int64_t dst_cap,
+                                int32_t dst_mem_kind, int64_t *out_lengths) {
+    if (!e || (n > 0 && (!map_ids || !reduce_ids || !out_lengths)))
+        return fail(SGX_ERR_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    auto it = e->shuffles.find(shuffle_id);
+    if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
+    Shuffle &s = it->second;
+    HIP_TRY(hipSetDevice(e->device));
+    struct Src { const void *p; int64_t len; hipEvent_t ready; };
+    std::vector<Src> srcs((size_t)n);
+    int64_t total = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t mid = map_ids[i];
+        const int32_t r = reduce_ids[i];
+        if (r < 0 || r >= s.R) return fail(SGX_ERR_INVALID, "reduceId %d out of range [0, %d)", r, s.R);
+        bool found = false;
+        // received blocks (newest round first)
+        for (auto rt = s.rounds.rbegin(); rt != s.rounds.rend() && !found; ++rt) {
+            Round &rd = **rt;
+            if (r < rd.r0 || r >= rd.r1) continue;
+            for (size_t j = 0; j < rd.map_ids.size(); ++j) {
+                if (rd.map_ids[j] != mid) continue;
+                const int32_t nmine = rd.r1 - rd.r0;
+                srcs[(size_t)i] = Src{(const char *)rd.base() + rd.block_off[j * (size_t)nmine + (size_t)(r - rd.r0)],
+                                      rd.lens[j * (size_t)s.R + (size_t)r], rd.done};
+                found = true;
+                break;
+            }
+        }
+        if (!found) {
+            auto mt = s.maps.find(mid);
+            if (mt != s.maps.end()) {
+                MapOut &m = *mt->second;
+                SGX_TRY(finish_lengths(s, m));
+                int64_t off = 0;
+                for (int32_t q = 0; q < r; ++q) off += m.lengths[(size_t)q];
+                srcs[(size_t)i] = Src{(const char *)m.data.p + off, m.lengths[(size_t)r], m.done};
+                found = true;
+            }
+        }
+        if (!found)
+            return fail(SGX_ERR_NOT_FOUND, "shuffle_%d_%lld_%d is not registered", shuffle_id, (long long)mid, r);
+        out_lengths[i] = srcs[(size_t)i].len;
+        total += srcs[(size_t)i].len;
+    }
+    if (total > dst_cap)
+        return fail(SGX_ERR_INVALID, "destination capacity %lld < %lld bytes", (long long)dst_cap, (long long)total);
+    if (total > 0 && !dst) return fail(SGX_ERR_INVALID, "dst is NULL");
+    hipStream_t st = e->s_comp;
+    hipMemcpyKind kind = dst_mem_kind == SGX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
+    int64_t off = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (srcs[(size_t)i].ready) HIP_TRY(hipStreamWaitEvent(st, srcs[(size_t)i].ready, 0));
+        if (srcs[(size_t)i].len > 0)
+            HIP_TRY(hipMemcpyAsync((char *)dst + off, srcs[(size_t)i].p, (size_t)srcs[(size_t)i].len, kind, st));
+        off += srcs[(size_t)i].len;
+    }
+    HIP_TRY(hipStreamSynchronize(st));
+    return SGX_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// progress / sync / stats
+// ------------------------------------------------------------------------------------
+extern "C" int sgx_progress(sgx_engine *e) {
+    if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
+    hipError_t a = hipStreamQuery(e->s_comp), b = hipStreamQuery(e->s_comm);
+    if ((a != hipSuccess && a != hipErrorNotReady) || (b != hipSuccess && b != hipErrorNotReady))
+        return fail(SGX_ERR_HIP, "stream error: %s / %s", hipGetErrorString(a), hipGetErrorString(b));
+    return (a == hipSuccess && b == hipSuccess) ? 1 : 0;
+}
+
+extern "C" int sgx_sync(sgx_engine *e) {
+    if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipStreamSynchronize(e->s_comp));
+    HIP_TRY(hipStreamSynchronize(e->s_comm));
+    for (auto &kv : e->shuffles)
+        for (auto &m : kv.second.maps) SGX_TRY(finish_lengths(kv.second, *m.second));
+    return SGX_OK;
+}
+
+extern "C" int sgx_stats_reset(sgx_engine *e) {
+    if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->resolve_stats();
+    for (int i = 0; i < SGX_NUM_STAGES; ++i) { e->stage_ms[i] = 0; e->stage_n[i] = 0; }
+    return SGX_OK;
+}
+
+extern "C" int sgx_stats_get(sgx_engine *e, double *ms, int64_t *cnt) {
+    if (!e || !ms || !cnt) return fail(SGX_ERR_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    e->resolve_stats();
+    for (int i = 0; i < SGX_NUM_STAGES; ++i) { ms[i] = e->stage_ms[i]; cnt[i] = e->stage_n[i]; }
+    return SGX_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// generators and memory helpers
+// ------------------------------------------------------------------------------------
+extern "C" int sgx_gen_uniform16(sgx_engine *e, void *dst, int64_t n, uint64_t seed, int64_t vbase) {
+    if (!e || (n > 0 && !dst)) return fail(SGX_ERR_INVALID, "bad arguments");
+    HIP_TRY(hipSetDevice(e->device));
+    if (n > 0) HIP_TRY(launch_gen_uniform16(dst, n, seed, vbase, e->s_comp));
+    HIP_TRY(hipStreamSynchronize(e->s_comp));
+    return SGX_OK;
+}
+
+extern "C" int sgx_gen_zipf16(sgx_engine *e, void *dst, int64_t n, uint64_t seed, int64_t vbase,
+                              const double *cdf_host, int64_t K) {
+    if (!e || (n > 0 && !dst) || !cdf_host || K < 1) return fail(SGX_ERR_INVALID, "bad arguments");
+    HIP_TRY(hipSetDevice(e->device));
+    DevBuf cdf;
+    SGX_TRY(cdf.ensure((size_t)K * 8));
+    HIP_TRY(hipMemcpy(cdf.p, cdf_host, (size_t)K * 8, hipMemcpyHostToDevice));
+    if (n > 0) HIP_TRY(launch_gen_zipf16(dst, n, seed, vbase, (const double *)cdf.p, K, e->s_comp));
+    HIP_TRY(hipStreamSynchronize(e->s_comp));
+    cdf.release();
+    return SGX_OK;
+}
+
+extern "C" int sgx_gen_terasort100(sgx_engine *e, void *dst, int64_t n, uint64_t seed, int64_t ibase) {
+    if (!e || (n > 0 && !dst)) return fail(SGX_ERR_INVALID, "bad arguments");
+    HIP_TRY(hipSetDevice(e->device));
+    if (n > 0) HIP_TRY(launch_gen_terasort100(dst, n, seed, ibase, e->s_comp));
+    HIP_TRY(hipStreamSynchronize(e->s_comp));
+    return SGX_OK;
+}
+
+extern "C" int sgx_device_alloc(sgx_engine *e, int64_t bytes, void **out) {
+    if (!e || !out || bytes < 0) return fail(SGX_ERR_INVALID, "bad arguments");
+    HIP_TRY(hipSetDevice(e->device));
+    hipError_t er = hipMalloc(out, (size_t)(bytes ? bytes : 16));
+    if (er != hipSuccess) return fail(SGX_ERR_NOMEM, "hipMalloc(%lld): %s", (long long)bytes, hipGetErrorString(er));
+    return SGX_OK;
+}
+
+extern "C" int sgx_device_free(sgx_engine *e, void *p) {
+    if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
+    HIP_TRY(hipSetDevice(e->device));
+    if (p) HIP_TRY(hipFree(p));
+    return SGX_OK;
+}
+
+extern "C" int sgx_memcpy(sgx_engine *e, void *dst, const void *src, int64_t bytes) {
+    if (!e || bytes < 0) return fail(SGX_ERR_INVALID, "bad arguments");
+    HIP_TRY(hipSetDevice(e->device));
+    if (bytes > 0) HIP_TRY(hipMemcpy(dst, src, (size_t)bytes, hipMemcpyDefault));
+    return SGX_OK;
+}

@@ -1,0 +1,58 @@
+// sgx_internal.h — shared between the HIP kernels (sgx_kernels.hip) and the engine
+// (sgx_engine.cpp).  Not part of the public ABI (that is include/sgx.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace sgx {
+
+// Partitioner description as seen by the kernels (built by the engine from the shuffle's
+// registration; see sgx_engine.cpp make_part_params).
+struct PartParams {
+    int32_t kind;        // SGX_PART_*
+    uint32_t R;          // number of partitions
+    uint64_t fm_M;       // Lemire fastmod magic for R: floor((2^64-1)/R) + 1
+    uint32_t c31;        // 2^31 mod R (HashPartitioner's signed-int correction)
+    uint32_t nbits;      // bits needed to hold a partition id (ceil log2 R), >= 1
+    int32_t nb;          // range bounds count (R - 1)
+    int32_t ascending;   // RangePartitioner.ascending
+    const void *bounds;  // device: int64[nb] (RANGE_I64) or Key10[nb] (RANGE_BYTES10)
+};
+
+// 10-byte unsigned-lexicographic key, pre-split so tuple compare == byte compare.
+struct Key10 {
+    uint64_t hi;  // bytes 0..7 big-endian
+    uint32_t lo;  // bytes 8..9 big-endian (<< 0)
+    uint32_t pad;
+};
+
+// Tile geometry of the LDS-staged scatter (records per tile) for a partition count.
+struct ScatterGeom {
+    int waves;
+    int items;  // records per lane per tile
+    int tile;   // waves * items * 64
+    size_t lds_bytes;
+};
+ScatterGeom scatter_geom16(uint32_t R);
+ScatterGeom scatter_geom_wide(uint32_t R, int record_bytes);
+
+// Launchers (all asynchronous on `stream`).  counts / offs are [R][G] partition-major.
+hipError_t launch_hist(const void *in, int64_t n, int record_bytes, int64_t chunk, int G,
+                       const PartParams &pp, uint32_t *counts, hipStream_t stream);
+hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint64_t *status,
+                       uint32_t *ticket_err, uint32_t *part_off, int G, int R,
+                       hipStream_t stream);
+int64_t scan_tiles(int64_t len);
+hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes, int64_t chunk,
+                          int G, const PartParams &pp, const uint32_t *offs, hipStream_t stream);
+// items: [n][3] int64 {src_off, dst_off, bytes}; all offsets/bytes multiples of `align`.
+hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, int64_t n_items,
+                             int align, hipStream_t stream);
+hipError_t launch_gen_uniform16(void *dst, int64_t n, uint64_t seed, int64_t value_base,
+                                hipStream_t stream);
+hipError_t launch_gen_zipf16(void *dst, int64_t n, uint64_t seed, int64_t value_base,
+                             const double *cdf, int64_t K, hipStream_t stream);
+hipError_t launch_gen_terasort100(void *dst, int64_t n, uint64_t seed, int64_t index_base,
+                                  hipStream_t stream);
+
+}  // namespace sgx

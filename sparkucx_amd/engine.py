@@ -1,0 +1,261 @@
+"""Thin object wrapper over the C ABI (one ShuffleEngine per GPU = per executor).
+
+Buffers accepted wherever records go in or blocks come out:
+  * ``numpy.ndarray`` (host memory)            -> SGX_MEM_HOST
+  * ``DeviceBuffer`` (allocated by the engine) -> SGX_MEM_DEVICE
+  * any object with ``data_ptr()`` and ``is_cuda`` (a torch tensor on ``cuda:N``)
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Optional, Sequence, Tuple
+
+import numpy as np
+
+from . import _lib
+from ._lib import MEM_DEVICE, MEM_HOST, check, lib
+
+
+class DeviceBuffer:
+    """HBM allocation owned by the engine's device (freed by ``free()`` or GC)."""
+
+    def __init__(self, engine: "ShuffleEngine", nbytes: int):
+        self.engine = engine
+        self.nbytes = int(nbytes)
+        p = ctypes.c_void_p()
+        check(lib().sgx_device_alloc(engine.handle, self.nbytes, ctypes.byref(p)), "sgx_device_alloc")
+        self.ptr = int(p.value)
+
+    def free(self):
+        if self.ptr and self.engine.handle:
+            check(lib().sgx_device_free(self.engine.handle, self.ptr), "sgx_device_free")
+        self.ptr = 0
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+    def to_numpy(self, nbytes: Optional[int] = None, offset: int = 0) -> np.ndarray:
+        n = self.nbytes - offset if nbytes is None else int(nbytes)
+        out = np.empty(n, dtype=np.uint8)
+        if n:
+            check(lib().sgx_memcpy(self.engine.handle, out.ctypes.data, self.ptr + offset, n), "sgx_memcpy")
+        return out
+
+    def copy_from(self, arr: np.ndarray, offset: int = 0):
+        arr = np.ascontiguousarray(arr)
+        if arr.nbytes + offset > self.nbytes:
+            raise _lib.IllegalArgumentException("copy_from overflows the device buffer")
+        if arr.nbytes:
+            check(lib().sgx_memcpy(self.engine.handle, self.ptr + offset, arr.ctypes.data, arr.nbytes), "sgx_memcpy")
+
+
+def buffer_arg(buf) -> Tuple[int, int, int]:
+    """(pointer, nbytes, mem_kind) of a records/destination buffer."""
+    if isinstance(buf, DeviceBuffer):
+        return buf.ptr, buf.nbytes, MEM_DEVICE
+    if isinstance(buf, np.ndarray):
+        if not buf.flags["C_CONTIGUOUS"]:
+            raise _lib.IllegalArgumentException("host buffers must be C-contiguous")
+        return buf.ctypes.data, buf.nbytes, MEM_HOST
+    if hasattr(buf, "data_ptr") and getattr(buf, "is_cuda", False):
+        if not buf.is_contiguous():
+            raise _lib.IllegalArgumentException("device tensors must be contiguous")
+        return int(buf.data_ptr()), int(buf.numel() * buf.element_size()), MEM_DEVICE
+    raise _lib.IllegalArgumentException(f"unsupported buffer type {type(buf)!r}")
+
+
+@dataclass
+class StageStats:
+    ms: dict
+    count: dict
+
+
+class ShuffleEngine:
+    """One engine per GPU: owns the HIP streams, work buffers, map outputs in HBM and the
+    RCCL communicator (the role CommonUcxShuffleManager.startUcxTransport plays,
+    shuffle/ucx/CommonUcxShuffleManager.scala:67-100)."""
+
+    def __init__(self, device: int = 0, num_chunks: int = 0):
+        cfg = (ctypes.c_int32 * 4)(device, num_chunks, 0, 0)
+        h = ctypes.c_void_p()
+        check(lib().sgx_create(ctypes.cast(cfg, ctypes.c_void_p), ctypes.byref(h)), "sgx_create")
+        self.handle = h.value
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            lib().sgx_destroy(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- shuffle registry -------------------------------------------------------------
+    def register_shuffle(self, shuffle_id: int, num_partitions: int, kind: int = _lib.PART_HASH,
+                         bounds=None, ascending: bool = True, record_bytes: int = 16):
+        ptr, nb = None, 0
+        keep = None
+        if bounds is not None and kind != _lib.PART_HASH:
+            if kind == _lib.PART_RANGE_I64:
+                keep = np.ascontiguousarray(bounds, dtype=np.int64)
+                nb = keep.shape[0]
+            else:
+                keep = np.ascontiguousarray(bounds, dtype=np.uint8).reshape(-1, 10)
+                nb = keep.shape[0]
+            ptr = keep.ctypes.data if nb else None
+        check(lib().sgx_register_shuffle(self.handle, shuffle_id, num_partitions, kind, ptr, nb,
+                                         int(bool(ascending)), record_bytes), "registerShuffle")
+
+    def unregister_shuffle(self, shuffle_id: int):
+        check(lib().sgx_unregister_shuffle(self.handle, shuffle_id), "unregisterShuffle")
+
+    # -- map side -----------------------------------------------------------------------
+    def write_map(self, shuffle_id: int, map_id: int, records, nrecords: int, record_bytes: int,
+                  num_partitions: Optional[int] = None) -> Optional[np.ndarray]:
+        """Partition + scatter one map batch on the GPU. Returns per-partition byte lengths
+        when ``num_partitions`` is given (synchronous), else None (asynchronous)."""
+        ptr, nbytes, kind = buffer_arg(records)
+        if nrecords * record_bytes > nbytes:
+            raise _lib.IllegalArgumentException(
+                f"{nrecords} records of {record_bytes} B exceed the {nbytes} B buffer")
+        out = None
+        out_ptr = None
+        if num_partitions is not None:
+            out = np.empty(num_partitions, dtype=np.int64)
+            out_ptr = out.ctypes.data
+        check(lib().sgx_write_map(self.handle, shuffle_id, map_id, ptr, nrecords, record_bytes, kind,
+                                  out_ptr), "write_map")
+        return out
+
+    def map_lengths(self, shuffle_id: int, map_id: int, num_partitions: int) -> np.ndarray:
+        out = np.empty(num_partitions, dtype=np.int64)
+        check(lib().sgx_map_lengths(self.handle, shuffle_id, map_id, out.ctypes.data), "map_lengths")
+        return out
+
+    def map_data(self, shuffle_id: int, map_id: int) -> Tuple[int, int]:
+        p = ctypes.c_void_p()
+        n = ctypes.c_int64()
+        check(lib().sgx_map_data(self.handle, shuffle_id, map_id, ctypes.byref(p), ctypes.byref(n)), "map_data")
+        return int(p.value or 0), int(n.value)
+
+    def map_output_bytes(self, shuffle_id: int, map_id: int) -> np.ndarray:
+        ptr, n = self.map_data(shuffle_id, map_id)
+        out = np.empty(n, dtype=np.uint8)
+        if n:
+            check(lib().sgx_memcpy(self.handle, out.ctypes.data, ptr, n), "sgx_memcpy")
+        return out
+
+    def write_index(self, shuffle_id: int, map_id: int, index_path: str, data_path: str,
+                    num_partitions: int) -> np.ndarray:
+        out = np.empty(num_partitions, dtype=np.int64)
+        check(lib().sgx_write_index(self.handle, shuffle_id, map_id, index_path.encode(),
+                                    data_path.encode(), out.ctypes.data), "writeIndexFileAndCommit")
+        return out
+
+    # -- exchange / fetch -----------------------------------------------------------------
+    def comm_init(self, nranks: int, rank: int, unique_id: bytes):
+        if len(unique_id) != 128:
+            raise _lib.IllegalArgumentException("unique id must be 128 bytes")
+        buf = ctypes.create_string_buffer(bytes(unique_id), 128)
+        check(lib().sgx_comm_init(self.handle, nranks, rank, ctypes.cast(buf, ctypes.c_void_p)), "comm_init")
+
+    def exchange(self, shuffle_id: int, map_id: int):
+        check(lib().sgx_exchange(self.handle, shuffle_id, map_id), "exchange")
+
+    def fetch_blocks(self, shuffle_id: int, map_ids: Sequence[int], reduce_ids: Sequence[int], dst=None,
+                     dst_cap: Optional[int] = None):
+        """Copy blocks back to back into ``dst`` (host ndarray, DeviceBuffer or device tensor).
+        With ``dst`` None, a host buffer is sized by a first (length-only) pass.
+        Returns (dst, lengths)."""
+        m = np.ascontiguousarray(map_ids, dtype=np.int64)
+        r = np.ascontiguousarray(reduce_ids, dtype=np.int32)
+        lens = np.empty(len(m), dtype=np.int64)
+        if dst is None:
+            rc = lib().sgx_fetch_blocks(self.handle, shuffle_id, m.ctypes.data, r.ctypes.data, len(m), None, 0,
+                                        MEM_HOST, lens.ctypes.data)
+            if rc not in (0, _lib.SGX_ERR_INVALID):
+                check(rc, "fetchBlocks")
+            dst = np.empty(int(lens.sum()), dtype=np.uint8)
+        ptr, cap, kind = buffer_arg(dst)
+        if dst_cap is not None:
+            cap = dst_cap
+        check(lib().sgx_fetch_blocks(self.handle, shuffle_id, m.ctypes.data, r.ctypes.data, len(m),
+                                     ptr if cap else None, cap, kind, lens.ctypes.data), "fetchBlocks")
+        return dst, lens
+
+    def progress(self) -> bool:
+        return bool(check(lib().sgx_progress(self.handle), "progress"))
+
+    def sync(self):
+        check(lib().sgx_sync(self.handle), "sync")
+
+    def copy_items(self, src: DeviceBuffer, dst: DeviceBuffer, items: np.ndarray, align: int = 16):
+        it = np.ascontiguousarray(items, dtype=np.int64).reshape(-1, 3)
+        check(lib().sgx_copy_items(self.handle, src.ptr, dst.ptr, it.ctypes.data, it.shape[0], align),
+              "copy_items")
+
+    # -- measurement ----------------------------------------------------------------------
+    def stats_reset(self):
+        check(lib().sgx_stats_reset(self.handle), "stats_reset")
+
+    def stats(self) -> StageStats:
+        ms = np.zeros(len(_lib.STAGES), dtype=np.float64)
+        cnt = np.zeros(len(_lib.STAGES), dtype=np.int64)
+        check(lib().sgx_stats_get(self.handle, ms.ctypes.data, cnt.ctypes.data), "stats_get")
+        return StageStats(dict(zip(_lib.STAGES, ms.tolist())), dict(zip(_lib.STAGES, cnt.tolist())))
+
+    # -- synthetic inputs ------------------------------------------------------------------
+    def alloc(self, nbytes: int) -> DeviceBuffer:
+        return DeviceBuffer(self, nbytes)
+
+    def gen_uniform16(self, buf: DeviceBuffer, n: int, seed: int, value_base: int = 0):
+        check(lib().sgx_gen_uniform16(self.handle, buf.ptr, n, seed & (2**64 - 1), value_base), "gen_uniform16")
+
+    def gen_zipf16(self, buf: DeviceBuffer, n: int, seed: int, cdf: np.ndarray, value_base: int = 0):
+        cdf = np.ascontiguousarray(cdf, dtype=np.float64)
+        check(lib().sgx_gen_zipf16(self.handle, buf.ptr, n, seed & (2**64 - 1), value_base, cdf.ctypes.data,
+                                   len(cdf)), "gen_zipf16")
+
+    def gen_terasort100(self, buf: DeviceBuffer, n: int, seed: int, index_base: int = 0):
+        check(lib().sgx_gen_terasort100(self.handle, buf.ptr, n, seed & (2**64 - 1), index_base),
+              "gen_terasort100")
+
+
+def get_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    check(lib().sgx_get_unique_id(ctypes.cast(buf, ctypes.c_void_p)), "get_unique_id")
+    return buf.raw
+
+
+def plan_exchange(lengths_all: np.ndarray, rank: int, item_bytes: int = 0):
+    """Pure-host exchange plan (no GPU): returns (send_counts, send_displs, recv_counts,
+    recv_displs, items[n,3])."""
+    L = np.ascontiguousarray(lengths_all, dtype=np.int64)
+    P, R = L.shape
+    sc, sd, rc, rd = (np.zeros(P, np.int64) for _ in range(4))
+    n = ctypes.c_int64(0)
+    check(lib().sgx_plan_exchange(L.ctypes.data, P, R, rank, item_bytes, sc.ctypes.data, sd.ctypes.data,
+                                  rc.ctypes.data, rd.ctypes.data, None, ctypes.byref(n)), "plan_exchange")
+    items = np.zeros((max(n.value, 1), 3), np.int64)
+    cap = ctypes.c_int64(n.value)
+    check(lib().sgx_plan_exchange(L.ctypes.data, P, R, rank, item_bytes, sc.ctypes.data, sd.ctypes.data,
+                                  rc.ctypes.data, rd.ctypes.data, items.ctypes.data, ctypes.byref(cap)),
+          "plan_exchange")
+    return sc, sd, rc, rd, items[: n.value]
+
+
+def reducer_owner(reduce_id: int, num_partitions: int, nranks: int) -> int:
+    return int(lib().sgx_reducer_owner(reduce_id, num_partitions, nranks))

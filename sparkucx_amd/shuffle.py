@@ -1,0 +1,464 @@
+"""Host-side mirror of SparkUCX's plugin interface for the accelerated path.
+
+Names, argument meaning and error behaviour follow the reference (Spark 3.0 profile,
+/root/reference/src/main/scala/org/apache/spark/...):
+
+  UcxShuffleManager            shuffle/compat/spark_3_0/UcxShuffleManager.scala:25-80
+                               + shuffle/ucx/CommonUcxShuffleManager.scala:25-124
+  GpuShuffleMapOutputWriter    shuffle/ucx/NvkvShuffleMapOutputWriter.scala:75-148
+  UcxShuffleBlockResolver      IndexShuffleBlockResolver.scala:56-262 +
+                               shuffle/ucx/CommonUcxShuffleBlockResolver.scala:37-71
+  UcxShuffleReader             shuffle/compat/spark_3_0/UcxShuffleReader.scala:74-200
+  GpuShuffleTransport          shuffle/ucx/ShuffleTransport.scala:110-167
+
+The data path underneath is the HIP engine (libsgx.so); these classes hold no data and
+compute nothing on the CPU.
+"""
+from __future__ import annotations
+
+import enum
+import os
+import re
+import struct
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence
+
+import numpy as np
+
+from . import _lib
+from ._lib import IllegalArgumentException, IllegalStateException
+from .engine import DeviceBuffer, ShuffleEngine
+
+# ---------------------------------------------------------------------------------------
+# Partitioners / dependency / handle (Spark core types the plugin receives)
+# ---------------------------------------------------------------------------------------
+
+
+@dataclass(frozen=True)
+class HashPartitioner:
+    """org.apache.spark.HashPartitioner: nonNegativeMod(key.hashCode, numPartitions)."""
+
+    numPartitions: int
+    kind: int = _lib.PART_HASH
+
+    def __post_init__(self):
+        if self.numPartitions < 0:
+            raise IllegalArgumentException(
+                f"Number of partitions ({self.numPartitions}) cannot be negative.")
+
+
+@dataclass(frozen=True)
+class RangePartitioner:
+    """org.apache.spark.RangePartitioner with its (already sampled) rangeBounds.
+    ``rangeBounds``: int64 keys, or (n, 10) uint8 TeraSort keys (unsigned lexicographic)."""
+
+    rangeBounds: np.ndarray
+    ascending: bool = True
+
+    @property
+    def kind(self) -> int:
+        b = np.asarray(self.rangeBounds)
+        return _lib.PART_RANGE_BYTES10 if b.dtype == np.uint8 else _lib.PART_RANGE_I64
+
+    @property
+    def numPartitions(self) -> int:
+        b = np.asarray(self.rangeBounds)
+        n = b.shape[0] if b.ndim else 0
+        return n + 1
+
+
+@dataclass
+class ShuffleDependency:
+    partitioner: object
+    recordBytes: int = 16  # fixed-width record codec: 16 B (Long, Long) or 100 B TeraSort
+
+
+@dataclass
+class BaseShuffleHandle:
+    shuffleId: int
+    dependency: ShuffleDependency
+
+
+@dataclass
+class MapStatus:
+    mapId: int
+    partitionLengths: np.ndarray  # bytes per reduce partition
+
+
+# ---------------------------------------------------------------------------------------
+# Transport contract (ShuffleTransport.scala)
+# ---------------------------------------------------------------------------------------
+
+
+class OperationStatus(enum.Enum):
+    SUCCESS = 0
+    CANCELED = 1
+    FAILURE = 2
+
+
+@dataclass
+class MemoryBlock:
+    """ShuffleTransport.scala:15-20. The receiver owns it and must close() it."""
+
+    address: int
+    size: int
+    isHostMemory: bool = True
+    _owner: object = None
+    _on_close: Optional[Callable[[], None]] = None
+
+    def close(self):
+        if self._on_close is not None:
+            self._on_close()
+            self._on_close = None
+
+
+@dataclass(frozen=True)
+class UcxShuffleBlockId:
+    """UcxShuffleTransport.scala:55-72: serialized as [mapId:i32][reduceId:i32]; the
+    shuffleId is not on the wire (it decodes as 0)."""
+
+    shuffleId: int
+    mapId: int
+    reduceId: int
+    serializedSize: int = 8
+
+    def serialize(self) -> bytes:
+        return struct.pack(">ii", _to_i32(self.mapId), _to_i32(self.reduceId))
+
+    @staticmethod
+    def deserialize(buf: bytes) -> "UcxShuffleBlockId":
+        m, r = struct.unpack(">ii", buf[:8])
+        return UcxShuffleBlockId(0, m, r)
+
+
+def _to_i32(x: int) -> int:
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x & 0x80000000 else x
+
+
+@dataclass
+class OperationResult:
+    status: OperationStatus
+    data: Optional[MemoryBlock] = None
+    error: Optional[Exception] = None
+
+    def getStatus(self):
+        return self.status
+
+    def getData(self):
+        return self.data
+
+    def getError(self):
+        return self.error
+
+
+@dataclass
+class Request:
+    completed: bool = False
+
+    def isCompleted(self) -> bool:
+        return self.completed
+
+
+class GpuShuffleTransport:
+    """ShuffleTransport backed by the HIP engine: blocks are served from HBM (local map
+    outputs or data received by the RCCL exchange) instead of UCX AM round trips."""
+
+    def __init__(self, engine: ShuffleEngine):
+        self.engine = engine
+        self._pending: List[tuple] = []
+
+    def init(self):
+        return None
+
+    def close(self):
+        self._pending.clear()
+
+    def register(self, blockId, block=None):
+        return None  # map outputs register themselves when written
+
+    def unregister(self, blockId):
+        return None
+
+    def unregisterShuffle(self, shuffleId: int):
+        self.engine.unregister_shuffle(shuffleId)
+
+    def fetchBlocksByBlockIds(self, executorId: int, blockIds: Sequence[UcxShuffleBlockId],
+                              resultBufferAllocator: Callable[[int], MemoryBlock],
+                              callbacks: Sequence[Callable[[OperationResult], None]]) -> List[Request]:
+        """ShuffleTransport.scala:154-156.  Completion is delivered by progress() on the
+        submitting thread, as in the reference (:158-165)."""
+        if len(blockIds) != len(callbacks):
+            raise IllegalArgumentException("blockIds and callbacks differ in length")
+        reqs = []
+        for bid, cb in zip(blockIds, callbacks):
+            r = Request()
+            reqs.append(r)
+            self._pending.append((bid, resultBufferAllocator, cb, r))
+        return reqs
+
+    def progress(self):
+        pending, self._pending = self._pending, []
+        for bid, alloc, cb, req in pending:
+            try:
+                host, lens = self.engine.fetch_blocks(bid.shuffleId, [bid.mapId], [bid.reduceId])
+                mb = alloc(int(lens[0]))
+                if mb.size < int(lens[0]):
+                    raise IllegalStateException("allocator returned a block smaller than requested")
+                if lens[0]:
+                    import ctypes
+                    ctypes.memmove(mb.address, host.ctypes.data, int(lens[0]))
+                req.completed = True
+                cb(OperationResult(OperationStatus.SUCCESS, MemoryBlock(mb.address, int(lens[0]), True,
+                                                                          mb, mb.close)))
+            except _lib.ShuffleError as ex:
+                req.completed = True
+                cb(OperationResult(OperationStatus.FAILURE, None, ex))
+
+
+# ---------------------------------------------------------------------------------------
+# Writer side
+# ---------------------------------------------------------------------------------------
+
+
+class ShufflePartitionWriter:
+    def __init__(self, length: int):
+        self._length = length
+
+    def getNumBytesWritten(self) -> int:
+        return self._length
+
+
+class GpuShuffleMapOutputWriter:
+    """ShuffleMapOutputWriter contract (NvkvShuffleMapOutputWriter.scala:75-148) over a
+    map output already partitioned in HBM: partitions are visited in strictly increasing
+    order (:108) and commitAllPartitions returns the per-partition lengths (:116-148)."""
+
+    def __init__(self, shuffleId: int, mapId: int, lengths: np.ndarray):
+        self.shuffleId, self.mapId = shuffleId, mapId
+        self._lengths = lengths
+        self._last = -1
+
+    def getPartitionWriter(self, reducePartitionId: int) -> ShufflePartitionWriter:
+        if reducePartitionId <= self._last:
+            raise IllegalArgumentException("Partitions should be requested in increasing order.")
+        if not 0 <= reducePartitionId < len(self._lengths):
+            raise IllegalArgumentException(f"partition {reducePartitionId} out of range")
+        self._last = reducePartitionId
+        return ShufflePartitionWriter(int(self._lengths[reducePartitionId]))
+
+    def commitAllPartitions(self) -> np.ndarray:
+        return self._lengths.copy()
+
+    def abort(self, error: BaseException):
+        return None
+
+
+class GpuShuffleWriter:
+    """The ShuffleWriter getWriter returns (UcxShuffleManager.scala:32-53): one write() of a
+    record batch runs partition id -> histogram -> scan -> stable scatter on the GPU."""
+
+    def __init__(self, manager: "UcxShuffleManager", handle: BaseShuffleHandle, mapId: int):
+        self.manager, self.handle, self.mapId = manager, handle, mapId
+        self._status: Optional[MapStatus] = None
+
+    def write(self, records, numRecords: Optional[int] = None):
+        dep = self.handle.dependency
+        rb = dep.recordBytes
+        if numRecords is None:
+            if isinstance(records, np.ndarray):
+                numRecords = records.nbytes // rb
+            elif isinstance(records, DeviceBuffer):
+                numRecords = records.nbytes // rb
+            else:
+                numRecords = records.numel() * records.element_size() // rb
+        R = dep.partitioner.numPartitions
+        lengths = self.manager.engine.write_map(self.handle.shuffleId, self.mapId, records, numRecords, rb, R)
+        self.manager._map_written(self.handle.shuffleId, self.mapId)
+        self._status = MapStatus(self.mapId, lengths)
+
+    def mapOutputWriter(self) -> GpuShuffleMapOutputWriter:
+        if self._status is None:
+            raise IllegalStateException("write() was not called")
+        return GpuShuffleMapOutputWriter(self.handle.shuffleId, self.mapId, self._status.partitionLengths)
+
+    def getPartitionLengths(self) -> np.ndarray:
+        if self._status is None:
+            raise IllegalStateException("write() was not called")
+        return self._status.partitionLengths
+
+    def stop(self, success: bool) -> Optional[MapStatus]:
+        return self._status if success else None
+
+
+# ---------------------------------------------------------------------------------------
+# Index + data layout (IndexShuffleBlockResolver)
+# ---------------------------------------------------------------------------------------
+
+_BLOCK_RE = re.compile(r"^shuffle_(\d+)_(-?\d+)_(\d+)$")
+
+
+def parse_block_id(name: str):
+    """'shuffle_<s>_<m>_<r>' (UcxShuffleClient.scala:64 via BlockId.apply)."""
+    m = _BLOCK_RE.match(name)
+    if not m:
+        raise IllegalArgumentException(f"unexpected shuffle block id format: {name}")
+    return int(m.group(1)), int(m.group(2)), int(m.group(3))
+
+
+class UcxShuffleBlockResolver:
+    """Index/data files in Spark's layout, written from HBM. NOOP_REDUCE_ID = 0 (:271)."""
+
+    NOOP_REDUCE_ID = 0
+
+    def __init__(self, manager: "UcxShuffleManager", root: str):
+        self.manager = manager
+        self.root = root
+        os.makedirs(root, exist_ok=True)
+
+    def getDataFile(self, shuffleId: int, mapId: int) -> str:
+        return os.path.join(self.root, f"shuffle_{shuffleId}_{mapId}_{self.NOOP_REDUCE_ID}.data")
+
+    def getIndexFile(self, shuffleId: int, mapId: int) -> str:
+        return os.path.join(self.root, f"shuffle_{shuffleId}_{mapId}_{self.NOOP_REDUCE_ID}.index")
+
+    def writeIndexFileAndCommit(self, shuffleId: int, mapId: int, lengths: np.ndarray) -> None:
+        """IndexShuffleBlockResolver.scala:161-217; ``lengths`` is updated in place to the
+        committed attempt's lengths (an existing valid attempt wins)."""
+        got = self.manager.engine.write_index(shuffleId, mapId, self.getIndexFile(shuffleId, mapId),
+                                              self.getDataFile(shuffleId, mapId), len(lengths))
+        lengths[:] = got
+
+    def checkIndexAndDataFile(self, index: str, data: str, blocks: int) -> Optional[np.ndarray]:
+        out = np.empty(blocks, dtype=np.int64)
+        rc = _lib.lib().sgx_check_index_and_data(index.encode(), data.encode(), blocks, out.ctypes.data)
+        return out if rc == 0 else None
+
+    def getBlockData(self, blockId) -> bytes:
+        """IndexShuffleBlockResolver.scala:219-262 (ShuffleBlockId or (s, m, start, end))."""
+        if isinstance(blockId, str):
+            s, m, r = parse_block_id(blockId)
+            start, end = r, r + 1
+        elif len(blockId) == 3:
+            s, m, start = blockId
+            end = start + 1
+        elif len(blockId) == 4:
+            s, m, start, end = blockId
+        else:
+            raise IllegalArgumentException(f"unexpected shuffle block id format: {blockId}")
+        import ctypes
+        off, ln = ctypes.c_int64(), ctypes.c_int64()
+        _lib.check(_lib.lib().sgx_index_block_range(self.getIndexFile(s, m).encode(), start, end,
+                                                    ctypes.byref(off), ctypes.byref(ln)), "getBlockData")
+        with open(self.getDataFile(s, m), "rb") as f:
+            f.seek(off.value)
+            return f.read(ln.value)
+
+    def removeDataByMap(self, shuffleId: int, mapId: int):
+        for p in (self.getDataFile(shuffleId, mapId), self.getIndexFile(shuffleId, mapId)):
+            if os.path.exists(p):
+                os.unlink(p)
+
+
+# ---------------------------------------------------------------------------------------
+# Reader
+# ---------------------------------------------------------------------------------------
+
+
+class UcxShuffleReader:
+    """Reads reduce partitions [startPartition, endPartition) (UcxShuffleReader.scala:74-200).
+    Blocks are fetched per (map, reduce) from HBM; the result is returned in the canonical
+    order: reduce partition ascending, then map (source) ascending, map input order inside
+    each block (SURVEY.md §8(a) parity note)."""
+
+    def __init__(self, manager: "UcxShuffleManager", handle: BaseShuffleHandle, startPartition: int,
+                 endPartition: int, mapIds: Optional[Sequence[int]] = None):
+        R = handle.dependency.partitioner.numPartitions
+        if not 0 <= startPartition <= endPartition <= R:
+            raise IllegalArgumentException(f"bad partition range [{startPartition}, {endPartition})")
+        self.manager, self.handle = manager, handle
+        self.start, self.end = startPartition, endPartition
+        self.mapIds = list(mapIds) if mapIds is not None else None
+
+    def read_blocks(self):
+        maps = self.mapIds if self.mapIds is not None else self.manager.known_maps(self.handle.shuffleId)
+        mids, rids = [], []
+        for r in range(self.start, self.end):
+            for m in sorted(maps):
+                mids.append(m)
+                rids.append(r)
+        data, lens = self.manager.engine.fetch_blocks(self.handle.shuffleId, mids, rids)
+        return data, lens, mids, rids
+
+    def read(self) -> np.ndarray:
+        """All records of the partition range as an (n, recordBytes) uint8 array."""
+        data, _, _, _ = self.read_blocks()
+        return data.reshape(-1, self.handle.dependency.recordBytes)
+
+
+# ---------------------------------------------------------------------------------------
+# The manager
+# ---------------------------------------------------------------------------------------
+
+
+class UcxShuffleManager:
+    """spark.shuffle.manager=org.apache.spark.shuffle.UcxShuffleManager, MI355X edition."""
+
+    def __init__(self, conf: Optional[Dict[str, str]] = None, isDriver: bool = False, device: int = 0,
+                 localDir: Optional[str] = None):
+        self.conf = dict(conf or {})
+        self.isDriver = isDriver
+        self.engine = ShuffleEngine(device=device,
+                                    num_chunks=int(self.conf.get("spark.shuffle.ucx.gpu.numChunks", 0)))
+        self.ucxTransport = GpuShuffleTransport(self.engine)
+        root = localDir or self.conf.get("spark.local.dir") or os.path.join(os.getcwd(), "sgx-shuffle")
+        self.shuffleBlockResolver = UcxShuffleBlockResolver(self, root)
+        self._handles: Dict[int, BaseShuffleHandle] = {}
+        self._maps: Dict[int, set] = {}
+
+    def getTransport(self) -> GpuShuffleTransport:
+        return self.ucxTransport
+
+    def registerShuffle(self, shuffleId: int, dependency: ShuffleDependency) -> BaseShuffleHandle:
+        p = dependency.partitioner
+        bounds = getattr(p, "rangeBounds", None)
+        self.engine.register_shuffle(shuffleId, p.numPartitions, p.kind, bounds,
+                                     getattr(p, "ascending", True), dependency.recordBytes)
+        h = BaseShuffleHandle(shuffleId, dependency)
+        self._handles[shuffleId] = h
+        self._maps[shuffleId] = set()
+        return h
+
+    def getWriter(self, handle: BaseShuffleHandle, mapId: int, context=None, metrics=None) -> GpuShuffleWriter:
+        if handle.shuffleId not in self._handles:
+            raise IllegalStateException(f"shuffle {handle.shuffleId} is not registered")
+        return GpuShuffleWriter(self, handle, mapId)
+
+    def getReader(self, handle: BaseShuffleHandle, startPartition: int, endPartition: int, context=None,
+                  metrics=None, mapIds: Optional[Sequence[int]] = None) -> UcxShuffleReader:
+        return UcxShuffleReader(self, handle, startPartition, endPartition, mapIds)
+
+    def exchange(self, handle: BaseShuffleHandle, mapId: int):
+        """Push a local map output to the reducers' owners over RCCL (collective)."""
+        self.engine.exchange(handle.shuffleId, mapId)
+
+    def unregisterShuffle(self, shuffleId: int) -> bool:
+        if shuffleId not in self._handles:
+            return False
+        self.ucxTransport.unregisterShuffle(shuffleId)
+        del self._handles[shuffleId]
+        self._maps.pop(shuffleId, None)
+        return True
+
+    def stop(self):
+        for s in list(self._handles):
+            self.unregisterShuffle(s)
+        self.ucxTransport.close()
+        self.engine.close()
+
+    # bookkeeping for readers without a MapOutputTracker
+    def _map_written(self, shuffleId: int, mapId: int):
+        self._maps.setdefault(shuffleId, set()).add(mapId)
+
+    def known_maps(self, shuffleId: int) -> List[int]:
+        return sorted(self._maps.get(shuffleId, ()))

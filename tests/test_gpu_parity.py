@@ -1,0 +1,403 @@
+"""GPU parity: the HIP path (through the C ABI) against the oracle and the golden fixtures.
+
+Bit-exact bar (integer/byte work): identical partition lengths (=> identical index
+offsets), identical partition-contiguous bytes (=> identical partition ids and per-reducer
+record sequences in input order), identical index/data files."""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+_sid = [1000]
+
+
+def next_sid():
+    _sid[0] += 1
+    return _sid[0]
+
+
+def run_map(engine, recs, R, kind=0, bounds=None, ascending=True, host=True):
+    """Write one map through the C ABI; return (lengths, output bytes as (n, rb))."""
+    import sparkucx_amd as sgx
+
+    rb = recs.shape[1] if recs.ndim == 2 else 16
+    sid = next_sid()
+    engine.register_shuffle(sid, R, kind, bounds, ascending, rb)
+    try:
+        if host:
+            src = np.ascontiguousarray(recs)
+        else:
+            src = engine.alloc(max(recs.nbytes, 16))
+            src.copy_from(recs)
+        n = recs.shape[0]
+        lengths = engine.write_map(sid, 0, src, n, rb, R)
+        out = engine.map_output_bytes(sid, 0).reshape(-1, rb)
+        return lengths, out
+    finally:
+        engine.unregister_shuffle(sid)
+        _ = sgx
+
+
+def check_against_oracle(engine, oracle_lib, recs, R, kind=0, bounds=None, ascending=True, host=True):
+    want_out, want_counts = oracle_lib.map_write(recs, R, kind, bounds, ascending, nthreads=8)
+    lengths, out = run_map(engine, recs, R, kind, bounds, ascending, host)
+    rb = recs.shape[1]
+    assert np.array_equal(lengths, want_counts * rb), "partition lengths / index offsets differ"
+    assert out.shape == want_out.shape
+    if not np.array_equal(out, want_out):
+        bad = np.nonzero(np.any(out != want_out, axis=1))[0]
+        pytest.fail(f"{len(bad)} records differ, first at {bad[:5]}")
+
+
+# ---------------------------------------------------------------- golden fixtures ----
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "hash_*.npz"))))
+def test_golden_hash(engine, path):
+    z = np.load(path)
+    R = int(z["num_partitions"])
+    lengths, out = run_map(engine, z["records"], R)
+    assert np.array_equal(lengths, z["lengths"])
+    assert np.array_equal(out, z["out"])
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "range_*.npz"))))
+def test_golden_range(engine, path):
+    import sparkucx_amd as sgx
+
+    z = np.load(path)
+    R = int(z["num_partitions"])
+    kind = sgx.PART_RANGE_BYTES10 if z["records"].shape[1] == 100 else sgx.PART_RANGE_I64
+    lengths, out = run_map(engine, z["records"], R, kind, z["bounds"], bool(z["ascending"]))
+    assert np.array_equal(lengths, z["lengths"])
+    assert np.array_equal(out, z["out"])
+
+
+# ---------------------------------------------------------------- seeded random ------
+@pytest.mark.parametrize("R", [1, 2, 3, 7, 200, 1000, 1024, 2048, 4096, 5000])
+@pytest.mark.parametrize("n", [0, 1, 63, 64, 65, 8191, 8192, 8193, 100_003])
+def test_hash_random_sizes(engine, oracle_lib, R, n):
+    recs = oracle_lib.gen_uniform16(n, 0x5EEDC0DE + R + n)
+    check_against_oracle(engine, oracle_lib, recs, R)
+
+
+@pytest.mark.parametrize("R", [200, 1024, 4096])
+def test_hash_device_input_2m(engine, oracle_lib, R):
+    recs = oracle_lib.gen_uniform16(2_000_003, R)
+    check_against_oracle(engine, oracle_lib, recs, R, host=False)
+
+
+def test_device_generator_matches_oracle(engine, oracle_lib):
+    n = 1_000_001
+    buf = engine.alloc(n * 16)
+    engine.gen_uniform16(buf, n, 0xABCDEF, value_base=12345)
+    assert np.array_equal(buf.to_numpy().reshape(-1, 16), oracle_lib.gen_uniform16(n, 0xABCDEF, 12345))
+    cdf = oracle_lib.zipf_cdf(1.1, 2**16)
+    engine.gen_zipf16(buf, n, 77, cdf, value_base=3)
+    assert np.array_equal(buf.to_numpy().reshape(-1, 16), oracle_lib.gen_zipf16(n, 77, cdf, 3))
+    m = 10_001
+    tb = engine.alloc(m * 100)
+    engine.gen_terasort100(tb, m, 99, 5)
+    assert np.array_equal(tb.to_numpy().reshape(-1, 100), oracle_lib.gen_terasort100(m, 99, 5))
+
+
+def test_edge_keys_all_partition_counts(engine, oracle_lib):
+    import json
+
+    kats = json.load(open(os.path.join(GOLDEN, "kats.json")))
+    keys = sorted({k for k, _, _ in kats["edge_pids"]})
+    recs = np.zeros((len(keys) * 5, 16), np.uint8)
+    arr = np.array(keys * 5, dtype=np.int64)
+    recs[:, :8] = arr.view(np.uint8).reshape(-1, 8)
+    recs[:, 8:] = np.arange(len(arr), dtype=np.int64).view(np.uint8).reshape(-1, 8)
+    for R in (1, 2, 3, 7, 200, 1000, 1024, 4096, 5000):
+        check_against_oracle(engine, oracle_lib, recs, R)
+
+
+@pytest.mark.parametrize("num_chunks", [1, 3, 1024, 4096])
+def test_chunking_does_not_change_output(sgx_lib, oracle_lib, num_chunks):
+    recs = oracle_lib.gen_uniform16(300_007, 5)
+    with sgx_lib.ShuffleEngine(device=0, num_chunks=num_chunks) as e:
+        check_against_oracle(e, oracle_lib, recs, 1024)
+
+
+def test_zipf_skew_r4096(engine, oracle_lib):
+    cdf = oracle_lib.zipf_cdf(1.1, 2**24)
+    recs = oracle_lib.gen_zipf16(1_000_000, 11, cdf)
+    check_against_oracle(engine, oracle_lib, recs, 4096)
+
+
+def test_all_records_one_partition(engine, oracle_lib):
+    recs = oracle_lib.gen_uniform16(200_000, 1)
+    recs[:, :8] = np.frombuffer(np.int64(4242).tobytes(), np.uint8)  # same key everywhere
+    check_against_oracle(engine, oracle_lib, recs, 1024)
+
+
+# ---------------------------------------------------------------- range partitioners --
+@pytest.mark.parametrize("nb", [1, 50, 128, 129, 1023, 4095])
+@pytest.mark.parametrize("asc", [True, False])
+def test_range_i64_random(engine, oracle_lib, nb, asc):
+    import sparkucx_amd as sgx
+
+    rng = np.random.default_rng(nb)
+    recs = oracle_lib.gen_uniform16(50_000, nb + 3)
+    keys = recs[:, :8].copy().view(np.int64).ravel()
+    bounds = np.sort(rng.choice(keys, nb, replace=False))
+    recs[:nb, :8] = bounds.view(np.uint8).reshape(-1, 8)  # exact hits on bounds
+    check_against_oracle(engine, oracle_lib, recs, nb + 1, sgx.PART_RANGE_I64, bounds, asc)
+
+
+@pytest.mark.parametrize("nb", [63, 1023])
+def test_terasort_bytes10(engine, oracle_lib, nb):
+    import sparkucx_amd as sgx
+
+    recs = oracle_lib.gen_terasort100(60_000, nb)
+    rng = np.random.default_rng(nb)
+    sample = recs[rng.choice(len(recs), 20 * (nb + 1), replace=False), :10]
+    order = np.lexsort(sample.T[::-1])
+    sample = sample[order]
+    step = len(sample) / (nb + 1)
+    bounds = np.ascontiguousarray(sample[[int(step * (i + 1)) for i in range(nb)]])
+    check_against_oracle(engine, oracle_lib, recs, nb + 1, sgx.PART_RANGE_BYTES10, bounds)
+
+
+def test_hash_on_wide_records(engine, oracle_lib):
+    recs = oracle_lib.gen_terasort100(30_000, 4)
+    check_against_oracle(engine, oracle_lib, recs, 1024)
+
+
+# ---------------------------------------------------------------- plugin API ----------
+def test_manager_writer_resolver_reader(sgx_lib, oracle_lib, tmp_path):
+    R, n = 1024, 250_000
+    mgr = sgx_lib.UcxShuffleManager(localDir=str(tmp_path))
+    try:
+        h = mgr.registerShuffle(5, sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(R)))
+        maps = {}
+        for m in (3, 1, 2):
+            recs = oracle_lib.gen_uniform16(n + m, 100 + m, value_base=m << 40)
+            w = mgr.getWriter(h, m)
+            w.write(recs)
+            out, counts = oracle_lib.map_write(recs, R)
+            maps[m] = (out, counts)
+            assert np.array_equal(w.getPartitionLengths(), counts * 16)
+            st = w.stop(True)
+            assert st.mapId == m
+        # index + data files (IndexShuffleBlockResolver layout)
+        res = mgr.shuffleBlockResolver
+        lengths = maps[1][1] * 16
+        res.writeIndexFileAndCommit(5, 1, lengths)
+        assert open(res.getIndexFile(5, 1), "rb").read() == oracle_lib.index_bytes(lengths)
+        assert open(res.getDataFile(5, 1), "rb").read() == maps[1][0].tobytes()
+        assert np.array_equal(res.checkIndexAndDataFile(res.getIndexFile(5, 1), res.getDataFile(5, 1), R),
+                              lengths)
+        off = oracle_lib.offsets(maps[1][1])
+        assert res.getBlockData("shuffle_5_1_17") == maps[1][0][off[17]:off[18]].tobytes()
+        assert res.getBlockData((5, 1, 10, 20)) == maps[1][0][off[10]:off[20]].tobytes()
+        # reader: canonical order (reducer, then map ascending)
+        got = mgr.getReader(h, 100, 103).read()
+        want = []
+        for r in range(100, 103):
+            for m in sorted(maps):
+                o = oracle_lib.offsets(maps[m][1])
+                want.append(maps[m][0][o[r]:o[r + 1]])
+        assert np.array_equal(got, np.concatenate(want))
+    finally:
+        mgr.stop()
+
+
+def test_existing_attempt_wins(sgx_lib, oracle_lib, tmp_path):
+    R = 200
+    mgr = sgx_lib.UcxShuffleManager(localDir=str(tmp_path))
+    try:
+        h = mgr.registerShuffle(1, sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(R)))
+        a = oracle_lib.gen_uniform16(10_000, 1)
+        w = mgr.getWriter(h, 0)
+        w.write(a)
+        la = w.getPartitionLengths().copy()
+        mgr.shuffleBlockResolver.writeIndexFileAndCommit(1, 0, la.copy())
+        # a second attempt with different data: the committed first attempt wins
+        b = oracle_lib.gen_uniform16(12_000, 2)
+        w2 = mgr.getWriter(h, 0)
+        w2.write(b)
+        lb = w2.getPartitionLengths().copy()
+        mgr.shuffleBlockResolver.writeIndexFileAndCommit(1, 0, lb)
+        assert np.array_equal(lb, la)
+        assert open(mgr.shuffleBlockResolver.getDataFile(1, 0), "rb").read() == oracle_lib.map_write(a, R)[0].tobytes()
+        # a corrupt index is replaced by the new attempt
+        with open(mgr.shuffleBlockResolver.getIndexFile(1, 0), "r+b") as f:
+            f.write(b"\x01")
+        lc = w2.getPartitionLengths().copy()
+        mgr.shuffleBlockResolver.writeIndexFileAndCommit(1, 0, lc)
+        assert open(mgr.shuffleBlockResolver.getDataFile(1, 0), "rb").read() == oracle_lib.map_write(b, R)[0].tobytes()
+    finally:
+        mgr.stop()
+
+
+def test_fetch_blocks_and_errors(sgx_lib, oracle_lib, engine):
+    R = 1024
+    recs = oracle_lib.gen_uniform16(123_457, 3)
+    out, counts = oracle_lib.map_write(recs, R)
+    o = oracle_lib.offsets(counts) * 16
+    flat = out.reshape(-1)
+    sid = next_sid()
+    engine.register_shuffle(sid, R)
+    engine.write_map(sid, 9, recs, len(recs), 16, R)
+    rng = np.random.default_rng(0)
+    rids = rng.integers(0, R, 300)
+    data, lens = engine.fetch_blocks(sid, [9] * len(rids), rids)
+    want = np.concatenate([flat[o[r]:o[r + 1]] for r in rids])
+    assert np.array_equal(data, want)
+    assert np.array_equal(lens, (counts * 16)[rids])
+    dev = engine.alloc(int(lens.sum()))
+    engine.fetch_blocks(sid, [9] * len(rids), rids, dst=dev)
+    assert np.array_equal(dev.to_numpy(), want)
+    with pytest.raises(sgx_lib.BlockNotFoundException):
+        engine.fetch_blocks(sid, [8], [0])
+    with pytest.raises(sgx_lib.IllegalArgumentException):
+        engine.fetch_blocks(sid, [9], [R])
+    with pytest.raises(sgx_lib.IllegalArgumentException):
+        engine.fetch_blocks(sid, [9, 9], [1, 2], dst=np.empty(1, np.uint8))
+    engine.unregister_shuffle(sid)
+    with pytest.raises(sgx_lib.IllegalStateException):
+        engine.fetch_blocks(sid, [9], [0])
+    with pytest.raises(sgx_lib.IllegalStateException):
+        engine.write_map(sid, 0, recs, 10, 16)
+
+
+def test_registration_errors(sgx_lib, engine):
+    with pytest.raises(sgx_lib.IllegalArgumentException):
+        engine.register_shuffle(next_sid(), 0)
+    with pytest.raises(sgx_lib.UnsupportedOperationException):
+        engine.register_shuffle(next_sid(), 1_000_000)
+    with pytest.raises(sgx_lib.IllegalArgumentException):
+        engine.register_shuffle(next_sid(), 10, sgx_lib.PART_RANGE_I64, np.arange(3), True)
+    sid = next_sid()
+    engine.register_shuffle(sid, 10)
+    with pytest.raises(sgx_lib.IllegalStateException):
+        engine.register_shuffle(sid, 10)
+    with pytest.raises(sgx_lib.IllegalArgumentException):
+        engine.write_map(sid, 0, np.zeros((4, 100), np.uint8), 4, 100)
+    engine.unregister_shuffle(sid)
+
+
+def test_transport_fetch_blocks_by_block_ids(sgx_lib, oracle_lib):
+    import ctypes
+
+    R = 64
+    mgr = sgx_lib.UcxShuffleManager()
+    try:
+        h = mgr.registerShuffle(2, sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(R)))
+        recs = oracle_lib.gen_uniform16(5000, 8)
+        mgr.getWriter(h, 4).write(recs)
+        out, counts = oracle_lib.map_write(recs, R)
+        o = oracle_lib.offsets(counts) * 16
+        pool = []
+
+        def alloc(size):
+            buf = ctypes.create_string_buffer(max(int(size), 1))
+            pool.append(buf)
+            return sgx_lib.MemoryBlock(ctypes.addressof(buf), int(size))
+
+        got = {}
+        ids = [sgx_lib.UcxShuffleBlockId(2, 4, r) for r in (0, 5, 63)] + [sgx_lib.UcxShuffleBlockId(2, 99, 0)]
+
+        def cb_for(i):
+            def cb(res):
+                got[i] = res
+            return cb
+
+        t = mgr.getTransport()
+        reqs = t.fetchBlocksByBlockIds(1, ids, alloc, [cb_for(i) for i in range(len(ids))])
+        assert not any(r.isCompleted() for r in reqs)
+        t.progress()
+        assert all(r.isCompleted() for r in reqs)
+        for i, r in enumerate((0, 5, 63)):
+            res = got[i]
+            assert res.getStatus() == sgx_lib.OperationStatus.SUCCESS
+            mb = res.getData()
+            assert ctypes.string_at(mb.address, mb.size) == out.reshape(-1)[o[r]:o[r + 1]].tobytes()
+            mb.close()
+        assert got[3].getStatus() == sgx_lib.OperationStatus.FAILURE
+    finally:
+        mgr.stop()
+
+
+# ---------------------------------------------------------------- exchange -----------
+def test_exchange_single_rank_over_rccl(sgx_lib, oracle_lib):
+    R = 1024
+    with sgx_lib.ShuffleEngine(device=0) as e:
+        e.comm_init(1, 0, sgx_lib.get_unique_id())
+        e.register_shuffle(1, R)
+        recs = oracle_lib.gen_uniform16(400_000, 21)
+        e.write_map(1, 6, recs, len(recs), 16, R)
+        e.exchange(1, 6)
+        e.sync()
+        data, lens = e.fetch_blocks(1, [6] * R, list(range(R)))
+        out, counts = oracle_lib.map_write(recs, R)
+        assert np.array_equal(data.reshape(-1, 16), out)
+        st = e.stats()
+        assert st.count["alltoall"] >= 1 and st.count["regroup"] >= 1
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_regroup_kernel_multi_rank_plan(sgx_lib, oracle_lib, engine, P):
+    """Simulate the receive side of a P-rank exchange on one GPU: build each source rank's
+    map output with the oracle, lay the receive buffer out exactly as ncclAllToAllv would,
+    run the K5 regroup kernel with the engine's plan and compare with the canonical
+    per-reducer sequences."""
+    R = 1024
+    outs = []
+    for s in range(P):
+        recs = oracle_lib.gen_uniform16(50_000 + 17 * s, 1000 + s, value_base=s << 40)
+        outs.append(oracle_lib.map_write(recs, R))
+    L = np.stack([c * 16 for _, c in outs])
+    for rank in range(P):
+        sc, sd, rc, rd, items = sgx_lib.plan_exchange(L, rank, 64 * 1024)
+        # what each source sends to `rank`: its contiguous slice of my reducers
+        recv = []
+        for s in range(P):
+            s_sc, s_sd, _, _, _ = sgx_lib.plan_exchange(L, s, 0)
+            flat = outs[s][0].reshape(-1)
+            recv.append(flat[s_sd[rank]:s_sd[rank] + s_sc[rank]])
+        recv = np.concatenate(recv) if recv else np.zeros(0, np.uint8)
+        assert recv.nbytes == rc.sum()
+        src = engine.alloc(max(recv.nbytes, 16))
+        src.copy_from(recv)
+        dst = engine.alloc(max(recv.nbytes, 16))
+        engine.copy_items(src, dst, items, 16)
+        got = dst.to_numpy(recv.nbytes)
+        seqs = oracle_lib.canonical_reducer_sequences(outs, R, 16)
+        mine = [r for r in range(R) if (r * P) // R == rank]
+        want = np.concatenate([seqs[r] for r in mine]).reshape(-1)
+        assert np.array_equal(got, want)
+
+
+# ---------------------------------------------------------------- determinism / size --
+def test_repeatable_bitwise(engine, oracle_lib):
+    recs = oracle_lib.gen_uniform16(1_000_000, 31)
+    a = run_map(engine, recs, 1024, host=False)
+    b = run_map(engine, recs, 1024, host=False)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1])
+
+
+@pytest.mark.slow
+def test_full_c1_size_bit_exact(engine, oracle_lib):
+    """BASELINE config C1 at full size: 2^28 uniform 16 B records, R = 1024, on-device
+    input; compared byte for byte with the multi-threaded oracle."""
+    n, R, seed = 1 << 28, 1024, 0x5EEDC0DE
+    buf = engine.alloc(n * 16)
+    engine.gen_uniform16(buf, n, seed)
+    sid = next_sid()
+    engine.register_shuffle(sid, R)
+    lengths = engine.write_map(sid, 0, buf, n, 16, R)
+    got = engine.map_output_bytes(sid, 0)
+    engine.unregister_shuffle(sid)
+    buf.free()
+    recs = oracle_lib.gen_uniform16(n, seed)
+    want, counts = oracle_lib.map_write(recs, R, nthreads=16)
+    del recs
+    assert np.array_equal(lengths, counts * 16)
+    assert np.array_equal(got, want.reshape(-1))
