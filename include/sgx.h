@@ -53,8 +53,8 @@ typedef struct sgx_engine sgx_engine;
 typedef struct sgx_config {
     int32_t device;          /* HIP device ordinal for this executor                     */
     int32_t num_chunks;      /* map-side work chunks per batch (0 = one per CU)           */
-    int32_t flags;           /* reserved, 0                                               */
-    int32_t reserved;
+    int32_t scatter_waves;   /* K4 geometry override (0 = auto): waves per workgroup       */
+    int32_t scatter_items;   /* K4 geometry override (0 = auto): records per lane per tile */
 } sgx_config;
 
 /* ---- engine lifetime: replaces CommonUcxShuffleManager.startUcxTransport

@@ -19,6 +19,7 @@
 #include <cerrno>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -156,6 +157,8 @@ struct sgx_engine {
     int device = 0;
     int num_cus = 256;
     int G = 256;
+    int sc_waves = 0, sc_items = 0;  // K4 geometry override
+    int diag = 0;                    // SGX_SCATTER_DIAG: measurement-only K4 ablation (wrong output)
     hipStream_t s_comp = nullptr, s_comm = nullptr;
     // work buffers of the map-side pipeline
     DevBuf counts, offs, status, part_off_dev, input_stage;
@@ -234,6 +237,9 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     e->device = dev;
     e->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     e->G = (cfg && cfg->num_chunks > 0) ? cfg->num_chunks : e->num_cus;
+    e->sc_waves = cfg ? cfg->scatter_waves : 0;
+    e->sc_items = cfg ? cfg->scatter_items : 0;
+    if (const char *d = getenv("SGX_SCATTER_DIAG")) e->diag = atoi(d);
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
     *out = e.release();
@@ -406,7 +412,18 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
     }
 
     // chunking: G chunks, each a whole number of scatter tiles where possible
-    const int tile = rb == 16 ? scatter_geom16((uint32_t)s.R).tile : scatter_geom_wide((uint32_t)s.R, rb).tile;
+    ScatterGeom geo = rb == 16 ? scatter_geom16((uint32_t)s.R, e->sc_waves, e->sc_items)
+                               : scatter_geom_wide((uint32_t)s.R, rb);
+    // hash partitioner, 16 B records: the LDS-DMA pipelined kernel unless a geometry is forced
+    if (e->diag > 0 && rb == 16) geo = scatter_geom16((uint32_t)s.R, 8, 16);
+    if (rb == 16 && s.kind == SGX_PART_HASH && e->sc_waves == 0 && e->sc_items == 0 && e->diag == 0) {
+        const ScatterGeom d = scatter_geom16_dma((uint32_t)s.R);
+        if (d.items) geo = d;
+    }
+    if (geo.items == 0)
+        return fail(SGX_ERR_UNSUPPORTED, "no scatter geometry (waves %d, items %d) fits R=%d", e->sc_waves,
+                    e->sc_items, s.R);
+    const int tile = geo.tile;
     int64_t chunk = n > 0 ? (n + e->G - 1) / e->G : 1;
     chunk = (chunk + tile - 1) / tile * tile;
     const int G = n > 0 ? (int)((n + chunk - 1) / chunk) : 1;
@@ -420,27 +437,35 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
     uint64_t *status = (uint64_t *)((char *)e->status.p + 16);
     HIP_TRY(hipMemsetAsync(e->status.p, 0, (size_t)(16 + tiles * 8), st));
 
-    hipEvent_t t0 = e->ev(), t1 = e->ev(), t2 = e->ev(), t3 = e->ev();
-    HIP_TRY(hipEventRecord(t0, st));
+    // one event pair per stage: an event is owned by exactly one pending record
+    hipEvent_t h0 = e->ev(), h1 = e->ev(), c0 = e->ev(), c1 = e->ev(), x0 = e->ev(), x1 = e->ev();
+    HIP_TRY(hipEventRecord(h0, st));
     if (n > 0) {
         HIP_TRY(launch_hist(in, n, rb, chunk, G, s.pp, (uint32_t *)e->counts.p, st));
     } else {
         HIP_TRY(hipMemsetAsync(e->counts.p, 0, (size_t)len * 4, st));
     }
-    HIP_TRY(hipEventRecord(t1, st));
+    HIP_TRY(hipEventRecord(h1, st));
+    HIP_TRY(hipEventRecord(c0, st));
     HIP_TRY(launch_scan((const uint32_t *)e->counts.p, (uint32_t *)e->offs.p, len, status, ticket_err,
                         (uint32_t *)e->part_off_dev.p, G, s.R, st));
-    HIP_TRY(hipEventRecord(t2, st));
-    if (n > 0) HIP_TRY(launch_scatter(in, m.data.p, n, rb, chunk, G, s.pp, (const uint32_t *)e->offs.p, st));
-    HIP_TRY(hipEventRecord(t3, st));
+    HIP_TRY(hipEventRecord(c1, st));
+    HIP_TRY(hipEventRecord(x0, st));
+    if (n > 0) {
+        if (e->diag > 0 && rb == 16 && s.kind == SGX_PART_HASH)  // measurement-only ablation
+            HIP_TRY(launch_scatter_diag(e->diag, in, m.data.p, n, chunk, G, s.pp, (const uint32_t *)e->offs.p, st));
+        else
+            HIP_TRY(launch_scatter(in, m.data.p, n, rb, chunk, G, s.pp, (const uint32_t *)e->offs.p, geo, st));
+    }
+    HIP_TRY(hipEventRecord(x1, st));
     // (R+1) offsets then the look-back give-up flag
     HIP_TRY(hipMemcpyAsync((char *)e->part_off_dev.p + (size_t)(s.R + 1) * 4, ticket_err + 1, 4,
                            hipMemcpyDeviceToDevice, st));
     HIP_TRY(hipMemcpyAsync(m.part_off.p, e->part_off_dev.p, (size_t)(s.R + 2) * 4, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipEventRecord(m.done, st));
-    record_stage(e, SGX_STAGE_HIST, t0, t1);
-    record_stage(e, SGX_STAGE_SCAN, t1, t2);
-    record_stage(e, SGX_STAGE_SCATTER, t2, t3);
+    record_stage(e, SGX_STAGE_HIST, h0, h1);
+    record_stage(e, SGX_STAGE_SCAN, c0, c1);
+    record_stage(e, SGX_STAGE_SCATTER, x0, x1);
     if (out_lengths) {
         SGX_TRY(finish_lengths(s, m));
         std::memcpy(out_lengths, m.lengths.data(), sizeof(int64_t) * (size_t)s.R);

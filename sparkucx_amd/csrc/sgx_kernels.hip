@@ -130,8 +130,8 @@ __device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t x, uint32_t lan
 
 // Exclusive scan of in[0..R) into out[0..R) by the whole block; scratch >= waves u32.
 // Ends with a barrier.
-__device__ void block_exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t R,
-                                     uint32_t *scratch) {
+template <typename E>
+__device__ void block_exclusive_scan(const E *in, E *out, uint32_t R, uint32_t *scratch) {
     const uint32_t T = blockDim.x, tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t per = (R + T - 1) / T;
     const uint32_t beg = min(tid * per, R), end = min(beg + per, R);
@@ -144,7 +144,7 @@ __device__ void block_exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t
     for (uint32_t v = 0; v < w; ++v) run += scratch[v];
     for (uint32_t i = beg; i < end; ++i) {
         const uint32_t c = in[i];
-        out[i] = run;
+        out[i] = (E)run;
         run += c;
     }
     __syncthreads();
@@ -156,6 +156,10 @@ __device__ void block_exclusive_scan(const uint32_t *in, uint32_t *out, uint32_t
 constexpr int HIST_THREADS = 512;
 constexpr int HIST_UNROLL = 8;
 
+// grid = G * HIST_SPLIT: sub-block `sub` of chunk g counts records [begin + sub*sub_len, ...)
+// and adds its LDS histogram into counts[p][g] (zeroed by the launcher's memset).
+constexpr int HIST_SPLIT = 4;
+
 template <int KIND, bool REC16>
 __global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ in, int64_t n,
                                                        int rb, int64_t chunk, PartParams pp,
@@ -165,9 +169,12 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ 
     const uint32_t tid = threadIdx.x, T = blockDim.x;
     for (uint32_t p = tid; p < pp.R; p += T) hist[p] = 0;
     __syncthreads();
-    const int g = blockIdx.x;
-    const int64_t begin = (int64_t)g * chunk;
-    const int64_t end = min(n, begin + chunk);
+    const int g = blockIdx.x / HIST_SPLIT, sub = blockIdx.x % HIST_SPLIT;
+    const int64_t cbeg = (int64_t)g * chunk;
+    const int64_t cend = min(n, cbeg + chunk);
+    const int64_t sub_len = (chunk + HIST_SPLIT - 1) / HIST_SPLIT;
+    const int64_t begin = min(cend, cbeg + (int64_t)sub * sub_len);
+    const int64_t end = min(cend, begin + sub_len);
     for (int64_t base = begin; base < end; base += (int64_t)T * HIST_UNROLL) {
         uint32_t x[HIST_UNROLL], y[HIST_UNROLL], z[HIST_UNROLL];
 #pragma unroll
@@ -191,16 +198,21 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ 
         }
     }
     __syncthreads();
-    for (uint32_t p = tid; p < pp.R; p += T) counts[(int64_t)p * G + g] = hist[p];
+    for (uint32_t p = tid; p < pp.R; p += T) {
+        const uint32_t c = hist[p];
+        if (c) atomicAdd(&counts[(int64_t)p * G + g], c);
+    }
 }
 
 hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
                        const PartParams &pp, uint32_t *counts, hipStream_t stream) {
     const size_t lds = (size_t)pp.R * 4;
     const char *p = (const char *)in;
+    hipError_t ze = hipMemsetAsync(counts, 0, (size_t)pp.R * G * 4, stream);
+    if (ze != hipSuccess) return ze;
     const bool r16 = (rb == 16);
 #define SGX_HIST(K, B) \
-    hipLaunchKernelGGL((k_hist<K, B>), dim3(G), dim3(HIST_THREADS), lds, stream, p, n, rb, chunk, pp, counts, G)
+    hipLaunchKernelGGL((k_hist<K, B>), dim3(G * HIST_SPLIT), dim3(HIST_THREADS), lds, stream, p, n, rb, chunk, pp, counts, G)
     switch (pp.kind) {
     case SGX_PART_HASH: if (r16) SGX_HIST(SGX_PART_HASH, true); else SGX_HIST(SGX_PART_HASH, false); break;
     case SGX_PART_RANGE_I64: if (r16) SGX_HIST(SGX_PART_RANGE_I64, true); else SGX_HIST(SGX_PART_RANGE_I64, false); break;
@@ -315,41 +327,72 @@ hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint
 //           partition run is written by consecutive lanes (coalesced), and
 //           cursor[p] += tcnt[p].  cursor starts at offs[p][g] (K3).
 // ------------------------------------------------------------------------------------
-constexpr int SC_WAVES = 8;
-constexpr int SC_THREADS = SC_WAVES * 64;
 constexpr size_t LDS_MAX = 160 * 1024;
+constexpr int WIDE_WAVES = 8;
+constexpr int DMA_WAVES = 8, DMA_ITEMS = 8;
+constexpr int DMA_T = DMA_WAVES * 64, DMA_TILE = DMA_WAVES * DMA_ITEMS * 64;
+size_t scatter16_dma_lds(uint32_t R);
+constexpr int WIDE_THREADS = WIDE_WAVES * 64;
 
-static size_t scatter_lds16(uint32_t R, int tile) {
-    return (size_t)tile * 16 + (size_t)SC_WAVES * R * 2 + (size_t)3 * R * 4 + 64;
+__host__ __device__ constexpr size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+// LDS of the 16 B scatter: stage[TILE] uint4 | wcnt[WAVES][R] u16 | lstart[R] u16 |
+// tcnt[R] u16 | cursor[R] u32.  The block-scan scratch borrows the (idle) stage.
+__host__ __device__ size_t scatter16_lds(uint32_t R, int waves, int items) {
+    const size_t tile = (size_t)waves * items * 64;
+    return tile * 16 + al16((size_t)waves * R * 2) + 2 * al16((size_t)R * 2) + al16((size_t)R * 4);
 }
 
-ScatterGeom scatter_geom16(uint32_t R) {
-    static const int cand[] = {16, 12, 8, 6, 4, 3, 2, 1};
-    for (int items : cand) {
-        const int tile = SC_WAVES * items * 64;
-        const size_t lds = scatter_lds16(R, tile);
-        if (lds <= LDS_MAX) return ScatterGeom{SC_WAVES, items, tile, lds};
+struct Geo16 { int waves, items; };
+// every instantiated geometry (launch_scatter's switch must list the same set)
+static const Geo16 kGeos16[] = {{4, 16}, {8, 16}, {4, 12}, {8, 8}, {4, 8}, {8, 4}, {4, 4}, {4, 2}, {4, 1}};
+
+ScatterGeom scatter_geom16_dma(uint32_t R) {
+    const size_t lds = scatter16_dma_lds(R);
+    if (lds > LDS_MAX) return ScatterGeom{0, 0, 0, 0};
+    return ScatterGeom{DMA_GEOM_TAG, DMA_ITEMS, DMA_TILE, lds};
+}
+
+ScatterGeom scatter_geom16(uint32_t R, int force_waves, int force_items) {
+    ScatterGeom best{0, 0, 0, 0};
+    long best_score = -1;
+    int best_occ = 0;
+    for (const Geo16 &g : kGeos16) {
+        if (force_waves && force_waves != g.waves) continue;
+        if (force_items && force_items != g.items) continue;
+        const size_t lds = scatter16_lds(R, g.waves, g.items);
+        if (lds > LDS_MAX) continue;
+        const int occ = (int)(LDS_MAX / lds);
+        const int tile = g.waves * g.items * 64;
+        // records in flight per CU (capped at two workgroups), then occupancy
+        const long score = (long)tile * (occ < 2 ? occ : 2);
+        if (score > best_score || (score == best_score && occ > best_occ)) {
+            best = ScatterGeom{g.waves, g.items, tile, lds};
+            best_score = score;
+            best_occ = occ;
+        }
     }
-    return ScatterGeom{SC_WAVES, 0, 0, 0};
+    return best;
 }
 
 static size_t scatter_lds_wide(uint32_t R) {
-    return (size_t)SC_WAVES * R * 2 + (size_t)2 * R * 4 + 64;
+    return al16((size_t)WIDE_WAVES * R * 2) + (size_t)2 * R * 4 + 64;
 }
 
 ScatterGeom scatter_geom_wide(uint32_t R, int /*rb*/) {
     const size_t lds = scatter_lds_wide(R);
-    if (lds > LDS_MAX) return ScatterGeom{SC_WAVES, 0, 0, 0};
-    return ScatterGeom{SC_WAVES, 4, SC_WAVES * 4 * 64, lds};
+    if (lds > LDS_MAX) return ScatterGeom{WIDE_WAVES, 0, 0, 0};
+    return ScatterGeom{WIDE_WAVES, 4, WIDE_WAVES * 4 * 64, lds};
 }
 
 // Slot -> partition for the drain: the last p with lstart[p] <= s (empty partitions
 // before p share p's start, every later partition starts after s).
-__device__ __forceinline__ uint32_t slot_partition(const uint32_t *lstart, uint32_t R, uint32_t s) {
+template <typename T>
+__device__ __forceinline__ uint32_t slot_partition(const T *lstart, uint32_t R, uint32_t s) {
     uint32_t lo = 0, hi = R - 1;
     while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
-        if (lstart[mid] <= s) lo = mid; else hi = mid - 1;
+        if ((uint32_t)lstart[mid] <= s) lo = mid; else hi = mid - 1;
     }
     return lo;
 }
@@ -372,104 +415,339 @@ __device__ __forceinline__ void rank_items(const uint32_t (&pid)[ITEMS], const b
     }
 }
 
-template <int KIND, int ITEMS>
-__global__ __launch_bounds__(SC_THREADS, 1) void k_scatter16(const uint4 *__restrict__ in,
+// LDS-only barrier: waits for this wave's LDS ops, then s_barrier.  Unlike
+// __syncthreads() it does not drain outstanding global loads/stores (vmcnt), so the next
+// tile's prefetch and this tile's stores stay in flight across it.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+}
+
+// Shared LDS carve-up of k_scatter16.
+struct Sc16Lds {
+    uint4 *stage;
+    uint16_t *wcnt, *lstart, *tcnt;
+    uint32_t *cursor, *scratch;
+};
+
+template <int WAVES, int ITEMS>
+__device__ __forceinline__ Sc16Lds sc16_lds(char *smem, uint32_t R) {
+    constexpr int TILE = WAVES * ITEMS * 64;
+    Sc16Lds L;
+    L.stage = (uint4 *)smem;
+    L.wcnt = (uint16_t *)(smem + (size_t)TILE * 16);
+    L.lstart = (uint16_t *)((char *)L.wcnt + al16((size_t)WAVES * R * 2));
+    L.tcnt = (uint16_t *)((char *)L.lstart + al16((size_t)R * 2));
+    L.cursor = (uint32_t *)((char *)L.tcnt + al16((size_t)R * 2));
+    L.scratch = (uint32_t *)smem;  // block-scan scratch: stage is idle then
+    return L;
+}
+
+// Rank + merge + scan + stage of one tile whose records/pids are in registers.
+// Returns with the tile partition-sorted in L.stage (after a barrier).
+template <int WAVES, int ITEMS>
+__device__ __forceinline__ void sc16_rank_stage(const Sc16Lds &L, uint32_t R, const uint4 (&rec)[ITEMS],
+                                                const uint32_t (&pid)[ITEMS], const bool (&valid)[ITEMS],
+                                                uint32_t nbits) {
+    constexpr int T = WAVES * 64;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t rank[ITEMS];
+    rank_items<ITEMS>(pid, valid, rank, L.wcnt + (size_t)w * R, nbits, lane);
+    lds_barrier();
+    for (uint32_t p = tid; p < R; p += T) {
+        uint32_t s = 0;
+#pragma unroll
+        for (int v = 0; v < WAVES; ++v) {
+            const uint32_t c = L.wcnt[(size_t)v * R + p];
+            L.wcnt[(size_t)v * R + p] = (uint16_t)s;
+            s += c;
+        }
+        L.tcnt[p] = (uint16_t)s;
+    }
+    lds_barrier();
+    block_exclusive_scan(L.tcnt, L.lstart, R, L.scratch);
+    const uint16_t *mycnt = L.wcnt + (size_t)w * R;
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        if (valid[k]) {
+            const uint32_t p = pid[k];
+            L.stage[(uint32_t)L.lstart[p] + mycnt[p] + rank[k]] = rec[k];
+        }
+    }
+    lds_barrier();
+}
+
+// Generic (guarded) tile: used for the partial tail tile and for non-hash partitioners.
+// DIAG (measurement-only builds, never the product path): 1 = no global stores,
+// 2 = no ballot ranking, 3 = no global loads, 4 = no LDS stage/drain, 5 = no ranking and
+// identity staging (memory + barriers only).  Values that a skipped phase would consume
+// are kept alive with empty asm so the compiler cannot delete the phases that remain.
+template <int KIND, int WAVES, int ITEMS, int DIAG = 0>
+__device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 *__restrict__ in,
+                                                  uint4 *__restrict__ out, int64_t tbase, int64_t end,
+                                                  const PartParams &pp) {
+    constexpr int T = WAVES * 64;
+    constexpr int TILE = WAVES * ITEMS * 64;
+    const uint32_t R = pp.R;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (uint32_t i = tid; i < (uint32_t)(WAVES * R / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
+    uint4 rec[ITEMS];
+    uint32_t pid[ITEMS];
+    bool valid[ITEMS];
+    const int64_t wbase = tbase + (int64_t)w * ITEMS * 64 + lane;
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        const int64_t i = wbase + (int64_t)k * 64;
+        valid[k] = i < end;
+        if constexpr (DIAG == 3) {
+            rec[k] = make_uint4((uint32_t)i * 2654435761u, (uint32_t)(i >> 7), (uint32_t)i, 0);
+        } else {
+            rec[k] = valid[k] ? in[i] : make_uint4(0, 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
+    __syncthreads();  // wcnt zeroed
+    if constexpr (DIAG == 2 || DIAG == 5) {
+        // skip the ballot ranking: identity-ish placement, keep every pid alive
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(pid[k]));
+        for (uint32_t p = tid; p < R; p += T) { L.tcnt[p] = (uint16_t)(TILE / R); L.lstart[p] = (uint16_t)(p * (TILE / R)); }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) L.stage[(w * ITEMS + k) * 64 + lane] = rec[k];
+        __syncthreads();
+    } else if constexpr (DIAG == 4) {
+        sc16_rank_stage<WAVES, ITEMS>(L, R, rec, pid, valid, pp.nbits);
+    } else {
+        sc16_rank_stage<WAVES, ITEMS>(L, R, rec, pid, valid, pp.nbits);
+    }
+    const uint32_t tile_n = (uint32_t)min<int64_t>(TILE, end - tbase);
+    if constexpr (DIAG == 4) {
+        // no drain: write each register record straight back to its input slot
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k)
+            if (valid[k]) out[(size_t)(wbase + (int64_t)k * 64)] = rec[k];
+    } else {
+        for (uint32_t s = tid; s < tile_n; s += T) {
+            const uint4 r = L.stage[s];
+            uint32_t p;
+            if constexpr (KIND == SGX_PART_HASH) p = hash_pid(r.x, r.y, pp);
+            else p = slot_partition(L.lstart, R, s);
+            uint32_t d;
+            if constexpr (DIAG == 5) d = (uint32_t)(tbase + s) + 0u * p;
+            else d = L.cursor[p] + (s - (uint32_t)L.lstart[p]);
+            if constexpr (DIAG == 1) {
+                asm volatile("" ::"v"(r.x), "v"(r.y), "v"(r.z), "v"(r.w), "v"(d));
+            } else {
+                out[(size_t)d] = r;
+            }
+        }
+    }
+    __syncthreads();
+    for (uint32_t p = tid; p < R; p += T) L.cursor[p] += L.tcnt[p];
+    __syncthreads();
+}
+
+template <int KIND, int WAVES, int ITEMS>
+__global__ __launch_bounds__(WAVES * 64, 2) void k_scatter16(const uint4 *__restrict__ in,
                                                              uint4 *__restrict__ out, int64_t n,
                                                              int64_t chunk, PartParams pp,
                                                              const uint32_t *__restrict__ offs,
                                                              int G) {
-    constexpr int TILE = SC_WAVES * ITEMS * 64;
+    constexpr int T = WAVES * 64;
+    constexpr int TILE = WAVES * ITEMS * 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t R = pp.R;
-    uint4 *stage = (uint4 *)smem;
-    uint16_t *wcnt = (uint16_t *)(smem + (size_t)TILE * 16);
-    uint32_t *lstart = (uint32_t *)(smem + (size_t)TILE * 16 + (((size_t)SC_WAVES * R * 2 + 15) & ~(size_t)15));
-    uint32_t *cursor = lstart + R;
-    uint32_t *tcnt = cursor + R;
-    uint32_t *scratch = tcnt + R;
-
-    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const Sc16Lds L = sc16_lds<WAVES, ITEMS>(smem, R);
+    const uint32_t tid = threadIdx.x;
     const int g = blockIdx.x;
     const int64_t begin = (int64_t)g * chunk;
     const int64_t end = min(n, begin + chunk);
-    for (uint32_t p = tid; p < R; p += SC_THREADS) cursor[p] = offs[(int64_t)p * G + g];
+    for (uint32_t p = tid; p < R; p += T) L.cursor[p] = offs[(int64_t)p * G + g];
+    __syncthreads();
+    for (int64_t tbase = begin; tbase < end; tbase += TILE)
+        sc16_tile_generic<KIND, WAVES, ITEMS>(L, in, out, tbase, end, pp);
+}
 
-    for (int64_t tbase = begin; tbase < end; tbase += TILE) {
-        for (uint32_t i = tid; i < SC_WAVES * R / 2; i += SC_THREADS) ((uint32_t *)wcnt)[i] = 0;
-        // load this wave's sub-tile (coalesced: 1 KiB per wave-instruction)
-        uint4 rec[ITEMS];
-        uint32_t pid[ITEMS], rank[ITEMS];
-        bool valid[ITEMS];
-        const int64_t wbase = tbase + (int64_t)w * ITEMS * 64 + lane;
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const int64_t i = wbase + (int64_t)k * 64;
-            valid[k] = i < end;
-            rec[k] = valid[k] ? in[i] : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
-        __syncthreads();  // wcnt zeroed
-        rank_items<ITEMS>(pid, valid, rank, wcnt + (size_t)w * R, pp.nbits, lane);
-        __syncthreads();
-        for (uint32_t p = tid; p < R; p += SC_THREADS) {
-            uint32_t s = 0;
-#pragma unroll
-            for (int v = 0; v < SC_WAVES; ++v) {
-                const uint32_t c = wcnt[(size_t)v * R + p];
-                wcnt[(size_t)v * R + p] = (uint16_t)s;
-                s += c;
-            }
-            tcnt[p] = s;
-        }
-        __syncthreads();
-        block_exclusive_scan(tcnt, lstart, R, scratch);
-        const uint16_t *mycnt = wcnt + (size_t)w * R;
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            if (valid[k]) {
-                const uint32_t p = pid[k];
-                stage[lstart[p] + mycnt[p] + rank[k]] = rec[k];
-            }
-        }
-        __syncthreads();
-        const uint32_t tile_n = (uint32_t)min<int64_t>(TILE, end - tbase);
-        for (uint32_t s = tid; s < tile_n; s += SC_THREADS) {
-            const uint4 r = stage[s];
-            uint32_t p;
-            if constexpr (KIND == SGX_PART_HASH) p = hash_pid(r.x, r.y, pp);
-            else p = slot_partition(lstart, R, s);
-            out[(size_t)(cursor[p] + (s - lstart[p]))] = r;
-        }
-        __syncthreads();
-        for (uint32_t p = tid; p < R; p += SC_THREADS) cursor[p] += tcnt[p];
+template <int DIAG>
+__global__ __launch_bounds__(512, 2) void k_scatter16_diag(const uint4 *__restrict__ in,
+                                                           uint4 *__restrict__ out, int64_t n,
+                                                           int64_t chunk, PartParams pp,
+                                                           const uint32_t *__restrict__ offs, int G) {
+    constexpr int WAVES = 8, ITEMS = 16, T = WAVES * 64, TILE = WAVES * ITEMS * 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint32_t R = pp.R;
+    const Sc16Lds L = sc16_lds<WAVES, ITEMS>(smem, R);
+    const uint32_t tid = threadIdx.x;
+    const int g = blockIdx.x;
+    const int64_t begin = (int64_t)g * chunk;
+    const int64_t end = min(n, begin + chunk);
+    for (uint32_t p = tid; p < R; p += T) L.cursor[p] = offs[(int64_t)p * G + g];
+    __syncthreads();
+    for (int64_t tbase = begin; tbase < end; tbase += TILE)
+        sc16_tile_generic<SGX_PART_HASH, WAVES, ITEMS, DIAG>(L, in, out, tbase, end, pp);
+}
+
+hipError_t launch_scatter_diag(int mode, const void *in, void *out, int64_t n, int64_t chunk, int G,
+                               const PartParams &pp, const uint32_t *offs, hipStream_t stream) {
+    const size_t lds = scatter16_lds(pp.R, 8, 16);
+    if (lds > LDS_MAX || pp.kind != SGX_PART_HASH) return hipErrorInvalidValue;
+#define SGX_DIAGK(M)                                                                            \
+    do {                                                                                        \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_diag<M>,                           \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
+        hipLaunchKernelGGL(k_scatter16_diag<M>, dim3(G), dim3(512), lds, stream, (const uint4 *)in, \
+                           (uint4 *)out, n, chunk, pp, offs, G);                                \
+    } while (0)
+    switch (mode) {
+    case 1: SGX_DIAGK(1); break;
+    case 2: SGX_DIAGK(2); break;
+    case 3: SGX_DIAGK(3); break;
+    case 4: SGX_DIAGK(4); break;
+    case 5: SGX_DIAGK(5); break;
+    default: SGX_DIAGK(0); break;
     }
+#undef SGX_DIAGK
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// K4 (hash, full tiles): LDS-DMA software pipeline.
+//
+// Each wave moves its own sub-tile of tile t+1 from HBM straight into the LDS buffer X
+// with global_load_lds_dwordx4 (1 KiB per wave-instruction, no VGPRs) while tile t is
+// ranked, staged and drained.  A wave reads back only the bytes it DMA'd itself, so the
+// only synchronisation a prefetch needs is that wave's own s_waitcnt vmcnt: the DMA of
+// tile t+1 is issued before the ITEMS drain stores of tile t, hence vmcnt(ITEMS) at the
+// top of the next tile retires exactly the DMA (counters retire in issue order) and lets
+// the stores keep streaming.  The DMA is inline asm, invisible to hipcc's waitcnt pass
+// (cdna_hip_programming.md §5.7), so no compiler-inserted vmcnt(0) drains it; every
+// barrier in the loop is an LDS-only barrier (lgkmcnt(0) + s_barrier).
+// ------------------------------------------------------------------------------------
+size_t scatter16_dma_lds(uint32_t R) {
+    return scatter16_lds(R, DMA_WAVES, DMA_ITEMS) + (size_t)DMA_TILE * 16;
+}
+
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst) {
+    uint32_t keep;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(keep)
+        : "v"(gsrc), "s"(lds_dst)
+        : "memory");
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__global__ __launch_bounds__(DMA_T, 2) void k_scatter16_dma(const uint4 *__restrict__ in,
+                                                           uint4 *__restrict__ out, int64_t n,
+                                                           int64_t chunk, PartParams pp,
+                                                           const uint32_t *__restrict__ offs,
+                                                           int G) {
+    constexpr int T = DMA_T, TILE = DMA_TILE, ITEMS = DMA_ITEMS;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint32_t R = pp.R;
+    const Sc16Lds L = sc16_lds<DMA_WAVES, DMA_ITEMS>(smem, R);
+    const size_t xoff = scatter16_lds(R, DMA_WAVES, DMA_ITEMS);
+    const uint4 *X = (const uint4 *)(smem + xoff);
+    const uint32_t tid = threadIdx.x, lane = tid & 63;
+    const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    // LDS byte address of this wave's slice of X (wave-uniform, for M0)
+    const uint32_t x_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char *)smem) +
+                           (uint32_t)xoff + w * (ITEMS * 64 * 16);
+    const int g = blockIdx.x;
+    const int64_t begin = (int64_t)g * chunk;
+    const int64_t end = min(n, begin + chunk);
+    for (uint32_t p = tid; p < R; p += T) L.cursor[p] = offs[(int64_t)p * G + g];
+    for (uint32_t i = tid; i < (uint32_t)(DMA_WAVES * R / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
+    const int64_t nfull = end > begin ? (end - begin) / TILE : 0;
+    const uint4 *src = in + begin + (int64_t)w * ITEMS * 64 + lane;
+    if (nfull > 0) {
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) glds16(src + k * 64, x_lds + k * 1024);
+    }
+    __syncthreads();  // cursor + wcnt initialised (drains nothing of ours: DMA is asm)
+    for (int64_t t = 0; t < nfull; ++t) {
+        // this wave's DMA of tile t is older than its ITEMS drain stores of tile t-1
+        if (t == 0) wait_vmcnt<0>(); else wait_vmcnt<ITEMS>();
+        uint4 rec[ITEMS];
+        uint32_t pid[ITEMS];
+        bool valid[ITEMS];
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) rec[k] = X[(w * ITEMS + k) * 64 + lane];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        // X is free again for this wave: prefetch tile t+1 (clamped: the last tile reloads
+        // itself, which keeps the vmcnt arithmetic unconditional)
+        {
+            const int64_t tn = t + 1 < nfull ? t + 1 : t;
+            const uint4 *s2 = src + tn * TILE;
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k) glds16(s2 + k * 64, x_lds + k * 1024);
+        }
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            valid[k] = true;
+            pid[k] = hash_pid(rec[k].x, rec[k].y, pp);
+        }
+        sc16_rank_stage<DMA_WAVES, DMA_ITEMS>(L, R, rec, pid, valid, pp.nbits);
+#pragma unroll
+        for (int k0 = 0; k0 < ITEMS; k0 += 4) {
+            uint4 r[4];
+            uint32_t d[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) r[j] = L.stage[(k0 + j) * T + tid];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t p = hash_pid(r[j].x, r[j].y, pp);
+                d[j] = L.cursor[p] - (uint32_t)L.lstart[p];
+            }
+#pragma unroll
+            for (int j = 0; j < 4; ++j) out[(size_t)(d[j] + (uint32_t)((k0 + j) * T + tid))] = r[j];
+        }
+        lds_barrier();
+        for (uint32_t p = tid; p < R; p += T) L.cursor[p] += L.tcnt[p];
+        for (uint32_t i = tid; i < (uint32_t)(DMA_WAVES * R / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
+        lds_barrier();
+    }
+    wait_vmcnt<0>();  // retire the clamped re-prefetch before X/stage are reused
+    __syncthreads();
+    for (int64_t tbase = begin + nfull * TILE; tbase < end; tbase += TILE)
+        sc16_tile_generic<SGX_PART_HASH, DMA_WAVES, DMA_ITEMS>(L, in, out, tbase, end, pp);
 }
 
 // Wide records (record_bytes multiple of 4, e.g. TeraSort's 100 B): same ranking, each
 // lane then copies its record straight to its destination.
 template <int KIND, int ITEMS>
-__global__ __launch_bounds__(SC_THREADS, 1) void k_scatter_wide(const char *__restrict__ in,
+__global__ __launch_bounds__(WIDE_THREADS, 1) void k_scatter_wide(const char *__restrict__ in,
                                                                 char *__restrict__ out, int64_t n,
                                                                 int rb, int64_t chunk,
                                                                 PartParams pp,
                                                                 const uint32_t *__restrict__ offs,
                                                                 int G) {
-    constexpr int TILE = SC_WAVES * ITEMS * 64;
+    constexpr int TILE = WIDE_WAVES * ITEMS * 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t R = pp.R;
     uint16_t *wcnt = (uint16_t *)smem;
-    uint32_t *cursor = (uint32_t *)(smem + (((size_t)SC_WAVES * R * 2 + 15) & ~(size_t)15));
+    uint32_t *cursor = (uint32_t *)(smem + (((size_t)WIDE_WAVES * R * 2 + 15) & ~(size_t)15));
     uint32_t *tcnt = cursor + R;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int g = blockIdx.x;
     const int64_t begin = (int64_t)g * chunk;
     const int64_t end = min(n, begin + chunk);
     const int dw = rb >> 2;
-    for (uint32_t p = tid; p < R; p += SC_THREADS) cursor[p] = offs[(int64_t)p * G + g];
+    for (uint32_t p = tid; p < R; p += WIDE_THREADS) cursor[p] = offs[(int64_t)p * G + g];
 
     for (int64_t tbase = begin; tbase < end; tbase += TILE) {
-        for (uint32_t i = tid; i < SC_WAVES * R / 2; i += SC_THREADS) ((uint32_t *)wcnt)[i] = 0;
+        for (uint32_t i = tid; i < WIDE_WAVES * R / 2; i += WIDE_THREADS) ((uint32_t *)wcnt)[i] = 0;
         uint32_t pid[ITEMS], rank[ITEMS];
         bool valid[ITEMS];
         const int64_t wbase = tbase + (int64_t)w * ITEMS * 64 + lane;
@@ -486,10 +764,10 @@ __global__ __launch_bounds__(SC_THREADS, 1) void k_scatter_wide(const char *__re
         __syncthreads();
         rank_items<ITEMS>(pid, valid, rank, wcnt + (size_t)w * R, pp.nbits, lane);
         __syncthreads();
-        for (uint32_t p = tid; p < R; p += SC_THREADS) {
+        for (uint32_t p = tid; p < R; p += WIDE_THREADS) {
             uint32_t s = 0;
 #pragma unroll
-            for (int v = 0; v < SC_WAVES; ++v) {
+            for (int v = 0; v < WIDE_WAVES; ++v) {
                 const uint32_t c = wcnt[(size_t)v * R + p];
                 wcnt[(size_t)v * R + p] = (uint16_t)s;
                 s += c;
@@ -510,35 +788,47 @@ __global__ __launch_bounds__(SC_THREADS, 1) void k_scatter_wide(const char *__re
             }
         }
         __syncthreads();
-        for (uint32_t p = tid; p < R; p += SC_THREADS) cursor[p] += tcnt[p];
+        for (uint32_t p = tid; p < R; p += WIDE_THREADS) cursor[p] += tcnt[p];
     }
 }
 
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t chunk, int G,
-                          const PartParams &pp, const uint32_t *offs, hipStream_t stream) {
+                          const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
+                          hipStream_t stream) {
+    if (rb == 16 && geo.waves == DMA_GEOM_TAG) {
+        (void)hipFuncSetAttribute((const void *)k_scatter16_dma, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)geo.lds_bytes);
+        hipLaunchKernelGGL(k_scatter16_dma, dim3(G), dim3(DMA_T), geo.lds_bytes, stream, (const uint4 *)in,
+                           (uint4 *)out, n, chunk, pp, offs, G);
+        return hipGetLastError();
+    }
     if (rb == 16) {
-        const ScatterGeom geo = scatter_geom16(pp.R);
         if (geo.items == 0) return hipErrorInvalidValue;
         const uint4 *i4 = (const uint4 *)in;
         uint4 *o4 = (uint4 *)out;
-#define SGX_SC16(K, I)                                                                          \
+#define SGX_SC16(K, W, I)                                                                       \
     do {                                                                                        \
-        (void)hipFuncSetAttribute((const void *)k_scatter16<K, I>,                             \
+        (void)hipFuncSetAttribute((const void *)k_scatter16<K, W, I>,                          \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
-        hipLaunchKernelGGL((k_scatter16<K, I>), dim3(G), dim3(SC_THREADS), geo.lds_bytes, stream,  \
+        hipLaunchKernelGGL((k_scatter16<K, W, I>), dim3(G), dim3(W * 64), geo.lds_bytes, stream, \
                            i4, o4, n, chunk, pp, offs, G);                                     \
     } while (0)
-#define SGX_SC16_K(K)                                \
-    switch (geo.items) {                             \
-    case 16: SGX_SC16(K, 16); break;                 \
-    case 12: SGX_SC16(K, 12); break;                 \
-    case 8: SGX_SC16(K, 8); break;                   \
-    case 6: SGX_SC16(K, 6); break;                   \
-    case 4: SGX_SC16(K, 4); break;                   \
-    case 3: SGX_SC16(K, 3); break;                   \
-    case 2: SGX_SC16(K, 2); break;                   \
-    default: SGX_SC16(K, 1); break;                  \
-    }
+#define SGX_SC16_K(K)                                                        \
+    do {                                                                     \
+        const int key = geo.waves * 100 + geo.items;                         \
+        switch (key) {                                                       \
+        case 416: SGX_SC16(K, 4, 16); break;                                 \
+        case 816: SGX_SC16(K, 8, 16); break;                                 \
+        case 412: SGX_SC16(K, 4, 12); break;                                 \
+        case 808: SGX_SC16(K, 8, 8); break;                                  \
+        case 408: SGX_SC16(K, 4, 8); break;                                  \
+        case 804: SGX_SC16(K, 8, 4); break;                                  \
+        case 404: SGX_SC16(K, 4, 4); break;                                  \
+        case 402: SGX_SC16(K, 4, 2); break;                                  \
+        case 401: SGX_SC16(K, 4, 1); break;                                  \
+        default: return hipErrorInvalidValue;                                \
+        }                                                                    \
+    } while (0)
         switch (pp.kind) {
         case SGX_PART_HASH: SGX_SC16_K(SGX_PART_HASH); break;
         case SGX_PART_RANGE_I64: SGX_SC16_K(SGX_PART_RANGE_I64); break;
@@ -547,7 +837,6 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
 #undef SGX_SC16_K
 #undef SGX_SC16
     } else {
-        const ScatterGeom geo = scatter_geom_wide(pp.R, rb);
         if (geo.items == 0 || (rb & 3) != 0 || rb < 12) return hipErrorInvalidValue;
         const char *ic = (const char *)in;
         char *oc = (char *)out;
@@ -555,7 +844,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
     do {                                                                                        \
         (void)hipFuncSetAttribute((const void *)k_scatter_wide<K, 4>,                          \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
-        hipLaunchKernelGGL((k_scatter_wide<K, 4>), dim3(G), dim3(SC_THREADS), geo.lds_bytes,     \
+        hipLaunchKernelGGL((k_scatter_wide<K, 4>), dim3(G), dim3(WIDE_THREADS), geo.lds_bytes,   \
                            stream, ic, oc, n, rb, chunk, pp, offs, G);                         \
     } while (0)
         switch (pp.kind) {

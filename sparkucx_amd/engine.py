@@ -79,8 +79,8 @@ class ShuffleEngine:
     RCCL communicator (the role CommonUcxShuffleManager.startUcxTransport plays,
     shuffle/ucx/CommonUcxShuffleManager.scala:67-100)."""
 
-    def __init__(self, device: int = 0, num_chunks: int = 0):
-        cfg = (ctypes.c_int32 * 4)(device, num_chunks, 0, 0)
+    def __init__(self, device: int = 0, num_chunks: int = 0, scatter_waves: int = 0, scatter_items: int = 0):
+        cfg = (ctypes.c_int32 * 4)(device, num_chunks, scatter_waves, scatter_items)
         h = ctypes.c_void_p()
         check(lib().sgx_create(ctypes.cast(cfg, ctypes.c_void_p), ctypes.byref(h)), "sgx_create")
         self.handle = h.value

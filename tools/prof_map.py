@@ -1,0 +1,45 @@
+#!/usr/bin/env python3
+"""Profiling driver: run the map-side write (C1 by default) a few times so rocprofv3 can
+trace / count the kernels.  Usage under the profiler (program directly after --):
+  rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 tools/prof_map.py
+  rocprofv3 --pmc FETCH_SIZE -d gpurun_out/pmc1 -o run -- python3 tools/prof_map.py
+"""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=1 << 28)
+    ap.add_argument("--partitions", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--num-chunks", type=int, default=0)
+    ap.add_argument("--dist", default="uniform")
+    a = ap.parse_args()
+    import numpy as np
+
+    import sparkucx_amd as sgx
+
+    e = sgx.ShuffleEngine(0, a.num_chunks)
+    buf = e.alloc(a.records * 16)
+    if a.dist == "uniform":
+        e.gen_uniform16(buf, a.records, 0x5EEDC0DE)
+    else:
+        r = np.arange(1, (1 << 24) + 1, dtype=np.float64)
+        cdf = np.cumsum(r ** -1.1)
+        cdf /= cdf[-1]
+        e.gen_zipf16(buf, a.records, 0x5EEDC0DE, cdf)
+    e.register_shuffle(1, a.partitions)
+    for i in range(a.iters):
+        e.write_map(1, i & 1, buf, a.records, 16, a.partitions)
+    e.sync()
+    st = e.stats()
+    print({k: round(v / max(1, st.count[k]), 4) for k, v in st.ms.items() if st.count[k]})
+    e.close()
+
+
+if __name__ == "__main__":
+    main()
