@@ -159,6 +159,7 @@ struct sgx_engine {
     int G = 256;
     int sc_waves = 0, sc_items = 0;  // K4 geometry override
     int diag = 0;                    // SGX_SCATTER_DIAG: measurement-only K4 ablation (wrong output)
+    int no_table = 0;                // SGX_NO_PEER_TABLE=1: ballots-only ranking (A/B)
     hipStream_t s_comp = nullptr, s_comm = nullptr;
     // work buffers of the map-side pipeline
     DevBuf counts, offs, status, part_off_dev, input_stage;
@@ -240,6 +241,7 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     e->sc_waves = cfg ? cfg->scatter_waves : 0;
     e->sc_items = cfg ? cfg->scatter_items : 0;
     if (const char *d = getenv("SGX_SCATTER_DIAG")) e->diag = atoi(d);
+    if (const char *d = getenv("SGX_NO_PEER_TABLE")) e->no_table = atoi(d);
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
     *out = e.release();
@@ -362,7 +364,10 @@ static int finish_lengths(Shuffle &s, MapOut &m) {
     if (m.ready) return SGX_OK;
     HIP_TRY(hipEventSynchronize(m.done));
     const uint32_t *po = (const uint32_t *)m.part_off.p;
-    if (po[s.R + 1] != 0) return fail(SGX_ERR_TIMEOUT, "scan look-back spin gave up (device flag %u)", po[s.R + 1]);
+    if (po[s.R + 1] & 1u) return fail(SGX_ERR_TIMEOUT, "scan look-back spin gave up (device flag %u)", po[s.R + 1]);
+    if (po[s.R + 1] & 2u)
+        return fail(SGX_ERR_HIP, "internal error: a scatter destination was out of range (device flag %u)",
+                    po[s.R + 1]);
     if ((int64_t)po[s.R] != m.nrec)
         return fail(SGX_ERR_HIP, "partition offsets do not sum to the record count (%u vs %lld)", po[s.R],
                     (long long)m.nrec);
@@ -451,11 +456,14 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
                         (uint32_t *)e->part_off_dev.p, G, s.R, st));
     HIP_TRY(hipEventRecord(c1, st));
     HIP_TRY(hipEventRecord(x0, st));
+    PartParams lpp = s.pp;
+    lpp.mbits = e->no_table ? 0u : (uint32_t)geo.mbits;
+    if (e->diag > 0) lpp.mbits = e->no_table ? 0u : (uint32_t)scatter_geom16((uint32_t)s.R, 8, 16).mbits;
     if (n > 0) {
         if (e->diag > 0 && rb == 16 && s.kind == SGX_PART_HASH)  // measurement-only ablation
-            HIP_TRY(launch_scatter_diag(e->diag, in, m.data.p, n, chunk, G, s.pp, (const uint32_t *)e->offs.p, st));
+            HIP_TRY(launch_scatter_diag(e->diag, in, m.data.p, n, chunk, G, lpp, (const uint32_t *)e->offs.p, ticket_err + 1, st));
         else
-            HIP_TRY(launch_scatter(in, m.data.p, n, rb, chunk, G, s.pp, (const uint32_t *)e->offs.p, geo, st));
+            HIP_TRY(launch_scatter(in, m.data.p, n, rb, chunk, G, lpp, (const uint32_t *)e->offs.p, geo, ticket_err + 1, st));
     }
     HIP_TRY(hipEventRecord(x1, st));
     // (R+1) offsets then the look-back give-up flag

@@ -16,6 +16,7 @@ struct PartParams {
     uint32_t nbits;      // bits needed to hold a partition id (ceil log2 R), >= 1
     int32_t nb;          // range bounds count (R - 1)
     int32_t ascending;   // RangePartitioner.ascending
+    uint32_t mbits;      // K4 peer-table width for this launch (0 = ballots only)
     const void *bounds;  // device: int64[nb] (RANGE_I64) or Key10[nb] (RANGE_BYTES10)
 };
 
@@ -32,12 +33,13 @@ struct ScatterGeom {
     int items;  // records per lane per tile
     int tile;   // waves * items * 64
     size_t lds_bytes;
+    int mbits;  // LDS peer-table width (0 = ballots only)
 };
 ScatterGeom scatter_geom16(uint32_t R, int force_waves = 0, int force_items = 0);
 // The LDS-DMA pipelined hash kernel (waves == DMA_GEOM_TAG); items == 0 if R does not fit.
 constexpr int DMA_GEOM_TAG = -1;
 ScatterGeom scatter_geom16_dma(uint32_t R);
-__host__ __device__ size_t scatter16_lds(uint32_t R, int waves, int items);
+__host__ __device__ size_t scatter16_lds(uint32_t R, int waves, int items, int mbits);
 ScatterGeom scatter_geom_wide(uint32_t R, int record_bytes);
 
 // Launchers (all asynchronous on `stream`).  counts / offs are [R][G] partition-major.
@@ -49,10 +51,11 @@ hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint
 int64_t scan_tiles(int64_t len);
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes, int64_t chunk,
                           int G, const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
-                          hipStream_t stream);
+                          uint32_t *err, hipStream_t stream);
 // Measurement-only ablations of the 8x16 hash scatter (SGX_SCATTER_DIAG=1..5; wrong output).
 hipError_t launch_scatter_diag(int mode, const void *in, void *out, int64_t n, int64_t chunk, int G,
-                               const PartParams &pp, const uint32_t *offs, hipStream_t stream);
+                               const PartParams &pp, const uint32_t *offs, uint32_t *err,
+                               hipStream_t stream);
 // items: [n][3] int64 {src_off, dst_off, bytes}; all offsets/bytes multiples of `align`.
 hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, int64_t n_items,
                              int align, hipStream_t stream);

@@ -328,19 +328,31 @@ hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint
 //           cursor[p] += tcnt[p].  cursor starts at offs[p][g] (K3).
 // ------------------------------------------------------------------------------------
 constexpr size_t LDS_MAX = 160 * 1024;
+constexpr uint32_t SCATTER_OOB = 2u;  // error bit: a scatter destination was out of range
 constexpr int WIDE_WAVES = 8;
 constexpr int DMA_WAVES = 8, DMA_ITEMS = 8;
 constexpr int DMA_T = DMA_WAVES * 64, DMA_TILE = DMA_WAVES * DMA_ITEMS * 64;
-size_t scatter16_dma_lds(uint32_t R);
+size_t scatter16_dma_lds(uint32_t R, int mbits);
 constexpr int WIDE_THREADS = WIDE_WAVES * 64;
 
 __host__ __device__ constexpr size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
+// Per-wave u16 counter rows are padded to an even length so each row starts on a dword:
+// rank_items updates them two-per-dword with ds_add_rtn_u32.
+__host__ __device__ constexpr uint32_t rowstride(uint32_t R) { return (R + 1u) & ~1u; }
 
 // LDS of the 16 B scatter: stage[TILE] uint4 | wcnt[WAVES][R] u16 | lstart[R] u16 |
 // tcnt[R] u16 | cursor[R] u32.  The block-scan scratch borrows the (idle) stage.
-__host__ __device__ size_t scatter16_lds(uint32_t R, int waves, int items) {
+__host__ __device__ size_t scatter16_lds(uint32_t R, int waves, int items, int mbits) {
     const size_t tile = (size_t)waves * items * 64;
-    return tile * 16 + al16((size_t)waves * R * 2) + 2 * al16((size_t)R * 2) + al16((size_t)R * 4);
+    return tile * 16 + al16((size_t)waves * rowstride(R) * 2) + 2 * al16((size_t)R * 2) + al16((size_t)R * 4) +
+           (mbits ? (size_t)waves * ((size_t)8 << mbits) : 0);
+}
+
+// Largest peer-table width (<= nbits, <= 8) that still fits next to a geometry.
+static int table_bits(uint32_t R, int waves, int items, uint32_t nbits, size_t budget) {
+    for (int mb = (int)(nbits < 8 ? nbits : 8); mb >= 1; --mb)
+        if (scatter16_lds(R, waves, items, mb) <= budget) return mb;
+    return 0;
 }
 
 struct Geo16 { int waves, items; };
@@ -348,26 +360,32 @@ struct Geo16 { int waves, items; };
 static const Geo16 kGeos16[] = {{4, 16}, {8, 16}, {4, 12}, {8, 8}, {4, 8}, {8, 4}, {4, 4}, {4, 2}, {4, 1}};
 
 ScatterGeom scatter_geom16_dma(uint32_t R) {
-    const size_t lds = scatter16_dma_lds(R);
-    if (lds > LDS_MAX) return ScatterGeom{0, 0, 0, 0};
-    return ScatterGeom{DMA_GEOM_TAG, DMA_ITEMS, DMA_TILE, lds};
+    if (scatter16_dma_lds(R, 0) > LDS_MAX) return ScatterGeom{0, 0, 0, 0, 0};
+    uint32_t nb = 0;
+    while ((1ull << nb) < R) ++nb;
+    int mb = (int)(nb < 8 ? (nb ? nb : 1) : 8);
+    while (mb > 0 && scatter16_dma_lds(R, mb) > LDS_MAX) --mb;
+    return ScatterGeom{DMA_GEOM_TAG, DMA_ITEMS, DMA_TILE, scatter16_dma_lds(R, mb), mb};
 }
 
 ScatterGeom scatter_geom16(uint32_t R, int force_waves, int force_items) {
-    ScatterGeom best{0, 0, 0, 0};
+    ScatterGeom best{0, 0, 0, 0, 0};
     long best_score = -1;
     int best_occ = 0;
     for (const Geo16 &g : kGeos16) {
         if (force_waves && force_waves != g.waves) continue;
         if (force_items && force_items != g.items) continue;
-        const size_t lds = scatter16_lds(R, g.waves, g.items);
-        if (lds > LDS_MAX) continue;
-        const int occ = (int)(LDS_MAX / lds);
+        const size_t base = scatter16_lds(R, g.waves, g.items, 0);
+        if (base > LDS_MAX) continue;
+        const int occ = (int)(LDS_MAX / base);
         const int tile = g.waves * g.items * 64;
         // records in flight per CU (capped at two workgroups), then occupancy
         const long score = (long)tile * (occ < 2 ? occ : 2);
         if (score > best_score || (score == best_score && occ > best_occ)) {
-            best = ScatterGeom{g.waves, g.items, tile, lds};
+            uint32_t nb = 0;
+            while ((1ull << nb) < R) ++nb;
+            const int mb = table_bits(R, g.waves, g.items, nb ? nb : 1, LDS_MAX / occ);
+            best = ScatterGeom{g.waves, g.items, tile, scatter16_lds(R, g.waves, g.items, mb), mb};
             best_score = score;
             best_occ = occ;
         }
@@ -376,13 +394,13 @@ ScatterGeom scatter_geom16(uint32_t R, int force_waves, int force_items) {
 }
 
 static size_t scatter_lds_wide(uint32_t R) {
-    return al16((size_t)WIDE_WAVES * R * 2) + (size_t)2 * R * 4 + 64;
+    return al16((size_t)WIDE_WAVES * rowstride(R) * 2) + (size_t)2 * R * 4 + 64;
 }
 
 ScatterGeom scatter_geom_wide(uint32_t R, int /*rb*/) {
     const size_t lds = scatter_lds_wide(R);
-    if (lds > LDS_MAX) return ScatterGeom{WIDE_WAVES, 0, 0, 0};
-    return ScatterGeom{WIDE_WAVES, 4, WIDE_WAVES * 4 * 64, lds};
+    if (lds > LDS_MAX) return ScatterGeom{WIDE_WAVES, 0, 0, 0, 0};
+    return ScatterGeom{WIDE_WAVES, 4, WIDE_WAVES * 4 * 64, lds, 0};
 }
 
 // Slot -> partition for the drain: the last p with lstart[p] <= s (empty partitions
@@ -397,21 +415,60 @@ __device__ __forceinline__ uint32_t slot_partition(const T *lstart, uint32_t R, 
     return lo;
 }
 
+// Stable within-wave ranking of ITEMS records per lane (input order = item, then lane).
+// Equal-id lanes ("peers") are found exactly: with a per-wave LDS mask table of 2^mbits
+// u64 entries, every valid lane ORs its lane bit into entry (pid & (2^mbits-1)), reads the
+// entry back (candidates = lanes sharing the low mbits bits) and clears it; the remaining
+// high id bits are matched with one ballot each (mbits == 0: one ballot per id bit).
+// Counters: the wave's u16 counters are packed two per dword; each item's leader (lowest
+// peer) does one ds_add_rtn_u32 of popc(peers) into its half, and the old value is
+// broadcast to the peers with ds_bpermute.  Every phase is issued for all ITEMS items
+// back to back (LDS executes a wave's ops in order, so the OR / read / clear sequence of
+// item k+1 is correct without waiting for item k) and waits once: the ranking is
+// throughput-bound, not LDS-latency-bound.
 template <int ITEMS>
 __device__ __forceinline__ void rank_items(const uint32_t (&pid)[ITEMS], const bool (&valid)[ITEMS],
                                            uint32_t (&rank)[ITEMS], uint16_t *mycnt, uint32_t nbits,
-                                           uint32_t lane) {
+                                           uint32_t lane, uint64_t *mytab, uint32_t mbits) {
     const uint64_t lt = (1ull << lane) - 1ull;
+    const uint64_t mybit = 1ull << lane;
+    uint64_t peers[ITEMS];
+    if (mbits) {
+        const uint32_t mmask = (1u << mbits) - 1u;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            volatile uint64_t *slot = (volatile uint64_t *)(mytab + (pid[k] & mmask));
+            if (valid[k]) atomicOr((unsigned long long *)slot, (unsigned long long)mybit);
+            peers[k] = valid[k] ? *slot : 0ull;
+            if (valid[k]) *slot = 0ull;
+        }
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            for (uint32_t b = mbits; b < nbits; ++b) {
+                const bool bit = (pid[k] >> b) & 1u;
+                const uint64_t m = __ballot(bit);
+                peers[k] &= bit ? m : ~m;
+            }
+        }
+    } else {
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) peers[k] = match_peers(pid[k], __ballot(valid[k]), nbits);
+    }
+    uint32_t old[ITEMS];
+    uint32_t *words = (uint32_t *)mycnt;
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
-        const uint64_t vm = __ballot(valid[k]);
-        const uint32_t p = pid[k];
-        const uint64_t peers = match_peers(p, vm, nbits);
-        const uint64_t below = peers & lt;
-        uint32_t base = 0;
-        if (valid[k]) base = mycnt[p];
-        rank[k] = base + (uint32_t)__popcll(below);
-        if (valid[k] && below == 0) mycnt[p] = (uint16_t)(base + (uint32_t)__popcll(peers));
+        old[k] = 0;
+        if (valid[k] && (peers[k] & lt) == 0) {
+            const uint32_t sh = (pid[k] & 1u) << 4;
+            old[k] = (atomicAdd(&words[pid[k] >> 1], (uint32_t)__popcll(peers[k]) << sh) >> sh) & 0xFFFFu;
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        const int leader = valid[k] ? (int)__ffsll((unsigned long long)peers[k]) - 1 : (int)lane;
+        const uint32_t base = (uint32_t)__builtin_amdgcn_ds_bpermute(leader << 2, (int)old[k]);
+        rank[k] = base + (uint32_t)__popcll(peers[k] & lt);
     }
 }
 
@@ -429,18 +486,24 @@ struct Sc16Lds {
     uint4 *stage;
     uint16_t *wcnt, *lstart, *tcnt;
     uint32_t *cursor, *scratch;
+    uint64_t *mtab;  // [WAVES][2^mbits] peer masks (mbits = pp.mbits, may be 0)
+    uint32_t mbits;
 };
 
 template <int WAVES, int ITEMS>
-__device__ __forceinline__ Sc16Lds sc16_lds(char *smem, uint32_t R) {
+__device__ __forceinline__ Sc16Lds sc16_lds(char *smem, uint32_t R, uint32_t mbits) {
     constexpr int TILE = WAVES * ITEMS * 64;
     Sc16Lds L;
     L.stage = (uint4 *)smem;
     L.wcnt = (uint16_t *)(smem + (size_t)TILE * 16);
-    L.lstart = (uint16_t *)((char *)L.wcnt + al16((size_t)WAVES * R * 2));
+    L.lstart = (uint16_t *)((char *)L.wcnt + al16((size_t)WAVES * rowstride(R) * 2));
     L.tcnt = (uint16_t *)((char *)L.lstart + al16((size_t)R * 2));
     L.cursor = (uint32_t *)((char *)L.tcnt + al16((size_t)R * 2));
+    L.mtab = (uint64_t *)((char *)L.cursor + al16((size_t)R * 4));
     L.scratch = (uint32_t *)smem;  // block-scan scratch: stage is idle then
+    L.mbits = mbits;
+    // the peer table starts (and, item by item, stays) all zero
+    for (uint32_t i = threadIdx.x; i < (uint32_t)(WAVES << mbits) && mbits; i += WAVES * 64) L.mtab[i] = 0ull;
     return L;
 }
 
@@ -453,26 +516,28 @@ __device__ __forceinline__ void sc16_rank_stage(const Sc16Lds &L, uint32_t R, co
     constexpr int T = WAVES * 64;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint32_t rank[ITEMS];
-    rank_items<ITEMS>(pid, valid, rank, L.wcnt + (size_t)w * R, nbits, lane);
+    rank_items<ITEMS>(pid, valid, rank, L.wcnt + (size_t)w * rowstride(R), nbits, lane,
+                      L.mtab + ((size_t)w << L.mbits), L.mbits);
     lds_barrier();
     for (uint32_t p = tid; p < R; p += T) {
         uint32_t s = 0;
 #pragma unroll
         for (int v = 0; v < WAVES; ++v) {
-            const uint32_t c = L.wcnt[(size_t)v * R + p];
-            L.wcnt[(size_t)v * R + p] = (uint16_t)s;
+            const uint32_t c = L.wcnt[(size_t)v * rowstride(R) + p];
+            L.wcnt[(size_t)v * rowstride(R) + p] = (uint16_t)s;
             s += c;
         }
         L.tcnt[p] = (uint16_t)s;
     }
     lds_barrier();
     block_exclusive_scan(L.tcnt, L.lstart, R, L.scratch);
-    const uint16_t *mycnt = L.wcnt + (size_t)w * R;
+    const uint16_t *mycnt = L.wcnt + (size_t)w * rowstride(R);
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
         if (valid[k]) {
             const uint32_t p = pid[k];
-            L.stage[(uint32_t)L.lstart[p] + mycnt[p] + rank[k]] = rec[k];
+            const uint32_t slot = (uint32_t)L.lstart[p] + mycnt[p] + rank[k];
+            if (slot < (uint32_t)(WAVES * ITEMS * 64)) L.stage[slot] = rec[k];
         }
     }
     lds_barrier();
@@ -486,12 +551,12 @@ __device__ __forceinline__ void sc16_rank_stage(const Sc16Lds &L, uint32_t R, co
 template <int KIND, int WAVES, int ITEMS, int DIAG = 0>
 __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 *__restrict__ in,
                                                   uint4 *__restrict__ out, int64_t tbase, int64_t end,
-                                                  const PartParams &pp) {
+                                                  const PartParams &pp, int64_t n, uint32_t *err) {
     constexpr int T = WAVES * 64;
     constexpr int TILE = WAVES * ITEMS * 64;
     const uint32_t R = pp.R;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (uint32_t i = tid; i < (uint32_t)(WAVES * R / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)(WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
     uint4 rec[ITEMS];
     uint32_t pid[ITEMS];
     bool valid[ITEMS];
@@ -529,6 +594,7 @@ __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k)
             if (valid[k]) out[(size_t)(wbase + (int64_t)k * 64)] = rec[k];
+        (void)n; (void)err;
     } else {
         for (uint32_t s = tid; s < tile_n; s += T) {
             const uint4 r = L.stage[s];
@@ -541,7 +607,8 @@ __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 
             if constexpr (DIAG == 1) {
                 asm volatile("" ::"v"(r.x), "v"(r.y), "v"(r.z), "v"(r.w), "v"(d));
             } else {
-                out[(size_t)d] = r;
+                if ((int64_t)d < n) out[(size_t)d] = r;
+                else atomicOr(err, SCATTER_OOB);
             }
         }
     }
@@ -555,12 +622,12 @@ __global__ __launch_bounds__(WAVES * 64, 2) void k_scatter16(const uint4 *__rest
                                                              uint4 *__restrict__ out, int64_t n,
                                                              int64_t chunk, PartParams pp,
                                                              const uint32_t *__restrict__ offs,
-                                                             int G) {
+                                                             int G, uint32_t *err) {
     constexpr int T = WAVES * 64;
     constexpr int TILE = WAVES * ITEMS * 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t R = pp.R;
-    const Sc16Lds L = sc16_lds<WAVES, ITEMS>(smem, R);
+    const Sc16Lds L = sc16_lds<WAVES, ITEMS>(smem, R, pp.mbits);
     const uint32_t tid = threadIdx.x;
     const int g = blockIdx.x;
     const int64_t begin = (int64_t)g * chunk;
@@ -568,18 +635,19 @@ __global__ __launch_bounds__(WAVES * 64, 2) void k_scatter16(const uint4 *__rest
     for (uint32_t p = tid; p < R; p += T) L.cursor[p] = offs[(int64_t)p * G + g];
     __syncthreads();
     for (int64_t tbase = begin; tbase < end; tbase += TILE)
-        sc16_tile_generic<KIND, WAVES, ITEMS>(L, in, out, tbase, end, pp);
+        sc16_tile_generic<KIND, WAVES, ITEMS>(L, in, out, tbase, end, pp, n, err);
 }
 
 template <int DIAG>
 __global__ __launch_bounds__(512, 2) void k_scatter16_diag(const uint4 *__restrict__ in,
                                                            uint4 *__restrict__ out, int64_t n,
                                                            int64_t chunk, PartParams pp,
-                                                           const uint32_t *__restrict__ offs, int G) {
+                                                           const uint32_t *__restrict__ offs, int G,
+                                                           uint32_t *err) {
     constexpr int WAVES = 8, ITEMS = 16, T = WAVES * 64, TILE = WAVES * ITEMS * 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t R = pp.R;
-    const Sc16Lds L = sc16_lds<WAVES, ITEMS>(smem, R);
+    const Sc16Lds L = sc16_lds<WAVES, ITEMS>(smem, R, pp.mbits);
     const uint32_t tid = threadIdx.x;
     const int g = blockIdx.x;
     const int64_t begin = (int64_t)g * chunk;
@@ -587,19 +655,20 @@ __global__ __launch_bounds__(512, 2) void k_scatter16_diag(const uint4 *__restri
     for (uint32_t p = tid; p < R; p += T) L.cursor[p] = offs[(int64_t)p * G + g];
     __syncthreads();
     for (int64_t tbase = begin; tbase < end; tbase += TILE)
-        sc16_tile_generic<SGX_PART_HASH, WAVES, ITEMS, DIAG>(L, in, out, tbase, end, pp);
+        sc16_tile_generic<SGX_PART_HASH, WAVES, ITEMS, DIAG>(L, in, out, tbase, end, pp, n, err);
 }
 
 hipError_t launch_scatter_diag(int mode, const void *in, void *out, int64_t n, int64_t chunk, int G,
-                               const PartParams &pp, const uint32_t *offs, hipStream_t stream) {
-    const size_t lds = scatter16_lds(pp.R, 8, 16);
+                               const PartParams &pp, const uint32_t *offs, uint32_t *err,
+                               hipStream_t stream) {
+    const size_t lds = scatter16_lds(pp.R, 8, 16, pp.mbits);
     if (lds > LDS_MAX || pp.kind != SGX_PART_HASH) return hipErrorInvalidValue;
 #define SGX_DIAGK(M)                                                                            \
     do {                                                                                        \
         (void)hipFuncSetAttribute((const void *)k_scatter16_diag<M>,                           \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
         hipLaunchKernelGGL(k_scatter16_diag<M>, dim3(G), dim3(512), lds, stream, (const uint4 *)in, \
-                           (uint4 *)out, n, chunk, pp, offs, G);                                \
+                           (uint4 *)out, n, chunk, pp, offs, G, err);                           \
     } while (0)
     switch (mode) {
     case 1: SGX_DIAGK(1); break;
@@ -626,8 +695,8 @@ hipError_t launch_scatter_diag(int mode, const void *in, void *out, int64_t n, i
 // (cdna_hip_programming.md §5.7), so no compiler-inserted vmcnt(0) drains it; every
 // barrier in the loop is an LDS-only barrier (lgkmcnt(0) + s_barrier).
 // ------------------------------------------------------------------------------------
-size_t scatter16_dma_lds(uint32_t R) {
-    return scatter16_lds(R, DMA_WAVES, DMA_ITEMS) + (size_t)DMA_TILE * 16;
+size_t scatter16_dma_lds(uint32_t R, int mbits) {
+    return scatter16_lds(R, DMA_WAVES, DMA_ITEMS, mbits) + (size_t)DMA_TILE * 16;
 }
 
 __device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst) {
@@ -652,12 +721,12 @@ __global__ __launch_bounds__(DMA_T, 2) void k_scatter16_dma(const uint4 *__restr
                                                            uint4 *__restrict__ out, int64_t n,
                                                            int64_t chunk, PartParams pp,
                                                            const uint32_t *__restrict__ offs,
-                                                           int G) {
+                                                           int G, uint32_t *err) {
     constexpr int T = DMA_T, TILE = DMA_TILE, ITEMS = DMA_ITEMS;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t R = pp.R;
-    const Sc16Lds L = sc16_lds<DMA_WAVES, DMA_ITEMS>(smem, R);
-    const size_t xoff = scatter16_lds(R, DMA_WAVES, DMA_ITEMS);
+    const Sc16Lds L = sc16_lds<DMA_WAVES, DMA_ITEMS>(smem, R, pp.mbits);
+    const size_t xoff = scatter16_lds(R, DMA_WAVES, DMA_ITEMS, pp.mbits);
     const uint4 *X = (const uint4 *)(smem + xoff);
     const uint32_t tid = threadIdx.x, lane = tid & 63;
     const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -668,7 +737,7 @@ __global__ __launch_bounds__(DMA_T, 2) void k_scatter16_dma(const uint4 *__restr
     const int64_t begin = (int64_t)g * chunk;
     const int64_t end = min(n, begin + chunk);
     for (uint32_t p = tid; p < R; p += T) L.cursor[p] = offs[(int64_t)p * G + g];
-    for (uint32_t i = tid; i < (uint32_t)(DMA_WAVES * R / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
+    for (uint32_t i = tid; i < (uint32_t)(DMA_WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
     const int64_t nfull = end > begin ? (end - begin) / TILE : 0;
     const uint4 *src = in + begin + (int64_t)w * ITEMS * 64 + lane;
     if (nfull > 0) {
@@ -711,17 +780,21 @@ __global__ __launch_bounds__(DMA_T, 2) void k_scatter16_dma(const uint4 *__restr
                 d[j] = L.cursor[p] - (uint32_t)L.lstart[p];
             }
 #pragma unroll
-            for (int j = 0; j < 4; ++j) out[(size_t)(d[j] + (uint32_t)((k0 + j) * T + tid))] = r[j];
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t dst = d[j] + (uint32_t)((k0 + j) * T + tid);
+                if ((int64_t)dst < n) out[(size_t)dst] = r[j];
+                else atomicOr(err, SCATTER_OOB);
+            }
         }
         lds_barrier();
         for (uint32_t p = tid; p < R; p += T) L.cursor[p] += L.tcnt[p];
-        for (uint32_t i = tid; i < (uint32_t)(DMA_WAVES * R / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
+        for (uint32_t i = tid; i < (uint32_t)(DMA_WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
         lds_barrier();
     }
     wait_vmcnt<0>();  // retire the clamped re-prefetch before X/stage are reused
     __syncthreads();
     for (int64_t tbase = begin + nfull * TILE; tbase < end; tbase += TILE)
-        sc16_tile_generic<SGX_PART_HASH, DMA_WAVES, DMA_ITEMS>(L, in, out, tbase, end, pp);
+        sc16_tile_generic<SGX_PART_HASH, DMA_WAVES, DMA_ITEMS>(L, in, out, tbase, end, pp, n, err);
 }
 
 // Wide records (record_bytes multiple of 4, e.g. TeraSort's 100 B): same ranking, each
@@ -732,12 +805,12 @@ __global__ __launch_bounds__(WIDE_THREADS, 1) void k_scatter_wide(const char *__
                                                                 int rb, int64_t chunk,
                                                                 PartParams pp,
                                                                 const uint32_t *__restrict__ offs,
-                                                                int G) {
+                                                                int G, uint32_t *err) {
     constexpr int TILE = WIDE_WAVES * ITEMS * 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t R = pp.R;
     uint16_t *wcnt = (uint16_t *)smem;
-    uint32_t *cursor = (uint32_t *)(smem + (((size_t)WIDE_WAVES * R * 2 + 15) & ~(size_t)15));
+    uint32_t *cursor = (uint32_t *)(smem + al16((size_t)WIDE_WAVES * rowstride(R) * 2));
     uint32_t *tcnt = cursor + R;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int g = blockIdx.x;
@@ -747,7 +820,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 1) void k_scatter_wide(const char *__
     for (uint32_t p = tid; p < R; p += WIDE_THREADS) cursor[p] = offs[(int64_t)p * G + g];
 
     for (int64_t tbase = begin; tbase < end; tbase += TILE) {
-        for (uint32_t i = tid; i < WIDE_WAVES * R / 2; i += WIDE_THREADS) ((uint32_t *)wcnt)[i] = 0;
+        for (uint32_t i = tid; i < WIDE_WAVES * rowstride(R) / 2; i += WIDE_THREADS) ((uint32_t *)wcnt)[i] = 0;
         uint32_t pid[ITEMS], rank[ITEMS];
         bool valid[ITEMS];
         const int64_t wbase = tbase + (int64_t)w * ITEMS * 64 + lane;
@@ -762,26 +835,27 @@ __global__ __launch_bounds__(WIDE_THREADS, 1) void k_scatter_wide(const char *__
             }
         }
         __syncthreads();
-        rank_items<ITEMS>(pid, valid, rank, wcnt + (size_t)w * R, pp.nbits, lane);
+        rank_items<ITEMS>(pid, valid, rank, wcnt + (size_t)w * rowstride(R), pp.nbits, lane, nullptr, 0u);
         __syncthreads();
         for (uint32_t p = tid; p < R; p += WIDE_THREADS) {
             uint32_t s = 0;
 #pragma unroll
             for (int v = 0; v < WIDE_WAVES; ++v) {
-                const uint32_t c = wcnt[(size_t)v * R + p];
-                wcnt[(size_t)v * R + p] = (uint16_t)s;
+                const uint32_t c = wcnt[(size_t)v * rowstride(R) + p];
+                wcnt[(size_t)v * rowstride(R) + p] = (uint16_t)s;
                 s += c;
             }
             tcnt[p] = s;
         }
         __syncthreads();
-        const uint16_t *mycnt = wcnt + (size_t)w * R;
+        const uint16_t *mycnt = wcnt + (size_t)w * rowstride(R);
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) {
             if (valid[k]) {
                 const int64_t i = wbase + (int64_t)k * 64;
                 const uint32_t p = pid[k];
                 const uint64_t dst = (uint64_t)cursor[p] + mycnt[p] + rank[k];
+                if ((int64_t)dst >= n) { atomicOr(err, SCATTER_OOB); continue; }
                 const uint32_t *s = (const uint32_t *)(in + i * rb);
                 uint32_t *d = (uint32_t *)(out + dst * (uint64_t)rb);
                 for (int q = 0; q < dw; ++q) d[q] = s[q];
@@ -794,12 +868,12 @@ __global__ __launch_bounds__(WIDE_THREADS, 1) void k_scatter_wide(const char *__
 
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t chunk, int G,
                           const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
-                          hipStream_t stream) {
+                          uint32_t *err, hipStream_t stream) {
     if (rb == 16 && geo.waves == DMA_GEOM_TAG) {
         (void)hipFuncSetAttribute((const void *)k_scatter16_dma, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)geo.lds_bytes);
         hipLaunchKernelGGL(k_scatter16_dma, dim3(G), dim3(DMA_T), geo.lds_bytes, stream, (const uint4 *)in,
-                           (uint4 *)out, n, chunk, pp, offs, G);
+                           (uint4 *)out, n, chunk, pp, offs, G, err);
         return hipGetLastError();
     }
     if (rb == 16) {
@@ -811,7 +885,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         (void)hipFuncSetAttribute((const void *)k_scatter16<K, W, I>,                          \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
         hipLaunchKernelGGL((k_scatter16<K, W, I>), dim3(G), dim3(W * 64), geo.lds_bytes, stream, \
-                           i4, o4, n, chunk, pp, offs, G);                                     \
+                           i4, o4, n, chunk, pp, offs, G, err);                                \
     } while (0)
 #define SGX_SC16_K(K)                                                        \
     do {                                                                     \
@@ -845,7 +919,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         (void)hipFuncSetAttribute((const void *)k_scatter_wide<K, 4>,                          \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
         hipLaunchKernelGGL((k_scatter_wide<K, 4>), dim3(G), dim3(WIDE_THREADS), geo.lds_bytes,   \
-                           stream, ic, oc, n, rb, chunk, pp, offs, G);                         \
+                           stream, ic, oc, n, rb, chunk, pp, offs, G, err);                    \
     } while (0)
         switch (pp.kind) {
         case SGX_PART_HASH: SGX_SCW(SGX_PART_HASH); break;
