@@ -157,9 +157,12 @@ struct sgx_engine {
     int device = 0;
     int num_cus = 256;
     int G = 256;
+    bool G_forced = false;
     int sc_waves = 0, sc_items = 0;  // K4 geometry override
     int diag = 0;                    // SGX_SCATTER_DIAG: measurement-only K4 ablation (wrong output)
     int no_table = 0;                // SGX_NO_PEER_TABLE=1: ballots-only ranking (A/B)
+    int direct = 0;                  // SGX_SCATTER_DIRECT=WWII: direct-store K4 (A/B)
+    int use_dma = 0;                 // SGX_SCATTER_DMA=1: LDS-DMA pipelined K4 (A/B)
     hipStream_t s_comp = nullptr, s_comm = nullptr;
     // work buffers of the map-side pipeline
     DevBuf counts, offs, status, part_off_dev, input_stage;
@@ -238,10 +241,13 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     e->device = dev;
     e->num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
     e->G = (cfg && cfg->num_chunks > 0) ? cfg->num_chunks : e->num_cus;
+    e->G_forced = cfg && cfg->num_chunks > 0;
     e->sc_waves = cfg ? cfg->scatter_waves : 0;
     e->sc_items = cfg ? cfg->scatter_items : 0;
     if (const char *d = getenv("SGX_SCATTER_DIAG")) e->diag = atoi(d);
     if (const char *d = getenv("SGX_NO_PEER_TABLE")) e->no_table = atoi(d);
+    if (const char *d = getenv("SGX_SCATTER_DIRECT")) e->direct = atoi(d);
+    if (const char *d = getenv("SGX_SCATTER_DMA")) e->use_dma = atoi(d);
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
     *out = e.release();
@@ -419,9 +425,14 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
     // chunking: G chunks, each a whole number of scatter tiles where possible
     ScatterGeom geo = rb == 16 ? scatter_geom16((uint32_t)s.R, e->sc_waves, e->sc_items)
                                : scatter_geom_wide((uint32_t)s.R, rb);
-    // hash partitioner, 16 B records: the LDS-DMA pipelined kernel unless a geometry is forced
     if (e->diag > 0 && rb == 16) geo = scatter_geom16((uint32_t)s.R, 8, 16);
-    if (rb == 16 && s.kind == SGX_PART_HASH && e->sc_waves == 0 && e->sc_items == 0 && e->diag == 0) {
+    // experiment hook: SGX_SCATTER_DIRECT=<waves><items as 2 digits> selects the direct kernel
+    if (e->direct > 0 && rb == 16) {
+        const ScatterGeom d = scatter_geom16_direct((uint32_t)s.R, e->direct / 100, e->direct % 100);
+        if (d.items) geo = d;
+    }
+    if (rb == 16 && s.kind == SGX_PART_HASH && e->sc_waves == 0 && e->sc_items == 0 && e->diag == 0 &&
+        e->direct == 0 && e->use_dma) {
         const ScatterGeom d = scatter_geom16_dma((uint32_t)s.R);
         if (d.items) geo = d;
     }
@@ -429,7 +440,15 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
         return fail(SGX_ERR_UNSUPPORTED, "no scatter geometry (waves %d, items %d) fits R=%d", e->sc_waves,
                     e->sc_items, s.R);
     const int tile = geo.tile;
-    int64_t chunk = n > 0 ? (n + e->G - 1) / e->G : 1;
+    int Gt = e->G;
+    if (geo.waves >= DIRECT_GEOM_BASE && !e->G_forced) {
+        // several direct-store workgroups per CU: one chunk per resident workgroup
+        const int wv = geo.waves - DIRECT_GEOM_BASE;
+        int occ = (int)((160 * 1024) / geo.lds_bytes);
+        if (occ > 32 / wv) occ = 32 / wv;
+        Gt = e->num_cus * (occ > 0 ? occ : 1);
+    }
+    int64_t chunk = n > 0 ? (n + Gt - 1) / Gt : 1;
     chunk = (chunk + tile - 1) / tile * tile;
     const int G = n > 0 ? (int)((n + chunk - 1) / chunk) : 1;
     const int64_t len = (int64_t)s.R * G;

@@ -39,6 +39,9 @@ ScatterGeom scatter_geom16(uint32_t R, int force_waves = 0, int force_items = 0)
 // The LDS-DMA pipelined hash kernel (waves == DMA_GEOM_TAG); items == 0 if R does not fit.
 constexpr int DMA_GEOM_TAG = -1;
 ScatterGeom scatter_geom16_dma(uint32_t R);
+// Direct-store kernel (waves == DIRECT_GEOM_BASE + real waves).
+constexpr int DIRECT_GEOM_BASE = 1000;
+ScatterGeom scatter_geom16_direct(uint32_t R, int waves, int items);
 __host__ __device__ size_t scatter16_lds(uint32_t R, int waves, int items, int mbits);
 ScatterGeom scatter_geom_wide(uint32_t R, int record_bytes);
 

@@ -330,6 +330,7 @@ hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint
 constexpr size_t LDS_MAX = 160 * 1024;
 constexpr uint32_t SCATTER_OOB = 2u;  // error bit: a scatter destination was out of range
 constexpr int WIDE_WAVES = 8;
+__host__ __device__ size_t scatter16_direct_lds(uint32_t R, int waves, int mbits);
 constexpr int DMA_WAVES = 8, DMA_ITEMS = 8;
 constexpr int DMA_T = DMA_WAVES * 64, DMA_TILE = DMA_WAVES * DMA_ITEMS * 64;
 size_t scatter16_dma_lds(uint32_t R, int mbits);
@@ -359,6 +360,19 @@ struct Geo16 { int waves, items; };
 // every instantiated geometry (launch_scatter's switch must list the same set)
 static const Geo16 kGeos16[] = {{4, 16}, {8, 16}, {4, 12}, {8, 8}, {4, 8}, {8, 4}, {4, 4}, {4, 2}, {4, 1}};
 
+ScatterGeom scatter_geom16_direct(uint32_t R, int waves, int items) {
+    static const int ok[][2] = {{4, 16}, {4, 8}, {8, 16}, {8, 8}, {8, 4}};
+    bool found = false;
+    for (auto &g : ok) found |= (g[0] == waves && g[1] == items);
+    if (!found) return ScatterGeom{0, 0, 0, 0, 0};
+    uint32_t nb = 0;
+    while ((1ull << nb) < R) ++nb;
+    int mb = (int)(nb < 7 ? (nb ? nb : 1) : 7);
+    if (scatter16_direct_lds(R, waves, 0) > LDS_MAX) return ScatterGeom{0, 0, 0, 0, 0};
+    while (mb > 0 && scatter16_direct_lds(R, waves, mb) > LDS_MAX / 2) --mb;
+    return ScatterGeom{DIRECT_GEOM_BASE + waves, items, waves * items * 64, scatter16_direct_lds(R, waves, mb), mb};
+}
+
 ScatterGeom scatter_geom16_dma(uint32_t R) {
     if (scatter16_dma_lds(R, 0) > LDS_MAX) return ScatterGeom{0, 0, 0, 0, 0};
     uint32_t nb = 0;
@@ -379,8 +393,9 @@ ScatterGeom scatter_geom16(uint32_t R, int force_waves, int force_items) {
         if (base > LDS_MAX) continue;
         const int occ = (int)(LDS_MAX / base);
         const int tile = g.waves * g.items * 64;
-        // records in flight per CU (capped at two workgroups), then occupancy
-        const long score = (long)tile * (occ < 2 ? occ : 2);
+        // biggest tile first (longest partition runs, least per-tile O(R) overhead; one
+        // chunk per CU keeps a second resident workgroup idle anyway), then occupancy
+        const long score = (long)tile;
         if (score > best_score || (score == best_score && occ > best_occ)) {
             uint32_t nb = 0;
             while ((1ull << nb) < R) ++nb;
@@ -437,10 +452,12 @@ __device__ __forceinline__ void rank_items(const uint32_t (&pid)[ITEMS], const b
         const uint32_t mmask = (1u << mbits) - 1u;
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) {
-            volatile uint64_t *slot = (volatile uint64_t *)(mytab + (pid[k] & mmask));
-            if (valid[k]) atomicOr((unsigned long long *)slot, (unsigned long long)mybit);
-            peers[k] = valid[k] ? *slot : 0ull;
-            if (valid[k]) *slot = 0ull;
+            // relaxed workgroup-scope atomics (not volatile: volatile defeats LDS address-space
+            // inference and turns these into flat ops that wait on vmcnt)
+            uint64_t *slot = mytab + (pid[k] & mmask);
+            if (valid[k]) __hip_atomic_fetch_or(slot, mybit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            peers[k] = valid[k] ? __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) : 0ull;
+            if (valid[k]) __hip_atomic_store(slot, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) {
@@ -481,6 +498,18 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
+// Diagnostic phase stamps (DIAG == 6 only; never in the product kernels): wave 0 / lane 0
+// of every workgroup accumulates s_memtime deltas per phase; summed over workgroups here.
+__device__ unsigned long long g_sgx_stamps[8];
+
+__device__ __forceinline__ uint64_t stamp_now() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+
 // Shared LDS carve-up of k_scatter16.
 struct Sc16Lds {
     uint4 *stage;
@@ -509,16 +538,27 @@ __device__ __forceinline__ Sc16Lds sc16_lds(char *smem, uint32_t R, uint32_t mbi
 
 // Rank + merge + scan + stage of one tile whose records/pids are in registers.
 // Returns with the tile partition-sorted in L.stage (after a barrier).
-template <int WAVES, int ITEMS>
+template <int WAVES, int ITEMS, bool ST = false>
 __device__ __forceinline__ void sc16_rank_stage(const Sc16Lds &L, uint32_t R, const uint4 (&rec)[ITEMS],
                                                 const uint32_t (&pid)[ITEMS], const bool (&valid)[ITEMS],
-                                                uint32_t nbits) {
+                                                uint32_t nbits, uint64_t *acc = nullptr) {
     constexpr int T = WAVES * 64;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint32_t rank[ITEMS];
+    uint64_t t0 = 0;
+    if constexpr (ST) t0 = stamp_now();
     rank_items<ITEMS>(pid, valid, rank, L.wcnt + (size_t)w * rowstride(R), nbits, lane,
                       L.mtab + ((size_t)w << L.mbits), L.mbits);
+    if constexpr (ST) {
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(rank[k]));
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const uint64_t t1 = stamp_now();
+        acc[2] += t1 - t0;  // rank (this wave)
+        t0 = t1;
+    }
     lds_barrier();
+    if constexpr (ST) { const uint64_t t1 = stamp_now(); acc[3] += t1 - t0; t0 = t1; }  // wait for all waves
     for (uint32_t p = tid; p < R; p += T) {
         uint32_t s = 0;
 #pragma unroll
@@ -531,6 +571,7 @@ __device__ __forceinline__ void sc16_rank_stage(const Sc16Lds &L, uint32_t R, co
     }
     lds_barrier();
     block_exclusive_scan(L.tcnt, L.lstart, R, L.scratch);
+    if constexpr (ST) { const uint64_t t1 = stamp_now(); acc[4] += t1 - t0; t0 = t1; }  // merge + scan
     const uint16_t *mycnt = L.wcnt + (size_t)w * rowstride(R);
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
@@ -551,11 +592,22 @@ __device__ __forceinline__ void sc16_rank_stage(const Sc16Lds &L, uint32_t R, co
 template <int KIND, int WAVES, int ITEMS, int DIAG = 0>
 __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 *__restrict__ in,
                                                   uint4 *__restrict__ out, int64_t tbase, int64_t end,
-                                                  const PartParams &pp, int64_t n, uint32_t *err) {
+                                                  const PartParams &pp, int64_t n, uint32_t *err,
+                                                  uint64_t *acc = nullptr) {
     constexpr int T = WAVES * 64;
     constexpr int TILE = WAVES * ITEMS * 64;
+    constexpr bool ST = DIAG == 6;
     const uint32_t R = pp.R;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint64_t t_prev = 0;
+    auto mark = [&](int ph) {
+        if constexpr (ST) {
+            const uint64_t t = stamp_now();
+            if (ph > 0) acc[ph - 1] += t - t_prev;
+            t_prev = t;
+        }
+    };
+    mark(0);
     for (uint32_t i = tid; i < (uint32_t)(WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
     uint4 rec[ITEMS];
     uint32_t pid[ITEMS];
@@ -573,7 +625,9 @@ __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 
     }
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
+    if constexpr (ST) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); mark(1); }
     __syncthreads();  // wcnt zeroed
+    mark(2);
     if constexpr (DIAG == 2 || DIAG == 5) {
         // skip the ballot ranking: identity-ish placement, keep every pid alive
 #pragma unroll
@@ -586,8 +640,9 @@ __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 
     } else if constexpr (DIAG == 4) {
         sc16_rank_stage<WAVES, ITEMS>(L, R, rec, pid, valid, pp.nbits);
     } else {
-        sc16_rank_stage<WAVES, ITEMS>(L, R, rec, pid, valid, pp.nbits);
+        sc16_rank_stage<WAVES, ITEMS, ST>(L, R, rec, pid, valid, pp.nbits, acc);
     }
+    mark(6);
     const uint32_t tile_n = (uint32_t)min<int64_t>(TILE, end - tbase);
     if constexpr (DIAG == 4) {
         // no drain: write each register record straight back to its input slot
@@ -612,9 +667,11 @@ __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 
             }
         }
     }
+    mark(7);
     __syncthreads();
     for (uint32_t p = tid; p < R; p += T) L.cursor[p] += L.tcnt[p];
     __syncthreads();
+    mark(8);
 }
 
 template <int KIND, int WAVES, int ITEMS>
@@ -654,8 +711,22 @@ __global__ __launch_bounds__(512, 2) void k_scatter16_diag(const uint4 *__restri
     const int64_t end = min(n, begin + chunk);
     for (uint32_t p = tid; p < R; p += T) L.cursor[p] = offs[(int64_t)p * G + g];
     __syncthreads();
+    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     for (int64_t tbase = begin; tbase < end; tbase += TILE)
-        sc16_tile_generic<SGX_PART_HASH, WAVES, ITEMS, DIAG>(L, in, out, tbase, end, pp, n, err);
+        sc16_tile_generic<SGX_PART_HASH, WAVES, ITEMS, DIAG>(L, in, out, tbase, end, pp, n, err, acc);
+    if constexpr (DIAG == 6) {
+        if (threadIdx.x == 0)
+            for (int i = 0; i < 8; ++i) atomicAdd(&g_sgx_stamps[i], (unsigned long long)acc[i]);
+    }
+}
+
+extern "C" int sgx_diag_stamps(unsigned long long *out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sgx_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -3;
+    if (reset) {
+        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sgx_stamps), z, sizeof z) != hipSuccess) return -3;
+    }
+    return 0;
 }
 
 hipError_t launch_scatter_diag(int mode, const void *in, void *out, int64_t n, int64_t chunk, int G,
@@ -676,10 +747,91 @@ hipError_t launch_scatter_diag(int mode, const void *in, void *out, int64_t n, i
     case 3: SGX_DIAGK(3); break;
     case 4: SGX_DIAGK(4); break;
     case 5: SGX_DIAGK(5); break;
+    case 6: SGX_DIAGK(6); break;
     default: SGX_DIAGK(0); break;
     }
 #undef SGX_DIAGK
     return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// K4 (direct): no LDS staging of records.  Each tile's records are loaded coalesced,
+// ranked exactly as above, and stored straight from registers to
+// cursor[p] + (earlier waves' count of p) + rank.  Only the per-wave counters, the peer
+// table, tcnt and cursor live in LDS (~30 KB at R = 1024), so several workgroups share a
+// CU and overlap each other's load / rank / store phases.  Consecutive records of one
+// partition land in consecutive 16 B slots from different instructions of the same CU;
+// the XCD's L2 merges them into full lines before write-back.
+// ------------------------------------------------------------------------------------
+__host__ __device__ size_t scatter16_direct_lds(uint32_t R, int waves, int mbits) {
+    return al16((size_t)waves * rowstride(R) * 2) + al16((size_t)R * 2) + al16((size_t)R * 4) +
+           (mbits ? (size_t)waves * ((size_t)8 << mbits) : 0);
+}
+
+template <int KIND, int WAVES, int ITEMS>
+__global__ __launch_bounds__(WAVES * 64) void k_scatter16_direct(const uint4 *__restrict__ in,
+                                                                uint4 *__restrict__ out, int64_t n,
+                                                                int64_t chunk, PartParams pp,
+                                                                const uint32_t *__restrict__ offs,
+                                                                int G, uint32_t *err) {
+    constexpr int T = WAVES * 64;
+    constexpr int TILE = WAVES * ITEMS * 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint32_t R = pp.R, RS = rowstride(R);
+    uint16_t *wcnt = (uint16_t *)smem;
+    uint16_t *tcnt = (uint16_t *)(smem + al16((size_t)WAVES * RS * 2));
+    uint32_t *cursor = (uint32_t *)((char *)tcnt + al16((size_t)R * 2));
+    uint64_t *mtab = (uint64_t *)((char *)cursor + al16((size_t)R * 4));
+    const uint32_t mbits = pp.mbits;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int g = blockIdx.x;
+    const int64_t begin = (int64_t)g * chunk;
+    const int64_t end = min(n, begin + chunk);
+    for (uint32_t p = tid; p < R; p += T) cursor[p] = offs[(int64_t)p * G + g];
+    if (mbits)
+        for (uint32_t i = tid; i < ((uint32_t)WAVES << mbits); i += T) mtab[i] = 0ull;
+    for (int64_t tbase = begin; tbase < end; tbase += TILE) {
+        for (uint32_t i = tid; i < (uint32_t)(WAVES * RS / 2); i += T) ((uint32_t *)wcnt)[i] = 0;
+        uint4 rec[ITEMS];
+        uint32_t pid[ITEMS], rank[ITEMS];
+        bool valid[ITEMS];
+        const int64_t wbase = tbase + (int64_t)w * ITEMS * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const int64_t i = wbase + (int64_t)k * 64;
+            valid[k] = i < end;
+            rec[k] = in[valid[k] ? i : begin];  // unconditional load (clamped), masked use
+        }
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
+        lds_barrier();  // wcnt zeroed (and cursor/table initialised on the first tile)
+        rank_items<ITEMS>(pid, valid, rank, wcnt + (size_t)w * RS, pp.nbits, lane, mtab + ((size_t)w << mbits),
+                          mbits);
+        lds_barrier();
+        for (uint32_t p = tid; p < R; p += T) {
+            uint32_t s = 0;
+#pragma unroll
+            for (int v = 0; v < WAVES; ++v) {
+                const uint32_t c = wcnt[(size_t)v * RS + p];
+                wcnt[(size_t)v * RS + p] = (uint16_t)s;
+                s += c;
+            }
+            tcnt[p] = (uint16_t)s;
+        }
+        lds_barrier();
+        const uint16_t *mycnt = wcnt + (size_t)w * RS;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            if (valid[k]) {
+                const uint32_t p = pid[k];
+                const uint32_t dst = cursor[p] + mycnt[p] + rank[k];
+                if ((int64_t)dst < n) out[(size_t)dst] = rec[k];
+                else atomicOr(err, SCATTER_OOB);
+            }
+        }
+        lds_barrier();
+        for (uint32_t p = tid; p < R; p += T) cursor[p] += tcnt[p];
+    }
 }
 
 // ------------------------------------------------------------------------------------
@@ -869,6 +1021,35 @@ __global__ __launch_bounds__(WIDE_THREADS, 1) void k_scatter_wide(const char *__
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t chunk, int G,
                           const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
                           uint32_t *err, hipStream_t stream) {
+    if (rb == 16 && geo.waves >= DIRECT_GEOM_BASE) {
+        const int W = geo.waves - DIRECT_GEOM_BASE;
+#define SGX_SCD(K, WV, I)                                                                       \
+    do {                                                                                        \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_direct<K, WV, I>,                  \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
+        hipLaunchKernelGGL((k_scatter16_direct<K, WV, I>), dim3(G), dim3(WV * 64), geo.lds_bytes, \
+                           stream, (const uint4 *)in, (uint4 *)out, n, chunk, pp, offs, G, err); \
+    } while (0)
+#define SGX_SCD_K(K)                                                       \
+    do {                                                                   \
+        switch (W * 100 + geo.items) {                                     \
+        case 416: SGX_SCD(K, 4, 16); break;                                \
+        case 408: SGX_SCD(K, 4, 8); break;                                 \
+        case 816: SGX_SCD(K, 8, 16); break;                                \
+        case 808: SGX_SCD(K, 8, 8); break;                                 \
+        case 804: SGX_SCD(K, 8, 4); break;                                 \
+        default: return hipErrorInvalidValue;                              \
+        }                                                                  \
+    } while (0)
+        switch (pp.kind) {
+        case SGX_PART_HASH: SGX_SCD_K(SGX_PART_HASH); break;
+        case SGX_PART_RANGE_I64: SGX_SCD_K(SGX_PART_RANGE_I64); break;
+        default: SGX_SCD_K(SGX_PART_RANGE_BYTES10); break;
+        }
+#undef SGX_SCD_K
+#undef SGX_SCD
+        return hipGetLastError();
+    }
     if (rb == 16 && geo.waves == DMA_GEOM_TAG) {
         (void)hipFuncSetAttribute((const void *)k_scatter16_dma, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)geo.lds_bytes);
