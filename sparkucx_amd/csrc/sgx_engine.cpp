@@ -163,10 +163,12 @@ struct sgx_engine {
     int no_table = 0;                // SGX_NO_PEER_TABLE=1: ballots-only ranking (A/B)
     int direct = 0;                  // SGX_SCATTER_DIRECT=WWII: direct-store K4 (A/B)
     int use_dma = 0;                 // SGX_SCATTER_DMA=1: LDS-DMA pipelined K4 (A/B)
+    int nt = 0;                      // SGX_SCATTER_NT=1/2/3: nontemporal loads/stores (A/B)
+    int chain = 0;                   // SGX_SCATTER_CHAIN=WWII: chained look-back K4 (A/B)
     hipStream_t s_comp = nullptr, s_comm = nullptr;
     // work buffers of the map-side pipeline
     DevBuf counts, offs, status, part_off_dev, input_stage;
-    DevBuf ag_send, ag_recv, recv, items_dev;
+    DevBuf ag_send, ag_recv, recv, items_dev, chain_buf;
     HostPinned ag_host;
     std::map<int32_t, Shuffle> shuffles;
     // RCCL
@@ -248,6 +250,8 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     if (const char *d = getenv("SGX_NO_PEER_TABLE")) e->no_table = atoi(d);
     if (const char *d = getenv("SGX_SCATTER_DIRECT")) e->direct = atoi(d);
     if (const char *d = getenv("SGX_SCATTER_DMA")) e->use_dma = atoi(d);
+    if (const char *d = getenv("SGX_SCATTER_NT")) e->nt = atoi(d);
+    if (const char *d = getenv("SGX_SCATTER_CHAIN")) e->chain = atoi(d);
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
     *out = e.release();
@@ -277,7 +281,7 @@ extern "C" void sgx_destroy(sgx_engine *e) {
         kv.second.bounds.release();
     }
     for (DevBuf *b : {&e->counts, &e->offs, &e->status, &e->part_off_dev, &e->input_stage, &e->ag_send,
-                      &e->ag_recv, &e->recv, &e->items_dev})
+                      &e->ag_recv, &e->recv, &e->items_dev, &e->chain_buf})
         b->release();
     e->ag_host.release();
     for (hipEvent_t ev : e->ev_free) (void)hipEventDestroy(ev);
@@ -436,6 +440,7 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
         const ScatterGeom d = scatter_geom16_dma((uint32_t)s.R);
         if (d.items) geo = d;
     }
+    geo.nt = e->nt;
     if (geo.items == 0)
         return fail(SGX_ERR_UNSUPPORTED, "no scatter geometry (waves %d, items %d) fits R=%d", e->sc_waves,
                     e->sc_items, s.R);
@@ -478,7 +483,26 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
     PartParams lpp = s.pp;
     lpp.mbits = e->no_table ? 0u : (uint32_t)geo.mbits;
     if (e->diag > 0) lpp.mbits = e->no_table ? 0u : (uint32_t)scatter_geom16((uint32_t)s.R, 8, 16).mbits;
-    if (n > 0) {
+    const int cw = e->chain / 100, ci = e->chain % 100;
+    const ScatterGeom cg = (e->chain > 0 && rb == 16) ? scatter_geom16((uint32_t)s.R, cw, ci) : ScatterGeom{0, 0, 0, 0, 0};
+    if (n > 0 && cg.items > 0 && n < (1ll << 30)) {
+        // chained K4: tiles in ticket order, per-partition decoupled look-back across tiles
+        int mb = e->no_table ? 0 : cg.mbits;
+        while (mb > 0 && scatter16_chain_lds((uint32_t)s.R, cw, ci, mb) > 160 * 1024) --mb;
+        PartParams cpp = s.pp;
+        cpp.mbits = (uint32_t)mb;
+        const int ctile = cw * ci * 64;
+        const int64_t ntiles = (n + ctile - 1) / ctile;
+        const size_t sbytes = 16 + (size_t)ntiles * (size_t)s.R * 4;
+        SGX_TRY(e->chain_buf.ensure(sbytes));
+        HIP_TRY(hipMemsetAsync(e->chain_buf.p, 0, sbytes, st));
+        int occ = (int)((160 * 1024) / scatter16_chain_lds((uint32_t)s.R, cw, ci, mb));
+        if (occ > 32 / cw) occ = 32 / cw;
+        if (occ < 1) occ = 1;
+        HIP_TRY(launch_scatter_chain(in, m.data.p, n, cpp, (const uint32_t *)e->part_off_dev.p,
+                                     (uint32_t *)((char *)e->chain_buf.p + 16), (uint32_t *)e->chain_buf.p,
+                                     ticket_err + 1, cw, ci, e->num_cus * occ, st));
+    } else if (n > 0) {
         if (e->diag > 0 && rb == 16 && s.kind == SGX_PART_HASH)  // measurement-only ablation
             HIP_TRY(launch_scatter_diag(e->diag, in, m.data.p, n, chunk, G, lpp, (const uint32_t *)e->offs.p, ticket_err + 1, st));
         else

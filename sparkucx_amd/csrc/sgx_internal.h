@@ -34,6 +34,7 @@ struct ScatterGeom {
     int tile;   // waves * items * 64
     size_t lds_bytes;
     int mbits;  // LDS peer-table width (0 = ballots only)
+    int nt = 0; // A/B: bit0 nontemporal loads, bit1 nontemporal stores (8x16 staged only)
 };
 ScatterGeom scatter_geom16(uint32_t R, int force_waves = 0, int force_items = 0);
 // The LDS-DMA pipelined hash kernel (waves == DMA_GEOM_TAG); items == 0 if R does not fit.
@@ -59,6 +60,12 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes
 hipError_t launch_scatter_diag(int mode, const void *in, void *out, int64_t n, int64_t chunk, int G,
                                const PartParams &pp, const uint32_t *offs, uint32_t *err,
                                hipStream_t stream);
+// K4 chained variant (tiles in ticket order, per-partition look-back); base = K3's
+// partition offsets; status: [ceil(n/tile)][R] u32 and ticket zeroed by the caller.
+hipError_t launch_scatter_chain(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *base,
+                                uint32_t *status, uint32_t *ticket, uint32_t *err, int waves, int items,
+                                int grid, hipStream_t stream);
+__host__ __device__ size_t scatter16_chain_lds(uint32_t R, int waves, int items, int mbits);
 // items: [n][3] int64 {src_off, dst_off, bytes}; all offsets/bytes multiples of `align`.
 hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, int64_t n_items,
                              int align, hipStream_t stream);

@@ -22,6 +22,8 @@
 
 namespace sgx {
 
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
 // ------------------------------------------------------------------------------------
 // Partition ids
 // ------------------------------------------------------------------------------------
@@ -358,7 +360,7 @@ static int table_bits(uint32_t R, int waves, int items, uint32_t nbits, size_t b
 
 struct Geo16 { int waves, items; };
 // every instantiated geometry (launch_scatter's switch must list the same set)
-static const Geo16 kGeos16[] = {{4, 16}, {8, 16}, {4, 12}, {8, 8}, {4, 8}, {8, 4}, {4, 4}, {4, 2}, {4, 1}};
+static const Geo16 kGeos16[] = {{4, 16}, {8, 16}, {12, 10}, {14, 9}, {16, 7}, {4, 12}, {8, 8}, {4, 8}, {8, 4}, {4, 4}, {4, 2}, {4, 1}};
 
 ScatterGeom scatter_geom16_direct(uint32_t R, int waves, int items) {
     static const int ok[][2] = {{4, 16}, {4, 8}, {8, 16}, {8, 8}, {8, 4}};
@@ -589,7 +591,7 @@ __device__ __forceinline__ void sc16_rank_stage(const Sc16Lds &L, uint32_t R, co
 // 2 = no ballot ranking, 3 = no global loads, 4 = no LDS stage/drain, 5 = no ranking and
 // identity staging (memory + barriers only).  Values that a skipped phase would consume
 // are kept alive with empty asm so the compiler cannot delete the phases that remain.
-template <int KIND, int WAVES, int ITEMS, int DIAG = 0>
+template <int KIND, int WAVES, int ITEMS, int DIAG = 0, int NT = 0>
 __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 *__restrict__ in,
                                                   uint4 *__restrict__ out, int64_t tbase, int64_t end,
                                                   const PartParams &pp, int64_t n, uint32_t *err,
@@ -619,6 +621,13 @@ __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 
         valid[k] = i < end;
         if constexpr (DIAG == 3) {
             rec[k] = make_uint4((uint32_t)i * 2654435761u, (uint32_t)(i >> 7), (uint32_t)i, 0);
+        } else if constexpr (NT & 1) {
+            if (valid[k]) {
+                const u32x4 v = __builtin_nontemporal_load((const u32x4 *)&in[i]);
+                rec[k] = make_uint4(v.x, v.y, v.z, v.w);
+            } else {
+                rec[k] = make_uint4(0, 0, 0, 0);
+            }
         } else {
             rec[k] = valid[k] ? in[i] : make_uint4(0, 0, 0, 0);
         }
@@ -662,8 +671,15 @@ __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 
             if constexpr (DIAG == 1) {
                 asm volatile("" ::"v"(r.x), "v"(r.y), "v"(r.z), "v"(r.w), "v"(d));
             } else {
-                if ((int64_t)d < n) out[(size_t)d] = r;
-                else atomicOr(err, SCATTER_OOB);
+                if ((int64_t)d < n) {
+                    if constexpr ((NT & 2) != 0) {
+                        u32x4 v = {r.x, r.y, r.z, r.w};
+                        __builtin_nontemporal_store(v, (u32x4 *)&out[(size_t)d]);
+                    }
+                    else out[(size_t)d] = r;
+                } else {
+                    atomicOr(err, SCATTER_OOB);
+                }
             }
         }
     }
@@ -674,7 +690,57 @@ __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 
     mark(8);
 }
 
+// One full tile of the pipelined staged path: rank + stage tile t (records in `rec`),
+// prefetch tile tn into `rec` (issued in a pinned order, before the drain stores), drain t.
 template <int KIND, int WAVES, int ITEMS>
+__device__ __forceinline__ void sc16_full_tile(const Sc16Lds &L, uint4 (&rec)[ITEMS], const uint4 *src,
+                                               int64_t tn, uint4 *__restrict__ out, int64_t n,
+                                               const PartParams &pp, uint32_t &bad) {
+    constexpr int T = WAVES * 64;
+    constexpr int TILE = WAVES * ITEMS * 64;
+    const uint32_t R = pp.R;
+    const uint32_t tid = threadIdx.x;
+    uint32_t pid[ITEMS];
+    bool valid[ITEMS];
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        valid[k] = true;
+        pid[k] = pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp);
+    }
+    sc16_rank_stage<WAVES, ITEMS>(L, R, rec, pid, valid, pp.nbits);
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        rec[k] = src[tn * TILE + k * 64];
+        asm volatile("" ::: "memory");  // keep the issue order identical in every copy
+    }
+    constexpr int BATCH = ITEMS % 4 == 0 ? 4 : (ITEMS % 2 == 0 ? 2 : 1);
+#pragma unroll
+    for (int k0 = 0; k0 < ITEMS; k0 += BATCH) {
+        uint4 r[BATCH];
+        uint32_t d[BATCH];
+#pragma unroll
+        for (int j = 0; j < BATCH; ++j) r[j] = L.stage[(k0 + j) * T + tid];
+#pragma unroll
+        for (int j = 0; j < BATCH; ++j) {
+            const uint32_t s = (uint32_t)((k0 + j) * T + tid);
+            uint32_t p;
+            if constexpr (KIND == SGX_PART_HASH) p = hash_pid(r[j].x, r[j].y, pp);
+            else p = slot_partition(L.lstart, R, s);
+            d[j] = L.cursor[p] + (s - (uint32_t)L.lstart[p]);
+            const bool ok = (int64_t)d[j] < n;
+            bad |= ok ? 0u : 1u;
+            d[j] = ok ? d[j] : (uint32_t)(n - 1);
+        }
+#pragma unroll
+        for (int j = 0; j < BATCH; ++j) out[(size_t)d[j]] = r[j];
+    }
+    lds_barrier();
+    for (uint32_t p = tid; p < R; p += T) L.cursor[p] += L.tcnt[p];
+    for (uint32_t i = tid; i < (uint32_t)(WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
+    lds_barrier();
+}
+
+template <int KIND, int WAVES, int ITEMS, int NT = 0>
 __global__ __launch_bounds__(WAVES * 64, 2) void k_scatter16(const uint4 *__restrict__ in,
                                                              uint4 *__restrict__ out, int64_t n,
                                                              int64_t chunk, PartParams pp,
@@ -685,14 +751,38 @@ __global__ __launch_bounds__(WAVES * 64, 2) void k_scatter16(const uint4 *__rest
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t R = pp.R;
     const Sc16Lds L = sc16_lds<WAVES, ITEMS>(smem, R, pp.mbits);
-    const uint32_t tid = threadIdx.x;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int g = blockIdx.x;
     const int64_t begin = (int64_t)g * chunk;
     const int64_t end = min(n, begin + chunk);
     for (uint32_t p = tid; p < R; p += T) L.cursor[p] = offs[(int64_t)p * G + g];
-    __syncthreads();
-    for (int64_t tbase = begin; tbase < end; tbase += TILE)
-        sc16_tile_generic<KIND, WAVES, ITEMS>(L, in, out, tbase, end, pp, n, err);
+    const int64_t nfull = NT == 0 && end > begin ? (end - begin) / TILE : 0;
+    int64_t tbase = begin;
+    if (nfull > 0) {
+        // Steady state (full tiles): tile t+1's loads are issued right after tile t is staged
+        // in LDS -- before tile t's drain stores -- so the in-order vmcnt wait before ranking
+        // t+1 retires exactly those loads and tile t's stores keep draining behind the next
+        // tile's compute.  Tile 0 is peeled so both paths into the loop carry the same
+        // outstanding (ITEMS loads, ITEMS stores) and hipcc's counted waits stay exact; loads
+        // (clamped) and drain stores are branch-free; an out-of-range destination (only if
+        // counts were corrupt) is clamped and reported through a register flag.
+        const uint4 *src = in + begin + (int64_t)w * ITEMS * 64 + lane;
+        uint4 rec[ITEMS];
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) rec[k] = src[k * 64];
+        for (uint32_t i = tid; i < (uint32_t)(WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
+        __syncthreads();
+        uint32_t bad = 0;
+        sc16_full_tile<KIND, WAVES, ITEMS>(L, rec, src, nfull > 1 ? 1 : 0, out, n, pp, bad);
+        for (int64_t t = 1; t < nfull; ++t)
+            sc16_full_tile<KIND, WAVES, ITEMS>(L, rec, src, t + 1 < nfull ? t + 1 : t, out, n, pp, bad);
+        if (bad) atomicOr(err, SCATTER_OOB);
+        tbase = begin + nfull * TILE;
+    } else {
+        __syncthreads();
+    }
+    for (; tbase < end; tbase += TILE)
+        sc16_tile_generic<KIND, WAVES, ITEMS, 0, NT>(L, in, out, tbase, end, pp, n, err);
 }
 
 template <int DIAG>
@@ -751,6 +841,159 @@ hipError_t launch_scatter_diag(int mode, const void *in, void *out, int64_t n, i
     default: SGX_DIAGK(0); break;
     }
 #undef SGX_DIAGK
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// K4 (chained): tiles in dispatch order with a decoupled look-back PER PARTITION across
+// tiles (the Onesweep structure).  Tile t's run of partition p starts at
+//   base[p] + sum_{t' < t} count[t'][p]
+// where base[] comes from K1-K3.  Consecutive tiles are processed concurrently by
+// different CUs, so the runs of one partition are written side by side at about the same
+// time: the output is ~R near-sequential write streams (instead of R x chunks private
+// ones), and the line shared by two consecutive runs is completed while still cached.
+// Status: one u32 granule per (tile, partition) = {flag:2 | count:30}, written by relaxed
+// agent-scope atomic stores and polled by relaxed agent-scope atomic loads (the count is
+// the flag: no fences).  FLAG_A = this tile's count, FLAG_P = inclusive prefix.  Tiles
+// are taken from an atomic ticket, so a tile only waits on tiles already running; spins
+// are bounded (error bit 1 on give-up).  Needs n < 2^30 (30-bit counts).
+// ------------------------------------------------------------------------------------
+constexpr uint32_t CH_A = 1u << 30, CH_P = 2u << 30, CH_V = (1u << 30) - 1u;
+
+__host__ __device__ size_t scatter16_chain_lds(uint32_t R, int waves, int items, int mbits) {
+    return scatter16_lds(R, waves, items, mbits) + 16;
+}
+
+template <int KIND, int WAVES, int ITEMS>
+__global__ __launch_bounds__(WAVES * 64, 2) void k_scatter16_chain(const uint4 *__restrict__ in,
+                                                                  uint4 *__restrict__ out, int64_t n,
+                                                                  int64_t ntiles, PartParams pp,
+                                                                  const uint32_t *__restrict__ base,
+                                                                  uint32_t *status, uint32_t *ticket,
+                                                                  uint32_t *err) {
+    constexpr int T = WAVES * 64;
+    constexpr int TILE = WAVES * ITEMS * 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint32_t R = pp.R;
+    const Sc16Lds L = sc16_lds<WAVES, ITEMS>(smem, R, pp.mbits);
+    uint32_t *s_tile = (uint32_t *)(smem + scatter16_lds(R, WAVES, ITEMS, pp.mbits));
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    for (;;) {
+        for (uint32_t i = tid; i < (uint32_t)(WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
+        if (tid == 0) *s_tile = atomicAdd(ticket, 1u);
+        __syncthreads();
+        const int64_t t = (int64_t)*s_tile;
+        if (t >= ntiles) break;
+        const int64_t tbase = t * TILE;
+        const int64_t end = min(n, tbase + TILE);
+        uint4 rec[ITEMS];
+        uint32_t pid[ITEMS], rank[ITEMS];
+        bool valid[ITEMS];
+        const int64_t wbase = tbase + (int64_t)w * ITEMS * 64 + lane;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const int64_t i = wbase + (int64_t)k * 64;
+            valid[k] = i < end;
+            rec[k] = valid[k] ? in[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
+        rank_items<ITEMS>(pid, valid, rank, L.wcnt + (size_t)w * rowstride(R), pp.nbits, lane,
+                          L.mtab + ((size_t)w << L.mbits), L.mbits);
+        lds_barrier();
+        uint32_t *st = status + (size_t)t * R;
+        for (uint32_t p = tid; p < R; p += T) {
+            uint32_t c = 0;
+#pragma unroll
+            for (int v = 0; v < WAVES; ++v) {
+                const uint32_t x = L.wcnt[(size_t)v * rowstride(R) + p];
+                L.wcnt[(size_t)v * rowstride(R) + p] = (uint16_t)c;
+                c += x;
+            }
+            L.tcnt[p] = (uint16_t)c;
+            // publish this tile's count as early as possible (successors look back on it)
+            __hip_atomic_store(&st[p], (t == 0 ? CH_P : CH_A) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        lds_barrier();
+        block_exclusive_scan(L.tcnt, L.lstart, R, L.scratch);
+        const uint16_t *mycnt = L.wcnt + (size_t)w * rowstride(R);
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            if (valid[k]) {
+                const uint32_t p = pid[k];
+                const uint32_t slot = (uint32_t)L.lstart[p] + mycnt[p] + rank[k];
+                if (slot < (uint32_t)TILE) L.stage[slot] = rec[k];
+            }
+        }
+        // look back per partition (overlaps the stage writes' LDS traffic)
+        for (uint32_t p = tid; p < R; p += T) {
+            uint32_t prefix = 0;
+            if (t > 0) {
+                int64_t j = t - 1;
+                uint32_t spins = 0;
+                while (j >= 0) {
+                    const uint32_t v = __hip_atomic_load(&status[(size_t)j * R + p], __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT);
+                    const uint32_t f = v & ~CH_V;
+                    if (f == 0) {
+                        if (++spins > (1u << 24)) { atomicOr(err, 1u); break; }
+                        __builtin_amdgcn_s_sleep(1);
+                        continue;
+                    }
+                    prefix += v & CH_V;
+                    if (f == CH_P) break;
+                    --j;
+                }
+                __hip_atomic_store(&st[p], CH_P | (prefix + L.tcnt[p]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            L.cursor[p] = base[p] + prefix - (uint32_t)L.lstart[p];  // drain: dst = cursor[p] + slot
+        }
+        lds_barrier();
+        const uint32_t tile_n = (uint32_t)(end - tbase);
+        for (uint32_t s = tid; s < tile_n; s += T) {
+            const uint4 r = L.stage[s];
+            uint32_t p;
+            if constexpr (KIND == SGX_PART_HASH) p = hash_pid(r.x, r.y, pp);
+            else p = slot_partition(L.lstart, R, s);
+            const uint32_t d = L.cursor[p] + s;
+            if ((int64_t)d < n) out[(size_t)d] = r;
+            else atomicOr(err, SCATTER_OOB);
+        }
+        __syncthreads();
+    }
+}
+
+hipError_t launch_scatter_chain(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *base,
+                                uint32_t *status, uint32_t *ticket, uint32_t *err, int waves, int items,
+                                int grid, hipStream_t stream) {
+    const int tile = waves * items * 64;
+    const int64_t ntiles = (n + tile - 1) / tile;
+    const size_t lds = scatter16_chain_lds(pp.R, waves, items, pp.mbits);
+    if (lds > LDS_MAX || n >= (int64_t)CH_V) return hipErrorInvalidValue;
+#define SGX_SCC(K, W, I)                                                                        \
+    do {                                                                                        \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_chain<K, W, I>,                    \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
+        hipLaunchKernelGGL((k_scatter16_chain<K, W, I>), dim3(grid), dim3(W * 64), lds, stream,  \
+                           (const uint4 *)in, (uint4 *)out, n, ntiles, pp, base, status, ticket, err); \
+    } while (0)
+#define SGX_SCC_K(K)                                             \
+    do {                                                         \
+        switch (waves * 100 + items) {                           \
+        case 816: SGX_SCC(K, 8, 16); break;                      \
+        case 416: SGX_SCC(K, 4, 16); break;                      \
+        case 808: SGX_SCC(K, 8, 8); break;                       \
+        case 1607: SGX_SCC(K, 16, 7); break;                     \
+        default: return hipErrorInvalidValue;                    \
+        }                                                        \
+    } while (0)
+    switch (pp.kind) {
+    case SGX_PART_HASH: SGX_SCC_K(SGX_PART_HASH); break;
+    case SGX_PART_RANGE_I64: SGX_SCC_K(SGX_PART_RANGE_I64); break;
+    default: SGX_SCC_K(SGX_PART_RANGE_BYTES10); break;
+    }
+#undef SGX_SCC_K
+#undef SGX_SCC
     return hipGetLastError();
 }
 
@@ -869,6 +1112,7 @@ __device__ __forceinline__ void wait_vmcnt() {
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+static_assert(DMA_ITEMS % 4 == 0, "k_scatter16_dma drains in batches of 4");
 __global__ __launch_bounds__(DMA_T, 2) void k_scatter16_dma(const uint4 *__restrict__ in,
                                                            uint4 *__restrict__ out, int64_t n,
                                                            int64_t chunk, PartParams pp,
@@ -1068,12 +1312,28 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         hipLaunchKernelGGL((k_scatter16<K, W, I>), dim3(G), dim3(W * 64), geo.lds_bytes, stream, \
                            i4, o4, n, chunk, pp, offs, G, err);                                \
     } while (0)
+#define SGX_SC16NT(K, W, I, NTV)                                                                 \
+    do {                                                                                        \
+        (void)hipFuncSetAttribute((const void *)k_scatter16<K, W, I, NTV>,                     \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
+        hipLaunchKernelGGL((k_scatter16<K, W, I, NTV>), dim3(G), dim3(W * 64), geo.lds_bytes, stream, \
+                           i4, o4, n, chunk, pp, offs, G, err);                                \
+    } while (0)
 #define SGX_SC16_K(K)                                                        \
     do {                                                                     \
         const int key = geo.waves * 100 + geo.items;                         \
+        if (geo.nt && key == 816) {                                          \
+            if (geo.nt == 1) SGX_SC16NT(K, 8, 16, 1);                        \
+            else if (geo.nt == 2) SGX_SC16NT(K, 8, 16, 2);                   \
+            else SGX_SC16NT(K, 8, 16, 3);                                    \
+            break;                                                           \
+        }                                                                    \
         switch (key) {                                                       \
         case 416: SGX_SC16(K, 4, 16); break;                                 \
         case 816: SGX_SC16(K, 8, 16); break;                                 \
+        case 1210: SGX_SC16(K, 12, 10); break;                               \
+        case 1409: SGX_SC16(K, 14, 9); break;                                \
+        case 1607: SGX_SC16(K, 16, 7); break;                                \
         case 412: SGX_SC16(K, 4, 12); break;                                 \
         case 808: SGX_SC16(K, 8, 8); break;                                  \
         case 408: SGX_SC16(K, 4, 8); break;                                  \
@@ -1090,6 +1350,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         default: SGX_SC16_K(SGX_PART_RANGE_BYTES10); break;
         }
 #undef SGX_SC16_K
+#undef SGX_SC16NT
 #undef SGX_SC16
     } else {
         if (geo.items == 0 || (rb & 3) != 0 || rb < 12) return hipErrorInvalidValue;

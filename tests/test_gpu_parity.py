@@ -124,6 +124,37 @@ def test_chunking_does_not_change_output(sgx_lib, oracle_lib, num_chunks):
         check_against_oracle(e, oracle_lib, recs, 1024)
 
 
+GEOMETRIES = [(4, 16), (8, 16), (12, 10), (16, 7), (4, 12), (8, 8), (4, 8), (8, 4), (4, 4), (4, 2), (4, 1)]
+
+
+@pytest.mark.parametrize("waves,items", GEOMETRIES)
+@pytest.mark.parametrize("R", [7, 200, 1024, 4096])
+def test_every_staged_geometry(sgx_lib, oracle_lib, waves, items, R):
+    """Every instantiated K4 geometry, full tiles + a ragged tail, multiple chunks."""
+    tile = waves * items * 64
+    n = 5 * tile * 3 + tile // 3 + 7
+    recs = oracle_lib.gen_uniform16(n, 0xC0FFEE + R)
+    with sgx_lib.ShuffleEngine(device=0, num_chunks=3, scatter_waves=waves, scatter_items=items) as e:
+        try:
+            check_against_oracle(e, oracle_lib, recs, R)
+        except sgx_lib.UnsupportedOperationException:  # geometry's LDS does not fit this R
+            pytest.skip(f"geometry {waves}x{items} does not fit R={R}")
+
+
+@pytest.mark.parametrize("env", ["SGX_SCATTER_DMA=1", "SGX_SCATTER_DIRECT=816", "SGX_SCATTER_DIRECT=408",
+                                 "SGX_SCATTER_CHAIN=816", "SGX_SCATTER_CHAIN=1607", "SGX_NO_PEER_TABLE=1",
+                                 "SGX_SCATTER_NT=1"])
+def test_alternative_scatter_variants(sgx_lib, oracle_lib, monkeypatch, env):
+    """The A/B variants kept for measurement must stay bit-exact too (engine reads the env
+    at creation)."""
+    k, v = env.split("=")
+    monkeypatch.setenv(k, v)
+    recs = oracle_lib.gen_uniform16(3 * 8192 * 5 + 1234, 99)
+    with sgx_lib.ShuffleEngine(device=0) as e:
+        for R in (200, 1024):
+            check_against_oracle(e, oracle_lib, recs, R)
+
+
 def test_zipf_skew_r4096(engine, oracle_lib):
     cdf = oracle_lib.zipf_cdf(1.1, 2**24)
     recs = oracle_lib.gen_zipf16(1_000_000, 11, cdf)
