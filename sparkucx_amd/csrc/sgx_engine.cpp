@@ -163,7 +163,8 @@ struct sgx_engine {
     int no_table = 0;                // SGX_NO_PEER_TABLE=1: ballots-only ranking (A/B)
     int direct = 0;                  // SGX_SCATTER_DIRECT=WWII: direct-store K4 (A/B)
     int use_dma = 0;                 // SGX_SCATTER_DMA=1: LDS-DMA pipelined K4 (A/B)
-    int nt = 0;                      // SGX_SCATTER_NT=1/2/3: nontemporal loads/stores (A/B)
+    int rank_match = 0;              // SGX_RANK=match: ballot/peer-table ranking in K4
+    int nt = 0;                      // SGX_SCATTER_NT=1/2/3: nontemporal loads/stores; 4: double-buffered (A/B)
     int chain = 0;                   // SGX_SCATTER_CHAIN=WWII: chained look-back K4 (A/B)
     hipStream_t s_comp = nullptr, s_comm = nullptr;
     // work buffers of the map-side pipeline
@@ -214,7 +215,7 @@ static PartParams make_part_params(const Shuffle &s) {
     PartParams pp{};
     pp.kind = s.kind;
     pp.R = (uint32_t)s.R;
-    pp.fm_M = UINT64_MAX / (uint64_t)s.R + 1;  // R == 1 wraps to 0 -> fastmod 0, as needed
+    mod_params((uint32_t)s.R, &pp.mg_m, &pp.mg_s);
     pp.c31 = (uint32_t)((1ull << 31) % (uint64_t)s.R);
     pp.nbits = bits_for((uint32_t)s.R);
     pp.nb = s.nb;
@@ -251,6 +252,7 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     if (const char *d = getenv("SGX_SCATTER_DIRECT")) e->direct = atoi(d);
     if (const char *d = getenv("SGX_SCATTER_DMA")) e->use_dma = atoi(d);
     if (const char *d = getenv("SGX_SCATTER_NT")) e->nt = atoi(d);
+    if (const char *d = getenv("SGX_RANK")) e->rank_match = std::strcmp(d, "match") == 0;
     if (const char *d = getenv("SGX_SCATTER_CHAIN")) e->chain = atoi(d);
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
@@ -441,12 +443,19 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
         if (d.items) geo = d;
     }
     geo.nt = e->nt;
+    // default K4 for hash partitioners: lane-ordered ranking (SGX_RANK=match keeps the
+    // ballot/peer-table ranker; the A/B kernels above keep theirs)
+    if (rb == 16 && s.kind == SGX_PART_HASH && !e->rank_match && e->diag == 0 && e->direct == 0 &&
+        !e->use_dma && e->nt == 0 && e->chain == 0) {
+        const ScatterGeom o = scatter_geom16_ord((uint32_t)s.R, e->sc_waves, e->sc_items);
+        if (o.items) geo = o;
+    }
     if (geo.items == 0)
         return fail(SGX_ERR_UNSUPPORTED, "no scatter geometry (waves %d, items %d) fits R=%d", e->sc_waves,
                     e->sc_items, s.R);
     const int tile = geo.tile;
     int Gt = e->G;
-    if (geo.waves >= DIRECT_GEOM_BASE && !e->G_forced) {
+    if (is_direct_geom(geo.waves) && !e->G_forced) {
         // several direct-store workgroups per CU: one chunk per resident workgroup
         const int wv = geo.waves - DIRECT_GEOM_BASE;
         int occ = (int)((160 * 1024) / geo.lds_bytes);

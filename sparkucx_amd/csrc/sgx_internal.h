@@ -11,7 +11,8 @@ namespace sgx {
 struct PartParams {
     int32_t kind;        // SGX_PART_*
     uint32_t R;          // number of partitions
-    uint64_t fm_M;       // Lemire fastmod magic for R: floor((2^64-1)/R) + 1
+    uint32_t mg_m;       // Granlund-Montgomery magic for u32 mod R (R >= 2): see mod_params()
+    uint32_t mg_s;       //   and its shift, ceil(log2 R) - 1
     uint32_t c31;        // 2^31 mod R (HashPartitioner's signed-int correction)
     uint32_t nbits;      // bits needed to hold a partition id (ceil log2 R), >= 1
     int32_t nb;          // range bounds count (R - 1)
@@ -19,6 +20,16 @@ struct PartParams {
     uint32_t mbits;      // K4 peer-table width for this launch (0 = ballots only)
     const void *bounds;  // device: int64[nb] (RANGE_I64) or Key10[nb] (RANGE_BYTES10)
 };
+
+// Granlund-Montgomery parameters of mod_u32 (sgx_kernels.hip) for 2 <= R < 2^31:
+// l = ceil(log2 R), m = floor(2^32 (2^l - R) / R) + 1, shift = l - 1.
+inline void mod_params(uint32_t R, uint32_t *m, uint32_t *shift) {
+    if (R < 2) { *m = 0; *shift = 0; return; }
+    uint32_t l = 0;
+    while ((1ull << l) < R) ++l;
+    *m = (uint32_t)(((1ull << 32) * ((1ull << l) - R)) / R + 1);
+    *shift = l - 1;
+}
 
 // 10-byte unsigned-lexicographic key, pre-split so tuple compare == byte compare.
 struct Key10 {
@@ -42,6 +53,10 @@ constexpr int DMA_GEOM_TAG = -1;
 ScatterGeom scatter_geom16_dma(uint32_t R);
 // Direct-store kernel (waves == DIRECT_GEOM_BASE + real waves).
 constexpr int DIRECT_GEOM_BASE = 1000;
+// Lane-ordered-ranking staged kernel (waves == ORD_GEOM_BASE + real waves, mbits == PP).
+constexpr int ORD_GEOM_BASE = 2000;
+ScatterGeom scatter_geom16_ord(uint32_t R, int force_waves = 0, int force_items = 0);
+inline bool is_direct_geom(int waves) { return waves >= DIRECT_GEOM_BASE && waves < ORD_GEOM_BASE; }
 ScatterGeom scatter_geom16_direct(uint32_t R, int waves, int items);
 __host__ __device__ size_t scatter16_lds(uint32_t R, int waves, int items, int mbits);
 ScatterGeom scatter_geom_wide(uint32_t R, int record_bytes);

@@ -28,20 +28,28 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 // Partition ids
 // ------------------------------------------------------------------------------------
 
-// Lemire fastmod (exact for every 32-bit u and divisor d >= 1).
-__device__ __forceinline__ uint32_t fastmod_u32(uint32_t u, uint64_t M, uint32_t d) {
-    const uint64_t low = M * (uint64_t)u;
-    return (uint32_t)__umul64hi(low, (uint64_t)d);
+// u mod R for every 32-bit u, 2 <= R < 2^31 (Granlund-Montgomery round-up multiplier,
+// all 32-bit VALU): q = (t + ((u - t) >> 1)) >> (l - 1), t = mulhi(m, u),
+// m = floor(2^32 (2^l - R) / R) + 1, l = ceil(log2 R).  R == 1 is special-cased by callers.
+__device__ __forceinline__ uint32_t mod_u32(uint32_t u, const PartParams &pp) {
+    const uint32_t t = __umulhi(pp.mg_m, u);
+    const uint32_t q = (t + ((u - t) >> 1)) >> pp.mg_s;
+    return u - q * pp.R;
 }
 
 // nonNegativeMod((int)(k ^ (k >>> 32)), R) with k = khi:klo.
 // h (signed) mod R == ((h + 2^31) mod R - 2^31 mod R) mod R, evaluated unsigned.
 __device__ __forceinline__ uint32_t hash_pid(uint32_t klo, uint32_t khi, const PartParams &pp) {
     const uint32_t u = (klo ^ khi) ^ 0x80000000u;
-    const uint32_t r = fastmod_u32(u, pp.fm_M, pp.R);
+    const uint32_t r = mod_u32(u, pp);
     const uint32_t t = r + pp.R - pp.c31;
-    return t >= pp.R ? t - pp.R : t;
+    const uint32_t v = t >= pp.R ? t - pp.R : t;
+    return pp.R == 1 ? 0u : v;
 }
+
+// Kernel-internal partitioner kind: HashPartitioner with a power-of-two R, where
+// nonNegativeMod(h, R) == h & (R - 1) for two's-complement h.
+constexpr int KIND_HASH_POW2 = 100;
 
 __device__ __forceinline__ uint32_t range_pid_i64(int64_t key, const PartParams &pp) {
     const int64_t *b = (const int64_t *)pp.bounds;
@@ -96,6 +104,8 @@ template <int KIND>
 __device__ __forceinline__ uint32_t pid_of(uint32_t x, uint32_t y, uint32_t z, const PartParams &pp) {
     if constexpr (KIND == SGX_PART_HASH) {
         return hash_pid(x, y, pp);
+    } else if constexpr (KIND == KIND_HASH_POW2) {
+        return (x ^ y) & (pp.R - 1u);
     } else if constexpr (KIND == SGX_PART_RANGE_I64) {
         return range_pid_i64((int64_t)(((uint64_t)y << 32) | x), pp);
     } else {
@@ -216,7 +226,13 @@ hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
 #define SGX_HIST(K, B) \
     hipLaunchKernelGGL((k_hist<K, B>), dim3(G * HIST_SPLIT), dim3(HIST_THREADS), lds, stream, p, n, rb, chunk, pp, counts, G)
     switch (pp.kind) {
-    case SGX_PART_HASH: if (r16) SGX_HIST(SGX_PART_HASH, true); else SGX_HIST(SGX_PART_HASH, false); break;
+    case SGX_PART_HASH:
+        if ((pp.R & (pp.R - 1)) == 0) {
+            if (r16) SGX_HIST(KIND_HASH_POW2, true); else SGX_HIST(KIND_HASH_POW2, false);
+        } else {
+            if (r16) SGX_HIST(SGX_PART_HASH, true); else SGX_HIST(SGX_PART_HASH, false);
+        }
+        break;
     case SGX_PART_RANGE_I64: if (r16) SGX_HIST(SGX_PART_RANGE_I64, true); else SGX_HIST(SGX_PART_RANGE_I64, false); break;
     default: if (r16) SGX_HIST(SGX_PART_RANGE_BYTES10, true); else SGX_HIST(SGX_PART_RANGE_BYTES10, false); break;
     }
@@ -740,8 +756,59 @@ __device__ __forceinline__ void sc16_full_tile(const Sc16Lds &L, uint4 (&rec)[IT
     lds_barrier();
 }
 
+// Double-buffered variant (NT & 4): tile t+1's loads are issued into a second register
+// buffer at the very start of tile t, so they are in flight during tile t's whole rank /
+// stage / drain instead of only its drain.
+template <int KIND, int WAVES, int ITEMS>
+__device__ __forceinline__ void sc16_db_tile(const Sc16Lds &L, const uint4 (&cur)[ITEMS], uint4 (&nxt)[ITEMS],
+                                             const uint4 *src, int64_t tn, uint4 *__restrict__ out, int64_t n,
+                                             const PartParams &pp, uint32_t &bad) {
+    constexpr int T = WAVES * 64;
+    constexpr int TILE = WAVES * ITEMS * 64;
+    const uint32_t R = pp.R;
+    const uint32_t tid = threadIdx.x;
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        nxt[k] = src[tn * TILE + k * 64];
+        asm volatile("" ::: "memory");
+    }
+    uint32_t pid[ITEMS];
+    bool valid[ITEMS];
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        valid[k] = true;
+        pid[k] = pid_of<KIND>(cur[k].x, cur[k].y, cur[k].z, pp);
+    }
+    sc16_rank_stage<WAVES, ITEMS>(L, R, cur, pid, valid, pp.nbits);
+    constexpr int BATCH = ITEMS % 4 == 0 ? 4 : (ITEMS % 2 == 0 ? 2 : 1);
+#pragma unroll
+    for (int k0 = 0; k0 < ITEMS; k0 += BATCH) {
+        uint4 r[BATCH];
+        uint32_t d[BATCH];
+#pragma unroll
+        for (int j = 0; j < BATCH; ++j) r[j] = L.stage[(k0 + j) * T + tid];
+#pragma unroll
+        for (int j = 0; j < BATCH; ++j) {
+            const uint32_t s = (uint32_t)((k0 + j) * T + tid);
+            uint32_t p;
+            if constexpr (KIND == SGX_PART_HASH) p = hash_pid(r[j].x, r[j].y, pp);
+            else p = slot_partition(L.lstart, R, s);
+            d[j] = L.cursor[p] + (s - (uint32_t)L.lstart[p]);
+            const bool ok = (int64_t)d[j] < n;
+            bad |= ok ? 0u : 1u;
+            d[j] = ok ? d[j] : (uint32_t)(n - 1);
+        }
+#pragma unroll
+        for (int j = 0; j < BATCH; ++j) out[(size_t)d[j]] = r[j];
+    }
+    lds_barrier();
+    for (uint32_t p = tid; p < R; p += T) L.cursor[p] += L.tcnt[p];
+    for (uint32_t i = tid; i < (uint32_t)(WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
+    lds_barrier();
+}
+
 template <int KIND, int WAVES, int ITEMS, int NT = 0>
-__global__ __launch_bounds__(WAVES * 64, 2) void k_scatter16(const uint4 *__restrict__ in,
+__global__ __launch_bounds__(WAVES * 64, (NT & 4) ? 1 : 2) void k_scatter16(const uint4 *__restrict__ in,
                                                              uint4 *__restrict__ out, int64_t n,
                                                              int64_t chunk, PartParams pp,
                                                              const uint32_t *__restrict__ offs,
@@ -756,9 +823,28 @@ __global__ __launch_bounds__(WAVES * 64, 2) void k_scatter16(const uint4 *__rest
     const int64_t begin = (int64_t)g * chunk;
     const int64_t end = min(n, begin + chunk);
     for (uint32_t p = tid; p < R; p += T) L.cursor[p] = offs[(int64_t)p * G + g];
-    const int64_t nfull = NT == 0 && end > begin ? (end - begin) / TILE : 0;
+    const int64_t nfull = (NT & 3) == 0 && end > begin ? (end - begin) / TILE : 0;
     int64_t tbase = begin;
-    if (nfull > 0) {
+    if constexpr ((NT & 4) != 0) {
+        if (nfull > 0) {
+            const uint4 *src = in + begin + (int64_t)w * ITEMS * 64 + lane;
+            uint4 a[ITEMS], b[ITEMS];
+#pragma unroll
+            for (int k = 0; k < ITEMS; ++k) a[k] = src[k * 64];
+            for (uint32_t i = tid; i < (uint32_t)(WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
+            __syncthreads();
+            uint32_t bad = 0;
+            for (int64_t t = 0; t < nfull; t += 2) {
+                sc16_db_tile<KIND, WAVES, ITEMS>(L, a, b, src, t + 1 < nfull ? t + 1 : nfull - 1, out, n, pp, bad);
+                if (t + 1 < nfull)
+                    sc16_db_tile<KIND, WAVES, ITEMS>(L, b, a, src, t + 2 < nfull ? t + 2 : nfull - 1, out, n, pp, bad);
+            }
+            if (bad) atomicOr(err, SCATTER_OOB);
+            tbase = begin + nfull * TILE;
+        } else {
+            __syncthreads();
+        }
+    } else if (nfull > 0) {
         // Steady state (full tiles): tile t+1's loads are issued right after tile t is staged
         // in LDS -- before tile t's drain stores -- so the in-order vmcnt wait before ranking
         // t+1 retires exactly those loads and tile t's stores keep draining behind the next
@@ -783,6 +869,225 @@ __global__ __launch_bounds__(WAVES * 64, 2) void k_scatter16(const uint4 *__rest
     }
     for (; tbase < end; tbase += TILE)
         sc16_tile_generic<KIND, WAVES, ITEMS, 0, NT>(L, in, out, tbase, end, pp, n, err);
+}
+
+// ------------------------------------------------------------------------------------
+// K4 (default for hash partitioners): staged scatter with lane-ordered atomic ranking.
+//
+// Ranking is ONE ds_add_rtn_u32 per record into the wave's own packed-u16 counter row:
+// the LDS atomic unit resolves the lanes of one instruction that hit the same dword in
+// lane order (probed on gfx950: tools/mb_lds_atomic_order.hip, no violation in 3.4e10
+// same-address lane pairs), and one wave's LDS ops execute in issue order,
+// so the returned old value IS the record's stable rank among the wave's earlier records
+// of its partition (item-major, then lane).  The match-based ranker (k_scatter16) remains
+// selectable with SGX_RANK=match and is parity-tested the same way.
+//
+// Per tile (4 barriers):
+//   rank      pid + atomic rank per record, counts land in row w
+//   B1
+//   owners    thread t owns partition pairs [t*PP, t*PP+PP): exclusive sum over the wave
+//             rows (packed: both halves at once), block scan of the owned totals, then
+//             row[v][p] = lstart[p] + before_v[p], dlt[p] = cursor[p] - lstart[p],
+//             cursor[p] += total[p]                         (B2 inside the block scan)
+//   B3
+//   stage     stage[row[w][p] + rank] = record; the wave then zeroes its own row (only it
+//             reads that row after B3, in LDS order), so no barrier guards the next
+//             tile's atomics; the next tile's loads are issued here
+//   B4
+//   drain     slot s (partition-sorted) -> out[dlt[p] + s]: partition runs leave as
+//             contiguous bursts
+// LDS: stage[TILE] 16 B | rows[W][RS] u16 | cursor[RS] u32 | dlt[RS] u32 | scratch[64] u32
+// with RS = R rounded up to 8 (pad partitions have count 0).
+// ------------------------------------------------------------------------------------
+__host__ __device__ constexpr uint32_t rs8(uint32_t R) { return (R + 7u) & ~7u; }
+
+__host__ __device__ size_t scatter16_ord_lds(uint32_t R, int waves, int items) {
+    return (size_t)waves * items * 64 * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 8 + 64 * 4;
+}
+
+template <int KIND, int WAVES, int ITEMS, int PP, bool FULL>
+__device__ __forceinline__ void ord_tile(char *smem, u32x4 (&rec)[ITEMS], const bool (&valid)[ITEMS],
+                                         uint32_t tile_n, const u32x4 *nsrc, u32x4 *__restrict__ out,
+                                         int64_t n, const PartParams &pp, uint32_t &bad) {
+    constexpr int T = WAVES * 64;
+    constexpr int TILE = WAVES * ITEMS * 64;
+    const uint32_t R = pp.R, RS = rs8(R), NP = RS / 2;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    u32x4 *stage = (u32x4 *)smem;
+    uint16_t *rows = (uint16_t *)(smem + (size_t)TILE * 16);
+    uint32_t *cursor = (uint32_t *)(rows + (size_t)WAVES * RS);
+    uint32_t *dlt = cursor + RS;
+    uint32_t *scratch = dlt + RS;
+    uint16_t *myrow = rows + (size_t)w * RS;
+
+    // ---- rank
+    uint32_t pid[ITEMS], rank[ITEMS];
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) pid[k] = (FULL || valid[k]) ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        rank[k] = 0;
+        if (FULL || valid[k]) {
+            const uint32_t sh = (pid[k] & 1u) << 4;
+            const uint32_t old = __hip_atomic_fetch_add((uint32_t *)myrow + (pid[k] >> 1), 1u << sh,
+                                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            rank[k] = (old >> sh) & 0xFFFFu;
+        }
+        asm volatile("" ::: "memory");  // item order of the atomics is the stable order
+    }
+    lds_barrier();  // B1
+
+    // ---- owners: merge the wave rows, scan, offsets
+    uint32_t tot[PP], before[PP][WAVES];
+    uint32_t S = 0;
+#pragma unroll
+    for (int i = 0; i < PP; ++i) {
+        const uint32_t j = tid * PP + i;
+        uint32_t run = 0;
+        if (j < NP) {
+#pragma unroll
+            for (int v = 0; v < WAVES; ++v) {
+                const uint32_t c = ((const uint32_t *)(rows + (size_t)v * RS))[j];
+                before[i][v] = run;
+                run += c;  // packed: the two u16 halves never carry (<= TILE each)
+            }
+        }
+        tot[i] = run;
+        S += (run & 0xFFFFu) + (run >> 16);
+    }
+    const uint32_t x = wave_inclusive_scan(S, lane);
+    if (lane == 63) scratch[w] = x;
+    lds_barrier();  // B2
+    uint32_t base = x - S;
+    for (uint32_t v = 0; v < w; ++v) base += scratch[v];
+#pragma unroll
+    for (int i = 0; i < PP; ++i) {
+        const uint32_t j = tid * PP + i;
+        if (j < NP) {
+            const uint32_t lo = base, hi = base + (tot[i] & 0xFFFFu);
+            base = hi + (tot[i] >> 16);
+            const uint32_t L = lo | (hi << 16);
+#pragma unroll
+            for (int v = 0; v < WAVES; ++v) ((uint32_t *)(rows + (size_t)v * RS))[j] = before[i][v] + L;
+            const uint2 c = ((const uint2 *)cursor)[j];
+            ((uint2 *)dlt)[j] = make_uint2(c.x - lo, c.y - hi);
+            ((uint2 *)cursor)[j] = make_uint2(c.x + (tot[i] & 0xFFFFu), c.y + (tot[i] >> 16));
+        }
+    }
+    lds_barrier();  // B3
+
+    // ---- stage, zero own row, prefetch the next tile
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) {
+        if (FULL || valid[k]) {
+            const uint32_t slot = (uint32_t)myrow[pid[k]] + rank[k];
+            if (FULL || slot < (uint32_t)TILE) stage[slot] = rec[k];
+        }
+    }
+    for (uint32_t i = lane; i < RS / 8; i += 64) ((u32x4 *)myrow)[i] = u32x4{0, 0, 0, 0};
+    if (nsrc) {
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            rec[k] = nsrc[k * 64];
+            asm volatile("" ::: "memory");
+        }
+    }
+    lds_barrier();  // B4
+
+    // ---- drain
+    constexpr int BATCH = ITEMS % 4 == 0 ? 4 : (ITEMS % 2 == 0 ? 2 : 1);
+#pragma unroll
+    for (int k0 = 0; k0 < ITEMS; k0 += BATCH) {
+        u32x4 r[BATCH];
+        uint32_t d[BATCH];
+        bool live[BATCH];
+#pragma unroll
+        for (int j = 0; j < BATCH; ++j) {
+            const uint32_t s = (uint32_t)((k0 + j) * T + tid);
+            live[j] = FULL || s < tile_n;
+            r[j] = live[j] ? stage[s] : u32x4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int j = 0; j < BATCH; ++j) {
+            const uint32_t s = (uint32_t)((k0 + j) * T + tid);
+            const uint32_t p = pid_of<KIND>(r[j].x, r[j].y, r[j].z, pp);
+            d[j] = dlt[p] + s;
+        }
+#pragma unroll
+        for (int j = 0; j < BATCH; ++j) {
+            if (live[j]) {
+                const bool ok = (int64_t)d[j] < n;
+                bad |= ok ? 0u : 1u;
+                out[(size_t)(ok ? d[j] : (uint32_t)(n - 1))] = r[j];
+            }
+        }
+    }
+}
+
+template <int KIND, int WAVES, int ITEMS, int PP>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_ord(const u32x4 *__restrict__ in,
+                                                                 u32x4 *__restrict__ out, int64_t n,
+                                                                 int64_t chunk, PartParams pp,
+                                                                 const uint32_t *__restrict__ offs,
+                                                                 int G, uint32_t *err) {
+    constexpr int T = WAVES * 64;
+    constexpr int TILE = WAVES * ITEMS * 64;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint32_t R = pp.R, RS = rs8(R);
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t *rows32 = (uint32_t *)(smem + (size_t)TILE * 16);
+    uint32_t *cursor = rows32 + (size_t)WAVES * RS / 2;
+    const int g = blockIdx.x;
+    const int64_t begin = (int64_t)g * chunk;
+    const int64_t end = min(n, begin + chunk);
+    for (uint32_t p = tid; p < RS; p += T) cursor[p] = p < R ? offs[(int64_t)p * G + g] : 0u;
+    for (uint32_t i = tid; i < (uint32_t)WAVES * RS / 2; i += T) rows32[i] = 0u;
+    const int64_t len = end > begin ? end - begin : 0;
+    const int64_t nfull = len / TILE;
+    const u32x4 *src = in + begin + (int64_t)w * ITEMS * 64 + lane;
+    u32x4 rec[ITEMS];
+    bool valid[ITEMS];
+#pragma unroll
+    for (int k = 0; k < ITEMS; ++k) valid[k] = true;
+    if (nfull > 0) {
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) rec[k] = src[k * 64];
+    }
+    __syncthreads();
+    uint32_t bad = 0;
+    for (int64_t t = 0; t < nfull; ++t)
+        ord_tile<KIND, WAVES, ITEMS, PP, true>(smem, rec, valid, (uint32_t)TILE,
+                                               t + 1 < nfull ? src + (t + 1) * TILE : nullptr, out, n, pp, bad);
+    const int64_t rem = len - nfull * TILE;
+    if (rem > 0) {
+        const u32x4 *tsrc = src + nfull * TILE;
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            valid[k] = (int64_t)w * ITEMS * 64 + k * 64 + lane < rem;
+            rec[k] = valid[k] ? tsrc[k * 64] : u32x4{0, 0, 0, 0};
+        }
+        ord_tile<KIND, WAVES, ITEMS, PP, false>(smem, rec, valid, (uint32_t)rem, nullptr, out, n, pp, bad);
+    }
+    if (bad) atomicOr(err, SCATTER_OOB);
+}
+
+struct OrdGeo { int waves, items, pp; };
+// every instantiated lane-ordered geometry (launch_scatter's switch lists the same set)
+static const OrdGeo kOrdGeos[] = {{8, 16, 1}, {12, 10, 1}, {16, 7, 1}, {8, 8, 2}, {4, 16, 8}};
+
+ScatterGeom scatter_geom16_ord(uint32_t R, int force_waves, int force_items) {
+    ScatterGeom best{0, 0, 0, 0, 0};
+    for (const OrdGeo &g : kOrdGeos) {
+        if (force_waves && force_waves != g.waves) continue;
+        if (force_items && force_items != g.items) continue;
+        const uint32_t T = (uint32_t)g.waves * 64;
+        if ((rs8(R) / 2 + T - 1) / T > (uint32_t)g.pp) continue;
+        const size_t lds = scatter16_ord_lds(R, g.waves, g.items);
+        if (lds > LDS_MAX) continue;
+        const int tile = g.waves * g.items * 64;
+        if (tile > best.tile) best = ScatterGeom{ORD_GEOM_BASE + g.waves, g.items, tile, lds, g.pp};
+    }
+    return best;
 }
 
 template <int DIAG>
@@ -1265,7 +1570,7 @@ __global__ __launch_bounds__(WIDE_THREADS, 1) void k_scatter_wide(const char *__
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t chunk, int G,
                           const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
                           uint32_t *err, hipStream_t stream) {
-    if (rb == 16 && geo.waves >= DIRECT_GEOM_BASE) {
+    if (rb == 16 && is_direct_geom(geo.waves)) {
         const int W = geo.waves - DIRECT_GEOM_BASE;
 #define SGX_SCD(K, WV, I)                                                                       \
     do {                                                                                        \
@@ -1292,6 +1597,33 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         }
 #undef SGX_SCD_K
 #undef SGX_SCD
+        return hipGetLastError();
+    }
+    if (rb == 16 && geo.waves >= ORD_GEOM_BASE) {
+        const int W = geo.waves - ORD_GEOM_BASE;
+#define SGX_ORD(K, WV, I, P)                                                                     \
+    do {                                                                                         \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_ord<K, WV, I, P>,                   \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
+        hipLaunchKernelGGL((k_scatter16_ord<K, WV, I, P>), dim3(G), dim3(WV * 64), geo.lds_bytes, \
+                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err); \
+    } while (0)
+#define SGX_ORD_K(K)                                                      \
+    do {                                                                  \
+        switch (W * 10000 + geo.items * 100 + geo.mbits) {                \
+        case 81601: SGX_ORD(K, 8, 16, 1); break;                          \
+        case 121001: SGX_ORD(K, 12, 10, 1); break;                        \
+        case 160701: SGX_ORD(K, 16, 7, 1); break;                         \
+        case 80802: SGX_ORD(K, 8, 8, 2); break;                           \
+        case 41608: SGX_ORD(K, 4, 16, 8); break;                          \
+        default: return hipErrorInvalidValue;                             \
+        }                                                                 \
+    } while (0)
+        if (pp.kind != SGX_PART_HASH) return hipErrorInvalidValue;
+        if ((pp.R & (pp.R - 1)) == 0) SGX_ORD_K(KIND_HASH_POW2);
+        else SGX_ORD_K(SGX_PART_HASH);
+#undef SGX_ORD_K
+#undef SGX_ORD
         return hipGetLastError();
     }
     if (rb == 16 && geo.waves == DMA_GEOM_TAG) {
@@ -1325,7 +1657,8 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         if (geo.nt && key == 816) {                                          \
             if (geo.nt == 1) SGX_SC16NT(K, 8, 16, 1);                        \
             else if (geo.nt == 2) SGX_SC16NT(K, 8, 16, 2);                   \
-            else SGX_SC16NT(K, 8, 16, 3);                                    \
+            else if (geo.nt == 3) SGX_SC16NT(K, 8, 16, 3);                   \
+            else SGX_SC16NT(K, 8, 16, 4);                                    \
             break;                                                           \
         }                                                                    \
         switch (key) {                                                       \

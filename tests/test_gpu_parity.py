@@ -124,13 +124,18 @@ def test_chunking_does_not_change_output(sgx_lib, oracle_lib, num_chunks):
         check_against_oracle(e, oracle_lib, recs, 1024)
 
 
-GEOMETRIES = [(4, 16), (8, 16), (12, 10), (16, 7), (4, 12), (8, 8), (4, 8), (8, 4), (4, 4), (4, 2), (4, 1)]
+GEOMETRIES = [(4, 16), (8, 16), (12, 10), (14, 9), (16, 7), (4, 12), (8, 8), (4, 8), (8, 4), (4, 4), (4, 2), (4, 1)]
 
 
+@pytest.mark.parametrize("rank", ["ordered", "match"])
 @pytest.mark.parametrize("waves,items", GEOMETRIES)
-@pytest.mark.parametrize("R", [7, 200, 1024, 4096])
-def test_every_staged_geometry(sgx_lib, oracle_lib, waves, items, R):
-    """Every instantiated K4 geometry, full tiles + a ragged tail, multiple chunks."""
+@pytest.mark.parametrize("R", [7, 200, 1024, 1536, 4096])
+def test_every_staged_geometry(sgx_lib, oracle_lib, monkeypatch, waves, items, R, rank):
+    """Every instantiated K4 geometry of both rankers (lane-ordered atomics, ballot/peer
+    table), full tiles + a ragged tail, multiple chunks.  A (waves, items) pair the
+    lane-ordered kernel lacks falls back to the match kernel, which is then re-tested."""
+    if rank == "match":
+        monkeypatch.setenv("SGX_RANK", "match")
     tile = waves * items * 64
     n = 5 * tile * 3 + tile // 3 + 7
     recs = oracle_lib.gen_uniform16(n, 0xC0FFEE + R)
@@ -143,7 +148,7 @@ def test_every_staged_geometry(sgx_lib, oracle_lib, waves, items, R):
 
 @pytest.mark.parametrize("env", ["SGX_SCATTER_DMA=1", "SGX_SCATTER_DIRECT=816", "SGX_SCATTER_DIRECT=408",
                                  "SGX_SCATTER_CHAIN=816", "SGX_SCATTER_CHAIN=1607", "SGX_NO_PEER_TABLE=1",
-                                 "SGX_SCATTER_NT=1"])
+                                 "SGX_SCATTER_NT=1", "SGX_SCATTER_NT=4", "SGX_RANK=match"])
 def test_alternative_scatter_variants(sgx_lib, oracle_lib, monkeypatch, env):
     """The A/B variants kept for measurement must stay bit-exact too (engine reads the env
     at creation)."""
@@ -159,6 +164,18 @@ def test_zipf_skew_r4096(engine, oracle_lib):
     cdf = oracle_lib.zipf_cdf(1.1, 2**24)
     recs = oracle_lib.gen_zipf16(1_000_000, 11, cdf)
     check_against_oracle(engine, oracle_lib, recs, 4096)
+
+
+@pytest.mark.parametrize("distinct", [2, 5, 64, 300])
+@pytest.mark.parametrize("R", [7, 1024, 4096])
+def test_heavy_collisions(engine, oracle_lib, distinct, R):
+    """Few distinct keys: many lanes of one ranking atomic hit the same counter dword, the
+    case where stability rests on lane-ordered LDS atomics."""
+    recs = oracle_lib.gen_uniform16(300_001, distinct * 7 + R)
+    keys = np.arange(distinct, dtype=np.int64) * 7919 - 3
+    pick = np.random.default_rng(distinct).integers(0, distinct, len(recs))
+    recs[:, :8] = keys[pick].view(np.uint8).reshape(-1, 8)
+    check_against_oracle(engine, oracle_lib, recs, R)
 
 
 def test_all_records_one_partition(engine, oracle_lib):

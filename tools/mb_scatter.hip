@@ -1,0 +1,85 @@
+// Memory-only floor for K4's store pattern (measurement tool, not product code).
+//
+// N 16 B records, G chunks (one workgroup each), R partitions.  Tile t of chunk g holds
+// TILE records already "sorted": slot s belongs to partition p = s / RUN (RUN = TILE / R)
+// and goes to out[p * (N/R) + g * (N/R/G) + t * RUN + s % RUN] -- exactly where a uniform
+// hash shuffle sends it.  No LDS, no ranking: coalesced loads, arithmetic destinations.
+//
+//   mode 0: coalesced copy (out[i] = in[i])
+//   mode 1: the scatter pattern above
+//
+// build: hipcc -O3 --offload-arch=gfx950 -o /tmp/mb_scatter tools/mb_scatter.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+
+#define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s: %s\n", #x, hipGetErrorString(e_)); exit(1); } } while (0)
+
+template <int WAVES, int ITEMS, int MODE>
+__global__ __launch_bounds__(WAVES * 64) void k(const uint4 *__restrict__ in, uint4 *__restrict__ out,
+                                                long n, long chunk, int R, int G) {
+    constexpr int T = WAVES * 64, TILE = T * ITEMS;
+    const int g = blockIdx.x;
+    const long begin = (long)g * chunk, end = begin + chunk;
+    const long per_part = n / R, per_chunk = per_part / G;
+    const int run = TILE / R;
+    for (long tb = begin; tb < end; tb += TILE) {
+        uint4 r[ITEMS];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) r[j] = in[tb + j * T + threadIdx.x];
+#pragma unroll
+        for (int j = 0; j < ITEMS; ++j) {
+            const int s = j * T + threadIdx.x;
+            long d;
+            if (MODE == 0) d = tb + s;
+            else {
+                const long t = (tb - begin) / TILE;
+                const int p = s / run;
+                d = (long)p * per_part + (long)g * per_chunk + t * run + s % run;
+            }
+            out[d] = r[j];
+        }
+    }
+}
+
+template <int W, int I, int M>
+float timeit(const uint4 *in, uint4 *out, long n, int R, int G, int reps) {
+    const long chunk = n / G;
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    std::vector<float> ts;
+    for (int i = 0; i < reps + 2; ++i) {
+        CK(hipEventRecord(a));
+        k<W, I, M><<<G, W * 64>>>(in, out, n, chunk, R, G);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        if (i >= 2) ts.push_back(ms);
+    }
+    std::sort(ts.begin(), ts.end());
+    return ts[ts.size() / 2];
+}
+
+int main(int argc, char **argv) {
+    const long n = 1L << 28;
+    uint4 *in, *out;
+    CK(hipMalloc(&in, n * 16));
+    CK(hipMalloc(&out, n * 16));
+    CK(hipMemset(in, 1, n * 16));
+    CK(hipMemset(out, 0, n * 16));
+    const double gb = 32.0 * n / 1e9;
+    auto rep = [&](const char *name, int R, int G, float ms) {
+        printf("{\"kernel\": \"%s\", \"R\": %d, \"G\": %d, \"ms\": %.4f, \"GBs\": %.1f}\n", name, R, G, ms, gb / ms * 1e3);
+    };
+    for (int G : {256, 512, 1024, 2048}) {
+        rep("copy_8x16", 0, G, timeit<8, 16, 0>(in, out, n, 1, G, 10));
+        for (int R : {1024, 512, 256, 128, 64}) rep("scatter_8x16", R, G, timeit<8, 16, 1>(in, out, n, R, G, 10));
+        rep("scatter_4x16", 1024, G, timeit<4, 16, 1>(in, out, n, 1024, G, 10));
+        rep("scatter_8x8", 512, G, timeit<8, 8, 1>(in, out, n, 512, G, 10));
+    }
+    return 0;
+}

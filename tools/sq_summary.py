@@ -1,0 +1,22 @@
+#!/usr/bin/env python3
+"""Per-kernel medians of the counters collected by tools/sq_counters.sh."""
+import csv
+import glob
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+d = sys.argv[1]
+vals = defaultdict(lambda: defaultdict(list))
+for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
+    with open(f) as fh:
+        for r in csv.DictReader(fh):
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+for k, cs in vals.items():
+    if len(sys.argv) > 2 and sys.argv[2] not in k:
+        continue
+    print(k)
+    for c, v in sorted(cs.items()):
+        print(f"  {c:28s} {statistics.median(v):16.0f}   (n={len(v)})")
