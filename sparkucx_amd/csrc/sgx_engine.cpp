@@ -166,6 +166,7 @@ struct sgx_engine {
     int rank_match = 0;              // SGX_RANK=match: ballot/peer-table ranking in K4
     int nt = 0;                      // SGX_SCATTER_NT=1/2/3: nontemporal loads/stores; 4: double-buffered (A/B)
     int chain = 0;                   // SGX_SCATTER_CHAIN=WWII: chained look-back K4 (A/B)
+    int wc = 1;                      // SGX_SCATTER_WC=0: no write-combining K4 (A/B)
     hipStream_t s_comp = nullptr, s_comm = nullptr;
     // work buffers of the map-side pipeline
     DevBuf counts, offs, status, part_off_dev, input_stage;
@@ -254,6 +255,7 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     if (const char *d = getenv("SGX_SCATTER_NT")) e->nt = atoi(d);
     if (const char *d = getenv("SGX_RANK")) e->rank_match = std::strcmp(d, "match") == 0;
     if (const char *d = getenv("SGX_SCATTER_CHAIN")) e->chain = atoi(d);
+    if (const char *d = getenv("SGX_SCATTER_WC")) e->wc = atoi(d);
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
     *out = e.release();
@@ -449,6 +451,11 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
         !e->use_dma && e->nt == 0 && e->chain == 0) {
         const ScatterGeom o = scatter_geom16_ord((uint32_t)s.R, e->sc_waves, e->sc_items);
         if (o.items) geo = o;
+        // write-combining K4 (whole 128 B lines only) where its LDS fits (R <= 1024)
+        if (e->wc && e->sc_waves == 0 && e->sc_items == 0) {
+            const ScatterGeom w = scatter_geom16_wc((uint32_t)s.R);
+            if (w.items) geo = w;
+        }
     }
     if (geo.items == 0)
         return fail(SGX_ERR_UNSUPPORTED, "no scatter geometry (waves %d, items %d) fits R=%d", e->sc_waves,

@@ -56,6 +56,10 @@ constexpr int DIRECT_GEOM_BASE = 1000;
 // Lane-ordered-ranking staged kernel (waves == ORD_GEOM_BASE + real waves, mbits == PP).
 constexpr int ORD_GEOM_BASE = 2000;
 ScatterGeom scatter_geom16_ord(uint32_t R, int force_waves = 0, int force_items = 0);
+// Write-combining staged kernel (waves == WC_GEOM_BASE + real waves, items == new records
+// per lane, mbits == stage slots per lane).
+constexpr int WC_GEOM_BASE = 3000;
+ScatterGeom scatter_geom16_wc(uint32_t R);
 inline bool is_direct_geom(int waves) { return waves >= DIRECT_GEOM_BASE && waves < ORD_GEOM_BASE; }
 ScatterGeom scatter_geom16_direct(uint32_t R, int waves, int items);
 __host__ __device__ size_t scatter16_lds(uint32_t R, int waves, int items, int mbits);

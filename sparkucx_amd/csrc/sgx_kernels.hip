@@ -1090,6 +1090,244 @@ ScatterGeom scatter_geom16_ord(uint32_t R, int force_waves, int force_items) {
     return best;
 }
 
+// ------------------------------------------------------------------------------------
+// K4 (write-combining, default for hash partitioners with R <= 1024): only whole,
+// 128 B-aligned output lines leave the CU.
+//
+// Why: a tile of T records gives every partition a run of ~T/R records (8 at T = 8192,
+// R = 1024: ONE line's worth) starting at an arbitrary record offset, so nearly every
+// run straddles two 128 B lines, each completed by the NEXT tile's run tens of µs later.
+// Those half-written lines leave L2 as partial-line writes that cost a full line of HBM
+// time: tools/mb_scatter.hip measures the store pattern alone at 2.98 ms for unaligned
+// runs vs 1.99 ms for line-aligned runs (C1, memory only, no ranking) -- and the ranked
+// kernels above run at 2.9 ms, i.e. AT the unaligned floor.
+//
+// How: each (partition, chunk) output stream keeps its incomplete last line ON CHIP.
+// Per tile, partition p's stage segment is [deferred records of p][new records of p],
+// covering output positions [a_p, e_p) with a_p = c_p - dl_p (c_p = cursor of the first
+// new record, dl_p <= 7 deferred records).  The drain writes positions [a_p, LE_p) with
+// LE_p = max(e_p & ~7, a_p): every line it writes is complete (only a stream's first line
+// can be partial: its head belongs to the previous stream).  Records at [LE_p, e_p) stay
+// in the REGISTERS of the lane that drained them (slot k of the lane's SI drain items,
+// with their output position) and are staged again, ahead of the next tile's new records.
+// The chunk's last tile flushes everything; so does a tile whose deferred records would
+// not fit next to a full tile (sum dl > DCAP: rare, R <= 585 never), which only costs a
+// few partial lines.  The output is byte-identical to every other K4: positions come from
+// the same counts and the same stable ranks.
+//
+// Tile: NI new records per lane (TNEW = T*NI) + up to DCAP = T*SI - TNEW deferred ones.
+// LDS: stage[T*SI] 16 B | rows[W][RS] u16 | cur[RS] u32 | dlt[RS] u32 | lim[RS] u32 |
+// dl[RS] u16 (RS = R rounded up to 8).  The merge's block-scan scratch borrows the stage
+// (free between B1 and B3: every wave has drained the previous tile before B1).
+// ------------------------------------------------------------------------------------
+__host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
+    return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 14;
+}
+
+template <int KIND, int WAVES, int NI, int SI>
+__global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__restrict__ in,
+                                                                u32x4 *__restrict__ out, int64_t n,
+                                                                int64_t chunk, PartParams pp,
+                                                                const uint32_t *__restrict__ offs,
+                                                                int G, uint32_t *err) {
+    constexpr int T = WAVES * 64;
+    constexpr int TNEW = T * NI;
+    constexpr int STAGE = T * SI;
+    constexpr uint32_t DCAP = (uint32_t)(STAGE - TNEW);
+    static_assert(SI > NI && SI <= 32, "deferred slots are tracked in a 32-bit mask");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint32_t R = pp.R, RS = rs8(R), NP = RS / 2;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    u32x4 *stage = (u32x4 *)smem;
+    uint16_t *rows = (uint16_t *)(smem + (size_t)STAGE * 16);
+    uint32_t *cur = (uint32_t *)(rows + (size_t)WAVES * RS);
+    uint32_t *dlt = cur + RS;
+    uint32_t *lim = dlt + RS;
+    uint16_t *dl = (uint16_t *)(lim + RS);
+    uint32_t *scratch = (uint32_t *)smem;  // merge only (B1..B3)
+    uint16_t *myrow = rows + (size_t)w * RS;
+
+    const int g = blockIdx.x;
+    const int64_t begin = (int64_t)g * chunk;
+    const int64_t end = min(n, begin + chunk);
+    const int64_t len = end > begin ? end - begin : 0;
+    const int64_t ntiles = (len + TNEW - 1) / TNEW;
+    for (uint32_t p = tid; p < RS; p += T) {
+        cur[p] = p < R ? offs[(int64_t)p * G + g] : 0u;
+        dl[p] = 0;
+    }
+    for (uint32_t i = tid; i < (uint32_t)WAVES * RS / 2; i += T) ((uint32_t *)rows)[i] = 0u;
+
+    const u32x4 *src = in + begin + (int64_t)w * NI * 64 + lane;
+    u32x4 rec[NI];
+    bool valid[NI];
+    u32x4 dk[SI];
+    uint32_t dpos[SI];
+    uint32_t dmask = 0;
+#pragma unroll
+    for (int k = 0; k < SI; ++k) { dk[k] = u32x4{0, 0, 0, 0}; dpos[k] = 0; }
+    if (ntiles > 0) {
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            valid[k] = (int64_t)w * NI * 64 + k * 64 + lane < len;
+            rec[k] = valid[k] ? src[k * 64] : u32x4{0, 0, 0, 0};
+        }
+    }
+    __syncthreads();
+    uint32_t bad = 0;
+    for (int64_t t = 0; t < ntiles; ++t) {
+        const bool last = t == ntiles - 1;
+        // ---- rank the new records (stable: item-major, then lane, one LDS atomic each)
+        uint32_t pid[NI], rank[NI];
+#pragma unroll
+        for (int k = 0; k < NI; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            rank[k] = 0;
+            if (valid[k]) {
+                const uint32_t sh = (pid[k] & 1u) << 4;
+                const uint32_t old = __hip_atomic_fetch_add((uint32_t *)myrow + (pid[k] >> 1), 1u << sh,
+                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                rank[k] = (old >> sh) & 0xFFFFu;
+            }
+            asm volatile("" ::: "memory");
+        }
+        lds_barrier();  // B1
+
+        // ---- merge: per partition pair (one pair per thread), both u16 halves at once
+        const uint32_t j = tid;
+        uint32_t before[WAVES], tot = 0, dlp = 0, seg = 0, dnf_lo = 0, dnf_hi = 0;
+        uint2 c = make_uint2(0, 0);
+        uint32_t S = 0, D = 0;
+        if (j < NP) {
+#pragma unroll
+            for (int v = 0; v < WAVES; ++v) {
+                const uint32_t x = ((const uint32_t *)(rows + (size_t)v * RS))[j];
+                before[v] = tot;
+                tot += x;  // <= TNEW per half: no carry between halves
+            }
+            dlp = ((const uint32_t *)dl)[j];
+            seg = tot + dlp;
+            c = ((const uint2 *)cur)[j];
+            const uint32_t e0 = c.x + (tot & 0xFFFFu), e1 = c.y + (tot >> 16);
+            const uint32_t a0 = c.x - (dlp & 0xFFFFu), a1 = c.y - (dlp >> 16);
+            dnf_lo = e0 - max(e0 & ~7u, a0);
+            dnf_hi = e1 - max(e1 & ~7u, a1);
+            S = (seg & 0xFFFFu) + (seg >> 16);
+            D = dnf_lo + dnf_hi;
+        }
+        const uint32_t xs = wave_inclusive_scan(S | (D << 16), lane);  // S <= STAGE, D <= 7R
+        if (lane == 63) scratch[w] = xs;
+        lds_barrier();  // B2
+        uint32_t base = (xs - (S | (D << 16))) & 0xFFFFu, total = 0, dsum = 0;
+#pragma unroll
+        for (int v = 0; v < WAVES; ++v) {
+            const uint32_t y = scratch[v];
+            if (v < (int)w) base += y & 0xFFFFu;
+            total += y & 0xFFFFu;
+            dsum += y >> 16;
+        }
+        const bool flush = last || dsum > DCAP;
+        if (j < NP) {
+            const uint32_t ls0 = base, ls1 = base + (seg & 0xFFFFu);
+            const uint32_t t0 = tot & 0xFFFFu, t1 = tot >> 16;
+            const uint32_t dl0 = dlp & 0xFFFFu, dl1 = dlp >> 16;
+            const uint32_t L = (ls0 + dl0) | ((ls1 + dl1) << 16);  // new records start after the deferred
+#pragma unroll
+            for (int v = 0; v < WAVES; ++v) ((uint32_t *)(rows + (size_t)v * RS))[j] = before[v] + L;
+            const uint32_t e0 = c.x + t0, e1 = c.y + t1;
+            const uint32_t a0 = c.x - dl0, a1 = c.y - dl1;
+            const uint32_t le0 = flush ? e0 : e0 - dnf_lo, le1 = flush ? e1 : e1 - dnf_hi;
+            ((uint2 *)dlt)[j] = make_uint2(a0 - ls0, a1 - ls1);
+            ((uint2 *)lim)[j] = make_uint2(le0, le1);
+            ((uint2 *)cur)[j] = make_uint2(e0, e1);
+            ((uint32_t *)dl)[j] = (e0 - le0) | ((e1 - le1) << 16);
+        }
+        lds_barrier();  // B3
+
+        // ---- stage: deferred records first (their slots follow from their positions), then
+        //      the new ones; zero this wave's counter row; prefetch the next tile
+#pragma unroll
+        for (int k = 0; k < SI; ++k) {
+            if ((dmask >> k) & 1u) {
+                const uint32_t p = pid_of<KIND>(dk[k].x, dk[k].y, dk[k].z, pp);
+                const uint32_t slot = dpos[k] - dlt[p];
+                if (slot < (uint32_t)STAGE) stage[slot] = dk[k];
+                else bad = 1;
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < NI; ++k) {
+            if (valid[k]) {
+                const uint32_t slot = (uint32_t)myrow[pid[k]] + rank[k];
+                if (slot < (uint32_t)STAGE) stage[slot] = rec[k];
+                else bad = 1;
+            }
+        }
+        for (uint32_t i = lane; i < RS / 8; i += 64) ((u32x4 *)myrow)[i] = u32x4{0, 0, 0, 0};
+        if (!last) {
+            const int64_t nb = (t + 1) * TNEW;
+            const u32x4 *s2 = src + nb;
+#pragma unroll
+            for (int k = 0; k < NI; ++k) {
+                valid[k] = nb + (int64_t)w * NI * 64 + k * 64 + lane < len;
+                rec[k] = valid[k] ? s2[k * 64] : u32x4{0, 0, 0, 0};
+                asm volatile("" ::: "memory");
+            }
+        }
+        lds_barrier();  // B4
+
+        // ---- drain: whole lines out, the rest back into registers
+        dmask = 0;
+#pragma unroll
+        for (int k0 = 0; k0 < SI; k0 += 4) {
+            u32x4 r[4];
+            uint32_t pos[4];
+            bool live[4], wr[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t s = (uint32_t)((k0 + q) * T + tid);
+                live[q] = s < total;
+                r[q] = live[q] ? stage[s] : u32x4{0, 0, 0, 0};
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint32_t s = (uint32_t)((k0 + q) * T + tid);
+                const uint32_t p = pid_of<KIND>(r[q].x, r[q].y, r[q].z, pp);
+                pos[q] = dlt[p] + s;
+                wr[q] = live[q] && pos[q] < lim[p];
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                if (wr[q]) {
+                    const bool ok = (int64_t)pos[q] < n;
+                    bad |= ok ? 0u : 1u;
+                    out[(size_t)(ok ? pos[q] : (uint32_t)(n - 1))] = r[q];
+                } else if (live[q]) {
+                    dk[k0 + q] = r[q];
+                    dpos[k0 + q] = pos[q];
+                    dmask |= 1u << (k0 + q);
+                }
+            }
+        }
+    }
+    if (bad) atomicOr(err, SCATTER_OOB);
+}
+
+static_assert(16 % 4 == 0, "k_scatter16_wc drains in groups of 4 slots");
+
+// geometry: waves = WC_GEOM_BASE + 8, items = NI (new records per lane), mbits = SI
+ScatterGeom scatter_geom16_wc(uint32_t R) {
+    constexpr int W = 8, SI = 16;
+    const uint32_t T = W * 64;
+    if (rs8(R) / 2 > T) return ScatterGeom{0, 0, 0, 0, 0};
+    const size_t lds = scatter16_wc_lds(R, W, SI);
+    if (lds > LDS_MAX) return ScatterGeom{0, 0, 0, 0, 0};
+    // biggest new-record share whose deferred cap (T*SI - T*NI) still holds 7 per partition
+    const int ni = 7u * rs8(R) <= T * (SI - 12) ? 12 : 8;
+    return ScatterGeom{WC_GEOM_BASE + W, ni, (int)T * ni, lds, SI};
+}
+
 template <int DIAG>
 __global__ __launch_bounds__(512, 2) void k_scatter16_diag(const uint4 *__restrict__ in,
                                                            uint4 *__restrict__ out, int64_t n,
@@ -1597,6 +1835,26 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         }
 #undef SGX_SCD_K
 #undef SGX_SCD
+        return hipGetLastError();
+    }
+    if (rb == 16 && geo.waves >= WC_GEOM_BASE) {
+        if (pp.kind != SGX_PART_HASH || geo.waves != WC_GEOM_BASE + 8 || geo.mbits != 16) return hipErrorInvalidValue;
+#define SGX_WC(K, NI)                                                                            \
+    do {                                                                                         \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, 8, NI, 16>,                   \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
+        hipLaunchKernelGGL((k_scatter16_wc<K, 8, NI, 16>), dim3(G), dim3(512), geo.lds_bytes,     \
+                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err); \
+    } while (0)
+        const bool pow2 = (pp.R & (pp.R - 1)) == 0;
+        if (geo.items == 12) {
+            if (pow2) SGX_WC(KIND_HASH_POW2, 12); else SGX_WC(SGX_PART_HASH, 12);
+        } else if (geo.items == 8) {
+            if (pow2) SGX_WC(KIND_HASH_POW2, 8); else SGX_WC(SGX_PART_HASH, 8);
+        } else {
+            return hipErrorInvalidValue;
+        }
+#undef SGX_WC
         return hipGetLastError();
     }
     if (rb == 16 && geo.waves >= ORD_GEOM_BASE) {

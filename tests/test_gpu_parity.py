@@ -148,7 +148,7 @@ def test_every_staged_geometry(sgx_lib, oracle_lib, monkeypatch, waves, items, R
 
 @pytest.mark.parametrize("env", ["SGX_SCATTER_DMA=1", "SGX_SCATTER_DIRECT=816", "SGX_SCATTER_DIRECT=408",
                                  "SGX_SCATTER_CHAIN=816", "SGX_SCATTER_CHAIN=1607", "SGX_NO_PEER_TABLE=1",
-                                 "SGX_SCATTER_NT=1", "SGX_SCATTER_NT=4", "SGX_RANK=match"])
+                                 "SGX_SCATTER_NT=1", "SGX_SCATTER_NT=4", "SGX_RANK=match", "SGX_SCATTER_WC=0"])
 def test_alternative_scatter_variants(sgx_lib, oracle_lib, monkeypatch, env):
     """The A/B variants kept for measurement must stay bit-exact too (engine reads the env
     at creation)."""
@@ -157,6 +157,24 @@ def test_alternative_scatter_variants(sgx_lib, oracle_lib, monkeypatch, env):
     recs = oracle_lib.gen_uniform16(3 * 8192 * 5 + 1234, 99)
     with sgx_lib.ShuffleEngine(device=0) as e:
         for R in (200, 1024):
+            check_against_oracle(e, oracle_lib, recs, R)
+
+
+@pytest.mark.parametrize("R", [200, 585, 586, 1000, 1024])
+@pytest.mark.parametrize("group", [7, 15, 1])
+def test_write_combining_carry_pressure(sgx_lib, oracle_lib, R, group):
+    """Write-combining K4: records arrive in runs of `group` per partition, so most
+    partitions end every tile with a 7-record tail; the deferred records then exceed the
+    tile's carry capacity and force the flush path, alternating with normal tiles.  Several
+    chunks, a ragged last tile; bit-exact against the oracle."""
+    n = 3 * 4096 * 7 + 1234
+    recs = oracle_lib.gen_uniform16(n, 0xCA11 + R + group)
+    rng = np.random.default_rng(R * 31 + group)
+    pids = np.concatenate([np.repeat(rng.permutation(R), group) for _ in range(n // (R * group) + 1)])[:n]
+    keys = (pids + R * rng.integers(0, 1000, n)).astype(np.int64)  # 0 <= key < 2^31: pid = key % R
+    recs[:, :8] = keys.view(np.uint8).reshape(-1, 8)
+    for chunks in (1, 3):
+        with sgx_lib.ShuffleEngine(device=0, num_chunks=chunks) as e:
             check_against_oracle(e, oracle_lib, recs, R)
 
 

@@ -6,7 +6,10 @@
 // hash shuffle sends it.  No LDS, no ranking: coalesced loads, arithmetic destinations.
 //
 //   mode 0: coalesced copy (out[i] = in[i])
-//   mode 1: the scatter pattern above
+//   mode 1: the scatter pattern above (every run starts on a 128 B line)
+//   mode 2: same runs, each (chunk, partition) stream shifted by 0..7 records: runs straddle
+//           lines the way real cursors do (a line is finished by the next tile's run)
+//   mode 3: shift 0 or 4 records: runs start on 64 B but not always on 128 B
 //
 // build: hipcc -O3 --offload-arch=gfx950 -o /tmp/mb_scatter tools/mb_scatter.hip
 #include <hip/hip_runtime.h>
@@ -38,6 +41,8 @@ __global__ __launch_bounds__(WAVES * 64) void k(const uint4 *__restrict__ in, ui
                 const long t = (tb - begin) / TILE;
                 const int p = s / run;
                 d = (long)p * per_part + (long)g * per_chunk + t * run + s % run;
+                if (MODE == 2) d += (g * 7 + p * 13) & 7;
+                if (MODE == 3) d += ((g * 7 + p * 13) & 1) * 4;
             }
             out[d] = r[j];
         }
@@ -68,18 +73,20 @@ int main(int argc, char **argv) {
     const long n = 1L << 28;
     uint4 *in, *out;
     CK(hipMalloc(&in, n * 16));
-    CK(hipMalloc(&out, n * 16));
+    CK(hipMalloc(&out, (n + 64) * 16));
     CK(hipMemset(in, 1, n * 16));
     CK(hipMemset(out, 0, n * 16));
     const double gb = 32.0 * n / 1e9;
     auto rep = [&](const char *name, int R, int G, float ms) {
         printf("{\"kernel\": \"%s\", \"R\": %d, \"G\": %d, \"ms\": %.4f, \"GBs\": %.1f}\n", name, R, G, ms, gb / ms * 1e3);
     };
-    for (int G : {256, 512, 1024, 2048}) {
+    for (int G : {256, 512, 2048}) {
         rep("copy_8x16", 0, G, timeit<8, 16, 0>(in, out, n, 1, G, 10));
-        for (int R : {1024, 512, 256, 128, 64}) rep("scatter_8x16", R, G, timeit<8, 16, 1>(in, out, n, R, G, 10));
-        rep("scatter_4x16", 1024, G, timeit<4, 16, 1>(in, out, n, 1024, G, 10));
-        rep("scatter_8x8", 512, G, timeit<8, 8, 1>(in, out, n, 512, G, 10));
+        rep("scatter_8x16_aligned128", 1024, G, timeit<8, 16, 1>(in, out, n, 1024, G, 10));
+        rep("scatter_8x16_unaligned", 1024, G, timeit<8, 16, 2>(in, out, n, 1024, G, 10));
+        rep("scatter_8x16_aligned64", 1024, G, timeit<8, 16, 3>(in, out, n, 1024, G, 10));
+        rep("scatter_8x16_unaligned_R512", 512, G, timeit<8, 16, 2>(in, out, n, 512, G, 10));
+        rep("scatter_8x16_unaligned_R4096", 4096, G, timeit<8, 16, 2>(in, out, n, 4096, G, 10));
     }
     return 0;
 }

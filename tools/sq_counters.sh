@@ -11,5 +11,5 @@ P3="SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_INST_CYCLES_VMEM_WR SQ_INST_CYCLES
 i=0
 for p in "$P1" "$P2" "$P3"; do
   i=$((i+1))
-  timeout -k 10 240 rocprofv3 --pmc $p -d "$out/p$i" -o run -- python3 tools/prof_map.py --iters 2 "$@" > "$out/p$i.log" 2>&1
+  timeout -k 10 240 rocprofv3 --pmc $p --output-format csv -d "$out/p$i" -o run -- python3 tools/prof_map.py "$@" > "$out/p$i.log" 2>&1
 done

@@ -24,8 +24,21 @@ def main():
 
     import sparkucx_amd as sgx
 
-    variants = [tuple(int(x) for x in v.split(":")) for v in a.variants.split(",")]
-    engines = [sgx.ShuffleEngine(0, g, w, i) for g, w, i in variants]
+    # variant = chunks:waves:items[:ENV=VALUE] (the engine reads its A/B switches at creation)
+    variants, engines = [], []
+    for v in a.variants.split(","):
+        f = v.split(":")
+        g, w, i = (int(x) for x in f[:3])
+        env = dict(kv.split("=") for kv in f[3:])
+        old = {k: os.environ.get(k) for k in env}
+        os.environ.update(env)
+        engines.append(sgx.ShuffleEngine(0, g, w, i))
+        for k, o in old.items():
+            if o is None:
+                os.environ.pop(k)
+            else:
+                os.environ[k] = o
+        variants.append(v)
     n, R = a.records, a.partitions
     buf = engines[0].alloc(n * 16)
     if a.dist == "uniform":
@@ -62,7 +75,7 @@ def main():
                 res[vi][k].extend(per[k])
     out = []
     for vi, v in enumerate(variants):
-        row = {"variant(num_chunks:waves:items)": ":".join(map(str, v))}
+        row = {"variant(num_chunks:waves:items[:env])": v}
         for k, xs in res[vi].items():
             row[k + "_med"] = round(statistics.median(xs), 4)
             row[k + "_min"] = round(min(xs), 4)
