@@ -168,8 +168,11 @@ __device__ void block_exclusive_scan(const E *in, E *out, uint32_t R, uint32_t *
 constexpr int HIST_THREADS = 512;
 constexpr int HIST_UNROLL = 8;
 
-// grid = G * HIST_SPLIT: sub-block `sub` of chunk g counts records [begin + sub*sub_len, ...)
-// and adds its LDS histogram into counts[p][g] (zeroed by the launcher's memset).
+// grid = G * HIST_SPLIT: the HIST_SPLIT workgroups of chunk g walk it together, BACKWARD,
+// in steps of HIST_SPLIT * T * HIST_UNROLL records (sub-block `sub` takes its T * HIST_UNROLL
+// slice of each step), and add their LDS histograms into counts[p][g] (zeroed by the
+// launcher's memset).  Backward, so the last bytes this pass reads -- the ones still in
+// the 256 MiB Infinity Cache when K4 starts -- are the chunk heads K4 reads first.
 constexpr int HIST_SPLIT = 4;
 
 template <int KIND, bool REC16>
@@ -184,16 +187,16 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ 
     const int g = blockIdx.x / HIST_SPLIT, sub = blockIdx.x % HIST_SPLIT;
     const int64_t cbeg = (int64_t)g * chunk;
     const int64_t cend = min(n, cbeg + chunk);
-    const int64_t sub_len = (chunk + HIST_SPLIT - 1) / HIST_SPLIT;
-    const int64_t begin = min(cend, cbeg + (int64_t)sub * sub_len);
-    const int64_t end = min(cend, begin + sub_len);
-    for (int64_t base = begin; base < end; base += (int64_t)T * HIST_UNROLL) {
+    const int64_t slice = (int64_t)T * HIST_UNROLL, step = slice * HIST_SPLIT;
+    const int64_t nsteps = cend > cbeg ? (cend - cbeg + step - 1) / step : 0;
+    for (int64_t st = nsteps - 1; st >= 0; --st) {
+        const int64_t base = cbeg + st * step + sub * slice;
         uint32_t x[HIST_UNROLL], y[HIST_UNROLL], z[HIST_UNROLL];
 #pragma unroll
         for (int u = 0; u < HIST_UNROLL; ++u) {
             const int64_t i = base + (int64_t)u * T + tid;
             x[u] = y[u] = z[u] = 0;
-            if (i < end) {
+            if (i < cend) {
                 if constexpr (REC16) {
                     const uint4 r = ((const uint4 *)in)[i];
                     x[u] = r.x; y[u] = r.y; z[u] = r.z;
@@ -206,7 +209,7 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ 
 #pragma unroll
         for (int u = 0; u < HIST_UNROLL; ++u) {
             const int64_t i = base + (int64_t)u * T + tid;
-            if (i < end) atomicAdd(&hist[pid_of<KIND>(x[u], y[u], z[u], pp)], 1u);
+            if (i < cend) atomicAdd(&hist[pid_of<KIND>(x[u], y[u], z[u], pp)], 1u);
         }
     }
     __syncthreads();
@@ -1121,7 +1124,7 @@ ScatterGeom scatter_geom16_ord(uint32_t R, int force_waves, int force_items) {
 // (free between B1 and B3: every wave has drained the previous tile before B1).
 // ------------------------------------------------------------------------------------
 __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
-    return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 14;
+    return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 14;  // cur 4 + dlim 8 + dl 2
 }
 
 template <int KIND, int WAVES, int NI, int SI>
@@ -1134,18 +1137,19 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     constexpr int TNEW = T * NI;
     constexpr int STAGE = T * SI;
     constexpr uint32_t DCAP = (uint32_t)(STAGE - TNEW);
-    static_assert(SI > NI && SI <= 32, "deferred slots are tracked in a 32-bit mask");
+    static_assert(SI > NI && SI <= 32 && SI % 8 == 0, "deferred slots: 32-bit mask, drained 8 at a time");
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t R = pp.R, RS = rs8(R), NP = RS / 2;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     u32x4 *stage = (u32x4 *)smem;
     uint16_t *rows = (uint16_t *)(smem + (size_t)STAGE * 16);
     uint32_t *cur = (uint32_t *)(rows + (size_t)WAVES * RS);
-    uint32_t *dlt = cur + RS;
-    uint32_t *lim = dlt + RS;
-    uint16_t *dl = (uint16_t *)(lim + RS);
+    uint2 *dlim = (uint2 *)(cur + RS);          // {dlt_p, lim_p}: one ds_read_b64 per drained slot
+    uint16_t *dl = (uint16_t *)(dlim + RS);
     uint32_t *scratch = (uint32_t *)smem;  // merge only (B1..B3)
     uint16_t *myrow = rows + (size_t)w * RS;
+    uint32_t *myrow32 = (uint32_t *)myrow;
+    const uint32_t n32 = (uint32_t)n;  // n < 2^32 (sgx_write_map)
 
     const int g = blockIdx.x;
     const int64_t begin = (int64_t)g * chunk;
@@ -1177,20 +1181,17 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     uint32_t bad = 0;
     for (int64_t t = 0; t < ntiles; ++t) {
         const bool last = t == ntiles - 1;
-        // ---- rank the new records (stable: item-major, then lane, one LDS atomic each)
-        uint32_t pid[NI], rank[NI];
+        // ---- rank the new records: one LDS atomic each, issued back to back in item order
+        //      (a wave's LDS ops execute in issue order; lanes of one op in lane order), one
+        //      wait at the end.  An invalid item adds 0 (branch-free issue).
+        uint32_t pid[NI], old[NI];
 #pragma unroll
         for (int k = 0; k < NI; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
-            rank[k] = 0;
-            if (valid[k]) {
-                const uint32_t sh = (pid[k] & 1u) << 4;
-                const uint32_t old = __hip_atomic_fetch_add((uint32_t *)myrow + (pid[k] >> 1), 1u << sh,
-                                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                rank[k] = (old >> sh) & 0xFFFFu;
-            }
-            asm volatile("" ::: "memory");
+            const uint32_t inc = valid[k] ? 1u << ((pid[k] & 1u) << 4) : 0u;
+            old[k] = __hip_atomic_fetch_add(myrow32 + (pid[k] >> 1), inc, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         lds_barrier();  // B1
 
@@ -1238,83 +1239,72 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             const uint32_t e0 = c.x + t0, e1 = c.y + t1;
             const uint32_t a0 = c.x - dl0, a1 = c.y - dl1;
             const uint32_t le0 = flush ? e0 : e0 - dnf_lo, le1 = flush ? e1 : e1 - dnf_hi;
-            ((uint2 *)dlt)[j] = make_uint2(a0 - ls0, a1 - ls1);
-            ((uint2 *)lim)[j] = make_uint2(le0, le1);
+            // every position this tile writes is below lim <= e <= n by construction; a
+            // corrupt count is reported and clamped here, never per record
+            bad |= (e0 > n32 || e1 > n32) ? 1u : 0u;
+            ((u32x4 *)dlim)[j] = u32x4{a0 - ls0, min(le0, n32), a1 - ls1, min(le1, n32)};
             ((uint2 *)cur)[j] = make_uint2(e0, e1);
             ((uint32_t *)dl)[j] = (e0 - le0) | ((e1 - le1) << 16);
         }
         lds_barrier();  // B3
 
         // ---- stage: deferred records first (their slots follow from their positions), then
-        //      the new ones; zero this wave's counter row; prefetch the next tile
+        //      the new ones.  LDS reads of a phase are issued together, one wait each.
+        {
+            uint32_t dd[SI];
 #pragma unroll
-        for (int k = 0; k < SI; ++k) {
-            if ((dmask >> k) & 1u) {
-                const uint32_t p = pid_of<KIND>(dk[k].x, dk[k].y, dk[k].z, pp);
-                const uint32_t slot = dpos[k] - dlt[p];
-                if (slot < (uint32_t)STAGE) stage[slot] = dk[k];
-                else bad = 1;
-            }
-        }
+            for (int k = 0; k < SI; ++k) dd[k] = dlim[pid_of<KIND>(dk[k].x, dk[k].y, dk[k].z, pp)].x;
+            uint32_t rb[NI];
 #pragma unroll
-        for (int k = 0; k < NI; ++k) {
-            if (valid[k]) {
-                const uint32_t slot = (uint32_t)myrow[pid[k]] + rank[k];
-                if (slot < (uint32_t)STAGE) stage[slot] = rec[k];
-                else bad = 1;
+            for (int k = 0; k < NI; ++k) rb[k] = myrow[pid[k]];
+#pragma unroll
+            for (int k = 0; k < SI; ++k)
+                if ((dmask >> k) & 1u) stage[dpos[k] - dd[k]] = dk[k];
+#pragma unroll
+            for (int k = 0; k < NI; ++k) {
+                const uint32_t sh = (pid[k] & 1u) << 4;
+                if (valid[k]) stage[rb[k] + ((old[k] >> sh) & 0xFFFFu)] = rec[k];
             }
         }
         for (uint32_t i = lane; i < RS / 8; i += 64) ((u32x4 *)myrow)[i] = u32x4{0, 0, 0, 0};
         if (!last) {
             const int64_t nb = (t + 1) * TNEW;
-            const u32x4 *s2 = src + nb;
+            const u32x4 *cb = in + begin;
 #pragma unroll
             for (int k = 0; k < NI; ++k) {
-                valid[k] = nb + (int64_t)w * NI * 64 + k * 64 + lane < len;
-                rec[k] = valid[k] ? s2[k * 64] : u32x4{0, 0, 0, 0};
-                asm volatile("" ::: "memory");
+                const int64_t i = nb + (int64_t)w * NI * 64 + k * 64 + lane;
+                valid[k] = i < len;
+                rec[k] = cb[valid[k] ? i : 0];  // branch-free: an invalid item re-reads the chunk head
             }
         }
         lds_barrier();  // B4
 
-        // ---- drain: whole lines out, the rest back into registers
+        // ---- drain: whole lines out, the rest stays in this lane's registers (dk/dpos)
         dmask = 0;
 #pragma unroll
-        for (int k0 = 0; k0 < SI; k0 += 4) {
-            u32x4 r[4];
-            uint32_t pos[4];
-            bool live[4], wr[4];
+        for (int k0 = 0; k0 < SI; k0 += 8) {
+            uint2 dm[8];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < 8; ++q) {
                 const uint32_t s = (uint32_t)((k0 + q) * T + tid);
-                live[q] = s < total;
-                r[q] = live[q] ? stage[s] : u32x4{0, 0, 0, 0};
+                dk[k0 + q] = stage[s];  // slots past `total` hold stale records: never used
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint32_t s = (uint32_t)((k0 + q) * T + tid);
-                const uint32_t p = pid_of<KIND>(r[q].x, r[q].y, r[q].z, pp);
-                pos[q] = dlt[p] + s;
-                wr[q] = live[q] && pos[q] < lim[p];
-            }
+            for (int q = 0; q < 8; ++q) dm[q] = dlim[pid_of<KIND>(dk[k0 + q].x, dk[k0 + q].y, dk[k0 + q].z, pp)];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                if (wr[q]) {
-                    const bool ok = (int64_t)pos[q] < n;
-                    bad |= ok ? 0u : 1u;
-                    out[(size_t)(ok ? pos[q] : (uint32_t)(n - 1))] = r[q];
-                } else if (live[q]) {
-                    dk[k0 + q] = r[q];
-                    dpos[k0 + q] = pos[q];
-                    dmask |= 1u << (k0 + q);
-                }
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t s = (uint32_t)((k0 + q) * T + tid);
+                const bool live = s < total;
+                const uint32_t pos = dm[q].x + s;
+                dpos[k0 + q] = pos;
+                if (live && pos < dm[q].y) out[pos] = dk[k0 + q];
+                else if (live) dmask |= 1u << (k0 + q);
             }
         }
     }
     if (bad) atomicOr(err, SCATTER_OOB);
 }
 
-static_assert(16 % 4 == 0, "k_scatter16_wc drains in groups of 4 slots");
 
 // geometry: waves = WC_GEOM_BASE + 8, items = NI (new records per lane), mbits = SI
 ScatterGeom scatter_geom16_wc(uint32_t R) {
