@@ -113,7 +113,9 @@ int sgx_comm_init(sgx_engine *e, int32_t nranks, int32_t rank, const uint8_t id[
 int sgx_comm_size(sgx_engine *e, int32_t *nranks, int32_t *rank);
 /* Push map `map_id` of `shuffle_id` to the reducer owners (reducer r lives on rank
  * floor(r*P/R)); every rank calls it collectively with its own map.  Asynchronous on the
- * engine's exchange stream; completes at sgx_sync. */
+ * engine's exchange stream; completes at sgx_sync.  Received blocks stay in the
+ * all-to-all's receive layout ([source rank][reducer]); sgx_fetch_blocks gathers them in
+ * the order asked for (reducer-major, map-minor gives the canonical per-reducer sequence). */
 int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id);
 
 /* ---- ShuffleTransport.fetchBlocksByBlockIds (ucx/ShuffleTransport.scala:154-156) /
@@ -133,6 +135,7 @@ int sgx_sync(sgx_engine *e);
 
 /* ---- measurement: HIP-event times of the last write_map / exchange stages, and
  *      accumulated per-stage sums since the last reset (index = enum sgx_stage). ---- */
+/* SGX_STAGE_REGROUP times the fetch-side gather kernel (blocks into request order). */
 enum sgx_stage { SGX_STAGE_HIST = 0, SGX_STAGE_SCAN = 1, SGX_STAGE_SCATTER = 2,
                  SGX_STAGE_ALLGATHER = 3, SGX_STAGE_ALLTOALL = 4, SGX_STAGE_REGROUP = 5,
                  SGX_NUM_STAGES = 6 };

@@ -127,13 +127,16 @@ struct MapOut {
 };
 
 // One exchange round: every rank pushed one map; this rank holds its reducers' blocks.
+// The receive buffer keeps ncclAllToAllv's layout, [source rank][my reducers]: every
+// (map, reducer) block is contiguous in it, so blocks are served from it directly and the
+// per-reducer canonical order (reducer, then source map) is produced by the fetch that
+// asks for it (one gather launch), not by an extra pass over every received byte.
 struct Round {
     std::vector<int64_t> map_ids;        // [P] the map pushed by each source rank
     std::vector<int64_t> lens;           // [P][R] bytes
     std::vector<int64_t> block_off;      // [P][nmine] byte offset in `data`
-    std::vector<int64_t> items;          // regroup copy list (kept alive for the async H2D)
     int32_t r0 = 0, r1 = 0;              // my reducers [r0, r1)
-    DevBuf data;                          // regrouped: reducer-major, source-minor
+    DevBuf data;                          // receive buffer, [source][my reducers]
     const void *alias = nullptr;          // P == 1: the local map output itself
     hipEvent_t done = nullptr;
     const void *base() const { return alias ? alias : data.p; }
@@ -170,7 +173,8 @@ struct sgx_engine {
     hipStream_t s_comp = nullptr, s_comm = nullptr;
     // work buffers of the map-side pipeline
     DevBuf counts, offs, status, part_off_dev, input_stage;
-    DevBuf ag_send, ag_recv, recv, items_dev, chain_buf;
+    DevBuf ag_send, ag_recv, recv, items_dev, chain_buf, gather_stage;
+    HostPinned gather_items;
     HostPinned ag_host;
     std::map<int32_t, Shuffle> shuffles;
     // RCCL
@@ -285,9 +289,10 @@ extern "C" void sgx_destroy(sgx_engine *e) {
         kv.second.bounds.release();
     }
     for (DevBuf *b : {&e->counts, &e->offs, &e->status, &e->part_off_dev, &e->input_stage, &e->ag_send,
-                      &e->ag_recv, &e->recv, &e->items_dev, &e->chain_buf})
+                      &e->ag_recv, &e->recv, &e->items_dev, &e->chain_buf, &e->gather_stage})
         b->release();
     e->ag_host.release();
+    e->gather_items.release();
     for (hipEvent_t ev : e->ev_free) (void)hipEventDestroy(ev);
     if (e->comm) (void)ncclCommDestroy(e->comm);
     (void)hipStreamDestroy(e->s_comp);
@@ -880,25 +885,20 @@ extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
         rd->map_ids[(size_t)j] = agh[row * (size_t)(j + 1)];
         std::memcpy(&rd->lens[(size_t)j * R], agh + row * (size_t)(j + 1) + 1, sizeof(int64_t) * (size_t)R);
     }
-    // (2) plan
+    // (2) plan: send/recv counts and displacements (no copy list: blocks stay where they land)
     std::vector<int64_t> sc(P), sd(P), rc(P), rdp(P);
     int64_t nitems = 0;
-    SGX_TRY(sgx_plan_exchange(rd->lens.data(), P, R, e->rank, ITEM_BYTES, sc.data(), sd.data(), rc.data(),
-                              rdp.data(), nullptr, &nitems));
-    rd->items.assign((size_t)(nitems > 0 ? nitems : 1) * 3, 0);
-    int64_t cap = nitems;
-    SGX_TRY(sgx_plan_exchange(rd->lens.data(), P, R, e->rank, ITEM_BYTES, sc.data(), sd.data(), rc.data(),
-                              rdp.data(), rd->items.data(), &cap));
+    SGX_TRY(sgx_plan_exchange(rd->lens.data(), P, R, e->rank, 0, sc.data(), sd.data(), rc.data(), rdp.data(),
+                              nullptr, &nitems));
     int64_t total_recv = 0;
     for (int32_t j = 0; j < P; ++j) total_recv += rc[(size_t)j];
     rd->block_off.assign((size_t)P * nmine, 0);
-    {
-        int64_t off = 0;
-        for (int32_t r = rd->r0; r < rd->r1; ++r)
-            for (int32_t j = 0; j < P; ++j) {
-                rd->block_off[(size_t)j * nmine + (size_t)(r - rd->r0)] = off;
-                off += rd->lens[(size_t)j * R + r];
-            }
+    for (int32_t j = 0; j < P; ++j) {
+        int64_t off = rdp[(size_t)j];
+        for (int32_t r = rd->r0; r < rd->r1; ++r) {
+            rd->block_off[(size_t)j * nmine + (size_t)(r - rd->r0)] = off;
+            off += rd->lens[(size_t)j * R + r];
+        }
     }
     // A round with the same source maps replaces the previous one (a re-attempt): reuse
     // its HBM once every reader of it has finished.
@@ -911,8 +911,8 @@ extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
             break;
         }
     }
-    // (3) all-to-all of the partition-contiguous map output (already destination-grouped)
-    SGX_TRY(e->recv.ensure((size_t)total_recv));
+    // (3) all-to-all of the partition-contiguous map output (already destination-grouped,
+    //     reducer r lives on rank floor(r*P/R)): no pack step before, no regroup after
     SGX_TRY(rd->data.ensure((size_t)total_recv));
     HIP_TRY(hipStreamWaitEvent(st, m->done, 0));
     std::vector<size_t> scz(P), sdz(P), rcz(P), rdz(P);
@@ -923,23 +923,12 @@ extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
         rdz[(size_t)j] = (size_t)rdp[(size_t)j];
     }
     HIP_TRY(hipEventRecord(a2, st));
-    NCCL_TRY(ncclAllToAllv(m->data.p, scz.data(), sdz.data(), e->recv.p, rcz.data(), rdz.data(), ncclUint8,
+    NCCL_TRY(ncclAllToAllv(m->data.p, scz.data(), sdz.data(), rd->data.p, rcz.data(), rdz.data(), ncclUint8,
                            e->comm, st));
     HIP_TRY(hipEventRecord(a3, st));
-    // (4) regroup (src, reducer) -> (reducer, src)
-    SGX_TRY(e->items_dev.ensure((size_t)(nitems > 0 ? nitems : 1) * 24));
-    hipEvent_t a3b = e->ev(), a4 = e->ev();
-    HIP_TRY(hipEventRecord(a3b, st));
-    if (nitems > 0) {
-        HIP_TRY(hipMemcpyAsync(e->items_dev.p, rd->items.data(), (size_t)nitems * 24, hipMemcpyHostToDevice, st));
-        HIP_TRY(launch_copy_items(e->recv.p, rd->data.p, (const int64_t *)e->items_dev.p, nitems,
-                                  (s->rb % 16 == 0) ? 16 : 4, st));
-    }
-    HIP_TRY(hipEventRecord(a4, st));
     HIP_TRY(hipEventRecord(rd->done, st));
     record_stage(e, SGX_STAGE_ALLGATHER, a0, a1);
     record_stage(e, SGX_STAGE_ALLTOALL, a2, a3);
-    record_stage(e, SGX_STAGE_REGROUP, a3b, a4);
     s->rounds.push_back(std::move(rd));
     return SGX_OK;
 }
@@ -997,15 +986,49 @@ extern "C" int sgx_fetch_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t
     if (total > dst_cap)
         return fail(SGX_ERR_INVALID, "destination capacity %lld < %lld bytes", (long long)dst_cap, (long long)total);
     if (total > 0 && !dst) return fail(SGX_ERR_INVALID, "dst is NULL");
+    if (total == 0) return SGX_OK;
     hipStream_t st = e->s_comp;
-    hipMemcpyKind kind = dst_mem_kind == SGX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost;
-    int64_t off = 0;
+    // every source must be complete: wait on each distinct producer event once
+    std::vector<hipEvent_t> waited;
     for (int64_t i = 0; i < n; ++i) {
-        if (srcs[(size_t)i].ready) HIP_TRY(hipStreamWaitEvent(st, srcs[(size_t)i].ready, 0));
-        if (srcs[(size_t)i].len > 0)
-            HIP_TRY(hipMemcpyAsync((char *)dst + off, srcs[(size_t)i].p, (size_t)srcs[(size_t)i].len, kind, st));
+        hipEvent_t ev = srcs[(size_t)i].ready;
+        if (ev && std::find(waited.begin(), waited.end(), ev) == waited.end()) {
+            HIP_TRY(hipStreamWaitEvent(st, ev, 0));
+            waited.push_back(ev);
+        }
+    }
+    // one gather launch: {src, dst, bytes} pieces of <= 64 KiB, back to back in request
+    // order (the reader asks reducer-major, map-minor: the canonical per-reducer sequence)
+    const bool dev_dst = dst_mem_kind == SGX_MEM_DEVICE;
+    char *gdst = (char *)dst;
+    if (!dev_dst) {
+        SGX_TRY(e->gather_stage.ensure((size_t)total));
+        gdst = (char *)e->gather_stage.p;
+    }
+    int64_t npieces = 0;
+    for (int64_t i = 0; i < n; ++i) npieces += (srcs[(size_t)i].len + ITEM_BYTES - 1) / ITEM_BYTES;
+    SGX_TRY(e->gather_items.ensure((size_t)npieces * 24));
+    SGX_TRY(e->items_dev.ensure((size_t)npieces * 24));
+    int64_t *gi = (int64_t *)e->gather_items.p, k = 0, off = 0;
+    bool al16 = ((uintptr_t)gdst & 15) == 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const char *sp = (const char *)srcs[(size_t)i].p;
+        for (int64_t done = 0; done < srcs[(size_t)i].len; done += ITEM_BYTES, ++k) {
+            const int64_t b = std::min<int64_t>(ITEM_BYTES, srcs[(size_t)i].len - done);
+            gi[3 * k] = (int64_t)(uintptr_t)(sp + done);
+            gi[3 * k + 1] = (int64_t)(uintptr_t)(gdst + off + done);
+            gi[3 * k + 2] = b;
+            al16 = al16 && (((uintptr_t)(sp + done) | (uintptr_t)(off + done) | (uintptr_t)b) & 15) == 0;
+        }
         off += srcs[(size_t)i].len;
     }
+    hipEvent_t g0 = e->ev(), g1 = e->ev();
+    HIP_TRY(hipEventRecord(g0, st));
+    HIP_TRY(hipMemcpyAsync(e->items_dev.p, gi, (size_t)npieces * 24, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_gather_items((const int64_t *)e->items_dev.p, npieces, al16 ? 16 : 4, st));
+    HIP_TRY(hipEventRecord(g1, st));
+    record_stage(e, SGX_STAGE_REGROUP, g0, g1);
+    if (!dev_dst) HIP_TRY(hipMemcpyAsync(dst, gdst, (size_t)total, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     return SGX_OK;
 }

@@ -88,6 +88,8 @@ __host__ __device__ size_t scatter16_chain_lds(uint32_t R, int waves, int items,
 // items: [n][3] int64 {src_off, dst_off, bytes}; all offsets/bytes multiples of `align`.
 hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, int64_t n_items,
                              int align, hipStream_t stream);
+// items: [n][3] int64 {src address, dst address, bytes} (device memory on both sides).
+hipError_t launch_gather_items(const int64_t *items, int64_t n_items, int align, hipStream_t stream);
 hipError_t launch_gen_uniform16(void *dst, int64_t n, uint64_t seed, int64_t value_base,
                                 hipStream_t stream);
 hipError_t launch_gen_zipf16(void *dst, int64_t n, uint64_t seed, int64_t value_base,

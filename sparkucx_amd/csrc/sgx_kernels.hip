@@ -1989,6 +1989,33 @@ hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, i
     return hipGetLastError();
 }
 
+// Gather (fetchBlocksByBlockIds): items {src address, dst address, bytes}, one workgroup
+// per <= 64 KiB piece; ALIGN 16 when every address and size is 16-byte aligned, else 4
+// (blocks are whole records: 16 B or 100 B).
+template <int ALIGN>
+__global__ __launch_bounds__(256) void k_gather_items(const int64_t *__restrict__ items) {
+    const int64_t *it = items + 3 * (int64_t)blockIdx.x;
+    const int64_t bytes = it[2];
+    if constexpr (ALIGN == 16) {
+        const uint4 *s = (const uint4 *)(uintptr_t)it[0];
+        uint4 *d = (uint4 *)(uintptr_t)it[1];
+        for (int64_t i = threadIdx.x; i < (bytes >> 4); i += 256) d[i] = s[i];
+    } else {
+        const uint32_t *s = (const uint32_t *)(uintptr_t)it[0];
+        uint32_t *d = (uint32_t *)(uintptr_t)it[1];
+        for (int64_t i = threadIdx.x; i < (bytes >> 2); i += 256) d[i] = s[i];
+    }
+}
+
+hipError_t launch_gather_items(const int64_t *items, int64_t n_items, int align, hipStream_t stream) {
+    if (n_items <= 0) return hipSuccess;
+    if (align == 16)
+        hipLaunchKernelGGL(k_gather_items<16>, dim3((unsigned)n_items), dim3(256), 0, stream, items);
+    else
+        hipLaunchKernelGGL(k_gather_items<4>, dim3((unsigned)n_items), dim3(256), 0, stream, items);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------
 // Synthetic input generators (same definitions as oracle/shuffle_oracle.c).
 // ------------------------------------------------------------------------------------
