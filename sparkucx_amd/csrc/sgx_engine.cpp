@@ -170,6 +170,7 @@ struct sgx_engine {
     int nt = 0;                      // SGX_SCATTER_NT=1/2/3: nontemporal loads/stores; 4: double-buffered (A/B)
     int chain = 0;                   // SGX_SCATTER_CHAIN=WWII: chained look-back K4 (A/B)
     int wc = 1;                      // SGX_SCATTER_WC=0: no write-combining K4 (A/B)
+    int wc_diag = 0;                 // SGX_WC_DIAG=1..3: measurement-only ablation of the wc K4 (wrong output)
     hipStream_t s_comp = nullptr, s_comm = nullptr;
     // work buffers of the map-side pipeline
     DevBuf counts, offs, status, part_off_dev, input_stage;
@@ -260,6 +261,7 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     if (const char *d = getenv("SGX_RANK")) e->rank_match = std::strcmp(d, "match") == 0;
     if (const char *d = getenv("SGX_SCATTER_CHAIN")) e->chain = atoi(d);
     if (const char *d = getenv("SGX_SCATTER_WC")) e->wc = atoi(d);
+    if (const char *d = getenv("SGX_WC_DIAG")) e->wc_diag = atoi(d);
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
     *out = e.release();
@@ -458,7 +460,8 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
         if (o.items) geo = o;
         // write-combining K4 (whole 128 B lines only) where its LDS fits (R <= 1024)
         if (e->wc && e->sc_waves == 0 && e->sc_items == 0) {
-            const ScatterGeom w = scatter_geom16_wc((uint32_t)s.R);
+            ScatterGeom w = scatter_geom16_wc((uint32_t)s.R);
+            if (e->wc_diag >= 1 && e->wc_diag <= 3) w.nt = 100 + e->wc_diag;
             if (w.items) geo = w;
         }
     }

@@ -1127,7 +1127,9 @@ __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
     return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 14;  // cur 4 + dlim 8 + dl 2
 }
 
-template <int KIND, int WAVES, int NI, int SI>
+// DIAG (measurement-only builds, SGX_WC_DIAG; wrong output): 1 = no global stores,
+// 2 = no global loads after the first tile (the tile's registers are reused), 3 = both.
+template <int KIND, int WAVES, int NI, int SI, int DIAG = 0>
 __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__restrict__ in,
                                                                 u32x4 *__restrict__ out, int64_t n,
                                                                 int64_t chunk, PartParams pp,
@@ -1267,7 +1269,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             }
         }
         for (uint32_t i = lane; i < RS / 8; i += 64) ((u32x4 *)myrow)[i] = u32x4{0, 0, 0, 0};
-        if (!last) {
+        if (!last && (DIAG & 2) == 0) {
             const int64_t nb = (t + 1) * TNEW;
             const u32x4 *cb = in + begin;
 #pragma unroll
@@ -1297,8 +1299,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 const bool live = s < total;
                 const uint32_t pos = dm[q].x + s;
                 dpos[k0 + q] = pos;
-                if (live && pos < dm[q].y) out[pos] = dk[k0 + q];
-                else if (live) dmask |= 1u << (k0 + q);
+                if (live && pos < dm[q].y) {
+                    if constexpr ((DIAG & 1) == 0) out[pos] = dk[k0 + q];
+                    else asm volatile("" ::"v"(dk[k0 + q].x), "v"(dk[k0 + q].w), "v"(pos));
+                } else if (live) {
+                    dmask |= 1u << (k0 + q);
+                }
             }
         }
     }
@@ -1829,12 +1835,19 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
     }
     if (rb == 16 && geo.waves >= WC_GEOM_BASE) {
         if (pp.kind != SGX_PART_HASH || geo.waves != WC_GEOM_BASE + 8 || geo.mbits != 16) return hipErrorInvalidValue;
+#define SGX_WC1(K, NI, DG)                                                                       \
+    do {                                                                                         \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, 8, NI, 16, DG>,               \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
+        hipLaunchKernelGGL((k_scatter16_wc<K, 8, NI, 16, DG>), dim3(G), dim3(512), geo.lds_bytes, \
+                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err); \
+    } while (0)
 #define SGX_WC(K, NI)                                                                            \
     do {                                                                                         \
-        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, 8, NI, 16>,                   \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
-        hipLaunchKernelGGL((k_scatter16_wc<K, 8, NI, 16>), dim3(G), dim3(512), geo.lds_bytes,     \
-                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err); \
+        if (NI == 8 && geo.nt == 101) SGX_WC1(K, 8, 1);                                          \
+        else if (NI == 8 && geo.nt == 102) SGX_WC1(K, 8, 2);                                     \
+        else if (NI == 8 && geo.nt == 103) SGX_WC1(K, 8, 3);                                     \
+        else SGX_WC1(K, NI, 0);                                                                  \
     } while (0)
         const bool pow2 = (pp.R & (pp.R - 1)) == 0;
         if (geo.items == 12) {
@@ -1845,6 +1858,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
             return hipErrorInvalidValue;
         }
 #undef SGX_WC
+#undef SGX_WC1
         return hipGetLastError();
     }
     if (rb == 16 && geo.waves >= ORD_GEOM_BASE) {
