@@ -170,6 +170,7 @@ struct sgx_engine {
     int nt = 0;                      // SGX_SCATTER_NT=1/2/3: nontemporal loads/stores; 4: double-buffered (A/B)
     int chain = 0;                   // SGX_SCATTER_CHAIN=WWII: chained look-back K4 (A/B)
     int wc = 1;                      // SGX_SCATTER_WC=0: no write-combining K4 (A/B)
+    int wide2 = 1;                   // SGX_SCATTER_WIDE2=0: per-lane wide-record K4 (A/B)
     int wc_diag = 0;                 // SGX_WC_DIAG=1..3: measurement-only ablation of the wc K4 (wrong output)
     hipStream_t s_comp = nullptr, s_comm = nullptr;
     // work buffers of the map-side pipeline
@@ -261,6 +262,7 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     if (const char *d = getenv("SGX_RANK")) e->rank_match = std::strcmp(d, "match") == 0;
     if (const char *d = getenv("SGX_SCATTER_CHAIN")) e->chain = atoi(d);
     if (const char *d = getenv("SGX_SCATTER_WC")) e->wc = atoi(d);
+    if (const char *d = getenv("SGX_SCATTER_WIDE2")) e->wide2 = atoi(d);
     if (const char *d = getenv("SGX_WC_DIAG")) e->wc_diag = atoi(d);
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
@@ -464,6 +466,11 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
             if (e->wc_diag >= 1 && e->wc_diag <= 3) w.nt = 100 + e->wc_diag;
             if (w.items) geo = w;
         }
+    }
+    // wide records: the LDS-staged dword-stream kernel where it applies (16 B-aligned input)
+    if (rb != 16 && e->wide2 && ((uintptr_t)in & 15) == 0) {
+        const ScatterGeom w2 = scatter_geom_wide2((uint32_t)s.R, rb, s.kind, s.nb);
+        if (w2.items) geo = w2;
     }
     if (geo.items == 0)
         return fail(SGX_ERR_UNSUPPORTED, "no scatter geometry (waves %d, items %d) fits R=%d", e->sc_waves,

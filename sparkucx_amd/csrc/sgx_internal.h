@@ -64,6 +64,10 @@ inline bool is_direct_geom(int waves) { return waves >= DIRECT_GEOM_BASE && wave
 ScatterGeom scatter_geom16_direct(uint32_t R, int waves, int items);
 __host__ __device__ size_t scatter16_lds(uint32_t R, int waves, int items, int mbits);
 ScatterGeom scatter_geom_wide(uint32_t R, int record_bytes);
+// Wide-record staged kernel (100 B TeraSort records; waves == WIDE2_GEOM_TAG), items == 0
+// when it does not apply (R > 2048, other widths, LDS).
+constexpr int WIDE2_GEOM_TAG = -2;
+ScatterGeom scatter_geom_wide2(uint32_t R, int record_bytes, int kind, int nb);
 
 // Launchers (all asynchronous on `stream`).  counts / offs are [R][G] partition-major.
 hipError_t launch_hist(const void *in, int64_t n, int record_bytes, int64_t chunk, int G,

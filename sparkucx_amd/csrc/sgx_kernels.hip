@@ -51,9 +51,9 @@ __device__ __forceinline__ uint32_t hash_pid(uint32_t klo, uint32_t khi, const P
 // nonNegativeMod(h, R) == h & (R - 1) for two's-complement h.
 constexpr int KIND_HASH_POW2 = 100;
 
-__device__ __forceinline__ uint32_t range_pid_i64(int64_t key, const PartParams &pp) {
-    const int64_t *b = (const int64_t *)pp.bounds;
-    const int nb = pp.nb;
+// RangePartitioner.getPartition over bounds `b` (global memory, or an LDS copy).
+template <typename BP>
+__device__ __forceinline__ uint32_t range_pid_i64(int64_t key, BP b, int nb, int ascending) {
     int p = 0;
     if (nb <= 128) {
         while (p < nb && key > b[p]) ++p;
@@ -70,16 +70,15 @@ __device__ __forceinline__ uint32_t range_pid_i64(int64_t key, const PartParams 
         if (!found) p = low;
         if (p > nb) p = nb;
     }
-    return (uint32_t)(pp.ascending ? p : nb - p);
+    return (uint32_t)(ascending ? p : nb - p);
 }
 
 __device__ __forceinline__ bool k10_lt(uint64_t ahi, uint32_t alo, uint64_t bhi, uint32_t blo) {
     return ahi < bhi || (ahi == bhi && alo < blo);
 }
 
-__device__ __forceinline__ uint32_t range_pid_k10(uint64_t khi, uint32_t klo, const PartParams &pp) {
-    const Key10 *b = (const Key10 *)pp.bounds;
-    const int nb = pp.nb;
+template <typename BP>
+__device__ __forceinline__ uint32_t range_pid_k10(uint64_t khi, uint32_t klo, BP b, int nb, int ascending) {
     int p = 0;
     if (nb <= 128) {
         while (p < nb && k10_lt(b[p].hi, b[p].lo, khi, klo)) ++p;
@@ -88,31 +87,39 @@ __device__ __forceinline__ uint32_t range_pid_k10(uint64_t khi, uint32_t klo, co
         bool found = false;
         while (low <= high) {
             const int mid = (int)(((unsigned)low + (unsigned)high) >> 1);
-            const Key10 mv = b[mid];
-            if (k10_lt(mv.hi, mv.lo, khi, klo)) low = mid + 1;
-            else if (k10_lt(khi, klo, mv.hi, mv.lo)) high = mid - 1;
+            const uint64_t mhi = b[mid].hi;
+            const uint32_t mlo = b[mid].lo;
+            if (k10_lt(mhi, mlo, khi, klo)) low = mid + 1;
+            else if (k10_lt(khi, klo, mhi, mlo)) high = mid - 1;
             else { p = mid; found = true; break; }
         }
         if (!found) p = low;
         if (p > nb) p = nb;
     }
-    return (uint32_t)(pp.ascending ? p : nb - p);
+    return (uint32_t)(ascending ? p : nb - p);
 }
 
-// Partition id from the first 12 bytes of a record (x, y, z little-endian dwords).
-template <int KIND>
-__device__ __forceinline__ uint32_t pid_of(uint32_t x, uint32_t y, uint32_t z, const PartParams &pp) {
+// Partition id from the first 12 bytes of a record (x, y, z little-endian dwords), range
+// bounds read through `bounds` (pp.bounds in global memory, or a copy in LDS).
+template <int KIND, typename BI64 = const int64_t *, typename BK10 = const Key10 *>
+__device__ __forceinline__ uint32_t pid_of_b(uint32_t x, uint32_t y, uint32_t z, const PartParams &pp,
+                                             BI64 bi64, BK10 bk10) {
     if constexpr (KIND == SGX_PART_HASH) {
         return hash_pid(x, y, pp);
     } else if constexpr (KIND == KIND_HASH_POW2) {
         return (x ^ y) & (pp.R - 1u);
     } else if constexpr (KIND == SGX_PART_RANGE_I64) {
-        return range_pid_i64((int64_t)(((uint64_t)y << 32) | x), pp);
+        return range_pid_i64((int64_t)(((uint64_t)y << 32) | x), bi64, pp.nb, pp.ascending);
     } else {
         const uint64_t hi = ((uint64_t)__builtin_bswap32(x) << 32) | __builtin_bswap32(y);
         const uint32_t lo = __builtin_bswap32(z) >> 16;
-        return range_pid_k10(hi, lo, pp);
+        return range_pid_k10(hi, lo, bk10, pp.nb, pp.ascending);
     }
+}
+
+template <int KIND>
+__device__ __forceinline__ uint32_t pid_of(uint32_t x, uint32_t y, uint32_t z, const PartParams &pp) {
+    return pid_of_b<KIND>(x, y, z, pp, (const int64_t *)pp.bounds, (const Key10 *)pp.bounds);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1801,6 +1808,193 @@ __global__ __launch_bounds__(WIDE_THREADS, 1) void k_scatter_wide(const char *__
     }
 }
 
+// ------------------------------------------------------------------------------------
+// K4 for wide records (TeraSort 100 B): the tile's bytes are staged in LDS by coalesced
+// 16 B loads (issued one tile ahead into registers, so they fly during the whole previous
+// tile), the records are ranked exactly like the 16 B kernels (one LDS atomic per record,
+// lane-ordered, per-wave rows merged in wave order), a partition-sorted index of the tile
+// is built in LDS, and the drain streams the tile out as DWORDS in sorted order: thread t
+// moves dword d = t, t + T, ... of the sorted tile, so every partition run leaves the CU
+// as consecutive lanes.  Range bounds (RangePartitioner) are copied to LDS once.
+// LDS: stage[TR * RB] | bounds[nb] | rows[W][RS] u16 | cur[RS] u32 | dlt[RS] u32 | idx[TR] u32
+// ------------------------------------------------------------------------------------
+constexpr int WIDE2_TR = 1024;
+
+__host__ __device__ size_t scatter_wide2_lds(uint32_t R, int rb, int kind, int nb) {
+    const size_t bsz = kind == SGX_PART_RANGE_BYTES10 ? sizeof(Key10) : 8;
+    return al16((size_t)WIDE2_TR * rb) + (kind == SGX_PART_HASH ? 0 : al16((size_t)nb * bsz)) +
+           (size_t)8 * rs8(R) * 2 + (size_t)rs8(R) * 8 + (size_t)WIDE2_TR * 4 + 64 * 4;
+}
+
+template <int KIND, int RB>
+__global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restrict__ in, uint32_t *__restrict__ out,
+                                                          int64_t n, int64_t chunk, PartParams pp,
+                                                          const uint32_t *__restrict__ offs, int G,
+                                                          uint32_t *err) {
+    constexpr int T = 512, W = 8, TR = WIDE2_TR, ITEMS = TR / T;  // 2 records per lane
+    constexpr int DW = RB / 4;                                     // dwords per record
+    constexpr int NCH = TR * RB / 16;                              // 16 B chunks per full tile
+    constexpr int LD = (NCH + T - 1) / T;
+    static_assert(RB % 16 == 4 || RB % 16 == 8 || RB % 16 == 12 || RB % 16 == 0, "RB multiple of 4");
+    static_assert((TR * RB) % 16 == 0, "tiles start 16 B aligned");
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint32_t R = pp.R, RS = rs8(R), NP = RS / 2;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    char *sp = smem;
+    uint32_t *stage = (uint32_t *)sp;
+    sp += al16((size_t)TR * RB);
+    const Key10 *bk10 = (const Key10 *)sp;
+    const int64_t *bi64 = (const int64_t *)sp;
+    if constexpr (KIND == SGX_PART_RANGE_BYTES10) {
+        for (int i = tid; i < pp.nb; i += T) ((Key10 *)sp)[i] = ((const Key10 *)pp.bounds)[i];
+        sp += al16((size_t)pp.nb * sizeof(Key10));
+    } else if constexpr (KIND == SGX_PART_RANGE_I64) {
+        for (int i = tid; i < pp.nb; i += T) ((int64_t *)sp)[i] = ((const int64_t *)pp.bounds)[i];
+        sp += al16((size_t)pp.nb * 8);
+    }
+    uint16_t *rows = (uint16_t *)sp;
+    uint32_t *cur = (uint32_t *)(rows + (size_t)W * RS);
+    uint32_t *dlt = cur + RS;
+    uint32_t *idx = dlt + RS;
+    uint32_t *scratch = idx + TR;
+    uint16_t *myrow = rows + (size_t)w * RS;
+    uint32_t *myrow32 = (uint32_t *)myrow;
+
+    const int g = blockIdx.x;
+    const int64_t begin = (int64_t)g * chunk;
+    const int64_t end = min(n, begin + chunk);
+    const int64_t len = end > begin ? end - begin : 0;
+    // tile counts in 32 bits, the last tile's size computed once: a 64-bit min() of the
+    // per-tile remainder was mis-selected by the compiler (s_cselect on a stale SCC)
+    const int ntiles = (int)((len + TR - 1) / TR);
+    const int lastn = ntiles > 0 ? (int)(len - (int64_t)(ntiles - 1) * TR) : 0;
+    for (uint32_t p = tid; p < RS; p += T) cur[p] = p < R ? offs[(int64_t)p * G + g] : 0u;
+    for (uint32_t i = tid; i < (uint32_t)W * RS / 2; i += T) ((uint32_t *)rows)[i] = 0u;
+
+    // tile loads: 16 B chunks of a full tile; the input's last (partial) tile goes dword-wise
+    u32x4 ld[LD];
+    auto issue = [&](int t) {
+        const u32x4 *tb = (const u32x4 *)((const char *)in + (begin + (int64_t)t * TR) * RB);
+        const int nrec = t + 1 < ntiles ? TR : lastn;
+        const int nch = nrec == TR ? NCH : 0;  // partial tiles are loaded dword-wise below
+#pragma unroll
+        for (int i = 0; i < LD; ++i) {
+            const int c = i * T + tid;
+            ld[i] = c < nch ? tb[c] : u32x4{0, 0, 0, 0};
+        }
+    };
+    if (ntiles > 0) issue(0);
+    uint32_t bad = 0;
+    for (int t = 0; t < ntiles; ++t) {
+        const int nrec = t + 1 < ntiles ? TR : lastn;
+        // ---- land the tile in LDS (the previous drain finished at the last barrier)
+        if (nrec == TR) {
+#pragma unroll
+            for (int i = 0; i < LD; ++i) {
+                const int c = i * T + tid;
+                if (c < NCH) ((u32x4 *)stage)[c] = ld[i];
+            }
+        } else {
+            const uint32_t *tb = (const uint32_t *)((const char *)in + (begin + (int64_t)t * TR) * RB);
+            for (int d = tid; d < nrec * DW; d += T) stage[d] = tb[d];
+        }
+        __syncthreads();
+        if (t + 1 < ntiles) issue(t + 1);  // in flight during this whole tile
+        // ---- partition ids + rank (records w*128 + k*64 + lane: input order = (wave, item, lane))
+        uint32_t pid[ITEMS], old[ITEMS];
+        bool valid[ITEMS];
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint32_t r = w * (TR / W) + k * 64 + lane;
+            valid[k] = r < (uint32_t)nrec;
+            const uint32_t *rp = stage + (valid[k] ? r : 0) * DW;
+            pid[k] = valid[k] ? pid_of_b<KIND>(rp[0], rp[1], rp[2], pp, bi64, bk10) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint32_t inc = valid[k] ? 1u << ((pid[k] & 1u) << 4) : 0u;
+            old[k] = __hip_atomic_fetch_add(myrow32 + (pid[k] >> 1), inc, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        lds_barrier();
+        // ---- merge: per partition pair, prefix over the wave rows, block scan
+        constexpr int PPM = 2;  // pairs per thread (R <= 2048)
+        uint32_t before[PPM][W], tot[PPM], S = 0;
+#pragma unroll
+        for (int i = 0; i < PPM; ++i) {
+            const uint32_t j = tid * PPM + i;
+            tot[i] = 0;
+            if (j < NP) {
+#pragma unroll
+                for (int v = 0; v < W; ++v) {
+                    before[i][v] = tot[i];
+                    tot[i] += ((const uint32_t *)(rows + (size_t)v * RS))[j];
+                }
+            }
+            S += (tot[i] & 0xFFFFu) + (tot[i] >> 16);
+        }
+        const uint32_t xs = wave_inclusive_scan(S, lane);
+        if (lane == 63) scratch[w] = xs;
+        lds_barrier();
+        uint32_t base = xs - S;
+        for (uint32_t v = 0; v < w; ++v) base += scratch[v];
+#pragma unroll
+        for (int i = 0; i < PPM; ++i) {
+            const uint32_t j = tid * PPM + i;
+            if (j < NP) {
+                const uint32_t lo = base, hi = base + (tot[i] & 0xFFFFu);
+                base = hi + (tot[i] >> 16);
+                const uint32_t L = lo | (hi << 16);
+#pragma unroll
+                for (int v = 0; v < W; ++v) ((uint32_t *)(rows + (size_t)v * RS))[j] = before[i][v] + L;
+                const uint2 c = ((const uint2 *)cur)[j];
+                ((uint2 *)dlt)[j] = make_uint2(c.x - lo, c.y - hi);
+                ((uint2 *)cur)[j] = make_uint2(c.x + (tot[i] & 0xFFFFu), c.y + (tot[i] >> 16));
+                bad |= (c.x + (tot[i] & 0xFFFFu) > (uint32_t)n || c.y + (tot[i] >> 16) > (uint32_t)n) ? 1u : 0u;
+            }
+        }
+        lds_barrier();
+        // ---- sorted index of the tile: idx[slot] = source record | partition << 16
+#pragma unroll
+        for (int k = 0; k < ITEMS; ++k) {
+            const uint32_t sh = (pid[k] & 1u) << 4;
+            const uint32_t rb16 = myrow[pid[k]];
+            if (valid[k]) idx[rb16 + ((old[k] >> sh) & 0xFFFFu)] = (w * (TR / W) + k * 64 + lane) | (pid[k] << 16);
+        }
+        for (uint32_t i = lane; i < RS / 8; i += 64) ((u32x4 *)myrow)[i] = u32x4{0, 0, 0, 0};
+        lds_barrier();
+        // ---- drain: the sorted tile as a dword stream, consecutive lanes -> consecutive dwords
+        const int total = (int)nrec * DW;
+        for (int d0 = 0; d0 < total; d0 += 8 * T) {
+            uint32_t v[8], dst[8], wi[8];
+            bool live[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const int d = d0 + q * T + (int)tid;
+                live[q] = d < total;
+                const uint32_t dd = live[q] ? (uint32_t)d : 0u;
+                const uint32_t s = dd / DW;
+                wi[q] = dd - s * DW;
+                const uint32_t e = idx[s];
+                v[q] = stage[(e & 0xFFFFu) * DW + wi[q]];
+                dst[q] = dlt[e >> 16] + s;
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if (live[q] && dst[q] < (uint32_t)n) out[(uint64_t)dst[q] * DW + wi[q]] = v[q];
+        }
+        __syncthreads();  // stage / idx reused by the next tile
+    }
+    if (bad) atomicOr(err, SCATTER_OOB);
+}
+
+ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
+    if (rb != 100 || rs8(R) / 2 > 2u * 512u) return ScatterGeom{0, 0, 0, 0, 0};
+    const size_t lds = scatter_wide2_lds(R, rb, kind, nb);
+    if (lds > LDS_MAX) return ScatterGeom{0, 0, 0, 0, 0};
+    return ScatterGeom{WIDE2_GEOM_TAG, 2, WIDE2_TR, lds, 0};
+}
+
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t chunk, int G,
                           const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
                           uint32_t *err, hipStream_t stream) {
@@ -1947,6 +2141,23 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
 #undef SGX_SC16_K
 #undef SGX_SC16NT
 #undef SGX_SC16
+    } else if (rb == 100 && geo.waves == WIDE2_GEOM_TAG) {
+        if (((uintptr_t)in & 15) != 0) return hipErrorInvalidValue;
+#define SGX_W2(K)                                                                                \
+    do {                                                                                         \
+        (void)hipFuncSetAttribute((const void *)k_scatter_wide2<K, 100>,                        \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
+        hipLaunchKernelGGL((k_scatter_wide2<K, 100>), dim3(G), dim3(512), geo.lds_bytes, stream,  \
+                           (const u32x4 *)in, (uint32_t *)out, n, chunk, pp, offs, G, err);     \
+    } while (0)
+        switch (pp.kind) {
+        case SGX_PART_HASH:
+            if ((pp.R & (pp.R - 1)) == 0) SGX_W2(KIND_HASH_POW2); else SGX_W2(SGX_PART_HASH);
+            break;
+        case SGX_PART_RANGE_I64: SGX_W2(SGX_PART_RANGE_I64); break;
+        default: SGX_W2(SGX_PART_RANGE_BYTES10); break;
+        }
+#undef SGX_W2
     } else {
         if (geo.items == 0 || (rb & 3) != 0 || rb < 12) return hipErrorInvalidValue;
         const char *ic = (const char *)in;

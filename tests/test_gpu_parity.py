@@ -230,6 +230,25 @@ def test_terasort_bytes10(engine, oracle_lib, nb):
     check_against_oracle(engine, oracle_lib, recs, nb + 1, sgx.PART_RANGE_BYTES10, bounds)
 
 
+@pytest.mark.parametrize("wide2", ["1", "0"])
+@pytest.mark.parametrize("R", [1, 7, 1000, 2048, 4096])
+@pytest.mark.parametrize("n", [1, 1023, 1024, 5 * 1024 + 77])
+def test_wide_records_every_path(sgx_lib, oracle_lib, monkeypatch, wide2, R, n):
+    """100 B records: the LDS-staged dword-stream K4 (R <= 2048) and the per-lane kernel
+    (SGX_SCATTER_WIDE2=0, and R = 4096), hash and range partitioners, partial tiles and
+    several chunks."""
+    monkeypatch.setenv("SGX_SCATTER_WIDE2", wide2)
+    recs = oracle_lib.gen_terasort100(n, R + n)
+    with sgx_lib.ShuffleEngine(device=0, num_chunks=3) as e:
+        check_against_oracle(e, oracle_lib, recs, R)
+        if R > 1:
+            rng = np.random.default_rng(R)
+            sample = recs[rng.choice(n, min(n, 8 * R), replace=n < 8 * R), :10]
+            sample = sample[np.lexsort(sample.T[::-1])]
+            bounds = np.ascontiguousarray(sample[np.linspace(0, len(sample) - 1, R - 1).astype(int)])
+            check_against_oracle(e, oracle_lib, recs, R, sgx_lib.PART_RANGE_BYTES10, bounds)
+
+
 def test_hash_on_wide_records(engine, oracle_lib):
     recs = oracle_lib.gen_terasort100(30_000, 4)
     check_against_oracle(engine, oracle_lib, recs, 1024)
