@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 METRIC = "shuffled GB/s (partition+exchange) at 1/2/4/8 GPUs; % of HBM/xGMI roofline"
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md: HBM3E 8 TB/s spec
 ALGO_BYTES_PER_REC = 32    # 16 B read + 16 B write per record
+XGMI_LINK_GBS = 153.0      # per directed link; one link per GPU pair
 
 
 def parse():
@@ -154,9 +155,25 @@ def main():
     st = eng.stats()
 
     verified = None
+    lens = eng.map_lengths(sid, rank, R)
     if not args.no_verify:
-        lens = eng.map_lengths(sid, rank, R)
         verified = bool(lens.sum() == 16 * n)
+    xgmi = None
+    if world > 1:
+        # bytes this rank's map sends over xGMI (reducer r lives on rank floor(r*P/R))
+        owner = (np.arange(R, dtype=np.int64) * world) // R
+        sent = float(lens[owner != rank].sum())
+        a2a_ms = st.ms["alltoall"] / max(1, st.count["alltoall"])
+        t = torch.tensor([sent, a2a_ms], dtype=torch.float64)
+        tmax = t.clone()
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        peak = XGMI_LINK_GBS * world * (world - 1)
+        ach = float(t[0]) / (float(tmax[1]) * 1e-3) / 1e9
+        xgmi = {"bound": "xgmi", "achieved": round(ach, 1), "peak": peak, "unit": "GB/s",
+                "frac": round(ach / peak, 4), "bytes_per_step": float(t[0]),
+                "alltoall_ms_max_rank": round(float(tmax[1]), 4),
+                "note": "all ranks' cross-GPU bytes / slowest rank's ncclAllToAllv time; peak = P(P-1) x 153 GB/s"}
 
     if rank == 0:
         ms_per_step = dt * 1e3 / args.steps
@@ -183,6 +200,8 @@ def main():
                                                              / max(1, st.count["scatter"]) * 1e-3) / 1e9, 1),
             "verified_lengths_sum": verified,
         }
+        if xgmi is not None:
+            out["xgmi_roofline"] = xgmi
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, n)
         elif world == 1:

@@ -124,6 +124,7 @@ struct MapOut {
     std::vector<int64_t> lengths;  // bytes per partition (valid once `ready`)
     bool ready = false;
     hipEvent_t done = nullptr;  // recorded on the compute stream after the scatter
+    hipEvent_t read_done = nullptr;  // recorded on the exchange stream after the all-to-all read `data`
 };
 
 // One exchange round: every rank pushed one map; this rank holds its reducers' blocks.
@@ -271,6 +272,9 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
 }
 
 static void free_map(MapOut &m) {
+    if (m.read_done) (void)hipEventSynchronize(m.read_done);  // an all-to-all may still read `data`
+    if (m.read_done) (void)hipEventDestroy(m.read_done);
+    m.read_done = nullptr;
     m.data.release();
     m.part_off.release();
     if (m.done) (void)hipEventDestroy(m.done);
@@ -425,6 +429,8 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
     // A re-attempt of the same map replaces the previous output (the in-HBM analogue of the
     // index commit; the file commit keeps "first valid attempt wins", sgx_write_index).
     if (m.done) HIP_TRY(hipEventSynchronize(m.done));
+    // ... and must not overwrite the previous output while an exchange still sends it
+    if (m.read_done) HIP_TRY(hipStreamWaitEvent(st, m.read_done, 0));
     m.ready = false;
     m.nrec = n;
     m.bytes = n * rb;
@@ -937,6 +943,8 @@ extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
                            e->comm, st));
     HIP_TRY(hipEventRecord(a3, st));
     HIP_TRY(hipEventRecord(rd->done, st));
+    if (!m->read_done) HIP_TRY(hipEventCreateWithFlags(&m->read_done, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(m->read_done, st));
     record_stage(e, SGX_STAGE_ALLGATHER, a0, a1);
     record_stage(e, SGX_STAGE_ALLTOALL, a2, a3);
     s->rounds.push_back(std::move(rd));
