@@ -175,7 +175,16 @@ struct sgx_engine {
     int wc_diag = 0;                 // SGX_WC_DIAG=1..3: measurement-only ablation of the wc K4 (wrong output)
     hipStream_t s_comp = nullptr, s_comm = nullptr;
     // work buffers of the map-side pipeline
-    DevBuf counts, offs, status, part_off_dev, input_stage;
+    // map-side work buffers, a ring of two: with SGX_PIPELINE the next map's histogram +
+    // scan (on s_hist) fill one set while the previous map's scatter (on s_comp) reads the other
+    struct WorkSet {
+        DevBuf counts, offs, status, part_off_dev;
+        hipEvent_t used = nullptr;  // recorded on s_comp after the scatter that read this set
+    } ws[2];
+    int ws_next = 0;
+    int pipeline = 0;                // SGX_PIPELINE=1: hist+scan of map k+1 overlap map k's scatter
+    hipStream_t s_hist = nullptr;
+    DevBuf input_stage, junk;
     DevBuf ag_send, ag_recv, recv, items_dev, chain_buf, gather_stage;
     HostPinned gather_items;
     HostPinned ag_host;
@@ -267,6 +276,8 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     if (const char *d = getenv("SGX_WC_DIAG")) e->wc_diag = atoi(d);
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comp, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&e->s_hist, hipStreamNonBlocking));
+    if (const char *d = getenv("SGX_PIPELINE")) e->pipeline = atoi(d);
     *out = e.release();
     return SGX_OK;
 }
@@ -296,7 +307,12 @@ extern "C" void sgx_destroy(sgx_engine *e) {
         for (auto &r : kv.second.rounds) free_round(*r);
         kv.second.bounds.release();
     }
-    for (DevBuf *b : {&e->counts, &e->offs, &e->status, &e->part_off_dev, &e->input_stage, &e->ag_send,
+    for (auto &w : e->ws) {
+        for (DevBuf *b : {&w.counts, &w.offs, &w.status, &w.part_off_dev}) b->release();
+        if (w.used) (void)hipEventDestroy(w.used);
+        w.used = nullptr;
+    }
+    for (DevBuf *b : {&e->junk, &e->input_stage, &e->ag_send,
                       &e->ag_recv, &e->recv, &e->items_dev, &e->chain_buf, &e->gather_stage})
         b->release();
     e->ag_host.release();
@@ -305,6 +321,7 @@ extern "C" void sgx_destroy(sgx_engine *e) {
     if (e->comm) (void)ncclCommDestroy(e->comm);
     (void)hipStreamDestroy(e->s_comp);
     (void)hipStreamDestroy(e->s_comm);
+    (void)hipStreamDestroy(e->s_hist);
     delete e;
 }
 
@@ -469,7 +486,7 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
         // write-combining K4 (whole 128 B lines only) where its LDS fits (R <= 1024)
         if (e->wc && e->sc_waves == 0 && e->sc_items == 0) {
             ScatterGeom w = scatter_geom16_wc((uint32_t)s.R);
-            if (e->wc_diag >= 1 && e->wc_diag <= 3) w.nt = 100 + e->wc_diag;
+            if ((e->wc_diag >= 1 && e->wc_diag <= 4) || e->wc_diag == 8) w.nt = 100 + e->wc_diag;
             if (w.items) geo = w;
         }
     }
@@ -495,29 +512,38 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
     const int G = n > 0 ? (int)((n + chunk - 1) / chunk) : 1;
     const int64_t len = (int64_t)s.R * G;
     const int64_t tiles = scan_tiles(len);
-    SGX_TRY(e->counts.ensure((size_t)len * 4));
-    SGX_TRY(e->offs.ensure((size_t)len * 4));
-    SGX_TRY(e->status.ensure((size_t)(16 + tiles * 8)));
-    SGX_TRY(e->part_off_dev.ensure((size_t)(s.R + 2) * 4));
-    uint32_t *ticket_err = (uint32_t *)e->status.p;
-    uint64_t *status = (uint64_t *)((char *)e->status.p + 16);
-    HIP_TRY(hipMemsetAsync(e->status.p, 0, (size_t)(16 + tiles * 8), st));
+    // the pipelined map side: device input, and the write-combining K4 it was sized for
+    const bool pipe = e->pipeline && mem_kind == SGX_MEM_DEVICE && rb == 16 && geo.waves >= WC_GEOM_BASE &&
+                      e->diag == 0 && e->chain == 0;
+    auto &W = e->ws[pipe ? (e->ws_next ^= 1) : 0];
+    hipStream_t sh = pipe ? e->s_hist : st;
+    if (pipe && W.used) HIP_TRY(hipStreamWaitEvent(sh, W.used, 0));  // its last reader (K4) is done
+    SGX_TRY(W.counts.ensure((size_t)len * 4));
+    SGX_TRY(W.offs.ensure((size_t)len * 4));
+    SGX_TRY(W.status.ensure((size_t)(16 + tiles * 8)));
+    SGX_TRY(W.part_off_dev.ensure((size_t)(s.R + 2) * 4));
+    uint32_t *ticket_err = (uint32_t *)W.status.p;
+    uint64_t *status = (uint64_t *)((char *)W.status.p + 16);
+    HIP_TRY(hipMemsetAsync(W.status.p, 0, (size_t)(16 + tiles * 8), sh));
 
     // one event pair per stage: an event is owned by exactly one pending record
     hipEvent_t h0 = e->ev(), h1 = e->ev(), c0 = e->ev(), c1 = e->ev(), x0 = e->ev(), x1 = e->ev();
-    HIP_TRY(hipEventRecord(h0, st));
+    HIP_TRY(hipEventRecord(h0, sh));
     if (n > 0) {
-        HIP_TRY(launch_hist(in, n, rb, chunk, G, s.pp, (uint32_t *)e->counts.p, st));
+        HIP_TRY(launch_hist(in, n, rb, chunk, G, s.pp, (uint32_t *)W.counts.p, sh, pipe));
     } else {
-        HIP_TRY(hipMemsetAsync(e->counts.p, 0, (size_t)len * 4, st));
+        HIP_TRY(hipMemsetAsync(W.counts.p, 0, (size_t)len * 4, sh));
     }
-    HIP_TRY(hipEventRecord(h1, st));
-    HIP_TRY(hipEventRecord(c0, st));
-    HIP_TRY(launch_scan((const uint32_t *)e->counts.p, (uint32_t *)e->offs.p, len, status, ticket_err,
-                        (uint32_t *)e->part_off_dev.p, G, s.R, st));
-    HIP_TRY(hipEventRecord(c1, st));
+    HIP_TRY(hipEventRecord(h1, sh));
+    HIP_TRY(hipEventRecord(c0, sh));
+    HIP_TRY(launch_scan((const uint32_t *)W.counts.p, (uint32_t *)W.offs.p, len, status, ticket_err,
+                        (uint32_t *)W.part_off_dev.p, G, s.R, sh));
+    HIP_TRY(hipEventRecord(c1, sh));
+    if (pipe) HIP_TRY(hipStreamWaitEvent(st, c1, 0));
     HIP_TRY(hipEventRecord(x0, st));
     PartParams lpp = s.pp;
+    SGX_TRY(e->junk.ensure((size_t)G * JUNK_BYTES_PER_WG));
+    lpp.junk = e->junk.p;
     lpp.mbits = e->no_table ? 0u : (uint32_t)geo.mbits;
     if (e->diag > 0) lpp.mbits = e->no_table ? 0u : (uint32_t)scatter_geom16((uint32_t)s.R, 8, 16).mbits;
     const int cw = e->chain / 100, ci = e->chain % 100;
@@ -536,20 +562,24 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
         int occ = (int)((160 * 1024) / scatter16_chain_lds((uint32_t)s.R, cw, ci, mb));
         if (occ > 32 / cw) occ = 32 / cw;
         if (occ < 1) occ = 1;
-        HIP_TRY(launch_scatter_chain(in, m.data.p, n, cpp, (const uint32_t *)e->part_off_dev.p,
+        HIP_TRY(launch_scatter_chain(in, m.data.p, n, cpp, (const uint32_t *)W.part_off_dev.p,
                                      (uint32_t *)((char *)e->chain_buf.p + 16), (uint32_t *)e->chain_buf.p,
                                      ticket_err + 1, cw, ci, e->num_cus * occ, st));
     } else if (n > 0) {
         if (e->diag > 0 && rb == 16 && s.kind == SGX_PART_HASH)  // measurement-only ablation
-            HIP_TRY(launch_scatter_diag(e->diag, in, m.data.p, n, chunk, G, lpp, (const uint32_t *)e->offs.p, ticket_err + 1, st));
+            HIP_TRY(launch_scatter_diag(e->diag, in, m.data.p, n, chunk, G, lpp, (const uint32_t *)W.offs.p, ticket_err + 1, st));
         else
-            HIP_TRY(launch_scatter(in, m.data.p, n, rb, chunk, G, lpp, (const uint32_t *)e->offs.p, geo, ticket_err + 1, st));
+            HIP_TRY(launch_scatter(in, m.data.p, n, rb, chunk, G, lpp, (const uint32_t *)W.offs.p, geo, ticket_err + 1, st));
     }
     HIP_TRY(hipEventRecord(x1, st));
     // (R+1) offsets then the look-back give-up flag
-    HIP_TRY(hipMemcpyAsync((char *)e->part_off_dev.p + (size_t)(s.R + 1) * 4, ticket_err + 1, 4,
+    HIP_TRY(hipMemcpyAsync((char *)W.part_off_dev.p + (size_t)(s.R + 1) * 4, ticket_err + 1, 4,
                            hipMemcpyDeviceToDevice, st));
-    HIP_TRY(hipMemcpyAsync(m.part_off.p, e->part_off_dev.p, (size_t)(s.R + 2) * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(m.part_off.p, W.part_off_dev.p, (size_t)(s.R + 2) * 4, hipMemcpyDeviceToHost, st));
+    if (pipe) {
+        if (!W.used) HIP_TRY(hipEventCreateWithFlags(&W.used, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(W.used, st));
+    }
     HIP_TRY(hipEventRecord(m.done, st));
     record_stage(e, SGX_STAGE_HIST, h0, h1);
     record_stage(e, SGX_STAGE_SCAN, c0, c1);
@@ -1068,6 +1098,7 @@ extern "C" int sgx_sync(sgx_engine *e) {
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipStreamSynchronize(e->s_comp));
     HIP_TRY(hipStreamSynchronize(e->s_comm));
+    HIP_TRY(hipStreamSynchronize(e->s_hist));
     for (auto &kv : e->shuffles)
         for (auto &m : kv.second.maps) SGX_TRY(finish_lengths(kv.second, *m.second));
     return SGX_OK;

@@ -19,7 +19,10 @@ struct PartParams {
     int32_t ascending;   // RangePartitioner.ascending
     uint32_t mbits;      // K4 peer-table width for this launch (0 = ballots only)
     const void *bounds;  // device: int64[nb] (RANGE_I64) or Key10[nb] (RANGE_BYTES10)
+    void *junk;          // device: JUNK_BYTES_PER_WG per scatter workgroup, write-only target of
+                         // the masked-off lanes of branch-free stores (never read)
 };
+constexpr size_t JUNK_BYTES_PER_WG = 64 * 16;
 
 // Granlund-Montgomery parameters of mod_u32 (sgx_kernels.hip) for 2 <= R < 2^31:
 // l = ceil(log2 R), m = floor(2^32 (2^l - R) / R) + 1, shift = l - 1.
@@ -71,7 +74,7 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int record_bytes, int kind, int nb);
 
 // Launchers (all asynchronous on `stream`).  counts / offs are [R][G] partition-major.
 hipError_t launch_hist(const void *in, int64_t n, int record_bytes, int64_t chunk, int G,
-                       const PartParams &pp, uint32_t *counts, hipStream_t stream);
+                       const PartParams &pp, uint32_t *counts, hipStream_t stream, bool lean = false);
 hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint64_t *status,
                        uint32_t *ticket_err, uint32_t *part_off, int G, int R,
                        hipStream_t stream);

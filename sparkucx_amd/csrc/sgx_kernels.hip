@@ -182,25 +182,24 @@ constexpr int HIST_UNROLL = 8;
 // the 256 MiB Infinity Cache when K4 starts -- are the chunk heads K4 reads first.
 constexpr int HIST_SPLIT = 4;
 
-template <int KIND, bool REC16>
-__global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ in, int64_t n,
-                                                       int rb, int64_t chunk, PartParams pp,
-                                                       uint32_t *__restrict__ counts, int G) {
+template <int KIND, bool REC16, int UNROLL, int SPLIT>
+__device__ __forceinline__ void hist_body(const char *__restrict__ in, int64_t n, int rb, int64_t chunk,
+                                          const PartParams &pp, uint32_t *__restrict__ counts, int G) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     uint32_t *hist = (uint32_t *)smem;
     const uint32_t tid = threadIdx.x, T = blockDim.x;
     for (uint32_t p = tid; p < pp.R; p += T) hist[p] = 0;
     __syncthreads();
-    const int g = blockIdx.x / HIST_SPLIT, sub = blockIdx.x % HIST_SPLIT;
+    const int g = blockIdx.x / SPLIT, sub = blockIdx.x % SPLIT;
     const int64_t cbeg = (int64_t)g * chunk;
     const int64_t cend = min(n, cbeg + chunk);
-    const int64_t slice = (int64_t)T * HIST_UNROLL, step = slice * HIST_SPLIT;
+    const int64_t slice = (int64_t)T * UNROLL, step = slice * SPLIT;
     const int64_t nsteps = cend > cbeg ? (cend - cbeg + step - 1) / step : 0;
     for (int64_t st = nsteps - 1; st >= 0; --st) {
         const int64_t base = cbeg + st * step + sub * slice;
-        uint32_t x[HIST_UNROLL], y[HIST_UNROLL], z[HIST_UNROLL];
+        uint32_t x[UNROLL], y[UNROLL], z[UNROLL];
 #pragma unroll
-        for (int u = 0; u < HIST_UNROLL; ++u) {
+        for (int u = 0; u < UNROLL; ++u) {
             const int64_t i = base + (int64_t)u * T + tid;
             x[u] = y[u] = z[u] = 0;
             if (i < cend) {
@@ -214,7 +213,7 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ 
             }
         }
 #pragma unroll
-        for (int u = 0; u < HIST_UNROLL; ++u) {
+        for (int u = 0; u < UNROLL; ++u) {
             const int64_t i = base + (int64_t)u * T + tid;
             if (i < cend) atomicAdd(&hist[pid_of<KIND>(x[u], y[u], z[u], pp)], 1u);
         }
@@ -226,15 +225,44 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ 
     }
 }
 
+template <int KIND, bool REC16>
+__global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ in, int64_t n, int rb,
+                                                       int64_t chunk, PartParams pp,
+                                                       uint32_t *__restrict__ counts, int G) {
+    hist_body<KIND, REC16, HIST_UNROLL, HIST_SPLIT>(in, n, rb, chunk, pp, counts, G);
+}
+
+// Lean histogram for the pipelined map side (SGX_PIPELINE, opt-in): one wave per SIMD and
+// at most 32 VGPRs, so a workgroup fits beside a write-combining K4 workgroup (2 waves x 240
+// VGPRs per SIMD, 156 KB of LDS) and the next map's histogram streams while the CU sorts.
+// Measured (C1): the overlap happens but the two kernels share one HBM budget -- K4 slows
+// from 1.88 to 2.24-2.37 ms, and the next K4 waits for CUs the histogram holds -- so the
+// pipelined step is 2.71-2.80 ms against 2.63-2.68 serial.  With one workgroup per chunk
+// (fewer waves) the histogram crawls (3.1 ms) and the step is 4.1 ms.
+constexpr int HIST_LEAN_THREADS = 256;
+template <int KIND, bool REC16>
+__global__ __launch_bounds__(HIST_LEAN_THREADS) __attribute__((amdgpu_num_vgpr(32))) void k_hist_lean(
+    const char *__restrict__ in, int64_t n, int rb, int64_t chunk, PartParams pp,
+    uint32_t *__restrict__ counts, int G) {
+    hist_body<KIND, REC16, 4, HIST_SPLIT>(in, n, rb, chunk, pp, counts, G);
+}
+
 hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
-                       const PartParams &pp, uint32_t *counts, hipStream_t stream) {
+                       const PartParams &pp, uint32_t *counts, hipStream_t stream, bool lean) {
     const size_t lds = (size_t)pp.R * 4;
     const char *p = (const char *)in;
     hipError_t ze = hipMemsetAsync(counts, 0, (size_t)pp.R * G * 4, stream);
     if (ze != hipSuccess) return ze;
     const bool r16 = (rb == 16);
-#define SGX_HIST(K, B) \
-    hipLaunchKernelGGL((k_hist<K, B>), dim3(G * HIST_SPLIT), dim3(HIST_THREADS), lds, stream, p, n, rb, chunk, pp, counts, G)
+#define SGX_HIST(K, B)                                                                                        \
+    do {                                                                                                      \
+        if (lean)                                                                                             \
+            hipLaunchKernelGGL((k_hist_lean<K, B>), dim3(G * HIST_SPLIT), dim3(HIST_LEAN_THREADS), lds, stream, \
+                               p, n, rb, chunk, pp, counts, G);                                               \
+        else                                                                                                  \
+            hipLaunchKernelGGL((k_hist<K, B>), dim3(G * HIST_SPLIT), dim3(HIST_THREADS), lds, stream, p, n, rb, \
+                               chunk, pp, counts, G);                                                         \
+    } while (0)
     switch (pp.kind) {
     case SGX_PART_HASH:
         if ((pp.R & (pp.R - 1)) == 0) {
@@ -1126,12 +1154,13 @@ ScatterGeom scatter_geom16_ord(uint32_t R, int force_waves, int force_items) {
 // the same counts and the same stable ranks.
 //
 // Tile: NI new records per lane (TNEW = T*NI) + up to DCAP = T*SI - TNEW deferred ones.
-// LDS: stage[T*SI] 16 B | rows[W][RS] u16 | cur[RS] u32 | dlt[RS] u32 | lim[RS] u32 |
-// dl[RS] u16 (RS = R rounded up to 8).  The merge's block-scan scratch borrows the stage
+// LDS: stage[T*SI] 16 B | rows[W][RS] u16 | cur[RS] u32 | dlt[RS] u32 | lim[RS] u32
+// (RS = R rounded up to 8); a stream's deferred count is cur - lim (no array of its own:
+// the 2 KB it saved at R = 1024 let a histogram workgroup share the CU, 156 + 4 KB).  The merge's block-scan scratch borrows the stage
 // (free between B1 and B3: every wave has drained the previous tile before B1).
 // ------------------------------------------------------------------------------------
 __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
-    return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 14;  // cur 4 + dlim 8 + dl 2
+    return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 12;  // cur 4 + dlim 8
 }
 
 // DIAG (measurement-only builds, SGX_WC_DIAG; wrong output): 1 = no global stores,
@@ -1154,11 +1183,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     uint16_t *rows = (uint16_t *)(smem + (size_t)STAGE * 16);
     uint32_t *cur = (uint32_t *)(rows + (size_t)WAVES * RS);
     uint2 *dlim = (uint2 *)(cur + RS);          // {dlt_p, lim_p}: one ds_read_b64 per drained slot
-    uint16_t *dl = (uint16_t *)(dlim + RS);
     uint32_t *scratch = (uint32_t *)smem;  // merge only (B1..B3)
     uint16_t *myrow = rows + (size_t)w * RS;
     uint32_t *myrow32 = (uint32_t *)myrow;
     const uint32_t n32 = (uint32_t)n;  // n < 2^32 (sgx_write_map)
+    u32x4 *junk = (u32x4 *)((char *)pp.junk + (size_t)blockIdx.x * JUNK_BYTES_PER_WG) + lane;
 
     const int g = blockIdx.x;
     const int64_t begin = (int64_t)g * chunk;
@@ -1166,8 +1195,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     const int64_t len = end > begin ? end - begin : 0;
     const int64_t ntiles = (len + TNEW - 1) / TNEW;
     for (uint32_t p = tid; p < RS; p += T) {
-        cur[p] = p < R ? offs[(int64_t)p * G + g] : 0u;
-        dl[p] = 0;
+        const uint32_t c0 = p < R ? offs[(int64_t)p * G + g] : 0u;
+        cur[p] = c0;
+        dlim[p] = make_uint2(0u, c0);  // lim = cur: nothing deferred
     }
     for (uint32_t i = tid; i < (uint32_t)WAVES * RS / 2; i += T) ((uint32_t *)rows)[i] = 0u;
 
@@ -1194,6 +1224,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         //      (a wave's LDS ops execute in issue order; lanes of one op in lane order), one
         //      wait at the end.  An invalid item adds 0 (branch-free issue).
         uint32_t pid[NI], old[NI];
+        if constexpr ((DIAG & 8) != 0) {
+            // A/B (DIAG 8): this tile's records were loaded by inline asm ahead of the
+            // previous tile's SI branch-free stores; wait for the loads only.
+            if (t > 0) {
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SI) : "memory");
+#pragma unroll
+                for (int k = 0; k < NI; ++k) asm volatile("" : "+v"(rec[k]));
+            }
+        }
 #pragma unroll
         for (int k = 0; k < NI; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
 #pragma unroll
@@ -1216,9 +1255,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 before[v] = tot;
                 tot += x;  // <= TNEW per half: no carry between halves
             }
-            dlp = ((const uint32_t *)dl)[j];
-            seg = tot + dlp;
             c = ((const uint2 *)cur)[j];
+            const u32x4 pl = ((const u32x4 *)dlim)[j];  // previous tile's limits
+            dlp = ((c.x - pl.y) & 0xFFFFu) | ((c.y - pl.w) << 16);
+            seg = tot + dlp;
             const uint32_t e0 = c.x + (tot & 0xFFFFu), e1 = c.y + (tot >> 16);
             const uint32_t a0 = c.x - (dlp & 0xFFFFu), a1 = c.y - (dlp >> 16);
             dnf_lo = e0 - max(e0 & ~7u, a0);
@@ -1253,7 +1293,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             bad |= (e0 > n32 || e1 > n32) ? 1u : 0u;
             ((u32x4 *)dlim)[j] = u32x4{a0 - ls0, min(le0, n32), a1 - ls1, min(le1, n32)};
             ((uint2 *)cur)[j] = make_uint2(e0, e1);
-            ((uint32_t *)dl)[j] = (e0 - le0) | ((e1 - le1) << 16);
         }
         lds_barrier();  // B3
 
@@ -1283,7 +1322,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             for (int k = 0; k < NI; ++k) {
                 const int64_t i = nb + (int64_t)w * NI * 64 + k * 64 + lane;
                 valid[k] = i < len;
-                rec[k] = cb[valid[k] ? i : 0];  // branch-free: an invalid item re-reads the chunk head
+                // branch-free: an invalid item re-reads the chunk head
+                if constexpr ((DIAG & 8) != 0)
+                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rec[k]) : "v"(cb + (valid[k] ? i : 0)) : "memory");
+                else
+                    rec[k] = cb[valid[k] ? i : 0];
             }
         }
         lds_barrier();  // B4
@@ -1305,13 +1348,22 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 const uint32_t s = (uint32_t)((k0 + q) * T + tid);
                 const bool live = s < total;
                 const uint32_t pos = dm[q].x + s;
+                const bool wr = live && pos < dm[q].y;
                 dpos[k0 + q] = pos;
-                if (live && pos < dm[q].y) {
-                    if constexpr ((DIAG & 1) == 0) out[pos] = dk[k0 + q];
-                    else asm volatile("" ::"v"(dk[k0 + q].x), "v"(dk[k0 + q].w), "v"(pos));
-                } else if (live) {
-                    dmask |= 1u << (k0 + q);
+                if constexpr ((DIAG & 12) != 0 && (DIAG & 1) == 0) {
+                    // A/B (DIAG 4, 8): branch-free, every lane stores, masked-off lanes into
+                    // this workgroup's junk line, so the next tile can wait for its loads
+                    // only (DIAG 8: vmcnt(SI)) instead of the compiler's vmcnt(0) behind
+                    // conditional stores.  Measured slower (C1: 2.01-2.04 vs 1.92-1.96 ms):
+                    // the junk lines cost more than the per-tile store drain.
+                    u32x4 *dst = wr ? out + pos : junk;
+                    *dst = dk[k0 + q];
+                } else if constexpr ((DIAG & 1) == 0) {
+                    if (wr) out[pos] = dk[k0 + q];
+                } else {
+                    if (wr) asm volatile("" ::"v"(dk[k0 + q].x), "v"(dk[k0 + q].w), "v"(pos));
                 }
+                dmask |= (live && !wr) ? 1u << (k0 + q) : 0u;
             }
         }
     }
@@ -2041,6 +2093,8 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         if (NI == 8 && geo.nt == 101) SGX_WC1(K, 8, 1);                                          \
         else if (NI == 8 && geo.nt == 102) SGX_WC1(K, 8, 2);                                     \
         else if (NI == 8 && geo.nt == 103) SGX_WC1(K, 8, 3);                                     \
+        else if (NI == 8 && geo.nt == 104) SGX_WC1(K, 8, 4);                                     \
+        else if (NI == 8 && geo.nt == 108) SGX_WC1(K, 8, 8);                                     \
         else SGX_WC1(K, NI, 0);                                                                  \
     } while (0)
         const bool pow2 = (pp.R & (pp.R - 1)) == 0;
