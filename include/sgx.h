@@ -133,12 +133,47 @@ int sgx_fetch_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids,
 int sgx_progress(sgx_engine *e);
 int sgx_sync(sgx_engine *e);
 
+/* ---- reduce side after the fetch: UcxShuffleReader.read (spark_3_0/UcxShuffleReader.scala:
+ *      137-191).  Input = the blocks (map_ids[0..nmaps) x reducers [start, end)) this engine
+ *      holds (local map outputs or blocks received by sgx_exchange), taken in the canonical
+ *      order (reducer-major, then map order, then record order).
+ *
+ * sgx_read_sorted: dep.keyOrdering (sortByKey, TeraSort's reduce side; ExternalSorter with an
+ * ordering, :166-181): every reducer's records sorted STABLY by key -- signed Long for 16 B
+ * records, the 10-byte unsigned big-endian key for 100 B records -- written back to back,
+ * reducer-major, into dst (dst_mem_kind).  *out_bytes = total bytes; dst NULL with dst_cap 0
+ * is a size query.  LSD radix passes of the map side's own partition kernels (8-bit digits)
+ * plus one pass by the shuffle's partitioner (skipped for an ascending RangePartitioner,
+ * whose partition order is key order).  SGX_ERR_UNSUPPORTED for other record widths. */
+int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
+                    int32_t start_partition, int32_t end_partition, void *dst, int64_t dst_cap,
+                    int32_t dst_mem_kind, int64_t *out_bytes);
+
+/* sgx_read_grouped: dep.aggregator with mapSideCombine = false (Aggregator.combineValuesByKey,
+ * :155-164) on (Long, Long) records.  Groups are emitted in ascending key order per reducer
+ * (Spark's hash-map iteration order is unspecified; this is the canonical order the parity
+ * tests compare), values of a group in the canonical arrival order.
+ *   SGX_AGG_GROUP (groupByKey): keys[G], group_starts[G] (index of the group's first value),
+ *                               values[N] (every value, grouped).
+ *   SGX_AGG_SUM   (reduceByKey(_ + _)): keys[G], values[G] = wrapping Long sums;
+ *                               group_starts may be NULL.
+ * Capacities in elements: cap_groups for keys / group_starts, cap_values for values.  A call
+ * with keys NULL and both capacities 0 only reports *out_groups / *out_values.  Output memory
+ * kind: mem_kind (all three arrays). */
+enum sgx_agg { SGX_AGG_GROUP = 0, SGX_AGG_SUM = 1 };
+int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
+                     int32_t start_partition, int32_t end_partition, int32_t agg, int64_t *keys,
+                     int64_t *group_starts, int64_t *values, int64_t cap_groups, int64_t cap_values,
+                     int32_t mem_kind, int64_t *out_groups, int64_t *out_values);
+
 /* ---- measurement: HIP-event times of the last write_map / exchange stages, and
  *      accumulated per-stage sums since the last reset (index = enum sgx_stage). ---- */
 /* SGX_STAGE_REGROUP times the fetch-side gather kernel (blocks into request order). */
 enum sgx_stage { SGX_STAGE_HIST = 0, SGX_STAGE_SCAN = 1, SGX_STAGE_SCATTER = 2,
                  SGX_STAGE_ALLGATHER = 3, SGX_STAGE_ALLTOALL = 4, SGX_STAGE_REGROUP = 5,
-                 SGX_NUM_STAGES = 6 };
+                 SGX_STAGE_SORT = 6, SGX_STAGE_GROUP = 7, SGX_NUM_STAGES = 8 };
+/* SGX_STAGE_SORT times sgx_read_sorted's radix + partitioner passes (the fetch gather is
+ * REGROUP), SGX_STAGE_GROUP the grouping / summing kernels of sgx_read_grouped. */
 int sgx_stats_reset(sgx_engine *e);
 /* out_ms[SGX_NUM_STAGES] summed milliseconds, out_count[SGX_NUM_STAGES] launches. */
 int sgx_stats_get(sgx_engine *e, double *out_ms, int64_t *out_count);

@@ -163,3 +163,63 @@ def canonical_reducer_sequences(map_outputs, num_partitions: int, record_bytes: 
         parts = [d[o[r]:o[r + 1]] for (d, _), o in zip(map_outputs, offs)]
         seqs.append(np.concatenate(parts) if parts else np.empty((0, record_bytes), np.uint8))
     return seqs
+
+
+# ---------------------------------------------------------------- reduce side -----
+# UcxShuffleReader.read after the fetch (spark_3_0/UcxShuffleReader.scala:137-191), on the
+# canonical per-reducer sequences above.  Spark 3.0.1 semantics restated (spark-core, not
+# vendored in the reference):
+#  * keyOrdering: ExternalSorter(ordering = keyOrd).insertAll -> sorted iterator; the sort
+#    is TimSort (java.util / Spark's Sorter), i.e. STABLE: equal keys keep arrival order.
+#    Long keys compare signed; TeraSort's 10-byte keys compare unsigned lexicographically.
+#  * aggregator, mapSideCombine = false: Aggregator.combineValuesByKey ->
+#    ExternalAppendOnlyMap; groupByKey's combiner is a CompactBuffer appended in arrival
+#    order; reduceByKey(_ + _) on Longs adds with two's-complement wrap-around.  Spark's
+#    output order of groups is hash-map order (unspecified); the canonical form compared
+#    here is ascending key order within each reducer.
+def sort_key_order(records: np.ndarray) -> np.ndarray:
+    """Stable permutation sorting fixed-width records by key (16 B: signed LE int64 at 0;
+    100 B: 10-byte unsigned big-endian key at 0)."""
+    records = np.ascontiguousarray(records)
+    n, rb = records.shape
+    if rb == 16:
+        keys = records[:, :8].copy().view("<i8").reshape(n)
+        return np.argsort(keys, kind="stable")
+    if rb == 100:
+        # lexsort: last key is primary; byte 0 most significant
+        return np.lexsort(tuple(records[:, i] for i in range(9, -1, -1)))
+    raise ValueError(f"record width {rb}")
+
+
+def reduce_sorted(seqs) -> np.ndarray:
+    """keyOrdering read: each reducer's canonical sequence sorted stably by key, reducer-major."""
+    parts = [s[sort_key_order(s)] for s in seqs if len(s)]
+    if not parts:
+        w = seqs[0].shape[1] if seqs else 16
+        return np.empty((0, w), dtype=np.uint8)
+    return np.concatenate(parts)
+
+
+def reduce_grouped(seqs, agg: str = "group"):
+    """groupByKey ('group') -> (keys, group_starts, values); reduceByKey sum ('sum') ->
+    (keys, sums).  Keys ascending per reducer, reducer-major; values in arrival order."""
+    keys_l, starts_l, vals_l, sums_l = [], [], [], []
+    base = 0
+    for s in seqs:
+        if not len(s):
+            continue
+        srt = s[sort_key_order(s)]
+        k = srt[:, :8].copy().view("<i8").reshape(-1)
+        v = srt[:, 8:16].copy().view("<i8").reshape(-1)
+        first = np.ones(len(k), dtype=bool)
+        first[1:] = k[1:] != k[:-1]
+        st = np.nonzero(first)[0]
+        keys_l.append(k[st])
+        starts_l.append(st + base)
+        vals_l.append(v)
+        sums_l.append(np.add.reduceat(v.astype(np.uint64), st).astype(np.int64))  # wraps mod 2^64
+        base += len(k)
+    cat = lambda xs: np.concatenate(xs) if xs else np.empty(0, dtype=np.int64)  # noqa: E731
+    if agg == "sum":
+        return cat(keys_l), cat(sums_l)
+    return cat(keys_l), cat(starts_l), cat(vals_l)

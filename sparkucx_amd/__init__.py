@@ -6,13 +6,13 @@ RCCL all-to-all exchange, regroup) runs in the in-tree HIP library ``libsgx.so``
 CPU fallback and raises if the library is missing.
 """
 from ._lib import (  # noqa: F401
-    MEM_DEVICE, MEM_HOST, PART_HASH, PART_RANGE_BYTES10, PART_RANGE_I64, STAGES,
+    AGG_GROUP, AGG_SUM, MEM_DEVICE, MEM_HOST, PART_HASH, PART_RANGE_BYTES10, PART_RANGE_I64, STAGES,
     BlockNotFoundException, DeviceError, IllegalArgumentException, IllegalStateException,
     ShuffleError, ShuffleIOException, TransportError, UnsupportedOperationException, lib,
 )
 from .engine import DeviceBuffer, ShuffleEngine, get_unique_id, plan_exchange, reducer_owner  # noqa: F401
 from .shuffle import (  # noqa: F401
-    BaseShuffleHandle, GpuShuffleMapOutputWriter, GpuShuffleTransport, GpuShuffleWriter,
+    Aggregator, BaseShuffleHandle, GpuShuffleMapOutputWriter, GpuShuffleTransport, GpuShuffleWriter,
     HashPartitioner, MapStatus, MemoryBlock, OperationResult, OperationStatus, RangePartitioner,
     ShuffleDependency, UcxShuffleBlockId, UcxShuffleBlockResolver, UcxShuffleManager,
     UcxShuffleReader, parse_block_id,

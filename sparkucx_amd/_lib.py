@@ -20,7 +20,8 @@ SGX_ERR_INVALID, SGX_ERR_STATE, SGX_ERR_HIP, SGX_ERR_COMM = -1, -2, -3, -4
 SGX_ERR_IO, SGX_ERR_NOMEM, SGX_ERR_NOT_FOUND, SGX_ERR_UNSUPPORTED, SGX_ERR_TIMEOUT = -5, -6, -7, -8, -9
 PART_HASH, PART_RANGE_I64, PART_RANGE_BYTES10 = 0, 1, 2
 MEM_HOST, MEM_DEVICE = 0, 1
-STAGES = ("hist", "scan", "scatter", "allgather", "alltoall", "regroup")
+AGG_GROUP, AGG_SUM = 0, 1
+STAGES = ("hist", "scan", "scatter", "allgather", "alltoall", "regroup", "sort", "group")
 
 
 class ShuffleError(RuntimeError):
@@ -94,6 +95,9 @@ SIGNATURES = {
     "sgx_comm_size": (ctypes.c_int, [_vp, _P32, _P32]),
     "sgx_exchange": (ctypes.c_int, [_vp, _i32, _i64]),
     "sgx_fetch_blocks": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i64, _vp, _i64, _i32, _vp]),
+    "sgx_read_sorted": (ctypes.c_int, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i64, _i32, _vp]),
+    "sgx_read_grouped": (ctypes.c_int, [_vp, _i32, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _i64, _i64, _i32,
+                                        _vp, _vp]),
     "sgx_progress": (ctypes.c_int, [_vp]),
     "sgx_sync": (ctypes.c_int, [_vp]),
     "sgx_stats_reset": (ctypes.c_int, [_vp]),

@@ -185,6 +185,8 @@ struct sgx_engine {
     int pipeline = 0;                // SGX_PIPELINE=1: hist+scan of map k+1 overlap map k's scatter
     hipStream_t s_hist = nullptr;
     DevBuf input_stage, junk;
+    // reduce side: sort ping-pong buffers, per-pass error words, grouping work buffers
+    DevBuf sort_buf[2], sort_err, grp_flags, grp_offs, grp_status, grp_out, grp_prefix;
     DevBuf ag_send, ag_recv, recv, items_dev, chain_buf, gather_stage;
     HostPinned gather_items;
     HostPinned ag_host;
@@ -312,6 +314,9 @@ extern "C" void sgx_destroy(sgx_engine *e) {
         if (w.used) (void)hipEventDestroy(w.used);
         w.used = nullptr;
     }
+    for (DevBuf *b : {&e->sort_buf[0], &e->sort_buf[1], &e->sort_err, &e->grp_flags, &e->grp_offs, &e->grp_status,
+                      &e->grp_out, &e->grp_prefix})
+        b->release();
     for (DevBuf *b : {&e->junk, &e->input_stage, &e->ag_send,
                       &e->ag_recv, &e->recv, &e->items_dev, &e->chain_buf, &e->gather_stage})
         b->release();
@@ -425,6 +430,151 @@ static void record_stage(sgx_engine *e, int stage, hipEvent_t a, hipEvent_t b) {
     e->pending.push_back(PendingStage{stage, a, b});
 }
 
+// One stable partition pass (K1+K2 hist -> K3 scan -> K4 scatter) of `n` records of `rb`
+// bytes from device memory `in` to `out` under partitioner `spp` (R partitions, `kind`, `nb`
+// range bounds).  Asynchronous on e->s_comp (the histogram + scan on e->s_hist when the
+// pipelined mode applies).  The (R+1) record offsets and the device error word land in
+// `host_off` (R+2 u32, pinned) when given; the error word alone in `err_slot` (device) when
+// given.  `stats` records the per-stage events.
+static int partition_pass(sgx_engine *e, const void *in, void *out, int64_t n, int rb, const PartParams &spp,
+                          int32_t R, int32_t kind, int32_t nb, int32_t mem_kind, uint32_t *host_off,
+                          uint32_t *err_slot, bool stats) {
+    hipStream_t st = e->s_comp;
+    // chunking: G chunks, each a whole number of scatter tiles where possible
+    ScatterGeom geo = rb == 16 ? scatter_geom16((uint32_t)R, e->sc_waves, e->sc_items)
+                               : scatter_geom_wide((uint32_t)R, rb);
+    if (e->diag > 0 && rb == 16) geo = scatter_geom16((uint32_t)R, 8, 16);
+    // experiment hook: SGX_SCATTER_DIRECT=<waves><items as 2 digits> selects the direct kernel
+    if (e->direct > 0 && rb == 16) {
+        const ScatterGeom d = scatter_geom16_direct((uint32_t)R, e->direct / 100, e->direct % 100);
+        if (d.items) geo = d;
+    }
+    if (rb == 16 && kind == SGX_PART_HASH && e->sc_waves == 0 && e->sc_items == 0 && e->diag == 0 &&
+        e->direct == 0 && e->use_dma) {
+        const ScatterGeom d = scatter_geom16_dma((uint32_t)R);
+        if (d.items) geo = d;
+    }
+    geo.nt = e->nt;
+    // default K4 for hash partitioners: lane-ordered ranking (SGX_RANK=match keeps the
+    // ballot/peer-table ranker; the A/B kernels above keep theirs)
+    if (rb == 16 && kind == SGX_PART_HASH && !e->rank_match && e->diag == 0 && e->direct == 0 &&
+        !e->use_dma && e->nt == 0 && e->chain == 0) {
+        const ScatterGeom o = scatter_geom16_ord((uint32_t)R, e->sc_waves, e->sc_items);
+        if (o.items) geo = o;
+        // write-combining K4 (whole 128 B lines only) where its LDS fits (R <= 1024)
+        if (e->wc && e->sc_waves == 0 && e->sc_items == 0) {
+            ScatterGeom w = scatter_geom16_wc((uint32_t)R);
+            if ((e->wc_diag >= 1 && e->wc_diag <= 4) || e->wc_diag == 8) w.nt = 100 + e->wc_diag;
+            if (w.items) geo = w;
+        }
+    }
+    // wide records: the LDS-staged dword-stream kernel where it applies (16 B-aligned input)
+    if (rb != 16 && e->wide2 && ((uintptr_t)in & 15) == 0) {
+        const ScatterGeom w2 = scatter_geom_wide2((uint32_t)R, rb, kind, nb);
+        if (w2.items) geo = w2;
+    }
+    // the reduce side's digit passes run on the write-combining / wide-record kernels only
+    if (kind == KIND_DIGIT) {
+        if (rb == 16) geo = scatter_geom16_wc((uint32_t)R);
+        if (geo.waves < WC_GEOM_BASE && geo.waves != WIDE2_GEOM_TAG)
+            return fail(SGX_ERR_UNSUPPORTED, "digit pass on %d B records at this alignment", rb);
+    }
+    if (geo.items == 0)
+        return fail(SGX_ERR_UNSUPPORTED, "no scatter geometry (waves %d, items %d) fits R=%d", e->sc_waves,
+                    e->sc_items, R);
+    const int tile = geo.tile;
+    int Gt = e->G;
+    if (is_direct_geom(geo.waves) && !e->G_forced) {
+        // several direct-store workgroups per CU: one chunk per resident workgroup
+        const int wv = geo.waves - DIRECT_GEOM_BASE;
+        int occ = (int)((160 * 1024) / geo.lds_bytes);
+        if (occ > 32 / wv) occ = 32 / wv;
+        Gt = e->num_cus * (occ > 0 ? occ : 1);
+    }
+    int64_t chunk = n > 0 ? (n + Gt - 1) / Gt : 1;
+    chunk = (chunk + tile - 1) / tile * tile;
+    const int G = n > 0 ? (int)((n + chunk - 1) / chunk) : 1;
+    const int64_t len = (int64_t)R * G;
+    const int64_t tiles = scan_tiles(len);
+    // the pipelined map side: device input, and the write-combining K4 it was sized for
+    const bool pipe = e->pipeline && mem_kind == SGX_MEM_DEVICE && rb == 16 && geo.waves >= WC_GEOM_BASE &&
+                      e->diag == 0 && e->chain == 0;
+    auto &W = e->ws[pipe ? (e->ws_next ^= 1) : 0];
+    hipStream_t sh = pipe ? e->s_hist : st;
+    if (pipe && W.used) HIP_TRY(hipStreamWaitEvent(sh, W.used, 0));  // its last reader (K4) is done
+    SGX_TRY(W.counts.ensure((size_t)len * 4));
+    SGX_TRY(W.offs.ensure((size_t)len * 4));
+    SGX_TRY(W.status.ensure((size_t)(16 + tiles * 8)));
+    SGX_TRY(W.part_off_dev.ensure((size_t)(R + 2) * 4));
+    uint32_t *ticket_err = (uint32_t *)W.status.p;
+    uint64_t *status = (uint64_t *)((char *)W.status.p + 16);
+    HIP_TRY(hipMemsetAsync(W.status.p, 0, (size_t)(16 + tiles * 8), sh));
+
+    // one event pair per stage: an event is owned by exactly one pending record
+    hipEvent_t h0 = e->ev(), h1 = e->ev(), c0 = e->ev(), c1 = e->ev(), x0 = e->ev(), x1 = e->ev();
+    HIP_TRY(hipEventRecord(h0, sh));
+    if (n > 0) {
+        HIP_TRY(launch_hist(in, n, rb, chunk, G, spp, (uint32_t *)W.counts.p, sh, pipe));
+    } else {
+        HIP_TRY(hipMemsetAsync(W.counts.p, 0, (size_t)len * 4, sh));
+    }
+    HIP_TRY(hipEventRecord(h1, sh));
+    HIP_TRY(hipEventRecord(c0, sh));
+    HIP_TRY(launch_scan((const uint32_t *)W.counts.p, (uint32_t *)W.offs.p, len, status, ticket_err,
+                        (uint32_t *)W.part_off_dev.p, G, R, sh));
+    HIP_TRY(hipEventRecord(c1, sh));
+    if (pipe) HIP_TRY(hipStreamWaitEvent(st, c1, 0));
+    HIP_TRY(hipEventRecord(x0, st));
+    PartParams lpp = spp;
+    SGX_TRY(e->junk.ensure((size_t)G * JUNK_BYTES_PER_WG));
+    lpp.junk = e->junk.p;
+    lpp.mbits = e->no_table ? 0u : (uint32_t)geo.mbits;
+    if (e->diag > 0) lpp.mbits = e->no_table ? 0u : (uint32_t)scatter_geom16((uint32_t)R, 8, 16).mbits;
+    const int cw = e->chain / 100, ci = e->chain % 100;
+    const ScatterGeom cg = (e->chain > 0 && rb == 16) ? scatter_geom16((uint32_t)R, cw, ci) : ScatterGeom{0, 0, 0, 0, 0};
+    if (n > 0 && cg.items > 0 && n < (1ll << 30)) {
+        // chained K4: tiles in ticket order, per-partition decoupled look-back across tiles
+        int mb = e->no_table ? 0 : cg.mbits;
+        while (mb > 0 && scatter16_chain_lds((uint32_t)R, cw, ci, mb) > 160 * 1024) --mb;
+        PartParams cpp = spp;
+        cpp.mbits = (uint32_t)mb;
+        const int ctile = cw * ci * 64;
+        const int64_t ntiles = (n + ctile - 1) / ctile;
+        const size_t sbytes = 16 + (size_t)ntiles * (size_t)R * 4;
+        SGX_TRY(e->chain_buf.ensure(sbytes));
+        HIP_TRY(hipMemsetAsync(e->chain_buf.p, 0, sbytes, st));
+        int occ = (int)((160 * 1024) / scatter16_chain_lds((uint32_t)R, cw, ci, mb));
+        if (occ > 32 / cw) occ = 32 / cw;
+        if (occ < 1) occ = 1;
+        HIP_TRY(launch_scatter_chain(in, out, n, cpp, (const uint32_t *)W.part_off_dev.p,
+                                     (uint32_t *)((char *)e->chain_buf.p + 16), (uint32_t *)e->chain_buf.p,
+                                     ticket_err + 1, cw, ci, e->num_cus * occ, st));
+    } else if (n > 0) {
+        if (e->diag > 0 && rb == 16 && kind == SGX_PART_HASH)  // measurement-only ablation
+            HIP_TRY(launch_scatter_diag(e->diag, in, out, n, chunk, G, lpp, (const uint32_t *)W.offs.p, ticket_err + 1, st));
+        else
+            HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, lpp, (const uint32_t *)W.offs.p, geo, ticket_err + 1, st));
+    }
+    HIP_TRY(hipEventRecord(x1, st));
+    // (R+1) offsets then the look-back give-up flag
+    HIP_TRY(hipMemcpyAsync((char *)W.part_off_dev.p + (size_t)(R + 1) * 4, ticket_err + 1, 4,
+                           hipMemcpyDeviceToDevice, st));
+    if (host_off) HIP_TRY(hipMemcpyAsync(host_off, W.part_off_dev.p, (size_t)(R + 2) * 4, hipMemcpyDeviceToHost, st));
+    if (err_slot) HIP_TRY(hipMemcpyAsync(err_slot, ticket_err + 1, 4, hipMemcpyDeviceToDevice, st));
+    if (pipe) {
+        if (!W.used) HIP_TRY(hipEventCreateWithFlags(&W.used, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(W.used, st));
+    }
+    if (stats) {
+        record_stage(e, SGX_STAGE_HIST, h0, h1);
+        record_stage(e, SGX_STAGE_SCAN, c0, c1);
+        record_stage(e, SGX_STAGE_SCATTER, x0, x1);
+    } else {
+        for (hipEvent_t v : {h0, h1, c0, c1, x0, x1}) e->ev_free.push_back(v);
+    }
+    return SGX_OK;
+}
+
 extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records,
                              int64_t n, int32_t rb, int32_t mem_kind, int64_t *out_lengths) {
     if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
@@ -462,128 +612,9 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
         in = e->input_stage.p;
     }
 
-    // chunking: G chunks, each a whole number of scatter tiles where possible
-    ScatterGeom geo = rb == 16 ? scatter_geom16((uint32_t)s.R, e->sc_waves, e->sc_items)
-                               : scatter_geom_wide((uint32_t)s.R, rb);
-    if (e->diag > 0 && rb == 16) geo = scatter_geom16((uint32_t)s.R, 8, 16);
-    // experiment hook: SGX_SCATTER_DIRECT=<waves><items as 2 digits> selects the direct kernel
-    if (e->direct > 0 && rb == 16) {
-        const ScatterGeom d = scatter_geom16_direct((uint32_t)s.R, e->direct / 100, e->direct % 100);
-        if (d.items) geo = d;
-    }
-    if (rb == 16 && s.kind == SGX_PART_HASH && e->sc_waves == 0 && e->sc_items == 0 && e->diag == 0 &&
-        e->direct == 0 && e->use_dma) {
-        const ScatterGeom d = scatter_geom16_dma((uint32_t)s.R);
-        if (d.items) geo = d;
-    }
-    geo.nt = e->nt;
-    // default K4 for hash partitioners: lane-ordered ranking (SGX_RANK=match keeps the
-    // ballot/peer-table ranker; the A/B kernels above keep theirs)
-    if (rb == 16 && s.kind == SGX_PART_HASH && !e->rank_match && e->diag == 0 && e->direct == 0 &&
-        !e->use_dma && e->nt == 0 && e->chain == 0) {
-        const ScatterGeom o = scatter_geom16_ord((uint32_t)s.R, e->sc_waves, e->sc_items);
-        if (o.items) geo = o;
-        // write-combining K4 (whole 128 B lines only) where its LDS fits (R <= 1024)
-        if (e->wc && e->sc_waves == 0 && e->sc_items == 0) {
-            ScatterGeom w = scatter_geom16_wc((uint32_t)s.R);
-            if ((e->wc_diag >= 1 && e->wc_diag <= 4) || e->wc_diag == 8) w.nt = 100 + e->wc_diag;
-            if (w.items) geo = w;
-        }
-    }
-    // wide records: the LDS-staged dword-stream kernel where it applies (16 B-aligned input)
-    if (rb != 16 && e->wide2 && ((uintptr_t)in & 15) == 0) {
-        const ScatterGeom w2 = scatter_geom_wide2((uint32_t)s.R, rb, s.kind, s.nb);
-        if (w2.items) geo = w2;
-    }
-    if (geo.items == 0)
-        return fail(SGX_ERR_UNSUPPORTED, "no scatter geometry (waves %d, items %d) fits R=%d", e->sc_waves,
-                    e->sc_items, s.R);
-    const int tile = geo.tile;
-    int Gt = e->G;
-    if (is_direct_geom(geo.waves) && !e->G_forced) {
-        // several direct-store workgroups per CU: one chunk per resident workgroup
-        const int wv = geo.waves - DIRECT_GEOM_BASE;
-        int occ = (int)((160 * 1024) / geo.lds_bytes);
-        if (occ > 32 / wv) occ = 32 / wv;
-        Gt = e->num_cus * (occ > 0 ? occ : 1);
-    }
-    int64_t chunk = n > 0 ? (n + Gt - 1) / Gt : 1;
-    chunk = (chunk + tile - 1) / tile * tile;
-    const int G = n > 0 ? (int)((n + chunk - 1) / chunk) : 1;
-    const int64_t len = (int64_t)s.R * G;
-    const int64_t tiles = scan_tiles(len);
-    // the pipelined map side: device input, and the write-combining K4 it was sized for
-    const bool pipe = e->pipeline && mem_kind == SGX_MEM_DEVICE && rb == 16 && geo.waves >= WC_GEOM_BASE &&
-                      e->diag == 0 && e->chain == 0;
-    auto &W = e->ws[pipe ? (e->ws_next ^= 1) : 0];
-    hipStream_t sh = pipe ? e->s_hist : st;
-    if (pipe && W.used) HIP_TRY(hipStreamWaitEvent(sh, W.used, 0));  // its last reader (K4) is done
-    SGX_TRY(W.counts.ensure((size_t)len * 4));
-    SGX_TRY(W.offs.ensure((size_t)len * 4));
-    SGX_TRY(W.status.ensure((size_t)(16 + tiles * 8)));
-    SGX_TRY(W.part_off_dev.ensure((size_t)(s.R + 2) * 4));
-    uint32_t *ticket_err = (uint32_t *)W.status.p;
-    uint64_t *status = (uint64_t *)((char *)W.status.p + 16);
-    HIP_TRY(hipMemsetAsync(W.status.p, 0, (size_t)(16 + tiles * 8), sh));
-
-    // one event pair per stage: an event is owned by exactly one pending record
-    hipEvent_t h0 = e->ev(), h1 = e->ev(), c0 = e->ev(), c1 = e->ev(), x0 = e->ev(), x1 = e->ev();
-    HIP_TRY(hipEventRecord(h0, sh));
-    if (n > 0) {
-        HIP_TRY(launch_hist(in, n, rb, chunk, G, s.pp, (uint32_t *)W.counts.p, sh, pipe));
-    } else {
-        HIP_TRY(hipMemsetAsync(W.counts.p, 0, (size_t)len * 4, sh));
-    }
-    HIP_TRY(hipEventRecord(h1, sh));
-    HIP_TRY(hipEventRecord(c0, sh));
-    HIP_TRY(launch_scan((const uint32_t *)W.counts.p, (uint32_t *)W.offs.p, len, status, ticket_err,
-                        (uint32_t *)W.part_off_dev.p, G, s.R, sh));
-    HIP_TRY(hipEventRecord(c1, sh));
-    if (pipe) HIP_TRY(hipStreamWaitEvent(st, c1, 0));
-    HIP_TRY(hipEventRecord(x0, st));
-    PartParams lpp = s.pp;
-    SGX_TRY(e->junk.ensure((size_t)G * JUNK_BYTES_PER_WG));
-    lpp.junk = e->junk.p;
-    lpp.mbits = e->no_table ? 0u : (uint32_t)geo.mbits;
-    if (e->diag > 0) lpp.mbits = e->no_table ? 0u : (uint32_t)scatter_geom16((uint32_t)s.R, 8, 16).mbits;
-    const int cw = e->chain / 100, ci = e->chain % 100;
-    const ScatterGeom cg = (e->chain > 0 && rb == 16) ? scatter_geom16((uint32_t)s.R, cw, ci) : ScatterGeom{0, 0, 0, 0, 0};
-    if (n > 0 && cg.items > 0 && n < (1ll << 30)) {
-        // chained K4: tiles in ticket order, per-partition decoupled look-back across tiles
-        int mb = e->no_table ? 0 : cg.mbits;
-        while (mb > 0 && scatter16_chain_lds((uint32_t)s.R, cw, ci, mb) > 160 * 1024) --mb;
-        PartParams cpp = s.pp;
-        cpp.mbits = (uint32_t)mb;
-        const int ctile = cw * ci * 64;
-        const int64_t ntiles = (n + ctile - 1) / ctile;
-        const size_t sbytes = 16 + (size_t)ntiles * (size_t)s.R * 4;
-        SGX_TRY(e->chain_buf.ensure(sbytes));
-        HIP_TRY(hipMemsetAsync(e->chain_buf.p, 0, sbytes, st));
-        int occ = (int)((160 * 1024) / scatter16_chain_lds((uint32_t)s.R, cw, ci, mb));
-        if (occ > 32 / cw) occ = 32 / cw;
-        if (occ < 1) occ = 1;
-        HIP_TRY(launch_scatter_chain(in, m.data.p, n, cpp, (const uint32_t *)W.part_off_dev.p,
-                                     (uint32_t *)((char *)e->chain_buf.p + 16), (uint32_t *)e->chain_buf.p,
-                                     ticket_err + 1, cw, ci, e->num_cus * occ, st));
-    } else if (n > 0) {
-        if (e->diag > 0 && rb == 16 && s.kind == SGX_PART_HASH)  // measurement-only ablation
-            HIP_TRY(launch_scatter_diag(e->diag, in, m.data.p, n, chunk, G, lpp, (const uint32_t *)W.offs.p, ticket_err + 1, st));
-        else
-            HIP_TRY(launch_scatter(in, m.data.p, n, rb, chunk, G, lpp, (const uint32_t *)W.offs.p, geo, ticket_err + 1, st));
-    }
-    HIP_TRY(hipEventRecord(x1, st));
-    // (R+1) offsets then the look-back give-up flag
-    HIP_TRY(hipMemcpyAsync((char *)W.part_off_dev.p + (size_t)(s.R + 1) * 4, ticket_err + 1, 4,
-                           hipMemcpyDeviceToDevice, st));
-    HIP_TRY(hipMemcpyAsync(m.part_off.p, W.part_off_dev.p, (size_t)(s.R + 2) * 4, hipMemcpyDeviceToHost, st));
-    if (pipe) {
-        if (!W.used) HIP_TRY(hipEventCreateWithFlags(&W.used, hipEventDisableTiming));
-        HIP_TRY(hipEventRecord(W.used, st));
-    }
+    SGX_TRY(partition_pass(e, in, m.data.p, n, rb, s.pp, s.R, s.kind, s.nb, mem_kind, (uint32_t *)m.part_off.p,
+                           nullptr, true));
     HIP_TRY(hipEventRecord(m.done, st));
-    record_stage(e, SGX_STAGE_HIST, h0, h1);
-    record_stage(e, SGX_STAGE_SCAN, c0, c1);
-    record_stage(e, SGX_STAGE_SCATTER, x0, x1);
     if (out_lengths) {
         SGX_TRY(finish_lengths(s, m));
         std::memcpy(out_lengths, m.lengths.data(), sizeof(int64_t) * (size_t)s.R);
@@ -984,12 +1015,11 @@ extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
 // ------------------------------------------------------------------------------------
 // fetchBlocksByBlockIds
 // ------------------------------------------------------------------------------------
-extern "C" int sgx_fetch_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids,
-                                const int32_t *reduce_ids, int64_t n, void *dst, int64_t dst_cap,
-                                int32_t dst_mem_kind, int64_t *out_lengths) {
-    if (!e || (n > 0 && (!map_ids || !reduce_ids || !out_lengths)))
-        return fail(SGX_ERR_INVALID, "NULL argument");
-    std::lock_guard<std::mutex> lk(e->mu);
+// fetchBlocksByBlockIds body (caller holds e->mu).  `sync`: wait for the copy before
+// returning (the public call); the reduce side chains its sort behind it on s_comp instead.
+static int fetch_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, const int32_t *reduce_ids,
+                        int64_t n, void *dst, int64_t dst_cap, int32_t dst_mem_kind, int64_t *out_lengths,
+                        bool sync) {
     auto it = e->shuffles.find(shuffle_id);
     if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
     Shuffle &s = it->second;
@@ -1077,6 +1107,220 @@ extern "C" int sgx_fetch_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t
     HIP_TRY(hipEventRecord(g1, st));
     record_stage(e, SGX_STAGE_REGROUP, g0, g1);
     if (!dev_dst) HIP_TRY(hipMemcpyAsync(dst, gdst, (size_t)total, hipMemcpyDeviceToHost, st));
+    if (sync) HIP_TRY(hipStreamSynchronize(st));
+    return SGX_OK;
+}
+
+extern "C" int sgx_fetch_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids,
+                                const int32_t *reduce_ids, int64_t n, void *dst, int64_t dst_cap,
+                                int32_t dst_mem_kind, int64_t *out_lengths) {
+    if (!e || (n > 0 && (!map_ids || !reduce_ids || !out_lengths)))
+        return fail(SGX_ERR_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(e->mu);
+    return fetch_locked(e, shuffle_id, map_ids, reduce_ids, n, dst, dst_cap, dst_mem_kind, out_lengths, true);
+}
+
+// ------------------------------------------------------------------------------------
+// Reduce side after the fetch (UcxShuffleReader.scala:137-191): stable sort by key per
+// reducer, then groupByKey / reduceByKey on (Long, Long) records
+// ------------------------------------------------------------------------------------
+// Fetch the canonical blocks of reducers [r0, r1) x maps into e->sort_buf[0] and sort them
+// stably by key within each reducer.  On return (asynchronous on s_comp) *sorted points at
+// the device buffer holding the result and *nrec its record count.
+static int sort_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps, int32_t r0,
+                       int32_t r1, const void **sorted, int64_t *nrec) {
+    auto it = e->shuffles.find(shuffle_id);
+    if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
+    Shuffle &s = it->second;
+    if (r0 < 0 || r1 > s.R || r0 > r1)
+        return fail(SGX_ERR_INVALID, "partition range [%d, %d) outside [0, %d)", r0, r1, s.R);
+    if (nmaps < 0 || (nmaps > 0 && !map_ids)) return fail(SGX_ERR_INVALID, "bad map list");
+    const int rb = s.rb;
+    if (rb != 16 && rb != 100)
+        return fail(SGX_ERR_UNSUPPORTED, "sorted read needs 16 B (Long, Long) or 100 B TeraSort records, not %d B", rb);
+    const int64_t nreq = (int64_t)(r1 - r0) * nmaps;
+    std::vector<int64_t> mids((size_t)nreq), lens((size_t)nreq);
+    std::vector<int32_t> rids((size_t)nreq);
+    for (int32_t r = r0; r < r1; ++r)
+        for (int64_t j = 0; j < nmaps; ++j) {
+            mids[(size_t)((r - r0) * nmaps + j)] = map_ids[j];
+            rids[(size_t)((r - r0) * nmaps + j)] = r;
+        }
+    // size query (fails with SGX_ERR_INVALID on capacity, after filling the lengths)
+    int rc = fetch_locked(e, shuffle_id, mids.data(), rids.data(), nreq, nullptr, 0, SGX_MEM_DEVICE, lens.data(), false);
+    if (rc != SGX_OK && rc != SGX_ERR_INVALID) return rc;
+    int64_t total = 0;
+    for (int64_t L : lens) total += L;
+    const int64_t n = total / rb;
+    if (n >= (int64_t)INT32_MAX) return fail(SGX_ERR_INVALID, "%lld records exceed one sorted read", (long long)n);
+    *nrec = n;
+    SGX_TRY(e->sort_buf[0].ensure((size_t)total));
+    SGX_TRY(e->sort_buf[1].ensure((size_t)total));
+    *sorted = e->sort_buf[0].p;
+    if (n == 0) return SGX_OK;
+    SGX_TRY(fetch_locked(e, shuffle_id, mids.data(), rids.data(), nreq, e->sort_buf[0].p, total, SGX_MEM_DEVICE,
+                         lens.data(), false));
+    hipStream_t st = e->s_comp;
+    constexpr int MAXP = 12;
+    SGX_TRY(e->sort_err.ensure(MAXP * 4));
+    HIP_TRY(hipMemsetAsync(e->sort_err.p, 0, MAXP * 4, st));
+    uint32_t *errs = (uint32_t *)e->sort_err.p;
+    hipEvent_t t0 = e->ev(), t1 = e->ev();
+    HIP_TRY(hipEventRecord(t0, st));
+    // LSD digit passes, least significant byte first: i64 keys (bytes 0..7 of the record,
+    // sign flip on the top byte), or TeraSort's 10-byte big-endian keys (bytes 9..0)
+    const int ndig = rb == 16 ? 8 : 10;
+    int cur = 0, np = 0;
+    for (int d = 0; d < ndig; ++d, ++np) {
+        PartParams dp{};
+        dp.kind = KIND_DIGIT;
+        dp.R = DIGIT_R;
+        dp.nbits = 8;
+        dp.dshift = rb == 16 ? 8u * (uint32_t)d : 8u * (uint32_t)(9 - d);
+        dp.dflip = (rb == 16 && d == 7) ? 0x80u : 0u;
+        SGX_TRY(partition_pass(e, e->sort_buf[cur].p, e->sort_buf[cur ^ 1].p, n, rb, dp, (int32_t)DIGIT_R,
+                               KIND_DIGIT, 0, SGX_MEM_DEVICE, nullptr, errs + np, false));
+        cur ^= 1;
+    }
+    // records back into reducer order: the shuffle's own partitioner, stable (an ascending
+    // RangePartitioner's partition order is already key order)
+    const bool range_asc = s.kind != SGX_PART_HASH && s.asc;
+    if (!range_asc && s.R > 1) {
+        SGX_TRY(partition_pass(e, e->sort_buf[cur].p, e->sort_buf[cur ^ 1].p, n, rb, s.pp, s.R, s.kind, s.nb,
+                               SGX_MEM_DEVICE, nullptr, errs + np, false));
+        cur ^= 1;
+        ++np;
+    }
+    HIP_TRY(hipEventRecord(t1, st));
+    record_stage(e, SGX_STAGE_SORT, t0, t1);
+    uint32_t herr[MAXP];
+    HIP_TRY(hipMemcpyAsync(herr, e->sort_err.p, MAXP * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int i = 0; i < np; ++i) {
+        if (herr[i] & 1u) return fail(SGX_ERR_TIMEOUT, "sort pass %d: scan look-back spin gave up", i);
+        if (herr[i] & 2u) return fail(SGX_ERR_HIP, "sort pass %d: a scatter destination was out of range", i);
+    }
+    *sorted = e->sort_buf[cur].p;
+    return SGX_OK;
+}
+
+static int copy_out(sgx_engine *e, void *dst, const void *src, int64_t bytes, int32_t mem_kind) {
+    if (bytes <= 0) return SGX_OK;
+    HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes,
+                           mem_kind == SGX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, e->s_comp));
+    return SGX_OK;
+}
+
+extern "C" int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
+                               int32_t start_partition, int32_t end_partition, void *dst, int64_t dst_cap,
+                               int32_t dst_mem_kind, int64_t *out_bytes) {
+    if (!e || !out_bytes) return fail(SGX_ERR_INVALID, "NULL argument");
+    if (dst_mem_kind != SGX_MEM_HOST && dst_mem_kind != SGX_MEM_DEVICE)
+        return fail(SGX_ERR_INVALID, "unknown mem_kind %d", dst_mem_kind);
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    auto it = e->shuffles.find(shuffle_id);
+    if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
+    const int rb = it->second.rb;
+    if (!dst && dst_cap == 0) {  // size query: lengths only
+        const int64_t nreq = (int64_t)std::max(0, end_partition - start_partition) * std::max<int64_t>(0, nmaps);
+        if (start_partition < 0 || end_partition > it->second.R || start_partition > end_partition || nmaps < 0 ||
+            (nmaps > 0 && !map_ids))
+            return fail(SGX_ERR_INVALID, "bad partition range or map list");
+        std::vector<int64_t> mids((size_t)nreq), lens((size_t)nreq);
+        std::vector<int32_t> rids((size_t)nreq);
+        for (int64_t q = 0; q < nreq; ++q) {
+            mids[(size_t)q] = map_ids[q % nmaps];
+            rids[(size_t)q] = start_partition + (int32_t)(q / nmaps);
+        }
+        int rc = fetch_locked(e, shuffle_id, mids.data(), rids.data(), nreq, nullptr, 0, SGX_MEM_DEVICE, lens.data(), false);
+        if (rc != SGX_OK && rc != SGX_ERR_INVALID) return rc;
+        int64_t total = 0;
+        for (int64_t L : lens) total += L;
+        *out_bytes = total;
+        return SGX_OK;
+    }
+    const void *sorted = nullptr;
+    int64_t n = 0;
+    SGX_TRY(sort_locked(e, shuffle_id, map_ids, nmaps, start_partition, end_partition, &sorted, &n));
+    *out_bytes = n * rb;
+    if (n * rb > dst_cap) return fail(SGX_ERR_INVALID, "destination capacity %lld < %lld bytes", (long long)dst_cap,
+                                      (long long)(n * rb));
+    if (n > 0 && !dst) return fail(SGX_ERR_INVALID, "dst is NULL");
+    SGX_TRY(copy_out(e, dst, sorted, n * rb, dst_mem_kind));
+    HIP_TRY(hipStreamSynchronize(e->s_comp));
+    return SGX_OK;
+}
+
+extern "C" int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
+                                int32_t start_partition, int32_t end_partition, int32_t agg, int64_t *keys,
+                                int64_t *group_starts, int64_t *values, int64_t cap_groups, int64_t cap_values,
+                                int32_t mem_kind, int64_t *out_groups, int64_t *out_values) {
+    if (!e || !out_groups || !out_values) return fail(SGX_ERR_INVALID, "NULL argument");
+    if (agg != SGX_AGG_GROUP && agg != SGX_AGG_SUM) return fail(SGX_ERR_INVALID, "unknown aggregation %d", agg);
+    if (mem_kind != SGX_MEM_HOST && mem_kind != SGX_MEM_DEVICE)
+        return fail(SGX_ERR_INVALID, "unknown mem_kind %d", mem_kind);
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    auto it = e->shuffles.find(shuffle_id);
+    if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
+    if (it->second.rb != 16)
+        return fail(SGX_ERR_UNSUPPORTED, "grouped read needs 16 B (Long, Long) records, not %d B", it->second.rb);
+    const void *sorted = nullptr;
+    int64_t n = 0;
+    SGX_TRY(sort_locked(e, shuffle_id, map_ids, nmaps, start_partition, end_partition, &sorted, &n));
+    hipStream_t st = e->s_comp;
+    // group ids: flags of key changes, exclusive scan (K3 with one partition: offs[i] is the
+    // group of record i minus its flag; part_off[1] the group count)
+    const int64_t tiles = scan_tiles(n);
+    SGX_TRY(e->grp_flags.ensure((size_t)std::max<int64_t>(n, 1) * 4));
+    SGX_TRY(e->grp_offs.ensure((size_t)std::max<int64_t>(n, 1) * 4));
+    SGX_TRY(e->grp_status.ensure((size_t)(16 + tiles * 8 + 16)));
+    uint32_t *ticket_err = (uint32_t *)e->grp_status.p;
+    uint32_t *gcount = (uint32_t *)((char *)e->grp_status.p + 16 + tiles * 8);  // [0, total]
+    int64_t ngroups = 0;
+    hipEvent_t t0 = e->ev(), t1 = e->ev();
+    HIP_TRY(hipEventRecord(t0, st));
+    if (n > 0) {
+        HIP_TRY(hipMemsetAsync(e->grp_status.p, 0, (size_t)(16 + tiles * 8 + 16), st));
+        HIP_TRY(launch_group_flags(sorted, n, (uint32_t *)e->grp_flags.p, st));
+        HIP_TRY(launch_scan((const uint32_t *)e->grp_flags.p, (uint32_t *)e->grp_offs.p, n,
+                            (uint64_t *)((char *)e->grp_status.p + 16), ticket_err, gcount, (int)n, 1, st));
+        uint32_t h[2] = {0, 0}, terr[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(h, gcount, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(terr, ticket_err, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (terr[1] & 1u) return fail(SGX_ERR_TIMEOUT, "group scan look-back spin gave up");
+        ngroups = h[1];
+    }
+    const int64_t nvals = agg == SGX_AGG_GROUP ? n : ngroups;
+    *out_groups = ngroups;
+    *out_values = nvals;
+    if (!keys && cap_groups == 0 && cap_values == 0) {
+        (void)hipEventRecord(t1, st);
+        record_stage(e, SGX_STAGE_GROUP, t0, t1);
+        return SGX_OK;  // size query
+    }
+    if (ngroups > cap_groups || nvals > cap_values)
+        return fail(SGX_ERR_INVALID, "capacity (%lld groups, %lld values) < (%lld, %lld)", (long long)cap_groups,
+                    (long long)cap_values, (long long)ngroups, (long long)nvals);
+    if (n == 0) return SGX_OK;
+    if (!keys || !values || (agg == SGX_AGG_GROUP && !group_starts))
+        return fail(SGX_ERR_INVALID, "NULL output array");
+    SGX_TRY(e->grp_out.ensure((size_t)(ngroups * 16 + nvals * 8)));
+    int64_t *dkeys = (int64_t *)e->grp_out.p, *dstarts = dkeys + ngroups, *dvals = dstarts + ngroups;
+    HIP_TRY(launch_group_emit(sorted, n, (const uint32_t *)e->grp_flags.p, (const uint32_t *)e->grp_offs.p, dkeys,
+                              dstarts, agg == SGX_AGG_GROUP ? dvals : nullptr, st));
+    if (agg == SGX_AGG_SUM) {
+        SGX_TRY(e->grp_prefix.ensure((size_t)(n + prefix64_blocks(n)) * 8));
+        uint64_t *P = (uint64_t *)e->grp_prefix.p, *bsum = P + n;
+        HIP_TRY(launch_group_sums(sorted, n, dstarts, ngroups, bsum, P, dvals, st));
+    }
+    HIP_TRY(hipEventRecord(t1, st));
+    record_stage(e, SGX_STAGE_GROUP, t0, t1);
+    SGX_TRY(copy_out(e, keys, dkeys, ngroups * 8, mem_kind));
+    if (group_starts) SGX_TRY(copy_out(e, group_starts, dstarts, ngroups * 8, mem_kind));
+    SGX_TRY(copy_out(e, values, dvals, nvals * 8, mem_kind));
     HIP_TRY(hipStreamSynchronize(st));
     return SGX_OK;
 }

@@ -19,10 +19,16 @@ struct PartParams {
     int32_t ascending;   // RangePartitioner.ascending
     uint32_t mbits;      // K4 peer-table width for this launch (0 = ballots only)
     const void *bounds;  // device: int64[nb] (RANGE_I64) or Key10[nb] (RANGE_BYTES10)
+    uint32_t dshift;     // KIND_DIGIT: bit offset of the digit in the record's first 12 bytes (LE)
+    uint32_t dflip;      // KIND_DIGIT: XORed into the digit (0x80 = sign flip of an i64 key's top byte)
     void *junk;          // device: JUNK_BYTES_PER_WG per scatter workgroup, write-only target of
                          // the masked-off lanes of branch-free stores (never read)
 };
 constexpr size_t JUNK_BYTES_PER_WG = 64 * 16;
+// Internal partition kind of the reduce side's LSD radix passes: pid = 8-bit digit of the
+// key (R = 256), see PartParams::dshift / dflip.  Never registered through the C ABI.
+constexpr int KIND_DIGIT = 200;
+constexpr uint32_t DIGIT_R = 256;
 
 // Granlund-Montgomery parameters of mod_u32 (sgx_kernels.hip) for 2 <= R < 2^31:
 // l = ceil(log2 R), m = floor(2^32 (2^l - R) / R) + 1, shift = l - 1.
@@ -97,6 +103,13 @@ hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, i
                              int align, hipStream_t stream);
 // items: [n][3] int64 {src address, dst address, bytes} (device memory on both sides).
 hipError_t launch_gather_items(const int64_t *items, int64_t n_items, int align, hipStream_t stream);
+// Reduce side (sgx_reduce.hip), key-sorted (Long, Long) records
+hipError_t launch_group_flags(const void *rec, int64_t n, uint32_t *flags, hipStream_t st);
+hipError_t launch_group_emit(const void *rec, int64_t n, const uint32_t *flags, const uint32_t *offs,
+                             int64_t *keys, int64_t *starts, int64_t *values, hipStream_t st);
+int64_t prefix64_blocks(int64_t n);
+hipError_t launch_group_sums(const void *rec, int64_t n, const int64_t *starts, int64_t ngroups,
+                             uint64_t *bsum, uint64_t *P, int64_t *sums, hipStream_t st);
 hipError_t launch_gen_uniform16(void *dst, int64_t n, uint64_t seed, int64_t value_base,
                                 hipStream_t stream);
 hipError_t launch_gen_zipf16(void *dst, int64_t n, uint64_t seed, int64_t value_base,

@@ -106,6 +106,11 @@ __device__ __forceinline__ uint32_t pid_of_b(uint32_t x, uint32_t y, uint32_t z,
                                              BI64 bi64, BK10 bk10) {
     if constexpr (KIND == SGX_PART_HASH) {
         return hash_pid(x, y, pp);
+    } else if constexpr (KIND == KIND_DIGIT) {
+        // 8-bit digit of the 96-bit little-endian view {x, y, z} at bit dshift (a multiple of 8)
+        const uint32_t sh = pp.dshift;
+        const uint32_t w = sh < 32 ? x : (sh < 64 ? y : z);
+        return ((w >> (sh & 31u)) & 0xFFu) ^ pp.dflip;
     } else if constexpr (KIND == KIND_HASH_POW2) {
         return (x ^ y) & (pp.R - 1u);
     } else if constexpr (KIND == SGX_PART_RANGE_I64) {
@@ -271,6 +276,7 @@ hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
             if (r16) SGX_HIST(SGX_PART_HASH, true); else SGX_HIST(SGX_PART_HASH, false);
         }
         break;
+    case KIND_DIGIT: if (r16) SGX_HIST(KIND_DIGIT, true); else SGX_HIST(KIND_DIGIT, false); break;
     case SGX_PART_RANGE_I64: if (r16) SGX_HIST(SGX_PART_RANGE_I64, true); else SGX_HIST(SGX_PART_RANGE_I64, false); break;
     default: if (r16) SGX_HIST(SGX_PART_RANGE_BYTES10, true); else SGX_HIST(SGX_PART_RANGE_BYTES10, false); break;
     }
@@ -2080,7 +2086,8 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         return hipGetLastError();
     }
     if (rb == 16 && geo.waves >= WC_GEOM_BASE) {
-        if (pp.kind != SGX_PART_HASH || geo.waves != WC_GEOM_BASE + 8 || geo.mbits != 16) return hipErrorInvalidValue;
+        if ((pp.kind != SGX_PART_HASH && pp.kind != KIND_DIGIT) || geo.waves != WC_GEOM_BASE + 8 || geo.mbits != 16)
+            return hipErrorInvalidValue;
 #define SGX_WC1(K, NI, DG)                                                                       \
     do {                                                                                         \
         (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, 8, NI, 16, DG>,               \
@@ -2098,7 +2105,10 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         else SGX_WC1(K, NI, 0);                                                                  \
     } while (0)
         const bool pow2 = (pp.R & (pp.R - 1)) == 0;
-        if (geo.items == 12) {
+        if (pp.kind == KIND_DIGIT) {
+            if (geo.items != 12 || pp.R != DIGIT_R) return hipErrorInvalidValue;
+            SGX_WC1(KIND_DIGIT, 12, 0);
+        } else if (geo.items == 12) {
             if (pow2) SGX_WC(KIND_HASH_POW2, 12); else SGX_WC(SGX_PART_HASH, 12);
         } else if (geo.items == 8) {
             if (pow2) SGX_WC(KIND_HASH_POW2, 8); else SGX_WC(SGX_PART_HASH, 8);
@@ -2208,6 +2218,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         case SGX_PART_HASH:
             if ((pp.R & (pp.R - 1)) == 0) SGX_W2(KIND_HASH_POW2); else SGX_W2(SGX_PART_HASH);
             break;
+        case KIND_DIGIT: SGX_W2(KIND_DIGIT); break;
         case SGX_PART_RANGE_I64: SGX_W2(SGX_PART_RANGE_I64); break;
         default: SGX_W2(SGX_PART_RANGE_BYTES10); break;
         }

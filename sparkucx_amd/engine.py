@@ -196,6 +196,43 @@ class ShuffleEngine:
                                      ptr if cap else None, cap, kind, lens.ctypes.data), "fetchBlocks")
         return dst, lens
 
+    def read_sorted(self, shuffle_id: int, map_ids: Sequence[int], start_partition: int, end_partition: int,
+                    dst=None) -> np.ndarray:
+        """UcxShuffleReader.read with dep.keyOrdering (sortByKey / TeraSort reduce side): the
+        canonical blocks of reducers [start, end) x map_ids, each reducer's records sorted
+        stably by key, back to back (host ndarray of bytes unless ``dst`` is given)."""
+        m = np.ascontiguousarray(map_ids, dtype=np.int64)
+        nbytes = ctypes.c_int64(0)
+        check(lib().sgx_read_sorted(self.handle, shuffle_id, m.ctypes.data, len(m), start_partition, end_partition,
+                                    None, 0, MEM_HOST, ctypes.byref(nbytes)), "readSorted")
+        if dst is None:
+            dst = np.empty(nbytes.value, dtype=np.uint8)
+        ptr, cap, kind = buffer_arg(dst)
+        check(lib().sgx_read_sorted(self.handle, shuffle_id, m.ctypes.data, len(m), start_partition, end_partition,
+                                    ptr if cap else None, cap, kind, ctypes.byref(nbytes)), "readSorted")
+        return dst
+
+    def read_grouped(self, shuffle_id: int, map_ids: Sequence[int], start_partition: int, end_partition: int,
+                     agg: int = _lib.AGG_GROUP):
+        """UcxShuffleReader.read with an aggregator (mapSideCombine = false) on (Long, Long)
+        records.  AGG_GROUP -> (keys, group_starts, values); AGG_SUM -> (keys, sums).
+        Keys ascending per reducer, values in canonical arrival order."""
+        m = np.ascontiguousarray(map_ids, dtype=np.int64)
+        nbytes = ctypes.c_int64(0)
+        check(lib().sgx_read_sorted(self.handle, shuffle_id, m.ctypes.data, len(m), start_partition, end_partition,
+                                    None, 0, MEM_HOST, ctypes.byref(nbytes)), "readGrouped")
+        n = nbytes.value // 16  # upper bound of groups and values
+        keys = np.empty(n, dtype=np.int64)
+        starts = np.empty(n, dtype=np.int64)
+        vals = np.empty(n, dtype=np.int64)
+        ng, nv = ctypes.c_int64(0), ctypes.c_int64(0)
+        check(lib().sgx_read_grouped(self.handle, shuffle_id, m.ctypes.data, len(m), start_partition, end_partition,
+                                     agg, keys.ctypes.data, starts.ctypes.data, vals.ctypes.data, n, n, MEM_HOST,
+                                     ctypes.byref(ng), ctypes.byref(nv)), "readGrouped")
+        if agg == _lib.AGG_SUM:
+            return keys[:ng.value], vals[:nv.value]
+        return keys[:ng.value], starts[:ng.value], vals[:nv.value]
+
     def progress(self) -> bool:
         return bool(check(lib().sgx_progress(self.handle), "progress"))
 

@@ -26,7 +26,7 @@ from typing import Callable, Dict, List, Optional, Sequence
 import numpy as np
 
 from . import _lib
-from ._lib import IllegalArgumentException, IllegalStateException
+from ._lib import IllegalArgumentException, IllegalStateException, UnsupportedOperationException
 from .engine import DeviceBuffer, ShuffleEngine
 
 # ---------------------------------------------------------------------------------------
@@ -68,9 +68,28 @@ class RangePartitioner:
 
 
 @dataclass
+class Aggregator:
+    """Spark's Aggregator for the two reduce-side combines the engine runs on (Long, Long)
+    records (mapSideCombine = false): "group" = groupByKey (CompactBuffer append), "sum" =
+    reduceByKey(_ + _) on Long values (wrapping)."""
+    kind: str = "group"
+
+    def __post_init__(self):
+        if self.kind not in ("group", "sum"):
+            raise IllegalArgumentException(f"unsupported aggregator {self.kind!r} (group, sum)")
+
+
+@dataclass
 class ShuffleDependency:
     partitioner: object
     recordBytes: int = 16  # fixed-width record codec: 16 B (Long, Long) or 100 B TeraSort
+    aggregator: Optional[Aggregator] = None  # dep.aggregator (reduce side only)
+    keyOrdering: bool = False                # dep.keyOrdering: sort each reducer by key
+    mapSideCombine: bool = False
+
+    def __post_init__(self):
+        if self.mapSideCombine:
+            raise UnsupportedOperationException("map-side combine is not part of the GPU path (SURVEY §8(a) a1)")
 
 
 @dataclass
@@ -390,10 +409,29 @@ class UcxShuffleReader:
         data, lens = self.manager.engine.fetch_blocks(self.handle.shuffleId, mids, rids)
         return data, lens, mids, rids
 
-    def read(self) -> np.ndarray:
-        """All records of the partition range as an (n, recordBytes) uint8 array."""
+    def _maps(self):
+        return sorted(self.mapIds if self.mapIds is not None else self.manager.known_maps(self.handle.shuffleId))
+
+    def read(self):
+        """UcxShuffleReader.read (:74-200) on the GPU.
+        * no aggregator, no keyOrdering: every record of the partition range in the canonical
+          order, as an (n, recordBytes) uint8 array;
+        * keyOrdering (sortByKey, TeraSort): the same records, each reducer sorted stably by
+          key (ExternalSorter with an ordering, :166-181);
+        * aggregator "group" (groupByKey, combineValuesByKey :155-164): (keys, group_starts,
+          values) -- keys ascending per reducer, values in arrival order;
+        * aggregator "sum" (reduceByKey(_ + _)): (keys, sums)."""
+        dep = self.handle.dependency
+        sid = self.handle.shuffleId
+        if dep.aggregator is not None:
+            if dep.recordBytes != 16:
+                raise UnsupportedOperationException("aggregation needs (Long, Long) 16 B records")
+            agg = _lib.AGG_SUM if dep.aggregator.kind == "sum" else _lib.AGG_GROUP
+            return self.manager.engine.read_grouped(sid, self._maps(), self.start, self.end, agg)
+        if dep.keyOrdering:
+            return self.manager.engine.read_sorted(sid, self._maps(), self.start, self.end).reshape(-1, dep.recordBytes)
         data, _, _, _ = self.read_blocks()
-        return data.reshape(-1, self.handle.dependency.recordBytes)
+        return data.reshape(-1, dep.recordBytes)
 
 
 # ---------------------------------------------------------------------------------------

@@ -1,0 +1,203 @@
+"""Reduce side after the fetch (UcxShuffleReader.scala:137-191): sortByKey / TeraSort
+(dep.keyOrdering) and groupByKey / reduceByKey(_ + _) (dep.aggregator, mapSideCombine =
+false) on the GPU, against the oracle's restatement (oracle.reduce_sorted /
+oracle.reduce_grouped).
+
+CPU tests pin the oracle's reduce-side functions to plain-Python restatements of Spark's
+semantics (stable TimSort order; CompactBuffer append order; wrapping Long sums).  GPU tests
+(marked gpu) run the engine through the C ABI: bit-exact sorted bytes, identical keys /
+group starts / values / sums."""
+import numpy as np
+import pytest
+
+# ---------------------------------------------------------------- CPU: oracle pinning --
+
+
+def _py_groupbykey(pairs):
+    """ExternalAppendOnlyMap + CompactBuffer, restated with a dict (insertion-ordered values)."""
+    d = {}
+    for k, v in pairs:
+        d.setdefault(k, []).append(v)
+    return d
+
+
+def _records16(keys, vals):
+    a = np.empty((len(keys), 16), np.uint8)
+    a[:, :8] = np.asarray(keys, dtype="<i8").reshape(-1, 1).view(np.uint8)
+    a[:, 8:] = np.asarray(vals, dtype="<i8").reshape(-1, 1).view(np.uint8)
+    return a
+
+
+def test_oracle_sort_is_stable_signed(oracle_lib):
+    keys = [3, -1, 3, -(2**63), 2**63 - 1, -1, 0, 3]
+    recs = _records16(keys, range(len(keys)))
+    got = oracle_lib.reduce_sorted([recs])
+    want = sorted(zip(keys, range(len(keys))), key=lambda kv: kv[0])  # Python sort is stable
+    assert np.array_equal(got, _records16([k for k, _ in want], [v for _, v in want]))
+
+
+def test_oracle_sort_terasort_unsigned_lex(oracle_lib):
+    rng = np.random.default_rng(5)
+    recs = rng.integers(0, 256, size=(300, 100), dtype=np.uint8)
+    recs[:40, :10] = recs[0, :10]  # duplicates: stability matters
+    recs[40:60, 0] = 0xFF          # high bytes sort last (unsigned)
+    got = oracle_lib.reduce_sorted([recs])
+    order = sorted(range(len(recs)), key=lambda i: bytes(recs[i, :10]))  # stable
+    assert np.array_equal(got, recs[order])
+
+
+@pytest.mark.parametrize("agg", ["group", "sum"])
+def test_oracle_grouped_matches_dict(oracle_lib, agg):
+    rng = np.random.default_rng(11)
+    seqs = []
+    for _ in range(3):
+        n = int(rng.integers(0, 200))
+        keys = rng.integers(-6, 6, size=n)
+        vals = rng.integers(-(2**63), 2**63 - 1, size=n, dtype=np.int64)
+        seqs.append(_records16(keys, vals))
+    res = oracle_lib.reduce_grouped(seqs, agg)
+    base = 0
+    for gi, s in enumerate(seqs):
+        k = s[:, :8].copy().view("<i8").reshape(-1).tolist()
+        v = s[:, 8:].copy().view("<i8").reshape(-1).tolist()
+        d = _py_groupbykey(zip(k, v))
+        for key in sorted(d):
+            if agg == "group":
+                keys, starts, vals = res
+                g = np.nonzero((starts >= base) & (keys == key))[0][0]
+                st = starts[g]
+                assert vals[st:st + len(d[key])].tolist() == d[key]
+            else:
+                keys, sums = res
+                total = sum(d[key]) % 2**64
+                total = total - 2**64 if total >= 2**63 else total
+                idx = [i for i in range(len(keys)) if keys[i] == key]
+                assert any(int(sums[i]) == total for i in idx)
+        base += len(k)
+
+
+# ---------------------------------------------------------------- GPU parity ----------
+_sid = [5000]
+
+
+def _run(sgx_lib, oracle_lib, maps, R, kind=0, bounds=None, ascending=True, rng_part=None, agg=None):
+    """Write `maps` (list of record arrays) as map ids 0..M-1, read [r0, r1) back on the
+    GPU (sorted, or grouped with `agg`), compare with the oracle."""
+    _sid[0] += 1
+    sid = _sid[0]
+    rb = maps[0].shape[1]
+    r0, r1 = rng_part or (0, R)
+    with sgx_lib.ShuffleEngine(device=0, num_chunks=5) as e:
+        e.register_shuffle(sid, R, kind, bounds, ascending, rb)
+        outs = []
+        for mid, recs in enumerate(maps):
+            e.write_map(sid, mid, np.ascontiguousarray(recs), len(recs), rb, R)
+            outs.append(oracle_lib.map_write(recs, R, kind, bounds, ascending))
+        seqs = oracle_lib.canonical_reducer_sequences(outs, R, rb)[r0:r1]
+        mids = list(range(len(maps)))
+        if agg is None:
+            got = e.read_sorted(sid, mids, r0, r1).reshape(-1, rb)
+            want = oracle_lib.reduce_sorted(seqs) if seqs else np.empty((0, rb), np.uint8)
+            assert got.shape == want.shape
+            if not np.array_equal(got, want):
+                bad = np.nonzero(np.any(got != want, axis=1))[0]
+                pytest.fail(f"{len(bad)} sorted records differ, first at {bad[:5]}")
+        else:
+            a = sgx_lib.AGG_SUM if agg == "sum" else sgx_lib.AGG_GROUP
+            got = e.read_grouped(sid, mids, r0, r1, a)
+            want = oracle_lib.reduce_grouped(seqs, agg)
+            assert len(got) == len(want)
+            for g, w in zip(got, want):
+                assert np.array_equal(g, w)
+        e.unregister_shuffle(sid)
+
+
+def _zipfish(rng, n, K=50):
+    keys = (rng.zipf(1.3, size=n) % K) - K // 3  # heavy duplicates, negatives
+    return _records16(keys, rng.integers(-(2**63), 2**63 - 1, size=n, dtype=np.int64))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 7, 256, 1024, 4096])
+def test_sorted_hash_uniform(sgx_lib, oracle_lib, R):
+    maps = [oracle_lib.gen_uniform16(n, 100 + i, value_base=i << 32) for i, n in enumerate((30_000, 0, 17_777))]
+    _run(sgx_lib, oracle_lib, maps, R)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [3, 1024])
+def test_sorted_hash_duplicates_and_signs(sgx_lib, oracle_lib, R):
+    rng = np.random.default_rng(R)
+    maps = [_zipfish(rng, 20_000), _zipfish(rng, 5_001)]
+    maps[0][:3, :8] = np.array([-(2**63), 2**63 - 1, -1], dtype="<i8").reshape(-1, 1).view(np.uint8)
+    _run(sgx_lib, oracle_lib, maps, R)
+    _run(sgx_lib, oracle_lib, maps, R, rng_part=(1, R) if R > 1 else (0, 1))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ascending", [True, False])
+def test_sorted_range_i64(sgx_lib, oracle_lib, ascending):
+    rng = np.random.default_rng(3)
+    maps = [_zipfish(rng, 12_000, K=5000), oracle_lib.gen_uniform16(9_000, 7)]
+    allk = np.concatenate([m[:, :8].copy().view("<i8").reshape(-1) for m in maps])
+    bounds = np.unique(np.sort(rng.choice(allk, 63)))
+    _run(sgx_lib, oracle_lib, maps, len(bounds) + 1, sgx_lib.PART_RANGE_I64, bounds, ascending)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("kind", ["range", "hash"])
+def test_sorted_terasort(sgx_lib, oracle_lib, kind):
+    maps = [oracle_lib.gen_terasort100(n, 40 + i) for i, n in enumerate((6_000, 2_345))]
+    maps[0][100:400, :10] = maps[0][99, :10]  # duplicate keys across a tile: stability
+    R = 64
+    if kind == "range":
+        rng = np.random.default_rng(1)
+        sample = np.concatenate(maps)[rng.choice(8345, 20 * R, replace=False), :10]
+        sample = sample[np.lexsort(sample.T[::-1])]
+        bounds = np.ascontiguousarray(sample[np.linspace(0, len(sample) - 1, R - 1).astype(int)])
+        _run(sgx_lib, oracle_lib, maps, R, sgx_lib.PART_RANGE_BYTES10, bounds)
+    else:
+        _run(sgx_lib, oracle_lib, maps, R)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("agg", ["group", "sum"])
+@pytest.mark.parametrize("R", [1, 200, 1024])
+def test_grouped(sgx_lib, oracle_lib, agg, R):
+    rng = np.random.default_rng(R + len(agg))
+    maps = [_zipfish(rng, 40_000, K=3000), oracle_lib.gen_uniform16(10_000, 9), _zipfish(rng, 1)]
+    _run(sgx_lib, oracle_lib, maps, R, agg=agg)
+
+
+@pytest.mark.gpu
+def test_grouped_empty_range(sgx_lib, oracle_lib):
+    maps = [oracle_lib.gen_uniform16(1000, 1)]
+    _run(sgx_lib, oracle_lib, maps, 16, rng_part=(5, 5), agg="group")
+    _run(sgx_lib, oracle_lib, maps, 16, rng_part=(5, 5))
+
+
+@pytest.mark.gpu
+def test_reader_dispatch(sgx_lib, oracle_lib, tmp_path):
+    """UcxShuffleReader.read picks the path from the dependency (aggregator / keyOrdering)."""
+    recs = _zipfish(np.random.default_rng(0), 5000, K=100)
+    mgr = sgx_lib.UcxShuffleManager(device=0, localDir=str(tmp_path))
+    try:
+        out, cnt = oracle_lib.map_write(recs, 8)
+        seqs = oracle_lib.canonical_reducer_sequences([(out, cnt)], 8, 16)
+        for sid, dep in enumerate([
+                sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(8), 16, keyOrdering=True),
+                sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(8), 16, aggregator=sgx_lib.Aggregator("group")),
+                sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(8), 16, aggregator=sgx_lib.Aggregator("sum"))]):
+            h = mgr.registerShuffle(sid, dep)
+            w = mgr.getWriter(h, 0)
+            w.write(recs)
+            w.stop(True)
+            got = mgr.getReader(h, 2, 6).read()
+            if dep.keyOrdering:
+                assert np.array_equal(got, oracle_lib.reduce_sorted(seqs[2:6]))
+            else:
+                want = oracle_lib.reduce_grouped(seqs[2:6], dep.aggregator.kind)
+                for g, wv in zip(got, want):
+                    assert np.array_equal(g, wv)
+    finally:
+        mgr.stop()

@@ -1,0 +1,79 @@
+#!/usr/bin/env python3
+"""Reduce-side timings on one GPU (UcxShuffleReader.read after the fetch): one map of N
+records (uniform or Zipf 16 B, or TeraSort 100 B with sampled RangePartitioner bounds) is
+written, then every reducer is read back sorted by key (sortByKey / TeraSort) or grouped
+(groupByKey, reduceByKey sum), on device memory.  Prints one JSON line per case with the
+engine's per-stage HIP-event times (regroup = fetch gather, sort = LSD digit passes +
+partitioner pass, group = grouping kernels)."""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=1 << 26)
+    ap.add_argument("--partitions", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--cases", default="sorted:uniform,group:uniform,sum:zipf,sorted:terasort")
+    a = ap.parse_args()
+    import numpy as np
+
+    import sparkucx_amd as sgx
+
+    e = sgx.ShuffleEngine(0)
+    R = a.partitions
+    sid = 0
+    for case in a.cases.split(","):
+        op, dist = case.split(":")
+        sid += 1
+        n = a.records if dist != "terasort" else a.records * 16 // 100
+        rb = 100 if dist == "terasort" else 16
+        buf = e.alloc(n * rb)
+        kind, bounds = sgx.PART_HASH, None
+        if dist == "uniform":
+            e.gen_uniform16(buf, n, 0x5EEDC0DE)
+        elif dist == "zipf":
+            r = np.arange(1, (1 << 24) + 1, dtype=np.float64)
+            cdf = np.cumsum(r ** -1.1)
+            cdf /= cdf[-1]
+            e.gen_zipf16(buf, n, 0x5EEDC0DE, cdf)
+        else:
+            e.gen_terasort100(buf, n, 0x5EEDC0DE)
+            keys = buf.to_numpy(min(n, 1 << 20) * 100).reshape(-1, 100)[:, :10]
+            rng = np.random.default_rng(1)
+            sample = keys[rng.choice(len(keys), 20 * R, replace=False)]
+            sample = sample[np.lexsort(sample.T[::-1])]
+            bounds = np.ascontiguousarray(sample[np.linspace(0, len(sample) - 1, R - 1).astype(int)])
+            kind = sgx.PART_RANGE_BYTES10
+        e.register_shuffle(sid, R, kind, bounds, True, rb)
+        e.write_map(sid, 0, buf, n, rb, R)
+        dst = e.alloc(n * rb) if op == "sorted" else None
+        e.stats_reset()
+        walls = []
+        for _ in range(a.iters):
+            t0 = time.perf_counter()
+            if op == "sorted":
+                e.read_sorted(sid, [0], 0, R, dst)
+            else:
+                e.read_grouped(sid, [0], 0, R, sgx.AGG_SUM if op == "sum" else sgx.AGG_GROUP)
+            walls.append(time.perf_counter() - t0)
+        st = e.stats()
+        ms = {k: round(v / max(1, st.count[k]), 3) for k, v in st.ms.items() if st.count[k]}
+        dev_ms = ms.get("regroup", 0) + ms.get("sort", 0) + ms.get("group", 0)
+        print(json.dumps({"case": case, "records": n, "record_bytes": rb, "partitions": R, "stages_ms": ms,
+                          "device_ms": round(dev_ms, 3), "device_GBs": round(n * rb / dev_ms / 1e6, 1),
+                          "wall_ms_min": round(min(walls) * 1e3, 2)}), flush=True)
+        e.unregister_shuffle(sid)
+        if dst is not None:
+            dst.free()
+        buf.free()
+    e.close()
+
+
+if __name__ == "__main__":
+    main()
