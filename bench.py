@@ -164,6 +164,11 @@ def main():
         owner = (np.arange(R, dtype=np.int64) * world) // R
         sent = float(lens[owner != rank].sum())
         a2a_ms = st.ms["alltoall"] / max(1, st.count["alltoall"])
+        # bytes each rank receives (load balance of the reducer ranges, config C3)
+        recv = torch.zeros(world, dtype=torch.float64)
+        for j in range(world):
+            recv[j] = float(lens[owner == j].sum())
+        dist.all_reduce(recv, op=dist.ReduceOp.SUM)
         t = torch.tensor([sent, a2a_ms], dtype=torch.float64)
         tmax = t.clone()
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
@@ -173,6 +178,7 @@ def main():
         xgmi = {"bound": "xgmi", "achieved": round(ach, 1), "peak": peak, "unit": "GB/s",
                 "frac": round(ach / peak, 4), "bytes_per_step": float(t[0]),
                 "alltoall_ms_max_rank": round(float(tmax[1]), 4),
+                "recv_bytes_max_over_mean": round(float(recv.max() / recv.mean()), 4),
                 "note": "all ranks' cross-GPU bytes / slowest rank's ncclAllToAllv time; peak = P(P-1) x 153 GB/s"}
 
     if rank == 0:

@@ -1224,6 +1224,49 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     }
     __syncthreads();
     uint32_t bad = 0;
+    // ---- drain: whole lines out, the rest stays in this lane's registers (dk/dpos).
+    //      LATE (A/B, DIAG 16): the drain of tile t runs after tile t+1's ranking, so the
+    //      wait for tile t+1's loads (the compiler's vmcnt(0): pending loads + stores count
+    //      as out of order) does not also wait for tile t's stores.  Measured slightly
+    //      slower (C1: 1.90-1.97 vs 1.86-1.95 ms): the store drain is not what bounds K4.
+    constexpr bool LATE = (DIAG & 16) != 0;
+    uint32_t total_prev = 0;
+    auto drain = [&](const uint32_t ntot) {
+        dmask = 0;
+#pragma unroll
+        for (int k0 = 0; k0 < SI; k0 += 8) {
+            uint2 dm[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t s = (uint32_t)((k0 + q) * T + tid);
+                dk[k0 + q] = stage[s];  // slots past `total` hold stale records: never used
+            }
+#pragma unroll
+            for (int q = 0; q < 8; ++q) dm[q] = dlim[pid_of<KIND>(dk[k0 + q].x, dk[k0 + q].y, dk[k0 + q].z, pp)];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) {
+                const uint32_t s = (uint32_t)((k0 + q) * T + tid);
+                const bool live = s < ntot;
+                const uint32_t pos = dm[q].x + s;
+                const bool wr = live && pos < dm[q].y;
+                dpos[k0 + q] = pos;
+                if constexpr ((DIAG & 12) != 0 && (DIAG & 1) == 0) {
+                    // A/B (DIAG 4, 8): branch-free, every lane stores, masked-off lanes into
+                    // this workgroup's junk line, so the next tile can wait for its loads
+                    // only (DIAG 8: vmcnt(SI)) instead of the compiler's vmcnt(0) behind
+                    // conditional stores.  Measured slower (C1: 2.01-2.04 vs 1.92-1.96 ms):
+                    // the junk lines cost more than the per-tile store drain.
+                    u32x4 *dst = wr ? out + pos : junk;
+                    *dst = dk[k0 + q];
+                } else if constexpr ((DIAG & 1) == 0) {
+                    if (wr) out[pos] = dk[k0 + q];
+                } else {
+                    if (wr) asm volatile("" ::"v"(dk[k0 + q].x), "v"(dk[k0 + q].w), "v"(pos));
+                }
+                dmask |= (live && !wr) ? 1u << (k0 + q) : 0u;
+            }
+        }
+    };
     for (int64_t t = 0; t < ntiles; ++t) {
         const bool last = t == ntiles - 1;
         // ---- rank the new records: one LDS atomic each, issued back to back in item order
@@ -1246,6 +1289,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             const uint32_t inc = valid[k] ? 1u << ((pid[k] & 1u) << 4) : 0u;
             old[k] = __hip_atomic_fetch_add(myrow32 + (pid[k] >> 1), inc, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        if constexpr (LATE) {
+            if (t > 0) drain(total_prev);
         }
         lds_barrier();  // B1
 
@@ -1335,43 +1381,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                     rec[k] = cb[valid[k] ? i : 0];
             }
         }
-        lds_barrier();  // B4
-
-        // ---- drain: whole lines out, the rest stays in this lane's registers (dk/dpos)
-        dmask = 0;
-#pragma unroll
-        for (int k0 = 0; k0 < SI; k0 += 8) {
-            uint2 dm[8];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const uint32_t s = (uint32_t)((k0 + q) * T + tid);
-                dk[k0 + q] = stage[s];  // slots past `total` hold stale records: never used
-            }
-#pragma unroll
-            for (int q = 0; q < 8; ++q) dm[q] = dlim[pid_of<KIND>(dk[k0 + q].x, dk[k0 + q].y, dk[k0 + q].z, pp)];
-#pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const uint32_t s = (uint32_t)((k0 + q) * T + tid);
-                const bool live = s < total;
-                const uint32_t pos = dm[q].x + s;
-                const bool wr = live && pos < dm[q].y;
-                dpos[k0 + q] = pos;
-                if constexpr ((DIAG & 12) != 0 && (DIAG & 1) == 0) {
-                    // A/B (DIAG 4, 8): branch-free, every lane stores, masked-off lanes into
-                    // this workgroup's junk line, so the next tile can wait for its loads
-                    // only (DIAG 8: vmcnt(SI)) instead of the compiler's vmcnt(0) behind
-                    // conditional stores.  Measured slower (C1: 2.01-2.04 vs 1.92-1.96 ms):
-                    // the junk lines cost more than the per-tile store drain.
-                    u32x4 *dst = wr ? out + pos : junk;
-                    *dst = dk[k0 + q];
-                } else if constexpr ((DIAG & 1) == 0) {
-                    if (wr) out[pos] = dk[k0 + q];
-                } else {
-                    if (wr) asm volatile("" ::"v"(dk[k0 + q].x), "v"(dk[k0 + q].w), "v"(pos));
-                }
-                dmask |= (live && !wr) ? 1u << (k0 + q) : 0u;
-            }
-        }
+        lds_barrier();  // B4 (LATE: the drain of this tile follows the next tile's ranking)
+        if constexpr (!LATE) drain(total);
+        else total_prev = total;
+    }
+    if constexpr (LATE) {
+        if (ntiles > 0) drain(total_prev);
     }
     if (bad) atomicOr(err, SCATTER_OOB);
 }
@@ -2102,6 +2117,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         else if (NI == 8 && geo.nt == 103) SGX_WC1(K, 8, 3);                                     \
         else if (NI == 8 && geo.nt == 104) SGX_WC1(K, 8, 4);                                     \
         else if (NI == 8 && geo.nt == 108) SGX_WC1(K, 8, 8);                                     \
+        else if (NI == 8 && geo.nt == 116) SGX_WC1(K, 8, 16);                                    \
         else SGX_WC1(K, NI, 0);                                                                  \
     } while (0)
         const bool pow2 = (pp.R & (pp.R - 1)) == 0;
