@@ -166,6 +166,23 @@ int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, 
                      int64_t *group_starts, int64_t *values, int64_t cap_groups, int64_t cap_values,
                      int32_t mem_kind, int64_t *out_groups, int64_t *out_values);
 
+/* ---- RangePartitioner's bounds from the data (Spark 3.0.1 RangePartitioner: the
+ *      rangeBounds initialiser, RangePartitioner.sketch and RangePartitioner.determineBounds;
+ *      the partitioner is built where the dependency is, UcxShuffleManager.scala:50).
+ * batches[i] (nrecords[i] records of record_bytes, memory kind mem_kind) is input partition i
+ * of the RDD with id rdd_id; keys are signed Longs (16 B records) or 10-byte unsigned keys
+ * (100 B records).  sampleSize = min(sample_points_per_partition * num_partitions, 1e6),
+ * k = ceil(3 * sampleSize / nbatches) keys per partition by reservoir sampling with
+ * XORShiftRandom(byteswap32(i ^ (rdd_id << 16))) -- on the GPU, every record's draw in
+ * parallel by GF(2) jump-ahead -- then determineBounds on the host.  Writes up to
+ * num_partitions - 1 bounds (int64 or 10-byte keys) to out_bounds (host) and their count to
+ * *out_nbounds (fewer when keys repeat; the shuffle then has *out_nbounds + 1 partitions).
+ * SGX_ERR_UNSUPPORTED when a partition is imbalanced enough for Spark's re-sampling pass
+ * (fraction * n > k), which this engine does not reproduce. */
+int sgx_range_bounds(sgx_engine *e, const void *const *batches, const int64_t *nrecords, int32_t nbatches,
+                     int32_t record_bytes, int32_t mem_kind, int32_t num_partitions, int32_t rdd_id,
+                     int32_t sample_points_per_partition, void *out_bounds, int32_t *out_nbounds);
+
 /* ---- measurement: HIP-event times of the last write_map / exchange stages, and
  *      accumulated per-stage sums since the last reset (index = enum sgx_stage). ---- */
 /* SGX_STAGE_REGROUP times the fetch-side gather kernel (blocks into request order). */

@@ -255,3 +255,168 @@ def map_side_shuffle(records: Sequence[Tuple[int, int]], num_partitions: int):
 def reducer_owner(reduce_id: int, num_partitions: int, world: int) -> int:
     """Contiguous reducer ownership used by the multi-GPU exchange: ``floor(r*P/R)``."""
     return (reduce_id * world) // num_partitions
+
+
+# ------------------------------------------------------------------ RangePartitioner bounds
+# Spark 3.0.1 RangePartitioner (spark-core, external): the rangeBounds initialiser,
+# RangePartitioner.sketch, SamplingUtils.reservoirSampleAndCount, XORShiftRandom (+ its
+# hashSeed over scala.util.hashing.MurmurHash3.bytesHash) and RangePartitioner.determineBounds,
+# restated sequentially.  Parity of this row is UNPINNED: no Spark runs here and the reference
+# holds no fixture for it (DESIGN.md §10).
+M32 = 0xFFFFFFFF
+M64 = 0xFFFFFFFFFFFFFFFF
+
+
+def _rotl32(x, r):
+    return ((x << r) | (x >> (32 - r))) & M32
+
+
+def _mm3_mix_last(h, k):
+    k = (k * 0xCC9E2D51) & M32
+    k = _rotl32(k, 15)
+    k = (k * 0x1B873593) & M32
+    return h ^ k
+
+
+def _mm3_mix(h, k):
+    h = _mm3_mix_last(h, k)
+    h = _rotl32(h, 13)
+    return (h * 5 + 0xE6546B64) & M32
+
+
+def murmur3_bytes_hash(data: bytes, seed: int) -> int:
+    """scala.util.hashing.MurmurHash3.bytesHash (unsigned 32-bit result)."""
+    h = seed & M32
+    n = len(data)
+    i = 0
+    while n - i >= 4:
+        k = data[i] | (data[i + 1] << 8) | (data[i + 2] << 16) | (data[i + 3] << 24)
+        h = _mm3_mix(h, k)
+        i += 4
+    rem = n - i
+    k = 0
+    if rem == 3:
+        k ^= data[i + 2] << 16
+    if rem >= 2:
+        k ^= data[i + 1] << 8
+    if rem >= 1:
+        k ^= data[i]
+        h = _mm3_mix_last(h, k)
+    h ^= n
+    h ^= h >> 16
+    h = (h * 0x85EBCA6B) & M32
+    h ^= h >> 13
+    h = (h * 0xC2B2AE35) & M32
+    h ^= h >> 16
+    return h
+
+
+def xorshift_hash_seed(seed: int) -> int:
+    b = (seed & M64).to_bytes(8, "big")  # ByteBuffer.putLong: big-endian
+    lo = murmur3_bytes_hash(b, 0x3C074A61)  # MurmurHash3.arraySeed
+    hi = murmur3_bytes_hash(b, lo)
+    return (hi << 32) | lo
+
+
+class XORShiftRandom:
+    """org.apache.spark.util.random.XORShiftRandom: next(bits) + java.util.Random.nextDouble."""
+
+    def __init__(self, seed: int):
+        self.s = xorshift_hash_seed(seed)
+
+    def next(self, bits: int) -> int:
+        s = self.s
+        s ^= (s << 21) & M64
+        s ^= s >> 35
+        s ^= (s << 4) & M64
+        self.s = s
+        return s & ((1 << bits) - 1)
+
+    def next_double(self) -> float:
+        return ((self.next(26) << 27) + self.next(27)) * (2.0 ** -53)
+
+
+def byteswap32(v: int) -> int:
+    hc = (v * 0x9E3775CD) & M32
+    hc = int.from_bytes(hc.to_bytes(4, "little"), "big")
+    return to_i32(hc * 0x9E3775CD)
+
+
+def reservoir_sample_and_count(keys: Sequence, k: int, seed: int):
+    """SamplingUtils.reservoirSampleAndCount."""
+    res = list(keys[:k])
+    if len(keys) < k:
+        return res, len(keys)
+    rnd = XORShiftRandom(seed)
+    l = k
+    for item in keys[k:]:
+        l += 1
+        r = int(rnd.next_double() * l)  # .toLong truncates; the product is non-negative
+        if r < k:
+            res[r] = item
+    return res, l
+
+
+def range_bounds(partitions_keys: Sequence[Sequence], num_partitions: int, rdd_id: int = 0,
+                 sample_points_per_partition: int = 20, lt=None):
+    """RangePartitioner.rangeBounds for input partitions given as key lists (no re-sampling
+    of imbalanced partitions: raises instead, as the engine does)."""
+    import math
+
+    if num_partitions <= 1 or not partitions_keys:
+        return []
+    sample_size = min(float(sample_points_per_partition) * num_partitions, 1e6)
+    k = int(math.ceil(3.0 * sample_size / len(partitions_keys)))
+    sketched = []
+    for idx, keys in enumerate(partitions_keys):
+        seed = byteswap32(to_i32(idx ^ (rdd_id << 16)))
+        sample, n = reservoir_sample_and_count(list(keys), k, seed)
+        sketched.append((idx, n, sample))
+    num_items = sum(n for _, n, _ in sketched)
+    if num_items == 0:
+        return []
+    fraction = min(sample_size / max(num_items, 1), 1.0)
+    cand = []
+    for idx, n, sample in sketched:
+        if fraction * n > k:
+            raise NotImplementedError("imbalanced partition: Spark re-samples it")
+        if sample:
+            w = float(np_float32(n / len(sample)))
+            cand.extend((key, w) for key in sample)
+    return determine_bounds(cand, min(num_partitions, len(cand)), lt)
+
+
+def np_float32(x: float) -> float:
+    import struct as _s
+
+    return _s.unpack("<f", _s.pack("<f", x))[0]
+
+
+def determine_bounds(candidates, partitions: int, lt=None):
+    """RangePartitioner.determineBounds: stable sort by key, weights summed in sorted order."""
+    import functools
+
+    if lt is None:
+        ordered = sorted(candidates, key=lambda kw: kw[0])
+    else:
+        ordered = sorted(candidates, key=functools.cmp_to_key(
+            lambda a, b: -1 if lt(a[0], b[0]) else (1 if lt(b[0], a[0]) else 0)))
+    gt = (lambda a, b: a > b) if lt is None else (lambda a, b: lt(b, a))
+    sum_w = 0.0
+    for _, w in ordered:
+        sum_w += w
+    step = sum_w / partitions
+    cum, target = 0.0, step
+    bounds, prev = [], None
+    i = j = 0
+    while i < len(ordered) and j < partitions - 1:
+        key, w = ordered[i]
+        cum += w
+        if cum >= target:
+            if prev is None or gt(key, prev):
+                bounds.append(key)
+                target += step
+                j += 1
+                prev = key
+        i += 1
+    return bounds

@@ -110,6 +110,11 @@ hipError_t launch_group_emit(const void *rec, int64_t n, const uint32_t *flags, 
 int64_t prefix64_blocks(int64_t n);
 hipError_t launch_group_sums(const void *rec, int64_t n, const int64_t *starts, int64_t ngroups,
                              uint64_t *bsum, uint64_t *P, int64_t *sums, hipStream_t st);
+// RangePartitioner.sketch (sgx_sample.hip): reservoir of k keys of n records, XORShiftRandom
+// state s0 (already hashSeed'ed), jump = [48][64] column-form powers M^(2^t) of one step.
+int64_t reservoir_threads(int64_t n, int64_t k);
+hipError_t launch_reservoir(const void *recs, int64_t n, int rb, int key_bytes, int64_t k, uint64_t s0,
+                            const uint64_t *jump_dev, long long *winner, void *out_keys, hipStream_t st);
 hipError_t launch_gen_uniform16(void *dst, int64_t n, uint64_t seed, int64_t value_base,
                                 hipStream_t stream);
 hipError_t launch_gen_zipf16(void *dst, int64_t n, uint64_t seed, int64_t value_base,

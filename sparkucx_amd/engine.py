@@ -233,6 +233,26 @@ class ShuffleEngine:
             return keys[:ng.value], vals[:nv.value]
         return keys[:ng.value], starts[:ng.value], vals[:nv.value]
 
+    def range_bounds(self, batches: Sequence, nrecords: Sequence[int], record_bytes: int, num_partitions: int,
+                     rdd_id: int = 0, sample_points_per_partition: int = 20) -> np.ndarray:
+        """RangePartitioner.rangeBounds from the data (sketch on the GPU + determineBounds):
+        int64[nb] for 16 B records, uint8[nb, 10] for 100 B TeraSort records.  ``batches``
+        are the RDD's input partitions (all host ndarrays or all device buffers)."""
+        args = [buffer_arg(b) for b in batches]
+        kinds = {k for _, _, k in args}
+        if len(kinds) > 1:
+            raise _lib.IllegalArgumentException("mixed host / device batches")
+        ptrs = (ctypes.c_void_p * max(1, len(args)))(*[p for p, _, _ in args])
+        ns = np.ascontiguousarray(nrecords, dtype=np.int64)
+        kb = 8 if record_bytes == 16 else 10
+        out = np.empty(max(1, num_partitions - 1) * kb, dtype=np.uint8)
+        nb = ctypes.c_int32(0)
+        check(lib().sgx_range_bounds(self.handle, ptrs, ns.ctypes.data, len(args), record_bytes,
+                                     kinds.pop() if kinds else MEM_HOST, num_partitions, rdd_id,
+                                     sample_points_per_partition, out.ctypes.data, ctypes.byref(nb)), "rangeBounds")
+        out = out[:nb.value * kb]
+        return out.view("<i8").copy() if kb == 8 else out.reshape(-1, 10).copy()
+
     def progress(self) -> bool:
         return bool(check(lib().sgx_progress(self.handle), "progress"))
 

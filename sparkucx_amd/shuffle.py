@@ -66,6 +66,15 @@ class RangePartitioner:
         n = b.shape[0] if b.ndim else 0
         return n + 1
 
+    @classmethod
+    def fromData(cls, engine, partitions: Sequence, nrecords: Sequence[int], recordBytes: int, numPartitions: int,
+                 rddId: int = 0, ascending: bool = True, samplePointsPerPartitionHint: int = 20):
+        """new RangePartitioner(partitions, rdd, ascending, samplePointsPerPartitionHint): the
+        bounds come from RangePartitioner.sketch (GPU reservoir sampling with Spark's seeds)
+        and determineBounds.  ``partitions`` are the RDD's input partitions (record batches)."""
+        b = engine.range_bounds(partitions, nrecords, recordBytes, numPartitions, rddId, samplePointsPerPartitionHint)
+        return cls(b, ascending)
+
 
 @dataclass
 class Aggregator:
