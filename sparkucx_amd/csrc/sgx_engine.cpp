@@ -191,6 +191,8 @@ struct sgx_engine {
     DevBuf sort_buf[2], sort_err, grp_flags, grp_offs, grp_status, grp_out, grp_prefix;
     // RangePartitioner.sketch: XORShiftRandom jump table, reservoir winners and keys
     DevBuf jump_dev, sample_winner, sample_keys;
+    DevBuf digit_hist;               // sorted read: [digits][256] histogram of the fetched keys
+    int sort_skip = 1;               // SGX_SORT_SKIP=0: run every digit pass (A/B, tests)
     DevBuf ag_send, ag_recv, recv, items_dev, chain_buf, gather_stage;
     HostPinned gather_items;
     HostPinned ag_host;
@@ -284,6 +286,7 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->s_hist, hipStreamNonBlocking));
     if (const char *d = getenv("SGX_PIPELINE")) e->pipeline = atoi(d);
+    if (const char *d = getenv("SGX_SORT_SKIP")) e->sort_skip = atoi(d);
     *out = e.release();
     return SGX_OK;
 }
@@ -319,7 +322,8 @@ extern "C" void sgx_destroy(sgx_engine *e) {
         w.used = nullptr;
     }
     for (DevBuf *b : {&e->sort_buf[0], &e->sort_buf[1], &e->sort_err, &e->grp_flags, &e->grp_offs, &e->grp_status,
-                      &e->grp_out, &e->grp_prefix, &e->jump_dev, &e->sample_winner, &e->sample_keys})
+                      &e->grp_out, &e->grp_prefix, &e->jump_dev, &e->sample_winner, &e->sample_keys,
+                      &e->digit_hist})
         b->release();
     for (DevBuf *b : {&e->junk, &e->input_stage, &e->ag_send,
                       &e->ag_recv, &e->recv, &e->items_dev, &e->chain_buf, &e->gather_stage})
@@ -1172,10 +1176,23 @@ static int sort_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids
     hipEvent_t t0 = e->ev(), t1 = e->ev();
     HIP_TRY(hipEventRecord(t0, st));
     // LSD digit passes, least significant byte first: i64 keys (bytes 0..7 of the record,
-    // sign flip on the top byte), or TeraSort's 10-byte big-endian keys (bytes 9..0)
+    // sign flip on the top byte), or TeraSort's 10-byte big-endian keys (bytes 9..0).  One
+    // read of the keys histograms every digit; a digit with a single non-empty bucket is
+    // the identity permutation and is skipped.
     const int ndig = rb == 16 ? 8 : 10;
+    SGX_TRY(e->digit_hist.ensure((size_t)ndig * 256 * 4));
+    HIP_TRY(launch_digit_hist(e->sort_buf[0].p, n, rb, (uint32_t *)e->digit_hist.p, e->num_cus, st));
+    std::vector<uint32_t> dh((size_t)ndig * 256);
+    HIP_TRY(hipMemcpyAsync(dh.data(), e->digit_hist.p, dh.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     int cur = 0, np = 0;
-    for (int d = 0; d < ndig; ++d, ++np) {
+    for (int d = 0; d < ndig; ++d) {
+        const int byte = rb == 16 ? d : 9 - d;  // digit d of the LSD order
+        bool trivial = false;
+        for (int b = 0; b < 256; ++b)
+            if (dh[(size_t)byte * 256 + (size_t)b] == (uint32_t)n) trivial = true;
+        if (trivial && e->sort_skip) continue;
+        ++np;
         PartParams dp{};
         dp.kind = KIND_DIGIT;
         dp.R = DIGIT_R;
@@ -1183,7 +1200,7 @@ static int sort_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids
         dp.dshift = rb == 16 ? 8u * (uint32_t)d : 8u * (uint32_t)(9 - d);
         dp.dflip = (rb == 16 && d == 7) ? 0x80u : 0u;
         SGX_TRY(partition_pass(e, e->sort_buf[cur].p, e->sort_buf[cur ^ 1].p, n, rb, dp, (int32_t)DIGIT_R,
-                               KIND_DIGIT, 0, SGX_MEM_DEVICE, nullptr, errs + np, false));
+                               KIND_DIGIT, 0, SGX_MEM_DEVICE, nullptr, errs + np - 1, false));
         cur ^= 1;
     }
     // records back into reducer order: the shuffle's own partitioner, stable (an ascending

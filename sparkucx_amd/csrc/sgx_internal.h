@@ -104,6 +104,7 @@ hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, i
 // items: [n][3] int64 {src address, dst address, bytes} (device memory on both sides).
 hipError_t launch_gather_items(const int64_t *items, int64_t n_items, int align, hipStream_t stream);
 // Reduce side (sgx_reduce.hip), key-sorted (Long, Long) records
+hipError_t launch_digit_hist(const void *rec, int64_t n, int rb, uint32_t *hist, int num_cus, hipStream_t st);
 hipError_t launch_group_flags(const void *rec, int64_t n, uint32_t *flags, hipStream_t st);
 hipError_t launch_group_emit(const void *rec, int64_t n, const uint32_t *flags, const uint32_t *offs,
                              int64_t *keys, int64_t *starts, int64_t *values, hipStream_t st);

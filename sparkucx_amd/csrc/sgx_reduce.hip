@@ -12,6 +12,8 @@
 // value} little-endian, 16 B each, n < 2^31.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "sgx_internal.h"
 
 namespace sgx {
@@ -133,6 +135,49 @@ __global__ __launch_bounds__(RT) void k_group_sums(const uint64_t *__restrict__ 
     if (g >= ngroups) return;
     const int64_t s = starts[g], e = g + 1 < ngroups ? starts[g + 1] : n;
     sums[g] = (int64_t)(P[e - 1] - (s > 0 ? P[s - 1] : 0ull));
+}
+
+// All digit histograms of the sort in one read: hist[d][b] = records whose digit d (byte
+// dshift/8 of the record, the top byte of a Long key sign-flipped) is b.  A digit whose
+// histogram has a single non-empty bucket is a no-op pass (keys that share that byte) and
+// sgx_read_sorted skips it -- Zipf ranks or small-range ids leave most high bytes constant.
+template <int RB>
+__global__ __launch_bounds__(RT) void k_digit_hist(const uint8_t *__restrict__ rec, int64_t n,
+                                                   uint32_t *__restrict__ hist) {
+    constexpr int ND = RB == 16 ? 8 : 10;
+    __shared__ uint32_t h[ND * 256];
+    for (int i = threadIdx.x; i < ND * 256; i += RT) h[i] = 0;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * RT;
+    for (int64_t i = (int64_t)blockIdx.x * RT + threadIdx.x; i < n; i += stride) {
+        const uint8_t *r = rec + i * RB;
+        uint32_t w[3];
+        w[0] = *(const uint32_t *)r;
+        w[1] = *(const uint32_t *)(r + 4);
+        w[2] = ND > 8 ? *(const uint32_t *)(r + 8) : 0u;
+#pragma unroll
+        for (int d = 0; d < ND; ++d) {
+            uint32_t b = (w[d >> 2] >> ((d & 3) * 8)) & 0xFFu;
+            if (RB == 16 && d == 7) b ^= 0x80u;
+            atomicAdd(&h[d * 256 + b], 1u);
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < ND * 256; i += RT)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+hipError_t launch_digit_hist(const void *rec, int64_t n, int rb, uint32_t *hist, int num_cus, hipStream_t st) {
+    const int nd = rb == 16 ? 8 : 10;
+    hipError_t e = hipMemsetAsync(hist, 0, (size_t)nd * 256 * 4, st);
+    if (e != hipSuccess || n <= 0) return e;
+    const int64_t want = (n + RT * 16 - 1) / (RT * 16);
+    const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(want, (int64_t)num_cus * 4));
+    if (rb == 16)
+        hipLaunchKernelGGL(k_digit_hist<16>, dim3(grid), dim3(RT), 0, st, (const uint8_t *)rec, n, hist);
+    else
+        hipLaunchKernelGGL(k_digit_hist<100>, dim3(grid), dim3(RT), 0, st, (const uint8_t *)rec, n, hist);
+    return hipGetLastError();
 }
 
 hipError_t launch_group_flags(const void *rec, int64_t n, uint32_t *flags, hipStream_t st) {

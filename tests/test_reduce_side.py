@@ -201,3 +201,25 @@ def test_reader_dispatch(sgx_lib, oracle_lib, tmp_path):
                     assert np.array_equal(g, wv)
     finally:
         mgr.stop()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("skip", ["1", "0"])
+@pytest.mark.parametrize("keys", ["small_nonneg", "all_equal", "two_values_high_byte"])
+def test_sorted_trivial_digits(sgx_lib, oracle_lib, monkeypatch, skip, keys):
+    """Digit passes whose byte is constant over the fetched keys are skipped (SGX_SORT_SKIP=1,
+    the default); the result must not depend on it."""
+    monkeypatch.setenv("SGX_SORT_SKIP", skip)
+    rng = np.random.default_rng(len(keys))
+    n = 30_000
+    if keys == "small_nonneg":
+        k = rng.integers(0, 3000, size=n)
+    elif keys == "all_equal":
+        k = np.full(n, -12345)
+    else:
+        k = np.where(rng.random(n) < 0.5, 1 << 56, -(1 << 60)) + 7
+    maps = [_records16(k[: n // 2], rng.integers(0, 1 << 62, size=n // 2)),
+            _records16(k[n // 2:], rng.integers(0, 1 << 62, size=n - n // 2))]
+    for R in (1, 16):
+        _run(sgx_lib, oracle_lib, maps, R)
+        _run(sgx_lib, oracle_lib, maps, R, agg="group")
