@@ -472,7 +472,9 @@ static int partition_pass(sgx_engine *e, const void *in, void *out, int64_t n, i
         // write-combining K4 (whole 128 B lines only) where its LDS fits (R <= 1024)
         if (e->wc && e->sc_waves == 0 && e->sc_items == 0) {
             ScatterGeom w = scatter_geom16_wc((uint32_t)R);
-            if ((e->wc_diag >= 1 && e->wc_diag <= 4) || e->wc_diag == 8 || e->wc_diag == 16) w.nt = 100 + e->wc_diag;
+            if ((e->wc_diag >= 1 && e->wc_diag <= 4) || e->wc_diag == 8 || e->wc_diag == 16 || e->wc_diag == 32 ||
+                e->wc_diag == 64 || e->wc_diag == 96)
+                w.nt = 100 + e->wc_diag;
             if (w.items) geo = w;
         }
     }

@@ -1259,7 +1259,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                     u32x4 *dst = wr ? out + pos : junk;
                     *dst = dk[k0 + q];
                 } else if constexpr ((DIAG & 1) == 0) {
-                    if (wr) out[pos] = dk[k0 + q];
+                    if (wr) {
+                        // nontemporal: the map output is read back much later (exchange /
+                        // fetch); streaming it past the caches keeps the input's lines in the
+                        // Infinity Cache for the next histogram (C1: map side 2.65 -> 2.63 ms,
+                        // profiles/r01_wc_nt_ab.txt).  DIAG 32: plain stores (A/B).
+                        if constexpr ((DIAG & 32) == 0) __builtin_nontemporal_store(dk[k0 + q], out + pos);
+                        else out[pos] = dk[k0 + q];
+                    }
                 } else {
                     if (wr) asm volatile("" ::"v"(dk[k0 + q].x), "v"(dk[k0 + q].w), "v"(pos));
                 }
@@ -1377,6 +1384,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 // branch-free: an invalid item re-reads the chunk head
                 if constexpr ((DIAG & 8) != 0)
                     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rec[k]) : "v"(cb + (valid[k] ? i : 0)) : "memory");
+                else if constexpr ((DIAG & 64) != 0)
+                    rec[k] = __builtin_nontemporal_load(cb + (valid[k] ? i : 0));  // A/B
                 else
                     rec[k] = cb[valid[k] ? i : 0];
             }
@@ -2118,6 +2127,9 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         else if (NI == 8 && geo.nt == 104) SGX_WC1(K, 8, 4);                                     \
         else if (NI == 8 && geo.nt == 108) SGX_WC1(K, 8, 8);                                     \
         else if (NI == 8 && geo.nt == 116) SGX_WC1(K, 8, 16);                                    \
+        else if (NI == 8 && geo.nt == 132) SGX_WC1(K, 8, 32);                                    \
+        else if (NI == 8 && geo.nt == 164) SGX_WC1(K, 8, 64);                                    \
+        else if (NI == 8 && geo.nt == 196) SGX_WC1(K, 8, 96);                                    \
         else SGX_WC1(K, NI, 0);                                                                  \
     } while (0)
         const bool pow2 = (pp.R & (pp.R - 1)) == 0;
