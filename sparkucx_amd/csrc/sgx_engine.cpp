@@ -193,6 +193,7 @@ struct sgx_engine {
     DevBuf jump_dev, sample_winner, sample_keys;
     DevBuf digit_hist;               // sorted read: [digits][256] histogram of the fetched keys
     int sort_skip = 1;               // SGX_SORT_SKIP=0: run every digit pass (A/B, tests)
+    int hist_variant = 0;            // SGX_HIST_VARIANT=2..6: histogram geometry A/B
     DevBuf ag_send, ag_recv, recv, items_dev, chain_buf, gather_stage;
     HostPinned gather_items;
     HostPinned ag_host;
@@ -287,6 +288,7 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     HIP_TRY(hipStreamCreateWithFlags(&e->s_hist, hipStreamNonBlocking));
     if (const char *d = getenv("SGX_PIPELINE")) e->pipeline = atoi(d);
     if (const char *d = getenv("SGX_SORT_SKIP")) e->sort_skip = atoi(d);
+    if (const char *d = getenv("SGX_HIST_VARIANT")) e->hist_variant = atoi(d);
     *out = e.release();
     return SGX_OK;
 }
@@ -524,7 +526,7 @@ static int partition_pass(sgx_engine *e, const void *in, void *out, int64_t n, i
     hipEvent_t h0 = e->ev(), h1 = e->ev(), c0 = e->ev(), c1 = e->ev(), x0 = e->ev(), x1 = e->ev();
     HIP_TRY(hipEventRecord(h0, sh));
     if (n > 0) {
-        HIP_TRY(launch_hist(in, n, rb, chunk, G, spp, (uint32_t *)W.counts.p, sh, pipe));
+        HIP_TRY(launch_hist(in, n, rb, chunk, G, spp, (uint32_t *)W.counts.p, sh, pipe ? 1 : e->hist_variant));
     } else {
         HIP_TRY(hipMemsetAsync(W.counts.p, 0, (size_t)len * 4, sh));
     }

@@ -80,7 +80,7 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int record_bytes, int kind, int nb);
 
 // Launchers (all asynchronous on `stream`).  counts / offs are [R][G] partition-major.
 hipError_t launch_hist(const void *in, int64_t n, int record_bytes, int64_t chunk, int G,
-                       const PartParams &pp, uint32_t *counts, hipStream_t stream, bool lean = false);
+                       const PartParams &pp, uint32_t *counts, hipStream_t stream, int mode = 0);
 hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint64_t *status,
                        uint32_t *ticket_err, uint32_t *part_off, int G, int R,
                        hipStream_t stream);

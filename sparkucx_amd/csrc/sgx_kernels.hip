@@ -177,7 +177,7 @@ __device__ void block_exclusive_scan(const E *in, E *out, uint32_t R, uint32_t *
 // ------------------------------------------------------------------------------------
 // K1+K2: partition ids + per-chunk histogram
 // ------------------------------------------------------------------------------------
-constexpr int HIST_THREADS = 512;
+constexpr int HIST_THREADS = 1024;  // 512 -> 1024: 0.730 -> 0.720 ms at C1 (profiles/r01_hist_geometry_ab*.txt)
 constexpr int HIST_UNROLL = 8;
 
 // grid = G * HIST_SPLIT: the HIST_SPLIT workgroups of chunk g walk it together, BACKWARD,
@@ -245,6 +245,17 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ 
 // pipelined step is 2.71-2.80 ms against 2.63-2.68 serial.  With one workgroup per chunk
 // (fewer waves) the histogram crawls (3.1 ms) and the step is 4.1 ms.
 constexpr int HIST_LEAN_THREADS = 256;
+
+// A/B geometries of the histogram (SGX_HIST_VARIANT, hash partitioners on 16 B records):
+// (unroll, split, threads): 2 = (4, 4, 1024), 3 = (8, 2, 1024), 4 = (8, 8, 1024),
+// 5 = (8, 4, 1024), 6 = (16, 2, 1024).  Measured before: (16, 4, 512) 0.84 ms, (8, 2, 512)
+// 0.77, (8, 8, 512) 0.75, (8, 8, 256) 0.76 against the default (8, 4, 512) 0.733.
+template <int KIND, int UNROLL, int SPLIT, int THREADS>
+__global__ __launch_bounds__(THREADS) void k_hist_var(const char *__restrict__ in, int64_t n, int rb,
+                                                      int64_t chunk, PartParams pp,
+                                                      uint32_t *__restrict__ counts, int G) {
+    hist_body<KIND, true, UNROLL, SPLIT>(in, n, rb, chunk, pp, counts, G);
+}
 template <int KIND, bool REC16>
 __global__ __launch_bounds__(HIST_LEAN_THREADS) __attribute__((amdgpu_num_vgpr(32))) void k_hist_lean(
     const char *__restrict__ in, int64_t n, int rb, int64_t chunk, PartParams pp,
@@ -253,12 +264,31 @@ __global__ __launch_bounds__(HIST_LEAN_THREADS) __attribute__((amdgpu_num_vgpr(3
 }
 
 hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
-                       const PartParams &pp, uint32_t *counts, hipStream_t stream, bool lean) {
+                       const PartParams &pp, uint32_t *counts, hipStream_t stream, int mode) {
     const size_t lds = (size_t)pp.R * 4;
     const char *p = (const char *)in;
     hipError_t ze = hipMemsetAsync(counts, 0, (size_t)pp.R * G * 4, stream);
     if (ze != hipSuccess) return ze;
     const bool r16 = (rb == 16);
+    const bool lean = mode == 1;
+    if (mode >= 2 && r16 && pp.kind == SGX_PART_HASH) {
+#define SGX_HV(K, U, S, T) \
+    hipLaunchKernelGGL((k_hist_var<K, U, S, T>), dim3(G * S), dim3(T), lds, stream, p, n, rb, chunk, pp, counts, G)
+#define SGX_HVK(K)                                          \
+    do {                                                    \
+        switch (mode) {                                     \
+        case 2: SGX_HV(K, 4, 4, 1024); break;               \
+        case 3: SGX_HV(K, 8, 2, 1024); break;               \
+        case 4: SGX_HV(K, 8, 8, 1024); break;               \
+        case 5: SGX_HV(K, 8, 4, 1024); break;               \
+        default: SGX_HV(K, 16, 2, 1024); break;             \
+        }                                                   \
+    } while (0)
+        if ((pp.R & (pp.R - 1)) == 0) SGX_HVK(KIND_HASH_POW2); else SGX_HVK(SGX_PART_HASH);
+#undef SGX_HVK
+#undef SGX_HV
+        return hipGetLastError();
+    }
 #define SGX_HIST(K, B)                                                                                        \
     do {                                                                                                      \
         if (lean)                                                                                             \
