@@ -486,3 +486,53 @@ def test_full_c1_size_bit_exact(engine, oracle_lib):
     del recs
     assert np.array_equal(lengths, counts * 16)
     assert np.array_equal(got, want.reshape(-1))
+
+
+@pytest.mark.slow
+def test_full_c3_shard_zipf_r4096_bit_exact(engine, oracle_lib):
+    """Config C3's per-GPU share at full size: 2^31 / 8 = 2^28 Zipf(1.1) records over
+    K = 2^24 ranks, R = 4096 (hot reducer ~11.5 % of the records), on-device input."""
+    import sparkucx_amd as sgx  # noqa: F401
+
+    n, R, seed = 1 << 28, 4096, 0x5EEDC0DE + 3
+    cdf = oracle_lib.zipf_cdf(1.1, 1 << 24)
+    buf = engine.alloc(n * 16)
+    engine.gen_zipf16(buf, n, seed, cdf)
+    sid = next_sid()
+    engine.register_shuffle(sid, R)
+    lengths = engine.write_map(sid, 0, buf, n, 16, R)
+    got = engine.map_output_bytes(sid, 0)
+    engine.unregister_shuffle(sid)
+    buf.free()
+    recs = oracle_lib.gen_zipf16(n, seed, cdf)
+    want, counts = oracle_lib.map_write(recs, R, nthreads=16)
+    del recs
+    assert counts[1] > 0.1 * n  # the hot reducer (rank 1 -> pid 1)
+    assert np.array_equal(lengths, counts * 16)
+    assert np.array_equal(got, want.reshape(-1))
+
+
+@pytest.mark.slow
+def test_full_c4_shard_terasort_bit_exact(engine, oracle_lib):
+    """Config C4's record shape at one GPU's full share of bytes (2^28 x 16 B = 4.3 GB of
+    100 B TeraSort records), 1023 sampled bounds, RangePartitioner over 10-byte keys."""
+    import sparkucx_amd as sgx
+
+    n, R, seed = (1 << 28) * 16 // 100, 1024, 0x7E7A
+    buf = engine.alloc(n * 100)
+    engine.gen_terasort100(buf, n, seed)
+    recs = oracle_lib.gen_terasort100(n, seed)
+    rng = np.random.default_rng(4)
+    sample = recs[rng.choice(n, 20 * R, replace=False), :10]
+    sample = sample[np.lexsort(sample.T[::-1])]
+    bounds = np.ascontiguousarray(sample[np.linspace(0, len(sample) - 1, R - 1).astype(int)])
+    sid = next_sid()
+    engine.register_shuffle(sid, R, sgx.PART_RANGE_BYTES10, bounds, True, 100)
+    lengths = engine.write_map(sid, 0, buf, n, 100, R)
+    got = engine.map_output_bytes(sid, 0)
+    engine.unregister_shuffle(sid)
+    buf.free()
+    want, counts = oracle_lib.map_write(recs, R, sgx.PART_RANGE_BYTES10, bounds, nthreads=16)
+    del recs
+    assert np.array_equal(lengths, counts * 100)
+    assert np.array_equal(got, want.reshape(-1))
