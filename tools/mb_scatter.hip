@@ -10,6 +10,13 @@
 //   mode 2: same runs, each (chunk, partition) stream shifted by 0..7 records: runs straddle
 //           lines the way real cursors do (a line is finished by the next tile's run)
 //   mode 3: shift 0 or 4 records: runs start on 64 B but not always on 128 B
+//   mode 4: INTERLEAVED tiles: workgroup g's t-th tile is global tile t*G + g, and within a
+//           partition the runs of consecutive global tiles are adjacent (one stream per
+//           partition, shifted 0..7 records): a line straddling two runs is finished by the
+//           neighbouring workgroup at about the same time, on another XCD
+//   mode 5: as 4, XCD-aware: the 32 workgroups of one XCD (g % 8) take 32 consecutive global
+//           tiles, so both halves of a straddling line meet in the same L2
+//   mode 6: as 5 with every stream line-aligned (row locality of adjacent runs, no halves)
 //
 // build: hipcc -O3 --offload-arch=gfx950 -o /tmp/mb_scatter tools/mb_scatter.hip
 #include <hip/hip_runtime.h>
@@ -37,7 +44,13 @@ __global__ __launch_bounds__(WAVES * 64) void k(const uint4 *__restrict__ in, ui
             const int s = j * T + threadIdx.x;
             long d;
             if (MODE == 0) d = tb + s;
-            else {
+            else if (MODE >= 4) {
+                const long t = (tb - begin) / TILE;
+                const int p = s / run;
+                const long gt = MODE == 4 ? t * G + g : t * G + (long)(g % 8) * (G / 8) + g / 8;
+                d = (long)p * per_part + gt * run + s % run;
+                if (MODE != 6) d += (p * 13) & 7;
+            } else {
                 const long t = (tb - begin) / TILE;
                 const int p = s / run;
                 d = (long)p * per_part + (long)g * per_chunk + t * run + s % run;
@@ -87,6 +100,10 @@ int main(int argc, char **argv) {
         rep("scatter_8x16_aligned64", 1024, G, timeit<8, 16, 3>(in, out, n, 1024, G, 10));
         rep("scatter_8x16_unaligned_R512", 512, G, timeit<8, 16, 2>(in, out, n, 512, G, 10));
         rep("scatter_8x16_unaligned_R4096", 4096, G, timeit<8, 16, 2>(in, out, n, 4096, G, 10));
+        rep("interleaved_unaligned", 1024, G, timeit<8, 16, 4>(in, out, n, 1024, G, 10));
+        rep("interleaved_xcd_unaligned", 1024, G, timeit<8, 16, 5>(in, out, n, 1024, G, 10));
+        rep("interleaved_xcd_aligned", 1024, G, timeit<8, 16, 6>(in, out, n, 1024, G, 10));
+        rep("interleaved_xcd_unaligned_R4096", 4096, G, timeit<8, 16, 5>(in, out, n, 4096, G, 10));
     }
     return 0;
 }
