@@ -109,6 +109,15 @@ int sgx_index_block_range(const char *index_path, int32_t start_reduce, int32_t 
  *      sgx_comm_init once per engine (the unique id travels over the host's control plane,
  *      which replaces the ExecutorAdded/IntroduceAllExecutors RPC in the rpc/ package). ---- */
 int sgx_get_unique_id(uint8_t out_id[128]);
+/* Host control plane for the id (§8(f) row 4; replaces the ExecutorAdded /
+ * IntroduceAllExecutors RPC of rpc/UcxDriverRpcEndpoint.scala:21-42 and
+ * rpc/UcxExecutorRpcEndpoint.scala:19-39): rank 0 serves `id` on TCP `port` until ranks
+ * 1..nranks-1 have each fetched it once (SGX_ERR_TIMEOUT after timeout_ms); rank r joins
+ * host:port, retrying until the server is up, and receives the id and the world size.
+ * No GPU is touched: the id may travel on Spark RPC instead. */
+int sgx_bootstrap_serve(int32_t port, int32_t nranks, const uint8_t id[128], int32_t timeout_ms);
+int sgx_bootstrap_join(const char *host, int32_t port, int32_t rank, int32_t timeout_ms, uint8_t out_id[128],
+                       int32_t *out_nranks);
 int sgx_comm_init(sgx_engine *e, int32_t nranks, int32_t rank, const uint8_t id[128]);
 int sgx_comm_size(sgx_engine *e, int32_t *nranks, int32_t *rank);
 /* Push map `map_id` of `shuffle_id` to the reducer owners (reducer r lives on rank

@@ -10,7 +10,9 @@ from ._lib import (  # noqa: F401
     BlockNotFoundException, DeviceError, IllegalArgumentException, IllegalStateException,
     ShuffleError, ShuffleIOException, TransportError, UnsupportedOperationException, lib,
 )
-from .engine import DeviceBuffer, ShuffleEngine, get_unique_id, plan_exchange, reducer_owner  # noqa: F401
+from .engine import (  # noqa: F401
+    DeviceBuffer, ShuffleEngine, bootstrap_join, bootstrap_serve, get_unique_id, plan_exchange, reducer_owner,
+)
 from .shuffle import (  # noqa: F401
     Aggregator, BaseShuffleHandle, GpuShuffleMapOutputWriter, GpuShuffleTransport, GpuShuffleWriter,
     HashPartitioner, MapStatus, MemoryBlock, OperationResult, OperationStatus, RangePartitioner,

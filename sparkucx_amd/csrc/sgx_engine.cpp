@@ -49,6 +49,17 @@ static int fail(int code, const char *fmt, ...) {
     return code;
 }
 
+// the same error path for the other host-side translation units (sgx_bootstrap.cpp)
+int sgx::fail_msg(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    t_last_error = buf;
+    return code;
+}
+
 #define HIP_TRY(expr)                                                                          \
     do {                                                                                       \
         hipError_t _e = (expr);                                                                \

@@ -25,6 +25,8 @@ struct PartParams {
                          // the masked-off lanes of branch-free stores (never read)
 };
 constexpr size_t JUNK_BYTES_PER_WG = 64 * 16;
+// Sets the thread-local sgx_last_error() message and returns `code` (host code only).
+int fail_msg(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 // Internal partition kind of the reduce side's LSD radix passes: pid = 8-bit digit of the
 // key (R = 256), see PartParams::dshift / dflip.  Never registered through the C ABI.
 constexpr int KIND_DIGIT = 200;

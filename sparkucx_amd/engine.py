@@ -291,6 +291,22 @@ class ShuffleEngine:
               "gen_terasort100")
 
 
+def bootstrap_serve(port: int, nranks: int, unique_id: bytes, timeout_ms: int = 60_000):
+    """Driver side of the id exchange (replaces ExecutorAdded / IntroduceAllExecutors):
+    blocks until ranks 1..nranks-1 fetched ``unique_id`` (128 bytes)."""
+    buf = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(unique_id).ljust(128, b"\0")[:128])
+    check(lib().sgx_bootstrap_serve(port, nranks, ctypes.cast(buf, ctypes.c_void_p), timeout_ms), "bootstrapServe")
+
+
+def bootstrap_join(host: str, port: int, rank: int, timeout_ms: int = 60_000) -> Tuple[bytes, int]:
+    """Executor side: fetch (unique_id, nranks) from the serving rank."""
+    buf = (ctypes.c_uint8 * 128)()
+    nr = ctypes.c_int32(0)
+    check(lib().sgx_bootstrap_join(host.encode(), port, rank, timeout_ms, ctypes.cast(buf, ctypes.c_void_p),
+                                   ctypes.byref(nr)), "bootstrapJoin")
+    return bytes(buf), nr.value
+
+
 def get_unique_id() -> bytes:
     buf = ctypes.create_string_buffer(128)
     check(lib().sgx_get_unique_id(ctypes.cast(buf, ctypes.c_void_p)), "get_unique_id")
