@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--serializer", choices=["fixed", "kryo"], default="fixed",
+                    help="kryo: also frame each map output as Spark's Kryo stream (SURVEY §8(f) row 2)")
     return ap.parse_args()
 
 
@@ -122,7 +124,7 @@ def main():
         cdf /= cdf[-1]
         eng.gen_zipf16(buf, n, args.seed + rank, cdf, value_base=rank * n)
     sid = 1
-    eng.register_shuffle(sid, R)
+    eng.register_shuffle(sid, R, serializer=sgx.SER_KRYO if args.serializer == "kryo" else sgx.SER_FIXED)
 
     def step(k):
         mid = (k & 1) * world + rank  # two alternating map slots per rank
@@ -157,7 +159,7 @@ def main():
     verified = None
     lens = eng.map_lengths(sid, rank, R)
     if not args.no_verify:
-        verified = bool(lens.sum() == 16 * n)
+        verified = bool(lens.sum() == 16 * n) if args.serializer == "fixed" else bool(lens.sum() >= 4 * n)
     xgmi = None
     if world > 1:
         # bytes this rank's map sends over xGMI (reducer r lives on rank floor(r*P/R))
@@ -208,6 +210,27 @@ def main():
         }
         if xgmi is not None:
             out["xgmi_roofline"] = xgmi
+        if args.serializer == "kryo":
+            ser_ms = st.ms["serialize"] / max(1, st.count["serialize"])
+            kbytes = float(lens.sum())
+            out["config"]["serializer"] = "KryoSerializer, spark.shuffle.compress=false"
+            out["kryo"] = {"kernel": "k_kryo_ser16", "ms": round(ser_ms, 4), "stream_bytes": kbytes,
+                           "algo_bytes": 16.0 * n + kbytes,
+                           "achieved_GBs": round((16.0 * n + kbytes) / (ser_ms * 1e-3) / 1e9, 1)}
+            if world == 1:
+                # reduce side of the same shuffle: every block of the last map, decoded on the GPU
+                dst = eng.alloc(n * 16)
+                last_mid = ((args.steps + args.warmup - 1) & 1) * world + rank
+                for _ in range(3):
+                    eng.stats_reset()
+                    eng.read_records(sid, [last_mid], 0, R, dst=dst)
+                st2 = eng.stats()
+                de_ms = st2.ms["deserialize"] / max(1, st2.count["deserialize"])
+                out["kryo"]["deserialize"] = {
+                    "kernel": "k_kryo_deser16", "ms": round(de_ms, 4), "algo_bytes": kbytes + 16.0 * n,
+                    "achieved_GBs": round((kbytes + 16.0 * n) / (de_ms * 1e-3) / 1e9, 1),
+                    "gather_ms": round(st2.ms["regroup"] / max(1, st2.count["regroup"]), 4)}
+                dst.free()
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args, n)
         elif world == 1:

@@ -72,6 +72,18 @@ int32_t sgx_abi_version(void);
 int sgx_register_shuffle(sgx_engine *e, int32_t shuffle_id, int32_t num_partitions,
                          int32_t partitioner_kind, const void *bounds, int64_t nbounds,
                          int32_t ascending, int32_t record_bytes);
+/* dep.serializer (ShuffleDependency; the writers built at spark_3_0/UcxShuffleManager.scala:
+ * 37-51 serialize every record with it).  SGX_SER_FIXED: the engine's fixed-width record
+ * codec (lengths = records x record_bytes).  SGX_SER_KRYO: Spark's KryoSerializer stream with
+ * spark.shuffle.compress=false, for (Long, Long) 16 B records: per record
+ * [0x09][zigzag varlong key][0x09][zigzag varlong value] (kryo.writeClassAndObject of two
+ * java.lang.Long), framed on the GPU after the scatter; partition lengths, index offsets,
+ * the data file, fetched blocks and exchanged bytes are then those of the Kryo stream, so
+ * Spark's own reader deserializes them.  Set before the first sgx_write_map of the shuffle
+ * (SGX_ERR_STATE after).  The reduce side (sgx_read_records / _sorted / _grouped) decodes the
+ * fetched Kryo stream back to records on the GPU before sorting / grouping. */
+enum sgx_serializer { SGX_SER_FIXED = 0, SGX_SER_KRYO = 1 };
+int sgx_set_serializer(sgx_engine *e, int32_t shuffle_id, int32_t serializer);
 /* unregisterShuffle: CommonUcxShuffleManager.scala:103-106 -> removeShuffle
  * (CommonUcxShuffleBlockResolver.scala:63-71). Frees the shuffle's HBM. */
 int sgx_unregister_shuffle(sgx_engine *e, int32_t shuffle_id);
@@ -158,6 +170,16 @@ int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, i
                     int32_t start_partition, int32_t end_partition, void *dst, int64_t dst_cap,
                     int32_t dst_mem_kind, int64_t *out_bytes);
 
+/* sgx_read_records: no aggregator, no key ordering -- the records of reducers [start, end)
+ * in the canonical order (what the reader's deserializeStream(...).asKeyValueIterator
+ * yields, :137-145), back to back into dst.  For a fixed-codec shuffle this is the fetched
+ * blocks; for a Kryo shuffle the fetched Kryo stream is decoded to 16 B (Long, Long) records
+ * on the GPU (SGX_ERR_INVALID if it is not a Kryo stream of Long pairs).  dst NULL with
+ * dst_cap 0 is a size query. */
+int sgx_read_records(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
+                     int32_t start_partition, int32_t end_partition, void *dst, int64_t dst_cap,
+                     int32_t dst_mem_kind, int64_t *out_bytes);
+
 /* sgx_read_grouped: dep.aggregator with mapSideCombine = false (Aggregator.combineValuesByKey,
  * :155-164) on (Long, Long) records.  Groups are emitted in ascending key order per reducer
  * (Spark's hash-map iteration order is unspecified; this is the canonical order the parity
@@ -197,9 +219,12 @@ int sgx_range_bounds(sgx_engine *e, const void *const *batches, const int64_t *n
 /* SGX_STAGE_REGROUP times the fetch-side gather kernel (blocks into request order). */
 enum sgx_stage { SGX_STAGE_HIST = 0, SGX_STAGE_SCAN = 1, SGX_STAGE_SCATTER = 2,
                  SGX_STAGE_ALLGATHER = 3, SGX_STAGE_ALLTOALL = 4, SGX_STAGE_REGROUP = 5,
-                 SGX_STAGE_SORT = 6, SGX_STAGE_GROUP = 7, SGX_NUM_STAGES = 8 };
+                 SGX_STAGE_SORT = 6, SGX_STAGE_GROUP = 7, SGX_STAGE_SERIALIZE = 8,
+                 SGX_STAGE_DESERIALIZE = 9, SGX_NUM_STAGES = 10 };
 /* SGX_STAGE_SORT times sgx_read_sorted's radix + partitioner passes (the fetch gather is
- * REGROUP), SGX_STAGE_GROUP the grouping / summing kernels of sgx_read_grouped. */
+ * REGROUP), SGX_STAGE_GROUP the grouping / summing kernels of sgx_read_grouped,
+ * SGX_STAGE_SERIALIZE the Kryo framing kernel of sgx_write_map (SGX_SER_KRYO),
+ * SGX_STAGE_DESERIALIZE the Kryo decoder of the reduce-side reads. */
 int sgx_stats_reset(sgx_engine *e);
 /* out_ms[SGX_NUM_STAGES] summed milliseconds, out_count[SGX_NUM_STAGES] launches. */
 int sgx_stats_get(sgx_engine *e, double *out_ms, int64_t *out_count);

@@ -223,3 +223,51 @@ def reduce_grouped(seqs, agg: str = "group"):
     if agg == "sum":
         return cat(keys_l), cat(sums_l)
     return cat(keys_l), cat(starts_l), cat(vals_l)
+
+
+def kryo_record_lengths(records: np.ndarray) -> np.ndarray:
+    """Bytes of each (Long, Long) record in Spark's Kryo stream (spark_semantics.kryo_*)."""
+    kv = np.ascontiguousarray(records).view(np.uint64).reshape(-1, 2)
+    z = (kv << np.uint64(1)) ^ (kv.view(np.int64) >> np.int64(63)).view(np.uint64)
+    bits = np.zeros(z.shape, dtype=np.int64)
+    for b in range(64):
+        bits = np.where((z >> np.uint64(b)) != 0, b + 1, bits)
+    vl = np.minimum(np.maximum((bits + 6) // 7, 1), 9)
+    return (2 + vl[:, 0] + vl[:, 1]).astype(np.int64)
+
+
+def kryo_serialize(records: np.ndarray) -> np.ndarray:
+    """Vectorised Kryo framing of (n, 16) uint8 (Long, Long) records -> uint8 stream.  Same
+    definition as spark_semantics.kryo_serialize_pairs (the tests pin one to the other)."""
+    kv = np.ascontiguousarray(records).view(np.uint64).reshape(-1, 2)
+    n = kv.shape[0]
+    z = (kv << np.uint64(1)) ^ (kv.view(np.int64) >> np.int64(63)).view(np.uint64)
+    mat = np.zeros((n, 20), dtype=np.uint8)
+    use = np.zeros((n, 20), dtype=bool)
+    col = 0
+    for f in range(2):
+        mat[:, col] = 0x09
+        use[:, col] = True
+        col += 1
+        x = z[:, f].copy()
+        done = np.zeros(n, dtype=bool)
+        for i in range(9):
+            last = (x < np.uint64(0x80)) | (i == 8)
+            byte = np.where(last, x & np.uint64(0xFF), (x & np.uint64(0x7F)) | np.uint64(0x80)).astype(np.uint8)
+            live = ~done
+            mat[:, col + i] = np.where(live, byte, 0)
+            use[:, col + i] = live
+            done = done | last
+            x = x >> np.uint64(7)
+        # compact this field's 9 columns left so the next field starts right after it
+        col += 9
+    # row-major order of the used cells = the stream
+    return mat[use]
+
+
+def kryo_partition_offsets(records: np.ndarray, counts: np.ndarray) -> np.ndarray:
+    """Byte offsets (R+1) of the Kryo-framed partitions of a partition-contiguous output."""
+    lens = kryo_record_lengths(records)
+    cum = np.zeros(len(lens) + 1, dtype=np.int64)
+    np.cumsum(lens, out=cum[1:])
+    return cum[offsets(counts)]

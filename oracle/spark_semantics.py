@@ -420,3 +420,80 @@ def determine_bounds(candidates, partitions: int, lt=None):
                 prev = key
         i += 1
     return bounds
+
+
+# ---------------------------------------------------------------------------------------
+# Kryo framing of (Long, Long) records.  Spark's KryoSerializer
+# (spark-core 3.0.1, kryo-shaded 4.0.2, both external): KryoSerializationStream.writeKey /
+# writeValue -> kryo.writeClassAndObject(output, java.lang.Long).  Restated from Kryo's
+# published sources:
+#   * Kryo's constructor registers int, String, float, boolean, byte, char, short, long,
+#     double, void as ids 0..9 (primitive wrappers share the primitive's registration), so
+#     java.lang.Long is id 7 and DefaultClassResolver.writeClass writes varint(7 + 2) = 0x09;
+#   * MapReferenceResolver.useReferences is false for wrapper classes: no reference byte;
+#   * DefaultSerializers.LongSerializer.write = output.writeLong(v, false), which in Kryo 4
+#     is writeVarLong(v, optimizePositive = false): zigzag, then 7 bits per byte, low group
+#     first, 0x80 = more follows; the 9th byte (if any) carries bits 56..63 whole.
+# With spark.shuffle.compress = false (and no encryption) SerializerManager.wrapStream is the
+# identity, so a partition's bytes are its records' encodings back to back.
+# Parity unpinned against a JVM (none here); pinned by hand-computed known answers.
+# ---------------------------------------------------------------------------------------
+KRYO_LONG_CLASS_BYTE = 0x09
+
+
+def kryo_write_var_long(v: int, optimize_positive: bool = False) -> bytes:
+    """Kryo 4 Output.writeVarLong."""
+    z = v & 0xFFFFFFFFFFFFFFFF
+    if not optimize_positive:
+        z = ((z << 1) ^ (0xFFFFFFFFFFFFFFFF if v < 0 else 0)) & 0xFFFFFFFFFFFFFFFF
+    out = bytearray()
+    for _ in range(8):
+        if z < 0x80:
+            break
+        out.append((z & 0x7F) | 0x80)
+        z >>= 7
+    out.append(z & 0xFF)
+    return bytes(out)
+
+
+def kryo_read_var_long(buf: bytes, pos: int, optimize_positive: bool = False) -> Tuple[int, int]:
+    """Kryo 4 Input.readVarLong: returns (value, new position)."""
+    z, shift = 0, 0
+    for i in range(9):
+        b = buf[pos]
+        pos += 1
+        if i == 8:
+            z |= b << 56
+            break
+        z |= (b & 0x7F) << shift
+        shift += 7
+        if not b & 0x80:
+            break
+    if not optimize_positive:
+        z = (z >> 1) ^ (-(z & 1) & 0xFFFFFFFFFFFFFFFF)
+    return to_i64(z), pos
+
+
+def kryo_serialize_pairs(records: Sequence[Tuple[int, int]]) -> bytes:
+    """KryoSerializationStream of writeKey(k); writeValue(v) for each (Long, Long)."""
+    out = bytearray()
+    for k, v in records:
+        out.append(KRYO_LONG_CLASS_BYTE)
+        out += kryo_write_var_long(k)
+        out.append(KRYO_LONG_CLASS_BYTE)
+        out += kryo_write_var_long(v)
+    return bytes(out)
+
+
+def kryo_deserialize_pairs(buf: bytes) -> List[Tuple[int, int]]:
+    """KryoDeserializationStream.asKeyValueIterator over (Long, Long): readClassAndObject x 2."""
+    out, pos = [], 0
+    while pos < len(buf):
+        pair = []
+        for _ in range(2):
+            if buf[pos] != KRYO_LONG_CLASS_BYTE:
+                raise ValueError(f"class byte {buf[pos]:#x} at {pos} is not java.lang.Long")
+            x, pos = kryo_read_var_long(buf, pos + 1)
+            pair.append(x)
+        out.append((pair[0], pair[1]))
+    return out

@@ -6,7 +6,8 @@ RCCL all-to-all exchange, regroup) runs in the in-tree HIP library ``libsgx.so``
 CPU fallback and raises if the library is missing.
 """
 from ._lib import (  # noqa: F401
-    AGG_GROUP, AGG_SUM, MEM_DEVICE, MEM_HOST, PART_HASH, PART_RANGE_BYTES10, PART_RANGE_I64, STAGES,
+    AGG_GROUP, AGG_SUM, MEM_DEVICE, MEM_HOST, PART_HASH, PART_RANGE_BYTES10, PART_RANGE_I64, SER_FIXED, SER_KRYO,
+    STAGES,
     BlockNotFoundException, DeviceError, IllegalArgumentException, IllegalStateException,
     ShuffleError, ShuffleIOException, TransportError, UnsupportedOperationException, lib,
 )

@@ -21,7 +21,9 @@ SGX_ERR_IO, SGX_ERR_NOMEM, SGX_ERR_NOT_FOUND, SGX_ERR_UNSUPPORTED, SGX_ERR_TIMEO
 PART_HASH, PART_RANGE_I64, PART_RANGE_BYTES10 = 0, 1, 2
 MEM_HOST, MEM_DEVICE = 0, 1
 AGG_GROUP, AGG_SUM = 0, 1
-STAGES = ("hist", "scan", "scatter", "allgather", "alltoall", "regroup", "sort", "group")
+SER_FIXED, SER_KRYO = 0, 1
+STAGES = ("hist", "scan", "scatter", "allgather", "alltoall", "regroup", "sort", "group", "serialize",
+          "deserialize")
 
 
 class ShuffleError(RuntimeError):
@@ -84,6 +86,7 @@ SIGNATURES = {
     "sgx_abi_version": (_i32, []),
     "sgx_register_shuffle": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _i64, _i32, _i32]),
     "sgx_unregister_shuffle": (ctypes.c_int, [_vp, _i32]),
+    "sgx_set_serializer": (ctypes.c_int, [_vp, _i32, _i32]),
     "sgx_write_map": (ctypes.c_int, [_vp, _i32, _i64, _vp, _i64, _i32, _i32, _vp]),
     "sgx_map_lengths": (ctypes.c_int, [_vp, _i32, _i64, _vp]),
     "sgx_map_data": (ctypes.c_int, [_vp, _i32, _i64, ctypes.POINTER(_vp), _P64]),
@@ -96,6 +99,7 @@ SIGNATURES = {
     "sgx_exchange": (ctypes.c_int, [_vp, _i32, _i64]),
     "sgx_fetch_blocks": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i64, _vp, _i64, _i32, _vp]),
     "sgx_read_sorted": (ctypes.c_int, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i64, _i32, _vp]),
+    "sgx_read_records": (ctypes.c_int, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i64, _i32, _vp]),
     "sgx_range_bounds": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "sgx_bootstrap_serve": (ctypes.c_int, [_i32, _i32, _vp, _i32]),
     "sgx_bootstrap_join": (ctypes.c_int, [ctypes.c_char_p, _i32, _i32, _i32, _vp, _vp]),

@@ -138,6 +138,13 @@ struct MapOut {
     bool ready = false;
     hipEvent_t done = nullptr;  // recorded on the compute stream after the scatter
     hipEvent_t read_done = nullptr;  // recorded on the exchange stream after the all-to-all read `data`
+    // serializer KRYO (sgx_set_serializer): the map's published bytes are the Kryo stream of
+    // its records (data file, fetch, exchange); `data` keeps the 16 B records
+    DevBuf ser;                // Kryo-framed partition-contiguous bytes (capacity 20 n + 16)
+    DevBuf ser_work;           // ser_off_dev (R+1) i64 | ticket, error u32 x 4 | look-back status
+    HostPinned ser_off;        // (R+1) i64 byte offsets + the error word, landed async
+    int64_t out_bytes = 0;     // published bytes (n * rb, or the Kryo total once `ready`)
+    const void *view() const { return ser.p ? ser.p : data.p; }
 };
 
 // One exchange round: every rank pushed one map; this rank holds its reducers' blocks.
@@ -158,6 +165,7 @@ struct Round {
 
 struct Shuffle {
     int32_t R = 0, kind = 0, nb = 0, asc = 1, rb = 16;
+    int32_t ser = SGX_SER_FIXED;  // dep.serializer (sgx_set_serializer)
     DevBuf bounds;
     PartParams pp{};
     std::map<int64_t, std::unique_ptr<MapOut>> maps;
@@ -198,7 +206,9 @@ struct sgx_engine {
     int pipeline = 0;                // SGX_PIPELINE=1: hist+scan of map k+1 overlap map k's scatter
     hipStream_t s_hist = nullptr;
     DevBuf input_stage, junk;
+    const uint32_t *last_off_dev = nullptr;  // device (R+1) record offsets of the last partition pass
     // reduce side: sort ping-pong buffers, per-pass error words, grouping work buffers
+    DevBuf kryo_in, kryo_work;  // reduce side of a Kryo shuffle: fetched stream, decoder state
     DevBuf sort_buf[2], sort_err, grp_flags, grp_offs, grp_status, grp_out, grp_prefix;
     // RangePartitioner.sketch: XORShiftRandom jump table, reservoir winners and keys
     DevBuf jump_dev, sample_winner, sample_keys;
@@ -310,6 +320,9 @@ static void free_map(MapOut &m) {
     m.read_done = nullptr;
     m.data.release();
     m.part_off.release();
+    m.ser.release();
+    m.ser_work.release();
+    m.ser_off.release();
     if (m.done) (void)hipEventDestroy(m.done);
     m.done = nullptr;
 }
@@ -334,7 +347,7 @@ extern "C" void sgx_destroy(sgx_engine *e) {
         if (w.used) (void)hipEventDestroy(w.used);
         w.used = nullptr;
     }
-    for (DevBuf *b : {&e->sort_buf[0], &e->sort_buf[1], &e->sort_err, &e->grp_flags, &e->grp_offs, &e->grp_status,
+    for (DevBuf *b : {&e->kryo_in, &e->kryo_work, &e->sort_buf[0], &e->sort_buf[1], &e->sort_err, &e->grp_flags, &e->grp_offs, &e->grp_status,
                       &e->grp_out, &e->grp_prefix, &e->jump_dev, &e->sample_winner, &e->sample_keys,
                       &e->digit_hist})
         b->release();
@@ -442,7 +455,22 @@ static int finish_lengths(Shuffle &s, MapOut &m) {
         return fail(SGX_ERR_HIP, "partition offsets do not sum to the record count (%u vs %lld)", po[s.R],
                     (long long)m.nrec);
     m.lengths.assign((size_t)s.R, 0);
-    for (int32_t p = 0; p < s.R; ++p) m.lengths[(size_t)p] = ((int64_t)po[p + 1] - (int64_t)po[p]) * s.rb;
+    if (s.ser == SGX_SER_KRYO) {
+        const int64_t *so = (const int64_t *)m.ser_off.p;
+        const uint32_t serr = (uint32_t)so[s.R + 1];
+        if (serr & 1u) return fail(SGX_ERR_TIMEOUT, "serializer look-back spin gave up (device flag %u)", serr);
+        int64_t prev = 0;
+        for (int32_t p = 0; p < s.R; ++p) {
+            m.lengths[(size_t)p] = so[p + 1] - so[p];
+            if (so[p] != prev || m.lengths[(size_t)p] < 0 || m.lengths[(size_t)p] > 20 * ((int64_t)po[p + 1] - po[p]))
+                return fail(SGX_ERR_HIP, "internal error: Kryo partition offsets inconsistent at %d", p);
+            prev = so[p + 1];
+        }
+        m.out_bytes = so[s.R];
+    } else {
+        for (int32_t p = 0; p < s.R; ++p) m.lengths[(size_t)p] = ((int64_t)po[p + 1] - (int64_t)po[p]) * s.rb;
+        m.out_bytes = m.nrec * s.rb;
+    }
     m.ready = true;
     return SGX_OK;
 }
@@ -529,6 +557,7 @@ static int partition_pass(sgx_engine *e, const void *in, void *out, int64_t n, i
     SGX_TRY(W.offs.ensure((size_t)len * 4));
     SGX_TRY(W.status.ensure((size_t)(16 + tiles * 8)));
     SGX_TRY(W.part_off_dev.ensure((size_t)(R + 2) * 4));
+    e->last_off_dev = (const uint32_t *)W.part_off_dev.p;
     uint32_t *ticket_err = (uint32_t *)W.status.p;
     uint64_t *status = (uint64_t *)((char *)W.status.p + 16);
     HIP_TRY(hipMemsetAsync(W.status.p, 0, (size_t)(16 + tiles * 8), sh));
@@ -598,6 +627,46 @@ static int partition_pass(sgx_engine *e, const void *in, void *out, int64_t n, i
     return SGX_OK;
 }
 
+// Kryo framing of the partition-contiguous 16 B records just written (sgx_serde.hip), on
+// the compute stream behind the scatter; byte offsets land in m.ser_off (pinned).
+static int serialize_kryo(sgx_engine *e, Shuffle &s, MapOut &m) {
+    hipStream_t st = e->s_comp;
+    const int64_t n = m.nrec;
+    const int64_t tiles = kryo_ser16_tiles(n);
+    const size_t offb = (size_t)(s.R + 1) * 8;
+    SGX_TRY(m.ser.ensure((size_t)(20 * n + 16)));
+    SGX_TRY(m.ser_work.ensure(offb + 16 + (size_t)tiles * 8));
+    SGX_TRY(m.ser_off.ensure(offb + 8));
+    int64_t *off_dev = (int64_t *)m.ser_work.p;
+    uint32_t *tick = (uint32_t *)((char *)m.ser_work.p + offb);
+    uint64_t *status = (uint64_t *)((char *)m.ser_work.p + offb + 16);
+    HIP_TRY(hipMemsetAsync(m.ser_work.p, 0, offb + 16 + (size_t)tiles * 8, st));
+    hipEvent_t k0 = e->ev(), k1 = e->ev();
+    HIP_TRY(hipEventRecord(k0, st));
+    HIP_TRY(launch_kryo_ser16(m.data.p, n, m.ser.p, e->last_off_dev, s.R, off_dev, status, tick, st));
+    HIP_TRY(hipEventRecord(k1, st));
+    record_stage(e, SGX_STAGE_SERIALIZE, k0, k1);
+    // (R+1) offsets, then the error word in the low half of slot R+1
+    HIP_TRY(hipMemcpyAsync(m.ser_off.p, off_dev, offb, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync((char *)m.ser_off.p + offb, tick + 1, 4, hipMemcpyDeviceToHost, st));
+    return SGX_OK;
+}
+
+extern "C" int sgx_set_serializer(sgx_engine *e, int32_t shuffle_id, int32_t serializer) {
+    if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    auto it = e->shuffles.find(shuffle_id);
+    if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
+    Shuffle &s = it->second;
+    if (serializer != SGX_SER_FIXED && serializer != SGX_SER_KRYO)
+        return fail(SGX_ERR_INVALID, "unknown serializer %d", serializer);
+    if (!s.maps.empty()) return fail(SGX_ERR_STATE, "shuffle %d already has map outputs", shuffle_id);
+    if (serializer == SGX_SER_KRYO && (s.rb != 16 || s.kind == SGX_PART_RANGE_BYTES10))
+        return fail(SGX_ERR_UNSUPPORTED, "Kryo framing is for (Long, Long) 16 B records, not %d B", s.rb);
+    s.ser = serializer;
+    return SGX_OK;
+}
+
 extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records,
                              int64_t n, int32_t rb, int32_t mem_kind, int64_t *out_lengths) {
     if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
@@ -622,6 +691,7 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
     // ... and must not overwrite the previous output while an exchange still sends it
     if (m.read_done) HIP_TRY(hipStreamWaitEvent(st, m.read_done, 0));
     m.ready = false;
+    if (s.ser != SGX_SER_KRYO) m.ser.release();
     m.nrec = n;
     m.bytes = n * rb;
     SGX_TRY(m.data.ensure((size_t)m.bytes));
@@ -637,6 +707,7 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
 
     SGX_TRY(partition_pass(e, in, m.data.p, n, rb, s.pp, s.R, s.kind, s.nb, mem_kind, (uint32_t *)m.part_off.p,
                            nullptr, true));
+    if (s.ser == SGX_SER_KRYO) SGX_TRY(serialize_kryo(e, s, m));
     HIP_TRY(hipEventRecord(m.done, st));
     if (out_lengths) {
         SGX_TRY(finish_lengths(s, m));
@@ -673,8 +744,9 @@ extern "C" int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, v
     Shuffle *s;
     MapOut *m;
     SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
-    *ptr = m->data.p;
-    *bytes = m->bytes;
+    SGX_TRY(finish_lengths(*s, *m));
+    *ptr = const_cast<void *>(m->view());
+    *bytes = m->out_bytes;
     return SGX_OK;
 }
 
@@ -786,8 +858,8 @@ extern "C" int sgx_write_index(sgx_engine *e, int32_t shuffle_id, int64_t map_id
     const std::string index_tmp = std::string(index_path) + ".sgx.tmp";
     // map output -> data tmp (dataTmp of writeIndexFileAndCommit)
     {
-        std::vector<uint8_t> host((size_t)m->bytes);
-        if (m->bytes) HIP_TRY(hipMemcpy(host.data(), m->data.p, (size_t)m->bytes, hipMemcpyDeviceToHost));
+        std::vector<uint8_t> host((size_t)m->out_bytes);
+        if (m->out_bytes) HIP_TRY(hipMemcpy(host.data(), m->view(), (size_t)m->out_bytes, hipMemcpyDeviceToHost));
         SGX_TRY(write_all(data_tmp.c_str(), host.data(), host.size()));
     }
     std::vector<int64_t> existing;
@@ -957,7 +1029,7 @@ extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
         rd->block_off.assign((size_t)nmine, 0);
         int64_t off = 0;
         for (int32_t r = 0; r < R; ++r) { rd->block_off[(size_t)r] = off; off += m->lengths[(size_t)r]; }
-        rd->alias = m->data.p;
+        rd->alias = m->view();
         HIP_TRY(hipEventRecord(rd->done, e->s_comp));
         for (auto it = s->rounds.begin(); it != s->rounds.end(); ++it)
             if ((*it)->map_ids == rd->map_ids) { free_round(**it); s->rounds.erase(it); break; }
@@ -1023,7 +1095,7 @@ extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
         rdz[(size_t)j] = (size_t)rdp[(size_t)j];
     }
     HIP_TRY(hipEventRecord(a2, st));
-    NCCL_TRY(ncclAllToAllv(m->data.p, scz.data(), sdz.data(), rd->data.p, rcz.data(), rdz.data(), ncclUint8,
+    NCCL_TRY(ncclAllToAllv(m->view(), scz.data(), sdz.data(), rd->data.p, rcz.data(), rdz.data(), ncclUint8,
                            e->comm, st));
     HIP_TRY(hipEventRecord(a3, st));
     HIP_TRY(hipEventRecord(rd->done, st));
@@ -1075,7 +1147,7 @@ static int fetch_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_id
                 SGX_TRY(finish_lengths(s, m));
                 int64_t off = 0;
                 for (int32_t q = 0; q < r; ++q) off += m.lengths[(size_t)q];
-                srcs[(size_t)i] = Src{(const char *)m.data.p + off, m.lengths[(size_t)r], m.done};
+                srcs[(size_t)i] = Src{(const char *)m.view() + off, m.lengths[(size_t)r], m.done};
                 found = true;
             }
         }
@@ -1111,7 +1183,7 @@ static int fetch_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_id
     SGX_TRY(e->gather_items.ensure((size_t)npieces * 24));
     SGX_TRY(e->items_dev.ensure((size_t)npieces * 24));
     int64_t *gi = (int64_t *)e->gather_items.p, k = 0, off = 0;
-    bool al16 = ((uintptr_t)gdst & 15) == 0;
+    bool al16 = ((uintptr_t)gdst & 15) == 0, al4 = ((uintptr_t)gdst & 3) == 0;
     for (int64_t i = 0; i < n; ++i) {
         const char *sp = (const char *)srcs[(size_t)i].p;
         for (int64_t done = 0; done < srcs[(size_t)i].len; done += ITEM_BYTES, ++k) {
@@ -1119,14 +1191,16 @@ static int fetch_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_id
             gi[3 * k] = (int64_t)(uintptr_t)(sp + done);
             gi[3 * k + 1] = (int64_t)(uintptr_t)(gdst + off + done);
             gi[3 * k + 2] = b;
-            al16 = al16 && (((uintptr_t)(sp + done) | (uintptr_t)(off + done) | (uintptr_t)b) & 15) == 0;
+            const uintptr_t bits = (uintptr_t)(sp + done) | (uintptr_t)(off + done) | (uintptr_t)b;
+            al16 = al16 && (bits & 15) == 0;
+            al4 = al4 && (bits & 3) == 0;
         }
         off += srcs[(size_t)i].len;
     }
     hipEvent_t g0 = e->ev(), g1 = e->ev();
     HIP_TRY(hipEventRecord(g0, st));
     HIP_TRY(hipMemcpyAsync(e->items_dev.p, gi, (size_t)npieces * 24, hipMemcpyHostToDevice, st));
-    HIP_TRY(launch_gather_items((const int64_t *)e->items_dev.p, npieces, al16 ? 16 : 4, st));
+    HIP_TRY(launch_gather_items((const int64_t *)e->items_dev.p, npieces, al16 ? 16 : al4 ? 4 : 1, st));
     HIP_TRY(hipEventRecord(g1, st));
     record_stage(e, SGX_STAGE_REGROUP, g0, g1);
     if (!dev_dst) HIP_TRY(hipMemcpyAsync(dst, gdst, (size_t)total, hipMemcpyDeviceToHost, st));
@@ -1147,11 +1221,11 @@ extern "C" int sgx_fetch_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t
 // Reduce side after the fetch (UcxShuffleReader.scala:137-191): stable sort by key per
 // reducer, then groupByKey / reduceByKey on (Long, Long) records
 // ------------------------------------------------------------------------------------
-// Fetch the canonical blocks of reducers [r0, r1) x maps into e->sort_buf[0] and sort them
-// stably by key within each reducer.  On return (asynchronous on s_comp) *sorted points at
-// the device buffer holding the result and *nrec its record count.
-static int sort_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps, int32_t r0,
-                       int32_t r1, const void **sorted, int64_t *nrec) {
+// Gather the canonical blocks of reducers [r0, r1) x maps into e->sort_buf[0] as records
+// (a Kryo shuffle's stream is decoded on the GPU on the way); sort_buf[1] is sized to match.
+// *nrec = records; asynchronous on s_comp except for a Kryo shuffle's record count.
+static int records_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps, int32_t r0,
+                          int32_t r1, int64_t *nrec) {
     auto it = e->shuffles.find(shuffle_id);
     if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
     Shuffle &s = it->second;
@@ -1159,8 +1233,6 @@ static int sort_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids
         return fail(SGX_ERR_INVALID, "partition range [%d, %d) outside [0, %d)", r0, r1, s.R);
     if (nmaps < 0 || (nmaps > 0 && !map_ids)) return fail(SGX_ERR_INVALID, "bad map list");
     const int rb = s.rb;
-    if (rb != 16 && rb != 100)
-        return fail(SGX_ERR_UNSUPPORTED, "sorted read needs 16 B (Long, Long) or 100 B TeraSort records, not %d B", rb);
     const int64_t nreq = (int64_t)(r1 - r0) * nmaps;
     std::vector<int64_t> mids((size_t)nreq), lens((size_t)nreq);
     std::vector<int32_t> rids((size_t)nreq);
@@ -1174,15 +1246,68 @@ static int sort_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids
     if (rc != SGX_OK && rc != SGX_ERR_INVALID) return rc;
     int64_t total = 0;
     for (int64_t L : lens) total += L;
+    hipStream_t st = e->s_comp;
+    if (s.ser == SGX_SER_KRYO) {
+        // the fetched Kryo stream (blocks back to back are one valid stream) -> records
+        *nrec = 0;
+        const int64_t cap = total / 4;  // a record takes >= 4 bytes
+        SGX_TRY(e->sort_buf[0].ensure((size_t)cap * 16));
+        if (total == 0) return SGX_OK;
+        SGX_TRY(e->kryo_in.ensure((size_t)total + 64));
+        SGX_TRY(fetch_locked(e, shuffle_id, mids.data(), rids.data(), nreq, e->kryo_in.p, total, SGX_MEM_DEVICE,
+                             lens.data(), false));
+        const int64_t tiles = kryo_deser16_tiles(total);
+        const size_t wb = 16 + 8 + (size_t)tiles * 8;
+        SGX_TRY(e->kryo_work.ensure(wb));
+        HIP_TRY(hipMemsetAsync(e->kryo_work.p, 0, wb, st));
+        uint32_t *tick = (uint32_t *)e->kryo_work.p;
+        int64_t *cnt_dev = (int64_t *)((char *)e->kryo_work.p + 16);
+        uint64_t *status = (uint64_t *)((char *)e->kryo_work.p + 24);
+        hipEvent_t k0 = e->ev(), k1 = e->ev();
+        HIP_TRY(hipEventRecord(k0, st));
+        HIP_TRY(launch_kryo_deser16(e->kryo_in.p, total, e->sort_buf[0].p, cap, status, tick, cnt_dev, st));
+        HIP_TRY(hipEventRecord(k1, st));
+        record_stage(e, SGX_STAGE_DESERIALIZE, k0, k1);
+        uint32_t herr[4];
+        int64_t hcnt = 0;
+        HIP_TRY(hipMemcpyAsync(herr, tick, 16, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&hcnt, cnt_dev, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (herr[1] & 1u) return fail(SGX_ERR_TIMEOUT, "Kryo decoder look-back spin gave up");
+        if (herr[1] & 2u) return fail(SGX_ERR_INVALID, "fetched blocks are not a Kryo stream of (Long, Long) pairs");
+        if (hcnt < 0 || hcnt > cap) return fail(SGX_ERR_HIP, "internal error: Kryo record count %lld", (long long)hcnt);
+        if (hcnt >= (int64_t)INT32_MAX) return fail(SGX_ERR_INVALID, "%lld records exceed one read", (long long)hcnt);
+        *nrec = hcnt;
+        SGX_TRY(e->sort_buf[1].ensure((size_t)hcnt * 16));
+        return SGX_OK;
+    }
     const int64_t n = total / rb;
     if (n >= (int64_t)INT32_MAX) return fail(SGX_ERR_INVALID, "%lld records exceed one sorted read", (long long)n);
     *nrec = n;
     SGX_TRY(e->sort_buf[0].ensure((size_t)total));
     SGX_TRY(e->sort_buf[1].ensure((size_t)total));
-    *sorted = e->sort_buf[0].p;
     if (n == 0) return SGX_OK;
     SGX_TRY(fetch_locked(e, shuffle_id, mids.data(), rids.data(), nreq, e->sort_buf[0].p, total, SGX_MEM_DEVICE,
                          lens.data(), false));
+    return SGX_OK;
+}
+
+// Fetch the canonical blocks of reducers [r0, r1) x maps into e->sort_buf[0] and sort them
+// stably by key within each reducer.  On return (asynchronous on s_comp) *sorted points at
+// the device buffer holding the result and *nrec its record count.
+static int sort_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps, int32_t r0,
+                       int32_t r1, const void **sorted, int64_t *nrec) {
+    auto it = e->shuffles.find(shuffle_id);
+    if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
+    Shuffle &s = it->second;
+    const int rb = s.rb;
+    if (rb != 16 && rb != 100)
+        return fail(SGX_ERR_UNSUPPORTED, "sorted read needs 16 B (Long, Long) or 100 B TeraSort records, not %d B", rb);
+    int64_t n = 0;
+    SGX_TRY(records_locked(e, shuffle_id, map_ids, nmaps, r0, r1, &n));
+    *nrec = n;
+    *sorted = e->sort_buf[0].p;
+    if (n == 0) return SGX_OK;
     hipStream_t st = e->s_comp;
     constexpr int MAXP = 12;
     SGX_TRY(e->sort_err.ensure(MAXP * 4));
@@ -1258,6 +1383,12 @@ extern "C" int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t 
     auto it = e->shuffles.find(shuffle_id);
     if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
     const int rb = it->second.rb;
+    if (!dst && dst_cap == 0 && it->second.ser == SGX_SER_KRYO) {  // size query: decoded records
+        int64_t n = 0;
+        SGX_TRY(records_locked(e, shuffle_id, map_ids, nmaps, start_partition, end_partition, &n));
+        *out_bytes = n * rb;
+        return SGX_OK;
+    }
     if (!dst && dst_cap == 0) {  // size query: lengths only
         const int64_t nreq = (int64_t)std::max(0, end_partition - start_partition) * std::max<int64_t>(0, nmaps);
         if (start_partition < 0 || end_partition > it->second.R || start_partition > end_partition || nmaps < 0 ||
@@ -1284,6 +1415,29 @@ extern "C" int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t 
                                       (long long)(n * rb));
     if (n > 0 && !dst) return fail(SGX_ERR_INVALID, "dst is NULL");
     SGX_TRY(copy_out(e, dst, sorted, n * rb, dst_mem_kind));
+    HIP_TRY(hipStreamSynchronize(e->s_comp));
+    return SGX_OK;
+}
+
+extern "C" int sgx_read_records(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
+                                int32_t start_partition, int32_t end_partition, void *dst, int64_t dst_cap,
+                                int32_t dst_mem_kind, int64_t *out_bytes) {
+    if (!e || !out_bytes) return fail(SGX_ERR_INVALID, "NULL argument");
+    if (dst_mem_kind != SGX_MEM_HOST && dst_mem_kind != SGX_MEM_DEVICE)
+        return fail(SGX_ERR_INVALID, "unknown mem_kind %d", dst_mem_kind);
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    auto it = e->shuffles.find(shuffle_id);
+    if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
+    const int rb = it->second.rb;
+    int64_t n = 0;
+    SGX_TRY(records_locked(e, shuffle_id, map_ids, nmaps, start_partition, end_partition, &n));
+    *out_bytes = n * rb;
+    if (!dst && dst_cap == 0) return SGX_OK;  // size query
+    if (n * rb > dst_cap) return fail(SGX_ERR_INVALID, "destination capacity %lld < %lld bytes", (long long)dst_cap,
+                                      (long long)(n * rb));
+    if (n > 0 && !dst) return fail(SGX_ERR_INVALID, "dst is NULL");
+    SGX_TRY(copy_out(e, dst, e->sort_buf[0].p, n * rb, dst_mem_kind));
     HIP_TRY(hipStreamSynchronize(e->s_comp));
     return SGX_OK;
 }

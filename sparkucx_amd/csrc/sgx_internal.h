@@ -118,6 +118,19 @@ hipError_t launch_group_sums(const void *rec, int64_t n, const int64_t *starts, 
 int64_t reservoir_threads(int64_t n, int64_t k);
 hipError_t launch_reservoir(const void *recs, int64_t n, int rb, int key_bytes, int64_t k, uint64_t s0,
                             const uint64_t *jump_dev, long long *winner, void *out_keys, hipStream_t st);
+// Kryo (Long, Long) framing (sgx_serde.hip): n partition-contiguous 16 B records -> their
+// KryoSerializationStream bytes in `out` (capacity 20 n), partition byte offsets ser_off[R+1]
+// from the record offsets rec_off[R+1]; status: [kryo_ser16_tiles(n)] u64 and ticket_err[2]
+// zeroed by the caller (ticket_err[1] bit 0 = look-back gave up).
+int64_t kryo_ser16_tiles(int64_t n);
+hipError_t launch_kryo_ser16(const void *in, int64_t n, void *out, const uint32_t *rec_off, int R, int64_t *ser_off,
+                             uint64_t *status, uint32_t *ticket_err, hipStream_t st);
+// Kryo (Long, Long) stream of `bytes` bytes (16 B-aligned, readable to bytes + 32) -> 16 B
+// records (at most out_cap); *count_out = records; status [kryo_deser16_tiles] u64 and
+// ticket_err[2] zeroed by the caller (ticket_err[1]: bit 0 look-back gave up, bit 1 malformed).
+int64_t kryo_deser16_tiles(int64_t bytes);
+hipError_t launch_kryo_deser16(const void *in, int64_t bytes, void *out, int64_t out_cap, uint64_t *status,
+                               uint32_t *ticket_err, int64_t *count_out, hipStream_t st);
 hipError_t launch_gen_uniform16(void *dst, int64_t n, uint64_t seed, int64_t value_base,
                                 hipStream_t stream);
 hipError_t launch_gen_zipf16(void *dst, int64_t n, uint64_t seed, int64_t value_base,

@@ -2348,10 +2348,14 @@ __global__ __launch_bounds__(256) void k_gather_items(const int64_t *__restrict_
         const uint4 *s = (const uint4 *)(uintptr_t)it[0];
         uint4 *d = (uint4 *)(uintptr_t)it[1];
         for (int64_t i = threadIdx.x; i < (bytes >> 4); i += 256) d[i] = s[i];
-    } else {
+    } else if constexpr (ALIGN == 4) {
         const uint32_t *s = (const uint32_t *)(uintptr_t)it[0];
         uint32_t *d = (uint32_t *)(uintptr_t)it[1];
         for (int64_t i = threadIdx.x; i < (bytes >> 2); i += 256) d[i] = s[i];
+    } else {  // byte-granular blocks (Kryo-framed shuffles)
+        const uint8_t *s = (const uint8_t *)(uintptr_t)it[0];
+        uint8_t *d = (uint8_t *)(uintptr_t)it[1];
+        for (int64_t i = threadIdx.x; i < bytes; i += 256) d[i] = s[i];
     }
 }
 
@@ -2359,8 +2363,10 @@ hipError_t launch_gather_items(const int64_t *items, int64_t n_items, int align,
     if (n_items <= 0) return hipSuccess;
     if (align == 16)
         hipLaunchKernelGGL(k_gather_items<16>, dim3((unsigned)n_items), dim3(256), 0, stream, items);
-    else
+    else if (align == 4)
         hipLaunchKernelGGL(k_gather_items<4>, dim3((unsigned)n_items), dim3(256), 0, stream, items);
+    else
+        hipLaunchKernelGGL(k_gather_items<1>, dim3((unsigned)n_items), dim3(256), 0, stream, items);
     return hipGetLastError();
 }
 

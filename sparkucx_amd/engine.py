@@ -105,7 +105,8 @@ class ShuffleEngine:
 
     # -- shuffle registry -------------------------------------------------------------
     def register_shuffle(self, shuffle_id: int, num_partitions: int, kind: int = _lib.PART_HASH,
-                         bounds=None, ascending: bool = True, record_bytes: int = 16):
+                         bounds=None, ascending: bool = True, record_bytes: int = 16,
+                         serializer: int = _lib.SER_FIXED):
         ptr, nb = None, 0
         keep = None
         if bounds is not None and kind != _lib.PART_HASH:
@@ -118,6 +119,12 @@ class ShuffleEngine:
             ptr = keep.ctypes.data if nb else None
         check(lib().sgx_register_shuffle(self.handle, shuffle_id, num_partitions, kind, ptr, nb,
                                          int(bool(ascending)), record_bytes), "registerShuffle")
+        if serializer != _lib.SER_FIXED:
+            self.set_serializer(shuffle_id, serializer)
+
+    def set_serializer(self, shuffle_id: int, serializer: int):
+        """dep.serializer: SER_FIXED (fixed-width records) or SER_KRYO (Spark's Kryo stream)."""
+        check(lib().sgx_set_serializer(self.handle, shuffle_id, serializer), "setSerializer")
 
     def unregister_shuffle(self, shuffle_id: int):
         check(lib().sgx_unregister_shuffle(self.handle, shuffle_id), "unregisterShuffle")
@@ -210,6 +217,22 @@ class ShuffleEngine:
         ptr, cap, kind = buffer_arg(dst)
         check(lib().sgx_read_sorted(self.handle, shuffle_id, m.ctypes.data, len(m), start_partition, end_partition,
                                     ptr if cap else None, cap, kind, ctypes.byref(nbytes)), "readSorted")
+        return dst
+
+    def read_records(self, shuffle_id: int, map_ids: Sequence[int], start_partition: int, end_partition: int,
+                     dst=None) -> np.ndarray:
+        """UcxShuffleReader.read without aggregator or key ordering: the records of reducers
+        [start, end) x map_ids in the canonical order (a Kryo shuffle's stream decoded on the
+        GPU), back to back (host ndarray of bytes unless ``dst`` is given)."""
+        m = np.ascontiguousarray(map_ids, dtype=np.int64)
+        nbytes = ctypes.c_int64(0)
+        check(lib().sgx_read_records(self.handle, shuffle_id, m.ctypes.data, len(m), start_partition, end_partition,
+                                     None, 0, MEM_HOST, ctypes.byref(nbytes)), "readRecords")
+        if dst is None:
+            dst = np.empty(nbytes.value, dtype=np.uint8)
+        ptr, cap, kind = buffer_arg(dst)
+        check(lib().sgx_read_records(self.handle, shuffle_id, m.ctypes.data, len(m), start_partition, end_partition,
+                                     ptr if cap else None, cap, kind, ctypes.byref(nbytes)), "readRecords")
         return dst
 
     def read_grouped(self, shuffle_id: int, map_ids: Sequence[int], start_partition: int, end_partition: int,

@@ -88,6 +88,10 @@ class Aggregator:
             raise IllegalArgumentException(f"unsupported aggregator {self.kind!r} (group, sum)")
 
 
+_SERIALIZERS = {"fixed": _lib.SER_FIXED, "kryo": _lib.SER_KRYO,
+                "org.apache.spark.serializer.KryoSerializer": _lib.SER_KRYO}
+
+
 @dataclass
 class ShuffleDependency:
     partitioner: object
@@ -95,10 +99,18 @@ class ShuffleDependency:
     aggregator: Optional[Aggregator] = None  # dep.aggregator (reduce side only)
     keyOrdering: bool = False                # dep.keyOrdering: sort each reducer by key
     mapSideCombine: bool = False
+    # dep.serializer: "fixed" = the engine's fixed-width record codec; "kryo" =
+    # org.apache.spark.serializer.KryoSerializer with spark.shuffle.compress=false (the data
+    # file, index offsets and fetched blocks are Spark's own Kryo stream bytes)
+    serializer: str = "fixed"
 
     def __post_init__(self):
         if self.mapSideCombine:
             raise UnsupportedOperationException("map-side combine is not part of the GPU path (SURVEY §8(a) a1)")
+        if self.serializer not in _SERIALIZERS:
+            raise IllegalArgumentException(f"unknown serializer {self.serializer!r} (fixed, kryo)")
+        if self.serializer == "kryo" and self.recordBytes != 16:
+            raise UnsupportedOperationException("Kryo framing is for (Long, Long) 16 B records")
 
 
 @dataclass
@@ -439,6 +451,8 @@ class UcxShuffleReader:
             return self.manager.engine.read_grouped(sid, self._maps(), self.start, self.end, agg)
         if dep.keyOrdering:
             return self.manager.engine.read_sorted(sid, self._maps(), self.start, self.end).reshape(-1, dep.recordBytes)
+        if _SERIALIZERS[dep.serializer] != _lib.SER_FIXED:  # the Kryo stream, decoded on the GPU
+            return self.manager.engine.read_records(sid, self._maps(), self.start, self.end).reshape(-1, 16)
         data, _, _, _ = self.read_blocks()
         return data.reshape(-1, dep.recordBytes)
 
@@ -470,7 +484,8 @@ class UcxShuffleManager:
         p = dependency.partitioner
         bounds = getattr(p, "rangeBounds", None)
         self.engine.register_shuffle(shuffleId, p.numPartitions, p.kind, bounds,
-                                     getattr(p, "ascending", True), dependency.recordBytes)
+                                     getattr(p, "ascending", True), dependency.recordBytes,
+                                     _SERIALIZERS[dependency.serializer])
         h = BaseShuffleHandle(shuffleId, dependency)
         self._handles[shuffleId] = h
         self._maps[shuffleId] = set()

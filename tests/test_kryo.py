@@ -1,0 +1,225 @@
+"""Kryo-framed map output: Spark's KryoSerializer stream of (Long,
+Long) records with spark.shuffle.compress=false, written and read back on the GPU.
+
+CPU tests pin the two oracle restatements (pure Python, numpy) to the hand-computed known
+answers and to each other.  GPU tests compare the HIP path, through the C ABI, with the
+oracle and the golden fixtures byte for byte: partition lengths (= index offsets), the
+partition-contiguous Kryo stream, the index and data files, fetched blocks, and the
+decoded records / sorted / grouped reads of a Kryo shuffle against the fixed-codec ones.
+Parity against a JVM is unpinned (no JVM here)."""
+import glob
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+
+def _edge_records(n, seed):
+    rng = np.random.default_rng(seed)
+    k = rng.integers(-2**63, 2**63 - 1, size=n, dtype=np.int64, endpoint=True)
+    v = rng.integers(-2**63, 2**63 - 1, size=n, dtype=np.int64, endpoint=True)
+    sh = rng.integers(0, 64, size=n)
+    k = np.where(np.arange(n) % 3 == 0, k, k >> sh)
+    v = np.where(np.arange(n) % 2 == 0, v >> rng.integers(0, 64, size=n), v)
+    kv = np.stack([k, v], axis=1)
+    return np.ascontiguousarray(kv).view(np.uint8).reshape(-1, 16)
+
+
+# --------------------------------------------------------------------------- CPU ----
+def test_kats_python_restatement():
+    from oracle import spark_semantics as S
+
+    with open(os.path.join(GOLDEN, "kats_kryo.json")) as f:
+        kats = json.load(f)
+    for v, h in kats["varlong"]:
+        assert S.kryo_write_var_long(v).hex() == h
+        assert S.kryo_read_var_long(bytes.fromhex(h), 0) == (v, len(h) // 2)
+    for kv, h in kats["record"]:
+        assert S.kryo_serialize_pairs([tuple(kv)]).hex() == h
+        assert S.kryo_deserialize_pairs(bytes.fromhex(h)) == [tuple(kv)]
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_numpy_restatement_matches_python(seed):
+    import oracle
+    from oracle import spark_semantics as S
+
+    recs = _edge_records(2000 + seed, seed)
+    pairs = [tuple(map(int, r)) for r in recs.view(np.int64).reshape(-1, 2)]
+    want = S.kryo_serialize_pairs(pairs)
+    assert oracle.kryo_serialize(recs).tobytes() == want
+    assert int(oracle.kryo_record_lengths(recs).sum()) == len(want)
+    assert S.kryo_deserialize_pairs(want) == pairs
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "kryo_*.npz"))))
+def test_golden_fixtures_consistent(path, oracle_lib):
+    z = np.load(path)
+    R = int(z["num_partitions"])
+    out, counts = oracle_lib.map_write(z["records"], R)
+    assert np.array_equal(oracle_lib.kryo_serialize(out), z["kryo_stream"])
+    off = oracle_lib.kryo_partition_offsets(out, counts)
+    assert np.array_equal(np.diff(off), z["kryo_lengths"])
+    assert oracle_lib.index_bytes(z["kryo_lengths"]) == z["index"].tobytes()
+
+
+def test_dependency_rejects_kryo_on_wide_records(sgx_lib):
+    with pytest.raises(sgx_lib.UnsupportedOperationException):
+        sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(4), 100, serializer="kryo")
+    with pytest.raises(sgx_lib.IllegalArgumentException):
+        sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(4), 16, serializer="java")
+
+
+# --------------------------------------------------------------------------- GPU ----
+_sid = [5000]
+
+
+def _next_sid():
+    _sid[0] += 1
+    return _sid[0]
+
+
+def _kryo_map(engine, recs, R, map_id=0, sid=None, device=False):
+    import sparkucx_amd as sgx
+
+    if sid is None:
+        sid = _next_sid()
+        engine.register_shuffle(sid, R, serializer=sgx.SER_KRYO)
+    src = np.ascontiguousarray(recs)
+    if device:
+        buf = engine.alloc(max(src.nbytes, 16))
+        buf.copy_from(src)
+        src = buf
+    lengths = engine.write_map(sid, map_id, src, recs.shape[0], 16, R)
+    return sid, lengths
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "kryo_*.npz"))))
+def test_gpu_golden_kryo(engine, path, tmp_path):
+    z = np.load(path)
+    R = int(z["num_partitions"])
+    sid, lengths = _kryo_map(engine, z["records"], R)
+    try:
+        assert np.array_equal(lengths, z["kryo_lengths"]), "Kryo partition lengths differ"
+        assert np.array_equal(engine.map_output_bytes(sid, 0), z["kryo_stream"]), "Kryo stream differs"
+        idx, dat = str(tmp_path / "i"), str(tmp_path / "d")
+        engine.write_index(sid, 0, idx, dat, R)
+        assert open(idx, "rb").read() == z["index"].tobytes()
+        assert open(dat, "rb").read() == z["kryo_stream"].tobytes()
+    finally:
+        engine.unregister_shuffle(sid)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,R,seed", [(0, 16, 0), (1, 1, 1), (2047, 7, 2), (2048, 1024, 3), (2049, 200, 4),
+                                      (100_003, 1024, 5), (1 << 20, 1024, 6), (300_001, 4096, 7)])
+def test_gpu_kryo_vs_oracle(engine, oracle_lib, n, R, seed):
+    recs = _edge_records(n, seed) if seed % 2 else oracle_lib.gen_uniform16(n, 0x5EEDC0DE + seed)
+    out, counts = oracle_lib.map_write(recs, R, nthreads=8)
+    want = oracle_lib.kryo_serialize(out)
+    off = oracle_lib.kryo_partition_offsets(out, counts)
+    sid, lengths = _kryo_map(engine, recs, R, device=bool(seed & 2))
+    try:
+        assert np.array_equal(lengths, np.diff(off))
+        got = engine.map_output_bytes(sid, 0)
+        if not np.array_equal(got, want):
+            bad = np.nonzero(got != want)[0] if got.shape == want.shape else [-1]
+            pytest.fail(f"Kryo stream differs ({got.size} vs {want.size} bytes), first at {bad[:5]}")
+    finally:
+        engine.unregister_shuffle(sid)
+
+
+@pytest.mark.gpu
+def test_gpu_kryo_fetch_and_reduce_side(engine, oracle_lib):
+    """Blocks of several maps: fetched bytes are the Kryo slices (byte-granular gather);
+    read_records decodes them on the GPU to the canonical records; sorted and grouped reads
+    of the Kryo shuffle equal those of the same data under the fixed codec."""
+    import sparkucx_amd as sgx
+
+    R, nmaps = 64, 3
+    maps = [(_edge_records(5000 + 37 * m, 11 + m) if m == 1 else oracle_lib.gen_uniform16(5000 + 37 * m, 99 + m))
+            for m in range(nmaps)]
+    sk, sf = _next_sid(), _next_sid()
+    engine.register_shuffle(sk, R, serializer=sgx.SER_KRYO)
+    engine.register_shuffle(sf, R)
+    try:
+        outs = []
+        for m, recs in enumerate(maps):
+            _kryo_map(engine, recs, R, map_id=m, sid=sk)
+            engine.write_map(sf, m, np.ascontiguousarray(recs), recs.shape[0], 16, R)
+            outs.append(oracle_lib.map_write(recs, R))
+        # fetch: arbitrary block order, byte-exact slices of each map's Kryo stream
+        mids = [2, 0, 1, 1, 0, 2]
+        rids = [5, 63, 0, 17, 17, 40]
+        data, lens = engine.fetch_blocks(sk, mids, rids)
+        pos = 0
+        for m, r, L in zip(mids, rids, lens):
+            out, counts = outs[m]
+            o = oracle_lib.offsets(counts)
+            want = oracle_lib.kryo_serialize(out[o[r]:o[r + 1]])
+            assert L == want.size
+            assert np.array_equal(data[pos:pos + L], want)
+            pos += L
+        # decoded records, canonical order, against the fixed-codec blocks
+        for r0, r1 in [(0, R), (5, 6), (10, 40)]:
+            got = engine.read_records(sk, list(range(nmaps)), r0, r1)
+            want = engine.read_records(sf, list(range(nmaps)), r0, r1)
+            assert np.array_equal(got, want)
+            assert np.array_equal(engine.read_sorted(sk, list(range(nmaps)), r0, r1),
+                                  engine.read_sorted(sf, list(range(nmaps)), r0, r1))
+            for agg in (sgx.AGG_GROUP, sgx.AGG_SUM):
+                a = engine.read_grouped(sk, list(range(nmaps)), r0, r1, agg)
+                b = engine.read_grouped(sf, list(range(nmaps)), r0, r1, agg)
+                for x, y in zip(a, b):
+                    assert np.array_equal(x, y)
+        assert engine.read_records(sk, [0], 3, 3).size == 0
+    finally:
+        engine.unregister_shuffle(sk)
+        engine.unregister_shuffle(sf)
+
+
+@pytest.mark.gpu
+def test_gpu_kryo_plugin_mirror(tmp_path, oracle_lib):
+    """The plugin mirror end to end with serializer="kryo": writer lengths, index file
+    through the resolver, and the reader's records."""
+    import sparkucx_amd as sgx
+
+    R = 200
+    recs = oracle_lib.gen_uniform16(20_000, 7)
+    out, counts = oracle_lib.map_write(recs, R)
+    off = oracle_lib.kryo_partition_offsets(out, counts)
+    mgr = sgx.UcxShuffleManager(device=0, localDir=str(tmp_path))
+    try:
+        h = mgr.registerShuffle(3, sgx.ShuffleDependency(sgx.HashPartitioner(R), 16, serializer="kryo"))
+        w = mgr.getWriter(h, 0)
+        w.write(recs)
+        assert np.array_equal(w.getPartitionLengths(), np.diff(off))
+        got = mgr.getReader(h, 0, R).read()
+        assert np.array_equal(got, out)
+    finally:
+        mgr.stop()
+
+
+@pytest.mark.gpu
+def test_gpu_set_serializer_state_rules(engine):
+    import sparkucx_amd as sgx
+
+    sid = _next_sid()
+    engine.register_shuffle(sid, 8)
+    try:
+        engine.write_map(sid, 0, np.zeros((4, 16), np.uint8), 4, 16, 8)
+        with pytest.raises(sgx.IllegalStateException):
+            engine.set_serializer(sid, sgx.SER_KRYO)
+    finally:
+        engine.unregister_shuffle(sid)
+    sid = _next_sid()
+    engine.register_shuffle(sid, 8, record_bytes=100)
+    try:
+        with pytest.raises(sgx.UnsupportedOperationException):
+            engine.set_serializer(sid, sgx.SER_KRYO)
+    finally:
+        engine.unregister_shuffle(sid)
