@@ -141,7 +141,7 @@ struct MapOut {
     // serializer KRYO (sgx_set_serializer): the map's published bytes are the Kryo stream of
     // its records (data file, fetch, exchange); `data` keeps the 16 B records
     DevBuf ser;                // Kryo-framed partition-contiguous bytes (capacity 20 n + 16)
-    DevBuf ser_work;           // ser_off_dev (R+1) i64 | ticket, error u32 x 4 | look-back status
+    DevBuf ser_work;           // ser_off_dev (R+1) i64 | error u32 x 4 | tile prefixes u64, tile sums u32
     HostPinned ser_off;        // (R+1) i64 byte offsets + the error word, landed async
     int64_t out_bytes = 0;     // published bytes (n * rb, or the Kryo total once `ready`)
     const void *view() const { return ser.p ? ser.p : data.p; }
@@ -635,15 +635,15 @@ static int serialize_kryo(sgx_engine *e, Shuffle &s, MapOut &m) {
     const int64_t tiles = kryo_ser16_tiles(n);
     const size_t offb = (size_t)(s.R + 1) * 8;
     SGX_TRY(m.ser.ensure((size_t)(20 * n + 16)));
-    SGX_TRY(m.ser_work.ensure(offb + 16 + (size_t)tiles * 8));
+    SGX_TRY(m.ser_work.ensure(offb + 16 + (size_t)kryo_work_bytes(tiles)));
     SGX_TRY(m.ser_off.ensure(offb + 8));
     int64_t *off_dev = (int64_t *)m.ser_work.p;
     uint32_t *tick = (uint32_t *)((char *)m.ser_work.p + offb);
     uint64_t *status = (uint64_t *)((char *)m.ser_work.p + offb + 16);
-    HIP_TRY(hipMemsetAsync(m.ser_work.p, 0, offb + 16 + (size_t)tiles * 8, st));
+    HIP_TRY(hipMemsetAsync(m.ser_work.p, 0, offb + 16, st));  // partition offsets, error word
     hipEvent_t k0 = e->ev(), k1 = e->ev();
     HIP_TRY(hipEventRecord(k0, st));
-    HIP_TRY(launch_kryo_ser16(m.data.p, n, m.ser.p, e->last_off_dev, s.R, off_dev, status, tick, st));
+    HIP_TRY(launch_kryo_ser16(m.data.p, n, m.ser.p, e->last_off_dev, s.R, off_dev, status, tick, e->num_cus, st));
     HIP_TRY(hipEventRecord(k1, st));
     record_stage(e, SGX_STAGE_SERIALIZE, k0, k1);
     // (R+1) offsets, then the error word in the low half of slot R+1
@@ -1257,9 +1257,8 @@ static int records_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_
         SGX_TRY(fetch_locked(e, shuffle_id, mids.data(), rids.data(), nreq, e->kryo_in.p, total, SGX_MEM_DEVICE,
                              lens.data(), false));
         const int64_t tiles = kryo_deser16_tiles(total);
-        const size_t wb = 16 + 8 + (size_t)tiles * 8;
-        SGX_TRY(e->kryo_work.ensure(wb));
-        HIP_TRY(hipMemsetAsync(e->kryo_work.p, 0, wb, st));
+        SGX_TRY(e->kryo_work.ensure(24 + (size_t)kryo_work_bytes(tiles)));
+        HIP_TRY(hipMemsetAsync(e->kryo_work.p, 0, 24, st));  // error word, record count
         uint32_t *tick = (uint32_t *)e->kryo_work.p;
         int64_t *cnt_dev = (int64_t *)((char *)e->kryo_work.p + 16);
         uint64_t *status = (uint64_t *)((char *)e->kryo_work.p + 24);

@@ -2352,10 +2352,25 @@ __global__ __launch_bounds__(256) void k_gather_items(const int64_t *__restrict_
         const uint32_t *s = (const uint32_t *)(uintptr_t)it[0];
         uint32_t *d = (uint32_t *)(uintptr_t)it[1];
         for (int64_t i = threadIdx.x; i < (bytes >> 2); i += 256) d[i] = s[i];
-    } else {  // byte-granular blocks (Kryo-framed shuffles)
+    } else {
+        // byte-granular blocks (Kryo-framed shuffles): the destination's whole dwords are
+        // built from two aligned source dwords (a dword that holds a valid source byte lies
+        // inside the allocation), the head / tail bytes are copied one by one
         const uint8_t *s = (const uint8_t *)(uintptr_t)it[0];
         uint8_t *d = (uint8_t *)(uintptr_t)it[1];
-        for (int64_t i = threadIdx.x; i < bytes; i += 256) d[i] = s[i];
+        const int64_t hb = min<int64_t>(bytes, (int64_t)((4u - ((uintptr_t)d & 3u)) & 3u));
+        const int64_t nw = (bytes - hb) >> 2;
+        const int64_t tb = hb + 4 * nw;
+        if ((int64_t)threadIdx.x < hb) d[threadIdx.x] = s[threadIdx.x];
+        if ((int64_t)threadIdx.x < bytes - tb) d[tb + threadIdx.x] = s[tb + threadIdx.x];
+        const uint8_t *sb = s + hb;
+        const uint32_t sh = 8u * (uint32_t)((uintptr_t)sb & 3u);
+        const uint32_t *sw = (const uint32_t *)((uintptr_t)sb & ~(uintptr_t)3);
+        uint32_t *dw = (uint32_t *)(d + hb);
+        for (int64_t i = threadIdx.x; i < nw; i += 256) {
+            const uint32_t lo = sw[i];
+            dw[i] = sh ? (lo >> sh) | (sw[i + 1] << (32u - sh)) : lo;
+        }
     }
 }
 

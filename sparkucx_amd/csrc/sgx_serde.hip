@@ -13,21 +13,20 @@
 // its records' encodings back to back in map order; the index offsets
 // (IndexShuffleBlockResolver.writeIndexFileAndCommit, :161-217) are byte offsets of that.
 //
-// One pass over the partition-contiguous 16 B records (K4's output): a tile of 2048
-// records computes every record's encoded length, scans them (block scan + decoupled
-// look-back over tiles for the 64-bit byte prefix), encodes the tile into LDS at its final
-// alignment, and writes it out with 16 B stores (byte stores only for the two edge words
-// it shares with the neighbouring tiles).  The tile that holds a partition's first record
-// also writes that partition's byte offset.  HBM-bound: 16 B read + the encoded bytes
-// written per record.
+// Reduce-then-scan over the partition-contiguous 16 B records (K4's output): (1) every tile
+// of 1024 records sums its records' encoded lengths, (2) one workgroup scans the tile sums
+// into 64-bit byte prefixes, (3) every tile computes its records' offsets (block scan),
+// encodes them into LDS at the output's 16 B phase and writes the tile out with 16 B stores
+// (byte stores only for the two edge words it shares with its neighbours).  The tile that
+// holds a partition's first record also writes that partition's byte offset.  HBM-bound:
+// 16 B read twice + the encoded bytes written per record.
 #include "sgx_internal.h"
 
 namespace sgx {
 namespace {
 
-constexpr int KS_THREADS = 256, KS_ITEMS = 8, KS_TILE = KS_THREADS * KS_ITEMS;
+constexpr int KS_THREADS = 256, KS_ITEMS = 4, KS_TILE = KS_THREADS * KS_ITEMS;
 constexpr int KS_MAXREC = 20;  // 2 class bytes + 2 x 9 varlong bytes
-constexpr uint64_t KS_AGG = 1ull << 62, KS_PRE = 2ull << 62, KS_VAL = (1ull << 62) - 1;
 
 __device__ __forceinline__ uint64_t zigzag(uint64_t v) { return (v << 1) ^ (uint64_t)((int64_t)v >> 63); }
 
@@ -69,63 +68,100 @@ __device__ __forceinline__ void or_shifted(uint64_t w[3], uint64_t lo, uint64_t 
 }
 
 
-// Decoupled look-back by one whole wave (call from wave 0 only, every lane): publishes this
-// tile's aggregate, then reads 64 predecessors' status words per step, from the nearest
-// back; stops at the first inclusive prefix.  A walk of d tiles costs ~d/64 L2 round trips
-// (one lane walking one tile per round trip made every tile wait ~tens of µs).  Returns the
-// exclusive prefix (every lane); publishes the inclusive one.  Bounded spin -> err bit 0.
-__device__ uint64_t wave_look_back(uint64_t *status, uint32_t tile, uint64_t agg, uint32_t lane, uint32_t *err) {
-    if (tile == 0) {
-        if (lane == 0) __hip_atomic_store(&status[0], KS_PRE | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return 0;
-    }
-    if (lane == 0) __hip_atomic_store(&status[tile], KS_AGG | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t excl = 0;
-    int64_t j = (int64_t)tile - 1;  // lane l looks at tile j - l
-    uint32_t spins = 0;
-    while (true) {
-        const int64_t idx = j - (int64_t)lane;
-        const uint64_t st = idx >= 0 ? __hip_atomic_load(&status[idx], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                     : KS_PRE;  // before tile 0: prefix 0
-        const uint64_t flag = st & ~KS_VAL;
-        const uint64_t pre = __ballot(flag == KS_PRE);
-        const uint64_t notready = __ballot(flag == 0);
-        const uint32_t last = pre ? (uint32_t)__ffsll((long long)pre) - 1u : 63u;  // lanes 0..last count
-        const uint64_t upto = last == 63u ? ~0ull : ((1ull << (last + 1u)) - 1ull);
-        if (notready & upto) {
-            if (++spins > (1u << 24)) {
-                if (lane == 0) atomicOr(err, 1u);
-                break;
-            }
-            __builtin_amdgcn_s_sleep(1);
-            continue;
-        }
-        uint64_t v = lane <= last ? (st & KS_VAL) : 0ull;
+// Exclusive scan of per-tile u32 aggregates into u64 prefixes (one workgroup; a few
+// hundred thousand tiles take tens of µs).  The serializer and decoder are reduce-then-scan:
+// a single pass with decoupled look-back measured ~20 µs per tile of waiting on gfx950 (the
+// status words are agent-coherent, i.e. they cross the XCDs' L2s), bounding both kernels by
+// latency, not by HBM.
+constexpr int TS_THREADS = 1024, TS_PER = 4, TS_BLOCK = TS_THREADS * TS_PER;
+// Workspace after the tile sums: excl[tiles] (exclusive prefix within a block of TS_BLOCK
+// tiles) | btot[ceil(tiles / TS_BLOCK)] (block totals).  tile_base() adds the totals of the
+// blocks before the tile's: at most a few hundred values, one wave, coalesced.
+__global__ __launch_bounds__(TS_THREADS) void k_tile_scan64(const uint32_t *__restrict__ agg, int64_t ntiles,
+                                                            uint64_t *__restrict__ excl, uint64_t *__restrict__ btot) {
+    __shared__ uint64_t s_w[TS_THREADS / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t b = (int64_t)blockIdx.x * TS_BLOCK + (int64_t)tid * TS_PER;
+    uint32_t v[TS_PER];
+    uint64_t sum = 0;
 #pragma unroll
-        for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-        excl += v;
-        if (pre) break;
-        j -= 64;
+    for (int i = 0; i < TS_PER; ++i) {
+        v[i] = b + i < ntiles ? agg[b + i] : 0u;
+        sum += v[i];
     }
-    if (lane == 0)
-        __hip_atomic_store(&status[tile], KS_PRE | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return excl;
+    uint64_t x = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = __shfl_up(x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint64_t run = x - sum, tot = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < TS_THREADS / 64; ++q) {
+        if (q < w) run += s_w[q];
+        tot += s_w[q];
+    }
+#pragma unroll
+    for (int i = 0; i < TS_PER; ++i) {
+        if (b + i < ntiles) excl[b + i] = run;
+        run += v[i];
+    }
+    if (tid == 0) btot[blockIdx.x] = tot;
+}
+
+// prefix of `tile` (call from a whole wave; every lane gets it)
+__device__ __forceinline__ uint64_t tile_base(const uint64_t *excl, const uint64_t *btot, uint32_t tile,
+                                              uint32_t lane) {
+    const uint32_t nb = tile / TS_BLOCK;
+    uint64_t v = 0;
+    for (uint32_t i = lane; i < nb; i += 64) v += btot[i];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v + excl[tile];
+}
+
+__global__ __launch_bounds__(KS_THREADS) void k_kryo_len16(const uint4 *__restrict__ in, int64_t n,
+                                                           uint32_t *__restrict__ agg) {
+    __shared__ uint32_t s_w[KS_THREADS / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t t0 = (int64_t)blockIdx.x * KS_TILE;
+    const int64_t tn = min((int64_t)KS_TILE, n - t0);
+    uint32_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < KS_ITEMS; ++k) {
+        const int64_t i = (int64_t)k * KS_THREADS + tid;
+        if (i < tn) {
+            const uint4 r = in[t0 + i];
+            sum += 2u + varlong_len(zigzag((uint64_t)r.x | ((uint64_t)r.y << 32))) +
+                   varlong_len(zigzag((uint64_t)r.z | ((uint64_t)r.w << 32)));
+        }
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) sum += __shfl_xor(sum, d, 64);
+    if (lane == 0) s_w[w] = sum;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t t = 0;
+        for (int q = 0; q < KS_THREADS / 64; ++q) t += s_w[q];
+        agg[blockIdx.x] = t;
+    }
 }
 
 __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(const uint4 *__restrict__ in, int64_t n,
                                                            uint8_t *__restrict__ out,
                                                            const uint32_t *__restrict__ rec_off, int R,
-                                                           int64_t *__restrict__ ser_off, uint64_t *status,
-                                                           uint32_t *ticket_err) {
+                                                           int64_t *__restrict__ ser_off, const uint64_t *status,
+                                                           const uint64_t *btot, uint32_t *ticket_err) {
     __shared__ __attribute__((aligned(16))) uint8_t s_len[KS_TILE];
     __shared__ __attribute__((aligned(16))) uint32_t s_off[KS_TILE];
     __shared__ __attribute__((aligned(16))) uint8_t s_out[KS_TILE * KS_MAXREC + 16];
-    __shared__ uint32_t s_tile, s_wsum[KS_THREADS / 64];
+    __shared__ uint32_t s_wsum[KS_THREADS / 64];
     __shared__ uint64_t s_base;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(&ticket_err[0], 1u);  // dispatch-order tiles: look-back progress
-    __syncthreads();
-    const uint32_t tile = s_tile;
+    const uint32_t tile = blockIdx.x;
+    (void)ticket_err;
     const int64_t t0 = (int64_t)tile * KS_TILE;
     const int64_t tn = min((int64_t)KS_TILE, n - t0);
 
@@ -142,16 +178,13 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(const uint4 *__restri
         s_len[i] = i < tn ? (uint8_t)(2u + varlong_len(zigzag(key)) + varlong_len(zigzag(val))) : (uint8_t)0;
     }
     __syncthreads();
-    // thread t owns records [8t, 8t+8) for the scan
-    const uint2 l8 = ((const uint2 *)s_len)[tid];
+    // thread t owns records [KS_ITEMS t, KS_ITEMS (t+1)) for the scan
     uint32_t lv[KS_ITEMS], sum = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        lv[j] = (l8.x >> (8 * j)) & 0xFFu;
-        lv[4 + j] = (l8.y >> (8 * j)) & 0xFFu;
+    for (int j = 0; j < KS_ITEMS; ++j) {
+        lv[j] = s_len[tid * KS_ITEMS + j];
+        sum += lv[j];
     }
-#pragma unroll
-    for (int j = 0; j < KS_ITEMS; ++j) sum += lv[j];
     const uint32_t incl = ks_wave_scan(sum, lane);
     if (lane == 63) s_wsum[w] = incl;
     __syncthreads();
@@ -162,16 +195,13 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(const uint4 *__restri
         agg += s_wsum[q];
     }
     {
-        uint32_t o[KS_ITEMS];
 #pragma unroll
-        for (int j = 0; j < KS_ITEMS; ++j) { o[j] = run; run += lv[j]; }
-        ((uint4 *)s_off)[2 * tid] = make_uint4(o[0], o[1], o[2], o[3]);
-        ((uint4 *)s_off)[2 * tid + 1] = make_uint4(o[4], o[5], o[6], o[7]);
+        for (int j = 0; j < KS_ITEMS; ++j) { s_off[tid * KS_ITEMS + j] = run; run += lv[j]; }
     }
-    // decoupled look-back over tiles (wave 0): 64-bit byte prefix
+    // the tile's byte prefix from the reduce-then-scan pre-pass
     if (w == 0) {
-        const uint64_t excl = wave_look_back(status, tile, agg, lane, &ticket_err[1]);
-        if (lane == 0) s_base = excl;
+        const uint64_t b0 = tile_base(status, btot, tile, lane);
+        if (lane == 0) s_base = b0;
     }
     __syncthreads();
     const uint64_t B = s_base;
@@ -248,108 +278,193 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(const uint4 *__restri
 // has it set -- except a 9-byte varlong's last byte, which may have it set; that byte is the
 // 9th of a run of 9 high bytes (runs are at most 9 long: a varlong is framed by class
 // bytes).  So "token end" = a low byte, or a high byte after 8 high bytes; every record
-// holds exactly 4 token ends, and record k+1 starts right after token end 4k+3.  One pass:
-// flag the token ends of a tile (32 bytes per thread), count them (block scan + decoupled
-// look-back over tiles), and the thread holding token end 4k+3 parses record k+1 from the
-// next byte (record 0 from byte 0).  Class bytes are checked, reads stay below B, writes
-// below out_cap; err bit 1 = malformed stream, bit 0 = look-back gave up.
+// holds exactly 4 token ends, and record k+1 starts right after token end 4k+3.
+// Reduce-then-scan: (1) every tile of 16 KB counts its token ends, (2) the tile counts are
+// scanned, (3) every tile stages its bytes in LDS, flags its token ends again (64 bytes per
+// thread), and the thread holding token end 4k+3 parses record k+1 from the next byte
+// (record 0 from byte 0) with a branch-free varlong decode.  Class bytes are checked,
+// reads stay below B, writes below out_cap; err bit 1 = malformed stream.
 // ------------------------------------------------------------------------------------
-constexpr int KD_THREADS = 256, KD_BYTES = 32, KD_TILE = KD_THREADS * KD_BYTES;
+constexpr int KD_THREADS = 256, KD_BYTES = 64, KD_TILE = KD_THREADS * KD_BYTES;
+constexpr int KD_STAGE = 16 + KD_TILE + 64;  // bytes [t0 - 16, t0 + KD_TILE + 64) of the stream
 
-__device__ __forceinline__ bool parse_pair(const uint8_t *__restrict__ in, int64_t B, int64_t p, uint64_t *kv) {
+// 24 bytes of the LDS stage from byte offset q (q + 28 <= KD_STAGE) as 3 little-endian u64
+__device__ __forceinline__ void lds_window(const uint32_t *s32, uint32_t q, uint64_t W[3]) {
+    const uint32_t b = q >> 2, sh = 8u * (q & 3u);
+    uint32_t d[7];
 #pragma unroll
-    for (int f = 0; f < 2; ++f) {
-        if (p >= B || in[p] != 0x09) return false;
-        ++p;
-        uint64_t z = 0;
-        for (int i = 0; i < 9; ++i) {
-            if (p >= B) return false;
-            const uint64_t b = in[p++];
-            if (i == 8) { z |= b << 56; break; }
-            z |= (b & 0x7Full) << (7 * i);
-            if (!(b & 0x80ull)) break;
-        }
-        kv[f] = (z >> 1) ^ (0ull - (z & 1ull));
+    for (int i = 0; i < 7; ++i) d[i] = s32[b + i];
+    uint32_t x[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) x[i] = sh ? (d[i] >> sh) | (d[i + 1] << (32u - sh)) : d[i];
+    W[0] = (uint64_t)x[0] | ((uint64_t)x[1] << 32);
+    W[1] = (uint64_t)x[2] | ((uint64_t)x[3] << 32);
+    W[2] = (uint64_t)x[4] | ((uint64_t)x[5] << 32);
+}
+
+// the 8 bytes at byte offset q (0 <= q <= 16) of the window, and the byte at q + 8
+__device__ __forceinline__ uint64_t win8(const uint64_t W[3], uint32_t q) {
+    const uint32_t r = 8u * (q & 7u);
+    const uint64_t a = q < 8 ? W[0] : (q < 16 ? W[1] : W[2]);
+    const uint64_t b = q < 8 ? W[1] : W[2];
+    return r ? (a >> r) | (b << (64u - r)) : a;
+}
+
+// Kryo 4 Input.readVarLong(false) on 9 window bytes: lo = bytes 0..7, hi = byte 8.
+__device__ __forceinline__ uint64_t varlong_decode(uint64_t lo, uint32_t hi, uint32_t &L) {
+    const uint64_t m = ~lo & 0x8080808080808080ull;  // bytes without the continuation bit
+    L = m ? (uint32_t)(__ffsll((long long)m) - 1) / 8u + 1u : 9u;
+    const uint64_t keep = L >= 8 ? ~0ull : ((1ull << (8 * L)) - 1ull);
+    const uint64_t x = lo & keep;
+    uint64_t z = 0;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) z |= ((x >> (8 * i)) & 0x7Full) << (7 * i);
+    if (L == 9) z |= (uint64_t)(hi & 0xFFu) << 56;
+    return (z >> 1) ^ (0ull - (z & 1ull));
+}
+
+// one (Long, Long) record at stage offset q (stream position p); false if malformed
+__device__ __forceinline__ bool parse_pair_lds(const uint32_t *s32, uint32_t q, int64_t p, int64_t B,
+                                               uint64_t kv[2]) {
+    uint64_t W[3];
+    lds_window(s32, q, W);
+    uint32_t L1, L2;
+    const uint64_t lo1 = win8(W, 1);
+    kv[0] = varlong_decode(lo1, (uint32_t)(win8(W, 9) & 0xFFu), L1);
+    const uint32_t c2 = 1u + L1;
+    const uint32_t cls2 = (uint32_t)(win8(W, c2) & 0xFFu);
+    kv[1] = varlong_decode(win8(W, c2 + 1u), (uint32_t)(win8(W, c2 + 9u) & 0xFFu), L2);
+    return (W[0] & 0xFFu) == 0x09u && cls2 == 0x09u && p + 2 + (int64_t)L1 + (int64_t)L2 <= B;
+}
+
+// top bits of a dword's 4 bytes as a nibble (byte 0 -> bit 0): one multiply
+__device__ __forceinline__ uint32_t top_bits4(uint32_t d) {
+    return (((d >> 7) & 0x01010101u) * 0x10204080u) >> 28;
+}
+
+// token-end mask of the 64 bytes [p0, p0 + 64) given bytes [p0 - 16, p0 + 64) as q[0..4]:
+// per 32-byte half, h = top bits of bytes [ph - 16, ph + 32) (48 bits, missing bytes 0);
+// a byte ends a token if its top bit is clear or it and the 8 bytes before it are all high
+__device__ __forceinline__ uint64_t tok_mask64(const uint4 q[5], int64_t p0, int64_t B) {
+    uint32_t nib[20];
+#pragma unroll
+    for (int v = 0; v < 5; ++v) {
+        nib[4 * v + 0] = top_bits4(q[v].x);
+        nib[4 * v + 1] = top_bits4(q[v].y);
+        nib[4 * v + 2] = top_bits4(q[v].z);
+        nib[4 * v + 3] = top_bits4(q[v].w);
     }
-    return true;
+    uint64_t tok = 0;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        const int64_t ph = p0 + 32 * half;
+        uint64_t h = 0;
+#pragma unroll
+        for (int k = 0; k < 12; ++k) h |= (uint64_t)nib[8 * half + k] << (4 * k);
+        // bytes before the stream start or at / past B do not exist
+        const int64_t lo = -(ph - 16), hi = B - (ph - 16);  // valid bit range [lo, hi)
+        const uint64_t above = lo <= 0 ? ~0ull : (lo >= 64 ? 0ull : ~0ull << lo);
+        const uint64_t below = hi >= 64 ? ~0ull : (hi <= 0 ? 0ull : (1ull << hi) - 1ull);
+        h &= above & below;
+        uint64_t a = h & (h << 1);
+        a &= a << 2;
+        a &= a << 4;
+        a &= h << 8;  // bit i: bytes i-8 .. i all high
+        const uint64_t t = ((~h | a) >> 16) & 0xFFFFFFFFull & below >> 16;
+        tok |= t << (32 * half);
+    }
+    return tok;
+}
+
+__global__ __launch_bounds__(KD_THREADS) void k_kryo_tok(const uint8_t *__restrict__ in, int64_t B,
+                                                         uint32_t *__restrict__ agg) {
+    __shared__ uint32_t s_w[KD_THREADS / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t p0 = (int64_t)blockIdx.x * KD_TILE + (int64_t)tid * KD_BYTES;
+    uint32_t cnt = 0;
+    if (p0 < B) {  // bytes [p0 - 16, p0 + 64) are readable (the buffer holds B + 64)
+        uint4 q[5];
+#pragma unroll
+        for (int v = 0; v < 5; ++v) {
+            const int64_t g = p0 - 16 + 16 * v;
+            q[v] = g >= 0 ? *(const uint4 *)(in + g) : make_uint4(0, 0, 0, 0);
+        }
+        cnt = (uint32_t)__popcll(tok_mask64(q, p0, B));
+    }
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) cnt += __shfl_xor(cnt, d, 64);
+    if (lane == 0) s_w[w] = cnt;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t t = 0;
+        for (int q = 0; q < KD_THREADS / 64; ++q) t += s_w[q];
+        agg[blockIdx.x] = t;
+    }
 }
 
 __global__ __launch_bounds__(KD_THREADS) void k_kryo_deser16(const uint8_t *__restrict__ in, int64_t B,
                                                              uint4 *__restrict__ out, int64_t out_cap,
-                                                             uint64_t *status, uint32_t *ticket_err,
-                                                             int64_t *count_out) {
-    __shared__ uint32_t s_tile, s_wsum[KD_THREADS / 64];
+                                                             const uint64_t *status, const uint64_t *btot,
+                                                             uint32_t *ticket_err, int64_t *count_out) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[KD_STAGE];
+    __shared__ uint32_t s_wsum[KD_THREADS / 64];
     __shared__ uint64_t s_base;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(&ticket_err[0], 1u);
+    const uint32_t *s32 = (const uint32_t *)s_in;
+    const uint32_t tile = blockIdx.x;
+    const int64_t t0 = (int64_t)tile * KD_TILE;
+    // stage [t0 - 16, t0 + KD_TILE + 64): the buffer is readable to B + 64 (16 B-aligned)
+    for (uint32_t i = tid; i < KD_STAGE / 16; i += KD_THREADS) {
+        const int64_t g = t0 - 16 + 16 * (int64_t)i;
+        ((uint4 *)s_in)[i] = (g >= 0 && g + 16 <= B + 64) ? *(const uint4 *)(in + g) : make_uint4(0, 0, 0, 0);
+    }
     __syncthreads();
-    const uint32_t tile = s_tile;
-    const int64_t p0 = (int64_t)tile * KD_TILE + (int64_t)tid * KD_BYTES;
-    // bytes [p0 - 16, p0 + 32): the 8 before p0 decide whether an early high byte is a 9th
-    uint4 q[3];
-    q[0] = p0 >= 16 ? *(const uint4 *)(in + p0 - 16) : make_uint4(0, 0, 0, 0);
-    q[1] = p0 < B ? *(const uint4 *)(in + p0) : make_uint4(0, 0, 0, 0);
-    q[2] = p0 + 16 < B ? *(const uint4 *)(in + p0 + 16) : make_uint4(0, 0, 0, 0);
-    uint64_t hi = 0;  // bit i: byte p0 - 16 + i has its top bit set (and exists)
+    const int64_t p0 = t0 + (int64_t)tid * KD_BYTES;
+    uint4 q5[5];
 #pragma unroll
-    for (int v = 0; v < 3; ++v) {
-        const uint32_t d[4] = {q[v].x, q[v].y, q[v].z, q[v].w};
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-#pragma unroll
-            for (int b = 0; b < 4; ++b) {
-                const int i = v * 16 + c * 4 + b;
-                const int64_t pos = p0 - 16 + i;
-                if (pos >= 0 && pos < B && ((d[c] >> (8 * b + 7)) & 1u)) hi |= 1ull << i;
-            }
-    }
-    uint32_t tok = 0;  // bit j: byte p0 + j ends a token
-#pragma unroll
-    for (int j = 0; j < KD_BYTES; ++j) {
-        const int i = 16 + j;
-        if (p0 + j >= B) break;
-        const bool h = (hi >> i) & 1ull;
-        const bool ninth = h && ((hi >> (i - 8)) & 0xFFull) == 0xFFull;
-        if (!h || ninth) tok |= 1u << j;
-    }
-    const uint32_t cnt = (uint32_t)__popc(tok);
-    uint32_t incl = cnt;
-#pragma unroll
-    for (int d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(incl, d, 64);
-        if (lane >= (uint32_t)d) incl += y;
-    }
+    for (int v = 0; v < 5; ++v) q5[v] = ((const uint4 *)s_in)[(KD_BYTES / 16) * tid + v];
+    const uint64_t tok = tok_mask64(q5, p0, B);
+    const uint32_t cnt = (uint32_t)__popcll(tok);
+    const uint32_t incl = ks_wave_scan(cnt, lane);
     if (lane == 63) s_wsum[w] = incl;
-    __syncthreads();
-    uint32_t texcl = incl - cnt, agg = 0;
-#pragma unroll
-    for (uint32_t qq = 0; qq < KD_THREADS / 64; ++qq) {
-        if (qq < w) texcl += s_wsum[qq];
-        agg += s_wsum[qq];
-    }
     if (w == 0) {
-        const uint64_t excl = wave_look_back(status, tile, agg, lane, &ticket_err[1]);
-        if (lane == 0) s_base = excl;
+        const uint64_t b0 = tile_base(status, btot, tile, lane);
+        if (lane == 0) s_base = b0;
     }
     __syncthreads();
-    uint64_t c = s_base + texcl;  // global index of this thread's first token end
+    uint32_t texcl = incl - cnt;
+#pragma unroll
+    for (uint32_t qq = 0; qq < KD_THREADS / 64; ++qq)
+        if (qq < w) texcl += s_wsum[qq];
+    const uint64_t c0 = s_base + texcl;  // global index of this thread's first token end
     bool bad = false;
     if (p0 == 0 && B > 0) {
         uint64_t kv[2];
-        if (!parse_pair(in, B, 0, kv) || out_cap < 1) bad = true;
+        if (!parse_pair_lds(s32, 16u, 0, B, kv) || out_cap < 1) bad = true;
         else out[0] = make_uint4((uint32_t)kv[0], (uint32_t)(kv[0] >> 32), (uint32_t)kv[1], (uint32_t)(kv[1] >> 32));
     }
-    for (uint32_t m = tok; m; m &= m - 1, ++c) {
-        const int j = __ffs(m) - 1;
-        if ((c & 3u) != 3u || p0 + j + 1 >= B) continue;
+    // record ends = token ends of global index 3 mod 4: skip to the first, then every 4th
+    // set bit (one iteration per record, so the lanes of a wave stay within one iteration)
+    uint64_t m = tok;
+    const uint32_t r0 = (3u - (uint32_t)(c0 & 3u)) & 3u;
+    for (uint32_t i = 0; i < r0; ++i) m &= m - 1;
+    for (uint64_t c = c0 + r0; m; c += 4) {
+        const int j = __ffsll((long long)m) - 1;
+        m &= m - 1;
+        m &= m - 1;
+        m &= m - 1;
+        m &= m - 1;
+        if (p0 + j + 1 >= B) continue;
         const int64_t k = (int64_t)(c >> 2) + 1;
         uint64_t kv[2];
-        if (k >= out_cap || !parse_pair(in, B, p0 + j + 1, kv)) { bad = true; continue; }
+        const uint32_t q = 16u + tid * KD_BYTES + (uint32_t)j + 1u;  // <= 16 + KD_TILE: window fits
+        if (k >= out_cap || !parse_pair_lds(s32, q, p0 + j + 1, B, kv)) { bad = true; continue; }
         out[k] = make_uint4((uint32_t)kv[0], (uint32_t)(kv[0] >> 32), (uint32_t)kv[1], (uint32_t)(kv[1] >> 32));
     }
     if (p0 <= B - 1 && B - 1 < p0 + KD_BYTES) {  // the thread holding the last byte: totals
-        if (c & 3u) bad = true;
-        *count_out = (int64_t)(c >> 2);
+        const uint64_t cend = c0 + cnt;
+        if (cend & 3u) bad = true;
+        *count_out = (int64_t)(cend >> 2);
     }
     if (bad) atomicOr(&ticket_err[1], 2u);
 }
@@ -358,23 +473,52 @@ __global__ __launch_bounds__(KD_THREADS) void k_kryo_deser16(const uint8_t *__re
 
 int64_t kryo_deser16_tiles(int64_t bytes) { return (bytes + KD_TILE - 1) / KD_TILE; }
 
+int64_t kryo_work_bytes(int64_t tiles) {
+    return (tiles + (tiles + TS_BLOCK - 1) / TS_BLOCK + 1) * 8 + tiles * 4;
+}
+
+// workspace: excl[tiles] u64 | btot[nblk] u64 | agg[tiles] u32
+static void work_split(uint64_t *ws, int64_t tiles, uint64_t **excl, uint64_t **btot, uint32_t **agg,
+                       int64_t *nblk) {
+    *nblk = (tiles + TS_BLOCK - 1) / TS_BLOCK;
+    *excl = ws;
+    *btot = ws + tiles;
+    *agg = (uint32_t *)(ws + tiles + *nblk + 1);
+}
+
 hipError_t launch_kryo_deser16(const void *in, int64_t bytes, void *out, int64_t out_cap, uint64_t *status,
                                uint32_t *ticket_err, int64_t *count_out, hipStream_t st) {
     if (bytes <= 0) return hipSuccess;
     const int64_t tiles = kryo_deser16_tiles(bytes);
+    uint64_t *excl, *btot;
+    uint32_t *agg;
+    int64_t nblk;
+    work_split(status, tiles, &excl, &btot, &agg, &nblk);
+    hipLaunchKernelGGL(k_kryo_tok, dim3((unsigned)tiles), dim3(KD_THREADS), 0, st, (const uint8_t *)in, bytes, agg);
+    hipLaunchKernelGGL(k_tile_scan64, dim3((unsigned)nblk), dim3(TS_THREADS), 0, st, (const uint32_t *)agg, tiles,
+                       excl, btot);
     hipLaunchKernelGGL(k_kryo_deser16, dim3((unsigned)tiles), dim3(KD_THREADS), 0, st, (const uint8_t *)in, bytes,
-                       (uint4 *)out, out_cap, status, ticket_err, count_out);
+                       (uint4 *)out, out_cap, (const uint64_t *)excl, (const uint64_t *)btot, ticket_err, count_out);
     return hipGetLastError();
 }
 
 int64_t kryo_ser16_tiles(int64_t n) { return (n + KS_TILE - 1) / KS_TILE; }
 
 hipError_t launch_kryo_ser16(const void *in, int64_t n, void *out, const uint32_t *rec_off, int R, int64_t *ser_off,
-                             uint64_t *status, uint32_t *ticket_err, hipStream_t st) {
+                             uint64_t *status, uint32_t *ticket_err, int num_cus, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const int64_t tiles = kryo_ser16_tiles(n);
+    (void)num_cus;
+    uint64_t *excl, *btot;
+    uint32_t *agg;
+    int64_t nblk;
+    work_split(status, tiles, &excl, &btot, &agg, &nblk);
+    hipLaunchKernelGGL(k_kryo_len16, dim3((unsigned)tiles), dim3(KS_THREADS), 0, st, (const uint4 *)in, n, agg);
+    hipLaunchKernelGGL(k_tile_scan64, dim3((unsigned)nblk), dim3(TS_THREADS), 0, st, (const uint32_t *)agg, tiles,
+                       excl, btot);
     hipLaunchKernelGGL(k_kryo_ser16, dim3((unsigned)tiles), dim3(KS_THREADS), 0, st, (const uint4 *)in, n,
-                       (uint8_t *)out, rec_off, R, ser_off, status, ticket_err);
+                       (uint8_t *)out, rec_off, R, ser_off, (const uint64_t *)excl, (const uint64_t *)btot,
+                       ticket_err);
     return hipGetLastError();
 }
 

@@ -223,3 +223,23 @@ def test_gpu_set_serializer_state_rules(engine):
             engine.set_serializer(sid, sgx.SER_KRYO)
     finally:
         engine.unregister_shuffle(sid)
+
+
+@pytest.mark.gpu
+def test_gpu_kryo_multi_block_scan_round_trip(engine, oracle_lib):
+    """> 4096 tiles on both sides (two-level tile scan): 5M records framed and decoded."""
+    import sparkucx_amd as sgx
+
+    n, R = 5_000_000, 1024
+    recs = oracle_lib.gen_uniform16(n, 1234)
+    out, counts = oracle_lib.map_write(recs, R, nthreads=8)
+    off = oracle_lib.kryo_partition_offsets(out, counts)
+    sid, lengths = _kryo_map(engine, recs, R, device=True)
+    try:
+        assert np.array_equal(lengths, np.diff(off))
+        assert np.array_equal(engine.map_output_bytes(sid, 0), oracle_lib.kryo_serialize(out))
+        got = engine.read_records(sid, [0], 0, R).reshape(-1, 16)
+        assert np.array_equal(got, out)
+    finally:
+        engine.unregister_shuffle(sid)
+        _ = sgx
