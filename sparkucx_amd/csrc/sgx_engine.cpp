@@ -199,7 +199,7 @@ struct sgx_engine {
     // map-side work buffers, a ring of two: with SGX_PIPELINE the next map's histogram +
     // scan (on s_hist) fill one set while the previous map's scatter (on s_comp) reads the other
     struct WorkSet {
-        DevBuf counts, offs, status, part_off_dev;
+        DevBuf offs, status;  // status: counts | ticket | look-back status | partition offsets | error
         hipEvent_t used = nullptr;  // recorded on s_comp after the scatter that read this set
     } ws[2];
     int ws_next = 0;
@@ -249,6 +249,9 @@ struct sgx_engine {
             ev_free.push_back(p.b);
         }
         pending.clear();
+        // consecutive stages may share their boundary event: return each event once
+        std::sort(ev_free.begin(), ev_free.end());
+        ev_free.erase(std::unique(ev_free.begin(), ev_free.end()), ev_free.end());
     }
 };
 
@@ -343,7 +346,7 @@ extern "C" void sgx_destroy(sgx_engine *e) {
         kv.second.bounds.release();
     }
     for (auto &w : e->ws) {
-        for (DevBuf *b : {&w.counts, &w.offs, &w.status, &w.part_off_dev}) b->release();
+        for (DevBuf *b : {&w.offs, &w.status}) b->release();
         if (w.used) (void)hipEventDestroy(w.used);
         w.used = nullptr;
     }
@@ -553,30 +556,39 @@ static int partition_pass(sgx_engine *e, const void *in, void *out, int64_t n, i
     auto &W = e->ws[pipe ? (e->ws_next ^= 1) : 0];
     hipStream_t sh = pipe ? e->s_hist : st;
     if (pipe && W.used) HIP_TRY(hipStreamWaitEvent(sh, W.used, 0));  // its last reader (K4) is done
-    SGX_TRY(W.counts.ensure((size_t)len * 4));
     SGX_TRY(W.offs.ensure((size_t)len * 4));
-    SGX_TRY(W.status.ensure((size_t)(16 + tiles * 8)));
-    SGX_TRY(W.part_off_dev.ensure((size_t)(R + 2) * 4));
-    e->last_off_dev = (const uint32_t *)W.part_off_dev.p;
-    uint32_t *ticket_err = (uint32_t *)W.status.p;
-    uint64_t *status = (uint64_t *)((char *)W.status.p + 16);
-    HIP_TRY(hipMemsetAsync(W.status.p, 0, (size_t)(16 + tiles * 8), sh));
+    // one work block, zeroed by ONE memset (each fill / copy between kernels costs ~5-10 µs):
+    // [counts u32 x R*G][ticket u32 | pad][look-back status u64 x tiles]
+    // [partition offsets u32 x (R+1) | error] -- the error word sits right after the
+    // offsets so one copy lands both on the host
+    const size_t counts_bytes = ((size_t)len * 4 + 15) & ~(size_t)15;
+    const size_t status_bytes = ((size_t)(16 + tiles * 8) + 15) & ~(size_t)15;
+    const size_t work_bytes = counts_bytes + status_bytes + (((size_t)(R + 2) * 4 + 15) & ~(size_t)15);
+    SGX_TRY(W.status.ensure(work_bytes));
+    uint32_t *counts = (uint32_t *)W.status.p;
+    uint32_t *ticket = (uint32_t *)((char *)W.status.p + counts_bytes);
+    uint64_t *status = (uint64_t *)((char *)ticket + 16);
+    uint32_t *part_off_dev = (uint32_t *)((char *)ticket + status_bytes);
+    uint32_t *err = part_off_dev + R + 1;
+    e->last_off_dev = part_off_dev;
+    HIP_TRY(hipMemsetAsync(W.status.p, 0, work_bytes, sh));
 
-    // one event pair per stage: an event is owned by exactly one pending record
-    hipEvent_t h0 = e->ev(), h1 = e->ev(), c0 = e->ev(), c1 = e->ev(), x0 = e->ev(), x1 = e->ev();
+    // stage events: consecutive stages on one stream share their boundary event (every
+    // timing marker between two kernels measured ~5 µs of idle GPU); the pipelined mode's
+    // stages sit on two streams and keep their own pairs
+    hipEvent_t h0 = e->ev(), h1 = e->ev(), c0 = pipe ? e->ev() : h1, c1 = e->ev(), x0 = pipe ? e->ev() : c1,
+               x1 = e->ev();
     HIP_TRY(hipEventRecord(h0, sh));
     if (n > 0) {
-        HIP_TRY(launch_hist(in, n, rb, chunk, G, spp, (uint32_t *)W.counts.p, sh, pipe ? 1 : e->hist_variant));
-    } else {
-        HIP_TRY(hipMemsetAsync(W.counts.p, 0, (size_t)len * 4, sh));
+        HIP_TRY(launch_hist(in, n, rb, chunk, G, spp, counts, sh, pipe ? 1 : e->hist_variant, true));
     }
     HIP_TRY(hipEventRecord(h1, sh));
-    HIP_TRY(hipEventRecord(c0, sh));
-    HIP_TRY(launch_scan((const uint32_t *)W.counts.p, (uint32_t *)W.offs.p, len, status, ticket_err,
-                        (uint32_t *)W.part_off_dev.p, G, R, sh));
+    if (c0 != h1) HIP_TRY(hipEventRecord(c0, sh));
+    HIP_TRY(launch_scan((const uint32_t *)counts, (uint32_t *)W.offs.p, len, status, ticket, err,
+                        part_off_dev, G, R, sh));
     HIP_TRY(hipEventRecord(c1, sh));
     if (pipe) HIP_TRY(hipStreamWaitEvent(st, c1, 0));
-    HIP_TRY(hipEventRecord(x0, st));
+    if (x0 != c1) HIP_TRY(hipEventRecord(x0, st));
     PartParams lpp = spp;
     SGX_TRY(e->junk.ensure((size_t)G * JUNK_BYTES_PER_WG));
     lpp.junk = e->junk.p;
@@ -598,21 +610,19 @@ static int partition_pass(sgx_engine *e, const void *in, void *out, int64_t n, i
         int occ = (int)((160 * 1024) / scatter16_chain_lds((uint32_t)R, cw, ci, mb));
         if (occ > 32 / cw) occ = 32 / cw;
         if (occ < 1) occ = 1;
-        HIP_TRY(launch_scatter_chain(in, out, n, cpp, (const uint32_t *)W.part_off_dev.p,
+        HIP_TRY(launch_scatter_chain(in, out, n, cpp, (const uint32_t *)part_off_dev,
                                      (uint32_t *)((char *)e->chain_buf.p + 16), (uint32_t *)e->chain_buf.p,
-                                     ticket_err + 1, cw, ci, e->num_cus * occ, st));
+                                     err, cw, ci, e->num_cus * occ, st));
     } else if (n > 0) {
         if (e->diag > 0 && rb == 16 && kind == SGX_PART_HASH)  // measurement-only ablation
-            HIP_TRY(launch_scatter_diag(e->diag, in, out, n, chunk, G, lpp, (const uint32_t *)W.offs.p, ticket_err + 1, st));
+            HIP_TRY(launch_scatter_diag(e->diag, in, out, n, chunk, G, lpp, (const uint32_t *)W.offs.p, err, st));
         else
-            HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, lpp, (const uint32_t *)W.offs.p, geo, ticket_err + 1, st));
+            HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, lpp, (const uint32_t *)W.offs.p, geo, err, st));
     }
     HIP_TRY(hipEventRecord(x1, st));
-    // (R+1) offsets then the look-back give-up flag
-    HIP_TRY(hipMemcpyAsync((char *)W.part_off_dev.p + (size_t)(R + 1) * 4, ticket_err + 1, 4,
-                           hipMemcpyDeviceToDevice, st));
-    if (host_off) HIP_TRY(hipMemcpyAsync(host_off, W.part_off_dev.p, (size_t)(R + 2) * 4, hipMemcpyDeviceToHost, st));
-    if (err_slot) HIP_TRY(hipMemcpyAsync(err_slot, ticket_err + 1, 4, hipMemcpyDeviceToDevice, st));
+    // (R+1) offsets then the error word, one copy
+    if (host_off) HIP_TRY(hipMemcpyAsync(host_off, part_off_dev, (size_t)(R + 2) * 4, hipMemcpyDeviceToHost, st));
+    if (err_slot) HIP_TRY(hipMemcpyAsync(err_slot, err, 4, hipMemcpyDeviceToDevice, st));
     if (pipe) {
         if (!W.used) HIP_TRY(hipEventCreateWithFlags(&W.used, hipEventDisableTiming));
         HIP_TRY(hipEventRecord(W.used, st));
@@ -622,7 +632,8 @@ static int partition_pass(sgx_engine *e, const void *in, void *out, int64_t n, i
         record_stage(e, SGX_STAGE_SCAN, c0, c1);
         record_stage(e, SGX_STAGE_SCATTER, x0, x1);
     } else {
-        for (hipEvent_t v : {h0, h1, c0, c1, x0, x1}) e->ev_free.push_back(v);
+        for (hipEvent_t v : {h0, h1, c1, x1}) e->ev_free.push_back(v);
+        if (pipe) for (hipEvent_t v : {c0, x0}) e->ev_free.push_back(v);
     }
     return SGX_OK;
 }
@@ -1474,7 +1485,8 @@ extern "C" int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t
         HIP_TRY(hipMemsetAsync(e->grp_status.p, 0, (size_t)(16 + tiles * 8 + 16), st));
         HIP_TRY(launch_group_flags(sorted, n, (uint32_t *)e->grp_flags.p, st));
         HIP_TRY(launch_scan((const uint32_t *)e->grp_flags.p, (uint32_t *)e->grp_offs.p, n,
-                            (uint64_t *)((char *)e->grp_status.p + 16), ticket_err, gcount, (int)n, 1, st));
+                            (uint64_t *)((char *)e->grp_status.p + 16), ticket_err, ticket_err + 1, gcount, (int)n,
+                            1, st));
         uint32_t h[2] = {0, 0}, terr[2] = {0, 0};
         HIP_TRY(hipMemcpyAsync(h, gcount, 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(terr, ticket_err, 8, hipMemcpyDeviceToHost, st));

@@ -81,10 +81,13 @@ constexpr int WIDE2_GEOM_TAG = -2;
 ScatterGeom scatter_geom_wide2(uint32_t R, int record_bytes, int kind, int nb);
 
 // Launchers (all asynchronous on `stream`).  counts / offs are [R][G] partition-major.
+// counts: [R][G] u32, zeroed here unless `zeroed` (the caller's memset covered them)
 hipError_t launch_hist(const void *in, int64_t n, int record_bytes, int64_t chunk, int G,
-                       const PartParams &pp, uint32_t *counts, hipStream_t stream, int mode = 0);
+                       const PartParams &pp, uint32_t *counts, hipStream_t stream, int mode = 0,
+                       bool zeroed = false);
+// ticket: zeroed dispatch-order counter; err: sticky error word (bit 0: look-back gave up)
 hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint64_t *status,
-                       uint32_t *ticket_err, uint32_t *part_off, int G, int R,
+                       uint32_t *ticket, uint32_t *err, uint32_t *part_off, int G, int R,
                        hipStream_t stream);
 int64_t scan_tiles(int64_t len);
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes, int64_t chunk,

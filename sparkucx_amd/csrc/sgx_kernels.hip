@@ -264,11 +264,13 @@ __global__ __launch_bounds__(HIST_LEAN_THREADS) __attribute__((amdgpu_num_vgpr(3
 }
 
 hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
-                       const PartParams &pp, uint32_t *counts, hipStream_t stream, int mode) {
+                       const PartParams &pp, uint32_t *counts, hipStream_t stream, int mode, bool zeroed) {
     const size_t lds = (size_t)pp.R * 4;
     const char *p = (const char *)in;
-    hipError_t ze = hipMemsetAsync(counts, 0, (size_t)pp.R * G * 4, stream);
-    if (ze != hipSuccess) return ze;
+    if (!zeroed) {
+        hipError_t ze = hipMemsetAsync(counts, 0, (size_t)pp.R * G * 4, stream);
+        if (ze != hipSuccess) return ze;
+    }
     const bool r16 = (rb == 16);
     const bool lean = mode == 1;
     if (mode >= 2 && r16 && pp.kind == SGX_PART_HASH) {
@@ -331,13 +333,13 @@ int64_t scan_tiles(int64_t len) { return (len + SCAN_TILE - 1) / SCAN_TILE; }
 
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const uint32_t *__restrict__ in,
                                                        uint32_t *__restrict__ out, int64_t len,
-                                                       uint64_t *status, uint32_t *ticket_err,
+                                                       uint64_t *status, uint32_t *ticket, uint32_t *err,
                                                        uint32_t *__restrict__ part_off, int G,
                                                        int R) {
     __shared__ uint32_t s_tile, s_prefix_lo;
     __shared__ uint32_t s_wsum[SCAN_THREADS / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    if (tid == 0) s_tile = atomicAdd(&ticket_err[0], 1u);
+    if (tid == 0) s_tile = atomicAdd(ticket, 1u);
     __syncthreads();
     const uint32_t tile = s_tile;
     const int64_t base = (int64_t)tile * SCAN_TILE + (int64_t)tid * SCAN_ITEMS;
@@ -370,7 +372,7 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const uint32_t *__restric
                 const uint64_t s = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
                 const uint64_t flag = s & ~ST_VAL;
                 if (flag == 0) {
-                    if (++spins > (1u << 26)) { atomicOr(&ticket_err[1], 1u); break; }
+                    if (++spins > (1u << 26)) { atomicOr(err, 1u); break; }
                     __builtin_amdgcn_s_sleep(1);
                     continue;
                 }
@@ -397,10 +399,10 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const uint32_t *__restric
 }
 
 hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint64_t *status,
-                       uint32_t *ticket_err, uint32_t *part_off, int G, int R, hipStream_t stream) {
+                       uint32_t *ticket, uint32_t *err, uint32_t *part_off, int G, int R, hipStream_t stream) {
     const int64_t tiles = scan_tiles(len);
     hipLaunchKernelGGL(k_scan, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, stream, counts, offs,
-                       len, status, ticket_err, part_off, G, R);
+                       len, status, ticket, err, part_off, G, R);
     return hipGetLastError();
 }
 
