@@ -243,3 +243,26 @@ def test_gpu_kryo_multi_block_scan_round_trip(engine, oracle_lib):
     finally:
         engine.unregister_shuffle(sid)
         _ = sgx
+
+
+@pytest.mark.gpu
+def test_gpu_kryo_exchange_single_rank(engine, oracle_lib):
+    """sgx_exchange on a Kryo shuffle (one rank, no communicator: the received blocks alias
+    the map's Kryo stream); fetched blocks and decoded records come from the round."""
+    import sparkucx_amd as sgx
+
+    R = 32
+    recs = _edge_records(20_000, 77)
+    out, counts = oracle_lib.map_write(recs, R)
+    o = oracle_lib.offsets(counts)
+    sid, lengths = _kryo_map(engine, recs, R, map_id=4)
+    try:
+        engine.exchange(sid, 4)
+        engine.sync()
+        data, lens = engine.fetch_blocks(sid, [4, 4], [31, 0])
+        want = np.concatenate([oracle_lib.kryo_serialize(out[o[31]:o[32]]), oracle_lib.kryo_serialize(out[o[0]:o[1]])])
+        assert np.array_equal(data, want)
+        assert np.array_equal(engine.read_records(sid, [4], 0, R).reshape(-1, 16), out)
+    finally:
+        engine.unregister_shuffle(sid)
+        _ = sgx
