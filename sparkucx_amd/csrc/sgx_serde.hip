@@ -111,6 +111,23 @@ __global__ __launch_bounds__(TS_THREADS) void k_tile_scan64(const uint32_t *__re
     if (tid == 0) btot[blockIdx.x] = tot;
 }
 
+// first index p in [0, n) with a[p] >= x (n if none) of a nondecreasing array, by one
+// whole wave: 64 probes per round trip instead of log2(n) dependent loads per thread
+__device__ __forceinline__ int wave_lower_bound(const uint32_t *a, int n, int64_t x, uint32_t lane) {
+    int lo = 0, hi = n;  // the answer is in [lo, hi]
+    while (hi - lo > 64) {
+        const int step = (hi - lo + 63) / 64;
+        const int idx = lo + (int)lane * step;
+        const uint64_t m = __ballot(idx < hi && (int64_t)a[idx] < x);  // a prefix of the probes
+        const int c = __popcll(m);
+        const int nlo = c ? lo + (c - 1) * step + 1 : lo;
+        hi = min(hi, lo + c * step);
+        lo = nlo;
+    }
+    const int idx = lo + (int)lane;
+    return lo + __popcll(__ballot(idx < hi && (int64_t)a[idx] < x));
+}
+
 // prefix of `tile` (call from a whole wave; every lane gets it)
 __device__ __forceinline__ uint64_t tile_base(const uint64_t *excl, const uint64_t *btot, uint32_t tile,
                                               uint32_t lane) {
@@ -159,6 +176,7 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(const uint4 *__restri
     __shared__ __attribute__((aligned(16))) uint8_t s_out[KS_TILE * KS_MAXREC + 16];
     __shared__ uint32_t s_wsum[KS_THREADS / 64];
     __shared__ uint64_t s_base;
+    __shared__ int s_p0;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t tile = blockIdx.x;
     (void)ticket_err;
@@ -198,10 +216,15 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(const uint4 *__restri
 #pragma unroll
         for (int j = 0; j < KS_ITEMS; ++j) { s_off[tid * KS_ITEMS + j] = run; run += lv[j]; }
     }
-    // the tile's byte prefix from the reduce-then-scan pre-pass
+    // the tile's byte prefix from the reduce-then-scan pre-pass; the first partition that
+    // starts in this tile
     if (w == 0) {
         const uint64_t b0 = tile_base(status, btot, tile, lane);
-        if (lane == 0) s_base = b0;
+        const int p0 = wave_lower_bound(rec_off, R + 1, t0, lane);
+        if (lane == 0) {
+            s_base = b0;
+            s_p0 = p0;
+        }
     }
     __syncthreads();
     const uint64_t B = s_base;
@@ -255,12 +278,7 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(const uint4 *__restri
     // writes those that start at n: the total)
     const int64_t t1 = t0 + tn;
     const bool last = t1 >= n;
-    int lo = 0, hi = R + 1;  // first p with rec_off[p] >= t0
-    while (lo < hi) {
-        const int mid = (lo + hi) >> 1;
-        if ((int64_t)rec_off[mid] < t0) lo = mid + 1; else hi = mid;
-    }
-    for (int p = lo + (int)tid; p <= R; p += KS_THREADS) {
+    for (int p = s_p0 + (int)tid; p <= R; p += KS_THREADS) {
         const int64_t ro = (int64_t)rec_off[p];
         if (ro < t1) ser_off[p] = (int64_t)(B + s_off[ro - t0]);
         else if (last && ro == n) ser_off[p] = (int64_t)(B + agg);
