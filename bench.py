@@ -206,6 +206,11 @@ def main():
             "stages_ms_per_step": {k: round(v / max(1, st.count[k]), 4) for k, v in st.ms.items() if st.count[k]},
             "map_side_GBs_hist_scan_scatter": round(16.0 * n / ((st.ms["hist"] + st.ms["scan"] + st.ms["scatter"])
                                                              / max(1, st.count["scatter"]) * 1e-3) / 1e9, 1),
+            # the two-pass map side must move 48 B per AoS record (hist reads the 16 B record
+            # for its 8 B key; K4 reads 16 + writes 16): its HBM stream rate against 8 TB/s
+            "map_side_hbm": (lambda t: {"bytes_per_record": 48, "achieved": round(48.0 * n / t / 1e9, 1),
+                                        "frac": round(48.0 * n / t / 1e9 / HBM_PEAK_GBS, 4)})(
+                (st.ms["hist"] + st.ms["scan"] + st.ms["scatter"]) / max(1, st.count["scatter"]) * 1e-3),
             "verified_lengths_sum": verified,
         }
         if xgmi is not None:
