@@ -141,7 +141,7 @@ struct MapOut {
     // serializer KRYO (sgx_set_serializer): the map's published bytes are the Kryo stream of
     // its records (data file, fetch, exchange); `data` keeps the 16 B records
     DevBuf ser;                // Kryo-framed partition-contiguous bytes (capacity 20 n + 16)
-    DevBuf ser_work;           // ser_off_dev (R+1) i64 | error u32 x 4 | tile prefixes u64, tile sums u32
+    DevBuf ser_work;           // ser_off_dev (R+1) i64 | tile prefixes, block totals u64 | tile sums u32
     HostPinned ser_off;        // (R+1) i64 byte offsets + the error word, landed async
     int64_t out_bytes = 0;     // published bytes (n * rb, or the Kryo total once `ready`)
     const void *view() const { return ser.p ? ser.p : data.p; }
@@ -460,8 +460,6 @@ static int finish_lengths(Shuffle &s, MapOut &m) {
     m.lengths.assign((size_t)s.R, 0);
     if (s.ser == SGX_SER_KRYO) {
         const int64_t *so = (const int64_t *)m.ser_off.p;
-        const uint32_t serr = (uint32_t)so[s.R + 1];
-        if (serr & 1u) return fail(SGX_ERR_TIMEOUT, "serializer look-back spin gave up (device flag %u)", serr);
         int64_t prev = 0;
         for (int32_t p = 0; p < s.R; ++p) {
             m.lengths[(size_t)p] = so[p + 1] - so[p];
@@ -646,20 +644,17 @@ static int serialize_kryo(sgx_engine *e, Shuffle &s, MapOut &m) {
     const int64_t tiles = kryo_ser16_tiles(n);
     const size_t offb = (size_t)(s.R + 1) * 8;
     SGX_TRY(m.ser.ensure((size_t)(20 * n + 16)));
-    SGX_TRY(m.ser_work.ensure(offb + 16 + (size_t)kryo_work_bytes(tiles)));
-    SGX_TRY(m.ser_off.ensure(offb + 8));
+    SGX_TRY(m.ser_work.ensure(offb + (size_t)kryo_work_bytes(tiles)));
+    SGX_TRY(m.ser_off.ensure(offb));
     int64_t *off_dev = (int64_t *)m.ser_work.p;
-    uint32_t *tick = (uint32_t *)((char *)m.ser_work.p + offb);
-    uint64_t *status = (uint64_t *)((char *)m.ser_work.p + offb + 16);
-    HIP_TRY(hipMemsetAsync(m.ser_work.p, 0, offb + 16, st));  // partition offsets, error word
+    uint64_t *work = (uint64_t *)((char *)m.ser_work.p + offb);
+    if (n == 0) HIP_TRY(hipMemsetAsync(off_dev, 0, offb, st));  // no tile writes them
     hipEvent_t k0 = e->ev(), k1 = e->ev();
     HIP_TRY(hipEventRecord(k0, st));
-    HIP_TRY(launch_kryo_ser16(m.data.p, n, m.ser.p, e->last_off_dev, s.R, off_dev, status, tick, e->num_cus, st));
+    HIP_TRY(launch_kryo_ser16(m.data.p, n, m.ser.p, e->last_off_dev, s.R, off_dev, work, st));
     HIP_TRY(hipEventRecord(k1, st));
     record_stage(e, SGX_STAGE_SERIALIZE, k0, k1);
-    // (R+1) offsets, then the error word in the low half of slot R+1
-    HIP_TRY(hipMemcpyAsync(m.ser_off.p, off_dev, offb, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipMemcpyAsync((char *)m.ser_off.p + offb, tick + 1, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipMemcpyAsync(m.ser_off.p, off_dev, offb, hipMemcpyDeviceToHost, st));  // (R+1) byte offsets
     return SGX_OK;
 }
 

@@ -170,7 +170,7 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(const uint4 *__restri
                                                            uint8_t *__restrict__ out,
                                                            const uint32_t *__restrict__ rec_off, int R,
                                                            int64_t *__restrict__ ser_off, const uint64_t *status,
-                                                           const uint64_t *btot, uint32_t *ticket_err) {
+                                                           const uint64_t *btot) {
     __shared__ __attribute__((aligned(16))) uint8_t s_len[KS_TILE];
     __shared__ __attribute__((aligned(16))) uint32_t s_off[KS_TILE];
     __shared__ __attribute__((aligned(16))) uint8_t s_out[KS_TILE * KS_MAXREC + 16];
@@ -179,7 +179,6 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(const uint4 *__restri
     __shared__ int s_p0;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t tile = blockIdx.x;
-    (void)ticket_err;
     const int64_t t0 = (int64_t)tile * KS_TILE;
     const int64_t tn = min((int64_t)KS_TILE, n - t0);
 
@@ -523,20 +522,18 @@ hipError_t launch_kryo_deser16(const void *in, int64_t bytes, void *out, int64_t
 int64_t kryo_ser16_tiles(int64_t n) { return (n + KS_TILE - 1) / KS_TILE; }
 
 hipError_t launch_kryo_ser16(const void *in, int64_t n, void *out, const uint32_t *rec_off, int R, int64_t *ser_off,
-                             uint64_t *status, uint32_t *ticket_err, int num_cus, hipStream_t st) {
+                             uint64_t *work, hipStream_t st) {
     if (n <= 0) return hipSuccess;
     const int64_t tiles = kryo_ser16_tiles(n);
-    (void)num_cus;
     uint64_t *excl, *btot;
     uint32_t *agg;
     int64_t nblk;
-    work_split(status, tiles, &excl, &btot, &agg, &nblk);
+    work_split(work, tiles, &excl, &btot, &agg, &nblk);
     hipLaunchKernelGGL(k_kryo_len16, dim3((unsigned)tiles), dim3(KS_THREADS), 0, st, (const uint4 *)in, n, agg);
     hipLaunchKernelGGL(k_tile_scan64, dim3((unsigned)nblk), dim3(TS_THREADS), 0, st, (const uint32_t *)agg, tiles,
                        excl, btot);
     hipLaunchKernelGGL(k_kryo_ser16, dim3((unsigned)tiles), dim3(KS_THREADS), 0, st, (const uint4 *)in, n,
-                       (uint8_t *)out, rec_off, R, ser_off, (const uint64_t *)excl, (const uint64_t *)btot,
-                       ticket_err);
+                       (uint8_t *)out, rec_off, R, ser_off, (const uint64_t *)excl, (const uint64_t *)btot);
     return hipGetLastError();
 }
 
