@@ -149,7 +149,7 @@ def test_every_staged_geometry(sgx_lib, oracle_lib, monkeypatch, waves, items, R
 @pytest.mark.parametrize("env", ["SGX_SCATTER_DMA=1", "SGX_SCATTER_DIRECT=816", "SGX_SCATTER_DIRECT=408",
                                  "SGX_SCATTER_CHAIN=816", "SGX_SCATTER_CHAIN=1607", "SGX_NO_PEER_TABLE=1",
                                  "SGX_SCATTER_NT=1", "SGX_SCATTER_NT=4", "SGX_RANK=match", "SGX_SCATTER_WC=0",
-                                 "SGX_PIPELINE=1"])
+                                 "SGX_PIPELINE=1", "SGX_HIST_VARIANT=7"])
 def test_alternative_scatter_variants(sgx_lib, oracle_lib, monkeypatch, env):
     """The A/B variants kept for measurement must stay bit-exact too (engine reads the env
     at creation)."""
