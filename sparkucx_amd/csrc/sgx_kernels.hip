@@ -1960,7 +1960,7 @@ __host__ __device__ size_t scatter_wide2_lds(uint32_t R, int rb, int kind, int n
            (size_t)8 * rs8(R) * 2 + (size_t)rs8(R) * 8 + (size_t)WIDE2_TR * 4 + 64 * 4;
 }
 
-template <int KIND, int RB>
+template <int KIND, int RB, bool NT = false>
 __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restrict__ in, uint32_t *__restrict__ out,
                                                           int64_t n, int64_t chunk, PartParams pp,
                                                           const uint32_t *__restrict__ offs, int G,
@@ -2115,7 +2115,10 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q)
-                if (live[q] && dst[q] < (uint32_t)n) out[(uint64_t)dst[q] * DW + wi[q]] = v[q];
+                if (live[q] && dst[q] < (uint32_t)n) {
+                    if constexpr (NT) __builtin_nontemporal_store(v[q], out + (uint64_t)dst[q] * DW + wi[q]);
+                    else out[(uint64_t)dst[q] * DW + wi[q]] = v[q];
+                }
         }
         __syncthreads();  // stage / idx reused by the next tile
     }
@@ -2287,12 +2290,18 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
 #undef SGX_SC16
     } else if (rb == 100 && geo.waves == WIDE2_GEOM_TAG) {
         if (((uintptr_t)in & 15) != 0) return hipErrorInvalidValue;
+        // SGX_WIDE2_NT=1 (A/B): nontemporal dword stores in the drain
+        static const bool w2nt = getenv("SGX_WIDE2_NT") && atoi(getenv("SGX_WIDE2_NT")) != 0;
+#define SGX_W2NT(K, NTV)                                                                         \
+    do {                                                                                         \
+        (void)hipFuncSetAttribute((const void *)k_scatter_wide2<K, 100, NTV>,                   \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
+        hipLaunchKernelGGL((k_scatter_wide2<K, 100, NTV>), dim3(G), dim3(512), geo.lds_bytes, stream, \
+                           (const u32x4 *)in, (uint32_t *)out, n, chunk, pp, offs, G, err);     \
+    } while (0)
 #define SGX_W2(K)                                                                                \
     do {                                                                                         \
-        (void)hipFuncSetAttribute((const void *)k_scatter_wide2<K, 100>,                        \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
-        hipLaunchKernelGGL((k_scatter_wide2<K, 100>), dim3(G), dim3(512), geo.lds_bytes, stream,  \
-                           (const u32x4 *)in, (uint32_t *)out, n, chunk, pp, offs, G, err);     \
+        if (w2nt) SGX_W2NT(K, true); else SGX_W2NT(K, false);                                    \
     } while (0)
         switch (pp.kind) {
         case SGX_PART_HASH:
@@ -2303,6 +2312,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         default: SGX_W2(SGX_PART_RANGE_BYTES10); break;
         }
 #undef SGX_W2
+#undef SGX_W2NT
     } else {
         if (geo.items == 0 || (rb & 3) != 0 || rb < 12) return hipErrorInvalidValue;
         const char *ic = (const char *)in;
