@@ -84,6 +84,23 @@ int sgx_register_shuffle(sgx_engine *e, int32_t shuffle_id, int32_t num_partitio
  * fetched Kryo stream back to records on the GPU before sorting / grouping. */
 enum sgx_serializer { SGX_SER_FIXED = 0, SGX_SER_KRYO = 1 };
 int sgx_set_serializer(sgx_engine *e, int32_t shuffle_id, int32_t serializer);
+/* spark.shuffle.compress=true, spark.io.compression.codec=lz4 (Spark 3.0.1 defaults): every
+ * partition stream is wrapped on its own (ShufflePartitionPairsWriter.open ->
+ * SerializerManager.wrapStream, invoked by the writers built at
+ * spark_3_0/UcxShuffleManager.scala:37-51, bytes landing in NvkvShuffleMapOutputWriter's
+ * PartitionWriterStream, ucx/NvkvShuffleMapOutputWriter.scala:228-246) in lz4-java's
+ * LZ4BlockOutputStream(block_size, fast compressor, XXH32 seed 0x9747b28c).  Frames the
+ * partition streams [part_offsets[r], part_offsets[r+1]) of stream_dev (device bytes, e.g. the
+ * Kryo stream of sgx_map_data) on the GPU, byte-identical to lz4-java 1.7.1 / liblz4 1.9.x:
+ * 32 KiB blocks by default, LZ4 or RAW per block, the 21-byte end mark per non-empty partition.
+ * part_offsets: host int64[R+1]; out_lengths: caller-owned int64[R] (framed bytes per
+ * partition; 0 for an empty partition, whose stream Spark never opens).  dst_dev NULL only
+ * measures; otherwise the frames are written back to back into dst_dev (dst_cap bytes,
+ * SGX_ERR_INVALID if too small, out_lengths still filled).  block_size in [64, 32768].
+ * Synchronous. */
+int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, const int64_t *part_offsets,
+                             int32_t num_partitions, int32_t block_size, void *dst_dev, int64_t dst_cap,
+                             int64_t *out_lengths);
 /* unregisterShuffle: CommonUcxShuffleManager.scala:103-106 -> removeShuffle
  * (CommonUcxShuffleBlockResolver.scala:63-71). Frees the shuffle's HBM. */
 int sgx_unregister_shuffle(sgx_engine *e, int32_t shuffle_id);

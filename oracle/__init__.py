@@ -68,6 +68,12 @@ def lib() -> ctypes.CDLL:
         L.orc_zipf_cdf.restype = None
         L.orc_gen_zipf16.argtypes = [vp, i64, u64, i64, vp, i64]
         L.orc_gen_zipf16.restype = None
+        L.orc_lz4_compress_block.argtypes = [vp, ctypes.c_int, vp]
+        L.orc_lz4_compress_block.restype = ctypes.c_int
+        L.orc_xxh32.argtypes = [vp, i64, ctypes.c_uint32]
+        L.orc_xxh32.restype = ctypes.c_uint32
+        L.orc_lz4_frame_partitions.argtypes = [vp, vp, i32, ctypes.c_int, vp, vp]
+        L.orc_lz4_frame_partitions.restype = i64
         _lib = L
     return _lib
 
@@ -271,3 +277,35 @@ def kryo_partition_offsets(records: np.ndarray, counts: np.ndarray) -> np.ndarra
     cum = np.zeros(len(lens) + 1, dtype=np.int64)
     np.cumsum(lens, out=cum[1:])
     return cum[offsets(counts)]
+
+
+# ---------------------------------------------------------------- LZ4 framing -----
+# spark.shuffle.compress=true with the lz4 codec: lz4_oracle.c (restatement of liblz4 1.9.x
+# LZ4_compress_default, XXH32 and lz4-java's LZ4BlockOutputStream framing).
+LZ4_BLOCK_SIZE = 32 * 1024  # spark.io.compression.lz4.blockSize default
+
+
+def lz4_compress_block(block: bytes) -> bytes:
+    src = np.frombuffer(bytes(block), dtype=np.uint8)
+    dst = np.empty(len(src) + len(src) // 255 + 16, dtype=np.uint8)
+    n = lib().orc_lz4_compress_block(_ptr(src) if len(src) else None, len(src), _ptr(dst))
+    return dst[:n].tobytes()
+
+
+def xxh32(data: bytes, seed: int) -> int:
+    src = np.frombuffer(bytes(data), dtype=np.uint8)
+    return int(lib().orc_xxh32(_ptr(src) if len(src) else None, len(src), seed & 0xFFFFFFFF))
+
+
+def lz4_frame_partitions(stream: np.ndarray, offs: np.ndarray, block_size: int = LZ4_BLOCK_SIZE):
+    """Each partition stream [offs[r], offs[r+1]) framed as Spark's LZ4BlockOutputStream writes
+    it -> (framed bytes uint8, framed lengths int64[R])."""
+    stream = np.ascontiguousarray(stream, dtype=np.uint8)
+    offs = np.ascontiguousarray(offs, dtype=np.int64)
+    R = len(offs) - 1
+    lens = np.empty(R, dtype=np.int64)
+    sp = _ptr(stream) if len(stream) else None
+    total = lib().orc_lz4_frame_partitions(sp, _ptr(offs), R, block_size, None, _ptr(lens))
+    out = np.empty(max(total, 1), dtype=np.uint8)
+    lib().orc_lz4_frame_partitions(sp, _ptr(offs), R, block_size, _ptr(out), _ptr(lens))
+    return out[:total], lens

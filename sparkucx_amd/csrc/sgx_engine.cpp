@@ -1811,3 +1811,76 @@ extern "C" int sgx_range_bounds(sgx_engine *e, const void *const *batches, const
     *out_nbounds = j;
     return SGX_OK;
 }
+
+// ------------------------------------------------------------------------------------
+// LZ4BlockOutputStream framing of partition streams (spark.shuffle.compress=true, lz4)
+// ------------------------------------------------------------------------------------
+extern "C" int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, const int64_t *part_offsets,
+                                        int32_t num_partitions, int32_t block_size, void *dst_dev,
+                                        int64_t dst_cap, int64_t *out_lengths) {
+    if (!e || !part_offsets || !out_lengths || num_partitions < 1)
+        return fail(SGX_ERR_INVALID, "sgx_lz4_frame_partitions: bad arguments");
+    if (block_size < 64 || block_size > sgx::lz4_max_block())
+        return fail(SGX_ERR_UNSUPPORTED, "LZ4 block size %d outside [64, %d]", block_size, sgx::lz4_max_block());
+    const int R = num_partitions;
+    std::vector<int64_t> blocks;  // {src offset, length} per block
+    std::vector<int32_t> first(R + 1);
+    for (int r = 0; r < R; ++r) {
+        first[r] = (int32_t)(blocks.size() / 2);
+        int64_t a = part_offsets[r], b = part_offsets[r + 1];
+        if (b < a || a < 0) return fail(SGX_ERR_INVALID, "partition offsets decrease at %d", r);
+        for (int64_t p = a; p < b; p += block_size) {
+            blocks.push_back(p);
+            blocks.push_back(std::min<int64_t>(block_size, b - p));
+        }
+    }
+    const int64_t nb = (int64_t)blocks.size() / 2;
+    first[R] = (int32_t)nb;
+    if (nb > 0 && !stream_dev) return fail(SGX_ERR_INVALID, "stream is NULL");
+    // lz4-java: level = max(0, 32 - nlz(blockSize - 1) - COMPRESSION_LEVEL_BASE (10))
+    const int level = std::max(0, 32 - __builtin_clz((unsigned)(block_size - 1)) - 10);
+    const int64_t slot = ((int64_t)21 + block_size + block_size / 255 + 16 + 15) / 16 * 16;
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    DevBuf d_blocks, d_slots, d_sizes, d_offs;
+    std::vector<int32_t> sizes(nb);
+    if (nb > 0) {
+        SGX_TRY(d_blocks.ensure((size_t)nb * 16));
+        SGX_TRY(d_slots.ensure((size_t)(nb * slot)));
+        SGX_TRY(d_sizes.ensure((size_t)nb * 4));
+        HIP_TRY(hipMemcpyAsync(d_blocks.p, blocks.data(), (size_t)nb * 16, hipMemcpyHostToDevice, e->s_comp));
+        HIP_TRY(sgx::launch_lz4_blocks((const uint8_t *)stream_dev, (const int64_t *)d_blocks.p, nb, level,
+                                       (uint8_t *)d_slots.p, slot, (int32_t *)d_sizes.p, e->s_comp));
+        HIP_TRY(hipMemcpyAsync(sizes.data(), d_sizes.p, (size_t)nb * 4, hipMemcpyDeviceToHost, e->s_comp));
+        HIP_TRY(hipStreamSynchronize(e->s_comp));
+    }
+    // frame offsets (blocks of a partition back to back, then its end mark)
+    std::vector<int64_t> offs((size_t)nb + R);  // nb frame offsets | end-mark offsets
+    int64_t total = 0, nends = 0;
+    for (int r = 0; r < R; ++r) {
+        int64_t start = total;
+        for (int32_t b = first[r]; b < first[r + 1]; ++b) {
+            if (sizes[b] < 21 || sizes[b] > slot) return fail(SGX_ERR_HIP, "LZ4 block %d: bad frame size %d", b, sizes[b]);
+            offs[b] = total;
+            total += sizes[b];
+        }
+        if (first[r + 1] > first[r]) {
+            offs[nb + nends++] = total;
+            total += 21;
+        }
+        out_lengths[r] = total - start;
+    }
+    if (!dst_dev) return SGX_OK;
+    if (total > dst_cap)
+        return fail(SGX_ERR_INVALID, "LZ4 frames need %lld bytes, destination holds %lld", (long long)total,
+                    (long long)dst_cap);
+    if (nb > 0) {
+        SGX_TRY(d_offs.ensure((size_t)(nb + nends) * 8));
+        HIP_TRY(hipMemcpyAsync(d_offs.p, offs.data(), (size_t)(nb + nends) * 8, hipMemcpyHostToDevice, e->s_comp));
+        HIP_TRY(sgx::launch_lz4_gather((const uint8_t *)d_slots.p, slot, (const int32_t *)d_sizes.p,
+                                       (const int64_t *)d_offs.p, nb, (const int64_t *)d_offs.p + nb, nends, level,
+                                       (uint8_t *)dst_dev, e->s_comp));
+        HIP_TRY(hipStreamSynchronize(e->s_comp));
+    }
+    return SGX_OK;
+}

@@ -104,6 +104,14 @@ hipError_t launch_scatter_chain(const void *in, void *out, int64_t n, const Part
                                 int grid, hipStream_t stream);
 __host__ __device__ size_t scatter16_chain_lds(uint32_t R, int waves, int items, int mbits);
 // items: [n][3] int64 {src_off, dst_off, bytes}; all offsets/bytes multiples of `align`.
+// LZ4BlockOutputStream framing (sgx_lz4.hip)
+int lz4_lanes_per_workgroup();
+int lz4_max_block();
+hipError_t launch_lz4_blocks(const uint8_t *stream, const int64_t *blocks, int64_t nblocks, int level,
+                             uint8_t *slots, int64_t slot_bytes, int32_t *sizes, hipStream_t s);
+hipError_t launch_lz4_gather(const uint8_t *slots, int64_t slot_bytes, const int32_t *sizes,
+                             const int64_t *frame_off, int64_t nblocks, const int64_t *end_off, int64_t nends,
+                             int level, uint8_t *dst, hipStream_t s);
 hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, int64_t n_items,
                              int align, hipStream_t stream);
 // items: [n][3] int64 {src address, dst address, bytes} (device memory on both sides).

@@ -1,0 +1,253 @@
+// Spark shuffle compression on the GPU: every partition stream of a map output framed as
+// lz4-java's LZ4BlockOutputStream writes it (spark.shuffle.compress=true, codec lz4, the
+// Spark 3.0.1 defaults; SerializerManager.wrapStream per partition in
+// ShufflePartitionPairsWriter.open).  Byte-identical to liblz4 1.9.x LZ4_compress_default
+// per 32 KiB block + XXH32 (seed 0x9747b28c, masked to 28 bits) + the 21-byte block headers and
+// the end mark; see oracle/lz4_oracle.c for the restated algorithm and DESIGN.md §12.
+//
+// Two kernels:
+//   k_lz4_blocks  one LANE per block: the block's input bytes and its 8192-entry u16 hash
+//                 table live in LDS (48 KiB per lane), so the greedy match search -- a serial
+//                 dependence chain by construction of LZ4_compress_default's skip acceleration
+//                 and table updates -- runs at LDS latency.  The frame (header + payload) goes
+//                 to a fixed-size slot; its size to sizes[b].
+//   k_lz4_gather  one workgroup per block copies the slot to the frame's final offset
+//                 (offsets scanned on the host from sizes), and writes the partition end marks.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "sgx_internal.h"
+
+namespace sgx {
+namespace {
+
+constexpr int kMinMatch = 4;
+constexpr int kLastLiterals = 5;
+constexpr int kMfLimit = 12;
+constexpr int kHashLog = 13;                       // byU16 table: LZ4_HASHLOG + 1
+constexpr int kTable = 1 << kHashLog;              // 8192 u16 entries
+constexpr int kMaxBlock = 32768;                   // LDS staging limit per lane
+constexpr int kLanes = 3;                          // lanes (blocks) per workgroup: 3 x 48 KiB LDS
+constexpr int kHeader = 21;
+
+__device__ __forceinline__ uint32_t lds32(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+__device__ __forceinline__ uint32_t hash4(uint32_t seq) { return (seq * 2654435761u) >> (32 - kHashLog); }
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+
+__device__ uint32_t xxh32_lds(const uint8_t *p, int len, uint32_t seed) {
+    const uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u,
+                   P5 = 374761393u;
+    const uint8_t *end = p + len;
+    uint32_t h;
+    if (len >= 16) {
+        uint32_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+        const uint8_t *limit = end - 16;
+        do {
+            v1 = rotl(v1 + lds32(p) * P2, 13) * P1;
+            v2 = rotl(v2 + lds32(p + 4) * P2, 13) * P1;
+            v3 = rotl(v3 + lds32(p + 8) * P2, 13) * P1;
+            v4 = rotl(v4 + lds32(p + 12) * P2, 13) * P1;
+            p += 16;
+        } while (p <= limit);
+        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+    } else {
+        h = seed + P5;
+    }
+    h += (uint32_t)len;
+    while (p + 4 <= end) { h = rotl(h + lds32(p) * P3, 17) * P4; p += 4; }
+    while (p < end) { h = rotl(h + (uint32_t)(*p) * P5, 11) * P1; p++; }
+    h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
+    return h;
+}
+
+// LZ4_compress_default of src[0, n) (n < 65547) into out; returns the compressed size.
+// `src` and `table` are this lane's LDS slices; output bytes go straight to HBM.
+// `table` must be zeroed (LZ4_initStream).
+__device__ int lz4_compress_lane(const uint8_t *src, int n, uint16_t *table, uint8_t *out) {
+    const uint8_t *ip = src, *anchor = src, *iend = src + n;
+    const uint8_t *mflimit_plus_one = iend - kMfLimit + 1;
+    const uint8_t *matchlimit = iend - kLastLiterals;
+    uint8_t *op = out;
+    if (n >= kMfLimit + 1) {
+        table[hash4(lds32(ip))] = 0;
+        ip++;
+        uint32_t fwd_h = hash4(lds32(ip));
+        for (;;) {
+            const uint8_t *match;
+            uint8_t *token;
+            bool found = false;
+            {
+                const uint8_t *fwd = ip;
+                int step = 1, search = 1 << 6;
+                for (;;) {
+                    uint32_t h = fwd_h;
+                    uint32_t cur = (uint32_t)(fwd - src);
+                    uint32_t midx = table[h];
+                    ip = fwd;
+                    fwd += step;
+                    step = search++ >> 6;
+                    if (fwd > mflimit_plus_one) break;
+                    match = src + midx;
+                    fwd_h = hash4(lds32(fwd));
+                    table[h] = (uint16_t)cur;
+                    if (lds32(match) == lds32(ip)) { found = true; break; }
+                }
+            }
+            if (!found) break;
+            while (ip > anchor && match > src && ip[-1] == match[-1]) { ip--; match--; }
+            {
+                unsigned lit = (unsigned)(ip - anchor);
+                token = op++;
+                uint8_t tk;
+                if (lit >= 15) {
+                    int len = (int)lit - 15;
+                    tk = 15 << 4;
+                    for (; len >= 255; len -= 255) *op++ = 255;
+                    *op++ = (uint8_t)len;
+                } else {
+                    tk = (uint8_t)(lit << 4);
+                }
+                for (unsigned i = 0; i < lit; ++i) op[i] = anchor[i];
+                op += lit;
+                for (;;) {  // _next_match
+                    uint32_t off = (uint32_t)(ip - match);
+                    op[0] = (uint8_t)off;
+                    op[1] = (uint8_t)(off >> 8);
+                    op += 2;
+                    const uint8_t *a = ip + kMinMatch, *b = match + kMinMatch;
+                    while (a < matchlimit && *a == *b) { a++; b++; }
+                    unsigned mc = (unsigned)(a - (ip + kMinMatch));
+                    ip = a;
+                    if (mc >= 15) {
+                        tk += 15;
+                        mc -= 15;
+                        for (; mc >= 255; mc -= 255) *op++ = 255;
+                        *op++ = (uint8_t)mc;
+                    } else {
+                        tk += (uint8_t)mc;
+                    }
+                    *token = tk;
+                    anchor = ip;
+                    if (ip >= mflimit_plus_one) goto last_literals;
+                    table[hash4(lds32(ip - 2))] = (uint16_t)(ip - 2 - src);
+                    uint32_t h = hash4(lds32(ip));
+                    uint32_t cur = (uint32_t)(ip - src);
+                    match = src + table[h];
+                    table[h] = (uint16_t)cur;
+                    if (lds32(match) != lds32(ip)) break;
+                    token = op++;
+                    tk = 0;
+                }
+            }
+            fwd_h = hash4(lds32(++ip));
+        }
+    }
+last_literals:
+    {
+        int last = (int)(iend - anchor);
+        if (last >= 15) {
+            int acc = last - 15;
+            *op++ = 15 << 4;
+            for (; acc >= 255; acc -= 255) *op++ = 255;
+            *op++ = (uint8_t)acc;
+        } else {
+            *op++ = (uint8_t)(last << 4);
+        }
+        for (int i = 0; i < last; ++i) op[i] = anchor[i];
+        op += last;
+    }
+    return (int)(op - out);
+}
+
+__device__ __forceinline__ void st32le(uint8_t *p, uint32_t v) {
+    p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
+}
+
+__device__ __forceinline__ void put_header(uint8_t *h, uint8_t token, uint32_t clen, uint32_t olen,
+                                           uint32_t check) {
+    h[0] = 'L'; h[1] = 'Z'; h[2] = '4'; h[3] = 'B'; h[4] = 'l'; h[5] = 'o'; h[6] = 'c'; h[7] = 'k';
+    h[8] = token;
+    st32le(h + 9, clen);
+    st32le(h + 13, olen);
+    st32le(h + 17, check);
+}
+
+// blocks[b] = {src byte offset, length}; one lane per block, kLanes lanes per workgroup.
+__global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ stream,
+                                                   const int64_t *__restrict__ blocks, int64_t nblocks,
+                                                   int level, uint8_t *__restrict__ slots,
+                                                   int64_t slot_bytes, int32_t *__restrict__ sizes) {
+    __shared__ uint8_t s_in[kLanes][kMaxBlock];
+    __shared__ uint16_t s_tab[kLanes][kTable];
+    const int lane = threadIdx.x;
+    const int64_t b = (int64_t)blockIdx.x * kLanes + lane;
+    // stage this workgroup's blocks cooperatively (all 64 threads, 4 B per thread-step)
+    for (int l = 0; l < kLanes; ++l) {
+        int64_t bb = (int64_t)blockIdx.x * kLanes + l;
+        if (bb >= nblocks) break;
+        const uint8_t *g = stream + blocks[2 * bb];
+        int n = (int)blocks[2 * bb + 1];
+        for (int i = threadIdx.x; i < n; i += 64) s_in[l][i] = g[i];
+    }
+    for (int i = threadIdx.x; i < kLanes * kTable / 2; i += 64) ((uint32_t *)s_tab)[i] = 0u;
+    __syncthreads();
+    if (lane >= kLanes || b >= nblocks) return;
+    const int n = (int)blocks[2 * b + 1];
+    uint8_t *slot = slots + b * slot_bytes;
+    int c = lz4_compress_lane(s_in[lane], n, s_tab[lane], slot + kHeader);
+    const bool raw = c >= n;
+    if (raw) {
+        for (int i = 0; i < n; ++i) slot[kHeader + i] = s_in[lane][i];
+        c = n;
+    }
+    uint32_t check = xxh32_lds(s_in[lane], n, 0x9747b28cu) & 0x0FFFFFFFu;
+    put_header(slot, (uint8_t)((raw ? 0x10 : 0x20) | level), (uint32_t)c, (uint32_t)n, check);
+    sizes[b] = kHeader + c;
+}
+
+// frame b: copy sizes[b] bytes of slot b to dst + frame_off[b]; workgroups past nblocks write
+// end marks at end_off[r] (partitions with bytes only).
+__global__ __launch_bounds__(256) void k_lz4_gather(const uint8_t *__restrict__ slots, int64_t slot_bytes,
+                                                    const int32_t *__restrict__ sizes,
+                                                    const int64_t *__restrict__ frame_off, int64_t nblocks,
+                                                    const int64_t *__restrict__ end_off, int64_t nends,
+                                                    int level, uint8_t *__restrict__ dst) {
+    const int64_t b = blockIdx.x;
+    if (b < nblocks) {
+        const uint8_t *s = slots + b * slot_bytes;
+        uint8_t *d = dst + frame_off[b];
+        const int n = sizes[b];
+        for (int i = threadIdx.x; i < n; i += 256) d[i] = s[i];
+        return;
+    }
+    const int64_t e = (b - nblocks) * 256 + threadIdx.x;
+    if (e < nends) put_header(dst + end_off[e], (uint8_t)(0x10 | level), 0u, 0u, 0u);
+}
+
+}  // namespace
+
+int lz4_lanes_per_workgroup() { return kLanes; }
+int lz4_max_block() { return kMaxBlock; }
+
+hipError_t launch_lz4_blocks(const uint8_t *stream, const int64_t *blocks, int64_t nblocks, int level,
+                             uint8_t *slots, int64_t slot_bytes, int32_t *sizes, hipStream_t stream_) {
+    if (nblocks <= 0) return hipSuccess;
+    int64_t grid = (nblocks + kLanes - 1) / kLanes;
+    hipLaunchKernelGGL(k_lz4_blocks, dim3((unsigned)grid), dim3(64), 0, stream_, stream, blocks, nblocks,
+                       level, slots, slot_bytes, sizes);
+    return hipGetLastError();
+}
+
+hipError_t launch_lz4_gather(const uint8_t *slots, int64_t slot_bytes, const int32_t *sizes,
+                             const int64_t *frame_off, int64_t nblocks, const int64_t *end_off, int64_t nends,
+                             int level, uint8_t *dst, hipStream_t stream_) {
+    int64_t grid = nblocks + (nends + 255) / 256;
+    if (grid <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_lz4_gather, dim3((unsigned)grid), dim3(256), 0, stream_, slots, slot_bytes, sizes,
+                       frame_off, nblocks, end_off, nends, level, dst);
+    return hipGetLastError();
+}
+
+}  // namespace sgx

@@ -16,6 +16,8 @@ import numpy as np
 from . import _lib
 from ._lib import MEM_DEVICE, MEM_HOST, check, lib
 
+LZ4_BLOCK_SIZE = 32 * 1024  # spark.io.compression.lz4.blockSize default (Spark 3.0.1)
+
 
 class DeviceBuffer:
     """HBM allocation owned by the engine's device (freed by ``free()`` or GC)."""
@@ -164,6 +166,34 @@ class ShuffleEngine:
         if n:
             check(lib().sgx_memcpy(self.handle, out.ctypes.data, ptr, n), "sgx_memcpy")
         return out
+
+    def lz4_frame(self, stream_ptr: int, part_offsets, block_size: int = LZ4_BLOCK_SIZE):
+        """spark.shuffle.compress=true (lz4): frame the partition streams
+        [part_offsets[r], part_offsets[r+1]) of the device bytes at ``stream_ptr`` as lz4-java's
+        LZ4BlockOutputStream writes them, on the GPU.  Returns (framed bytes on the host,
+        framed lengths int64[R])."""
+        offs = np.ascontiguousarray(part_offsets, dtype=np.int64)
+        R = len(offs) - 1
+        lens = np.empty(R, dtype=np.int64)
+        check(lib().sgx_lz4_frame_partitions(self.handle, stream_ptr or None, offs.ctypes.data, R, block_size,
+                                              None, 0, lens.ctypes.data), "lz4 frame (measure)")
+        total = int(lens.sum())
+        buf = self.alloc(max(total, 1))
+        try:
+            check(lib().sgx_lz4_frame_partitions(self.handle, stream_ptr or None, offs.ctypes.data, R, block_size,
+                                                  buf.ptr, total, lens.ctypes.data), "lz4 frame")
+            return buf.to_numpy(total), lens
+        finally:
+            buf.free()
+
+    def lz4_frame_map(self, shuffle_id: int, map_id: int, num_partitions: int,
+                      block_size: int = LZ4_BLOCK_SIZE):
+        """The map output's published partition streams (fixed codec or Kryo) LZ4-framed."""
+        lens = self.map_lengths(shuffle_id, map_id, num_partitions)
+        ptr, _ = self.map_data(shuffle_id, map_id)
+        offs = np.zeros(num_partitions + 1, dtype=np.int64)
+        np.cumsum(lens, out=offs[1:])
+        return self.lz4_frame(ptr, offs, block_size)
 
     def write_index(self, shuffle_id: int, map_id: int, index_path: str, data_path: str,
                     num_partitions: int) -> np.ndarray:

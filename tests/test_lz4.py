@@ -1,0 +1,181 @@
+"""spark.shuffle.compress=true with the lz4 codec (compression half).
+
+CPU: the oracle's restatement (oracle/lz4_oracle.c) is pinned against the system liblz4
+(LZ4_compress_default / LZ4_decompress_safe, 1.9.x) and the `xxhash` module, and against the
+golden fixtures tests/golden/lz4_*.npz (made by make_golden_lz4.py from liblz4 + xxhash, not
+from the oracle).  GPU: sgx_lz4_frame_partitions (k_lz4_blocks / k_lz4_gather) must be byte
+identical to the oracle and the fixtures: every frame header, checksum, payload and end mark.
+"""
+import ctypes
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+
+FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "lz4_*.npz")))
+
+
+def _liblz4():
+    try:
+        L = ctypes.CDLL("liblz4.so.1")
+    except OSError:
+        pytest.skip("system liblz4 not present")
+    L.LZ4_compress_default.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+    L.LZ4_decompress_safe.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+    return L
+
+
+def _cases(oracle):
+    rng = np.random.default_rng(7)
+    recs = oracle.gen_uniform16(20000, 0x5EEDC0DE)
+    kry = oracle.kryo_serialize(recs).tobytes()
+    out = [b"", b"a", b"abcabcabcabcabcabc", bytes(1000), kry[:32768], kry[5:30005],
+           rng.integers(0, 256, 32768, dtype=np.uint8).tobytes(),
+           rng.integers(0, 4, 30000, dtype=np.uint8).tobytes(), (b"xyz" * 20000)[:32768]]
+    out += [rng.integers(0, 3, n, dtype=np.uint8).tobytes() for n in range(0, 40)]
+    return out
+
+
+def parse_frames(buf: bytes):
+    """-> list of (token, compressed_len, original_len, checksum, payload); stops at end mark."""
+    frames, p = [], 0
+    while p < len(buf):
+        assert buf[p:p + 8] == b"LZ4Block"
+        tok = buf[p + 8]
+        cl, ol, ck = (int.from_bytes(buf[p + 9 + 4 * i:p + 13 + 4 * i], "little") for i in range(3))
+        frames.append((tok, cl, ol, ck, buf[p + 21:p + 21 + cl]))
+        p += 21 + cl
+    return frames
+
+
+def test_oracle_block_matches_liblz4(oracle_lib):
+    L = _liblz4()
+    for c in _cases(oracle_lib):
+        out = ctypes.create_string_buffer(len(c) + len(c) // 255 + 64)
+        n = L.LZ4_compress_default(c, out, len(c), len(out))
+        assert oracle_lib.lz4_compress_block(c) == out.raw[:n], len(c)
+
+
+def test_oracle_xxh32_matches_xxhash(oracle_lib):
+    xxhash = pytest.importorskip("xxhash")
+    for c in _cases(oracle_lib):
+        for seed in (0, 0x9747B28C):
+            assert oracle_lib.xxh32(c, seed) == xxhash.xxh32_intdigest(c, seed)
+    # published known answer: XXH32 of the empty input, seed 0
+    assert oracle_lib.xxh32(b"", 0) == 0x02CC5D05
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
+def test_oracle_matches_golden(path, oracle_lib):
+    g = np.load(path)
+    framed, lens = oracle_lib.lz4_frame_partitions(g["stream"], g["offsets"], int(g["block_size"]))
+    assert np.array_equal(lens, g["lengths"])
+    assert framed.tobytes() == g["framed"].tobytes()
+
+
+@pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
+def test_golden_frames_decode(path):
+    """Frames round-trip: LZ4_decompress_safe of each payload (or the RAW bytes) with a valid
+    masked XXH32, the partition streams restored byte for byte, one end mark per stream."""
+    L = _liblz4()
+    xxhash = pytest.importorskip("xxhash")
+    g = np.load(path)
+    stream, offs, framed, lens = g["stream"].tobytes(), g["offsets"], g["framed"].tobytes(), g["lengths"]
+    pos = 0
+    for r in range(len(lens)):
+        part = framed[pos:pos + lens[r]]
+        pos += lens[r]
+        want = stream[offs[r]:offs[r + 1]]
+        if not want:
+            assert lens[r] == 0
+            continue
+        frames = parse_frames(part)
+        assert frames[-1][1:4] == (0, 0, 0) and frames[-1][0] & 0xF0 == 0x10
+        got = b""
+        for tok, cl, ol, ck, pay in frames[:-1]:
+            if tok & 0xF0 == 0x10:
+                blk = pay
+            else:
+                out = ctypes.create_string_buffer(ol)
+                assert L.LZ4_decompress_safe(pay, out, cl, ol) == ol
+                blk = out.raw
+            assert ck == xxhash.xxh32_intdigest(blk, 0x9747B28C) & 0x0FFFFFFF
+            got += blk
+        assert got == want
+
+
+# ------------------------------------------------------------------------ GPU ------
+def _to_device(engine, data: bytes):
+    buf = engine.alloc(max(len(data), 1))
+    if data:
+        buf.copy_from(np.frombuffer(data, np.uint8))
+    return buf
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
+def test_gpu_matches_golden(path, engine):
+    g = np.load(path)
+    buf = _to_device(engine, g["stream"].tobytes())
+    try:
+        framed, lens = engine.lz4_frame(buf.ptr, g["offsets"], int(g["block_size"]))
+    finally:
+        buf.free()
+    assert np.array_equal(lens, g["lengths"])
+    assert framed.tobytes() == g["framed"].tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("block_size", [32768, 4096, 64])
+def test_gpu_matches_oracle_mixed_partitions(engine, oracle_lib, block_size):
+    cases = _cases(oracle_lib)
+    stream = b"".join(cases)
+    offs = np.zeros(len(cases) + 1, dtype=np.int64)
+    np.cumsum([len(c) for c in cases], out=offs[1:])
+    buf = _to_device(engine, stream)
+    try:
+        framed, lens = engine.lz4_frame(buf.ptr, offs, block_size)
+    finally:
+        buf.free()
+    want, wlens = oracle_lib.lz4_frame_partitions(np.frombuffer(stream, np.uint8), offs, block_size)
+    assert np.array_equal(lens, wlens)
+    assert framed.tobytes() == want.tobytes()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 200])
+def test_gpu_kryo_map_output_compressed(engine, oracle_lib, R):
+    """A Kryo (Long, Long) map output written by the engine, then LZ4-framed on the GPU: the
+    bytes Spark commits to the data file with spark.shuffle.compress=true."""
+    sid = 900 + R
+    n = 300_000
+    recs = oracle_lib.gen_uniform16(n, 0x5EEDC0DE)
+    # low-entropy keys as well, so blocks compress (values = record index)
+    recs[n // 2:, :8] = (np.arange(n - n // 2, dtype=np.int64) % 777).view(np.uint8).reshape(-1, 8)
+    engine.register_shuffle(sid, R)
+    try:
+        engine.set_serializer(sid, 1)
+        engine.write_map(sid, 0, recs, n, 16, num_partitions=R)
+        framed, lens = engine.lz4_frame_map(sid, 0, R)
+        out, counts = oracle_lib.map_write(recs, R)
+        kry = oracle_lib.kryo_serialize(out)
+        koffs = oracle_lib.kryo_partition_offsets(out, counts)
+        want, wlens = oracle_lib.lz4_frame_partitions(kry, koffs)
+        assert np.array_equal(lens, wlens)
+        assert framed.tobytes() == want.tobytes()
+        assert int(wlens.sum()) < int(koffs[-1])  # the low-entropy half compresses
+    finally:
+        engine.unregister_shuffle(sid)
+
+
+@pytest.mark.gpu
+def test_gpu_rejects_bad_block_size(engine, sgx_lib):
+    buf = _to_device(engine, b"x" * 100)
+    try:
+        with pytest.raises(sgx_lib._lib.UnsupportedOperationException):
+            engine.lz4_frame(buf.ptr, np.array([0, 100], np.int64), 65536)
+    finally:
+        buf.free()
