@@ -27,11 +27,17 @@ constexpr int kMfLimit = 12;
 constexpr int kHashLog = 13;                       // byU16 table: LZ4_HASHLOG + 1
 constexpr int kTable = 1 << kHashLog;              // 8192 u16 entries
 constexpr int kMaxBlock = 32768;                   // LDS staging limit per lane
-constexpr int kLanes = 3;                          // lanes (blocks) per workgroup: 3 x 48 KiB LDS
+constexpr int kLanes = 1;                          // one block per workgroup (one wave, one busy lane):
+                                                   // 48 KiB LDS -> 3 workgroups per CU on separate
+                                                   // SIMDs, so the serial lanes never share a wave
 constexpr int kHeader = 21;
 
+// unaligned little-endian 32-bit read from the LDS staging buffer: the two aligned dwords
+// around it + one v_alignbyte (instead of four ds_read_u8); the buffer is padded by 8 bytes
 __device__ __forceinline__ uint32_t lds32(const uint8_t *p) {
-    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3u));
 }
 __device__ __forceinline__ uint32_t hash4(uint32_t seq) { return (seq * 2654435761u) >> (32 - kHashLog); }
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
@@ -179,7 +185,7 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
                                                    const int64_t *__restrict__ blocks, int64_t nblocks,
                                                    int level, uint8_t *__restrict__ slots,
                                                    int64_t slot_bytes, int32_t *__restrict__ sizes) {
-    __shared__ uint8_t s_in[kLanes][kMaxBlock];
+    __shared__ __attribute__((aligned(16))) uint8_t s_in[kLanes][kMaxBlock + 16];
     __shared__ uint16_t s_tab[kLanes][kTable];
     const int lane = threadIdx.x;
     const int64_t b = (int64_t)blockIdx.x * kLanes + lane;
@@ -187,22 +193,31 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
     for (int l = 0; l < kLanes; ++l) {
         int64_t bb = (int64_t)blockIdx.x * kLanes + l;
         if (bb >= nblocks) break;
+        // aligned dword copy that keeps the source's misalignment (sh bytes) in LDS; the
+        // last dword is read byte-wise so nothing past the stream's end is touched
         const uint8_t *g = stream + blocks[2 * bb];
-        int n = (int)blocks[2 * bb + 1];
-        for (int i = threadIdx.x; i < n; i += 64) s_in[l][i] = g[i];
+        const int n = (int)blocks[2 * bb + 1];
+        const int sh = (int)((uintptr_t)g & 3u);
+        const uint32_t *gw = (const uint32_t *)(g - sh);
+        const int full = (sh + n) >> 2;
+        uint32_t *sw = (uint32_t *)s_in[l];
+#pragma unroll 8
+        for (int i = threadIdx.x; i < full; i += 64) sw[i] = gw[i];
+        if (threadIdx.x < ((sh + n) & 3)) s_in[l][full * 4 + threadIdx.x] = g[full * 4 - sh + threadIdx.x];
     }
     for (int i = threadIdx.x; i < kLanes * kTable / 2; i += 64) ((uint32_t *)s_tab)[i] = 0u;
     __syncthreads();
     if (lane >= kLanes || b >= nblocks) return;
     const int n = (int)blocks[2 * b + 1];
+    const uint8_t *src = s_in[lane] + ((uintptr_t)(stream + blocks[2 * b]) & 3u);
     uint8_t *slot = slots + b * slot_bytes;
-    int c = lz4_compress_lane(s_in[lane], n, s_tab[lane], slot + kHeader);
+    int c = lz4_compress_lane(src, n, s_tab[lane], slot + kHeader);
     const bool raw = c >= n;
     if (raw) {
-        for (int i = 0; i < n; ++i) slot[kHeader + i] = s_in[lane][i];
+        for (int i = 0; i < n; ++i) slot[kHeader + i] = src[i];
         c = n;
     }
-    uint32_t check = xxh32_lds(s_in[lane], n, 0x9747b28cu) & 0x0FFFFFFFu;
+    uint32_t check = xxh32_lds(src, n, 0x9747b28cu) & 0x0FFFFFFFu;
     put_header(slot, (uint8_t)((raw ? 0x10 : 0x20) | level), (uint32_t)c, (uint32_t)n, check);
     sizes[b] = kHeader + c;
 }
