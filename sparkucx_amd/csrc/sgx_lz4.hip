@@ -35,9 +35,11 @@ constexpr int kHeader = 21;
 // unaligned little-endian 32-bit read from the LDS staging buffer: the two aligned dwords
 // around it + one v_alignbyte (instead of four ds_read_u8); the buffer is padded by 8 bytes
 __device__ __forceinline__ uint32_t lds32(const uint8_t *p) {
-    const uintptr_t a = (uintptr_t)p;
-    const uint32_t *w = (const uint32_t *)(a & ~(uintptr_t)3);
-    return __builtin_amdgcn_alignbyte(w[1], w[0], (uint32_t)(a & 3u));
+    // pointer arithmetic (no int-to-pointer cast) keeps the LDS address space visible to the
+    // compiler: ds_read, not flat loads that would also wait on the pending HBM stores
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t *w = (const uint32_t *)(p - sh);
+    return __builtin_amdgcn_alignbyte(w[1], w[0], sh);
 }
 __device__ __forceinline__ uint32_t hash4(uint32_t seq) { return (seq * 2654435761u) >> (32 - kHashLog); }
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
@@ -123,7 +125,17 @@ __device__ int lz4_compress_lane(const uint8_t *src, int n, uint16_t *table, uin
                     op[1] = (uint8_t)(off >> 8);
                     op += 2;
                     const uint8_t *a = ip + kMinMatch, *b = match + kMinMatch;
-                    while (a < matchlimit && *a == *b) { a++; b++; }
+                    // LZ4_count: 4 bytes per step (first differing byte = ctz of the xor)
+                    for (;;) {
+                        if (a + 4 > matchlimit) {
+                            while (a < matchlimit && *a == *b) { a++; b++; }
+                            break;
+                        }
+                        const uint32_t d = lds32(a) ^ lds32(b);
+                        if (d) { a += __builtin_ctz(d) >> 3; break; }
+                        a += 4;
+                        b += 4;
+                    }
                     unsigned mc = (unsigned)(a - (ip + kMinMatch));
                     ip = a;
                     if (mc >= 15) {
