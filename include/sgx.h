@@ -101,6 +101,15 @@ int sgx_set_serializer(sgx_engine *e, int32_t shuffle_id, int32_t serializer);
 int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, const int64_t *part_offsets,
                              int32_t num_partitions, int32_t block_size, void *dst_dev, int64_t dst_cap,
                              int64_t *out_lengths);
+/* The reduce side of the same codec (lz4-java LZ4BlockInputStream, what
+ * SerializerManager.wrapStream does to each fetched block before deserialization,
+ * spark_3_0/UcxShuffleReader.scala:137-145): framed_dev holds any number of LZ4-framed
+ * partition streams back to back (e.g. the blocks of sgx_fetch_blocks); their decompressed
+ * bytes are written back to back into dst_dev.  *out_bytes = decompressed size; dst_dev NULL
+ * only measures.  Headers, lengths, block contents (LZ4_decompress_safe bounds) and every
+ * XXH32 are checked: SGX_ERR_INVALID on a malformed or corrupt stream.  Synchronous. */
+int sgx_lz4_unframe(sgx_engine *e, const void *framed_dev, int64_t framed_bytes, void *dst_dev, int64_t dst_cap,
+                    int64_t *out_bytes);
 /* unregisterShuffle: CommonUcxShuffleManager.scala:103-106 -> removeShuffle
  * (CommonUcxShuffleBlockResolver.scala:63-71). Frees the shuffle's HBM. */
 int sgx_unregister_shuffle(sgx_engine *e, int32_t shuffle_id);

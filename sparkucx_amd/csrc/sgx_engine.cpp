@@ -1884,3 +1884,51 @@ extern "C" int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, c
     }
     return SGX_OK;
 }
+
+// LZ4BlockInputStream on the reduce side: decompress fetched LZ4-framed partition streams
+extern "C" int sgx_lz4_unframe(sgx_engine *e, const void *framed_dev, int64_t framed_bytes, void *dst_dev,
+                               int64_t dst_cap, int64_t *out_bytes) {
+    if (!e || !out_bytes || framed_bytes < 0 || (framed_bytes > 0 && !framed_dev))
+        return fail(SGX_ERR_INVALID, "sgx_lz4_unframe: bad arguments");
+    *out_bytes = 0;
+    if (framed_bytes == 0) return SGX_OK;
+    std::lock_guard<std::mutex> lk(e->mu);
+    HIP_TRY(hipSetDevice(e->device));
+    // one walk normally suffices: room for a frame per 512 B of input (frames of full 32 KiB
+    // blocks are ~64x sparser); a denser stream (tiny partitions) is walked again with room
+    // for every frame
+    int64_t cap = framed_bytes / 512 + 4096;
+    DevBuf d_info, d_desc;
+    SGX_TRY(d_info.ensure(64));
+    int64_t info[5];
+    for (int pass = 0; pass < 2; ++pass) {
+        SGX_TRY(d_desc.ensure((size_t)cap * 16));
+        HIP_TRY(hipMemsetAsync(d_info.p, 0, 64, e->s_comp));
+        HIP_TRY(sgx::launch_lz4_walk((const uint8_t *)framed_dev, framed_bytes, (int64_t *)d_desc.p, cap,
+                                     (int64_t *)d_info.p, e->s_comp));
+        HIP_TRY(hipMemcpyAsync(info, d_info.p, 40, hipMemcpyDeviceToHost, e->s_comp));
+        HIP_TRY(hipStreamSynchronize(e->s_comp));
+        if (info[2] != 0 || info[0] <= cap || !dst_dev) break;
+        cap = info[0];
+    }
+    static const char *why[] = {"", "truncated header", "bad magic", "unknown compression method",
+                                "malformed end mark", "bad block lengths"};
+    if (info[2] != 0)
+        return fail(SGX_ERR_INVALID, "LZ4 stream: %s at byte %lld", why[info[2] < 6 ? info[2] : 0],
+                    (long long)info[3]);
+    const int64_t nframes = info[0];
+    *out_bytes = info[1];
+    if (!dst_dev) return SGX_OK;
+    if (info[1] > dst_cap)
+        return fail(SGX_ERR_INVALID, "LZ4 stream decodes to %lld bytes, destination holds %lld",
+                    (long long)info[1], (long long)dst_cap);
+    if (nframes == 0) return SGX_OK;
+    HIP_TRY(sgx::launch_lz4_decode((const uint8_t *)framed_dev, (const int64_t *)d_desc.p, nframes,
+                                   (uint8_t *)dst_dev, (uint32_t *)((int64_t *)d_info.p + 4), e->s_comp));
+    uint32_t derr = 0;
+    HIP_TRY(hipMemcpyAsync(&derr, (int64_t *)d_info.p + 4, 4, hipMemcpyDeviceToHost, e->s_comp));
+    HIP_TRY(hipStreamSynchronize(e->s_comp));
+    if (derr & 1u) return fail(SGX_ERR_INVALID, "LZ4 stream: corrupt compressed block");
+    if (derr & 2u) return fail(SGX_ERR_INVALID, "LZ4 stream: block checksum mismatch");
+    return SGX_OK;
+}

@@ -112,6 +112,10 @@ hipError_t launch_lz4_blocks(const uint8_t *stream, const int64_t *blocks, int64
 hipError_t launch_lz4_gather(const uint8_t *slots, int64_t slot_bytes, const int32_t *sizes,
                              const int64_t *frame_off, int64_t nblocks, const int64_t *end_off, int64_t nends,
                              int level, uint8_t *dst, hipStream_t s);
+hipError_t launch_lz4_walk(const uint8_t *in, int64_t nbytes, int64_t *desc, int64_t desc_cap, int64_t *info,
+                           hipStream_t s);
+hipError_t launch_lz4_decode(const uint8_t *in, const int64_t *desc, int64_t nframes, uint8_t *out,
+                             uint32_t *err, hipStream_t s);
 hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, int64_t n_items,
                              int align, hipStream_t stream);
 // items: [n][3] int64 {src address, dst address, bytes} (device memory on both sides).

@@ -253,6 +253,121 @@ __global__ __launch_bounds__(256) void k_lz4_gather(const uint8_t *__restrict__ 
     if (e < nends) put_header(dst + end_off[e], (uint8_t)(0x10 | level), 0u, 0u, 0u);
 }
 
+
+// ---------------------------------------------------------------------------------------
+// reduce side: LZ4BlockInputStream over fetched bytes (any number of partition streams back
+// to back, each ended by its end mark)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t g32le(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+// One thread walks the frame headers (each header gives the next one's position: a serial
+// pointer chase, ~1 HBM latency per frame) and records desc[k] = {frame offset, output
+// offset} for the first desc_cap frames.  info = {frames, output bytes, error code, error
+// position}.
+__global__ void k_lz4_walk(const uint8_t *__restrict__ in, int64_t nbytes, int64_t *__restrict__ desc,
+                           int64_t desc_cap, int64_t *__restrict__ info) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    int64_t p = 0, k = 0, out = 0, err = 0;
+    while (p < nbytes) {
+        if (p + kHeader > nbytes) { err = 1; break; }
+        const uint8_t *h = in + p;
+        if (h[0] != 'L' || h[1] != 'Z' || h[2] != '4' || h[3] != 'B' || h[4] != 'l' || h[5] != 'o' ||
+            h[6] != 'c' || h[7] != 'k') { err = 2; break; }
+        const uint32_t tok = h[8], clen = g32le(h + 9), olen = g32le(h + 13), check = g32le(h + 17);
+        const uint32_t method = tok & 0xF0u;
+        if (method != 0x10u && method != 0x20u) { err = 3; break; }
+        if (olen == 0) {  // end mark
+            if (clen != 0 || check != 0) { err = 4; break; }
+            p += kHeader;
+            continue;
+        }
+        if (olen > (uint32_t)kMaxBlock || clen == 0 || (method == 0x10u && clen != olen) ||
+            p + kHeader + (int64_t)clen > nbytes) { err = 5; break; }
+        if (k < desc_cap) {  // past the capacity the walk only counts (caller re-walks)
+            desc[2 * k + 0] = p;
+            desc[2 * k + 1] = out;
+        }
+        ++k;
+        out += olen;
+        p += kHeader + clen;
+    }
+    info[0] = k;
+    info[1] = out;
+    info[2] = err;
+    info[3] = p;
+}
+
+// One frame per workgroup: lane 0 decodes the LZ4 block sequence by sequence into LDS
+// (bounds-checked: LZ4_decompress_safe semantics), the wave copies RAW payloads, lane 0
+// verifies XXH32, the wave writes the block out.  Errors: atomicOr into *err.
+__global__ __launch_bounds__(64) void k_lz4_decode(const uint8_t *__restrict__ in,
+                                                   const int64_t *__restrict__ desc, int64_t nframes,
+                                                   uint8_t *__restrict__ out, uint32_t *__restrict__ err) {
+    __shared__ __attribute__((aligned(16))) uint8_t s_out[kMaxBlock + 16];
+    __shared__ int s_bad;
+    const int64_t f = blockIdx.x;
+    if (f >= nframes) return;
+    const uint8_t *h = in + desc[2 * f + 0];  // header fields validated by the walk
+    const uint8_t *src = h + kHeader;
+    const uint32_t tok = h[8], clen = g32le(h + 9), olen = g32le(h + 13), check = g32le(h + 17);
+    if (threadIdx.x == 0) s_bad = 0;
+    if ((tok & 0xF0u) == 0x10u)
+        for (uint32_t i = threadIdx.x; i < olen; i += 64) s_out[i] = src[i];
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        int bad = 0;
+        if ((tok & 0xF0u) == 0x20u) {
+            uint32_t ip = 0, op = 0;
+            for (;;) {
+                if (ip >= clen) { bad = 1; break; }
+                const uint32_t t = src[ip++];
+                uint32_t lit = t >> 4;
+                if (lit == 15) {
+                    uint32_t b;
+                    do {
+                        if (ip >= clen) { bad = 1; break; }
+                        b = src[ip++];
+                        lit += b;
+                    } while (b == 255);
+                    if (bad) break;
+                }
+                if (ip + lit > clen || op + lit > olen) { bad = 1; break; }
+                for (uint32_t i = 0; i < lit; ++i) s_out[op + i] = src[ip + i];
+                ip += lit;
+                op += lit;
+                if (ip == clen) break;  // the last sequence has literals only
+                if (ip + 2 > clen) { bad = 1; break; }
+                const uint32_t off = (uint32_t)src[ip] | ((uint32_t)src[ip + 1] << 8);
+                ip += 2;
+                uint32_t ml = (t & 15u) + kMinMatch;
+                if ((t & 15u) == 15u) {
+                    uint32_t b;
+                    do {
+                        if (ip >= clen) { bad = 1; break; }
+                        b = src[ip++];
+                        ml += b;
+                    } while (b == 255);
+                    if (bad) break;
+                }
+                if (off == 0 || off > op || op + ml > olen) { bad = 1; break; }
+                for (uint32_t i = 0; i < ml; ++i) s_out[op + i] = s_out[op - off + i];
+                op += ml;
+            }
+            if (!bad && op != olen) bad = 1;
+        }
+        if (!bad && (xxh32_lds(s_out, (int)olen, 0x9747b28cu) & 0x0FFFFFFFu) != check) bad = 2;
+        s_bad = bad;
+    }
+    __syncthreads();
+    if (s_bad) {
+        if (threadIdx.x == 0) atomicOr(err, (uint32_t)s_bad);
+        return;
+    }
+    uint8_t *d = out + desc[2 * f + 1];
+    for (uint32_t i = threadIdx.x; i < olen; i += 64) d[i] = s_out[i];
+}
 }  // namespace
 
 int lz4_lanes_per_workgroup() { return kLanes; }
@@ -277,4 +392,19 @@ hipError_t launch_lz4_gather(const uint8_t *slots, int64_t slot_bytes, const int
     return hipGetLastError();
 }
 
+}  // namespace sgx
+
+namespace sgx {
+hipError_t launch_lz4_walk(const uint8_t *in, int64_t nbytes, int64_t *desc, int64_t desc_cap, int64_t *info,
+                           hipStream_t s) {
+    hipLaunchKernelGGL(k_lz4_walk, dim3(1), dim3(64), 0, s, in, nbytes, desc, desc_cap, info);
+    return hipGetLastError();
+}
+
+hipError_t launch_lz4_decode(const uint8_t *in, const int64_t *desc, int64_t nframes, uint8_t *out,
+                             uint32_t *err, hipStream_t s) {
+    if (nframes <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_lz4_decode, dim3((unsigned)nframes), dim3(64), 0, s, in, desc, nframes, out, err);
+    return hipGetLastError();
+}
 }  // namespace sgx

@@ -186,6 +186,33 @@ class ShuffleEngine:
         finally:
             buf.free()
 
+    def lz4_unframe(self, framed) -> np.ndarray:
+        """LZ4BlockInputStream on the GPU: ``framed`` (host bytes/ndarray or DeviceBuffer) holds
+        LZ4-framed partition streams back to back; returns their decompressed bytes (host)."""
+        own = None
+        if isinstance(framed, DeviceBuffer):
+            ptr, n = framed.ptr, framed.nbytes
+        else:
+            arr = np.frombuffer(bytes(framed), np.uint8) if not isinstance(framed, np.ndarray) else framed
+            n = int(arr.nbytes)
+            own = self.alloc(max(n, 1))
+            if n:
+                own.copy_from(np.ascontiguousarray(arr).view(np.uint8).reshape(-1))
+            ptr = own.ptr
+        try:
+            total = ctypes.c_int64()
+            check(lib().sgx_lz4_unframe(self.handle, ptr, n, None, 0, ctypes.byref(total)), "lz4 unframe (measure)")
+            out = self.alloc(max(total.value, 1))
+            try:
+                check(lib().sgx_lz4_unframe(self.handle, ptr, n, out.ptr, total.value, ctypes.byref(total)),
+                      "lz4 unframe")
+                return out.to_numpy(total.value)
+            finally:
+                out.free()
+        finally:
+            if own is not None:
+                own.free()
+
     def lz4_frame_map(self, shuffle_id: int, map_id: int, num_partitions: int,
                       block_size: int = LZ4_BLOCK_SIZE):
         """The map output's published partition streams (fixed codec or Kryo) LZ4-framed."""

@@ -179,3 +179,61 @@ def test_gpu_rejects_bad_block_size(engine, sgx_lib):
             engine.lz4_frame(buf.ptr, np.array([0, 100], np.int64), 65536)
     finally:
         buf.free()
+
+
+# ------------------------------------------------------------- GPU decode (reduce side) --
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
+def test_gpu_unframe_golden(path, engine):
+    """LZ4BlockInputStream on the GPU over all partitions' frames back to back = the stream."""
+    g = np.load(path)
+    got = engine.lz4_unframe(g["framed"])
+    assert got.tobytes() == g["stream"].tobytes()
+
+
+@pytest.mark.gpu
+def test_gpu_frame_unframe_round_trip(engine, oracle_lib):
+    cases = _cases(oracle_lib)
+    stream = b"".join(cases)
+    offs = np.zeros(len(cases) + 1, dtype=np.int64)
+    np.cumsum([len(c) for c in cases], out=offs[1:])
+    buf = _to_device(engine, stream)
+    try:
+        framed, lens = engine.lz4_frame(buf.ptr, offs, 4096)
+    finally:
+        buf.free()
+    assert engine.lz4_unframe(framed).tobytes() == stream
+    # any subset of partitions (fetched blocks in any order) decodes to those streams
+    fo = np.zeros(len(lens) + 1, dtype=np.int64)
+    np.cumsum(lens, out=fo[1:])
+    pick = [7, 3, 5, 0, 8]
+    sub = b"".join(framed[fo[r]:fo[r + 1]].tobytes() for r in pick)
+    assert engine.lz4_unframe(sub).tobytes() == b"".join(cases[r] for r in pick)
+
+
+@pytest.mark.gpu
+def test_gpu_unframe_rejects_corrupt(engine, sgx_lib):
+    g = np.load(FIXTURES[0])
+    framed = bytearray(g["framed"].tobytes())
+    bad_magic = bytes(framed)
+    bad_magic = b"X" + bad_magic[1:]
+    with pytest.raises(sgx_lib._lib.IllegalArgumentException):
+        engine.lz4_unframe(bad_magic)
+    flipped = bytearray(framed)
+    flipped[30] ^= 0x5A  # inside the first payload
+    with pytest.raises(sgx_lib._lib.IllegalArgumentException):
+        engine.lz4_unframe(bytes(flipped))
+    with pytest.raises(sgx_lib._lib.IllegalArgumentException):
+        engine.lz4_unframe(bytes(framed[:-5]))  # truncated end mark
+
+
+@pytest.mark.gpu
+def test_gpu_unframe_dense_frames(engine, oracle_lib):
+    """5000 tiny partition streams: more frames than the first walk's table holds (re-walk)."""
+    rng = np.random.default_rng(3)
+    parts = [rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8).tobytes() for _ in range(5000)]
+    stream = b"".join(parts)
+    offs = np.zeros(len(parts) + 1, dtype=np.int64)
+    np.cumsum([len(p) for p in parts], out=offs[1:])
+    want, _ = oracle_lib.lz4_frame_partitions(np.frombuffer(stream, np.uint8), offs)
+    assert engine.lz4_unframe(want).tobytes() == stream

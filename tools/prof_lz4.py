@@ -54,6 +54,17 @@ def main():
                                                  flen.ctypes.data), "frame")
             ts.append(time.perf_counter() - t0)
         t = float(np.median(ts[1:]))
+        # reduce side: decompress all frames back (LZ4BlockInputStream on the GPU)
+        out = e.alloc(int(nbytes))
+        got = ctypes.c_int64()
+        ds = []
+        for _ in range(a.iters + 1):
+            t0 = time.perf_counter()
+            check(lib().sgx_lz4_unframe(e.handle, dst.ptr, total, out.ptr, int(nbytes), ctypes.byref(got)), "unframe")
+            ds.append(time.perf_counter() - t0)
+        assert got.value == nbytes
+        td = float(np.median(ds[1:]))
+        out.free()
         # CPU oracle on a bounded sample: the first 64 partitions' streams
         stream = np.empty(int(offs[64]), dtype=np.uint8)
         check(lib().sgx_memcpy(e.handle, stream.ctypes.data, ptr, int(offs[64])), "copy")
@@ -63,6 +74,7 @@ def main():
         print(json.dumps({"case": case, "records": n, "partitions": R, "stream_bytes": int(nbytes),
                           "framed_bytes": total, "ratio": round(total / nbytes, 4),
                           "gpu_ms": round(t * 1e3, 3), "gpu_input_GBs": round(nbytes / t / 1e9, 2),
+                          "gpu_decode_ms": round(td * 1e3, 3), "gpu_decode_out_GBs": round(nbytes / td / 1e9, 2),
                           "cpu_oracle_1thread_GBs": round(int(offs[64]) / ct / 1e9, 3),
                           "cpu_sample_bytes": int(offs[64])}), flush=True)
         dst.free()
