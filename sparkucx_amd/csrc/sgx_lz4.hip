@@ -200,7 +200,7 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
     __shared__ __attribute__((aligned(16))) uint8_t s_in[kLanes][kMaxBlock + 16];
     __shared__ uint16_t s_tab[kLanes][kTable];
     const int lane = threadIdx.x;
-    const int64_t b = (int64_t)blockIdx.x * kLanes + lane;
+    const int64_t b = (int64_t)blockIdx.x * kLanes;
     // stage this workgroup's blocks cooperatively (all 64 threads, 4 B per thread-step)
     for (int l = 0; l < kLanes; ++l) {
         int64_t bb = (int64_t)blockIdx.x * kLanes + l;
@@ -219,16 +219,19 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
     }
     for (int i = threadIdx.x; i < kLanes * kTable / 2; i += 64) ((uint32_t *)s_tab)[i] = 0u;
     __syncthreads();
-    if (lane >= kLanes || b >= nblocks) return;
+    static_assert(kLanes == 1, "the tail below assumes one block per workgroup");
+    __shared__ int s_c;
+    if (b >= nblocks) return;  // uniform across the workgroup
     const int n = (int)blocks[2 * b + 1];
-    const uint8_t *src = s_in[lane] + ((uintptr_t)(stream + blocks[2 * b]) & 3u);
+    const uint8_t *src = s_in[0] + ((uintptr_t)(stream + blocks[2 * b]) & 3u);
     uint8_t *slot = slots + b * slot_bytes;
-    int c = lz4_compress_lane(src, n, s_tab[lane], slot + kHeader);
-    const bool raw = c >= n;
-    if (raw) {
-        for (int i = 0; i < n; ++i) slot[kHeader + i] = src[i];
-        c = n;
-    }
+    if (lane == 0) s_c = lz4_compress_lane(src, n, s_tab[0], slot + kHeader);
+    __syncthreads();
+    const bool raw = s_c >= n;  // the compressed block did not shrink: RAW, copied by the wave
+    const int c = raw ? n : s_c;
+    if (raw)
+        for (int i = lane; i < n; i += 64) slot[kHeader + i] = src[i];
+    if (lane != 0) return;
     uint32_t check = xxh32_lds(src, n, 0x9747b28cu) & 0x0FFFFFFFu;
     put_header(slot, (uint8_t)((raw ? 0x10 : 0x20) | level), (uint32_t)c, (uint32_t)n, check);
     sizes[b] = kHeader + c;
