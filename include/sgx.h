@@ -101,6 +101,15 @@ int sgx_set_serializer(sgx_engine *e, int32_t shuffle_id, int32_t serializer);
 int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, const int64_t *part_offsets,
                              int32_t num_partitions, int32_t block_size, void *dst_dev, int64_t dst_cap,
                              int64_t *out_lengths);
+/* The same compression as a shuffle property: with SGX_CODEC_LZ4 every map output of the
+ * shuffle publishes its LZ4-framed partition streams (block_size, 32768 = Spark's default)
+ * instead of the raw Kryo stream -- partition lengths, index offsets, data file, fetched and
+ * exchanged blocks are then the bytes Spark writes with spark.shuffle.compress=true.  Needs
+ * SGX_SER_KRYO (set first); set before the first sgx_write_map (SGX_ERR_STATE after).  The
+ * engine's own decoding reads (sgx_read_records / _sorted / _grouped) return
+ * SGX_ERR_UNSUPPORTED on such a shuffle: fetch the blocks and sgx_lz4_unframe them. */
+enum sgx_codec { SGX_CODEC_NONE = 0, SGX_CODEC_LZ4 = 1 };
+int sgx_set_compression(sgx_engine *e, int32_t shuffle_id, int32_t codec, int32_t block_size);
 /* The reduce side of the same codec (lz4-java LZ4BlockInputStream, what
  * SerializerManager.wrapStream does to each fetched block before deserialization,
  * spark_3_0/UcxShuffleReader.scala:137-145): framed_dev holds any number of LZ4-framed

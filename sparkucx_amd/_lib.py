@@ -89,6 +89,7 @@ SIGNATURES = {
     "sgx_set_serializer": (ctypes.c_int, [_vp, _i32, _i32]),
     "sgx_lz4_frame_partitions": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
     "sgx_lz4_unframe": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _P64]),
+    "sgx_set_compression": (ctypes.c_int, [_vp, _i32, _i32, _i32]),
     "sgx_write_map": (ctypes.c_int, [_vp, _i32, _i64, _vp, _i64, _i32, _i32, _vp]),
     "sgx_map_lengths": (ctypes.c_int, [_vp, _i32, _i64, _vp]),
     "sgx_map_data": (ctypes.c_int, [_vp, _i32, _i64, ctypes.POINTER(_vp), _P64]),

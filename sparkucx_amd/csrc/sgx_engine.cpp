@@ -104,6 +104,12 @@ struct DevBuf {
     }
 };
 
+// releases a scratch DevBuf when the scope ends (DevBuf itself is a plain member type)
+struct DevBufScope {
+    DevBuf &b;
+    ~DevBufScope() { b.release(); }
+};
+
 struct HostPinned {
     void *p = nullptr;
     size_t cap = 0;
@@ -144,7 +150,8 @@ struct MapOut {
     DevBuf ser_work;           // ser_off_dev (R+1) i64 | tile prefixes, block totals u64 | tile sums u32
     HostPinned ser_off;        // (R+1) i64 byte offsets + the error word, landed async
     int64_t out_bytes = 0;     // published bytes (n * rb, or the Kryo total once `ready`)
-    const void *view() const { return ser.p ? ser.p : data.p; }
+    DevBuf comp;               // LZ4-framed partition streams (sgx_set_compression), once `ready`
+    const void *view() const { return comp.p ? comp.p : (ser.p ? ser.p : data.p); }
 };
 
 // One exchange round: every rank pushed one map; this rank holds its reducers' blocks.
@@ -166,6 +173,7 @@ struct Round {
 struct Shuffle {
     int32_t R = 0, kind = 0, nb = 0, asc = 1, rb = 16;
     int32_t ser = SGX_SER_FIXED;  // dep.serializer (sgx_set_serializer)
+    int32_t lz4_block = 0;        // spark.shuffle.compress with lz4 (sgx_set_compression): block size
     DevBuf bounds;
     PartParams pp{};
     std::map<int64_t, std::unique_ptr<MapOut>> maps;
@@ -324,6 +332,7 @@ static void free_map(MapOut &m) {
     m.data.release();
     m.part_off.release();
     m.ser.release();
+    m.comp.release();
     m.ser_work.release();
     m.ser_off.release();
     if (m.done) (void)hipEventDestroy(m.done);
@@ -446,7 +455,11 @@ extern "C" int sgx_unregister_shuffle(sgx_engine *e, int32_t shuffle_id) {
 // ------------------------------------------------------------------------------------
 // map-side write: K1+K2 hist -> K3 scan -> K4 scatter (all on the compute stream)
 // ------------------------------------------------------------------------------------
-static int finish_lengths(Shuffle &s, MapOut &m) {
+static int lz4_frame_impl(sgx_engine *e, const void *stream_dev, const int64_t *part_offsets, int32_t R,
+                          int32_t block_size, DevBuf *alloc_dst, void *dst_dev, int64_t dst_cap,
+                          int64_t *out_lengths);
+
+static int finish_lengths(sgx_engine *e, Shuffle &s, MapOut &m) {
     if (m.ready) return SGX_OK;
     HIP_TRY(hipEventSynchronize(m.done));
     const uint32_t *po = (const uint32_t *)m.part_off.p;
@@ -471,6 +484,16 @@ static int finish_lengths(Shuffle &s, MapOut &m) {
     } else {
         for (int32_t p = 0; p < s.R; ++p) m.lengths[(size_t)p] = ((int64_t)po[p + 1] - (int64_t)po[p]) * s.rb;
         m.out_bytes = m.nrec * s.rb;
+    }
+    if (s.lz4_block > 0) {  // publish the LZ4-framed partition streams instead
+        std::vector<int64_t> offs((size_t)s.R + 1, 0);
+        for (int32_t p = 0; p < s.R; ++p) offs[(size_t)p + 1] = offs[(size_t)p] + m.lengths[(size_t)p];
+        std::vector<int64_t> clen((size_t)s.R, 0);
+        SGX_TRY(lz4_frame_impl(e, m.view(), offs.data(), s.R, s.lz4_block, &m.comp, nullptr, 0, clen.data()));
+        int64_t total = 0;
+        for (int32_t p = 0; p < s.R; ++p) total += clen[(size_t)p];
+        m.lengths = clen;
+        m.out_bytes = total;
     }
     m.ready = true;
     return SGX_OK;
@@ -673,6 +696,24 @@ extern "C" int sgx_set_serializer(sgx_engine *e, int32_t shuffle_id, int32_t ser
     return SGX_OK;
 }
 
+extern "C" int sgx_set_compression(sgx_engine *e, int32_t shuffle_id, int32_t codec, int32_t block_size) {
+    if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    auto it = e->shuffles.find(shuffle_id);
+    if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
+    Shuffle &s = it->second;
+    if (codec != SGX_CODEC_NONE && codec != SGX_CODEC_LZ4) return fail(SGX_ERR_INVALID, "unknown codec %d", codec);
+    if (!s.maps.empty()) return fail(SGX_ERR_STATE, "shuffle %d already has map outputs", shuffle_id);
+    if (codec == SGX_CODEC_LZ4) {
+        if (s.ser != SGX_SER_KRYO)
+            return fail(SGX_ERR_UNSUPPORTED, "LZ4 compression is published over the Kryo stream (sgx_set_serializer first)");
+        if (block_size < 64 || block_size > sgx::lz4_max_block())
+            return fail(SGX_ERR_UNSUPPORTED, "LZ4 block size %d outside [64, %d]", block_size, sgx::lz4_max_block());
+    }
+    s.lz4_block = codec == SGX_CODEC_LZ4 ? block_size : 0;
+    return SGX_OK;
+}
+
 extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records,
                              int64_t n, int32_t rb, int32_t mem_kind, int64_t *out_lengths) {
     if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
@@ -716,7 +757,7 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
     if (s.ser == SGX_SER_KRYO) SGX_TRY(serialize_kryo(e, s, m));
     HIP_TRY(hipEventRecord(m.done, st));
     if (out_lengths) {
-        SGX_TRY(finish_lengths(s, m));
+        SGX_TRY(finish_lengths(e, s, m));
         std::memcpy(out_lengths, m.lengths.data(), sizeof(int64_t) * (size_t)s.R);
     }
     return SGX_OK;
@@ -739,7 +780,7 @@ extern "C" int sgx_map_lengths(sgx_engine *e, int32_t shuffle_id, int64_t map_id
     Shuffle *s;
     MapOut *m;
     SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
-    SGX_TRY(finish_lengths(*s, *m));
+    SGX_TRY(finish_lengths(e, *s, *m));
     std::memcpy(out, m->lengths.data(), sizeof(int64_t) * (size_t)s->R);
     return SGX_OK;
 }
@@ -750,7 +791,7 @@ extern "C" int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, v
     Shuffle *s;
     MapOut *m;
     SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
-    SGX_TRY(finish_lengths(*s, *m));
+    SGX_TRY(finish_lengths(e, *s, *m));
     *ptr = const_cast<void *>(m->view());
     *bytes = m->out_bytes;
     return SGX_OK;
@@ -858,7 +899,7 @@ extern "C" int sgx_write_index(sgx_engine *e, int32_t shuffle_id, int64_t map_id
     Shuffle *s;
     MapOut *m;
     SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
-    SGX_TRY(finish_lengths(*s, *m));
+    SGX_TRY(finish_lengths(e, *s, *m));
     HIP_TRY(hipSetDevice(e->device));
     const std::string data_tmp = std::string(data_path) + ".sgx.tmp";
     const std::string index_tmp = std::string(index_path) + ".sgx.tmp";
@@ -1021,7 +1062,7 @@ extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
     MapOut *m;
     SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
     HIP_TRY(hipSetDevice(e->device));
-    SGX_TRY(finish_lengths(*s, *m));
+    SGX_TRY(finish_lengths(e, *s, *m));
     const int32_t P = e->nranks, R = s->R;
     std::unique_ptr<Round> rd(new Round());
     rd->map_ids.assign((size_t)P, 0);
@@ -1150,7 +1191,7 @@ static int fetch_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_id
             auto mt = s.maps.find(mid);
             if (mt != s.maps.end()) {
                 MapOut &m = *mt->second;
-                SGX_TRY(finish_lengths(s, m));
+                SGX_TRY(finish_lengths(e, s, m));
                 int64_t off = 0;
                 for (int32_t q = 0; q < r; ++q) off += m.lengths[(size_t)q];
                 srcs[(size_t)i] = Src{(const char *)m.view() + off, m.lengths[(size_t)r], m.done};
@@ -1235,6 +1276,8 @@ static int records_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_
     auto it = e->shuffles.find(shuffle_id);
     if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
     Shuffle &s = it->second;
+    if (s.lz4_block > 0)
+        return fail(SGX_ERR_UNSUPPORTED, "shuffle %d is LZ4-compressed: fetch its blocks and sgx_lz4_unframe them", shuffle_id);
     if (r0 < 0 || r1 > s.R || r0 > r1)
         return fail(SGX_ERR_INVALID, "partition range [%d, %d) outside [0, %d)", r0, r1, s.R);
     if (nmaps < 0 || (nmaps > 0 && !map_ids)) return fail(SGX_ERR_INVALID, "bad map list");
@@ -1540,7 +1583,7 @@ extern "C" int sgx_sync(sgx_engine *e) {
     HIP_TRY(hipStreamSynchronize(e->s_comm));
     HIP_TRY(hipStreamSynchronize(e->s_hist));
     for (auto &kv : e->shuffles)
-        for (auto &m : kv.second.maps) SGX_TRY(finish_lengths(kv.second, *m.second));
+        for (auto &m : kv.second.maps) SGX_TRY(finish_lengths(e, kv.second, *m.second));
     return SGX_OK;
 }
 
@@ -1815,9 +1858,10 @@ extern "C" int sgx_range_bounds(sgx_engine *e, const void *const *batches, const
 // ------------------------------------------------------------------------------------
 // LZ4BlockOutputStream framing of partition streams (spark.shuffle.compress=true, lz4)
 // ------------------------------------------------------------------------------------
-extern "C" int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, const int64_t *part_offsets,
-                                        int32_t num_partitions, int32_t block_size, void *dst_dev,
-                                        int64_t dst_cap, int64_t *out_lengths) {
+// caller holds e->mu; alloc_dst: allocate the destination (exact size) instead of dst_dev
+static int lz4_frame_impl(sgx_engine *e, const void *stream_dev, const int64_t *part_offsets,
+                          int32_t num_partitions, int32_t block_size, DevBuf *alloc_dst, void *dst_dev,
+                          int64_t dst_cap, int64_t *out_lengths) {
     if (!e || !part_offsets || !out_lengths || num_partitions < 1)
         return fail(SGX_ERR_INVALID, "sgx_lz4_frame_partitions: bad arguments");
     if (block_size < 64 || block_size > sgx::lz4_max_block())
@@ -1840,9 +1884,9 @@ extern "C" int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, c
     // lz4-java: level = max(0, 32 - nlz(blockSize - 1) - COMPRESSION_LEVEL_BASE (10))
     const int level = std::max(0, 32 - __builtin_clz((unsigned)(block_size - 1)) - 10);
     const int64_t slot = ((int64_t)21 + block_size + block_size / 255 + 16 + 15) / 16 * 16;
-    std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->device));
     DevBuf d_blocks, d_slots, d_sizes, d_offs;
+    DevBufScope g1{d_blocks}, g2{d_slots}, g3{d_sizes}, g4{d_offs};
     std::vector<int32_t> sizes(nb);
     if (nb > 0) {
         SGX_TRY(d_blocks.ensure((size_t)nb * 16));
@@ -1870,6 +1914,11 @@ extern "C" int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, c
         }
         out_lengths[r] = total - start;
     }
+    if (alloc_dst) {
+        SGX_TRY(alloc_dst->ensure((size_t)total));
+        dst_dev = alloc_dst->p;
+        dst_cap = total;
+    }
     if (!dst_dev) return SGX_OK;
     if (total > dst_cap)
         return fail(SGX_ERR_INVALID, "LZ4 frames need %lld bytes, destination holds %lld", (long long)total,
@@ -1883,6 +1932,15 @@ extern "C" int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, c
         HIP_TRY(hipStreamSynchronize(e->s_comp));
     }
     return SGX_OK;
+}
+
+extern "C" int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, const int64_t *part_offsets,
+                                        int32_t num_partitions, int32_t block_size, void *dst_dev,
+                                        int64_t dst_cap, int64_t *out_lengths) {
+    if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    return lz4_frame_impl(e, stream_dev, part_offsets, num_partitions, block_size, nullptr, dst_dev, dst_cap,
+                          out_lengths);
 }
 
 // LZ4BlockInputStream on the reduce side: decompress fetched LZ4-framed partition streams
@@ -1899,6 +1957,7 @@ extern "C" int sgx_lz4_unframe(sgx_engine *e, const void *framed_dev, int64_t fr
     // for every frame
     int64_t cap = framed_bytes / 512 + 4096;
     DevBuf d_info, d_desc;
+    DevBufScope g1{d_info}, g2{d_desc};
     SGX_TRY(d_info.ensure(64));
     int64_t info[5];
     for (int pass = 0; pass < 2; ++pass) {

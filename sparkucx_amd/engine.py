@@ -128,6 +128,14 @@ class ShuffleEngine:
         """dep.serializer: SER_FIXED (fixed-width records) or SER_KRYO (Spark's Kryo stream)."""
         check(lib().sgx_set_serializer(self.handle, shuffle_id, serializer), "setSerializer")
 
+    def set_compression(self, shuffle_id: int, codec: str = "lz4", block_size: int = LZ4_BLOCK_SIZE):
+        """spark.shuffle.compress / spark.io.compression.codec: "lz4" publishes every map output's
+        partition streams LZ4-framed (needs the Kryo serializer); "none" turns it off."""
+        codes = {"none": 0, "lz4": 1}
+        if codec not in codes:
+            raise _lib.IllegalArgumentException(f"unknown codec {codec!r} (none, lz4)")
+        check(lib().sgx_set_compression(self.handle, shuffle_id, codes[codec], block_size), "setCompression")
+
     def unregister_shuffle(self, shuffle_id: int):
         check(lib().sgx_unregister_shuffle(self.handle, shuffle_id), "unregisterShuffle")
 

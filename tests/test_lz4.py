@@ -237,3 +237,55 @@ def test_gpu_unframe_dense_frames(engine, oracle_lib):
     np.cumsum([len(p) for p in parts], out=offs[1:])
     want, _ = oracle_lib.lz4_frame_partitions(np.frombuffer(stream, np.uint8), offs)
     assert engine.lz4_unframe(want).tobytes() == stream
+
+
+# ------------------------------------------------- shuffle-level compression (engine) --
+@pytest.mark.gpu
+def test_gpu_compressed_shuffle_publishes_lz4_frames(engine, oracle_lib, sgx_lib, tmp_path):
+    """sgx_set_compression(LZ4) on a Kryo shuffle: lengths, map bytes, fetched blocks and the
+    committed index/data files are the LZ4BlockOutputStream bytes Spark writes with
+    spark.shuffle.compress=true."""
+    sid, R, n = 950, 64, 200_000
+    recs = oracle_lib.gen_uniform16(n, 0x5EEDC0DE)
+    recs[::2, :8] = (np.arange(0, n, 2, dtype=np.int64) % 999).view(np.uint8).reshape(-1, 8)
+    engine.register_shuffle(sid, R)
+    try:
+        engine.set_serializer(sid, 1)
+        engine.set_compression(sid, "lz4")
+        lens = engine.write_map(sid, 0, recs, n, 16, num_partitions=R)
+        out, counts = oracle_lib.map_write(recs, R)
+        want, wlens = oracle_lib.lz4_frame_partitions(oracle_lib.kryo_serialize(out),
+                                                      oracle_lib.kryo_partition_offsets(out, counts))
+        assert np.array_equal(lens, wlens)
+        assert engine.map_output_bytes(sid, 0).tobytes() == want.tobytes()
+        fo = oracle_lib.offsets(wlens)
+        pick = [5, 0, 63, 17]
+        got, glens = engine.fetch_blocks(sid, [0] * len(pick), pick)
+        assert got.tobytes() == b"".join(want[fo[r]:fo[r + 1]].tobytes() for r in pick)
+        # the reduce side decodes what it fetched: LZ4 -> Kryo stream of those partitions
+        kry = oracle_lib.kryo_serialize(out)
+        ko = oracle_lib.kryo_partition_offsets(out, counts)
+        assert engine.lz4_unframe(got).tobytes() == b"".join(kry[ko[r]:ko[r + 1]].tobytes() for r in pick)
+        idx, dat = str(tmp_path / "s.index"), str(tmp_path / "s.data")
+        committed = engine.write_index(sid, 0, idx, dat, R)
+        assert np.array_equal(committed, wlens)
+        assert open(dat, "rb").read() == want.tobytes()
+        assert open(idx, "rb").read() == oracle_lib.index_bytes(wlens)
+        with pytest.raises(sgx_lib._lib.UnsupportedOperationException):
+            engine.read_records(sid, [0], 0, R)
+        with pytest.raises(sgx_lib._lib.IllegalStateException):
+            engine.set_compression(sid, "none")
+    finally:
+        engine.unregister_shuffle(sid)
+
+
+@pytest.mark.gpu
+def test_gpu_compression_needs_kryo(engine, sgx_lib):
+    engine.register_shuffle(951, 8)
+    try:
+        with pytest.raises(sgx_lib._lib.UnsupportedOperationException):
+            engine.set_compression(951, "lz4")
+        with pytest.raises(sgx_lib._lib.IllegalArgumentException):
+            engine.set_compression(951, "snappy")
+    finally:
+        engine.unregister_shuffle(951)
