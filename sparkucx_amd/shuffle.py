@@ -430,6 +430,15 @@ class UcxShuffleReader:
         data, lens = self.manager.engine.fetch_blocks(self.handle.shuffleId, mids, rids)
         return data, lens, mids, rids
 
+    def readSerialized(self) -> np.ndarray:
+        """The partition range's serialized bytes as Spark's reader sees them after
+        SerializerManager.wrapStream (UcxShuffleReader.scala:137-145): fetched blocks, LZ4
+        frames decompressed on the GPU when the shuffle is compressed."""
+        data, _, _, _ = self.read_blocks()
+        if self.manager.compressed(self.handle.shuffleId):
+            return self.manager.engine.lz4_unframe(data)
+        return data
+
     def _maps(self):
         return sorted(self.mapIds if self.mapIds is not None else self.manager.known_maps(self.handle.shuffleId))
 
@@ -444,6 +453,10 @@ class UcxShuffleReader:
         * aggregator "sum" (reduceByKey(_ + _)): (keys, sums)."""
         dep = self.handle.dependency
         sid = self.handle.shuffleId
+        if self.manager.compressed(sid):
+            raise UnsupportedOperationException(
+                "this shuffle is LZ4-compressed (spark.shuffle.compress=true): readSerialized() returns its "
+                "decompressed serialized stream; record decoding of compressed shuffles is not on the GPU path yet")
         if dep.aggregator is not None:
             if dep.recordBytes != 16:
                 raise UnsupportedOperationException("aggregation needs (Long, Long) 16 B records")
@@ -476,6 +489,10 @@ class UcxShuffleManager:
         self.shuffleBlockResolver = UcxShuffleBlockResolver(self, root)
         self._handles: Dict[int, BaseShuffleHandle] = {}
         self._maps: Dict[int, set] = {}
+        self._compressed: set = set()
+
+    def compressed(self, shuffleId: int) -> bool:
+        return shuffleId in self._compressed
 
     def getTransport(self) -> GpuShuffleTransport:
         return self.ucxTransport
@@ -486,6 +503,17 @@ class UcxShuffleManager:
         self.engine.register_shuffle(shuffleId, p.numPartitions, p.kind, bounds,
                                      getattr(p, "ascending", True), dependency.recordBytes,
                                      _SERIALIZERS[dependency.serializer])
+        # spark.shuffle.compress (Spark's default is true) with spark.io.compression.codec lz4:
+        # applied to Kryo shuffles, whose bytes are Spark's own; the fixed codec stays raw
+        if (self.conf.get("spark.shuffle.compress", "false").lower() == "true"
+                and _SERIALIZERS[dependency.serializer] == _lib.SER_KRYO):
+            codec = self.conf.get("spark.io.compression.codec", "lz4").lower()
+            if codec not in ("lz4", "org.apache.spark.io.lz4compressioncodec"):
+                raise UnsupportedOperationException(f"compression codec {codec!r}: only lz4 is on the GPU path")
+            bs = self.conf.get("spark.io.compression.lz4.blockSize", "32k").lower()
+            block = int(bs[:-1]) * 1024 if bs.endswith("k") else int(bs)
+            self.engine.set_compression(shuffleId, "lz4", block)
+            self._compressed.add(shuffleId)
         h = BaseShuffleHandle(shuffleId, dependency)
         self._handles[shuffleId] = h
         self._maps[shuffleId] = set()
@@ -510,6 +538,7 @@ class UcxShuffleManager:
         self.ucxTransport.unregisterShuffle(shuffleId)
         del self._handles[shuffleId]
         self._maps.pop(shuffleId, None)
+        self._compressed.discard(shuffleId)
         return True
 
     def stop(self):

@@ -289,3 +289,33 @@ def test_gpu_compression_needs_kryo(engine, sgx_lib):
             engine.set_compression(951, "snappy")
     finally:
         engine.unregister_shuffle(951)
+
+
+@pytest.mark.gpu
+def test_gpu_plugin_spark_shuffle_compress(sgx_lib, oracle_lib, tmp_path):
+    """UcxShuffleManager with spark.shuffle.compress=true and the Kryo serializer: the writer's
+    lengths and the committed data file are LZ4 frames; readSerialized() returns the Kryo
+    stream of the partition range (GPU decompression); read() refuses to decode."""
+    R, n = 128, 120_000
+    mgr = sgx_lib.UcxShuffleManager(conf={"spark.shuffle.compress": "true",
+                                          "spark.io.compression.lz4.blockSize": "16k"}, localDir=str(tmp_path))
+    try:
+        h = mgr.registerShuffle(7, sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(R), serializer="kryo"))
+        recs = oracle_lib.gen_uniform16(n, 4242)
+        recs[::3, :8] = (np.arange(0, n, 3, dtype=np.int64) % 321).view(np.uint8).reshape(-1, 8)
+        w = mgr.getWriter(h, 0)
+        w.write(recs)
+        out, counts = oracle_lib.map_write(recs, R)
+        kry = oracle_lib.kryo_serialize(out)
+        ko = oracle_lib.kryo_partition_offsets(out, counts)
+        want, wlens = oracle_lib.lz4_frame_partitions(kry, ko, 16 * 1024)
+        assert np.array_equal(w.getPartitionLengths(), wlens)
+        lengths = w.getPartitionLengths().copy()
+        mgr.shuffleBlockResolver.writeIndexFileAndCommit(7, 0, lengths)
+        assert open(mgr.shuffleBlockResolver.getDataFile(7, 0), "rb").read() == want.tobytes()
+        rd = mgr.getReader(h, 10, 20)
+        assert rd.readSerialized().tobytes() == kry[ko[10]:ko[20]].tobytes()
+        with pytest.raises(sgx_lib._lib.UnsupportedOperationException):
+            rd.read()
+    finally:
+        mgr.stop()
