@@ -106,8 +106,8 @@ int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, const int64_
  * instead of the raw Kryo stream -- partition lengths, index offsets, data file, fetched and
  * exchanged blocks are then the bytes Spark writes with spark.shuffle.compress=true.  Needs
  * SGX_SER_KRYO (set first); set before the first sgx_write_map (SGX_ERR_STATE after).  The
- * engine's own decoding reads (sgx_read_records / _sorted / _grouped) return
- * SGX_ERR_UNSUPPORTED on such a shuffle: fetch the blocks and sgx_lz4_unframe them. */
+ * reduce-side reads (sgx_read_records / _sorted / _grouped) fetch the frames, decompress them
+ * on the GPU and decode the Kryo stream. */
 enum sgx_codec { SGX_CODEC_NONE = 0, SGX_CODEC_LZ4 = 1 };
 int sgx_set_compression(sgx_engine *e, int32_t shuffle_id, int32_t codec, int32_t block_size);
 /* The reduce side of the same codec (lz4-java LZ4BlockInputStream, what

@@ -459,6 +459,9 @@ static int lz4_frame_impl(sgx_engine *e, const void *stream_dev, const int64_t *
                           int32_t block_size, DevBuf *alloc_dst, void *dst_dev, int64_t dst_cap,
                           int64_t *out_lengths);
 
+static int lz4_unframe_impl(sgx_engine *e, const void *framed_dev, int64_t framed_bytes, DevBuf *alloc_dst,
+                            void *dst_dev, int64_t dst_cap, int64_t *out_bytes);
+
 static int finish_lengths(sgx_engine *e, Shuffle &s, MapOut &m) {
     if (m.ready) return SGX_OK;
     HIP_TRY(hipEventSynchronize(m.done));
@@ -1276,8 +1279,6 @@ static int records_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_
     auto it = e->shuffles.find(shuffle_id);
     if (it == e->shuffles.end()) return fail(SGX_ERR_STATE, "shuffle %d is not registered", shuffle_id);
     Shuffle &s = it->second;
-    if (s.lz4_block > 0)
-        return fail(SGX_ERR_UNSUPPORTED, "shuffle %d is LZ4-compressed: fetch its blocks and sgx_lz4_unframe them", shuffle_id);
     if (r0 < 0 || r1 > s.R || r0 > r1)
         return fail(SGX_ERR_INVALID, "partition range [%d, %d) outside [0, %d)", r0, r1, s.R);
     if (nmaps < 0 || (nmaps > 0 && !map_ids)) return fail(SGX_ERR_INVALID, "bad map list");
@@ -1299,12 +1300,26 @@ static int records_locked(sgx_engine *e, int32_t shuffle_id, const int64_t *map_
     if (s.ser == SGX_SER_KRYO) {
         // the fetched Kryo stream (blocks back to back are one valid stream) -> records
         *nrec = 0;
+        if (s.lz4_block > 0 && total > 0) {
+            // a compressed shuffle: fetch the LZ4 frames, decompress them into the Kryo input
+            // (LZ4BlockInputStream, same stream, so no host round trip between the two)
+            DevBuf comp;
+            DevBufScope gc{comp};
+            SGX_TRY(comp.ensure((size_t)total));
+            SGX_TRY(fetch_locked(e, shuffle_id, mids.data(), rids.data(), nreq, comp.p, total, SGX_MEM_DEVICE,
+                                 lens.data(), false));
+            int64_t dec = 0;
+            SGX_TRY(lz4_unframe_impl(e, comp.p, total, &e->kryo_in, nullptr, 0, &dec));
+            total = dec;
+        }
         const int64_t cap = total / 4;  // a record takes >= 4 bytes
         SGX_TRY(e->sort_buf[0].ensure((size_t)cap * 16));
         if (total == 0) return SGX_OK;
-        SGX_TRY(e->kryo_in.ensure((size_t)total + 64));
-        SGX_TRY(fetch_locked(e, shuffle_id, mids.data(), rids.data(), nreq, e->kryo_in.p, total, SGX_MEM_DEVICE,
-                             lens.data(), false));
+        if (s.lz4_block == 0) {
+            SGX_TRY(e->kryo_in.ensure((size_t)total + 64));
+            SGX_TRY(fetch_locked(e, shuffle_id, mids.data(), rids.data(), nreq, e->kryo_in.p, total, SGX_MEM_DEVICE,
+                                 lens.data(), false));
+        }
         const int64_t tiles = kryo_deser16_tiles(total);
         SGX_TRY(e->kryo_work.ensure(24 + (size_t)kryo_work_bytes(tiles)));
         HIP_TRY(hipMemsetAsync(e->kryo_work.p, 0, 24, st));  // error word, record count
@@ -1946,11 +1961,18 @@ extern "C" int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, c
 // LZ4BlockInputStream on the reduce side: decompress fetched LZ4-framed partition streams
 extern "C" int sgx_lz4_unframe(sgx_engine *e, const void *framed_dev, int64_t framed_bytes, void *dst_dev,
                                int64_t dst_cap, int64_t *out_bytes) {
+    if (!e) return fail(SGX_ERR_INVALID, "engine is NULL");
+    std::lock_guard<std::mutex> lk(e->mu);
+    return lz4_unframe_impl(e, framed_dev, framed_bytes, nullptr, dst_dev, dst_cap, out_bytes);
+}
+
+// caller holds e->mu; alloc_dst: size (decompressed + 64 B of decoder padding) and use it
+static int lz4_unframe_impl(sgx_engine *e, const void *framed_dev, int64_t framed_bytes, DevBuf *alloc_dst,
+                            void *dst_dev, int64_t dst_cap, int64_t *out_bytes) {
     if (!e || !out_bytes || framed_bytes < 0 || (framed_bytes > 0 && !framed_dev))
         return fail(SGX_ERR_INVALID, "sgx_lz4_unframe: bad arguments");
     *out_bytes = 0;
     if (framed_bytes == 0) return SGX_OK;
-    std::lock_guard<std::mutex> lk(e->mu);
     HIP_TRY(hipSetDevice(e->device));
     // one walk normally suffices: room for a frame per 512 B of input (frames of full 32 KiB
     // blocks are ~64x sparser); a denser stream (tiny partitions) is walked again with room
@@ -1967,7 +1989,7 @@ extern "C" int sgx_lz4_unframe(sgx_engine *e, const void *framed_dev, int64_t fr
                                      (int64_t *)d_info.p, e->s_comp));
         HIP_TRY(hipMemcpyAsync(info, d_info.p, 40, hipMemcpyDeviceToHost, e->s_comp));
         HIP_TRY(hipStreamSynchronize(e->s_comp));
-        if (info[2] != 0 || info[0] <= cap || !dst_dev) break;
+        if (info[2] != 0 || info[0] <= cap || (!dst_dev && !alloc_dst)) break;
         cap = info[0];
     }
     static const char *why[] = {"", "truncated header", "bad magic", "unknown compression method",
@@ -1977,6 +1999,11 @@ extern "C" int sgx_lz4_unframe(sgx_engine *e, const void *framed_dev, int64_t fr
                     (long long)info[3]);
     const int64_t nframes = info[0];
     *out_bytes = info[1];
+    if (alloc_dst) {
+        SGX_TRY(alloc_dst->ensure((size_t)info[1] + 64));
+        dst_dev = alloc_dst->p;
+        dst_cap = info[1];
+    }
     if (!dst_dev) return SGX_OK;
     if (info[1] > dst_cap)
         return fail(SGX_ERR_INVALID, "LZ4 stream decodes to %lld bytes, destination holds %lld",

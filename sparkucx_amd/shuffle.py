@@ -453,10 +453,6 @@ class UcxShuffleReader:
         * aggregator "sum" (reduceByKey(_ + _)): (keys, sums)."""
         dep = self.handle.dependency
         sid = self.handle.shuffleId
-        if self.manager.compressed(sid):
-            raise UnsupportedOperationException(
-                "this shuffle is LZ4-compressed (spark.shuffle.compress=true): readSerialized() returns its "
-                "decompressed serialized stream; record decoding of compressed shuffles is not on the GPU path yet")
         if dep.aggregator is not None:
             if dep.recordBytes != 16:
                 raise UnsupportedOperationException("aggregation needs (Long, Long) 16 B records")

@@ -271,8 +271,13 @@ def test_gpu_compressed_shuffle_publishes_lz4_frames(engine, oracle_lib, sgx_lib
         assert np.array_equal(committed, wlens)
         assert open(dat, "rb").read() == want.tobytes()
         assert open(idx, "rb").read() == oracle_lib.index_bytes(wlens)
-        with pytest.raises(sgx_lib._lib.UnsupportedOperationException):
-            engine.read_records(sid, [0], 0, R)
+        # reduce side: fetch -> LZ4 decompress -> Kryo decode, all on the GPU
+        recs_read = engine.read_records(sid, [0], 3, 40)
+        o = oracle_lib.offsets(counts)
+        assert recs_read.tobytes() == out[o[3]:o[40]].tobytes()
+        ks, ss = engine.read_grouped(sid, [0], 0, R, sgx_lib._lib.AGG_SUM)
+        wk, wsum = oracle_lib.reduce_grouped(oracle_lib.canonical_reducer_sequences([(out, counts)], R, 16), "sum")
+        assert np.array_equal(ks, wk) and np.array_equal(ss, wsum)
         with pytest.raises(sgx_lib._lib.IllegalStateException):
             engine.set_compression(sid, "none")
     finally:
@@ -295,7 +300,7 @@ def test_gpu_compression_needs_kryo(engine, sgx_lib):
 def test_gpu_plugin_spark_shuffle_compress(sgx_lib, oracle_lib, tmp_path):
     """UcxShuffleManager with spark.shuffle.compress=true and the Kryo serializer: the writer's
     lengths and the committed data file are LZ4 frames; readSerialized() returns the Kryo
-    stream of the partition range (GPU decompression); read() refuses to decode."""
+    stream of the partition range and read() its records (GPU decompression + decode)."""
     R, n = 128, 120_000
     mgr = sgx_lib.UcxShuffleManager(conf={"spark.shuffle.compress": "true",
                                           "spark.io.compression.lz4.blockSize": "16k"}, localDir=str(tmp_path))
@@ -315,7 +320,7 @@ def test_gpu_plugin_spark_shuffle_compress(sgx_lib, oracle_lib, tmp_path):
         assert open(mgr.shuffleBlockResolver.getDataFile(7, 0), "rb").read() == want.tobytes()
         rd = mgr.getReader(h, 10, 20)
         assert rd.readSerialized().tobytes() == kry[ko[10]:ko[20]].tobytes()
-        with pytest.raises(sgx_lib._lib.UnsupportedOperationException):
-            rd.read()
+        o = oracle_lib.offsets(counts)
+        assert rd.read().tobytes() == out[o[10]:o[20]].tobytes()
     finally:
         mgr.stop()
