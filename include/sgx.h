@@ -13,7 +13,11 @@
  *   - sgx_last_error() returns a thread-local message for the last failure on this thread;
  *   - buffers passed in are caller-owned; map outputs and received blocks are engine-owned
  *     and live in HBM until sgx_unregister_shuffle / sgx_destroy;
- *   - one engine per GPU (= per executor); calls on one engine are serialised internally.
+ *   - one engine per GPU (= per executor).  The engine is thread-safe: every calling thread
+ *     gets its own HIP stream and scratch buffers (the reference routes each calling thread
+ *     to its own UCX worker, shuffle/ucx/UcxShuffleTransport.scala:277-296), so concurrent
+ *     map tasks of one executor run side by side on the GPU; collectives (sgx_exchange) are
+ *     issued by one thread at a time on the engine's exchange stream.
  */
 #ifndef SGX_H
 #define SGX_H
@@ -23,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SGX_ABI_VERSION 1
+#define SGX_ABI_VERSION 2
 
 enum sgx_status {
     SGX_OK = 0,
@@ -50,17 +54,38 @@ enum sgx_mem_kind { SGX_MEM_HOST = 0, SGX_MEM_DEVICE = 1 };
 
 typedef struct sgx_engine sgx_engine;
 
+/* Kernel choices (every choice produces the same bytes; they differ in speed only). */
+enum sgx_hist_mode { SGX_HIST_ATOMIC = 0,   /* one LDS atomic per record (default)            */
+                     SGX_HIST_BALLOT = 1 }; /* wave-aggregated: peers by 64-lane ballots, the
+                                               lowest peer adds popcount(peers) (16 B hash)   */
+enum sgx_rank_mode { SGX_RANK_ORDERED = 0,  /* K4 ranks by lane-ordered LDS atomics (default) */
+                     SGX_RANK_MATCH = 1 };  /* K4 ranks by ballot peer matching               */
+enum sgx_flags {
+    SGX_FLAG_NO_WRITE_COMBINING = 1,  /* hash K4 without on-chip line write-combining      */
+    SGX_FLAG_NO_WIDE_STAGED = 2,      /* 100 B records: per-lane K4 instead of LDS-staged   */
+    SGX_FLAG_SORT_ALL_DIGITS = 4      /* sorted reads run every digit pass (no skipping)    */
+};
+
 typedef struct sgx_config {
     int32_t device;          /* HIP device ordinal for this executor                     */
     int32_t num_chunks;      /* map-side work chunks per batch (0 = one per CU)           */
     int32_t scatter_waves;   /* K4 geometry override (0 = auto): waves per workgroup       */
     int32_t scatter_items;   /* K4 geometry override (0 = auto): records per lane per tile */
+    int32_t hist_mode;       /* enum sgx_hist_mode                                         */
+    int32_t rank_mode;       /* enum sgx_rank_mode                                         */
+    int32_t flags;           /* enum sgx_flags, or-ed                                      */
+    int32_t comm_timeout_ms; /* bound on any wait for the exchange (0 = 300 s): a dead peer
+                                aborts the communicator and fails with SGX_ERR_TIMEOUT
+                                instead of spinning forever (UcxShuffleClient.scala:44-46) */
 } sgx_config;
 
 /* ---- engine lifetime: replaces CommonUcxShuffleManager.startUcxTransport
  *      (shuffle/ucx/CommonUcxShuffleManager.scala:67-100) and stop() (:111-124) ---- */
 int sgx_create(const sgx_config *cfg, sgx_engine **out);
 void sgx_destroy(sgx_engine *e);
+/* Frees the calling thread's stream and scratch buffers (an executor thread that leaves the
+ * pool); they are recreated on the thread's next call. */
+int sgx_release_thread(sgx_engine *e);
 const char *sgx_last_error(void);
 int32_t sgx_abi_version(void);
 
@@ -119,6 +144,16 @@ int sgx_set_compression(sgx_engine *e, int32_t shuffle_id, int32_t codec, int32_
  * XXH32 are checked: SGX_ERR_INVALID on a malformed or corrupt stream.  Synchronous. */
 int sgx_lz4_unframe(sgx_engine *e, const void *framed_dev, int64_t framed_bytes, void *dst_dev, int64_t dst_cap,
                     int64_t *out_bytes);
+/* dep.mapSideCombine with dep.aggregator (reduceByKey: Spark's default is mapSideCombine =
+ * true; the writer built at spark_3_0/UcxShuffleManager.scala:48-51 then runs
+ * ExternalSorter.insertAll with the aggregator, and the reader merges combiners with
+ * combineCombinersByKey, spark_3_0/UcxShuffleReader.scala:158-161).  SGX_AGG_SUM on (Long,
+ * Long) records: every map output holds one record {key, wrapping sum of the map's values of
+ * key} per distinct key, partitioned by the shuffle's partitioner, keys ascending within a
+ * partition (Spark's PartitionedAppendOnlyMap iteration order is unspecified; this is the
+ * canonical order the parity tests compare).  Set before the first write (SGX_ERR_STATE
+ * after).  sgx_read_grouped(SGX_AGG_SUM) on such a shuffle is combineCombinersByKey. */
+int sgx_set_map_side_combine(sgx_engine *e, int32_t shuffle_id, int32_t agg);
 /* unregisterShuffle: CommonUcxShuffleManager.scala:103-106 -> removeShuffle
  * (CommonUcxShuffleBlockResolver.scala:63-71). Frees the shuffle's HBM. */
 int sgx_unregister_shuffle(sgx_engine *e, int32_t shuffle_id);
@@ -133,6 +168,18 @@ int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void 
                   int64_t nrecords, int32_t record_bytes, int32_t mem_kind,
                   int64_t *out_partition_lengths);
 int sgx_map_lengths(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *out_lengths);
+/* Streaming map output: the map task's records arrive as any number of batches (Spark's
+ * writer sees unbounded partition streams and merges spills in spill order,
+ * ucx/NvkvShuffleMapOutputWriter.scala:106-113,228-246).  sgx_map_begin opens the map;
+ * every sgx_map_append partitions one batch on the GPU (K1-K4, Kryo framing) and keeps it in
+ * HBM; sgx_map_commit concatenates, per partition, the batches in append order (one gather
+ * launch) -- the result is byte-identical to sgx_write_map of all batches concatenated, then
+ * LZ4 framing / map-side combine apply as for sgx_write_map.  out_lengths as sgx_write_map
+ * (may be NULL).  Each batch holds < 2^32 records. */
+int sgx_map_begin(sgx_engine *e, int32_t shuffle_id, int64_t map_id);
+int sgx_map_append(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records, int64_t nrecords,
+                   int32_t record_bytes, int32_t mem_kind);
+int sgx_map_commit(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *out_partition_lengths);
 /* Device pointer + byte size of a map output (partition-contiguous data). */
 int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, void **out_dev_ptr,
                  int64_t *out_bytes);
@@ -166,6 +213,21 @@ int sgx_bootstrap_serve(int32_t port, int32_t nranks, const uint8_t id[128], int
 int sgx_bootstrap_join(const char *host, int32_t port, int32_t rank, int32_t timeout_ms, uint8_t out_id[128],
                        int32_t *out_nranks);
 int sgx_comm_init(sgx_engine *e, int32_t nranks, int32_t rank, const uint8_t id[128]);
+/* Host collective backend (the fake exchange backend of SURVEY §4, and the path for ranks
+ * that share one GPU, which RCCL refuses): the exchange runs exactly as over RCCL -- counts
+ * all-gather, sgx_plan_exchange, all-to-all of the partition-contiguous map output into the
+ * [source][my reducers] receive layout, block fetches from HBM -- but the two collectives are
+ * the caller's functions over host memory (the map output is staged device -> host and the
+ * received bytes host -> device).  Return 0 on success; anything else fails the exchange with
+ * SGX_ERR_COMM.  allgather: every rank contributes `bytes` bytes, recv receives nranks * bytes,
+ * rank-major.  alltoallv: byte counts / displacements, as ncclAllToAllv. */
+typedef struct sgx_host_comm {
+    void *user;
+    int (*allgather)(void *user, const void *send, int64_t bytes, void *recv);
+    int (*alltoallv)(void *user, const void *send, const int64_t *send_counts, const int64_t *send_displs,
+                     void *recv, const int64_t *recv_counts, const int64_t *recv_displs);
+} sgx_host_comm;
+int sgx_comm_init_host(sgx_engine *e, int32_t nranks, int32_t rank, const sgx_host_comm *comm);
 int sgx_comm_size(sgx_engine *e, int32_t *nranks, int32_t *rank);
 /* Push map `map_id` of `shuffle_id` to the reducer owners (reducer r lives on rank
  * floor(r*P/R)); every rank calls it collectively with its own map.  Asynchronous on the
@@ -255,9 +317,10 @@ int sgx_range_bounds(sgx_engine *e, const void *const *batches, const int64_t *n
 enum sgx_stage { SGX_STAGE_HIST = 0, SGX_STAGE_SCAN = 1, SGX_STAGE_SCATTER = 2,
                  SGX_STAGE_ALLGATHER = 3, SGX_STAGE_ALLTOALL = 4, SGX_STAGE_REGROUP = 5,
                  SGX_STAGE_SORT = 6, SGX_STAGE_GROUP = 7, SGX_STAGE_SERIALIZE = 8,
-                 SGX_STAGE_DESERIALIZE = 9, SGX_NUM_STAGES = 10 };
+                 SGX_STAGE_DESERIALIZE = 9, SGX_STAGE_COMBINE = 10, SGX_NUM_STAGES = 11 };
 /* SGX_STAGE_SORT times sgx_read_sorted's radix + partitioner passes (the fetch gather is
  * REGROUP), SGX_STAGE_GROUP the grouping / summing kernels of sgx_read_grouped,
+ * SGX_STAGE_COMBINE the map-side combine of sgx_write_map (sort + sum + repartition),
  * SGX_STAGE_SERIALIZE the Kryo framing kernel of sgx_write_map (SGX_SER_KRYO),
  * SGX_STAGE_DESERIALIZE the Kryo decoder of the reduce-side reads. */
 int sgx_stats_reset(sgx_engine *e);

@@ -231,6 +231,34 @@ def reduce_grouped(seqs, agg: str = "group"):
     return cat(keys_l), cat(starts_l), cat(vals_l)
 
 
+def map_combine_sum(records: np.ndarray, num_partitions: int, kind: int = PART_HASH, bounds=None,
+                    ascending: bool = True):
+    """Map-side combine of reduceByKey(_ + _) on (Long, Long) records (Spark 3.0.1: the writer
+    built at UcxShuffleManager.scala:48-51 runs ExternalSorter.insertAll with the aggregator
+    -- PartitionedAppendOnlyMap, createCombiner(v) = v, mergeValue(c, v) = c + v with Long
+    wrap-around -- and writes one (key, combiner) pair per distinct key and partition).
+    Spark iterates a partition's combiners in hash-map order (unspecified); the canonical
+    order here is ascending key.  Returns (records (G, 16) partition-contiguous, counts[R]).
+    Restated again in pure Python by spark_semantics.map_side_combine_sum."""
+    records = np.ascontiguousarray(records)
+    R = num_partitions
+    if len(records) == 0:
+        return np.empty((0, 16), np.uint8), np.zeros(R, np.int64)
+    pids = partition_ids(records, R, kind, bounds, ascending).astype(np.int64)
+    k = records[:, :8].copy().view("<i8").reshape(-1)
+    v = records[:, 8:16].copy().view("<u8").reshape(-1)
+    order = np.lexsort((k, pids))
+    ks, ps, vs = k[order], pids[order], v[order]
+    first = np.ones(len(ks), dtype=bool)
+    first[1:] = (ks[1:] != ks[:-1]) | (ps[1:] != ps[:-1])
+    st = np.nonzero(first)[0]
+    out = np.empty((len(st), 16), np.uint8)
+    out[:, :8] = ks[st].view(np.uint8).reshape(-1, 8)
+    out[:, 8:] = np.add.reduceat(vs, st).view(np.uint8).reshape(-1, 8)  # uint64 adds wrap
+    counts = np.bincount(ps[st], minlength=R).astype(np.int64)
+    return out, counts
+
+
 def kryo_record_lengths(records: np.ndarray) -> np.ndarray:
     """Bytes of each (Long, Long) record in Spark's Kryo stream (spark_semantics.kryo_*)."""
     kv = np.ascontiguousarray(records).view(np.uint64).reshape(-1, 2)

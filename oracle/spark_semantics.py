@@ -497,3 +497,20 @@ def kryo_deserialize_pairs(buf: bytes) -> List[Tuple[int, int]]:
             pair.append(x)
         out.append((pair[0], pair[1]))
     return out
+
+
+# ---------------------------------------------------------------------------------------
+# Map-side combine (dep.mapSideCombine = true, reduceByKey's default).  Spark 3.0.1
+# SortShuffleWriter -> ExternalSorter(aggregator = Some(agg)).insertAll: every record goes
+# through PartitionedAppendOnlyMap.changeValue((getPartition(k), k), update) with
+# update(hadValue, old) = hadValue ? mergeValue(old, v) : createCombiner(v); for
+# reduceByKey(_ + _) on Longs createCombiner = identity, mergeValue = + (two's-complement
+# wrap).  writePartitionedMapOutput then emits each partition's (k, combiner) pairs; the
+# within-partition iteration order of the hash map is unspecified -- canonical: ascending key.
+# ---------------------------------------------------------------------------------------
+def map_side_combine_sum(records: Sequence[Tuple[int, int]], num_partitions: int):
+    combiners = {}
+    for k, v in records:
+        key = (hash_partition(k, num_partitions), k)
+        combiners[key] = to_i64(combiners[key] + v) if key in combiners else to_i64(v)
+    return [(k, c) for (_, k), c in sorted(combiners.items())]

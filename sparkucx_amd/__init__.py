@@ -6,8 +6,9 @@ RCCL all-to-all exchange, regroup) runs in the in-tree HIP library ``libsgx.so``
 CPU fallback and raises if the library is missing.
 """
 from ._lib import (  # noqa: F401
-    AGG_GROUP, AGG_SUM, MEM_DEVICE, MEM_HOST, PART_HASH, PART_RANGE_BYTES10, PART_RANGE_I64, SER_FIXED, SER_KRYO,
-    STAGES,
+    AGG_GROUP, AGG_SUM, FLAG_NO_WIDE_STAGED, FLAG_NO_WRITE_COMBINING, FLAG_SORT_ALL_DIGITS, HIST_ATOMIC,
+    HIST_BALLOT, MEM_DEVICE, MEM_HOST, PART_HASH, PART_RANGE_BYTES10, PART_RANGE_I64, RANK_MATCH, RANK_ORDERED,
+    SER_FIXED, SER_KRYO, STAGES,
     BlockNotFoundException, DeviceError, IllegalArgumentException, IllegalStateException,
     ShuffleError, ShuffleIOException, TransportError, UnsupportedOperationException, lib,
 )
@@ -18,7 +19,7 @@ from .shuffle import (  # noqa: F401
     Aggregator, BaseShuffleHandle, GpuShuffleMapOutputWriter, GpuShuffleTransport, GpuShuffleWriter,
     HashPartitioner, MapStatus, MemoryBlock, OperationResult, OperationStatus, RangePartitioner,
     ShuffleDependency, UcxShuffleBlockId, UcxShuffleBlockResolver, UcxShuffleManager,
-    UcxShuffleReader, parse_block_id,
+    UcxShuffleReader, byte_string, parse_block_id,
 )
 
 __all__ = [n for n in dir() if not n.startswith("_")]

@@ -23,7 +23,11 @@ MEM_HOST, MEM_DEVICE = 0, 1
 AGG_GROUP, AGG_SUM = 0, 1
 SER_FIXED, SER_KRYO = 0, 1
 STAGES = ("hist", "scan", "scatter", "allgather", "alltoall", "regroup", "sort", "group", "serialize",
-          "deserialize")
+          "deserialize", "combine")
+HIST_ATOMIC, HIST_BALLOT = 0, 1
+RANK_ORDERED, RANK_MATCH = 0, 1
+FLAG_NO_WRITE_COMBINING, FLAG_NO_WIDE_STAGED, FLAG_SORT_ALL_DIGITS = 1, 2, 4
+ABI_VERSION = 2
 
 
 class ShuffleError(RuntimeError):
@@ -82,6 +86,12 @@ _P64, _P32 = ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int32)
 SIGNATURES = {
     "sgx_create": (ctypes.c_int, [_vp, ctypes.POINTER(_vp)]),
     "sgx_destroy": (None, [_vp]),
+    "sgx_release_thread": (ctypes.c_int, [_vp]),
+    "sgx_set_map_side_combine": (ctypes.c_int, [_vp, _i32, _i32]),
+    "sgx_map_begin": (ctypes.c_int, [_vp, _i32, _i64]),
+    "sgx_map_append": (ctypes.c_int, [_vp, _i32, _i64, _vp, _i64, _i32, _i32]),
+    "sgx_map_commit": (ctypes.c_int, [_vp, _i32, _i64, _vp]),
+    "sgx_comm_init_host": (ctypes.c_int, [_vp, _i32, _i32, _vp]),
     "sgx_last_error": (_cp, []),
     "sgx_abi_version": (_i32, []),
     "sgx_register_shuffle": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _i64, _i32, _i32]),
@@ -135,12 +145,24 @@ def lib() -> ctypes.CDLL:
                     "(python -c 'import __graft_entry__ as g; g.build()'); "
                     "sparkucx_amd has no CPU fallback")
             L = ctypes.CDLL(LIB_PATH)
+            L.sgx_abi_version.restype = _i32
+            if L.sgx_abi_version() != ABI_VERSION:
+                raise ImportError(f"{LIB_PATH} has ABI {L.sgx_abi_version()}, the bindings expect {ABI_VERSION}: rebuild")
             for name, (res, args) in SIGNATURES.items():
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args
             _lib = L
     return _lib
+
+
+# sgx_host_comm (include/sgx.h): the caller's collectives of the host exchange backend
+ALLGATHER_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, _vp, _i64, _vp)
+ALLTOALLV_FN = ctypes.CFUNCTYPE(ctypes.c_int, _vp, _vp, _P64, _P64, _vp, _P64, _P64)
+
+
+class HostCommStruct(ctypes.Structure):
+    _fields_ = [("user", _vp), ("allgather", ALLGATHER_FN), ("alltoallv", ALLTOALLV_FN)]
 
 
 def last_error() -> str:

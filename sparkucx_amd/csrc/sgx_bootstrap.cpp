@@ -20,13 +20,16 @@
 #include <unistd.h>
 
 #include <cerrno>
+#include <cstdio>
 #include <chrono>
 #include <cstring>
 #include <thread>
 #include <vector>
 
 #include "../../include/sgx.h"
-#include "sgx_internal.h"
+#include "sgx_host.h"
+
+#include <algorithm>
 
 namespace {
 

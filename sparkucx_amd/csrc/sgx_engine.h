@@ -1,0 +1,314 @@
+// sgx_engine.h — the engine's internal state, shared by the C-ABI translation units
+// (sgx_engine.cpp, sgx_map.cpp, sgx_exchange.cpp, sgx_read.cpp, sgx_lz4_host.cpp,
+// sgx_range.cpp).  Not part of the public ABI (include/sgx.h).
+//
+// Threading model (SURVEY §8(b) "Threading"; the reference routes each calling thread to its
+// own UCX worker, UcxShuffleTransport.scala:277-296): every calling thread gets its own
+// context -- a HIP stream plus private scratch buffers -- so concurrent map tasks of one
+// executor run their kernels side by side on the GPU and never share a work buffer.  Shared
+// state is guarded by short-lived locks, never held across a device wait of another thread:
+//   reg_mu     the shuffle registry and the context table
+//   Shuffle::mu   a shuffle's map / round containers
+//   MapOut::mu    one map output (its writer, its lengths)
+//   comm_mu    the exchange: collectives are issued by one thread at a time, in call order,
+//              on the engine's exchange stream (RCCL needs the same order on every rank)
+//   stats_mu   stage timing events
+// Lock order: reg_mu -> Shuffle::mu -> MapOut::mu; comm_mu before Shuffle::mu.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <map>
+#include <memory>
+#include <mutex>
+#include <string>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/sgx.h"
+#include "sgx_internal.h"
+
+namespace sgx {
+
+#define HIP_TRY(expr)                                                                          \
+    do {                                                                                       \
+        hipError_t _e = (expr);                                                                \
+        if (_e != hipSuccess)                                                                  \
+            return ::sgx::fail_msg(SGX_ERR_HIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), \
+                                   __FILE__, __LINE__);                                        \
+    } while (0)
+#define NCCL_TRY(expr)                                                                         \
+    do {                                                                                       \
+        ncclResult_t _r = (expr);                                                              \
+        if (_r != ncclSuccess)                                                                 \
+            return ::sgx::fail_msg(SGX_ERR_COMM, "%s failed: %s", #expr, ncclGetErrorString(_r)); \
+    } while (0)
+#define SGX_TRY(expr)                                                                          \
+    do {                                                                                       \
+        int _c = (expr);                                                                       \
+        if (_c != SGX_OK) return _c;                                                           \
+    } while (0)
+
+// ------------------------------------------------------------------------------------
+// buffers
+// ------------------------------------------------------------------------------------
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    DevBuf() = default;
+    DevBuf(const DevBuf &) = delete;
+    DevBuf &operator=(const DevBuf &) = delete;
+    ~DevBuf() { release(); }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    // grow-only: keeps the allocation when it is large enough
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return SGX_OK;
+        release();
+        size_t want = bytes ? bytes : 16;
+        hipError_t e = hipMalloc(&p, want);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail_msg(SGX_ERR_NOMEM, "hipMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+        }
+        cap = want;
+        return SGX_OK;
+    }
+    void swap(DevBuf &o) {
+        std::swap(p, o.p);
+        std::swap(cap, o.cap);
+    }
+};
+
+struct HostPinned {
+    void *p = nullptr;
+    size_t cap = 0;
+    HostPinned() = default;
+    HostPinned(const HostPinned &) = delete;
+    HostPinned &operator=(const HostPinned &) = delete;
+    ~HostPinned() { release(); }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    int ensure(size_t bytes) {
+        if (bytes <= cap && p) return SGX_OK;
+        release();
+        size_t want = bytes ? bytes : 16;
+        hipError_t e = hipHostMalloc(&p, want, hipHostMallocDefault);
+        if (e != hipSuccess) {
+            p = nullptr;
+            return fail_msg(SGX_ERR_NOMEM, "hipHostMalloc(%zu) failed: %s", want, hipGetErrorString(e));
+        }
+        cap = want;
+        return SGX_OK;
+    }
+};
+
+struct Event {  // a lazily created, timing-disabled event
+    hipEvent_t ev = nullptr;
+    Event() = default;
+    Event(const Event &) = delete;
+    Event &operator=(const Event &) = delete;
+    ~Event() {
+        if (ev) (void)hipEventDestroy(ev);
+    }
+    hipError_t record(hipStream_t st) {
+        if (!ev) {
+            hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+            if (e != hipSuccess) return e;
+        }
+        return hipEventRecord(ev, st);
+    }
+    hipError_t wait_host() const { return ev ? hipEventSynchronize(ev) : hipSuccess; }
+};
+
+// ------------------------------------------------------------------------------------
+// registry
+// ------------------------------------------------------------------------------------
+// One partition-contiguous batch of records of a streaming map output (a "spill": the
+// reference's writer receives unbounded partition streams, NvkvShuffleMapOutputWriter.scala:
+// 106-113, 228-246; Spark merges spills in spill order).
+struct Spill {
+    DevBuf data;                   // published bytes of this batch, partition-contiguous
+    std::vector<int64_t> lengths;  // [R] published bytes per partition
+    int64_t nrec = 0;
+};
+
+struct MapOut {
+    std::mutex mu;             // serialises the writer(s) and the length finisher of this map
+    bool written = false;      // a write was enqueued successfully
+    DevBuf data;               // partition-contiguous records (engine-owned HBM)
+    int64_t nrec = 0;
+    HostPinned part_off;       // (R+1) u32 record offsets + 1 u32 error word, landed async
+    std::vector<int64_t> lengths;  // published bytes per partition (valid once `ready`)
+    bool ready = false;
+    Event done;                // recorded on the writer's stream after the last producer kernel
+    Event read_done;           // recorded on the exchange stream after an all-to-all read it
+    // serializer KRYO: the published bytes are the Kryo stream of the records
+    DevBuf ser;                // Kryo-framed partition-contiguous bytes (capacity 20 n + 16)
+    DevBuf ser_work;           // device (R+1) i64 byte offsets | tile prefixes | tile sums
+    HostPinned ser_off;        // (R+1) i64 byte offsets, landed async
+    int64_t out_bytes = 0;     // published bytes
+    DevBuf comp;               // LZ4-framed partition streams (sgx_set_compression), once `ready`
+    bool comp_valid = false;   // `comp` holds this write's frames (false until finish_lengths)
+    // streaming writes (sgx_map_begin / _append / _commit): the batches so far
+    bool open = false;
+    std::vector<std::unique_ptr<Spill>> spills;
+    const void *view() const { return comp_valid ? comp.p : (ser.p && ser_valid ? ser.p : data.p); }
+    bool ser_valid = false;    // `ser` holds this write's Kryo stream
+    ~MapOut() {
+        (void)read_done.wait_host();  // an all-to-all may still read `data`
+        (void)done.wait_host();
+    }
+};
+
+// One exchange round: every rank pushed one map; this rank holds its reducers' blocks.
+// The receive buffer keeps ncclAllToAllv's layout, [source rank][my reducers]: every
+// (map, reducer) block is contiguous in it, so blocks are served from it directly and the
+// per-reducer canonical order (reducer, then source map) is produced by the fetch that
+// asks for it (one gather launch), not by an extra pass over every received byte.
+struct Round {
+    std::vector<int64_t> map_ids;        // [P] the map pushed by each source rank
+    std::vector<int64_t> lens;           // [P][R] bytes
+    std::vector<int64_t> block_off;      // [P][nmine] byte offset in `data`
+    int32_t r0 = 0, r1 = 0;              // my reducers [r0, r1)
+    DevBuf data;                          // receive buffer, [source][my reducers]
+    std::shared_ptr<MapOut> alias;        // P == 1 without a communicator: the map output itself
+    Event done;
+    const void *base() const { return alias ? alias->view() : data.p; }
+    ~Round() { (void)done.wait_host(); }
+};
+
+struct Shuffle {
+    std::mutex mu;                // maps / rounds containers
+    int32_t id = 0;
+    int32_t R = 0, kind = 0, nb = 0, asc = 1, rb = 16;
+    int32_t ser = SGX_SER_FIXED;  // dep.serializer (sgx_set_serializer)
+    int32_t lz4_block = 0;        // spark.shuffle.compress with lz4 (sgx_set_compression): block size
+    int32_t combine = -1;         // map-side combine aggregation (sgx_set_map_side_combine), -1 = none
+    DevBuf bounds;
+    PartParams pp{};
+    std::map<int64_t, std::shared_ptr<MapOut>> maps;
+    std::vector<std::shared_ptr<Round>> rounds;
+    bool configurable() {  // serializer / codec / combine may change until the first write
+        std::lock_guard<std::mutex> lk(mu);
+        return maps.empty();
+    }
+};
+
+// ------------------------------------------------------------------------------------
+// per-thread context: a HIP stream and private scratch
+// ------------------------------------------------------------------------------------
+struct Ctx {
+    hipStream_t st = nullptr;
+    // map side: [counts][ticket | look-back status][partition offsets | error] + offs[R][G]
+    DevBuf offs, work;
+    DevBuf input_stage;
+    const uint32_t *last_off_dev = nullptr;  // device (R+1) record offsets of the last partition pass
+    // reduce side and map-side combine
+    DevBuf kryo_in, kryo_work, sort_buf[2], sort_err, grp_flags, grp_offs, grp_status, grp_out, grp_prefix;
+    DevBuf digit_hist, items_dev, gather_stage, fetch_tmp, comb_buf;
+    HostPinned gather_items;
+    // LZ4 framing / unframing scratch (grow-only)
+    DevBuf lz4_blocks, lz4_slots, lz4_sizes, lz4_offs, lz4_info, lz4_desc;
+    // RangePartitioner.sketch
+    DevBuf sample_winner, sample_keys, cdf;
+    ~Ctx() {
+        if (st) {
+            (void)hipStreamSynchronize(st);
+            (void)hipStreamDestroy(st);
+        }
+    }
+};
+
+struct PendingStage {
+    int stage;
+    hipEvent_t a, b;
+};
+
+}  // namespace sgx
+
+struct sgx_engine {
+    int device = 0;
+    int num_cus = 256;
+    int G = 256;
+    bool G_forced = false;
+    int sc_waves = 0, sc_items = 0;  // K4 geometry override (sgx_config)
+    int hist_mode = 0;               // sgx_config.hist_mode
+    int rank_mode = 0;               // sgx_config.rank_mode
+    int flags = 0;                   // sgx_config.flags
+    int64_t comm_timeout_ms = 300000;
+
+    std::mutex reg_mu;
+    std::map<int32_t, std::shared_ptr<sgx::Shuffle>> shuffles;
+    std::unordered_map<std::thread::id, std::unique_ptr<sgx::Ctx>> ctxs;
+
+    // exchange
+    std::mutex comm_mu;
+    hipStream_t s_comm = nullptr;
+    ncclComm_t comm = nullptr;
+    bool host_comm = false;
+    sgx_host_comm hc{};
+    bool comm_broken = false;
+    int32_t nranks = 1, rank = 0;
+    sgx::DevBuf ag_send, ag_recv;
+    sgx::HostPinned ag_host, x_send, x_recv;
+    sgx::DevBuf jump_dev;  // XORShiftRandom jump table (built once, read-only after)
+    std::mutex jump_mu;
+
+    // stats
+    std::mutex stats_mu;
+    std::vector<hipEvent_t> ev_free;
+    std::vector<sgx::PendingStage> pending;
+    double stage_ms[SGX_NUM_STAGES] = {0};
+    int64_t stage_n[SGX_NUM_STAGES] = {0};
+
+    // the calling thread's context (created on first use); nullptr + last_error on failure
+    sgx::Ctx *ctx();
+    hipEvent_t ev();
+    void record_stage(int stage, hipEvent_t a, hipEvent_t b);
+    void release_events(std::initializer_list<hipEvent_t> evs);
+    void resolve_stats();
+    std::shared_ptr<sgx::Shuffle> find_shuffle(int32_t shuffle_id);
+};
+
+namespace sgx {
+
+// ---- shared internals (defined across the engine's translation units) ----
+PartParams make_part_params(const Shuffle &s);
+// One stable partition pass (K1+K2 hist -> K3 scan -> K4 scatter) on the context's stream.
+int partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_t n, int rb, const PartParams &spp,
+                   int32_t R, int32_t kind, uint32_t *host_off, uint32_t *err_slot, bool stats);
+// Lengths / published bytes of a written map (waits for its kernels).  Caller holds m.mu.
+int finish_lengths(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m);
+// Look up a map output (shared pointer: stays alive while used).
+int find_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, std::shared_ptr<Shuffle> *ps,
+             std::shared_ptr<MapOut> *pm);
+// Gather blocks into dst (request order) on the context's stream; see sgx_read.cpp.  `keep`
+// receives references to every source so it outlives an asynchronous gather.
+int fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, const int32_t *reduce_ids, int64_t n,
+               void *dst, int64_t dst_cap, int32_t dst_mem_kind, int64_t *out_lengths, bool sync,
+               std::vector<std::shared_ptr<void>> *keep);
+// Group n key-sorted (Long, Long) records (device) by key, synchronously: *ngroups, and
+// device arrays in the context's grp_out: keys[G], starts[G] (may be NULL), vals[G] sums
+// (SGX_AGG_SUM) or vals[n] every value (SGX_AGG_GROUP).
+int group_records(sgx_engine *e, Ctx &c, const void *sorted, int64_t n, int32_t agg, int64_t *ngroups,
+                  int64_t **keys, int64_t **starts, int64_t **vals);
+// Stable sort of n 16 B / 100 B records in c.sort_buf[0] by key, then by the shuffle's
+// partitioner (when `by_partition`): *sorted = the buffer holding the result.
+int sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool by_partition, const void **sorted);
+// LZ4 framing / unframing on the context's stream (sgx_lz4_host.cpp).
+int lz4_frame_impl(sgx_engine *e, Ctx &c, const void *stream_dev, const int64_t *part_offsets, int32_t R,
+                   int32_t block_size, DevBuf *alloc_dst, void *dst_dev, int64_t dst_cap, int64_t *out_lengths);
+int lz4_unframe_impl(sgx_engine *e, Ctx &c, const void *framed_dev, int64_t framed_bytes, DevBuf *alloc_dst,
+                     void *dst_dev, int64_t dst_cap, int64_t *out_bytes);
+// Wait for the exchange stream with RCCL async-error polling and the engine's timeout.
+int comm_wait(sgx_engine *e);
+
+}  // namespace sgx

@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "sgx_host.h"
+
 namespace sgx {
 
 // Partitioner description as seen by the kernels (built by the engine from the shuffle's
@@ -21,12 +23,7 @@ struct PartParams {
     const void *bounds;  // device: int64[nb] (RANGE_I64) or Key10[nb] (RANGE_BYTES10)
     uint32_t dshift;     // KIND_DIGIT: bit offset of the digit in the record's first 12 bytes (LE)
     uint32_t dflip;      // KIND_DIGIT: XORed into the digit (0x80 = sign flip of an i64 key's top byte)
-    void *junk;          // device: JUNK_BYTES_PER_WG per scatter workgroup, write-only target of
-                         // the masked-off lanes of branch-free stores (never read)
 };
-constexpr size_t JUNK_BYTES_PER_WG = 64 * 16;
-// Sets the thread-local sgx_last_error() message and returns `code` (host code only).
-int fail_msg(int code, const char *fmt, ...) __attribute__((format(printf, 2, 3)));
 // Internal partition kind of the reduce side's LSD radix passes: pid = 8-bit digit of the
 // key (R = 256), see PartParams::dshift / dflip.  Never registered through the C ABI.
 constexpr int KIND_DIGIT = 200;
@@ -56,14 +53,8 @@ struct ScatterGeom {
     int tile;   // waves * items * 64
     size_t lds_bytes;
     int mbits;  // LDS peer-table width (0 = ballots only)
-    int nt = 0; // A/B: bit0 nontemporal loads, bit1 nontemporal stores (8x16 staged only)
 };
 ScatterGeom scatter_geom16(uint32_t R, int force_waves = 0, int force_items = 0);
-// The LDS-DMA pipelined hash kernel (waves == DMA_GEOM_TAG); items == 0 if R does not fit.
-constexpr int DMA_GEOM_TAG = -1;
-ScatterGeom scatter_geom16_dma(uint32_t R);
-// Direct-store kernel (waves == DIRECT_GEOM_BASE + real waves).
-constexpr int DIRECT_GEOM_BASE = 1000;
 // Lane-ordered-ranking staged kernel (waves == ORD_GEOM_BASE + real waves, mbits == PP).
 constexpr int ORD_GEOM_BASE = 2000;
 ScatterGeom scatter_geom16_ord(uint32_t R, int force_waves = 0, int force_items = 0);
@@ -71,8 +62,6 @@ ScatterGeom scatter_geom16_ord(uint32_t R, int force_waves = 0, int force_items 
 // per lane, mbits == stage slots per lane).
 constexpr int WC_GEOM_BASE = 3000;
 ScatterGeom scatter_geom16_wc(uint32_t R);
-inline bool is_direct_geom(int waves) { return waves >= DIRECT_GEOM_BASE && waves < ORD_GEOM_BASE; }
-ScatterGeom scatter_geom16_direct(uint32_t R, int waves, int items);
 __host__ __device__ size_t scatter16_lds(uint32_t R, int waves, int items, int mbits);
 ScatterGeom scatter_geom_wide(uint32_t R, int record_bytes);
 // Wide-record staged kernel (100 B TeraSort records; waves == WIDE2_GEOM_TAG), items == 0
@@ -81,7 +70,10 @@ constexpr int WIDE2_GEOM_TAG = -2;
 ScatterGeom scatter_geom_wide2(uint32_t R, int record_bytes, int kind, int nb);
 
 // Launchers (all asynchronous on `stream`).  counts / offs are [R][G] partition-major.
-// counts: [R][G] u32, zeroed here unless `zeroed` (the caller's memset covered them)
+// counts: [R][G] u32, zeroed here unless `zeroed` (the caller's memset covered them).
+// mode: HIST_ATOMIC (one LDS atomic per record) or HIST_BALLOT (wave-aggregated: one
+// atomic per distinct partition id of a wave, peers found by ballots; 16 B hash only).
+constexpr int HIST_ATOMIC = 0, HIST_BALLOT = 1;
 hipError_t launch_hist(const void *in, int64_t n, int record_bytes, int64_t chunk, int G,
                        const PartParams &pp, uint32_t *counts, hipStream_t stream, int mode = 0,
                        bool zeroed = false);
@@ -93,16 +85,6 @@ int64_t scan_tiles(int64_t len);
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes, int64_t chunk,
                           int G, const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
                           uint32_t *err, hipStream_t stream);
-// Measurement-only ablations of the 8x16 hash scatter (SGX_SCATTER_DIAG=1..5; wrong output).
-hipError_t launch_scatter_diag(int mode, const void *in, void *out, int64_t n, int64_t chunk, int G,
-                               const PartParams &pp, const uint32_t *offs, uint32_t *err,
-                               hipStream_t stream);
-// K4 chained variant (tiles in ticket order, per-partition look-back); base = K3's
-// partition offsets; status: [ceil(n/tile)][R] u32 and ticket zeroed by the caller.
-hipError_t launch_scatter_chain(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *base,
-                                uint32_t *status, uint32_t *ticket, uint32_t *err, int waves, int items,
-                                int grid, hipStream_t stream);
-__host__ __device__ size_t scatter16_chain_lds(uint32_t R, int waves, int items, int mbits);
 // items: [n][3] int64 {src_off, dst_off, bytes}; all offsets/bytes multiples of `align`.
 // LZ4BlockOutputStream framing (sgx_lz4.hip)
 int lz4_lanes_per_workgroup();
@@ -128,6 +110,8 @@ hipError_t launch_group_emit(const void *rec, int64_t n, const uint32_t *flags, 
 int64_t prefix64_blocks(int64_t n);
 hipError_t launch_group_sums(const void *rec, int64_t n, const int64_t *starts, int64_t ngroups,
                              uint64_t *bsum, uint64_t *P, int64_t *sums, hipStream_t st);
+// keys[i], vals[i] -> 16 B records {key, value} (map-side combine output)
+hipError_t launch_pack_pairs(const int64_t *keys, const int64_t *vals, int64_t n, void *out, hipStream_t st);
 // RangePartitioner.sketch (sgx_sample.hip): reservoir of k keys of n records, XORShiftRandom
 // state s0 (already hashSeed'ed), jump = [48][64] column-form powers M^(2^t) of one step.
 int64_t reservoir_threads(int64_t n, int64_t k);

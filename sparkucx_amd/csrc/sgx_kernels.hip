@@ -187,9 +187,10 @@ constexpr int HIST_UNROLL = 8;
 // the 256 MiB Infinity Cache when K4 starts -- are the chunk heads K4 reads first.
 constexpr int HIST_SPLIT = 4;
 
-// AGG (A/B, SGX_HIST_VARIANT=7): wave-aggregated counting -- each lane's peers (same
-// partition id) from one ballot per id bit, and only the lowest peer adds popcount(peers).
-// Measured against plain LDS atomics on uniform and Zipf(1.1) keys.
+// AGG (sgx_config.hist_mode = SGX_HIST_BALLOT): wave-aggregated counting -- each lane's
+// peers (same partition id) from one ballot per id bit, and only the lowest peer adds
+// popcount(peers).  Measured against plain LDS atomics on uniform and Zipf(1.1) keys
+// (DESIGN.md §4): plain atomics are the default.
 template <int KIND, bool REC16, int UNROLL, int SPLIT, bool AGG = false>
 __device__ __forceinline__ void hist_body(const char *__restrict__ in, int64_t n, int rb, int64_t chunk,
                                           const PartParams &pp, uint32_t *__restrict__ counts, int G) {
@@ -248,32 +249,6 @@ __global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ 
     hist_body<KIND, REC16, HIST_UNROLL, HIST_SPLIT, AGG>(in, n, rb, chunk, pp, counts, G);
 }
 
-// Lean histogram for the pipelined map side (SGX_PIPELINE, opt-in): one wave per SIMD and
-// at most 32 VGPRs, so a workgroup fits beside a write-combining K4 workgroup (2 waves x 240
-// VGPRs per SIMD, 156 KB of LDS) and the next map's histogram streams while the CU sorts.
-// Measured (C1): the overlap happens but the two kernels share one HBM budget -- K4 slows
-// from 1.88 to 2.24-2.37 ms, and the next K4 waits for CUs the histogram holds -- so the
-// pipelined step is 2.71-2.80 ms against 2.63-2.68 serial.  With one workgroup per chunk
-// (fewer waves) the histogram crawls (3.1 ms) and the step is 4.1 ms.
-constexpr int HIST_LEAN_THREADS = 256;
-
-// A/B geometries of the histogram (SGX_HIST_VARIANT, hash partitioners on 16 B records):
-// (unroll, split, threads): 2 = (4, 4, 1024), 3 = (8, 2, 1024), 4 = (8, 8, 1024),
-// 5 = (8, 4, 1024), 6 = (16, 2, 1024).  Measured before: (16, 4, 512) 0.84 ms, (8, 2, 512)
-// 0.77, (8, 8, 512) 0.75, (8, 8, 256) 0.76 against the default (8, 4, 512) 0.733.
-template <int KIND, int UNROLL, int SPLIT, int THREADS>
-__global__ __launch_bounds__(THREADS) void k_hist_var(const char *__restrict__ in, int64_t n, int rb,
-                                                      int64_t chunk, PartParams pp,
-                                                      uint32_t *__restrict__ counts, int G) {
-    hist_body<KIND, true, UNROLL, SPLIT>(in, n, rb, chunk, pp, counts, G);
-}
-template <int KIND, bool REC16>
-__global__ __launch_bounds__(HIST_LEAN_THREADS) __attribute__((amdgpu_num_vgpr(32))) void k_hist_lean(
-    const char *__restrict__ in, int64_t n, int rb, int64_t chunk, PartParams pp,
-    uint32_t *__restrict__ counts, int G) {
-    hist_body<KIND, REC16, 4, HIST_SPLIT>(in, n, rb, chunk, pp, counts, G);
-}
-
 hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
                        const PartParams &pp, uint32_t *counts, hipStream_t stream, int mode, bool zeroed) {
     const size_t lds = (size_t)pp.R * 4;
@@ -283,43 +258,17 @@ hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
         if (ze != hipSuccess) return ze;
     }
     const bool r16 = (rb == 16);
-    const bool lean = mode == 1;
-    if (mode == 7 && r16 && pp.kind == SGX_PART_HASH) {  // A/B: wave-aggregated counting
+    const dim3 grid(G * HIST_SPLIT), block(HIST_THREADS);
+    if (mode == HIST_BALLOT && r16 && pp.kind == SGX_PART_HASH) {  // wave-aggregated counting
         if ((pp.R & (pp.R - 1)) == 0)
-            hipLaunchKernelGGL((k_hist<KIND_HASH_POW2, true, true>), dim3(G * HIST_SPLIT), dim3(HIST_THREADS), lds,
-                               stream, p, n, rb, chunk, pp, counts, G);
+            hipLaunchKernelGGL((k_hist<KIND_HASH_POW2, true, true>), grid, block, lds, stream, p, n, rb, chunk, pp,
+                               counts, G);
         else
-            hipLaunchKernelGGL((k_hist<SGX_PART_HASH, true, true>), dim3(G * HIST_SPLIT), dim3(HIST_THREADS), lds,
-                               stream, p, n, rb, chunk, pp, counts, G);
+            hipLaunchKernelGGL((k_hist<SGX_PART_HASH, true, true>), grid, block, lds, stream, p, n, rb, chunk, pp,
+                               counts, G);
         return hipGetLastError();
     }
-    if (mode >= 2 && mode <= 6 && r16 && pp.kind == SGX_PART_HASH) {
-#define SGX_HV(K, U, S, T) \
-    hipLaunchKernelGGL((k_hist_var<K, U, S, T>), dim3(G * S), dim3(T), lds, stream, p, n, rb, chunk, pp, counts, G)
-#define SGX_HVK(K)                                          \
-    do {                                                    \
-        switch (mode) {                                     \
-        case 2: SGX_HV(K, 4, 4, 1024); break;               \
-        case 3: SGX_HV(K, 8, 2, 1024); break;               \
-        case 4: SGX_HV(K, 8, 8, 1024); break;               \
-        case 5: SGX_HV(K, 8, 4, 1024); break;               \
-        default: SGX_HV(K, 16, 2, 1024); break;             \
-        }                                                   \
-    } while (0)
-        if ((pp.R & (pp.R - 1)) == 0) SGX_HVK(KIND_HASH_POW2); else SGX_HVK(SGX_PART_HASH);
-#undef SGX_HVK
-#undef SGX_HV
-        return hipGetLastError();
-    }
-#define SGX_HIST(K, B)                                                                                        \
-    do {                                                                                                      \
-        if (lean)                                                                                             \
-            hipLaunchKernelGGL((k_hist_lean<K, B>), dim3(G * HIST_SPLIT), dim3(HIST_LEAN_THREADS), lds, stream, \
-                               p, n, rb, chunk, pp, counts, G);                                               \
-        else                                                                                                  \
-            hipLaunchKernelGGL((k_hist<K, B>), dim3(G * HIST_SPLIT), dim3(HIST_THREADS), lds, stream, p, n, rb, \
-                               chunk, pp, counts, G);                                                         \
-    } while (0)
+#define SGX_HIST(K, B) hipLaunchKernelGGL((k_hist<K, B>), grid, block, lds, stream, p, n, rb, chunk, pp, counts, G)
     switch (pp.kind) {
     case SGX_PART_HASH:
         if ((pp.R & (pp.R - 1)) == 0) {
@@ -444,10 +393,6 @@ hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint
 constexpr size_t LDS_MAX = 160 * 1024;
 constexpr uint32_t SCATTER_OOB = 2u;  // error bit: a scatter destination was out of range
 constexpr int WIDE_WAVES = 8;
-__host__ __device__ size_t scatter16_direct_lds(uint32_t R, int waves, int mbits);
-constexpr int DMA_WAVES = 8, DMA_ITEMS = 8;
-constexpr int DMA_T = DMA_WAVES * 64, DMA_TILE = DMA_WAVES * DMA_ITEMS * 64;
-size_t scatter16_dma_lds(uint32_t R, int mbits);
 constexpr int WIDE_THREADS = WIDE_WAVES * 64;
 
 __host__ __device__ constexpr size_t al16(size_t x) { return (x + 15) & ~(size_t)15; }
@@ -473,28 +418,6 @@ static int table_bits(uint32_t R, int waves, int items, uint32_t nbits, size_t b
 struct Geo16 { int waves, items; };
 // every instantiated geometry (launch_scatter's switch must list the same set)
 static const Geo16 kGeos16[] = {{4, 16}, {8, 16}, {12, 10}, {14, 9}, {16, 7}, {4, 12}, {8, 8}, {4, 8}, {8, 4}, {4, 4}, {4, 2}, {4, 1}};
-
-ScatterGeom scatter_geom16_direct(uint32_t R, int waves, int items) {
-    static const int ok[][2] = {{4, 16}, {4, 8}, {8, 16}, {8, 8}, {8, 4}};
-    bool found = false;
-    for (auto &g : ok) found |= (g[0] == waves && g[1] == items);
-    if (!found) return ScatterGeom{0, 0, 0, 0, 0};
-    uint32_t nb = 0;
-    while ((1ull << nb) < R) ++nb;
-    int mb = (int)(nb < 7 ? (nb ? nb : 1) : 7);
-    if (scatter16_direct_lds(R, waves, 0) > LDS_MAX) return ScatterGeom{0, 0, 0, 0, 0};
-    while (mb > 0 && scatter16_direct_lds(R, waves, mb) > LDS_MAX / 2) --mb;
-    return ScatterGeom{DIRECT_GEOM_BASE + waves, items, waves * items * 64, scatter16_direct_lds(R, waves, mb), mb};
-}
-
-ScatterGeom scatter_geom16_dma(uint32_t R) {
-    if (scatter16_dma_lds(R, 0) > LDS_MAX) return ScatterGeom{0, 0, 0, 0, 0};
-    uint32_t nb = 0;
-    while ((1ull << nb) < R) ++nb;
-    int mb = (int)(nb < 8 ? (nb ? nb : 1) : 8);
-    while (mb > 0 && scatter16_dma_lds(R, mb) > LDS_MAX) --mb;
-    return ScatterGeom{DMA_GEOM_TAG, DMA_ITEMS, DMA_TILE, scatter16_dma_lds(R, mb), mb};
-}
 
 ScatterGeom scatter_geom16(uint32_t R, int force_waves, int force_items) {
     ScatterGeom best{0, 0, 0, 0, 0};
@@ -612,18 +535,6 @@ __device__ __forceinline__ void lds_barrier() {
     asm volatile("" ::: "memory");
 }
 
-// Diagnostic phase stamps (DIAG == 6 only; never in the product kernels): wave 0 / lane 0
-// of every workgroup accumulates s_memtime deltas per phase; summed over workgroups here.
-__device__ unsigned long long g_sgx_stamps[8];
-
-__device__ __forceinline__ uint64_t stamp_now() {
-    uint64_t t;
-    __builtin_amdgcn_sched_barrier(0);
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-    __builtin_amdgcn_sched_barrier(0);
-    return t;
-}
-
 // Shared LDS carve-up of k_scatter16.
 struct Sc16Lds {
     uint4 *stage;
@@ -652,27 +563,16 @@ __device__ __forceinline__ Sc16Lds sc16_lds(char *smem, uint32_t R, uint32_t mbi
 
 // Rank + merge + scan + stage of one tile whose records/pids are in registers.
 // Returns with the tile partition-sorted in L.stage (after a barrier).
-template <int WAVES, int ITEMS, bool ST = false>
+template <int WAVES, int ITEMS>
 __device__ __forceinline__ void sc16_rank_stage(const Sc16Lds &L, uint32_t R, const uint4 (&rec)[ITEMS],
                                                 const uint32_t (&pid)[ITEMS], const bool (&valid)[ITEMS],
-                                                uint32_t nbits, uint64_t *acc = nullptr) {
+                                                uint32_t nbits) {
     constexpr int T = WAVES * 64;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     uint32_t rank[ITEMS];
-    uint64_t t0 = 0;
-    if constexpr (ST) t0 = stamp_now();
     rank_items<ITEMS>(pid, valid, rank, L.wcnt + (size_t)w * rowstride(R), nbits, lane,
                       L.mtab + ((size_t)w << L.mbits), L.mbits);
-    if constexpr (ST) {
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(rank[k]));
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const uint64_t t1 = stamp_now();
-        acc[2] += t1 - t0;  // rank (this wave)
-        t0 = t1;
-    }
     lds_barrier();
-    if constexpr (ST) { const uint64_t t1 = stamp_now(); acc[3] += t1 - t0; t0 = t1; }  // wait for all waves
     for (uint32_t p = tid; p < R; p += T) {
         uint32_t s = 0;
 #pragma unroll
@@ -685,7 +585,6 @@ __device__ __forceinline__ void sc16_rank_stage(const Sc16Lds &L, uint32_t R, co
     }
     lds_barrier();
     block_exclusive_scan(L.tcnt, L.lstart, R, L.scratch);
-    if constexpr (ST) { const uint64_t t1 = stamp_now(); acc[4] += t1 - t0; t0 = t1; }  // merge + scan
     const uint16_t *mycnt = L.wcnt + (size_t)w * rowstride(R);
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) {
@@ -699,29 +598,14 @@ __device__ __forceinline__ void sc16_rank_stage(const Sc16Lds &L, uint32_t R, co
 }
 
 // Generic (guarded) tile: used for the partial tail tile and for non-hash partitioners.
-// DIAG (measurement-only builds, never the product path): 1 = no global stores,
-// 2 = no ballot ranking, 3 = no global loads, 4 = no LDS stage/drain, 5 = no ranking and
-// identity staging (memory + barriers only).  Values that a skipped phase would consume
-// are kept alive with empty asm so the compiler cannot delete the phases that remain.
-template <int KIND, int WAVES, int ITEMS, int DIAG = 0, int NT = 0>
+template <int KIND, int WAVES, int ITEMS>
 __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 *__restrict__ in,
                                                   uint4 *__restrict__ out, int64_t tbase, int64_t end,
-                                                  const PartParams &pp, int64_t n, uint32_t *err,
-                                                  uint64_t *acc = nullptr) {
+                                                  const PartParams &pp, int64_t n, uint32_t *err) {
     constexpr int T = WAVES * 64;
     constexpr int TILE = WAVES * ITEMS * 64;
-    constexpr bool ST = DIAG == 6;
     const uint32_t R = pp.R;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    uint64_t t_prev = 0;
-    auto mark = [&](int ph) {
-        if constexpr (ST) {
-            const uint64_t t = stamp_now();
-            if (ph > 0) acc[ph - 1] += t - t_prev;
-            t_prev = t;
-        }
-    };
-    mark(0);
     for (uint32_t i = tid; i < (uint32_t)(WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
     uint4 rec[ITEMS];
     uint32_t pid[ITEMS];
@@ -731,75 +615,25 @@ __device__ __forceinline__ void sc16_tile_generic(const Sc16Lds &L, const uint4 
     for (int k = 0; k < ITEMS; ++k) {
         const int64_t i = wbase + (int64_t)k * 64;
         valid[k] = i < end;
-        if constexpr (DIAG == 3) {
-            rec[k] = make_uint4((uint32_t)i * 2654435761u, (uint32_t)(i >> 7), (uint32_t)i, 0);
-        } else if constexpr (NT & 1) {
-            if (valid[k]) {
-                const u32x4 v = __builtin_nontemporal_load((const u32x4 *)&in[i]);
-                rec[k] = make_uint4(v.x, v.y, v.z, v.w);
-            } else {
-                rec[k] = make_uint4(0, 0, 0, 0);
-            }
-        } else {
-            rec[k] = valid[k] ? in[i] : make_uint4(0, 0, 0, 0);
-        }
+        rec[k] = valid[k] ? in[i] : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int k = 0; k < ITEMS; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
-    if constexpr (ST) { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); mark(1); }
     __syncthreads();  // wcnt zeroed
-    mark(2);
-    if constexpr (DIAG == 2 || DIAG == 5) {
-        // skip the ballot ranking: identity-ish placement, keep every pid alive
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) asm volatile("" ::"v"(pid[k]));
-        for (uint32_t p = tid; p < R; p += T) { L.tcnt[p] = (uint16_t)(TILE / R); L.lstart[p] = (uint16_t)(p * (TILE / R)); }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) L.stage[(w * ITEMS + k) * 64 + lane] = rec[k];
-        __syncthreads();
-    } else if constexpr (DIAG == 4) {
-        sc16_rank_stage<WAVES, ITEMS>(L, R, rec, pid, valid, pp.nbits);
-    } else {
-        sc16_rank_stage<WAVES, ITEMS, ST>(L, R, rec, pid, valid, pp.nbits, acc);
-    }
-    mark(6);
+    sc16_rank_stage<WAVES, ITEMS>(L, R, rec, pid, valid, pp.nbits);
     const uint32_t tile_n = (uint32_t)min<int64_t>(TILE, end - tbase);
-    if constexpr (DIAG == 4) {
-        // no drain: write each register record straight back to its input slot
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k)
-            if (valid[k]) out[(size_t)(wbase + (int64_t)k * 64)] = rec[k];
-        (void)n; (void)err;
-    } else {
-        for (uint32_t s = tid; s < tile_n; s += T) {
-            const uint4 r = L.stage[s];
-            uint32_t p;
-            if constexpr (KIND == SGX_PART_HASH) p = hash_pid(r.x, r.y, pp);
-            else p = slot_partition(L.lstart, R, s);
-            uint32_t d;
-            if constexpr (DIAG == 5) d = (uint32_t)(tbase + s) + 0u * p;
-            else d = L.cursor[p] + (s - (uint32_t)L.lstart[p]);
-            if constexpr (DIAG == 1) {
-                asm volatile("" ::"v"(r.x), "v"(r.y), "v"(r.z), "v"(r.w), "v"(d));
-            } else {
-                if ((int64_t)d < n) {
-                    if constexpr ((NT & 2) != 0) {
-                        u32x4 v = {r.x, r.y, r.z, r.w};
-                        __builtin_nontemporal_store(v, (u32x4 *)&out[(size_t)d]);
-                    }
-                    else out[(size_t)d] = r;
-                } else {
-                    atomicOr(err, SCATTER_OOB);
-                }
-            }
-        }
+    for (uint32_t s = tid; s < tile_n; s += T) {
+        const uint4 r = L.stage[s];
+        uint32_t p;
+        if constexpr (KIND == SGX_PART_HASH) p = hash_pid(r.x, r.y, pp);
+        else p = slot_partition(L.lstart, R, s);
+        const uint32_t d = L.cursor[p] + (s - (uint32_t)L.lstart[p]);
+        if ((int64_t)d < n) out[(size_t)d] = r;
+        else atomicOr(err, SCATTER_OOB);
     }
-    mark(7);
     __syncthreads();
     for (uint32_t p = tid; p < R; p += T) L.cursor[p] += L.tcnt[p];
     __syncthreads();
-    mark(8);
 }
 
 // One full tile of the pipelined staged path: rank + stage tile t (records in `rec`),
@@ -852,59 +686,8 @@ __device__ __forceinline__ void sc16_full_tile(const Sc16Lds &L, uint4 (&rec)[IT
     lds_barrier();
 }
 
-// Double-buffered variant (NT & 4): tile t+1's loads are issued into a second register
-// buffer at the very start of tile t, so they are in flight during tile t's whole rank /
-// stage / drain instead of only its drain.
 template <int KIND, int WAVES, int ITEMS>
-__device__ __forceinline__ void sc16_db_tile(const Sc16Lds &L, const uint4 (&cur)[ITEMS], uint4 (&nxt)[ITEMS],
-                                             const uint4 *src, int64_t tn, uint4 *__restrict__ out, int64_t n,
-                                             const PartParams &pp, uint32_t &bad) {
-    constexpr int T = WAVES * 64;
-    constexpr int TILE = WAVES * ITEMS * 64;
-    const uint32_t R = pp.R;
-    const uint32_t tid = threadIdx.x;
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-        nxt[k] = src[tn * TILE + k * 64];
-        asm volatile("" ::: "memory");
-    }
-    uint32_t pid[ITEMS];
-    bool valid[ITEMS];
-#pragma unroll
-    for (int k = 0; k < ITEMS; ++k) {
-        valid[k] = true;
-        pid[k] = pid_of<KIND>(cur[k].x, cur[k].y, cur[k].z, pp);
-    }
-    sc16_rank_stage<WAVES, ITEMS>(L, R, cur, pid, valid, pp.nbits);
-    constexpr int BATCH = ITEMS % 4 == 0 ? 4 : (ITEMS % 2 == 0 ? 2 : 1);
-#pragma unroll
-    for (int k0 = 0; k0 < ITEMS; k0 += BATCH) {
-        uint4 r[BATCH];
-        uint32_t d[BATCH];
-#pragma unroll
-        for (int j = 0; j < BATCH; ++j) r[j] = L.stage[(k0 + j) * T + tid];
-#pragma unroll
-        for (int j = 0; j < BATCH; ++j) {
-            const uint32_t s = (uint32_t)((k0 + j) * T + tid);
-            uint32_t p;
-            if constexpr (KIND == SGX_PART_HASH) p = hash_pid(r[j].x, r[j].y, pp);
-            else p = slot_partition(L.lstart, R, s);
-            d[j] = L.cursor[p] + (s - (uint32_t)L.lstart[p]);
-            const bool ok = (int64_t)d[j] < n;
-            bad |= ok ? 0u : 1u;
-            d[j] = ok ? d[j] : (uint32_t)(n - 1);
-        }
-#pragma unroll
-        for (int j = 0; j < BATCH; ++j) out[(size_t)d[j]] = r[j];
-    }
-    lds_barrier();
-    for (uint32_t p = tid; p < R; p += T) L.cursor[p] += L.tcnt[p];
-    for (uint32_t i = tid; i < (uint32_t)(WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
-    lds_barrier();
-}
-
-template <int KIND, int WAVES, int ITEMS, int NT = 0>
-__global__ __launch_bounds__(WAVES * 64, (NT & 4) ? 1 : 2) void k_scatter16(const uint4 *__restrict__ in,
+__global__ __launch_bounds__(WAVES * 64, 2) void k_scatter16(const uint4 *__restrict__ in,
                                                              uint4 *__restrict__ out, int64_t n,
                                                              int64_t chunk, PartParams pp,
                                                              const uint32_t *__restrict__ offs,
@@ -919,28 +702,9 @@ __global__ __launch_bounds__(WAVES * 64, (NT & 4) ? 1 : 2) void k_scatter16(cons
     const int64_t begin = (int64_t)g * chunk;
     const int64_t end = min(n, begin + chunk);
     for (uint32_t p = tid; p < R; p += T) L.cursor[p] = offs[(int64_t)p * G + g];
-    const int64_t nfull = (NT & 3) == 0 && end > begin ? (end - begin) / TILE : 0;
+    const int64_t nfull = end > begin ? (end - begin) / TILE : 0;
     int64_t tbase = begin;
-    if constexpr ((NT & 4) != 0) {
-        if (nfull > 0) {
-            const uint4 *src = in + begin + (int64_t)w * ITEMS * 64 + lane;
-            uint4 a[ITEMS], b[ITEMS];
-#pragma unroll
-            for (int k = 0; k < ITEMS; ++k) a[k] = src[k * 64];
-            for (uint32_t i = tid; i < (uint32_t)(WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
-            __syncthreads();
-            uint32_t bad = 0;
-            for (int64_t t = 0; t < nfull; t += 2) {
-                sc16_db_tile<KIND, WAVES, ITEMS>(L, a, b, src, t + 1 < nfull ? t + 1 : nfull - 1, out, n, pp, bad);
-                if (t + 1 < nfull)
-                    sc16_db_tile<KIND, WAVES, ITEMS>(L, b, a, src, t + 2 < nfull ? t + 2 : nfull - 1, out, n, pp, bad);
-            }
-            if (bad) atomicOr(err, SCATTER_OOB);
-            tbase = begin + nfull * TILE;
-        } else {
-            __syncthreads();
-        }
-    } else if (nfull > 0) {
+    if (nfull > 0) {
         // Steady state (full tiles): tile t+1's loads are issued right after tile t is staged
         // in LDS -- before tile t's drain stores -- so the in-order vmcnt wait before ranking
         // t+1 retires exactly those loads and tile t's stores keep draining behind the next
@@ -964,7 +728,7 @@ __global__ __launch_bounds__(WAVES * 64, (NT & 4) ? 1 : 2) void k_scatter16(cons
         __syncthreads();
     }
     for (; tbase < end; tbase += TILE)
-        sc16_tile_generic<KIND, WAVES, ITEMS, 0, NT>(L, in, out, tbase, end, pp, n, err);
+        sc16_tile_generic<KIND, WAVES, ITEMS>(L, in, out, tbase, end, pp, n, err);
 }
 
 // ------------------------------------------------------------------------------------
@@ -1221,9 +985,7 @@ __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
     return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 12;  // cur 4 + dlim 8
 }
 
-// DIAG (measurement-only builds, SGX_WC_DIAG; wrong output): 1 = no global stores,
-// 2 = no global loads after the first tile (the tile's registers are reused), 3 = both.
-template <int KIND, int WAVES, int NI, int SI, int DIAG = 0>
+template <int KIND, int WAVES, int NI, int SI>
 __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__restrict__ in,
                                                                 u32x4 *__restrict__ out, int64_t n,
                                                                 int64_t chunk, PartParams pp,
@@ -1245,7 +1007,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     uint16_t *myrow = rows + (size_t)w * RS;
     uint32_t *myrow32 = (uint32_t *)myrow;
     const uint32_t n32 = (uint32_t)n;  // n < 2^32 (sgx_write_map)
-    u32x4 *junk = (u32x4 *)((char *)pp.junk + (size_t)blockIdx.x * JUNK_BYTES_PER_WG) + lane;
 
     const int g = blockIdx.x;
     const int64_t begin = (int64_t)g * chunk;
@@ -1277,12 +1038,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     __syncthreads();
     uint32_t bad = 0;
     // ---- drain: whole lines out, the rest stays in this lane's registers (dk/dpos).
-    //      LATE (A/B, DIAG 16): the drain of tile t runs after tile t+1's ranking, so the
-    //      wait for tile t+1's loads (the compiler's vmcnt(0): pending loads + stores count
-    //      as out of order) does not also wait for tile t's stores.  Measured slightly
-    //      slower (C1: 1.90-1.97 vs 1.86-1.95 ms): the store drain is not what bounds K4.
-    constexpr bool LATE = (DIAG & 16) != 0;
-    uint32_t total_prev = 0;
+    //      (Draining tile t after tile t+1's ranking, so the wait for t+1's loads does not
+    //      also wait for t's stores, measured slightly slower: 1.90-1.97 vs 1.86-1.95 ms.)
     auto drain = [&](const uint32_t ntot) {
         dmask = 0;
 #pragma unroll
@@ -1302,26 +1059,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 const uint32_t pos = dm[q].x + s;
                 const bool wr = live && pos < dm[q].y;
                 dpos[k0 + q] = pos;
-                if constexpr ((DIAG & 12) != 0 && (DIAG & 1) == 0) {
-                    // A/B (DIAG 4, 8): branch-free, every lane stores, masked-off lanes into
-                    // this workgroup's junk line, so the next tile can wait for its loads
-                    // only (DIAG 8: vmcnt(SI)) instead of the compiler's vmcnt(0) behind
-                    // conditional stores.  Measured slower (C1: 2.01-2.04 vs 1.92-1.96 ms):
-                    // the junk lines cost more than the per-tile store drain.
-                    u32x4 *dst = wr ? out + pos : junk;
-                    *dst = dk[k0 + q];
-                } else if constexpr ((DIAG & 1) == 0) {
-                    if (wr) {
-                        // nontemporal: the map output is read back much later (exchange /
-                        // fetch); streaming it past the caches keeps the input's lines in the
-                        // Infinity Cache for the next histogram (C1: map side 2.65 -> 2.63 ms,
-                        // profiles/r01_wc_nt_ab.txt).  DIAG 32: plain stores (A/B).
-                        if constexpr ((DIAG & 32) == 0) __builtin_nontemporal_store(dk[k0 + q], out + pos);
-                        else out[pos] = dk[k0 + q];
-                    }
-                } else {
-                    if (wr) asm volatile("" ::"v"(dk[k0 + q].x), "v"(dk[k0 + q].w), "v"(pos));
-                }
+                // nontemporal: the map output is read back much later (exchange / fetch);
+                // streaming it past the caches keeps the input's lines in the Infinity
+                // Cache for the next histogram (C1: map side 2.65 -> 2.63 ms,
+                // profiles/r01_wc_nt_ab.txt).  (Branch-free stores with masked lanes into a
+                // junk line, so the next tile could wait for its loads only, measured slower:
+                // 2.01-2.04 vs 1.92-1.96 ms.)
+                if (wr) __builtin_nontemporal_store(dk[k0 + q], out + pos);
                 dmask |= (live && !wr) ? 1u << (k0 + q) : 0u;
             }
         }
@@ -1332,15 +1076,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         //      (a wave's LDS ops execute in issue order; lanes of one op in lane order), one
         //      wait at the end.  An invalid item adds 0 (branch-free issue).
         uint32_t pid[NI], old[NI];
-        if constexpr ((DIAG & 8) != 0) {
-            // A/B (DIAG 8): this tile's records were loaded by inline asm ahead of the
-            // previous tile's SI branch-free stores; wait for the loads only.
-            if (t > 0) {
-                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(SI) : "memory");
-#pragma unroll
-                for (int k = 0; k < NI; ++k) asm volatile("" : "+v"(rec[k]));
-            }
-        }
 #pragma unroll
         for (int k = 0; k < NI; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
 #pragma unroll
@@ -1348,9 +1083,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             const uint32_t inc = valid[k] ? 1u << ((pid[k] & 1u) << 4) : 0u;
             old[k] = __hip_atomic_fetch_add(myrow32 + (pid[k] >> 1), inc, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        if constexpr (LATE) {
-            if (t > 0) drain(total_prev);
         }
         lds_barrier();  // B1
 
@@ -1426,7 +1158,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             }
         }
         for (uint32_t i = lane; i < RS / 8; i += 64) ((u32x4 *)myrow)[i] = u32x4{0, 0, 0, 0};
-        if (!last && (DIAG & 2) == 0) {
+        if (!last) {
             const int64_t nb = (t + 1) * TNEW;
             const u32x4 *cb = in + begin;
 #pragma unroll
@@ -1434,20 +1166,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 const int64_t i = nb + (int64_t)w * NI * 64 + k * 64 + lane;
                 valid[k] = i < len;
                 // branch-free: an invalid item re-reads the chunk head
-                if constexpr ((DIAG & 8) != 0)
-                    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(rec[k]) : "v"(cb + (valid[k] ? i : 0)) : "memory");
-                else if constexpr ((DIAG & 64) != 0)
-                    rec[k] = __builtin_nontemporal_load(cb + (valid[k] ? i : 0));  // A/B
-                else
-                    rec[k] = cb[valid[k] ? i : 0];
+                rec[k] = cb[valid[k] ? i : 0];
             }
         }
-        lds_barrier();  // B4 (LATE: the drain of this tile follows the next tile's ranking)
-        if constexpr (!LATE) drain(total);
-        else total_prev = total;
-    }
-    if constexpr (LATE) {
-        if (ntiles > 0) drain(total_prev);
+        lds_barrier();  // B4
+        drain(total);
     }
     if (bad) atomicOr(err, SCATTER_OOB);
 }
@@ -1463,414 +1186,6 @@ ScatterGeom scatter_geom16_wc(uint32_t R) {
     // biggest new-record share whose deferred cap (T*SI - T*NI) still holds 7 per partition
     const int ni = 7u * rs8(R) <= T * (SI - 12) ? 12 : 8;
     return ScatterGeom{WC_GEOM_BASE + W, ni, (int)T * ni, lds, SI};
-}
-
-template <int DIAG>
-__global__ __launch_bounds__(512, 2) void k_scatter16_diag(const uint4 *__restrict__ in,
-                                                           uint4 *__restrict__ out, int64_t n,
-                                                           int64_t chunk, PartParams pp,
-                                                           const uint32_t *__restrict__ offs, int G,
-                                                           uint32_t *err) {
-    constexpr int WAVES = 8, ITEMS = 16, T = WAVES * 64, TILE = WAVES * ITEMS * 64;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const uint32_t R = pp.R;
-    const Sc16Lds L = sc16_lds<WAVES, ITEMS>(smem, R, pp.mbits);
-    const uint32_t tid = threadIdx.x;
-    const int g = blockIdx.x;
-    const int64_t begin = (int64_t)g * chunk;
-    const int64_t end = min(n, begin + chunk);
-    for (uint32_t p = tid; p < R; p += T) L.cursor[p] = offs[(int64_t)p * G + g];
-    __syncthreads();
-    uint64_t acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int64_t tbase = begin; tbase < end; tbase += TILE)
-        sc16_tile_generic<SGX_PART_HASH, WAVES, ITEMS, DIAG>(L, in, out, tbase, end, pp, n, err, acc);
-    if constexpr (DIAG == 6) {
-        if (threadIdx.x == 0)
-            for (int i = 0; i < 8; ++i) atomicAdd(&g_sgx_stamps[i], (unsigned long long)acc[i]);
-    }
-}
-
-extern "C" int sgx_diag_stamps(unsigned long long *out, int reset) {
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sgx_stamps), sizeof(unsigned long long) * 8) != hipSuccess) return -3;
-    if (reset) {
-        unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(g_sgx_stamps), z, sizeof z) != hipSuccess) return -3;
-    }
-    return 0;
-}
-
-hipError_t launch_scatter_diag(int mode, const void *in, void *out, int64_t n, int64_t chunk, int G,
-                               const PartParams &pp, const uint32_t *offs, uint32_t *err,
-                               hipStream_t stream) {
-    const size_t lds = scatter16_lds(pp.R, 8, 16, pp.mbits);
-    if (lds > LDS_MAX || pp.kind != SGX_PART_HASH) return hipErrorInvalidValue;
-#define SGX_DIAGK(M)                                                                            \
-    do {                                                                                        \
-        (void)hipFuncSetAttribute((const void *)k_scatter16_diag<M>,                           \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
-        hipLaunchKernelGGL(k_scatter16_diag<M>, dim3(G), dim3(512), lds, stream, (const uint4 *)in, \
-                           (uint4 *)out, n, chunk, pp, offs, G, err);                           \
-    } while (0)
-    switch (mode) {
-    case 1: SGX_DIAGK(1); break;
-    case 2: SGX_DIAGK(2); break;
-    case 3: SGX_DIAGK(3); break;
-    case 4: SGX_DIAGK(4); break;
-    case 5: SGX_DIAGK(5); break;
-    case 6: SGX_DIAGK(6); break;
-    default: SGX_DIAGK(0); break;
-    }
-#undef SGX_DIAGK
-    return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------
-// K4 (chained): tiles in dispatch order with a decoupled look-back PER PARTITION across
-// tiles (the Onesweep structure).  Tile t's run of partition p starts at
-//   base[p] + sum_{t' < t} count[t'][p]
-// where base[] comes from K1-K3.  Consecutive tiles are processed concurrently by
-// different CUs, so the runs of one partition are written side by side at about the same
-// time: the output is ~R near-sequential write streams (instead of R x chunks private
-// ones), and the line shared by two consecutive runs is completed while still cached.
-// Status: one u32 granule per (tile, partition) = {flag:2 | count:30}, written by relaxed
-// agent-scope atomic stores and polled by relaxed agent-scope atomic loads (the count is
-// the flag: no fences).  FLAG_A = this tile's count, FLAG_P = inclusive prefix.  Tiles
-// are taken from an atomic ticket, so a tile only waits on tiles already running; spins
-// are bounded (error bit 1 on give-up).  Needs n < 2^30 (30-bit counts).
-// ------------------------------------------------------------------------------------
-constexpr uint32_t CH_A = 1u << 30, CH_P = 2u << 30, CH_V = (1u << 30) - 1u;
-
-__host__ __device__ size_t scatter16_chain_lds(uint32_t R, int waves, int items, int mbits) {
-    return scatter16_lds(R, waves, items, mbits) + 16;
-}
-
-template <int KIND, int WAVES, int ITEMS>
-__global__ __launch_bounds__(WAVES * 64, 2) void k_scatter16_chain(const uint4 *__restrict__ in,
-                                                                  uint4 *__restrict__ out, int64_t n,
-                                                                  int64_t ntiles, PartParams pp,
-                                                                  const uint32_t *__restrict__ base,
-                                                                  uint32_t *status, uint32_t *ticket,
-                                                                  uint32_t *err) {
-    constexpr int T = WAVES * 64;
-    constexpr int TILE = WAVES * ITEMS * 64;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const uint32_t R = pp.R;
-    const Sc16Lds L = sc16_lds<WAVES, ITEMS>(smem, R, pp.mbits);
-    uint32_t *s_tile = (uint32_t *)(smem + scatter16_lds(R, WAVES, ITEMS, pp.mbits));
-    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    for (;;) {
-        for (uint32_t i = tid; i < (uint32_t)(WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
-        if (tid == 0) *s_tile = atomicAdd(ticket, 1u);
-        __syncthreads();
-        const int64_t t = (int64_t)*s_tile;
-        if (t >= ntiles) break;
-        const int64_t tbase = t * TILE;
-        const int64_t end = min(n, tbase + TILE);
-        uint4 rec[ITEMS];
-        uint32_t pid[ITEMS], rank[ITEMS];
-        bool valid[ITEMS];
-        const int64_t wbase = tbase + (int64_t)w * ITEMS * 64 + lane;
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const int64_t i = wbase + (int64_t)k * 64;
-            valid[k] = i < end;
-            rec[k] = valid[k] ? in[i] : make_uint4(0, 0, 0, 0);
-        }
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
-        rank_items<ITEMS>(pid, valid, rank, L.wcnt + (size_t)w * rowstride(R), pp.nbits, lane,
-                          L.mtab + ((size_t)w << L.mbits), L.mbits);
-        lds_barrier();
-        uint32_t *st = status + (size_t)t * R;
-        for (uint32_t p = tid; p < R; p += T) {
-            uint32_t c = 0;
-#pragma unroll
-            for (int v = 0; v < WAVES; ++v) {
-                const uint32_t x = L.wcnt[(size_t)v * rowstride(R) + p];
-                L.wcnt[(size_t)v * rowstride(R) + p] = (uint16_t)c;
-                c += x;
-            }
-            L.tcnt[p] = (uint16_t)c;
-            // publish this tile's count as early as possible (successors look back on it)
-            __hip_atomic_store(&st[p], (t == 0 ? CH_P : CH_A) | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        lds_barrier();
-        block_exclusive_scan(L.tcnt, L.lstart, R, L.scratch);
-        const uint16_t *mycnt = L.wcnt + (size_t)w * rowstride(R);
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            if (valid[k]) {
-                const uint32_t p = pid[k];
-                const uint32_t slot = (uint32_t)L.lstart[p] + mycnt[p] + rank[k];
-                if (slot < (uint32_t)TILE) L.stage[slot] = rec[k];
-            }
-        }
-        // look back per partition (overlaps the stage writes' LDS traffic)
-        for (uint32_t p = tid; p < R; p += T) {
-            uint32_t prefix = 0;
-            if (t > 0) {
-                int64_t j = t - 1;
-                uint32_t spins = 0;
-                while (j >= 0) {
-                    const uint32_t v = __hip_atomic_load(&status[(size_t)j * R + p], __ATOMIC_RELAXED,
-                                                         __HIP_MEMORY_SCOPE_AGENT);
-                    const uint32_t f = v & ~CH_V;
-                    if (f == 0) {
-                        if (++spins > (1u << 24)) { atomicOr(err, 1u); break; }
-                        __builtin_amdgcn_s_sleep(1);
-                        continue;
-                    }
-                    prefix += v & CH_V;
-                    if (f == CH_P) break;
-                    --j;
-                }
-                __hip_atomic_store(&st[p], CH_P | (prefix + L.tcnt[p]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
-            L.cursor[p] = base[p] + prefix - (uint32_t)L.lstart[p];  // drain: dst = cursor[p] + slot
-        }
-        lds_barrier();
-        const uint32_t tile_n = (uint32_t)(end - tbase);
-        for (uint32_t s = tid; s < tile_n; s += T) {
-            const uint4 r = L.stage[s];
-            uint32_t p;
-            if constexpr (KIND == SGX_PART_HASH) p = hash_pid(r.x, r.y, pp);
-            else p = slot_partition(L.lstart, R, s);
-            const uint32_t d = L.cursor[p] + s;
-            if ((int64_t)d < n) out[(size_t)d] = r;
-            else atomicOr(err, SCATTER_OOB);
-        }
-        __syncthreads();
-    }
-}
-
-hipError_t launch_scatter_chain(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *base,
-                                uint32_t *status, uint32_t *ticket, uint32_t *err, int waves, int items,
-                                int grid, hipStream_t stream) {
-    const int tile = waves * items * 64;
-    const int64_t ntiles = (n + tile - 1) / tile;
-    const size_t lds = scatter16_chain_lds(pp.R, waves, items, pp.mbits);
-    if (lds > LDS_MAX || n >= (int64_t)CH_V) return hipErrorInvalidValue;
-#define SGX_SCC(K, W, I)                                                                        \
-    do {                                                                                        \
-        (void)hipFuncSetAttribute((const void *)k_scatter16_chain<K, W, I>,                    \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);        \
-        hipLaunchKernelGGL((k_scatter16_chain<K, W, I>), dim3(grid), dim3(W * 64), lds, stream,  \
-                           (const uint4 *)in, (uint4 *)out, n, ntiles, pp, base, status, ticket, err); \
-    } while (0)
-#define SGX_SCC_K(K)                                             \
-    do {                                                         \
-        switch (waves * 100 + items) {                           \
-        case 816: SGX_SCC(K, 8, 16); break;                      \
-        case 416: SGX_SCC(K, 4, 16); break;                      \
-        case 808: SGX_SCC(K, 8, 8); break;                       \
-        case 1607: SGX_SCC(K, 16, 7); break;                     \
-        default: return hipErrorInvalidValue;                    \
-        }                                                        \
-    } while (0)
-    switch (pp.kind) {
-    case SGX_PART_HASH: SGX_SCC_K(SGX_PART_HASH); break;
-    case SGX_PART_RANGE_I64: SGX_SCC_K(SGX_PART_RANGE_I64); break;
-    default: SGX_SCC_K(SGX_PART_RANGE_BYTES10); break;
-    }
-#undef SGX_SCC_K
-#undef SGX_SCC
-    return hipGetLastError();
-}
-
-// ------------------------------------------------------------------------------------
-// K4 (direct): no LDS staging of records.  Each tile's records are loaded coalesced,
-// ranked exactly as above, and stored straight from registers to
-// cursor[p] + (earlier waves' count of p) + rank.  Only the per-wave counters, the peer
-// table, tcnt and cursor live in LDS (~30 KB at R = 1024), so several workgroups share a
-// CU and overlap each other's load / rank / store phases.  Consecutive records of one
-// partition land in consecutive 16 B slots from different instructions of the same CU;
-// the XCD's L2 merges them into full lines before write-back.
-// ------------------------------------------------------------------------------------
-__host__ __device__ size_t scatter16_direct_lds(uint32_t R, int waves, int mbits) {
-    return al16((size_t)waves * rowstride(R) * 2) + al16((size_t)R * 2) + al16((size_t)R * 4) +
-           (mbits ? (size_t)waves * ((size_t)8 << mbits) : 0);
-}
-
-template <int KIND, int WAVES, int ITEMS>
-__global__ __launch_bounds__(WAVES * 64) void k_scatter16_direct(const uint4 *__restrict__ in,
-                                                                uint4 *__restrict__ out, int64_t n,
-                                                                int64_t chunk, PartParams pp,
-                                                                const uint32_t *__restrict__ offs,
-                                                                int G, uint32_t *err) {
-    constexpr int T = WAVES * 64;
-    constexpr int TILE = WAVES * ITEMS * 64;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const uint32_t R = pp.R, RS = rowstride(R);
-    uint16_t *wcnt = (uint16_t *)smem;
-    uint16_t *tcnt = (uint16_t *)(smem + al16((size_t)WAVES * RS * 2));
-    uint32_t *cursor = (uint32_t *)((char *)tcnt + al16((size_t)R * 2));
-    uint64_t *mtab = (uint64_t *)((char *)cursor + al16((size_t)R * 4));
-    const uint32_t mbits = pp.mbits;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int g = blockIdx.x;
-    const int64_t begin = (int64_t)g * chunk;
-    const int64_t end = min(n, begin + chunk);
-    for (uint32_t p = tid; p < R; p += T) cursor[p] = offs[(int64_t)p * G + g];
-    if (mbits)
-        for (uint32_t i = tid; i < ((uint32_t)WAVES << mbits); i += T) mtab[i] = 0ull;
-    for (int64_t tbase = begin; tbase < end; tbase += TILE) {
-        for (uint32_t i = tid; i < (uint32_t)(WAVES * RS / 2); i += T) ((uint32_t *)wcnt)[i] = 0;
-        uint4 rec[ITEMS];
-        uint32_t pid[ITEMS], rank[ITEMS];
-        bool valid[ITEMS];
-        const int64_t wbase = tbase + (int64_t)w * ITEMS * 64 + lane;
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const int64_t i = wbase + (int64_t)k * 64;
-            valid[k] = i < end;
-            rec[k] = in[valid[k] ? i : begin];  // unconditional load (clamped), masked use
-        }
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
-        lds_barrier();  // wcnt zeroed (and cursor/table initialised on the first tile)
-        rank_items<ITEMS>(pid, valid, rank, wcnt + (size_t)w * RS, pp.nbits, lane, mtab + ((size_t)w << mbits),
-                          mbits);
-        lds_barrier();
-        for (uint32_t p = tid; p < R; p += T) {
-            uint32_t s = 0;
-#pragma unroll
-            for (int v = 0; v < WAVES; ++v) {
-                const uint32_t c = wcnt[(size_t)v * RS + p];
-                wcnt[(size_t)v * RS + p] = (uint16_t)s;
-                s += c;
-            }
-            tcnt[p] = (uint16_t)s;
-        }
-        lds_barrier();
-        const uint16_t *mycnt = wcnt + (size_t)w * RS;
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            if (valid[k]) {
-                const uint32_t p = pid[k];
-                const uint32_t dst = cursor[p] + mycnt[p] + rank[k];
-                if ((int64_t)dst < n) out[(size_t)dst] = rec[k];
-                else atomicOr(err, SCATTER_OOB);
-            }
-        }
-        lds_barrier();
-        for (uint32_t p = tid; p < R; p += T) cursor[p] += tcnt[p];
-    }
-}
-
-// ------------------------------------------------------------------------------------
-// K4 (hash, full tiles): LDS-DMA software pipeline.
-//
-// Each wave moves its own sub-tile of tile t+1 from HBM straight into the LDS buffer X
-// with global_load_lds_dwordx4 (1 KiB per wave-instruction, no VGPRs) while tile t is
-// ranked, staged and drained.  A wave reads back only the bytes it DMA'd itself, so the
-// only synchronisation a prefetch needs is that wave's own s_waitcnt vmcnt: the DMA of
-// tile t+1 is issued before the ITEMS drain stores of tile t, hence vmcnt(ITEMS) at the
-// top of the next tile retires exactly the DMA (counters retire in issue order) and lets
-// the stores keep streaming.  The DMA is inline asm, invisible to hipcc's waitcnt pass
-// (cdna_hip_programming.md §5.7), so no compiler-inserted vmcnt(0) drains it; every
-// barrier in the loop is an LDS-only barrier (lgkmcnt(0) + s_barrier).
-// ------------------------------------------------------------------------------------
-size_t scatter16_dma_lds(uint32_t R, int mbits) {
-    return scatter16_lds(R, DMA_WAVES, DMA_ITEMS, mbits) + (size_t)DMA_TILE * 16;
-}
-
-__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst) {
-    uint32_t keep;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %2\n\t"
-        "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %1, off\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(keep)
-        : "v"(gsrc), "s"(lds_dst)
-        : "memory");
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-static_assert(DMA_ITEMS % 4 == 0, "k_scatter16_dma drains in batches of 4");
-__global__ __launch_bounds__(DMA_T, 2) void k_scatter16_dma(const uint4 *__restrict__ in,
-                                                           uint4 *__restrict__ out, int64_t n,
-                                                           int64_t chunk, PartParams pp,
-                                                           const uint32_t *__restrict__ offs,
-                                                           int G, uint32_t *err) {
-    constexpr int T = DMA_T, TILE = DMA_TILE, ITEMS = DMA_ITEMS;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const uint32_t R = pp.R;
-    const Sc16Lds L = sc16_lds<DMA_WAVES, DMA_ITEMS>(smem, R, pp.mbits);
-    const size_t xoff = scatter16_lds(R, DMA_WAVES, DMA_ITEMS, pp.mbits);
-    const uint4 *X = (const uint4 *)(smem + xoff);
-    const uint32_t tid = threadIdx.x, lane = tid & 63;
-    const uint32_t w = __builtin_amdgcn_readfirstlane(tid >> 6);
-    // LDS byte address of this wave's slice of X (wave-uniform, for M0)
-    const uint32_t x_lds = (uint32_t)(uintptr_t)((__attribute__((address_space(3))) char *)smem) +
-                           (uint32_t)xoff + w * (ITEMS * 64 * 16);
-    const int g = blockIdx.x;
-    const int64_t begin = (int64_t)g * chunk;
-    const int64_t end = min(n, begin + chunk);
-    for (uint32_t p = tid; p < R; p += T) L.cursor[p] = offs[(int64_t)p * G + g];
-    for (uint32_t i = tid; i < (uint32_t)(DMA_WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
-    const int64_t nfull = end > begin ? (end - begin) / TILE : 0;
-    const uint4 *src = in + begin + (int64_t)w * ITEMS * 64 + lane;
-    if (nfull > 0) {
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) glds16(src + k * 64, x_lds + k * 1024);
-    }
-    __syncthreads();  // cursor + wcnt initialised (drains nothing of ours: DMA is asm)
-    for (int64_t t = 0; t < nfull; ++t) {
-        // this wave's DMA of tile t is older than its ITEMS drain stores of tile t-1
-        if (t == 0) wait_vmcnt<0>(); else wait_vmcnt<ITEMS>();
-        uint4 rec[ITEMS];
-        uint32_t pid[ITEMS];
-        bool valid[ITEMS];
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) rec[k] = X[(w * ITEMS + k) * 64 + lane];
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        // X is free again for this wave: prefetch tile t+1 (clamped: the last tile reloads
-        // itself, which keeps the vmcnt arithmetic unconditional)
-        {
-            const int64_t tn = t + 1 < nfull ? t + 1 : t;
-            const uint4 *s2 = src + tn * TILE;
-#pragma unroll
-            for (int k = 0; k < ITEMS; ++k) glds16(s2 + k * 64, x_lds + k * 1024);
-        }
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            valid[k] = true;
-            pid[k] = hash_pid(rec[k].x, rec[k].y, pp);
-        }
-        sc16_rank_stage<DMA_WAVES, DMA_ITEMS>(L, R, rec, pid, valid, pp.nbits);
-#pragma unroll
-        for (int k0 = 0; k0 < ITEMS; k0 += 4) {
-            uint4 r[4];
-            uint32_t d[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) r[j] = L.stage[(k0 + j) * T + tid];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t p = hash_pid(r[j].x, r[j].y, pp);
-                d[j] = L.cursor[p] - (uint32_t)L.lstart[p];
-            }
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const uint32_t dst = d[j] + (uint32_t)((k0 + j) * T + tid);
-                if ((int64_t)dst < n) out[(size_t)dst] = r[j];
-                else atomicOr(err, SCATTER_OOB);
-            }
-        }
-        lds_barrier();
-        for (uint32_t p = tid; p < R; p += T) L.cursor[p] += L.tcnt[p];
-        for (uint32_t i = tid; i < (uint32_t)(DMA_WAVES * rowstride(R) / 2); i += T) ((uint32_t *)L.wcnt)[i] = 0;
-        lds_barrier();
-    }
-    wait_vmcnt<0>();  // retire the clamped re-prefetch before X/stage are reused
-    __syncthreads();
-    for (int64_t tbase = begin + nfull * TILE; tbase < end; tbase += TILE)
-        sc16_tile_generic<SGX_PART_HASH, DMA_WAVES, DMA_ITEMS>(L, in, out, tbase, end, pp, n, err);
 }
 
 // Wide records (record_bytes multiple of 4, e.g. TeraSort's 100 B): same ranking, each
@@ -1960,7 +1275,7 @@ __host__ __device__ size_t scatter_wide2_lds(uint32_t R, int rb, int kind, int n
            (size_t)8 * rs8(R) * 2 + (size_t)rs8(R) * 8 + (size_t)WIDE2_TR * 4 + 64 * 4;
 }
 
-template <int KIND, int RB, bool NT = false>
+template <int KIND, int RB>
 __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restrict__ in, uint32_t *__restrict__ out,
                                                           int64_t n, int64_t chunk, PartParams pp,
                                                           const uint32_t *__restrict__ offs, int G,
@@ -2115,10 +1430,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q)
-                if (live[q] && dst[q] < (uint32_t)n) {
-                    if constexpr (NT) __builtin_nontemporal_store(v[q], out + (uint64_t)dst[q] * DW + wi[q]);
-                    else out[(uint64_t)dst[q] * DW + wi[q]] = v[q];
-                }
+                if (live[q] && dst[q] < (uint32_t)n) out[(uint64_t)dst[q] * DW + wi[q]] = v[q];
         }
         __syncthreads();  // stage / idx reused by the next tile
     }
@@ -2135,62 +1447,20 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t chunk, int G,
                           const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
                           uint32_t *err, hipStream_t stream) {
-    if (rb == 16 && is_direct_geom(geo.waves)) {
-        const int W = geo.waves - DIRECT_GEOM_BASE;
-#define SGX_SCD(K, WV, I)                                                                       \
-    do {                                                                                        \
-        (void)hipFuncSetAttribute((const void *)k_scatter16_direct<K, WV, I>,                  \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
-        hipLaunchKernelGGL((k_scatter16_direct<K, WV, I>), dim3(G), dim3(WV * 64), geo.lds_bytes, \
-                           stream, (const uint4 *)in, (uint4 *)out, n, chunk, pp, offs, G, err); \
-    } while (0)
-#define SGX_SCD_K(K)                                                       \
-    do {                                                                   \
-        switch (W * 100 + geo.items) {                                     \
-        case 416: SGX_SCD(K, 4, 16); break;                                \
-        case 408: SGX_SCD(K, 4, 8); break;                                 \
-        case 816: SGX_SCD(K, 8, 16); break;                                \
-        case 808: SGX_SCD(K, 8, 8); break;                                 \
-        case 804: SGX_SCD(K, 8, 4); break;                                 \
-        default: return hipErrorInvalidValue;                              \
-        }                                                                  \
-    } while (0)
-        switch (pp.kind) {
-        case SGX_PART_HASH: SGX_SCD_K(SGX_PART_HASH); break;
-        case SGX_PART_RANGE_I64: SGX_SCD_K(SGX_PART_RANGE_I64); break;
-        default: SGX_SCD_K(SGX_PART_RANGE_BYTES10); break;
-        }
-#undef SGX_SCD_K
-#undef SGX_SCD
-        return hipGetLastError();
-    }
+    const bool pow2 = (pp.R & (pp.R - 1)) == 0;
     if (rb == 16 && geo.waves >= WC_GEOM_BASE) {
         if ((pp.kind != SGX_PART_HASH && pp.kind != KIND_DIGIT) || geo.waves != WC_GEOM_BASE + 8 || geo.mbits != 16)
             return hipErrorInvalidValue;
-#define SGX_WC1(K, NI, DG)                                                                       \
-    do {                                                                                         \
-        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, 8, NI, 16, DG>,               \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
-        hipLaunchKernelGGL((k_scatter16_wc<K, 8, NI, 16, DG>), dim3(G), dim3(512), geo.lds_bytes, \
-                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err); \
-    } while (0)
 #define SGX_WC(K, NI)                                                                            \
     do {                                                                                         \
-        if (NI == 8 && geo.nt == 101) SGX_WC1(K, 8, 1);                                          \
-        else if (NI == 8 && geo.nt == 102) SGX_WC1(K, 8, 2);                                     \
-        else if (NI == 8 && geo.nt == 103) SGX_WC1(K, 8, 3);                                     \
-        else if (NI == 8 && geo.nt == 104) SGX_WC1(K, 8, 4);                                     \
-        else if (NI == 8 && geo.nt == 108) SGX_WC1(K, 8, 8);                                     \
-        else if (NI == 8 && geo.nt == 116) SGX_WC1(K, 8, 16);                                    \
-        else if (NI == 8 && geo.nt == 132) SGX_WC1(K, 8, 32);                                    \
-        else if (NI == 8 && geo.nt == 164) SGX_WC1(K, 8, 64);                                    \
-        else if (NI == 8 && geo.nt == 196) SGX_WC1(K, 8, 96);                                    \
-        else SGX_WC1(K, NI, 0);                                                                  \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, 8, NI, 16>,                   \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
+        hipLaunchKernelGGL((k_scatter16_wc<K, 8, NI, 16>), dim3(G), dim3(512), geo.lds_bytes,     \
+                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err); \
     } while (0)
-        const bool pow2 = (pp.R & (pp.R - 1)) == 0;
         if (pp.kind == KIND_DIGIT) {
             if (geo.items != 12 || pp.R != DIGIT_R) return hipErrorInvalidValue;
-            SGX_WC1(KIND_DIGIT, 12, 0);
+            SGX_WC(KIND_DIGIT, 12);
         } else if (geo.items == 12) {
             if (pow2) SGX_WC(KIND_HASH_POW2, 12); else SGX_WC(SGX_PART_HASH, 12);
         } else if (geo.items == 8) {
@@ -2199,7 +1469,6 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
             return hipErrorInvalidValue;
         }
 #undef SGX_WC
-#undef SGX_WC1
         return hipGetLastError();
     }
     if (rb == 16 && geo.waves >= ORD_GEOM_BASE) {
@@ -2223,17 +1492,10 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         }                                                                 \
     } while (0)
         if (pp.kind != SGX_PART_HASH) return hipErrorInvalidValue;
-        if ((pp.R & (pp.R - 1)) == 0) SGX_ORD_K(KIND_HASH_POW2);
+        if (pow2) SGX_ORD_K(KIND_HASH_POW2);
         else SGX_ORD_K(SGX_PART_HASH);
 #undef SGX_ORD_K
 #undef SGX_ORD
-        return hipGetLastError();
-    }
-    if (rb == 16 && geo.waves == DMA_GEOM_TAG) {
-        (void)hipFuncSetAttribute((const void *)k_scatter16_dma, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  (int)geo.lds_bytes);
-        hipLaunchKernelGGL(k_scatter16_dma, dim3(G), dim3(DMA_T), geo.lds_bytes, stream, (const uint4 *)in,
-                           (uint4 *)out, n, chunk, pp, offs, G, err);
         return hipGetLastError();
     }
     if (rb == 16) {
@@ -2247,24 +1509,9 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         hipLaunchKernelGGL((k_scatter16<K, W, I>), dim3(G), dim3(W * 64), geo.lds_bytes, stream, \
                            i4, o4, n, chunk, pp, offs, G, err);                                \
     } while (0)
-#define SGX_SC16NT(K, W, I, NTV)                                                                 \
-    do {                                                                                        \
-        (void)hipFuncSetAttribute((const void *)k_scatter16<K, W, I, NTV>,                     \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
-        hipLaunchKernelGGL((k_scatter16<K, W, I, NTV>), dim3(G), dim3(W * 64), geo.lds_bytes, stream, \
-                           i4, o4, n, chunk, pp, offs, G, err);                                \
-    } while (0)
 #define SGX_SC16_K(K)                                                        \
     do {                                                                     \
-        const int key = geo.waves * 100 + geo.items;                         \
-        if (geo.nt && key == 816) {                                          \
-            if (geo.nt == 1) SGX_SC16NT(K, 8, 16, 1);                        \
-            else if (geo.nt == 2) SGX_SC16NT(K, 8, 16, 2);                   \
-            else if (geo.nt == 3) SGX_SC16NT(K, 8, 16, 3);                   \
-            else SGX_SC16NT(K, 8, 16, 4);                                    \
-            break;                                                           \
-        }                                                                    \
-        switch (key) {                                                       \
+        switch (geo.waves * 100 + geo.items) {                               \
         case 416: SGX_SC16(K, 4, 16); break;                                 \
         case 816: SGX_SC16(K, 8, 16); break;                                 \
         case 1210: SGX_SC16(K, 12, 10); break;                               \
@@ -2286,33 +1533,25 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         default: SGX_SC16_K(SGX_PART_RANGE_BYTES10); break;
         }
 #undef SGX_SC16_K
-#undef SGX_SC16NT
 #undef SGX_SC16
     } else if (rb == 100 && geo.waves == WIDE2_GEOM_TAG) {
         if (((uintptr_t)in & 15) != 0) return hipErrorInvalidValue;
-        // SGX_WIDE2_NT=1 (A/B): nontemporal dword stores in the drain
-        static const bool w2nt = getenv("SGX_WIDE2_NT") && atoi(getenv("SGX_WIDE2_NT")) != 0;
-#define SGX_W2NT(K, NTV)                                                                         \
-    do {                                                                                         \
-        (void)hipFuncSetAttribute((const void *)k_scatter_wide2<K, 100, NTV>,                   \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
-        hipLaunchKernelGGL((k_scatter_wide2<K, 100, NTV>), dim3(G), dim3(512), geo.lds_bytes, stream, \
-                           (const u32x4 *)in, (uint32_t *)out, n, chunk, pp, offs, G, err);     \
-    } while (0)
 #define SGX_W2(K)                                                                                \
     do {                                                                                         \
-        if (w2nt) SGX_W2NT(K, true); else SGX_W2NT(K, false);                                    \
+        (void)hipFuncSetAttribute((const void *)k_scatter_wide2<K, 100>,                        \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
+        hipLaunchKernelGGL((k_scatter_wide2<K, 100>), dim3(G), dim3(512), geo.lds_bytes, stream,  \
+                           (const u32x4 *)in, (uint32_t *)out, n, chunk, pp, offs, G, err);     \
     } while (0)
         switch (pp.kind) {
         case SGX_PART_HASH:
-            if ((pp.R & (pp.R - 1)) == 0) SGX_W2(KIND_HASH_POW2); else SGX_W2(SGX_PART_HASH);
+            if (pow2) SGX_W2(KIND_HASH_POW2); else SGX_W2(SGX_PART_HASH);
             break;
         case KIND_DIGIT: SGX_W2(KIND_DIGIT); break;
         case SGX_PART_RANGE_I64: SGX_W2(SGX_PART_RANGE_I64); break;
         default: SGX_W2(SGX_PART_RANGE_BYTES10); break;
         }
 #undef SGX_W2
-#undef SGX_W2NT
     } else {
         if (geo.items == 0 || (rb & 3) != 0 || rb < 12) return hipErrorInvalidValue;
         const char *ic = (const char *)in;

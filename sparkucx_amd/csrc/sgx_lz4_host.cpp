@@ -1,0 +1,161 @@
+// sgx_lz4_host.cpp — host side of the LZ4 codec (spark.shuffle.compress=true with
+// spark.io.compression.codec=lz4, Spark 3.0.1's defaults): lz4-java's
+// LZ4BlockOutputStream framing of partition streams and LZ4BlockInputStream on fetched
+// blocks, both on the GPU (sgx_lz4.hip) with grow-only per-thread scratch.
+#include "sgx_engine.h"
+
+#include <algorithm>
+#include <cstring>
+
+using namespace sgx;
+
+// alloc_dst: allocate the destination (exact size) instead of dst_dev.  Scratch: the
+// context's grow-only lz4_* buffers (one allocation per size class, not per call).
+int sgx::lz4_frame_impl(sgx_engine *e, Ctx &c, const void *stream_dev, const int64_t *part_offsets,
+                        int32_t num_partitions, int32_t block_size, DevBuf *alloc_dst, void *dst_dev,
+                        int64_t dst_cap, int64_t *out_lengths) {
+    if (!e || !part_offsets || !out_lengths || num_partitions < 1)
+        return fail_msg(SGX_ERR_INVALID, "sgx_lz4_frame_partitions: bad arguments");
+    if (block_size < 64 || block_size > sgx::lz4_max_block())
+        return fail_msg(SGX_ERR_UNSUPPORTED, "LZ4 block size %d outside [64, %d]", block_size, sgx::lz4_max_block());
+    const int R = num_partitions;
+    std::vector<int64_t> blocks;  // {src offset, length} per block
+    std::vector<int32_t> first(R + 1);
+    for (int r = 0; r < R; ++r) {
+        first[r] = (int32_t)(blocks.size() / 2);
+        int64_t a = part_offsets[r], b = part_offsets[r + 1];
+        if (b < a || a < 0) return fail_msg(SGX_ERR_INVALID, "partition offsets decrease at %d", r);
+        for (int64_t p = a; p < b; p += block_size) {
+            blocks.push_back(p);
+            blocks.push_back(std::min<int64_t>(block_size, b - p));
+        }
+    }
+    const int64_t nb = (int64_t)blocks.size() / 2;
+    first[R] = (int32_t)nb;
+    if (nb > 0 && !stream_dev) return fail_msg(SGX_ERR_INVALID, "stream is NULL");
+    // lz4-java: level = max(0, 32 - nlz(blockSize - 1) - COMPRESSION_LEVEL_BASE (10))
+    const int level = std::max(0, 32 - __builtin_clz((unsigned)(block_size - 1)) - 10);
+    const int64_t slot = ((int64_t)21 + block_size + block_size / 255 + 16 + 15) / 16 * 16;
+    HIP_TRY(hipSetDevice(e->device));
+    DevBuf &d_blocks = c.lz4_blocks, &d_slots = c.lz4_slots, &d_sizes = c.lz4_sizes, &d_offs = c.lz4_offs;
+    hipStream_t st = c.st;
+    std::vector<int32_t> sizes(nb);
+    if (nb > 0) {
+        SGX_TRY(d_blocks.ensure((size_t)nb * 16));
+        SGX_TRY(d_slots.ensure((size_t)(nb * slot)));
+        SGX_TRY(d_sizes.ensure((size_t)nb * 4));
+        HIP_TRY(hipMemcpyAsync(d_blocks.p, blocks.data(), (size_t)nb * 16, hipMemcpyHostToDevice, st));
+        HIP_TRY(sgx::launch_lz4_blocks((const uint8_t *)stream_dev, (const int64_t *)d_blocks.p, nb, level,
+                                       (uint8_t *)d_slots.p, slot, (int32_t *)d_sizes.p, st));
+        HIP_TRY(hipMemcpyAsync(sizes.data(), d_sizes.p, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    // frame offsets (blocks of a partition back to back, then its end mark)
+    std::vector<int64_t> offs((size_t)nb + R);  // nb frame offsets | end-mark offsets
+    int64_t total = 0, nends = 0;
+    for (int r = 0; r < R; ++r) {
+        int64_t start = total;
+        for (int32_t b = first[r]; b < first[r + 1]; ++b) {
+            if (sizes[b] < 21 || sizes[b] > slot) return fail_msg(SGX_ERR_HIP, "LZ4 block %d: bad frame size %d", b, sizes[b]);
+            offs[b] = total;
+            total += sizes[b];
+        }
+        if (first[r + 1] > first[r]) {
+            offs[nb + nends++] = total;
+            total += 21;
+        }
+        out_lengths[r] = total - start;
+    }
+    if (alloc_dst) {
+        SGX_TRY(alloc_dst->ensure((size_t)total));
+        dst_dev = alloc_dst->p;
+        dst_cap = total;
+    }
+    if (!dst_dev) return SGX_OK;
+    if (total > dst_cap)
+        return fail_msg(SGX_ERR_INVALID, "LZ4 frames need %lld bytes, destination holds %lld", (long long)total,
+                    (long long)dst_cap);
+    if (nb > 0) {
+        SGX_TRY(d_offs.ensure((size_t)(nb + nends) * 8));
+        HIP_TRY(hipMemcpyAsync(d_offs.p, offs.data(), (size_t)(nb + nends) * 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(sgx::launch_lz4_gather((const uint8_t *)d_slots.p, slot, (const int32_t *)d_sizes.p,
+                                       (const int64_t *)d_offs.p, nb, (const int64_t *)d_offs.p + nb, nends, level,
+                                       (uint8_t *)dst_dev, st));
+        HIP_TRY(hipStreamSynchronize(st));
+    }
+    return SGX_OK;
+}
+
+extern "C" int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, const int64_t *part_offsets,
+                                        int32_t num_partitions, int32_t block_size, void *dst_dev,
+                                        int64_t dst_cap, int64_t *out_lengths) {
+    if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    return lz4_frame_impl(e, *c, stream_dev, part_offsets, num_partitions, block_size, nullptr, dst_dev, dst_cap,
+                          out_lengths);
+}
+
+// LZ4BlockInputStream on the reduce side: decompress fetched LZ4-framed partition streams
+extern "C" int sgx_lz4_unframe(sgx_engine *e, const void *framed_dev, int64_t framed_bytes, void *dst_dev,
+                               int64_t dst_cap, int64_t *out_bytes) {
+    if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    return lz4_unframe_impl(e, *c, framed_dev, framed_bytes, nullptr, dst_dev, dst_cap, out_bytes);
+}
+
+// alloc_dst: size (decompressed + 64 B of decoder padding) and use it
+int sgx::lz4_unframe_impl(sgx_engine *e, Ctx &c, const void *framed_dev, int64_t framed_bytes, DevBuf *alloc_dst,
+                          void *dst_dev, int64_t dst_cap, int64_t *out_bytes) {
+    if (!e || !out_bytes || framed_bytes < 0 || (framed_bytes > 0 && !framed_dev))
+        return fail_msg(SGX_ERR_INVALID, "sgx_lz4_unframe: bad arguments");
+    *out_bytes = 0;
+    if (framed_bytes == 0) return SGX_OK;
+    HIP_TRY(hipSetDevice(e->device));
+    // one walk normally suffices: room for a frame per 512 B of input (frames of full 32 KiB
+    // blocks are ~64x sparser); a denser stream (tiny partitions) is walked again with room
+    // for every frame
+    int64_t cap = framed_bytes / 512 + 4096;
+    DevBuf &d_info = c.lz4_info, &d_desc = c.lz4_desc;
+    hipStream_t st = c.st;
+    SGX_TRY(d_info.ensure(64));
+    int64_t info[5];
+    for (int pass = 0; pass < 2; ++pass) {
+        SGX_TRY(d_desc.ensure((size_t)cap * 16));
+        HIP_TRY(hipMemsetAsync(d_info.p, 0, 64, st));
+        HIP_TRY(sgx::launch_lz4_walk((const uint8_t *)framed_dev, framed_bytes, (int64_t *)d_desc.p, cap,
+                                     (int64_t *)d_info.p, st));
+        HIP_TRY(hipMemcpyAsync(info, d_info.p, 40, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (info[2] != 0 || info[0] <= cap || (!dst_dev && !alloc_dst)) break;
+        cap = info[0];
+    }
+    static const char *why[] = {"", "truncated header", "bad magic", "unknown compression method",
+                                "malformed end mark", "bad block lengths"};
+    if (info[2] != 0)
+        return fail_msg(SGX_ERR_INVALID, "LZ4 stream: %s at byte %lld", why[info[2] < 6 ? info[2] : 0],
+                    (long long)info[3]);
+    const int64_t nframes = info[0];
+    *out_bytes = info[1];
+    if (alloc_dst) {
+        SGX_TRY(alloc_dst->ensure((size_t)info[1] + 64));
+        dst_dev = alloc_dst->p;
+        dst_cap = info[1];
+    }
+    if (!dst_dev) return SGX_OK;
+    if (info[1] > dst_cap)
+        return fail_msg(SGX_ERR_INVALID, "LZ4 stream decodes to %lld bytes, destination holds %lld",
+                    (long long)info[1], (long long)dst_cap);
+    if (nframes == 0) return SGX_OK;
+    HIP_TRY(sgx::launch_lz4_decode((const uint8_t *)framed_dev, (const int64_t *)d_desc.p, nframes,
+                                   (uint8_t *)dst_dev, (uint32_t *)((int64_t *)d_info.p + 4), st));
+    uint32_t derr = 0;
+    HIP_TRY(hipMemcpyAsync(&derr, (int64_t *)d_info.p + 4, 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    if (derr & 1u) return fail_msg(SGX_ERR_INVALID, "LZ4 stream: corrupt compressed block");
+    if (derr & 2u) return fail_msg(SGX_ERR_INVALID, "LZ4 stream: block checksum mismatch");
+    return SGX_OK;
+}

@@ -1,0 +1,476 @@
+// sgx_map.cpp — the map side: getWriter(...).write(records) + commitAllPartitions
+// (spark_3_0/UcxShuffleManager.scala:32-53; ucx/NvkvShuffleMapOutputWriter.scala:105-148).
+//
+//   sgx_write_map    one batch: K1+K2 histogram -> K3 scan -> K4 stable scatter on the calling
+//                    thread's stream, then (dep.serializer = Kryo) the Kryo framing kernels;
+//                    with dep.mapSideCombine the records are first combined per key (sort by
+//                    key within partition + segmented sum + repartition).
+//   sgx_map_begin / _append / _commit   a map task whose records arrive in several batches
+//                    (spills): every batch is partitioned on arrival, the commit concatenates
+//                    the batches per partition in append order.
+//   finish_lengths   long[R] partition lengths (commitAllPartitions' return value) and the
+//                    published bytes: fixed records, the Kryo stream, or its LZ4 frames.
+#include "sgx_engine.h"
+
+#include <algorithm>
+#include <cstring>
+
+using namespace sgx;
+
+// ------------------------------------------------------------------------------------
+// one stable partition pass
+// ------------------------------------------------------------------------------------
+// K1+K2 hist -> K3 scan -> K4 scatter of `n` records of `rb` bytes from device memory `in`
+// to `out` under partitioner `spp` (R partitions, `kind`), asynchronous on the context's
+// stream.  The (R+1) record offsets and the device error word land in `host_off` (R+2 u32,
+// pinned) when given; the error word alone in `err_slot` (device) when given; the device
+// offsets stay in c.last_off_dev until the context's next pass.
+int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_t n, int rb, const PartParams &spp,
+                        int32_t R, int32_t kind, uint32_t *host_off, uint32_t *err_slot, bool stats) {
+    hipStream_t st = c.st;
+    // K4 choice (every choice is byte-identical):
+    //   hash, 16 B, R <= 1024   write-combining staged kernel (whole 128 B lines only)
+    //   hash, 16 B, R > 1024    lane-ordered staged kernel
+    //   range, 16 B             ballot-matched staged kernel (slot -> partition search)
+    //   100 B                   LDS-staged dword-stream kernel (R <= 2048), else per-lane copy
+    ScatterGeom geo = rb == 16 ? scatter_geom16((uint32_t)R, e->sc_waves, e->sc_items)
+                               : scatter_geom_wide((uint32_t)R, rb);
+    if (rb == 16 && kind == SGX_PART_HASH && e->rank_mode == SGX_RANK_ORDERED) {
+        const ScatterGeom o = scatter_geom16_ord((uint32_t)R, e->sc_waves, e->sc_items);
+        if (o.items) geo = o;
+        if (!(e->flags & SGX_FLAG_NO_WRITE_COMBINING) && e->sc_waves == 0 && e->sc_items == 0) {
+            const ScatterGeom w = scatter_geom16_wc((uint32_t)R);
+            if (w.items) geo = w;
+        }
+    }
+    if (rb != 16 && !(e->flags & SGX_FLAG_NO_WIDE_STAGED) && ((uintptr_t)in & 15) == 0) {
+        const ScatterGeom w2 = scatter_geom_wide2((uint32_t)R, rb, kind, spp.nb);
+        if (w2.items) geo = w2;
+    }
+    // the reduce side's digit passes run on the write-combining / wide-record kernels only
+    if (kind == KIND_DIGIT) {
+        if (rb == 16) geo = scatter_geom16_wc((uint32_t)R);
+        if (geo.waves < WC_GEOM_BASE && geo.waves != WIDE2_GEOM_TAG)
+            return fail_msg(SGX_ERR_UNSUPPORTED, "digit pass on %d B records at this alignment", rb);
+    }
+    if (geo.items == 0)
+        return fail_msg(SGX_ERR_UNSUPPORTED, "no scatter geometry (waves %d, items %d) fits R=%d", e->sc_waves,
+                        e->sc_items, R);
+    const int tile = geo.tile;
+    int64_t chunk = n > 0 ? (n + e->G - 1) / e->G : 1;
+    chunk = (chunk + tile - 1) / tile * tile;
+    const int G = n > 0 ? (int)((n + chunk - 1) / chunk) : 1;
+    const int64_t len = (int64_t)R * G;
+    const int64_t tiles = scan_tiles(len);
+    SGX_TRY(c.offs.ensure((size_t)len * 4));
+    // one work block, zeroed by ONE memset (each fill / copy between kernels costs ~5-10 µs):
+    // [counts u32 x R*G][ticket u32 | pad][look-back status u64 x tiles]
+    // [partition offsets u32 x (R+1) | error] -- the error word sits right after the
+    // offsets so one copy lands both on the host
+    const size_t counts_bytes = ((size_t)len * 4 + 15) & ~(size_t)15;
+    const size_t status_bytes = ((size_t)(16 + tiles * 8) + 15) & ~(size_t)15;
+    const size_t work_bytes = counts_bytes + status_bytes + (((size_t)(R + 2) * 4 + 15) & ~(size_t)15);
+    SGX_TRY(c.work.ensure(work_bytes));
+    uint32_t *counts = (uint32_t *)c.work.p;
+    uint32_t *ticket = (uint32_t *)((char *)c.work.p + counts_bytes);
+    uint64_t *status = (uint64_t *)((char *)ticket + 16);
+    uint32_t *part_off_dev = (uint32_t *)((char *)ticket + status_bytes);
+    uint32_t *err = part_off_dev + R + 1;
+    c.last_off_dev = part_off_dev;
+    HIP_TRY(hipMemsetAsync(c.work.p, 0, work_bytes, st));
+
+    // stage events: consecutive stages share their boundary event (every timing marker
+    // between two kernels measured ~5 µs of idle GPU)
+    hipEvent_t h0 = e->ev(), h1 = e->ev(), c1 = e->ev(), x1 = e->ev();
+    HIP_TRY(hipEventRecord(h0, st));
+    if (n > 0) HIP_TRY(launch_hist(in, n, rb, chunk, G, spp, counts, st, e->hist_mode, true));
+    HIP_TRY(hipEventRecord(h1, st));
+    HIP_TRY(launch_scan((const uint32_t *)counts, (uint32_t *)c.offs.p, len, status, ticket, err, part_off_dev, G, R,
+                        st));
+    HIP_TRY(hipEventRecord(c1, st));
+    PartParams lpp = spp;
+    lpp.mbits = (uint32_t)geo.mbits;
+    if (n > 0) HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, lpp, (const uint32_t *)c.offs.p, geo, err, st));
+    HIP_TRY(hipEventRecord(x1, st));
+    // (R+1) offsets then the error word, one copy
+    if (host_off) HIP_TRY(hipMemcpyAsync(host_off, part_off_dev, (size_t)(R + 2) * 4, hipMemcpyDeviceToHost, st));
+    if (err_slot) HIP_TRY(hipMemcpyAsync(err_slot, err, 4, hipMemcpyDeviceToDevice, st));
+    if (stats) {
+        e->record_stage(SGX_STAGE_HIST, h0, h1);
+        e->record_stage(SGX_STAGE_SCAN, h1, c1);
+        e->record_stage(SGX_STAGE_SCATTER, c1, x1);
+    } else {
+        e->release_events({h0, h1, c1, x1});
+    }
+    return SGX_OK;
+}
+
+// Kryo framing of the partition-contiguous 16 B records just written (sgx_serde.hip), on
+// the context's stream behind the scatter; byte offsets land in m.ser_off (pinned).
+// rec_off_dev: device (R+1) u32 record offsets of m.data.
+static int serialize_kryo(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const uint32_t *rec_off_dev) {
+    hipStream_t st = c.st;
+    const int64_t n = m.nrec;
+    const int64_t tiles = kryo_ser16_tiles(n);
+    const size_t offb = (size_t)(s.R + 1) * 8;
+    SGX_TRY(m.ser.ensure((size_t)(20 * n + 16)));
+    SGX_TRY(m.ser_work.ensure(offb + (size_t)kryo_work_bytes(tiles)));
+    SGX_TRY(m.ser_off.ensure(offb));
+    int64_t *off_dev = (int64_t *)m.ser_work.p;
+    uint64_t *work = (uint64_t *)((char *)m.ser_work.p + offb);
+    if (n == 0) HIP_TRY(hipMemsetAsync(off_dev, 0, offb, st));  // no tile writes them
+    hipEvent_t k0 = e->ev(), k1 = e->ev();
+    HIP_TRY(hipEventRecord(k0, st));
+    HIP_TRY(launch_kryo_ser16(m.data.p, n, m.ser.p, rec_off_dev, s.R, off_dev, work, st));
+    HIP_TRY(hipEventRecord(k1, st));
+    e->record_stage(SGX_STAGE_SERIALIZE, k0, k1);
+    HIP_TRY(hipMemcpyAsync(m.ser_off.p, off_dev, offb, hipMemcpyDeviceToHost, st));  // (R+1) byte offsets
+    m.ser_valid = true;
+    return SGX_OK;
+}
+
+// Map-side combine, SGX_AGG_SUM (ExternalSorter.insertAll with the aggregator's
+// mergeValue; the canonical combiner order is (partition, key ascending)): the n records at
+// `in` (device) are copied to the context's sort buffer, sorted stably by key and then by
+// the shuffle's partitioner (LSD digit passes + one partition pass, sgx_read.cpp), grouped,
+// summed (wrapping), packed back into {key, sum} records and partitioned into m.data (an
+// identity permutation that yields the partition offsets through the usual machinery).
+// Synchronous (the group count decides the output size).
+static int combine_sum(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n) {
+    hipStream_t st = c.st;
+    hipEvent_t t0 = e->ev(), t1 = e->ev();
+    HIP_TRY(hipEventRecord(t0, st));
+    SGX_TRY(c.sort_buf[0].ensure((size_t)std::max<int64_t>(n, 1) * 16));
+    SGX_TRY(c.sort_buf[1].ensure((size_t)std::max<int64_t>(n, 1) * 16));
+    if (n > 0) HIP_TRY(hipMemcpyAsync(c.sort_buf[0].p, in, (size_t)n * 16, hipMemcpyDeviceToDevice, st));
+    const void *sorted = c.sort_buf[0].p;
+    int64_t ng = 0;
+    int64_t *keys = nullptr, *sums = nullptr;
+    if (n > 0) {
+        SGX_TRY(sort_records(e, c, s, n, true, &sorted));
+        SGX_TRY(group_records(e, c, sorted, n, SGX_AGG_SUM, &ng, &keys, nullptr, &sums));
+    }
+    SGX_TRY(c.comb_buf.ensure((size_t)std::max<int64_t>(ng, 1) * 16));
+    HIP_TRY(launch_pack_pairs(keys, sums, ng, c.comb_buf.p, st));
+    m.nrec = ng;
+    SGX_TRY(m.data.ensure((size_t)std::max<int64_t>(ng, 1) * 16));
+    SGX_TRY(partition_pass(e, c, c.comb_buf.p, m.data.p, ng, 16, s.pp, s.R, s.kind, (uint32_t *)m.part_off.p,
+                           nullptr, false));
+    HIP_TRY(hipEventRecord(t1, st));
+    e->record_stage(SGX_STAGE_COMBINE, t0, t1);
+    return SGX_OK;
+}
+
+// After the records of a map are known (device `in`, n records, or already partitioned in
+// m.data when `partitioned`): partition / combine, then frame.  Asynchronous except for the
+// combine.  m.done is recorded behind the last kernel.
+static int run_map_pipeline(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n,
+                            bool partitioned, const uint32_t *part_dev) {
+    m.ready = false;
+    m.ser_valid = false;
+    m.comp_valid = false;
+    const uint32_t *rec_off_dev = part_dev;
+    if (s.combine == SGX_AGG_SUM) {
+        SGX_TRY(combine_sum(e, c, s, m, partitioned ? m.data.p : in, n));
+        rec_off_dev = c.last_off_dev;
+    } else if (!partitioned) {
+        m.nrec = n;
+        SGX_TRY(m.data.ensure((size_t)std::max<int64_t>(n * s.rb, 16)));
+        SGX_TRY(partition_pass(e, c, in, m.data.p, n, s.rb, s.pp, s.R, s.kind, (uint32_t *)m.part_off.p, nullptr,
+                               true));
+        rec_off_dev = c.last_off_dev;
+    }
+    if (s.ser == SGX_SER_KRYO) SGX_TRY(serialize_kryo(e, c, s, m, rec_off_dev));
+    HIP_TRY(m.done.record(c.st));
+    m.written = true;
+    return SGX_OK;
+}
+
+int sgx::finish_lengths(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
+    if (m.ready) return SGX_OK;
+    if (!m.written) return fail_msg(SGX_ERR_STATE, "map output was not committed");
+    HIP_TRY(m.done.wait_host());
+    const uint32_t *po = (const uint32_t *)m.part_off.p;
+    if (po[s.R + 1] & 1u)
+        return fail_msg(SGX_ERR_TIMEOUT, "scan look-back spin gave up (device flag %u)", po[s.R + 1]);
+    if (po[s.R + 1] & 2u)
+        return fail_msg(SGX_ERR_HIP, "internal error: a scatter destination was out of range (device flag %u)",
+                        po[s.R + 1]);
+    if ((int64_t)po[s.R] != m.nrec)
+        return fail_msg(SGX_ERR_HIP, "partition offsets do not sum to the record count (%u vs %lld)", po[s.R],
+                        (long long)m.nrec);
+    m.lengths.assign((size_t)s.R, 0);
+    if (s.ser == SGX_SER_KRYO) {
+        const int64_t *so = (const int64_t *)m.ser_off.p;
+        int64_t prev = 0;
+        for (int32_t p = 0; p < s.R; ++p) {
+            m.lengths[(size_t)p] = so[p + 1] - so[p];
+            if (so[p] != prev || m.lengths[(size_t)p] < 0 ||
+                m.lengths[(size_t)p] > 20 * ((int64_t)po[p + 1] - po[p]))
+                return fail_msg(SGX_ERR_HIP, "internal error: Kryo partition offsets inconsistent at %d", p);
+            prev = so[p + 1];
+        }
+        m.out_bytes = so[s.R];
+    } else {
+        for (int32_t p = 0; p < s.R; ++p) m.lengths[(size_t)p] = ((int64_t)po[p + 1] - (int64_t)po[p]) * s.rb;
+        m.out_bytes = m.nrec * s.rb;
+    }
+    if (s.lz4_block > 0) {  // publish the LZ4-framed partition streams instead
+        // the source is this write's Kryo stream, named explicitly: `comp` may still hold an
+        // earlier attempt's frames
+        const void *src = m.ser_valid ? m.ser.p : m.data.p;
+        std::vector<int64_t> offs((size_t)s.R + 1, 0);
+        for (int32_t p = 0; p < s.R; ++p) offs[(size_t)p + 1] = offs[(size_t)p] + m.lengths[(size_t)p];
+        std::vector<int64_t> clen((size_t)s.R, 0);
+        m.comp_valid = false;
+        SGX_TRY(lz4_frame_impl(e, c, src, offs.data(), s.R, s.lz4_block, &m.comp, nullptr, 0, clen.data()));
+        int64_t total = 0;
+        for (int32_t p = 0; p < s.R; ++p) total += clen[(size_t)p];
+        m.lengths = clen;
+        m.out_bytes = total;
+        m.comp_valid = true;
+    }
+    m.ready = true;
+    return SGX_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// the map output slot of a (re-)attempt
+// ------------------------------------------------------------------------------------
+// A re-attempt of the same map replaces the previous output (the in-HBM analogue of the
+// index commit; the file commit keeps "first valid attempt wins", sgx_write_index).  The
+// slot's buffers are reused when nobody else holds the old output; otherwise (a reader or an
+// exchange round still references it) a fresh output takes the slot and the old one lives
+// until its last reference drops.  Returns with m->mu locked (lk).
+static int claim_slot(Shuffle &s, int64_t map_id, std::shared_ptr<MapOut> *pm, std::unique_lock<std::mutex> *lk) {
+    std::lock_guard<std::mutex> sl(s.mu);
+    std::shared_ptr<MapOut> &slot = s.maps[map_id];
+    if (!slot || slot.use_count() > 1) slot = std::make_shared<MapOut>();
+    *pm = slot;
+    *lk = std::unique_lock<std::mutex>(slot->mu);
+    return SGX_OK;
+}
+
+static void drop_slot(Shuffle &s, int64_t map_id, const std::shared_ptr<MapOut> &m) {
+    std::lock_guard<std::mutex> sl(s.mu);
+    auto it = s.maps.find(map_id);
+    if (it != s.maps.end() && it->second == m) s.maps.erase(it);
+}
+
+static int check_batch(const Shuffle &s, const void *records, int64_t n, int32_t rb, int32_t mem_kind) {
+    if (rb != s.rb) return fail_msg(SGX_ERR_INVALID, "record_bytes %d != registered %d", rb, s.rb);
+    if (n < 0 || n >= (int64_t)UINT32_MAX) return fail_msg(SGX_ERR_INVALID, "nrecords %lld out of range", (long long)n);
+    if (n > 0 && !records) return fail_msg(SGX_ERR_INVALID, "records is NULL");
+    if (mem_kind != SGX_MEM_HOST && mem_kind != SGX_MEM_DEVICE)
+        return fail_msg(SGX_ERR_INVALID, "unknown mem_kind %d", mem_kind);
+    return SGX_OK;
+}
+
+// device pointer of a batch (host batches are staged through the context's buffer)
+static int device_input(Ctx &c, const void *records, int64_t bytes, int32_t mem_kind, const void **in) {
+    *in = records;
+    if (mem_kind == SGX_MEM_HOST && bytes > 0) {
+        SGX_TRY(c.input_stage.ensure((size_t)bytes));
+        HIP_TRY(hipMemcpyAsync(c.input_stage.p, records, (size_t)bytes, hipMemcpyHostToDevice, c.st));
+        *in = c.input_stage.p;
+    }
+    return SGX_OK;
+}
+
+extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records,
+                             int64_t n, int32_t rb, int32_t mem_kind, int64_t *out_lengths) {
+    if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
+    std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
+    if (!s) return SGX_ERR_STATE;
+    SGX_TRY(check_batch(*s, records, n, rb, mem_kind));
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    std::shared_ptr<MapOut> m;
+    std::unique_lock<std::mutex> lk;
+    SGX_TRY(claim_slot(*s, map_id, &m, &lk));
+    // the previous attempt's kernels and any all-to-all still reading its bytes come first
+    HIP_TRY(m->done.wait_host());
+    if (m->read_done.ev) HIP_TRY(hipStreamWaitEvent(c->st, m->read_done.ev, 0));
+    m->written = false;
+    m->open = false;
+    m->spills.clear();
+    SGX_TRY(m->part_off.ensure((size_t)(s->R + 2) * 4));
+    const void *in = nullptr;
+    int rc = device_input(*c, records, n * rb, mem_kind, &in);
+    if (rc == SGX_OK) rc = run_map_pipeline(e, *c, *s, *m, in, n, false, nullptr);
+    if (rc == SGX_OK && out_lengths) {
+        rc = finish_lengths(e, *c, *s, *m);
+        if (rc == SGX_OK) std::memcpy(out_lengths, m->lengths.data(), sizeof(int64_t) * (size_t)s->R);
+    }
+    if (rc != SGX_OK && !m->written) {
+        lk.unlock();
+        drop_slot(*s, map_id, m);
+    }
+    return rc;
+}
+
+// ------------------------------------------------------------------------------------
+// streaming map outputs
+// ------------------------------------------------------------------------------------
+extern "C" int sgx_map_begin(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
+    if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
+    std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
+    if (!s) return SGX_ERR_STATE;
+    HIP_TRY(hipSetDevice(e->device));
+    std::shared_ptr<MapOut> m;
+    std::unique_lock<std::mutex> lk;
+    SGX_TRY(claim_slot(*s, map_id, &m, &lk));
+    HIP_TRY(m->done.wait_host());
+    if (m->read_done.ev) HIP_TRY(m->read_done.wait_host());
+    m->written = false;
+    m->ready = false;
+    m->open = true;
+    m->spills.clear();
+    return SGX_OK;
+}
+
+extern "C" int sgx_map_append(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records, int64_t n,
+                              int32_t rb, int32_t mem_kind) {
+    if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
+    std::shared_ptr<Shuffle> s;
+    std::shared_ptr<MapOut> m;
+    SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
+    SGX_TRY(check_batch(*s, records, n, rb, mem_kind));
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (!m->open) return fail_msg(SGX_ERR_STATE, "map %lld of shuffle %d is not open (sgx_map_begin)",
+                                  (long long)map_id, shuffle_id);
+    std::unique_ptr<Spill> sp(new Spill());
+    sp->nrec = n;
+    const void *in = nullptr;
+    SGX_TRY(device_input(*c, records, n * rb, mem_kind, &in));
+    SGX_TRY(sp->data.ensure((size_t)std::max<int64_t>(n * rb, 16)));
+    SGX_TRY(m->part_off.ensure((size_t)(s->R + 2) * 4));
+    uint32_t *po = (uint32_t *)m->part_off.p;
+    SGX_TRY(partition_pass(e, *c, in, sp->data.p, n, rb, s->pp, s->R, s->kind, po, nullptr, true));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    if (po[s->R + 1] != 0 || (int64_t)po[s->R] != n)
+        return fail_msg(SGX_ERR_HIP, "internal error: batch partition pass failed (flag %u)", po[s->R + 1]);
+    sp->lengths.resize((size_t)s->R);
+    for (int32_t p = 0; p < s->R; ++p) sp->lengths[(size_t)p] = (int64_t)po[p + 1] - po[p];  // records
+    m->spills.push_back(std::move(sp));
+    return SGX_OK;
+}
+
+extern "C" int sgx_map_commit(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *out_lengths) {
+    if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
+    std::shared_ptr<Shuffle> s;
+    std::shared_ptr<MapOut> m;
+    SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    std::lock_guard<std::mutex> lk(m->mu);
+    if (!m->open) return fail_msg(SGX_ERR_STATE, "map %lld of shuffle %d is not open", (long long)map_id, shuffle_id);
+    const int32_t R = s->R;
+    const int rb = s->rb;
+    int64_t total = 0;
+    for (auto &sp : m->spills) total += sp->nrec;
+    if (total >= (int64_t)UINT32_MAX)
+        return fail_msg(SGX_ERR_INVALID, "map %lld holds %lld records (>= 2^32)", (long long)map_id, (long long)total);
+    // merged partition offsets (records): partition-major, batches in append order
+    SGX_TRY(m->part_off.ensure((size_t)(R + 2) * 4));
+    uint32_t *po = (uint32_t *)m->part_off.p;
+    std::vector<int64_t> items;
+    int64_t off = 0;
+    std::vector<int64_t> bo(m->spills.size(), 0);  // running offset inside each batch
+    for (int32_t p = 0; p < R; ++p) {
+        po[p] = (uint32_t)off;
+        for (size_t b = 0; b < m->spills.size(); ++b) {
+            const int64_t cnt = m->spills[b]->lengths[(size_t)p];
+            const int64_t bytes = cnt * rb;
+            for (int64_t d = 0; d < bytes; d += 65536) {
+                items.push_back((int64_t)(uintptr_t)((char *)m->spills[b]->data.p + bo[b] * rb + d));
+                items.push_back(off * rb + d);  // destination offset, rebased below
+                items.push_back(std::min<int64_t>(65536, bytes - d));
+            }
+            bo[b] += cnt;
+            off += cnt;
+        }
+    }
+    po[R] = (uint32_t)off;
+    po[R + 1] = 0;
+    // the merged records, then the usual pipeline on an already partitioned map
+    SGX_TRY(m->data.ensure((size_t)std::max<int64_t>(total * rb, 16)));
+    m->nrec = total;
+    const int64_t nitems = (int64_t)items.size() / 3;
+    for (int64_t i = 0; i < nitems; ++i) items[3 * i + 1] += (int64_t)(uintptr_t)m->data.p;
+    if (nitems > 0) {
+        SGX_TRY(c->gather_items.ensure((size_t)nitems * 24));
+        SGX_TRY(c->items_dev.ensure((size_t)nitems * 24));
+        std::memcpy(c->gather_items.p, items.data(), (size_t)nitems * 24);
+        HIP_TRY(hipMemcpyAsync(c->items_dev.p, c->gather_items.p, (size_t)nitems * 24, hipMemcpyHostToDevice, c->st));
+        HIP_TRY(launch_gather_items((const int64_t *)c->items_dev.p, nitems, rb % 16 == 0 ? 16 : 4, c->st));
+    }
+    // device copy of the merged offsets (the Kryo framing reads them)
+    SGX_TRY(c->work.ensure((size_t)(R + 2) * 4));
+    HIP_TRY(hipMemcpyAsync(c->work.p, po, (size_t)(R + 2) * 4, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));  // the pinned offsets are rewritten by the pipeline
+    m->open = false;
+    SGX_TRY(run_map_pipeline(e, *c, *s, *m, m->data.p, total, true, (const uint32_t *)c->work.p));
+    m->spills.clear();
+    if (out_lengths) {
+        SGX_TRY(finish_lengths(e, *c, *s, *m));
+        std::memcpy(out_lengths, m->lengths.data(), sizeof(int64_t) * (size_t)R);
+    }
+    return SGX_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// lengths / data
+// ------------------------------------------------------------------------------------
+extern "C" int sgx_map_lengths(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *out) {
+    if (!e || !out) return fail_msg(SGX_ERR_INVALID, "NULL argument");
+    std::shared_ptr<Shuffle> s;
+    std::shared_ptr<MapOut> m;
+    SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    std::lock_guard<std::mutex> lk(m->mu);
+    SGX_TRY(finish_lengths(e, *c, *s, *m));
+    std::memcpy(out, m->lengths.data(), sizeof(int64_t) * (size_t)s->R);
+    return SGX_OK;
+}
+
+extern "C" int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, void **ptr, int64_t *bytes) {
+    if (!e || !ptr || !bytes) return fail_msg(SGX_ERR_INVALID, "NULL argument");
+    std::shared_ptr<Shuffle> s;
+    std::shared_ptr<MapOut> m;
+    SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    std::lock_guard<std::mutex> lk(m->mu);
+    SGX_TRY(finish_lengths(e, *c, *s, *m));
+    *ptr = const_cast<void *>(m->view());
+    *bytes = m->out_bytes;
+    return SGX_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// IndexShuffleBlockResolver.writeIndexFileAndCommit (IndexShuffleBlockResolver.scala:161-217)
+// ------------------------------------------------------------------------------------
+extern "C" int sgx_write_index(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const char *index_path,
+                               const char *data_path, int64_t *out_lengths) {
+    if (!e || !index_path || !data_path) return fail_msg(SGX_ERR_INVALID, "NULL argument");
+    std::shared_ptr<Shuffle> s;
+    std::shared_ptr<MapOut> m;
+    SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    std::lock_guard<std::mutex> lk(m->mu);
+    SGX_TRY(finish_lengths(e, *c, *s, *m));
+    std::vector<uint8_t> host((size_t)m->out_bytes);
+    if (m->out_bytes) HIP_TRY(hipMemcpy(host.data(), m->view(), (size_t)m->out_bytes, hipMemcpyDeviceToHost));
+    return commit_index_files(index_path, data_path, s->R, m->lengths.data(), host.data(), m->out_bytes, out_lengths);
+}

@@ -1,0 +1,478 @@
+// sgx_read.cpp — the reduce side: ShuffleTransport.fetchBlocksByBlockIds
+// (ucx/ShuffleTransport.scala:154-156) / BlockStoreClient.fetchBlocks
+// (spark_3_0/UcxShuffleClient.scala:49-91) served from HBM, and what UcxShuffleReader.read
+// does after the fetch (spark_3_0/UcxShuffleReader.scala:137-191): deserialize (Kryo, LZ4),
+// sort by key (keyOrdering), group / sum (aggregator).
+#include "sgx_engine.h"
+
+#include <algorithm>
+#include <cstring>
+
+using namespace sgx;
+
+static constexpr int64_t ITEM_BYTES = 64 * 1024;
+
+// ------------------------------------------------------------------------------------
+// fetchBlocksByBlockIds
+// ------------------------------------------------------------------------------------
+int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, const int32_t *reduce_ids, int64_t n,
+                    void *dst, int64_t dst_cap, int32_t dst_mem_kind, int64_t *out_lengths, bool sync,
+                    std::vector<std::shared_ptr<void>> *keep) {
+    struct Src {
+        const void *p;
+        int64_t len;
+        hipEvent_t ready;
+    };
+    // snapshot the shuffle's rounds and the maps asked for (references keep them alive)
+    std::vector<std::shared_ptr<Round>> rounds;
+    std::map<int64_t, std::shared_ptr<MapOut>> maps;
+    {
+        std::lock_guard<std::mutex> lk(s.mu);
+        rounds = s.rounds;
+        for (int64_t i = 0; i < n; ++i) {
+            auto mt = s.maps.find(map_ids[i]);
+            if (mt != s.maps.end()) maps[map_ids[i]] = mt->second;
+        }
+    }
+    std::map<int64_t, std::vector<int64_t>> map_off;  // per local map: partition byte offsets
+    std::vector<Src> srcs((size_t)n);
+    int64_t total = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const int64_t mid = map_ids[i];
+        const int32_t r = reduce_ids[i];
+        if (r < 0 || r >= s.R) return fail_msg(SGX_ERR_INVALID, "reduceId %d out of range [0, %d)", r, s.R);
+        bool found = false;
+        // received blocks (newest round first)
+        for (auto rt = rounds.rbegin(); rt != rounds.rend() && !found; ++rt) {
+            Round &rd = **rt;
+            if (r < rd.r0 || r >= rd.r1) continue;
+            for (size_t j = 0; j < rd.map_ids.size(); ++j) {
+                if (rd.map_ids[j] != mid) continue;
+                const int32_t nmine = rd.r1 - rd.r0;
+                srcs[(size_t)i] = Src{(const char *)rd.base() + rd.block_off[j * (size_t)nmine + (size_t)(r - rd.r0)],
+                                      rd.lens[j * (size_t)s.R + (size_t)r], rd.done.ev};
+                found = true;
+                break;
+            }
+        }
+        if (!found) {
+            auto mt = maps.find(mid);
+            if (mt != maps.end()) {
+                MapOut &m = *mt->second;
+                auto ot = map_off.find(mid);
+                if (ot == map_off.end()) {
+                    std::lock_guard<std::mutex> lk(m.mu);
+                    if (m.open) return fail_msg(SGX_ERR_STATE, "map %lld is still open", (long long)mid);
+                    SGX_TRY(finish_lengths(e, c, s, m));
+                    std::vector<int64_t> o((size_t)s.R + 1, 0);
+                    for (int32_t q = 0; q < s.R; ++q) o[(size_t)q + 1] = o[(size_t)q] + m.lengths[(size_t)q];
+                    ot = map_off.emplace(mid, std::move(o)).first;
+                }
+                srcs[(size_t)i] = Src{(const char *)m.view() + ot->second[(size_t)r],
+                                      ot->second[(size_t)r + 1] - ot->second[(size_t)r], m.done.ev};
+                found = true;
+            }
+        }
+        if (!found)
+            return fail_msg(SGX_ERR_NOT_FOUND, "shuffle_%d_%lld_%d is not registered", s.id, (long long)mid, r);
+        out_lengths[i] = srcs[(size_t)i].len;
+        total += srcs[(size_t)i].len;
+    }
+    if (total > dst_cap)
+        return fail_msg(SGX_ERR_INVALID, "destination capacity %lld < %lld bytes", (long long)dst_cap, (long long)total);
+    if (total > 0 && !dst) return fail_msg(SGX_ERR_INVALID, "dst is NULL");
+    if (total == 0) return SGX_OK;
+    hipStream_t st = c.st;
+    // every source must be complete: wait on each distinct producer event once
+    std::vector<hipEvent_t> waited;
+    for (int64_t i = 0; i < n; ++i) {
+        hipEvent_t ev = srcs[(size_t)i].ready;
+        if (ev && std::find(waited.begin(), waited.end(), ev) == waited.end()) {
+            HIP_TRY(hipStreamWaitEvent(st, ev, 0));
+            waited.push_back(ev);
+        }
+    }
+    // one gather launch: {src, dst, bytes} pieces of <= 64 KiB, back to back in request
+    // order (the reader asks reducer-major, map-minor: the canonical per-reducer sequence)
+    const bool dev_dst = dst_mem_kind == SGX_MEM_DEVICE;
+    char *gdst = (char *)dst;
+    if (!dev_dst) {
+        SGX_TRY(c.gather_stage.ensure((size_t)total));
+        gdst = (char *)c.gather_stage.p;
+    }
+    int64_t npieces = 0;
+    for (int64_t i = 0; i < n; ++i) npieces += (srcs[(size_t)i].len + ITEM_BYTES - 1) / ITEM_BYTES;
+    SGX_TRY(c.gather_items.ensure((size_t)npieces * 24));
+    SGX_TRY(c.items_dev.ensure((size_t)npieces * 24));
+    // the pinned item list is rewritten only after the previous gather's copy has landed
+    HIP_TRY(hipStreamSynchronize(st));
+    int64_t *gi = (int64_t *)c.gather_items.p, k = 0, off = 0;
+    bool al16 = ((uintptr_t)gdst & 15) == 0, al4 = ((uintptr_t)gdst & 3) == 0;
+    for (int64_t i = 0; i < n; ++i) {
+        const char *sp = (const char *)srcs[(size_t)i].p;
+        for (int64_t done = 0; done < srcs[(size_t)i].len; done += ITEM_BYTES, ++k) {
+            const int64_t b = std::min<int64_t>(ITEM_BYTES, srcs[(size_t)i].len - done);
+            gi[3 * k] = (int64_t)(uintptr_t)(sp + done);
+            gi[3 * k + 1] = (int64_t)(uintptr_t)(gdst + off + done);
+            gi[3 * k + 2] = b;
+            const uintptr_t bits = (uintptr_t)(sp + done) | (uintptr_t)(off + done) | (uintptr_t)b;
+            al16 = al16 && (bits & 15) == 0;
+            al4 = al4 && (bits & 3) == 0;
+        }
+        off += srcs[(size_t)i].len;
+    }
+    hipEvent_t g0 = e->ev(), g1 = e->ev();
+    HIP_TRY(hipEventRecord(g0, st));
+    HIP_TRY(hipMemcpyAsync(c.items_dev.p, gi, (size_t)npieces * 24, hipMemcpyHostToDevice, st));
+    HIP_TRY(launch_gather_items((const int64_t *)c.items_dev.p, npieces, al16 ? 16 : al4 ? 4 : 1, st));
+    HIP_TRY(hipEventRecord(g1, st));
+    e->record_stage(SGX_STAGE_REGROUP, g0, g1);
+    if (!dev_dst) HIP_TRY(hipMemcpyAsync(dst, gdst, (size_t)total, hipMemcpyDeviceToHost, st));
+    if (keep) {
+        for (auto &r : rounds) keep->push_back(r);
+        for (auto &kv : maps) keep->push_back(kv.second);
+    }
+    if (sync) HIP_TRY(hipStreamSynchronize(st));
+    return SGX_OK;
+}
+
+extern "C" int sgx_fetch_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids,
+                                const int32_t *reduce_ids, int64_t n, void *dst, int64_t dst_cap,
+                                int32_t dst_mem_kind, int64_t *out_lengths) {
+    if (!e || (n > 0 && (!map_ids || !reduce_ids || !out_lengths))) return fail_msg(SGX_ERR_INVALID, "NULL argument");
+    std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
+    if (!s) return SGX_ERR_STATE;
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    return fetch_impl(e, *c, *s, map_ids, reduce_ids, n, dst, dst_cap, dst_mem_kind, out_lengths, true, nullptr);
+}
+
+// ------------------------------------------------------------------------------------
+// records of a partition range (deserialized), sorting, grouping
+// ------------------------------------------------------------------------------------
+// The canonical block list of reducers [r0, r1) x maps: reducer-major, map order as given.
+static void canonical_blocks(const int64_t *map_ids, int64_t nmaps, int32_t r0, int32_t r1, std::vector<int64_t> &mids,
+                             std::vector<int32_t> &rids) {
+    const int64_t nreq = (int64_t)(r1 - r0) * nmaps;
+    mids.resize((size_t)nreq);
+    rids.resize((size_t)nreq);
+    for (int32_t r = r0; r < r1; ++r)
+        for (int64_t j = 0; j < nmaps; ++j) {
+            mids[(size_t)((r - r0) * nmaps + j)] = map_ids[j];
+            rids[(size_t)((r - r0) * nmaps + j)] = r;
+        }
+}
+
+// Gather the canonical blocks of reducers [r0, r1) x maps into c.sort_buf[0] as records (a
+// Kryo shuffle's stream -- LZ4-decompressed first when compressed -- is decoded on the GPU on
+// the way); c.sort_buf[1] is sized to match.  *nrec = records.  Synchronous.
+static int records_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, int64_t nmaps, int32_t r0,
+                        int32_t r1, int64_t *nrec) {
+    if (r0 < 0 || r1 > s.R || r0 > r1)
+        return fail_msg(SGX_ERR_INVALID, "partition range [%d, %d) outside [0, %d)", r0, r1, s.R);
+    if (nmaps < 0 || (nmaps > 0 && !map_ids)) return fail_msg(SGX_ERR_INVALID, "bad map list");
+    const int rb = s.rb;
+    std::vector<int64_t> mids, lens;
+    std::vector<int32_t> rids;
+    canonical_blocks(map_ids, nmaps, r0, r1, mids, rids);
+    const int64_t nreq = (int64_t)mids.size();
+    lens.resize((size_t)nreq);
+    std::vector<std::shared_ptr<void>> keep;
+    // size query (fails with SGX_ERR_INVALID on capacity, after filling the lengths)
+    int rc = fetch_impl(e, c, s, mids.data(), rids.data(), nreq, nullptr, 0, SGX_MEM_DEVICE, lens.data(), false, nullptr);
+    if (rc != SGX_OK && rc != SGX_ERR_INVALID) return rc;
+    int64_t total = 0;
+    for (int64_t L : lens) total += L;
+    hipStream_t st = c.st;
+    if (s.ser == SGX_SER_KRYO) {
+        // the fetched Kryo stream (blocks back to back are one valid stream) -> records
+        *nrec = 0;
+        if (s.lz4_block > 0 && total > 0) {
+            // a compressed shuffle: fetch the LZ4 frames, decompress them into the Kryo input
+            // (LZ4BlockInputStream, same stream, so no host round trip between the two)
+            SGX_TRY(c.fetch_tmp.ensure((size_t)total));
+            SGX_TRY(fetch_impl(e, c, s, mids.data(), rids.data(), nreq, c.fetch_tmp.p, total, SGX_MEM_DEVICE,
+                               lens.data(), false, &keep));
+            int64_t dec = 0;
+            SGX_TRY(lz4_unframe_impl(e, c, c.fetch_tmp.p, total, &c.kryo_in, nullptr, 0, &dec));
+            total = dec;
+        }
+        const int64_t cap = total / 4;  // a record takes >= 4 bytes
+        SGX_TRY(c.sort_buf[0].ensure((size_t)cap * 16));
+        if (total == 0) return SGX_OK;
+        if (s.lz4_block == 0) {
+            SGX_TRY(c.kryo_in.ensure((size_t)total + 64));
+            SGX_TRY(fetch_impl(e, c, s, mids.data(), rids.data(), nreq, c.kryo_in.p, total, SGX_MEM_DEVICE,
+                               lens.data(), false, &keep));
+        }
+        const int64_t tiles = kryo_deser16_tiles(total);
+        SGX_TRY(c.kryo_work.ensure(24 + (size_t)kryo_work_bytes(tiles)));
+        HIP_TRY(hipMemsetAsync(c.kryo_work.p, 0, 24, st));  // error word, record count
+        uint32_t *tick = (uint32_t *)c.kryo_work.p;
+        int64_t *cnt_dev = (int64_t *)((char *)c.kryo_work.p + 16);
+        uint64_t *status = (uint64_t *)((char *)c.kryo_work.p + 24);
+        hipEvent_t k0 = e->ev(), k1 = e->ev();
+        HIP_TRY(hipEventRecord(k0, st));
+        HIP_TRY(launch_kryo_deser16(c.kryo_in.p, total, c.sort_buf[0].p, cap, status, tick, cnt_dev, st));
+        HIP_TRY(hipEventRecord(k1, st));
+        e->record_stage(SGX_STAGE_DESERIALIZE, k0, k1);
+        uint32_t herr[4];
+        int64_t hcnt = 0;
+        HIP_TRY(hipMemcpyAsync(herr, tick, 16, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(&hcnt, cnt_dev, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (herr[1] & 1u) return fail_msg(SGX_ERR_TIMEOUT, "Kryo decoder look-back spin gave up");
+        if (herr[1] & 2u) return fail_msg(SGX_ERR_INVALID, "fetched blocks are not a Kryo stream of (Long, Long) pairs");
+        if (hcnt < 0 || hcnt > cap) return fail_msg(SGX_ERR_HIP, "internal error: Kryo record count %lld", (long long)hcnt);
+        if (hcnt >= (int64_t)INT32_MAX) return fail_msg(SGX_ERR_INVALID, "%lld records exceed one read", (long long)hcnt);
+        *nrec = hcnt;
+        SGX_TRY(c.sort_buf[1].ensure((size_t)hcnt * 16));
+        return SGX_OK;
+    }
+    const int64_t n = total / rb;
+    if (n >= (int64_t)INT32_MAX) return fail_msg(SGX_ERR_INVALID, "%lld records exceed one sorted read", (long long)n);
+    *nrec = n;
+    SGX_TRY(c.sort_buf[0].ensure((size_t)total));
+    SGX_TRY(c.sort_buf[1].ensure((size_t)total));
+    if (n == 0) return SGX_OK;
+    SGX_TRY(fetch_impl(e, c, s, mids.data(), rids.data(), nreq, c.sort_buf[0].p, total, SGX_MEM_DEVICE, lens.data(),
+                       false, &keep));
+    HIP_TRY(hipStreamSynchronize(st));  // `keep` holds the sources until here
+    return SGX_OK;
+}
+
+// Stable sort of the n records in c.sort_buf[0]: LSD digit passes that are the map side's
+// own K1-K4 with an internal digit partitioner (R = 256, KIND_DIGIT), least significant byte
+// first -- i64 keys (bytes 0..7, the top byte sign-flipped) or TeraSort's 10-byte big-endian
+// keys (bytes 9..0) -- then, with `by_partition`, one pass by the shuffle's partitioner
+// (skipped for an ascending RangePartitioner, whose partition order is key order).  One read
+// of the keys histograms every digit; a digit with a single non-empty bucket is the identity
+// permutation and is skipped (unless SGX_FLAG_SORT_ALL_DIGITS).
+int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool by_partition, const void **sorted) {
+    const int rb = s.rb;
+    if (rb != 16 && rb != 100)
+        return fail_msg(SGX_ERR_UNSUPPORTED, "sorted read needs 16 B (Long, Long) or 100 B TeraSort records, not %d B",
+                        rb);
+    *sorted = c.sort_buf[0].p;
+    if (n == 0) return SGX_OK;
+    hipStream_t st = c.st;
+    constexpr int MAXP = 12;
+    SGX_TRY(c.sort_err.ensure(MAXP * 4));
+    HIP_TRY(hipMemsetAsync(c.sort_err.p, 0, MAXP * 4, st));
+    uint32_t *errs = (uint32_t *)c.sort_err.p;
+    hipEvent_t t0 = e->ev(), t1 = e->ev();
+    HIP_TRY(hipEventRecord(t0, st));
+    const int ndig = rb == 16 ? 8 : 10;
+    SGX_TRY(c.digit_hist.ensure((size_t)ndig * 256 * 4));
+    HIP_TRY(launch_digit_hist(c.sort_buf[0].p, n, rb, (uint32_t *)c.digit_hist.p, e->num_cus, st));
+    std::vector<uint32_t> dh((size_t)ndig * 256);
+    HIP_TRY(hipMemcpyAsync(dh.data(), c.digit_hist.p, dh.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    const bool skip = !(e->flags & SGX_FLAG_SORT_ALL_DIGITS);
+    int cur = 0, np = 0;
+    for (int d = 0; d < ndig; ++d) {
+        const int byte = rb == 16 ? d : 9 - d;  // digit d of the LSD order
+        bool trivial = false;
+        for (int b = 0; b < 256; ++b)
+            if (dh[(size_t)byte * 256 + (size_t)b] == (uint32_t)n) trivial = true;
+        if (trivial && skip) continue;
+        ++np;
+        PartParams dp{};
+        dp.kind = KIND_DIGIT;
+        dp.R = DIGIT_R;
+        dp.nbits = 8;
+        dp.dshift = rb == 16 ? 8u * (uint32_t)d : 8u * (uint32_t)(9 - d);
+        dp.dflip = (rb == 16 && d == 7) ? 0x80u : 0u;
+        SGX_TRY(partition_pass(e, c, c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, dp, (int32_t)DIGIT_R, KIND_DIGIT,
+                               nullptr, errs + np - 1, false));
+        cur ^= 1;
+    }
+    const bool range_asc = s.kind != SGX_PART_HASH && s.asc;
+    if (by_partition && !range_asc && s.R > 1) {
+        SGX_TRY(partition_pass(e, c, c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, s.pp, s.R, s.kind, nullptr,
+                               errs + np, false));
+        cur ^= 1;
+        ++np;
+    }
+    HIP_TRY(hipEventRecord(t1, st));
+    e->record_stage(SGX_STAGE_SORT, t0, t1);
+    uint32_t herr[MAXP];
+    HIP_TRY(hipMemcpyAsync(herr, c.sort_err.p, MAXP * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    for (int i = 0; i < np; ++i) {
+        if (herr[i] & 1u) return fail_msg(SGX_ERR_TIMEOUT, "sort pass %d: scan look-back spin gave up", i);
+        if (herr[i] & 2u) return fail_msg(SGX_ERR_HIP, "sort pass %d: a scatter destination was out of range", i);
+    }
+    *sorted = c.sort_buf[cur].p;
+    return SGX_OK;
+}
+
+int sgx::group_records(sgx_engine *e, Ctx &c, const void *sorted, int64_t n, int32_t agg, int64_t *ngroups,
+                       int64_t **keys, int64_t **starts, int64_t **vals) {
+    hipStream_t st = c.st;
+    *ngroups = 0;
+    // group ids: flags of key changes, exclusive scan (K3 with one partition: offs[i] is the
+    // group of record i minus its flag; part_off[1] the group count)
+    const int64_t tiles = scan_tiles(n);
+    SGX_TRY(c.grp_flags.ensure((size_t)std::max<int64_t>(n, 1) * 4));
+    SGX_TRY(c.grp_offs.ensure((size_t)std::max<int64_t>(n, 1) * 4));
+    SGX_TRY(c.grp_status.ensure((size_t)(16 + tiles * 8 + 16)));
+    uint32_t *ticket_err = (uint32_t *)c.grp_status.p;
+    uint32_t *gcount = (uint32_t *)((char *)c.grp_status.p + 16 + tiles * 8);  // [0, total]
+    hipEvent_t t0 = e->ev(), t1 = e->ev();
+    HIP_TRY(hipEventRecord(t0, st));
+    int64_t ng = 0;
+    if (n > 0) {
+        HIP_TRY(hipMemsetAsync(c.grp_status.p, 0, (size_t)(16 + tiles * 8 + 16), st));
+        HIP_TRY(launch_group_flags(sorted, n, (uint32_t *)c.grp_flags.p, st));
+        HIP_TRY(launch_scan((const uint32_t *)c.grp_flags.p, (uint32_t *)c.grp_offs.p, n,
+                            (uint64_t *)((char *)c.grp_status.p + 16), ticket_err, ticket_err + 1, gcount, (int)n, 1,
+                            st));
+        uint32_t h[2] = {0, 0}, terr[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(h, gcount, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(terr, ticket_err, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        if (terr[1] & 1u) return fail_msg(SGX_ERR_TIMEOUT, "group scan look-back spin gave up");
+        ng = h[1];
+    }
+    const int64_t nvals = agg == SGX_AGG_GROUP ? n : ng;
+    SGX_TRY(c.grp_out.ensure((size_t)std::max<int64_t>(ng * 16 + nvals * 8, 16)));
+    int64_t *dkeys = (int64_t *)c.grp_out.p, *dstarts = dkeys + ng, *dvals = dstarts + ng;
+    if (n > 0) {
+        HIP_TRY(launch_group_emit(sorted, n, (const uint32_t *)c.grp_flags.p, (const uint32_t *)c.grp_offs.p, dkeys,
+                                  dstarts, agg == SGX_AGG_GROUP ? dvals : nullptr, st));
+        if (agg == SGX_AGG_SUM) {
+            SGX_TRY(c.grp_prefix.ensure((size_t)(n + prefix64_blocks(n)) * 8));
+            uint64_t *P = (uint64_t *)c.grp_prefix.p, *bsum = P + n;
+            HIP_TRY(launch_group_sums(sorted, n, dstarts, ng, bsum, P, dvals, st));
+        }
+    }
+    HIP_TRY(hipEventRecord(t1, st));
+    e->record_stage(SGX_STAGE_GROUP, t0, t1);
+    *ngroups = ng;
+    *keys = dkeys;
+    if (starts) *starts = dstarts;
+    *vals = dvals;
+    return SGX_OK;
+}
+
+static int copy_out(Ctx &c, void *dst, const void *src, int64_t bytes, int32_t mem_kind) {
+    if (bytes <= 0) return SGX_OK;
+    HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes,
+                           mem_kind == SGX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c.st));
+    return SGX_OK;
+}
+
+// Common entry checks of the reads; *s and *c on success.
+static int read_entry(sgx_engine *e, int32_t shuffle_id, int32_t mem_kind, std::shared_ptr<Shuffle> *s, Ctx **c) {
+    if (mem_kind != SGX_MEM_HOST && mem_kind != SGX_MEM_DEVICE) return fail_msg(SGX_ERR_INVALID, "unknown mem_kind %d", mem_kind);
+    *s = e->find_shuffle(shuffle_id);
+    if (!*s) return SGX_ERR_STATE;
+    HIP_TRY(hipSetDevice(e->device));
+    *c = e->ctx();
+    return *c ? SGX_OK : SGX_ERR_HIP;
+}
+
+extern "C" int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
+                               int32_t start_partition, int32_t end_partition, void *dst, int64_t dst_cap,
+                               int32_t dst_mem_kind, int64_t *out_bytes) {
+    if (!e || !out_bytes) return fail_msg(SGX_ERR_INVALID, "NULL argument");
+    std::shared_ptr<Shuffle> s;
+    Ctx *c = nullptr;
+    SGX_TRY(read_entry(e, shuffle_id, dst_mem_kind, &s, &c));
+    const int rb = s->rb;
+    if (!dst && dst_cap == 0 && s->ser == SGX_SER_KRYO) {  // size query: decoded records
+        int64_t n = 0;
+        SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
+        *out_bytes = n * rb;
+        return SGX_OK;
+    }
+    if (!dst && dst_cap == 0) {  // size query: lengths only
+        if (start_partition < 0 || end_partition > s->R || start_partition > end_partition || nmaps < 0 ||
+            (nmaps > 0 && !map_ids))
+            return fail_msg(SGX_ERR_INVALID, "bad partition range or map list");
+        std::vector<int64_t> mids, lens;
+        std::vector<int32_t> rids;
+        canonical_blocks(map_ids, nmaps, start_partition, end_partition, mids, rids);
+        lens.resize(mids.size());
+        int rc = fetch_impl(e, *c, *s, mids.data(), rids.data(), (int64_t)mids.size(), nullptr, 0, SGX_MEM_DEVICE,
+                            lens.data(), false, nullptr);
+        if (rc != SGX_OK && rc != SGX_ERR_INVALID) return rc;
+        int64_t total = 0;
+        for (int64_t L : lens) total += L;
+        *out_bytes = total;
+        return SGX_OK;
+    }
+    int64_t n = 0;
+    SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
+    const void *sorted = nullptr;
+    SGX_TRY(sort_records(e, *c, *s, n, true, &sorted));
+    *out_bytes = n * rb;
+    if (n * rb > dst_cap)
+        return fail_msg(SGX_ERR_INVALID, "destination capacity %lld < %lld bytes", (long long)dst_cap,
+                        (long long)(n * rb));
+    if (n > 0 && !dst) return fail_msg(SGX_ERR_INVALID, "dst is NULL");
+    SGX_TRY(copy_out(*c, dst, sorted, n * rb, dst_mem_kind));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SGX_OK;
+}
+
+extern "C" int sgx_read_records(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
+                                int32_t start_partition, int32_t end_partition, void *dst, int64_t dst_cap,
+                                int32_t dst_mem_kind, int64_t *out_bytes) {
+    if (!e || !out_bytes) return fail_msg(SGX_ERR_INVALID, "NULL argument");
+    std::shared_ptr<Shuffle> s;
+    Ctx *c = nullptr;
+    SGX_TRY(read_entry(e, shuffle_id, dst_mem_kind, &s, &c));
+    const int rb = s->rb;
+    int64_t n = 0;
+    SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
+    *out_bytes = n * rb;
+    if (!dst && dst_cap == 0) return SGX_OK;  // size query
+    if (n * rb > dst_cap)
+        return fail_msg(SGX_ERR_INVALID, "destination capacity %lld < %lld bytes", (long long)dst_cap,
+                        (long long)(n * rb));
+    if (n > 0 && !dst) return fail_msg(SGX_ERR_INVALID, "dst is NULL");
+    SGX_TRY(copy_out(*c, dst, c->sort_buf[0].p, n * rb, dst_mem_kind));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SGX_OK;
+}
+
+extern "C" int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
+                                int32_t start_partition, int32_t end_partition, int32_t agg, int64_t *keys,
+                                int64_t *group_starts, int64_t *values, int64_t cap_groups, int64_t cap_values,
+                                int32_t mem_kind, int64_t *out_groups, int64_t *out_values) {
+    if (!e || !out_groups || !out_values) return fail_msg(SGX_ERR_INVALID, "NULL argument");
+    if (agg != SGX_AGG_GROUP && agg != SGX_AGG_SUM) return fail_msg(SGX_ERR_INVALID, "unknown aggregation %d", agg);
+    std::shared_ptr<Shuffle> s;
+    Ctx *c = nullptr;
+    SGX_TRY(read_entry(e, shuffle_id, mem_kind, &s, &c));
+    if (s->rb != 16)
+        return fail_msg(SGX_ERR_UNSUPPORTED, "grouped read needs 16 B (Long, Long) records, not %d B", s->rb);
+    // a map-side-combined shuffle holds combiners: only combineCombinersByKey (sum) applies
+    if (s->combine == SGX_AGG_SUM && agg != SGX_AGG_SUM)
+        return fail_msg(SGX_ERR_UNSUPPORTED, "shuffle %d was combined map-side (sum): read it with SGX_AGG_SUM",
+                        shuffle_id);
+    int64_t n = 0;
+    SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
+    const void *sorted = nullptr;
+    SGX_TRY(sort_records(e, *c, *s, n, true, &sorted));
+    int64_t ng = 0;
+    int64_t *dkeys = nullptr, *dstarts = nullptr, *dvals = nullptr;
+    SGX_TRY(group_records(e, *c, sorted, n, agg, &ng, &dkeys, &dstarts, &dvals));
+    const int64_t nvals = agg == SGX_AGG_GROUP ? n : ng;
+    *out_groups = ng;
+    *out_values = nvals;
+    if (!keys && cap_groups == 0 && cap_values == 0) return SGX_OK;  // size query
+    if (ng > cap_groups || nvals > cap_values)
+        return fail_msg(SGX_ERR_INVALID, "capacity (%lld groups, %lld values) < (%lld, %lld)", (long long)cap_groups,
+                        (long long)cap_values, (long long)ng, (long long)nvals);
+    if (n == 0) return SGX_OK;
+    if (!keys || !values || (agg == SGX_AGG_GROUP && !group_starts)) return fail_msg(SGX_ERR_INVALID, "NULL output array");
+    SGX_TRY(copy_out(*c, keys, dkeys, ng * 8, mem_kind));
+    if (group_starts) SGX_TRY(copy_out(*c, group_starts, dstarts, ng * 8, mem_kind));
+    SGX_TRY(copy_out(*c, values, dvals, nvals * 8, mem_kind));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    return SGX_OK;
+}

@@ -210,4 +210,20 @@ hipError_t launch_group_sums(const void *rec, int64_t n, const int64_t *starts, 
     return hipGetLastError();
 }
 
+// Map-side combine (reduceByKey's mapSideCombine = true): the combiners of one map task,
+// keys[g] and sums[g] of its groups, become 16 B (Long, Long) records again -- the map
+// output Spark writes after ExternalSorter.insertAll with an Aggregator.
+__global__ __launch_bounds__(RT) void k_pack_pairs(const int64_t *__restrict__ keys, const int64_t *__restrict__ vals,
+                                                   int64_t n, longlong2 *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * RT + threadIdx.x;
+    if (i < n) out[i] = make_longlong2(keys[i], vals[i]);
+}
+
+hipError_t launch_pack_pairs(const int64_t *keys, const int64_t *vals, int64_t n, void *out, hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pack_pairs, dim3((unsigned)((n + RT - 1) / RT)), dim3(RT), 0, st, keys, vals, n,
+                       (longlong2 *)out);
+    return hipGetLastError();
+}
+
 }  // namespace sgx

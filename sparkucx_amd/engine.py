@@ -81,12 +81,17 @@ class ShuffleEngine:
     RCCL communicator (the role CommonUcxShuffleManager.startUcxTransport plays,
     shuffle/ucx/CommonUcxShuffleManager.scala:67-100)."""
 
-    def __init__(self, device: int = 0, num_chunks: int = 0, scatter_waves: int = 0, scatter_items: int = 0):
-        cfg = (ctypes.c_int32 * 4)(device, num_chunks, scatter_waves, scatter_items)
+    def __init__(self, device: int = 0, num_chunks: int = 0, scatter_waves: int = 0, scatter_items: int = 0,
+                 hist_mode: int = _lib.HIST_ATOMIC, rank_mode: int = _lib.RANK_ORDERED, flags: int = 0,
+                 comm_timeout_ms: int = 0):
+        """sgx_config (include/sgx.h): kernel choices that change speed, never bytes."""
+        cfg = (ctypes.c_int32 * 8)(device, num_chunks, scatter_waves, scatter_items, hist_mode, rank_mode, flags,
+                                   comm_timeout_ms)
         h = ctypes.c_void_p()
         check(lib().sgx_create(ctypes.cast(cfg, ctypes.c_void_p), ctypes.byref(h)), "sgx_create")
         self.handle = h.value
         self.device = device
+        self._host_comm = None
 
     def close(self):
         if self.handle:
@@ -136,6 +141,15 @@ class ShuffleEngine:
             raise _lib.IllegalArgumentException(f"unknown codec {codec!r} (none, lz4)")
         check(lib().sgx_set_compression(self.handle, shuffle_id, codes[codec], block_size), "setCompression")
 
+    def set_map_side_combine(self, shuffle_id: int, agg: int = _lib.AGG_SUM):
+        """dep.mapSideCombine with a sum aggregator (reduceByKey): map outputs hold one
+        {key, sum} combiner per distinct key and partition."""
+        check(lib().sgx_set_map_side_combine(self.handle, shuffle_id, agg), "setMapSideCombine")
+
+    def release_thread(self):
+        """Free the calling thread's HIP stream and scratch (recreated on its next call)."""
+        check(lib().sgx_release_thread(self.handle), "release_thread")
+
     def unregister_shuffle(self, shuffle_id: int):
         check(lib().sgx_unregister_shuffle(self.handle, shuffle_id), "unregisterShuffle")
 
@@ -155,6 +169,25 @@ class ShuffleEngine:
             out_ptr = out.ctypes.data
         check(lib().sgx_write_map(self.handle, shuffle_id, map_id, ptr, nrecords, record_bytes, kind,
                                   out_ptr), "write_map")
+        return out
+
+    def map_begin(self, shuffle_id: int, map_id: int):
+        """Open a streaming map output (batches appended with map_append, merged by map_commit)."""
+        check(lib().sgx_map_begin(self.handle, shuffle_id, map_id), "map_begin")
+
+    def map_append(self, shuffle_id: int, map_id: int, records, nrecords: int, record_bytes: int):
+        ptr, nbytes, kind = buffer_arg(records)
+        if nrecords * record_bytes > nbytes:
+            raise _lib.IllegalArgumentException(
+                f"{nrecords} records of {record_bytes} B exceed the {nbytes} B buffer")
+        check(lib().sgx_map_append(self.handle, shuffle_id, map_id, ptr, nrecords, record_bytes, kind), "map_append")
+
+    def map_commit(self, shuffle_id: int, map_id: int, num_partitions: Optional[int] = None) -> Optional[np.ndarray]:
+        out = None
+        if num_partitions is not None:
+            out = np.empty(num_partitions, dtype=np.int64)
+        check(lib().sgx_map_commit(self.handle, shuffle_id, map_id, out.ctypes.data if out is not None else None),
+              "map_commit")
         return out
 
     def map_lengths(self, shuffle_id: int, map_id: int, num_partitions: int) -> np.ndarray:
@@ -183,14 +216,16 @@ class ShuffleEngine:
         offs = np.ascontiguousarray(part_offsets, dtype=np.int64)
         R = len(offs) - 1
         lens = np.empty(R, dtype=np.int64)
-        check(lib().sgx_lz4_frame_partitions(self.handle, stream_ptr or None, offs.ctypes.data, R, block_size,
-                                              None, 0, lens.ctypes.data), "lz4 frame (measure)")
-        total = int(lens.sum())
-        buf = self.alloc(max(total, 1))
+        # one compression pass into a bound-sized buffer: a frame is at most its 21-byte header
+        # plus the block (RAW when LZ4 does not shrink it), plus a 21-byte end mark per stream
+        plen = np.diff(offs)
+        nblk = (plen + block_size - 1) // block_size
+        bound = int((nblk * (21 + block_size) + np.where(plen > 0, 21, 0)).sum())
+        buf = self.alloc(max(bound, 1))
         try:
             check(lib().sgx_lz4_frame_partitions(self.handle, stream_ptr or None, offs.ctypes.data, R, block_size,
-                                                  buf.ptr, total, lens.ctypes.data), "lz4 frame")
-            return buf.to_numpy(total), lens
+                                                  buf.ptr, bound, lens.ctypes.data), "lz4 frame")
+            return buf.to_numpy(int(lens.sum())), lens
         finally:
             buf.free()
 
@@ -243,6 +278,15 @@ class ShuffleEngine:
             raise _lib.IllegalArgumentException("unique id must be 128 bytes")
         buf = ctypes.create_string_buffer(bytes(unique_id), 128)
         check(lib().sgx_comm_init(self.handle, nranks, rank, ctypes.cast(buf, ctypes.c_void_p)), "comm_init")
+
+    def comm_init_host(self, nranks: int, rank: int, collectives=None):
+        """Exchange over the host collective backend: ``collectives`` has allgather(bytes) and
+        alltoallv(bytes, send_counts, recv_counts) (default: torch.distributed's group)."""
+        from .hostcomm import HostCommBinding, TorchDistributedCollectives
+
+        binding = HostCommBinding(collectives if collectives is not None else TorchDistributedCollectives())
+        check(lib().sgx_comm_init_host(self.handle, nranks, rank, ctypes.byref(binding.struct)), "comm_init_host")
+        self._host_comm = binding  # the callbacks must outlive the engine's use of them
 
     def exchange(self, shuffle_id: int, map_id: int):
         check(lib().sgx_exchange(self.handle, shuffle_id, map_id), "exchange")

@@ -78,9 +78,9 @@ class RangePartitioner:
 
 @dataclass
 class Aggregator:
-    """Spark's Aggregator for the two reduce-side combines the engine runs on (Long, Long)
-    records (mapSideCombine = false): "group" = groupByKey (CompactBuffer append), "sum" =
-    reduceByKey(_ + _) on Long values (wrapping)."""
+    """Spark's Aggregator for the two combines the engine runs on (Long, Long) records:
+    "group" = groupByKey (CompactBuffer append; Spark builds it with mapSideCombine = false),
+    "sum" = reduceByKey(_ + _) on Long values (wrapping), with or without map-side combine."""
     kind: str = "group"
 
     def __post_init__(self):
@@ -96,8 +96,11 @@ _SERIALIZERS = {"fixed": _lib.SER_FIXED, "kryo": _lib.SER_KRYO,
 class ShuffleDependency:
     partitioner: object
     recordBytes: int = 16  # fixed-width record codec: 16 B (Long, Long) or 100 B TeraSort
-    aggregator: Optional[Aggregator] = None  # dep.aggregator (reduce side only)
+    aggregator: Optional[Aggregator] = None  # dep.aggregator
     keyOrdering: bool = False                # dep.keyOrdering: sort each reducer by key
+    # dep.mapSideCombine (reduceByKey's default is true): the writer combines per key before
+    # the shuffle (ExternalSorter.insertAll with the aggregator), the reader merges the
+    # combiners (combineCombinersByKey, UcxShuffleReader.scala:158-161)
     mapSideCombine: bool = False
     # dep.serializer: "fixed" = the engine's fixed-width record codec; "kryo" =
     # org.apache.spark.serializer.KryoSerializer with spark.shuffle.compress=false (the data
@@ -106,7 +109,13 @@ class ShuffleDependency:
 
     def __post_init__(self):
         if self.mapSideCombine:
-            raise UnsupportedOperationException("map-side combine is not part of the GPU path (SURVEY §8(a) a1)")
+            # Spark's own check (ShuffleDependency: "Map-side combine without Aggregator
+            # specified!")
+            if self.aggregator is None:
+                raise IllegalArgumentException("Map-side combine without Aggregator specified!")
+            if self.aggregator.kind != "sum" or self.recordBytes != 16:
+                raise UnsupportedOperationException(
+                    "map-side combine runs on the GPU for reduceByKey(_ + _) on (Long, Long) records")
         if self.serializer not in _SERIALIZERS:
             raise IllegalArgumentException(f"unknown serializer {self.serializer!r} (fixed, kryo)")
         if self.serializer == "kryo" and self.recordBytes != 16:
@@ -469,6 +478,27 @@ class UcxShuffleReader:
 # ---------------------------------------------------------------------------------------
 # The manager
 # ---------------------------------------------------------------------------------------
+_BYTE_UNITS = {"b": 1, "k": 1 << 10, "kb": 1 << 10, "m": 1 << 20, "mb": 1 << 20, "g": 1 << 30, "gb": 1 << 30,
+               "t": 1 << 40, "tb": 1 << 40, "p": 1 << 50, "pb": 1 << 50}
+_BYTE_RE = re.compile(r"^\s*([0-9]+)\s*([a-z]*)\s*$")
+
+
+def byte_string(value: str) -> int:
+    """JavaUtils.byteStringAs(value, ByteUnit.BYTE) -- how Spark reads a bytes conf such as
+    spark.io.compression.lz4.blockSize: a bare number is bytes, suffixes b/k/kb/m/mb/g/gb/t/tb/
+    p/pb (case-insensitive) scale by 1024."""
+    m = _BYTE_RE.match(str(value).lower())
+    if not m or m.group(2) not in ("",) + tuple(_BYTE_UNITS):
+        raise NumberFormatException(f"Size must be specified as bytes (b), kibibytes (k), mebibytes (m), "
+                                    f"gibibytes (g), tebibytes (t), or pebibytes(p). E.g. 50b, 100k, or 250m. "
+                                    f"Failed to parse byte string: {value}")
+    return int(m.group(1)) * (_BYTE_UNITS[m.group(2)] if m.group(2) else 1)
+
+
+class NumberFormatException(IllegalArgumentException):
+    """java.lang.NumberFormatException (an IllegalArgumentException) of byteStringAs."""
+
+
 
 
 class UcxShuffleManager:
@@ -499,15 +529,20 @@ class UcxShuffleManager:
         self.engine.register_shuffle(shuffleId, p.numPartitions, p.kind, bounds,
                                      getattr(p, "ascending", True), dependency.recordBytes,
                                      _SERIALIZERS[dependency.serializer])
-        # spark.shuffle.compress (Spark's default is true) with spark.io.compression.codec lz4:
-        # applied to Kryo shuffles, whose bytes are Spark's own; the fixed codec stays raw
-        if (self.conf.get("spark.shuffle.compress", "false").lower() == "true"
+        if dependency.mapSideCombine:
+            self.engine.set_map_side_combine(shuffleId, _lib.AGG_SUM)
+        # spark.shuffle.compress (Spark 3.0.1's default: true) with spark.io.compression.codec
+        # lz4 (the default): applied to Kryo shuffles, whose bytes are Spark's own; the fixed
+        # 16 B / 100 B record codec is the engine's own format and stays raw
+        if (self.conf.get("spark.shuffle.compress", "true").lower() == "true"
                 and _SERIALIZERS[dependency.serializer] == _lib.SER_KRYO):
             codec = self.conf.get("spark.io.compression.codec", "lz4").lower()
             if codec not in ("lz4", "org.apache.spark.io.lz4compressioncodec"):
                 raise UnsupportedOperationException(f"compression codec {codec!r}: only lz4 is on the GPU path")
-            bs = self.conf.get("spark.io.compression.lz4.blockSize", "32k").lower()
-            block = int(bs[:-1]) * 1024 if bs.endswith("k") else int(bs)
+            block = byte_string(self.conf.get("spark.io.compression.lz4.blockSize", "32k"))
+            if block > 32 * 1024:
+                raise UnsupportedOperationException(
+                    f"spark.io.compression.lz4.blockSize {block} B: the GPU codec takes blocks up to 32 KiB")
             self.engine.set_compression(shuffleId, "lz4", block)
             self._compressed.add(shuffleId)
         h = BaseShuffleHandle(shuffleId, dependency)

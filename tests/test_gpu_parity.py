@@ -130,35 +130,36 @@ GEOMETRIES = [(4, 16), (8, 16), (12, 10), (14, 9), (16, 7), (4, 12), (8, 8), (4,
 @pytest.mark.parametrize("rank", ["ordered", "match"])
 @pytest.mark.parametrize("waves,items", GEOMETRIES)
 @pytest.mark.parametrize("R", [7, 200, 1024, 1536, 4096])
-def test_every_staged_geometry(sgx_lib, oracle_lib, monkeypatch, waves, items, R, rank):
+def test_every_staged_geometry(sgx_lib, oracle_lib, waves, items, R, rank):
     """Every instantiated K4 geometry of both rankers (lane-ordered atomics, ballot/peer
     table), full tiles + a ragged tail, multiple chunks.  A (waves, items) pair the
     lane-ordered kernel lacks falls back to the match kernel, which is then re-tested."""
-    if rank == "match":
-        monkeypatch.setenv("SGX_RANK", "match")
+    rank_mode = sgx_lib.RANK_MATCH if rank == "match" else sgx_lib.RANK_ORDERED
     tile = waves * items * 64
     n = 5 * tile * 3 + tile // 3 + 7
     recs = oracle_lib.gen_uniform16(n, 0xC0FFEE + R)
-    with sgx_lib.ShuffleEngine(device=0, num_chunks=3, scatter_waves=waves, scatter_items=items) as e:
+    with sgx_lib.ShuffleEngine(device=0, num_chunks=3, scatter_waves=waves, scatter_items=items,
+                               rank_mode=rank_mode) as e:
         try:
             check_against_oracle(e, oracle_lib, recs, R)
         except sgx_lib.UnsupportedOperationException:  # geometry's LDS does not fit this R
             pytest.skip(f"geometry {waves}x{items} does not fit R={R}")
 
 
-@pytest.mark.parametrize("env", ["SGX_SCATTER_DMA=1", "SGX_SCATTER_DIRECT=816", "SGX_SCATTER_DIRECT=408",
-                                 "SGX_SCATTER_CHAIN=816", "SGX_SCATTER_CHAIN=1607", "SGX_NO_PEER_TABLE=1",
-                                 "SGX_SCATTER_NT=1", "SGX_SCATTER_NT=4", "SGX_RANK=match", "SGX_SCATTER_WC=0",
-                                 "SGX_PIPELINE=1", "SGX_HIST_VARIANT=7"])
-def test_alternative_scatter_variants(sgx_lib, oracle_lib, monkeypatch, env):
-    """The A/B variants kept for measurement must stay bit-exact too (engine reads the env
-    at creation)."""
-    k, v = env.split("=")
-    monkeypatch.setenv(k, v)
+@pytest.mark.parametrize("cfg", [dict(hist_mode=1), dict(rank_mode=1), dict(flags=1), dict(hist_mode=1, flags=1)])
+def test_kernel_choices_are_byte_identical(sgx_lib, oracle_lib, cfg):
+    """sgx_config's kernel choices -- the ballot/popcount wave-aggregated histogram
+    (SGX_HIST_BALLOT), ballot-matched K4 ranking (SGX_RANK_MATCH), K4 without write-combining
+    (SGX_FLAG_NO_WRITE_COMBINING) -- change speed, never bytes."""
     recs = oracle_lib.gen_uniform16(3 * 8192 * 5 + 1234, 99)
-    with sgx_lib.ShuffleEngine(device=0) as e:
-        for R in (200, 1024):
+    with sgx_lib.ShuffleEngine(device=0, **cfg) as e:
+        for R in (7, 200, 1024, 4096):
             check_against_oracle(e, oracle_lib, recs, R)
+    cdf = oracle_lib.zipf_cdf(1.1, 2**20)
+    zrecs = oracle_lib.gen_zipf16(300_001, 5, cdf)
+    with sgx_lib.ShuffleEngine(device=0, **cfg) as e:
+        for R in (1024, 4096):
+            check_against_oracle(e, oracle_lib, zrecs, R)
 
 
 @pytest.mark.parametrize("R", [200, 585, 586, 1000, 1024])
@@ -234,13 +235,13 @@ def test_terasort_bytes10(engine, oracle_lib, nb):
 @pytest.mark.parametrize("wide2", ["1", "0"])
 @pytest.mark.parametrize("R", [1, 7, 1000, 2048, 4096])
 @pytest.mark.parametrize("n", [1, 1023, 1024, 5 * 1024 + 77])
-def test_wide_records_every_path(sgx_lib, oracle_lib, monkeypatch, wide2, R, n):
+def test_wide_records_every_path(sgx_lib, oracle_lib, wide2, R, n):
     """100 B records: the LDS-staged dword-stream K4 (R <= 2048) and the per-lane kernel
-    (SGX_SCATTER_WIDE2=0, and R = 4096), hash and range partitioners, partial tiles and
+    (SGX_FLAG_NO_WIDE_STAGED, and R = 4096), hash and range partitioners, partial tiles and
     several chunks."""
-    monkeypatch.setenv("SGX_SCATTER_WIDE2", wide2)
+    flags = 0 if wide2 == "1" else sgx_lib.FLAG_NO_WIDE_STAGED
     recs = oracle_lib.gen_terasort100(n, R + n)
-    with sgx_lib.ShuffleEngine(device=0, num_chunks=3) as e:
+    with sgx_lib.ShuffleEngine(device=0, num_chunks=3, flags=flags) as e:
         check_against_oracle(e, oracle_lib, recs, R)
         if R > 1:
             rng = np.random.default_rng(R)

@@ -192,7 +192,7 @@ def test_gpu_kryo_plugin_mirror(tmp_path, oracle_lib):
     recs = oracle_lib.gen_uniform16(20_000, 7)
     out, counts = oracle_lib.map_write(recs, R)
     off = oracle_lib.kryo_partition_offsets(out, counts)
-    mgr = sgx.UcxShuffleManager(device=0, localDir=str(tmp_path))
+    mgr = sgx.UcxShuffleManager(conf={"spark.shuffle.compress": "false"}, device=0, localDir=str(tmp_path))
     try:
         h = mgr.registerShuffle(3, sgx.ShuffleDependency(sgx.HashPartitioner(R), 16, serializer="kryo"))
         w = mgr.getWriter(h, 0)

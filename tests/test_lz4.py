@@ -324,3 +324,36 @@ def test_gpu_plugin_spark_shuffle_compress(sgx_lib, oracle_lib, tmp_path):
         assert rd.read().tobytes() == out[o[10]:o[20]].tobytes()
     finally:
         mgr.stop()
+
+
+@pytest.mark.gpu
+def test_gpu_rewrite_compressed_map_with_other_data(sgx_lib, oracle_lib):
+    """A second attempt of the same map on an LZ4 shuffle (smaller, then larger than the
+    first) publishes the frames of ITS Kryo stream -- never the earlier attempt's frames."""
+    R = 64
+    with sgx_lib.ShuffleEngine(device=0) as e:
+        e.register_shuffle(1, R, serializer=sgx_lib.SER_KRYO)
+        e.set_compression(1, "lz4", 4096)
+        for k, n in enumerate((40_000, 7_000, 90_000)):
+            recs = oracle_lib.gen_uniform16(n, 0x1234 + k)
+            if k == 2:
+                recs[:, 8:] = 0  # compressible values: LZ4 blocks, not RAW
+            lens = e.write_map(1, 0, recs, n, 16, R)
+            out, counts = oracle_lib.map_write(recs, R)
+            kryo = oracle_lib.kryo_serialize(out)
+            frames, flen = oracle_lib.lz4_frame_partitions(kryo, oracle_lib.kryo_partition_offsets(out, counts), 4096)
+            assert np.array_equal(lens, flen), f"attempt {k}"
+            assert np.array_equal(e.map_output_bytes(1, 0), frames), f"attempt {k}"
+            got = e.read_records(1, [0], 0, R).reshape(-1, 16)
+            assert np.array_equal(got, out), f"attempt {k}"
+
+
+@pytest.mark.gpu
+def test_gpu_serializer_cannot_leave_kryo_while_compressed(sgx_lib):
+    with sgx_lib.ShuffleEngine(device=0) as e:
+        e.register_shuffle(1, 8, serializer=sgx_lib.SER_KRYO)
+        e.set_compression(1, "lz4", 32768)
+        with pytest.raises(sgx_lib.IllegalStateException):
+            e.set_serializer(1, sgx_lib.SER_FIXED)
+        e.set_compression(1, "none")
+        e.set_serializer(1, sgx_lib.SER_FIXED)  # allowed once compression is off

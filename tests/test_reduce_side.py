@@ -80,14 +80,14 @@ def test_oracle_grouped_matches_dict(oracle_lib, agg):
 _sid = [5000]
 
 
-def _run(sgx_lib, oracle_lib, maps, R, kind=0, bounds=None, ascending=True, rng_part=None, agg=None):
+def _run(sgx_lib, oracle_lib, maps, R, kind=0, bounds=None, ascending=True, rng_part=None, agg=None, flags=0):
     """Write `maps` (list of record arrays) as map ids 0..M-1, read [r0, r1) back on the
     GPU (sorted, or grouped with `agg`), compare with the oracle."""
     _sid[0] += 1
     sid = _sid[0]
     rb = maps[0].shape[1]
     r0, r1 = rng_part or (0, R)
-    with sgx_lib.ShuffleEngine(device=0, num_chunks=5) as e:
+    with sgx_lib.ShuffleEngine(device=0, num_chunks=5, flags=flags) as e:
         e.register_shuffle(sid, R, kind, bounds, ascending, rb)
         outs = []
         for mid, recs in enumerate(maps):
@@ -206,10 +206,10 @@ def test_reader_dispatch(sgx_lib, oracle_lib, tmp_path):
 @pytest.mark.gpu
 @pytest.mark.parametrize("skip", ["1", "0"])
 @pytest.mark.parametrize("keys", ["small_nonneg", "all_equal", "two_values_high_byte"])
-def test_sorted_trivial_digits(sgx_lib, oracle_lib, monkeypatch, skip, keys):
-    """Digit passes whose byte is constant over the fetched keys are skipped (SGX_SORT_SKIP=1,
-    the default); the result must not depend on it."""
-    monkeypatch.setenv("SGX_SORT_SKIP", skip)
+def test_sorted_trivial_digits(sgx_lib, oracle_lib, skip, keys):
+    """Digit passes whose byte is constant over the fetched keys are skipped (the default;
+    SGX_FLAG_SORT_ALL_DIGITS runs them all); the result must not depend on it."""
+    flags = 0 if skip == "1" else sgx_lib.FLAG_SORT_ALL_DIGITS
     rng = np.random.default_rng(len(keys))
     n = 30_000
     if keys == "small_nonneg":
@@ -221,5 +221,43 @@ def test_sorted_trivial_digits(sgx_lib, oracle_lib, monkeypatch, skip, keys):
     maps = [_records16(k[: n // 2], rng.integers(0, 1 << 62, size=n // 2)),
             _records16(k[n // 2:], rng.integers(0, 1 << 62, size=n - n // 2))]
     for R in (1, 16):
-        _run(sgx_lib, oracle_lib, maps, R)
-        _run(sgx_lib, oracle_lib, maps, R, agg="group")
+        _run(sgx_lib, oracle_lib, maps, R, flags=flags)
+        _run(sgx_lib, oracle_lib, maps, R, agg="group", flags=flags)
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+@pytest.mark.parametrize("codec", ["fixed", "kryo+lz4"])
+def test_c0_groupbykey_full_size(sgx_lib, oracle_lib, codec, tmp_path):
+    """BASELINE config C0 at its size: groupByKey of 10M (Long, Long) records -- two map
+    shards of 5M (the two executors of local-cluster[2,1,2048]) -- to 200 reducers through
+    UcxShuffleManager -> getWriter -> getReader().read() (the GroupByTest shapes of
+    buildlib/test.sh:163-173; combineValuesByKey, spark_3_0/UcxShuffleReader.scala:155-164),
+    with the engine's fixed codec and with Spark's KryoSerializer + spark.shuffle.compress
+    (LZ4), against oracle.reduce_grouped."""
+    n, R, seed = 10_000_000, 200, 0x5EEDC0DE
+    recs = oracle_lib.gen_uniform16(n, seed)
+    conf = {"spark.shuffle.compress": "true" if codec != "fixed" else "false"}
+    mgr = sgx_lib.UcxShuffleManager(conf=conf, localDir=str(tmp_path))
+    try:
+        dep = sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(R), 16, aggregator=sgx_lib.Aggregator("group"),
+                                        serializer="fixed" if codec == "fixed" else "kryo")
+        h = mgr.registerShuffle(0, dep)
+        outs = []
+        for m in range(2):
+            shard = recs[m * (n // 2):(m + 1) * (n // 2)]
+            w = mgr.getWriter(h, m)
+            w.write(shard)
+            out, counts = oracle_lib.map_write(shard, R, nthreads=8)
+            outs.append((out, counts))
+            if codec == "fixed":
+                assert np.array_equal(w.getPartitionLengths(), counts * 16)
+        keys, starts, values = mgr.getReader(h, 0, R).read()
+        seqs = oracle_lib.canonical_reducer_sequences(outs, R, 16)
+        wk, ws, wv = oracle_lib.reduce_grouped(seqs, "group")
+        assert np.array_equal(keys, wk)
+        assert np.array_equal(starts, ws)
+        assert np.array_equal(values, wv)
+        assert len(values) == n
+    finally:
+        mgr.stop()

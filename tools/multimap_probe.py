@@ -39,10 +39,16 @@ def main():
     ap.add_argument("--partitions", type=int, default=1024)
     ap.add_argument("--maps", default="1,8,16,32,64")
     ap.add_argument("--iters", type=int, default=4)
+    ap.add_argument("--chunks", default="0", help="comma list of num_chunks (0 = one per CU)")
     a = ap.parse_args()
     import sparkucx_amd as sgx
 
-    e = sgx.ShuffleEngine(0)
+    for G in [int(x) for x in a.chunks.split(",")]:
+        run(sgx, a, G)
+
+
+def run(sgx, a, G):
+    e = sgx.ShuffleEngine(0, num_chunks=G)
     n, R = a.records, a.partitions
     buf = e.alloc(n * 16)
     e.gen_uniform16(buf, n, 0x5EEDC0DE)
@@ -63,7 +69,7 @@ def main():
             if it:
                 walls.append(dt)
         st = e.stats()
-        row = {"maps": M, "records_per_map": per, "MB_per_map": per * 16 / 2**20,
+        row = {"chunks": G, "maps": M, "records_per_map": per, "MB_per_map": per * 16 / 2**20,
                "wall_ms_per_step": round(1e3 * min(walls), 3),
                "shuffled_GBs": round(16 * n / min(walls) / 1e9, 1)}
         for k in ("hist", "scan", "scatter"):
@@ -72,6 +78,7 @@ def main():
         row["k4_algo_GBs"] = round(32 * n / (row["scatter_ms_sum_per_step"] * 1e-3) / 1e9, 1)
         print(json.dumps(row), flush=True)
         e.unregister_shuffle(sid)
+    buf.free()
     e.close()
 
 
