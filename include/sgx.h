@@ -63,7 +63,9 @@ enum sgx_rank_mode { SGX_RANK_ORDERED = 0,  /* K4 ranks by lane-ordered LDS atom
 enum sgx_flags {
     SGX_FLAG_NO_WRITE_COMBINING = 1,  /* hash K4 without on-chip line write-combining      */
     SGX_FLAG_NO_WIDE_STAGED = 2,      /* 100 B records: per-lane K4 instead of LDS-staged   */
-    SGX_FLAG_SORT_ALL_DIGITS = 4      /* sorted reads run every digit pass (no skipping)    */
+    SGX_FLAG_SORT_ALL_DIGITS = 4,     /* sorted reads run every digit pass (no skipping)    */
+    SGX_FLAG_DEBUG_SYNC = 8           /* debugging: synchronise after every kernel and name the
+                                         kernel in the error of a device fault (slow)         */
 };
 
 typedef struct sgx_config {
@@ -310,6 +312,18 @@ int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, 
 int sgx_range_bounds(sgx_engine *e, const void *const *batches, const int64_t *nrecords, int32_t nbatches,
                      int32_t record_bytes, int32_t mem_kind, int32_t num_partitions, int32_t rdd_id,
                      int32_t sample_points_per_partition, void *out_bounds, int32_t *out_nbounds);
+
+/* ---- MemoryPool (memory/MemoryPool.scala:22-147): the BufferAllocator of the fetch contract
+ *      (ShuffleTransport.scala:113).  Blocks come in power-of-two size classes from 4 KiB
+ *      (spark.shuffle.ucx.memory.minBufferSize), pinned host memory (SGX_MEM_HOST: DMA-able)
+ *      or HBM (SGX_MEM_DEVICE); sgx_pool_put returns a block (MemoryBlock.close()) to its
+ *      class's free list, sgx_pool_preallocate fills a class ahead of time
+ *      (spark.shuffle.ucx.memory.preAllocateBuffers, :141-147).  Thread-safe; freed with the
+ *      engine. ---- */
+int sgx_pool_get(sgx_engine *e, int64_t size, int32_t mem_kind, void **out_ptr, int64_t *out_capacity);
+int sgx_pool_put(sgx_engine *e, void *ptr);
+int sgx_pool_preallocate(sgx_engine *e, int64_t size, int32_t count, int32_t mem_kind);
+int sgx_pool_stats(sgx_engine *e, int64_t *out_allocated_bytes, int64_t *out_idle_bytes);
 
 /* ---- measurement: HIP-event times of the last write_map / exchange stages, and
  *      accumulated per-stage sums since the last reset (index = enum sgx_stage). ---- */

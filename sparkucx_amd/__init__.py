@@ -16,10 +16,10 @@ from .engine import (  # noqa: F401
     DeviceBuffer, ShuffleEngine, bootstrap_join, bootstrap_serve, get_unique_id, plan_exchange, reducer_owner,
 )
 from .shuffle import (  # noqa: F401
-    Aggregator, BaseShuffleHandle, GpuShuffleMapOutputWriter, GpuShuffleTransport, GpuShuffleWriter,
-    HashPartitioner, MapStatus, MemoryBlock, OperationResult, OperationStatus, RangePartitioner,
+    Aggregator, BaseShuffleHandle, BlockFetchingListener, GpuShuffleMapOutputWriter, GpuShuffleTransport, GpuShuffleWriter,
+    HashPartitioner, MapStatus, MemoryBlock, MemoryPool, OperationResult, OperationStatus, RangePartitioner,
     ShuffleDependency, UcxShuffleBlockId, UcxShuffleBlockResolver, UcxShuffleManager,
-    UcxShuffleReader, byte_string, parse_block_id,
+    UcxShuffleClient, UcxShuffleReader, byte_string, parse_block_id,
 )
 
 __all__ = [n for n in dir() if not n.startswith("_")]

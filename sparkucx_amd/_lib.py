@@ -26,7 +26,7 @@ STAGES = ("hist", "scan", "scatter", "allgather", "alltoall", "regroup", "sort",
           "deserialize", "combine")
 HIST_ATOMIC, HIST_BALLOT = 0, 1
 RANK_ORDERED, RANK_MATCH = 0, 1
-FLAG_NO_WRITE_COMBINING, FLAG_NO_WIDE_STAGED, FLAG_SORT_ALL_DIGITS = 1, 2, 4
+FLAG_NO_WRITE_COMBINING, FLAG_NO_WIDE_STAGED, FLAG_SORT_ALL_DIGITS, FLAG_DEBUG_SYNC = 1, 2, 4, 8
 ABI_VERSION = 2
 
 
@@ -92,6 +92,10 @@ SIGNATURES = {
     "sgx_map_append": (ctypes.c_int, [_vp, _i32, _i64, _vp, _i64, _i32, _i32]),
     "sgx_map_commit": (ctypes.c_int, [_vp, _i32, _i64, _vp]),
     "sgx_comm_init_host": (ctypes.c_int, [_vp, _i32, _i32, _vp]),
+    "sgx_pool_get": (ctypes.c_int, [_vp, _i64, _i32, ctypes.POINTER(_vp), _P64]),
+    "sgx_pool_put": (ctypes.c_int, [_vp, _vp]),
+    "sgx_pool_preallocate": (ctypes.c_int, [_vp, _i64, _i32, _i32]),
+    "sgx_pool_stats": (ctypes.c_int, [_vp, _P64, _P64]),
     "sgx_last_error": (_cp, []),
     "sgx_abi_version": (_i32, []),
     "sgx_register_shuffle": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _i64, _i32, _i32]),

@@ -110,6 +110,15 @@ static uint32_t bits_for(uint32_t R) {
     return b ? b : 1;
 }
 
+int sgx::debug_sync(sgx_engine *e, hipStream_t st, const char *what) {
+    if (!(e->flags & SGX_FLAG_DEBUG_SYNC)) return SGX_OK;
+    const hipError_t a = hipStreamSynchronize(st);
+    const hipError_t b = hipGetLastError();
+    if (a != hipSuccess || b != hipSuccess)
+        return fail_msg(SGX_ERR_HIP, "%s: %s / %s", what, hipGetErrorString(a), hipGetErrorString(b));
+    return SGX_OK;
+}
+
 PartParams sgx::make_part_params(const Shuffle &s) {
     PartParams pp{};
     pp.kind = s.kind;
@@ -135,7 +144,7 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     if (dev < 0 || dev >= ndev) return fail_msg(SGX_ERR_INVALID, "sgx_create: device %d of %d", dev, ndev);
     if (cfg && (cfg->hist_mode < SGX_HIST_ATOMIC || cfg->hist_mode > SGX_HIST_BALLOT ||
                 cfg->rank_mode < SGX_RANK_ORDERED || cfg->rank_mode > SGX_RANK_MATCH || cfg->flags < 0 ||
-                cfg->flags > 7 || cfg->comm_timeout_ms < 0 || cfg->num_chunks < 0))
+                cfg->flags > 15 || cfg->comm_timeout_ms < 0 || cfg->num_chunks < 0))
         return fail_msg(SGX_ERR_INVALID, "sgx_create: bad configuration");
     HIP_TRY(hipSetDevice(dev));
     hipDeviceProp_t prop;

@@ -217,6 +217,7 @@ struct Ctx {
     HostPinned gather_items;
     // LZ4 framing / unframing scratch (grow-only)
     DevBuf lz4_blocks, lz4_slots, lz4_sizes, lz4_offs, lz4_info, lz4_desc;
+    HostPinned lz4_host;  // pinned staging of the block list / frame sizes / frame offsets
     // RangePartitioner.sketch
     DevBuf sample_winner, sample_keys, cdf;
     ~Ctx() {
@@ -231,6 +232,8 @@ struct PendingStage {
     int stage;
     hipEvent_t a, b;
 };
+
+struct PoolState;  // sgx_pool.cpp
 
 }  // namespace sgx
 
@@ -261,6 +264,7 @@ struct sgx_engine {
     sgx::HostPinned ag_host, x_send, x_recv;
     sgx::DevBuf jump_dev;  // XORShiftRandom jump table (built once, read-only after)
     std::mutex jump_mu;
+    std::shared_ptr<sgx::PoolState> pool;  // MemoryPool (sgx_pool.cpp), created on first use
 
     // stats
     std::mutex stats_mu;
@@ -281,6 +285,8 @@ struct sgx_engine {
 namespace sgx {
 
 // ---- shared internals (defined across the engine's translation units) ----
+// SGX_FLAG_DEBUG_SYNC: synchronise `st` and report a device error naming `what`.
+int debug_sync(sgx_engine *e, hipStream_t st, const char *what);
 PartParams make_part_params(const Shuffle &s);
 // One stable partition pass (K1+K2 hist -> K3 scan -> K4 scatter) on the context's stream.
 int partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_t n, int rb, const PartParams &spp,

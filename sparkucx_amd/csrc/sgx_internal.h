@@ -89,8 +89,10 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes
 // LZ4BlockOutputStream framing (sgx_lz4.hip)
 int lz4_lanes_per_workgroup();
 int lz4_max_block();
-hipError_t launch_lz4_blocks(const uint8_t *stream, const int64_t *blocks, int64_t nblocks, int level,
-                             uint8_t *slots, int64_t slot_bytes, int32_t *sizes, hipStream_t s);
+// err: 4 int64 {flags, block, offset, length}, zeroed by the caller (see k_lz4_blocks)
+hipError_t launch_lz4_blocks(const uint8_t *stream, int64_t stream_len, const int64_t *blocks, int64_t nblocks,
+                             int level, uint8_t *slots, int64_t slot_bytes, int32_t *sizes, int64_t *err,
+                             hipStream_t s);
 hipError_t launch_lz4_gather(const uint8_t *slots, int64_t slot_bytes, const int32_t *sizes,
                              const int64_t *frame_off, int64_t nblocks, const int64_t *end_off, int64_t nends,
                              int level, uint8_t *dst, hipStream_t s);

@@ -70,14 +70,17 @@ __device__ uint32_t xxh32_lds(const uint8_t *p, int len, uint32_t seed) {
     return h;
 }
 
-// LZ4_compress_default of src[0, n) (n < 65547) into out; returns the compressed size.
+// LZ4_compress_default of src[0, n) (n < 65547) into out[0, cap); returns the compressed
+// size, or -1 if the output would pass `cap` (LZ4_compressBound(n) <= cap by construction,
+// so this is a guard against corrupt input, never a path of correct runs).
 // `src` and `table` are this lane's LDS slices; output bytes go straight to HBM.
 // `table` must be zeroed (LZ4_initStream).
-__device__ int lz4_compress_lane(const uint8_t *src, int n, uint16_t *table, uint8_t *out) {
+__device__ int lz4_compress_lane(const uint8_t *src, int n, uint16_t *table, uint8_t *out, int cap) {
     const uint8_t *ip = src, *anchor = src, *iend = src + n;
     const uint8_t *mflimit_plus_one = iend - kMfLimit + 1;
     const uint8_t *matchlimit = iend - kLastLiterals;
     uint8_t *op = out;
+    uint8_t *const oend = out + cap;
     if (n >= kMfLimit + 1) {
         table[hash4(lds32(ip))] = 0;
         ip++;
@@ -107,6 +110,8 @@ __device__ int lz4_compress_lane(const uint8_t *src, int n, uint16_t *table, uin
             while (ip > anchor && match > src && ip[-1] == match[-1]) { ip--; match--; }
             {
                 unsigned lit = (unsigned)(ip - anchor);
+                // token + literal length + literals + offset + 1 match-length byte at most
+                if (op + 1 + lit / 255 + 1 + lit + 2 + 1 > oend) return -1;
                 token = op++;
                 uint8_t tk;
                 if (lit >= 15) {
@@ -137,6 +142,7 @@ __device__ int lz4_compress_lane(const uint8_t *src, int n, uint16_t *table, uin
                         b += 4;
                     }
                     unsigned mc = (unsigned)(a - (ip + kMinMatch));
+                    if (op + mc / 255 + 1 + 3 > oend) return -1;  // run bytes + the next token, offset
                     ip = a;
                     if (mc >= 15) {
                         tk += 15;
@@ -165,6 +171,7 @@ __device__ int lz4_compress_lane(const uint8_t *src, int n, uint16_t *table, uin
 last_literals:
     {
         int last = (int)(iend - anchor);
+        if (op + 1 + last / 255 + 1 + last > oend) return -1;
         if (last >= 15) {
             int acc = last - 15;
             *op++ = 15 << 4;
@@ -193,10 +200,14 @@ __device__ __forceinline__ void put_header(uint8_t *h, uint8_t token, uint32_t c
 }
 
 // blocks[b] = {src byte offset, length}; one lane per block, kLanes lanes per workgroup.
-__global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ stream,
+// Every global access is checked against stream_len / the slot: a block outside the stream
+// or an output past its slot sets err[0] (1 = bad block, 2 = output overflow) and records
+// {block, offset, length} in err[1..3] instead of touching memory.
+__global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ stream, int64_t stream_len,
                                                    const int64_t *__restrict__ blocks, int64_t nblocks,
                                                    int level, uint8_t *__restrict__ slots,
-                                                   int64_t slot_bytes, int32_t *__restrict__ sizes) {
+                                                   int64_t slot_bytes, int32_t *__restrict__ sizes,
+                                                   int64_t *__restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint8_t s_in[kLanes][kMaxBlock + 16];
     __shared__ uint16_t s_tab[kLanes][kTable];
     const int lane = threadIdx.x;
@@ -207,8 +218,18 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
         if (bb >= nblocks) break;
         // aligned dword copy that keeps the source's misalignment (sh bytes) in LDS; the
         // last dword is read byte-wise so nothing past the stream's end is touched
-        const uint8_t *g = stream + blocks[2 * bb];
-        const int n = (int)blocks[2 * bb + 1];
+        const int64_t boff = blocks[2 * bb], blen = blocks[2 * bb + 1];
+        if (boff < 0 || blen < 0 || blen > kMaxBlock || boff + blen > stream_len) {
+            if (threadIdx.x == 0) {
+                err[1] = bb;
+                err[2] = boff;
+                err[3] = blen;
+                atomicOr((unsigned long long *)err, 1ull);
+            }
+            return;  // uniform: the whole workgroup leaves before any barrier
+        }
+        const uint8_t *g = stream + boff;
+        const int n = (int)blen;
         const int sh = (int)((uintptr_t)g & 3u);
         const uint32_t *gw = (const uint32_t *)(g - sh);
         const int full = (sh + n) >> 2;
@@ -225,8 +246,17 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
     const int n = (int)blocks[2 * b + 1];
     const uint8_t *src = s_in[0] + ((uintptr_t)(stream + blocks[2 * b]) & 3u);
     uint8_t *slot = slots + b * slot_bytes;
-    if (lane == 0) s_c = lz4_compress_lane(src, n, s_tab[0], slot + kHeader);
+    if (lane == 0) s_c = lz4_compress_lane(src, n, s_tab[0], slot + kHeader, (int)(slot_bytes - kHeader));
     __syncthreads();
+    if (s_c < 0) {
+        if (lane == 0) {
+            err[1] = b;
+            err[2] = blocks[2 * b];
+            err[3] = n;
+            atomicOr((unsigned long long *)err, 2ull);
+        }
+        return;
+    }
     const bool raw = s_c >= n;  // the compressed block did not shrink: RAW, copied by the wave
     const int c = raw ? n : s_c;
     if (raw)
@@ -376,12 +406,13 @@ __global__ __launch_bounds__(64) void k_lz4_decode(const uint8_t *__restrict__ i
 int lz4_lanes_per_workgroup() { return kLanes; }
 int lz4_max_block() { return kMaxBlock; }
 
-hipError_t launch_lz4_blocks(const uint8_t *stream, const int64_t *blocks, int64_t nblocks, int level,
-                             uint8_t *slots, int64_t slot_bytes, int32_t *sizes, hipStream_t stream_) {
+hipError_t launch_lz4_blocks(const uint8_t *stream, int64_t stream_len, const int64_t *blocks, int64_t nblocks,
+                             int level, uint8_t *slots, int64_t slot_bytes, int32_t *sizes, int64_t *err,
+                             hipStream_t stream_) {
     if (nblocks <= 0) return hipSuccess;
     int64_t grid = (nblocks + kLanes - 1) / kLanes;
-    hipLaunchKernelGGL(k_lz4_blocks, dim3((unsigned)grid), dim3(64), 0, stream_, stream, blocks, nblocks,
-                       level, slots, slot_bytes, sizes);
+    hipLaunchKernelGGL(k_lz4_blocks, dim3((unsigned)grid), dim3(64), 0, stream_, stream, stream_len, blocks,
+                       nblocks, level, slots, slot_bytes, sizes, err);
     return hipGetLastError();
 }
 

@@ -39,19 +39,34 @@ int sgx::lz4_frame_impl(sgx_engine *e, Ctx &c, const void *stream_dev, const int
     HIP_TRY(hipSetDevice(e->device));
     DevBuf &d_blocks = c.lz4_blocks, &d_slots = c.lz4_slots, &d_sizes = c.lz4_sizes, &d_offs = c.lz4_offs;
     hipStream_t st = c.st;
-    std::vector<int32_t> sizes(nb);
+    // pinned staging: [block list nb x 16 | kernel error 32 | frame sizes nb x 4 | frame offsets (nb + R) x 8]
+    const size_t h_blocks = 0, h_err = (size_t)nb * 16, h_sizes = h_err + 32, h_offs = (h_sizes + (size_t)nb * 4 + 7) & ~(size_t)7;
+    SGX_TRY(c.lz4_host.ensure(h_offs + ((size_t)nb + R) * 8));
+    char *hb = (char *)c.lz4_host.p;
+    const int32_t *sizes = (const int32_t *)(hb + h_sizes);
     if (nb > 0) {
         SGX_TRY(d_blocks.ensure((size_t)nb * 16));
         SGX_TRY(d_slots.ensure((size_t)(nb * slot)));
         SGX_TRY(d_sizes.ensure((size_t)nb * 4));
-        HIP_TRY(hipMemcpyAsync(d_blocks.p, blocks.data(), (size_t)nb * 16, hipMemcpyHostToDevice, st));
-        HIP_TRY(sgx::launch_lz4_blocks((const uint8_t *)stream_dev, (const int64_t *)d_blocks.p, nb, level,
-                                       (uint8_t *)d_slots.p, slot, (int32_t *)d_sizes.p, st));
-        HIP_TRY(hipMemcpyAsync(sizes.data(), d_sizes.p, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
+        SGX_TRY(c.lz4_info.ensure(64));
+        std::memcpy(hb + h_blocks, blocks.data(), (size_t)nb * 16);
+        HIP_TRY(hipMemsetAsync(c.lz4_info.p, 0, 32, st));
+        HIP_TRY(hipMemcpyAsync(d_blocks.p, hb + h_blocks, (size_t)nb * 16, hipMemcpyHostToDevice, st));
+        HIP_TRY(sgx::launch_lz4_blocks((const uint8_t *)stream_dev, part_offsets[R], (const int64_t *)d_blocks.p, nb,
+                                       level, (uint8_t *)d_slots.p, slot, (int32_t *)d_sizes.p,
+                                       (int64_t *)c.lz4_info.p, st));
+        SGX_TRY(debug_sync(e, st, "k_lz4_blocks"));
+        HIP_TRY(hipMemcpyAsync(hb + h_sizes, d_sizes.p, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemcpyAsync(hb + h_err, c.lz4_info.p, 32, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
+        const int64_t *kerr = (const int64_t *)(hb + h_err);
+        if (kerr[0])
+            return fail_msg(SGX_ERR_HIP, "internal error: LZ4 block %lld (offset %lld, %lld bytes) %s", (long long)kerr[1],
+                            (long long)kerr[2], (long long)kerr[3],
+                            (kerr[0] & 1) ? "lies outside the stream" : "overflowed its frame slot");
     }
     // frame offsets (blocks of a partition back to back, then its end mark)
-    std::vector<int64_t> offs((size_t)nb + R);  // nb frame offsets | end-mark offsets
+    int64_t *offs = (int64_t *)(hb + h_offs);  // nb frame offsets | end-mark offsets
     int64_t total = 0, nends = 0;
     for (int r = 0; r < R; ++r) {
         int64_t start = total;
@@ -77,10 +92,11 @@ int sgx::lz4_frame_impl(sgx_engine *e, Ctx &c, const void *stream_dev, const int
                     (long long)dst_cap);
     if (nb > 0) {
         SGX_TRY(d_offs.ensure((size_t)(nb + nends) * 8));
-        HIP_TRY(hipMemcpyAsync(d_offs.p, offs.data(), (size_t)(nb + nends) * 8, hipMemcpyHostToDevice, st));
+        HIP_TRY(hipMemcpyAsync(d_offs.p, offs, (size_t)(nb + nends) * 8, hipMemcpyHostToDevice, st));
         HIP_TRY(sgx::launch_lz4_gather((const uint8_t *)d_slots.p, slot, (const int32_t *)d_sizes.p,
                                        (const int64_t *)d_offs.p, nb, (const int64_t *)d_offs.p + nb, nends, level,
                                        (uint8_t *)dst_dev, st));
+        SGX_TRY(debug_sync(e, st, "k_lz4_gather"));
         HIP_TRY(hipStreamSynchronize(st));
     }
     return SGX_OK;

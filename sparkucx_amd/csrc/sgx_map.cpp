@@ -84,13 +84,16 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     hipEvent_t h0 = e->ev(), h1 = e->ev(), c1 = e->ev(), x1 = e->ev();
     HIP_TRY(hipEventRecord(h0, st));
     if (n > 0) HIP_TRY(launch_hist(in, n, rb, chunk, G, spp, counts, st, e->hist_mode, true));
+    SGX_TRY(debug_sync(e, st, "K1+K2 k_hist"));
     HIP_TRY(hipEventRecord(h1, st));
     HIP_TRY(launch_scan((const uint32_t *)counts, (uint32_t *)c.offs.p, len, status, ticket, err, part_off_dev, G, R,
                         st));
+    SGX_TRY(debug_sync(e, st, "K3 k_scan"));
     HIP_TRY(hipEventRecord(c1, st));
     PartParams lpp = spp;
     lpp.mbits = (uint32_t)geo.mbits;
     if (n > 0) HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, lpp, (const uint32_t *)c.offs.p, geo, err, st));
+    SGX_TRY(debug_sync(e, st, "K4 scatter"));
     HIP_TRY(hipEventRecord(x1, st));
     // (R+1) offsets then the error word, one copy
     if (host_off) HIP_TRY(hipMemcpyAsync(host_off, part_off_dev, (size_t)(R + 2) * 4, hipMemcpyDeviceToHost, st));
@@ -122,6 +125,7 @@ static int serialize_kryo(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const ui
     hipEvent_t k0 = e->ev(), k1 = e->ev();
     HIP_TRY(hipEventRecord(k0, st));
     HIP_TRY(launch_kryo_ser16(m.data.p, n, m.ser.p, rec_off_dev, s.R, off_dev, work, st));
+    SGX_TRY(debug_sync(e, st, "Kryo serializer"));
     HIP_TRY(hipEventRecord(k1, st));
     e->record_stage(SGX_STAGE_SERIALIZE, k0, k1);
     HIP_TRY(hipMemcpyAsync(m.ser_off.p, off_dev, offb, hipMemcpyDeviceToHost, st));  // (R+1) byte offsets

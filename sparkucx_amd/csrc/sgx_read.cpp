@@ -125,6 +125,7 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
     HIP_TRY(hipEventRecord(g0, st));
     HIP_TRY(hipMemcpyAsync(c.items_dev.p, gi, (size_t)npieces * 24, hipMemcpyHostToDevice, st));
     HIP_TRY(launch_gather_items((const int64_t *)c.items_dev.p, npieces, al16 ? 16 : al4 ? 4 : 1, st));
+    SGX_TRY(debug_sync(e, st, "k_gather_items"));
     HIP_TRY(hipEventRecord(g1, st));
     e->record_stage(SGX_STAGE_REGROUP, g0, g1);
     if (!dev_dst) HIP_TRY(hipMemcpyAsync(dst, gdst, (size_t)total, hipMemcpyDeviceToHost, st));
@@ -215,6 +216,7 @@ static int records_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_id
         hipEvent_t k0 = e->ev(), k1 = e->ev();
         HIP_TRY(hipEventRecord(k0, st));
         HIP_TRY(launch_kryo_deser16(c.kryo_in.p, total, c.sort_buf[0].p, cap, status, tick, cnt_dev, st));
+        SGX_TRY(debug_sync(e, st, "Kryo decoder"));
         HIP_TRY(hipEventRecord(k1, st));
         e->record_stage(SGX_STAGE_DESERIALIZE, k0, k1);
         uint32_t herr[4];

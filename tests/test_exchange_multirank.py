@@ -113,12 +113,14 @@ def run_world(tmp_path, world, backend, codec, R, n):
 
     mp.start_processes(worker, args=(world, free_port(), backend, codec, R, n, str(tmp_path)), nprocs=world,
                        start_method="spawn", join=True)
-    for r in range(world):
-        assert (tmp_path / f"rank{r}").read_text() == "ok", f"rank {r}"
+    msgs = {r: (tmp_path / f"rank{r}").read_text() for r in range(world)}
+    bad = {r: m for r, m in msgs.items() if m != "ok"}
+    assert not bad, "\n".join(f"rank {r}: {m}" for r, m in bad.items())
 
 
 @pytest.mark.parametrize("world,codec,R,n", [(2, "fixed", 1024, 200_000), (4, "fixed", 1024, 100_000),
                                              (4, "fixed", 3, 5_000), (2, "kryo", 200, 60_000),
+                                             (4, "kryo", 200, 40_000),
                                              (4, "kryo+lz4", 200, 40_000), (2, "kryo+lz4", 7, 20_000)])
 def test_exchange_host_backend_ranks_share_one_gpu(sgx_lib, oracle_lib, tmp_path, world, codec, R, n):
     run_world(tmp_path, world, "host", codec, R, n)

@@ -538,3 +538,89 @@ def test_full_c4_shard_terasort_bit_exact(engine, oracle_lib):
     del recs
     assert np.array_equal(lengths, counts * 100)
     assert np.array_equal(got, want.reshape(-1))
+
+
+def test_shuffle_client_fetch_blocks_split_and_listener(sgx_lib, oracle_lib):
+    """UcxShuffleClient.fetchBlocks (spark_3_0/UcxShuffleClient.scala:49-91): 130 block ids are
+    split into requests of at most maxBlocksPerRequest (default 50, :53-58), every block
+    reaches onBlockFetchSuccess with its bytes, and a request holding an unknown block
+    reports onBlockFetchFailure for each of its blocks (the reference never does)."""
+    R = 64
+    mgr = sgx_lib.UcxShuffleManager(conf={"spark.shuffle.ucx.maxBlocksPerRequest": "50"})
+    try:
+        h = mgr.registerShuffle(3, sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(R)))
+        outs = {}
+        for m in (0, 1, 2):
+            recs = oracle_lib.gen_uniform16(20_000 + m, 50 + m)
+            mgr.getWriter(h, m).write(recs)
+            outs[m] = oracle_lib.map_write(recs, R)
+
+        class Listener(sgx_lib.BlockFetchingListener):
+            def __init__(self):
+                self.ok, self.failed = {}, {}
+
+            def onBlockFetchSuccess(self, blockId, data):
+                self.ok[blockId] = bytes(data)
+
+            def onBlockFetchFailure(self, blockId, exception):
+                self.failed[blockId] = exception
+
+        ids = [f"shuffle_3_{m}_{r}" for r in range(R) for m in (0, 1)][:130]
+        lst = Listener()
+        client = mgr.shuffleClient
+        client.fetchBlocks("localhost", 1338, "1", ids, lst)
+        assert client.requests == 3 and not lst.failed
+        for b in ids:
+            _, m, r = sgx_lib.parse_block_id(b)
+            out, counts = outs[m]
+            o = oracle_lib.offsets(counts)
+            assert lst.ok[b] == out[o[r]:o[r + 1]].tobytes()
+        bad = Listener()
+        client.fetchBlocks("localhost", 1338, "1", ["shuffle_3_0_1", "shuffle_3_9_1"], bad)
+        assert set(bad.failed) == {"shuffle_3_0_1", "shuffle_3_9_1"} and not bad.ok
+        assert isinstance(bad.failed["shuffle_3_9_1"], sgx_lib.BlockNotFoundException)
+    finally:
+        mgr.stop()
+
+
+def test_memory_pool_size_classes_and_reuse(sgx_lib, oracle_lib):
+    """MemoryPool (memory/MemoryPool.scala:34-147): power-of-two classes from 4 KiB, close()
+    returns a block to its class, preallocation fills a class; pool blocks serve as the
+    fetch allocator of fetchBlocksByBlockIds."""
+    import ctypes
+
+    mgr = sgx_lib.UcxShuffleManager()
+    try:
+        pool = mgr.getTransport().hostBounceBufferMemoryPool
+        a = pool.get(1)
+        assert a.size == 4096 and a.isHostMemory
+        b = pool.get(4097)
+        assert b.size == 8192
+        ctypes.memset(b.address, 7, b.size)  # host-visible pinned memory
+        addr = b.address
+        b.close()
+        c = pool.get(5000)
+        assert c.address == addr  # reused from the class's free list
+        pool.preallocate(70_000, 3)
+        alloc, idle = pool.stats()
+        assert idle == 3 * 131072 and alloc >= idle + 4096 + 8192
+        d = pool.get(100_000, host=False)
+        assert d.size == 131072 and not d.isHostMemory
+        for blk in (a, c, d):
+            blk.close()
+        # as the fetch allocator
+        h = mgr.registerShuffle(4, sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(16)))
+        recs = oracle_lib.gen_uniform16(3000, 4)
+        mgr.getWriter(h, 0).write(recs)
+        out, counts = oracle_lib.map_write(recs, 16)
+        got = {}
+        t = mgr.getTransport()
+        t.fetchBlocksByBlockIds(1, [sgx_lib.UcxShuffleBlockId(4, 0, 5)], pool.get,
+                                [lambda res: got.setdefault("r", res)])
+        t.progress()
+        mb = got["r"].getData()
+        o = oracle_lib.offsets(counts) * 16
+        assert ctypes.string_at(mb.address, mb.size) == out.reshape(-1)[o[5]:o[6]].tobytes()
+        mb.close()
+    finally:
+        mgr.stop()
