@@ -236,7 +236,10 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
         uint32_t *sw = (uint32_t *)s_in[l];
 #pragma unroll 8
         for (int i = threadIdx.x; i < full; i += 64) sw[i] = gw[i];
-        if (threadIdx.x < ((sh + n) & 3)) s_in[l][full * 4 + threadIdx.x] = g[full * 4 - sh + threadIdx.x];
+        // signed index: threadIdx.x is unsigned, and full * 4 - sh < 0 for a block of
+        // n < 4 - sh bytes (a 1-byte tail block at an odd offset reads g[-1..0])
+        const int t = (int)threadIdx.x;
+        if (t < ((sh + n) & 3)) s_in[l][full * 4 + t] = g[full * 4 - sh + t];
     }
     for (int i = threadIdx.x; i < kLanes * kTable / 2; i += 64) ((uint32_t *)s_tab)[i] = 0u;
     __syncthreads();

@@ -146,6 +146,31 @@ def test_gpu_matches_oracle_mixed_partitions(engine, oracle_lib, block_size):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("block_size", [4096, 64])
+def test_gpu_tiny_blocks_at_every_byte_phase(engine, oracle_lib, block_size):
+    """Partitions whose tail block (and whole partitions) of 1..5 bytes start at every byte
+    phase of a dword: a block of n < 4 - phase bytes is staged from g[-phase..n) (the
+    regression of round 2's multi-rank LZ4 fault, a 1-byte tail at an odd offset)."""
+    rng = np.random.default_rng(17)
+    plen = []
+    for phase in range(4):
+        for tail in range(1, 6):
+            pad = (phase - sum(plen)) % 4  # next partition starts at `phase` mod 4
+            plen += [pad + 4, block_size + tail, tail]
+    stream = rng.integers(0, 256, size=sum(plen), dtype=np.uint8)
+    offs = np.zeros(len(plen) + 1, dtype=np.int64)
+    np.cumsum(plen, out=offs[1:])
+    buf = _to_device(engine, stream.tobytes())
+    try:
+        framed, lens = engine.lz4_frame(buf.ptr, offs, block_size)
+    finally:
+        buf.free()
+    want, wlens = oracle_lib.lz4_frame_partitions(stream, offs, block_size)
+    assert np.array_equal(lens, wlens)
+    assert framed.tobytes() == want.tobytes()
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("R", [1, 200])
 def test_gpu_kryo_map_output_compressed(engine, oracle_lib, R):
     """A Kryo (Long, Long) map output written by the engine, then LZ4-framed on the GPU: the
