@@ -42,7 +42,8 @@ def parse():
     ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
     ap.add_argument("--seed", type=int, default=0x5EEDC0DE)
     ap.add_argument("--num-chunks", type=int, default=0)
-    ap.add_argument("--cpu-baseline-seconds", type=float, default=10.0)
+    ap.add_argument("--cpu-baseline-seconds", type=float, default=16.0,
+                    help="budget of the CPU baseline's timed legs (plus ~5 s of C0 and setup)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--serializer", choices=["fixed", "kryo"], default="fixed",
@@ -50,42 +51,100 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(args, n_total_hint):
-    """Oracle (C restatement, pthreads) on a bounded sample of the same workload."""
+def _cpu_share():
+    """Threads the CPU baseline may use: the affinity mask, capped by a cgroup CPU quota when
+    one is set (cgroup v2 cpu.max or v1 cfs quota).  Returns (threads, affinity, quota)."""
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    quota = None
+    for path, parse in (("/sys/fs/cgroup/cpu.max", lambda t: t.split()),
+                        ("/sys/fs/cgroup/cpu/cpu.cfs_quota_us", lambda t: [t.strip(), open(
+                            "/sys/fs/cgroup/cpu/cpu.cfs_period_us").read().strip()])):
+        try:
+            with open(path) as f:
+                q, per = parse(f.read())
+            if q not in ("max", "-1"):
+                quota = max(1, int(int(q) / int(per)))
+            break
+        except (OSError, ValueError):
+            continue
+    return (min(aff, quota) if quota else aff), aff, quota
+
+
+def _time_leg(fn, seconds):
+    fn()  # warm-up (page faults, thread start)
+    t0 = time.perf_counter()
+    reps = 0
+    while True:
+        fn()
+        reps += 1
+        dt = time.perf_counter() - t0
+        if dt >= seconds:
+            return reps, dt
+
+
+def cpu_baseline(args):
+    """SURVEY §8(d) CPU baseline: the oracle's C restatement of the map-side write (pthreads:
+    per-thread histogram, prefix, stable scatter; oracle/shuffle_oracle.c orc_map_write) on
+    bounded samples of the BASELINE configs' per-GPU inputs, with every usable core and with
+    one; C0 (groupByKey 2 x 5M -> 200) also runs the reduce-side grouping of the restatement
+    (numpy, one thread).  ``value`` is the C1 all-cores leg, the workload of the GPU line."""
     import numpy as np
 
     import oracle
 
-    try:
-        cores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        cores = os.cpu_count() or 1
-    cores = max(1, min(cores, 16))  # the GPU box's CPU share is 16
+    threads, aff, quota = _cpu_share()
+    per = max(0.5, args.cpu_baseline_seconds / 8.0)
+    legs = {}
+
+    def leg(name, recs, R, kind=oracle.PART_HASH, bounds=None):
+        rb = recs.shape[1]
+        for nt in (threads, 1):
+            sample = recs if nt > 1 else recs[: max(1, len(recs) // 4)]
+            reps, dt = _time_leg(lambda: oracle.map_write(sample, R, kind, bounds, True, nthreads=nt), per)
+            legs[f"{name}_{'all' if nt > 1 else '1'}core"] = {
+                "GBs": round(rb * len(sample) * reps / dt / 1e9, 3), "threads": nt, "records": len(sample),
+                "record_bytes": rb, "partitions": R, "reps": reps, "seconds": round(dt, 2)}
+
     n = 1 << 24
     recs = oracle.gen_uniform16(n, args.seed)
-    oracle.map_write(recs, args.partitions, nthreads=cores)  # warm-up (page faults)
-    t0 = time.perf_counter()
-    reps = 0
-    while True:
-        oracle.map_write(recs, args.partitions, nthreads=cores)
-        reps += 1
-        if time.perf_counter() - t0 >= args.cpu_baseline_seconds:
-            break
-    dt = time.perf_counter() - t0
+    leg("C1_uniform_R1024", recs, 1024)
     del recs
-    return {"value": round(16.0 * n * reps / dt / 1e9, 3), "unit": "GB/s", "cores": cores, "kind": "port",
-            "sample": f"{reps} x map-side write of {n} uniform 16 B records, R={args.partitions} "
-                      f"(oracle/shuffle_oracle.c orc_map_write, {cores} threads, {dt:.1f} s)"}
+    recs = oracle.gen_zipf16(n, args.seed, oracle.zipf_cdf(1.1, 1 << 24))
+    leg("C3_zipf_R4096", recs, 4096)
+    del recs
+    nt = n * 16 // 100
+    recs = oracle.gen_terasort100(nt, args.seed)
+    keys = recs[np.random.default_rng(7).choice(nt, 20 * 1024, replace=False), :10]
+    keys = keys[np.lexsort(keys.T[::-1])]
+    bounds = np.ascontiguousarray(keys[[int(len(keys) / 1024 * (i + 1)) for i in range(1023)]])
+    leg("C4_terasort_R1024", recs, 1024, oracle.PART_RANGE_BYTES10, bounds)
+    del recs
+    # C0: two maps of 5M (Long, Long) records -> 200 reducers, groupByKey on the reduce side
+    t0 = time.perf_counter()
+    outs = [oracle.map_write(oracle.gen_uniform16(5_000_000, args.seed + m), 200, nthreads=threads) for m in range(2)]
+    t1 = time.perf_counter()
+    keys_, starts, vals = oracle.reduce_grouped(oracle.canonical_reducer_sequences(outs, 200, 16), "group")
+    t2 = time.perf_counter()
+    legs["C0_groupByKey_2x5M_R200"] = {"map_side_s": round(t1 - t0, 3), "reduce_group_s": round(t2 - t1, 3),
+                                       "records": 10_000_000, "groups": int(len(keys_)),
+                                       "threads_map_side": threads, "threads_reduce": 1}
+    c1 = legs["C1_uniform_R1024_allcore"]
+    return {"value": c1["GBs"], "unit": "GB/s", "cores": threads, "kind": "port",
+            "affinity_cores": aff, "cgroup_cpu_quota": quota,
+            "sample": f"map-side write (orc_map_write) of {c1['records']} uniform 16 B records, R=1024, "
+                      f"{c1['reps']} reps in {c1['seconds']} s on {threads} threads; other legs below",
+            "legs": legs}
 
 
-def load_traffic(config_key):
-    """HBM bytes per K4 launch from the committed rocprofv3 PMC summary (or None)."""
-    path = os.path.join(ROOT, "profiles", "pmc_scatter.json")
+def load_pmc(dist, n, R, rb=16):
+    """HBM bytes per launch of K4 and of the whole map side from the committed rocprofv3 PMC
+    summary (profiles/pmc_map.json, written by tools/summarize_prof.py), or None."""
     try:
-        with open(path) as f:
-            d = json.load(f)
-        e = d.get(config_key)
-        return None if e is None else e.get("hbm_bytes_per_launch")
+        with open(os.path.join(ROOT, "profiles", "pmc_map.json")) as f:
+            return json.load(f).get(f"{dist}_n{n}_R{R}_rb{rb}")
     except (OSError, ValueError):
         return None
 
@@ -189,7 +248,10 @@ def main():
         value = total_bytes / dt / 1e9
         sc_ms = st.ms["scatter"] / max(1, st.count["scatter"])
         achieved = ALGO_BYTES_PER_REC * n / (sc_ms * 1e-3) / 1e9
-        traffic = load_traffic(f"uniform_n{n}_R{R}" if args.dist == "uniform" else f"zipf_n{n}_R{R}")
+        pmc = load_pmc(args.dist, n, R) or {}
+        k4_pmc, side_pmc = pmc.get("scatter") or {}, pmc.get("map_side") or {}
+        side_ms = (st.ms["hist"] + st.ms["scan"] + st.ms["scatter"]) / max(1, st.count["scatter"])
+        side_ach = ALGO_BYTES_PER_REC * n / (side_ms * 1e-3) / 1e9
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -201,16 +263,22 @@ def main():
                        "records_per_gpu": n, "partitions": R, "record_bytes": 16,
                        "parallelism": f"dp{world} (map shards per GPU, reducers owned floor(r*P/R))"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": "k_scatter16 (K4)", "algo_bytes_per_record": ALGO_BYTES_PER_REC},
+                         "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": k4_pmc.get("hbm_bytes_per_launch"),
+                         "kernel": k4_pmc.get("kernel", "K4 scatter"), "algo_bytes_per_record": ALGO_BYTES_PER_REC,
+                         "traffic_source": pmc.get("source")},
+            # the whole map side (K1+K2 histogram, K3 scan, K4 scatter, their memsets) against
+            # the same 32 B/record: what north_star's partition+scatter target is quoted on
+            "roofline_map_side": {"bound": "hbm", "achieved": round(side_ach, 1), "peak": HBM_PEAK_GBS,
+                                  "unit": "GB/s", "frac": round(side_ach / HBM_PEAK_GBS, 4),
+                                  "ms": round(side_ms, 4), "algo_bytes_per_record": ALGO_BYTES_PER_REC,
+                                  "traffic": side_pmc.get("hbm_bytes_per_write"),
+                                  "traffic_over_algorithmic": side_pmc.get("ratio")},
             "stages_ms_per_step": {k: round(v / max(1, st.count[k]), 4) for k, v in st.ms.items() if st.count[k]},
-            "map_side_GBs_hist_scan_scatter": round(16.0 * n / ((st.ms["hist"] + st.ms["scan"] + st.ms["scatter"])
-                                                             / max(1, st.count["scatter"]) * 1e-3) / 1e9, 1),
             # the two-pass map side must move 48 B per AoS record (hist reads the 16 B record
             # for its 8 B key; K4 reads 16 + writes 16): its HBM stream rate against 8 TB/s
-            "map_side_hbm": (lambda t: {"bytes_per_record": 48, "achieved": round(48.0 * n / t / 1e9, 1),
-                                        "frac": round(48.0 * n / t / 1e9 / HBM_PEAK_GBS, 4)})(
-                (st.ms["hist"] + st.ms["scan"] + st.ms["scatter"]) / max(1, st.count["scatter"]) * 1e-3),
+            "map_side_two_pass_hbm": {"bytes_per_record": 48, "achieved": round(48.0 * n / side_ms / 1e6, 1),
+                                      "frac": round(48.0 * n / side_ms / 1e6 / HBM_PEAK_GBS, 4)},
             "verified_lengths_sum": verified,
         }
         if xgmi is not None:
@@ -237,7 +305,7 @@ def main():
                     "gather_ms": round(st2.ms["regroup"] / max(1, st2.count["regroup"]), 4)}
                 dst.free()
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(args, n)
+            out["cpu_baseline"] = cpu_baseline(args)
         elif world == 1:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)

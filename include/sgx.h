@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SGX_ABI_VERSION 2
+#define SGX_ABI_VERSION 3
 
 enum sgx_status {
     SGX_OK = 0,
@@ -146,6 +146,12 @@ int sgx_set_compression(sgx_engine *e, int32_t shuffle_id, int32_t codec, int32_
  * XXH32 are checked: SGX_ERR_INVALID on a malformed or corrupt stream.  Synchronous. */
 int sgx_lz4_unframe(sgx_engine *e, const void *framed_dev, int64_t framed_bytes, void *dst_dev, int64_t dst_cap,
                     int64_t *out_bytes);
+/* The same over fetched blocks whose extents are known (stream_lens[nstreams], summing to the
+ * buffer's bytes; each one LZ4 stream, e.g. one partition block of one map): the frame walks run
+ * one per stream in parallel instead of one serial walk over the whole buffer.  The reduce-side
+ * reads (sgx_read_*) of a compressed shuffle decode this way. */
+int sgx_lz4_unframe_streams(sgx_engine *e, const void *framed_dev, const int64_t *stream_lens, int64_t nstreams,
+                            void *dst_dev, int64_t dst_cap, int64_t *out_bytes);
 /* dep.mapSideCombine with dep.aggregator (reduceByKey: Spark's default is mapSideCombine =
  * true; the writer built at spark_3_0/UcxShuffleManager.scala:48-51 then runs
  * ExternalSorter.insertAll with the aggregator, and the reader merges combiners with
@@ -331,12 +337,15 @@ int sgx_pool_stats(sgx_engine *e, int64_t *out_allocated_bytes, int64_t *out_idl
 enum sgx_stage { SGX_STAGE_HIST = 0, SGX_STAGE_SCAN = 1, SGX_STAGE_SCATTER = 2,
                  SGX_STAGE_ALLGATHER = 3, SGX_STAGE_ALLTOALL = 4, SGX_STAGE_REGROUP = 5,
                  SGX_STAGE_SORT = 6, SGX_STAGE_GROUP = 7, SGX_STAGE_SERIALIZE = 8,
-                 SGX_STAGE_DESERIALIZE = 9, SGX_STAGE_COMBINE = 10, SGX_NUM_STAGES = 11 };
+                 SGX_STAGE_DESERIALIZE = 9, SGX_STAGE_COMBINE = 10, SGX_STAGE_COMPRESS = 11,
+                 SGX_STAGE_DECOMPRESS = 12, SGX_NUM_STAGES = 13 };
 /* SGX_STAGE_SORT times sgx_read_sorted's radix + partitioner passes (the fetch gather is
  * REGROUP), SGX_STAGE_GROUP the grouping / summing kernels of sgx_read_grouped,
  * SGX_STAGE_COMBINE the map-side combine of sgx_write_map (sort + sum + repartition),
  * SGX_STAGE_SERIALIZE the Kryo framing kernel of sgx_write_map (SGX_SER_KRYO),
- * SGX_STAGE_DESERIALIZE the Kryo decoder of the reduce-side reads. */
+ * SGX_STAGE_DESERIALIZE the Kryo decoder of the reduce-side reads, SGX_STAGE_COMPRESS the LZ4
+ * block kernel of a compressed map output (spark.shuffle.compress), SGX_STAGE_DECOMPRESS the
+ * LZ4 block decoder of the reduce side (frame walks excluded). */
 int sgx_stats_reset(sgx_engine *e);
 /* out_ms[SGX_NUM_STAGES] summed milliseconds, out_count[SGX_NUM_STAGES] launches. */
 int sgx_stats_get(sgx_engine *e, double *out_ms, int64_t *out_count);

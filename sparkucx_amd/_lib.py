@@ -23,11 +23,11 @@ MEM_HOST, MEM_DEVICE = 0, 1
 AGG_GROUP, AGG_SUM = 0, 1
 SER_FIXED, SER_KRYO = 0, 1
 STAGES = ("hist", "scan", "scatter", "allgather", "alltoall", "regroup", "sort", "group", "serialize",
-          "deserialize", "combine")
+          "deserialize", "combine", "compress", "decompress")
 HIST_ATOMIC, HIST_BALLOT = 0, 1
 RANK_ORDERED, RANK_MATCH = 0, 1
 FLAG_NO_WRITE_COMBINING, FLAG_NO_WIDE_STAGED, FLAG_SORT_ALL_DIGITS, FLAG_DEBUG_SYNC = 1, 2, 4, 8
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 
 class ShuffleError(RuntimeError):
@@ -103,6 +103,7 @@ SIGNATURES = {
     "sgx_set_serializer": (ctypes.c_int, [_vp, _i32, _i32]),
     "sgx_lz4_frame_partitions": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _vp, _i64, _vp]),
     "sgx_lz4_unframe": (ctypes.c_int, [_vp, _vp, _i64, _vp, _i64, _P64]),
+    "sgx_lz4_unframe_streams": (ctypes.c_int, [_vp, _vp, _vp, _i64, _vp, _i64, _P64]),
     "sgx_set_compression": (ctypes.c_int, [_vp, _i32, _i32, _i32]),
     "sgx_write_map": (ctypes.c_int, [_vp, _i32, _i64, _vp, _i64, _i32, _i32, _vp]),
     "sgx_map_lengths": (ctypes.c_int, [_vp, _i32, _i64, _vp]),

@@ -313,7 +313,8 @@ int sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool by_par
 int lz4_frame_impl(sgx_engine *e, Ctx &c, const void *stream_dev, const int64_t *part_offsets, int32_t R,
                    int32_t block_size, DevBuf *alloc_dst, void *dst_dev, int64_t dst_cap, int64_t *out_lengths);
 int lz4_unframe_impl(sgx_engine *e, Ctx &c, const void *framed_dev, int64_t framed_bytes, DevBuf *alloc_dst,
-                     void *dst_dev, int64_t dst_cap, int64_t *out_bytes);
+                     void *dst_dev, int64_t dst_cap, int64_t *out_bytes, const int64_t *stream_lens = nullptr,
+                     int64_t nstreams = 0);
 // Wait for the exchange stream with RCCL async-error polling and the engine's timeout.
 int comm_wait(sgx_engine *e);
 

@@ -98,6 +98,10 @@ hipError_t launch_lz4_gather(const uint8_t *slots, int64_t slot_bytes, const int
                              int level, uint8_t *dst, hipStream_t s);
 hipError_t launch_lz4_walk(const uint8_t *in, int64_t nbytes, int64_t *desc, int64_t desc_cap, int64_t *info,
                            hipStream_t s);
+// per-stream walk (see k_lz4_walk_streams): soff[nstreams + 1]; cnt [nstreams][2]; err: one
+// u64, initialised to ~0 by the caller (min of position << 8 | code)
+hipError_t launch_lz4_walk_streams(const uint8_t *in, const int64_t *soff, int64_t nstreams, int64_t *cnt,
+                                   int64_t *desc, unsigned long long *err, bool write, hipStream_t s);
 hipError_t launch_lz4_decode(const uint8_t *in, const int64_t *desc, int64_t nframes, uint8_t *out,
                              uint32_t *err, hipStream_t s);
 hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, int64_t n_items,

@@ -44,28 +44,50 @@ __device__ __forceinline__ uint32_t lds32(const uint8_t *p) {
 __device__ __forceinline__ uint32_t hash4(uint32_t seq) { return (seq * 2654435761u) >> (32 - kHashLog); }
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 
-__device__ uint32_t xxh32_lds(const uint8_t *p, int len, uint32_t seed) {
+// XXH32 (seed 0x9747b28c, LZ4BlockOutputStream's) of the LDS bytes [base + sh, base + sh +
+// len), base 16 B-aligned, sh < 4: whole stripes from a rolling window of ds_read_b128 (one
+// per stripe, realigned with v_alignbyte), four stripes in flight per step.  The buffer is
+// readable 16 B past the data.
+__device__ uint32_t xxh32_lds_window(const uint8_t *base, int sh, int len, uint32_t seed) {
     const uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u,
                    P5 = 374761393u;
-    const uint8_t *end = p + len;
+    const uint4 *q = (const uint4 *)base;
+    const uint32_t s8 = (uint32_t)sh;
     uint32_t h;
+    int i = 0;
     if (len >= 16) {
         uint32_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
-        const uint8_t *limit = end - 16;
-        do {
-            v1 = rotl(v1 + lds32(p) * P2, 13) * P1;
-            v2 = rotl(v2 + lds32(p + 4) * P2, 13) * P1;
-            v3 = rotl(v3 + lds32(p + 8) * P2, 13) * P1;
-            v4 = rotl(v4 + lds32(p + 12) * P2, 13) * P1;
-            p += 16;
-        } while (p <= limit);
+        const int ns = len >> 4;
+        uint4 prev = q[0];
+        int k = 0;
+        auto step = [&](const uint4 &nx) {
+            const uint32_t a0 = __builtin_amdgcn_alignbyte(prev.y, prev.x, s8);
+            const uint32_t a1 = __builtin_amdgcn_alignbyte(prev.z, prev.y, s8);
+            const uint32_t a2 = __builtin_amdgcn_alignbyte(prev.w, prev.z, s8);
+            const uint32_t a3 = __builtin_amdgcn_alignbyte(nx.x, prev.w, s8);
+            v1 = rotl(v1 + a0 * P2, 13) * P1;
+            v2 = rotl(v2 + a1 * P2, 13) * P1;
+            v3 = rotl(v3 + a2 * P2, 13) * P1;
+            v4 = rotl(v4 + a3 * P2, 13) * P1;
+            prev = nx;
+        };
+        for (; k + 4 <= ns; k += 4) {
+            uint4 x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) x[u] = q[k + 1 + u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) step(x[u]);
+        }
+        for (; k < ns; ++k) step(q[k + 1]);
         h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+        i = ns << 4;
     } else {
         h = seed + P5;
     }
     h += (uint32_t)len;
-    while (p + 4 <= end) { h = rotl(h + lds32(p) * P3, 17) * P4; p += 4; }
-    while (p < end) { h = rotl(h + (uint32_t)(*p) * P5, 11) * P1; p++; }
+    const uint8_t *p = base + sh;
+    for (; i + 4 <= len; i += 4) h = rotl(h + lds32(p + i) * P3, 17) * P4;
+    for (; i < len; ++i) h = rotl(h + (uint32_t)p[i] * P5, 11) * P1;
     h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
     return h;
 }
@@ -265,7 +287,7 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
     if (raw)
         for (int i = lane; i < n; i += 64) slot[kHeader + i] = src[i];
     if (lane != 0) return;
-    uint32_t check = xxh32_lds(src, n, 0x9747b28cu) & 0x0FFFFFFFu;
+    uint32_t check = xxh32_lds_window(s_in[0], (int)(src - s_in[0]), n, 0x9747b28cu) & 0x0FFFFFFFu;
     put_header(slot, (uint8_t)((raw ? 0x10 : 0x20) | level), (uint32_t)c, (uint32_t)n, check);
     sizes[b] = kHeader + c;
 }
@@ -320,7 +342,10 @@ __global__ void k_lz4_walk(const uint8_t *__restrict__ in, int64_t nbytes, int64
             continue;
         }
         if (olen > (uint32_t)kMaxBlock || clen == 0 || (method == 0x10u && clen != olen) ||
-            p + kHeader + (int64_t)clen > nbytes) { err = 5; break; }
+            (method == 0x20u && clen > olen + (olen >> 8) + 32) || p + kHeader + (int64_t)clen > nbytes) {
+            err = 5;  // (a compressed block past LZ4_compressBound cannot come from a compressor)
+            break;
+        }
         if (k < desc_cap) {  // past the capacity the walk only counts (caller re-walks)
             desc[2 * k + 0] = p;
             desc[2 * k + 1] = out;
@@ -335,74 +360,185 @@ __global__ void k_lz4_walk(const uint8_t *__restrict__ in, int64_t nbytes, int64
     info[3] = p;
 }
 
-// One frame per workgroup: lane 0 decodes the LZ4 block sequence by sequence into LDS
-// (bounds-checked: LZ4_decompress_safe semantics), the wave copies RAW payloads, lane 0
-// verifies XXH32, the wave writes the block out.  Errors: atomicOr into *err.
+// Per-stream walk, for callers that know where every LZ4 stream of the buffer starts (the
+// reader does: each fetched block is one partition stream): one thread per stream, so the
+// pointer chase is as long as the longest stream's frame count instead of the sum of all.
+// soff[nstreams + 1]: stream byte offsets.  Pass 0 (WRITE false) writes cnt[s] = {frames,
+// output bytes}; pass 1 (WRITE true) reads cnt[s] = {first frame index, output offset} (the
+// host's exclusive scan of pass 0) and writes desc[k] = {frame offset, output offset}.
+// Malformed input: atomicMin of (byte position << 8 | code) into *err (codes of k_lz4_walk).
+template <bool WRITE>
+__global__ __launch_bounds__(256) void k_lz4_walk_streams(const uint8_t *__restrict__ in,
+                                                          const int64_t *__restrict__ soff, int64_t nstreams,
+                                                          int64_t *__restrict__ cnt, int64_t *__restrict__ desc,
+                                                          unsigned long long *__restrict__ err) {
+    const int64_t s = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (s >= nstreams) return;
+    const int64_t end = soff[s + 1];
+    int64_t p = soff[s], k = 0, out = 0, code = 0;
+    if (WRITE) {
+        k = cnt[2 * s];
+        out = cnt[2 * s + 1];
+    }
+    while (p < end) {
+        if (p + kHeader > end) { code = 1; break; }
+        const uint8_t *h = in + p;
+        if (g32le(h) != 0x42345a4cu || g32le(h + 4) != 0x6b636f6cu) { code = 2; break; }  // "LZ4B" "lock"
+        const uint32_t tok = h[8], clen = g32le(h + 9), olen = g32le(h + 13), check = g32le(h + 17);
+        const uint32_t method = tok & 0xF0u;
+        if (method != 0x10u && method != 0x20u) { code = 3; break; }
+        if (olen == 0) {
+            if (clen != 0 || check != 0) { code = 4; break; }
+            p += kHeader;
+            continue;
+        }
+        if (olen > (uint32_t)kMaxBlock || clen == 0 || (method == 0x10u && clen != olen) ||
+            (method == 0x20u && clen > olen + (olen >> 8) + 32) || p + kHeader + (int64_t)clen > end) {
+            code = 5;
+            break;
+        }
+        if (WRITE) {
+            desc[2 * k + 0] = p;
+            desc[2 * k + 1] = out;
+        }
+        ++k;
+        out += olen;
+        p += kHeader + clen;
+    }
+    if (code) {
+        atomicMin(err, ((unsigned long long)p << 8) | (unsigned long long)code);
+        return;
+    }
+    if (!WRITE) {
+        cnt[2 * s] = k;
+        cnt[2 * s + 1] = out;
+    }
+}
+
+// LZ4_DECOMPRESS_INPLACE_BUFFER_SIZE(kMaxBlock): a compressed block placed at the end of a
+// buffer this long decodes in place -- the output never overtakes the unread input (liblz4's
+// in-place margin, (size >> 8) + 32).  One buffer instead of two keeps 4 workgroups per CU.
+constexpr int kInplace = kMaxBlock + (kMaxBlock >> 8) + 32;
+
+// One frame per workgroup (one wave).  The payload is staged in LDS by aligned dword loads
+// (keeping its misalignment): a RAW block is the output as staged; a compressed one is staged
+// at the end of the buffer and decoded in place by the 64 lanes in lockstep -- every lane parses
+// the same token bytes (uniform control flow, broadcast LDS reads) and copies its share of each
+// sequence's literals and match bytes.  A match byte i reads out[op - off + i mod off]: bytes
+// before op, already written even when the match overlaps itself (off < length), so the copy
+// is lane-parallel with LZ4_decompress_safe's result.  A literal step reads input at or after
+// the bytes it writes (in-place margin), and a wave's LDS operations complete in issue order.
+// Bounds are checked as LZ4_decompress_safe does (corrupt input can at worst garble its own
+// block, then fails the checksum); XXH32 runs over the LDS output (lane 0), then the wave
+// writes the block out with dword stores.  Errors: atomicOr into *err.
 __global__ __launch_bounds__(64) void k_lz4_decode(const uint8_t *__restrict__ in,
                                                    const int64_t *__restrict__ desc, int64_t nframes,
                                                    uint8_t *__restrict__ out, uint32_t *__restrict__ err) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_out[kMaxBlock + 16];
+    __shared__ __attribute__((aligned(16))) uint8_t s_buf[kInplace + 48];
     __shared__ int s_bad;
     const int64_t f = blockIdx.x;
     if (f >= nframes) return;
+    const int lane = (int)threadIdx.x;
     const uint8_t *h = in + desc[2 * f + 0];  // header fields validated by the walk
-    const uint8_t *src = h + kHeader;
     const uint32_t tok = h[8], clen = g32le(h + 9), olen = g32le(h + 13), check = g32le(h + 17);
-    if (threadIdx.x == 0) s_bad = 0;
-    if ((tok & 0xF0u) == 0x10u)
-        for (uint32_t i = threadIdx.x; i < olen; i += 64) s_out[i] = src[i];
+    const bool raw = (tok & 0xF0u) == 0x10u;
+    const uint8_t *g = h + kHeader;
+    const int sh = (int)((uintptr_t)g & 3u);
+    const int n = (int)clen;
+    // input position in LDS: RAW at sh (it is the output), compressed at the in-place end
+    // (rounded up to the source's byte phase)
+    int x = sh;
+    if (!raw) {
+        const int x0 = (int)olen + ((int)olen >> 8) + 32 - n;
+        x = x0 + ((sh - x0) & 3);
+    }
+    {
+        const uint32_t *gw = (const uint32_t *)(g - sh);
+        const int full = (sh + n) >> 2;
+        uint32_t *sw = (uint32_t *)(s_buf + x - sh);
+        for (int i = lane; i < full; i += 64) sw[i] = gw[i];
+        if (lane < ((sh + n) & 3)) s_buf[x - sh + full * 4 + lane] = g[full * 4 - sh + lane];
+    }
+    if (lane == 0) s_bad = 0;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        int bad = 0;
-        if ((tok & 0xF0u) == 0x20u) {
-            uint32_t ip = 0, op = 0;
-            for (;;) {
-                if (ip >= clen) { bad = 1; break; }
-                const uint32_t t = src[ip++];
-                uint32_t lit = t >> 4;
-                if (lit == 15) {
-                    uint32_t b;
-                    do {
-                        if (ip >= clen) { bad = 1; break; }
-                        b = src[ip++];
-                        lit += b;
-                    } while (b == 255);
-                    if (bad) break;
-                }
-                if (ip + lit > clen || op + lit > olen) { bad = 1; break; }
-                for (uint32_t i = 0; i < lit; ++i) s_out[op + i] = src[ip + i];
-                ip += lit;
-                op += lit;
-                if (ip == clen) break;  // the last sequence has literals only
-                if (ip + 2 > clen) { bad = 1; break; }
-                const uint32_t off = (uint32_t)src[ip] | ((uint32_t)src[ip + 1] << 8);
-                ip += 2;
-                uint32_t ml = (t & 15u) + kMinMatch;
-                if ((t & 15u) == 15u) {
-                    uint32_t b;
-                    do {
-                        if (ip >= clen) { bad = 1; break; }
-                        b = src[ip++];
-                        ml += b;
-                    } while (b == 255);
-                    if (bad) break;
-                }
-                if (off == 0 || off > op || op + ml > olen) { bad = 1; break; }
-                for (uint32_t i = 0; i < ml; ++i) s_out[op + i] = s_out[op - off + i];
-                op += ml;
+    int bad = 0;
+    int ob = sh;  // output position in LDS
+    if (!raw) {
+        ob = 0;
+        const uint8_t *src = s_buf + x;
+        uint8_t *o = s_buf;
+        uint32_t ip = 0, op = 0;
+        for (;;) {  // wave-uniform: every lane reads the same bytes
+            if (ip >= clen) { bad = 1; break; }
+            const uint32_t t = src[ip++];
+            uint32_t lit = t >> 4;
+            if (lit == 15) {
+                uint32_t b;
+                do {
+                    if (ip >= clen) { bad = 1; break; }
+                    b = src[ip++];
+                    lit += b;
+                } while (b == 255);
+                if (bad) break;
             }
-            if (!bad && op != olen) bad = 1;
+            if (ip + lit > clen || op + lit > olen) { bad = 1; break; }
+            for (uint32_t i = lane; i < lit; i += 64) o[op + i] = src[ip + i];
+            ip += lit;
+            op += lit;
+            if (ip == clen) break;  // the last sequence has literals only
+            if (ip + 2 > clen) { bad = 1; break; }
+            const uint32_t off = (uint32_t)src[ip] | ((uint32_t)src[ip + 1] << 8);
+            ip += 2;
+            uint32_t ml = (t & 15u) + kMinMatch;
+            if ((t & 15u) == 15u) {
+                uint32_t b;
+                do {
+                    if (ip >= clen) { bad = 1; break; }
+                    b = src[ip++];
+                    ml += b;
+                } while (b == 255);
+                if (bad) break;
+            }
+            if (off == 0 || off > op || op + ml > olen) { bad = 1; break; }
+            const uint32_t base = op - off;
+            if (off >= 64 || off >= ml) {
+                // every byte read was written before this loop (off >= ml) or in an earlier
+                // step of it (off >= 64)
+                for (uint32_t i = lane; i < ml; i += 64) o[op + i] = o[base + i];
+            } else {
+                const uint32_t stp = 64u % off;
+                uint32_t m = (uint32_t)lane % off;
+                for (uint32_t i = lane; i < ml; i += 64) {
+                    o[op + i] = o[base + m];
+                    m += stp;
+                    m = m >= off ? m - off : m;
+                }
+            }
+            op += ml;
         }
-        if (!bad && (xxh32_lds(s_out, (int)olen, 0x9747b28cu) & 0x0FFFFFFFu) != check) bad = 2;
+        if (!bad && op != olen) bad = 1;
+    }
+    __syncthreads();
+    if (lane == 0) {
+        if (!bad && (xxh32_lds_window(s_buf, ob, (int)olen, 0x9747b28cu) & 0x0FFFFFFFu) != check) bad = 2;
         s_bad = bad;
     }
     __syncthreads();
     if (s_bad) {
-        if (threadIdx.x == 0) atomicOr(err, (uint32_t)s_bad);
+        if (lane == 0) atomicOr(err, (uint32_t)s_bad);
         return;
     }
+    // write out: head bytes to a dword boundary, dword stores, tail bytes
+    const uint8_t *ls = s_buf + ob;
     uint8_t *d = out + desc[2 * f + 1];
-    for (uint32_t i = threadIdx.x; i < olen; i += 64) d[i] = s_out[i];
+    const int on = (int)olen;
+    const int head = min(on, (int)((4u - ((uintptr_t)d & 3u)) & 3u));
+    if (lane < head) d[lane] = ls[lane];
+    const int nw = (on - head) >> 2;
+    uint32_t *dw = (uint32_t *)(d + head);
+    for (int i = lane; i < nw; i += 64) dw[i] = lds32(ls + head + 4 * i);
+    const int tail0 = head + 4 * nw;
+    if (lane < on - tail0) d[tail0 + lane] = ls[tail0 + lane];
 }
 }  // namespace
 
@@ -435,6 +571,17 @@ namespace sgx {
 hipError_t launch_lz4_walk(const uint8_t *in, int64_t nbytes, int64_t *desc, int64_t desc_cap, int64_t *info,
                            hipStream_t s) {
     hipLaunchKernelGGL(k_lz4_walk, dim3(1), dim3(64), 0, s, in, nbytes, desc, desc_cap, info);
+    return hipGetLastError();
+}
+
+hipError_t launch_lz4_walk_streams(const uint8_t *in, const int64_t *soff, int64_t nstreams, int64_t *cnt,
+                                   int64_t *desc, unsigned long long *err, bool write, hipStream_t s) {
+    if (nstreams <= 0) return hipSuccess;
+    const dim3 grid((unsigned)((nstreams + 255) / 256));
+    if (write)
+        hipLaunchKernelGGL(k_lz4_walk_streams<true>, grid, dim3(256), 0, s, in, soff, nstreams, cnt, desc, err);
+    else
+        hipLaunchKernelGGL(k_lz4_walk_streams<false>, grid, dim3(256), 0, s, in, soff, nstreams, cnt, desc, err);
     return hipGetLastError();
 }
 

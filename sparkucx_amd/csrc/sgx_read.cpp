@@ -196,7 +196,8 @@ static int records_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_id
             SGX_TRY(fetch_impl(e, c, s, mids.data(), rids.data(), nreq, c.fetch_tmp.p, total, SGX_MEM_DEVICE,
                                lens.data(), false, &keep));
             int64_t dec = 0;
-            SGX_TRY(lz4_unframe_impl(e, c, c.fetch_tmp.p, total, &c.kryo_in, nullptr, 0, &dec));
+            // every fetched block is one partition stream: walk them in parallel
+            SGX_TRY(lz4_unframe_impl(e, c, c.fetch_tmp.p, total, &c.kryo_in, nullptr, 0, &dec, lens.data(), nreq));
             total = dec;
         }
         const int64_t cap = total / 4;  // a record takes >= 4 bytes

@@ -229,9 +229,17 @@ class ShuffleEngine:
         finally:
             buf.free()
 
-    def lz4_unframe(self, framed) -> np.ndarray:
+    def lz4_unframe(self, framed, stream_lens=None) -> np.ndarray:
         """LZ4BlockInputStream on the GPU: ``framed`` (host bytes/ndarray or DeviceBuffer) holds
-        LZ4-framed partition streams back to back; returns their decompressed bytes (host)."""
+        LZ4-framed partition streams back to back; returns their decompressed bytes (host).
+        ``stream_lens``: the streams' byte lengths when known (parallel per-stream walks)."""
+        sl = None if stream_lens is None else np.ascontiguousarray(stream_lens, dtype=np.int64)
+
+        def call(ptr, n, dst, cap, total):
+            if sl is None:
+                return lib().sgx_lz4_unframe(self.handle, ptr, n, dst, cap, total)
+            return lib().sgx_lz4_unframe_streams(self.handle, ptr, sl.ctypes.data, len(sl), dst, cap, total)
+
         own = None
         if isinstance(framed, DeviceBuffer):
             ptr, n = framed.ptr, framed.nbytes
@@ -244,11 +252,10 @@ class ShuffleEngine:
             ptr = own.ptr
         try:
             total = ctypes.c_int64()
-            check(lib().sgx_lz4_unframe(self.handle, ptr, n, None, 0, ctypes.byref(total)), "lz4 unframe (measure)")
+            check(call(ptr, n, None, 0, ctypes.byref(total)), "lz4 unframe (measure)")
             out = self.alloc(max(total.value, 1))
             try:
-                check(lib().sgx_lz4_unframe(self.handle, ptr, n, out.ptr, total.value, ctypes.byref(total)),
-                      "lz4 unframe")
+                check(call(ptr, n, out.ptr, total.value, ctypes.byref(total)), "lz4 unframe")
                 return out.to_numpy(total.value)
             finally:
                 out.free()

@@ -264,6 +264,76 @@ def test_gpu_unframe_dense_frames(engine, oracle_lib):
     assert engine.lz4_unframe(want).tobytes() == stream
 
 
+def _overlap_cases():
+    """Streams whose LZ4 blocks are full of self-overlapping matches (offsets 1..130, the
+    lane-parallel copy's i mod off path and its off >= 64 path), long match-length runs, long
+    literal runs, and mixtures -- each its own partition stream."""
+    rng = np.random.default_rng(11)
+    out = [bytes(40000), b"\x07" * 33000]
+    for period in (2, 3, 5, 7, 16, 31, 63, 64, 65, 100, 130):
+        pat = rng.integers(0, 256, period, dtype=np.uint8).tobytes()
+        out.append((pat * (70000 // period + 1))[:70000])
+    mixed = bytearray()
+    while len(mixed) < 100000:
+        k = int(rng.integers(0, 4))
+        if k == 0:
+            mixed += rng.integers(0, 256, int(rng.integers(1, 300)), dtype=np.uint8).tobytes()
+        elif k == 1:
+            mixed += bytes([int(rng.integers(0, 256))]) * int(rng.integers(1, 2000))
+        elif k == 2 and len(mixed) > 70:
+            s = int(rng.integers(0, len(mixed) - 64))
+            mixed += mixed[s:s + int(rng.integers(4, 64))]
+        else:
+            mixed += (rng.integers(0, 256, 3, dtype=np.uint8).tobytes() * 50)
+    out.append(bytes(mixed))
+    return out
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("per_stream", [False, True], ids=["one-walk", "per-stream-walk"])
+def test_gpu_unframe_overlapping_matches(engine, oracle_lib, per_stream):
+    """The in-place, lane-parallel decoder against the streams themselves (frames from the
+    oracle, whose compressor is pinned to liblz4), through the single walk and the per-stream
+    walks of sgx_lz4_unframe_streams."""
+    parts = _overlap_cases()
+    stream = b"".join(parts)
+    offs = np.zeros(len(parts) + 1, dtype=np.int64)
+    np.cumsum([len(p) for p in parts], out=offs[1:])
+    for bs in (32768, 4096, 64):
+        framed, flens = oracle_lib.lz4_frame_partitions(np.frombuffer(stream, np.uint8), offs, bs)
+        assert len(framed) < len(stream)  # the blocks really are compressed
+        got = engine.lz4_unframe(framed, flens if per_stream else None)
+        assert got.tobytes() == stream, bs
+
+
+@pytest.mark.gpu
+def test_gpu_unframe_streams_errors(engine, oracle_lib, sgx_lib):
+    parts = _overlap_cases()[:4]
+    stream = b"".join(parts)
+    offs = np.zeros(len(parts) + 1, dtype=np.int64)
+    np.cumsum([len(p) for p in parts], out=offs[1:])
+    framed, flens = oracle_lib.lz4_frame_partitions(np.frombuffer(stream, np.uint8), offs, 32768)
+    fb = bytearray(framed.tobytes())
+    # the stream lengths must cover the buffer
+    with pytest.raises(sgx_lib._lib.IllegalArgumentException):
+        engine.lz4_unframe(bytes(fb), np.concatenate([flens[:-1], [flens[-1] - 1]]))
+    # a bad magic in the third stream is reported at its byte position
+    pos = int(flens[:2].sum())
+    bad = bytearray(fb)
+    bad[pos] = ord("X")
+    with pytest.raises(sgx_lib._lib.IllegalArgumentException, match=f"bad magic at byte {pos}"):
+        engine.lz4_unframe(bytes(bad), flens)
+    # a flipped payload byte fails the block (corrupt sequence or checksum)
+    bad = bytearray(fb)
+    bad[pos + 40] ^= 0x5A
+    with pytest.raises(sgx_lib._lib.IllegalArgumentException):
+        engine.lz4_unframe(bytes(bad), flens)
+    # a block cut short inside the second stream
+    with pytest.raises(sgx_lib._lib.IllegalArgumentException):
+        engine.lz4_unframe(bytes(fb), np.concatenate([[flens[0] + flens[1] - 5, 5], flens[2:]]))
+    assert engine.lz4_unframe(bytes(fb), flens).tobytes() == stream
+
+
 # ------------------------------------------------- shuffle-level compression (engine) --
 @pytest.mark.gpu
 def test_gpu_compressed_shuffle_publishes_lz4_frames(engine, oracle_lib, sgx_lib, tmp_path):

@@ -1,15 +1,17 @@
 #!/usr/bin/env python3
-"""Turn rocprofv3 outputs (kernel-trace stats + separate FETCH_SIZE / WRITE_SIZE PMC passes)
-into committed summaries under profiles/:
+"""Turn rocprofv3 outputs of tools/gpu_prof.sh (kernel-trace stats + separate FETCH_SIZE /
+WRITE_SIZE PMC passes over tools/prof_map.py) into committed summaries under profiles/:
 
   profiles/<tag>_kernel_stats.csv   copy of rocprofv3's per-kernel stats
-  profiles/<tag>_summary.md          per-kernel mean duration, HBM traffic per launch
-  profiles/pmc_scatter.json          K4 HBM bytes per launch, read by bench.py
+  profiles/<tag>_summary.md          per-kernel mean duration and HBM traffic per launch
+  profiles/pmc_map.json              per workload: K4 and whole-map-side HBM bytes per step,
+                                     read by bench.py (roofline.traffic, roofline_map_side)
 
 HBM traffic per MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) reads exactly half of a wide
-coalesced stream on gfx950, so it is doubled; WRITE_SIZE (KiB) is taken as is.
+coalesced stream on gfx950, so it is doubled; WRITE_SIZE (KiB) is taken as is.  The map side
+is every kernel of the write except the input generator, per write (calls / iters).
 
-usage: summarize_prof.py <tag> <kernel_trace_dir> <fetch_dir> <write_dir> <records> <R>
+usage: summarize_prof.py <tag> <out_dir of gpu_prof.sh> <records> <R> <dist> [record_bytes]
 """
 import csv
 import json
@@ -28,46 +30,60 @@ def short(name):
 
 def pmc(d, counter):
     out = defaultdict(list)
-    with open(os.path.join(d, "run_counter_collection.csv")) as f:
-        for r in csv.DictReader(f):
-            if r["Counter_Name"] == counter:
-                out[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
+    for fn in ("run_counter_collection.csv",):
+        with open(os.path.join(d, fn)) as f:
+            for r in csv.DictReader(f):
+                if r["Counter_Name"] == counter:
+                    out[short(r["Kernel_Name"])].append(float(r["Counter_Value"]))
     return out
 
 
 def main():
-    tag, kt, fd, wd, n, R = sys.argv[1:7]
+    tag, d, n, R, dist = sys.argv[1:6]
+    rb = int(sys.argv[6]) if len(sys.argv) > 6 else 16
     n, R = int(n), int(R)
     prof = os.path.join(ROOT, "profiles")
-    shutil.copy(os.path.join(kt, "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
+    shutil.copy(os.path.join(d, "kt", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
     stats = {}
-    with open(os.path.join(kt, "run_kernel_stats.csv")) as f:
+    with open(os.path.join(d, "kt", "run_kernel_stats.csv")) as f:
         for r in csv.DictReader(f):
             stats[short(r["Name"])] = (int(r["Calls"]), float(r["AverageNs"]))
-    fetch, write = pmc(fd, "FETCH_SIZE"), pmc(wd, "WRITE_SIZE")
-    lines = [f"# rocprofv3 summary `{tag}` — map-side write, {n} x 16 B records, R = {R}", "",
-             "| kernel | calls | mean µs | HBM read GB/launch (FETCH×2) | HBM write GB/launch | traffic GB/s |",
+    fetch, write = pmc(os.path.join(d, "fetch"), "FETCH_SIZE"), pmc(os.path.join(d, "write"), "WRITE_SIZE")
+    iters_kt, iters_pmc = 5, 2
+    algo = 2 * rb * n
+    lines = [f"# rocprofv3 summary `{tag}` — map-side write, {n} x {rb} B records ({dist}), R = {R}", "",
+             "| kernel | calls/write | mean µs | HBM read GB/launch (FETCH×2) | HBM write GB/launch | traffic GB/s |",
              "|---|---|---|---|---|---|"]
-    out_json = {}
+    side = {"read_bytes": 0.0, "write_bytes": 0.0, "us": 0.0}
+    k4 = None
     for k, (calls, avg) in sorted(stats.items(), key=lambda kv: -kv[1][0] * kv[1][1]):
-        rd = statistics.median(fetch[k]) * 2 * 1024 if k in fetch else None
-        wr = statistics.median(write[k]) * 1024 if k in write else None
-        tr = (rd + wr) / (avg * 1e-9) / 1e9 if rd is not None and wr is not None else None
-        lines.append(f"| `{k}` | {calls} | {avg / 1e3:.1f} | {rd / 1e9 if rd else 0:.3f} | "
-                     f"{wr / 1e9 if wr else 0:.3f} | {tr or 0:.0f} |")
-        if "k_scatter16" in k and rd is not None and wr is not None:
-            out_json[f"uniform_n{n}_R{R}"] = {"kernel": k, "hbm_bytes_per_launch": int(rd + wr),
-                                              "read_bytes": int(rd), "write_bytes": int(wr),
-                                              "algorithmic_bytes": 32 * n, "mean_ns": avg, "source": tag}
-    lines += ["", f"Algorithmic bytes of K4 per launch: 32 x {n} = {32 * n / 1e9:.3f} GB "
-              "(16 B read + 16 B write per record)."]
+        if k.replace("sgx::", "").startswith("k_gen"):
+            continue
+        per = calls / iters_kt
+        rd = statistics.median(fetch[k]) * 2 * 1024 if k in fetch else 0.0
+        wr = statistics.median(write[k]) * 1024 if k in write else 0.0
+        tr = (rd + wr) / (avg * 1e-9) / 1e9
+        lines.append(f"| `{k}` | {per:g} | {avg / 1e3:.1f} | {rd / 1e9:.3f} | {wr / 1e9:.3f} | {tr:.0f} |")
+        side["read_bytes"] += rd * per
+        side["write_bytes"] += wr * per
+        side["us"] += avg / 1e3 * per
+        if k.replace("sgx::", "").startswith("k_scatter") and (k4 is None or avg > k4["mean_ns"]):
+            k4 = {"kernel": k, "hbm_bytes_per_launch": int(rd + wr), "read_bytes": int(rd), "write_bytes": int(wr),
+                  "algorithmic_bytes": algo, "mean_ns": avg}
+    tot = side["read_bytes"] + side["write_bytes"]
+    lines += ["", f"Map side per write: {side['us']:.1f} µs of kernels, HBM {tot / 1e9:.3f} GB "
+              f"(read {side['read_bytes'] / 1e9:.3f}, write {side['write_bytes'] / 1e9:.3f}); algorithmic "
+              f"{algo / 1e9:.3f} GB ({2 * rb} B x records: the record read once and written once) -> "
+              f"{tot / algo:.3f}x."]
     with open(os.path.join(prof, f"{tag}_summary.md"), "w") as f:
         f.write("\n".join(lines) + "\n")
-    if out_json:
-        path = os.path.join(prof, "pmc_scatter.json")
-        cur = json.load(open(path)) if os.path.exists(path) else {}
-        cur.update(out_json)
-        json.dump(cur, open(path, "w"), indent=1)
+    path = os.path.join(prof, "pmc_map.json")
+    cur = json.load(open(path)) if os.path.exists(path) else {}
+    cur[f"{dist}_n{n}_R{R}_rb{rb}"] = {"scatter": k4, "map_side": {
+        "hbm_bytes_per_write": int(tot), "read_bytes": int(side["read_bytes"]),
+        "write_bytes": int(side["write_bytes"]), "kernel_us": round(side["us"], 1),
+        "algorithmic_bytes": algo, "ratio": round(tot / algo, 4)}, "source": tag}
+    json.dump(cur, open(path, "w"), indent=1, sort_keys=True)
     print("\n".join(lines))
 
 
