@@ -36,6 +36,7 @@ Ctx *sgx_engine::ctx() {
         }
         slot = std::move(c);
     }
+    slot->ops++;
     return slot.get();
 }
 
@@ -214,6 +215,7 @@ static int max_partitions(int rb) {
 extern "C" int sgx_register_shuffle(sgx_engine *e, int32_t shuffle_id, int32_t R, int32_t kind,
                                     const void *bounds, int64_t nbounds, int32_t ascending,
                                     int32_t rb) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     if (R < 1) return fail_msg(SGX_ERR_INVALID, "numPartitions must be positive, got %d", R);
     if (kind < SGX_PART_HASH || kind > SGX_PART_RANGE_BYTES10)
@@ -259,6 +261,7 @@ extern "C" int sgx_register_shuffle(sgx_engine *e, int32_t shuffle_id, int32_t R
 }
 
 extern "C" int sgx_unregister_shuffle(sgx_engine *e, int32_t shuffle_id) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     HIP_TRY(hipSetDevice(e->device));
     std::shared_ptr<Shuffle> s;
@@ -276,6 +279,7 @@ extern "C" int sgx_unregister_shuffle(sgx_engine *e, int32_t shuffle_id) {
 }
 
 extern "C" int sgx_set_serializer(sgx_engine *e, int32_t shuffle_id, int32_t serializer) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
     if (!s) return SGX_ERR_STATE;
@@ -293,6 +297,7 @@ extern "C" int sgx_set_serializer(sgx_engine *e, int32_t shuffle_id, int32_t ser
 }
 
 extern "C" int sgx_set_compression(sgx_engine *e, int32_t shuffle_id, int32_t codec, int32_t block_size) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
     if (!s) return SGX_ERR_STATE;
@@ -311,6 +316,7 @@ extern "C" int sgx_set_compression(sgx_engine *e, int32_t shuffle_id, int32_t co
 }
 
 extern "C" int sgx_set_map_side_combine(sgx_engine *e, int32_t shuffle_id, int32_t agg) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
     if (!s) return SGX_ERR_STATE;

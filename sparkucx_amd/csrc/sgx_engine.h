@@ -20,6 +20,7 @@
 
 #include <map>
 #include <memory>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -207,6 +208,19 @@ struct Shuffle {
 // ------------------------------------------------------------------------------------
 struct Ctx {
     hipStream_t st = nullptr;
+    uint64_t ops = 0;  // API calls made with this context (sgx_engine::ctx)
+    // The last reduce-side result computed on this context: a size query (NULL destination)
+    // leaves it here and the filling call that follows it directly on the same thread, with
+    // the same arguments and no mutation of the engine in between, reuses it instead of
+    // fetching / decoding / sorting / grouping again.
+    struct ReadCache {
+        uint64_t ops = ~0ull, epoch = 0;
+        int32_t sid = -1, kind = -1, agg = -1, r0 = 0, r1 = 0;
+        std::vector<int64_t> maps;
+        int64_t n = 0, ng = 0;
+        const void *sorted = nullptr;
+        int64_t *keys = nullptr, *starts = nullptr, *vals = nullptr;
+    } rc;
     // map side: [counts][ticket | look-back status][partition offsets | error] + offs[R][G]
     DevBuf offs, work;
     DevBuf input_stage;
@@ -238,6 +252,10 @@ struct PoolState;  // sgx_pool.cpp
 }  // namespace sgx
 
 struct sgx_engine {
+    // bumped by every call that changes what a read could return (maps, rounds, shuffle
+    // properties): a cached read result is valid only for the epoch it was computed in
+    std::atomic<uint64_t> epoch{0};
+    void mutated() { epoch.fetch_add(1, std::memory_order_relaxed); }
     int device = 0;
     int num_cus = 256;
     int G = 256;

@@ -26,6 +26,7 @@ extern "C" int sgx_get_unique_id(uint8_t out_id[128]) {
 }
 
 extern "C" int sgx_comm_init(sgx_engine *e, int32_t nranks, int32_t rank, const uint8_t id[128]) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e || !id || nranks < 1 || rank < 0 || rank >= nranks) return fail_msg(SGX_ERR_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(e->comm_mu);
     if (e->comm || e->host_comm) return fail_msg(SGX_ERR_STATE, "communicator already initialised");
@@ -39,6 +40,7 @@ extern "C" int sgx_comm_init(sgx_engine *e, int32_t nranks, int32_t rank, const 
 }
 
 extern "C" int sgx_comm_init_host(sgx_engine *e, int32_t nranks, int32_t rank, const sgx_host_comm *hc) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e || !hc || !hc->allgather || !hc->alltoallv || nranks < 1 || rank < 0 || rank >= nranks)
         return fail_msg(SGX_ERR_INVALID, "bad arguments");
     std::lock_guard<std::mutex> lk(e->comm_mu);
@@ -94,6 +96,7 @@ int sgx::comm_wait(sgx_engine *e) {
 }
 
 extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     HIP_TRY(hipSetDevice(e->device));
     Ctx *c = e->ctx();

@@ -283,6 +283,7 @@ static int device_input(Ctx &c, const void *records, int64_t bytes, int32_t mem_
 
 extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records,
                              int64_t n, int32_t rb, int32_t mem_kind, int64_t *out_lengths) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
     if (!s) return SGX_ERR_STATE;
@@ -318,6 +319,7 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
 // streaming map outputs
 // ------------------------------------------------------------------------------------
 extern "C" int sgx_map_begin(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
     if (!s) return SGX_ERR_STATE;
@@ -336,6 +338,7 @@ extern "C" int sgx_map_begin(sgx_engine *e, int32_t shuffle_id, int64_t map_id) 
 
 extern "C" int sgx_map_append(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records, int64_t n,
                               int32_t rb, int32_t mem_kind) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     std::shared_ptr<Shuffle> s;
     std::shared_ptr<MapOut> m;
@@ -365,6 +368,7 @@ extern "C" int sgx_map_append(sgx_engine *e, int32_t shuffle_id, int64_t map_id,
 }
 
 extern "C" int sgx_map_commit(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *out_lengths) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     std::shared_ptr<Shuffle> s;
     std::shared_ptr<MapOut> m;

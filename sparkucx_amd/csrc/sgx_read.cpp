@@ -368,6 +368,38 @@ static int copy_out(Ctx &c, void *dst, const void *src, int64_t bytes, int32_t m
 }
 
 // Common entry checks of the reads; *s and *c on success.
+// ------------------------------------------------------------------------------------
+// size query + fill: reuse of the size query's result (Ctx::ReadCache)
+// ------------------------------------------------------------------------------------
+enum { RC_RECORDS = 0, RC_SORTED = 1, RC_GROUPED = 2 };
+
+static bool rc_hit(const Ctx &c, uint64_t epoch, int kind, int agg, int32_t sid, const int64_t *maps, int64_t nmaps,
+                   int32_t r0, int32_t r1) {
+    const Ctx::ReadCache &k = c.rc;
+    return k.ops + 1 == c.ops && k.epoch == epoch && k.kind == kind && k.agg == agg && k.sid == sid && k.r0 == r0 &&
+           k.r1 == r1 && (int64_t)k.maps.size() == nmaps && (nmaps == 0 || std::equal(k.maps.begin(), k.maps.end(), maps));
+}
+
+static void rc_store(Ctx &c, uint64_t epoch, int kind, int agg, int32_t sid, const int64_t *maps, int64_t nmaps,
+                     int32_t r0, int32_t r1, int64_t n, int64_t ng, const void *sorted, int64_t *keys, int64_t *starts,
+                     int64_t *vals) {
+    Ctx::ReadCache &k = c.rc;
+    k.ops = c.ops;
+    k.epoch = epoch;
+    k.kind = kind;
+    k.agg = agg;
+    k.sid = sid;
+    k.r0 = r0;
+    k.r1 = r1;
+    k.maps.assign(maps, maps + nmaps);
+    k.n = n;
+    k.ng = ng;
+    k.sorted = sorted;
+    k.keys = keys;
+    k.starts = starts;
+    k.vals = vals;
+}
+
 static int read_entry(sgx_engine *e, int32_t shuffle_id, int32_t mem_kind, std::shared_ptr<Shuffle> *s, Ctx **c) {
     if (mem_kind != SGX_MEM_HOST && mem_kind != SGX_MEM_DEVICE) return fail_msg(SGX_ERR_INVALID, "unknown mem_kind %d", mem_kind);
     *s = e->find_shuffle(shuffle_id);
@@ -385,9 +417,14 @@ extern "C" int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t 
     Ctx *c = nullptr;
     SGX_TRY(read_entry(e, shuffle_id, dst_mem_kind, &s, &c));
     const int rb = s->rb;
-    if (!dst && dst_cap == 0 && s->ser == SGX_SER_KRYO) {  // size query: decoded records
+    const uint64_t epoch = e->epoch.load();
+    if (!dst && dst_cap == 0 && s->ser == SGX_SER_KRYO) {  // size query: decoded records, sorted and kept
         int64_t n = 0;
+        const void *sorted = nullptr;
         SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
+        SGX_TRY(sort_records(e, *c, *s, n, true, &sorted));
+        rc_store(*c, epoch, RC_SORTED, 0, shuffle_id, map_ids, nmaps, start_partition, end_partition, n, 0, sorted,
+                 nullptr, nullptr, nullptr);
         *out_bytes = n * rb;
         return SGX_OK;
     }
@@ -408,9 +445,14 @@ extern "C" int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t 
         return SGX_OK;
     }
     int64_t n = 0;
-    SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
     const void *sorted = nullptr;
-    SGX_TRY(sort_records(e, *c, *s, n, true, &sorted));
+    if (rc_hit(*c, epoch, RC_SORTED, 0, shuffle_id, map_ids, nmaps, start_partition, end_partition)) {
+        n = c->rc.n;
+        sorted = c->rc.sorted;
+    } else {
+        SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
+        SGX_TRY(sort_records(e, *c, *s, n, true, &sorted));
+    }
     *out_bytes = n * rb;
     if (n * rb > dst_cap)
         return fail_msg(SGX_ERR_INVALID, "destination capacity %lld < %lld bytes", (long long)dst_cap,
@@ -429,10 +471,18 @@ extern "C" int sgx_read_records(sgx_engine *e, int32_t shuffle_id, const int64_t
     Ctx *c = nullptr;
     SGX_TRY(read_entry(e, shuffle_id, dst_mem_kind, &s, &c));
     const int rb = s->rb;
+    const uint64_t epoch = e->epoch.load();
     int64_t n = 0;
-    SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
+    if (rc_hit(*c, epoch, RC_RECORDS, 0, shuffle_id, map_ids, nmaps, start_partition, end_partition))
+        n = c->rc.n;  // the records are still in c->sort_buf[0]
+    else
+        SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
     *out_bytes = n * rb;
-    if (!dst && dst_cap == 0) return SGX_OK;  // size query
+    if (!dst && dst_cap == 0) {  // size query
+        rc_store(*c, epoch, RC_RECORDS, 0, shuffle_id, map_ids, nmaps, start_partition, end_partition, n, 0,
+                 c->sort_buf[0].p, nullptr, nullptr, nullptr);
+        return SGX_OK;
+    }
     if (n * rb > dst_cap)
         return fail_msg(SGX_ERR_INVALID, "destination capacity %lld < %lld bytes", (long long)dst_cap,
                         (long long)(n * rb));
@@ -457,17 +507,29 @@ extern "C" int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t
     if (s->combine == SGX_AGG_SUM && agg != SGX_AGG_SUM)
         return fail_msg(SGX_ERR_UNSUPPORTED, "shuffle %d was combined map-side (sum): read it with SGX_AGG_SUM",
                         shuffle_id);
-    int64_t n = 0;
-    SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
-    const void *sorted = nullptr;
-    SGX_TRY(sort_records(e, *c, *s, n, true, &sorted));
-    int64_t ng = 0;
+    const uint64_t epoch = e->epoch.load();
+    int64_t n = 0, ng = 0;
     int64_t *dkeys = nullptr, *dstarts = nullptr, *dvals = nullptr;
-    SGX_TRY(group_records(e, *c, sorted, n, agg, &ng, &dkeys, &dstarts, &dvals));
+    if (rc_hit(*c, epoch, RC_GROUPED, agg, shuffle_id, map_ids, nmaps, start_partition, end_partition)) {
+        n = c->rc.n;
+        ng = c->rc.ng;
+        dkeys = c->rc.keys;
+        dstarts = c->rc.starts;
+        dvals = c->rc.vals;
+    } else {
+        SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
+        const void *sorted = nullptr;
+        SGX_TRY(sort_records(e, *c, *s, n, true, &sorted));
+        SGX_TRY(group_records(e, *c, sorted, n, agg, &ng, &dkeys, &dstarts, &dvals));
+    }
     const int64_t nvals = agg == SGX_AGG_GROUP ? n : ng;
     *out_groups = ng;
     *out_values = nvals;
-    if (!keys && cap_groups == 0 && cap_values == 0) return SGX_OK;  // size query
+    if (!keys && cap_groups == 0 && cap_values == 0) {  // size query
+        rc_store(*c, epoch, RC_GROUPED, agg, shuffle_id, map_ids, nmaps, start_partition, end_partition, n, ng, nullptr,
+                 dkeys, dstarts, dvals);
+        return SGX_OK;
+    }
     if (ng > cap_groups || nvals > cap_values)
         return fail_msg(SGX_ERR_INVALID, "capacity (%lld groups, %lld values) < (%lld, %lld)", (long long)cap_groups,
                         (long long)cap_values, (long long)ng, (long long)nvals);

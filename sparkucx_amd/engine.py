@@ -352,25 +352,40 @@ class ShuffleEngine:
         return dst
 
     def read_grouped(self, shuffle_id: int, map_ids: Sequence[int], start_partition: int, end_partition: int,
-                     agg: int = _lib.AGG_GROUP):
-        """UcxShuffleReader.read with an aggregator (mapSideCombine = false) on (Long, Long)
-        records.  AGG_GROUP -> (keys, group_starts, values); AGG_SUM -> (keys, sums).
-        Keys ascending per reducer, values in canonical arrival order."""
+                     agg: int = _lib.AGG_GROUP, device: bool = False):
+        """UcxShuffleReader.read with an aggregator on (Long, Long) records.  AGG_GROUP ->
+        (keys, group_starts, values); AGG_SUM -> (keys, sums).  Keys ascending per reducer,
+        values in canonical arrival order.  Host int64 arrays, or DeviceBuffers of int64 left
+        in HBM with ``device=True`` (the caller frees them).  The size query computes the
+        result and the filling call reuses it (one fetch + sort + group per read)."""
         m = np.ascontiguousarray(map_ids, dtype=np.int64)
-        nbytes = ctypes.c_int64(0)
-        check(lib().sgx_read_sorted(self.handle, shuffle_id, m.ctypes.data, len(m), start_partition, end_partition,
-                                    None, 0, MEM_HOST, ctypes.byref(nbytes)), "readGrouped")
-        n = nbytes.value // 16  # upper bound of groups and values
-        keys = np.empty(n, dtype=np.int64)
-        starts = np.empty(n, dtype=np.int64)
-        vals = np.empty(n, dtype=np.int64)
         ng, nv = ctypes.c_int64(0), ctypes.c_int64(0)
         check(lib().sgx_read_grouped(self.handle, shuffle_id, m.ctypes.data, len(m), start_partition, end_partition,
-                                     agg, keys.ctypes.data, starts.ctypes.data, vals.ctypes.data, n, n, MEM_HOST,
-                                     ctypes.byref(ng), ctypes.byref(nv)), "readGrouped")
-        if agg == _lib.AGG_SUM:
-            return keys[:ng.value], vals[:nv.value]
-        return keys[:ng.value], starts[:ng.value], vals[:nv.value]
+                                     agg, None, None, None, 0, 0, MEM_HOST, ctypes.byref(ng), ctypes.byref(nv)),
+              "readGrouped")
+        G, V = ng.value, nv.value
+        group = agg == _lib.AGG_GROUP
+        if device:
+            keys, vals = self.alloc(max(G, 1) * 8), self.alloc(max(V, 1) * 8)
+            starts = self.alloc(max(G, 1) * 8) if group else None
+            ptrs, kind = (keys.ptr, starts.ptr if group else None, vals.ptr), MEM_DEVICE
+        else:
+            keys, vals = np.empty(G, dtype=np.int64), np.empty(V, dtype=np.int64)
+            starts = np.empty(G, dtype=np.int64) if group else None
+            ptrs, kind = (keys.ctypes.data, starts.ctypes.data if group else None, vals.ctypes.data), MEM_HOST
+        try:
+            check(lib().sgx_read_grouped(self.handle, shuffle_id, m.ctypes.data, len(m), start_partition,
+                                         end_partition, agg, ptrs[0], ptrs[1], ptrs[2], G, V, kind,
+                                         ctypes.byref(ng), ctypes.byref(nv)), "readGrouped")
+        except Exception:
+            if device:
+                for b in (keys, starts, vals):
+                    if b is not None:
+                        b.free()
+            raise
+        if group:
+            return keys, starts, vals
+        return keys, vals
 
     def range_bounds(self, batches: Sequence, nrecords: Sequence[int], record_bytes: int, num_partitions: int,
                      rdd_id: int = 0, sample_points_per_partition: int = 20) -> np.ndarray:

@@ -261,3 +261,78 @@ def test_c0_groupbykey_full_size(sgx_lib, oracle_lib, codec, tmp_path):
         assert len(values) == n
     finally:
         mgr.stop()
+
+
+@pytest.mark.gpu
+def test_size_query_result_reuse_and_invalidation(sgx_lib, oracle_lib):
+    """A size query computes the read and the filling call right after it reuses it; any call
+    in between on the thread, or any change to the engine's shuffles, makes the filling call
+    recompute.  Results always equal the oracle's; device outputs equal host outputs."""
+    import ctypes
+
+    from sparkucx_amd._lib import lib
+
+    e = sgx_lib.ShuffleEngine(device=0)
+    R = 64
+    sid = 71
+    e.register_shuffle(sid, R, serializer=sgx_lib.SER_KRYO)
+    recs = [oracle_lib.gen_uniform16(40_000, 900 + i, value_base=i << 32) for i in range(2)]
+    recs[1][:, :8] = recs[0][:, :8]  # shared keys: real groups
+    for i, r in enumerate(recs):
+        e.write_map(sid, i, r, len(r), 16)
+    outs = [oracle_lib.map_write(r, R) for r in recs]
+    seqs = oracle_lib.canonical_reducer_sequences(outs, R, 16)
+
+    def want(r0, r1, agg):
+        return oracle_lib.reduce_grouped(seqs[r0:r1], agg)
+
+    m = np.array([0, 1], np.int64)
+
+    def query(r0, r1, agg):
+        ng, nv = ctypes.c_int64(), ctypes.c_int64()
+        sgx_lib._lib.check(lib().sgx_read_grouped(e.handle, sid, m.ctypes.data, 2, r0, r1, agg, None, None, None,
+                                                  0, 0, 0, ctypes.byref(ng), ctypes.byref(nv)), "q")
+        return ng.value, nv.value
+
+    def fill(r0, r1, agg, G, V):
+        k, s, v = np.empty(G, np.int64), np.empty(G, np.int64), np.empty(V, np.int64)
+        ng, nv = ctypes.c_int64(), ctypes.c_int64()
+        sgx_lib._lib.check(lib().sgx_read_grouped(e.handle, sid, m.ctypes.data, 2, r0, r1, agg, k.ctypes.data,
+                                                  s.ctypes.data, v.ctypes.data, G, V, 0, ctypes.byref(ng),
+                                                  ctypes.byref(nv)), "f")
+        return (k, s, v) if agg == sgx_lib.AGG_GROUP else (k, v)
+
+    try:
+        # reuse: query then fill
+        G, V = query(0, 32, sgx_lib.AGG_GROUP)
+        for g, w in zip(fill(0, 32, sgx_lib.AGG_GROUP, G, V), want(0, 32, "group")):
+            assert np.array_equal(g, w)
+        # another call on the thread in between: the fill recomputes its own range
+        G, V = query(0, 32, sgx_lib.AGG_SUM)
+        query(32, 64, sgx_lib.AGG_SUM)
+        for g, w in zip(fill(0, 32, sgx_lib.AGG_SUM, G, V), want(0, 32, "sum")):
+            assert np.array_equal(g, w)
+        # a write in between (another map id): recomputed, still the two maps asked for
+        G, V = query(16, 48, sgx_lib.AGG_GROUP)
+        e.write_map(sid, 9, recs[0][:1000], 1000, 16)
+        for g, w in zip(fill(16, 48, sgx_lib.AGG_GROUP, G, V), want(16, 48, "group")):
+            assert np.array_equal(g, w)
+        # the Python wrapper (size query + fill) and device outputs
+        for agg in ("group", "sum"):
+            a = sgx_lib.AGG_GROUP if agg == "group" else sgx_lib.AGG_SUM
+            host = e.read_grouped(sid, [0, 1], 0, R, a)
+            dev = e.read_grouped(sid, [0, 1], 0, R, a, device=True)
+            try:
+                for h, d, w in zip(host, dev, want(0, R, agg)):
+                    assert np.array_equal(h, w)
+                    assert np.array_equal(d.to_numpy(len(w) * 8).view(np.int64), w)
+            finally:
+                for d in dev:
+                    d.free()
+        # sorted / records reads of the Kryo shuffle (size query decodes and keeps the result)
+        got = e.read_sorted(sid, [0, 1], 0, R).reshape(-1, 16)
+        assert np.array_equal(got, oracle_lib.reduce_sorted(seqs))
+        got = e.read_records(sid, [0, 1], 0, R).reshape(-1, 16)
+        assert np.array_equal(got, np.concatenate(seqs))
+    finally:
+        e.close()
