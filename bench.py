@@ -46,6 +46,9 @@ def parse():
                     help="budget of the CPU baseline's timed legs (plus ~5 s of C0 and setup)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
+                    help="N > 1 exchange backend: RCCL over xGMI (the product path) or host collectives "
+                         "over gloo (lets several ranks share one GPU to rehearse the N > 1 path)")
     ap.add_argument("--serializer", choices=["fixed", "kryo"], default="fixed",
                     help="kryo: also frame each map output as Spark's Kryo stream (SURVEY §8(f) row 2)")
     return ap.parse_args()
@@ -166,11 +169,14 @@ def main():
         import torch.distributed as dist
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    torch.cuda.set_device(local_rank)
+    device = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(device)
 
     n, R = args.records, args.partitions
-    eng = sgx.ShuffleEngine(device=local_rank, num_chunks=args.num_chunks)
-    if world > 1:
+    eng = sgx.ShuffleEngine(device=device, num_chunks=args.num_chunks)
+    if world > 1 and args.comm == "host":
+        eng.comm_init_host(world, rank)
+    elif world > 1:
         uid = [sgx.get_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(world, rank, uid[0])
@@ -259,9 +265,12 @@ def main():
             "data": f"synthetic {args.dist} (Long,Long) 16 B records, splitmix64 seed {args.seed:#x}+rank",
             "config": {"workload": "C1: 2^28 x 16 B, HashPartitioner R=1024, partition+scatter per GPU"
                        if world == 1 else
-                       f"C2: {n} x 16 B per GPU ({n * world} total), R={R}, partition + RCCL alltoallv",
+                       f"C2: {n} x 16 B per GPU ({n * world} total), R={R}, partition + "
+                       + ("RCCL alltoallv" if args.comm == "rccl" else "host all-to-all (rehearsal)"),
                        "records_per_gpu": n, "partitions": R, "record_bytes": 16,
-                       "parallelism": f"dp{world} (map shards per GPU, reducers owned floor(r*P/R))"},
+                       "parallelism": f"dp{world} (map shards per GPU, reducers owned floor(r*P/R))",
+                       "exchange": None if world == 1 else (
+                           "RCCL ncclAllToAllv" if args.comm == "rccl" else "host collectives (gloo), rehearsal")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": k4_pmc.get("hbm_bytes_per_launch"),
