@@ -24,6 +24,8 @@ namespace sgx {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
+constexpr size_t LDS_MAX = 160 * 1024;  // per CU (gfx950)
+
 // ------------------------------------------------------------------------------------
 // Partition ids
 // ------------------------------------------------------------------------------------
@@ -191,13 +193,24 @@ constexpr int HIST_SPLIT = 4;
 // peers (same partition id) from one ballot per id bit, and only the lowest peer adds
 // popcount(peers).  Measured against plain LDS atomics on uniform and Zipf(1.1) keys
 // (DESIGN.md §4): plain atomics are the default.
-template <int KIND, bool REC16, int UNROLL, int SPLIT, bool AGG = false>
+template <int KIND, bool REC16, int UNROLL, int SPLIT, bool AGG = false, bool LB = true>
 __device__ __forceinline__ void hist_body(const char *__restrict__ in, int64_t n, int rb, int64_t chunk,
                                           const PartParams &pp, uint32_t *__restrict__ counts, int G) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     uint32_t *hist = (uint32_t *)smem;
     const uint32_t tid = threadIdx.x, T = blockDim.x;
     for (uint32_t p = tid; p < pp.R; p += T) hist[p] = 0;
+    // range partitioners: the bounds' binary search runs against an LDS copy (a dependent
+    // chain of ~log2(R) loads per record: LDS latency instead of L1/L2)
+    // (LB false: bounds too large for LDS, read from global memory)
+    char *bl = smem + (((size_t)pp.R * 4 + 15) & ~(size_t)15);
+    if constexpr (LB && KIND == SGX_PART_RANGE_BYTES10) {
+        for (int i = (int)tid; i < pp.nb; i += (int)T) ((Key10 *)bl)[i] = ((const Key10 *)pp.bounds)[i];
+    } else if constexpr (LB && KIND == SGX_PART_RANGE_I64) {
+        for (int i = (int)tid; i < pp.nb; i += (int)T) ((int64_t *)bl)[i] = ((const int64_t *)pp.bounds)[i];
+    }
+    const int64_t *bi64 = LB ? (const int64_t *)bl : (const int64_t *)pp.bounds;
+    const Key10 *bk10 = LB ? (const Key10 *)bl : (const Key10 *)pp.bounds;
     __syncthreads();
     const int g = blockIdx.x / SPLIT, sub = blockIdx.x % SPLIT;
     const int64_t cbeg = (int64_t)g * chunk;
@@ -226,12 +239,12 @@ __device__ __forceinline__ void hist_body(const char *__restrict__ in, int64_t n
             const int64_t i = base + (int64_t)u * T + tid;
             if constexpr (AGG) {
                 const bool live = i < cend;
-                const uint32_t p = live ? pid_of<KIND>(x[u], y[u], z[u], pp) : 0u;
+                const uint32_t p = live ? pid_of_b<KIND>(x[u], y[u], z[u], pp, bi64, bk10) : 0u;
                 const uint64_t peers = match_peers(p, __ballot(live), pp.nbits);
                 const uint32_t lane = tid & 63u;
                 if (live && (peers & ((1ull << lane) - 1ull)) == 0) atomicAdd(&hist[p], (uint32_t)__popcll(peers));
             } else {
-                if (i < cend) atomicAdd(&hist[pid_of<KIND>(x[u], y[u], z[u], pp)], 1u);
+                if (i < cend) atomicAdd(&hist[pid_of_b<KIND>(x[u], y[u], z[u], pp, bi64, bk10)], 1u);
             }
         }
     }
@@ -242,16 +255,21 @@ __device__ __forceinline__ void hist_body(const char *__restrict__ in, int64_t n
     }
 }
 
-template <int KIND, bool REC16, bool AGG = false>
+template <int KIND, bool REC16, bool AGG = false, bool LB = true>
 __global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ in, int64_t n, int rb,
                                                        int64_t chunk, PartParams pp,
                                                        uint32_t *__restrict__ counts, int G) {
-    hist_body<KIND, REC16, HIST_UNROLL, HIST_SPLIT, AGG>(in, n, rb, chunk, pp, counts, G);
+    hist_body<KIND, REC16, HIST_UNROLL, HIST_SPLIT, AGG, LB>(in, n, rb, chunk, pp, counts, G);
 }
 
 hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
                        const PartParams &pp, uint32_t *counts, hipStream_t stream, int mode, bool zeroed) {
-    const size_t lds = (size_t)pp.R * 4;
+    const size_t hlds = (((size_t)pp.R * 4 + 15) & ~(size_t)15);
+    size_t lds = hlds;
+    if (pp.kind == SGX_PART_RANGE_BYTES10) lds += (size_t)pp.nb * sizeof(Key10);
+    else if (pp.kind == SGX_PART_RANGE_I64) lds += (size_t)pp.nb * 8;
+    const bool lb = lds <= LDS_MAX;  // else the bounds stay in global memory
+    if (!lb) lds = hlds;
     const char *p = (const char *)in;
     if (!zeroed) {
         hipError_t ze = hipMemsetAsync(counts, 0, (size_t)pp.R * G * 4, stream);
@@ -278,10 +296,25 @@ hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
         }
         break;
     case KIND_DIGIT: if (r16) SGX_HIST(KIND_DIGIT, true); else SGX_HIST(KIND_DIGIT, false); break;
-    case SGX_PART_RANGE_I64: if (r16) SGX_HIST(SGX_PART_RANGE_I64, true); else SGX_HIST(SGX_PART_RANGE_I64, false); break;
-    default: if (r16) SGX_HIST(SGX_PART_RANGE_BYTES10, true); else SGX_HIST(SGX_PART_RANGE_BYTES10, false); break;
+    default: break;
     }
 #undef SGX_HIST
+    // range partitioners: bounds in LDS (LB) when they fit
+#define SGX_HIST_R(K, B, L)                                                                                   \
+    do {                                                                                                      \
+        if (lds > 65536)                                                                                      \
+            (void)hipFuncSetAttribute((const void *)k_hist<K, B, false, L>,                                   \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                  \
+        hipLaunchKernelGGL((k_hist<K, B, false, L>), grid, block, lds, stream, p, n, rb, chunk, pp, counts, G); \
+    } while (0)
+    if (pp.kind == SGX_PART_RANGE_I64) {
+        if (lb) { if (r16) SGX_HIST_R(SGX_PART_RANGE_I64, true, true); else SGX_HIST_R(SGX_PART_RANGE_I64, false, true); }
+        else { if (r16) SGX_HIST_R(SGX_PART_RANGE_I64, true, false); else SGX_HIST_R(SGX_PART_RANGE_I64, false, false); }
+    } else if (pp.kind == SGX_PART_RANGE_BYTES10) {
+        if (lb) { if (r16) SGX_HIST_R(SGX_PART_RANGE_BYTES10, true, true); else SGX_HIST_R(SGX_PART_RANGE_BYTES10, false, true); }
+        else { if (r16) SGX_HIST_R(SGX_PART_RANGE_BYTES10, true, false); else SGX_HIST_R(SGX_PART_RANGE_BYTES10, false, false); }
+    }
+#undef SGX_HIST_R
     return hipGetLastError();
 }
 
@@ -390,7 +423,6 @@ hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint
 //           partition run is written by consecutive lanes (coalesced), and
 //           cursor[p] += tcnt[p].  cursor starts at offs[p][g] (K3).
 // ------------------------------------------------------------------------------------
-constexpr size_t LDS_MAX = 160 * 1024;
 constexpr uint32_t SCATTER_OOB = 2u;  // error bit: a scatter destination was out of range
 constexpr int WIDE_WAVES = 8;
 constexpr int WIDE_THREADS = WIDE_WAVES * 64;
