@@ -49,6 +49,8 @@ def parse():
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                     help="N > 1 exchange backend: RCCL over xGMI (the product path) or host collectives "
                          "over gloo (lets several ranks share one GPU to rehearse the N > 1 path)")
+    ap.add_argument("--compress", action="store_true",
+                    help="with --serializer kryo: spark.shuffle.compress=true (LZ4 frames, Spark's default)")
     ap.add_argument("--serializer", choices=["fixed", "kryo"], default="fixed",
                     help="kryo: also frame each map output as Spark's Kryo stream (SURVEY §8(f) row 2)")
     return ap.parse_args()
@@ -190,6 +192,10 @@ def main():
         eng.gen_zipf16(buf, n, args.seed + rank, cdf, value_base=rank * n)
     sid = 1
     eng.register_shuffle(sid, R, serializer=sgx.SER_KRYO if args.serializer == "kryo" else sgx.SER_FIXED)
+    if args.compress:
+        if args.serializer != "kryo":
+            raise SystemExit("--compress needs --serializer kryo (spark.shuffle.compress applies to serialized streams)")
+        eng.set_compression(sid, "lz4")
 
     def step(k):
         mid = (k & 1) * world + rank  # two alternating map slots per rank
@@ -295,10 +301,14 @@ def main():
         if args.serializer == "kryo":
             ser_ms = st.ms["serialize"] / max(1, st.count["serialize"])
             kbytes = float(lens.sum())
-            out["config"]["serializer"] = "KryoSerializer, spark.shuffle.compress=false"
-            out["kryo"] = {"kernel": "k_kryo_ser16", "ms": round(ser_ms, 4), "stream_bytes": kbytes,
-                           "algo_bytes": 16.0 * n + kbytes,
-                           "achieved_GBs": round((16.0 * n + kbytes) / (ser_ms * 1e-3) / 1e9, 1)}
+            out["config"]["serializer"] = ("KryoSerializer, spark.shuffle.compress=" +
+                                           ("true (lz4, 32 KiB blocks)" if args.compress else "false"))
+            out["kryo"] = {"kernel": "k_kryo_ser16", "ms": round(ser_ms, 4), "published_bytes": kbytes,
+                           "achieved_GBs": round(16.0 * n / (ser_ms * 1e-3) / 1e9, 1)}
+            if args.compress:
+                c_ms = st.ms["compress"] / max(1, st.count["compress"])
+                out["lz4"] = {"kernel": "k_lz4_blocks", "ms": round(c_ms, 4), "framed_bytes": kbytes,
+                              "note": "latency-bound: one serial LZ4 search per 32 KiB block (DESIGN.md §14)"}
             if world == 1:
                 # reduce side of the same shuffle: every block of the last map, decoded on the GPU
                 dst = eng.alloc(n * 16)
@@ -309,9 +319,11 @@ def main():
                 st2 = eng.stats()
                 de_ms = st2.ms["deserialize"] / max(1, st2.count["deserialize"])
                 out["kryo"]["deserialize"] = {
-                    "kernel": "k_kryo_deser16", "ms": round(de_ms, 4), "algo_bytes": kbytes + 16.0 * n,
-                    "achieved_GBs": round((kbytes + 16.0 * n) / (de_ms * 1e-3) / 1e9, 1),
+                    "kernel": "k_kryo_deser16", "ms": round(de_ms, 4),
+                    "achieved_GBs": round(16.0 * n / (de_ms * 1e-3) / 1e9, 1),
                     "gather_ms": round(st2.ms["regroup"] / max(1, st2.count["regroup"]), 4)}
+                if args.compress:
+                    out["lz4"]["decompress_ms"] = round(st2.ms["decompress"] / max(1, st2.count["decompress"]), 4)
                 dst.free()
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
