@@ -134,3 +134,29 @@ def test_exchange_rccl_one_gpu_per_rank(sgx_lib, oracle_lib, tmp_path, world):
         pytest.skip(f"needs {world} GPUs (RCCL refuses ranks sharing a device)")
     run_world(tmp_path, world, "rccl", "fixed", 1024, 300_000)
     run_world(tmp_path, world, "rccl", "kryo+lz4", 200, 50_000)
+
+
+def test_bench_multi_rank_path_rehearsal(tmp_path):
+    """bench.py's N > 1 path (the driver's scaling run) end to end with 2 ranks on this box:
+    torch.distributed.run, one engine per rank, the host-collective exchange standing in for
+    RCCL (which needs a GPU per rank); rank 0 prints one JSON line with the contract's keys."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(root, "bench.py"),
+           "--gpus", "2", "--comm", "host", "--records", str(1 << 20), "--partitions", "64", "--steps", "3",
+           "--warmup", "1"]
+    p = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+              "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "xgmi_roofline"):
+        assert k in d, k
+    assert d["n_gpus"] == 2 and d["steps"] == 3 and d["scaling"] == "weak" and d["value"] > 0
+    assert d["verified_lengths_sum"] is True
+    assert d["xgmi_roofline"]["recv_bytes_max_over_mean"] < 1.1
