@@ -91,7 +91,10 @@ int sgx::comm_wait(sgx_engine *e) {
             return fail_msg(SGX_ERR_TIMEOUT, "exchange did not complete within %lld ms (communicator aborted)",
                             (long long)e->comm_timeout_ms);
         }
-        std::this_thread::sleep_for(std::chrono::microseconds(50));
+        // spin (yielding) through the first 2 ms -- the common wait, one collective -- then
+        // back off, so a long or stuck exchange does not burn a core
+        if (waited < 2) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
 }
 
