@@ -117,11 +117,12 @@ def test_edge_keys_all_partition_counts(engine, oracle_lib):
         check_against_oracle(engine, oracle_lib, recs, R)
 
 
+@pytest.mark.parametrize("R", [1024, 4096])
 @pytest.mark.parametrize("num_chunks", [1, 3, 1024, 4096])
-def test_chunking_does_not_change_output(sgx_lib, oracle_lib, num_chunks):
+def test_chunking_does_not_change_output(sgx_lib, oracle_lib, num_chunks, R):
     recs = oracle_lib.gen_uniform16(300_007, 5)
     with sgx_lib.ShuffleEngine(device=0, num_chunks=num_chunks) as e:
-        check_against_oracle(e, oracle_lib, recs, 1024)
+        check_against_oracle(e, oracle_lib, recs, R)
 
 
 GEOMETRIES = [(4, 16), (8, 16), (12, 10), (14, 9), (16, 7), (4, 12), (8, 8), (4, 8), (8, 4), (4, 4), (4, 2), (4, 1)]
@@ -162,13 +163,14 @@ def test_kernel_choices_are_byte_identical(sgx_lib, oracle_lib, cfg):
             check_against_oracle(e, oracle_lib, zrecs, R)
 
 
-@pytest.mark.parametrize("R", [200, 585, 586, 1000, 1024])
+@pytest.mark.parametrize("R", [200, 585, 586, 1000, 1024, 1025, 2048, 3000, 4096, 5000, 8192])
 @pytest.mark.parametrize("group", [7, 15, 1])
 def test_write_combining_carry_pressure(sgx_lib, oracle_lib, R, group):
     """Write-combining K4: records arrive in runs of `group` per partition, so most
     partitions end every tile with a 7-record tail; the deferred records then exceed the
     tile's carry capacity and force the flush path, alternating with normal tiles.  Several
-    chunks, a ragged last tile; bit-exact against the oracle."""
+    chunks, a ragged last tile; bit-exact against the oracle.  (R > 1024 runs the
+    lane-ordered kernel: the same input shapes on that path.)"""
     n = 3 * 4096 * 7 + 1234
     recs = oracle_lib.gen_uniform16(n, 0xCA11 + R + group)
     rng = np.random.default_rng(R * 31 + group)
@@ -198,10 +200,39 @@ def test_heavy_collisions(engine, oracle_lib, distinct, R):
     check_against_oracle(engine, oracle_lib, recs, R)
 
 
-def test_all_records_one_partition(engine, oracle_lib):
+@pytest.mark.parametrize("R", [1024, 4096, 6144])
+def test_all_records_one_partition(engine, oracle_lib, R):
     recs = oracle_lib.gen_uniform16(200_000, 1)
     recs[:, :8] = np.frombuffer(np.int64(4242).tobytes(), np.uint8)  # same key everywhere
-    check_against_oracle(engine, oracle_lib, recs, 1024)
+    check_against_oracle(engine, oracle_lib, recs, R)
+
+
+@pytest.mark.parametrize("R", [1025, 1536, 1537, 2048, 3072, 4096, 5000, 6144, 6145])
+@pytest.mark.parametrize("shape", ["uniform", "sorted", "edges", "hot"])
+def test_large_r_shapes(sgx_lib, oracle_lib, R, shape):
+    """R > 1024: the K4 shapes that stress a large-R scatter -- uniform keys; keys sorted by
+    partition (every chunk sees a different narrow band of partitions); only the first and
+    last partitions; one hot partition holding half the records -- over several chunk
+    counts and a ragged size, bit-exact against the oracle.  (These shapes were written
+    for the split write-combining K4 that was measured and rejected; they
+    run the lane-ordered kernel.)"""
+    n = 700_001
+    recs = oracle_lib.gen_uniform16(n, 0x5917 + R)
+    rng = np.random.default_rng(R)
+    if shape == "sorted":
+        pids = (np.arange(n, dtype=np.int64) * R) // n
+    elif shape == "edges":
+        pids = np.where(rng.integers(0, 2, n) == 0, 0, R - 1)
+    elif shape == "hot":
+        pids = np.where(rng.integers(0, 2, n) == 0, R // 3, rng.integers(0, R, n))
+    else:
+        pids = None
+    if pids is not None:  # 0 <= key < 2^31: HashPartitioner gives key % R
+        keys = (pids + R * rng.integers(0, 1000, n)).astype(np.int64)
+        recs[:, :8] = keys.view(np.uint8).reshape(-1, 8)
+    for chunks in (0, 5, 64):
+        with sgx_lib.ShuffleEngine(device=0, num_chunks=chunks) as e:
+            check_against_oracle(e, oracle_lib, recs, R)
 
 
 # ---------------------------------------------------------------- range partitioners --
