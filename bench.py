@@ -308,7 +308,8 @@ def main():
             if args.compress:
                 c_ms = st.ms["compress"] / max(1, st.count["compress"])
                 out["lz4"] = {"kernel": "k_lz4_blocks", "ms": round(c_ms, 4), "framed_bytes": kbytes,
-                              "note": "latency-bound: one serial LZ4 search per 32 KiB block (DESIGN.md §14)"}
+                              "note": "k_lz4_blocks + k_xxh32_blocks: one wave per 32 KiB block, LZ4_compress_default's "
+                                      "search 64 iterations per step (DESIGN.md §14)"}
             if world == 1:
                 # reduce side of the same shuffle: every block of the last map, decoded on the GPU
                 dst = eng.alloc(n * 16)

@@ -89,13 +89,14 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes
 // LZ4BlockOutputStream framing (sgx_lz4.hip)
 int lz4_lanes_per_workgroup();
 int lz4_max_block();
-// err: 4 int64 {flags, block, offset, length}, zeroed by the caller (see k_lz4_blocks)
+// err: 4 int64 {flags, block, offset, length}, zeroed by the caller (see k_lz4_blocks).
+// sizes[b] = 21 + payload bytes (RAW: the block's length); checks[b] = masked XXH32.
 hipError_t launch_lz4_blocks(const uint8_t *stream, int64_t stream_len, const int64_t *blocks, int64_t nblocks,
-                             int level, uint8_t *slots, int64_t slot_bytes, int32_t *sizes, int64_t *err,
-                             hipStream_t s);
-hipError_t launch_lz4_gather(const uint8_t *slots, int64_t slot_bytes, const int32_t *sizes,
-                             const int64_t *frame_off, int64_t nblocks, const int64_t *end_off, int64_t nends,
-                             int level, uint8_t *dst, hipStream_t s);
+                             int level, uint8_t *slots, int64_t slot_bytes, int32_t *sizes, uint32_t *checks,
+                             int64_t *err, hipStream_t s);
+hipError_t launch_lz4_gather(const uint8_t *stream, const int64_t *blocks, const uint8_t *slots, int64_t slot_bytes,
+                             const int32_t *sizes, const uint32_t *checks, const int64_t *frame_off, int64_t nblocks,
+                             const int64_t *end_off, int64_t nends, int level, uint8_t *dst, hipStream_t s);
 hipError_t launch_lz4_walk(const uint8_t *in, int64_t nbytes, int64_t *desc, int64_t desc_cap, int64_t *info,
                            hipStream_t s);
 // per-stream walk (see k_lz4_walk_streams): soff[nstreams + 1]; cnt [nstreams][2]; err: one

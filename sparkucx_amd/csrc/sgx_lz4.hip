@@ -6,11 +6,13 @@
 // the end mark; see oracle/lz4_oracle.c for the restated algorithm and DESIGN.md §12.
 //
 // Two kernels:
-//   k_lz4_blocks  one LANE per block: the block's input bytes and its 8192-entry u16 hash
-//                 table live in LDS (48 KiB per lane), so the greedy match search -- a serial
-//                 dependence chain by construction of LZ4_compress_default's skip acceleration
-//                 and table updates -- runs at LDS latency.  The frame (header + payload) goes
-//                 to a fixed-size slot; its size to sizes[b].
+//   k_lz4_blocks  one WAVE per block: the block's input bytes and its 8192-entry u16 hash
+//                 table live in LDS (48 KiB per wave), and the wave runs LZ4_compress_default's
+//                 greedy search 64 iterations at a time (lz4_compress_wave: the skip schedule
+//                 fixes the probed positions, same-hash conflicts inside a batch are resolved
+//                 by ballots), so a block costs ~1/64 of the serial chain where it searches,
+//                 and its match counts, catch-ups and literal copies are lane-parallel.  The
+//                 frame (header + payload) goes to a fixed-size slot; its size to sizes[b].
 //   k_lz4_gather  one workgroup per block copies the slot to the frame's final offset
 //                 (offsets scanned on the host from sizes), and writes the partition end marks.
 #include <hip/hip_runtime.h>
@@ -27,9 +29,8 @@ constexpr int kMfLimit = 12;
 constexpr int kHashLog = 13;                       // byU16 table: LZ4_HASHLOG + 1
 constexpr int kTable = 1 << kHashLog;              // 8192 u16 entries
 constexpr int kMaxBlock = 32768;                   // LDS staging limit per lane
-constexpr int kLanes = 1;                          // one block per workgroup (one wave, one busy lane):
-                                                   // 48 KiB LDS -> 3 workgroups per CU on separate
-                                                   // SIMDs, so the serial lanes never share a wave
+constexpr int kLanes = 1;                          // one block per workgroup (one wave):
+                                                   // 48 KiB LDS -> 3 workgroups per CU
 constexpr int kHeader = 21;
 
 // unaligned little-endian 32-bit read from the LDS staging buffer: the two aligned dwords
@@ -40,6 +41,14 @@ __device__ __forceinline__ uint32_t lds32(const uint8_t *p) {
     const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
     const uint32_t *w = (const uint32_t *)(p - sh);
     return __builtin_amdgcn_alignbyte(w[1], w[0], sh);
+}
+// unaligned little-endian 32-bit read of global bytes p[0..3]: the aligned dword holding p[0]
+// and (only when p is unaligned) the next one, which still holds p[3] -- nothing past p[3]'s
+// dword is touched
+__device__ __forceinline__ uint32_t g32(const uint8_t *p) {
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t *w = (const uint32_t *)(p - sh);
+    return __builtin_amdgcn_alignbyte(w[sh ? 1 : 0], w[0], sh);
 }
 __device__ __forceinline__ uint32_t hash4(uint32_t seq) { return (seq * 2654435761u) >> (32 - kHashLog); }
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
@@ -92,120 +101,186 @@ __device__ uint32_t xxh32_lds_window(const uint8_t *base, int sh, int len, uint3
     return h;
 }
 
-// LZ4_compress_default of src[0, n) (n < 65547) into out[0, cap); returns the compressed
-// size, or -1 if the output would pass `cap` (LZ4_compressBound(n) <= cap by construction,
-// so this is a guard against corrupt input, never a path of correct runs).
-// `src` and `table` are this lane's LDS slices; output bytes go straight to HBM.
-// `table` must be zeroed (LZ4_initStream).
-__device__ int lz4_compress_lane(const uint8_t *src, int n, uint16_t *table, uint8_t *out, int cap) {
-    const uint8_t *ip = src, *anchor = src, *iend = src + n;
-    const uint8_t *mflimit_plus_one = iend - kMfLimit + 1;
-    const uint8_t *matchlimit = iend - kLastLiterals;
-    uint8_t *op = out;
-    uint8_t *const oend = out + cap;
+// Skip schedule of LZ4_compress_default's search: iteration 0 steps 1, iteration i >= 1
+// steps (63 + i) >> 6.  skip_dist(m) = total distance of iterations [0, m): with
+// G(x) = sum_{j<=x} floor(j / 64) = 32 q (q - 1) + q (r + 1) (q = x / 64, r = x % 64),
+// skip_dist(m) = 1 + G(62 + m) for m >= 1.
+__device__ __forceinline__ int skip_dist(int m) {
+    const int x = 62 + m, q = x >> 6, r = x & 63;
+    return m == 0 ? 0 : 1 + 32 * q * (q - 1) + q * (r + 1);
+}
+__device__ __forceinline__ int first_clear(uint64_t m) { return m == ~0ull ? 64 : (int)__builtin_ctzll(~m); }
+__device__ __forceinline__ int lane_value(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
+
+// LZ4_compress_default of src[0, n) (n < 65547) into out[0, cap), run by ONE WAVE: returns
+// the compressed size in every lane, or -1 if the output would pass `cap`
+// (LZ4_compressBound(n) <= cap by construction: a guard against corrupt input, never a path
+// of correct runs).  `src` is the block in global memory (read through L1: the search
+// touches a few hundred bytes around the cursor at a time), `table` (zeroed:
+// LZ4_initStream) the wave's 16 KiB LDS slice -- the only LDS a block needs, so 10 blocks
+// are in flight per CU; output bytes go straight to HBM.
+//
+// Bit-exact with the serial algorithm (oracle/lz4_oracle.c, pinned to liblz4) because it
+// executes the same iterations, 64 at a time where the serial code has no data dependence
+// it cannot resolve in the wave:
+//  * the match search: from a search start the probed positions follow from the skip
+//    schedule alone (step 1, then (63 + i) >> 6 at iteration i), so lane k takes iteration
+//    it + k: its position (a wave prefix sum of the steps), its hash, the table entry as of
+//    the batch start -- overridden by the latest lower lane with the same hash (whose write
+//    the serial code would have made first) -- and the 4-byte comparison.  The first lane
+//    that matches (or whose next position passes mflimit) ends the search; the table then
+//    receives, per hash, the position of the last lane before it, as the serial writes
+//    would have left it.
+//  * LZ4_count: 64 4-byte comparisons per round, the first differing byte from a ballot.
+//  * the backward catch-up: 64 byte comparisons per round.
+//  * literal and length-run bytes: lane-parallel stores.
+__device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uint8_t *out, int cap) {
+    const int lane = (int)(threadIdx.x & 63);
+    const uint64_t below = (1ull << lane) - 1ull;
+    int anchor = 0, op = 0;
     if (n >= kMfLimit + 1) {
-        table[hash4(lds32(ip))] = 0;
-        ip++;
-        uint32_t fwd_h = hash4(lds32(ip));
+        const int lim = n - kMfLimit + 1;      // mflimit_plus_one
+        const int mlimit = n - kLastLiterals;  // matchlimit
+        if (lane == 0) table[hash4(g32(src))] = 0;
+        int ip = 1;
         for (;;) {
-            const uint8_t *match;
-            uint8_t *token;
+            // ---- match search from ip (step 1, search counter 64)
+            const int start = ip;
+            int it = 0, match = 0;
             bool found = false;
-            {
-                const uint8_t *fwd = ip;
-                int step = 1, search = 1 << 6;
-                for (;;) {
-                    uint32_t h = fwd_h;
-                    uint32_t cur = (uint32_t)(fwd - src);
-                    uint32_t midx = table[h];
-                    ip = fwd;
-                    fwd += step;
-                    step = search++ >> 6;
-                    if (fwd > mflimit_plus_one) break;
-                    match = src + midx;
-                    fwd_h = hash4(lds32(fwd));
-                    table[h] = (uint16_t)cur;
-                    if (lds32(match) == lds32(ip)) { found = true; break; }
+            for (;;) {
+                const int pos = start + skip_dist(it + lane);
+                const int nxt = start + skip_dist(it + lane + 1);  // the position after this one
+                const bool valid = nxt <= lim;
+                const uint32_t seq = g32(src + min(pos, n - 4));  // (invalid lanes: any bytes)
+                const uint32_t h = hash4(seq);
+                int cand = table[h];
+                uint64_t peers = ~0ull;  // lanes probing the same hash
+#pragma unroll
+                for (int bt = 0; bt < kHashLog; ++bt) {
+                    const bool bit = (h >> bt) & 1u;
+                    const uint64_t m = __ballot(bit);
+                    peers &= bit ? m : ~m;
                 }
+                const uint64_t lower = peers & below;
+                if (lower) cand = start + skip_dist(it + 63 - (int)__builtin_clzll(lower));
+                const bool hit = valid && g32(src + cand) == seq;
+                const uint64_t vm = __ballot(valid), hm = __ballot(hit);
+                const int kinv = first_clear(vm);
+                const int khit = hm ? (int)__builtin_ctzll(hm) : 64;
+                // iterations [0, kend) of this batch ran: each writes table[h] = pos
+                const int kend = khit < kinv ? khit + 1 : kinv;
+                const uint64_t ran = kend >= 64 ? ~0ull : (1ull << kend) - 1ull;
+                if ((ran >> lane) & 1ull) {
+                    if (((peers & ran) >> lane) == 1ull) table[h] = (uint16_t)pos;  // last writer of h
+                }
+                if (khit < kinv) {
+                    found = true;
+                    ip = start + skip_dist(it + khit);
+                    match = lane_value(cand, khit);
+                    break;
+                }
+                if (kinv < 64) break;  // next position past mflimit: no match in this block
+                it += 64;
             }
             if (!found) break;
-            while (ip > anchor && match > src && ip[-1] == match[-1]) { ip--; match--; }
-            {
-                unsigned lit = (unsigned)(ip - anchor);
-                // token + literal length + literals + offset + 1 match-length byte at most
-                if (op + 1 + lit / 255 + 1 + lit + 2 + 1 > oend) return -1;
-                token = op++;
-                uint8_t tk;
-                if (lit >= 15) {
-                    int len = (int)lit - 15;
-                    tk = 15 << 4;
-                    for (; len >= 255; len -= 255) *op++ = 255;
-                    *op++ = (uint8_t)len;
-                } else {
-                    tk = (uint8_t)(lit << 4);
-                }
-                for (unsigned i = 0; i < lit; ++i) op[i] = anchor[i];
-                op += lit;
-                for (;;) {  // _next_match
-                    uint32_t off = (uint32_t)(ip - match);
-                    op[0] = (uint8_t)off;
-                    op[1] = (uint8_t)(off >> 8);
-                    op += 2;
-                    const uint8_t *a = ip + kMinMatch, *b = match + kMinMatch;
-                    // LZ4_count: 4 bytes per step (first differing byte = ctz of the xor)
-                    for (;;) {
-                        if (a + 4 > matchlimit) {
-                            while (a < matchlimit && *a == *b) { a++; b++; }
-                            break;
-                        }
-                        const uint32_t d = lds32(a) ^ lds32(b);
-                        if (d) { a += __builtin_ctz(d) >> 3; break; }
-                        a += 4;
-                        b += 4;
-                    }
-                    unsigned mc = (unsigned)(a - (ip + kMinMatch));
-                    if (op + mc / 255 + 1 + 3 > oend) return -1;  // run bytes + the next token, offset
-                    ip = a;
-                    if (mc >= 15) {
-                        tk += 15;
-                        mc -= 15;
-                        for (; mc >= 255; mc -= 255) *op++ = 255;
-                        *op++ = (uint8_t)mc;
-                    } else {
-                        tk += (uint8_t)mc;
-                    }
-                    *token = tk;
-                    anchor = ip;
-                    if (ip >= mflimit_plus_one) goto last_literals;
-                    table[hash4(lds32(ip - 2))] = (uint16_t)(ip - 2 - src);
-                    uint32_t h = hash4(lds32(ip));
-                    uint32_t cur = (uint32_t)(ip - src);
-                    match = src + table[h];
-                    table[h] = (uint16_t)cur;
-                    if (lds32(match) != lds32(ip)) break;
-                    token = op++;
-                    tk = 0;
-                }
+            // ---- catch up backwards
+            for (;;) {
+                const int a = ip - 1 - lane, b = match - 1 - lane;
+                const bool eq = a >= anchor && b >= 0 && src[a] == src[b];
+                const int back = first_clear(__ballot(eq));
+                ip -= back;
+                match -= back;
+                if (back < 64) break;
             }
-            fwd_h = hash4(lds32(++ip));
+            // ---- literals
+            const int lit = ip - anchor;
+            if (op + 1 + lit / 255 + 1 + lit + 2 + 1 > cap) return -1;
+            int token = op++;
+            uint32_t tk;
+            if (lit >= 15) {
+                const int nrun = (lit - 15) / 255;  // 255-bytes, then the remainder
+                for (int j = lane; j <= nrun; j += 64) out[op + j] = j < nrun ? (uint8_t)255 : (uint8_t)((lit - 15) % 255);
+                op += nrun + 1;
+                tk = 15u << 4;
+            } else {
+                tk = (uint32_t)lit << 4;
+            }
+            for (int j = lane; j < lit; j += 64) out[op + j] = src[anchor + j];
+            op += lit;
+            for (;;) {  // _next_match
+                const uint32_t off = (uint32_t)(ip - match);
+                if (lane == 0) {
+                    out[op] = (uint8_t)off;
+                    out[op + 1] = (uint8_t)(off >> 8);
+                }
+                op += 2;
+                // LZ4_count from ip + 4 / match + 4 up to matchlimit
+                int a = ip + kMinMatch;
+                const int d0 = match - ip;  // b = a + d0
+                for (;;) {
+                    const int al = a + 4 * lane;
+                    const bool full = al + 4 <= mlimit;
+                    const uint32_t d = full ? g32(src + al) ^ g32(src + al + d0) : 0u;
+                    const uint64_t dm = __ballot(d != 0);
+                    if (dm) {
+                        const int k = (int)__builtin_ctzll(dm);
+                        a += 4 * k + ((int)__builtin_ctz((uint32_t)lane_value((int)d, k)) >> 3);
+                        break;
+                    }
+                    const int nfull = __popcll(__ballot(full));
+                    a += 4 * nfull;
+                    if (nfull < 64) {  // < 4 bytes before matchlimit: byte-wise
+                        while (a < mlimit && src[a] == src[a + d0]) ++a;
+                        break;
+                    }
+                }
+                uint32_t mc = (uint32_t)(a - (ip + kMinMatch));
+                if (op + (int)(mc / 255) + 1 + 3 > cap) return -1;  // run bytes + the next token, offset
+                ip = a;
+                if (mc >= 15) {
+                    tk += 15;
+                    mc -= 15;
+                    const int nrun = (int)(mc / 255);
+                    for (int j = lane; j <= nrun; j += 64) out[op + j] = j < nrun ? (uint8_t)255 : (uint8_t)(mc % 255);
+                    op += nrun + 1;
+                } else {
+                    tk += mc;
+                }
+                if (lane == 0) out[token] = (uint8_t)tk;
+                anchor = ip;
+                if (ip >= lim) goto last_literals;
+                if (lane == 0) table[hash4(g32(src + ip - 2))] = (uint16_t)(ip - 2);
+                __builtin_amdgcn_wave_barrier();  // the write above, then the read below
+                const uint32_t h = hash4(g32(src + ip));
+                const int m2 = table[h];
+                __builtin_amdgcn_wave_barrier();
+                if (lane == 0) table[h] = (uint16_t)ip;
+                if (g32(src + m2) != g32(src + ip)) break;
+                match = m2;
+                token = op++;
+                tk = 0;
+            }
+            ++ip;
         }
     }
 last_literals:
     {
-        int last = (int)(iend - anchor);
-        if (op + 1 + last / 255 + 1 + last > oend) return -1;
+        const int last = n - anchor;
+        if (op + 1 + last / 255 + 1 + last > cap) return -1;
         if (last >= 15) {
-            int acc = last - 15;
-            *op++ = 15 << 4;
-            for (; acc >= 255; acc -= 255) *op++ = 255;
-            *op++ = (uint8_t)acc;
+            const int nrun = (last - 15) / 255;
+            if (lane == 0) out[op] = 15u << 4;
+            for (int j = lane; j <= nrun; j += 64) out[op + 1 + j] = j < nrun ? (uint8_t)255 : (uint8_t)((last - 15) % 255);
+            op += nrun + 2;
         } else {
-            *op++ = (uint8_t)(last << 4);
+            if (lane == 0) out[op] = (uint8_t)(last << 4);
+            ++op;
         }
-        for (int i = 0; i < last; ++i) op[i] = anchor[i];
+        for (int j = lane; j < last; j += 64) out[op + j] = src[anchor + j];
         op += last;
     }
-    return (int)(op - out);
+    return op;
 }
 
 __device__ __forceinline__ void st32le(uint8_t *p, uint32_t v) {
@@ -221,7 +296,7 @@ __device__ __forceinline__ void put_header(uint8_t *h, uint8_t token, uint32_t c
     st32le(h + 17, check);
 }
 
-// blocks[b] = {src byte offset, length}; one lane per block, kLanes lanes per workgroup.
+// blocks[b] = {src byte offset, length}; one wave per block.
 // Every global access is checked against stream_len / the slot: a block outside the stream
 // or an output past its slot sets err[0] (1 = bad block, 2 = output overflow) and records
 // {block, offset, length} in err[1..3] instead of touching memory.
@@ -230,81 +305,102 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
                                                    int level, uint8_t *__restrict__ slots,
                                                    int64_t slot_bytes, int32_t *__restrict__ sizes,
                                                    int64_t *__restrict__ err) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_in[kLanes][kMaxBlock + 16];
-    __shared__ uint16_t s_tab[kLanes][kTable];
+    __shared__ uint16_t s_tab[kTable];
+    static_assert(kLanes == 1, "one block per workgroup");
     const int lane = threadIdx.x;
-    const int64_t b = (int64_t)blockIdx.x * kLanes;
-    // stage this workgroup's blocks cooperatively (all 64 threads, 4 B per thread-step)
-    for (int l = 0; l < kLanes; ++l) {
-        int64_t bb = (int64_t)blockIdx.x * kLanes + l;
-        if (bb >= nblocks) break;
-        // aligned dword copy that keeps the source's misalignment (sh bytes) in LDS; the
-        // last dword is read byte-wise so nothing past the stream's end is touched
-        const int64_t boff = blocks[2 * bb], blen = blocks[2 * bb + 1];
-        if (boff < 0 || blen < 0 || blen > kMaxBlock || boff + blen > stream_len) {
-            if (threadIdx.x == 0) {
-                err[1] = bb;
-                err[2] = boff;
-                err[3] = blen;
-                atomicOr((unsigned long long *)err, 1ull);
-            }
-            return;  // uniform: the whole workgroup leaves before any barrier
-        }
-        const uint8_t *g = stream + boff;
-        const int n = (int)blen;
-        const int sh = (int)((uintptr_t)g & 3u);
-        const uint32_t *gw = (const uint32_t *)(g - sh);
-        const int full = (sh + n) >> 2;
-        uint32_t *sw = (uint32_t *)s_in[l];
-#pragma unroll 8
-        for (int i = threadIdx.x; i < full; i += 64) sw[i] = gw[i];
-        // signed index: threadIdx.x is unsigned, and full * 4 - sh < 0 for a block of
-        // n < 4 - sh bytes (a 1-byte tail block at an odd offset reads g[-1..0])
-        const int t = (int)threadIdx.x;
-        if (t < ((sh + n) & 3)) s_in[l][full * 4 + t] = g[full * 4 - sh + t];
-    }
-    for (int i = threadIdx.x; i < kLanes * kTable / 2; i += 64) ((uint32_t *)s_tab)[i] = 0u;
-    __syncthreads();
-    static_assert(kLanes == 1, "the tail below assumes one block per workgroup");
-    __shared__ int s_c;
+    const int64_t b = blockIdx.x;
     if (b >= nblocks) return;  // uniform across the workgroup
-    const int n = (int)blocks[2 * b + 1];
-    const uint8_t *src = s_in[0] + ((uintptr_t)(stream + blocks[2 * b]) & 3u);
-    uint8_t *slot = slots + b * slot_bytes;
-    if (lane == 0) s_c = lz4_compress_lane(src, n, s_tab[0], slot + kHeader, (int)(slot_bytes - kHeader));
-    __syncthreads();
-    if (s_c < 0) {
+    const int64_t boff = blocks[2 * b], blen = blocks[2 * b + 1];
+    if (boff < 0 || blen < 0 || blen > kMaxBlock || boff + blen > stream_len) {
         if (lane == 0) {
             err[1] = b;
-            err[2] = blocks[2 * b];
+            err[2] = boff;
+            err[3] = blen;
+            atomicOr((unsigned long long *)err, 1ull);
+        }
+        return;
+    }
+    for (int i = lane; i < kTable / 2; i += 64) ((uint32_t *)s_tab)[i] = 0u;
+    __syncthreads();
+    const int n = (int)blen;
+    const uint8_t *src = stream + boff;
+    uint8_t *slot = slots + b * slot_bytes;
+    const int sc = lz4_compress_wave(src, n, s_tab, slot + kHeader, (int)(slot_bytes - kHeader));
+    if (sc < 0) {
+        if (lane == 0) {
+            err[1] = b;
+            err[2] = boff;
             err[3] = n;
             atomicOr((unsigned long long *)err, 2ull);
         }
         return;
     }
-    const bool raw = s_c >= n;  // the compressed block did not shrink: RAW, copied by the wave
-    const int c = raw ? n : s_c;
-    if (raw)
-        for (int i = lane; i < n; i += 64) slot[kHeader + i] = src[i];
-    if (lane != 0) return;
-    uint32_t check = xxh32_lds_window(s_in[0], (int)(src - s_in[0]), n, 0x9747b28cu) & 0x0FFFFFFFu;
-    put_header(slot, (uint8_t)((raw ? 0x10 : 0x20) | level), (uint32_t)c, (uint32_t)n, check);
-    sizes[b] = kHeader + c;
+    // a block that did not shrink is RAW: k_lz4_gather copies it from the stream
+    if (lane == 0) sizes[b] = kHeader + (sc >= n ? n : sc);
 }
 
-// frame b: copy sizes[b] bytes of slot b to dst + frame_off[b]; workgroups past nblocks write
-// end marks at end_off[r] (partitions with bytes only).
-__global__ __launch_bounds__(256) void k_lz4_gather(const uint8_t *__restrict__ slots, int64_t slot_bytes,
+// XXH32 (LZ4BlockOutputStream's seed, masked to 28 bits) of every block: one LANE per block,
+// so the serial fold (four accumulators over 16 B stripes) runs for 64 blocks per wave
+// instruction.  Reads: aligned dwords, realigned per lane with v_alignbyte.
+__global__ __launch_bounds__(256) void k_xxh32_blocks(const uint8_t *__restrict__ stream,
+                                                      const int64_t *__restrict__ blocks, int64_t nblocks,
+                                                      uint32_t *__restrict__ checks) {
+    const int64_t b = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (b >= nblocks) return;
+    const uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u,
+                   P5 = 374761393u, seed = 0x9747b28cu;
+    const uint8_t *p = stream + blocks[2 * b];
+    const int len = (int)blocks[2 * b + 1];
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t *w = (const uint32_t *)(p - sh);  // aligned dwords; the fold reads whole stripes
+    uint32_t h;
+    int i = 0;
+    if (len >= 16) {
+        uint32_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+        const int ns = len >> 4;
+        for (int k = 0; k < ns; ++k) {
+            // stripe k = bytes [sh + 16k, sh + 16k + 16) of w: dwords 4k .. 4k+3, and 4k+4
+            // only when sh > 0 (it then holds the stripe's last bytes: nothing past them is read)
+            const uint32_t w0 = w[4 * k], w1 = w[4 * k + 1], w2 = w[4 * k + 2], w3 = w[4 * k + 3];
+            const uint32_t w4 = w[4 * k + (sh ? 4 : 3)];
+            v1 = rotl(v1 + __builtin_amdgcn_alignbyte(w1, w0, sh) * P2, 13) * P1;
+            v2 = rotl(v2 + __builtin_amdgcn_alignbyte(w2, w1, sh) * P2, 13) * P1;
+            v3 = rotl(v3 + __builtin_amdgcn_alignbyte(w3, w2, sh) * P2, 13) * P1;
+            v4 = rotl(v4 + __builtin_amdgcn_alignbyte(w4, w3, sh) * P2, 13) * P1;
+        }
+        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+        i = ns << 4;
+    } else {
+        h = seed + P5;
+    }
+    h += (uint32_t)len;
+    for (; i + 4 <= len; i += 4) h = rotl(h + g32(p + i) * P3, 17) * P4;
+    for (; i < len; ++i) h = rotl(h + (uint32_t)p[i] * P5, 11) * P1;
+    h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
+    checks[b] = h & 0x0FFFFFFFu;
+}
+
+// frame b: its header (method from the size: a RAW block keeps its length) and payload --
+// the slot's compressed bytes or, RAW, the block straight from the stream -- to
+// dst + frame_off[b]; workgroups past nblocks write end marks at end_off[r] (partitions with
+// bytes only).
+__global__ __launch_bounds__(256) void k_lz4_gather(const uint8_t *__restrict__ stream,
+                                                    const int64_t *__restrict__ blocks,
+                                                    const uint8_t *__restrict__ slots, int64_t slot_bytes,
                                                     const int32_t *__restrict__ sizes,
+                                                    const uint32_t *__restrict__ checks,
                                                     const int64_t *__restrict__ frame_off, int64_t nblocks,
                                                     const int64_t *__restrict__ end_off, int64_t nends,
                                                     int level, uint8_t *__restrict__ dst) {
     const int64_t b = blockIdx.x;
     if (b < nblocks) {
-        const uint8_t *s = slots + b * slot_bytes;
+        const int n = (int)blocks[2 * b + 1];
+        const int c = sizes[b] - kHeader;
+        const bool raw = c == n;  // compressed payloads are strictly shorter
+        const uint8_t *s = raw ? stream + blocks[2 * b] : slots + b * slot_bytes + kHeader;
         uint8_t *d = dst + frame_off[b];
-        const int n = sizes[b];
-        for (int i = threadIdx.x; i < n; i += 256) d[i] = s[i];
+        if (threadIdx.x == 0) put_header(d, (uint8_t)((raw ? 0x10 : 0x20) | level), (uint32_t)c, (uint32_t)n, checks[b]);
+        for (int i = threadIdx.x; i < c; i += 256) d[kHeader + i] = s[i];
         return;
     }
     const int64_t e = (b - nblocks) * 256 + threadIdx.x;
@@ -546,22 +642,27 @@ int lz4_lanes_per_workgroup() { return kLanes; }
 int lz4_max_block() { return kMaxBlock; }
 
 hipError_t launch_lz4_blocks(const uint8_t *stream, int64_t stream_len, const int64_t *blocks, int64_t nblocks,
-                             int level, uint8_t *slots, int64_t slot_bytes, int32_t *sizes, int64_t *err,
-                             hipStream_t stream_) {
+                             int level, uint8_t *slots, int64_t slot_bytes, int32_t *sizes, uint32_t *checks,
+                             int64_t *err, hipStream_t stream_) {
     if (nblocks <= 0) return hipSuccess;
+    (void)level;
     int64_t grid = (nblocks + kLanes - 1) / kLanes;
     hipLaunchKernelGGL(k_lz4_blocks, dim3((unsigned)grid), dim3(64), 0, stream_, stream, stream_len, blocks,
                        nblocks, level, slots, slot_bytes, sizes, err);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_xxh32_blocks, dim3((unsigned)((nblocks + 255) / 256)), dim3(256), 0, stream_, stream, blocks,
+                       nblocks, checks);
     return hipGetLastError();
 }
 
-hipError_t launch_lz4_gather(const uint8_t *slots, int64_t slot_bytes, const int32_t *sizes,
-                             const int64_t *frame_off, int64_t nblocks, const int64_t *end_off, int64_t nends,
-                             int level, uint8_t *dst, hipStream_t stream_) {
-    int64_t grid = nblocks + (nends + 255) / 256;
+hipError_t launch_lz4_gather(const uint8_t *stream, const int64_t *blocks, const uint8_t *slots, int64_t slot_bytes,
+                             const int32_t *sizes, const uint32_t *checks, const int64_t *frame_off, int64_t nblocks,
+                             const int64_t *end_off, int64_t nends, int level, uint8_t *dst, hipStream_t stream_) {
+    const int64_t grid = nblocks + (nends + 255) / 256;
     if (grid <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_lz4_gather, dim3((unsigned)grid), dim3(256), 0, stream_, slots, slot_bytes, sizes,
-                       frame_off, nblocks, end_off, nends, level, dst);
+    hipLaunchKernelGGL(k_lz4_gather, dim3((unsigned)grid), dim3(256), 0, stream_, stream, blocks, slots, slot_bytes,
+                       sizes, checks, frame_off, nblocks, end_off, nends, level, dst);
     return hipGetLastError();
 }
 

@@ -47,7 +47,7 @@ int sgx::lz4_frame_impl(sgx_engine *e, Ctx &c, const void *stream_dev, const int
     if (nb > 0) {
         SGX_TRY(d_blocks.ensure((size_t)nb * 16));
         SGX_TRY(d_slots.ensure((size_t)(nb * slot)));
-        SGX_TRY(d_sizes.ensure((size_t)nb * 4));
+        SGX_TRY(d_sizes.ensure((size_t)nb * 8));  // sizes | checks
         SGX_TRY(c.lz4_info.ensure(64));
         std::memcpy(hb + h_blocks, blocks.data(), (size_t)nb * 16);
         HIP_TRY(hipMemsetAsync(c.lz4_info.p, 0, 32, st));
@@ -56,8 +56,8 @@ int sgx::lz4_frame_impl(sgx_engine *e, Ctx &c, const void *stream_dev, const int
         HIP_TRY(hipEventRecord(c0, st));
         HIP_TRY(sgx::launch_lz4_blocks((const uint8_t *)stream_dev, part_offsets[R], (const int64_t *)d_blocks.p, nb,
                                        level, (uint8_t *)d_slots.p, slot, (int32_t *)d_sizes.p,
-                                       (int64_t *)c.lz4_info.p, st));
-        SGX_TRY(debug_sync(e, st, "k_lz4_blocks"));
+                                       (uint32_t *)d_sizes.p + nb, (int64_t *)c.lz4_info.p, st));
+        SGX_TRY(debug_sync(e, st, "k_lz4_blocks + k_xxh32_blocks"));
         HIP_TRY(hipEventRecord(c1, st));
         e->record_stage(SGX_STAGE_COMPRESS, c0, c1);
         HIP_TRY(hipMemcpyAsync(hb + h_sizes, d_sizes.p, (size_t)nb * 4, hipMemcpyDeviceToHost, st));
@@ -97,9 +97,10 @@ int sgx::lz4_frame_impl(sgx_engine *e, Ctx &c, const void *stream_dev, const int
     if (nb > 0) {
         SGX_TRY(d_offs.ensure((size_t)(nb + nends) * 8));
         HIP_TRY(hipMemcpyAsync(d_offs.p, offs, (size_t)(nb + nends) * 8, hipMemcpyHostToDevice, st));
-        HIP_TRY(sgx::launch_lz4_gather((const uint8_t *)d_slots.p, slot, (const int32_t *)d_sizes.p,
-                                       (const int64_t *)d_offs.p, nb, (const int64_t *)d_offs.p + nb, nends, level,
-                                       (uint8_t *)dst_dev, st));
+        HIP_TRY(sgx::launch_lz4_gather((const uint8_t *)stream_dev, (const int64_t *)d_blocks.p,
+                                       (const uint8_t *)d_slots.p, slot, (const int32_t *)d_sizes.p,
+                                       (const uint32_t *)d_sizes.p + nb, (const int64_t *)d_offs.p, nb,
+                                       (const int64_t *)d_offs.p + nb, nends, level, (uint8_t *)dst_dev, st));
         SGX_TRY(debug_sync(e, st, "k_lz4_gather"));
         HIP_TRY(hipStreamSynchronize(st));
     }

@@ -36,6 +36,24 @@ def _cases(oracle):
            rng.integers(0, 256, 32768, dtype=np.uint8).tobytes(),
            rng.integers(0, 4, 30000, dtype=np.uint8).tobytes(), (b"xyz" * 20000)[:32768]]
     out += [rng.integers(0, 3, n, dtype=np.uint8).tobytes() for n in range(0, 40)]
+    # shapes for the wave-parallel search (64 iterations per batch, lane-parallel counts,
+    # catch-ups and literal runs): incompressible runs long enough to reach large skip
+    # steps before a repeat, matches longer than 64 x 4 bytes, literal runs past 15 / 270,
+    # periods around the wave width, and random splices of earlier bytes
+    rnd = rng.integers(0, 256, 32768, dtype=np.uint8).tobytes()
+    out += [rnd[:20000] + rnd[3000:6000] + rnd[20000:29000], bytes(32768), rnd[:300] + bytes(5000) + rnd[:300]]
+    out += [(rnd[:p] * (32768 // p + 1))[:32768] for p in (7, 63, 64, 65, 255, 257, 1000)]
+    out += [b"".join(rnd[i * 700:i * 700 + L] + bytes(40) for i, L in enumerate((14, 15, 16, 269, 270, 271, 600)))]
+    spl, cur = bytearray(rnd[:64]), 64
+    while len(spl) < 32768:
+        spl += rnd[cur:cur + int(rng.integers(1, 100))]
+        cur = (cur + 100) % 32000
+        L, o = int(rng.integers(4, 300)), int(rng.integers(0, len(spl)))
+        spl += bytes(spl[o:o + L])
+    out += [bytes(spl[:32768]), bytes(spl[:32768])[::-1]]
+    low = oracle.gen_uniform16(2048, 0x10E)
+    low[:, :8] = (np.arange(2048, dtype=np.int64) % 97).view(np.uint8).reshape(-1, 8)
+    out += [oracle.kryo_serialize(low).tobytes()[:32768]]
     return out
 
 
