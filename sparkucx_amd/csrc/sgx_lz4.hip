@@ -3,18 +3,21 @@
 // Spark 3.0.1 defaults; SerializerManager.wrapStream per partition in
 // ShufflePartitionPairsWriter.open).  Byte-identical to liblz4 1.9.x LZ4_compress_default
 // per 32 KiB block + XXH32 (seed 0x9747b28c, masked to 28 bits) + the 21-byte block headers and
-// the end mark; see oracle/lz4_oracle.c for the restated algorithm and DESIGN.md §12.
+// the end mark; see oracle/lz4_oracle.c for the restated algorithm and DESIGN.md §14.
 //
-// Two kernels:
-//   k_lz4_blocks  one WAVE per block: the block's input bytes and its 8192-entry u16 hash
-//                 table live in LDS (48 KiB per wave), and the wave runs LZ4_compress_default's
-//                 greedy search 64 iterations at a time (lz4_compress_wave: the skip schedule
-//                 fixes the probed positions, same-hash conflicts inside a batch are resolved
-//                 by ballots), so a block costs ~1/64 of the serial chain where it searches,
-//                 and its match counts, catch-ups and literal copies are lane-parallel.  The
-//                 frame (header + payload) goes to a fixed-size slot; its size to sizes[b].
-//   k_lz4_gather  one workgroup per block copies the slot to the frame's final offset
-//                 (offsets scanned on the host from sizes), and writes the partition end marks.
+// Three kernels:
+//   k_lz4_blocks    one WAVE per block: the block's 8192-entry u16 hash table lives in LDS
+//                   (16 KiB: 10 blocks per CU; the input is read through L1), and the wave
+//                   runs LZ4_compress_default's greedy search 64 iterations at a time
+//                   (lz4_compress_wave: the skip schedule fixes the probed positions,
+//                   same-hash conflicts inside a batch are resolved by ballots), so a block
+//                   costs ~1/64 of the serial chain where it searches, and its match counts,
+//                   catch-ups and literal copies are lane-parallel.  The payload goes to a
+//                   fixed-size slot; the frame size to sizes[b].
+//   k_xxh32_blocks  XXH32 of every block, one lane per block.
+//   k_lz4_gather    one workgroup per block writes the header and copies the payload (the
+//                   slot, or the stream itself for a RAW block) to the frame's final offset
+//                   (offsets scanned on the host from sizes), and writes the partition end marks.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -28,9 +31,9 @@ constexpr int kLastLiterals = 5;
 constexpr int kMfLimit = 12;
 constexpr int kHashLog = 13;                       // byU16 table: LZ4_HASHLOG + 1
 constexpr int kTable = 1 << kHashLog;              // 8192 u16 entries
-constexpr int kMaxBlock = 32768;                   // LDS staging limit per lane
+constexpr int kMaxBlock = 32768;                   // largest block (lz4-java's 32 KiB blockSize)
 constexpr int kLanes = 1;                          // one block per workgroup (one wave):
-                                                   // 48 KiB LDS -> 3 workgroups per CU
+                                                   // 16 KiB LDS -> 10 workgroups per CU
 constexpr int kHeader = 21;
 
 // unaligned little-endian 32-bit read from the LDS staging buffer: the two aligned dwords
