@@ -1316,6 +1316,9 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
     constexpr int DW = RB / 4;                                     // dwords per record
     constexpr int NCH = TR * RB / 16;                              // 16 B chunks per full tile
     constexpr int LD = (NCH + T - 1) / T;
+    constexpr int PC = (RB + 15) / 16;                             // drain pieces per record
+    constexpr int TAILW = (RB % 16) ? (RB % 16) / 4 : 4;           // dwords in the last piece
+    constexpr int DRB = 7;                                         // pieces per lane per batch
     static_assert(RB % 16 == 4 || RB % 16 == 8 || RB % 16 == 12 || RB % 16 == 0, "RB multiple of 4");
     static_assert((TR * RB) % 16 == 0, "tiles start 16 B aligned");
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1444,25 +1447,46 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
         }
         for (uint32_t i = lane; i < RS / 8; i += 64) ((u32x4 *)myrow)[i] = u32x4{0, 0, 0, 0};
         lds_barrier();
-        // ---- drain: the sorted tile as a dword stream, consecutive lanes -> consecutive dwords
-        const int total = (int)nrec * DW;
-        for (int d0 = 0; d0 < total; d0 += 8 * T) {
-            uint32_t v[8], dst[8], wi[8];
-            bool live[8];
+        // ---- drain: the sorted tile in 16 B pieces, PC per record (RB = 100: six of 16 B and
+        //      one of 4 B), consecutive lanes -> consecutive pieces, so a partition run still
+        //      leaves the CU as consecutive lanes, with a quarter of the store instructions and
+        //      LDS lookups of a dword stream.  Records are 4 B-aligned in the stage and in the
+        //      output: the pieces are read as dwords (ds_read2_b32 pairs) and stored as one
+        //      dwordx4 at a 4 B-aligned address (global memory needs only dword alignment).
+        const int units = (int)nrec * PC;
+        for (int u0 = 0; u0 < units; u0 += DRB * T) {
+            u32x4 v[DRB];
+            uint32_t dst[DRB], pc[DRB];
+            bool live[DRB];
 #pragma unroll
-            for (int q = 0; q < 8; ++q) {
-                const int d = d0 + q * T + (int)tid;
-                live[q] = d < total;
-                const uint32_t dd = live[q] ? (uint32_t)d : 0u;
-                const uint32_t s = dd / DW;
-                wi[q] = dd - s * DW;
+            for (int q = 0; q < DRB; ++q) {
+                const int u = u0 + q * T + (int)tid;
+                live[q] = u < units;
+                const uint32_t uu = live[q] ? (uint32_t)u : 0u;
+                const uint32_t s = uu / PC;
+                pc[q] = uu - s * PC;
                 const uint32_t e = idx[s];
-                v[q] = stage[(e & 0xFFFFu) * DW + wi[q]];
+                const uint32_t *sp = stage + (e & 0xFFFFu) * DW + 4 * pc[q];
+                if (TAILW == 4 || pc[q] + 1 < PC) {
+                    v[q] = u32x4{sp[0], sp[1], sp[2], sp[3]};
+                } else {
+                    v[q] = u32x4{sp[0], TAILW > 1 ? sp[1] : 0u, TAILW > 2 ? sp[2] : 0u, 0u};
+                }
                 dst[q] = dlt[e >> 16] + s;
             }
 #pragma unroll
-            for (int q = 0; q < 8; ++q)
-                if (live[q] && dst[q] < (uint32_t)n) out[(uint64_t)dst[q] * DW + wi[q]] = v[q];
+            for (int q = 0; q < DRB; ++q) {
+                if (live[q] && dst[q] < (uint32_t)n) {
+                    uint32_t *d = out + (uint64_t)dst[q] * DW + 4 * pc[q];
+                    if (TAILW == 4 || pc[q] + 1 < PC) {
+                        *(u32x4 *)d = v[q];
+                    } else {
+                        d[0] = v[q].x;
+                        if (TAILW > 1) d[1] = v[q].y;
+                        if (TAILW > 2) d[2] = v[q].z;
+                    }
+                }
+            }
         }
         __syncthreads();  // stage / idx reused by the next tile
     }
