@@ -64,8 +64,10 @@ enum sgx_flags {
     SGX_FLAG_NO_WRITE_COMBINING = 1,  /* hash K4 without on-chip line write-combining      */
     SGX_FLAG_NO_WIDE_STAGED = 2,      /* 100 B records: per-lane K4 instead of LDS-staged   */
     SGX_FLAG_SORT_ALL_DIGITS = 4,     /* sorted reads run every digit pass (no skipping)    */
-    SGX_FLAG_DEBUG_SYNC = 8           /* debugging: synchronise after every kernel and name the
+    SGX_FLAG_DEBUG_SYNC = 8,          /* debugging: synchronise after every kernel and name the
                                          kernel in the error of a device fault (slow)         */
+    SGX_FLAG_LZ4_LANE_DECODE = 16     /* LZ4 reads decode every compressed frame one lane per
+                                         frame (default: only from 32768 frames up)           */
 };
 
 typedef struct sgx_config {

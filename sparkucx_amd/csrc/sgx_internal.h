@@ -103,8 +103,9 @@ hipError_t launch_lz4_walk(const uint8_t *in, int64_t nbytes, int64_t *desc, int
 // u64, initialised to ~0 by the caller (min of position << 8 | code)
 hipError_t launch_lz4_walk_streams(const uint8_t *in, const int64_t *soff, int64_t nstreams, int64_t *cnt,
                                    int64_t *desc, unsigned long long *err, bool write, hipStream_t s);
+// force_lanes: compressed frames one lane per frame whatever their number (SGX_FLAG_LZ4_LANE_DECODE)
 hipError_t launch_lz4_decode(const uint8_t *in, const int64_t *desc, int64_t nframes, uint8_t *out,
-                             uint32_t *err, hipStream_t s);
+                             uint32_t *err, bool force_lanes, hipStream_t s);
 hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, int64_t n_items,
                              int align, hipStream_t stream);
 // items: [n][3] int64 {src address, dst address, bytes} (device memory on both sides).

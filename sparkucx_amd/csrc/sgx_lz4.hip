@@ -532,7 +532,8 @@ constexpr int kInplace = kMaxBlock + (kMaxBlock >> 8) + 32;
 // writes the block out with dword stores.  Errors: atomicOr into *err.
 __global__ __launch_bounds__(64) void k_lz4_decode(const uint8_t *__restrict__ in,
                                                    const int64_t *__restrict__ desc, int64_t nframes,
-                                                   uint8_t *__restrict__ out, uint32_t *__restrict__ err) {
+                                                   uint8_t *__restrict__ out, uint32_t *__restrict__ err,
+                                                   int skip_compressed) {
     __shared__ __attribute__((aligned(16))) uint8_t s_buf[kInplace + 48];
     __shared__ int s_bad;
     const int64_t f = blockIdx.x;
@@ -541,6 +542,7 @@ __global__ __launch_bounds__(64) void k_lz4_decode(const uint8_t *__restrict__ i
     const uint8_t *h = in + desc[2 * f + 0];  // header fields validated by the walk
     const uint32_t tok = h[8], clen = g32le(h + 9), olen = g32le(h + 13), check = g32le(h + 17);
     const bool raw = (tok & 0xF0u) == 0x10u;
+    if (!raw && skip_compressed) return;  // k_lz4_decode_lanes
     const uint8_t *g = h + kHeader;
     const int sh = (int)((uintptr_t)g & 3u);
     const int n = (int)clen;
@@ -639,6 +641,122 @@ __global__ __launch_bounds__(64) void k_lz4_decode(const uint8_t *__restrict__ i
     const int tail0 = head + 4 * nw;
     if (lane < on - tail0) d[tail0 + lane] = ls[tail0 + lane];
 }
+
+// Compressed frames, one LANE per frame (when there are enough frames to fill the chip with
+// lanes: kLaneDecodeMinFrames).  The sequence stream is a serial chain per frame, so one frame
+// per lane makes every wave instruction advance 64 frames, where the wave-per-frame decoder
+// above spends ~30 VALU + ~70 SALU instructions of the whole wave per sequence at one wave
+// per SIMD (its 33 KB of LDS per frame).  The lane decodes straight into the destination
+// (bytes of its own frame only; every write is checked against the frame's output length
+// first, as LZ4_decompress_safe does), reading literals from the fetched payload and match
+// sources from its own earlier output -- a same-thread store -> load through global memory,
+// which the hardware keeps in order.  Copies go 8 bytes at a time: a chunk's 8 loads are
+// issued before its stores (one memory round trip per chunk), which is also what makes the
+// self-overlapping copy exact: chunk [i, i + 8) of a match at offset >= 8 reads bytes
+// written before it, and an offset below 8 repeats the match's first `off` bytes from
+// registers.  Then XXH32 of the frame's output (re-read, L2-resident) against the header.
+// RAW frames stay with k_lz4_decode (skip_compressed).  Errors: atomicOr into *err.
+// (A variant that kept each lane's last 256 output bytes in an LDS ring, so that no load
+// follows the lane's own stores, measured slower: 17.3 / 30.2 ms against 11.9 / 24.6 ms,
+// profiles/r02_lz4_decode_lanes_ab.jsonl.)
+constexpr int64_t kLaneDecodeMinFrames = 32768;  // below: k_lz4_decode does every frame
+
+__device__ uint32_t xxh32_global(const uint8_t *p, int len, uint32_t seed) {
+    const uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u,
+                   P5 = 374761393u;
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t *w = (const uint32_t *)(p - sh);  // aligned dwords, realigned with v_alignbyte
+    uint32_t h;
+    int i = 0;
+    if (len >= 16) {
+        uint32_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+        const int ns = len >> 4;
+        for (int k = 0; k < ns; ++k) {
+            const uint32_t w0 = w[4 * k], w1 = w[4 * k + 1], w2 = w[4 * k + 2], w3 = w[4 * k + 3];
+            const uint32_t w4 = w[4 * k + (sh ? 4 : 3)];  // only when it holds stripe bytes
+            v1 = rotl(v1 + __builtin_amdgcn_alignbyte(w1, w0, sh) * P2, 13) * P1;
+            v2 = rotl(v2 + __builtin_amdgcn_alignbyte(w2, w1, sh) * P2, 13) * P1;
+            v3 = rotl(v3 + __builtin_amdgcn_alignbyte(w3, w2, sh) * P2, 13) * P1;
+            v4 = rotl(v4 + __builtin_amdgcn_alignbyte(w4, w3, sh) * P2, 13) * P1;
+        }
+        h = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+        i = ns << 4;
+    } else {
+        h = seed + P5;
+    }
+    h += (uint32_t)len;
+    for (; i + 4 <= len; i += 4) h = rotl(h + g32(p + i) * P3, 17) * P4;
+    for (; i < len; ++i) h = rotl(h + (uint32_t)p[i] * P5, 11) * P1;
+    h ^= h >> 15; h *= P2; h ^= h >> 13; h *= P3; h ^= h >> 16;
+    return h;
+}
+
+// d and s may overlap (a match copy): each 8-byte chunk is read before it is written
+__device__ __forceinline__ void copy8_chunks(uint8_t *d, const uint8_t *s, uint32_t len) {
+    uint32_t i = 0;
+    for (; i + 8 <= len; i += 8) {
+        uint8_t b[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b[k] = s[i + k];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) d[i + k] = b[k];
+    }
+    if (i < len) {
+        uint8_t b[8];
+        const uint32_t r = len - i;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) b[k] = (uint32_t)k < r ? s[i + k] : (uint8_t)0;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            if ((uint32_t)k < r) d[i + k] = b[k];
+    }
+}
+__global__ __launch_bounds__(64) void k_lz4_decode_lanes(const uint8_t *__restrict__ in,
+                                                         const int64_t *__restrict__ desc, int64_t nframes,
+                                                         uint8_t *__restrict__ out, uint32_t *__restrict__ err) {
+    const int64_t f = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (f >= nframes) return;
+    const uint8_t *h = in + desc[2 * f + 0];
+    if ((h[8] & 0xF0u) == 0x10u) return;
+    const uint32_t clen = g32le(h + 9), olen = g32le(h + 13), check = g32le(h + 17);
+    const uint8_t *src = h + kHeader;
+    uint8_t *o = out + desc[2 * f + 1];
+    uint32_t ip = 0, op = 0, bad = 0;
+    for (;;) {
+        if (ip >= clen) { bad = 1; break; }
+        const uint32_t t = src[ip++];
+        uint32_t lit = t >> 4;
+        if (lit == 15) { uint32_t b; do { if (ip >= clen) { bad = 1; break; } b = src[ip++]; lit += b; } while (b == 255); if (bad) break; }
+        if (ip + lit > clen || op + lit > olen) { bad = 1; break; }
+        copy8_chunks(o + op, src + ip, lit);
+        ip += lit; op += lit;
+        if (ip == clen) break;
+        if (ip + 2 > clen) { bad = 1; break; }
+        const uint32_t off = (uint32_t)src[ip] | ((uint32_t)src[ip + 1] << 8);
+        ip += 2;
+        uint32_t ml = (t & 15u) + kMinMatch;
+        if ((t & 15u) == 15u) { uint32_t b; do { if (ip >= clen) { bad = 1; break; } b = src[ip++]; ml += b; } while (b == 255); if (bad) break; }
+        if (off == 0 || off > op || op + ml > olen) { bad = 1; break; }
+        if (off >= 8) copy8_chunks(o + op, o + op - off, ml);
+        else {
+            uint8_t pat[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) pat[k] = (uint32_t)k < off ? o[op - off + k] : (uint8_t)0;
+            uint32_t m = 0;
+            for (uint32_t i = 0; i < ml; ++i) {
+                uint8_t v = pat[0];
+#pragma unroll
+                for (int k = 1; k < 8; ++k) v = (uint32_t)k == m ? pat[k] : v;
+                o[op + i] = v;
+                m = m + 1 == off ? 0u : m + 1;
+            }
+        }
+        op += ml;
+    }
+    if (!bad && op != olen) bad = 1;
+    if (!bad && (xxh32_global(o, (int)olen, 0x9747b28cu) & 0x0FFFFFFFu) != check) bad = 2;
+    if (bad) atomicOr(err, bad);
+}
 }  // namespace
 
 int lz4_lanes_per_workgroup() { return kLanes; }
@@ -690,9 +808,19 @@ hipError_t launch_lz4_walk_streams(const uint8_t *in, const int64_t *soff, int64
 }
 
 hipError_t launch_lz4_decode(const uint8_t *in, const int64_t *desc, int64_t nframes, uint8_t *out,
-                             uint32_t *err, hipStream_t s) {
+                             uint32_t *err, bool force_lanes, hipStream_t s) {
     if (nframes <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_lz4_decode, dim3((unsigned)nframes), dim3(64), 0, s, in, desc, nframes, out, err);
+    // lane-per-frame decoding of the compressed frames pays off only with enough frames to
+    // fill the chip with lanes: measured (tools/prof_lz4.py, bench.py --compress) 4,056
+    // frames 10.2 (waves) vs 11.9 ms (lanes), ~32K frames 4.31 vs 4.32 ms, 127K frames 58.3
+    // vs 24.6 ms
+    const bool lanes = force_lanes || nframes >= kLaneDecodeMinFrames;
+    hipLaunchKernelGGL(k_lz4_decode, dim3((unsigned)nframes), dim3(64), 0, s, in, desc, nframes, out, err,
+                       lanes ? 1 : 0);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess || !lanes) return e;
+    hipLaunchKernelGGL(k_lz4_decode_lanes, dim3((unsigned)((nframes + 63) / 64)), dim3(64), 0, s, in, desc, nframes,
+                       out, err);
     return hipGetLastError();
 }
 }  // namespace sgx

@@ -261,7 +261,8 @@ int sgx::lz4_unframe_impl(sgx_engine *e, Ctx &c, const void *framed_dev, int64_t
     HIP_TRY(hipMemsetAsync(derr, 0, 4, st));
     hipEvent_t d0 = e->ev(), d1 = e->ev();
     HIP_TRY(hipEventRecord(d0, st));
-    HIP_TRY(sgx::launch_lz4_decode(framed, (const int64_t *)c.lz4_desc.p, nframes, (uint8_t *)dst_dev, derr, st));
+    HIP_TRY(sgx::launch_lz4_decode(framed, (const int64_t *)c.lz4_desc.p, nframes, (uint8_t *)dst_dev, derr,
+                                   (e->flags & SGX_FLAG_LZ4_LANE_DECODE) != 0, st));
     SGX_TRY(debug_sync(e, st, "k_lz4_decode"));
     HIP_TRY(hipEventRecord(d1, st));
     e->record_stage(SGX_STAGE_DECOMPRESS, d0, d1);

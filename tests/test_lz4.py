@@ -86,6 +86,15 @@ def test_oracle_xxh32_matches_xxhash(oracle_lib):
     assert oracle_lib.xxh32(b"", 0) == 0x02CC5D05
 
 
+
+@pytest.fixture(scope="module", params=["wave-decode", "lane-decode"])
+def dec_engine(request, sgx_lib):
+    """An engine per LZ4 decoder: k_lz4_decode for every frame (the default below 32768
+    frames), and k_lz4_decode_lanes for every compressed frame (SGX_FLAG_LZ4_LANE_DECODE)."""
+    flags = sgx_lib.FLAG_LZ4_LANE_DECODE if request.param == "lane-decode" else 0
+    with sgx_lib.ShuffleEngine(device=0, flags=flags) as e:
+        yield e
+
 @pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
 def test_oracle_matches_golden(path, oracle_lib):
     g = np.load(path)
@@ -165,7 +174,7 @@ def test_gpu_matches_oracle_mixed_partitions(engine, oracle_lib, block_size):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("block_size", [4096, 64])
-def test_gpu_tiny_blocks_at_every_byte_phase(engine, oracle_lib, block_size):
+def test_gpu_tiny_blocks_at_every_byte_phase(dec_engine, oracle_lib, block_size):
     """Partitions whose tail block (and whole partitions) of 1..5 bytes start at every byte
     phase of a dword: a block of n < 4 - phase bytes is staged from g[-phase..n) (the
     regression of round 2's multi-rank LZ4 fault, a 1-byte tail at an odd offset)."""
@@ -178,9 +187,9 @@ def test_gpu_tiny_blocks_at_every_byte_phase(engine, oracle_lib, block_size):
     stream = rng.integers(0, 256, size=sum(plen), dtype=np.uint8)
     offs = np.zeros(len(plen) + 1, dtype=np.int64)
     np.cumsum(plen, out=offs[1:])
-    buf = _to_device(engine, stream.tobytes())
+    buf = _to_device(dec_engine, stream.tobytes())
     try:
-        framed, lens = engine.lz4_frame(buf.ptr, offs, block_size)
+        framed, lens = dec_engine.lz4_frame(buf.ptr, offs, block_size)
     finally:
         buf.free()
     want, wlens = oracle_lib.lz4_frame_partitions(stream, offs, block_size)
@@ -227,51 +236,51 @@ def test_gpu_rejects_bad_block_size(engine, sgx_lib):
 # ------------------------------------------------------------- GPU decode (reduce side) --
 @pytest.mark.gpu
 @pytest.mark.parametrize("path", FIXTURES, ids=os.path.basename)
-def test_gpu_unframe_golden(path, engine):
+def test_gpu_unframe_golden(path, dec_engine):
     """LZ4BlockInputStream on the GPU over all partitions' frames back to back = the stream."""
     g = np.load(path)
-    got = engine.lz4_unframe(g["framed"])
+    got = dec_engine.lz4_unframe(g["framed"])
     assert got.tobytes() == g["stream"].tobytes()
 
 
 @pytest.mark.gpu
-def test_gpu_frame_unframe_round_trip(engine, oracle_lib):
+def test_gpu_frame_unframe_round_trip(dec_engine, oracle_lib):
     cases = _cases(oracle_lib)
     stream = b"".join(cases)
     offs = np.zeros(len(cases) + 1, dtype=np.int64)
     np.cumsum([len(c) for c in cases], out=offs[1:])
-    buf = _to_device(engine, stream)
+    buf = _to_device(dec_engine, stream)
     try:
-        framed, lens = engine.lz4_frame(buf.ptr, offs, 4096)
+        framed, lens = dec_engine.lz4_frame(buf.ptr, offs, 4096)
     finally:
         buf.free()
-    assert engine.lz4_unframe(framed).tobytes() == stream
+    assert dec_engine.lz4_unframe(framed).tobytes() == stream
     # any subset of partitions (fetched blocks in any order) decodes to those streams
     fo = np.zeros(len(lens) + 1, dtype=np.int64)
     np.cumsum(lens, out=fo[1:])
     pick = [7, 3, 5, 0, 8]
     sub = b"".join(framed[fo[r]:fo[r + 1]].tobytes() for r in pick)
-    assert engine.lz4_unframe(sub).tobytes() == b"".join(cases[r] for r in pick)
+    assert dec_engine.lz4_unframe(sub).tobytes() == b"".join(cases[r] for r in pick)
 
 
 @pytest.mark.gpu
-def test_gpu_unframe_rejects_corrupt(engine, sgx_lib):
+def test_gpu_unframe_rejects_corrupt(dec_engine, sgx_lib):
     g = np.load(FIXTURES[0])
     framed = bytearray(g["framed"].tobytes())
     bad_magic = bytes(framed)
     bad_magic = b"X" + bad_magic[1:]
     with pytest.raises(sgx_lib._lib.IllegalArgumentException):
-        engine.lz4_unframe(bad_magic)
+        dec_engine.lz4_unframe(bad_magic)
     flipped = bytearray(framed)
     flipped[30] ^= 0x5A  # inside the first payload
     with pytest.raises(sgx_lib._lib.IllegalArgumentException):
-        engine.lz4_unframe(bytes(flipped))
+        dec_engine.lz4_unframe(bytes(flipped))
     with pytest.raises(sgx_lib._lib.IllegalArgumentException):
-        engine.lz4_unframe(bytes(framed[:-5]))  # truncated end mark
+        dec_engine.lz4_unframe(bytes(framed[:-5]))  # truncated end mark
 
 
 @pytest.mark.gpu
-def test_gpu_unframe_dense_frames(engine, oracle_lib):
+def test_gpu_unframe_dense_frames(dec_engine, oracle_lib):
     """5000 tiny partition streams: more frames than the first walk's table holds (re-walk)."""
     rng = np.random.default_rng(3)
     parts = [rng.integers(0, 256, int(rng.integers(1, 9)), dtype=np.uint8).tobytes() for _ in range(5000)]
@@ -279,16 +288,17 @@ def test_gpu_unframe_dense_frames(engine, oracle_lib):
     offs = np.zeros(len(parts) + 1, dtype=np.int64)
     np.cumsum([len(p) for p in parts], out=offs[1:])
     want, _ = oracle_lib.lz4_frame_partitions(np.frombuffer(stream, np.uint8), offs)
-    assert engine.lz4_unframe(want).tobytes() == stream
+    assert dec_engine.lz4_unframe(want).tobytes() == stream
 
 
 def _overlap_cases():
     """Streams whose LZ4 blocks are full of self-overlapping matches (offsets 1..130, the
-    lane-parallel copy's i mod off path and its off >= 64 path), long match-length runs, long
+    lane-parallel copy's i mod off path and its off >= 64 path), matches around and past the
+    lane decoder's 256 B history ring (periods 248..520), long match-length runs, long
     literal runs, and mixtures -- each its own partition stream."""
     rng = np.random.default_rng(11)
     out = [bytes(40000), b"\x07" * 33000]
-    for period in (2, 3, 5, 7, 16, 31, 63, 64, 65, 100, 130):
+    for period in (2, 3, 5, 7, 16, 31, 63, 64, 65, 100, 130, 248, 255, 256, 257, 263, 300, 520):
         pat = rng.integers(0, 256, period, dtype=np.uint8).tobytes()
         out.append((pat * (70000 // period + 1))[:70000])
     mixed = bytearray()
@@ -299,7 +309,7 @@ def _overlap_cases():
         elif k == 1:
             mixed += bytes([int(rng.integers(0, 256))]) * int(rng.integers(1, 2000))
         elif k == 2 and len(mixed) > 70:
-            s = int(rng.integers(0, len(mixed) - 64))
+            s = int(rng.integers(max(0, len(mixed) - 600), len(mixed) - 64))
             mixed += mixed[s:s + int(rng.integers(4, 64))]
         else:
             mixed += (rng.integers(0, 256, 3, dtype=np.uint8).tobytes() * 50)
@@ -309,7 +319,7 @@ def _overlap_cases():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("per_stream", [False, True], ids=["one-walk", "per-stream-walk"])
-def test_gpu_unframe_overlapping_matches(engine, oracle_lib, per_stream):
+def test_gpu_unframe_overlapping_matches(dec_engine, oracle_lib, per_stream):
     """The in-place, lane-parallel decoder against the streams themselves (frames from the
     oracle, whose compressor is pinned to liblz4), through the single walk and the per-stream
     walks of sgx_lz4_unframe_streams."""
@@ -319,13 +329,14 @@ def test_gpu_unframe_overlapping_matches(engine, oracle_lib, per_stream):
     np.cumsum([len(p) for p in parts], out=offs[1:])
     for bs in (32768, 4096, 64):
         framed, flens = oracle_lib.lz4_frame_partitions(np.frombuffer(stream, np.uint8), offs, bs)
-        assert len(framed) < len(stream)  # the blocks really are compressed
-        got = engine.lz4_unframe(framed, flens if per_stream else None)
+        if bs >= 4096:
+            assert len(framed) < len(stream)  # the blocks really are compressed
+        got = dec_engine.lz4_unframe(framed, flens if per_stream else None)
         assert got.tobytes() == stream, bs
 
 
 @pytest.mark.gpu
-def test_gpu_unframe_streams_errors(engine, oracle_lib, sgx_lib):
+def test_gpu_unframe_streams_errors(dec_engine, oracle_lib, sgx_lib):
     parts = _overlap_cases()[:4]
     stream = b"".join(parts)
     offs = np.zeros(len(parts) + 1, dtype=np.int64)
@@ -334,67 +345,67 @@ def test_gpu_unframe_streams_errors(engine, oracle_lib, sgx_lib):
     fb = bytearray(framed.tobytes())
     # the stream lengths must cover the buffer
     with pytest.raises(sgx_lib._lib.IllegalArgumentException):
-        engine.lz4_unframe(bytes(fb), np.concatenate([flens[:-1], [flens[-1] - 1]]))
+        dec_engine.lz4_unframe(bytes(fb), np.concatenate([flens[:-1], [flens[-1] - 1]]))
     # a bad magic in the third stream is reported at its byte position
     pos = int(flens[:2].sum())
     bad = bytearray(fb)
     bad[pos] = ord("X")
     with pytest.raises(sgx_lib._lib.IllegalArgumentException, match=f"bad magic at byte {pos}"):
-        engine.lz4_unframe(bytes(bad), flens)
+        dec_engine.lz4_unframe(bytes(bad), flens)
     # a flipped payload byte fails the block (corrupt sequence or checksum)
     bad = bytearray(fb)
     bad[pos + 40] ^= 0x5A
     with pytest.raises(sgx_lib._lib.IllegalArgumentException):
-        engine.lz4_unframe(bytes(bad), flens)
+        dec_engine.lz4_unframe(bytes(bad), flens)
     # a block cut short inside the second stream
     with pytest.raises(sgx_lib._lib.IllegalArgumentException):
-        engine.lz4_unframe(bytes(fb), np.concatenate([[flens[0] + flens[1] - 5, 5], flens[2:]]))
-    assert engine.lz4_unframe(bytes(fb), flens).tobytes() == stream
+        dec_engine.lz4_unframe(bytes(fb), np.concatenate([[flens[0] + flens[1] - 5, 5], flens[2:]]))
+    assert dec_engine.lz4_unframe(bytes(fb), flens).tobytes() == stream
 
 
 # ------------------------------------------------- shuffle-level compression (engine) --
 @pytest.mark.gpu
-def test_gpu_compressed_shuffle_publishes_lz4_frames(engine, oracle_lib, sgx_lib, tmp_path):
+def test_gpu_compressed_shuffle_publishes_lz4_frames(dec_engine, oracle_lib, sgx_lib, tmp_path):
     """sgx_set_compression(LZ4) on a Kryo shuffle: lengths, map bytes, fetched blocks and the
     committed index/data files are the LZ4BlockOutputStream bytes Spark writes with
     spark.shuffle.compress=true."""
     sid, R, n = 950, 64, 200_000
     recs = oracle_lib.gen_uniform16(n, 0x5EEDC0DE)
     recs[::2, :8] = (np.arange(0, n, 2, dtype=np.int64) % 999).view(np.uint8).reshape(-1, 8)
-    engine.register_shuffle(sid, R)
+    dec_engine.register_shuffle(sid, R)
     try:
-        engine.set_serializer(sid, 1)
-        engine.set_compression(sid, "lz4")
-        lens = engine.write_map(sid, 0, recs, n, 16, num_partitions=R)
+        dec_engine.set_serializer(sid, 1)
+        dec_engine.set_compression(sid, "lz4")
+        lens = dec_engine.write_map(sid, 0, recs, n, 16, num_partitions=R)
         out, counts = oracle_lib.map_write(recs, R)
         want, wlens = oracle_lib.lz4_frame_partitions(oracle_lib.kryo_serialize(out),
                                                       oracle_lib.kryo_partition_offsets(out, counts))
         assert np.array_equal(lens, wlens)
-        assert engine.map_output_bytes(sid, 0).tobytes() == want.tobytes()
+        assert dec_engine.map_output_bytes(sid, 0).tobytes() == want.tobytes()
         fo = oracle_lib.offsets(wlens)
         pick = [5, 0, 63, 17]
-        got, glens = engine.fetch_blocks(sid, [0] * len(pick), pick)
+        got, glens = dec_engine.fetch_blocks(sid, [0] * len(pick), pick)
         assert got.tobytes() == b"".join(want[fo[r]:fo[r + 1]].tobytes() for r in pick)
         # the reduce side decodes what it fetched: LZ4 -> Kryo stream of those partitions
         kry = oracle_lib.kryo_serialize(out)
         ko = oracle_lib.kryo_partition_offsets(out, counts)
-        assert engine.lz4_unframe(got).tobytes() == b"".join(kry[ko[r]:ko[r + 1]].tobytes() for r in pick)
+        assert dec_engine.lz4_unframe(got).tobytes() == b"".join(kry[ko[r]:ko[r + 1]].tobytes() for r in pick)
         idx, dat = str(tmp_path / "s.index"), str(tmp_path / "s.data")
-        committed = engine.write_index(sid, 0, idx, dat, R)
+        committed = dec_engine.write_index(sid, 0, idx, dat, R)
         assert np.array_equal(committed, wlens)
         assert open(dat, "rb").read() == want.tobytes()
         assert open(idx, "rb").read() == oracle_lib.index_bytes(wlens)
         # reduce side: fetch -> LZ4 decompress -> Kryo decode, all on the GPU
-        recs_read = engine.read_records(sid, [0], 3, 40)
+        recs_read = dec_engine.read_records(sid, [0], 3, 40)
         o = oracle_lib.offsets(counts)
         assert recs_read.tobytes() == out[o[3]:o[40]].tobytes()
-        ks, ss = engine.read_grouped(sid, [0], 0, R, sgx_lib._lib.AGG_SUM)
+        ks, ss = dec_engine.read_grouped(sid, [0], 0, R, sgx_lib._lib.AGG_SUM)
         wk, wsum = oracle_lib.reduce_grouped(oracle_lib.canonical_reducer_sequences([(out, counts)], R, 16), "sum")
         assert np.array_equal(ks, wk) and np.array_equal(ss, wsum)
         with pytest.raises(sgx_lib._lib.IllegalStateException):
-            engine.set_compression(sid, "none")
+            dec_engine.set_compression(sid, "none")
     finally:
-        engine.unregister_shuffle(sid)
+        dec_engine.unregister_shuffle(sid)
 
 
 @pytest.mark.gpu
