@@ -49,6 +49,10 @@ def parse():
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                     help="N > 1 exchange backend: RCCL over xGMI (the product path) or host collectives "
                          "over gloo (lets several ranks share one GPU to rehearse the N > 1 path)")
+    ap.add_argument("--self-exchange", action="store_true",
+                    help="N=1 only: run every step's exchange through a one-rank RCCL communicator "
+                         "(counts all-gather + ncclAllToAllv to itself), to measure the overlap of map k+1 "
+                         "with the all-to-all of map k on one GPU (a rehearsal, never the default line)")
     ap.add_argument("--compress", action="store_true",
                     help="with --serializer kryo: spark.shuffle.compress=true (LZ4 frames, Spark's default)")
     ap.add_argument("--serializer", choices=["fixed", "kryo"], default="fixed",
@@ -176,8 +180,11 @@ def main():
 
     n, R = args.records, args.partitions
     eng = sgx.ShuffleEngine(device=device, num_chunks=args.num_chunks)
+    self_x = args.self_exchange and world == 1
     if world > 1 and args.comm == "host":
         eng.comm_init_host(world, rank)
+    elif self_x:
+        eng.comm_init(1, 0, sgx.get_unique_id())
     elif world > 1:
         uid = [sgx.get_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -199,7 +206,7 @@ def main():
 
     def step(k):
         mid = (k & 1) * world + rank  # two alternating map slots per rank
-        if world > 1:
+        if world > 1 or self_x:
             eng.write_map(sid, mid, buf, n, 16)
             eng.exchange(sid, mid)
         else:
@@ -269,13 +276,14 @@ def main():
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
             "data": f"synthetic {args.dist} (Long,Long) 16 B records, splitmix64 seed {args.seed:#x}+rank",
-            "config": {"workload": "C1: 2^28 x 16 B, HashPartitioner R=1024, partition+scatter per GPU"
+            "config": {"workload": ("C1: 2^28 x 16 B, HashPartitioner R=1024, partition+scatter per GPU"
+                                    + (" + exchange through a 1-rank RCCL communicator (rehearsal)" if self_x else ""))
                        if world == 1 else
                        f"C2: {n} x 16 B per GPU ({n * world} total), R={R}, partition + "
                        + ("RCCL alltoallv" if args.comm == "rccl" else "host all-to-all (rehearsal)"),
                        "records_per_gpu": n, "partitions": R, "record_bytes": 16,
                        "parallelism": f"dp{world} (map shards per GPU, reducers owned floor(r*P/R))",
-                       "exchange": None if world == 1 else (
+                       "exchange": ("RCCL ncclAllToAllv, 1 rank (rehearsal)" if self_x else None) if world == 1 else (
                            "RCCL ncclAllToAllv" if args.comm == "rccl" else "host collectives (gloo), rehearsal")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
