@@ -266,3 +266,33 @@ def test_gpu_kryo_exchange_single_rank(engine, oracle_lib):
     finally:
         engine.unregister_shuffle(sid)
         _ = sgx
+
+
+def test_varlong_pinned_to_protobuf_sint64():
+    """Kryo 4's writeVarLong(v, optimizePositive=false) is zigzag + little-endian base-128
+    groups, like protobuf's sint64 varint, except that Kryo stops at 9 bytes (the 9th holds
+    8 bits).  Below 2^56 after zigzag -- encodings of 1..8 bytes -- the two must agree byte for
+    byte: the restatement (and the numpy oracle the GPU tests compare with) is checked
+    against protobuf's independent encoder there; the 9-byte form stays restated."""
+    pb = pytest.importorskip("google.protobuf.internal.encoder")
+    wf = pytest.importorskip("google.protobuf.internal.wire_format")
+    from oracle import spark_semantics as ss
+
+    import oracle as orc
+
+    rng = np.random.default_rng(3)
+    vals = [0, 1, -1, 63, -64, 64, -65, 2**55 - 1, -(2**55)]
+    for bits in range(1, 56):
+        vals += [int(x) for x in rng.integers(-(2**bits), 2**bits, 20)]
+    for v in vals:
+        z = wf.ZigZagEncode(v)
+        assert z < 2**56
+        want = pb._VarintBytes(z)
+        assert ss.kryo_write_var_long(v) == want, v
+    recs = np.zeros((len(vals), 2), dtype=np.int64)
+    recs[:, 0] = vals
+    recs[:, 1] = vals[::-1]
+    stream = orc.kryo_serialize(recs.view(np.uint8).reshape(-1, 16)).tobytes()
+    want = b"".join(b"\x09" + pb._VarintBytes(wf.ZigZagEncode(int(k))) + b"\x09" + pb._VarintBytes(wf.ZigZagEncode(int(x)))
+                    for k, x in recs)
+    assert stream == want

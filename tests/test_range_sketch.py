@@ -120,3 +120,26 @@ def test_terasort_end_to_end_with_sampled_bounds(sgx_lib, oracle_lib, tmp_path):
         assert np.array_equal(got, want)
     finally:
         mgr.stop()
+
+
+def test_murmur3_bytes_hash_pinned_to_scikit_learn():
+    """scala.util.hashing.MurmurHash3.bytesHash (the XORShiftRandom seed hash of the sketch)
+    is MurmurHash3_x86_32; the restatement agrees with scikit-learn's independent C
+    implementation (sklearn.utils.murmurhash3_32) on every tail length, random seeds, Scala's
+    arraySeed and the 8-byte big-endian seeds XORShiftRandom hashes.  This pins one building
+    block of the sketch to an implementation outside this repository; the rest of the row
+    stays unpinned (no JVM here)."""
+    from oracle import spark_semantics as semantics
+
+    murmurhash3_32 = pytest.importorskip("sklearn.utils").murmurhash3_32
+    rng = np.random.default_rng(7)
+    for n in list(range(0, 41)) + [64, 100, 1000]:
+        for seed in (0, 1, 0x3C074A61, 0xFFFFFFFF, int(rng.integers(0, 2**32))):
+            data = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+            want = murmurhash3_32(data, seed=seed, positive=True)
+            assert semantics.murmur3_bytes_hash(data, seed) == want, (n, seed)
+    for s in (0, 1, -1, 42, 2**40 + 7, -(2**63)):
+        b = (s & (2**64 - 1)).to_bytes(8, "big")
+        lo = murmurhash3_32(b, seed=0x3C074A61, positive=True)
+        hi = murmurhash3_32(b, seed=lo, positive=True)
+        assert semantics.xorshift_hash_seed(s) == (hi << 32) | lo
