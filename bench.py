@@ -37,9 +37,14 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--records", type=int, default=1 << 28, help="records per GPU")
-    ap.add_argument("--partitions", type=int, default=1024)
-    ap.add_argument("--dist", choices=["uniform", "zipf"], default="uniform")
+    ap.add_argument("--workload", choices=["c1", "c3", "c4"], default="c1",
+                    help="c1/c2: uniform 16 B records, R=1024 (the default line); c3: Zipf(1.1) keys, "
+                         "R=4096; c4: TeraSort 100 B records (10 B keys), RangePartitioner R=1024 with "
+                         "bounds sampled from the data (rank 0's batch, sketch on the GPU)")
+    ap.add_argument("--records", type=int, default=0,
+                    help="records per GPU (default 2^28; c4: 2^25, i.e. C4's 2^28 records at N=8)")
+    ap.add_argument("--partitions", type=int, default=0, help="default: 1024 (c3: 4096)")
+    ap.add_argument("--dist", choices=["uniform", "zipf"], default=None)
     ap.add_argument("--seed", type=int, default=0x5EEDC0DE)
     ap.add_argument("--num-chunks", type=int, default=0)
     ap.add_argument("--cpu-baseline-seconds", type=float, default=16.0,
@@ -57,7 +62,14 @@ def parse():
                     help="with --serializer kryo: spark.shuffle.compress=true (LZ4 frames, Spark's default)")
     ap.add_argument("--serializer", choices=["fixed", "kryo"], default="fixed",
                     help="kryo: also frame each map output as Spark's Kryo stream (SURVEY §8(f) row 2)")
-    return ap.parse_args()
+    a = ap.parse_args()
+    a.record_bytes = 100 if a.workload == "c4" else 16
+    a.records = a.records or (1 << 25 if a.workload == "c4" else 1 << 28)
+    a.partitions = a.partitions or (4096 if a.workload == "c3" else 1024)
+    a.dist = a.dist or ("zipf" if a.workload == "c3" else "uniform")
+    if a.record_bytes != 16 and (a.serializer != "fixed" or a.dist != "uniform"):
+        ap.error("c4 (100 B TeraSort records) runs with the fixed codec and its own key generator")
+    return a
 
 
 def _cpu_share():
@@ -158,6 +170,21 @@ def load_pmc(dist, n, R, rb=16):
         return None
 
 
+def _workload_name(args, n, R, world, self_x):
+    x = ("RCCL alltoallv" if args.comm == "rccl" else "host all-to-all (rehearsal)") if world > 1 else (
+        "exchange through a 1-rank RCCL communicator (rehearsal)" if self_x else None)
+    if args.workload == "c4":
+        w = f"C4: {n} x 100 B TeraSort records per GPU, RangePartitioner R={R} (sampled bounds), partition+scatter"
+    elif args.workload == "c3":
+        w = f"C3: {n} x 16 B Zipf(1.1) records per GPU, HashPartitioner R={R}, partition+scatter"
+    elif world == 1:
+        w = "C1: 2^28 x 16 B, HashPartitioner R=1024, partition+scatter per GPU" if (n, R) == (1 << 28, 1024) else \
+            f"C1-shaped: {n} x 16 B, HashPartitioner R={R}, partition+scatter per GPU"
+    else:
+        w = f"C2: {n} x 16 B per GPU ({n * world} total), R={R}, partition"
+    return w + (f" + {x}" if x else "")
+
+
 def main():
     args = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -178,7 +205,7 @@ def main():
     device = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(device)
 
-    n, R = args.records, args.partitions
+    n, R, rb = args.records, args.partitions, args.record_bytes
     eng = sgx.ShuffleEngine(device=device, num_chunks=args.num_chunks)
     self_x = args.self_exchange and world == 1
     if world > 1 and args.comm == "host":
@@ -189,8 +216,18 @@ def main():
         uid = [sgx.get_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(world, rank, uid[0])
-    buf = eng.alloc(n * 16)
-    if args.dist == "uniform":
+    buf = eng.alloc(n * rb)
+    bounds = None
+    if rb == 100:
+        # TeraSort: 10 random key bytes + a 90 B payload; RangePartitioner bounds from the
+        # data (RangePartitioner.sketch + determineBounds, the GPU sketch), computed on rank 0
+        # and shared, as Spark's driver does
+        eng.gen_terasort100(buf, n, args.seed + rank, index_base=rank * n)
+        bl = [eng.range_bounds([buf], [n], 100, R) if rank == 0 else None]
+        if dist is not None:
+            dist.broadcast_object_list(bl, src=0)
+        bounds = bl[0]
+    elif args.dist == "uniform":
         eng.gen_uniform16(buf, n, args.seed + rank, value_base=rank * n)
     else:
         ranks = np.arange(1, (1 << 24) + 1, dtype=np.float64)
@@ -198,7 +235,10 @@ def main():
         cdf /= cdf[-1]
         eng.gen_zipf16(buf, n, args.seed + rank, cdf, value_base=rank * n)
     sid = 1
-    eng.register_shuffle(sid, R, serializer=sgx.SER_KRYO if args.serializer == "kryo" else sgx.SER_FIXED)
+    if rb == 100:
+        eng.register_shuffle(sid, R, sgx.PART_RANGE_BYTES10, bounds, True, 100)
+    else:
+        eng.register_shuffle(sid, R, serializer=sgx.SER_KRYO if args.serializer == "kryo" else sgx.SER_FIXED)
     if args.compress:
         if args.serializer != "kryo":
             raise SystemExit("--compress needs --serializer kryo (spark.shuffle.compress applies to serialized streams)")
@@ -207,10 +247,10 @@ def main():
     def step(k):
         mid = (k & 1) * world + rank  # two alternating map slots per rank
         if world > 1 or self_x:
-            eng.write_map(sid, mid, buf, n, 16)
+            eng.write_map(sid, mid, buf, n, rb)
             eng.exchange(sid, mid)
         else:
-            eng.write_map(sid, mid, buf, n, 16)
+            eng.write_map(sid, mid, buf, n, rb)
 
     def barrier():
         if dist is not None:
@@ -237,7 +277,7 @@ def main():
     verified = None
     lens = eng.map_lengths(sid, rank, R)
     if not args.no_verify:
-        verified = bool(lens.sum() == 16 * n) if args.serializer == "fixed" else bool(lens.sum() >= 4 * n)
+        verified = bool(lens.sum() == rb * n) if args.serializer == "fixed" else bool(lens.sum() >= 4 * n)
     xgmi = None
     if world > 1:
         # bytes this rank's map sends over xGMI (reducer r lives on rank floor(r*P/R))
@@ -263,45 +303,44 @@ def main():
 
     if rank == 0:
         ms_per_step = dt * 1e3 / args.steps
-        total_bytes = 16.0 * n * world * args.steps
+        total_bytes = float(rb) * n * world * args.steps
         value = total_bytes / dt / 1e9
         sc_ms = st.ms["scatter"] / max(1, st.count["scatter"])
-        achieved = ALGO_BYTES_PER_REC * n / (sc_ms * 1e-3) / 1e9
-        pmc = load_pmc(args.dist, n, R) or {}
+        algo = 2 * rb  # the record read once and written once
+        achieved = algo * n / (sc_ms * 1e-3) / 1e9
+        pmc = load_pmc(args.dist if rb == 16 else "terasort", n, R, rb) or {}
         k4_pmc, side_pmc = pmc.get("scatter") or {}, pmc.get("map_side") or {}
         side_ms = (st.ms["hist"] + st.ms["scan"] + st.ms["scatter"]) / max(1, st.count["scatter"])
-        side_ach = ALGO_BYTES_PER_REC * n / (side_ms * 1e-3) / 1e9
+        side_ach = algo * n / (side_ms * 1e-3) / 1e9
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "int64",
-            "data": f"synthetic {args.dist} (Long,Long) 16 B records, splitmix64 seed {args.seed:#x}+rank",
-            "config": {"workload": ("C1: 2^28 x 16 B, HashPartitioner R=1024, partition+scatter per GPU"
-                                    + (" + exchange through a 1-rank RCCL communicator (rehearsal)" if self_x else ""))
-                       if world == 1 else
-                       f"C2: {n} x 16 B per GPU ({n * world} total), R={R}, partition + "
-                       + ("RCCL alltoallv" if args.comm == "rccl" else "host all-to-all (rehearsal)"),
-                       "records_per_gpu": n, "partitions": R, "record_bytes": 16,
+            "data": (f"synthetic {args.dist} (Long,Long) 16 B records, splitmix64 seed {args.seed:#x}+rank"
+                     if rb == 16 else f"synthetic TeraSort 100 B records (10 random key bytes), seed {args.seed:#x}+rank, "
+                     f"{len(bounds)} bounds sampled from rank 0's batch"),
+            "config": {"workload": _workload_name(args, n, R, world, self_x),
+                       "records_per_gpu": n, "partitions": R, "record_bytes": rb,
                        "parallelism": f"dp{world} (map shards per GPU, reducers owned floor(r*P/R))",
                        "exchange": ("RCCL ncclAllToAllv, 1 rank (rehearsal)" if self_x else None) if world == 1 else (
                            "RCCL ncclAllToAllv" if args.comm == "rccl" else "host collectives (gloo), rehearsal")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": k4_pmc.get("hbm_bytes_per_launch"),
-                         "kernel": k4_pmc.get("kernel", "K4 scatter"), "algo_bytes_per_record": ALGO_BYTES_PER_REC,
+                         "kernel": k4_pmc.get("kernel", "K4 scatter"), "algo_bytes_per_record": algo,
                          "traffic_source": pmc.get("source")},
             # the whole map side (K1+K2 histogram, K3 scan, K4 scatter, their memsets) against
             # the same 32 B/record: what north_star's partition+scatter target is quoted on
             "roofline_map_side": {"bound": "hbm", "achieved": round(side_ach, 1), "peak": HBM_PEAK_GBS,
                                   "unit": "GB/s", "frac": round(side_ach / HBM_PEAK_GBS, 4),
-                                  "ms": round(side_ms, 4), "algo_bytes_per_record": ALGO_BYTES_PER_REC,
+                                  "ms": round(side_ms, 4), "algo_bytes_per_record": algo,
                                   "traffic": side_pmc.get("hbm_bytes_per_write"),
                                   "traffic_over_algorithmic": side_pmc.get("ratio")},
             "stages_ms_per_step": {k: round(v / max(1, st.count[k]), 4) for k, v in st.ms.items() if st.count[k]},
-            # the two-pass map side must move 48 B per AoS record (hist reads the 16 B record
+            # the two-pass map side must move 3 x record bytes (hist reads the record
             # for its 8 B key; K4 reads 16 + writes 16): its HBM stream rate against 8 TB/s
-            "map_side_two_pass_hbm": {"bytes_per_record": 48, "achieved": round(48.0 * n / side_ms / 1e6, 1),
-                                      "frac": round(48.0 * n / side_ms / 1e6 / HBM_PEAK_GBS, 4)},
+            "map_side_two_pass_hbm": {"bytes_per_record": 3 * rb, "achieved": round(3.0 * rb * n / side_ms / 1e6, 1),
+                                      "frac": round(3.0 * rb * n / side_ms / 1e6 / HBM_PEAK_GBS, 4)},
             "verified_lengths_sum": verified,
         }
         if xgmi is not None:
