@@ -54,6 +54,9 @@ def parse():
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                     help="N > 1 exchange backend: RCCL over xGMI (the product path) or host collectives "
                          "over gloo (lets several ranks share one GPU to rehearse the N > 1 path)")
+    ap.add_argument("--placement", choices=["even", "bytes"], default=None,
+                    help="N > 1 reducer placement: even (floor(r*P/R); the default) or bytes (contiguous "
+                         "ranges balancing each rank's received bytes; the default for c3's skewed keys)")
     ap.add_argument("--self-exchange", action="store_true",
                     help="N=1 only: run every step's exchange through a one-rank RCCL communicator "
                          "(counts all-gather + ncclAllToAllv to itself), to measure the overlap of map k+1 "
@@ -67,6 +70,7 @@ def parse():
     a.records = a.records or (1 << 25 if a.workload == "c4" else 1 << 28)
     a.partitions = a.partitions or (4096 if a.workload == "c3" else 1024)
     a.dist = a.dist or ("zipf" if a.workload == "c3" else "uniform")
+    a.placement = a.placement or ("bytes" if a.workload == "c3" else "even")
     if a.record_bytes != 16 and (a.serializer != "fixed" or a.dist != "uniform"):
         ap.error("c4 (100 B TeraSort records) runs with the fixed codec and its own key generator")
     return a
@@ -239,6 +243,8 @@ def main():
         eng.register_shuffle(sid, R, sgx.PART_RANGE_BYTES10, bounds, True, 100)
     else:
         eng.register_shuffle(sid, R, serializer=sgx.SER_KRYO if args.serializer == "kryo" else sgx.SER_FIXED)
+    if args.placement == "bytes":
+        eng.set_reducer_placement(sid, "bytes")
     if args.compress:
         if args.serializer != "kryo":
             raise SystemExit("--compress needs --serializer kryo (spark.shuffle.compress applies to serialized streams)")
@@ -281,7 +287,13 @@ def main():
     xgmi = None
     if world > 1:
         # bytes this rank's map sends over xGMI (reducer r lives on rank floor(r*P/R))
-        owner = (np.arange(R, dtype=np.int64) * world) // R
+        r0, r1 = eng.round_reducers(sid, rank)  # the round of map `rank`, whose lengths `lens` are
+        rr = torch.tensor([r0, r1], dtype=torch.int64)
+        allr = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
+        dist.all_gather(allr, rr)
+        owner = np.zeros(R, dtype=np.int64)
+        for j, t in enumerate(allr):
+            owner[int(t[0]):int(t[1])] = j
         sent = float(lens[owner != rank].sum())
         a2a_ms = st.ms["alltoall"] / max(1, st.count["alltoall"])
         # bytes each rank receives (load balance of the reducer ranges, config C3)
@@ -321,7 +333,8 @@ def main():
                      f"{len(bounds)} bounds sampled from rank 0's batch"),
             "config": {"workload": _workload_name(args, n, R, world, self_x),
                        "records_per_gpu": n, "partitions": R, "record_bytes": rb,
-                       "parallelism": f"dp{world} (map shards per GPU, reducers owned floor(r*P/R))",
+                       "parallelism": f"dp{world} (map shards per GPU, reducers owned "
+                                      + ("floor(r*P/R))" if args.placement == "even" else "in byte-balanced ranges)"),
                        "exchange": ("RCCL ncclAllToAllv, 1 rank (rehearsal)" if self_x else None) if world == 1 else (
                            "RCCL ncclAllToAllv" if args.comm == "rccl" else "host collectives (gloo), rehearsal")},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",

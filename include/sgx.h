@@ -164,6 +164,21 @@ int sgx_lz4_unframe_streams(sgx_engine *e, const void *framed_dev, const int64_t
  * canonical order the parity tests compare).  Set before the first write (SGX_ERR_STATE
  * after).  sgx_read_grouped(SGX_AGG_SUM) on such a shuffle is combineCombinersByKey. */
 int sgx_set_map_side_combine(sgx_engine *e, int32_t shuffle_id, int32_t agg);
+
+/* Reducer placement of a shuffle's exchange rounds (sgx_exchange).  SGX_PLACE_EVEN (the
+ * default): rank j holds the reducers r with floor(r * P / R) == j.  SGX_PLACE_BYTES:
+ * contiguous reducer ranges that balance the bytes each rank receives in the round
+ * (sgx_balanced_ranges over the all-gathered lengths, the same on every rank), for skewed
+ * keys (config C3: Zipf(1.1) puts most of the head of the distribution on rank 0 under the
+ * even split).  Which ranks run which reduce tasks is the engine's choice -- Spark's
+ * scheduler places reduce tasks itself (UcxShuffleReader.scala:74-103 reads whichever
+ * partition range it is given); the canonical per-reducer sequences do not change.
+ * Placement may change between rounds. */
+enum sgx_placement { SGX_PLACE_EVEN = 0, SGX_PLACE_BYTES = 1 };
+int sgx_set_reducer_placement(sgx_engine *e, int32_t shuffle_id, int32_t placement);
+/* The reducers [*r0, *r1) this rank holds for the exchange round that carried map_id (the
+ * map of any rank in that round). */
+int sgx_round_reducers(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int32_t *r0, int32_t *r1);
 /* unregisterShuffle: CommonUcxShuffleManager.scala:103-106 -> removeShuffle
  * (CommonUcxShuffleBlockResolver.scala:63-71). Frees the shuffle's HBM. */
 int sgx_unregister_shuffle(sgx_engine *e, int32_t shuffle_id);
@@ -362,6 +377,18 @@ int sgx_plan_exchange(const int64_t *lengths_all, int32_t P, int32_t R, int32_t 
                       int64_t item_bytes, int64_t *send_counts, int64_t *send_displs,
                       int64_t *recv_counts, int64_t *recv_displs, int64_t *items,
                       int64_t *n_items);
+/* sgx_plan_exchange for explicit contiguous reducer ranges: rank j holds [bounds[j],
+ * bounds[j + 1]) (bounds[P + 1], bounds[0] = 0, non-decreasing, bounds[P] = R). */
+int sgx_plan_exchange_ranges(const int64_t *lengths_all, int32_t P, int32_t R, int32_t rank,
+                             const int32_t *bounds, int64_t item_bytes, int64_t *send_counts,
+                             int64_t *send_displs, int64_t *recv_counts, int64_t *recv_displs,
+                             int64_t *items, int64_t *n_items);
+/* Byte-balanced placement: bounds[P + 1] of P contiguous reducer ranges minimising the largest
+ * per-rank total of sum_j lengths_all[j][r] (binary search on the bound + greedy cuts; a
+ * round with no bytes gets the even split).  Deterministic: every rank computes the same. */
+int sgx_balanced_ranges(const int64_t *lengths_all, int32_t P, int32_t R, int32_t *bounds);
+/* The even placement's bounds[P + 1] (floor(r * P / R) == j). */
+int sgx_even_ranges(int32_t P, int32_t R, int32_t *bounds);
 /* Apply a regroup copy list (items[n][3] host array, as produced by sgx_plan_exchange)
  * from src_dev to dst_dev with the K5 kernel; synchronous. */
 int sgx_copy_items(sgx_engine *e, const void *src_dev, void *dst_dev, const int64_t *items,

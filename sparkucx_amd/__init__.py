@@ -8,13 +8,15 @@ CPU fallback and raises if the library is missing.
 from ._lib import (  # noqa: F401
     AGG_GROUP, AGG_SUM, FLAG_DEBUG_SYNC, FLAG_LZ4_LANE_DECODE, FLAG_NO_WIDE_STAGED, FLAG_NO_WRITE_COMBINING,
     FLAG_SORT_ALL_DIGITS, HIST_ATOMIC,
-    HIST_BALLOT, MEM_DEVICE, MEM_HOST, PART_HASH, PART_RANGE_BYTES10, PART_RANGE_I64, RANK_MATCH, RANK_ORDERED,
+    HIST_BALLOT, MEM_DEVICE, MEM_HOST, PART_HASH, PART_RANGE_BYTES10, PART_RANGE_I64, PLACE_BYTES, PLACE_EVEN,
+    RANK_MATCH, RANK_ORDERED,
     SER_FIXED, SER_KRYO, STAGES,
     BlockNotFoundException, DeviceError, IllegalArgumentException, IllegalStateException,
     ShuffleError, ShuffleIOException, TransportError, UnsupportedOperationException, lib,
 )
 from .engine import (  # noqa: F401
-    DeviceBuffer, ShuffleEngine, bootstrap_join, bootstrap_serve, get_unique_id, plan_exchange, reducer_owner,
+    DeviceBuffer, ShuffleEngine, balanced_ranges, bootstrap_join, bootstrap_serve, even_ranges, get_unique_id,
+    plan_exchange, reducer_owner,
 )
 from .shuffle import (  # noqa: F401
     Aggregator, BaseShuffleHandle, BlockFetchingListener, GpuShuffleMapOutputWriter, GpuShuffleTransport, GpuShuffleWriter,

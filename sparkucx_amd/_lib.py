@@ -28,6 +28,7 @@ HIST_ATOMIC, HIST_BALLOT = 0, 1
 RANK_ORDERED, RANK_MATCH = 0, 1
 FLAG_NO_WRITE_COMBINING, FLAG_NO_WIDE_STAGED, FLAG_SORT_ALL_DIGITS, FLAG_DEBUG_SYNC = 1, 2, 4, 8
 FLAG_LZ4_LANE_DECODE = 16
+PLACE_EVEN, PLACE_BYTES = 0, 1
 ABI_VERSION = 3
 
 
@@ -131,6 +132,11 @@ SIGNATURES = {
     "sgx_plan_exchange": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _P64]),
     "sgx_copy_items": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i32]),
     "sgx_reducer_owner": (_i32, [_i32, _i32, _i32]),
+    "sgx_plan_exchange_ranges": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _P64]),
+    "sgx_balanced_ranges": (ctypes.c_int, [_vp, _i32, _i32, _vp]),
+    "sgx_even_ranges": (ctypes.c_int, [_i32, _i32, _vp]),
+    "sgx_set_reducer_placement": (ctypes.c_int, [_vp, _i32, _i32]),
+    "sgx_round_reducers": (ctypes.c_int, [_vp, _i32, _i64, _vp, _vp]),
     "sgx_gen_uniform16": (ctypes.c_int, [_vp, _vp, _i64, _u64, _i64]),
     "sgx_gen_zipf16": (ctypes.c_int, [_vp, _vp, _i64, _u64, _i64, _vp, _i64]),
     "sgx_gen_terasort100": (ctypes.c_int, [_vp, _vp, _i64, _u64, _i64]),

@@ -329,6 +329,16 @@ extern "C" int sgx_set_map_side_combine(sgx_engine *e, int32_t shuffle_id, int32
     return SGX_OK;
 }
 
+extern "C" int sgx_set_reducer_placement(sgx_engine *e, int32_t shuffle_id, int32_t placement) {
+    if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
+    if (placement != SGX_PLACE_EVEN && placement != SGX_PLACE_BYTES)
+        return fail_msg(SGX_ERR_INVALID, "unknown reducer placement %d", placement);
+    std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
+    if (!s) return SGX_ERR_STATE;
+    s->placement.store(placement);  // applies from the next exchange round on
+    return SGX_OK;
+}
+
 // ------------------------------------------------------------------------------------
 // progress / sync / stats
 // ------------------------------------------------------------------------------------

@@ -193,6 +193,7 @@ struct Shuffle {
     int32_t ser = SGX_SER_FIXED;  // dep.serializer (sgx_set_serializer)
     int32_t lz4_block = 0;        // spark.shuffle.compress with lz4 (sgx_set_compression): block size
     int32_t combine = -1;         // map-side combine aggregation (sgx_set_map_side_combine), -1 = none
+    std::atomic<int32_t> placement{SGX_PLACE_EVEN};  // reducer placement of exchange rounds
     DevBuf bounds;
     PartParams pp{};
     std::map<int64_t, std::shared_ptr<MapOut>> maps;

@@ -121,13 +121,12 @@ extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
     auto rd = std::make_shared<Round>();
     rd->map_ids.assign((size_t)P, 0);
     rd->lens.assign((size_t)P * R, 0);
-    my_reducers(R, P, e->rank, &rd->r0, &rd->r1);
-    const int32_t nmine = rd->r1 - rd->r0;
+    my_reducers(R, P, e->rank, &rd->r0, &rd->r1);  // the collective path re-places after the all-gather
     if (e->comm_broken) return fail_msg(SGX_ERR_STATE, "the communicator was aborted after an exchange failure");
     if (P == 1 && !e->comm && !e->host_comm) {
         rd->map_ids[0] = map_id;
         std::memcpy(rd->lens.data(), mylens.data(), sizeof(int64_t) * (size_t)R);
-        rd->block_off.assign((size_t)nmine, 0);
+        rd->block_off.assign((size_t)R, 0);
         int64_t off = 0;
         for (int32_t r = 0; r < R; ++r) {
             rd->block_off[(size_t)r] = off;
@@ -173,11 +172,20 @@ extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
         rd->map_ids[(size_t)j] = agh[row * (size_t)(j + 1)];
         std::memcpy(&rd->lens[(size_t)j * R], agh + row * (size_t)(j + 1) + 1, sizeof(int64_t) * (size_t)R);
     }
-    // (2) plan: send/recv counts and displacements (no copy list: blocks stay where they land)
+    // (2) placement (the same on every rank: it depends on the all-gathered lengths only) and
+    //     plan: send/recv counts and displacements (no copy list: blocks stay where they land)
+    std::vector<int32_t> bounds((size_t)P + 1);
+    if (s->placement.load() == SGX_PLACE_BYTES)
+        SGX_TRY(sgx_balanced_ranges(rd->lens.data(), P, R, bounds.data()));
+    else
+        SGX_TRY(sgx_even_ranges(P, R, bounds.data()));
+    rd->r0 = bounds[(size_t)e->rank];
+    rd->r1 = bounds[(size_t)e->rank + 1];
+    const int32_t nmine = rd->r1 - rd->r0;
     std::vector<int64_t> sc(P), sd(P), rc(P), rdp(P);
     int64_t nitems = 0;
-    SGX_TRY(sgx_plan_exchange(rd->lens.data(), P, R, e->rank, 0, sc.data(), sd.data(), rc.data(), rdp.data(), nullptr,
-                              &nitems));
+    SGX_TRY(sgx_plan_exchange_ranges(rd->lens.data(), P, R, e->rank, bounds.data(), 0, sc.data(), sd.data(), rc.data(),
+                                     rdp.data(), nullptr, &nitems));
     if (sd[(size_t)P - 1] + sc[(size_t)P - 1] != out_bytes)
         return fail_msg(SGX_ERR_HIP, "internal error: send plan covers %lld of %lld bytes",
                         (long long)(sd[(size_t)P - 1] + sc[(size_t)P - 1]), (long long)out_bytes);
@@ -261,4 +269,20 @@ extern "C" int sgx_copy_items(sgx_engine *e, const void *src, void *dst, const i
     HIP_TRY(launch_copy_items(src, dst, (const int64_t *)c->items_dev.p, n_items, align, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
     return SGX_OK;
+}
+
+extern "C" int sgx_round_reducers(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int32_t *r0, int32_t *r1) {
+    if (!e || !r0 || !r1) return fail_msg(SGX_ERR_INVALID, "NULL argument");
+    std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
+    if (!s) return SGX_ERR_STATE;
+    std::lock_guard<std::mutex> sl(s->mu);
+    for (auto it = s->rounds.rbegin(); it != s->rounds.rend(); ++it)
+        for (int64_t m : (*it)->map_ids)
+            if (m == map_id) {
+                *r0 = (*it)->r0;
+                *r1 = (*it)->r1;
+                return SGX_OK;
+            }
+    return fail_msg(SGX_ERR_NOT_FOUND, "no exchange round of shuffle %d carried map %lld", shuffle_id,
+                    (long long)map_id);
 }

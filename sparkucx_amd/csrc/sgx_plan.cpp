@@ -13,25 +13,97 @@ extern "C" int32_t sgx_reducer_owner(int32_t r, int32_t R, int32_t P) {
     return sgx::reducer_owner(r, R, P);
 }
 
+extern "C" int sgx_even_ranges(int32_t P, int32_t R, int32_t *bounds) {
+    if (P < 1 || R < 0 || !bounds) return sgx::fail_msg(SGX_ERR_INVALID, "sgx_even_ranges: bad arguments");
+    for (int32_t j = 0; j < P; ++j) {
+        int32_t r0, r1;
+        sgx::my_reducers(R, P, j, &r0, &r1);
+        bounds[j] = r0;
+    }
+    bounds[P] = R;
+    return SGX_OK;
+}
+
+// Linear partition of the per-reducer totals T[r] = sum_j L[j][r] into P contiguous ranges
+// minimising the largest range total: the smallest X for which greedy left-to-right cuts
+// (close a range before it would pass X) need at most P ranges, found by binary search;
+// then the same greedy cuts at that X.  O(R log sum).
+extern "C" int sgx_balanced_ranges(const int64_t *L, int32_t P, int32_t R, int32_t *bounds) {
+    if (!L || P < 1 || R < 1 || !bounds) return sgx::fail_msg(SGX_ERR_INVALID, "sgx_balanced_ranges: bad arguments");
+    std::vector<int64_t> T((size_t)R, 0);
+    int64_t total = 0, big = 0;
+    for (int32_t j = 0; j < P; ++j)
+        for (int32_t r = 0; r < R; ++r) {
+            const int64_t v = L[(int64_t)j * R + r];
+            if (v < 0) return sgx::fail_msg(SGX_ERR_INVALID, "sgx_balanced_ranges: negative length");
+            T[(size_t)r] += v;
+        }
+    for (int32_t r = 0; r < R; ++r) {
+        total += T[(size_t)r];
+        big = T[(size_t)r] > big ? T[(size_t)r] : big;
+    }
+    if (total == 0) return sgx_even_ranges(P, R, bounds);
+    auto ranges_at = [&](int64_t X, int32_t *b) {  // greedy cuts; returns the number of ranges
+        int32_t k = 0;
+        int64_t acc = 0;
+        if (b) b[0] = 0;
+        for (int32_t r = 0; r < R; ++r) {
+            if (acc > 0 && acc + T[(size_t)r] > X) {
+                ++k;
+                if (b && k < P) b[k] = r;
+                acc = 0;
+            }
+            acc += T[(size_t)r];
+        }
+        return k + 1;
+    };
+    int64_t lo = big, hi = total;  // ranges_at(hi) == 1 <= P
+    while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (ranges_at(mid, nullptr) <= P) hi = mid;
+        else lo = mid + 1;
+    }
+    const int32_t k = ranges_at(lo, bounds);
+    for (int32_t j = k; j <= P; ++j) bounds[j] = R;  // ranks past the last cut hold nothing
+    return SGX_OK;
+}
+
 extern "C" int sgx_plan_exchange(const int64_t *L, int32_t P, int32_t R, int32_t rank, int64_t item_bytes,
                                  int64_t *send_counts, int64_t *send_displs, int64_t *recv_counts,
                                  int64_t *recv_displs, int64_t *items, int64_t *n_items) {
-    if (!L || P < 1 || R < 1 || rank < 0 || rank >= P || !send_counts || !send_displs || !recv_counts ||
+    if (P < 1 || R < 1) return sgx::fail_msg(SGX_ERR_INVALID, "sgx_plan_exchange: bad arguments");
+    std::vector<int32_t> b((size_t)P + 1);
+    sgx_even_ranges(P, R, b.data());
+    return sgx_plan_exchange_ranges(L, P, R, rank, b.data(), item_bytes, send_counts, send_displs, recv_counts,
+                                    recv_displs, items, n_items);
+}
+
+extern "C" int sgx_plan_exchange_ranges(const int64_t *L, int32_t P, int32_t R, int32_t rank, const int32_t *bounds,
+                                        int64_t item_bytes, int64_t *send_counts, int64_t *send_displs,
+                                        int64_t *recv_counts, int64_t *recv_displs, int64_t *items,
+                                        int64_t *n_items) {
+    if (!L || P < 1 || R < 1 || rank < 0 || rank >= P || !bounds || !send_counts || !send_displs || !recv_counts ||
         !recv_displs || !n_items || *n_items < 0 || item_bytes < 0)
         return sgx::fail_msg(SGX_ERR_INVALID, "sgx_plan_exchange: bad arguments");
+    if (bounds[0] != 0 || bounds[P] != R)
+        return sgx::fail_msg(SGX_ERR_INVALID, "sgx_plan_exchange: ranges must cover [0, %d)", R);
+    for (int32_t j = 0; j < P; ++j)
+        if (bounds[j] > bounds[j + 1])
+            return sgx::fail_msg(SGX_ERR_INVALID, "sgx_plan_exchange: ranges out of order at rank %d", j);
     const int64_t *mine = L + (int64_t)rank * R;
-    for (int32_t j = 0; j < P; ++j) send_counts[j] = 0;
-    for (int32_t r = 0; r < R; ++r) {
-        if (mine[r] < 0) return sgx::fail_msg(SGX_ERR_INVALID, "sgx_plan_exchange: negative length at %d", r);
-        send_counts[sgx::reducer_owner(r, R, P)] += mine[r];
+    for (int32_t j = 0; j < P; ++j) {
+        send_counts[j] = 0;
+        for (int32_t r = bounds[j]; r < bounds[j + 1]; ++r) {
+            if (mine[r] < 0) return sgx::fail_msg(SGX_ERR_INVALID, "sgx_plan_exchange: negative length at %d", r);
+            send_counts[j] += mine[r];
+        }
     }
     int64_t run = 0;
     for (int32_t j = 0; j < P; ++j) {
         send_displs[j] = run;
         run += send_counts[j];
     }
-    int32_t r0, r1;
-    sgx::my_reducers(R, P, rank, &r0, &r1);
+    const int32_t r0 = bounds[rank], r1 = bounds[rank + 1];
     run = 0;
     for (int32_t sidx = 0; sidx < P; ++sidx) {
         int64_t c = 0;

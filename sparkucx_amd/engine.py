@@ -146,6 +146,21 @@ class ShuffleEngine:
         {key, sum} combiner per distinct key and partition."""
         check(lib().sgx_set_map_side_combine(self.handle, shuffle_id, agg), "setMapSideCombine")
 
+    def set_reducer_placement(self, shuffle_id: int, placement: str = "bytes"):
+        """Reducer placement of the shuffle's exchange rounds: "even" (floor(r*P/R), the
+        default) or "bytes" (contiguous ranges balancing each rank's received bytes)."""
+        codes = {"even": _lib.PLACE_EVEN, "bytes": _lib.PLACE_BYTES}
+        if placement not in codes:
+            raise _lib.IllegalArgumentException(f"unknown placement {placement!r} (even, bytes)")
+        check(lib().sgx_set_reducer_placement(self.handle, shuffle_id, codes[placement]), "setReducerPlacement")
+
+    def round_reducers(self, shuffle_id: int, map_id: int) -> Tuple[int, int]:
+        """[r0, r1): the reducers this rank holds for the exchange round that carried map_id."""
+        r0, r1 = ctypes.c_int32(0), ctypes.c_int32(0)
+        check(lib().sgx_round_reducers(self.handle, shuffle_id, map_id, ctypes.byref(r0), ctypes.byref(r1)),
+              "roundReducers")
+        return r0.value, r1.value
+
     def release_thread(self):
         """Free the calling thread's HIP stream and scratch (recreated on its next call)."""
         check(lib().sgx_release_thread(self.handle), "release_thread")
@@ -467,21 +482,41 @@ def get_unique_id() -> bytes:
     return buf.raw
 
 
-def plan_exchange(lengths_all: np.ndarray, rank: int, item_bytes: int = 0):
+def plan_exchange(lengths_all: np.ndarray, rank: int, item_bytes: int = 0, bounds=None):
     """Pure-host exchange plan (no GPU): returns (send_counts, send_displs, recv_counts,
-    recv_displs, items[n,3])."""
+    recv_displs, items[n,3]).  bounds: the P + 1 reducer-range bounds (default: the even
+    placement, floor(r*P/R))."""
     L = np.ascontiguousarray(lengths_all, dtype=np.int64)
     P, R = L.shape
+    b = even_ranges(P, R) if bounds is None else np.ascontiguousarray(bounds, dtype=np.int32)
     sc, sd, rc, rd = (np.zeros(P, np.int64) for _ in range(4))
     n = ctypes.c_int64(0)
-    check(lib().sgx_plan_exchange(L.ctypes.data, P, R, rank, item_bytes, sc.ctypes.data, sd.ctypes.data,
-                                  rc.ctypes.data, rd.ctypes.data, None, ctypes.byref(n)), "plan_exchange")
+
+    def call(items, cnt):
+        check(lib().sgx_plan_exchange_ranges(L.ctypes.data, P, R, rank, b.ctypes.data, item_bytes, sc.ctypes.data,
+                                             sd.ctypes.data, rc.ctypes.data, rd.ctypes.data, items, ctypes.byref(cnt)),
+              "plan_exchange")
+
+    call(None, n)
     items = np.zeros((max(n.value, 1), 3), np.int64)
-    cap = ctypes.c_int64(n.value)
-    check(lib().sgx_plan_exchange(L.ctypes.data, P, R, rank, item_bytes, sc.ctypes.data, sd.ctypes.data,
-                                  rc.ctypes.data, rd.ctypes.data, items.ctypes.data, ctypes.byref(cap)),
-          "plan_exchange")
+    call(items.ctypes.data, ctypes.c_int64(n.value))
     return sc, sd, rc, rd, items[: n.value]
+
+
+def even_ranges(P: int, R: int) -> np.ndarray:
+    """Bounds [P + 1] of the even placement: rank j holds [b[j], b[j + 1])."""
+    b = np.zeros(P + 1, np.int32)
+    check(lib().sgx_even_ranges(P, R, b.ctypes.data), "even_ranges")
+    return b
+
+
+def balanced_ranges(lengths_all: np.ndarray) -> np.ndarray:
+    """Bounds [P + 1] of the byte-balanced placement over [P][R] lengths (sgx_balanced_ranges)."""
+    L = np.ascontiguousarray(lengths_all, dtype=np.int64)
+    P, R = L.shape
+    b = np.zeros(P + 1, np.int32)
+    check(lib().sgx_balanced_ranges(L.ctypes.data, P, R, b.ctypes.data), "balanced_ranges")
+    return b
 
 
 def reducer_owner(reduce_id: int, num_partitions: int, nranks: int) -> int:

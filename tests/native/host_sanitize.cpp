@@ -28,7 +28,46 @@ static int failures = 0;
         }                                                                                   \
     } while (0)
 
+static void placement_checks() {
+    std::mt19937_64 rng(7);
+    for (int P : {1, 2, 3, 8}) {
+        for (int R : {1, 2, 7, 1024, 4099}) {
+            std::vector<int64_t> L((size_t)P * R);
+            for (auto &x : L) x = (int64_t)(rng() % 100 == 0 ? 100000 : rng() % 5000) * 16;
+            std::vector<int32_t> b((size_t)P + 1);
+            CHECK(sgx_balanced_ranges(L.data(), P, R, b.data()) == SGX_OK);
+            CHECK(b[0] == 0 && b[(size_t)P] == R);
+            for (int j = 0; j < P; ++j) CHECK(b[(size_t)j] <= b[(size_t)j + 1]);
+            int64_t total = 0;
+            for (int rank = 0; rank < P; ++rank) {
+                std::vector<int64_t> sc(P), sd(P), rc(P), rd(P);
+                int64_t n = 0;
+                CHECK(sgx_plan_exchange_ranges(L.data(), P, R, rank, b.data(), 0, sc.data(), sd.data(), rc.data(),
+                                               rd.data(), nullptr, &n) == SGX_OK);
+                for (int j = 0; j < P; ++j) total += rc[j];
+            }
+            int64_t all = 0;
+            for (int64_t x : L) all += x;
+            CHECK(total == all);
+            std::vector<int32_t> bad(b);
+            if (P > 1) {
+                bad[1] = R + 1;
+                int64_t n = 0;
+                std::vector<int64_t> sc(P), sd(P), rc(P), rd(P);
+                CHECK(sgx_plan_exchange_ranges(L.data(), P, R, 0, bad.data(), 0, sc.data(), sd.data(), rc.data(),
+                                               rd.data(), nullptr, &n) == SGX_ERR_INVALID);
+            }
+        }
+    }
+    std::vector<int64_t> zeros(12, 0);
+    std::vector<int32_t> b(5), e(5);
+    CHECK(sgx_balanced_ranges(zeros.data(), 4, 3, b.data()) == SGX_OK);
+    CHECK(sgx_even_ranges(4, 3, e.data()) == SGX_OK);
+    CHECK(b == e);
+}
+
 static void plan_checks() {
+    placement_checks();
     std::mt19937_64 rng(42);
     for (int P : {1, 2, 3, 4, 8}) {
         for (int R : {1, 3, 200, 1024, 4099}) {

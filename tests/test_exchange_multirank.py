@@ -27,11 +27,19 @@ def free_port():
         return s.getsockname()[1]
 
 
-def batch(oracle, rank, k, n):
+_ZIPF = {}
+
+
+def batch(oracle, rank, k, n, keys="uniform"):
+    if keys == "zipf":  # config C3's key distribution: Zipf(1.1) ranks over 2^20 keys
+        if "cdf" not in _ZIPF:
+            _ZIPF["cdf"] = oracle.zipf_cdf(1.1, 1 << 20)
+        return oracle.gen_zipf16(n + 101 * rank + 7 * k, 0xB0 + 16 * k + rank, _ZIPF["cdf"],
+                                 value_base=(rank << 40) | (k << 36))
     return oracle.gen_uniform16(n + 101 * rank + 7 * k, 0xA0 + 16 * k + rank, value_base=(rank << 40) | (k << 36))
 
 
-def worker(rank, world, port, backend, codec, R, n, result_dir):
+def worker(rank, world, port, backend, codec, R, n, result_dir, placement="even", keys="uniform"):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -52,16 +60,29 @@ def worker(rank, world, port, backend, codec, R, n, result_dir):
         e.register_shuffle(sid, R, serializer=sgx.SER_FIXED if codec == "fixed" else sgx.SER_KRYO)
         if codec == "kryo+lz4":
             e.set_compression(sid, "lz4", 4096)
+        if placement == "bytes":
+            e.set_reducer_placement(sid, "bytes")
         mine = [r for r in range(R) if sgx.reducer_owner(r, R, world) == rank]
         for k in range(3):  # three rounds: map slots reused, receive buffers recycled
             mid = k * world + rank
-            recs = batch(oracle, rank, k, n)
+            recs = batch(oracle, rank, k, n, keys)
             e.write_map(sid, mid, recs, len(recs), 16)
             e.exchange(sid, mid)
             e.sync()
-            outs = [oracle.map_write(batch(oracle, r, k, n), R) for r in range(world)]
+            outs = [oracle.map_write(batch(oracle, r, k, n, keys), R) for r in range(world)]
             seqs = oracle.canonical_reducer_sequences(outs, R, 16)
             maps = [k * world + r for r in range(world)]
+            r0, r1 = e.round_reducers(sid, mid)
+            if placement == "bytes":
+                mine = list(range(r0, r1))
+                if codec == "fixed":  # the placement every rank must have computed
+                    want_b = sgx.balanced_ranges(np.stack([c * 16 for _, c in outs]))
+                    if (r0, r1) != (int(want_b[rank]), int(want_b[rank + 1])):
+                        msg = f"round {k}: placement [{r0}, {r1}) differs from {want_b.tolist()}"
+                        break
+            elif (r0, r1) != ((mine[0], mine[-1] + 1) if mine else (r0, r0)):
+                msg = f"round {k}: even placement [{r0}, {r1}) differs"
+                break
             if not mine:
                 continue
             # raw blocks of my reducers, reducer-major / map-minor: the published bytes
@@ -108,11 +129,11 @@ def worker(rank, world, port, backend, codec, R, n, result_dir):
         dist.destroy_process_group()
 
 
-def run_world(tmp_path, world, backend, codec, R, n):
+def run_world(tmp_path, world, backend, codec, R, n, placement="even", keys="uniform"):
     import torch.multiprocessing as mp
 
-    mp.start_processes(worker, args=(world, free_port(), backend, codec, R, n, str(tmp_path)), nprocs=world,
-                       start_method="spawn", join=True)
+    mp.start_processes(worker, args=(world, free_port(), backend, codec, R, n, str(tmp_path), placement, keys),
+                       nprocs=world, start_method="spawn", join=True)
     msgs = {r: (tmp_path / f"rank{r}").read_text() for r in range(world)}
     bad = {r: m for r, m in msgs.items() if m != "ok"}
     assert not bad, "\n".join(f"rank {r}: {m}" for r, m in bad.items())
@@ -124,6 +145,15 @@ def run_world(tmp_path, world, backend, codec, R, n):
                                              (4, "kryo+lz4", 200, 40_000), (2, "kryo+lz4", 7, 20_000)])
 def test_exchange_host_backend_ranks_share_one_gpu(sgx_lib, oracle_lib, tmp_path, world, codec, R, n):
     run_world(tmp_path, world, "host", codec, R, n)
+
+
+@pytest.mark.parametrize("world,codec,R,n", [(4, "fixed", 4096, 100_000), (2, "fixed", 1024, 100_000),
+                                             (4, "kryo+lz4", 1024, 40_000), (3, "fixed", 5, 5_000)])
+def test_exchange_byte_balanced_placement_zipf(sgx_lib, oracle_lib, tmp_path, world, codec, R, n):
+    """Config C3's skew (Zipf(1.1) keys) with SGX_PLACE_BYTES: every rank's round range is the
+    byte-balanced placement of the all-gathered lengths, and what it fetches and reads back
+    for that range equals the oracle's canonical sequences."""
+    run_world(tmp_path, world, "host", codec, R, n, placement="bytes", keys="zipf")
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])

@@ -3,7 +3,9 @@
 * mod_u32 (sgx_kernels.hip): Granlund-Montgomery round-up multiplier, exact u mod R for
   every 32-bit u and 2 <= R < 2^31 with the parameters of mod_params (sgx_internal.h);
 * KIND_HASH_POW2: Utils.nonNegativeMod(h, R) == h & (R - 1) for power-of-two R
-  (reference: Spark Utils.nonNegativeMod, HashPartitioner.getPartition)."""
+  (reference: Spark Utils.nonNegativeMod, HashPartitioner.getPartition);
+* the exchange's reducer placement (sgx_even_ranges / sgx_balanced_ranges) and the plan
+  over explicit ranges (sgx_plan_exchange_ranges)."""
 import numpy as np
 
 M32 = (1 << 32) - 1
@@ -40,3 +42,62 @@ def test_pow2_hash_identity():
     for R in [1 << b for b in range(0, 14)]:
         want = np.mod(h, R)  # Java nonNegativeMod: ((h % R) + R) % R == floor mod
         assert np.array_equal(h.astype(np.int64) & (R - 1), want)
+
+
+def _best_max_brute(T, P):
+    """Smallest possible largest range total over all placements of P contiguous ranges."""
+    import itertools
+
+    R = len(T)
+    best = None
+    for cuts in itertools.combinations_with_replacement(range(R + 1), P - 1):
+        b = (0,) + cuts + (R,)
+        m = max(sum(T[b[j]:b[j + 1]]) for j in range(P))
+        best = m if best is None else min(best, m)
+    return best
+
+
+def test_balanced_ranges_optimal_and_contiguous(sgx_lib):
+    """sgx_balanced_ranges (byte-balanced reducer placement): contiguous, covering [0, R),
+    and its largest per-rank total equals the brute-force optimum on small cases; uniform
+    lengths give the even split; a round without bytes gets the even placement."""
+    rng = np.random.default_rng(5)
+    for trial in range(150):
+        P = int(rng.integers(1, 5))
+        R = int(rng.integers(1, 9))
+        L = rng.integers(0, 50, size=(P, R)) * (rng.random((P, R)) < 0.7)
+        if trial % 5 == 0:
+            L[:, int(rng.integers(0, R))] += 500  # one hot reducer (Zipf's head)
+        b = sgx_lib.balanced_ranges(L)
+        assert b[0] == 0 and b[-1] == R and np.all(np.diff(b) >= 0), b
+        T = L.sum(axis=0)
+        got = max(int(T[b[j]:b[j + 1]].sum()) for j in range(P))
+        assert got == _best_max_brute(list(map(int, T)), P), (L.tolist(), b)
+    for P, R in ((4, 1024), (8, 4096), (3, 7), (8, 3)):
+        assert np.array_equal(sgx_lib.balanced_ranges(np.ones((P, R), np.int64)),
+                              sgx_lib.balanced_ranges(np.ones((P, R), np.int64)))
+        assert np.array_equal(sgx_lib.balanced_ranges(np.zeros((P, R), np.int64)), sgx_lib.even_ranges(P, R))
+    assert np.array_equal(sgx_lib.balanced_ranges(np.full((4, 1024), 16, np.int64)), sgx_lib.even_ranges(4, 1024))
+    owners = [sgx_lib.reducer_owner(r, 1000, 8) for r in range(1000)]
+    eb = sgx_lib.even_ranges(8, 1000)
+    assert all(eb[owners[r]] <= r < eb[owners[r] + 1] for r in range(1000))
+
+
+def test_plan_with_ranges_is_consistent(sgx_lib):
+    """sgx_plan_exchange_ranges under the byte-balanced placement of Zipf-like lengths: what
+    every rank sends to j is what j expects from it, the receive layout covers j's range,
+    and the largest receive total drops well below the even placement's."""
+    rng = np.random.default_rng(9)
+    P, R = 8, 4096
+    w = 1.0 / np.arange(1, R + 1) ** 1.1
+    L = (rng.poisson(2000 * w[None, :] * R / w.sum() * 8, size=(P, R)) * 16).astype(np.int64)
+    for bounds in (sgx_lib.even_ranges(P, R), sgx_lib.balanced_ranges(L)):
+        plans = [sgx_lib.plan_exchange(L, k, 0, bounds) for k in range(P)]
+        for j in range(P):
+            for k in range(P):
+                assert plans[k][0][j] == plans[j][2][k]  # k sends to j == j receives from k
+            assert plans[j][2].sum() == L[:, bounds[j]:bounds[j + 1]].sum()
+    recv_even = [L[:, a:b].sum() for a, b in zip(sgx_lib.even_ranges(P, R)[:-1], sgx_lib.even_ranges(P, R)[1:])]
+    bb = sgx_lib.balanced_ranges(L)
+    recv_bal = [L[:, a:b].sum() for a, b in zip(bb[:-1], bb[1:])]
+    assert max(recv_bal) < 0.5 * max(recv_even)
