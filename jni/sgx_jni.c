@@ -305,6 +305,21 @@ JNIEXPORT void JNICALL JNI_FN(exchange)(JNIEnv *env, jclass c, jlong e, jint sid
     check(env, sgx_exchange(E(e), sid, mapId));
 }
 
+JNIEXPORT void JNICALL JNI_FN(setReducerPlacement)(JNIEnv *env, jclass c, jlong e, jint sid, jint placement) {
+    (void)c;
+    check(env, sgx_set_reducer_placement(E(e), sid, placement));
+}
+
+/* the executor's reducers [r0, r1) for the exchange round that carried mapId: int[2] */
+JNIEXPORT jintArray JNICALL JNI_FN(roundReducers)(JNIEnv *env, jclass c, jlong e, jint sid, jlong mapId) {
+    (void)c;
+    int32_t r[2] = {0, 0};
+    if (check(env, sgx_round_reducers(E(e), sid, mapId, &r[0], &r[1]))) return NULL;
+    jintArray out = (*env)->NewIntArray(env, 2);
+    if (out) (*env)->SetIntArrayRegion(env, out, 0, 2, (const jint *)r);
+    return out;
+}
+
 /* ---- fetchBlocksByBlockIds: blocks back to back into dst; returns long[n] lengths.  dst null
  *      (or too small) with a SGX_ERR_INVALID is a size query: the lengths are still returned. */
 JNIEXPORT jlongArray JNICALL JNI_FN(fetchBlocks)(JNIEnv *env, jclass c, jlong e, jint sid, jlongArray mapIds,

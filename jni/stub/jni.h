@@ -40,6 +40,7 @@ struct JNINativeInterface_ {
     void (*GetLongArrayRegion)(JNIEnv *env, jlongArray a, jsize start, jsize n, jlong *buf);
     void (*GetIntArrayRegion)(JNIEnv *env, jintArray a, jsize start, jsize n, jint *buf);
     void (*SetIntArrayRegion)(JNIEnv *env, jintArray a, jsize start, jsize n, const jint *buf);
+    jintArray (*NewIntArray)(JNIEnv *env, jsize n);
     jbyteArray (*NewByteArray)(JNIEnv *env, jsize n);
     void (*SetByteArrayRegion)(JNIEnv *env, jbyteArray a, jsize start, jsize n, const jbyte *buf);
     void (*GetByteArrayRegion)(JNIEnv *env, jbyteArray a, jsize start, jsize n, jbyte *buf);

@@ -27,6 +27,7 @@ public final class SgxNative {
   public static final int SER_FIXED = 0, SER_KRYO = 1;
   public static final int CODEC_NONE = 0, CODEC_LZ4 = 1;
   public static final int AGG_GROUP = 0, AGG_SUM = 1;
+  public static final int PLACE_EVEN = 0, PLACE_BYTES = 1;  // sgx_placement
 
   // engine lifetime: CommonUcxShuffleManager.startUcxTransport / stop
   public static native long create(int device, int numChunks, int flags, int commTimeoutMs);
@@ -40,6 +41,10 @@ public final class SgxNative {
   public static native void setSerializer(long e, int shuffleId, int serializer);
   public static native void setCompression(long e, int shuffleId, int codec, int blockSize);
   public static native void setMapSideCombine(long e, int shuffleId, int agg);
+  // reducer placement of the exchange rounds (PLACE_EVEN / PLACE_BYTES) and this executor's
+  // reducer range [r0, r1) of the round that carried mapId
+  public static native void setReducerPlacement(long e, int shuffleId, int placement);
+  public static native int[] roundReducers(long e, int shuffleId, long mapId);
   public static native void unregisterShuffle(long e, int shuffleId);
 
   // getWriter().write(records) + commitAllPartitions(): long[R] partition lengths

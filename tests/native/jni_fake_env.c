@@ -62,6 +62,10 @@ static void get_longs(JNIEnv *env, jlongArray a, jsize s, jsize n, jlong *b) {
     (void)env;
     memcpy(b, (jlong *)((obj *)a)->data + s, (size_t)n * 8);
 }
+static jintArray new_ints(JNIEnv *env, jsize n) {
+    (void)env;
+    return new_obj(K_INTS, n, 4);
+}
 static void get_ints(JNIEnv *env, jintArray a, jsize s, jsize n, jint *b) {
     (void)env;
     memcpy(b, (jint *)((obj *)a)->data + s, (size_t)n * 4);
@@ -94,8 +98,8 @@ static void release_utf(JNIEnv *env, jstring s, const char *p) {
 }
 
 static const struct JNINativeInterface_ g_table = {
-    NULL,      find_class, throw_new, direct_addr, direct_cap, array_len,  new_longs, set_longs,
-    get_longs, get_ints,   set_ints,  new_bytes,   set_bytes,  get_bytes, utf,       release_utf};
+    NULL,      find_class, throw_new, direct_addr, direct_cap, array_len, new_longs, set_longs,
+    get_longs, get_ints,   set_ints,  new_ints,    new_bytes,  set_bytes, get_bytes, utf,      release_utf};
 static JNIEnv g_env = &g_table;
 
 /* natives of jni/sgx_jni.c (declared here: the shim has no header of its own) */
