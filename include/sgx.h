@@ -66,10 +66,8 @@ enum sgx_flags {
     SGX_FLAG_SORT_ALL_DIGITS = 4,     /* sorted reads run every digit pass (no skipping)    */
     SGX_FLAG_DEBUG_SYNC = 8,          /* debugging: synchronise after every kernel and name the
                                          kernel in the error of a device fault (slow)         */
-    SGX_FLAG_LZ4_LANE_DECODE = 16,    /* LZ4 reads decode every compressed frame one lane per
+    SGX_FLAG_LZ4_LANE_DECODE = 16     /* LZ4 reads decode every compressed frame one lane per
                                          frame (default: only from 32768 frames up)           */
-    SGX_FLAG_WIDE_TWO_READ = 32       /* 100 B records: K4 with 4096-record tiles that re-reads
-                                         the records from the caches (k_scatter_wide3)        */
 };
 
 typedef struct sgx_config {

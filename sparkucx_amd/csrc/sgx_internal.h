@@ -68,10 +68,6 @@ ScatterGeom scatter_geom_wide(uint32_t R, int record_bytes);
 // when it does not apply (R > 2048, other widths, LDS).
 constexpr int WIDE2_GEOM_TAG = -2;
 ScatterGeom scatter_geom_wide2(uint32_t R, int record_bytes, int kind, int nb);
-// Wide-record two-read kernel (waves == WIDE3_GEOM_TAG): 4096-record tiles, keys and records
-// read from global memory (the second read from the cache hierarchy)
-constexpr int WIDE3_GEOM_TAG = -3;
-ScatterGeom scatter_geom_wide3(uint32_t R, int record_bytes, int kind, int nb);
 
 // Launchers (all asynchronous on `stream`).  counts / offs are [R][G] partition-major.
 // counts: [R][G] u32, zeroed here unless `zeroed` (the caller's memset covered them).

@@ -1493,185 +1493,6 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
     if (bad) atomicOr(err, SCATTER_OOB);
 }
 
-// ------------------------------------------------------------------------------------
-// K4 for wide records, two reads (k_scatter_wide3): tiles of 4096 records instead of the
-// 1024 that fit in LDS as bytes.  The tile is NOT staged: the ranking reads each record's
-// key (its first 12 bytes) from global memory, and the drain re-reads the records, in
-// sorted order, as 16 B pieces -- the first read pulled their lines into the L2 / the
-// 256 MiB Infinity Cache, so the second is served from there, not HBM.  With 4 records per
-// partition per tile (R = 1024) every partition run is ~400 B long: most of its 128 B lines
-// are whole, where the 1024-record tile leaves ~1 record = 100 B per run, i.e. only partial
-// lines.  LDS: bounds | rows[W][RS] u16 | cur[RS] | dlt[RS] | idx[TR] u32.
-// ------------------------------------------------------------------------------------
-constexpr int WIDE3_TR = 4096;
-
-__host__ __device__ size_t scatter_wide3_lds(uint32_t R, int kind, int nb) {
-    const size_t bsz = kind == SGX_PART_RANGE_BYTES10 ? sizeof(Key10) : 8;
-    return (kind == SGX_PART_HASH ? 0 : al16((size_t)nb * bsz)) + (size_t)8 * rs8(R) * 2 + (size_t)rs8(R) * 8 +
-           (size_t)WIDE3_TR * 4 + 64 * 4;
-}
-
-template <int KIND, int RB>
-__global__ __launch_bounds__(512, 2) void k_scatter_wide3(const uint8_t *__restrict__ in, uint32_t *__restrict__ out,
-                                                          int64_t n, int64_t chunk, PartParams pp,
-                                                          const uint32_t *__restrict__ offs, int G,
-                                                          uint32_t *err) {
-    constexpr int T = 512, W = 8, TR = WIDE3_TR, ITEMS = TR / T;  // 8 records per lane
-    constexpr int DW = RB / 4;                                     // dwords per record
-    constexpr int PC = (RB + 15) / 16;                             // drain pieces per record
-    constexpr int TAILW = (RB % 16) ? (RB % 16) / 4 : 4;           // dwords in the last piece
-    constexpr int DRB = 8;                                         // pieces per lane per batch
-    static_assert(RB % 4 == 0 && RB >= 12, "dword records holding a 12-byte key");
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const uint32_t R = pp.R, RS = rs8(R), NP = RS / 2;
-    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    char *sp = smem;
-    const Key10 *bk10 = (const Key10 *)sp;
-    const int64_t *bi64 = (const int64_t *)sp;
-    if constexpr (KIND == SGX_PART_RANGE_BYTES10) {
-        for (int i = tid; i < pp.nb; i += T) ((Key10 *)sp)[i] = ((const Key10 *)pp.bounds)[i];
-        sp += al16((size_t)pp.nb * sizeof(Key10));
-    } else if constexpr (KIND == SGX_PART_RANGE_I64) {
-        for (int i = tid; i < pp.nb; i += T) ((int64_t *)sp)[i] = ((const int64_t *)pp.bounds)[i];
-        sp += al16((size_t)pp.nb * 8);
-    }
-    uint16_t *rows = (uint16_t *)sp;
-    uint32_t *cur = (uint32_t *)(rows + (size_t)W * RS);
-    uint32_t *dlt = cur + RS;
-    uint32_t *idx = dlt + RS;
-    uint32_t *scratch = idx + TR;
-    uint16_t *myrow = rows + (size_t)w * RS;
-    uint32_t *myrow32 = (uint32_t *)myrow;
-
-    const int g = blockIdx.x;
-    const int64_t begin = (int64_t)g * chunk;
-    const int64_t end = min(n, begin + chunk);
-    const int64_t len = end > begin ? end - begin : 0;
-    const int ntiles = (int)((len + TR - 1) / TR);
-    const int lastn = ntiles > 0 ? (int)(len - (int64_t)(ntiles - 1) * TR) : 0;
-    for (uint32_t p = tid; p < RS; p += T) cur[p] = p < R ? offs[(int64_t)p * G + g] : 0u;
-    for (uint32_t i = tid; i < (uint32_t)W * RS / 2; i += T) ((uint32_t *)rows)[i] = 0u;
-    __syncthreads();
-    uint32_t bad = 0;
-    for (int t = 0; t < ntiles; ++t) {
-        const int nrec = t + 1 < ntiles ? TR : lastn;
-        const uint8_t *tb = in + (begin + (int64_t)t * TR) * RB;
-        // ---- partition ids (the key: first 12 bytes of each record) + rank
-        uint32_t pid[ITEMS], old[ITEMS];
-        bool valid[ITEMS];
-        uint32_t kx[ITEMS], ky[ITEMS], kz[ITEMS];
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const uint32_t r = w * (TR / W) + k * 64 + lane;
-            valid[k] = r < (uint32_t)nrec;
-            const uint32_t *rp = (const uint32_t *)(tb + (size_t)(valid[k] ? r : 0) * RB);
-            kx[k] = rp[0];
-            ky[k] = rp[1];
-            kz[k] = rp[2];
-        }
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) pid[k] = valid[k] ? pid_of_b<KIND>(kx[k], ky[k], kz[k], pp, bi64, bk10) : 0u;
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const uint32_t inc = valid[k] ? 1u << ((pid[k] & 1u) << 4) : 0u;
-            old[k] = __hip_atomic_fetch_add(myrow32 + (pid[k] >> 1), inc, __ATOMIC_RELAXED,
-                                            __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-        lds_barrier();
-        // ---- merge: per partition pair, prefix over the wave rows, block scan
-        constexpr int PPM = 2;  // pairs per thread (R <= 2048)
-        uint32_t before[PPM][W], tot[PPM], S = 0;
-#pragma unroll
-        for (int i = 0; i < PPM; ++i) {
-            const uint32_t j = tid * PPM + i;
-            tot[i] = 0;
-            if (j < NP) {
-#pragma unroll
-                for (int v = 0; v < W; ++v) {
-                    before[i][v] = tot[i];
-                    tot[i] += ((const uint32_t *)(rows + (size_t)v * RS))[j];
-                }
-            }
-            S += (tot[i] & 0xFFFFu) + (tot[i] >> 16);
-        }
-        const uint32_t xs = wave_inclusive_scan(S, lane);
-        if (lane == 63) scratch[w] = xs;
-        lds_barrier();
-        uint32_t base = xs - S;
-        for (uint32_t v = 0; v < w; ++v) base += scratch[v];
-#pragma unroll
-        for (int i = 0; i < PPM; ++i) {
-            const uint32_t j = tid * PPM + i;
-            if (j < NP) {
-                const uint32_t lo = base, hi = base + (tot[i] & 0xFFFFu);
-                base = hi + (tot[i] >> 16);
-                const uint32_t L = lo | (hi << 16);
-#pragma unroll
-                for (int v = 0; v < W; ++v) ((uint32_t *)(rows + (size_t)v * RS))[j] = before[i][v] + L;
-                const uint2 c = ((const uint2 *)cur)[j];
-                ((uint2 *)dlt)[j] = make_uint2(c.x - lo, c.y - hi);
-                ((uint2 *)cur)[j] = make_uint2(c.x + (tot[i] & 0xFFFFu), c.y + (tot[i] >> 16));
-                bad |= (c.x + (tot[i] & 0xFFFFu) > (uint32_t)n || c.y + (tot[i] >> 16) > (uint32_t)n) ? 1u : 0u;
-            }
-        }
-        lds_barrier();
-        // ---- sorted index of the tile: idx[slot] = source record | partition << 16
-#pragma unroll
-        for (int k = 0; k < ITEMS; ++k) {
-            const uint32_t sh = (pid[k] & 1u) << 4;
-            const uint32_t rb16 = myrow[pid[k]];
-            if (valid[k]) idx[rb16 + ((old[k] >> sh) & 0xFFFFu)] = (w * (TR / W) + k * 64 + lane) | (pid[k] << 16);
-        }
-        for (uint32_t i = lane; i < RS / 8; i += 64) ((u32x4 *)myrow)[i] = u32x4{0, 0, 0, 0};
-        lds_barrier();
-        // ---- drain: the sorted tile in 16 B pieces re-read from the cache hierarchy
-        const int units = nrec * PC;
-        for (int u0 = 0; u0 < units; u0 += DRB * T) {
-            u32x4 v[DRB];
-            uint32_t dst[DRB], pc[DRB];
-            bool live[DRB];
-#pragma unroll
-            for (int q = 0; q < DRB; ++q) {
-                const int u = u0 + q * T + (int)tid;
-                live[q] = u < units;
-                const uint32_t uu = live[q] ? (uint32_t)u : 0u;
-                const uint32_t s = uu / PC;
-                pc[q] = uu - s * PC;
-                const uint32_t e = idx[s];
-                const uint32_t *src = (const uint32_t *)(tb + (size_t)(e & 0xFFFFu) * RB) + 4 * pc[q];
-                if (TAILW == 4 || pc[q] + 1 < PC) {
-                    v[q] = *(const u32x4 *)src;
-                } else {
-                    v[q] = u32x4{src[0], TAILW > 1 ? src[1] : 0u, TAILW > 2 ? src[2] : 0u, 0u};
-                }
-                dst[q] = dlt[e >> 16] + s;
-            }
-#pragma unroll
-            for (int q = 0; q < DRB; ++q) {
-                if (live[q] && dst[q] < (uint32_t)n) {
-                    uint32_t *d = out + (uint64_t)dst[q] * DW + 4 * pc[q];
-                    if (TAILW == 4 || pc[q] + 1 < PC) {
-                        *(u32x4 *)d = v[q];
-                    } else {
-                        d[0] = v[q].x;
-                        if (TAILW > 1) d[1] = v[q].y;
-                        if (TAILW > 2) d[2] = v[q].z;
-                    }
-                }
-            }
-        }
-        __syncthreads();  // idx and the rows reused by the next tile
-    }
-    if (bad) atomicOr(err, SCATTER_OOB);
-}
-
-ScatterGeom scatter_geom_wide3(uint32_t R, int rb, int kind, int nb) {
-    if (rb != 100 || rs8(R) / 2 > 2u * 512u) return ScatterGeom{0, 0, 0, 0, 0};
-    const size_t lds = scatter_wide3_lds(R, kind, nb);
-    if (lds > LDS_MAX) return ScatterGeom{0, 0, 0, 0, 0};
-    return ScatterGeom{WIDE3_GEOM_TAG, 8, WIDE3_TR, lds, 0};
-}
-
 ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
     if (rb != 100 || rs8(R) / 2 > 2u * 512u) return ScatterGeom{0, 0, 0, 0, 0};
     const size_t lds = scatter_wide2_lds(R, rb, kind, nb);
@@ -1769,23 +1590,6 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         }
 #undef SGX_SC16_K
 #undef SGX_SC16
-    } else if (rb == 100 && geo.waves == WIDE3_GEOM_TAG) {
-#define SGX_W3(K)                                                                                \
-    do {                                                                                         \
-        (void)hipFuncSetAttribute((const void *)k_scatter_wide3<K, 100>,                        \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
-        hipLaunchKernelGGL((k_scatter_wide3<K, 100>), dim3(G), dim3(512), geo.lds_bytes, stream,  \
-                           (const uint8_t *)in, (uint32_t *)out, n, chunk, pp, offs, G, err);   \
-    } while (0)
-        switch (pp.kind) {
-        case SGX_PART_HASH:
-            if (pow2) SGX_W3(KIND_HASH_POW2); else SGX_W3(SGX_PART_HASH);
-            break;
-        case KIND_DIGIT: SGX_W3(KIND_DIGIT); break;
-        case SGX_PART_RANGE_I64: SGX_W3(SGX_PART_RANGE_I64); break;
-        default: SGX_W3(SGX_PART_RANGE_BYTES10); break;
-        }
-#undef SGX_W3
     } else if (rb == 100 && geo.waves == WIDE2_GEOM_TAG) {
         if (((uintptr_t)in & 15) != 0) return hipErrorInvalidValue;
 #define SGX_W2(K)                                                                                \

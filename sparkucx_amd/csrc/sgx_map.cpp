@@ -46,15 +46,11 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     if (rb != 16 && !(e->flags & SGX_FLAG_NO_WIDE_STAGED) && ((uintptr_t)in & 15) == 0) {
         const ScatterGeom w2 = scatter_geom_wide2((uint32_t)R, rb, kind, spp.nb);
         if (w2.items) geo = w2;
-        if (e->flags & SGX_FLAG_WIDE_TWO_READ) {
-            const ScatterGeom w3 = scatter_geom_wide3((uint32_t)R, rb, kind, spp.nb);
-            if (w3.items) geo = w3;
-        }
     }
     // the reduce side's digit passes run on the write-combining / wide-record kernels only
     if (kind == KIND_DIGIT) {
         if (rb == 16) geo = scatter_geom16_wc((uint32_t)R);
-        if (geo.waves < WC_GEOM_BASE && geo.waves != WIDE2_GEOM_TAG && geo.waves != WIDE3_GEOM_TAG)
+        if (geo.waves < WC_GEOM_BASE && geo.waves != WIDE2_GEOM_TAG)
             return fail_msg(SGX_ERR_UNSUPPORTED, "digit pass on %d B records at this alignment", rb);
     }
     if (geo.items == 0)

@@ -263,14 +263,14 @@ def test_terasort_bytes10(engine, oracle_lib, nb):
     check_against_oracle(engine, oracle_lib, recs, nb + 1, sgx.PART_RANGE_BYTES10, bounds)
 
 
-@pytest.mark.parametrize("wide2", ["1", "0", "two-read"])
+@pytest.mark.parametrize("wide2", ["1", "0"])
 @pytest.mark.parametrize("R", [1, 7, 1000, 2048, 4096])
 @pytest.mark.parametrize("n", [1, 1023, 1024, 5 * 1024 + 77, 3 * 4096 + 1001])
 def test_wide_records_every_path(sgx_lib, oracle_lib, wide2, R, n):
-    """100 B records: the LDS-staged K4 (R <= 2048), the two-read K4 with 4096-record tiles
-    (SGX_FLAG_WIDE_TWO_READ, R <= 2048) and the per-lane kernel (SGX_FLAG_NO_WIDE_STAGED, and
-    R = 4096), hash and range partitioners, partial tiles and several chunks."""
-    flags = {"1": 0, "0": sgx_lib.FLAG_NO_WIDE_STAGED, "two-read": sgx_lib.FLAG_WIDE_TWO_READ}[wide2]
+    """100 B records: the LDS-staged K4 (R <= 2048) and the per-lane kernel
+    (SGX_FLAG_NO_WIDE_STAGED, and R = 4096), hash and range partitioners, partial tiles and
+    several chunks."""
+    flags = 0 if wide2 == "1" else sgx_lib.FLAG_NO_WIDE_STAGED
     recs = oracle_lib.gen_terasort100(n, R + n)
     with sgx_lib.ShuffleEngine(device=0, num_chunks=3, flags=flags) as e:
         check_against_oracle(e, oracle_lib, recs, R)
