@@ -147,6 +147,15 @@ def test_exchange_host_backend_ranks_share_one_gpu(sgx_lib, oracle_lib, tmp_path
     run_world(tmp_path, world, "host", codec, R, n)
 
 
+@pytest.mark.parametrize("placement", ["even", "bytes"])
+def test_exchange_eight_ranks_share_one_gpu(sgx_lib, oracle_lib, tmp_path, placement):
+    """C2's rank count (P = 8) through the product's exchange, 8 executors sharing cuda:0 over
+    the host backend: every rank's fetched blocks, decoded / sorted / summed reads of its
+    reducer range equal the oracle's canonical sequences, with both reducer placements."""
+    run_world(tmp_path, 8, "host", "fixed", 1024, 250_000, placement=placement,
+              keys="zipf" if placement == "bytes" else "uniform")
+
+
 @pytest.mark.parametrize("world,codec,R,n", [(4, "fixed", 4096, 100_000), (2, "fixed", 1024, 100_000),
                                              (4, "kryo+lz4", 1024, 40_000), (3, "fixed", 5, 5_000)])
 def test_exchange_byte_balanced_placement_zipf(sgx_lib, oracle_lib, tmp_path, world, codec, R, n):
