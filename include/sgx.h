@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SGX_ABI_VERSION 3
+#define SGX_ABI_VERSION 4
 
 enum sgx_status {
     SGX_OK = 0,
