@@ -655,3 +655,28 @@ def test_memory_pool_size_classes_and_reuse(sgx_lib, oracle_lib):
         mb.close()
     finally:
         mgr.stop()
+
+
+@pytest.mark.parametrize("workload", ["c3", "c4"])
+def test_bench_other_workloads_json_line(workload):
+    """bench.py --workload c3 | c4 at a small size: one JSON line with the contract's keys,
+    the verified lengths, and the workload's record width and partition count."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--workload", workload, "--records", str(1 << 20),
+           "--steps", "2", "--warmup", "1", "--no-cpu-baseline"]
+    p = subprocess.run(cmd, cwd=root, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "ms_per_step", "roofline", "roofline_map_side", "config"):
+        assert k in d, k
+    assert d["verified_lengths_sum"] is True and d["value"] > 0
+    assert d["config"]["record_bytes"] == (100 if workload == "c4" else 16)
+    assert d["config"]["partitions"] == (4096 if workload == "c3" else 1024)
+    assert d["roofline"]["algo_bytes_per_record"] == 2 * d["config"]["record_bytes"]
