@@ -254,8 +254,10 @@ typedef struct sgx_host_comm {
 } sgx_host_comm;
 int sgx_comm_init_host(sgx_engine *e, int32_t nranks, int32_t rank, const sgx_host_comm *comm);
 int sgx_comm_size(sgx_engine *e, int32_t *nranks, int32_t *rank);
-/* Push map `map_id` of `shuffle_id` to the reducer owners (reducer r lives on rank
- * floor(r*P/R)); every rank calls it collectively with its own map.  Asynchronous on the
+/* Push map `map_id` of `shuffle_id` to the reducer owners (contiguous reducer ranges: the
+ * shuffle's placement, sgx_set_reducer_placement -- by default reducer r lives on rank
+ * floor(r*P/R); sgx_round_reducers reports the range); every rank calls it collectively
+ * with its own map.  Asynchronous on the
  * engine's exchange stream; completes at sgx_sync.  Received blocks stay in the
  * all-to-all's receive layout ([source rank][reducer]); sgx_fetch_blocks gathers them in
  * the order asked for (reducer-major, map-minor gives the canonical per-reducer sequence). */
