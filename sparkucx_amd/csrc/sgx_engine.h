@@ -30,7 +30,18 @@
 #include "../../include/sgx.h"
 #include "sgx_internal.h"
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 namespace sgx {
+// roctx range around a C-ABI call (SURVEY §5 tracing): `rocprofv3 --marker-trace` shows the
+// engine's calls beside the kernels they launch; a no-op when no tool is attached.
+struct TraceRange {
+    explicit TraceRange(const char *name) { roctxRangePushA(name); }
+    ~TraceRange() { roctxRangePop(); }
+    TraceRange(const TraceRange &) = delete;
+    TraceRange &operator=(const TraceRange &) = delete;
+};
+
 
 #define HIP_TRY(expr)                                                                          \
     do {                                                                                       \

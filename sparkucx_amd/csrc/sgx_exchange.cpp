@@ -99,6 +99,7 @@ int sgx::comm_wait(sgx_engine *e) {
 }
 
 extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
+    sgx::TraceRange trace_("sgx_exchange");
     if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     HIP_TRY(hipSetDevice(e->device));

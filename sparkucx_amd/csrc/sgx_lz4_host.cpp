@@ -110,6 +110,7 @@ int sgx::lz4_frame_impl(sgx_engine *e, Ctx &c, const void *stream_dev, const int
 extern "C" int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, const int64_t *part_offsets,
                                         int32_t num_partitions, int32_t block_size, void *dst_dev,
                                         int64_t dst_cap, int64_t *out_lengths) {
+    sgx::TraceRange trace_("sgx_lz4_frame_partitions");
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     HIP_TRY(hipSetDevice(e->device));
     Ctx *c = e->ctx();
@@ -121,6 +122,7 @@ extern "C" int sgx_lz4_frame_partitions(sgx_engine *e, const void *stream_dev, c
 // LZ4BlockInputStream on the reduce side: decompress fetched LZ4-framed partition streams
 extern "C" int sgx_lz4_unframe(sgx_engine *e, const void *framed_dev, int64_t framed_bytes, void *dst_dev,
                                int64_t dst_cap, int64_t *out_bytes) {
+    sgx::TraceRange trace_("sgx_lz4_unframe");
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     HIP_TRY(hipSetDevice(e->device));
     Ctx *c = e->ctx();
@@ -207,6 +209,7 @@ static int walk_single(sgx_engine *e, Ctx &c, const uint8_t *framed, int64_t fra
 
 extern "C" int sgx_lz4_unframe_streams(sgx_engine *e, const void *framed_dev, const int64_t *stream_lens,
                                        int64_t nstreams, void *dst_dev, int64_t dst_cap, int64_t *out_bytes) {
+    sgx::TraceRange trace_("sgx_lz4_unframe_streams");
     if (!e || nstreams < 0 || (nstreams > 0 && !stream_lens)) return fail_msg(SGX_ERR_INVALID, "bad arguments");
     HIP_TRY(hipSetDevice(e->device));
     Ctx *c = e->ctx();

@@ -283,6 +283,7 @@ static int device_input(Ctx &c, const void *records, int64_t bytes, int32_t mem_
 
 extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records,
                              int64_t n, int32_t rb, int32_t mem_kind, int64_t *out_lengths) {
+    sgx::TraceRange trace_("sgx_write_map");
     if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
@@ -338,6 +339,7 @@ extern "C" int sgx_map_begin(sgx_engine *e, int32_t shuffle_id, int64_t map_id) 
 
 extern "C" int sgx_map_append(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records, int64_t n,
                               int32_t rb, int32_t mem_kind) {
+    sgx::TraceRange trace_("sgx_map_append");
     if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     std::shared_ptr<Shuffle> s;
@@ -368,6 +370,7 @@ extern "C" int sgx_map_append(sgx_engine *e, int32_t shuffle_id, int64_t map_id,
 }
 
 extern "C" int sgx_map_commit(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *out_lengths) {
+    sgx::TraceRange trace_("sgx_map_commit");
     if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
     std::shared_ptr<Shuffle> s;
@@ -469,6 +472,7 @@ extern "C" int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, v
 // ------------------------------------------------------------------------------------
 extern "C" int sgx_write_index(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const char *index_path,
                                const char *data_path, int64_t *out_lengths) {
+    sgx::TraceRange trace_("sgx_write_index");
     if (!e || !index_path || !data_path) return fail_msg(SGX_ERR_INVALID, "NULL argument");
     std::shared_ptr<Shuffle> s;
     std::shared_ptr<MapOut> m;

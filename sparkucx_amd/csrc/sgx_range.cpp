@@ -102,6 +102,7 @@ struct Cand {
 extern "C" int sgx_range_bounds(sgx_engine *e, const void *const *batches, const int64_t *nrecords, int32_t nbatches,
                                 int32_t rb, int32_t mem_kind, int32_t num_partitions, int32_t rdd_id,
                                 int32_t sample_points_per_partition, void *out_bounds, int32_t *out_nbounds) {
+    sgx::TraceRange trace_("sgx_range_bounds");
     if (!e || !out_nbounds || (nbatches > 0 && (!batches || !nrecords))) return fail_msg(SGX_ERR_INVALID, "NULL argument");
     if (rb != 16 && rb != 100) return fail_msg(SGX_ERR_UNSUPPORTED, "range bounds need 16 B or 100 B records, not %d", rb);
     if (mem_kind != SGX_MEM_HOST && mem_kind != SGX_MEM_DEVICE) return fail_msg(SGX_ERR_INVALID, "unknown mem_kind");

@@ -140,6 +140,7 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
 extern "C" int sgx_fetch_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids,
                                 const int32_t *reduce_ids, int64_t n, void *dst, int64_t dst_cap,
                                 int32_t dst_mem_kind, int64_t *out_lengths) {
+    sgx::TraceRange trace_("sgx_fetch_blocks");
     if (!e || (n > 0 && (!map_ids || !reduce_ids || !out_lengths))) return fail_msg(SGX_ERR_INVALID, "NULL argument");
     std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
     if (!s) return SGX_ERR_STATE;
@@ -412,6 +413,7 @@ static int read_entry(sgx_engine *e, int32_t shuffle_id, int32_t mem_kind, std::
 extern "C" int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
                                int32_t start_partition, int32_t end_partition, void *dst, int64_t dst_cap,
                                int32_t dst_mem_kind, int64_t *out_bytes) {
+    sgx::TraceRange trace_("sgx_read_sorted");
     if (!e || !out_bytes) return fail_msg(SGX_ERR_INVALID, "NULL argument");
     std::shared_ptr<Shuffle> s;
     Ctx *c = nullptr;
@@ -466,6 +468,7 @@ extern "C" int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t 
 extern "C" int sgx_read_records(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
                                 int32_t start_partition, int32_t end_partition, void *dst, int64_t dst_cap,
                                 int32_t dst_mem_kind, int64_t *out_bytes) {
+    sgx::TraceRange trace_("sgx_read_records");
     if (!e || !out_bytes) return fail_msg(SGX_ERR_INVALID, "NULL argument");
     std::shared_ptr<Shuffle> s;
     Ctx *c = nullptr;
@@ -496,6 +499,7 @@ extern "C" int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t
                                 int32_t start_partition, int32_t end_partition, int32_t agg, int64_t *keys,
                                 int64_t *group_starts, int64_t *values, int64_t cap_groups, int64_t cap_values,
                                 int32_t mem_kind, int64_t *out_groups, int64_t *out_values) {
+    sgx::TraceRange trace_("sgx_read_grouped");
     if (!e || !out_groups || !out_values) return fail_msg(SGX_ERR_INVALID, "NULL argument");
     if (agg != SGX_AGG_GROUP && agg != SGX_AGG_SUM) return fail_msg(SGX_ERR_INVALID, "unknown aggregation %d", agg);
     std::shared_ptr<Shuffle> s;
