@@ -134,3 +134,34 @@ def test_multithreaded_equals_single_threaded(oracle_lib):
         for p in range(0, R, max(1, R // 17)):
             run = vals[o[p]:o[p + 1]]
             assert np.all(np.diff(run) > 0)
+
+
+def test_range_partitioner_matches_bisect_on_distinct_bounds(oracle_lib):
+    """RangePartitioner.getPartition (linear scan up to 128 bounds, Arrays.binarySearch above)
+    returns, for Spark's distinct sorted bounds, the first bound >= key -- Python's
+    bisect_left, an implementation outside this repository; descending order mirrors it.
+    Long keys (signed order) and TeraSort's 10-byte keys (unsigned lexicographic order),
+    with exact hits on bounds.  (Duplicate bounds, where the JDK's probe order decides, stay
+    pinned by the restatement only.)"""
+    import bisect
+
+    rng = np.random.default_rng(17)
+    for nb in (1, 7, 128, 129, 1023):
+        b = np.unique(rng.integers(-(2**62), 2**62, nb * 2))[:nb].astype(np.int64)
+        keys = np.concatenate([rng.integers(-(2**63), 2**63 - 1, 3000, dtype=np.int64), b, b + 1, b - 1])
+        recs = np.zeros((len(keys), 16), np.uint8)
+        recs[:, :8] = keys.view(np.uint8).reshape(-1, 8)
+        for asc in (True, False):
+            got = oracle_lib.partition_ids(recs, nb + 1, oracle_lib.PART_RANGE_I64, b, asc)
+            want = np.array([bisect.bisect_left(b.tolist(), int(k)) for k in keys])
+            assert np.array_equal(got, want if asc else nb - want), (nb, asc)
+    for nb in (5, 128, 300):
+        raw = rng.integers(0, 256, size=(nb * 3, 10), dtype=np.uint8)
+        bl = sorted({bytes(r) for r in raw})[:nb]
+        b10 = np.frombuffer(b"".join(bl), np.uint8).reshape(-1, 10)
+        recs = oracle_lib.gen_terasort100(4000, nb)
+        recs[:nb, :10] = b10  # exact hits
+        for asc in (True, False):
+            got = oracle_lib.partition_ids(recs, len(bl) + 1, oracle_lib.PART_RANGE_BYTES10, b10, asc)
+            want = np.array([bisect.bisect_left(bl, bytes(r[:10])) for r in recs])
+            assert np.array_equal(got, want if asc else len(bl) - want), (nb, asc)
