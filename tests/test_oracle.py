@@ -165,3 +165,24 @@ def test_range_partitioner_matches_bisect_on_distinct_bounds(oracle_lib):
             got = oracle_lib.partition_ids(recs, len(bl) + 1, oracle_lib.PART_RANGE_BYTES10, b10, asc)
             want = np.array([bisect.bisect_left(bl, bytes(r[:10])) for r in recs])
             assert np.array_equal(got, want if asc else len(bl) - want), (nb, asc)
+
+
+def test_stable_group_by_partition_matches_numpy_stable_sort(oracle_lib):
+    """a4's stable group-by-partition (ExternalSorter / ShuffleInMemorySorter: partition-
+    contiguous, map input order inside a partition) equals numpy's stable argsort of the
+    partition ids -- an independent stable sort -- for hash and range partitioners, with and
+    without threads; counts equal numpy's bincount."""
+    rng = np.random.default_rng(23)
+    for n, R in ((1, 1), (1000, 3), (50_000, 200), (200_003, 1024)):
+        recs = oracle_lib.gen_uniform16(n, 900 + R)
+        recs[: n // 3, :8] = recs[: 1, :8]  # many equal keys: order must come from the input
+        for nt in (1, 4):
+            out, counts = oracle_lib.map_write(recs, R, nthreads=nt)
+            pids = oracle_lib.partition_ids(recs, R)
+            order = np.argsort(pids, kind="stable")
+            assert np.array_equal(out, recs[order]) and np.array_equal(counts, np.bincount(pids, minlength=R))
+    b = np.sort(rng.integers(-(2**62), 2**62, 99)).astype(np.int64)
+    recs = oracle_lib.gen_uniform16(30_000, 5)
+    out, counts = oracle_lib.map_write(recs, 100, oracle_lib.PART_RANGE_I64, b)
+    pids = oracle_lib.partition_ids(recs, 100, oracle_lib.PART_RANGE_I64, b)
+    assert np.array_equal(out, recs[np.argsort(pids, kind="stable")])
