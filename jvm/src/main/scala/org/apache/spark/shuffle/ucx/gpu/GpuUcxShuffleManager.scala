@@ -49,6 +49,11 @@ class GpuUcxShuffleManager(conf: SparkConf, isDriver: Boolean) extends SortShuff
                                    conf.getSizeAsBytes("spark.io.compression.lz4.blockSize", "32k").toInt)
       }
       if (dependency.mapSideCombine) SgxNative.setMapSideCombine(engine, shuffleId, SgxNative.AGG_SUM)
+      // reducer placement of the exchange rounds: "even" (floor(r*P/R)) or "bytes" (ranges
+      // balanced on the round's lengths, for skewed keys); the executor's range of a round
+      // comes back from SgxNative.roundReducers for the scheduler's locality preferences
+      if (conf.get("spark.shuffle.ucx.gpu.reducerPlacement", "even") == "bytes")
+        SgxNative.setReducerPlacement(engine, shuffleId, SgxNative.PLACE_BYTES)
       onGpu.put(shuffleId, true)
     }
     handle
