@@ -137,6 +137,41 @@ __device__ __forceinline__ int lane_value(int v, int l) { return __builtin_amdgc
 //  * LZ4_count: 64 4-byte comparisons per round, the first differing byte from a ballot.
 //  * the backward catch-up: 64 byte comparisons per round.
 //  * literal and length-run bytes: lane-parallel stores.
+// The wave is latency-bound, so loads whose addresses are known early go out
+// together: the catch-up's and LZ4_count's first rounds (the catch-up never moves the match
+// end), a _next_match candidate's 4-byte test and its first count round, and the next
+// search's first 64 sequences with the _next_match test.  (Loading each search batch's
+// successor with the batch measured 2-3% slower: DESIGN §14.)  Only loads move; every table
+// access and every decision stays in the serial order.
+// LZ4_count's end: the first a' >= a with src[a'] != src[a' + d0], or mlimit.  (d, full) is
+// the first round's comparison at a + 4 * lane, issued by the caller.
+__device__ __forceinline__ int lz4_count_end(const uint8_t *src, int a, int d0, int mlimit, uint32_t d, bool full) {
+    const int lane = (int)(threadIdx.x & 63);
+    for (;;) {
+        const uint64_t dm = __ballot(d != 0);
+        if (dm) {
+            const int k = (int)__builtin_ctzll(dm);
+            return a + 4 * k + ((int)__builtin_ctz((uint32_t)lane_value((int)d, k)) >> 3);
+        }
+        const int nfull = __popcll(__ballot(full));
+        a += 4 * nfull;
+        if (nfull < 64) {  // < 4 bytes before matchlimit: byte-wise
+            while (a < mlimit && src[a] == src[a + d0]) ++a;
+            return a;
+        }
+        const int al = a + 4 * lane;
+        full = al + 4 <= mlimit;
+        d = full ? g32(src + al) ^ g32(src + al + d0) : 0u;
+    }
+}
+
+// The search's first batch of sequences from `start` (iteration lane); loaded ahead of the
+// table work that precedes the search, which they do not depend on.
+__device__ __forceinline__ uint32_t search_seq(const uint8_t *src, int start, int it, int n) {
+    const int lane = (int)(threadIdx.x & 63);
+    return g32(src + min(start + skip_dist(it + lane), n - 4));  // (invalid lanes: any bytes)
+}
+
 __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uint8_t *out, int cap) {
     const int lane = (int)(threadIdx.x & 63);
     const uint64_t below = (1ull << lane) - 1ull;
@@ -146,6 +181,7 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
         const int mlimit = n - kLastLiterals;  // matchlimit
         if (lane == 0) table[hash4(g32(src))] = 0;
         int ip = 1;
+        uint32_t seq0 = search_seq(src, ip, 0, n);
         for (;;) {
             // ---- match search from ip (step 1, search counter 64)
             const int start = ip;
@@ -155,7 +191,7 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
                 const int pos = start + skip_dist(it + lane);
                 const int nxt = start + skip_dist(it + lane + 1);  // the position after this one
                 const bool valid = nxt <= lim;
-                const uint32_t seq = g32(src + min(pos, n - 4));  // (invalid lanes: any bytes)
+                const uint32_t seq = it == 0 ? seq0 : search_seq(src, start, it, n);
                 const uint32_t h = hash4(seq);
                 int cand = table[h];
                 uint64_t peers = ~0ull;  // lanes probing the same hash
@@ -187,14 +223,23 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
                 it += 64;
             }
             if (!found) break;
-            // ---- catch up backwards
-            for (;;) {
-                const int a = ip - 1 - lane, b = match - 1 - lane;
-                const bool eq = a >= anchor && b >= 0 && src[a] == src[b];
-                const int back = first_clear(__ballot(eq));
-                ip -= back;
-                match -= back;
-                if (back < 64) break;
+            // ---- catch up backwards, and LZ4_count from ip + 4 in the same round trip: the
+            // bytes the catch-up adds before ip match, so the match end does not move
+            int aend;
+            {
+                const int d0 = match - ip, a0 = ip + kMinMatch;
+                const int al = a0 + 4 * lane;
+                const bool full = al + 4 <= mlimit;
+                const uint32_t d = full ? g32(src + al) ^ g32(src + al + d0) : 0u;
+                for (;;) {
+                    const int a = ip - 1 - lane, b = match - 1 - lane;
+                    const bool eq = a >= anchor && b >= 0 && src[a] == src[b];
+                    const int back = first_clear(__ballot(eq));
+                    ip -= back;
+                    match -= back;
+                    if (back < 64) break;
+                }
+                aend = lz4_count_end(src, a0, d0, mlimit, d, full);
             }
             // ---- literals
             const int lit = ip - anchor;
@@ -218,29 +263,11 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
                     out[op + 1] = (uint8_t)(off >> 8);
                 }
                 op += 2;
-                // LZ4_count from ip + 4 / match + 4 up to matchlimit
-                int a = ip + kMinMatch;
-                const int d0 = match - ip;  // b = a + d0
-                for (;;) {
-                    const int al = a + 4 * lane;
-                    const bool full = al + 4 <= mlimit;
-                    const uint32_t d = full ? g32(src + al) ^ g32(src + al + d0) : 0u;
-                    const uint64_t dm = __ballot(d != 0);
-                    if (dm) {
-                        const int k = (int)__builtin_ctzll(dm);
-                        a += 4 * k + ((int)__builtin_ctz((uint32_t)lane_value((int)d, k)) >> 3);
-                        break;
-                    }
-                    const int nfull = __popcll(__ballot(full));
-                    a += 4 * nfull;
-                    if (nfull < 64) {  // < 4 bytes before matchlimit: byte-wise
-                        while (a < mlimit && src[a] == src[a + d0]) ++a;
-                        break;
-                    }
-                }
-                uint32_t mc = (uint32_t)(a - (ip + kMinMatch));
+                // LZ4_count from ip + 4 / match + 4 up to matchlimit (for the search's match:
+                // counted above with the catch-up)
+                uint32_t mc = (uint32_t)(aend - (ip + kMinMatch));
                 if (op + (int)(mc / 255) + 1 + 3 > cap) return -1;  // run bytes + the next token, offset
-                ip = a;
+                ip = aend;
                 if (mc >= 15) {
                     tk += 15;
                     mc -= 15;
@@ -253,16 +280,24 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
                 if (lane == 0) out[token] = (uint8_t)tk;
                 anchor = ip;
                 if (ip >= lim) goto last_literals;
-                if (lane == 0) table[hash4(g32(src + ip - 2))] = (uint16_t)(ip - 2);
+                // the next search's first sequences load with this test's (unused on a hit)
+                seq0 = search_seq(src, ip + 1, 0, n);
+                const uint32_t s2 = g32(src + ip - 2), s0 = g32(src + ip);
+                if (lane == 0) table[hash4(s2)] = (uint16_t)(ip - 2);
                 __builtin_amdgcn_wave_barrier();  // the write above, then the read below
-                const uint32_t h = hash4(g32(src + ip));
+                const uint32_t h = hash4(s0);
                 const int m2 = table[h];
                 __builtin_amdgcn_wave_barrier();
                 if (lane == 0) table[h] = (uint16_t)ip;
-                if (g32(src + m2) != g32(src + ip)) break;
+                // a candidate's LZ4_count round loads with its test (m2 < ip: in bounds)
+                const int d0 = m2 - ip, al = ip + kMinMatch + 4 * lane;
+                const bool full = al + 4 <= mlimit;
+                const uint32_t d = full ? g32(src + al) ^ g32(src + al + d0) : 0u;
+                if (g32(src + m2) != s0) break;
                 match = m2;
                 token = op++;
                 tk = 0;
+                aend = lz4_count_end(src, ip + kMinMatch, d0, mlimit, d, full);  // no catch-up: ip is the anchor
             }
             ++ip;
         }
