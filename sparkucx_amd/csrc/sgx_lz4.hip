@@ -45,13 +45,12 @@ __device__ __forceinline__ uint32_t lds32(const uint8_t *p) {
     const uint32_t *w = (const uint32_t *)(p - sh);
     return __builtin_amdgcn_alignbyte(w[1], w[0], sh);
 }
-// unaligned little-endian 32-bit read of global bytes p[0..3]: the aligned dword holding p[0]
-// and (only when p is unaligned) the next one, which still holds p[3] -- nothing past p[3]'s
-// dword is touched
+// unaligned little-endian 32-bit read of global bytes p[0..3]: one global_load_dword (gfx950
+// serves unaligned dword loads; nothing outside p[0..3] is read)
 __device__ __forceinline__ uint32_t g32(const uint8_t *p) {
-    const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
-    const uint32_t *w = (const uint32_t *)(p - sh);
-    return __builtin_amdgcn_alignbyte(w[sh ? 1 : 0], w[0], sh);
+    uint32_t v;
+    __builtin_memcpy(&v, p, 4);
+    return v;
 }
 __device__ __forceinline__ uint32_t hash4(uint32_t seq) { return (seq * 2654435761u) >> (32 - kHashLog); }
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
@@ -194,13 +193,17 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
                 const uint32_t seq = it == 0 ? seq0 : search_seq(src, start, it, n);
                 const uint32_t h = hash4(seq);
                 int cand = table[h];
-                uint64_t peers = ~0ull;  // lanes probing the same hash
+                // lanes probing the same hash: those whose ballot bits agree with ours on all
+                // hash bits (diff: the lanes that differ on some bit)
+                uint32_t diff_lo = 0, diff_hi = 0;
 #pragma unroll
                 for (int bt = 0; bt < kHashLog; ++bt) {
-                    const bool bit = (h >> bt) & 1u;
-                    const uint64_t m = __ballot(bit);
-                    peers &= bit ? m : ~m;
+                    const uint32_t sx = (uint32_t)((int32_t)(h << (31 - bt)) >> 31);  // 0 or ~0
+                    const uint64_t m = __ballot(sx != 0);
+                    diff_lo |= (uint32_t)m ^ sx;
+                    diff_hi |= (uint32_t)(m >> 32) ^ sx;
                 }
+                const uint64_t peers = ~(((uint64_t)diff_hi << 32) | diff_lo);
                 const uint64_t lower = peers & below;
                 if (lower) cand = start + skip_dist(it + 63 - (int)__builtin_clzll(lower));
                 const bool hit = valid && g32(src + cand) == seq;
