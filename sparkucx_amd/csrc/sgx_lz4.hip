@@ -729,25 +729,21 @@ __device__ uint32_t xxh32_global(const uint8_t *p, int len, uint32_t seed) {
     return h;
 }
 
-// d and s may overlap (a match copy): each 8-byte chunk is read before it is written
+// d and s may overlap (a match copy): each 8-byte chunk is read before it is written (one
+// unaligned global_load_dwordx2 / global_store_dwordx2 per chunk)
 __device__ __forceinline__ void copy8_chunks(uint8_t *d, const uint8_t *s, uint32_t len) {
     uint32_t i = 0;
     for (; i + 8 <= len; i += 8) {
-        uint8_t b[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) b[k] = s[i + k];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) d[i + k] = b[k];
+        uint64_t v;
+        __builtin_memcpy(&v, s + i, 8);
+        __builtin_memcpy(d + i, &v, 8);
     }
-    if (i < len) {
-        uint8_t b[8];
-        const uint32_t r = len - i;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) b[k] = (uint32_t)k < r ? s[i + k] : (uint8_t)0;
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            if ((uint32_t)k < r) d[i + k] = b[k];
+    if (i + 4 <= len) {
+        const uint32_t w = g32(s + i);
+        __builtin_memcpy(d + i, &w, 4);
+        i += 4;
     }
+    for (; i < len; ++i) d[i] = s[i];
 }
 __global__ __launch_bounds__(64) void k_lz4_decode_lanes(const uint8_t *__restrict__ in,
                                                          const int64_t *__restrict__ desc, int64_t nframes,
@@ -777,17 +773,23 @@ __global__ __launch_bounds__(64) void k_lz4_decode_lanes(const uint8_t *__restri
         if (off == 0 || off > op || op + ml > olen) { bad = 1; break; }
         if (off >= 8) copy8_chunks(o + op, o + op - off, ml);
         else {
+            // the match repeats with period off, so also with period p = the first multiple of
+            // off >= 8: bytes [0, p) from the period held in registers, the rest as chunks
+            // from p bytes back
+            const uint32_t p = off * ((8u + off - 1u) / off);
+            const uint32_t head = ml < p ? ml : p;
             uint8_t pat[8];
 #pragma unroll
             for (int k = 0; k < 8; ++k) pat[k] = (uint32_t)k < off ? o[op - off + k] : (uint8_t)0;
             uint32_t m = 0;
-            for (uint32_t i = 0; i < ml; ++i) {
+            for (uint32_t i = 0; i < head; ++i) {
                 uint8_t v = pat[0];
 #pragma unroll
                 for (int k = 1; k < 8; ++k) v = (uint32_t)k == m ? pat[k] : v;
                 o[op + i] = v;
                 m = m + 1 == off ? 0u : m + 1;
             }
+            if (ml > p) copy8_chunks(o + op + p, o + op, ml - p);
         }
         op += ml;
     }
