@@ -109,7 +109,7 @@ __device__ uint32_t xxh32_lds_window(const uint8_t *base, int sh, int len, uint3
 // skip_dist(m) = 1 + G(62 + m) for m >= 1.
 __device__ __forceinline__ int skip_dist(int m) {
     const int x = 62 + m, q = x >> 6, r = x & 63;
-    return m == 0 ? 0 : 1 + 32 * q * (q - 1) + q * (r + 1);
+    return (1 + 32 * q * (q - 1) + q * (r + 1)) & -(int)(m != 0);  // (a mask, not a branch)
 }
 __device__ __forceinline__ int first_clear(uint64_t m) { return m == ~0ull ? 64 : (int)__builtin_ctzll(~m); }
 __device__ __forceinline__ int lane_value(int v, int l) { return __builtin_amdgcn_readlane(v, l); }
@@ -188,7 +188,7 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
             bool found = false;
             for (;;) {
                 const int pos = start + skip_dist(it + lane);
-                const int nxt = start + skip_dist(it + lane + 1);  // the position after this one
+                const int nxt = pos + max((it + lane + 63) >> 6, 1);  // the position after this one
                 const bool valid = nxt <= lim;
                 const uint32_t seq = it == 0 ? seq0 : search_seq(src, start, it, n);
                 const uint32_t h = hash4(seq);
@@ -206,7 +206,8 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
                 const uint64_t peers = ~(((uint64_t)diff_hi << 32) | diff_lo);
                 const uint64_t lower = peers & below;
                 if (lower) cand = start + skip_dist(it + 63 - (int)__builtin_clzll(lower));
-                const bool hit = valid && g32(src + cand) == seq;
+                // (a valid lane's candidate is in the block: a lower peer of a valid lane is valid)
+                const bool hit = g32(src + min(cand, n - 4)) == seq && valid;
                 const uint64_t vm = __ballot(valid), hm = __ballot(hit);
                 const int kinv = first_clear(vm);
                 const int khit = hm ? (int)__builtin_ctzll(hm) : 64;
