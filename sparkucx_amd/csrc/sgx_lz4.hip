@@ -186,11 +186,15 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
             const int start = ip;
             int it = 0, match = 0;
             bool found = false;
+            uint32_t seq = seq0;
             for (;;) {
                 const int pos = start + skip_dist(it + lane);
                 const int nxt = pos + max((it + lane + 63) >> 6, 1);  // the position after this one
                 const bool valid = nxt <= lim;
-                const uint32_t seq = it == 0 ? seq0 : search_seq(src, start, it, n);
+                // past the first batch a search tends to run on: the next batch's sequences
+                // load with this one's
+                uint32_t seqn = 0;
+                if (it > 0) seqn = search_seq(src, start, it + 64, n);
                 const uint32_t h = hash4(seq);
                 int cand = table[h];
                 // lanes probing the same hash: those whose ballot bits agree with ours on all
@@ -224,6 +228,7 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
                     break;
                 }
                 if (kinv < 64) break;  // next position past mflimit: no match in this block
+                seq = it == 0 ? search_seq(src, start, 64, n) : seqn;
                 it += 64;
             }
             if (!found) break;
@@ -237,7 +242,7 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
                 const uint32_t d = full ? g32(src + al) ^ g32(src + al + d0) : 0u;
                 for (;;) {
                     const int a = ip - 1 - lane, b = match - 1 - lane;
-                    const bool eq = a >= anchor && b >= 0 && src[a] == src[b];
+                    const bool eq = (src[max(a, 0)] == src[max(b, 0)]) && a >= anchor && b >= 0;  // (loads unconditional)
                     const int back = first_clear(__ballot(eq));
                     ip -= back;
                     match -= back;
@@ -347,7 +352,7 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
                                                    int level, uint8_t *__restrict__ slots,
                                                    int64_t slot_bytes, int32_t *__restrict__ sizes,
                                                    int64_t *__restrict__ err) {
-    __shared__ uint16_t s_tab[kTable];
+    __shared__ __attribute__((aligned(16))) uint16_t s_tab[kTable];
     static_assert(kLanes == 1, "one block per workgroup");
     const int lane = threadIdx.x;
     const int64_t b = blockIdx.x;
@@ -362,7 +367,7 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
         }
         return;
     }
-    for (int i = lane; i < kTable / 2; i += 64) ((uint32_t *)s_tab)[i] = 0u;
+    for (int i = lane; i < kTable / 8; i += 64) ((uint4 *)s_tab)[i] = make_uint4(0u, 0u, 0u, 0u);
     __syncthreads();
     const int n = (int)blen;
     const uint8_t *src = stream + boff;
