@@ -576,8 +576,7 @@ constexpr int kInplace = kMaxBlock + (kMaxBlock >> 8) + 32;
 // writes the block out with dword stores.  Errors: atomicOr into *err.
 __global__ __launch_bounds__(64) void k_lz4_decode(const uint8_t *__restrict__ in,
                                                    const int64_t *__restrict__ desc, int64_t nframes,
-                                                   uint8_t *__restrict__ out, uint32_t *__restrict__ err,
-                                                   int skip_compressed) {
+                                                   uint8_t *__restrict__ out, uint32_t *__restrict__ err) {
     __shared__ __attribute__((aligned(16))) uint8_t s_buf[kInplace + 48];
     __shared__ int s_bad;
     const int64_t f = blockIdx.x;
@@ -586,7 +585,6 @@ __global__ __launch_bounds__(64) void k_lz4_decode(const uint8_t *__restrict__ i
     const uint8_t *h = in + desc[2 * f + 0];  // header fields validated by the walk
     const uint32_t tok = h[8], clen = g32le(h + 9), olen = g32le(h + 13), check = g32le(h + 17);
     const bool raw = (tok & 0xF0u) == 0x10u;
-    if (!raw && skip_compressed) return;  // k_lz4_decode_lanes
     const uint8_t *g = h + kHeader;
     const int sh = (int)((uintptr_t)g & 3u);
     const int n = (int)clen;
@@ -695,11 +693,12 @@ __global__ __launch_bounds__(64) void k_lz4_decode(const uint8_t *__restrict__ i
 // first, as LZ4_decompress_safe does), reading literals from the fetched payload and match
 // sources from its own earlier output -- a same-thread store -> load through global memory,
 // which the hardware keeps in order.  Copies go 8 bytes at a time: a chunk's 8 loads are
-// issued before its stores (one memory round trip per chunk), which is also what makes the
-// self-overlapping copy exact: chunk [i, i + 8) of a match at offset >= 8 reads bytes
-// written before it, and an offset below 8 repeats the match's first `off` bytes from
-// registers.  Then XXH32 of the frame's output (re-read, L2-resident) against the header.
-// RAW frames stay with k_lz4_decode (skip_compressed).  Errors: atomicOr into *err.
+// one 8-byte load before its store (one memory round trip per chunk), which is also what
+// makes the self-overlapping copy exact: chunk [i, i + 8) of a match at offset >= 8 reads
+// bytes written before it; an offset below 8 writes the match's first p bytes (p the first
+// multiple of the offset >= 8) from registers, then copies chunks from p bytes back.  Then
+// XXH32 of the frame's output (re-read, L2-resident) against the header.  RAW frames go to
+// k_lz4_raw_lanes.  Errors: atomicOr into *err.
 // (A variant that kept each lane's last 256 output bytes in an LDS ring, so that no load
 // follows the lane's own stores, measured slower: 17.3 / 30.2 ms against 11.9 / 24.6 ms,
 // profiles/r02_lz4_decode_lanes_ab.jsonl.)
@@ -803,6 +802,56 @@ __global__ __launch_bounds__(64) void k_lz4_decode_lanes(const uint8_t *__restri
     if (!bad && (xxh32_global(o, (int)olen, 0x9747b28cu) & 0x0FFFFFFFu) != check) bad = 2;
     if (bad) atomicOr(err, bad);
 }
+
+// RAW frames of a lane-decoded stream, one per LANE: the payload is copied in 16-byte chunks
+// (one unaligned global_load_dwordx4 / global_store_dwordx4 each) and every chunk is also the
+// next XXH32 stripe, so the checksum reads nothing twice.  (k_lz4_decode's wave-per-frame
+// RAW path stages 32 KB in LDS -- 4 frames per CU -- and runs XXH32 on one lane.)
+__global__ __launch_bounds__(64) void k_lz4_raw_lanes(const uint8_t *__restrict__ in,
+                                                      const int64_t *__restrict__ desc, int64_t nframes,
+                                                      uint8_t *__restrict__ out, uint32_t *__restrict__ err) {
+    const int64_t f = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (f >= nframes) return;
+    const uint8_t *h = in + desc[2 * f + 0];
+    if ((h[8] & 0xF0u) != 0x10u) return;  // compressed: k_lz4_decode_lanes
+    const uint32_t olen = g32le(h + 13), check = g32le(h + 17);  // RAW: clen == olen (the walk)
+    const uint8_t *src = h + kHeader;
+    uint8_t *o = out + desc[2 * f + 1];
+    const uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u,
+                   P5 = 374761393u, seed = 0x9747b28cu;
+    const uint32_t ns = olen >> 4;
+    uint32_t hs;
+    if (ns) {
+        uint32_t v1 = seed + P1 + P2, v2 = seed + P2, v3 = seed, v4 = seed - P1;
+#pragma unroll 4
+        for (uint32_t k = 0; k < ns; ++k) {
+            uint4 x;
+            __builtin_memcpy(&x, src + 16 * k, 16);
+            __builtin_memcpy(o + 16 * k, &x, 16);
+            v1 = rotl(v1 + x.x * P2, 13) * P1;
+            v2 = rotl(v2 + x.y * P2, 13) * P1;
+            v3 = rotl(v3 + x.z * P2, 13) * P1;
+            v4 = rotl(v4 + x.w * P2, 13) * P1;
+        }
+        hs = rotl(v1, 1) + rotl(v2, 7) + rotl(v3, 12) + rotl(v4, 18);
+    } else {
+        hs = seed + P5;
+    }
+    hs += olen;
+    uint32_t i = ns << 4;
+    for (; i + 4 <= olen; i += 4) {
+        const uint32_t wd = g32(src + i);
+        __builtin_memcpy(o + i, &wd, 4);
+        hs = rotl(hs + wd * P3, 17) * P4;
+    }
+    for (; i < olen; ++i) {
+        const uint8_t b = src[i];
+        o[i] = b;
+        hs = rotl(hs + (uint32_t)b * P5, 11) * P1;
+    }
+    hs ^= hs >> 15; hs *= P2; hs ^= hs >> 13; hs *= P3; hs ^= hs >> 16;
+    if ((hs & 0x0FFFFFFFu) != check) atomicOr(err, 2u);
+}
 }  // namespace
 
 int lz4_lanes_per_workgroup() { return kLanes; }
@@ -861,10 +910,15 @@ hipError_t launch_lz4_decode(const uint8_t *in, const int64_t *desc, int64_t nfr
     // frames 10.2 (waves) vs 11.9 ms (lanes), ~32K frames 4.31 vs 4.32 ms, 127K frames 58.3
     // vs 24.6 ms
     const bool lanes = force_lanes || nframes >= kLaneDecodeMinFrames;
-    hipLaunchKernelGGL(k_lz4_decode, dim3((unsigned)nframes), dim3(64), 0, s, in, desc, nframes, out, err,
-                       lanes ? 1 : 0);
+    if (!lanes) {
+        hipLaunchKernelGGL(k_lz4_decode, dim3((unsigned)nframes), dim3(64), 0, s, in, desc, nframes, out, err);
+        return hipGetLastError();
+    }
+    // RAW frames one per lane as well (C1 Kryo+LZ4 decode 22.6 -> 17.2 ms)
+    hipLaunchKernelGGL(k_lz4_raw_lanes, dim3((unsigned)((nframes + 63) / 64)), dim3(64), 0, s, in, desc, nframes,
+                       out, err);
     hipError_t e = hipGetLastError();
-    if (e != hipSuccess || !lanes) return e;
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lz4_decode_lanes, dim3((unsigned)((nframes + 63) / 64)), dim3(64), 0, s, in, desc, nframes,
                        out, err);
     return hipGetLastError();
