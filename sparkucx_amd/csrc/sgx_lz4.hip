@@ -734,6 +734,12 @@ __device__ uint32_t xxh32_global(const uint8_t *p, int len, uint32_t seed) {
     return h;
 }
 
+// byte i (< 16) of a 16-byte little-endian register value
+__device__ __forceinline__ uint32_t byte_at(const uint4 &x, uint32_t i) {
+    const uint32_t w = i < 8u ? (i < 4u ? x.x : x.y) : (i < 12u ? x.z : x.w);
+    return (w >> (8u * (i & 3u))) & 0xFFu;
+}
+
 // d and s may overlap (a match copy): each 8-byte chunk is read before it is written (one
 // unaligned global_load_dwordx2 / global_store_dwordx2 per chunk)
 __device__ __forceinline__ void copy8_chunks(uint8_t *d, const uint8_t *s, uint32_t len) {
@@ -762,17 +768,41 @@ __global__ __launch_bounds__(64) void k_lz4_decode_lanes(const uint8_t *__restri
     uint8_t *o = out + desc[2 * f + 1];
     uint32_t ip = 0, op = 0, bad = 0;
     for (;;) {
-        if (ip >= clen) { bad = 1; break; }
-        const uint32_t t = src[ip++];
-        uint32_t lit = t >> 4;
-        if (lit == 15) { uint32_t b; do { if (ip >= clen) { bad = 1; break; } b = src[ip++]; lit += b; } while (b == 255); if (bad) break; }
-        if (ip + lit > clen || op + lit > olen) { bad = 1; break; }
-        copy8_chunks(o + op, src + ip, lit);
-        ip += lit; op += lit;
-        if (ip == clen) break;
-        if (ip + 2 > clen) { bad = 1; break; }
-        const uint32_t off = (uint32_t)src[ip] | ((uint32_t)src[ip + 1] << 8);
-        ip += 2;
+        uint32_t t = 0, off = 0;
+        bool fast = false;
+        if (ip + 16 <= clen && op + 16 <= olen) {
+            // a short sequence head in one 16-byte load: token, literals, offset.  The literals
+            // go out as one 16-byte store; its bytes past the literals land in [op + lit,
+            // op + 16), inside this frame, where this sequence's match or later sequences write
+            // before anything reads them (a match reads only bytes before its own position)
+            uint4 x;
+            __builtin_memcpy(&x, src + ip, 16);
+            t = x.x & 0xFFu;
+            const uint32_t lit = t >> 4;
+            if (lit <= 13u) {
+                fast = true;
+                const uint4 y = make_uint4(__builtin_amdgcn_alignbyte(x.y, x.x, 1),
+                                           __builtin_amdgcn_alignbyte(x.z, x.y, 1),
+                                           __builtin_amdgcn_alignbyte(x.w, x.z, 1), x.w >> 8);
+                __builtin_memcpy(o + op, &y, 16);
+                off = byte_at(x, 1u + lit) | (byte_at(x, 2u + lit) << 8);
+                ip += 3u + lit;
+                op += lit;
+            }
+        }
+        if (!fast) {
+            if (ip >= clen) { bad = 1; break; }
+            t = src[ip++];
+            uint32_t lit = t >> 4;
+            if (lit == 15) { uint32_t b; do { if (ip >= clen) { bad = 1; break; } b = src[ip++]; lit += b; } while (b == 255); if (bad) break; }
+            if (ip + lit > clen || op + lit > olen) { bad = 1; break; }
+            copy8_chunks(o + op, src + ip, lit);
+            ip += lit; op += lit;
+            if (ip == clen) break;
+            if (ip + 2 > clen) { bad = 1; break; }
+            off = (uint32_t)src[ip] | ((uint32_t)src[ip + 1] << 8);
+            ip += 2;
+        }
         uint32_t ml = (t & 15u) + kMinMatch;
         if ((t & 15u) == 15u) { uint32_t b; do { if (ip >= clen) { bad = 1; break; } b = src[ip++]; ml += b; } while (b == 255); if (bad) break; }
         if (off == 0 || off > op || op + ml > olen) { bad = 1; break; }
