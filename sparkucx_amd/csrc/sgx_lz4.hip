@@ -740,6 +740,16 @@ __device__ __forceinline__ uint32_t byte_at(const uint4 &x, uint32_t i) {
     return (w >> (8u * (i & 3u))) & 0xFFu;
 }
 
+// ceil(len / 16) 16-byte chunks (unaligned dwordx4): d[len, ceil16(len)) receives bytes that
+// later writes replace before anything reads them; s is >= 16 bytes before d (or elsewhere)
+__device__ __forceinline__ void copy16_over(uint8_t *d, const uint8_t *s, uint32_t len) {
+    for (uint32_t i = 0; i < len; i += 16) {
+        uint4 v;
+        __builtin_memcpy(&v, s + i, 16);
+        __builtin_memcpy(d + i, &v, 16);
+    }
+}
+
 // d and s may overlap (a match copy): each 8-byte chunk is read before it is written (one
 // unaligned global_load_dwordx2 / global_store_dwordx2 per chunk)
 __device__ __forceinline__ void copy8_chunks(uint8_t *d, const uint8_t *s, uint32_t len) {
@@ -796,7 +806,9 @@ __global__ __launch_bounds__(64) void k_lz4_decode_lanes(const uint8_t *__restri
             uint32_t lit = t >> 4;
             if (lit == 15) { uint32_t b; do { if (ip >= clen) { bad = 1; break; } b = src[ip++]; lit += b; } while (b == 255); if (bad) break; }
             if (ip + lit > clen || op + lit > olen) { bad = 1; break; }
-            copy8_chunks(o + op, src + ip, lit);
+            const uint32_t lr = (lit + 15u) & ~15u;
+            if (ip + lr <= clen && op + lr <= olen) copy16_over(o + op, src + ip, lit);
+            else copy8_chunks(o + op, src + ip, lit);
             ip += lit; op += lit;
             if (ip == clen) break;
             if (ip + 2 > clen) { bad = 1; break; }
@@ -806,7 +818,8 @@ __global__ __launch_bounds__(64) void k_lz4_decode_lanes(const uint8_t *__restri
         uint32_t ml = (t & 15u) + kMinMatch;
         if ((t & 15u) == 15u) { uint32_t b; do { if (ip >= clen) { bad = 1; break; } b = src[ip++]; ml += b; } while (b == 255); if (bad) break; }
         if (off == 0 || off > op || op + ml > olen) { bad = 1; break; }
-        if (off >= 8) copy8_chunks(o + op, o + op - off, ml);
+        if (off >= 16 && op + ((ml + 15u) & ~15u) <= olen) copy16_over(o + op, o + op - off, ml);
+        else if (off >= 8) copy8_chunks(o + op, o + op - off, ml);
         else {
             // the match repeats with period off, so also with period p = the first multiple of
             // off >= 8: bytes [0, p) from the period held in registers, the rest as chunks
