@@ -576,7 +576,8 @@ constexpr int kInplace = kMaxBlock + (kMaxBlock >> 8) + 32;
 // writes the block out with dword stores.  Errors: atomicOr into *err.
 __global__ __launch_bounds__(64) void k_lz4_decode(const uint8_t *__restrict__ in,
                                                    const int64_t *__restrict__ desc, int64_t nframes,
-                                                   uint8_t *__restrict__ out, uint32_t *__restrict__ err) {
+                                                   uint8_t *__restrict__ out, uint32_t *__restrict__ err,
+                                                   int skip_raw) {
     __shared__ __attribute__((aligned(16))) uint8_t s_buf[kInplace + 48];
     __shared__ int s_bad;
     const int64_t f = blockIdx.x;
@@ -585,6 +586,7 @@ __global__ __launch_bounds__(64) void k_lz4_decode(const uint8_t *__restrict__ i
     const uint8_t *h = in + desc[2 * f + 0];  // header fields validated by the walk
     const uint32_t tok = h[8], clen = g32le(h + 9), olen = g32le(h + 13), check = g32le(h + 17);
     const bool raw = (tok & 0xF0u) == 0x10u;
+    if (raw && skip_raw) return;  // k_lz4_raw_lanes
     const uint8_t *g = h + kHeader;
     const int sh = (int)((uintptr_t)g & 3u);
     const int n = (int)clen;
@@ -702,7 +704,8 @@ __global__ __launch_bounds__(64) void k_lz4_decode(const uint8_t *__restrict__ i
 // (A variant that kept each lane's last 256 output bytes in an LDS ring, so that no load
 // follows the lane's own stores, measured slower: 17.3 / 30.2 ms against 11.9 / 24.6 ms,
 // profiles/r02_lz4_decode_lanes_ab.jsonl.)
-constexpr int64_t kLaneDecodeMinFrames = 32768;  // below: k_lz4_decode does every frame
+constexpr int64_t kLaneDecodeMinFrames = 32768;  // below: k_lz4_decode does the compressed frames
+constexpr int64_t kRawLaneMinFrames = 2048;      // below: k_lz4_decode does the RAW frames too
 
 __device__ uint32_t xxh32_global(const uint8_t *p, int len, uint32_t seed) {
     const uint32_t P1 = 2654435761u, P2 = 2246822519u, P3 = 3266489917u, P4 = 668265263u,
@@ -953,15 +956,21 @@ hipError_t launch_lz4_decode(const uint8_t *in, const int64_t *desc, int64_t nfr
     // frames 10.2 (waves) vs 11.9 ms (lanes), ~32K frames 4.31 vs 4.32 ms, 127K frames 58.3
     // vs 24.6 ms
     const bool lanes = force_lanes || nframes >= kLaneDecodeMinFrames;
+    // RAW frames one per lane from fewer frames on (tools/prof_lz4.py: 1,889 frames 0.44 vs
+    // 0.49 ms, 7,651 frames 0.57 vs 1.37 ms; one lane's serial copy costs ~0.4 ms, so not for
+    // a handful of frames)
+    const bool raw_lanes = force_lanes || nframes >= kRawLaneMinFrames;
+    hipError_t e = hipSuccess;
+    if (raw_lanes) {
+        hipLaunchKernelGGL(k_lz4_raw_lanes, dim3((unsigned)((nframes + 63) / 64)), dim3(64), 0, s, in, desc, nframes,
+                           out, err);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
     if (!lanes) {
-        hipLaunchKernelGGL(k_lz4_decode, dim3((unsigned)nframes), dim3(64), 0, s, in, desc, nframes, out, err);
+        hipLaunchKernelGGL(k_lz4_decode, dim3((unsigned)nframes), dim3(64), 0, s, in, desc, nframes, out, err,
+                           raw_lanes ? 1 : 0);
         return hipGetLastError();
     }
-    // RAW frames one per lane as well (C1 Kryo+LZ4 decode 22.6 -> 17.2 ms)
-    hipLaunchKernelGGL(k_lz4_raw_lanes, dim3((unsigned)((nframes + 63) / 64)), dim3(64), 0, s, in, desc, nframes,
-                       out, err);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_lz4_decode_lanes, dim3((unsigned)((nframes + 63) / 64)), dim3(64), 0, s, in, desc, nframes,
                        out, err);
     return hipGetLastError();

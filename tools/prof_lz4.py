@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--records", type=int, default=1 << 24)
     ap.add_argument("--partitions", type=int, default=1024)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--lane-decode", action="store_true", help="force the lane-per-frame decoders")
     a = ap.parse_args()
     import numpy as np
 
@@ -28,7 +29,7 @@ def main():
     import sparkucx_amd as sgx
     from sparkucx_amd._lib import check, lib
 
-    e = sgx.ShuffleEngine(0)
+    e = sgx.ShuffleEngine(0, flags=sgx.FLAG_LZ4_LANE_DECODE if a.lane_decode else 0)
     R, n = a.partitions, a.records
     for case in ("uniform", "lowentropy"):
         recs = oracle.gen_uniform16(n, 0x5EEDC0DE)
@@ -83,7 +84,7 @@ def main():
         c0 = time.perf_counter()
         oracle.lz4_frame_partitions(stream, offs[:65])
         ct = time.perf_counter() - c0
-        print(json.dumps({"case": case, "records": n, "partitions": R, "stream_bytes": int(nbytes),
+        print(json.dumps({"case": case, "lane_decode": a.lane_decode, "records": n, "partitions": R, "stream_bytes": int(nbytes),
                           "framed_bytes": total, "ratio": round(total / nbytes, 4),
                           "gpu_ms": round(t * 1e3, 3), "gpu_input_GBs": round(nbytes / t / 1e9, 2),
                           "gpu_decode_ms": round(td * 1e3, 3), "gpu_decode_out_GBs": round(nbytes / td / 1e9, 2),
