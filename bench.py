@@ -250,13 +250,17 @@ def main():
             raise SystemExit("--compress needs --serializer kryo (spark.shuffle.compress applies to serialized streams)")
         eng.set_compression(sid, "lz4")
 
+    last = {"mid": None}  # the map the last step wrote (read back by the Kryo leg below)
+
     def step(k):
         mid = (k & 1) * world + rank  # two alternating map slots per rank
+        eng.write_map(sid, mid, buf, n, rb)
         if world > 1 or self_x:
-            eng.write_map(sid, mid, buf, n, rb)
-            eng.exchange(sid, mid)
-        else:
-            eng.write_map(sid, mid, buf, n, rb)
+            # this step's map through the shuffle's exchange (sgx_exchange_maps: the pipelined
+            # form -- the all-to-all of map k runs on the exchange stream while map k+1 is
+            # written on the compute stream)
+            eng.exchange(sid, [mid])
+        last["mid"] = mid
 
     def barrier():
         if dist is not None:
@@ -287,7 +291,7 @@ def main():
     xgmi = None
     if world > 1:
         # bytes this rank's map sends over xGMI (reducer r lives on rank floor(r*P/R))
-        r0, r1 = eng.round_reducers(sid, rank)  # the round of map `rank`, whose lengths `lens` are
+        r0, r1 = eng.shuffle_reducers(sid)  # this rank's reducers (fixed by the shuffle's first round)
         rr = torch.tensor([r0, r1], dtype=torch.int64)
         allr = [torch.zeros(2, dtype=torch.int64) for _ in range(world)]
         dist.all_gather(allr, rr)
@@ -373,7 +377,7 @@ def main():
             if world == 1:
                 # reduce side of the same shuffle: every block of the last map, decoded on the GPU
                 dst = eng.alloc(n * 16)
-                last_mid = ((args.steps + args.warmup - 1) & 1) * world + rank
+                last_mid = last["mid"]
                 for _ in range(3):
                     eng.stats_reset()
                     eng.read_records(sid, [last_mid], 0, R, dst=dst)

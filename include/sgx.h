@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SGX_ABI_VERSION 4
+#define SGX_ABI_VERSION 5
 
 enum sgx_status {
     SGX_OK = 0,
@@ -165,19 +165,24 @@ int sgx_lz4_unframe_streams(sgx_engine *e, const void *framed_dev, const int64_t
  * after).  sgx_read_grouped(SGX_AGG_SUM) on such a shuffle is combineCombinersByKey. */
 int sgx_set_map_side_combine(sgx_engine *e, int32_t shuffle_id, int32_t agg);
 
-/* Reducer placement of a shuffle's exchange rounds (sgx_exchange).  SGX_PLACE_EVEN (the
- * default): rank j holds the reducers r with floor(r * P / R) == j.  SGX_PLACE_BYTES:
- * contiguous reducer ranges that balance the bytes each rank receives in the round
- * (sgx_balanced_ranges over the all-gathered lengths, the same on every rank), for skewed
- * keys (config C3: Zipf(1.1) puts most of the head of the distribution on rank 0 under the
- * even split).  Which ranks run which reduce tasks is the engine's choice -- Spark's
- * scheduler places reduce tasks itself (UcxShuffleReader.scala:74-103 reads whichever
- * partition range it is given); the canonical per-reducer sequences do not change.
- * Placement may change between rounds. */
+/* Reducer placement of a shuffle's exchange (sgx_exchange).  SGX_PLACE_EVEN (the default):
+ * rank j holds the reducers r with floor(r * P / R) == j.  SGX_PLACE_BYTES: contiguous reducer
+ * ranges that balance the bytes each rank receives (sgx_balanced_ranges over the all-gathered
+ * lengths of the shuffle's first exchange round, the same on every rank), for skewed keys
+ * (config C3: Zipf(1.1) puts most of the head of the distribution on rank 0 under the even
+ * split).  Which ranks run which reduce tasks is the engine's choice -- Spark's scheduler
+ * places reduce tasks itself (UcxShuffleReader.scala:74-103 reads whichever partition range
+ * it is given); the canonical per-reducer sequences do not change.  The ranges are fixed by
+ * the shuffle's first exchange round and hold for every later round, so all blocks of a
+ * reducer land on one rank: set the placement before the first sgx_exchange (SGX_ERR_STATE
+ * after). */
 enum sgx_placement { SGX_PLACE_EVEN = 0, SGX_PLACE_BYTES = 1 };
 int sgx_set_reducer_placement(sgx_engine *e, int32_t shuffle_id, int32_t placement);
-/* The reducers [*r0, *r1) this rank holds for the exchange round that carried map_id (the
- * map of any rank in that round). */
+/* The reducers [*r0, *r1) this rank holds for shuffle_id (fixed by its first exchange round;
+ * SGX_ERR_STATE before it).  The executor's reduce tasks for these partitions read locally;
+ * INTEGRATION.md shows how the JVM side turns them into preferred locations. */
+int sgx_shuffle_reducers(sgx_engine *e, int32_t shuffle_id, int32_t *r0, int32_t *r1);
+/* The same, looked up through the exchange round that carried map_id (the map of any rank). */
 int sgx_round_reducers(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int32_t *r0, int32_t *r1);
 /* unregisterShuffle: CommonUcxShuffleManager.scala:103-106 -> removeShuffle
  * (CommonUcxShuffleBlockResolver.scala:63-71). Frees the shuffle's HBM. */
@@ -224,7 +229,7 @@ int sgx_index_block_range(const char *index_path, int32_t start_reduce, int32_t 
 
 /* ---- reduce-side exchange: replaces the per-block UCX AM fetch path
  *      (ucx/UcxWorkerWrapper.scala:96-186, spark_3_0/UcxShuffleClient.scala:17-91) with one
- *      counts all-gather + ncclAllToAllv over xGMI + a regroup kernel.  Call
+ *      lengths all-gather + one grouped all-to-all over xGMI per shuffle.  Call
  *      sgx_comm_init once per engine (the unique id travels over the host's control plane,
  *      which replaces the ExecutorAdded/IntroduceAllExecutors RPC in the rpc/ package). ---- */
 int sgx_get_unique_id(uint8_t out_id[128]);
@@ -254,14 +259,22 @@ typedef struct sgx_host_comm {
 } sgx_host_comm;
 int sgx_comm_init_host(sgx_engine *e, int32_t nranks, int32_t rank, const sgx_host_comm *comm);
 int sgx_comm_size(sgx_engine *e, int32_t *nranks, int32_t *rank);
-/* Push map `map_id` of `shuffle_id` to the reducer owners (contiguous reducer ranges: the
- * shuffle's placement, sgx_set_reducer_placement -- by default reducer r lives on rank
- * floor(r*P/R); sgx_round_reducers reports the range); every rank calls it collectively
- * with its own map.  Asynchronous on the
- * engine's exchange stream; completes at sgx_sync.  Received blocks stay in the
- * all-to-all's receive layout ([source rank][reducer]); sgx_fetch_blocks gathers them in
- * the order asked for (reducer-major, map-minor gives the canonical per-reducer sequence). */
-int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id);
+/* The exchange of shuffle_id (sgx_exchange(e, shuffle_id)), collective: every
+ * rank calls it, in the same order relative to its other exchanges, once its map tasks of the
+ * shuffle are committed.  Each rank contributes every committed map output of the shuffle it
+ * holds that no earlier exchange carried -- any number, none included: Spark's map tasks land
+ * on executors independently -- and afterwards every rank holds its reducers' blocks
+ * (sgx_shuffle_reducers) of every map of every rank.  Steps: an all-gather of each rank's map
+ * count, an all-gather of {map id, R lengths} per map, then ONE grouped exchange of the
+ * partition-contiguous map outputs (already grouped by destination: no pack step) into this
+ * rank's receive buffer, laid out [source rank][its maps][my reducers].  Asynchronous on the
+ * engine's exchange stream; completes at sgx_sync (fetches and reads wait for it on the GPU).
+ * Calling it again after more maps were written runs another round with just those maps (the
+ * reducer ranges stay those of the first round).  Map ids must be unique across ranks. */
+int sgx_exchange(sgx_engine *e, int32_t shuffle_id);
+/* The same collective with exactly the listed local maps (n >= 0; 0 = this rank contributes
+ * nothing this round): a pipelined writer exchanges map k while it writes map k + 1. */
+int sgx_exchange_maps(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t n);
 
 /* ---- ShuffleTransport.fetchBlocksByBlockIds (ucx/ShuffleTransport.scala:154-156) /
  *      BlockStoreClient.fetchBlocks (spark_3_0/UcxShuffleClient.scala:49-91): copy blocks
@@ -385,6 +398,14 @@ int sgx_plan_exchange_ranges(const int64_t *lengths_all, int32_t P, int32_t R, i
                              const int32_t *bounds, int64_t item_bytes, int64_t *send_counts,
                              int64_t *send_displs, int64_t *recv_counts, int64_t *recv_displs,
                              int64_t *items, int64_t *n_items);
+/* The per-shuffle exchange's plan: rank j contributes maps_per_rank[j] maps, lengths_all
+ * [M][R] source-rank-major.  send_counts/send_displs[P]: this rank's maps' bytes of each
+ * destination's reducers, packed [destination][map]; recv_counts/recv_displs[P]: the bytes
+ * from each source rank, [source rank][its maps][my reducers]; block_off[M][nmine] (may be
+ * NULL): where block (map m, my reducer r) lands in the receive buffer. */
+int sgx_plan_exchange_maps(const int64_t *lengths_all, const int64_t *maps_per_rank, int32_t P, int32_t R,
+                           int32_t rank, const int32_t *bounds, int64_t *send_counts, int64_t *send_displs,
+                           int64_t *recv_counts, int64_t *recv_displs, int64_t *block_off);
 /* Byte-balanced placement: bounds[P + 1] of P contiguous reducer ranges minimising the largest
  * per-rank total of sum_j lengths_all[j][r] (binary search on the bound + greedy cuts; a
  * round with no bytes gets the even split).  Deterministic: every rank computes the same. */

@@ -66,6 +66,14 @@ static int throw_arg(JNIEnv *env, const char *msg) {
 
 static sgx_engine *E(jlong h) { return (sgx_engine *)(intptr_t)h; }
 
+/* a long[] of map ids as a C array (n + 1 entries, so an empty list is not NULL); free() it */
+static int64_t *map_list(JNIEnv *env, jlongArray maps, jsize *n) {
+    *n = (*env)->GetArrayLength(env, maps);
+    int64_t *m = (int64_t *)calloc((size_t)*n + 1, sizeof(int64_t));
+    if (m) (*env)->GetLongArrayRegion(env, maps, 0, *n, (jlong *)m);
+    return m;
+}
+
 /* direct buffer -> (pointer, capacity in bytes); NULL buffer -> (NULL, 0) */
 static int direct(JNIEnv *env, jobject buf, void **p, int64_t *cap) {
     *p = NULL;
@@ -300,9 +308,31 @@ JNIEXPORT jbyteArray JNICALL JNI_FN(bootstrapJoin)(JNIEnv *env, jclass c, jstrin
     return out;
 }
 
-JNIEXPORT void JNICALL JNI_FN(exchange)(JNIEnv *env, jclass c, jlong e, jint sid, jlong mapId) {
+/* the shuffle's exchange (collective: every executor calls it, see GpuExchangeCoordinator) */
+JNIEXPORT void JNICALL JNI_FN(exchange)(JNIEnv *env, jclass c, jlong e, jint sid) {
     (void)c;
-    check(env, sgx_exchange(E(e), sid, mapId));
+    check(env, sgx_exchange(E(e), sid));
+}
+
+/* the pipelined form: exactly these local maps (an empty array contributes nothing) */
+JNIEXPORT void JNICALL JNI_FN(exchangeMaps)(JNIEnv *env, jclass c, jlong e, jint sid, jlongArray maps) {
+    (void)c;
+    jsize n;
+    int64_t *m = map_list(env, maps, &n);
+    if (!m) return;
+    const int rc = sgx_exchange_maps(E(e), sid, m, n);
+    free(m);
+    check(env, rc);
+}
+
+/* the executor's reducers [r0, r1) of the shuffle (fixed by its first exchange): int[2] */
+JNIEXPORT jintArray JNICALL JNI_FN(shuffleReducers)(JNIEnv *env, jclass c, jlong e, jint sid) {
+    (void)c;
+    int32_t r[2] = {0, 0};
+    if (check(env, sgx_shuffle_reducers(E(e), sid, &r[0], &r[1]))) return NULL;
+    jintArray out = (*env)->NewIntArray(env, 2);
+    if (out) (*env)->SetIntArrayRegion(env, out, 0, 2, (const jint *)r);
+    return out;
 }
 
 JNIEXPORT void JNICALL JNI_FN(setReducerPlacement)(JNIEnv *env, jclass c, jlong e, jint sid, jint placement) {
@@ -363,12 +393,6 @@ JNIEXPORT void JNICALL JNI_FN(sync)(JNIEnv *env, jclass c, jlong e) {
 }
 
 /* ---- reduce side after the fetch ---- */
-static int64_t *map_list(JNIEnv *env, jlongArray maps, jsize *n) {
-    *n = (*env)->GetArrayLength(env, maps);
-    int64_t *m = (int64_t *)calloc((size_t)*n + 1, sizeof(int64_t));
-    if (m) (*env)->GetLongArrayRegion(env, maps, 0, *n, (jlong *)m);
-    return m;
-}
 
 /* readRecords / readSorted: bytes written (dst null = size query) */
 JNIEXPORT jlong JNICALL JNI_FN(readRecords)(JNIEnv *env, jclass c, jlong e, jint sid, jlongArray maps, jint start,
@@ -412,7 +436,8 @@ JNIEXPORT jlongArray JNICALL JNI_FN(readGrouped)(JNIEnv *env, jclass c, jlong e,
     int64_t *m = map_list(env, maps, &n);
     if (!m) return NULL;
     int64_t r[2] = {0, 0};
-    const int64_t cap_groups = kp ? kc / 8 : 0, cap_values = vp ? vc / 8 : 0;
+    /* group_starts receives as many entries as keys: the smaller buffer bounds both */
+    const int64_t cap_groups = kp ? (sp && sc < kc ? sc : kc) / 8 : 0, cap_values = vp ? vc / 8 : 0;
     const int rc = sgx_read_grouped(E(e), sid, m, n, start, end, agg, (int64_t *)kp, (int64_t *)sp, (int64_t *)vp,
                                     cap_groups, cap_values, SGX_MEM_HOST, &r[0], &r[1]);
     free(m);

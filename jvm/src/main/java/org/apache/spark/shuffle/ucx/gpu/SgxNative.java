@@ -41,9 +41,10 @@ public final class SgxNative {
   public static native void setSerializer(long e, int shuffleId, int serializer);
   public static native void setCompression(long e, int shuffleId, int codec, int blockSize);
   public static native void setMapSideCombine(long e, int shuffleId, int agg);
-  // reducer placement of the exchange rounds (PLACE_EVEN / PLACE_BYTES) and this executor's
-  // reducer range [r0, r1) of the round that carried mapId
+  // reducer placement of the shuffle's exchange (PLACE_EVEN / PLACE_BYTES; before its first
+  // exchange) and this executor's reducer range [r0, r1) of the shuffle (after it)
   public static native void setReducerPlacement(long e, int shuffleId, int placement);
+  public static native int[] shuffleReducers(long e, int shuffleId);
   public static native int[] roundReducers(long e, int shuffleId, long mapId);
   public static native void unregisterShuffle(long e, int shuffleId);
 
@@ -68,7 +69,11 @@ public final class SgxNative {
   public static native void bootstrapServe(int port, int nranks, byte[] id, int timeoutMs);
   public static native byte[] bootstrapJoin(String host, int port, int rank, int timeoutMs,
                                             int[] nranksOut);
-  public static native void exchange(long e, int shuffleId, long mapId);
+  // the shuffle's exchange, collective over every executor of the world (sgx_exchange: every
+  // committed map of the shuffle this executor holds that no earlier exchange carried);
+  // exchangeMaps: exactly these local maps (the pipelined form)
+  public static native void exchange(long e, int shuffleId);
+  public static native void exchangeMaps(long e, int shuffleId, long[] mapIds);
 
   // fetchBlocksByBlockIds: blocks back to back in dst; returns their lengths (dst null = sizes)
   public static native long[] fetchBlocks(long e, int shuffleId, long[] mapIds, int[] reduceIds,

@@ -36,6 +36,15 @@ class GpuShuffleClient(engine: Long, conf: SparkConf) extends BlockStoreClient {
     val reduceIds = parsed.map(_.reduceId)
     try {
       val sizes = SgxNative.fetchBlocks(engine, shuffleId, mapIds, reduceIds, null)  // size query
+      if (sizes.sum > Int.MaxValue - 8) {
+        // one direct buffer holds < 2 GiB: split the request (a single block that large fails)
+        if (blockIds.length == 1)
+          throw new SgxFetchException(s"block ${blockIds(0)} of ${sizes(0)} bytes exceeds one direct buffer")
+        val (a, b) = blockIds.splitAt(blockIds.length / 2)
+        fetchBlocks(host, port, execId, a, listener, downloadFileManager)
+        fetchBlocks(host, port, execId, b, listener, downloadFileManager)
+        return
+      }
       val dst = ByteBuffer.allocateDirect(math.max(1L, sizes.sum).toInt)
       SgxNative.fetchBlocks(engine, shuffleId, mapIds, reduceIds, dst)
       var off = 0

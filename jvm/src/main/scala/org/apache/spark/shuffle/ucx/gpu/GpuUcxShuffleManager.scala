@@ -2,83 +2,155 @@
  * GpuUcxShuffleManager — spark.shuffle.manager for the MI355X engine.  Keeps the reference's
  * plugin shape (spark_3_0/UcxShuffleManager.scala:25-80 over CommonUcxShuffleManager.scala:
  * 25-124: registerShuffle inherited from SortShuffleManager, getWriter / getReader dispatch,
- * unregisterShuffle, stop) and routes (Long, Long) dependencies with a hash or range
- * partitioner to the GPU; anything else falls back to SortShuffleManager's own writer and
- * reader.  One engine per executor (= per GPU: the executor's GPU ordinal in
- * spark.shuffle.ucx.gpu.device); the RCCL id of the exchange travels over
- * SgxNative.bootstrapServe / bootstrapJoin (or Spark RPC), replacing ExecutorAdded /
- * IntroduceAllExecutors.
+ * unregisterShuffle, stop) and routes a dependency to the GPU only when the engine computes
+ * exactly what Spark would:
+ *   - (Long, Long) records: dep.keyClassName and dep.valueClassName are long / java.lang.Long
+ *     (the engine's 16 B record codec; anything else would throw ClassCastException in the
+ *     writer);
+ *   - a HashPartitioner, or a RangePartitioner over Long keys;
+ *   - no aggregator, or one DECLARED with spark.shuffle.ucx.gpu.aggregator.<shuffleId> =
+ *     "sum" (reduceByKey(_ + _) on Longs: the GPU sums with wrap-around, map-side combine
+ *     allowed) or "group" (groupByKey: mapSideCombine must be false).  Spark cannot look
+ *     inside an aggregator's closures, so an undeclared one -- reduceByKey(math.max),
+ *     combineByKey(...) -- stays on the CPU path instead of being guessed.
+ * Everything else falls back to SortShuffleManager's own writer and reader.
+ *
+ * registerShuffle runs on the DRIVER (the ShuffleDependency constructor calls it): it only
+ * decides, and marks the decision in the handle's type (GpuShuffleHandle).  Each executor
+ * registers the shuffle with its own engine on first use (getWriter / getReader), so the
+ * engine -- one per executor = per GPU, spark.shuffle.ucx.gpu.device -- never exists on the
+ * driver.  The exchange world (RCCL communicator, the collective per shuffle) is set up and
+ * driven by GpuExchangeCoordinator.
  */
 package org.apache.spark.shuffle.ucx.gpu
 
 import java.nio.{ByteBuffer, ByteOrder}
 
-import org.apache.spark.{HashPartitioner, RangePartitioner, ShuffleDependency, SparkConf, TaskContext}
+import org.apache.spark.{HashPartitioner, Partitioner, RangePartitioner, ShuffleDependency, SparkConf, TaskContext}
 import org.apache.spark.serializer.KryoSerializer
 import org.apache.spark.shuffle._
 import org.apache.spark.shuffle.sort.SortShuffleManager
 
-class GpuUcxShuffleManager(conf: SparkConf, isDriver: Boolean) extends SortShuffleManager(conf) {
-  private lazy val engine: Long = SgxNative.create(conf.getInt("spark.shuffle.ucx.gpu.device", 0),
-    conf.getInt("spark.shuffle.ucx.gpu.numChunks", 0), 0, conf.getInt("spark.shuffle.ucx.gpu.commTimeoutMs", 0))
-  private val onGpu = new java.util.concurrent.ConcurrentHashMap[Int, java.lang.Boolean]()
+/** A shuffle the GPU runs: same fields as BaseShuffleHandle, plus the declared aggregation. */
+class GpuShuffleHandle[K, V, C](shuffleId: Int, dependency: ShuffleDependency[K, V, C], val agg: Int)
+  extends BaseShuffleHandle[K, V, C](shuffleId, dependency)
 
-  private def isLongSum(dep: ShuffleDependency[_, _, _]): Boolean =
-    dep.aggregator.exists(a => conf.get("spark.shuffle.ucx.gpu.sumAggregator." + dep.shuffleId, "false") == "true")
+object GpuUcxShuffleManager {
+  val NO_AGG: Int = -1
+  private val LONG_CLASSES = Set("long", "java.lang.Long")
+
+  /** RangePartitioner keeps rangeBounds and ascending in private fields: read them by reflection. */
+  private[gpu] def rangeField[T](p: RangePartitioner[_, _], name: String): T = {
+    val f = classOf[RangePartitioner[_, _]].getDeclaredFields
+      .find(f => f.getName == name || f.getName.endsWith("$$" + name))
+      .getOrElse(throw new UnsupportedOperationException(s"RangePartitioner has no field $name"))
+    f.setAccessible(true)
+    f.get(p).asInstanceOf[T]
+  }
+}
+
+class GpuUcxShuffleManager(conf: SparkConf, isDriver: Boolean) extends SortShuffleManager(conf) {
+  import GpuUcxShuffleManager._
+
+  @volatile private var engineCreated = false
+  private lazy val engine: Long = {
+    val e = SgxNative.create(conf.getInt("spark.shuffle.ucx.gpu.device", 0),
+                             conf.getInt("spark.shuffle.ucx.gpu.numChunks", 0), 0,
+                             conf.getInt("spark.shuffle.ucx.gpu.commTimeoutMs", 0))
+    engineCreated = true
+    e
+  }
+  private[gpu] lazy val coordinator = new GpuExchangeCoordinator(conf, isDriver, () => engine)
+  if (conf.getInt("spark.shuffle.ucx.gpu.numExecutors", conf.getInt("spark.executor.instances", 1)) > 1)
+    coordinator  // start the world's setup (driver endpoint / executor join) right away
+  private val registered = new java.util.concurrent.ConcurrentHashMap[Int, java.lang.Boolean]()
+
+  /** The declared aggregation of a dependency, NO_AGG for none, None if the GPU cannot run it. */
+  private def gpuAgg(shuffleId: Int, dep: ShuffleDependency[_, _, _]): Option[Int] =
+    if (dep.aggregator.isEmpty) Some(NO_AGG)
+    else conf.get("spark.shuffle.ucx.gpu.aggregator." + shuffleId, "") match {
+      case "sum" => Some(SgxNative.AGG_SUM)
+      case "group" if !dep.mapSideCombine => Some(SgxNative.AGG_GROUP)
+      case _ => None
+    }
+
+  private def gpuPartitioner(p: Partitioner, dep: ShuffleDependency[_, _, _]): Boolean = p match {
+    case _: HashPartitioner => true
+    case _: RangePartitioner[_, _] => dep.keyOrdering.isDefined  // Long keys: checked by the class names
+    case _ => false
+  }
 
   override def registerShuffle[K, V, C](shuffleId: Int, dependency: ShuffleDependency[K, V, C]): ShuffleHandle = {
-    val handle = super.registerShuffle(shuffleId, dependency)
-    val gpu = dependency.partitioner match {
-      case p: HashPartitioner =>
-        SgxNative.registerShuffle(engine, shuffleId, p.numPartitions, SgxNative.PART_HASH, null, 0, true, 16)
-        true
-      case p: RangePartitioner[_, _] if dependency.keyOrdering.isDefined =>
-        val bounds = p.rangeBounds.asInstanceOf[Array[Long]]
-        val b = ByteBuffer.allocateDirect(math.max(8, bounds.length * 8)).order(ByteOrder.LITTLE_ENDIAN)
-        bounds.foreach(b.putLong)
-        SgxNative.registerShuffle(engine, shuffleId, p.numPartitions, SgxNative.PART_RANGE_I64, b, bounds.length,
-                                  p.ascending, 16)
-        true
-      case _ => false
+    val longs = LONG_CLASSES(dependency.keyClassName) && LONG_CLASSES(dependency.valueClassName)
+    val agg = if (longs && gpuPartitioner(dependency.partitioner, dependency)) gpuAgg(shuffleId, dependency) else None
+    agg match {
+      case Some(a) => new GpuShuffleHandle(shuffleId, dependency, a)
+      case None => super.registerShuffle(shuffleId, dependency)
     }
-    if (gpu) {
-      if (dependency.serializer.isInstanceOf[KryoSerializer]) {
-        SgxNative.setSerializer(engine, shuffleId, SgxNative.SER_KRYO)
+  }
+
+  /** Executor side, once per shuffle: the shuffle's partitioner, serializer, codec, combine and
+   *  reducer placement in this executor's engine. */
+  private def ensureRegistered(h: GpuShuffleHandle[_, _, _]): Unit = {
+    if (registered.containsKey(h.shuffleId)) return
+    registered.synchronized {  // handles are per-task copies: lock the executor's table
+      if (registered.containsKey(h.shuffleId)) return
+      val dep = h.dependency
+      dep.partitioner match {
+        case p: HashPartitioner =>
+          SgxNative.registerShuffle(engine, h.shuffleId, p.numPartitions, SgxNative.PART_HASH, null, 0, true, 16)
+        case p: RangePartitioner[_, _] =>
+          val bounds = rangeField[Array[_]](p, "rangeBounds").map(_.asInstanceOf[Long])
+          val b = ByteBuffer.allocateDirect(math.max(8, bounds.length * 8)).order(ByteOrder.LITTLE_ENDIAN)
+          bounds.foreach(b.putLong)
+          SgxNative.registerShuffle(engine, h.shuffleId, p.numPartitions, SgxNative.PART_RANGE_I64, b, bounds.length,
+                                    rangeField[Boolean](p, "ascending"), 16)
+      }
+      if (dep.serializer.isInstanceOf[KryoSerializer]) {
+        SgxNative.setSerializer(engine, h.shuffleId, SgxNative.SER_KRYO)
         if (conf.getBoolean("spark.shuffle.compress", true))
-          SgxNative.setCompression(engine, shuffleId, SgxNative.CODEC_LZ4,
+          SgxNative.setCompression(engine, h.shuffleId, SgxNative.CODEC_LZ4,
                                    conf.getSizeAsBytes("spark.io.compression.lz4.blockSize", "32k").toInt)
       }
-      if (dependency.mapSideCombine) SgxNative.setMapSideCombine(engine, shuffleId, SgxNative.AGG_SUM)
-      // reducer placement of the exchange rounds: "even" (floor(r*P/R)) or "bytes" (ranges
-      // balanced on the round's lengths, for skewed keys); the executor's range of a round
-      // comes back from SgxNative.roundReducers for the scheduler's locality preferences
+      if (dep.mapSideCombine && h.agg == SgxNative.AGG_SUM)
+        SgxNative.setMapSideCombine(engine, h.shuffleId, SgxNative.AGG_SUM)
+      // reducer placement, fixed by the shuffle's first exchange: "even" (floor(r*P/R)) or
+      // "bytes" (ranges balanced on the lengths, for skewed keys)
       if (conf.get("spark.shuffle.ucx.gpu.reducerPlacement", "even") == "bytes")
-        SgxNative.setReducerPlacement(engine, shuffleId, SgxNative.PLACE_BYTES)
-      onGpu.put(shuffleId, true)
+        SgxNative.setReducerPlacement(engine, h.shuffleId, SgxNative.PLACE_BYTES)
+      registered.put(h.shuffleId, true)
     }
-    handle
   }
 
   override def getWriter[K, V](handle: ShuffleHandle, mapId: Long, context: TaskContext,
-                               metrics: ShuffleWriteMetricsReporter): ShuffleWriter[K, V] =
-    if (onGpu.containsKey(handle.shuffleId))
-      new GpuShuffleWriter[K, V](engine, handle.asInstanceOf[BaseShuffleHandle[K, V, _]], mapId)
-    else super.getWriter(handle, mapId, context, metrics)
+                               metrics: ShuffleWriteMetricsReporter): ShuffleWriter[K, V] = handle match {
+    case h: GpuShuffleHandle[K @unchecked, V @unchecked, _] =>
+      ensureRegistered(h)
+      new GpuShuffleWriter[K, V](engine, h, mapId, conf, shuffleBlockResolver, metrics)
+    case _ => super.getWriter(handle, mapId, context, metrics)
+  }
 
   override def getReader[K, C](handle: ShuffleHandle, startPartition: Int, endPartition: Int,
                                context: TaskContext, metrics: ShuffleReadMetricsReporter): ShuffleReader[K, C] =
-    if (onGpu.containsKey(handle.shuffleId)) {
-      val h = handle.asInstanceOf[BaseShuffleHandle[K, _, C]]
-      new GpuShuffleReader[K, C](engine, h, startPartition, endPartition, context, isLongSum(h.dependency))
-    } else super.getReader(handle, startPartition, endPartition, context, metrics)
+    handle match {
+      case h: GpuShuffleHandle[K @unchecked, _, C @unchecked] =>
+        ensureRegistered(h)
+        new GpuShuffleReader[K, C](engine, h, startPartition, endPartition, context,
+                                   if (isWorld) Some(coordinator) else None)
+      case _ => super.getReader(handle, startPartition, endPartition, context, metrics)
+    }
+
+  private def isWorld: Boolean =
+    conf.getInt("spark.shuffle.ucx.gpu.numExecutors", conf.getInt("spark.executor.instances", 1)) > 1
 
   override def unregisterShuffle(shuffleId: Int): Boolean = {
-    if (onGpu.remove(shuffleId) != null) SgxNative.unregisterShuffle(engine, shuffleId)
+    if (registered.remove(shuffleId) != null) SgxNative.unregisterShuffle(engine, shuffleId)
     super.unregisterShuffle(shuffleId)
   }
 
   override def stop(): Unit = {
-    SgxNative.destroy(engine)
+    if (isWorld) coordinator.stop()
+    if (engineCreated) SgxNative.destroy(engine)
     super.stop()
   }
 }

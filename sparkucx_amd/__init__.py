@@ -16,7 +16,7 @@ from ._lib import (  # noqa: F401
 )
 from .engine import (  # noqa: F401
     DeviceBuffer, ShuffleEngine, balanced_ranges, bootstrap_join, bootstrap_serve, even_ranges, get_unique_id,
-    plan_exchange, reducer_owner,
+    plan_exchange, plan_exchange_maps, reducer_owner,
 )
 from .shuffle import (  # noqa: F401
     Aggregator, BaseShuffleHandle, BlockFetchingListener, GpuShuffleMapOutputWriter, GpuShuffleTransport, GpuShuffleWriter,

@@ -29,7 +29,7 @@ RANK_ORDERED, RANK_MATCH = 0, 1
 FLAG_NO_WRITE_COMBINING, FLAG_NO_WIDE_STAGED, FLAG_SORT_ALL_DIGITS, FLAG_DEBUG_SYNC = 1, 2, 4, 8
 FLAG_LZ4_LANE_DECODE = 16
 PLACE_EVEN, PLACE_BYTES = 0, 1
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 
 class ShuffleError(RuntimeError):
@@ -116,7 +116,10 @@ SIGNATURES = {
     "sgx_get_unique_id": (ctypes.c_int, [_vp]),
     "sgx_comm_init": (ctypes.c_int, [_vp, _i32, _i32, _vp]),
     "sgx_comm_size": (ctypes.c_int, [_vp, _P32, _P32]),
-    "sgx_exchange": (ctypes.c_int, [_vp, _i32, _i64]),
+    "sgx_exchange": (ctypes.c_int, [_vp, _i32]),
+    "sgx_exchange_maps": (ctypes.c_int, [_vp, _i32, _vp, _i64]),
+    "sgx_shuffle_reducers": (ctypes.c_int, [_vp, _i32, _vp, _vp]),
+    "sgx_plan_exchange_maps": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sgx_fetch_blocks": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i64, _vp, _i64, _i32, _vp]),
     "sgx_read_sorted": (ctypes.c_int, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i64, _i32, _vp]),
     "sgx_read_records": (ctypes.c_int, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i64, _i32, _vp]),

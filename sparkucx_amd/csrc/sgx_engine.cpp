@@ -335,7 +335,10 @@ extern "C" int sgx_set_reducer_placement(sgx_engine *e, int32_t shuffle_id, int3
         return fail_msg(SGX_ERR_INVALID, "unknown reducer placement %d", placement);
     std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
     if (!s) return SGX_ERR_STATE;
-    s->placement.store(placement);  // applies from the next exchange round on
+    std::lock_guard<std::mutex> sl(s->mu);
+    if (!s->place_bounds.empty())  // a reducer's blocks must all land on one rank
+        return fail_msg(SGX_ERR_STATE, "shuffle %d was already exchanged: its reducer ranges are fixed", shuffle_id);
+    s->placement.store(placement);
     return SGX_OK;
 }
 

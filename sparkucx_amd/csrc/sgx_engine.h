@@ -174,26 +174,34 @@ struct MapOut {
     std::vector<std::unique_ptr<Spill>> spills;
     const void *view() const { return comp_valid ? comp.p : (ser.p && ser_valid ? ser.p : data.p); }
     bool ser_valid = false;    // `ser` holds this write's Kryo stream
+    bool exchanged = false;    // an exchange round carried this write (sgx_exchange skips it)
     ~MapOut() {
         (void)read_done.wait_host();  // an all-to-all may still read `data`
         (void)done.wait_host();
     }
 };
 
-// One exchange round: every rank pushed one map; this rank holds its reducers' blocks.
-// The receive buffer keeps ncclAllToAllv's layout, [source rank][my reducers]: every
-// (map, reducer) block is contiguous in it, so blocks are served from it directly and the
-// per-reducer canonical order (reducer, then source map) is produced by the fetch that
-// asks for it (one gather launch), not by an extra pass over every received byte.
+// One exchange round: every rank pushed the maps it contributed (any number, 0 included);
+// this rank holds its reducers' blocks of all of them.  The receive buffer is laid out
+// [source rank][that rank's maps, in its order][my reducers]: every (map, reducer) block is
+// contiguous in it, so blocks are served from it directly and the per-reducer canonical
+// order (reducer, then map) is produced by the fetch that asks for it (one gather launch),
+// not by an extra pass over every received byte.
 struct Round {
-    std::vector<int64_t> map_ids;        // [P] the map pushed by each source rank
-    std::vector<int64_t> lens;           // [P][R] bytes
-    std::vector<int64_t> block_off;      // [P][nmine] byte offset in `data`
+    std::vector<int64_t> map_ids;        // [M] every map of the round, source-rank-major
+    std::vector<int32_t> src;            // [M] the rank that pushed it
+    std::vector<int64_t> lens;           // [M][R] bytes
+    std::vector<int64_t> block_off;      // [M][nmine] byte offset in `data` (or in alias[j])
     int32_t r0 = 0, r1 = 0;              // my reducers [r0, r1)
-    DevBuf data;                          // receive buffer, [source][my reducers]
-    std::shared_ptr<MapOut> alias;        // P == 1 without a communicator: the map output itself
+    DevBuf data;                          // receive buffer
+    // P == 1 without a communicator: the map outputs themselves ([M], block_off inside each)
+    std::vector<std::shared_ptr<MapOut>> alias;
     Event done;
-    const void *base() const { return alias ? alias->view() : data.p; }
+    const char *block_ptr(size_t j, int32_t r) const {
+        const size_t nmine = (size_t)(r1 - r0);
+        const char *b = alias.empty() ? (const char *)data.p : (const char *)alias[j]->view();
+        return b + block_off[j * nmine + (size_t)(r - r0)];
+    }
     ~Round() { (void)done.wait_host(); }
 };
 
@@ -205,6 +213,9 @@ struct Shuffle {
     int32_t lz4_block = 0;        // spark.shuffle.compress with lz4 (sgx_set_compression): block size
     int32_t combine = -1;         // map-side combine aggregation (sgx_set_map_side_combine), -1 = none
     std::atomic<int32_t> placement{SGX_PLACE_EVEN};  // reducer placement of exchange rounds
+    // the reducer ranges of every rank, bounds[P + 1], fixed by the shuffle's first exchange
+    // round (empty before): a reducer's blocks from every round land on the same rank
+    std::vector<int32_t> place_bounds;
     DevBuf bounds;
     PartParams pp{};
     std::map<int64_t, std::shared_ptr<MapOut>> maps;

@@ -1,16 +1,21 @@
 // sgx_exchange.cpp — the reduce-side exchange that replaces the per-block UCX Active Message
 // fetch path (ucx/UcxWorkerWrapper.scala:96-186, spark_3_0/UcxShuffleClient.scala:17-47):
-// every rank pushes one map output to the reducer owners with ONE all-to-all (reducer r lives
-// on rank floor(r*P/R), so the partition-contiguous map output is already grouped by
-// destination), after a counts all-gather that tells every receiver the (map, reducer) block
-// sizes.  Two collective backends behind the same code:
-//   * RCCL (sgx_comm_init): ncclAllGather + ncclAllToAllv over xGMI on the engine's exchange
-//     stream, asynchronous; waits poll ncclCommGetAsyncError and give up after the engine's
-//     timeout (the reference spins forever, UcxShuffleClient.scala:44-46);
+// sgx_exchange(e, shuffle_id) is one collective per shuffle (or per batch of maps, for
+// pipelining): every rank contributes the map outputs it holds -- any number, none included,
+// as Spark's map tasks land on executors independently -- and afterwards every rank holds its
+// reducers' blocks of every map of every rank.  Reducer r lives on one rank for the whole
+// shuffle (contiguous ranges, floor(r*P/R) or byte-balanced, fixed by the shuffle's first
+// round), so each partition-contiguous map output is already grouped by destination and is
+// sent without a pack step.  Two collective backends behind the same code:
+//   * RCCL (sgx_comm_init): ncclAllGather of the map counts and lengths, then one grouped
+//     ncclSend / ncclRecv exchange over xGMI on the engine's exchange stream, asynchronous;
+//     waits poll ncclCommGetAsyncError and give up after the engine's timeout (the reference
+//     spins forever, UcxShuffleClient.scala:44-46);
 //   * host (sgx_comm_init_host): the caller's all-gather / all-to-all over host memory --
 //     the fake backend of SURVEY §4, and the path for ranks sharing one GPU.
 #include "sgx_engine.h"
 
+#include <algorithm>
 #include <chrono>
 #include <cstring>
 #include <thread>
@@ -98,115 +103,151 @@ int sgx::comm_wait(sgx_engine *e) {
     }
 }
 
-extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
-    sgx::TraceRange trace_("sgx_exchange");
-    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
-    if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
-    HIP_TRY(hipSetDevice(e->device));
-    Ctx *c = e->ctx();
-    if (!c) return SGX_ERR_HIP;
-    std::shared_ptr<Shuffle> s;
-    std::shared_ptr<MapOut> m;
-    SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
-    std::lock_guard<std::mutex> clk(e->comm_mu);
-    std::vector<int64_t> mylens;
-    int64_t out_bytes = 0;
-    {
-        std::lock_guard<std::mutex> lk(m->mu);
-        if (m->open) return fail_msg(SGX_ERR_STATE, "map %lld is still open", (long long)map_id);
-        SGX_TRY(finish_lengths(e, *c, *s, *m));
-        mylens = m->lengths;
-        out_bytes = m->out_bytes;
-    }
-    const int32_t P = e->nranks, R = s->R;
-    auto rd = std::make_shared<Round>();
-    rd->map_ids.assign((size_t)P, 0);
-    rd->lens.assign((size_t)P * R, 0);
-    my_reducers(R, P, e->rank, &rd->r0, &rd->r1);  // the collective path re-places after the all-gather
-    if (e->comm_broken) return fail_msg(SGX_ERR_STATE, "the communicator was aborted after an exchange failure");
-    if (P == 1 && !e->comm && !e->host_comm) {
-        rd->map_ids[0] = map_id;
-        std::memcpy(rd->lens.data(), mylens.data(), sizeof(int64_t) * (size_t)R);
-        rd->block_off.assign((size_t)R, 0);
-        int64_t off = 0;
-        for (int32_t r = 0; r < R; ++r) {
-            rd->block_off[(size_t)r] = off;
-            off += mylens[(size_t)r];
-        }
-        rd->alias = m;
-        HIP_TRY(rd->done.record(c->st));
-        std::lock_guard<std::mutex> sl(s->mu);
-        for (auto it = s->rounds.begin(); it != s->rounds.end(); ++it)
-            if ((*it)->map_ids == rd->map_ids) {
-                s->rounds.erase(it);
-                break;
-            }
-        s->rounds.push_back(std::move(rd));
+// All-gather of int64 rows: every rank contributes `n` values, `recv` receives P * n,
+// rank-major.  Caller holds comm_mu.  With RCCL the call also drains the exchange stream
+// (the previous round's all-to-all: one communicator, one stream, the same order on every
+// rank).
+static int allgather_i64(sgx_engine *e, const int64_t *send, size_t n, int64_t *recv) {
+    const int32_t P = e->nranks;
+    hipStream_t st = e->s_comm;
+    if (e->comm) {
+        SGX_TRY(e->ag_send.ensure(n * 8));
+        SGX_TRY(e->ag_recv.ensure(n * 8 * (size_t)P));
+        SGX_TRY(e->ag_host.ensure(n * 8 * (size_t)(P + 1)));
+        int64_t *h = (int64_t *)e->ag_host.p;
+        std::memcpy(h, send, n * 8);
+        HIP_TRY(hipMemcpyAsync(e->ag_send.p, h, n * 8, hipMemcpyHostToDevice, st));
+        NCCL_TRY(ncclAllGather(e->ag_send.p, e->ag_recv.p, n, ncclInt64, e->comm, st));
+        HIP_TRY(hipMemcpyAsync(h + n, e->ag_recv.p, n * 8 * (size_t)P, hipMemcpyDeviceToHost, st));
+        SGX_TRY(comm_wait(e));
+        std::memcpy(recv, h + n, n * 8 * (size_t)P);
         return SGX_OK;
     }
-    if (!e->comm && !e->host_comm) return fail_msg(SGX_ERR_STATE, "sgx_comm_init was not called (world of %d ranks)", P);
-    hipStream_t st = e->s_comm;
-    // (1) counts exchange: all-gather {map_id, lengths[R]}
-    const size_t row = (size_t)R + 1;
-    SGX_TRY(e->ag_host.ensure(row * 8 * (size_t)(P + 1)));
-    int64_t *agh = (int64_t *)e->ag_host.p;
-    agh[0] = map_id;
-    std::memcpy(agh + 1, mylens.data(), sizeof(int64_t) * (size_t)R);
+    SGX_TRY(comm_wait(e));
+    if (e->hc.allgather(e->hc.user, send, (int64_t)(n * 8), recv) != 0)
+        return fail_msg(SGX_ERR_COMM, "host all-gather of the partition lengths failed");
+    return SGX_OK;
+}
+
+namespace {
+struct LocalMap {
+    int64_t id;
+    std::shared_ptr<MapOut> m;
+    std::vector<int64_t> lens;
+    int64_t bytes = 0;
+};
+}  // namespace
+
+// One exchange round of shuffle s with this rank's maps `mine` (any number, the same call
+// order on every rank).  (1) all-gather of every rank's map count, then of {map id, R
+// lengths} per map; (2) the shuffle's reducer ranges -- fixed by its first round, so every
+// round sends a reducer's blocks to the same rank; (3) one grouped point-to-point exchange
+// (RCCL: ncclSend / ncclRecv per (map, peer) straight out of the partition-contiguous map
+// outputs, which are already destination-grouped -- no pack step -- into the receive layout
+// [source rank][its maps][my reducers]; host backend: the same bytes through the caller's
+// all-to-all).
+static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> &s, std::vector<LocalMap> mine) {
+    std::lock_guard<std::mutex> clk(e->comm_mu);
+    const int32_t P = e->nranks, R = s->R;
+    for (auto &lm : mine) {
+        std::lock_guard<std::mutex> lk(lm.m->mu);
+        if (lm.m->open) return fail_msg(SGX_ERR_STATE, "map %lld is still open", (long long)lm.id);
+        SGX_TRY(finish_lengths(e, *c, *s, *lm.m));
+        lm.lens = lm.m->lengths;
+        lm.bytes = lm.m->out_bytes;
+    }
+    if (e->comm_broken) return fail_msg(SGX_ERR_STATE, "the communicator was aborted after an exchange failure");
+    const bool collective = e->comm || e->host_comm;
+    if (P > 1 && !collective) return fail_msg(SGX_ERR_STATE, "sgx_comm_init was not called (world of %d ranks)", P);
+    hipStream_t st = collective ? e->s_comm : c->st;
     hipEvent_t a0 = e->ev(), a1 = e->ev(), a2 = e->ev(), a3 = e->ev();
-    if (e->comm) {
-        SGX_TRY(e->ag_send.ensure(row * 8));
-        SGX_TRY(e->ag_recv.ensure(row * 8 * (size_t)P));
-        HIP_TRY(hipEventRecord(a0, st));
-        HIP_TRY(hipMemcpyAsync(e->ag_send.p, agh, row * 8, hipMemcpyHostToDevice, st));
-        NCCL_TRY(ncclAllGather(e->ag_send.p, e->ag_recv.p, row, ncclInt64, e->comm, st));
-        HIP_TRY(hipMemcpyAsync(agh + row, e->ag_recv.p, row * 8 * (size_t)P, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipEventRecord(a1, st));
-        SGX_TRY(comm_wait(e));  // also drains the previous round's all-to-all (one stream, one order)
+    HIP_TRY(hipEventRecord(a0, st));
+    // (1) who holds which maps, and their lengths
+    std::vector<int64_t> counts((size_t)P, 0);
+    std::vector<int64_t> ids, lens;  // [M], [M][R], source-rank-major
+    std::vector<int32_t> srcs;
+    const size_t row = (size_t)R + 1;
+    if (!collective) {
+        counts[0] = (int64_t)mine.size();
+        for (auto &lm : mine) {
+            ids.push_back(lm.id);
+            srcs.push_back(0);
+            lens.insert(lens.end(), lm.lens.begin(), lm.lens.end());
+        }
     } else {
-        SGX_TRY(comm_wait(e));
-        HIP_TRY(hipEventRecord(a0, st));
-        if (e->hc.allgather(e->hc.user, agh, (int64_t)(row * 8), agh + row) != 0)
-            return fail_msg(SGX_ERR_COMM, "host all-gather of the partition lengths failed");
-        HIP_TRY(hipEventRecord(a1, st));
+        const int64_t nloc = (int64_t)mine.size();
+        SGX_TRY(allgather_i64(e, &nloc, 1, counts.data()));
+        int64_t mmax = 0;
+        for (int64_t v : counts) mmax = std::max(mmax, v);
+        if (mmax > 0) {
+            std::vector<int64_t> send(row * (size_t)mmax, 0), recv(row * (size_t)mmax * (size_t)P, 0);
+            for (size_t k = 0; k < mine.size(); ++k) {
+                send[k * row] = mine[k].id;
+                std::memcpy(&send[k * row + 1], mine[k].lens.data(), sizeof(int64_t) * (size_t)R);
+            }
+            SGX_TRY(allgather_i64(e, send.data(), send.size(), recv.data()));
+            for (int32_t j = 0; j < P; ++j)
+                for (int64_t k = 0; k < counts[(size_t)j]; ++k) {
+                    const int64_t *q = &recv[((size_t)j * (size_t)mmax + (size_t)k) * row];
+                    ids.push_back(q[0]);
+                    srcs.push_back(j);
+                    lens.insert(lens.end(), q + 1, q + 1 + R);
+                }
+        }
     }
-    for (int32_t j = 0; j < P; ++j) {
-        rd->map_ids[(size_t)j] = agh[row * (size_t)(j + 1)];
-        std::memcpy(&rd->lens[(size_t)j * R], agh + row * (size_t)(j + 1) + 1, sizeof(int64_t) * (size_t)R);
+    HIP_TRY(hipEventRecord(a1, st));
+    const size_t M = ids.size();
+    {
+        std::vector<int64_t> sorted_ids(ids);
+        std::sort(sorted_ids.begin(), sorted_ids.end());
+        if (std::adjacent_find(sorted_ids.begin(), sorted_ids.end()) != sorted_ids.end())
+            return fail_msg(SGX_ERR_INVALID, "an exchange round of shuffle %d carries a map id twice", s->id);
     }
-    // (2) placement (the same on every rank: it depends on the all-gathered lengths only) and
-    //     plan: send/recv counts and displacements (no copy list: blocks stay where they land)
-    std::vector<int32_t> bounds((size_t)P + 1);
-    if (s->placement.load() == SGX_PLACE_BYTES)
-        SGX_TRY(sgx_balanced_ranges(rd->lens.data(), P, R, bounds.data()));
-    else
-        SGX_TRY(sgx_even_ranges(P, R, bounds.data()));
+    // (2) placement: the shuffle's reducer ranges, fixed by its first round (the same on
+    //     every rank: it depends on the all-gathered lengths only)
+    std::vector<int32_t> bounds;
+    {
+        std::lock_guard<std::mutex> sl(s->mu);
+        bounds = s->place_bounds;
+    }
+    if (bounds.size() != (size_t)P + 1) {
+        bounds.assign((size_t)P + 1, 0);
+        if (s->placement.load() == SGX_PLACE_BYTES && M > 0) {
+            std::vector<int64_t> per_rank((size_t)P * R, 0);  // [P][R]: each rank's maps summed
+            for (size_t m = 0; m < M; ++m)
+                for (int32_t r = 0; r < R; ++r) per_rank[(size_t)srcs[m] * R + r] += lens[m * R + r];
+            SGX_TRY(sgx_balanced_ranges(per_rank.data(), P, R, bounds.data()));
+        } else {
+            SGX_TRY(sgx_even_ranges(P, R, bounds.data()));
+        }
+        std::lock_guard<std::mutex> sl(s->mu);
+        if (s->place_bounds.empty()) s->place_bounds = bounds;
+        bounds = s->place_bounds;
+    }
+    auto rd = std::make_shared<Round>();
+    rd->map_ids = ids;
+    rd->src = srcs;
+    rd->lens = lens;
     rd->r0 = bounds[(size_t)e->rank];
     rd->r1 = bounds[(size_t)e->rank + 1];
     const int32_t nmine = rd->r1 - rd->r0;
     std::vector<int64_t> sc(P), sd(P), rc(P), rdp(P);
-    int64_t nitems = 0;
-    SGX_TRY(sgx_plan_exchange_ranges(rd->lens.data(), P, R, e->rank, bounds.data(), 0, sc.data(), sd.data(), rc.data(),
-                                     rdp.data(), nullptr, &nitems));
-    if (sd[(size_t)P - 1] + sc[(size_t)P - 1] != out_bytes)
-        return fail_msg(SGX_ERR_HIP, "internal error: send plan covers %lld of %lld bytes",
-                        (long long)(sd[(size_t)P - 1] + sc[(size_t)P - 1]), (long long)out_bytes);
-    int64_t total_recv = 0;
+    rd->block_off.assign(M * (size_t)nmine, 0);
+    SGX_TRY(sgx_plan_exchange_maps(lens.data(), counts.data(), P, R, e->rank, bounds.data(), sc.data(), sd.data(),
+                                   rc.data(), rdp.data(), rd->block_off.data()));
+    int64_t out_total = 0, total_recv = 0;
+    for (auto &lm : mine) out_total += lm.bytes;
     for (int32_t j = 0; j < P; ++j) total_recv += rc[(size_t)j];
-    rd->block_off.assign((size_t)P * nmine, 0);
-    for (int32_t j = 0; j < P; ++j) {
-        int64_t off = rdp[(size_t)j];
-        for (int32_t r = rd->r0; r < rd->r1; ++r) {
-            rd->block_off[(size_t)j * nmine + (size_t)(r - rd->r0)] = off;
-            off += rd->lens[(size_t)j * R + r];
-        }
-    }
-    // A round with the same source maps replaces the previous one (a re-attempt): reuse
-    // its HBM when nobody else still reads it.
+    if (sd[(size_t)P - 1] + sc[(size_t)P - 1] != out_total)
+        return fail_msg(SGX_ERR_HIP, "internal error: send plan covers %lld of %lld bytes",
+                        (long long)(sd[(size_t)P - 1] + sc[(size_t)P - 1]), (long long)out_total);
+    // A round with the same maps replaces the previous one (a re-run): reuse its HBM when
+    // nobody else still reads it.
     {
         std::lock_guard<std::mutex> sl(s->mu);
         for (auto it = s->rounds.begin(); it != s->rounds.end(); ++it) {
             if ((*it)->map_ids == rd->map_ids) {
-                if (it->use_count() == 1) {
+                if (it->use_count() == 1 && (*it)->alias.empty()) {
                     HIP_TRY((*it)->done.wait_host());
                     rd->data.swap((*it)->data);
                 }
@@ -215,43 +256,132 @@ extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
             }
         }
     }
-    // (3) all-to-all of the partition-contiguous map output (already destination-grouped):
-    //     no pack step before, no regroup after
-    SGX_TRY(rd->data.ensure((size_t)total_recv));
-    HIP_TRY(hipStreamWaitEvent(st, m->done.ev, 0));
-    const void *view = m->view();
-    if (e->comm) {
-        std::vector<size_t> scz(P), sdz(P), rcz(P), rdz(P);
-        for (int32_t j = 0; j < P; ++j) {
-            scz[(size_t)j] = (size_t)sc[(size_t)j];
-            sdz[(size_t)j] = (size_t)sd[(size_t)j];
-            rcz[(size_t)j] = (size_t)rc[(size_t)j];
-            rdz[(size_t)j] = (size_t)rdp[(size_t)j];
+    // (3) the bytes.  Piece (my map k, destination d) = map k's reducers [bounds[d],
+    //     bounds[d+1]), contiguous in the partition-contiguous map output.
+    auto piece = [&](size_t k, int32_t d, int64_t *off, int64_t *len) {
+        int64_t o = 0, l = 0;
+        for (int32_t r = 0; r < bounds[(size_t)d]; ++r) o += mine[k].lens[(size_t)r];
+        for (int32_t r = bounds[(size_t)d]; r < bounds[(size_t)d + 1]; ++r) l += mine[k].lens[(size_t)r];
+        *off = o;
+        *len = l;
+    };
+    if (!collective) {
+        // one rank, no communicator: the blocks are the map outputs themselves
+        rd->r0 = 0;
+        rd->r1 = R;
+        for (size_t k = 0; k < M; ++k) {
+            rd->alias.push_back(mine[k].m);
+            int64_t o = 0;
+            for (int32_t r = 0; r < R; ++r) {
+                rd->block_off[k * (size_t)R + (size_t)r] = o;
+                o += mine[k].lens[(size_t)r];
+            }
         }
         HIP_TRY(hipEventRecord(a2, st));
-        NCCL_TRY(ncclAllToAllv(view, scz.data(), sdz.data(), rd->data.p, rcz.data(), rdz.data(), ncclUint8, e->comm, st));
-        HIP_TRY(hipEventRecord(a3, st));
     } else {
-        // host backend: stage the map output out, exchange on the host, stage the blocks in
-        SGX_TRY(e->x_send.ensure((size_t)std::max<int64_t>(out_bytes, 16)));
-        SGX_TRY(e->x_recv.ensure((size_t)std::max<int64_t>(total_recv, 16)));
+        SGX_TRY(rd->data.ensure((size_t)std::max<int64_t>(total_recv, 16)));
+        for (auto &lm : mine) HIP_TRY(hipStreamWaitEvent(st, lm.m->done.ev, 0));
         HIP_TRY(hipEventRecord(a2, st));
-        if (out_bytes > 0) HIP_TRY(hipMemcpyAsync(e->x_send.p, view, (size_t)out_bytes, hipMemcpyDeviceToHost, st));
-        HIP_TRY(hipStreamSynchronize(st));
-        if (e->hc.alltoallv(e->hc.user, e->x_send.p, sc.data(), sd.data(), e->x_recv.p, rc.data(), rdp.data()) != 0)
-            return fail_msg(SGX_ERR_COMM, "host all-to-all of the map output failed");
-        if (total_recv > 0)
-            HIP_TRY(hipMemcpyAsync(rd->data.p, e->x_recv.p, (size_t)total_recv, hipMemcpyHostToDevice, st));
-        HIP_TRY(hipEventRecord(a3, st));
-        HIP_TRY(hipStreamSynchronize(st));  // the pinned staging buffers are reused next round
+        if (e->comm) {
+            // grouped point-to-point: my sends to d go map after map, and d posts its receives
+            // from me in the same order (it knows my map count and lengths from (1))
+            NCCL_TRY(ncclGroupStart());
+            for (int32_t d = 0; d < P; ++d)
+                for (size_t k = 0; k < mine.size(); ++k) {
+                    int64_t o, l;
+                    piece(k, d, &o, &l);
+                    if (l > 0)
+                        NCCL_TRY(ncclSend((const char *)mine[k].m->view() + o, (size_t)l, ncclUint8, d, e->comm, st));
+                }
+            size_t m = 0;
+            for (int32_t j = 0; j < P; ++j) {
+                int64_t off = rdp[(size_t)j];
+                for (int64_t k = 0; k < counts[(size_t)j]; ++k, ++m) {
+                    int64_t l = 0;
+                    for (int32_t r = rd->r0; r < rd->r1; ++r) l += lens[m * R + r];
+                    if (l > 0) NCCL_TRY(ncclRecv((char *)rd->data.p + off, (size_t)l, ncclUint8, j, e->comm, st));
+                    off += l;
+                }
+            }
+            NCCL_TRY(ncclGroupEnd());
+        } else {
+            // host backend: stage my pieces out packed [destination][map], exchange on the
+            // host, stage the received bytes in
+            SGX_TRY(e->x_send.ensure((size_t)std::max<int64_t>(out_total, 16)));
+            SGX_TRY(e->x_recv.ensure((size_t)std::max<int64_t>(total_recv, 16)));
+            int64_t pos = 0;
+            for (int32_t d = 0; d < P; ++d)
+                for (size_t k = 0; k < mine.size(); ++k) {
+                    int64_t o, l;
+                    piece(k, d, &o, &l);
+                    if (l > 0)
+                        HIP_TRY(hipMemcpyAsync((char *)e->x_send.p + pos, (const char *)mine[k].m->view() + o,
+                                               (size_t)l, hipMemcpyDeviceToHost, st));
+                    pos += l;
+                }
+            HIP_TRY(hipStreamSynchronize(st));
+            if (e->hc.alltoallv(e->hc.user, e->x_send.p, sc.data(), sd.data(), e->x_recv.p, rc.data(), rdp.data()) != 0)
+                return fail_msg(SGX_ERR_COMM, "host all-to-all of the map outputs failed");
+            if (total_recv > 0)
+                HIP_TRY(hipMemcpyAsync(rd->data.p, e->x_recv.p, (size_t)total_recv, hipMemcpyHostToDevice, st));
+            HIP_TRY(hipStreamSynchronize(st));  // the pinned staging buffers are reused next round
+        }
     }
+    HIP_TRY(hipEventRecord(a3, st));
     HIP_TRY(rd->done.record(st));
-    HIP_TRY(m->read_done.record(st));
+    for (auto &lm : mine) {
+        std::lock_guard<std::mutex> lk(lm.m->mu);
+        if (collective) HIP_TRY(lm.m->read_done.record(st));
+        lm.m->exchanged = true;
+    }
     e->record_stage(SGX_STAGE_ALLGATHER, a0, a1);
     e->record_stage(SGX_STAGE_ALLTOALL, a2, a3);
     std::lock_guard<std::mutex> sl(s->mu);
     s->rounds.push_back(std::move(rd));
     return SGX_OK;
+}
+
+extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id) {
+    sgx::TraceRange trace_("sgx_exchange");
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
+    if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
+    std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
+    if (!s) return SGX_ERR_STATE;
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    // every committed map output no earlier round carried, in map id order (snapshot now:
+    // the call's place in the caller's program order decides what it carries)
+    std::vector<LocalMap> mine;
+    {
+        std::lock_guard<std::mutex> sl(s->mu);
+        for (auto &kv : s->maps) mine.push_back(LocalMap{kv.first, kv.second, {}, 0});
+    }
+    std::vector<LocalMap> take;
+    for (auto &lm : mine) {
+        std::lock_guard<std::mutex> lk(lm.m->mu);
+        if (lm.m->written && !lm.m->open && !lm.m->exchanged) take.push_back(std::move(lm));
+    }
+    return exchange_round(e, c, s, std::move(take));
+}
+
+extern "C" int sgx_exchange_maps(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t n) {
+    sgx::TraceRange trace_("sgx_exchange_maps");
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
+    if (!e || n < 0 || (n > 0 && !map_ids)) return fail_msg(SGX_ERR_INVALID, "bad arguments");
+    std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
+    if (!s) return SGX_ERR_STATE;
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    std::vector<LocalMap> mine;
+    for (int64_t i = 0; i < n; ++i) {
+        std::shared_ptr<Shuffle> s2;
+        std::shared_ptr<MapOut> m;
+        SGX_TRY(find_map(e, shuffle_id, map_ids[i], &s2, &m));
+        mine.push_back(LocalMap{map_ids[i], m, {}, 0});
+    }
+    return exchange_round(e, c, s, std::move(mine));
 }
 
 extern "C" int sgx_copy_items(sgx_engine *e, const void *src, void *dst, const int64_t *items, int64_t n_items,
@@ -286,4 +416,16 @@ extern "C" int sgx_round_reducers(sgx_engine *e, int32_t shuffle_id, int64_t map
             }
     return fail_msg(SGX_ERR_NOT_FOUND, "no exchange round of shuffle %d carried map %lld", shuffle_id,
                     (long long)map_id);
+}
+
+extern "C" int sgx_shuffle_reducers(sgx_engine *e, int32_t shuffle_id, int32_t *r0, int32_t *r1) {
+    if (!e || !r0 || !r1) return fail_msg(SGX_ERR_INVALID, "NULL argument");
+    std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
+    if (!s) return SGX_ERR_STATE;
+    std::lock_guard<std::mutex> sl(s->mu);
+    if (s->place_bounds.size() != (size_t)e->nranks + 1)
+        return fail_msg(SGX_ERR_STATE, "shuffle %d has not been exchanged yet", shuffle_id);
+    *r0 = s->place_bounds[(size_t)e->rank];
+    *r1 = s->place_bounds[(size_t)e->rank + 1];
+    return SGX_OK;
 }

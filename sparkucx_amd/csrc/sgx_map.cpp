@@ -299,6 +299,7 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
     HIP_TRY(m->done.wait_host());
     if (m->read_done.ev) HIP_TRY(hipStreamWaitEvent(c->st, m->read_done.ev, 0));
     m->written = false;
+    m->exchanged = false;
     m->open = false;
     m->spills.clear();
     SGX_TRY(m->part_off.ensure((size_t)(s->R + 2) * 4));
@@ -331,6 +332,7 @@ extern "C" int sgx_map_begin(sgx_engine *e, int32_t shuffle_id, int64_t map_id) 
     HIP_TRY(m->done.wait_host());
     if (m->read_done.ev) HIP_TRY(m->read_done.wait_host());
     m->written = false;
+    m->exchanged = false;
     m->ready = false;
     m->open = true;
     m->spills.clear();

@@ -143,3 +143,52 @@ extern "C" int sgx_plan_exchange_ranges(const int64_t *L, int32_t P, int32_t R, 
         return sgx::fail_msg(SGX_ERR_INVALID, "item capacity %lld < %lld", (long long)cap, (long long)cnt);
     return SGX_OK;
 }
+
+// The per-shuffle exchange (sgx_exchange / sgx_exchange_maps): rank j contributes
+// maps_per_rank[j] maps, lengths [M][R] source-rank-major.  This rank's send to rank d is its
+// maps' bytes of d's reducers, map after map (packed [d][my map] at send_displs); what it
+// receives from rank j is j's maps' bytes of my reducers, map after map, at recv_displs[j];
+// block_off[M][nmine] is where block (map m, my reducer r) lands in the receive buffer.
+extern "C" int sgx_plan_exchange_maps(const int64_t *L, const int64_t *maps_per_rank, int32_t P, int32_t R,
+                                      int32_t rank, const int32_t *bounds, int64_t *send_counts,
+                                      int64_t *send_displs, int64_t *recv_counts, int64_t *recv_displs,
+                                      int64_t *block_off) {
+    if (!maps_per_rank || P < 1 || R < 1 || rank < 0 || rank >= P || !bounds || !send_counts || !send_displs ||
+        !recv_counts || !recv_displs)
+        return sgx::fail_msg(SGX_ERR_INVALID, "sgx_plan_exchange_maps: bad arguments");
+    if (bounds[0] != 0 || bounds[P] != R)
+        return sgx::fail_msg(SGX_ERR_INVALID, "sgx_plan_exchange_maps: ranges must cover [0, %d)", R);
+    for (int32_t j = 0; j < P; ++j)
+        if (bounds[j] > bounds[j + 1])
+            return sgx::fail_msg(SGX_ERR_INVALID, "sgx_plan_exchange_maps: ranges out of order at rank %d", j);
+    std::vector<int64_t> first((size_t)P + 1, 0);  // index of rank j's first map
+    for (int32_t j = 0; j < P; ++j) {
+        if (maps_per_rank[j] < 0) return sgx::fail_msg(SGX_ERR_INVALID, "sgx_plan_exchange_maps: negative map count");
+        first[(size_t)j + 1] = first[(size_t)j] + maps_per_rank[j];
+    }
+    const int64_t M = first[(size_t)P];
+    if (M > 0 && !L) return sgx::fail_msg(SGX_ERR_INVALID, "sgx_plan_exchange_maps: lengths are NULL");
+    for (int64_t i = 0; i < M * R; ++i)
+        if (L[i] < 0) return sgx::fail_msg(SGX_ERR_INVALID, "sgx_plan_exchange_maps: negative length");
+    int64_t run = 0;
+    for (int32_t d = 0; d < P; ++d) {
+        int64_t c = 0;
+        for (int64_t m = first[(size_t)rank]; m < first[(size_t)rank + 1]; ++m)
+            for (int32_t r = bounds[d]; r < bounds[d + 1]; ++r) c += L[m * R + r];
+        send_counts[d] = c;
+        send_displs[d] = run;
+        run += c;
+    }
+    const int32_t r0 = bounds[rank], r1 = bounds[rank + 1], nmine = r1 - r0;
+    run = 0;
+    for (int32_t j = 0; j < P; ++j) {
+        recv_displs[j] = run;
+        for (int64_t m = first[(size_t)j]; m < first[(size_t)j + 1]; ++m)
+            for (int32_t r = r0; r < r1; ++r) {
+                if (block_off) block_off[m * nmine + (r - r0)] = run;
+                run += L[m * R + r];
+            }
+        recv_counts[j] = run - recv_displs[j];
+    }
+    return SGX_OK;
+}

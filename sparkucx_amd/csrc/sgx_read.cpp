@@ -48,9 +48,7 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
             if (r < rd.r0 || r >= rd.r1) continue;
             for (size_t j = 0; j < rd.map_ids.size(); ++j) {
                 if (rd.map_ids[j] != mid) continue;
-                const int32_t nmine = rd.r1 - rd.r0;
-                srcs[(size_t)i] = Src{(const char *)rd.base() + rd.block_off[j * (size_t)nmine + (size_t)(r - rd.r0)],
-                                      rd.lens[j * (size_t)s.R + (size_t)r], rd.done.ev};
+                srcs[(size_t)i] = Src{rd.block_ptr(j, r), rd.lens[j * (size_t)s.R + (size_t)r], rd.done.ev};
                 found = true;
                 break;
             }

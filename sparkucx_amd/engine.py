@@ -154,6 +154,13 @@ class ShuffleEngine:
             raise _lib.IllegalArgumentException(f"unknown placement {placement!r} (even, bytes)")
         check(lib().sgx_set_reducer_placement(self.handle, shuffle_id, codes[placement]), "setReducerPlacement")
 
+    def shuffle_reducers(self, shuffle_id: int) -> Tuple[int, int]:
+        """[r0, r1): the reducers this rank holds for the shuffle (fixed by its first exchange)."""
+        r0, r1 = ctypes.c_int32(0), ctypes.c_int32(0)
+        check(lib().sgx_shuffle_reducers(self.handle, shuffle_id, ctypes.byref(r0), ctypes.byref(r1)),
+              "shuffleReducers")
+        return r0.value, r1.value
+
     def round_reducers(self, shuffle_id: int, map_id: int) -> Tuple[int, int]:
         """[r0, r1): the reducers this rank holds for the exchange round that carried map_id."""
         r0, r1 = ctypes.c_int32(0), ctypes.c_int32(0)
@@ -310,8 +317,16 @@ class ShuffleEngine:
         check(lib().sgx_comm_init_host(self.handle, nranks, rank, ctypes.byref(binding.struct)), "comm_init_host")
         self._host_comm = binding  # the callbacks must outlive the engine's use of them
 
-    def exchange(self, shuffle_id: int, map_id: int):
-        check(lib().sgx_exchange(self.handle, shuffle_id, map_id), "exchange")
+    def exchange(self, shuffle_id: int, map_ids: Optional[Sequence[int]] = None):
+        """The shuffle's exchange (collective, every rank calls it): with ``map_ids`` None, every
+        committed map output of the shuffle this rank holds that no earlier exchange carried
+        (sgx_exchange); otherwise exactly those local maps (sgx_exchange_maps, may be empty)."""
+        if map_ids is None:
+            check(lib().sgx_exchange(self.handle, shuffle_id), "exchange")
+            return
+        m = np.ascontiguousarray([int(x) for x in map_ids], dtype=np.int64)
+        check(lib().sgx_exchange_maps(self.handle, shuffle_id, m.ctypes.data if len(m) else None, len(m)),
+              "exchange")
 
     def fetch_blocks(self, shuffle_id: int, map_ids: Sequence[int], reduce_ids: Sequence[int], dst=None,
                      dst_cap: Optional[int] = None):
@@ -501,6 +516,24 @@ def plan_exchange(lengths_all: np.ndarray, rank: int, item_bytes: int = 0, bound
     items = np.zeros((max(n.value, 1), 3), np.int64)
     call(items.ctypes.data, ctypes.c_int64(n.value))
     return sc, sd, rc, rd, items[: n.value]
+
+
+def plan_exchange_maps(lengths_all: np.ndarray, maps_per_rank, rank: int, bounds=None):
+    """Pure-host plan of the per-shuffle exchange (sgx_plan_exchange_maps): ``lengths_all``
+    [M][R] of every rank's maps, source-rank-major, ``maps_per_rank`` [P].  Returns
+    (send_counts, send_displs, recv_counts, recv_displs, block_off[M][nmine])."""
+    L = np.ascontiguousarray(lengths_all, dtype=np.int64)
+    cnt = np.ascontiguousarray(maps_per_rank, dtype=np.int64)
+    P = len(cnt)
+    R = L.shape[1]  # lengths_all is [M][R], M may be 0
+    b = even_ranges(P, R) if bounds is None else np.ascontiguousarray(bounds, dtype=np.int32)
+    nmine = int(b[rank + 1] - b[rank])
+    sc, sd, rc, rd = (np.zeros(P, np.int64) for _ in range(4))
+    bo = np.zeros((max(len(L), 1), max(nmine, 1)), np.int64)
+    check(lib().sgx_plan_exchange_maps(L.ctypes.data if L.size else None, cnt.ctypes.data, P, R, rank, b.ctypes.data,
+                                       sc.ctypes.data, sd.ctypes.data, rc.ctypes.data, rd.ctypes.data, bo.ctypes.data),
+          "plan_exchange_maps")
+    return sc, sd, rc, rd, bo[: len(L), :nmine]
 
 
 def even_ranges(P: int, R: int) -> np.ndarray:

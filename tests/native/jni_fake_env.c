@@ -112,7 +112,7 @@ jlongArray Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_fetchBlocks(JNIEnv *,
 jbyteArray Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_bootstrapJoin(JNIEnv *, jclass, jstring, jint, jint, jint,
                                                                         jintArray);
 void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_bootstrapServe(JNIEnv *, jclass, jint, jint, jbyteArray, jint);
-void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchange(JNIEnv *, jclass, jlong, jint, jlong);
+void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchange(JNIEnv *, jclass, jlong, jint);
 
 static obj *jstr(const char *s) {
     obj *o = (obj *)calloc(1, sizeof(obj));
@@ -160,7 +160,7 @@ int fake_fetch_mismatched(int64_t engine) {
 }
 
 int fake_exchange(int64_t engine) {
-    Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchange(&g_env, NULL, engine, 1, 0);
+    Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchange(&g_env, NULL, engine, 1);
     return 0;
 }
 

@@ -451,7 +451,7 @@ def test_exchange_single_rank_over_rccl(sgx_lib, oracle_lib):
         e.register_shuffle(1, R)
         recs = oracle_lib.gen_uniform16(400_000, 21)
         e.write_map(1, 6, recs, len(recs), 16, R)
-        e.exchange(1, 6)
+        e.exchange(1)
         e.sync()
         data, lens = e.fetch_blocks(1, [6] * R, list(range(R)))
         out, counts = oracle_lib.map_write(recs, R)

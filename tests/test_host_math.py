@@ -101,3 +101,53 @@ def test_plan_with_ranges_is_consistent(sgx_lib):
     bb = sgx_lib.balanced_ranges(L)
     recv_bal = [L[:, a:b].sum() for a, b in zip(bb[:-1], bb[1:])]
     assert max(recv_bal) < 0.5 * max(recv_even)
+
+
+def test_plan_exchange_maps_simulated_all_to_all(sgx_lib):
+    """sgx_plan_exchange_maps (the per-shuffle exchange's plan, any number of maps per rank,
+    0 included) simulated end to end on the host: every rank packs its maps' pieces
+    [destination][map] at its send displacements, the all-to-all moves them, and every block
+    (map m, my reducer r) found at block_off is exactly that map's partition r."""
+    rng = np.random.default_rng(11)
+    for trial in range(60):
+        P = int(rng.integers(1, 7))
+        R = int(rng.integers(1, 40))
+        counts = rng.integers(0, 4, P)
+        if trial % 7 == 0:
+            counts[:] = 0
+        M = int(counts.sum())
+        L = rng.integers(0, 5, (M, R)).astype(np.int64)
+        L[rng.random((M, R)) < 0.3] = 0
+        first = np.concatenate([[0], np.cumsum(counts)])
+        # map m's partition-contiguous output: byte value = (m * 37 + r) mod 251 per partition
+        outs = [np.concatenate([np.full(L[m, r], (m * 37 + r) % 251, np.uint8) for r in range(R)])
+                if L[m].sum() else np.zeros(0, np.uint8) for m in range(M)]
+        bounds = sgx_lib.balanced_ranges(
+            np.stack([L[first[j]:first[j + 1]].sum(0) for j in range(P)])) if trial % 2 else \
+            sgx_lib.even_ranges(P, R)
+        plans = [sgx_lib.plan_exchange_maps(L.reshape(M, R), counts, k, bounds) for k in range(P)]
+        sends = []
+        for j, (sc, sd, _, _, _) in enumerate(plans):
+            buf = np.zeros(int(sc.sum()), np.uint8)
+            for d in range(P):
+                pos = int(sd[d])
+                for m in range(first[j], first[j + 1]):
+                    o = int(L[m, :bounds[d]].sum())
+                    ln = int(L[m, bounds[d]:bounds[d + 1]].sum())
+                    buf[pos:pos + ln] = outs[m][o:o + ln]
+                    pos += ln
+                assert pos == int(sd[d] + sc[d])
+            sends.append(buf)
+        for k, (sc, sd, rc, rd, bo) in enumerate(plans):
+            recv = np.zeros(int(rc.sum()), np.uint8)
+            for j in range(P):
+                sj_c, sj_d = plans[j][0], plans[j][1]
+                assert rc[j] == sj_c[k]
+                recv[rd[j]:rd[j] + rc[j]] = sends[j][sj_d[k]:sj_d[k] + sj_c[k]]
+            r0, r1 = int(bounds[k]), int(bounds[k + 1])
+            assert bo.shape == (M, r1 - r0)
+            for m in range(M):
+                po = np.concatenate([[0], np.cumsum(L[m])])
+                for r in range(r0, r1):
+                    got = recv[bo[m, r - r0]:bo[m, r - r0] + L[m, r]]
+                    assert np.array_equal(got, outs[m][po[r]:po[r + 1]]), (trial, k, m, r)

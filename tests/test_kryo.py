@@ -257,7 +257,7 @@ def test_gpu_kryo_exchange_single_rank(engine, oracle_lib):
     o = oracle_lib.offsets(counts)
     sid, lengths = _kryo_map(engine, recs, R, map_id=4)
     try:
-        engine.exchange(sid, 4)
+        engine.exchange(sid)
         engine.sync()
         data, lens = engine.fetch_blocks(sid, [4, 4], [31, 0])
         want = np.concatenate([oracle_lib.kryo_serialize(out[o[31]:o[32]]), oracle_lib.kryo_serialize(out[o[0]:o[1]])])
