@@ -8,9 +8,12 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
+#include <atomic>
 #include <cerrno>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -42,7 +45,10 @@ static int64_t load_be64(const uint8_t *p) {
     return (int64_t)u;
 }
 
-// checkIndexAndDataFile (:110-149): lengths if index and data agree, else false.
+// checkIndexAndDataFile (:110-149): lengths if index and data agree, else false.  The rules
+// are exactly Spark's: (blocks + 1) longs, the first 0, and the data file as long as the sum of
+// the lengths (offset differences, summed with Long wrap-around) -- a decreasing offset, i.e. a
+// negative length, is NOT rejected on its own, as the reference does not reject it.
 static bool check_index_and_data(const char *index_path, const char *data_path, int32_t blocks,
                                  std::vector<int64_t> &lengths) {
     const int64_t isz = file_size(index_path);
@@ -52,17 +58,31 @@ static bool check_index_and_data(const char *index_path, const char *data_path, 
     int64_t off = load_be64(idx.data());
     if (off != 0) return false;
     lengths.assign((size_t)blocks, 0);
-    int64_t sum = 0;
+    uint64_t sum = 0;  // Scala's lengths.sum wraps like uint64
     for (int32_t i = 0; i < blocks; ++i) {
         const int64_t nx = load_be64(idx.data() + 8 * (size_t)(i + 1));
-        if (nx < off) return false;  // a negative length: corrupt
-        lengths[(size_t)i] = nx - off;
-        sum += nx - off;
+        lengths[(size_t)i] = (int64_t)((uint64_t)nx - (uint64_t)off);
+        sum += (uint64_t)lengths[(size_t)i];
         off = nx;
     }
     const int64_t dsz = file_size(data_path);
-    return dsz >= 0 && dsz == sum;
+    return dsz >= 0 && (uint64_t)dsz == sum;
 }
+
+// Utils.tempFileWith (the reference's writeIndexFileAndCommit, :167): `<path>.<unique>`, so two
+// attempts of one map -- each with its own map output object -- never share a temp file.
+static std::string temp_file_with(const char *path) {
+    static std::atomic<uint64_t> seq{0};
+    const uint64_t t = (uint64_t)std::chrono::steady_clock::now().time_since_epoch().count();
+    char suffix[96];
+    snprintf(suffix, sizeof suffix, ".%d.%llu.%llx", (int)getpid(), (unsigned long long)seq.fetch_add(1),
+             (unsigned long long)(t * 0x9E3779B97F4A7C15ull));
+    return std::string(path) + suffix;
+}
+
+// "There is only one IndexShuffleBlockResolver per executor, this synchronization make sure
+// the following check and rename are atomic" (:170-171): one lock per process (= executor).
+static std::mutex g_commit_mu;
 
 extern "C" int sgx_check_index_and_data(const char *index_path, const char *data_path, int32_t blocks,
                                         int64_t *out_lengths) {
@@ -122,10 +142,14 @@ int sgx::commit_index_files(const char *index_path, const char *data_path, int32
     }
     if (sum != bytes) return fail_msg(SGX_ERR_INVALID, "lengths sum to %lld, data holds %lld", (long long)sum,
                                       (long long)bytes);
-    const std::string data_tmp = std::string(data_path) + ".sgx.tmp";
-    const std::string index_tmp = std::string(index_path) + ".sgx.tmp";
-    // map output -> data tmp (dataTmp of writeIndexFileAndCommit)
-    if (int rc0 = write_all(data_tmp.c_str(), data, (size_t)bytes)) return rc0;
+    const std::string data_tmp = temp_file_with(data_path);
+    const std::string index_tmp = temp_file_with(index_path);
+    // map output -> data tmp (dataTmp of writeIndexFileAndCommit, written before the lock)
+    if (int rc0 = write_all(data_tmp.c_str(), data, (size_t)bytes)) {
+        unlink(data_tmp.c_str());
+        return rc0;
+    }
+    std::lock_guard<std::mutex> lk(g_commit_mu);
     std::vector<int64_t> existing;
     if (check_index_and_data(index_path, data_path, R, existing)) {
         // another attempt already committed: use its lengths, drop our data
@@ -145,6 +169,7 @@ int sgx::commit_index_files(const char *index_path, const char *data_path, int32
     }
     int rc = write_all(index_tmp.c_str(), idx.data(), idx.size());
     if (rc) {
+        unlink(index_tmp.c_str());
         unlink(data_tmp.c_str());
         return rc;
     }

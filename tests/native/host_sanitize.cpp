@@ -148,7 +148,9 @@ static void index_checks(const std::string &dir) {
     std::vector<int64_t> neg = {-16, 112, 0, 0, 0};
     CHECK(sgx::commit_index_files(idx.c_str(), dat.c_str(), 5, neg.data(), data.data(), 96, out.data()) ==
           SGX_ERR_INVALID);
-    // an index with a decreasing offset is corrupt: replaced by the next attempt
+    // a decreasing offset (a negative length) whose lengths still sum to the data size is
+    // VALID for Spark (checkIndexAndDataFile only checks the count, off[0] == 0 and the sum,
+    // IndexShuffleBlockResolver.scala:110-149): the existing attempt still wins
     FILE *f = std::fopen(idx.c_str(), "r+b");
     CHECK(f != nullptr);
     if (f) {
@@ -157,9 +159,66 @@ static void index_checks(const std::string &dir) {
         std::fwrite(big, 1, 8, f);
         std::fclose(f);
     }
+    CHECK(sgx_check_index_and_data(idx.c_str(), dat.c_str(), 5, chk.data()) == SGX_OK);
+    CHECK(chk[1] > 0 && chk[2] < 0 && chk[0] + chk[1] + chk[2] + chk[3] + chk[4] == 96);
+    std::vector<int64_t> won(chk);
+    CHECK(sgx::commit_index_files(idx.c_str(), dat.c_str(), 5, other.data(), data.data(), 96, out.data()) == SGX_OK);
+    CHECK(out == won);
+    // a first offset != 0 is corrupt: replaced by the next attempt
+    f = std::fopen(idx.c_str(), "r+b");
+    if (f) {
+        uint8_t one[8] = {0, 0, 0, 0, 0, 0, 0, 1};
+        std::fwrite(one, 1, 8, f);
+        std::fclose(f);
+    }
     CHECK(sgx_check_index_and_data(idx.c_str(), dat.c_str(), 5, chk.data()) == SGX_ERR_NOT_FOUND);
     CHECK(sgx::commit_index_files(idx.c_str(), dat.c_str(), 5, other.data(), data.data(), 96, out.data()) == SGX_OK);
     CHECK(out == other);
+    // concurrent attempts of one map (Utils.tempFileWith names + the executor-wide commit lock):
+    // exactly one wins, every attempt reports the winner's lengths, the files hold the winner's
+    // bytes, and no temp file is left behind
+    const std::string idx2 = dir + "/shuffle_0_7_0.index", dat2 = dir + "/shuffle_0_7_0.data";
+    const int T = 8;
+    std::vector<std::vector<int64_t>> att((size_t)T), got((size_t)T, std::vector<int64_t>(5, -1));
+    std::vector<std::vector<uint8_t>> bytes((size_t)T, std::vector<uint8_t>(96));
+    std::vector<int> rcs((size_t)T, -100);
+    for (int t = 0; t < T; ++t) {
+        att[(size_t)t] = {(int64_t)(16 * (t % 6)), 0, 0, 0, (int64_t)(96 - 16 * (t % 6))};
+        for (size_t i = 0; i < 96; ++i) bytes[(size_t)t][i] = (uint8_t)(t * 31 + i);
+    }
+    std::vector<std::thread> th;
+    for (int t = 0; t < T; ++t)
+        th.emplace_back([&, t] {
+            rcs[(size_t)t] = sgx::commit_index_files(idx2.c_str(), dat2.c_str(), 5, att[(size_t)t].data(),
+                                                     bytes[(size_t)t].data(), 96, got[(size_t)t].data());
+        });
+    for (auto &x : th) x.join();
+    std::vector<int64_t> fin(5, -1);
+    CHECK(sgx_check_index_and_data(idx2.c_str(), dat2.c_str(), 5, fin.data()) == SGX_OK);
+    for (int t = 0; t < T; ++t) {
+        CHECK(rcs[(size_t)t] == SGX_OK);
+        CHECK(got[(size_t)t] == fin);
+    }
+    int winners = 0;
+    for (int t = 0; t < T; ++t) {
+        if (att[(size_t)t] != fin) continue;
+        FILE *d = std::fopen(dat2.c_str(), "rb");
+        std::vector<uint8_t> on(96);
+        const bool same = d && std::fread(on.data(), 1, 96, d) == 96 && on == bytes[(size_t)t];
+        if (d) std::fclose(d);
+        winners += same ? 1 : 0;
+    }
+    CHECK(winners == 1);
+    const std::string ls = "ls -1 '" + dir + "' | grep -c 'shuffle_0_7_0\\.\\(index\\|data\\)\\.' > '" + dir +
+                           "/tmpcount' || true";
+    CHECK(std::system(ls.c_str()) == 0);
+    FILE *cf = std::fopen((dir + "/tmpcount").c_str(), "r");
+    int leftover = -1;
+    if (cf) {
+        if (std::fscanf(cf, "%d", &leftover) != 1) leftover = -1;
+        std::fclose(cf);
+    }
+    CHECK(leftover == 0);
 }
 
 static void bootstrap_checks() {

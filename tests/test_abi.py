@@ -164,3 +164,25 @@ def test_map_output_writer_contract(sgx_lib):
     with pytest.raises(sgx_lib.IllegalArgumentException, match="increasing order"):
         w.getPartitionWriter(1)
     assert w.commitAllPartitions().tolist() == [16, 0, 32]
+
+
+def test_check_index_accepts_decreasing_offsets_like_spark(sgx_lib, oracle_lib, tmp_path):
+    """IndexShuffleBlockResolver.checkIndexAndDataFile (:110-149) checks the long count, the
+    first offset and that the lengths sum to the data size -- nothing else.  An index with a
+    decreasing offset (a negative length) whose lengths still sum to the data file's size is
+    valid, for the engine as for the restatement (oracle/spark_semantics.py)."""
+    import struct
+
+    from oracle import spark_semantics as S
+
+    offs = [0, 64, 16, 80, 96]  # lengths 64, -48, 64, 16: sum 96
+    idxb = b"".join(struct.pack(">q", o) for o in offs)
+    idx, dat = tmp_path / "d.index", tmp_path / "d.data"
+    idx.write_bytes(idxb)
+    dat.write_bytes(b"\1" * 96)
+    out = np.zeros(4, np.int64)
+    assert sgx_lib.lib().sgx_check_index_and_data(str(idx).encode(), str(dat).encode(), 4, out.ctypes.data) == 0
+    assert out.tolist() == [64, -48, 64, 16] == S.check_index_and_data(idxb, 96, 4)
+    dat.write_bytes(b"\1" * 80)
+    assert sgx_lib.lib().sgx_check_index_and_data(str(idx).encode(), str(dat).encode(), 4, out.ctypes.data) != 0
+    assert S.check_index_and_data(idxb, 80, 4) is None
