@@ -338,18 +338,23 @@ int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, 
  *      rangeBounds initialiser, RangePartitioner.sketch and RangePartitioner.determineBounds;
  *      the partitioner is built where the dependency is, UcxShuffleManager.scala:50).
  * batches[i] (nrecords[i] records of record_bytes, memory kind mem_kind) is input partition i
- * of the RDD with id rdd_id; keys are signed Longs (16 B records) or 10-byte unsigned keys
- * (100 B records).  sampleSize = min(sample_points_per_partition * num_partitions, 1e6),
+ * of the RDD; keys are signed Longs (16 B records) or 10-byte unsigned keys (100 B records).
+ * sampleSize = min(sample_points_per_partition * num_partitions, 1e6),
  * k = ceil(3 * sampleSize / nbatches) keys per partition by reservoir sampling with
- * XORShiftRandom(byteswap32(i ^ (rdd_id << 16))) -- on the GPU, every record's draw in
- * parallel by GF(2) jump-ahead -- then determineBounds on the host.  Writes up to
- * num_partitions - 1 bounds (int64 or 10-byte keys) to out_bounds (host) and their count to
- * *out_nbounds (fewer when keys repeat; the shuffle then has *out_nbounds + 1 partitions).
- * SGX_ERR_UNSUPPORTED when a partition is imbalanced enough for Spark's re-sampling pass
- * (fraction * n > k), which this engine does not reproduce. */
+ * XORShiftRandom(byteswap32(i ^ (rdd_id << 16))) -- rdd_id is the id of rdd.map(_._1), the
+ * RDD sketch runs on -- on the GPU, every record's draw in parallel by GF(2) jump-ahead.  A
+ * partition with fraction * n > k (fraction = min(sampleSize / numItems, 1)) is re-sampled as
+ * Spark does: RDD.sample(false, fraction, byteswap32(-parent_rdd_id - 1)) over the imbalanced
+ * partitions (parent_rdd_id: the id of the pair RDD the partitioner is built from), i.e. per
+ * partition a BernoulliSampler seeded from java.util.Random's nextLong -- gap sampling on the
+ * host when fraction <= 0.4, one draw per record on the GPU otherwise -- weighted
+ * (1 / fraction).toFloat.  Then determineBounds on the host.  Writes up to num_partitions - 1
+ * bounds (int64 or 10-byte keys) to out_bounds (host) and their count to *out_nbounds (fewer
+ * when keys repeat; the shuffle then has *out_nbounds + 1 partitions). */
 int sgx_range_bounds(sgx_engine *e, const void *const *batches, const int64_t *nrecords, int32_t nbatches,
                      int32_t record_bytes, int32_t mem_kind, int32_t num_partitions, int32_t rdd_id,
-                     int32_t sample_points_per_partition, void *out_bounds, int32_t *out_nbounds);
+                     int32_t parent_rdd_id, int32_t sample_points_per_partition, void *out_bounds,
+                     int32_t *out_nbounds);
 
 /* ---- MemoryPool (memory/MemoryPool.scala:22-147): the BufferAllocator of the fetch contract
  *      (ShuffleTransport.scala:113).  Blocks come in power-of-two size classes from 4 KiB

@@ -336,6 +336,56 @@ class XORShiftRandom:
         return ((self.next(26) << 27) + self.next(27)) * (2.0 ** -53)
 
 
+class JavaRandom:
+    """java.util.Random (48-bit LCG): next(bits), nextInt(), nextLong()."""
+
+    MULT, MASK = 0x5DEECE66D, (1 << 48) - 1
+
+    def __init__(self, seed: int):
+        self.s = (seed ^ self.MULT) & self.MASK
+
+    def next(self, bits: int) -> int:
+        self.s = (self.s * self.MULT + 0xB) & self.MASK
+        return to_i32(self.s >> (48 - bits))  # (int)(seed >>> (48 - bits))
+
+    def next_int(self) -> int:
+        return self.next(32)
+
+    def next_long(self) -> int:
+        return to_i64((self.next(32) << 32) + self.next(32))
+
+
+def bernoulli_sample(items: Sequence, fraction: float, seed: int) -> list:
+    """BernoulliSampler(fraction) after setSeed(seed) (its rng is an XORShiftRandom): fraction
+    <= 0.4 (RandomSampler.defaultMaxGapSamplingFraction) uses GapSampling(f, rng, 5e-11) -- one
+    advance() when it is built (lazily, at the first sample()), then one per kept item, each
+    dropping (log(max(u, eps)) / log1p(-f)).toInt items; otherwise one nextDouble per item,
+    kept iff <= fraction."""
+    import math
+
+    rng = XORShiftRandom(seed)
+    if fraction <= 0.0:
+        return []
+    if fraction >= 1.0:
+        return list(items)
+    if fraction <= 0.4:
+        lnq = math.log1p(-fraction)
+
+        def advance():
+            g = math.log(max(rng.next_double(), 5e-11)) / lnq
+            return 2147483647 if g >= 2147483647.0 else int(g)  # Scala Double.toInt saturates
+
+        out, drop = [], advance()
+        for it in items:
+            if drop > 0:
+                drop -= 1
+            else:
+                drop = advance()
+                out.append(it)
+        return out
+    return [it for it in items if rng.next_double() <= fraction]
+
+
 def byteswap32(v: int) -> int:
     hc = (v * 0x9E3775CD) & M32
     hc = int.from_bytes(hc.to_bytes(4, "little"), "big")
@@ -358,13 +408,18 @@ def reservoir_sample_and_count(keys: Sequence, k: int, seed: int):
 
 
 def range_bounds(partitions_keys: Sequence[Sequence], num_partitions: int, rdd_id: int = 0,
-                 sample_points_per_partition: int = 20, lt=None):
-    """RangePartitioner.rangeBounds for input partitions given as key lists (no re-sampling
-    of imbalanced partitions: raises instead, as the engine does)."""
+                 sample_points_per_partition: int = 20, lt=None, parent_rdd_id: Optional[int] = None):
+    """RangePartitioner.rangeBounds for input partitions given as key lists.  ``rdd_id`` is the
+    id of rdd.map(_._1) (the RDD sketch runs on), ``parent_rdd_id`` the pair RDD's (default
+    rdd_id - 1), which seeds the re-sampling of imbalanced partitions:
+    new PartitionPruningRDD(rdd.map(_._1), imbalanced).sample(false, fraction,
+    byteswap32(-rdd.id - 1)) -- PartitionwiseSampledRDD gives every kept partition, in order,
+    the next nextLong() of java.util.Random(seed) for its BernoulliSampler."""
     import math
 
     if num_partitions <= 1 or not partitions_keys:
         return []
+    parent = rdd_id - 1 if parent_rdd_id is None else parent_rdd_id
     sample_size = min(float(sample_points_per_partition) * num_partitions, 1e6)
     k = int(math.ceil(3.0 * sample_size / len(partitions_keys)))
     sketched = []
@@ -376,13 +431,18 @@ def range_bounds(partitions_keys: Sequence[Sequence], num_partitions: int, rdd_i
     if num_items == 0:
         return []
     fraction = min(sample_size / max(num_items, 1), 1.0)
-    cand = []
+    cand, imbalanced = [], []
     for idx, n, sample in sketched:
         if fraction * n > k:
-            raise NotImplementedError("imbalanced partition: Spark re-samples it")
-        if sample:
+            imbalanced.append(idx)
+        elif sample:
             w = float(np_float32(n / len(sample)))
             cand.extend((key, w) for key in sample)
+    if imbalanced:
+        jr = JavaRandom(byteswap32(to_i32(-parent - 1)))
+        w = float(np_float32(1.0 / fraction))
+        for idx in imbalanced:
+            cand.extend((key, w) for key in bernoulli_sample(list(partitions_keys[idx]), fraction, jr.next_long()))
     return determine_bounds(cand, min(num_partitions, len(cand)), lt)
 
 

@@ -123,7 +123,7 @@ SIGNATURES = {
     "sgx_fetch_blocks": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i64, _vp, _i64, _i32, _vp]),
     "sgx_read_sorted": (ctypes.c_int, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i64, _i32, _vp]),
     "sgx_read_records": (ctypes.c_int, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i64, _i32, _vp]),
-    "sgx_range_bounds": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
+    "sgx_range_bounds": (ctypes.c_int, [_vp, _vp, _vp, _i32, _i32, _i32, _i32, _i32, _i32, _i32, _vp, _vp]),
     "sgx_bootstrap_serve": (ctypes.c_int, [_i32, _i32, _vp, _i32]),
     "sgx_bootstrap_join": (ctypes.c_int, [ctypes.c_char_p, _i32, _i32, _i32, _vp, _vp]),
     "sgx_read_grouped": (ctypes.c_int, [_vp, _i32, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _i64, _i64, _i32,

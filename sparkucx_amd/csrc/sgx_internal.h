@@ -125,6 +125,12 @@ hipError_t launch_pack_pairs(const int64_t *keys, const int64_t *vals, int64_t n
 int64_t reservoir_threads(int64_t n, int64_t k);
 hipError_t launch_reservoir(const void *recs, int64_t n, int rb, int key_bytes, int64_t k, uint64_t s0,
                             const uint64_t *jump_dev, long long *winner, void *out_keys, hipStream_t st);
+// RangePartitioner re-sampling (BernoulliSampler): flags[i] = nextDouble #i <= fraction, and a
+// gather of the keys of selected record indices.
+hipError_t launch_bernoulli_flags(int64_t n, double fraction, uint64_t s0, const uint64_t *jump_dev, uint8_t *flags,
+                                  hipStream_t st);
+hipError_t launch_gather_keys(const void *recs, int rb, int key_bytes, const int64_t *idx_dev, int64_t m,
+                              void *out_keys, hipStream_t st);
 // Kryo (Long, Long) framing (sgx_serde.hip): n partition-contiguous 16 B records -> their
 // KryoSerializationStream bytes in `out` (capacity 20 n), partition byte offsets ser_off[R+1]
 // from the record offsets rec_off[R+1].  Workspace `work` / `status`: kryo_work_bytes(tiles)

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <array>
+#include <vector>
 #include <cmath>
 #include <cstring>
 
@@ -69,6 +70,43 @@ int32_t byteswap32(int32_t v) {
     return (int32_t)(hc * 0x9e3775cdu);
 }
 
+// java.util.Random (48-bit LCG): the seeds PartitionwiseSampledRDD.getPartitions gives each
+// partition it samples (new Random(seed).nextLong() per partition, in partition order)
+struct JavaRandom {
+    uint64_t s;
+    explicit JavaRandom(int64_t seed) : s(((uint64_t)seed ^ 0x5DEECE66Dull) & ((1ull << 48) - 1)) {}
+    int32_t next(int bits) {
+        s = (s * 0x5DEECE66Dull + 0xBull) & ((1ull << 48) - 1);
+        return (int32_t)(uint32_t)(s >> (48 - bits));
+    }
+    int64_t next_long() {
+        const int64_t hi = next(32);
+        const int64_t lo = next(32);
+        return (int64_t)((uint64_t)hi << 32) + lo;
+    }
+};
+
+// XORShiftRandom on the host (setSeed = hashSeed) and java.util.Random.nextDouble over it
+struct XorShift {
+    uint64_t s;
+    explicit XorShift(int64_t seed) : s(xorshift_hash_seed(seed)) {}
+    uint64_t next(int bits) {
+        s ^= s << 21;
+        s ^= s >> 35;
+        s ^= s << 4;
+        return s & ((1ull << bits) - 1);
+    }
+    double next_double() { return (double)((next(26) << 27) + next(27)) * 0x1.0p-53; }
+};
+
+// GapSampling(f, rng, epsilon = 5e-11).advance: items to drop before the next kept one,
+// (log(max(u, eps)) / log1p(-f)).toInt (a double past Int.MaxValue saturates, as in Scala)
+int64_t gap_advance(XorShift &rng, double lnq) {
+    const double u = std::max(rng.next_double(), 5e-11);
+    const double g = std::log(u) / lnq;
+    return g >= 2147483647.0 ? 2147483647 : (int64_t)g;
+}
+
 // column form of M^(2^t), t = 0..47, M = one XORShiftRandom step
 std::vector<uint64_t> xorshift_jump_table() {
     auto step = [](uint64_t s) {
@@ -101,7 +139,8 @@ struct Cand {
 
 extern "C" int sgx_range_bounds(sgx_engine *e, const void *const *batches, const int64_t *nrecords, int32_t nbatches,
                                 int32_t rb, int32_t mem_kind, int32_t num_partitions, int32_t rdd_id,
-                                int32_t sample_points_per_partition, void *out_bounds, int32_t *out_nbounds) {
+                                int32_t parent_rdd_id, int32_t sample_points_per_partition, void *out_bounds,
+                                int32_t *out_nbounds) {
     sgx::TraceRange trace_("sgx_range_bounds");
     if (!e || !out_nbounds || (nbatches > 0 && (!batches || !nrecords))) return fail_msg(SGX_ERR_INVALID, "NULL argument");
     if (rb != 16 && rb != 100) return fail_msg(SGX_ERR_UNSUPPORTED, "range bounds need 16 B or 100 B records, not %d", rb);
@@ -151,30 +190,81 @@ extern "C" int sgx_range_bounds(sgx_engine *e, const void *const *batches, const
         HIP_TRY(hipStreamSynchronize(st));
     }
     if (num_items == 0) return SGX_OK;
-    // candidates weighted by 1 / sampling probability; imbalanced partitions would be
-    // re-sampled by Spark (PartitionPruningRDD.sample): not reproduced here
+    // candidates weighted by 1 / sampling probability; a partition holding much more than its
+    // share is re-sampled instead (below)
     const double fraction = std::min(sample_size / (double)std::max<int64_t>(num_items, 1), 1.0);
     std::vector<Cand> cand;
+    auto add = [&](const uint8_t *p, float w) {
+        Cand c{};
+        if (kb == 8) {
+            int64_t v;
+            std::memcpy(&v, p, 8);
+            c.k64 = v;
+        } else {
+            std::memcpy(c.k10.data(), p, 10);
+        }
+        c.w = w;
+        cand.push_back(c);
+    };
+    std::vector<int32_t> imbalanced;
     for (int32_t i = 0; i < nbatches; ++i) {
         const int64_t n = nrecords[i];
         const int64_t len = (int64_t)samples[(size_t)i].size() / kb;
-        if (fraction * (double)n > (double)k)
-            return fail_msg(SGX_ERR_UNSUPPORTED, "partition %d is imbalanced (%lld records): Spark re-samples it", i,
-                        (long long)n);
+        if (fraction * (double)n > (double)k) {
+            imbalanced.push_back(i);
+            continue;
+        }
         if (len == 0) continue;
         const float w = (float)((double)n / (double)len);
-        for (int64_t j = 0; j < len; ++j) {
-            Cand c{};
-            const uint8_t *p = samples[(size_t)i].data() + j * kb;
-            if (kb == 8) {
-                int64_t v;
-                std::memcpy(&v, p, 8);
-                c.k64 = v;
+        for (int64_t j = 0; j < len; ++j) add(samples[(size_t)i].data() + j * kb, w);
+    }
+    if (!imbalanced.empty()) {
+        // new PartitionPruningRDD(rdd.map(_._1), imbalanced).sample(false, fraction,
+        // byteswap32(-rdd.id - 1)): PartitionwiseSampledRDD seeds each kept partition with the
+        // next nextLong() of java.util.Random(seed), in partition order, and runs a fresh
+        // BernoulliSampler(fraction) on it -- XORShiftRandom(that seed); gap sampling when
+        // fraction <= 0.4 (GapSampling: the first advance() at construction, then one per kept
+        // item), else one nextDouble per item, kept iff <= fraction.  Weight (1 / fraction).toFloat.
+        JavaRandom jr((int64_t)byteswap32((int32_t)(-(int64_t)parent_rdd_id - 1)));
+        const float w = (float)(1.0 / fraction);
+        for (int32_t i : imbalanced) {
+            const int64_t n = nrecords[i];
+            const int64_t pseed = jr.next_long();
+            std::vector<int64_t> idx;
+            if (fraction >= 1.0) {
+                idx.resize((size_t)n);
+                for (int64_t j = 0; j < n; ++j) idx[(size_t)j] = j;
+            } else if (fraction <= 0.4) {
+                XorShift rng(pseed);
+                const double lnq = std::log1p(-fraction);
+                for (int64_t pos = gap_advance(rng, lnq); pos < n; pos += 1 + gap_advance(rng, lnq))
+                    idx.push_back(pos);
             } else {
-                std::memcpy(c.k10.data(), p, 10);
+                SGX_TRY(c->sample_winner.ensure((size_t)std::max<int64_t>(n, 8)));
+                HIP_TRY(launch_bernoulli_flags(n, fraction, xorshift_hash_seed(pseed), (const uint64_t *)e->jump_dev.p,
+                                               (uint8_t *)c->sample_winner.p, st));
+                std::vector<uint8_t> flags((size_t)n);
+                HIP_TRY(hipMemcpyAsync(flags.data(), c->sample_winner.p, (size_t)n, hipMemcpyDeviceToHost, st));
+                HIP_TRY(hipStreamSynchronize(st));
+                for (int64_t j = 0; j < n; ++j)
+                    if (flags[(size_t)j]) idx.push_back(j);
             }
-            c.w = w;
-            cand.push_back(c);
+            if (idx.empty()) continue;
+            const void *src = batches[i];
+            if (mem_kind == SGX_MEM_HOST) {
+                SGX_TRY(c->input_stage.ensure((size_t)(n * rb)));
+                HIP_TRY(hipMemcpyAsync(c->input_stage.p, src, (size_t)(n * rb), hipMemcpyHostToDevice, st));
+                src = c->input_stage.p;
+            }
+            const int64_t m = (int64_t)idx.size();
+            SGX_TRY(c->sample_winner.ensure((size_t)m * 8));
+            SGX_TRY(c->sample_keys.ensure((size_t)m * (size_t)kb));
+            HIP_TRY(hipMemcpyAsync(c->sample_winner.p, idx.data(), (size_t)m * 8, hipMemcpyHostToDevice, st));
+            HIP_TRY(launch_gather_keys(src, rb, kb, (const int64_t *)c->sample_winner.p, m, c->sample_keys.p, st));
+            std::vector<uint8_t> keys((size_t)(m * kb));
+            HIP_TRY(hipMemcpyAsync(keys.data(), c->sample_keys.p, keys.size(), hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            for (int64_t j = 0; j < m; ++j) add(keys.data() + j * kb, w);
         }
     }
     // determineBounds(candidates, min(partitions, candidates.size)): stable sort by key,

@@ -78,6 +78,56 @@ __global__ __launch_bounds__(ST) void k_reservoir_gather(const char *__restrict_
     for (int b = 0; b < key_bytes; ++b) out[r * key_bytes + b] = recs[src * rb + b];
 }
 
+// RangePartitioner's re-sampling of an imbalanced partition with fraction > 0.4
+// (BernoulliSampler without gap sampling: one nextDouble per item, kept iff <= fraction).
+// Draw i of the partition's XORShiftRandom consumes steps 2i+1 and 2i+2; flags[i] = kept.
+__global__ __launch_bounds__(ST) void k_bernoulli(int64_t n, double fraction, uint64_t s0,
+                                                  const uint64_t *__restrict__ jump, uint8_t *__restrict__ flags) {
+    const int64_t t = (int64_t)blockIdx.x * ST + threadIdx.x;
+    const int64_t i0 = t * DRAWS;
+    if (i0 >= n) return;
+    uint64_t s = s0;
+    uint64_t m = (uint64_t)(2 * i0);
+    for (int b = 0; m; ++b, m >>= 1)
+        if (m & 1ull) s = gf2_apply(jump + (size_t)b * 64, s);
+    const int64_t i1 = min(n, i0 + DRAWS);
+    for (int64_t i = i0; i < i1; ++i) {
+        s = xs_step(s);
+        const uint64_t a = s & ((1ull << 26) - 1);
+        s = xs_step(s);
+        const uint64_t c = s & ((1ull << 27) - 1);
+        const double d = (double)((a << 27) + c) * 0x1.0p-53;
+        flags[i] = d <= fraction ? 1 : 0;
+    }
+}
+
+// keys of the records at idx[0..m) (sorted record indices), key_bytes each, back to back
+__global__ __launch_bounds__(ST) void k_gather_keys(const char *__restrict__ recs, int rb, int key_bytes,
+                                                    const int64_t *__restrict__ idx, int64_t m,
+                                                    char *__restrict__ out) {
+    const int64_t j = (int64_t)blockIdx.x * ST + threadIdx.x;
+    if (j >= m) return;
+    const char *src = recs + idx[j] * rb;
+    for (int b = 0; b < key_bytes; ++b) out[j * key_bytes + b] = src[b];
+}
+
+hipError_t launch_bernoulli_flags(int64_t n, double fraction, uint64_t s0, const uint64_t *jump_dev, uint8_t *flags,
+                                  hipStream_t st) {
+    if (n <= 0) return hipSuccess;
+    const int64_t nt = (n + DRAWS - 1) / DRAWS;
+    hipLaunchKernelGGL(k_bernoulli, dim3((unsigned)((nt + ST - 1) / ST)), dim3(ST), 0, st, n, fraction, s0, jump_dev,
+                       flags);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather_keys(const void *recs, int rb, int key_bytes, const int64_t *idx_dev, int64_t m,
+                              void *out_keys, hipStream_t st) {
+    if (m <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather_keys, dim3((unsigned)((m + ST - 1) / ST)), dim3(ST), 0, st, (const char *)recs, rb,
+                       key_bytes, idx_dev, m, (char *)out_keys);
+    return hipGetLastError();
+}
+
 int64_t reservoir_threads(int64_t n, int64_t k) { return n > k ? (n - k + DRAWS - 1) / DRAWS : 0; }
 
 hipError_t launch_reservoir(const void *recs, int64_t n, int rb, int key_bytes, int64_t k, uint64_t s0,

@@ -418,10 +418,15 @@ class ShuffleEngine:
         return keys, vals
 
     def range_bounds(self, batches: Sequence, nrecords: Sequence[int], record_bytes: int, num_partitions: int,
-                     rdd_id: int = 0, sample_points_per_partition: int = 20) -> np.ndarray:
-        """RangePartitioner.rangeBounds from the data (sketch on the GPU + determineBounds):
-        int64[nb] for 16 B records, uint8[nb, 10] for 100 B TeraSort records.  ``batches``
-        are the RDD's input partitions (all host ndarrays or all device buffers)."""
+                     rdd_id: int = 0, sample_points_per_partition: int = 20,
+                     parent_rdd_id: Optional[int] = None) -> np.ndarray:
+        """RangePartitioner.rangeBounds from the data (sketch on the GPU, Spark's re-sampling of
+        imbalanced partitions, determineBounds): int64[nb] for 16 B records, uint8[nb, 10] for
+        100 B TeraSort records.  ``batches`` are the RDD's input partitions (all host ndarrays
+        or all device buffers); ``rdd_id`` is the id of ``rdd.map(_._1)`` (the sketch's RDD),
+        ``parent_rdd_id`` that of the pair RDD (default rdd_id - 1: Spark creates the key RDD
+        inside the partitioner's constructor, right after nothing else in the usual case)."""
+        parent = rdd_id - 1 if parent_rdd_id is None else parent_rdd_id
         args = [buffer_arg(b) for b in batches]
         kinds = {k for _, _, k in args}
         if len(kinds) > 1:
@@ -432,7 +437,7 @@ class ShuffleEngine:
         out = np.empty(max(1, num_partitions - 1) * kb, dtype=np.uint8)
         nb = ctypes.c_int32(0)
         check(lib().sgx_range_bounds(self.handle, ptrs, ns.ctypes.data, len(args), record_bytes,
-                                     kinds.pop() if kinds else MEM_HOST, num_partitions, rdd_id,
+                                     kinds.pop() if kinds else MEM_HOST, num_partitions, rdd_id, parent,
                                      sample_points_per_partition, out.ctypes.data, ctypes.byref(nb)), "rangeBounds")
         out = out[:nb.value * kb]
         return out.view("<i8").copy() if kb == 8 else out.reshape(-1, 10).copy()

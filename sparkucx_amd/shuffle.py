@@ -68,11 +68,15 @@ class RangePartitioner:
 
     @classmethod
     def fromData(cls, engine, partitions: Sequence, nrecords: Sequence[int], recordBytes: int, numPartitions: int,
-                 rddId: int = 0, ascending: bool = True, samplePointsPerPartitionHint: int = 20):
+                 rddId: int = 0, ascending: bool = True, samplePointsPerPartitionHint: int = 20,
+                 parentRddId: Optional[int] = None):
         """new RangePartitioner(partitions, rdd, ascending, samplePointsPerPartitionHint): the
-        bounds come from RangePartitioner.sketch (GPU reservoir sampling with Spark's seeds)
-        and determineBounds.  ``partitions`` are the RDD's input partitions (record batches)."""
-        b = engine.range_bounds(partitions, nrecords, recordBytes, numPartitions, rddId, samplePointsPerPartitionHint)
+        bounds come from RangePartitioner.sketch (GPU reservoir sampling with Spark's seeds),
+        the re-sampling of imbalanced partitions and determineBounds.  ``partitions`` are the
+        RDD's input partitions (record batches); ``rddId`` is the id of rdd.map(_._1) the
+        sketch runs on, ``parentRddId`` the pair RDD's (default rddId - 1)."""
+        b = engine.range_bounds(partitions, nrecords, recordBytes, numPartitions, rddId, samplePointsPerPartitionHint,
+                                parentRddId)
         return cls(b, ascending)
 
 

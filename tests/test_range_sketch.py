@@ -143,3 +143,75 @@ def test_murmur3_bytes_hash_pinned_to_scikit_learn():
         lo = murmurhash3_32(b, seed=0x3C074A61, positive=True)
         hi = murmurhash3_32(b, seed=lo, positive=True)
         assert semantics.xorshift_hash_seed(s) == (hi << 32) | lo
+
+
+def test_java_random_known_answers():
+    """java.util.Random, whose nextLong() seeds each re-sampled partition
+    (PartitionwiseSampledRDD.getPartitions): the widely published first values."""
+    from oracle import spark_semantics as ss
+
+    assert ss.JavaRandom(42).next_int() == -1170105035
+    assert ss.JavaRandom(0).next_long() == -4962768465676381896
+
+
+def test_bernoulli_sampler_properties():
+    """BernoulliSampler restated: deterministic per seed, the kept fraction near f in both
+    regimes (gap sampling at f <= 0.4, one draw per item above), order preserved."""
+    from oracle import spark_semantics as ss
+
+    items = list(range(200_000))
+    for f in (0.01, 0.3, 0.5, 0.9):
+        a = ss.bernoulli_sample(items, f, 1234)
+        assert a == ss.bernoulli_sample(items, f, 1234) and a == sorted(a)
+        assert abs(len(a) - f * len(items)) < 6 * (f * (1 - f) * len(items)) ** 0.5, f
+    assert ss.bernoulli_sample(items, 0.0, 1) == [] and ss.bernoulli_sample(items[:10], 1.0, 1) == items[:10]
+
+
+def test_imbalanced_partitions_are_resampled():
+    """A partition holding more than 3 / #partitions of the items is re-sampled (RDD.sample),
+    not refused: bounds come out sorted, distinct and still balanced over the data."""
+    from oracle import spark_semantics as ss
+
+    rng = np.random.default_rng(5)
+    parts = [rng.integers(-(2**40), 2**40, size=n).tolist() for n in (40_000, 500, 500, 500, 500, 500, 500, 500)]
+    b = ss.range_bounds(parts, 64, rdd_id=4)
+    assert len(b) == 63 and b == sorted(b) and len(set(b)) == 63
+    allk = np.sort(np.concatenate(parts))
+    counts = np.diff(np.searchsorted(allk, b, side="right"))
+    assert counts.min() > 0.3 * len(allk) / 64 and counts.max() < 2.0 * len(allk) / 64
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("rb,R,sizes,rdd,parent", [
+    (16, 64, (50_000,) + (1_000,) * 7, 6, 5),      # fraction 0.022: gap sampling
+    (16, 200, (9_000, 100, 100, 100), 3, 1),       # fraction 0.43: one draw per record (GPU)
+    (100, 32, (30_000, 400, 400, 400, 400), 8, 2),  # TeraSort keys, gap sampling
+    (16, 16, (2_000, 0, 10), 1, 0),                 # fraction 0.16, an empty partition
+])
+def test_gpu_resampling_of_imbalanced_partitions(sgx_lib, oracle_lib, rb, R, sizes, rdd, parent):
+    """Spark's second pass for imbalanced partitions (RangePartitioner's rangeBounds:
+    fraction * n > sampleSizePerPartition -> RDD.sample(false, fraction,
+    byteswap32(-rdd.id - 1))) on the GPU path equals the sequential restatement, for host and
+    device batches, Long and 10-byte keys, both BernoulliSampler regimes."""
+    from oracle import spark_semantics as ss
+
+    batches = []
+    for i, n in enumerate(sizes):
+        recs = oracle_lib.gen_uniform16(n, 91 + i) if rb == 16 else oracle_lib.gen_terasort100(n, 91 + i)
+        batches.append(recs)
+    with sgx_lib.ShuffleEngine(device=0) as e:
+        got = e.range_bounds(batches, list(sizes), rb, R, rdd, parent_rdd_id=parent)
+        dev = [e.alloc(max(16, b.nbytes)) for b in batches]
+        for d, b in zip(dev, batches):
+            d.copy_from(b)
+        got_dev = e.range_bounds(dev, list(sizes), rb, R, rdd, parent_rdd_id=parent)
+    if rb == 16:
+        keys = [b[:, :8].copy().view("<i8").reshape(-1).tolist() for b in batches]
+        want = np.array(ss.range_bounds(keys, R, rdd, parent_rdd_id=parent), dtype=np.int64)
+    else:
+        keys = [[bytes(r[:10]) for r in b] for b in batches]
+        want = np.frombuffer(b"".join(ss.range_bounds(keys, R, rdd, parent_rdd_id=parent)),
+                             dtype=np.uint8).reshape(-1, 10)
+    assert len(want) > 0
+    assert np.array_equal(got, want)
+    assert np.array_equal(got_dev, want)
