@@ -66,8 +66,10 @@ enum sgx_flags {
     SGX_FLAG_SORT_ALL_DIGITS = 4,     /* sorted reads run every digit pass (no skipping)    */
     SGX_FLAG_DEBUG_SYNC = 8,          /* debugging: synchronise after every kernel and name the
                                          kernel in the error of a device fault (slow)         */
-    SGX_FLAG_LZ4_LANE_DECODE = 16     /* LZ4 reads decode every compressed frame one lane per
+    SGX_FLAG_LZ4_LANE_DECODE = 16,    /* LZ4 reads decode every compressed frame one lane per
                                          frame (default: only from 32768 frames up)           */
+    SGX_FLAG_NO_SPLIT_SCATTER = 32    /* hash K4 with R > 1024: one lane-ordered pass instead
+                                         of the two-level write-combining split               */
 };
 
 typedef struct sgx_config {

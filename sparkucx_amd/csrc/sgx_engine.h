@@ -246,6 +246,7 @@ struct Ctx {
     } rc;
     // map side: [counts][ticket | look-back status][partition offsets | error] + offs[R][G]
     DevBuf offs, work;
+    DevBuf split_work, split_tmp;  // R > 1024: the two-level split scatter's scratch and level-1 output
     DevBuf input_stage;
     const uint32_t *last_off_dev = nullptr;  // device (R+1) record offsets of the last partition pass
     // reduce side and map-side combine

@@ -27,7 +27,13 @@ struct PartParams {
 // Internal partition kind of the reduce side's LSD radix passes: pid = 8-bit digit of the
 // key (R = 256), see PartParams::dshift / dflip.  Never registered through the C ABI.
 constexpr int KIND_DIGIT = 200;
+// Kernel-internal kind: HashPartitioner with a power-of-two R (pid = (k_lo ^ k_hi) & (R - 1)).
+constexpr int KIND_HASH_POW2 = 100;
 constexpr uint32_t DIGIT_R = 256;
+// Internal partition kind of the two-level split scatter (hash, power-of-two R > 1024):
+// pid = ((k_lo ^ k_hi) >> dshift) & (R - 1), i.e. the top log2(R) bits of the full
+// power-of-two HashPartitioner id (its "super-partition"), with R super-partitions.
+constexpr int KIND_HASH_BITS = 300;
 
 // Granlund-Montgomery parameters of mod_u32 (sgx_kernels.hip) for 2 <= R < 2^31:
 // l = ceil(log2 R), m = floor(2^32 (2^l - R) / R) + 1, shift = l - 1.
@@ -82,6 +88,19 @@ hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint
                        uint32_t *ticket, uint32_t *err, uint32_t *part_off, int G, int R,
                        hipStream_t stream);
 int64_t scan_tiles(int64_t len);
+// Two-level split scatter (hash partitioner, power-of-two R > 1024, 16 B records):
+// csum[s][g] = sum over the Q sub-partitions q of counts[(s*Q + q)][g]   (S*G entries);
+// desc: the level-2 pieces cut from the level-1 offsets (offs1[S][G], u32) -- each piece a
+// run of whole (super, chunk) blocks inside one super-partition, about `target` records --
+// as {begin, end, super, first chunk} int64 quadruples, their count in *ndesc;
+// launch_scatter16_seg: level 2, write-combining K4 with R = Q over the pieces, cursors
+// offs[(super*Q + q)][chunk] of the single-level scan.
+hipError_t launch_super_counts(const uint32_t *counts, uint32_t *csum, int S, int Q, int G, hipStream_t stream);
+hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, int64_t n, int64_t target, int64_t *desc,
+                           uint32_t *ndesc, hipStream_t stream);
+hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
+                                int G, const int64_t *desc, const uint32_t *ndesc, int grid, const ScatterGeom &geo,
+                                uint32_t *err, hipStream_t stream);
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes, int64_t chunk,
                           int G, const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
                           uint32_t *err, hipStream_t stream);

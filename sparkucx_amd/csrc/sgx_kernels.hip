@@ -49,9 +49,8 @@ __device__ __forceinline__ uint32_t hash_pid(uint32_t klo, uint32_t khi, const P
     return pp.R == 1 ? 0u : v;
 }
 
-// Kernel-internal partitioner kind: HashPartitioner with a power-of-two R, where
+// KIND_HASH_POW2 (sgx_internal.h): HashPartitioner with a power-of-two R, where
 // nonNegativeMod(h, R) == h & (R - 1) for two's-complement h.
-constexpr int KIND_HASH_POW2 = 100;
 
 // RangePartitioner.getPartition over bounds `b` (global memory, or an LDS copy).
 template <typename BP>
@@ -115,6 +114,8 @@ __device__ __forceinline__ uint32_t pid_of_b(uint32_t x, uint32_t y, uint32_t z,
         return ((w >> (sh & 31u)) & 0xFFu) ^ pp.dflip;
     } else if constexpr (KIND == KIND_HASH_POW2) {
         return (x ^ y) & (pp.R - 1u);
+    } else if constexpr (KIND == KIND_HASH_BITS) {
+        return ((x ^ y) >> pp.dshift) & (pp.R - 1u);
     } else if constexpr (KIND == SGX_PART_RANGE_I64) {
         return range_pid_i64((int64_t)(((uint64_t)y << 32) | x), bi64, pp.nb, pp.ascending);
     } else {
@@ -1017,12 +1018,17 @@ __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
     return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 12;  // cur 4 + dlim 8
 }
 
-template <int KIND, int WAVES, int NI, int SI>
+// SEG (level 2 of the two-level split, launch_scatter16_seg): the workgroup's records are
+// desc[blockIdx.x] = {begin, end, super s, chunk g} instead of chunk blockIdx.x, and its R
+// streams start at offs[(s * R + p) * G + g].
+template <int KIND, int WAVES, int NI, int SI, bool SEG = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__restrict__ in,
                                                                 u32x4 *__restrict__ out, int64_t n,
                                                                 int64_t chunk, PartParams pp,
                                                                 const uint32_t *__restrict__ offs,
-                                                                int G, uint32_t *err) {
+                                                                int G, uint32_t *err,
+                                                                const int64_t *__restrict__ desc = nullptr,
+                                                                const uint32_t *__restrict__ ndesc = nullptr) {
     constexpr int T = WAVES * 64;
     constexpr int TNEW = T * NI;
     constexpr int STAGE = T * SI;
@@ -1040,13 +1046,20 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     uint32_t *myrow32 = (uint32_t *)myrow;
     const uint32_t n32 = (uint32_t)n;  // n < 2^32 (sgx_write_map)
 
-    const int g = blockIdx.x;
-    const int64_t begin = (int64_t)g * chunk;
-    const int64_t end = min(n, begin + chunk);
+    int g = blockIdx.x;
+    int64_t begin = (int64_t)g * chunk, end = min(n, begin + chunk), obase = 0;
+    if constexpr (SEG) {
+        if (blockIdx.x >= *ndesc) return;  // the whole workgroup, before any barrier
+        const int64_t *d = desc + 4 * (int64_t)blockIdx.x;
+        begin = d[0];
+        end = min(n, d[1]);
+        obase = d[2] * (int64_t)R;
+        g = (int)d[3];
+    }
     const int64_t len = end > begin ? end - begin : 0;
     const int64_t ntiles = (len + TNEW - 1) / TNEW;
     for (uint32_t p = tid; p < RS; p += T) {
-        const uint32_t c0 = p < R ? offs[(int64_t)p * G + g] : 0u;
+        const uint32_t c0 = p < R ? offs[(obase + p) * G + g] : 0u;
         cur[p] = c0;
         dlim[p] = make_uint2(0u, c0);  // lim = cur: nothing deferred
     }
@@ -1500,12 +1513,112 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
     return ScatterGeom{WIDE2_GEOM_TAG, 2, WIDE2_TR, lds, 0};
 }
 
+// ------------------------------------------------------------------------------------
+// Two-level split scatter for R > 1024 (hash partitioner, power-of-two R, 16 B records).
+//
+// A single pass at R = 4096 (k_scatter16_ord) gives every partition ~1 record per 4 K-record
+// tile: its runs start at arbitrary offsets and leave L2 as partial lines -- 7.0 GB written
+// per 4.3 GB of records (profiles/r02a_u4096_summary.md) -- and the write-combining kernel
+// cannot keep 4096 streams' incomplete lines on chip.  So the split runs two
+// write-combining passes of R <= 1024 each, both writing whole lines only:
+//   level 1: partition by the top log2(S) bits of the id (KIND_HASH_BITS, S super-partitions)
+//            into a scratch buffer, cursors from a scan of the per-chunk super counts;
+//   level 2: inside every super-partition, partition by the low log2(Q) bits (R = Q = 64),
+//            over pieces of whole (super, chunk) blocks: the level-1 output holds super s's
+//            records chunk after chunk in input order, so a piece starting at block (s, g)
+//            continues every sub-partition stream at exactly the single-level offset
+//            offs[(s*Q + q)][g] -- no second histogram, and the result is byte-identical to
+//            the single-pass scatter (both stable, same offsets).
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_super_counts(const uint32_t *__restrict__ counts, uint32_t *__restrict__ csum,
+                                                      int S, int Q, int G) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)S * G) return;
+    const int64_t sidx = i / G, g = i - sidx * G;
+    uint32_t acc = 0;
+    for (int q = 0; q < Q; ++q) acc += counts[(sidx * Q + q) * G + g];
+    csum[i] = acc;
+}
+
+hipError_t launch_super_counts(const uint32_t *counts, uint32_t *csum, int S, int Q, int G, hipStream_t stream) {
+    const int64_t n = (int64_t)S * G;
+    hipLaunchKernelGGL(k_super_counts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, counts, csum, S, Q, G);
+    return hipGetLastError();
+}
+
+// One workgroup: block i = s*G + g (s-major, the level-1 layout) starts a piece when g == 0
+// or when it crosses a multiple of `target` records; the pieces are compacted in order by a
+// block-wide scan of the flags.  A piece ends where the next begins (the supers are
+// contiguous), the last one at n.
+constexpr int DESC_THREADS = 1024;
+__global__ __launch_bounds__(DESC_THREADS) void k_seg_desc(const uint32_t *__restrict__ offs1, int S, int G, int64_t n,
+                                                           int64_t target, int64_t *__restrict__ desc,
+                                                           uint32_t *__restrict__ ndesc) {
+    __shared__ uint32_t scratch[DESC_THREADS / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t nb = (int64_t)S * G;
+    const int64_t per = (nb + DESC_THREADS - 1) / DESC_THREADS;
+    const int64_t i0 = min(nb, (int64_t)tid * per), i1 = min(nb, i0 + per);
+    auto flag = [&](int64_t i) {
+        const int64_t g = i % G;
+        return g == 0 || (int64_t)offs1[i] / target != (int64_t)offs1[i - 1] / target;
+    };
+    uint32_t cnt = 0;
+    for (int64_t i = i0; i < i1; ++i) cnt += flag(i) ? 1u : 0u;
+    const uint32_t x = wave_inclusive_scan(cnt, lane);
+    if (lane == 63) scratch[w] = x;
+    __syncthreads();
+    uint32_t k = x - cnt, total = 0;
+    for (uint32_t v = 0; v < DESC_THREADS / 64; ++v) {
+        if (v < w) k += scratch[v];
+        total += scratch[v];
+    }
+    for (int64_t i = i0; i < i1; ++i) {
+        if (!flag(i)) continue;
+        int64_t j = i + 1;  // the next piece's first block (a few blocks on: one per super at least)
+        while (j < nb && !flag(j)) ++j;
+        int64_t *d = desc + 4 * (int64_t)k;
+        d[0] = offs1[i];
+        d[1] = j < nb ? (int64_t)offs1[j] : n;
+        d[2] = i / G;
+        d[3] = i % G;
+        ++k;
+    }
+    if (tid == 0) *ndesc = total;
+}
+
+hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, int64_t n, int64_t target, int64_t *desc,
+                           uint32_t *ndesc, hipStream_t stream) {
+    hipLaunchKernelGGL(k_seg_desc, dim3(1), dim3(DESC_THREADS), 0, stream, offs1, S, G, n, target, desc, ndesc);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
+                                int G, const int64_t *desc, const uint32_t *ndesc, int grid, const ScatterGeom &geo,
+                                uint32_t *err, hipStream_t stream) {
+    if (geo.waves != WC_GEOM_BASE + 8 || geo.mbits != 16 || (pp.R & (pp.R - 1)) != 0) return hipErrorInvalidValue;
+#define SGX_WCS(NI)                                                                                          \
+    do {                                                                                                     \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<KIND_HASH_POW2, 8, NI, 16, true>,            \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes);           \
+        hipLaunchKernelGGL((k_scatter16_wc<KIND_HASH_POW2, 8, NI, 16, true>), dim3(grid), dim3(512),         \
+                           geo.lds_bytes, stream, (const u32x4 *)in, (u32x4 *)out, n, (int64_t)0, pp, offs, G, \
+                           err, desc, ndesc);                                                                \
+    } while (0)
+    if (geo.items == 12) SGX_WCS(12);
+    else if (geo.items == 8) SGX_WCS(8);
+    else return hipErrorInvalidValue;
+#undef SGX_WCS
+    return hipGetLastError();
+}
+
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t chunk, int G,
                           const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
                           uint32_t *err, hipStream_t stream) {
     const bool pow2 = (pp.R & (pp.R - 1)) == 0;
     if (rb == 16 && geo.waves >= WC_GEOM_BASE) {
-        if ((pp.kind != SGX_PART_HASH && pp.kind != KIND_DIGIT) || geo.waves != WC_GEOM_BASE + 8 || geo.mbits != 16)
+        if ((pp.kind != SGX_PART_HASH && pp.kind != KIND_DIGIT && pp.kind != KIND_HASH_BITS) ||
+            geo.waves != WC_GEOM_BASE + 8 || geo.mbits != 16)
             return hipErrorInvalidValue;
 #define SGX_WC(K, NI)                                                                            \
     do {                                                                                         \
@@ -1517,6 +1630,11 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         if (pp.kind == KIND_DIGIT) {
             if (geo.items != 12 || pp.R != DIGIT_R) return hipErrorInvalidValue;
             SGX_WC(KIND_DIGIT, 12);
+        } else if (pp.kind == KIND_HASH_BITS) {
+            if (!pow2) return hipErrorInvalidValue;
+            if (geo.items == 12) SGX_WC(KIND_HASH_BITS, 12);
+            else if (geo.items == 8) SGX_WC(KIND_HASH_BITS, 8);
+            else return hipErrorInvalidValue;
         } else if (geo.items == 12) {
             if (pow2) SGX_WC(KIND_HASH_POW2, 12); else SGX_WC(SGX_PART_HASH, 12);
         } else if (geo.items == 8) {

@@ -53,6 +53,21 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
         if (geo.waves < WC_GEOM_BASE && geo.waves != WIDE2_GEOM_TAG)
             return fail_msg(SGX_ERR_UNSUPPORTED, "digit pass on %d B records at this alignment", rb);
     }
+    // R > 1024 (power of two, hash, 16 B): the two-level split -- two write-combining passes
+    // (S = R / 64 super-partitions, then Q = 64 inside each) instead of one pass whose runs
+    // leave L2 as partial lines (sgx_kernels.hip, "Two-level split scatter")
+    const bool split = rb == 16 && kind == SGX_PART_HASH && R > 1024 && (R & (R - 1)) == 0 && R <= 65536 &&
+                       e->rank_mode == SGX_RANK_ORDERED && e->sc_waves == 0 && e->sc_items == 0 &&
+                       !(e->flags & (SGX_FLAG_NO_WRITE_COMBINING | SGX_FLAG_NO_SPLIT_SCATTER));
+    constexpr int32_t Q = 64;
+    const int32_t S = split ? R / Q : 0;
+    ScatterGeom geo1{}, geo2{};
+    if (split) {
+        geo1 = scatter_geom16_wc((uint32_t)S);
+        geo2 = scatter_geom16_wc((uint32_t)Q);
+        if (geo1.items == 0 || geo2.items == 0) return fail_msg(SGX_ERR_UNSUPPORTED, "split scatter geometry for R=%d", R);
+        geo = geo1;
+    }
     if (geo.items == 0)
         return fail_msg(SGX_ERR_UNSUPPORTED, "no scatter geometry (waves %d, items %d) fits R=%d", e->sc_waves,
                         e->sc_items, R);
@@ -62,21 +77,41 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     const int G = n > 0 ? (int)((n + chunk - 1) / chunk) : 1;
     const int64_t len = (int64_t)R * G;
     const int64_t tiles = scan_tiles(len);
+    const int64_t len1 = (int64_t)S * G;
+    const int64_t tiles1 = split ? scan_tiles(len1) : 0;
     SGX_TRY(c.offs.ensure((size_t)len * 4));
     // one work block, zeroed by ONE memset (each fill / copy between kernels costs ~5-10 µs):
     // [counts u32 x R*G][ticket u32 | pad][look-back status u64 x tiles]
     // [partition offsets u32 x (R+1) | error] -- the error word sits right after the
-    // offsets so one copy lands both on the host
+    // offsets so one copy lands both on the host -- [ticket | status of the split's scan]
     const size_t counts_bytes = ((size_t)len * 4 + 15) & ~(size_t)15;
     const size_t status_bytes = ((size_t)(16 + tiles * 8) + 15) & ~(size_t)15;
-    const size_t work_bytes = counts_bytes + status_bytes + (((size_t)(R + 2) * 4 + 15) & ~(size_t)15);
+    const size_t off_bytes = ((size_t)(R + 2) * 4 + 15) & ~(size_t)15;
+    const size_t status1_bytes = split ? ((size_t)(16 + tiles1 * 8) + 15) & ~(size_t)15 : 0;
+    const size_t work_bytes = counts_bytes + status_bytes + off_bytes + status1_bytes;
     SGX_TRY(c.work.ensure(work_bytes));
     uint32_t *counts = (uint32_t *)c.work.p;
     uint32_t *ticket = (uint32_t *)((char *)c.work.p + counts_bytes);
     uint64_t *status = (uint64_t *)((char *)ticket + 16);
     uint32_t *part_off_dev = (uint32_t *)((char *)ticket + status_bytes);
     uint32_t *err = part_off_dev + R + 1;
+    uint32_t *ticket1 = (uint32_t *)((char *)part_off_dev + off_bytes);
+    uint64_t *status1 = (uint64_t *)((char *)ticket1 + 16);
     c.last_off_dev = part_off_dev;
+    // the split's scratch: [csum u32 x S*G][offs1 u32 x S*G][part_off1 u32 x (S+2) | ndesc]
+    // [desc i64 x 4*S*G], and the level-1 output (n records)
+    uint32_t *csum = nullptr, *offs1 = nullptr, *part_off1 = nullptr, *ndesc = nullptr;
+    int64_t *desc = nullptr;
+    if (split) {
+        const size_t a = ((size_t)len1 * 4 + 15) & ~(size_t)15, b = ((size_t)(S + 4) * 4 + 15) & ~(size_t)15;
+        SGX_TRY(c.split_work.ensure(2 * a + b + (size_t)len1 * 32));
+        csum = (uint32_t *)c.split_work.p;
+        offs1 = (uint32_t *)((char *)c.split_work.p + a);
+        part_off1 = (uint32_t *)((char *)c.split_work.p + 2 * a);
+        ndesc = part_off1 + S + 2;
+        desc = (int64_t *)((char *)c.split_work.p + 2 * a + b);
+        SGX_TRY(c.split_tmp.ensure((size_t)std::max<int64_t>(n, 1) * 16));
+    }
     HIP_TRY(hipMemsetAsync(c.work.p, 0, work_bytes, st));
 
     // stage events: consecutive stages share their boundary event (every timing marker
@@ -89,11 +124,37 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     HIP_TRY(launch_scan((const uint32_t *)counts, (uint32_t *)c.offs.p, len, status, ticket, err, part_off_dev, G, R,
                         st));
     SGX_TRY(debug_sync(e, st, "K3 k_scan"));
-    HIP_TRY(hipEventRecord(c1, st));
     PartParams lpp = spp;
     lpp.mbits = (uint32_t)geo.mbits;
-    if (n > 0) HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, lpp, (const uint32_t *)c.offs.p, geo, err, st));
-    SGX_TRY(debug_sync(e, st, "K4 scatter"));
+    if (split && n > 0) {
+        // level-1 cursors: a scan of the per-chunk super counts; level-2 pieces from them
+        HIP_TRY(launch_super_counts(counts, csum, S, Q, G, st));
+        HIP_TRY(launch_scan(csum, offs1, len1, status1, ticket1, err, part_off1, G, S, st));
+        const int64_t pieces = std::max<int64_t>(1, (int64_t)e->num_cus - S);
+        const int64_t target = std::max<int64_t>(1, (n + pieces - 1) / pieces);
+        HIP_TRY(launch_seg_desc(offs1, S, G, n, target, desc, ndesc, st));
+        SGX_TRY(debug_sync(e, st, "split scan / pieces"));
+        HIP_TRY(hipEventRecord(c1, st));
+        PartParams p1 = spp;
+        p1.kind = KIND_HASH_BITS;
+        p1.R = (uint32_t)S;
+        p1.dshift = 6;  // log2(Q)
+        p1.mbits = (uint32_t)geo1.mbits;
+        HIP_TRY(launch_scatter(in, c.split_tmp.p, n, rb, chunk, G, p1, offs1, geo1, err, st));
+        SGX_TRY(debug_sync(e, st, "K4 split level 1"));
+        PartParams p2 = spp;
+        p2.kind = KIND_HASH_POW2;
+        p2.R = (uint32_t)Q;
+        p2.mbits = (uint32_t)geo2.mbits;
+        const int grid = (int)(S + (n + target - 1) / target + 1);
+        HIP_TRY(launch_scatter16_seg(c.split_tmp.p, out, n, p2, (const uint32_t *)c.offs.p, G, desc, ndesc, grid, geo2,
+                                     err, st));
+        SGX_TRY(debug_sync(e, st, "K4 split level 2"));
+    } else {
+        HIP_TRY(hipEventRecord(c1, st));
+        if (n > 0) HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, lpp, (const uint32_t *)c.offs.p, geo, err, st));
+        SGX_TRY(debug_sync(e, st, "K4 scatter"));
+    }
     HIP_TRY(hipEventRecord(x1, st));
     // (R+1) offsets then the error word, one copy
     if (host_off) HIP_TRY(hipMemcpyAsync(host_off, part_off_dev, (size_t)(R + 2) * 4, hipMemcpyDeviceToHost, st));

@@ -147,11 +147,13 @@ def test_every_staged_geometry(sgx_lib, oracle_lib, waves, items, R, rank):
             pytest.skip(f"geometry {waves}x{items} does not fit R={R}")
 
 
-@pytest.mark.parametrize("cfg", [dict(hist_mode=1), dict(rank_mode=1), dict(flags=1), dict(hist_mode=1, flags=1)])
+@pytest.mark.parametrize("cfg", [dict(hist_mode=1), dict(rank_mode=1), dict(flags=1), dict(hist_mode=1, flags=1),
+                                 dict(flags=32)])
 def test_kernel_choices_are_byte_identical(sgx_lib, oracle_lib, cfg):
     """sgx_config's kernel choices -- the ballot/popcount wave-aggregated histogram
     (SGX_HIST_BALLOT), ballot-matched K4 ranking (SGX_RANK_MATCH), K4 without write-combining
-    (SGX_FLAG_NO_WRITE_COMBINING) -- change speed, never bytes."""
+    (SGX_FLAG_NO_WRITE_COMBINING), one lane-ordered pass instead of the two-level split at
+    R > 1024 (SGX_FLAG_NO_SPLIT_SCATTER) -- change speed, never bytes."""
     recs = oracle_lib.gen_uniform16(3 * 8192 * 5 + 1234, 99)
     with sgx_lib.ShuffleEngine(device=0, **cfg) as e:
         for R in (7, 200, 1024, 4096):
@@ -180,6 +182,30 @@ def test_write_combining_carry_pressure(sgx_lib, oracle_lib, R, group):
     for chunks in (1, 3):
         with sgx_lib.ShuffleEngine(device=0, num_chunks=chunks) as e:
             check_against_oracle(e, oracle_lib, recs, R)
+
+
+@pytest.mark.parametrize("R", [2048, 4096, 8192])
+@pytest.mark.parametrize("shape", ["uniform", "one_super", "hot_partition", "tiny", "empty"])
+def test_two_level_split_scatter(sgx_lib, oracle_lib, R, shape):
+    """The two-level split K4 (hash, power-of-two R > 1024: S = R/64 super-partitions written
+    whole-line, then 64 sub-partitions inside each, over pieces of whole (super, chunk)
+    blocks): bit-exact against the oracle, and byte-identical to the single lane-ordered pass
+    (SGX_FLAG_NO_SPLIT_SCATTER), for uniform keys, every key in ONE super-partition (one piece
+    per chunk, all other supers empty), one hot partition holding most records, a map smaller
+    than one tile, and an empty map; 1, 5 and the default number of chunks."""
+    n = {"tiny": 1000, "empty": 0}.get(shape, 400_003)
+    recs = oracle_lib.gen_uniform16(max(n, 1), 0x5B1 + R)[:n]
+    rng = np.random.default_rng(R)
+    if shape == "one_super":  # pid in [64 s, 64 s + 64) for one s
+        pid = 64 * 3 + rng.integers(0, 64, n)
+        recs[:, :8] = (pid + R * rng.integers(0, 1 << 20, n)).astype(np.int64).view(np.uint8).reshape(-1, 8)
+    elif shape == "hot_partition":
+        pid = np.where(rng.random(n) < 0.8, 5, rng.integers(0, R, n))
+        recs[:, :8] = (pid + R * rng.integers(0, 1 << 20, n)).astype(np.int64).view(np.uint8).reshape(-1, 8)
+    for chunks in (0, 1, 5):
+        for flags in (0, sgx_lib.FLAG_NO_SPLIT_SCATTER):  # both bit-exact: byte-identical to each other
+            with sgx_lib.ShuffleEngine(device=0, num_chunks=chunks, flags=flags) as e:
+                check_against_oracle(e, oracle_lib, recs, R)
 
 
 def test_zipf_skew_r4096(engine, oracle_lib):
