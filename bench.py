@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--dist", choices=["uniform", "zipf"], default=None)
     ap.add_argument("--seed", type=int, default=0x5EEDC0DE)
     ap.add_argument("--num-chunks", type=int, default=0)
+    ap.add_argument("--no-split", action="store_true",
+                    help="R > 1024: one lane-ordered K4 pass instead of the two-level split (A/B measurement)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=16.0,
                     help="budget of the CPU baseline's timed legs (plus ~5 s of C0 and setup)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -210,7 +212,8 @@ def main():
     torch.cuda.set_device(device)
 
     n, R, rb = args.records, args.partitions, args.record_bytes
-    eng = sgx.ShuffleEngine(device=device, num_chunks=args.num_chunks)
+    eng = sgx.ShuffleEngine(device=device, num_chunks=args.num_chunks,
+                            flags=sgx.FLAG_NO_SPLIT_SCATTER if args.no_split else 0)
     self_x = args.self_exchange and world == 1
     if world > 1 and args.comm == "host":
         eng.comm_init_host(world, rank)
