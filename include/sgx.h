@@ -68,8 +68,10 @@ enum sgx_flags {
                                          kernel in the error of a device fault (slow)         */
     SGX_FLAG_LZ4_LANE_DECODE = 16,    /* LZ4 reads decode every compressed frame one lane per
                                          frame (default: only from 32768 frames up)           */
-    SGX_FLAG_NO_SPLIT_SCATTER = 32    /* hash K4 with R > 1024: one lane-ordered pass instead
+    SGX_FLAG_NO_SPLIT_SCATTER = 32,   /* hash K4 with R > 1024: one lane-ordered pass instead
                                          of the two-level write-combining split               */
+    SGX_FLAG_NO_BUCKET_SORT = 64      /* sorted reads / map-side combine: LSD digit passes only
+                                         (no key-window buckets sorted on chip)               */
 };
 
 typedef struct sgx_config {

@@ -29,6 +29,7 @@ RANK_ORDERED, RANK_MATCH = 0, 1
 FLAG_NO_WRITE_COMBINING, FLAG_NO_WIDE_STAGED, FLAG_SORT_ALL_DIGITS, FLAG_DEBUG_SYNC = 1, 2, 4, 8
 FLAG_LZ4_LANE_DECODE = 16
 FLAG_NO_SPLIT_SCATTER = 32
+FLAG_NO_BUCKET_SORT = 64
 PLACE_EVEN, PLACE_BYTES = 0, 1
 ABI_VERSION = 5
 

@@ -34,6 +34,10 @@ constexpr uint32_t DIGIT_R = 256;
 // pid = ((k_lo ^ k_hi) >> dshift) & (R - 1), i.e. the top log2(R) bits of the full
 // power-of-two HashPartitioner id (its "super-partition"), with R super-partitions.
 constexpr int KIND_HASH_BITS = 300;
+// Internal kind of the sorted read's bucket passes: pid = (W >> dshift) & (R - 1) over the
+// key's 64-bit order window W -- a 16 B record's signed Long key with its sign flipped
+// (dflip = 1), or a 100 B record's first 8 key bytes big-endian (dflip = 0).
+constexpr int KIND_KEY_BITS = 400;
 
 // Granlund-Montgomery parameters of mod_u32 (sgx_kernels.hip) for 2 <= R < 2^31:
 // l = ceil(log2 R), m = floor(2^32 (2^l - R) / R) + 1, shift = l - 1.
@@ -101,6 +105,13 @@ hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, int64_t n, int64
 hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
                                 int G, const int64_t *desc, const uint32_t *ndesc, int grid, const ScatterGeom &geo,
                                 uint32_t *err, hipStream_t stream);
+// The sorted read's last step: `in` is ordered by bucket = (P(key) << kbits) | key window
+// bits [kshift, kshift + kbits) (P the shuffle's hash partitioner when use_p, else 0); every
+// bucket is sorted stably by the full key on chip (16 B: signed Long; 100 B: 10-byte
+// unsigned big-endian) into `out`.  A bucket longer than the kernel's cap sets bit 4 of *err
+// and leaves `out` incomplete (the caller falls back to the LSD digit passes).
+hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, const PartParams &pp, int use_p,
+                              uint32_t kshift, uint32_t kbits, uint32_t *err, hipStream_t stream);
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes, int64_t chunk,
                           int G, const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
                           uint32_t *err, hipStream_t stream);

@@ -116,6 +116,10 @@ __device__ __forceinline__ uint32_t pid_of_b(uint32_t x, uint32_t y, uint32_t z,
         return (x ^ y) & (pp.R - 1u);
     } else if constexpr (KIND == KIND_HASH_BITS) {
         return ((x ^ y) >> pp.dshift) & (pp.R - 1u);
+    } else if constexpr (KIND == KIND_KEY_BITS) {
+        const uint64_t wnd = pp.dflip ? ((((uint64_t)y << 32) | x) ^ 0x8000000000000000ull)
+                                      : (((uint64_t)__builtin_bswap32(x) << 32) | __builtin_bswap32(y));
+        return (uint32_t)(wnd >> pp.dshift) & (pp.R - 1u);
     } else if constexpr (KIND == SGX_PART_RANGE_I64) {
         return range_pid_i64((int64_t)(((uint64_t)y << 32) | x), bi64, pp.nb, pp.ascending);
     } else {
@@ -297,6 +301,7 @@ hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
         }
         break;
     case KIND_DIGIT: if (r16) SGX_HIST(KIND_DIGIT, true); else SGX_HIST(KIND_DIGIT, false); break;
+    case KIND_KEY_BITS: if (r16) SGX_HIST(KIND_KEY_BITS, true); else SGX_HIST(KIND_KEY_BITS, false); break;
     default: break;
     }
 #undef SGX_HIST
@@ -1612,12 +1617,196 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------
+// The sorted read's bucket sort.  After the key-window passes (KIND_KEY_BITS) and the pass by
+// the shuffle's partitioner, the records are ordered by bucket = (P << kbits) | window bits;
+// each bucket (a few dozen records when the window is sized to the data) is sorted stably by
+// its full key ON CHIP: a workgroup owns the buckets that START in its TILE of positions
+// (plus a HALO to reach the last one's end), stages the records in LDS, finds every
+// record's bucket bounds by two block scans of the boundary flags, ranks each record among
+// its bucket by comparison (key, then position: stable) and writes the bucket region out
+// through the inverse permutation, coalesced.  One read + one write of every record instead
+// of the 7-9 LSD digit passes that remain below the window.
+// ------------------------------------------------------------------------------------
+constexpr int BS_THREADS = 256;
+
+template <int RB>
+struct BucketKey;
+template <>
+struct BucketKey<16> {  // signed Long key, compared as sign-flipped unsigned
+    uint64_t k;
+    __device__ static BucketKey at(const uint32_t *r) {
+        return BucketKey{(((uint64_t)r[1] << 32) | r[0]) ^ 0x8000000000000000ull};
+    }
+    __device__ bool lt(const BucketKey &o) const { return k < o.k; }
+    __device__ bool eq(const BucketKey &o) const { return k == o.k; }
+    __device__ uint64_t window() const { return k; }
+};
+template <>
+struct BucketKey<100> {  // 10-byte unsigned big-endian key
+    uint64_t hi;
+    uint32_t lo;
+    __device__ static BucketKey at(const uint32_t *r) {
+        return BucketKey{((uint64_t)__builtin_bswap32(r[0]) << 32) | __builtin_bswap32(r[1]),
+                         __builtin_bswap32(r[2]) >> 16};
+    }
+    __device__ bool lt(const BucketKey &o) const { return hi < o.hi || (hi == o.hi && lo < o.lo); }
+    __device__ bool eq(const BucketKey &o) const { return hi == o.hi && lo == o.lo; }
+    __device__ uint64_t window() const { return hi; }
+};
+
+template <int RB, int TILE, int HALO>
+__global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                            int64_t n, PartParams pp, int use_p, uint32_t kshift,
+                                                            uint32_t kbits, uint32_t *err) {
+    constexpr int DW = RB / 4;
+    constexpr int CAP = TILE + HALO + 1;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    uint32_t *rec = (uint32_t *)smem;                      // CAP records
+    uint16_t *bs = (uint16_t *)(rec + (size_t)CAP * DW);   // bucket start of each local position
+    uint16_t *be = bs + CAP;                               // bucket end
+    uint16_t *inv = be + CAP;                              // output slot -> local position
+    uint8_t *flag = (uint8_t *)(inv + CAP);                // a bucket starts here
+    __shared__ uint32_t s_a, s_b, s_scr[BS_THREADS / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t t0 = (int64_t)blockIdx.x * TILE;
+    if (t0 >= n) return;
+    const int64_t t1 = min(n, t0 + TILE);
+    const int64_t L0 = t0 > 0 ? t0 - 1 : 0, L1 = min(n, t1 + HALO);
+    const int m = (int)(L1 - L0);
+    const uint64_t wmask = kbits >= 64 ? ~0ull : ((1ull << kbits) - 1ull);
+    auto comp = [&](int j) -> uint64_t {
+        const uint32_t *r = rec + (size_t)j * DW;
+        const uint64_t bits = (BucketKey<RB>::at(r).window() >> kshift) & wmask;
+        const uint64_t p = use_p ? (uint64_t)hash_pid(r[0], r[1], pp) : 0ull;
+        return (p << kbits) | bits;
+    };
+    for (int u = (int)tid; u < m * DW; u += BS_THREADS) rec[u] = in[L0 * DW + u];
+    if (tid == 0) {
+        s_a = 0xFFFFFFFFu;
+        s_b = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    // boundary flags; the first nominal boundary (a) and the first boundary at or past t1 (b)
+    for (int j = (int)tid; j < m; j += BS_THREADS) {
+        const int64_t pos = L0 + j;
+        const bool f = pos == 0 || (j > 0 && comp(j) != comp(j - 1));
+        flag[j] = f ? 1 : 0;
+        if (f && pos >= t0 && pos < t1) atomicMin(&s_a, (uint32_t)j);
+        if (f && pos >= t1) atomicMin(&s_b, (uint32_t)j);
+    }
+    __syncthreads();
+    const uint32_t a = s_a;
+    uint32_t b = s_b;
+    if (b == 0xFFFFFFFFu) {
+        if (L1 == n) b = (uint32_t)m;  // the array's end closes the last bucket
+        else {
+            if (tid == 0 && a != 0xFFFFFFFFu) atomicOr(err, 4u);  // a bucket longer than the halo
+            return;
+        }
+    }
+    if (a == 0xFFFFFFFFu) return;  // no bucket starts in this tile
+    // bucket bounds of every position in [a, b): start = last flag <= j (prefix max), end =
+    // next flag > j (suffix min); one contiguous run of positions per thread
+    const int len = (int)(b - a);
+    const int per = (len + BS_THREADS - 1) / BS_THREADS;
+    const int j0 = (int)a + min(len, (int)tid * per), j1 = (int)a + min(len, ((int)tid + 1) * per);
+    {
+        int run = -1;
+        for (int j = j0; j < j1; ++j) if (flag[j]) run = j;
+        // exclusive prefix max over threads (run of the previous threads)
+        int x = run;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(x, d, 64);
+            if (lane >= (uint32_t)d) x = max(x, y);
+        }
+        if (lane == 63) s_scr[w] = (uint32_t)(x + 1);
+        __syncthreads();
+        int prev = __shfl_up(x, 1, 64);
+        if (lane == 0) prev = -1;
+        for (uint32_t v = 0; v < w; ++v) prev = max(prev, (int)s_scr[v] - 1);
+        int cur = prev;
+        for (int j = j0; j < j1; ++j) {
+            if (flag[j]) cur = j;
+            bs[j] = (uint16_t)cur;
+        }
+        __syncthreads();
+        int nxt = 0x7FFFFFFF;
+        for (int j = j1 - 1; j >= j0; --j) if (flag[j]) nxt = j;
+        int y2 = nxt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int z = __shfl_down(y2, d, 64);
+            if (lane + d < 64) y2 = min(y2, z);
+        }
+        if (lane == 0) s_scr[w] = (uint32_t)y2;
+        __syncthreads();
+        int after = __shfl_down(y2, 1, 64);
+        if (lane == 63) after = 0x7FFFFFFF;
+        for (uint32_t v = w + 1; v < BS_THREADS / 64; ++v) after = min(after, (int)s_scr[v]);
+        int e = min(after, (int)b);
+        for (int j = j1 - 1; j >= j0; --j) {
+            be[j] = (uint16_t)e;
+            if (flag[j]) e = j;
+        }
+    }
+    __syncthreads();
+    // stable rank inside the bucket: keys below, plus equal keys at earlier positions
+    for (int j = (int)a + (int)tid; j < (int)b; j += BS_THREADS) {
+        const int s0 = bs[j], e0 = be[j];
+        const BucketKey<RB> kj = BucketKey<RB>::at(rec + (size_t)j * DW);
+        int rank = 0;
+        for (int i = s0; i < e0; ++i) {
+            const BucketKey<RB> ki = BucketKey<RB>::at(rec + (size_t)i * DW);
+            rank += (ki.lt(kj) || (i < j && ki.eq(kj))) ? 1 : 0;
+        }
+        inv[s0 + rank] = (uint16_t)j;
+    }
+    __syncthreads();
+    // the bucket region, coalesced: output position L0 + p takes local record inv[p]
+    for (int u = (int)tid; u < len * DW; u += BS_THREADS) {
+        const int p = (int)a + u / DW, q = u % DW;
+        out[(L0 + p) * DW + q] = rec[(size_t)inv[p] * DW + q];
+    }
+}
+
+template <int RB, int TILE, int HALO>
+static size_t bucket_sort_lds() {
+    constexpr int CAP = TILE + HALO + 1;
+    return (size_t)CAP * RB + (size_t)CAP * 6 + (size_t)CAP + 16;
+}
+
+hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, const PartParams &pp, int use_p,
+                              uint32_t kshift, uint32_t kbits, uint32_t *err, hipStream_t stream) {
+    if (n <= 0) return hipSuccess;
+    if (rb == 16) {
+        constexpr int T = 2048, H = 512;
+        const size_t lds = bucket_sort_lds<16, T, H>();
+        (void)hipFuncSetAttribute((const void *)k_bucket_sort<16, T, H>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        hipLaunchKernelGGL((k_bucket_sort<16, T, H>), dim3((unsigned)((n + T - 1) / T)), dim3(BS_THREADS), lds, stream,
+                           (const uint32_t *)in, (uint32_t *)out, n, pp, use_p, kshift, kbits, err);
+    } else if (rb == 100) {
+        constexpr int T = 384, H = 256;
+        const size_t lds = bucket_sort_lds<100, T, H>();
+        (void)hipFuncSetAttribute((const void *)k_bucket_sort<100, T, H>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  (int)lds);
+        hipLaunchKernelGGL((k_bucket_sort<100, T, H>), dim3((unsigned)((n + T - 1) / T)), dim3(BS_THREADS), lds,
+                           stream, (const uint32_t *)in, (uint32_t *)out, n, pp, use_p, kshift, kbits, err);
+    } else {
+        return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t chunk, int G,
                           const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
                           uint32_t *err, hipStream_t stream) {
     const bool pow2 = (pp.R & (pp.R - 1)) == 0;
     if (rb == 16 && geo.waves >= WC_GEOM_BASE) {
-        if ((pp.kind != SGX_PART_HASH && pp.kind != KIND_DIGIT && pp.kind != KIND_HASH_BITS) ||
+        if ((pp.kind != SGX_PART_HASH && pp.kind != KIND_DIGIT && pp.kind != KIND_HASH_BITS &&
+             pp.kind != KIND_KEY_BITS) ||
             geo.waves != WC_GEOM_BASE + 8 || geo.mbits != 16)
             return hipErrorInvalidValue;
 #define SGX_WC(K, NI)                                                                            \
@@ -1630,6 +1819,11 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         if (pp.kind == KIND_DIGIT) {
             if (geo.items != 12 || pp.R != DIGIT_R) return hipErrorInvalidValue;
             SGX_WC(KIND_DIGIT, 12);
+        } else if (pp.kind == KIND_KEY_BITS) {
+            if (!pow2) return hipErrorInvalidValue;
+            if (geo.items == 12) SGX_WC(KIND_KEY_BITS, 12);
+            else if (geo.items == 8) SGX_WC(KIND_KEY_BITS, 8);
+            else return hipErrorInvalidValue;
         } else if (pp.kind == KIND_HASH_BITS) {
             if (!pow2) return hipErrorInvalidValue;
             if (geo.items == 12) SGX_WC(KIND_HASH_BITS, 12);
@@ -1722,6 +1916,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
             if (pow2) SGX_W2(KIND_HASH_POW2); else SGX_W2(SGX_PART_HASH);
             break;
         case KIND_DIGIT: SGX_W2(KIND_DIGIT); break;
+        case KIND_KEY_BITS: SGX_W2(KIND_KEY_BITS); break;
         case SGX_PART_RANGE_I64: SGX_W2(SGX_PART_RANGE_I64); break;
         default: SGX_W2(SGX_PART_RANGE_BYTES10); break;
         }

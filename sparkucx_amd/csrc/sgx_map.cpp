@@ -47,8 +47,9 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
         const ScatterGeom w2 = scatter_geom_wide2((uint32_t)R, rb, kind, spp.nb);
         if (w2.items) geo = w2;
     }
-    // the reduce side's digit passes run on the write-combining / wide-record kernels only
-    if (kind == KIND_DIGIT) {
+    // the reduce side's digit / key-window passes run on the write-combining / wide-record
+    // kernels only
+    if (kind == KIND_DIGIT || kind == KIND_KEY_BITS) {
         if (rb == 16) geo = scatter_geom16_wc((uint32_t)R);
         if (geo.waves < WC_GEOM_BASE && geo.waves != WIDE2_GEOM_TAG)
             return fail_msg(SGX_ERR_UNSUPPORTED, "digit pass on %d B records at this alignment", rb);

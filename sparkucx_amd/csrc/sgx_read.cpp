@@ -273,24 +273,77 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
     HIP_TRY(hipStreamSynchronize(st));
     const bool skip = !(e->flags & SGX_FLAG_SORT_ALL_DIGITS);
     int cur = 0, np = 0;
-    for (int d = 0; d < ndig; ++d) {
-        const int byte = rb == 16 ? d : 9 - d;  // digit d of the LSD order
-        bool trivial = false;
-        for (int b = 0; b < 256; ++b)
-            if (dh[(size_t)byte * 256 + (size_t)b] == (uint32_t)n) trivial = true;
-        if (trivial && skip) continue;
-        ++np;
-        PartParams dp{};
-        dp.kind = KIND_DIGIT;
-        dp.R = DIGIT_R;
-        dp.nbits = 8;
-        dp.dshift = rb == 16 ? 8u * (uint32_t)d : 8u * (uint32_t)(9 - d);
-        dp.dflip = (rb == 16 && d == 7) ? 0x80u : 0u;
-        SGX_TRY(partition_pass(e, c, c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, dp, (int32_t)DIGIT_R, KIND_DIGIT,
-                               nullptr, errs + np - 1, false));
-        cur ^= 1;
-    }
     const bool range_asc = s.kind != SGX_PART_HASH && s.asc;
+    // Bucket path: a window of the key's top varying bits, sized so a bucket (P, window)
+    // holds ~64 records, taken in <= 10-bit LSD passes (KIND_KEY_BITS), then the pass by the
+    // partitioner, then every bucket sorted on chip (launch_bucket_sort) -- 2-4 passes instead
+    // of up to 8-10 digit passes + 1.  Skewed keys (the top varying byte's largest value
+    // holding > 1/16 of the records) keep the digit passes, whose trivial digits are skipped.
+    const bool use_p = by_partition && !range_asc && s.R > 1;
+    if (skip && !(e->flags & SGX_FLAG_NO_BUCKET_SORT) && (use_p ? s.kind == SGX_PART_HASH : true)) {
+        int top_byte = -1;  // most significant varying key byte, as a bit position of the window
+        uint32_t maxbin = 0;
+        for (int d = ndig - 1; d >= 0 && top_byte < 0; --d) {
+            const int byte = rb == 16 ? d : 9 - d;
+            uint32_t mx = 0;
+            for (int b = 0; b < 256; ++b) mx = std::max(mx, dh[(size_t)byte * 256 + (size_t)b]);
+            if (mx == (uint32_t)n) continue;  // constant byte
+            maxbin = mx;
+            top_byte = byte;
+        }
+        // window top bit: 16 B -> 8 * (byte + 1) of the sign-flipped Long; 100 B -> the first 8
+        // key bytes big-endian, byte j ends at bit 64 - 8 j (bytes 8, 9 are outside the window)
+        const int top = top_byte < 0 ? 64 : (rb == 16 ? 8 * (top_byte + 1) : (top_byte < 8 ? 64 - 8 * top_byte : -1));
+        const double rp = use_p ? (double)s.R : 1.0;
+        int kbits = 0;
+        while (kbits < 30 && (double)n / (rp * (double)(1ull << kbits)) > 64.0) ++kbits;
+        kbits = std::min(kbits, std::max(top, 0));
+        const bool eligible = top_byte >= 0 && top > 0 && (uint64_t)maxbin * 16 <= (uint64_t)n &&
+                              (double)n / (rp * (double)(1ull << kbits)) <= 256.0;
+        if (eligible) {
+            const int lo = top - kbits;
+            for (int b0 = lo; b0 < top; b0 += 10) {  // least significant window chunk first
+                const int cb = std::min(10, top - b0);
+                PartParams kp{};
+                kp.kind = KIND_KEY_BITS;
+                kp.R = 1u << cb;
+                kp.nbits = (uint32_t)cb;
+                kp.dshift = (uint32_t)b0;
+                kp.dflip = rb == 16 ? 1u : 0u;
+                SGX_TRY(partition_pass(e, c, c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, kp, (int32_t)kp.R,
+                                       KIND_KEY_BITS, nullptr, errs + np, false));
+                cur ^= 1;
+                ++np;
+            }
+            if (use_p) {
+                SGX_TRY(partition_pass(e, c, c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, s.pp, s.R, s.kind,
+                                       nullptr, errs + np, false));
+                cur ^= 1;
+                ++np;
+            }
+            HIP_TRY(launch_bucket_sort(c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, s.pp, use_p ? 1 : 0,
+                                       (uint32_t)lo, (uint32_t)kbits, errs + np, st));
+            SGX_TRY(debug_sync(e, st, "bucket sort"));
+            ++np;
+            uint32_t herr[MAXP];
+            HIP_TRY(hipMemcpyAsync(herr, c.sort_err.p, MAXP * 4, hipMemcpyDeviceToHost, st));
+            HIP_TRY(hipStreamSynchronize(st));
+            for (int i = 0; i < np; ++i) {
+                if (herr[i] & 1u) return fail_msg(SGX_ERR_TIMEOUT, "sort pass %d: scan look-back spin gave up", i);
+                if (herr[i] & 2u) return fail_msg(SGX_ERR_HIP, "sort pass %d: a scatter destination was out of range", i);
+            }
+            if (!(herr[np - 1] & 4u)) {
+                HIP_TRY(hipEventRecord(t1, st));
+                e->record_stage(SGX_STAGE_SORT, t0, t1);
+                *sorted = c.sort_buf[cur ^ 1].p;
+                return SGX_OK;
+            }
+            // a bucket too long for the chip: the digit passes below finish from the bucket
+            // sort's input (stable passes: any stable order of the input sorts the same)
+            HIP_TRY(hipMemsetAsync(c.sort_err.p, 0, MAXP * 4, st));
+            np = 0;
+        }
+    }
     if (by_partition && !range_asc && s.R > 1) {
         SGX_TRY(partition_pass(e, c, c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, s.pp, s.R, s.kind, nullptr,
                                errs + np, false));

@@ -336,3 +336,46 @@ def test_size_query_result_reuse_and_invalidation(sgx_lib, oracle_lib):
         assert np.array_equal(got, np.concatenate(seqs))
     finally:
         e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [0, 64])  # bucket path / SGX_FLAG_NO_BUCKET_SORT (digit passes only)
+@pytest.mark.parametrize("case", ["hash16_R1", "hash16_R7", "hash16_R1024", "hash16_R4096", "range16_asc",
+                                  "range16_desc", "tera_range", "tera_hash", "dups_in_bucket", "long_bucket"])
+def test_sorted_bucket_path(sgx_lib, oracle_lib, flags, case):
+    """The sorted read's bucket path (key-window passes -> partitioner pass -> every (P, window)
+    bucket sorted on chip) against the oracle, at sizes where the window takes one or two
+    passes, for hash and range partitioners, 16 B and TeraSort 100 B records; equal keys
+    inside a bucket (stability on chip), and a bucket longer than the chip's halo (the kernel
+    gives up and the digit passes finish from its input)."""
+    rng = np.random.default_rng(hash(case) % 1000)
+    if case.startswith("hash16"):
+        R = int(case.split("_R")[1])
+        maps = [oracle_lib.gen_uniform16(n, 500 + i, value_base=i << 32) for i, n in enumerate((300_001, 77_777))]
+        _run(sgx_lib, oracle_lib, maps, R, flags=flags)
+    elif case.startswith("range16"):
+        maps = [oracle_lib.gen_uniform16(n, 600 + i) for i, n in enumerate((250_000, 50_000))]
+        allk = np.concatenate([m[:, :8].copy().view("<i8").reshape(-1) for m in maps])
+        bounds = np.unique(np.sort(rng.choice(allk, 255)))
+        _run(sgx_lib, oracle_lib, maps, len(bounds) + 1, sgx_lib.PART_RANGE_I64, bounds, case.endswith("asc"),
+             flags=flags)
+    elif case.startswith("tera"):
+        maps = [oracle_lib.gen_terasort100(n, 700 + i) for i, n in enumerate((120_000, 30_001))]
+        maps[0][1000:1100, :10] = maps[0][999, :10]  # 101 equal keys: one bucket, stable on chip
+        R = 128
+        if case == "tera_range":
+            sample = np.concatenate(maps)[rng.choice(150_001, 20 * R, replace=False), :10]
+            sample = sample[np.lexsort(sample.T[::-1])]
+            bounds = np.ascontiguousarray(sample[np.linspace(0, len(sample) - 1, R - 1).astype(int)])
+            _run(sgx_lib, oracle_lib, maps, R, sgx_lib.PART_RANGE_BYTES10, bounds, flags=flags)
+        else:
+            _run(sgx_lib, oracle_lib, maps, R, flags=flags)
+    elif case == "dups_in_bucket":
+        recs = oracle_lib.gen_uniform16(400_000, 800)
+        recs[::7, :8] = recs[1::7][:len(recs[::7]), :8]  # pairs of equal keys everywhere
+        recs[5000:5200, :8] = recs[4999, :8]              # 200 equal keys
+        _run(sgx_lib, oracle_lib, [recs], 1024, flags=flags)
+    else:  # long_bucket: 3000 equal keys in one reducer -> longer than the halo -> fallback
+        recs = oracle_lib.gen_uniform16(300_000, 900)
+        recs[10_000:13_000, :8] = recs[9_999, :8]
+        _run(sgx_lib, oracle_lib, [recs], 256, flags=flags)
