@@ -89,8 +89,10 @@ def test_oracle_xxh32_matches_xxhash(oracle_lib):
 
 @pytest.fixture(scope="module", params=["wave-decode", "lane-decode"])
 def dec_engine(request, sgx_lib):
-    """An engine per LZ4 decoder: k_lz4_decode for every frame (the default below 32768
-    frames), and k_lz4_decode_lanes for every compressed frame (SGX_FLAG_LZ4_LANE_DECODE)."""
+    """An engine per LZ4 decoder.  wave-decode (the default): compressed frames go through
+    k_lz4_decode (one wave per frame) below 32768 frames, and RAW frames through
+    k_lz4_raw_lanes (one lane per frame) from 2048 frames on (k_lz4_decode below that);
+    lane-decode (SGX_FLAG_LZ4_LANE_DECODE): every compressed frame through k_lz4_decode_lanes."""
     flags = sgx_lib.FLAG_LZ4_LANE_DECODE if request.param == "lane-decode" else 0
     with sgx_lib.ShuffleEngine(device=0, flags=flags) as e:
         yield e
@@ -289,6 +291,34 @@ def test_gpu_unframe_dense_frames(dec_engine, oracle_lib):
     np.cumsum([len(p) for p in parts], out=offs[1:])
     want, _ = oracle_lib.lz4_frame_partitions(np.frombuffer(stream, np.uint8), offs)
     assert dec_engine.lz4_unframe(want).tobytes() == stream
+
+
+def test_gpu_unframe_mixed_raw_and_compressed_many_frames(dec_engine, oracle_lib):
+    """>= 2048 frames mixing RAW frames (incompressible blocks) and LZ4 ones (repetitive
+    blocks) in one buffer: in the default engine the RAW ones take k_lz4_raw_lanes while the
+    compressed ones take k_lz4_decode with the RAW frames skipped -- both kernels write the
+    same output buffer; the result must equal the stream, also through the per-stream walks."""
+    rng = np.random.default_rng(21)
+    parts = []
+    for i in range(900):  # ~2.7 frames of 1 KiB blocks per stream -> ~2400 frames
+        blocks = []
+        for k in range(int(rng.integers(2, 5))):
+            if (i + k) % 3 == 0:  # incompressible: a RAW frame
+                blocks.append(rng.integers(0, 256, 1024, dtype=np.uint8).tobytes())
+            else:  # periodic: an LZ4 frame
+                pat = rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8).tobytes()
+                blocks.append((pat * (1024 // len(pat) + 1))[:1024])
+        parts.append(b"".join(blocks)[: int(rng.integers(1500, 4097))])
+    stream = b"".join(parts)
+    offs = np.zeros(len(parts) + 1, dtype=np.int64)
+    np.cumsum([len(p) for p in parts], out=offs[1:])
+    framed, lens = oracle_lib.lz4_frame_partitions(np.frombuffer(stream, np.uint8), offs, 1024)
+    frames = [f for r in range(len(lens)) for f in parse_frames(
+        framed.tobytes()[int(lens[:r].sum()):int(lens[:r + 1].sum())])[:-1]]
+    methods = {f[0] & 0xF0 for f in frames}
+    assert len(frames) >= 2048 and methods == {0x10, 0x20}, (len(frames), methods)
+    assert dec_engine.lz4_unframe(framed).tobytes() == stream
+    assert dec_engine.lz4_unframe(framed, stream_lens=lens).tobytes() == stream
 
 
 def _overlap_cases():
