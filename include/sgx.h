@@ -269,7 +269,8 @@ int sgx_comm_size(sgx_engine *e, int32_t *nranks, int32_t *rank);
  * holds that no earlier exchange carried -- any number, none included: Spark's map tasks land
  * on executors independently -- and afterwards every rank holds its reducers' blocks
  * (sgx_shuffle_reducers) of every map of every rank.  Steps: an all-gather of each rank's map
- * count, an all-gather of {map id, R lengths} per map, then ONE grouped exchange of the
+ * count with its first map's {map id, R lengths} (a second all-gather of every map's, only
+ * when some rank holds more than one), then ONE grouped exchange of the
  * partition-contiguous map outputs (already grouped by destination: no pack step) into this
  * rank's receive buffer, laid out [source rank][its maps][my reducers].  Asynchronous on the
  * engine's exchange stream; completes at sgx_sync (fetches and reads wait for it on the GPU).

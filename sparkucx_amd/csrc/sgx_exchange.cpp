@@ -175,11 +175,30 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
             lens.insert(lens.end(), lm.lens.begin(), lm.lens.end());
         }
     } else {
+        // first all-gather: [map count | the first map's {id, lengths}] per rank -- the whole
+        // round when every rank holds at most one map (the pipelined exchange_maps step)
         const int64_t nloc = (int64_t)mine.size();
-        SGX_TRY(allgather_i64(e, &nloc, 1, counts.data()));
+        std::vector<int64_t> first(1 + row, 0), firsts((1 + row) * (size_t)P, 0);
+        first[0] = nloc;
+        if (nloc > 0) {
+            first[1] = mine[0].id;
+            std::memcpy(&first[2], mine[0].lens.data(), sizeof(int64_t) * (size_t)R);
+        }
+        SGX_TRY(allgather_i64(e, first.data(), first.size(), firsts.data()));
         int64_t mmax = 0;
-        for (int64_t v : counts) mmax = std::max(mmax, v);
-        if (mmax > 0) {
+        for (int32_t j = 0; j < P; ++j) {
+            counts[(size_t)j] = firsts[(size_t)j * (1 + row)];
+            mmax = std::max(mmax, counts[(size_t)j]);
+        }
+        if (mmax <= 1) {
+            for (int32_t j = 0; j < P; ++j)
+                if (counts[(size_t)j] == 1) {
+                    const int64_t *q = &firsts[(size_t)j * (1 + row) + 1];
+                    ids.push_back(q[0]);
+                    srcs.push_back(j);
+                    lens.insert(lens.end(), q + 1, q + 1 + R);
+                }
+        } else {  // second all-gather: every map's {id, lengths}, padded to the largest count
             std::vector<int64_t> send(row * (size_t)mmax, 0), recv(row * (size_t)mmax * (size_t)P, 0);
             for (size_t k = 0; k < mine.size(); ++k) {
                 send[k * row] = mine[k].id;
