@@ -293,6 +293,7 @@ def test_gpu_unframe_dense_frames(dec_engine, oracle_lib):
     assert dec_engine.lz4_unframe(want).tobytes() == stream
 
 
+@pytest.mark.gpu
 def test_gpu_unframe_mixed_raw_and_compressed_many_frames(dec_engine, oracle_lib):
     """>= 2048 frames mixing RAW frames (incompressible blocks) and LZ4 ones (repetitive
     blocks) in one buffer: in the default engine the RAW ones take k_lz4_raw_lanes while the
