@@ -20,12 +20,13 @@ def main():
     ap.add_argument("--partitions", type=int, default=1024)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--cases", default="sorted:uniform,group:uniform,sum:zipf,sorted:terasort")
+    ap.add_argument("--flags", type=int, default=0, help="sgx_config.flags (64 = SGX_FLAG_NO_BUCKET_SORT)")
     a = ap.parse_args()
     import numpy as np
 
     import sparkucx_amd as sgx
 
-    e = sgx.ShuffleEngine(0)
+    e = sgx.ShuffleEngine(0, flags=a.flags)
     R = a.partitions
     sid = 0
     for case in a.cases.split(","):
