@@ -251,7 +251,8 @@ static int records_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_id
 // (skipped for an ascending RangePartitioner, whose partition order is key order).  One read
 // of the keys histograms every digit; a digit with a single non-empty bucket is the identity
 // permutation and is skipped (unless SGX_FLAG_SORT_ALL_DIGITS).
-int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool by_partition, const void **sorted) {
+int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool by_partition, const void **sorted,
+                      int32_t nparts) {
     const int rb = s.rb;
     if (rb != 16 && rb != 100)
         return fail_msg(SGX_ERR_UNSUPPORTED, "sorted read needs 16 B (Long, Long) or 100 B TeraSort records, not %d B",
@@ -294,7 +295,7 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
         // window top bit: 16 B -> 8 * (byte + 1) of the sign-flipped Long; 100 B -> the first 8
         // key bytes big-endian, byte j ends at bit 64 - 8 j (bytes 8, 9 are outside the window)
         const int top = top_byte < 0 ? 64 : (rb == 16 ? 8 * (top_byte + 1) : (top_byte < 8 ? 64 - 8 * top_byte : -1));
-        const double rp = use_p ? (double)s.R : 1.0;
+        const double rp = use_p ? (double)(nparts > 0 ? std::min(nparts, s.R) : s.R) : 1.0;
         int kbits = 0;
         while (kbits < 30 && (double)n / (rp * (double)(1ull << kbits)) > 64.0) ++kbits;
         kbits = std::min(kbits, std::max(top, 0));
@@ -343,6 +344,25 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
             HIP_TRY(hipMemsetAsync(c.sort_err.p, 0, MAXP * 4, st));
             np = 0;
         }
+    }
+    // LSD digit passes (8-bit digits, least significant first); a digit whose histogram has
+    // one non-empty bucket is the identity permutation and is skipped
+    for (int d = 0; d < ndig; ++d) {
+        const int byte = rb == 16 ? d : 9 - d;  // digit d of the LSD order
+        bool trivial = false;
+        for (int b = 0; b < 256; ++b)
+            if (dh[(size_t)byte * 256 + (size_t)b] == (uint32_t)n) trivial = true;
+        if (trivial && skip) continue;
+        ++np;
+        PartParams dp{};
+        dp.kind = KIND_DIGIT;
+        dp.R = DIGIT_R;
+        dp.nbits = 8;
+        dp.dshift = rb == 16 ? 8u * (uint32_t)d : 8u * (uint32_t)(9 - d);
+        dp.dflip = (rb == 16 && d == 7) ? 0x80u : 0u;
+        SGX_TRY(partition_pass(e, c, c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, dp, (int32_t)DIGIT_R, KIND_DIGIT,
+                               nullptr, errs + np - 1, false));
+        cur ^= 1;
     }
     if (by_partition && !range_asc && s.R > 1) {
         SGX_TRY(partition_pass(e, c, c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, s.pp, s.R, s.kind, nullptr,
@@ -475,7 +495,7 @@ extern "C" int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t 
         int64_t n = 0;
         const void *sorted = nullptr;
         SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
-        SGX_TRY(sort_records(e, *c, *s, n, true, &sorted));
+        SGX_TRY(sort_records(e, *c, *s, n, true, &sorted, end_partition - start_partition));
         rc_store(*c, epoch, RC_SORTED, 0, shuffle_id, map_ids, nmaps, start_partition, end_partition, n, 0, sorted,
                  nullptr, nullptr, nullptr);
         *out_bytes = n * rb;
@@ -504,7 +524,7 @@ extern "C" int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t 
         sorted = c->rc.sorted;
     } else {
         SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
-        SGX_TRY(sort_records(e, *c, *s, n, true, &sorted));
+        SGX_TRY(sort_records(e, *c, *s, n, true, &sorted, end_partition - start_partition));
     }
     *out_bytes = n * rb;
     if (n * rb > dst_cap)
@@ -574,7 +594,7 @@ extern "C" int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t
     } else {
         SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
         const void *sorted = nullptr;
-        SGX_TRY(sort_records(e, *c, *s, n, true, &sorted));
+        SGX_TRY(sort_records(e, *c, *s, n, true, &sorted, end_partition - start_partition));
         SGX_TRY(group_records(e, *c, sorted, n, agg, &ng, &dkeys, &dstarts, &dvals));
     }
     const int64_t nvals = agg == SGX_AGG_GROUP ? n : ng;
