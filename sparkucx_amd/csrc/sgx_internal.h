@@ -96,12 +96,15 @@ int64_t scan_tiles(int64_t len);
 // csum[s][g] = sum over the Q sub-partitions q of counts[(s*Q + q)][g]   (S*G entries);
 // desc: the level-2 pieces cut from the level-1 offsets (offs1[S][G], u32) -- each piece a
 // run of whole (super, chunk) blocks inside one super-partition, about `target` records --
-// as {begin, end, super, first chunk} int64 quadruples, their count in *ndesc;
+// as {begin, -, super, first chunk} int64 quadruples (a piece ends at the next one's begin),
+// their count in npieces[1] (flags / idx: S*G u32 scratch; status / ticket: a zeroed scan
+// work area of scan_tiles(S*G) tiles);
 // launch_scatter16_seg: level 2, write-combining K4 with R = Q over the pieces, cursors
 // offs[(super*Q + q)][chunk] of the single-level scan.
 hipError_t launch_super_counts(const uint32_t *counts, uint32_t *csum, int S, int Q, int G, hipStream_t stream);
 hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, int64_t n, int64_t target, int64_t *desc,
-                           uint32_t *ndesc, hipStream_t stream);
+                           uint32_t *flags, uint32_t *idx, uint64_t *status, uint32_t *ticket, uint32_t *err,
+                           uint32_t *npieces, hipStream_t stream);
 hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
                                 int G, const int64_t *desc, const uint32_t *ndesc, int grid, const ScatterGeom &geo,
                                 uint32_t *err, hipStream_t stream);

@@ -1024,8 +1024,8 @@ __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
 }
 
 // SEG (level 2 of the two-level split, launch_scatter16_seg): the workgroup's records are
-// desc[blockIdx.x] = {begin, end, super s, chunk g} instead of chunk blockIdx.x, and its R
-// streams start at offs[(s * R + p) * G + g].
+// piece desc[blockIdx.x] = {begin, -, super s, chunk g}, up to the next piece's begin,
+// instead of chunk blockIdx.x, and its R streams start at offs[(s * R + p) * G + g].
 template <int KIND, int WAVES, int NI, int SI, bool SEG = false>
 __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__restrict__ in,
                                                                 u32x4 *__restrict__ out, int64_t n,
@@ -1057,7 +1057,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         if (blockIdx.x >= *ndesc) return;  // the whole workgroup, before any barrier
         const int64_t *d = desc + 4 * (int64_t)blockIdx.x;
         begin = d[0];
-        end = min(n, d[1]);
+        end = blockIdx.x + 1 < *ndesc ? d[4] : n;  // the next piece's begin
         obase = d[2] * (int64_t)R;
         g = (int)d[3];
     }
@@ -1551,50 +1551,42 @@ hipError_t launch_super_counts(const uint32_t *counts, uint32_t *csum, int S, in
     return hipGetLastError();
 }
 
-// One workgroup: block i = s*G + g (s-major, the level-1 layout) starts a piece when g == 0
-// or when it crosses a multiple of `target` records; the pieces are compacted in order by a
-// block-wide scan of the flags.  A piece ends where the next begins (the supers are
-// contiguous), the last one at n.
-constexpr int DESC_THREADS = 1024;
-__global__ __launch_bounds__(DESC_THREADS) void k_seg_desc(const uint32_t *__restrict__ offs1, int S, int G, int64_t n,
-                                                           int64_t target, int64_t *__restrict__ desc,
-                                                           uint32_t *__restrict__ ndesc) {
-    __shared__ uint32_t scratch[DESC_THREADS / 64];
-    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const int64_t nb = (int64_t)S * G;
-    const int64_t per = (nb + DESC_THREADS - 1) / DESC_THREADS;
-    const int64_t i0 = min(nb, (int64_t)tid * per), i1 = min(nb, i0 + per);
-    auto flag = [&](int64_t i) {
-        const int64_t g = i % G;
-        return g == 0 || (int64_t)offs1[i] / target != (int64_t)offs1[i - 1] / target;
-    };
-    uint32_t cnt = 0;
-    for (int64_t i = i0; i < i1; ++i) cnt += flag(i) ? 1u : 0u;
-    const uint32_t x = wave_inclusive_scan(cnt, lane);
-    if (lane == 63) scratch[w] = x;
-    __syncthreads();
-    uint32_t k = x - cnt, total = 0;
-    for (uint32_t v = 0; v < DESC_THREADS / 64; ++v) {
-        if (v < w) k += scratch[v];
-        total += scratch[v];
-    }
-    for (int64_t i = i0; i < i1; ++i) {
-        if (!flag(i)) continue;
-        int64_t j = i + 1;  // the next piece's first block (a few blocks on: one per super at least)
-        while (j < nb && !flag(j)) ++j;
-        int64_t *d = desc + 4 * (int64_t)k;
-        d[0] = offs1[i];
-        d[1] = j < nb ? (int64_t)offs1[j] : n;
-        d[2] = i / G;
-        d[3] = i % G;
-        ++k;
-    }
-    if (tid == 0) *ndesc = total;
+// Level-2 pieces.  Block i = s*G + g (s-major, the level-1 layout) starts a piece when g == 0
+// or when it crosses a multiple of `target` records (k_seg_flags); an exclusive scan of the
+// flags (K3) numbers the pieces, and k_seg_desc writes piece k = {begin, -, super, chunk}.
+// A piece ends where the next begins (the supers are contiguous), the last one at n: the
+// level-2 kernel reads its end from its successor's begin.
+__global__ __launch_bounds__(256) void k_seg_flags(const uint32_t *__restrict__ offs1, int S, int G, int64_t target,
+                                                   uint32_t *__restrict__ flags) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)S * G) return;
+    const bool f = i % G == 0 || (int64_t)offs1[i] / target != (int64_t)offs1[i - 1] / target;
+    flags[i] = f ? 1u : 0u;
+}
+
+__global__ __launch_bounds__(256) void k_seg_desc(const uint32_t *__restrict__ offs1, const uint32_t *__restrict__ flags,
+                                                  const uint32_t *__restrict__ idx, int S, int G,
+                                                  int64_t *__restrict__ desc) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)S * G || !flags[i]) return;
+    int64_t *d = desc + 4 * (int64_t)idx[i];
+    d[0] = offs1[i];
+    d[2] = i / G;
+    d[3] = i % G;
 }
 
 hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, int64_t n, int64_t target, int64_t *desc,
-                           uint32_t *ndesc, hipStream_t stream) {
-    hipLaunchKernelGGL(k_seg_desc, dim3(1), dim3(DESC_THREADS), 0, stream, offs1, S, G, n, target, desc, ndesc);
+                           uint32_t *flags, uint32_t *idx, uint64_t *status, uint32_t *ticket, uint32_t *err,
+                           uint32_t *npieces, hipStream_t stream) {
+    const int64_t nb = (int64_t)S * G;
+    const unsigned grid = (unsigned)((nb + 255) / 256);
+    (void)n;
+    hipLaunchKernelGGL(k_seg_flags, dim3(grid), dim3(256), 0, stream, offs1, S, G, target, flags);
+    // one "partition" over all blocks: idx = exclusive prefix of the flags, npieces[1] = total
+    hipLaunchKernelGGL(k_scan, dim3((unsigned)scan_tiles(nb)), dim3(SCAN_THREADS), 0, stream, (const uint32_t *)flags,
+                       idx, nb, status, ticket, err, npieces, (int)nb, 1);
+    hipLaunchKernelGGL(k_seg_desc, dim3(grid), dim3(256), 0, stream, offs1, (const uint32_t *)flags,
+                       (const uint32_t *)idx, S, G, desc);
     return hipGetLastError();
 }
 

@@ -89,7 +89,7 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     const size_t status_bytes = ((size_t)(16 + tiles * 8) + 15) & ~(size_t)15;
     const size_t off_bytes = ((size_t)(R + 2) * 4 + 15) & ~(size_t)15;
     const size_t status1_bytes = split ? ((size_t)(16 + tiles1 * 8) + 15) & ~(size_t)15 : 0;
-    const size_t work_bytes = counts_bytes + status_bytes + off_bytes + status1_bytes;
+    const size_t work_bytes = counts_bytes + status_bytes + off_bytes + 2 * status1_bytes;
     SGX_TRY(c.work.ensure(work_bytes));
     uint32_t *counts = (uint32_t *)c.work.p;
     uint32_t *ticket = (uint32_t *)((char *)c.work.p + counts_bytes);
@@ -98,19 +98,24 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     uint32_t *err = part_off_dev + R + 1;
     uint32_t *ticket1 = (uint32_t *)((char *)part_off_dev + off_bytes);
     uint64_t *status1 = (uint64_t *)((char *)ticket1 + 16);
+    uint32_t *ticket2 = (uint32_t *)((char *)ticket1 + status1_bytes);  // the piece numbering's scan
+    uint64_t *status2 = (uint64_t *)((char *)ticket2 + 16);
     c.last_off_dev = part_off_dev;
-    // the split's scratch: [csum u32 x S*G][offs1 u32 x S*G][part_off1 u32 x (S+2) | ndesc]
-    // [desc i64 x 4*S*G], and the level-1 output (n records)
-    uint32_t *csum = nullptr, *offs1 = nullptr, *part_off1 = nullptr, *ndesc = nullptr;
+    // the split's scratch: [csum u32 x S*G][offs1 u32 x S*G][flags u32 x S*G][idx u32 x S*G]
+    // [part_off1 u32 x (S+2) | npieces u32 x 4][desc i64 x 4*S*G], and the level-1 output
+    uint32_t *csum = nullptr, *offs1 = nullptr, *part_off1 = nullptr, *npieces = nullptr, *pflags = nullptr,
+             *pidx = nullptr;
     int64_t *desc = nullptr;
     if (split) {
-        const size_t a = ((size_t)len1 * 4 + 15) & ~(size_t)15, b = ((size_t)(S + 4) * 4 + 15) & ~(size_t)15;
-        SGX_TRY(c.split_work.ensure(2 * a + b + (size_t)len1 * 32));
+        const size_t a = ((size_t)len1 * 4 + 15) & ~(size_t)15, b = ((size_t)(S + 6) * 4 + 15) & ~(size_t)15;
+        SGX_TRY(c.split_work.ensure(4 * a + b + (size_t)len1 * 32));
         csum = (uint32_t *)c.split_work.p;
         offs1 = (uint32_t *)((char *)c.split_work.p + a);
-        part_off1 = (uint32_t *)((char *)c.split_work.p + 2 * a);
-        ndesc = part_off1 + S + 2;
-        desc = (int64_t *)((char *)c.split_work.p + 2 * a + b);
+        pflags = (uint32_t *)((char *)c.split_work.p + 2 * a);
+        pidx = (uint32_t *)((char *)c.split_work.p + 3 * a);
+        part_off1 = (uint32_t *)((char *)c.split_work.p + 4 * a);
+        npieces = part_off1 + S + 2;
+        desc = (int64_t *)((char *)c.split_work.p + 4 * a + b);
         SGX_TRY(c.split_tmp.ensure((size_t)std::max<int64_t>(n, 1) * 16));
     }
     HIP_TRY(hipMemsetAsync(c.work.p, 0, work_bytes, st));
@@ -133,7 +138,7 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
         HIP_TRY(launch_scan(csum, offs1, len1, status1, ticket1, err, part_off1, G, S, st));
         const int64_t pieces = std::max<int64_t>(1, (int64_t)e->num_cus - S);
         const int64_t target = std::max<int64_t>(1, (n + pieces - 1) / pieces);
-        HIP_TRY(launch_seg_desc(offs1, S, G, n, target, desc, ndesc, st));
+        HIP_TRY(launch_seg_desc(offs1, S, G, n, target, desc, pflags, pidx, status2, ticket2, err, npieces, st));
         SGX_TRY(debug_sync(e, st, "split scan / pieces"));
         HIP_TRY(hipEventRecord(c1, st));
         PartParams p1 = spp;
@@ -148,8 +153,8 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
         p2.R = (uint32_t)Q;
         p2.mbits = (uint32_t)geo2.mbits;
         const int grid = (int)(S + (n + target - 1) / target + 1);
-        HIP_TRY(launch_scatter16_seg(c.split_tmp.p, out, n, p2, (const uint32_t *)c.offs.p, G, desc, ndesc, grid, geo2,
-                                     err, st));
+        HIP_TRY(launch_scatter16_seg(c.split_tmp.p, out, n, p2, (const uint32_t *)c.offs.p, G, desc, npieces + 1, grid,
+                                     geo2, err, st));
         SGX_TRY(debug_sync(e, st, "K4 split level 2"));
     } else {
         HIP_TRY(hipEventRecord(c1, st));
