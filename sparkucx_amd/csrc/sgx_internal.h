@@ -107,7 +107,11 @@ hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, int64_t n, int64
                            uint32_t *npieces, hipStream_t stream);
 hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
                                 int G, const int64_t *desc, const uint32_t *ndesc, int grid, const ScatterGeom &geo,
-                                uint32_t *err, hipStream_t stream);
+                                uint32_t *err, hipStream_t stream, const uint32_t *gate = nullptr,
+                                uint32_t gate_want = 0);
+// *gate = 1 when no partition holds more than 1/50 of the records (the split's kernels run),
+// 0 otherwise (the single lane-ordered pass runs): both are launched, gated on the flag.
+hipError_t launch_split_choice(const uint32_t *part_off, int R, uint32_t *gate, hipStream_t stream);
 // The sorted read's last step: `in` is ordered by bucket = (P(key) << kbits) | key window
 // bits [kshift, kshift + kbits) (P the shuffle's hash partitioner when use_p, else 0); every
 // bucket is sorted stably by the full key on chip (16 B: signed Long; 100 B: 10-byte
@@ -117,7 +121,7 @@ hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, cons
                               uint32_t kshift, uint32_t kbits, uint32_t *err, hipStream_t stream);
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes, int64_t chunk,
                           int G, const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
-                          uint32_t *err, hipStream_t stream);
+                          uint32_t *err, hipStream_t stream, const uint32_t *gate = nullptr, uint32_t gate_want = 0);
 // items: [n][3] int64 {src_off, dst_off, bytes}; all offsets/bytes multiples of `align`.
 // LZ4BlockOutputStream framing (sgx_lz4.hip)
 int lz4_lanes_per_workgroup();

@@ -927,7 +927,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_ord(const u32x4 *__
                                                                  u32x4 *__restrict__ out, int64_t n,
                                                                  int64_t chunk, PartParams pp,
                                                                  const uint32_t *__restrict__ offs,
-                                                                 int G, uint32_t *err) {
+                                                                 int G, uint32_t *err,
+                                                                 const uint32_t *__restrict__ gate = nullptr,
+                                                                 uint32_t gate_want = 0) {
+    if (gate && *gate != gate_want) return;  // the other kernel choice of this map runs
     constexpr int T = WAVES * 64;
     constexpr int TILE = WAVES * ITEMS * 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1033,7 +1036,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                                                                 const uint32_t *__restrict__ offs,
                                                                 int G, uint32_t *err,
                                                                 const int64_t *__restrict__ desc = nullptr,
-                                                                const uint32_t *__restrict__ ndesc = nullptr) {
+                                                                const uint32_t *__restrict__ ndesc = nullptr,
+                                                                const uint32_t *__restrict__ gate = nullptr,
+                                                                uint32_t gate_want = 0) {
     constexpr int T = WAVES * 64;
     constexpr int TNEW = T * NI;
     constexpr int STAGE = T * SI;
@@ -1051,6 +1056,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     uint32_t *myrow32 = (uint32_t *)myrow;
     const uint32_t n32 = (uint32_t)n;  // n < 2^32 (sgx_write_map)
 
+    if (gate && *gate != gate_want) return;  // the other kernel choice of this map runs
     int g = blockIdx.x;
     int64_t begin = (int64_t)g * chunk, end = min(n, begin + chunk), obase = 0;
     if constexpr (SEG) {
@@ -1590,9 +1596,29 @@ hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, int64_t n, int64
     return hipGetLastError();
 }
 
+// The split is chosen per map, on the device (no host round trip): *gate = 1 (split) unless one
+// partition holds more than 1/50 of the records -- skewed keys (Zipf: the hottest of 4096
+// reducers holds ~11.5 %) whose hot sub-partition serialises the write-combining ranking
+// atomics -- where the single lane-ordered pass runs instead (measured).
+__global__ __launch_bounds__(256) void k_split_choice(const uint32_t *__restrict__ part_off, int R, uint32_t *gate) {
+    __shared__ uint32_t s_max;
+    if (threadIdx.x == 0) s_max = 0;
+    __syncthreads();
+    uint32_t mx = 0;
+    for (int p = (int)threadIdx.x; p < R; p += 256) mx = max(mx, part_off[p + 1] - part_off[p]);
+    atomicMax(&s_max, mx);
+    __syncthreads();
+    if (threadIdx.x == 0) *gate = (uint64_t)s_max * 50 <= (uint64_t)part_off[R] ? 1u : 0u;
+}
+
+hipError_t launch_split_choice(const uint32_t *part_off, int R, uint32_t *gate, hipStream_t stream) {
+    hipLaunchKernelGGL(k_split_choice, dim3(1), dim3(256), 0, stream, part_off, R, gate);
+    return hipGetLastError();
+}
+
 hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
                                 int G, const int64_t *desc, const uint32_t *ndesc, int grid, const ScatterGeom &geo,
-                                uint32_t *err, hipStream_t stream) {
+                                uint32_t *err, hipStream_t stream, const uint32_t *gate, uint32_t gate_want) {
     if (geo.waves != WC_GEOM_BASE + 8 || geo.mbits != 16 || (pp.R & (pp.R - 1)) != 0) return hipErrorInvalidValue;
 #define SGX_WCS(NI)                                                                                          \
     do {                                                                                                     \
@@ -1600,7 +1626,7 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes);           \
         hipLaunchKernelGGL((k_scatter16_wc<KIND_HASH_POW2, 8, NI, 16, true>), dim3(grid), dim3(512),         \
                            geo.lds_bytes, stream, (const u32x4 *)in, (u32x4 *)out, n, (int64_t)0, pp, offs, G, \
-                           err, desc, ndesc);                                                                \
+                           err, desc, ndesc, gate, gate_want);                                               \
     } while (0)
     if (geo.items == 12) SGX_WCS(12);
     else if (geo.items == 8) SGX_WCS(8);
@@ -1794,7 +1820,7 @@ hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, cons
 
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t chunk, int G,
                           const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
-                          uint32_t *err, hipStream_t stream) {
+                          uint32_t *err, hipStream_t stream, const uint32_t *gate, uint32_t gate_want) {
     const bool pow2 = (pp.R & (pp.R - 1)) == 0;
     if (rb == 16 && geo.waves >= WC_GEOM_BASE) {
         if ((pp.kind != SGX_PART_HASH && pp.kind != KIND_DIGIT && pp.kind != KIND_HASH_BITS &&
@@ -1806,7 +1832,8 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, 8, NI, 16>,                   \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
         hipLaunchKernelGGL((k_scatter16_wc<K, 8, NI, 16>), dim3(G), dim3(512), geo.lds_bytes,     \
-                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err); \
+                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err,   \
+                           nullptr, nullptr, gate, gate_want);                                   \
     } while (0)
         if (pp.kind == KIND_DIGIT) {
             if (geo.items != 12 || pp.R != DIGIT_R) return hipErrorInvalidValue;
@@ -1838,7 +1865,8 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         (void)hipFuncSetAttribute((const void *)k_scatter16_ord<K, WV, I, P>,                   \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
         hipLaunchKernelGGL((k_scatter16_ord<K, WV, I, P>), dim3(G), dim3(WV * 64), geo.lds_bytes, \
-                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err); \
+                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err,  \
+                           gate, gate_want);                                                     \
     } while (0)
 #define SGX_ORD_K(K)                                                      \
     do {                                                                  \

@@ -62,11 +62,13 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
                        !(e->flags & (SGX_FLAG_NO_WRITE_COMBINING | SGX_FLAG_NO_SPLIT_SCATTER));
     constexpr int32_t Q = 64;
     const int32_t S = split ? R / Q : 0;
-    ScatterGeom geo1{}, geo2{};
+    ScatterGeom geo1{}, geo2{}, geo_ord{};
     if (split) {
         geo1 = scatter_geom16_wc((uint32_t)S);
         geo2 = scatter_geom16_wc((uint32_t)Q);
-        if (geo1.items == 0 || geo2.items == 0) return fail_msg(SGX_ERR_UNSUPPORTED, "split scatter geometry for R=%d", R);
+        geo_ord = scatter_geom16_ord((uint32_t)R, 0, 0);
+        if (geo1.items == 0 || geo2.items == 0 || geo_ord.items == 0)
+            return fail_msg(SGX_ERR_UNSUPPORTED, "split scatter geometry for R=%d", R);
         geo = geo1;
     }
     if (geo.items == 0)
@@ -133,6 +135,10 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     PartParams lpp = spp;
     lpp.mbits = (uint32_t)geo.mbits;
     if (split && n > 0) {
+        // per map, on the device: the split (gate 1) unless one partition holds > 1/50 of the
+        // records, where the single lane-ordered pass (gate 0) is faster
+        uint32_t *gate = npieces + 2;
+        HIP_TRY(launch_split_choice(part_off_dev, R, gate, st));
         // level-1 cursors: a scan of the per-chunk super counts; level-2 pieces from them
         HIP_TRY(launch_super_counts(counts, csum, S, Q, G, st));
         HIP_TRY(launch_scan(csum, offs1, len1, status1, ticket1, err, part_off1, G, S, st));
@@ -146,7 +152,7 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
         p1.R = (uint32_t)S;
         p1.dshift = 6;  // log2(Q)
         p1.mbits = (uint32_t)geo1.mbits;
-        HIP_TRY(launch_scatter(in, c.split_tmp.p, n, rb, chunk, G, p1, offs1, geo1, err, st));
+        HIP_TRY(launch_scatter(in, c.split_tmp.p, n, rb, chunk, G, p1, offs1, geo1, err, st, gate, 1u));
         SGX_TRY(debug_sync(e, st, "K4 split level 1"));
         PartParams p2 = spp;
         p2.kind = KIND_HASH_POW2;
@@ -154,8 +160,12 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
         p2.mbits = (uint32_t)geo2.mbits;
         const int grid = (int)(S + (n + target - 1) / target + 1);
         HIP_TRY(launch_scatter16_seg(c.split_tmp.p, out, n, p2, (const uint32_t *)c.offs.p, G, desc, npieces + 1, grid,
-                                     geo2, err, st));
+                                     geo2, err, st, gate, 1u));
         SGX_TRY(debug_sync(e, st, "K4 split level 2"));
+        PartParams po = spp;
+        po.mbits = (uint32_t)geo_ord.mbits;
+        HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, po, (const uint32_t *)c.offs.p, geo_ord, err, st, gate, 0u));
+        SGX_TRY(debug_sync(e, st, "K4 single pass (skewed map)"));
     } else {
         HIP_TRY(hipEventRecord(c1, st));
         if (n > 0) HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, lpp, (const uint32_t *)c.offs.p, geo, err, st));
