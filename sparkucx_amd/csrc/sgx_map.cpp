@@ -57,17 +57,19 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     // R > 1024 (power of two, hash, 16 B): the two-level split -- two write-combining passes
     // (S = R / 64 super-partitions, then Q = 64 inside each) instead of one pass whose runs
     // leave L2 as partial lines (sgx_kernels.hip, "Two-level split scatter")
+    // (skewed maps take the single lane-ordered pass instead, chosen on the device: so the
+    // split needs that kernel's geometry too -- R <= 4096)
+    const ScatterGeom geo_ord = rb == 16 ? scatter_geom16_ord((uint32_t)R, 0, 0) : ScatterGeom{0, 0, 0, 0, 0};
     const bool split = rb == 16 && kind == SGX_PART_HASH && R > 1024 && (R & (R - 1)) == 0 && R <= 65536 &&
-                       e->rank_mode == SGX_RANK_ORDERED && e->sc_waves == 0 && e->sc_items == 0 &&
-                       !(e->flags & (SGX_FLAG_NO_WRITE_COMBINING | SGX_FLAG_NO_SPLIT_SCATTER));
+                       geo_ord.items > 0 && e->rank_mode == SGX_RANK_ORDERED && e->sc_waves == 0 &&
+                       e->sc_items == 0 && !(e->flags & (SGX_FLAG_NO_WRITE_COMBINING | SGX_FLAG_NO_SPLIT_SCATTER));
     constexpr int32_t Q = 64;
     const int32_t S = split ? R / Q : 0;
-    ScatterGeom geo1{}, geo2{}, geo_ord{};
+    ScatterGeom geo1{}, geo2{};
     if (split) {
         geo1 = scatter_geom16_wc((uint32_t)S);
         geo2 = scatter_geom16_wc((uint32_t)Q);
-        geo_ord = scatter_geom16_ord((uint32_t)R, 0, 0);
-        if (geo1.items == 0 || geo2.items == 0 || geo_ord.items == 0)
+        if (geo1.items == 0 || geo2.items == 0)
             return fail_msg(SGX_ERR_UNSUPPORTED, "split scatter geometry for R=%d", R);
         geo = geo1;
     }
