@@ -1646,32 +1646,20 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
 // through the inverse permutation, coalesced.  One read + one write of every record instead
 // of the 7-9 LSD digit passes that remain below the window.
 // ------------------------------------------------------------------------------------
-constexpr int BS_THREADS = 256;
+constexpr int BS_THREADS = 512;
 
+// the order key of a staged record: 16 B -> the signed Long sign-flipped (hi), lo = 0;
+// 100 B -> the first 8 key bytes big-endian (hi) and the last 2 (lo)
 template <int RB>
-struct BucketKey;
-template <>
-struct BucketKey<16> {  // signed Long key, compared as sign-flipped unsigned
-    uint64_t k;
-    __device__ static BucketKey at(const uint32_t *r) {
-        return BucketKey{(((uint64_t)r[1] << 32) | r[0]) ^ 0x8000000000000000ull};
+__device__ __forceinline__ void bucket_key(const uint32_t *r, uint64_t &hi, uint32_t &lo) {
+    if constexpr (RB == 16) {
+        hi = (((uint64_t)r[1] << 32) | r[0]) ^ 0x8000000000000000ull;
+        lo = 0;
+    } else {
+        hi = ((uint64_t)__builtin_bswap32(r[0]) << 32) | __builtin_bswap32(r[1]);
+        lo = __builtin_bswap32(r[2]) >> 16;
     }
-    __device__ bool lt(const BucketKey &o) const { return k < o.k; }
-    __device__ bool eq(const BucketKey &o) const { return k == o.k; }
-    __device__ uint64_t window() const { return k; }
-};
-template <>
-struct BucketKey<100> {  // 10-byte unsigned big-endian key
-    uint64_t hi;
-    uint32_t lo;
-    __device__ static BucketKey at(const uint32_t *r) {
-        return BucketKey{((uint64_t)__builtin_bswap32(r[0]) << 32) | __builtin_bswap32(r[1]),
-                         __builtin_bswap32(r[2]) >> 16};
-    }
-    __device__ bool lt(const BucketKey &o) const { return hi < o.hi || (hi == o.hi && lo < o.lo); }
-    __device__ bool eq(const BucketKey &o) const { return hi == o.hi && lo == o.lo; }
-    __device__ uint64_t window() const { return hi; }
-};
+}
 
 template <int RB, int TILE, int HALO>
 __global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
@@ -1679,12 +1667,15 @@ __global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__re
                                                             uint32_t kbits, uint32_t *err) {
     constexpr int DW = RB / 4;
     constexpr int CAP = TILE + HALO + 1;
+    constexpr bool LO = RB != 16;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    uint32_t *rec = (uint32_t *)smem;                      // CAP records
-    uint16_t *bs = (uint16_t *)(rec + (size_t)CAP * DW);   // bucket start of each local position
-    uint16_t *be = bs + CAP;                               // bucket end
-    uint16_t *inv = be + CAP;                              // output slot -> local position
-    uint8_t *flag = (uint8_t *)(inv + CAP);                // a bucket starts here
+    uint32_t *rec = (uint32_t *)smem;                             // CAP records
+    uint64_t *khi = (uint64_t *)(rec + (size_t)CAP * DW);         // order keys (8-aligned: CAP*DW*4 % 8 == 0 below)
+    uint32_t *klo = (uint32_t *)(khi + CAP);                      // 100 B: the key's last 2 bytes
+    uint16_t *bs = (uint16_t *)(klo + (LO ? CAP : 0));            // bucket start of each local position
+    uint16_t *be = bs + CAP;                                      // bucket end
+    uint16_t *inv = be + CAP;                                     // output slot -> local position
+    uint8_t *flag = (uint8_t *)(inv + CAP);                       // a bucket starts here
     __shared__ uint32_t s_a, s_b, s_scr[BS_THREADS / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t t0 = (int64_t)blockIdx.x * TILE;
@@ -1693,20 +1684,27 @@ __global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__re
     const int64_t L0 = t0 > 0 ? t0 - 1 : 0, L1 = min(n, t1 + HALO);
     const int m = (int)(L1 - L0);
     const uint64_t wmask = kbits >= 64 ? ~0ull : ((1ull << kbits) - 1ull);
-    auto comp = [&](int j) -> uint64_t {
-        const uint32_t *r = rec + (size_t)j * DW;
-        const uint64_t bits = (BucketKey<RB>::at(r).window() >> kshift) & wmask;
-        const uint64_t p = use_p ? (uint64_t)hash_pid(r[0], r[1], pp) : 0ull;
-        return (p << kbits) | bits;
-    };
     for (int u = (int)tid; u < m * DW; u += BS_THREADS) rec[u] = in[L0 * DW + u];
     if (tid == 0) {
         s_a = 0xFFFFFFFFu;
         s_b = 0xFFFFFFFFu;
     }
     __syncthreads();
-    // boundary flags; the first nominal boundary (a) and the first boundary at or past t1 (b)
+    auto comp = [&](int j) -> uint64_t {
+        const uint32_t *r = rec + (size_t)j * DW;
+        uint64_t hi;
+        uint32_t lo;
+        bucket_key<RB>(r, hi, lo);
+        const uint64_t p = use_p ? (uint64_t)hash_pid(r[0], r[1], pp) : 0ull;
+        return (p << kbits) | ((hi >> kshift) & wmask);
+    };
+    // order keys, boundary flags; the first nominal boundary (a), the first one at or past t1 (b)
     for (int j = (int)tid; j < m; j += BS_THREADS) {
+        uint64_t hi;
+        uint32_t lo;
+        bucket_key<RB>(rec + (size_t)j * DW, hi, lo);
+        khi[j] = hi;
+        if constexpr (LO) klo[j] = lo;
         const int64_t pos = L0 + j;
         const bool f = pos == 0 || (j > 0 && comp(j) != comp(j - 1));
         flag[j] = f ? 1 : 0;
@@ -1732,7 +1730,6 @@ __global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__re
     {
         int run = -1;
         for (int j = j0; j < j1; ++j) if (flag[j]) run = j;
-        // exclusive prefix max over threads (run of the previous threads)
         int x = run;
 #pragma unroll
         for (int d = 1; d < 64; d <<= 1) {
@@ -1770,43 +1767,68 @@ __global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__re
         }
     }
     __syncthreads();
-    // stable rank inside the bucket: keys below, plus equal keys at earlier positions
+    // stable rank inside the bucket: keys below, plus equal keys at earlier positions.  Keys
+    // come from the compact key array four at a time (independent LDS loads, one wait).
     for (int j = (int)a + (int)tid; j < (int)b; j += BS_THREADS) {
         const int s0 = bs[j], e0 = be[j];
-        const BucketKey<RB> kj = BucketKey<RB>::at(rec + (size_t)j * DW);
-        int rank = 0;
-        for (int i = s0; i < e0; ++i) {
-            const BucketKey<RB> ki = BucketKey<RB>::at(rec + (size_t)i * DW);
-            rank += (ki.lt(kj) || (i < j && ki.eq(kj))) ? 1 : 0;
+        const uint64_t kh = khi[j];
+        const uint32_t kl = LO ? klo[j] : 0u;
+        int rank = 0, i = s0;
+        for (; i + 4 <= e0; i += 4) {
+            uint64_t h[4];
+            uint32_t l[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                h[q] = khi[i + q];
+                l[q] = LO ? klo[i + q] : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const bool lt = LO ? (h[q] < kh || (h[q] == kh && l[q] < kl)) : h[q] < kh;
+                const bool eq = LO ? (h[q] == kh && l[q] == kl) : h[q] == kh;
+                rank += (lt || (i + q < j && eq)) ? 1 : 0;
+            }
+        }
+        for (; i < e0; ++i) {
+            const uint64_t h = khi[i];
+            const uint32_t l = LO ? klo[i] : 0u;
+            const bool lt = LO ? (h < kh || (h == kh && l < kl)) : h < kh;
+            const bool eq = LO ? (h == kh && l == kl) : h == kh;
+            rank += (lt || (i < j && eq)) ? 1 : 0;
         }
         inv[s0 + rank] = (uint16_t)j;
     }
     __syncthreads();
     // the bucket region, coalesced: output position L0 + p takes local record inv[p]
-    for (int u = (int)tid; u < len * DW; u += BS_THREADS) {
-        const int p = (int)a + u / DW, q = u % DW;
-        out[(L0 + p) * DW + q] = rec[(size_t)inv[p] * DW + q];
+    if constexpr (RB == 16) {
+        for (int p = (int)a + (int)tid; p < (int)b; p += BS_THREADS)
+            ((u32x4 *)out)[L0 + p] = ((const u32x4 *)rec)[inv[p]];
+    } else {
+        for (int u = (int)tid; u < len * DW; u += BS_THREADS) {
+            const int p = (int)a + u / DW, q = u % DW;
+            out[(L0 + p) * DW + q] = rec[(size_t)inv[p] * DW + q];
+        }
     }
 }
 
 template <int RB, int TILE, int HALO>
 static size_t bucket_sort_lds() {
     constexpr int CAP = TILE + HALO + 1;
-    return (size_t)CAP * RB + (size_t)CAP * 6 + (size_t)CAP + 16;
+    return (size_t)CAP * RB + (size_t)CAP * 8 + (RB != 16 ? (size_t)CAP * 4 : 0) + (size_t)CAP * 6 + (size_t)CAP + 16;
 }
 
 hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, const PartParams &pp, int use_p,
                               uint32_t kshift, uint32_t kbits, uint32_t *err, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     if (rb == 16) {
-        constexpr int T = 2048, H = 512;
+        constexpr int T = 2048, H = 511;  // CAP = 2560: the key array stays 8-byte aligned
         const size_t lds = bucket_sort_lds<16, T, H>();
         (void)hipFuncSetAttribute((const void *)k_bucket_sort<16, T, H>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
         hipLaunchKernelGGL((k_bucket_sort<16, T, H>), dim3((unsigned)((n + T - 1) / T)), dim3(BS_THREADS), lds, stream,
                            (const uint32_t *)in, (uint32_t *)out, n, pp, use_p, kshift, kbits, err);
     } else if (rb == 100) {
-        constexpr int T = 384, H = 256;
+        constexpr int T = 384, H = 253;  // CAP = 638 (even: 100 B records keep the key array 8-aligned)
         const size_t lds = bucket_sort_lds<100, T, H>();
         (void)hipFuncSetAttribute((const void *)k_bucket_sort<100, T, H>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
