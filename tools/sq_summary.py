@@ -12,7 +12,7 @@ vals = defaultdict(lambda: defaultdict(list))
 for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv"), recursive=True)):
     with open(f) as fh:
         for r in csv.DictReader(fh):
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            k = r["Kernel_Name"].replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "")
             vals[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in vals.items():
     if len(sys.argv) > 2 and sys.argv[2] not in k:
