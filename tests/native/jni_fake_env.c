@@ -113,6 +113,8 @@ jbyteArray Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_bootstrapJoin(JNIEnv 
                                                                         jintArray);
 void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_bootstrapServe(JNIEnv *, jclass, jint, jint, jbyteArray, jint);
 void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchange(JNIEnv *, jclass, jlong, jint);
+void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchangeMaps(JNIEnv *, jclass, jlong, jint, jlongArray);
+jintArray Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_shuffleReducers(JNIEnv *, jclass, jlong, jint);
 
 static obj *jstr(const char *s) {
     obj *o = (obj *)calloc(1, sizeof(obj));
@@ -161,6 +163,22 @@ int fake_fetch_mismatched(int64_t engine) {
 
 int fake_exchange(int64_t engine) {
     Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchange(&g_env, NULL, engine, 1);
+    return 0;
+}
+
+/* exchangeMaps with n map ids 0..n-1 (an empty array included) */
+int fake_exchange_maps(int64_t engine, int n) {
+    obj *m = new_obj(K_LONGS, n, 8);
+    for (int i = 0; i < n; ++i) ((int64_t *)m->data)[i] = i;
+    Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchangeMaps(&g_env, NULL, engine, 1, m);
+    return 0;
+}
+
+/* shuffleReducers: 0 and r0, r1 in out2, or -1 for Java null (an exception is pending) */
+int fake_shuffle_reducers(int64_t engine, int32_t *out2) {
+    obj *r = (obj *)Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_shuffleReducers(&g_env, NULL, engine, 1);
+    if (!r) return -1;
+    memcpy(out2, r->data, 8);
     return 0;
 }
 

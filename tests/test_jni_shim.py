@@ -34,6 +34,8 @@ def shim(sgx_lib, tmp_path_factory):
     L.fake_write_map.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
     L.fake_fetch_mismatched.argtypes = [ctypes.c_int64]
     L.fake_exchange.argtypes = [ctypes.c_int64]
+    L.fake_exchange_maps.argtypes = [ctypes.c_int64, ctypes.c_int]
+    L.fake_shuffle_reducers.argtypes = [ctypes.c_int64, ctypes.c_void_p]
     L.fake_bootstrap_join.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                       ctypes.c_void_p]
     L.fake_bootstrap_serve.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
@@ -79,6 +81,15 @@ def test_argument_errors_become_illegal_argument(shim):
     assert exc(shim)[0] == "java/lang/IllegalArgumentException"
     shim.fake_clear()
     shim.fake_exchange(0)
+    assert exc(shim)[0] == "java/lang/IllegalArgumentException"
+    # the per-shuffle exchange's natives (GpuExchangeCoordinator, GpuShuffleReader)
+    for n in (0, 3):
+        shim.fake_clear()
+        shim.fake_exchange_maps(0, n)
+        assert exc(shim)[0] == "java/lang/IllegalArgumentException", n
+    shim.fake_clear()
+    r = np.zeros(2, np.int32)
+    assert shim.fake_shuffle_reducers(0, r.ctypes.data) == -1
     assert exc(shim)[0] == "java/lang/IllegalArgumentException"
 
 
