@@ -70,8 +70,10 @@ enum sgx_flags {
                                          frame (default: only from 32768 frames up)           */
     SGX_FLAG_NO_SPLIT_SCATTER = 32,   /* hash K4 with R > 1024: one lane-ordered pass instead
                                          of the two-level write-combining split               */
-    SGX_FLAG_NO_BUCKET_SORT = 64      /* sorted reads / map-side combine: LSD digit passes only
+    SGX_FLAG_NO_BUCKET_SORT = 64,     /* sorted reads / map-side combine: LSD digit passes only
                                          (no key-window buckets sorted on chip)               */
+    SGX_FLAG_ASSUME_LDS_DISORDER = 128 /* testing: act as if the engine-start LDS ordering
+                                          check had failed (see sgx_lds_order_ok)             */
 };
 
 typedef struct sgx_config {
@@ -96,6 +98,13 @@ void sgx_destroy(sgx_engine *e);
 int sgx_release_thread(sgx_engine *e);
 const char *sgx_last_error(void);
 int32_t sgx_abi_version(void);
+/* Result of the engine-start device check (sgx_create runs it once, ~1 ms): 1 if same-address
+ * LDS atomics issued back to back by one wave returned their old values in issue order, then
+ * lane order, on this device -- the property the default ranking (SGX_RANK_ORDERED) and the
+ * reduce side's sort passes rest on.  0 if it did not (or SGX_FLAG_ASSUME_LDS_DISORDER): the
+ * engine then ranks every scatter by ballot peer matching (SGX_RANK_MATCH, the per-lane
+ * kernels for sort passes and 100 B records) -- slower, same bytes.  -1 for a NULL engine. */
+int32_t sgx_lds_order_ok(const sgx_engine *e);
 
 /* ---- registerShuffle: SortShuffleManager.registerShuffle inherited at
  *      shuffle/ucx/CommonUcxShuffleManager.scala:25; the partitioner of the dependency.

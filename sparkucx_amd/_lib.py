@@ -30,6 +30,7 @@ FLAG_NO_WRITE_COMBINING, FLAG_NO_WIDE_STAGED, FLAG_SORT_ALL_DIGITS, FLAG_DEBUG_S
 FLAG_LZ4_LANE_DECODE = 16
 FLAG_NO_SPLIT_SCATTER = 32
 FLAG_NO_BUCKET_SORT = 64
+FLAG_ASSUME_LDS_DISORDER = 128
 PLACE_EVEN, PLACE_BYTES = 0, 1
 ABI_VERSION = 5
 
@@ -102,6 +103,7 @@ SIGNATURES = {
     "sgx_pool_stats": (ctypes.c_int, [_vp, _P64, _P64]),
     "sgx_last_error": (_cp, []),
     "sgx_abi_version": (_i32, []),
+    "sgx_lds_order_ok": (_i32, [_vp]),
     "sgx_register_shuffle": (ctypes.c_int, [_vp, _i32, _i32, _i32, _vp, _i64, _i32, _i32]),
     "sgx_unregister_shuffle": (ctypes.c_int, [_vp, _i32]),
     "sgx_set_serializer": (ctypes.c_int, [_vp, _i32, _i32]),

@@ -136,6 +136,23 @@ PartParams sgx::make_part_params(const Shuffle &s) {
 // ------------------------------------------------------------------------------------
 // lifetime
 // ------------------------------------------------------------------------------------
+// The default ranking's premise, checked on the device the engine runs on:
+// on a violation every scatter is ranked by ballot peer matching instead (same bytes, slower).
+static int check_lds_order(sgx_engine *e) {
+    uint32_t *bad = nullptr;
+    HIP_TRY(hipMalloc((void **)&bad, 4));
+    uint32_t h = 0;
+    hipError_t r = hipMemsetAsync(bad, 0, 4, e->s_comm);
+    if (r == hipSuccess) r = launch_lds_order_probe(bad, e->s_comm);
+    if (r == hipSuccess) r = hipMemcpyAsync(&h, bad, 4, hipMemcpyDeviceToHost, e->s_comm);
+    if (r == hipSuccess) r = hipStreamSynchronize(e->s_comm);
+    (void)hipFree(bad);
+    HIP_TRY(r);
+    e->lds_order_ok = h == 0 && !(e->flags & SGX_FLAG_ASSUME_LDS_DISORDER);
+    if (!e->lds_order_ok) e->rank_mode = SGX_RANK_MATCH;
+    return SGX_OK;
+}
+
 extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     if (!out) return fail_msg(SGX_ERR_INVALID, "sgx_create: out is NULL");
     *out = nullptr;
@@ -145,7 +162,7 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     if (dev < 0 || dev >= ndev) return fail_msg(SGX_ERR_INVALID, "sgx_create: device %d of %d", dev, ndev);
     if (cfg && (cfg->hist_mode < SGX_HIST_ATOMIC || cfg->hist_mode > SGX_HIST_BALLOT ||
                 cfg->rank_mode < SGX_RANK_ORDERED || cfg->rank_mode > SGX_RANK_MATCH || cfg->flags < 0 ||
-                cfg->flags > 127 || cfg->comm_timeout_ms < 0 || cfg->num_chunks < 0))
+                cfg->flags > 255 || cfg->comm_timeout_ms < 0 || cfg->num_chunks < 0))
         return fail_msg(SGX_ERR_INVALID, "sgx_create: bad configuration");
     HIP_TRY(hipSetDevice(dev));
     hipDeviceProp_t prop;
@@ -164,9 +181,12 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
         if (cfg->comm_timeout_ms > 0) e->comm_timeout_ms = cfg->comm_timeout_ms;
     }
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
+    SGX_TRY(check_lds_order(e.get()));
     *out = e.release();
     return SGX_OK;
 }
+
+extern "C" int32_t sgx_lds_order_ok(const sgx_engine *e) { return e ? (e->lds_order_ok ? 1 : 0) : -1; }
 
 extern "C" void sgx_destroy(sgx_engine *e) {
     if (!e) return;

@@ -288,6 +288,7 @@ struct sgx_engine {
     int hist_mode = 0;               // sgx_config.hist_mode
     int rank_mode = 0;               // sgx_config.rank_mode
     int flags = 0;                   // sgx_config.flags
+    bool lds_order_ok = true;        // engine-start check (sgx_create; sgx_lds_order_ok)
     int64_t comm_timeout_ms = 300000;
 
     std::mutex reg_mu;

@@ -119,6 +119,9 @@ hipError_t launch_split_choice(const uint32_t *part_off, int R, uint32_t *gate, 
 // and leaves `out` incomplete (the caller falls back to the LSD digit passes).
 hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, const PartParams &pp, int use_p,
                               uint32_t kshift, uint32_t kbits, uint32_t *err, hipStream_t stream);
+// Engine-start self-check of the lane-ordered LDS atomics the ordered ranking relies on:
+// *bad |= 1 on any violation (sgx_create).
+hipError_t launch_lds_order_probe(uint32_t *bad, hipStream_t stream);
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes, int64_t chunk,
                           int G, const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
                           uint32_t *err, hipStream_t stream, const uint32_t *gate = nullptr, uint32_t gate_want = 0);

@@ -1840,6 +1840,61 @@ hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, cons
     return hipGetLastError();
 }
 
+// ------------------------------------------------------------------------------------
+// Engine-start self-check of the ordering the lane-ordered ranking rests on (K4's
+// k_scatter16_wc / _ord / _wide2 and the reduce side's digit and key-window passes): NI
+// same-address LDS atomics issued back to back by one wave return their old values in
+// (issue order, then lane order).  Probed once per engine with the ranking's exact
+// instruction pattern (packed u16 counters, relaxed workgroup-scope fetch-add, one wait):
+// every (item k, lane l) must receive exactly the number of earlier (k' < k, or k' == k and
+// l' < l) increments of its counter.  A violation sets *bad.
+// ------------------------------------------------------------------------------------
+constexpr int PROBE_NI = 8, PROBE_ROUNDS = 96;
+__global__ __launch_bounds__(512) void k_lds_order_probe(uint32_t *bad) {
+    __shared__ uint32_t rows[8][64];  // per wave: 128 packed u16 counters
+    const uint32_t w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    uint32_t viol = 0;
+    for (int r = 0; r < PROBE_ROUNDS; ++r) {
+        rows[w][lane] = 0u;  // each wave zeroes its own row (a wave's LDS ops run in order)
+        const int K = 1 + (int)((blockIdx.x * 7u + (uint32_t)r * 13u + w) % 48u);  // 1..48 counters
+        uint32_t p[PROBE_NI], old[PROBE_NI];
+#pragma unroll
+        for (int k = 0; k < PROBE_NI; ++k) {
+            uint32_t h = (blockIdx.x * 2654435761u) ^ ((uint32_t)r * 40503u) ^ (w * 97u + (uint32_t)k * 1031u) ^
+                         (lane * 0x9E3779B9u);
+            h ^= h >> 15;
+            h *= 0x2C1B3C6Du;
+            h ^= h >> 12;
+            p[k] = h % (uint32_t)K;
+        }
+#pragma unroll
+        for (int k = 0; k < PROBE_NI; ++k)
+            old[k] = __hip_atomic_fetch_add(&rows[w][p[k] >> 1], 1u << ((p[k] & 1u) << 4), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+        for (int k = 0; k < PROBE_NI; ++k) {
+            const uint32_t got = (old[k] >> ((p[k] & 1u) << 4)) & 0xFFFFu;
+            uint32_t want = 0;
+            for (int k2 = 0; k2 <= k; ++k2) {
+                // lanes whose item k2 hit the same counter as my item k
+                uint64_t same = 0;
+                for (uint32_t v = 0; v < (uint32_t)K; ++v) {
+                    const uint64_t m = __ballot(p[k2] == v);
+                    if (v == p[k]) same = m;
+                }
+                want += (uint32_t)__popcll(k2 < k ? same : (same & ((1ull << lane) - 1ull)));
+            }
+            viol |= got != want ? 1u : 0u;
+        }
+    }
+    if (viol) atomicOr(bad, 1u);
+}
+
+hipError_t launch_lds_order_probe(uint32_t *bad, hipStream_t stream) {
+    hipLaunchKernelGGL(k_lds_order_probe, dim3(512), dim3(512), 0, stream, bad);
+    return hipGetLastError();
+}
+
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t chunk, int G,
                           const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
                           uint32_t *err, hipStream_t stream, const uint32_t *gate, uint32_t gate_want) {
@@ -1908,7 +1963,9 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
 #undef SGX_ORD
         return hipGetLastError();
     }
-    if (rb == 16) {
+    // (16 B digit / key-window passes reach the per-lane kernel below only when the engine-start
+    // LDS ordering check failed)
+    if (rb == 16 && pp.kind != KIND_DIGIT && pp.kind != KIND_KEY_BITS) {
         if (geo.items == 0) return hipErrorInvalidValue;
         const uint4 *i4 = (const uint4 *)in;
         uint4 *o4 = (uint4 *)out;
@@ -1940,7 +1997,8 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         switch (pp.kind) {
         case SGX_PART_HASH: SGX_SC16_K(SGX_PART_HASH); break;
         case SGX_PART_RANGE_I64: SGX_SC16_K(SGX_PART_RANGE_I64); break;
-        default: SGX_SC16_K(SGX_PART_RANGE_BYTES10); break;
+        case SGX_PART_RANGE_BYTES10: SGX_SC16_K(SGX_PART_RANGE_BYTES10); break;
+        default: return hipErrorInvalidValue;
         }
 #undef SGX_SC16_K
 #undef SGX_SC16
@@ -1960,7 +2018,8 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         case KIND_DIGIT: SGX_W2(KIND_DIGIT); break;
         case KIND_KEY_BITS: SGX_W2(KIND_KEY_BITS); break;
         case SGX_PART_RANGE_I64: SGX_W2(SGX_PART_RANGE_I64); break;
-        default: SGX_W2(SGX_PART_RANGE_BYTES10); break;
+        case SGX_PART_RANGE_BYTES10: SGX_W2(SGX_PART_RANGE_BYTES10); break;
+        default: return hipErrorInvalidValue;
         }
 #undef SGX_W2
     } else {
@@ -1976,8 +2035,11 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
     } while (0)
         switch (pp.kind) {
         case SGX_PART_HASH: SGX_SCW(SGX_PART_HASH); break;
+        case KIND_DIGIT: SGX_SCW(KIND_DIGIT); break;        // lds_order_ok == false
+        case KIND_KEY_BITS: SGX_SCW(KIND_KEY_BITS); break;  // lds_order_ok == false
         case SGX_PART_RANGE_I64: SGX_SCW(SGX_PART_RANGE_I64); break;
-        default: SGX_SCW(SGX_PART_RANGE_BYTES10); break;
+        case SGX_PART_RANGE_BYTES10: SGX_SCW(SGX_PART_RANGE_BYTES10); break;
+        default: return hipErrorInvalidValue;
         }
 #undef SGX_SCW
     }

@@ -43,13 +43,16 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
             if (w.items) geo = w;
         }
     }
-    if (rb != 16 && !(e->flags & SGX_FLAG_NO_WIDE_STAGED) && ((uintptr_t)in & 15) == 0) {
+    if (rb != 16 && !(e->flags & SGX_FLAG_NO_WIDE_STAGED) && e->lds_order_ok && ((uintptr_t)in & 15) == 0) {
         const ScatterGeom w2 = scatter_geom_wide2((uint32_t)R, rb, kind, spp.nb);
         if (w2.items) geo = w2;
     }
     // the reduce side's digit / key-window passes run on the write-combining / wide-record
-    // kernels only
-    if (kind == KIND_DIGIT || kind == KIND_KEY_BITS) {
+    // kernels, or on the per-lane ballot-matched kernel when the engine-start check of the
+    // lane-ordered ranking failed (sgx_create)
+    if ((kind == KIND_DIGIT || kind == KIND_KEY_BITS) && !e->lds_order_ok) {
+        geo = scatter_geom_wide((uint32_t)R, rb);
+    } else if (kind == KIND_DIGIT || kind == KIND_KEY_BITS) {
         if (rb == 16) geo = scatter_geom16_wc((uint32_t)R);
         if (geo.waves < WC_GEOM_BASE && geo.waves != WIDE2_GEOM_TAG)
             return fail_msg(SGX_ERR_UNSUPPORTED, "digit pass on %d B records at this alignment", rb);

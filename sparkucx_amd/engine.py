@@ -93,6 +93,12 @@ class ShuffleEngine:
         self.device = device
         self._host_comm = None
 
+    @property
+    def lds_order_ok(self) -> bool:
+        """sgx_lds_order_ok: the engine-start check of the lane-ordered LDS atomics the default
+        ranking rests on passed on this device (False: every scatter is ballot-ranked)."""
+        return lib().sgx_lds_order_ok(self.handle) == 1
+
     def close(self):
         if self.handle:
             lib().sgx_destroy(self.handle)

@@ -148,12 +148,13 @@ def test_every_staged_geometry(sgx_lib, oracle_lib, waves, items, R, rank):
 
 
 @pytest.mark.parametrize("cfg", [dict(hist_mode=1), dict(rank_mode=1), dict(flags=1), dict(hist_mode=1, flags=1),
-                                 dict(flags=32)])
+                                 dict(flags=32), dict(flags=128)])
 def test_kernel_choices_are_byte_identical(sgx_lib, oracle_lib, cfg):
     """sgx_config's kernel choices -- the ballot/popcount wave-aggregated histogram
     (SGX_HIST_BALLOT), ballot-matched K4 ranking (SGX_RANK_MATCH), K4 without write-combining
     (SGX_FLAG_NO_WRITE_COMBINING), one lane-ordered pass instead of the two-level split at
-    R > 1024 (SGX_FLAG_NO_SPLIT_SCATTER) -- change speed, never bytes."""
+    R > 1024 (SGX_FLAG_NO_SPLIT_SCATTER), the fallback taken when the engine-start LDS ordering
+    check fails (SGX_FLAG_ASSUME_LDS_DISORDER) -- change speed, never bytes."""
     recs = oracle_lib.gen_uniform16(3 * 8192 * 5 + 1234, 99)
     with sgx_lib.ShuffleEngine(device=0, **cfg) as e:
         for R in (7, 200, 1024, 4096):
@@ -163,6 +164,20 @@ def test_kernel_choices_are_byte_identical(sgx_lib, oracle_lib, cfg):
     with sgx_lib.ShuffleEngine(device=0, **cfg) as e:
         for R in (1024, 4096):
             check_against_oracle(e, oracle_lib, zrecs, R)
+
+
+def test_engine_start_lds_order_check(sgx_lib, oracle_lib):
+    """sgx_create probes, on the device it runs on, the property the default ranking rests on
+    (same-address LDS atomics of one wave return old values in issue order, then lane order);
+    it holds on MI355X.  When it does not (forced here by SGX_FLAG_ASSUME_LDS_DISORDER) the
+    engine ranks every scatter by ballot matching -- 100 B records included -- same bytes."""
+    with sgx_lib.ShuffleEngine(device=0) as e:
+        assert e.lds_order_ok
+    tera = oracle_lib.gen_terasort100(50_001, 17)
+    with sgx_lib.ShuffleEngine(device=0, flags=sgx_lib.FLAG_ASSUME_LDS_DISORDER, num_chunks=5) as e:
+        assert not e.lds_order_ok
+        for R in (1, 64, 2048):
+            check_against_oracle(e, oracle_lib, tera, R)
 
 
 @pytest.mark.parametrize("R", [200, 585, 586, 1000, 1024, 1025, 2048, 3000, 4096, 5000, 8192])

@@ -339,7 +339,9 @@ def test_size_query_result_reuse_and_invalidation(sgx_lib, oracle_lib):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("flags", [0, 64])  # bucket path / SGX_FLAG_NO_BUCKET_SORT (digit passes only)
+# bucket path / SGX_FLAG_NO_BUCKET_SORT (digit passes only) / SGX_FLAG_ASSUME_LDS_DISORDER (every
+# pass ballot-ranked on the per-lane kernel: the fallback if the engine-start check fails)
+@pytest.mark.parametrize("flags", [0, 64, 128])
 @pytest.mark.parametrize("case", ["hash16_R1", "hash16_R7", "hash16_R1024", "hash16_R4096", "range16_asc",
                                   "range16_desc", "tera_range", "tera_hash", "dups_in_bucket", "long_bucket"])
 def test_sorted_bucket_path(sgx_lib, oracle_lib, flags, case):
