@@ -1022,6 +1022,46 @@ ScatterGeom scatter_geom16_ord(uint32_t R, int force_waves, int force_items) {
 // the 2 KB it saved at R = 1024 let a histogram workgroup share the CU, 156 + 4 KB).  The merge's block-scan scratch borrows the stage
 // (free between B1 and B3: every wave has drained the previous tile before B1).
 // ------------------------------------------------------------------------------------
+#ifdef SGX_WC_STAMPS
+// Diagnostic build only (tools/build_variant.sh <tag> - -DSGX_WC_STAMPS, tools/wc_stamps.py):
+// per-phase s_memtime sums of the tile loop, read through sgx_diag_wc_stamps.  Never in
+// libsgx.so; read the SHARES, not the build's run time (the stamps' lgkmcnt(0) forbid overlaps).
+__device__ unsigned long long g_wc_stamps[16];
+__device__ __forceinline__ uint64_t wc_stamp() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+extern "C" int sgx_diag_wc_stamps(unsigned long long *out16, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_wc_stamps), sizeof(g_wc_stamps)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_wc_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#define WC_STAMP(i)                                \
+    do {                                           \
+        const uint64_t t_ = wc_stamp();            \
+        st_acc[i] += t_ - st_last;                 \
+        st_last = t_;                              \
+    } while (0)
+#else
+#define WC_STAMP(i) \
+    do {            \
+    } while (0)
+#endif
+
+// Drain groups (of 8 slots) whose stores are held back and issued during the next tile's
+// ranking atomics, so the CU's memory queue is not idle through the LDS-only phases
+// (C1 K4 ~1 % faster, profiles/r03_wc_late_stores_ab.jsonl).
+#ifndef SGX_WC_LATE
+#define SGX_WC_LATE 1
+#endif
+
 __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
     return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 12;  // cur 4 + dlim 8
 }
@@ -1044,6 +1084,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     constexpr int STAGE = T * SI;
     constexpr uint32_t DCAP = (uint32_t)(STAGE - TNEW);
     static_assert(SI > NI && SI <= 32 && SI % 8 == 0, "deferred slots: 32-bit mask, drained 8 at a time");
+    // drain slots [LATE_K, SI) store during the next tile's ranking (SGX_WC_LATE groups of 8,
+    // never the only group)
+    constexpr int LATE_K = SI - 8 * (SGX_WC_LATE < SI / 8 - 1 ? SGX_WC_LATE : SI / 8 - 1);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t R = pp.R, RS = rs8(R), NP = RS / 2;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1082,6 +1125,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     u32x4 dk[SI];
     uint32_t dpos[SI];
     uint32_t dmask = 0;
+    uint32_t wmask = 0;  // drained records whose store waits for the next tile's rank (SGX_WC_LATE)
 #pragma unroll
     for (int k = 0; k < SI; ++k) { dk[k] = u32x4{0, 0, 0, 0}; dpos[k] = 0; }
     if (ntiles > 0) {
@@ -1092,6 +1136,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         }
     }
     __syncthreads();
+#ifdef SGX_WC_STAMPS
+    uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_last = wc_stamp();
+#endif
     uint32_t bad = 0;
     // ---- drain: whole lines out, the rest stays in this lane's registers (dk/dpos).
     //      (Draining tile t after tile t+1's ranking, so the wait for t+1's loads does not
@@ -1108,6 +1156,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) dm[q] = dlim[pid_of<KIND>(dk[k0 + q].x, dk[k0 + q].y, dk[k0 + q].z, pp)];
+            WC_STAMP(9);  // drain: stage + dlim reads
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const uint32_t s = (uint32_t)((k0 + q) * T + tid);
@@ -1121,13 +1170,29 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 // profiles/r01_wc_nt_ab.txt).  (Branch-free stores with masked lanes into a
                 // junk line, so the next tile could wait for its loads only, measured slower:
                 // 2.01-2.04 vs 1.92-1.96 ms.)
-                if (wr) __builtin_nontemporal_store(dk[k0 + q], out + pos);
+                if (k0 >= LATE_K) wmask |= wr ? 1u << (k0 + q) : 0u;
+                else if (wr) __builtin_nontemporal_store(dk[k0 + q], out + pos);
                 dmask |= (live && !wr) ? 1u << (k0 + q) : 0u;
             }
+            WC_STAMP(10);  // drain: global stores issued
+        }
+    };
+    // the previous drain's held-back stores, issued while this tile's ranking atomics run
+    auto late_stores = [&]() {
+        if constexpr (LATE_K < SI) {
+#pragma unroll
+            for (int k = LATE_K; k < SI; ++k)
+                if ((wmask >> k) & 1u) __builtin_nontemporal_store(dk[k], out + dpos[k]);
+            wmask = 0;
         }
     };
     for (int64_t t = 0; t < ntiles; ++t) {
         const bool last = t == ntiles - 1;
+#ifdef SGX_WC_STAMPS
+        WC_STAMP(5);  // loop overhead
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the wait hipcc places here anyway
+        WC_STAMP(0);  // waiting for this tile's loads (and the last drain's stores)
+#endif
         // ---- rank the new records: one LDS atomic each, issued back to back in item order
         //      (a wave's LDS ops execute in issue order; lanes of one op in lane order), one
         //      wait at the end.  An invalid item adds 0 (branch-free issue).
@@ -1140,7 +1205,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             old[k] = __hip_atomic_fetch_add(myrow32 + (pid[k] >> 1), inc, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_WORKGROUP);
         }
+        late_stores();
         lds_barrier();  // B1
+        WC_STAMP(1);  // rank
 
         // ---- merge: per partition pair (one pair per thread), both u16 halves at once
         const uint32_t j = tid;
@@ -1194,6 +1261,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             ((uint2 *)cur)[j] = make_uint2(e0, e1);
         }
         lds_barrier();  // B3
+        WC_STAMP(2);  // merge
 
         // ---- stage: deferred records first (their slots follow from their positions), then
         //      the new ones.  LDS reads of a phase are issued together, one wait each.
@@ -1204,14 +1272,17 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             uint32_t rb[NI];
 #pragma unroll
             for (int k = 0; k < NI; ++k) rb[k] = myrow[pid[k]];
+            WC_STAMP(6);  // stage: dlt + row reads
 #pragma unroll
             for (int k = 0; k < SI; ++k)
                 if ((dmask >> k) & 1u) stage[dpos[k] - dd[k]] = dk[k];
+            WC_STAMP(7);  // stage: deferred writes
 #pragma unroll
             for (int k = 0; k < NI; ++k) {
                 const uint32_t sh = (pid[k] & 1u) << 4;
                 if (valid[k]) stage[rb[k] + ((old[k] >> sh) & 0xFFFFu)] = rec[k];
             }
+            WC_STAMP(8);  // stage: new writes
         }
         for (uint32_t i = lane; i < RS / 8; i += 64) ((u32x4 *)myrow)[i] = u32x4{0, 0, 0, 0};
         if (!last) {
@@ -1226,16 +1297,29 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             }
         }
         lds_barrier();  // B4
+        WC_STAMP(3);  // stage: zero rows, next loads, B4
         drain(total);
     }
+    late_stores();
+#ifdef SGX_WC_STAMPS
+    if (lane == 0) {
+        for (int i = 0; i < 12; ++i) atomicAdd(&g_wc_stamps[i], (unsigned long long)st_acc[i]);
+        atomicAdd(&g_wc_stamps[14], (unsigned long long)ntiles);
+        atomicAdd(&g_wc_stamps[15], 1ull);
+    }
+#endif
     if (bad) atomicOr(err, SCATTER_OOB);
 }
 
 
-// geometry: waves = WC_GEOM_BASE + 8, items = NI (new records per lane), mbits = SI
+// geometry: waves = WC_GEOM_BASE + 8, items = NI (new records per lane), mbits = SI (16)
 ScatterGeom scatter_geom16_wc(uint32_t R) {
-    constexpr int W = 8, SI = 16;
+    constexpr int W = 8;
     const uint32_t T = W * 64;
+    // (two 6-wave workgroups per CU with 8 drain slots per lane measured slower at small R:
+    // R = 200 1.82 -> 2.45 ms, the split's R = 64 levels 3.6 -> 4.0 ms;
+    // profiles/r03_wc_two_per_cu_rejected.jsonl)
+    constexpr int SI = 16;
     if (rs8(R) / 2 > T) return ScatterGeom{0, 0, 0, 0, 0};
     const size_t lds = scatter16_wc_lds(R, W, SI);
     if (lds > LDS_MAX) return ScatterGeom{0, 0, 0, 0, 0};
@@ -1619,17 +1703,18 @@ hipError_t launch_split_choice(const uint32_t *part_off, int R, uint32_t *gate, 
 hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
                                 int G, const int64_t *desc, const uint32_t *ndesc, int grid, const ScatterGeom &geo,
                                 uint32_t *err, hipStream_t stream, const uint32_t *gate, uint32_t gate_want) {
-    if (geo.waves != WC_GEOM_BASE + 8 || geo.mbits != 16 || (pp.R & (pp.R - 1)) != 0) return hipErrorInvalidValue;
-#define SGX_WCS(NI)                                                                                          \
+    if ((pp.R & (pp.R - 1)) != 0) return hipErrorInvalidValue;
+#define SGX_WCS(W, NI, SI)                                                                                   \
     do {                                                                                                     \
-        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<KIND_HASH_POW2, 8, NI, 16, true>,            \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<KIND_HASH_POW2, W, NI, SI, true>,            \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes);           \
-        hipLaunchKernelGGL((k_scatter16_wc<KIND_HASH_POW2, 8, NI, 16, true>), dim3(grid), dim3(512),         \
+        hipLaunchKernelGGL((k_scatter16_wc<KIND_HASH_POW2, W, NI, SI, true>), dim3(grid), dim3(W * 64),      \
                            geo.lds_bytes, stream, (const u32x4 *)in, (u32x4 *)out, n, (int64_t)0, pp, offs, G, \
                            err, desc, ndesc, gate, gate_want);                                               \
     } while (0)
-    if (geo.items == 12) SGX_WCS(12);
-    else if (geo.items == 8) SGX_WCS(8);
+    const int W = geo.waves - WC_GEOM_BASE;
+    if (W == 8 && geo.mbits == 16 && geo.items == 12) SGX_WCS(8, 12, 16);
+    else if (W == 8 && geo.mbits == 16 && geo.items == 8) SGX_WCS(8, 8, 16);
     else return hipErrorInvalidValue;
 #undef SGX_WCS
     return hipGetLastError();
@@ -1902,37 +1987,40 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
     if (rb == 16 && geo.waves >= WC_GEOM_BASE) {
         if ((pp.kind != SGX_PART_HASH && pp.kind != KIND_DIGIT && pp.kind != KIND_HASH_BITS &&
              pp.kind != KIND_KEY_BITS) ||
-            geo.waves != WC_GEOM_BASE + 8 || geo.mbits != 16)
+            geo.waves < WC_GEOM_BASE)
             return hipErrorInvalidValue;
-#define SGX_WC(K, NI)                                                                            \
+#define SGX_WC_SI(K, W, NI, SI)                                                                  \
     do {                                                                                         \
-        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, 8, NI, 16>,                   \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, W, NI, SI>,                   \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
-        hipLaunchKernelGGL((k_scatter16_wc<K, 8, NI, 16>), dim3(G), dim3(512), geo.lds_bytes,     \
+        hipLaunchKernelGGL((k_scatter16_wc<K, W, NI, SI>), dim3(G), dim3(W * 64), geo.lds_bytes,  \
                            stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err,   \
                            nullptr, nullptr, gate, gate_want);                                   \
     } while (0)
+        // geometries: 8 waves, NI 12 | 8, SI 16, one workgroup per CU
+        const int W = geo.waves - WC_GEOM_BASE;
+#define SGX_WC(K)                                                                                \
+    do {                                                                                         \
+        if (W == 8 && geo.mbits == 16 && geo.items == 12) SGX_WC_SI(K, 8, 12, 16);               \
+        else if (W == 8 && geo.mbits == 16 && geo.items == 8) SGX_WC_SI(K, 8, 8, 16);            \
+        else return hipErrorInvalidValue;                                                        \
+    } while (0)
         if (pp.kind == KIND_DIGIT) {
-            if (geo.items != 12 || pp.R != DIGIT_R) return hipErrorInvalidValue;
-            SGX_WC(KIND_DIGIT, 12);
+            if (pp.R != DIGIT_R) return hipErrorInvalidValue;
+            SGX_WC(KIND_DIGIT);
         } else if (pp.kind == KIND_KEY_BITS) {
             if (!pow2) return hipErrorInvalidValue;
-            if (geo.items == 12) SGX_WC(KIND_KEY_BITS, 12);
-            else if (geo.items == 8) SGX_WC(KIND_KEY_BITS, 8);
-            else return hipErrorInvalidValue;
+            SGX_WC(KIND_KEY_BITS);
         } else if (pp.kind == KIND_HASH_BITS) {
             if (!pow2) return hipErrorInvalidValue;
-            if (geo.items == 12) SGX_WC(KIND_HASH_BITS, 12);
-            else if (geo.items == 8) SGX_WC(KIND_HASH_BITS, 8);
-            else return hipErrorInvalidValue;
-        } else if (geo.items == 12) {
-            if (pow2) SGX_WC(KIND_HASH_POW2, 12); else SGX_WC(SGX_PART_HASH, 12);
-        } else if (geo.items == 8) {
-            if (pow2) SGX_WC(KIND_HASH_POW2, 8); else SGX_WC(SGX_PART_HASH, 8);
+            SGX_WC(KIND_HASH_BITS);
+        } else if (pow2) {
+            SGX_WC(KIND_HASH_POW2);
         } else {
-            return hipErrorInvalidValue;
+            SGX_WC(SGX_PART_HASH);
         }
 #undef SGX_WC
+#undef SGX_WC_SI
         return hipGetLastError();
     }
     if (rb == 16 && geo.waves >= ORD_GEOM_BASE) {

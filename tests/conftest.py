@@ -9,9 +9,19 @@ if ROOT not in sys.path:
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+def pytest_addoption(parser):
+    # A/B runs only (tools/build_variant.sh): run the suite against another build of the engine
+    parser.addoption("--sgx-lib", default=None, help="path of an alternate libsgx.so build")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libsgx.so on cuda:0)")
     config.addinivalue_line("markers", "slow: large inputs (full BASELINE sizes)")
+    alt = config.getoption("--sgx-lib")
+    if alt:
+        import sparkucx_amd._lib as L
+
+        L.LIB_PATH = os.path.abspath(alt)
 
 
 @pytest.fixture(scope="session")

@@ -1,0 +1,63 @@
+#!/usr/bin/env python3
+"""Phase shares of the write-combining K4's tile loop, from a stamp build:
+    bash tools/build_variant.sh stamps - -DSGX_WC_STAMPS
+    python tools/ab_run.py tools/ab/libsgx_stamps.so wc_stamps [--partitions 1024]
+Prints one JSON line: s_memtime cycles per tile per wave in each phase and their shares.
+The build's own run time is not a measurement (the stamps' waits forbid overlaps)."""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+PHASES = ["wait_loads", "rank", "merge", "stage_zero_loads_B4", "unused", "loop", "stage_reads", "stage_deferred_writes",
+          "stage_new_writes", "drain_lds_reads", "drain_stores", "unused2"]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--records", type=int, default=1 << 28)
+    ap.add_argument("--partitions", type=int, default=1024)
+    ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--dist", default="uniform")
+    a = ap.parse_args()
+    import numpy as np
+
+    import sparkucx_amd as sgx
+    import sparkucx_amd._lib as L
+
+    e = sgx.ShuffleEngine(0, 0)
+    so = ctypes.CDLL(L.LIB_PATH)
+    fn = so.sgx_diag_wc_stamps
+    fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
+    buf = e.alloc(a.records * 16)
+    if a.dist == "uniform":
+        e.gen_uniform16(buf, a.records, 0x5EEDC0DE)
+    else:
+        r = np.arange(1, (1 << 24) + 1, dtype=np.float64)
+        cdf = np.cumsum(r ** -1.1)
+        cdf /= cdf[-1]
+        e.gen_zipf16(buf, a.records, 0x5EEDC0DE, cdf)
+    e.register_shuffle(1, a.partitions)
+    out = (ctypes.c_ulonglong * 16)()
+    e.write_map(1, 0, buf, a.records, 16)  # warm-up
+    e.sync()
+    assert fn(out, 1) == 0
+    for i in range(a.iters):
+        e.write_map(1, 1 + i, buf, a.records, 16)
+    e.sync()
+    assert fn(out, 1) == 0
+    v = list(out)
+    waves_tiles = v[14]  # every wave adds its workgroup's tile count
+    tot = sum(v[:12])
+    res = {"partitions": a.partitions, "dist": a.dist, "workgroups": v[15] // 8, "tile_waves": v[14],
+           "cycles_per_tile_wave": {p: round(v[i] / max(1, waves_tiles), 1) for i, p in enumerate(PHASES)},
+           "share": {p: round(v[i] / max(1, tot), 4) for i, p in enumerate(PHASES)}}
+    print(json.dumps(res))
+    e.close()
+
+
+if __name__ == "__main__":
+    main()
