@@ -177,6 +177,23 @@ int sgx_lz4_unframe_streams(sgx_engine *e, const void *framed_dev, const int64_t
  * canonical order the parity tests compare).  Set before the first write (SGX_ERR_STATE
  * after).  sgx_read_grouped(SGX_AGG_SUM) on such a shuffle is combineCombinersByKey. */
 int sgx_set_map_side_combine(sgx_engine *e, int32_t shuffle_id, int32_t agg);
+/* The map writer Spark runs for the shuffle's handle.  SortShuffleManager.registerShuffle
+ * (inherited, shuffle/ucx/CommonUcxShuffleManager.scala:25) gives a dependency with a
+ * relocatable serializer (Kryo), no map-side combine and more partitions than
+ * spark.shuffle.sort.bypassMergeThreshold (200) a SerializedShuffleHandle, and the reference's
+ * getWriter (spark_3_0/UcxShuffleManager.scala:32-53) runs UnsafeShuffleWriter for it; every
+ * other handle gets SortShuffleWriter.  SGX_WRITER_SORT (the default): a map's spills are
+ * merged into ONE serialized -- and compressed -- stream per partition (ExternalSorter).
+ * SGX_WRITER_UNSAFE: UnsafeShuffleWriter with its fast spill merge
+ * (spark.shuffle.unsafe.fastMergeEnabled, LZ4 being a concatenable codec): each spill's
+ * partition segment is its own LZ4 stream (DiskBlockObjectWriter.commitAndGet per partition)
+ * and a partition's segments are concatenated in spill order.  The two differ only for a
+ * compressed Kryo map written in several batches (sgx_map_append); Spark's reader
+ * (LZ4BlockInputStream with concatenation) and sgx_read_* decode both.  Set before the first
+ * write; SGX_ERR_STATE together with map-side combine (Spark never gives such a dependency a
+ * SerializedShuffleHandle). */
+enum sgx_map_writer { SGX_WRITER_SORT = 0, SGX_WRITER_UNSAFE = 1 };
+int sgx_set_map_writer(sgx_engine *e, int32_t shuffle_id, int32_t writer);
 
 /* Reducer placement of a shuffle's exchange (sgx_exchange).  SGX_PLACE_EVEN (the default):
  * rank j holds the reducers r with floor(r * P / R) == j.  SGX_PLACE_BYTES: contiguous reducer

@@ -156,6 +156,12 @@ JNIEXPORT void JNICALL JNI_FN(setMapSideCombine)(JNIEnv *env, jclass c, jlong e,
     check(env, sgx_set_map_side_combine(E(e), sid, agg));
 }
 
+/* the map writer of the shuffle's handle (SGX_WRITER_SORT / SGX_WRITER_UNSAFE) */
+JNIEXPORT void JNICALL JNI_FN(setMapWriter)(JNIEnv *env, jclass c, jlong e, jint sid, jint writer) {
+    (void)c;
+    check(env, sgx_set_map_writer(E(e), sid, writer));
+}
+
 JNIEXPORT void JNICALL JNI_FN(unregisterShuffle)(JNIEnv *env, jclass c, jlong e, jint sid) {
     (void)c;
     check(env, sgx_unregister_shuffle(E(e), sid));

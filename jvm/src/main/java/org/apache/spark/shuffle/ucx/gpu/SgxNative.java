@@ -28,6 +28,7 @@ public final class SgxNative {
   public static final int CODEC_NONE = 0, CODEC_LZ4 = 1;
   public static final int AGG_GROUP = 0, AGG_SUM = 1;
   public static final int PLACE_EVEN = 0, PLACE_BYTES = 1;  // sgx_placement
+  public static final int WRITER_SORT = 0, WRITER_UNSAFE = 1;  // sgx_map_writer
 
   // engine lifetime: CommonUcxShuffleManager.startUcxTransport / stop
   public static native long create(int device, int numChunks, int flags, int commTimeoutMs);
@@ -41,6 +42,8 @@ public final class SgxNative {
   public static native void setSerializer(long e, int shuffleId, int serializer);
   public static native void setCompression(long e, int shuffleId, int codec, int blockSize);
   public static native void setMapSideCombine(long e, int shuffleId, int agg);
+  // the map writer of the shuffle's handle (WRITER_SORT / WRITER_UNSAFE; before the first write)
+  public static native void setMapWriter(long e, int shuffleId, int writer);
   // reducer placement of the shuffle's exchange (PLACE_EVEN / PLACE_BYTES; before its first
   // exchange) and this executor's reducer range [r0, r1) of the shuffle (after it)
   public static native void setReducerPlacement(long e, int shuffleId, int placement);

@@ -29,7 +29,7 @@ import java.nio.{ByteBuffer, ByteOrder}
 import org.apache.spark.{HashPartitioner, Partitioner, RangePartitioner, ShuffleDependency, SparkConf, TaskContext}
 import org.apache.spark.serializer.KryoSerializer
 import org.apache.spark.shuffle._
-import org.apache.spark.shuffle.sort.SortShuffleManager
+import org.apache.spark.shuffle.sort.{SortShuffleManager, SortShuffleWriter}
 
 /** A shuffle the GPU runs: same fields as BaseShuffleHandle, plus the declared aggregation. */
 class GpuShuffleHandle[K, V, C](shuffleId: Int, dependency: ShuffleDependency[K, V, C], val agg: Int)
@@ -114,6 +114,13 @@ class GpuUcxShuffleManager(conf: SparkConf, isDriver: Boolean) extends SortShuff
       }
       if (dep.mapSideCombine && h.agg == SgxNative.AGG_SUM)
         SgxNative.setMapSideCombine(engine, h.shuffleId, SgxNative.AGG_SUM)
+      // the writer Spark's own handle would run (SortShuffleManager.registerShuffle; the
+      // reference's getWriter, spark_3_0/UcxShuffleManager.scala:32-53): UnsafeShuffleWriter for
+      // a SerializedShuffleHandle, whose fast spill merge keeps each spill's partition segment
+      // as its own LZ4 stream (the batches GpuShuffleWriter appends are its spills)
+      if (!SortShuffleWriter.shouldBypassMergeSort(conf, dep) && SortShuffleManager.canUseSerializedShuffle(dep) &&
+          conf.getBoolean("spark.shuffle.unsafe.fastMergeEnabled", true))
+        SgxNative.setMapWriter(engine, h.shuffleId, SgxNative.WRITER_UNSAFE)
       // reducer placement, fixed by the shuffle's first exchange: "even" (floor(r*P/R)) or
       // "bytes" (ranges balanced on the lengths, for skewed keys)
       if (conf.get("spark.shuffle.ucx.gpu.reducerPlacement", "even") == "bytes")

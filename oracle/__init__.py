@@ -337,3 +337,35 @@ def lz4_frame_partitions(stream: np.ndarray, offs: np.ndarray, block_size: int =
     out = np.empty(max(total, 1), dtype=np.uint8)
     lib().orc_lz4_frame_partitions(sp, _ptr(offs), R, block_size, _ptr(out), _ptr(lens))
     return out[:total], lens
+
+
+def unsafe_writer_map_output(spills, num_partitions: int, kind: int = PART_HASH, bounds=None,
+                             block_size: int = LZ4_BLOCK_SIZE):
+    """UnsafeShuffleWriter (Spark 3.0.1; the reference runs it for a SerializedShuffleHandle,
+    spark_3_0/UcxShuffleManager.scala:37-45) over a map whose (Long, Long) records arrive in
+    `spills` (one (n, 16) uint8 array per spill), Kryo serializer, spark.shuffle.compress with
+    lz4.  Per spill, ShuffleExternalSorter.writeSortedFile: records stably grouped by partition
+    id (ShuffleInMemorySorter's radix sort on the partition), every non-empty partition segment
+    written through its own compressed stream and closed (DiskBlockObjectWriter.commitAndGet:
+    one LZ4BlockOutputStream per segment, ended by its end mark).  Then
+    UnsafeShuffleWriter.mergeSpillsWithTransferTo (fast merge: lz4 supports concatenation of
+    serialized streams): partition p of the data file = the spills' p segments back to back, in
+    spill order.  Returns (data bytes uint8, lengths int64[R])."""
+    R = num_partitions
+    segs = []  # per spill: (framed bytes, framed offsets[R+1])
+    for recs in spills:
+        recs = np.ascontiguousarray(recs, dtype=np.uint8).reshape(-1, 16)
+        out, counts = map_write(recs, R, kind, bounds)
+        ser = kryo_serialize(out) if len(out) else np.zeros(0, np.uint8)
+        framed, flens = lz4_frame_partitions(ser, kryo_partition_offsets(out, counts), block_size)
+        fo = np.zeros(R + 1, dtype=np.int64)
+        np.cumsum(flens, out=fo[1:])
+        segs.append((framed, fo))
+    parts, lengths = [], np.zeros(R, dtype=np.int64)
+    for p in range(R):
+        for framed, fo in segs:
+            parts.append(framed[fo[p]:fo[p + 1]])
+            lengths[p] += fo[p + 1] - fo[p]
+    data = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    return data, lengths
+

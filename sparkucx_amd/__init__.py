@@ -10,7 +10,7 @@ from ._lib import (  # noqa: F401
     FLAG_SORT_ALL_DIGITS, HIST_ATOMIC,
     HIST_BALLOT, MEM_DEVICE, MEM_HOST, PART_HASH, PART_RANGE_BYTES10, PART_RANGE_I64, PLACE_BYTES, PLACE_EVEN,
     RANK_MATCH, RANK_ORDERED,
-    SER_FIXED, SER_KRYO, STAGES,
+    SER_FIXED, SER_KRYO, STAGES, WRITER_SORT, WRITER_UNSAFE,
     BlockNotFoundException, DeviceError, IllegalArgumentException, IllegalStateException,
     ShuffleError, ShuffleIOException, TransportError, UnsupportedOperationException, lib,
 )
@@ -19,7 +19,7 @@ from .engine import (  # noqa: F401
     plan_exchange, plan_exchange_maps, reducer_owner,
 )
 from .shuffle import (  # noqa: F401
-    Aggregator, BaseShuffleHandle, BlockFetchingListener, GpuShuffleMapOutputWriter, GpuShuffleTransport, GpuShuffleWriter,
+    Aggregator, BaseShuffleHandle, BlockFetchingListener, BypassMergeSortShuffleHandle, SerializedShuffleHandle, GpuShuffleMapOutputWriter, GpuShuffleTransport, GpuShuffleWriter,
     HashPartitioner, MapStatus, MemoryBlock, MemoryPool, OperationResult, OperationStatus, RangePartitioner,
     ShuffleDependency, UcxShuffleBlockId, UcxShuffleBlockResolver, UcxShuffleManager,
     UcxShuffleClient, UcxShuffleReader, byte_string, parse_block_id,

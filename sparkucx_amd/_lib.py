@@ -32,6 +32,7 @@ FLAG_NO_SPLIT_SCATTER = 32
 FLAG_NO_BUCKET_SORT = 64
 FLAG_ASSUME_LDS_DISORDER = 128
 PLACE_EVEN, PLACE_BYTES = 0, 1
+WRITER_SORT, WRITER_UNSAFE = 0, 1
 ABI_VERSION = 5
 
 
@@ -93,6 +94,7 @@ SIGNATURES = {
     "sgx_destroy": (None, [_vp]),
     "sgx_release_thread": (ctypes.c_int, [_vp]),
     "sgx_set_map_side_combine": (ctypes.c_int, [_vp, _i32, _i32]),
+    "sgx_set_map_writer": (ctypes.c_int, [_vp, _i32, _i32]),
     "sgx_map_begin": (ctypes.c_int, [_vp, _i32, _i64]),
     "sgx_map_append": (ctypes.c_int, [_vp, _i32, _i64, _vp, _i64, _i32, _i32]),
     "sgx_map_commit": (ctypes.c_int, [_vp, _i32, _i64, _vp]),

@@ -345,7 +345,23 @@ extern "C" int sgx_set_map_side_combine(sgx_engine *e, int32_t shuffle_id, int32
     if (!s->configurable()) return fail_msg(SGX_ERR_STATE, "shuffle %d already has map outputs", shuffle_id);
     if (agg == SGX_AGG_SUM && (s->rb != 16 || s->kind == SGX_PART_RANGE_BYTES10))
         return fail_msg(SGX_ERR_UNSUPPORTED, "map-side combine needs (Long, Long) 16 B records");
+    if (agg == SGX_AGG_SUM && s->writer == SGX_WRITER_UNSAFE)
+        return fail_msg(SGX_ERR_STATE, "shuffle %d runs UnsafeShuffleWriter, which never combines", shuffle_id);
     s->combine = agg;
+    return SGX_OK;
+}
+
+extern "C" int sgx_set_map_writer(sgx_engine *e, int32_t shuffle_id, int32_t writer) {
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
+    if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
+    std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
+    if (!s) return SGX_ERR_STATE;
+    if (writer != SGX_WRITER_SORT && writer != SGX_WRITER_UNSAFE)
+        return fail_msg(SGX_ERR_INVALID, "unknown map writer %d", writer);
+    if (!s->configurable()) return fail_msg(SGX_ERR_STATE, "shuffle %d already has map outputs", shuffle_id);
+    if (writer == SGX_WRITER_UNSAFE && s->combine != -1)  // SortShuffleManager.canUseSerializedShuffle
+        return fail_msg(SGX_ERR_STATE, "shuffle %d combines map-side: Spark runs SortShuffleWriter for it", shuffle_id);
+    s->writer = writer;
     return SGX_OK;
 }
 

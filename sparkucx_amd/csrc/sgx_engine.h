@@ -165,7 +165,11 @@ struct MapOut {
     // serializer KRYO: the published bytes are the Kryo stream of the records
     DevBuf ser;                // Kryo-framed partition-contiguous bytes (capacity 20 n + 16)
     DevBuf ser_work;           // device (R+1) i64 byte offsets | tile prefixes | tile sums
-    HostPinned ser_off;        // (R+1) i64 byte offsets, landed async
+    HostPinned ser_off;        // (nseg+1) i64 byte offsets, landed async
+    // SGX_WRITER_UNSAFE, compressed, several spills: the Kryo stream is cut into nseg = R x
+    // spills segments (partition-major, spill-minor), each framed as its own LZ4 stream
+    int32_t seg_spills = 1;    // spills per partition segment list (1 = one segment per partition)
+    DevBuf seg_off;            // device (R x seg_spills + 1) u32 record offsets of the segments
     int64_t out_bytes = 0;     // published bytes
     DevBuf comp;               // LZ4-framed partition streams (sgx_set_compression), once `ready`
     bool comp_valid = false;   // `comp` holds this write's frames (false until finish_lengths)
@@ -212,6 +216,7 @@ struct Shuffle {
     int32_t ser = SGX_SER_FIXED;  // dep.serializer (sgx_set_serializer)
     int32_t lz4_block = 0;        // spark.shuffle.compress with lz4 (sgx_set_compression): block size
     int32_t combine = -1;         // map-side combine aggregation (sgx_set_map_side_combine), -1 = none
+    int32_t writer = SGX_WRITER_SORT;  // the map writer of the shuffle's handle (sgx_set_map_writer)
     std::atomic<int32_t> placement{SGX_PLACE_EVEN};  // reducer placement of exchange rounds
     // the reducer ranges of every rank, bounds[P + 1], fixed by the shuffle's first exchange
     // round (empty before): a reducer's blocks from every round land on the same rank
@@ -253,6 +258,7 @@ struct Ctx {
     DevBuf kryo_in, kryo_work, sort_buf[2], sort_err, grp_flags, grp_offs, grp_status, grp_out, grp_prefix;
     DevBuf digit_hist, items_dev, gather_stage, fetch_tmp, comb_buf;
     HostPinned gather_items;
+    HostPinned seg_host;  // (partition, spill) segment offsets of an UnsafeShuffleWriter commit
     // LZ4 framing / unframing scratch (grow-only)
     DevBuf lz4_blocks, lz4_slots, lz4_sizes, lz4_offs, lz4_info, lz4_desc;
     HostPinned lz4_host;  // pinned staging of the block list / frame sizes / frame offsets

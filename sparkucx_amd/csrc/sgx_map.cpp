@@ -193,11 +193,13 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
 // Kryo framing of the partition-contiguous 16 B records just written (sgx_serde.hip), on
 // the context's stream behind the scatter; byte offsets land in m.ser_off (pinned).
 // rec_off_dev: device (R+1) u32 record offsets of m.data.
-static int serialize_kryo(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const uint32_t *rec_off_dev) {
+// rec_off_dev: (nseg+1) u32 record offsets of the stream's segments (the R partitions, or
+// the (partition, spill) segments of SGX_WRITER_UNSAFE).
+static int serialize_kryo(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const uint32_t *rec_off_dev, int32_t nseg) {
     hipStream_t st = c.st;
     const int64_t n = m.nrec;
     const int64_t tiles = kryo_ser16_tiles(n);
-    const size_t offb = (size_t)(s.R + 1) * 8;
+    const size_t offb = (size_t)(nseg + 1) * 8;
     SGX_TRY(m.ser.ensure((size_t)(20 * n + 16)));
     SGX_TRY(m.ser_work.ensure(offb + (size_t)kryo_work_bytes(tiles)));
     SGX_TRY(m.ser_off.ensure(offb));
@@ -206,11 +208,11 @@ static int serialize_kryo(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const ui
     if (n == 0) HIP_TRY(hipMemsetAsync(off_dev, 0, offb, st));  // no tile writes them
     hipEvent_t k0 = e->ev(), k1 = e->ev();
     HIP_TRY(hipEventRecord(k0, st));
-    HIP_TRY(launch_kryo_ser16(m.data.p, n, m.ser.p, rec_off_dev, s.R, off_dev, work, st));
+    HIP_TRY(launch_kryo_ser16(m.data.p, n, m.ser.p, rec_off_dev, nseg, off_dev, work, st));
     SGX_TRY(debug_sync(e, st, "Kryo serializer"));
     HIP_TRY(hipEventRecord(k1, st));
     e->record_stage(SGX_STAGE_SERIALIZE, k0, k1);
-    HIP_TRY(hipMemcpyAsync(m.ser_off.p, off_dev, offb, hipMemcpyDeviceToHost, st));  // (R+1) byte offsets
+    HIP_TRY(hipMemcpyAsync(m.ser_off.p, off_dev, offb, hipMemcpyDeviceToHost, st));  // (nseg+1) byte offsets
     m.ser_valid = true;
     return SGX_OK;
 }
@@ -266,7 +268,12 @@ static int run_map_pipeline(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const 
                                true));
         rec_off_dev = c.last_off_dev;
     }
-    if (s.ser == SGX_SER_KRYO) SGX_TRY(serialize_kryo(e, c, s, m, rec_off_dev));
+    if (s.ser == SGX_SER_KRYO) {
+        if (m.seg_spills > 1)  // (partition, spill) segments, SGX_WRITER_UNSAFE
+            SGX_TRY(serialize_kryo(e, c, s, m, (const uint32_t *)m.seg_off.p, s.R * m.seg_spills));
+        else
+            SGX_TRY(serialize_kryo(e, c, s, m, rec_off_dev, s.R));
+    }
     HIP_TRY(m.done.record(c.st));
     m.written = true;
     return SGX_OK;
@@ -286,17 +293,18 @@ int sgx::finish_lengths(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
         return fail_msg(SGX_ERR_HIP, "partition offsets do not sum to the record count (%u vs %lld)", po[s.R],
                         (long long)m.nrec);
     m.lengths.assign((size_t)s.R, 0);
+    const int32_t S = s.ser == SGX_SER_KRYO ? m.seg_spills : 1;  // segments per partition
     if (s.ser == SGX_SER_KRYO) {
         const int64_t *so = (const int64_t *)m.ser_off.p;
         int64_t prev = 0;
         for (int32_t p = 0; p < s.R; ++p) {
-            m.lengths[(size_t)p] = so[p + 1] - so[p];
-            if (so[p] != prev || m.lengths[(size_t)p] < 0 ||
+            m.lengths[(size_t)p] = so[(size_t)(p + 1) * S] - so[(size_t)p * S];
+            if (so[(size_t)p * S] != prev || m.lengths[(size_t)p] < 0 ||
                 m.lengths[(size_t)p] > 20 * ((int64_t)po[p + 1] - po[p]))
                 return fail_msg(SGX_ERR_HIP, "internal error: Kryo partition offsets inconsistent at %d", p);
-            prev = so[p + 1];
+            prev = so[(size_t)(p + 1) * S];
         }
-        m.out_bytes = so[s.R];
+        m.out_bytes = so[(size_t)s.R * S];
     } else {
         for (int32_t p = 0; p < s.R; ++p) m.lengths[(size_t)p] = ((int64_t)po[p + 1] - (int64_t)po[p]) * s.rb;
         m.out_bytes = m.nrec * s.rb;
@@ -304,15 +312,28 @@ int sgx::finish_lengths(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
     if (s.lz4_block > 0) {  // publish the LZ4-framed partition streams instead
         // the source is this write's Kryo stream, named explicitly: `comp` may still hold an
         // earlier attempt's frames
+        // one LZ4 stream per segment: a partition (SortShuffleWriter), or a (partition, spill)
+        // segment whose streams the partition concatenates in spill order (UnsafeShuffleWriter's
+        // fast merge); the frames land partition-major, spill-minor
         const void *src = m.ser_valid ? m.ser.p : m.data.p;
-        std::vector<int64_t> offs((size_t)s.R + 1, 0);
-        for (int32_t p = 0; p < s.R; ++p) offs[(size_t)p + 1] = offs[(size_t)p] + m.lengths[(size_t)p];
-        std::vector<int64_t> clen((size_t)s.R, 0);
+        const int32_t nseg = s.R * S;
+        std::vector<int64_t> offs((size_t)nseg + 1, 0);
+        const int64_t *so = (const int64_t *)m.ser_off.p;
+        if (S > 1) {
+            for (int32_t i = 0; i <= nseg; ++i) offs[(size_t)i] = so[i];
+        } else {
+            for (int32_t p = 0; p < s.R; ++p) offs[(size_t)p + 1] = offs[(size_t)p] + m.lengths[(size_t)p];
+        }
+        std::vector<int64_t> clen((size_t)nseg, 0);
         m.comp_valid = false;
-        SGX_TRY(lz4_frame_impl(e, c, src, offs.data(), s.R, s.lz4_block, &m.comp, nullptr, 0, clen.data()));
+        SGX_TRY(lz4_frame_impl(e, c, src, offs.data(), nseg, s.lz4_block, &m.comp, nullptr, 0, clen.data()));
         int64_t total = 0;
-        for (int32_t p = 0; p < s.R; ++p) total += clen[(size_t)p];
-        m.lengths = clen;
+        for (int32_t p = 0; p < s.R; ++p) {
+            int64_t l = 0;
+            for (int32_t b = 0; b < S; ++b) l += clen[(size_t)p * S + b];
+            m.lengths[(size_t)p] = l;
+            total += l;
+        }
         m.out_bytes = total;
         m.comp_valid = true;
     }
@@ -384,6 +405,7 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
     m->exchanged = false;
     m->open = false;
     m->spills.clear();
+    m->seg_spills = 1;
     SGX_TRY(m->part_off.ensure((size_t)(s->R + 2) * 4));
     const void *in = nullptr;
     int rc = device_input(*c, records, n * rb, mem_kind, &in);
@@ -493,6 +515,24 @@ extern "C" int sgx_map_commit(sgx_engine *e, int32_t shuffle_id, int64_t map_id,
     }
     po[R] = (uint32_t)off;
     po[R + 1] = 0;
+    // UnsafeShuffleWriter's fast merge frames every (partition, spill) segment on its own:
+    // record offsets of the segments, partition-major, spill-minor (the merged layout)
+    const int32_t S = (int32_t)m->spills.size();
+    m->seg_spills = (s->writer == SGX_WRITER_UNSAFE && s->ser == SGX_SER_KRYO && s->lz4_block > 0 && S > 1) ? S : 1;
+    if (m->seg_spills > 1) {
+        const size_t nseg = (size_t)R * S;
+        SGX_TRY(c->seg_host.ensure((nseg + 1) * 4));
+        uint32_t *so = (uint32_t *)c->seg_host.p;
+        uint32_t o = 0;
+        for (int32_t p = 0; p < R; ++p)
+            for (int32_t b = 0; b < S; ++b) {
+                so[(size_t)p * S + b] = o;
+                o += (uint32_t)m->spills[(size_t)b]->lengths[(size_t)p];
+            }
+        so[nseg] = o;
+        SGX_TRY(m->seg_off.ensure((nseg + 1) * 4));
+        HIP_TRY(hipMemcpyAsync(m->seg_off.p, so, (nseg + 1) * 4, hipMemcpyHostToDevice, c->st));
+    }
     // the merged records, then the usual pipeline on an already partitioned map
     SGX_TRY(m->data.ensure((size_t)std::max<int64_t>(total * rb, 16)));
     m->nrec = total;

@@ -152,6 +152,15 @@ class ShuffleEngine:
         {key, sum} combiner per distinct key and partition."""
         check(lib().sgx_set_map_side_combine(self.handle, shuffle_id, agg), "setMapSideCombine")
 
+    def set_map_writer(self, shuffle_id: int, writer: str = "unsafe"):
+        """The map writer Spark runs for the shuffle's handle: "sort" (SortShuffleWriter, the
+        default: a multi-spill map's partition is one compressed stream) or "unsafe"
+        (UnsafeShuffleWriter's fast merge: one LZ4 stream per spill segment, concatenated)."""
+        codes = {"sort": _lib.WRITER_SORT, "unsafe": _lib.WRITER_UNSAFE}
+        if writer not in codes:
+            raise _lib.IllegalArgumentException(f"unknown map writer {writer!r} (sort, unsafe)")
+        check(lib().sgx_set_map_writer(self.handle, shuffle_id, codes[writer]), "setMapWriter")
+
     def set_reducer_placement(self, shuffle_id: int, placement: str = "bytes"):
         """Reducer placement of the shuffle's exchange rounds: "even" (floor(r*P/R), the
         default) or "bytes" (contiguous ranges balancing each rank's received bytes)."""

@@ -130,6 +130,24 @@ class ShuffleDependency:
 class BaseShuffleHandle:
     shuffleId: int
     dependency: ShuffleDependency
+    # the writer the reference's getWriter runs for this handle
+    # (spark_3_0/UcxShuffleManager.scala:32-53): UnsafeShuffleWriter for a
+    # SerializedShuffleHandle, SortShuffleWriter for every other handle (bypass included)
+    writerClass = "SortShuffleWriter"
+
+
+@dataclass
+class BypassMergeSortShuffleHandle(BaseShuffleHandle):
+    """SortShuffleWriter.shouldBypassMergeSort: no map-side combine and at most
+    spark.shuffle.sort.bypassMergeThreshold (200) partitions.  The reference's getWriter still
+    runs SortShuffleWriter for it."""
+
+
+@dataclass
+class SerializedShuffleHandle(BaseShuffleHandle):
+    """SortShuffleManager.canUseSerializedShuffle: a serializer that supports relocation of
+    serialized objects (Kryo), no map-side combine, at most 2^24 partitions."""
+    writerClass = "UnsafeShuffleWriter"
 
 
 @dataclass
@@ -402,8 +420,19 @@ class GpuShuffleWriter:
         self._status: Optional[MapStatus] = None
 
     def write(self, records, numRecords: Optional[int] = None):
+        """records: one batch (numpy / torch / DeviceBuffer), or a list of batches -- the
+        spills of the map task, appended in order (sgx_map_begin / _append / _commit)."""
         dep = self.handle.dependency
         rb = dep.recordBytes
+        if isinstance(records, (list, tuple)):
+            e, sid = self.manager.engine, self.handle.shuffleId
+            e.map_begin(sid, self.mapId)
+            for batch in records:
+                e.map_append(sid, self.mapId, batch, self._count(batch, rb), rb)
+            lengths = e.map_commit(sid, self.mapId, dep.partitioner.numPartitions)
+            self.manager._map_written(sid, self.mapId)
+            self._status = MapStatus(self.mapId, lengths)
+            return
         if numRecords is None:
             if isinstance(records, np.ndarray):
                 numRecords = records.nbytes // rb
@@ -415,6 +444,12 @@ class GpuShuffleWriter:
         lengths = self.manager.engine.write_map(self.handle.shuffleId, self.mapId, records, numRecords, rb, R)
         self.manager._map_written(self.handle.shuffleId, self.mapId)
         self._status = MapStatus(self.mapId, lengths)
+
+    @staticmethod
+    def _count(batch, rb: int) -> int:
+        if isinstance(batch, (np.ndarray, DeviceBuffer)):
+            return batch.nbytes // rb
+        return batch.numel() * batch.element_size() // rb
 
     def mapOutputWriter(self) -> GpuShuffleMapOutputWriter:
         if self._status is None:
@@ -622,6 +657,7 @@ class UcxShuffleManager:
                                      _SERIALIZERS[dependency.serializer])
         if dependency.mapSideCombine:
             self.engine.set_map_side_combine(shuffleId, _lib.AGG_SUM)
+        h = self._handle_for(shuffleId, dependency)
         # spark.shuffle.compress (Spark 3.0.1's default: true) with spark.io.compression.codec
         # lz4 (the default): applied to Kryo shuffles, whose bytes are Spark's own; the fixed
         # 16 B / 100 B record codec is the engine's own format and stays raw
@@ -636,10 +672,29 @@ class UcxShuffleManager:
                     f"spark.io.compression.lz4.blockSize {block} B: the GPU codec takes blocks up to 32 KiB")
             self.engine.set_compression(shuffleId, "lz4", block)
             self._compressed.add(shuffleId)
-        h = BaseShuffleHandle(shuffleId, dependency)
+        # UnsafeShuffleWriter merges its spills fast (spark.shuffle.unsafe.fastMergeEnabled,
+        # lz4 supports concatenation): each spill's partition segment stays its own stream;
+        # the slow merge re-compresses one stream per partition, as SortShuffleWriter writes
+        if (isinstance(h, SerializedShuffleHandle)
+                and self.conf.get("spark.shuffle.unsafe.fastMergeEnabled", "true").lower() == "true"):
+            self.engine.set_map_writer(shuffleId, "unsafe")
         self._handles[shuffleId] = h
         self._maps[shuffleId] = set()
         return h
+
+    def _handle_for(self, shuffleId: int, dep: ShuffleDependency) -> BaseShuffleHandle:
+        """SortShuffleManager.registerShuffle (Spark 3.0.1; inherited by the reference,
+        shuffle/ucx/CommonUcxShuffleManager.scala:25): bypass if SortShuffleWriter
+        .shouldBypassMergeSort, else serialized if SortShuffleManager.canUseSerializedShuffle,
+        else the base handle.  The engine's fixed record codec is not a Spark serializer: its
+        dependencies get the base handle."""
+        R = dep.partitioner.numPartitions
+        if not dep.mapSideCombine and R <= int(self.conf.get("spark.shuffle.sort.bypassMergeThreshold", "200")):
+            return BypassMergeSortShuffleHandle(shuffleId, dep)
+        relocatable = _SERIALIZERS[dep.serializer] == _lib.SER_KRYO  # KryoSerializer (autoReset on)
+        if relocatable and not dep.mapSideCombine and R <= (1 << 24):
+            return SerializedShuffleHandle(shuffleId, dep)
+        return BaseShuffleHandle(shuffleId, dep)
 
     def getWriter(self, handle: BaseShuffleHandle, mapId: int, context=None, metrics=None) -> GpuShuffleWriter:
         if handle.shuffleId not in self._handles:

@@ -114,6 +114,7 @@ jbyteArray Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_bootstrapJoin(JNIEnv 
 void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_bootstrapServe(JNIEnv *, jclass, jint, jint, jbyteArray, jint);
 void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchange(JNIEnv *, jclass, jlong, jint);
 void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchangeMaps(JNIEnv *, jclass, jlong, jint, jlongArray);
+void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_setMapWriter(JNIEnv *, jclass, jlong, jint, jint);
 jintArray Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_shuffleReducers(JNIEnv *, jclass, jlong, jint);
 
 static obj *jstr(const char *s) {
@@ -163,6 +164,11 @@ int fake_fetch_mismatched(int64_t engine) {
 
 int fake_exchange(int64_t engine) {
     Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchange(&g_env, NULL, engine, 1);
+    return 0;
+}
+
+int fake_set_map_writer(int64_t engine, int writer) {
+    Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_setMapWriter(&g_env, NULL, engine, 1, writer);
     return 0;
 }
 

@@ -35,6 +35,7 @@ def shim(sgx_lib, tmp_path_factory):
     L.fake_fetch_mismatched.argtypes = [ctypes.c_int64]
     L.fake_exchange.argtypes = [ctypes.c_int64]
     L.fake_exchange_maps.argtypes = [ctypes.c_int64, ctypes.c_int]
+    L.fake_set_map_writer.argtypes = [ctypes.c_int64, ctypes.c_int]
     L.fake_shuffle_reducers.argtypes = [ctypes.c_int64, ctypes.c_void_p]
     L.fake_bootstrap_join.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                       ctypes.c_void_p]
@@ -91,6 +92,11 @@ def test_argument_errors_become_illegal_argument(shim):
     r = np.zeros(2, np.int32)
     assert shim.fake_shuffle_reducers(0, r.ctypes.data) == -1
     assert exc(shim)[0] == "java/lang/IllegalArgumentException"
+    # the handle's map writer (GpuUcxShuffleManager: UnsafeShuffleWriter for a SerializedShuffleHandle)
+    for w in (0, 1):
+        shim.fake_clear()
+        shim.fake_set_map_writer(0, w)
+        assert exc(shim)[0] == "java/lang/IllegalArgumentException", w
 
 
 def test_bootstrap_natives_and_fetch_failure_mapping(shim):

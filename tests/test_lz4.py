@@ -136,6 +136,51 @@ def test_golden_frames_decode(path):
         assert got == want
 
 
+def test_unsafe_writer_fast_merge_restatement(oracle_lib):
+    """oracle.unsafe_writer_map_output (UnsafeShuffleWriter, fast spill merge): decoding each
+    partition with LZ4BlockInputStream's rules -- liblz4 per block, every XXH32 checked, an end
+    mark followed by more bytes starts the next concatenated stream -- gives the partition's
+    canonical Kryo stream; every spill segment holds one end mark; one spill equals the
+    SortShuffleWriter framing (oracle.lz4_frame_partitions of the whole map)."""
+    L = _liblz4()
+    xxhash = pytest.importorskip("xxhash")
+    R, block = 7, 4096
+    sizes = [3000, 0, 1, 5000, 17]
+    recs = oracle_lib.gen_uniform16(sum(sizes), 0x7700)
+    spills = np.split(recs, np.cumsum(sizes)[:-1])
+    data, lens = oracle_lib.unsafe_writer_map_output(spills, R, block_size=block)
+    out, counts = oracle_lib.map_write(recs, R)
+    kry = oracle_lib.kryo_serialize(out).tobytes()
+    koff = oracle_lib.kryo_partition_offsets(out, counts)
+    per_spill = [oracle_lib.map_write(sp, R)[1] for sp in spills]
+    pos = 0
+    for r in range(R):
+        part = data[pos:pos + lens[r]].tobytes()
+        pos += lens[r]
+        got, nend, p = b"", 0, 0
+        while p < len(part):  # LZ4BlockInputStream with concatenation (Spark 3.0.1's codec)
+            tok = part[p + 8]
+            cl, ol, ck = (int.from_bytes(part[p + 9 + 4 * i:p + 13 + 4 * i], "little") for i in range(3))
+            pay = part[p + 21:p + 21 + cl]
+            p += 21 + cl
+            if ol == 0:
+                nend += 1
+                continue
+            if tok & 0xF0 == 0x10:
+                blk = pay
+            else:
+                buf = ctypes.create_string_buffer(ol)
+                assert L.LZ4_decompress_safe(pay, buf, cl, ol) == ol
+                blk = buf.raw
+            assert ck == xxhash.xxh32_intdigest(blk, 0x9747B28C) & 0x0FFFFFFF
+            got += blk
+        assert got == kry[koff[r]:koff[r + 1]]
+        assert nend == sum(1 for c in per_spill if c[r] > 0)
+    one, one_len = oracle_lib.unsafe_writer_map_output([recs], R, block_size=block)
+    canon, canon_len = oracle_lib.lz4_frame_partitions(np.frombuffer(kry, np.uint8), koff, block)
+    assert np.array_equal(one_len, canon_len) and np.array_equal(one, canon)
+
+
 # ------------------------------------------------------------------------ GPU ------
 def _to_device(engine, data: bytes):
     buf = engine.alloc(max(len(data), 1))
@@ -477,6 +522,46 @@ def test_gpu_plugin_spark_shuffle_compress(sgx_lib, oracle_lib, tmp_path):
         assert rd.readSerialized().tobytes() == kry[ko[10]:ko[20]].tobytes()
         o = oracle_lib.offsets(counts)
         assert rd.read().tobytes() == out[o[10]:o[20]].tobytes()
+    finally:
+        mgr.stop()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,fast,handle", [(1024, "true", "SerializedShuffleHandle"),
+                                           (1024, "false", "SerializedShuffleHandle"),
+                                           (200, "true", "BypassMergeSortShuffleHandle")])
+def test_gpu_plugin_handle_selection_and_spills(sgx_lib, oracle_lib, tmp_path, R, fast, handle):
+    """registerShuffle picks Spark's handle (SortShuffleManager.registerShuffle) and the writer
+    the reference's getWriter runs for it (spark_3_0/UcxShuffleManager.scala:32-53); a map task
+    written in spills publishes UnsafeShuffleWriter's fast-merge framing for a
+    SerializedShuffleHandle and SortShuffleWriter's single stream per partition otherwise (slow
+    merge, bypass handle); the data file and read() agree with the restatement."""
+    mgr = sgx_lib.UcxShuffleManager(conf={"spark.shuffle.unsafe.fastMergeEnabled": fast}, localDir=str(tmp_path))
+    try:
+        h = mgr.registerShuffle(9, sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(R), serializer="kryo"))
+        assert type(h).__name__ == handle
+        assert h.writerClass == ("UnsafeShuffleWriter" if handle == "SerializedShuffleHandle" else "SortShuffleWriter")
+        recs = oracle_lib.gen_uniform16(120_000, 0x9090)
+        spills = [recs[:50_000], recs[50_000:50_001], recs[50_001:]]
+        w = mgr.getWriter(h, 0)
+        w.write(spills)
+        if handle == "SerializedShuffleHandle" and fast == "true":
+            want, wlens = oracle_lib.unsafe_writer_map_output(spills, R)
+        else:
+            out, counts = oracle_lib.map_write(recs, R)
+            want, wlens = oracle_lib.lz4_frame_partitions(oracle_lib.kryo_serialize(out),
+                                                          oracle_lib.kryo_partition_offsets(out, counts))
+        assert np.array_equal(w.getPartitionLengths(), wlens)
+        mgr.shuffleBlockResolver.writeIndexFileAndCommit(9, 0, w.getPartitionLengths().copy())
+        assert open(mgr.shuffleBlockResolver.getDataFile(9, 0), "rb").read() == want.tobytes()
+        out, counts = oracle_lib.map_write(recs, R)
+        o = oracle_lib.offsets(counts)
+        assert mgr.getReader(h, 3, R - 5).read().tobytes() == out[o[3]:o[R - 5]].tobytes()
+        # map-side combine: never a SerializedShuffleHandle
+        hc = mgr.registerShuffle(10, sgx_lib.ShuffleDependency(sgx_lib.HashPartitioner(R), serializer="kryo",
+                                                               aggregator=sgx_lib.Aggregator("sum"),
+                                                               mapSideCombine=True))
+        assert type(hc).__name__ == "BaseShuffleHandle" and hc.writerClass == "SortShuffleWriter"
     finally:
         mgr.stop()
 

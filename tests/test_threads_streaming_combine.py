@@ -163,6 +163,63 @@ def test_streaming_map_equals_one_batch(sgx_lib, oracle_lib, codec, R):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("R", [1, 3, 200, 1024])
+@pytest.mark.parametrize("block", [32768, 64])
+def test_unsafe_writer_fast_merge_framing(sgx_lib, oracle_lib, R, block):
+    """UnsafeShuffleWriter (SerializedShuffleHandle, spark_3_0/UcxShuffleManager.scala:37-45)
+    on a compressed Kryo shuffle: every spill's partition segment is its own LZ4 stream and a
+    partition concatenates them in spill order (mergeSpillsWithTransferTo's fast merge).
+    Lengths, published bytes and fetched blocks equal the restatement; one spill equals the
+    SortShuffleWriter output; the readers decode the concatenated streams."""
+    sizes = [70_001, 0, 1, 8192, 30_000, 3] if block == 32768 else [700, 0, 1, 90, 300, 3]
+    recs = oracle_lib.gen_uniform16(sum(sizes), 0x6600 + R)
+    spills, pos = [], 0
+    for sz in sizes:
+        spills.append(recs[pos:pos + sz])
+        pos += sz
+    want, want_len = oracle_lib.unsafe_writer_map_output(spills, R, block_size=block)
+    with sgx_lib.ShuffleEngine(device=0) as e:
+        for sid, writer in ((1, "unsafe"), (2, "sort"), (3, "unsafe")):
+            e.register_shuffle(sid, R, serializer=sgx_lib.SER_KRYO)
+            e.set_compression(sid, "lz4", block)
+            e.set_map_writer(sid, writer)
+        for sid in (1, 2):
+            e.map_begin(sid, 0)
+            for k, part in enumerate(spills):
+                e.map_append(sid, 0, np.ascontiguousarray(part), len(part), 16)
+            lengths = e.map_commit(sid, 0, R)
+            if sid == 1:
+                assert np.array_equal(lengths, want_len)
+                assert np.array_equal(e.map_output_bytes(1, 0), want)
+        # several spills: the two writers' bytes differ, their records do not
+        assert not np.array_equal(e.map_output_bytes(1, 0), e.map_output_bytes(2, 0))
+        seqs = oracle_lib.canonical_reducer_sequences([oracle_lib.map_write(recs, R)], R, 16)
+        for r0, r1 in ((0, R), (R // 2, R)):
+            got = e.read_records(1, [0], r0, r1).reshape(-1, 16)
+            assert np.array_equal(got, np.concatenate(seqs[r0:r1]))
+            assert np.array_equal(e.read_sorted(1, [0], r0, r1).reshape(-1, 16), oracle_lib.reduce_sorted(seqs[r0:r1]))
+        # every block is the partition's concatenated streams
+        off = np.concatenate([[0], np.cumsum(want_len)])
+        for r in {0, R // 2, R - 1}:
+            host, lens = e.fetch_blocks(1, [0], [r])
+            assert np.array_equal(host[:lens[0]], want[off[r]:off[r + 1]])
+        # one spill: UnsafeShuffleWriter writes what SortShuffleWriter writes
+        e.write_map(3, 0, recs, len(recs), 16, R)
+        one_len = e.map_lengths(3, 0, R)
+        e.map_begin(3, 1)
+        e.map_append(3, 1, recs, len(recs), 16)
+        assert np.array_equal(e.map_commit(3, 1, R), one_len)
+        assert np.array_equal(e.map_output_bytes(3, 1), e.map_output_bytes(3, 0))
+        # Spark never gives a combining dependency a SerializedShuffleHandle
+        e.register_shuffle(4, R, serializer=sgx_lib.SER_KRYO)
+        e.set_map_side_combine(4)
+        with pytest.raises(sgx_lib.IllegalStateException):
+            e.set_map_writer(4, "unsafe")
+        with pytest.raises(sgx_lib.IllegalStateException):
+            e.set_map_side_combine(1)  # shuffle 1 already has map outputs
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("codec", ["fixed", "kryo", "kryo+lz4"])
 @pytest.mark.parametrize("R,n,distinct", [(1, 10_000, 50), (200, 300_000, 20_000), (1024, 500_000, 3_000_000),
                                           (4096, 200_000, 700)])
