@@ -130,6 +130,7 @@ PartParams sgx::make_part_params(const Shuffle &s) {
     pp.nb = s.nb;
     pp.ascending = s.asc;
     pp.bounds = s.bounds.p;
+    pp.dir = s.dir_ok ? (const uint16_t *)((const char *)s.bounds.p + s.dir_off) : nullptr;
     return pp;
 }
 
@@ -258,20 +259,53 @@ extern "C" int sgx_register_shuffle(sgx_engine *e, int32_t shuffle_id, int32_t R
     s->nb = (int32_t)(kind == SGX_PART_HASH ? 0 : nbounds);
     s->asc = ascending ? 1 : 0;
     s->rb = rb;
-    if (kind == SGX_PART_RANGE_I64 && nbounds > 0) {
-        SGX_TRY(s->bounds.ensure((size_t)nbounds * 8));
-        HIP_TRY(hipMemcpy(s->bounds.p, bounds, (size_t)nbounds * 8, hipMemcpyHostToDevice));
-    } else if (kind == SGX_PART_RANGE_BYTES10 && nbounds > 0) {
-        std::vector<Key10> k((size_t)nbounds);
-        const uint8_t *b = (const uint8_t *)bounds;
-        for (int64_t i = 0; i < nbounds; ++i) {
-            const uint8_t *q = b + 10 * i;
-            uint64_t hi = 0;
-            for (int j = 0; j < 8; ++j) hi = (hi << 8) | q[j];
-            k[(size_t)i] = Key10{hi, ((uint32_t)q[8] << 8) | q[9], 0};
+    if (kind != SGX_PART_HASH && nbounds > 0) {
+        // bounds in the kernels' layout (i64, or Key10 = big-endian 10-byte keys), then the
+        // top-bits directory when the lower bound IS RangePartitioner.getPartition's answer
+        std::vector<uint64_t> top((size_t)nbounds);  // bounds as unsigned-ordered 64-bit tops
+        std::vector<Key10> k;
+        const size_t braw = kind == SGX_PART_RANGE_I64 ? (size_t)nbounds * 8 : (size_t)nbounds * sizeof(Key10);
+        const size_t boff = (braw + 15) & ~(size_t)15;
+        bool strict = true, sorted = true;
+        if (kind == SGX_PART_RANGE_I64) {
+            const int64_t *b = (const int64_t *)bounds;
+            for (int64_t i = 0; i < nbounds; ++i) {
+                top[(size_t)i] = (uint64_t)b[i] ^ 0x8000000000000000ull;  // signed order -> unsigned
+                if (i && b[i] <= b[i - 1]) { strict = false; sorted = sorted && b[i] == b[i - 1]; }
+            }
+        } else {
+            k.resize((size_t)nbounds);
+            const uint8_t *b = (const uint8_t *)bounds;
+            for (int64_t i = 0; i < nbounds; ++i) {
+                const uint8_t *q = b + 10 * i;
+                uint64_t hi = 0;
+                for (int j = 0; j < 8; ++j) hi = (hi << 8) | q[j];
+                k[(size_t)i] = Key10{hi, ((uint32_t)q[8] << 8) | q[9], 0};
+                top[(size_t)i] = hi;
+                if (i) {
+                    const Key10 &a = k[(size_t)i - 1], &c = k[(size_t)i];
+                    const bool le = c.hi < a.hi || (c.hi == a.hi && c.lo <= a.lo);
+                    if (le) { strict = false; sorted = sorted && c.hi == a.hi && c.lo == a.lo; }
+                }
+            }
         }
-        SGX_TRY(s->bounds.ensure((size_t)nbounds * sizeof(Key10)));
-        HIP_TRY(hipMemcpy(s->bounds.p, k.data(), k.size() * sizeof(Key10), hipMemcpyHostToDevice));
+        // Spark's linear branch (<= 128 bounds) is a lower bound for any sorted bounds; its
+        // binary search (JDK Arrays.binarySearch) is one for strictly increasing bounds (what
+        // RangePartitioner.determineBounds produces) -- otherwise keep the exact JDK loop
+        s->dir_ok = sorted && (strict || nbounds <= 128) && nbounds < 65535;
+        s->dir_off = boff;
+        SGX_TRY(s->bounds.ensure(boff + RDIR_BYTES));
+        if (kind == SGX_PART_RANGE_I64) HIP_TRY(hipMemcpy(s->bounds.p, bounds, braw, hipMemcpyHostToDevice));
+        else HIP_TRY(hipMemcpy(s->bounds.p, k.data(), braw, hipMemcpyHostToDevice));
+        if (s->dir_ok) {
+            std::vector<uint16_t> dir((size_t)RDIR_N);
+            int64_t i = 0;
+            for (int64_t j = 0; j < RDIR_N; ++j) {
+                while (i < nbounds && (int64_t)(top[(size_t)i] >> (64 - RDIR_BITS)) < j) ++i;
+                dir[(size_t)j] = (uint16_t)i;
+            }
+            HIP_TRY(hipMemcpy((char *)s->bounds.p + boff, dir.data(), dir.size() * 2, hipMemcpyHostToDevice));
+        }
     }
     s->pp = make_part_params(*s);
     std::lock_guard<std::mutex> lk(e->reg_mu);

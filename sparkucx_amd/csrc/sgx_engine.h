@@ -221,7 +221,9 @@ struct Shuffle {
     // the reducer ranges of every rank, bounds[P + 1], fixed by the shuffle's first exchange
     // round (empty before): a reducer's blocks from every round land on the same rank
     std::vector<int32_t> place_bounds;
-    DevBuf bounds;
+    DevBuf bounds;                // the bounds, then (dir_ok) their top-bits directory at dir_off
+    bool dir_ok = false;
+    size_t dir_off = 0;
     PartParams pp{};
     std::map<int64_t, std::shared_ptr<MapOut>> maps;
     std::vector<std::shared_ptr<Round>> rounds;

@@ -23,7 +23,14 @@ struct PartParams {
     const void *bounds;  // device: int64[nb] (RANGE_I64) or Key10[nb] (RANGE_BYTES10)
     uint32_t dshift;     // KIND_DIGIT: bit offset of the digit in the record's first 12 bytes (LE)
     uint32_t dflip;      // KIND_DIGIT: XORed into the digit (0x80 = sign flip of an i64 key's top byte)
+    // range kinds: directory of the bounds by the key's top RDIR_BITS bits (device u16
+    // [2^RDIR_BITS + 1]: dir[j] = first bound whose top bits are >= j), or null when the bounds
+    // need the JDK binary search's exact path (duplicates with more than 128 bounds)
+    const uint16_t *dir;
 };
+constexpr int RDIR_BITS = 10;
+constexpr int RDIR_N = (1 << RDIR_BITS) + 1;
+constexpr size_t RDIR_BYTES = ((size_t)RDIR_N * 2 + 15) & ~(size_t)15;
 // Internal partition kind of the reduce side's LSD radix passes: pid = 8-bit digit of the
 // key (R = 256), see PartParams::dshift / dflip.  Never registered through the C ABI.
 constexpr int KIND_DIGIT = 200;

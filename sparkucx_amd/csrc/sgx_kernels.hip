@@ -52,11 +52,24 @@ __device__ __forceinline__ uint32_t hash_pid(uint32_t klo, uint32_t khi, const P
 // KIND_HASH_POW2 (sgx_internal.h): HashPartitioner with a power-of-two R, where
 // nonNegativeMod(h, R) == h & (R - 1) for two's-complement h.
 
-// RangePartitioner.getPartition over bounds `b` (global memory, or an LDS copy).
-template <typename BP>
-__device__ __forceinline__ uint32_t range_pid_i64(int64_t key, BP b, int nb, int ascending) {
+// RangePartitioner.getPartition over bounds `b` (global memory, or an LDS copy).  With the
+// bounds' top-bits directory (PartParams::dir, built at registration only where the answer
+// is the lower bound: Spark's linear branch, or its binary search over strictly increasing
+// bounds) a key searches the few bounds sharing its top RDIR_BITS bits -- ~1 at R = 1024 --
+// instead of the JDK loop's ~10 dependent, lane-divergent steps.
+template <typename BP, typename DP>
+__device__ __forceinline__ uint32_t range_pid_i64(int64_t key, BP b, DP dir, int nb, int ascending) {
     int p = 0;
-    if (nb <= 128) {
+    if (dir) {
+        const uint32_t j = (uint32_t)(((uint64_t)key ^ 0x8000000000000000ull) >> (64 - RDIR_BITS));
+        int lo = dir[j], hi = dir[j + 1];
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (b[mid] < key) lo = mid + 1;
+            else hi = mid;
+        }
+        p = lo;
+    } else if (nb <= 128) {
         while (p < nb && key > b[p]) ++p;
     } else {  // JDK Arrays.binarySearch0 loop, then insertion point, then clamp
         int low = 0, high = nb - 1;
@@ -78,10 +91,19 @@ __device__ __forceinline__ bool k10_lt(uint64_t ahi, uint32_t alo, uint64_t bhi,
     return ahi < bhi || (ahi == bhi && alo < blo);
 }
 
-template <typename BP>
-__device__ __forceinline__ uint32_t range_pid_k10(uint64_t khi, uint32_t klo, BP b, int nb, int ascending) {
+template <typename BP, typename DP>
+__device__ __forceinline__ uint32_t range_pid_k10(uint64_t khi, uint32_t klo, BP b, DP dir, int nb, int ascending) {
     int p = 0;
-    if (nb <= 128) {
+    if (dir) {
+        const uint32_t j = (uint32_t)(khi >> (64 - RDIR_BITS));
+        int lo = dir[j], hi = dir[j + 1];
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (k10_lt(b[mid].hi, b[mid].lo, khi, klo)) lo = mid + 1;
+            else hi = mid;
+        }
+        p = lo;
+    } else if (nb <= 128) {
         while (p < nb && k10_lt(b[p].hi, b[p].lo, khi, klo)) ++p;
     } else {
         int low = 0, high = nb - 1;
@@ -104,7 +126,7 @@ __device__ __forceinline__ uint32_t range_pid_k10(uint64_t khi, uint32_t klo, BP
 // bounds read through `bounds` (pp.bounds in global memory, or a copy in LDS).
 template <int KIND, typename BI64 = const int64_t *, typename BK10 = const Key10 *>
 __device__ __forceinline__ uint32_t pid_of_b(uint32_t x, uint32_t y, uint32_t z, const PartParams &pp,
-                                             BI64 bi64, BK10 bk10) {
+                                             BI64 bi64, BK10 bk10, const uint16_t *bdir) {
     if constexpr (KIND == SGX_PART_HASH) {
         return hash_pid(x, y, pp);
     } else if constexpr (KIND == KIND_DIGIT) {
@@ -121,12 +143,18 @@ __device__ __forceinline__ uint32_t pid_of_b(uint32_t x, uint32_t y, uint32_t z,
                                       : (((uint64_t)__builtin_bswap32(x) << 32) | __builtin_bswap32(y));
         return (uint32_t)(wnd >> pp.dshift) & (pp.R - 1u);
     } else if constexpr (KIND == SGX_PART_RANGE_I64) {
-        return range_pid_i64((int64_t)(((uint64_t)y << 32) | x), bi64, pp.nb, pp.ascending);
+        return range_pid_i64((int64_t)(((uint64_t)y << 32) | x), bi64, bdir, pp.nb, pp.ascending);
     } else {
         const uint64_t hi = ((uint64_t)__builtin_bswap32(x) << 32) | __builtin_bswap32(y);
         const uint32_t lo = __builtin_bswap32(z) >> 16;
-        return range_pid_k10(hi, lo, bk10, pp.nb, pp.ascending);
+        return range_pid_k10(hi, lo, bk10, bdir, pp.nb, pp.ascending);
     }
+}
+
+template <int KIND, typename BI64 = const int64_t *, typename BK10 = const Key10 *>
+__device__ __forceinline__ uint32_t pid_of_b(uint32_t x, uint32_t y, uint32_t z, const PartParams &pp,
+                                             BI64 bi64, BK10 bk10) {
+    return pid_of_b<KIND>(x, y, z, pp, bi64, bk10, pp.dir);
 }
 
 template <int KIND>
@@ -209,13 +237,19 @@ __device__ __forceinline__ void hist_body(const char *__restrict__ in, int64_t n
     // chain of ~log2(R) loads per record: LDS latency instead of L1/L2)
     // (LB false: bounds too large for LDS, read from global memory)
     char *bl = smem + (((size_t)pp.R * 4 + 15) & ~(size_t)15);
+    uint16_t *dl = (uint16_t *)(bl + (((size_t)pp.nb * (KIND == SGX_PART_RANGE_BYTES10 ? sizeof(Key10) : 8) + 15) &
+                                      ~(size_t)15));
     if constexpr (LB && KIND == SGX_PART_RANGE_BYTES10) {
         for (int i = (int)tid; i < pp.nb; i += (int)T) ((Key10 *)bl)[i] = ((const Key10 *)pp.bounds)[i];
     } else if constexpr (LB && KIND == SGX_PART_RANGE_I64) {
         for (int i = (int)tid; i < pp.nb; i += (int)T) ((int64_t *)bl)[i] = ((const int64_t *)pp.bounds)[i];
     }
+    if constexpr (LB && (KIND == SGX_PART_RANGE_BYTES10 || KIND == SGX_PART_RANGE_I64))
+        if (pp.dir)
+            for (int i = (int)tid; i < RDIR_N; i += (int)T) dl[i] = pp.dir[i];
     const int64_t *bi64 = LB ? (const int64_t *)bl : (const int64_t *)pp.bounds;
     const Key10 *bk10 = LB ? (const Key10 *)bl : (const Key10 *)pp.bounds;
+    const uint16_t *bdir = (LB && pp.dir) ? (const uint16_t *)dl : pp.dir;
     __syncthreads();
     const int g = blockIdx.x / SPLIT, sub = blockIdx.x % SPLIT;
     const int64_t cbeg = (int64_t)g * chunk;
@@ -244,12 +278,12 @@ __device__ __forceinline__ void hist_body(const char *__restrict__ in, int64_t n
             const int64_t i = base + (int64_t)u * T + tid;
             if constexpr (AGG) {
                 const bool live = i < cend;
-                const uint32_t p = live ? pid_of_b<KIND>(x[u], y[u], z[u], pp, bi64, bk10) : 0u;
+                const uint32_t p = live ? pid_of_b<KIND>(x[u], y[u], z[u], pp, bi64, bk10, bdir) : 0u;
                 const uint64_t peers = match_peers(p, __ballot(live), pp.nbits);
                 const uint32_t lane = tid & 63u;
                 if (live && (peers & ((1ull << lane) - 1ull)) == 0) atomicAdd(&hist[p], (uint32_t)__popcll(peers));
             } else {
-                if (i < cend) atomicAdd(&hist[pid_of_b<KIND>(x[u], y[u], z[u], pp, bi64, bk10)], 1u);
+                if (i < cend) atomicAdd(&hist[pid_of_b<KIND>(x[u], y[u], z[u], pp, bi64, bk10, bdir)], 1u);
             }
         }
     }
@@ -271,8 +305,8 @@ hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
                        const PartParams &pp, uint32_t *counts, hipStream_t stream, int mode, bool zeroed) {
     const size_t hlds = (((size_t)pp.R * 4 + 15) & ~(size_t)15);
     size_t lds = hlds;
-    if (pp.kind == SGX_PART_RANGE_BYTES10) lds += (size_t)pp.nb * sizeof(Key10);
-    else if (pp.kind == SGX_PART_RANGE_I64) lds += (size_t)pp.nb * 8;
+    if (pp.kind == SGX_PART_RANGE_BYTES10) lds += (((size_t)pp.nb * sizeof(Key10) + 15) & ~(size_t)15) + RDIR_BYTES;
+    else if (pp.kind == SGX_PART_RANGE_I64) lds += (((size_t)pp.nb * 8 + 15) & ~(size_t)15) + RDIR_BYTES;
     const bool lb = lds <= LDS_MAX;  // else the bounds stay in global memory
     if (!lb) lds = hlds;
     const char *p = (const char *)in;
@@ -1411,7 +1445,7 @@ constexpr int WIDE2_TR = 1024;
 
 __host__ __device__ size_t scatter_wide2_lds(uint32_t R, int rb, int kind, int nb) {
     const size_t bsz = kind == SGX_PART_RANGE_BYTES10 ? sizeof(Key10) : 8;
-    return al16((size_t)WIDE2_TR * rb) + (kind == SGX_PART_HASH ? 0 : al16((size_t)nb * bsz)) +
+    return al16((size_t)WIDE2_TR * rb) + (kind == SGX_PART_HASH ? 0 : al16((size_t)nb * bsz) + RDIR_BYTES) +
            (size_t)8 * rs8(R) * 2 + (size_t)rs8(R) * 8 + (size_t)WIDE2_TR * 4 + 64 * 4;
 }
 
@@ -1437,12 +1471,20 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
     sp += al16((size_t)TR * RB);
     const Key10 *bk10 = (const Key10 *)sp;
     const int64_t *bi64 = (const int64_t *)sp;
+    const uint16_t *bdir = nullptr;
     if constexpr (KIND == SGX_PART_RANGE_BYTES10) {
         for (int i = tid; i < pp.nb; i += T) ((Key10 *)sp)[i] = ((const Key10 *)pp.bounds)[i];
         sp += al16((size_t)pp.nb * sizeof(Key10));
     } else if constexpr (KIND == SGX_PART_RANGE_I64) {
         for (int i = tid; i < pp.nb; i += T) ((int64_t *)sp)[i] = ((const int64_t *)pp.bounds)[i];
         sp += al16((size_t)pp.nb * 8);
+    }
+    if constexpr (KIND == SGX_PART_RANGE_BYTES10 || KIND == SGX_PART_RANGE_I64) {
+        if (pp.dir) {
+            for (int i = tid; i < RDIR_N; i += T) ((uint16_t *)sp)[i] = pp.dir[i];
+            bdir = (const uint16_t *)sp;
+        }
+        sp += RDIR_BYTES;
     }
     uint16_t *rows = (uint16_t *)sp;
     uint32_t *cur = (uint32_t *)(rows + (size_t)W * RS);
@@ -1477,8 +1519,23 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
     };
     if (ntiles > 0) issue(0);
     uint32_t bad = 0;
+#ifdef SGX_WC_STAMPS
+    uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_last = wc_stamp();
+#endif
+    auto store_piece = [&](const u32x4 &v, uint32_t dst, uint32_t pc) {
+        uint32_t *d = out + (uint64_t)dst * DW + 4 * pc;
+        if (TAILW == 4 || pc + 1 < PC) {
+            *(u32x4 *)d = v;
+        } else {
+            d[0] = v.x;
+            if (TAILW > 1) d[1] = v.y;
+            if (TAILW > 2) d[2] = v.z;
+        }
+    };
     for (int t = 0; t < ntiles; ++t) {
         const int nrec = t + 1 < ntiles ? TR : lastn;
+        WC_STAMP(0);  // loop top (previous drain's barrier)
         // ---- land the tile in LDS (the previous drain finished at the last barrier)
         if (nrec == TR) {
 #pragma unroll
@@ -1491,7 +1548,9 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
             for (int d = tid; d < nrec * DW; d += T) stage[d] = tb[d];
         }
         __syncthreads();
+        WC_STAMP(1);  // land: wait for the tile's loads, LDS stage writes, barrier
         if (t + 1 < ntiles) issue(t + 1);  // in flight during this whole tile
+        WC_STAMP(2);  // issue the next tile's loads
         // ---- partition ids + rank (records w*128 + k*64 + lane: input order = (wave, item, lane))
         uint32_t pid[ITEMS], old[ITEMS];
         bool valid[ITEMS];
@@ -1500,8 +1559,9 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
             const uint32_t r = w * (TR / W) + k * 64 + lane;
             valid[k] = r < (uint32_t)nrec;
             const uint32_t *rp = stage + (valid[k] ? r : 0) * DW;
-            pid[k] = valid[k] ? pid_of_b<KIND>(rp[0], rp[1], rp[2], pp, bi64, bk10) : 0u;
+            pid[k] = valid[k] ? pid_of_b<KIND>(rp[0], rp[1], rp[2], pp, bi64, bk10, bdir) : 0u;
         }
+        WC_STAMP(3);  // partition ids (range search in LDS)
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) {
             const uint32_t inc = valid[k] ? 1u << ((pid[k] & 1u) << 4) : 0u;
@@ -1509,6 +1569,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
                                             __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         lds_barrier();
+        WC_STAMP(4);  // rank atomics + barrier
         // ---- merge: per partition pair, prefix over the wave rows, block scan
         constexpr int PPM = 2;  // pairs per thread (R <= 2048)
         uint32_t before[PPM][W], tot[PPM], S = 0;
@@ -1546,6 +1607,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
             }
         }
         lds_barrier();
+        WC_STAMP(5);  // merge (two barriers)
         // ---- sorted index of the tile: idx[slot] = source record | partition << 16
 #pragma unroll
         for (int k = 0; k < ITEMS; ++k) {
@@ -1555,6 +1617,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
         }
         for (uint32_t i = lane; i < RS / 8; i += 64) ((u32x4 *)myrow)[i] = u32x4{0, 0, 0, 0};
         lds_barrier();
+        WC_STAMP(6);  // sorted index + barrier
         // ---- drain: the sorted tile in 16 B pieces, PC per record (RB = 100: six of 16 B and
         //      one of 4 B), consecutive lanes -> consecutive pieces, so a partition run still
         //      leaves the CU as consecutive lanes, with a quarter of the store instructions and
@@ -1582,22 +1645,24 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
                 }
                 dst[q] = dlt[e >> 16] + s;
             }
+            WC_STAMP(7);  // drain: LDS reads
+            // (holding the last batch's pieces back for the next tile's ranking, as the 16 B
+            // kernel does, measured slower here: DESIGN.md §6.4)
 #pragma unroll
-            for (int q = 0; q < DRB; ++q) {
-                if (live[q] && dst[q] < (uint32_t)n) {
-                    uint32_t *d = out + (uint64_t)dst[q] * DW + 4 * pc[q];
-                    if (TAILW == 4 || pc[q] + 1 < PC) {
-                        *(u32x4 *)d = v[q];
-                    } else {
-                        d[0] = v[q].x;
-                        if (TAILW > 1) d[1] = v[q].y;
-                        if (TAILW > 2) d[2] = v[q].z;
-                    }
-                }
-            }
+            for (int q = 0; q < DRB; ++q)
+                if (live[q] && dst[q] < (uint32_t)n) store_piece(v[q], dst[q], pc[q]);
+            WC_STAMP(8);  // drain: global stores
         }
         __syncthreads();  // stage / idx reused by the next tile
+        WC_STAMP(9);  // final barrier
     }
+#ifdef SGX_WC_STAMPS
+    if (lane == 0) {
+        for (int i = 0; i < 12; ++i) atomicAdd(&g_wc_stamps[i], (unsigned long long)st_acc[i]);
+        atomicAdd(&g_wc_stamps[14], (unsigned long long)ntiles);
+        atomicAdd(&g_wc_stamps[15], 1ull);
+    }
+#endif
     if (bad) atomicOr(err, SCATTER_OOB);
 }
 

@@ -304,6 +304,68 @@ def test_terasort_bytes10(engine, oracle_lib, nb):
     check_against_oracle(engine, oracle_lib, recs, nb + 1, sgx.PART_RANGE_BYTES10, bounds)
 
 
+@pytest.mark.parametrize("shape", ["one_bucket", "two_buckets", "dups_linear", "dups_jdk", "extremes"])
+@pytest.mark.parametrize("rb", [16, 100])
+def test_range_directory_edges(engine, oracle_lib, shape, rb):
+    """The bounds' top-bits directory (sgx_register_shuffle, range_pid_*): every bound sharing
+    the key's top 10 bits (one directory bucket holding the whole search), bounds split over
+    two buckets, duplicate bounds on Spark's linear branch (<= 128: a lower bound, directory
+    used) and on its binary search (> 128: the exact JDK loop, no directory), and keys at the
+    extremes of the key space -- every key also hitting a bound exactly -- against the oracle,
+    both orders, 16 B Long keys and 100 B TeraSort keys, on every scatter kernel."""
+    import sparkucx_amd as sgx
+
+    rng = np.random.default_rng(len(shape) * 100 + rb)
+    n = 40_000
+    recs = oracle_lib.gen_uniform16(n, 77) if rb == 16 else oracle_lib.gen_terasort100(n, 77)
+    if rb == 16:
+        kind = sgx.PART_RANGE_I64
+        top = np.int64(0x1230000000000000)
+        if shape == "one_bucket":
+            b = np.unique(top + rng.integers(0, 1 << 40, 700))
+        elif shape == "two_buckets":
+            b = np.unique(np.concatenate([top + rng.integers(0, 1 << 40, 300), -top + rng.integers(0, 1 << 40, 300)]))
+        elif shape == "dups_linear":
+            b = np.sort(np.repeat(rng.integers(-(1 << 62), 1 << 62, 40), 3))[:120]
+        elif shape == "dups_jdk":
+            b = np.sort(np.repeat(rng.integers(-(1 << 62), 1 << 62, 100), 3))
+        else:
+            b = np.array([-(1 << 63), -(1 << 63) + 1, -1, 0, 1, (1 << 63) - 2, (1 << 63) - 1], dtype=np.int64)
+        b = np.sort(b.astype(np.int64))
+        keys = recs[:, :8].copy().view(np.int64).ravel()
+        keys[:len(b)] = b  # exact hits
+        if shape == "one_bucket" or shape == "two_buckets":
+            keys[len(b):len(b) + 20000] = top + rng.integers(-(1 << 41), 1 << 41, 20000)
+        keys[-4:] = [-(1 << 63), (1 << 63) - 1, 0, -1]
+        recs[:, :8] = keys.view(np.uint8).reshape(-1, 8)  # (the strided view's ravel is a copy)
+        bounds = b
+    else:
+        kind = sgx.PART_RANGE_BYTES10
+        keys = recs[:, :10]
+        if shape == "one_bucket":
+            b = rng.integers(0, 256, (700, 10), dtype=np.uint8)
+            b[:, 0], b[:, 1] = 0x12, 0x30
+        elif shape == "two_buckets":
+            b = rng.integers(0, 256, (600, 10), dtype=np.uint8)
+            b[:300, 0], b[:300, 1], b[300:, 0], b[300:, 1] = 0x12, 0x30, 0xF0, 0x00
+        elif shape == "dups_linear":
+            b = np.repeat(rng.integers(0, 256, (40, 10), dtype=np.uint8), 3, axis=0)[:120]
+        elif shape == "dups_jdk":
+            b = np.repeat(rng.integers(0, 256, (100, 10), dtype=np.uint8), 3, axis=0)
+        else:
+            b = np.array([[0] * 10, [0] * 9 + [1], [0x7F] + [0xFF] * 9, [0xFF] * 9 + [0xFE], [0xFF] * 10], np.uint8)
+        b = b[np.lexsort(b.T[::-1])]
+        if shape in ("one_bucket", "two_buckets"):
+            b = np.unique(b, axis=0)
+        bounds = np.ascontiguousarray(b)
+        keys[:len(b)] = bounds
+        if shape in ("one_bucket", "two_buckets"):
+            keys[len(b):len(b) + 20000, 0], keys[len(b):len(b) + 20000, 1] = 0x12, 0x30
+        keys[-2:] = [[0] * 10, [0xFF] * 10]
+    for asc in (True, False):
+        check_against_oracle(engine, oracle_lib, recs, len(bounds) + 1, kind, bounds, asc)
+
+
 @pytest.mark.parametrize("wide2", ["1", "0"])
 @pytest.mark.parametrize("R", [1, 7, 1000, 2048, 4096])
 @pytest.mark.parametrize("n", [1, 1023, 1024, 5 * 1024 + 77, 3 * 4096 + 1001])

@@ -14,6 +14,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 PHASES = ["wait_loads", "rank", "merge", "stage_zero_loads_B4", "unused", "loop", "stage_reads", "stage_deferred_writes",
           "stage_new_writes", "drain_lds_reads", "drain_stores", "unused2"]
+# k_scatter_wide2 (TeraSort 100 B records, --record-bytes 100)
+PHASES_WIDE2 = ["loop_top", "land_stage_writes_barrier", "issue_next_loads", "partition_ids", "rank_barrier",
+                "merge", "sorted_index", "drain_lds_reads", "drain_stores", "final_barrier", "unused", "unused2"]
 
 
 def main():
@@ -22,6 +25,7 @@ def main():
     ap.add_argument("--partitions", type=int, default=1024)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--dist", default="uniform")
+    ap.add_argument("--record-bytes", type=int, default=16, choices=[16, 100])
     a = ap.parse_args()
     import numpy as np
 
@@ -32,29 +36,40 @@ def main():
     so = ctypes.CDLL(L.LIB_PATH)
     fn = so.sgx_diag_wc_stamps
     fn.argtypes = [ctypes.POINTER(ctypes.c_ulonglong), ctypes.c_int]
-    buf = e.alloc(a.records * 16)
-    if a.dist == "uniform":
+    rb = a.record_bytes
+    n = a.records if rb == 16 else a.records * 16 // 100
+    buf = e.alloc(n * rb)
+    if rb == 100:
+        e.gen_terasort100(buf, n, 0x5EEDC0DE)
+        hi = (np.arange(1, a.partitions, dtype=np.uint64) * (np.uint64(1 << 63) // np.uint64(a.partitions)) * 2)
+        bounds = np.zeros((a.partitions - 1, 10), np.uint8)
+        for j in range(8):
+            bounds[:, j] = (hi >> np.uint64(56 - 8 * j)) & np.uint64(0xFF)
+        e.register_shuffle(1, a.partitions, kind=sgx.PART_RANGE_BYTES10, bounds=bounds, record_bytes=100)
+    elif a.dist == "uniform":
         e.gen_uniform16(buf, a.records, 0x5EEDC0DE)
     else:
         r = np.arange(1, (1 << 24) + 1, dtype=np.float64)
         cdf = np.cumsum(r ** -1.1)
         cdf /= cdf[-1]
         e.gen_zipf16(buf, a.records, 0x5EEDC0DE, cdf)
-    e.register_shuffle(1, a.partitions)
+    if rb == 16:
+        e.register_shuffle(1, a.partitions)
     out = (ctypes.c_ulonglong * 16)()
-    e.write_map(1, 0, buf, a.records, 16)  # warm-up
+    e.write_map(1, 0, buf, n, rb)  # warm-up
     e.sync()
     assert fn(out, 1) == 0
     for i in range(a.iters):
-        e.write_map(1, 1 + i, buf, a.records, 16)
+        e.write_map(1, 1 + i, buf, n, rb)
     e.sync()
     assert fn(out, 1) == 0
     v = list(out)
     waves_tiles = v[14]  # every wave adds its workgroup's tile count
     tot = sum(v[:12])
-    res = {"partitions": a.partitions, "dist": a.dist, "workgroups": v[15] // 8, "tile_waves": v[14],
-           "cycles_per_tile_wave": {p: round(v[i] / max(1, waves_tiles), 1) for i, p in enumerate(PHASES)},
-           "share": {p: round(v[i] / max(1, tot), 4) for i, p in enumerate(PHASES)}}
+    names = PHASES_WIDE2 if rb == 100 else PHASES
+    res = {"partitions": a.partitions, "dist": a.dist if rb == 16 else "terasort", "workgroups": v[15] // 8, "tile_waves": v[14],
+           "cycles_per_tile_wave": {p: round(v[i] / max(1, waves_tiles), 1) for i, p in enumerate(names)},
+           "share": {p: round(v[i] / max(1, tot), 4) for i, p in enumerate(names)}}
     print(json.dumps(res))
     e.close()
 
