@@ -57,8 +57,8 @@ def main():
     side = {"read_bytes": 0.0, "write_bytes": 0.0, "us": 0.0}
     k4 = None
     for k, (calls, avg) in sorted(stats.items(), key=lambda kv: -kv[1][0] * kv[1][1]):
-        if k.replace("sgx::", "").startswith("k_gen"):
-            continue
+        if k.replace("sgx::", "").startswith(("k_gen", "k_lds_order_probe")):
+            continue  # the input generator; the engine-start LDS ordering check (once per engine)
         per = calls / iters_kt
         rd = statistics.median(fetch[k]) * 2 * 1024 if k in fetch else 0.0
         wr = statistics.median(write[k]) * 1024 if k in write else 0.0
