@@ -46,14 +46,21 @@ def main():
         else:
             n, rb = a.records, 16
             buf = e.alloc(n * rb)
-            if dist == "uniform":
+            if dist in ("uniform", "range"):
                 e.gen_uniform16(buf, n, 0x5EEDC0DE)
             else:
                 r = np.arange(1, (1 << 24) + 1, dtype=np.float64)
                 cdf = np.cumsum(r ** -1.1)
                 cdf /= cdf[-1]
                 e.gen_zipf16(buf, n, 0x5EEDC0DE, cdf)
-            e.register_shuffle(sid, R)
+            if dist == "range":  # RangePartitioner over the Long keys (sortByKey): sampled, distinct bounds
+                keys = buf.to_numpy(min(n, 1 << 20) * 16).reshape(-1, 16)[:, :8].copy().view(np.int64).ravel()
+                rng = np.random.default_rng(R)
+                smp = np.unique(keys[rng.choice(len(keys), 20 * R, replace=False)])
+                bounds = smp[np.linspace(0, len(smp) - 1, R + 1).astype(int)[1:-1]]
+                e.register_shuffle(sid, R, sgx.PART_RANGE_I64, bounds, True, 16)
+            else:
+                e.register_shuffle(sid, R)
         e.write_map(sid, 0, buf, n, rb, R)  # warm-up
         e.sync()
         e.stats_reset()
