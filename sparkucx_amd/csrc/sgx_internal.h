@@ -45,6 +45,15 @@ constexpr int KIND_HASH_BITS = 300;
 // key's 64-bit order window W -- a 16 B record's signed Long key with its sign flipped
 // (dflip = 1), or a 100 B record's first 8 key bytes big-endian (dflip = 0).
 constexpr int KIND_KEY_BITS = 400;
+// Internal kind of the hybrid split's level 1 (hash, power-of-two R > 1024): pid = stream of
+// the record's partition (k_lo ^ k_hi) & (2^dshift - 1), looked up in the per-map table
+// PartParams::dir (u16 [2^dshift], staged in LDS): the hot partitions' own streams
+// [0, SPLIT_HOT_CAP), then one stream per cold super-partition of 64 partitions.
+constexpr int KIND_HOT_SPLIT = 500;
+#ifndef SGX_SPLIT_HOT_CAP
+#define SGX_SPLIT_HOT_CAP 704
+#endif
+constexpr int SPLIT_HOT_CAP = SGX_SPLIT_HOT_CAP;  // + S <= 64 cold supers: <= 768 level-1 streams (LDS)
 
 // Granlund-Montgomery parameters of mod_u32 (sgx_kernels.hip) for 2 <= R < 2^31:
 // l = ceil(log2 R), m = floor(2^32 (2^l - R) / R) + 1, shift = l - 1.
@@ -103,22 +112,37 @@ int64_t scan_tiles(int64_t len);
 // csum[s][g] = sum over the Q sub-partitions q of counts[(s*Q + q)][g]   (S*G entries);
 // desc: the level-2 pieces cut from the level-1 offsets (offs1[S][G], u32) -- each piece a
 // run of whole (super, chunk) blocks inside one super-partition, about `target` records --
-// as {begin, -, super, first chunk} int64 quadruples (a piece ends at the next one's begin),
+// as {begin, -, super, first chunk} int64 quadruples (a piece ends at the next one's begin;
+// cut every *total / pieces records, *total = the level-1 record count on the device),
 // their count in npieces[1] (flags / idx: S*G u32 scratch; status / ticket: a zeroed scan
 // work area of scan_tiles(S*G) tiles);
 // launch_scatter16_seg: level 2, write-combining K4 with R = Q over the pieces, cursors
 // offs[(super*Q + q)][chunk] of the single-level scan.
 hipError_t launch_super_counts(const uint32_t *counts, uint32_t *csum, int S, int Q, int G, hipStream_t stream);
-hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, int64_t n, int64_t target, int64_t *desc,
+hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, const uint32_t *total, int64_t pieces, int64_t *desc,
                            uint32_t *flags, uint32_t *idx, uint64_t *status, uint32_t *ticket, uint32_t *err,
                            uint32_t *npieces, hipStream_t stream);
+// seg_end: device count of the level-1 records the pieces cover (the last piece's end)
 hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
-                                int G, const int64_t *desc, const uint32_t *ndesc, int grid, const ScatterGeom &geo,
-                                uint32_t *err, hipStream_t stream, const uint32_t *gate = nullptr,
-                                uint32_t gate_want = 0);
+                                int G, const int64_t *desc, const uint32_t *ndesc, const uint32_t *seg_end, int grid,
+                                const ScatterGeom &geo, uint32_t *err, hipStream_t stream,
+                                const uint32_t *gate = nullptr, uint32_t gate_want = 0);
 // *gate = 1 when no partition holds more than 1/50 of the records (the split's kernels run),
 // 0 otherwise (the single lane-ordered pass runs): both are launched, gated on the flag.
 hipError_t launch_split_choice(const uint32_t *part_off, int R, uint32_t *gate, hipStream_t stream);
+// Hybrid split: from the partition offsets, stream_of[p] = hot index for
+// about the SPLIT_HOT_CAP largest partitions (a coarse count histogram picks the cut; the hot
+// ones numbered in id order), else SPLIT_HOT_CAP + p / Q; hot_part[h] = the partition of hot
+// stream h (-1: unused).
+// csum[s][g] = the cold partitions' counts summed per super-partition s and chunk g;
+// cur1[(SPLIT_HOT_CAP + S) x G] = level-1 cursors: a hot stream's final offsets
+// offs[p][g], a cold super's scratch offsets offs1[s][g].
+hipError_t launch_hot_select(const uint32_t *part_off, int R, int Q, uint16_t *stream_of, int32_t *hot_part,
+                             hipStream_t stream);
+hipError_t launch_super_counts_cold(const uint32_t *counts, const uint16_t *stream_of, uint32_t *csum, int S, int Q,
+                                    int G, hipStream_t stream);
+hipError_t launch_hot_cursors(const uint32_t *offs, const int32_t *hot_part, const uint32_t *offs1, uint32_t *cur1,
+                              int S, int G, hipStream_t stream);
 // The sorted read's last step: `in` is ordered by bucket = (P(key) << kbits) | key window
 // bits [kshift, kshift + kbits) (P the shuffle's hash partitioner when use_p, else 0); every
 // bucket is sorted stably by the full key on chip (16 B: signed Long; 100 B: 10-byte
@@ -129,9 +153,11 @@ hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, cons
 // Engine-start self-check of the lane-ordered LDS atomics the ordered ranking relies on:
 // *bad |= 1 on any violation (sgx_create).
 hipError_t launch_lds_order_probe(uint32_t *bad, hipStream_t stream);
+// out2 / hot_cap: KIND_HOT_SPLIT only -- streams >= hot_cap go to out2 (the split's scratch)
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes, int64_t chunk,
                           int G, const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
-                          uint32_t *err, hipStream_t stream, const uint32_t *gate = nullptr, uint32_t gate_want = 0);
+                          uint32_t *err, hipStream_t stream, const uint32_t *gate = nullptr, uint32_t gate_want = 0,
+                          void *out2 = nullptr, uint32_t hot_cap = 0);
 // items: [n][3] int64 {src_off, dst_off, bytes}; all offsets/bytes multiples of `align`.
 // LZ4BlockOutputStream framing (sgx_lz4.hip)
 int lz4_lanes_per_workgroup();

@@ -138,6 +138,8 @@ __device__ __forceinline__ uint32_t pid_of_b(uint32_t x, uint32_t y, uint32_t z,
         return (x ^ y) & (pp.R - 1u);
     } else if constexpr (KIND == KIND_HASH_BITS) {
         return ((x ^ y) >> pp.dshift) & (pp.R - 1u);
+    } else if constexpr (KIND == KIND_HOT_SPLIT) {
+        return bdir[(x ^ y) & ((1u << pp.dshift) - 1u)];
     } else if constexpr (KIND == KIND_KEY_BITS) {
         const uint64_t wnd = pp.dflip ? ((((uint64_t)y << 32) | x) ^ 0x8000000000000000ull)
                                       : (((uint64_t)__builtin_bswap32(x) << 32) | __builtin_bswap32(y));
@@ -1112,7 +1114,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                                                                 const int64_t *__restrict__ desc = nullptr,
                                                                 const uint32_t *__restrict__ ndesc = nullptr,
                                                                 const uint32_t *__restrict__ gate = nullptr,
-                                                                uint32_t gate_want = 0) {
+                                                                uint32_t gate_want = 0,
+                                                                u32x4 *__restrict__ out2 = nullptr,
+                                                                uint32_t hot_cap = 0,
+                                                                const uint32_t *__restrict__ seg_end = nullptr) {
     constexpr int T = WAVES * 64;
     constexpr int TNEW = T * NI;
     constexpr int STAGE = T * SI;
@@ -1129,6 +1134,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     uint32_t *cur = (uint32_t *)(rows + (size_t)WAVES * RS);
     uint2 *dlim = (uint2 *)(cur + RS);          // {dlt_p, lim_p}: one ds_read_b64 per drained slot
     uint32_t *scratch = (uint32_t *)smem;  // merge only (B1..B3)
+    // KIND_HOT_SPLIT: the map's partition -> stream table, staged after dlim
+    uint16_t *tbl = (uint16_t *)(dlim + RS);
+    // a record's stream: the partition id, or (hybrid split) its partition's stream
+    auto pidf = [&](const u32x4 &r) __attribute__((always_inline)) -> uint32_t {
+        if constexpr (KIND == KIND_HOT_SPLIT) return tbl[(r.x ^ r.y) & ((1u << pp.dshift) - 1u)];
+        else return pid_of<KIND>(r.x, r.y, r.z, pp);
+    };
     uint16_t *myrow = rows + (size_t)w * RS;
     uint32_t *myrow32 = (uint32_t *)myrow;
     const uint32_t n32 = (uint32_t)n;  // n < 2^32 (sgx_write_map)
@@ -1140,7 +1152,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         if (blockIdx.x >= *ndesc) return;  // the whole workgroup, before any barrier
         const int64_t *d = desc + 4 * (int64_t)blockIdx.x;
         begin = d[0];
-        end = blockIdx.x + 1 < *ndesc ? d[4] : n;  // the next piece's begin
+        // the next piece's begin; the last piece ends with the level-1 records (the cold ones)
+        end = blockIdx.x + 1 < *ndesc ? d[4] : (int64_t)*seg_end;
         obase = d[2] * (int64_t)R;
         g = (int)d[3];
     }
@@ -1152,6 +1165,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         dlim[p] = make_uint2(0u, c0);  // lim = cur: nothing deferred
     }
     for (uint32_t i = tid; i < (uint32_t)WAVES * RS / 2; i += T) ((uint32_t *)rows)[i] = 0u;
+    if constexpr (KIND == KIND_HOT_SPLIT)
+        for (uint32_t i = tid; i < (1u << pp.dshift); i += T) tbl[i] = pp.dir[i];
 
     const u32x4 *src = in + begin + (int64_t)w * NI * 64 + lane;
     u32x4 rec[NI];
@@ -1178,18 +1193,22 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     // ---- drain: whole lines out, the rest stays in this lane's registers (dk/dpos).
     //      (Draining tile t after tile t+1's ranking, so the wait for t+1's loads does not
     //      also wait for t's stores, measured slightly slower: 1.90-1.97 vs 1.86-1.95 ms.)
-    auto drain = [&](const uint32_t ntot) {
+    auto drain = [&](const uint32_t ntot) __attribute__((always_inline)) {
         dmask = 0;
 #pragma unroll
         for (int k0 = 0; k0 < SI; k0 += 8) {
             uint2 dm[8];
+            uint32_t pq[8];
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const uint32_t s = (uint32_t)((k0 + q) * T + tid);
                 dk[k0 + q] = stage[s];  // slots past `total` hold stale records: never used
             }
 #pragma unroll
-            for (int q = 0; q < 8; ++q) dm[q] = dlim[pid_of<KIND>(dk[k0 + q].x, dk[k0 + q].y, dk[k0 + q].z, pp)];
+            for (int q = 0; q < 8; ++q) {
+                pq[q] = pidf(dk[k0 + q]);
+                dm[q] = dlim[pq[q]];
+            }
             WC_STAMP(9);  // drain: stage + dlim reads
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
@@ -1204,19 +1223,29 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 // profiles/r01_wc_nt_ab.txt).  (Branch-free stores with masked lanes into a
                 // junk line, so the next tile could wait for its loads only, measured slower:
                 // 2.01-2.04 vs 1.92-1.96 ms.)
+                uint64_t ob = (uint64_t)out;
+                if constexpr (KIND == KIND_HOT_SPLIT) {
+                    const bool o2 = pq[q] >= hot_cap;
+                    ob = o2 ? (uint64_t)out2 : ob;
+                }
                 if (k0 >= LATE_K) wmask |= wr ? 1u << (k0 + q) : 0u;
-                else if (wr) __builtin_nontemporal_store(dk[k0 + q], out + pos);
+                else if (wr) __builtin_nontemporal_store(dk[k0 + q], (u32x4 *)ob + pos);
                 dmask |= (live && !wr) ? 1u << (k0 + q) : 0u;
             }
             WC_STAMP(10);  // drain: global stores issued
         }
     };
     // the previous drain's held-back stores, issued while this tile's ranking atomics run
-    auto late_stores = [&]() {
+    auto late_stores = [&]() __attribute__((always_inline)) {
         if constexpr (LATE_K < SI) {
 #pragma unroll
-            for (int k = LATE_K; k < SI; ++k)
-                if ((wmask >> k) & 1u) __builtin_nontemporal_store(dk[k], out + dpos[k]);
+            for (int k = LATE_K; k < SI; ++k) {
+                // (a held record's buffer is looked up again: keeping a per-slot mask of it made
+                // hipcc move dk[] to scratch memory)
+                uint64_t ob = (uint64_t)out;
+                if constexpr (KIND == KIND_HOT_SPLIT) ob = pidf(dk[k]) >= hot_cap ? (uint64_t)out2 : ob;
+                if ((wmask >> k) & 1u) __builtin_nontemporal_store(dk[k], (u32x4 *)ob + dpos[k]);
+            }
             wmask = 0;
         }
     };
@@ -1232,7 +1261,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         //      wait at the end.  An invalid item adds 0 (branch-free issue).
         uint32_t pid[NI], old[NI];
 #pragma unroll
-        for (int k = 0; k < NI; ++k) pid[k] = valid[k] ? pid_of<KIND>(rec[k].x, rec[k].y, rec[k].z, pp) : 0u;
+        for (int k = 0; k < NI; ++k) pid[k] = valid[k] ? pidf(rec[k]) : 0u;
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
             const uint32_t inc = valid[k] ? 1u << ((pid[k] & 1u) << 4) : 0u;
@@ -1302,7 +1331,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         {
             uint32_t dd[SI];
 #pragma unroll
-            for (int k = 0; k < SI; ++k) dd[k] = dlim[pid_of<KIND>(dk[k].x, dk[k].y, dk[k].z, pp)].x;
+            for (int k = 0; k < SI; ++k) dd[k] = dlim[pidf(dk[k])].x;
             uint32_t rb[NI];
 #pragma unroll
             for (int k = 0; k < NI; ++k) rb[k] = myrow[pid[k]];
@@ -1711,10 +1740,13 @@ hipError_t launch_super_counts(const uint32_t *counts, uint32_t *csum, int S, in
 // flags (K3) numbers the pieces, and k_seg_desc writes piece k = {begin, -, super, chunk}.
 // A piece ends where the next begins (the supers are contiguous), the last one at n: the
 // level-2 kernel reads its end from its successor's begin.
-__global__ __launch_bounds__(256) void k_seg_flags(const uint32_t *__restrict__ offs1, int S, int G, int64_t target,
-                                                   uint32_t *__restrict__ flags) {
+// pieces: about `pieces` of them over the level-1 records (*total, on the device: the hybrid's
+// cold records), cut every `target` records
+__global__ __launch_bounds__(256) void k_seg_flags(const uint32_t *__restrict__ offs1, int S, int G, int64_t pieces,
+                                                   const uint32_t *__restrict__ total, uint32_t *__restrict__ flags) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (int64_t)S * G) return;
+    const int64_t target = max((int64_t)1, ((int64_t)*total + pieces - 1) / pieces);
     const bool f = i % G == 0 || (int64_t)offs1[i] / target != (int64_t)offs1[i - 1] / target;
     flags[i] = f ? 1u : 0u;
 }
@@ -1730,13 +1762,12 @@ __global__ __launch_bounds__(256) void k_seg_desc(const uint32_t *__restrict__ o
     d[3] = i % G;
 }
 
-hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, int64_t n, int64_t target, int64_t *desc,
+hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, const uint32_t *total, int64_t pieces, int64_t *desc,
                            uint32_t *flags, uint32_t *idx, uint64_t *status, uint32_t *ticket, uint32_t *err,
                            uint32_t *npieces, hipStream_t stream) {
     const int64_t nb = (int64_t)S * G;
     const unsigned grid = (unsigned)((nb + 255) / 256);
-    (void)n;
-    hipLaunchKernelGGL(k_seg_flags, dim3(grid), dim3(256), 0, stream, offs1, S, G, target, flags);
+    hipLaunchKernelGGL(k_seg_flags, dim3(grid), dim3(256), 0, stream, offs1, S, G, pieces, total, flags);
     // one "partition" over all blocks: idx = exclusive prefix of the flags, npieces[1] = total
     hipLaunchKernelGGL(k_scan, dim3((unsigned)scan_tiles(nb)), dim3(SCAN_THREADS), 0, stream, (const uint32_t *)flags,
                        idx, nb, status, ticket, err, npieces, (int)nb, 1);
@@ -1765,9 +1796,131 @@ hipError_t launch_split_choice(const uint32_t *part_off, int R, uint32_t *gate, 
     return hipGetLastError();
 }
 
+// Hybrid split.  Moving a hot partition's records twice is what made the
+// plain split lose on skewed keys, so level 1 writes about the SPLIT_HOT_CAP largest
+// partitions straight to the final output through streams of their own (write-combined like
+// every stream: a write-combining pass costs about the same at 768 streams as at 64), and
+// only the others go through their super-partition to level 2 -- fewer records for level 2
+// on any keys.  Any choice of hot set gives the same bytes: a hot stream's cursors are the
+// single-pass offsets, and level 2 sees every cold partition's records of a chunk in input
+// order.  The cut: a 256-bin histogram of the counts over [0, max], the highest bins holding
+// >= SPLIT_HOT_CAP partitions, then the first SPLIT_HOT_CAP of those in id order.
+// One workgroup; R <= 4 * 1024.
+constexpr int HS_THREADS = 1024, HS_PER = 4;
+__global__ __launch_bounds__(HS_THREADS) void k_hot_select(const uint32_t *__restrict__ part_off, int R, int Q,
+                                                           uint16_t *__restrict__ stream_of,
+                                                           int32_t *__restrict__ hot_part) {
+    __shared__ uint32_t s_w[HS_THREADS / 64];
+    __shared__ uint32_t s_hist[256];
+    __shared__ uint32_t s_max, s_bin;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t cnt[HS_PER], mx = 0;
+#pragma unroll
+    for (int i = 0; i < HS_PER; ++i) {
+        const int p = (int)tid * HS_PER + i;
+        cnt[i] = p < R ? part_off[p + 1] - part_off[p] : 0u;
+        mx = max(mx, cnt[i]);
+    }
+    if (tid < 256) s_hist[tid] = 0;
+    if (tid == 0) s_max = 0;
+    __syncthreads();
+    atomicMax(&s_max, mx);
+    __syncthreads();
+    const uint64_t span = (uint64_t)s_max + 1;
+#pragma unroll
+    for (int i = 0; i < HS_PER; ++i)
+        if ((int)tid * HS_PER + i < R && cnt[i]) atomicAdd(&s_hist[(uint32_t)((uint64_t)cnt[i] * 256 / span)], 1u);
+    __syncthreads();
+    if (tid == 0) {  // the lowest bin whose bins above hold >= SPLIT_HOT_CAP partitions
+        uint32_t b = 256, cum = 0;
+        while (b > 0 && cum < (uint32_t)SPLIT_HOT_CAP) cum += s_hist[--b];
+        s_bin = b;
+    }
+    __syncthreads();
+    const uint32_t bmin = s_bin;
+    uint32_t hot[HS_PER], c = 0;
+#pragma unroll
+    for (int i = 0; i < HS_PER; ++i) {
+        hot[i] = (cnt[i] > 0 && (uint32_t)((uint64_t)cnt[i] * 256 / span) >= bmin) ? 1u : 0u;
+        c += hot[i];
+    }
+    const uint32_t incl = wave_inclusive_scan(c, lane);
+    if (lane == 63) s_w[w] = incl;
+    __syncthreads();
+    uint32_t base = incl - c, total = 0;
+    for (uint32_t v = 0; v < HS_THREADS / 64; ++v) {
+        if (v < w) base += s_w[v];
+        total += s_w[v];
+    }
+#pragma unroll
+    for (int i = 0; i < HS_PER; ++i) {
+        const int p = (int)tid * HS_PER + i;
+        if (p >= R) break;
+        if (hot[i] && base < (uint32_t)SPLIT_HOT_CAP) {
+            stream_of[p] = (uint16_t)base;
+            hot_part[base] = p;
+        } else {
+            stream_of[p] = (uint16_t)(SPLIT_HOT_CAP + p / Q);
+        }
+        base += hot[i];
+    }
+    if (tid < (uint32_t)SPLIT_HOT_CAP && tid >= total) hot_part[tid] = -1;
+}
+
+hipError_t launch_hot_select(const uint32_t *part_off, int R, int Q, uint16_t *stream_of, int32_t *hot_part,
+                             hipStream_t stream) {
+    if (R > HS_THREADS * HS_PER) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_hot_select, dim3(1), dim3(HS_THREADS), 0, stream, part_off, R, Q, stream_of, hot_part);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_super_counts_cold(const uint32_t *__restrict__ counts,
+                                                           const uint16_t *__restrict__ stream_of,
+                                                           uint32_t *__restrict__ csum, int S, int Q, int G) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)S * G) return;
+    const int64_t sidx = i / G, g = i - sidx * G;
+    uint32_t acc = 0;
+    for (int q = 0; q < Q; ++q)
+        if (stream_of[sidx * Q + q] >= SPLIT_HOT_CAP) acc += counts[(sidx * Q + q) * G + g];
+    csum[i] = acc;
+}
+
+hipError_t launch_super_counts_cold(const uint32_t *counts, const uint16_t *stream_of, uint32_t *csum, int S, int Q,
+                                    int G, hipStream_t stream) {
+    const int64_t n = (int64_t)S * G;
+    hipLaunchKernelGGL(k_super_counts_cold, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, counts,
+                       stream_of, csum, S, Q, G);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_hot_cursors(const uint32_t *__restrict__ offs,
+                                                     const int32_t *__restrict__ hot_part,
+                                                     const uint32_t *__restrict__ offs1, uint32_t *__restrict__ cur1,
+                                                     int S, int G) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)(SPLIT_HOT_CAP + S) * G) return;
+    const int64_t st = i / G, g = i - st * G;
+    if (st < SPLIT_HOT_CAP) {
+        const int32_t p = hot_part[st];
+        cur1[i] = p >= 0 ? offs[(int64_t)p * G + g] : 0u;
+    } else {
+        cur1[i] = offs1[(st - SPLIT_HOT_CAP) * G + g];
+    }
+}
+
+hipError_t launch_hot_cursors(const uint32_t *offs, const int32_t *hot_part, const uint32_t *offs1, uint32_t *cur1,
+                              int S, int G, hipStream_t stream) {
+    const int64_t n = (int64_t)(SPLIT_HOT_CAP + S) * G;
+    hipLaunchKernelGGL(k_hot_cursors, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, offs, hot_part, offs1,
+                       cur1, S, G);
+    return hipGetLastError();
+}
+
 hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
-                                int G, const int64_t *desc, const uint32_t *ndesc, int grid, const ScatterGeom &geo,
-                                uint32_t *err, hipStream_t stream, const uint32_t *gate, uint32_t gate_want) {
+                                int G, const int64_t *desc, const uint32_t *ndesc, const uint32_t *seg_end, int grid,
+                                const ScatterGeom &geo, uint32_t *err, hipStream_t stream, const uint32_t *gate,
+                                uint32_t gate_want) {
     if ((pp.R & (pp.R - 1)) != 0) return hipErrorInvalidValue;
 #define SGX_WCS(W, NI, SI)                                                                                   \
     do {                                                                                                     \
@@ -1775,7 +1928,7 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes);           \
         hipLaunchKernelGGL((k_scatter16_wc<KIND_HASH_POW2, W, NI, SI, true>), dim3(grid), dim3(W * 64),      \
                            geo.lds_bytes, stream, (const u32x4 *)in, (u32x4 *)out, n, (int64_t)0, pp, offs, G, \
-                           err, desc, ndesc, gate, gate_want);                                               \
+                           err, desc, ndesc, gate, gate_want, nullptr, 0u, seg_end);                         \
     } while (0)
     const int W = geo.waves - WC_GEOM_BASE;
     if (W == 8 && geo.mbits == 16 && geo.items == 12) SGX_WCS(8, 12, 16);
@@ -2047,11 +2200,12 @@ hipError_t launch_lds_order_probe(uint32_t *bad, hipStream_t stream) {
 
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t chunk, int G,
                           const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
-                          uint32_t *err, hipStream_t stream, const uint32_t *gate, uint32_t gate_want) {
+                          uint32_t *err, hipStream_t stream, const uint32_t *gate, uint32_t gate_want,
+                          void *out2, uint32_t hot_cap) {
     const bool pow2 = (pp.R & (pp.R - 1)) == 0;
     if (rb == 16 && geo.waves >= WC_GEOM_BASE) {
         if ((pp.kind != SGX_PART_HASH && pp.kind != KIND_DIGIT && pp.kind != KIND_HASH_BITS &&
-             pp.kind != KIND_KEY_BITS) ||
+             pp.kind != KIND_KEY_BITS && pp.kind != KIND_HOT_SPLIT) ||
             geo.waves < WC_GEOM_BASE)
             return hipErrorInvalidValue;
 #define SGX_WC_SI(K, W, NI, SI)                                                                  \
@@ -2060,7 +2214,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
         hipLaunchKernelGGL((k_scatter16_wc<K, W, NI, SI>), dim3(G), dim3(W * 64), geo.lds_bytes,  \
                            stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err,   \
-                           nullptr, nullptr, gate, gate_want);                                   \
+                           nullptr, nullptr, gate, gate_want, (u32x4 *)out2, hot_cap);           \
     } while (0)
         // geometries: 8 waves, NI 12 | 8, SI 16, one workgroup per CU
         const int W = geo.waves - WC_GEOM_BASE;
@@ -2079,6 +2233,9 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         } else if (pp.kind == KIND_HASH_BITS) {
             if (!pow2) return hipErrorInvalidValue;
             SGX_WC(KIND_HASH_BITS);
+        } else if (pp.kind == KIND_HOT_SPLIT) {
+            if (!pp.dir || !out2 || pp.dshift > 13) return hipErrorInvalidValue;
+            SGX_WC(KIND_HOT_SPLIT);
         } else if (pow2) {
             SGX_WC(KIND_HASH_POW2);
         } else {

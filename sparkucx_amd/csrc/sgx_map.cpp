@@ -57,23 +57,25 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
         if (geo.waves < WC_GEOM_BASE && geo.waves != WIDE2_GEOM_TAG)
             return fail_msg(SGX_ERR_UNSUPPORTED, "digit pass on %d B records at this alignment", rb);
     }
-    // R > 1024 (power of two, hash, 16 B): the two-level split -- two write-combining passes
-    // (S = R / 64 super-partitions, then Q = 64 inside each) instead of one pass whose runs
-    // leave L2 as partial lines (sgx_kernels.hip, "Two-level split scatter")
-    // (skewed maps take the single lane-ordered pass instead, chosen on the device: so the
-    // split needs that kernel's geometry too -- R <= 4096)
-    const ScatterGeom geo_ord = rb == 16 ? scatter_geom16_ord((uint32_t)R, 0, 0) : ScatterGeom{0, 0, 0, 0, 0};
-    const bool split = rb == 16 && kind == SGX_PART_HASH && R > 1024 && (R & (R - 1)) == 0 && R <= 65536 &&
-                       geo_ord.items > 0 && e->rank_mode == SGX_RANK_ORDERED && e->sc_waves == 0 &&
-                       e->sc_items == 0 && !(e->flags & (SGX_FLAG_NO_WRITE_COMBINING | SGX_FLAG_NO_SPLIT_SCATTER));
+    // R > 1024 (power of two, hash, 16 B): the hybrid two-level split -- level 1 writes the
+    // hot partitions straight to the output and the cold ones into S = R / 64
+    // super-partitions, level 2 splits each super into Q = 64; both write-combining, whole
+    // lines only, instead of one pass whose runs leave L2 as partial lines (sgx_kernels.hip,
+    // "Two-level split scatter", "Hybrid split")
+    const bool split = rb == 16 && kind == SGX_PART_HASH && R > 1024 && (R & (R - 1)) == 0 && R <= 4096 &&
+                       e->rank_mode == SGX_RANK_ORDERED && e->sc_waves == 0 && e->sc_items == 0 &&
+                       !(e->flags & (SGX_FLAG_NO_WRITE_COMBINING | SGX_FLAG_NO_SPLIT_SCATTER));
     constexpr int32_t Q = 64;
     const int32_t S = split ? R / Q : 0;
     ScatterGeom geo1{}, geo2{};
     if (split) {
-        geo1 = scatter_geom16_wc((uint32_t)S);
+        geo1 = scatter_geom16_wc((uint32_t)(SPLIT_HOT_CAP + S));
         geo2 = scatter_geom16_wc((uint32_t)Q);
-        if (geo1.items == 0 || geo2.items == 0)
+        geo1.lds_bytes += ((size_t)R * 2 + 15) & ~(size_t)15;  // the partition -> stream table
+        if (geo1.items == 0 || geo2.items == 0 || geo1.lds_bytes > 160 * 1024)
             return fail_msg(SGX_ERR_UNSUPPORTED, "split scatter geometry for R=%d", R);
+        geo1.items = 8;  // 12 new records per lane spill registers in this kernel; 8 do not
+        geo1.tile = 8 * 512;
         geo = geo1;
     }
     if (geo.items == 0)
@@ -109,13 +111,18 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     uint64_t *status2 = (uint64_t *)((char *)ticket2 + 16);
     c.last_off_dev = part_off_dev;
     // the split's scratch: [csum u32 x S*G][offs1 u32 x S*G][flags u32 x S*G][idx u32 x S*G]
-    // [part_off1 u32 x (S+2) | npieces u32 x 4][desc i64 x 4*S*G], and the level-1 output
+    // [part_off1 u32 x (S+2) | npieces u32 x 4][desc i64 x 4*S*G][cur1 u32 x (HOT+S)*G]
+    // [stream_of u16 x R][hot_part i32 x HOT], and the level-1 output of the cold partitions
     uint32_t *csum = nullptr, *offs1 = nullptr, *part_off1 = nullptr, *npieces = nullptr, *pflags = nullptr,
-             *pidx = nullptr;
+             *pidx = nullptr, *cur1 = nullptr;
     int64_t *desc = nullptr;
+    uint16_t *stream_of = nullptr;
+    int32_t *hot_part = nullptr;
     if (split) {
         const size_t a = ((size_t)len1 * 4 + 15) & ~(size_t)15, b = ((size_t)(S + 6) * 4 + 15) & ~(size_t)15;
-        SGX_TRY(c.split_work.ensure(4 * a + b + (size_t)len1 * 32));
+        const size_t cb = ((size_t)(SPLIT_HOT_CAP + S) * G * 4 + 15) & ~(size_t)15;
+        const size_t tb = ((size_t)R * 2 + 15) & ~(size_t)15;
+        SGX_TRY(c.split_work.ensure(4 * a + b + (size_t)len1 * 32 + cb + tb + SPLIT_HOT_CAP * 4));
         csum = (uint32_t *)c.split_work.p;
         offs1 = (uint32_t *)((char *)c.split_work.p + a);
         pflags = (uint32_t *)((char *)c.split_work.p + 2 * a);
@@ -123,6 +130,9 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
         part_off1 = (uint32_t *)((char *)c.split_work.p + 4 * a);
         npieces = part_off1 + S + 2;
         desc = (int64_t *)((char *)c.split_work.p + 4 * a + b);
+        cur1 = (uint32_t *)((char *)desc + (size_t)len1 * 32);
+        stream_of = (uint16_t *)((char *)cur1 + cb);
+        hot_part = (int32_t *)((char *)stream_of + tb);
         SGX_TRY(c.split_tmp.ensure((size_t)std::max<int64_t>(n, 1) * 16));
     }
     HIP_TRY(hipMemsetAsync(c.work.p, 0, work_bytes, st));
@@ -140,37 +150,36 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     PartParams lpp = spp;
     lpp.mbits = (uint32_t)geo.mbits;
     if (split && n > 0) {
-        // per map, on the device: the split (gate 1) unless one partition holds > 1/50 of the
-        // records, where the single lane-ordered pass (gate 0) is faster
-        uint32_t *gate = npieces + 2;
-        HIP_TRY(launch_split_choice(part_off_dev, R, gate, st));
-        // level-1 cursors: a scan of the per-chunk super counts; level-2 pieces from them
-        HIP_TRY(launch_super_counts(counts, csum, S, Q, G, st));
+        // per map, on the device: the hot partitions (>= twice the mean count) and the
+        // partition -> stream table; level-1 cursors (a hot stream: its final offsets; a cold
+        // super: a scan of its cold partitions' per-chunk counts); level-2 pieces from those
+        HIP_TRY(launch_hot_select(part_off_dev, R, Q, stream_of, hot_part, st));
+        HIP_TRY(launch_super_counts_cold(counts, stream_of, csum, S, Q, G, st));
         HIP_TRY(launch_scan(csum, offs1, len1, status1, ticket1, err, part_off1, G, S, st));
+        HIP_TRY(launch_hot_cursors((const uint32_t *)c.offs.p, hot_part, offs1, cur1, S, G, st));
+        // level-2 pieces: cut from the cold records' count (on the device), about one per CU
         const int64_t pieces = std::max<int64_t>(1, (int64_t)e->num_cus - S);
-        const int64_t target = std::max<int64_t>(1, (n + pieces - 1) / pieces);
-        HIP_TRY(launch_seg_desc(offs1, S, G, n, target, desc, pflags, pidx, status2, ticket2, err, npieces, st));
+        HIP_TRY(launch_seg_desc(offs1, S, G, part_off1 + S, pieces, desc, pflags, pidx, status2, ticket2, err, npieces,
+                                st));
         SGX_TRY(debug_sync(e, st, "split scan / pieces"));
         HIP_TRY(hipEventRecord(c1, st));
         PartParams p1 = spp;
-        p1.kind = KIND_HASH_BITS;
-        p1.R = (uint32_t)S;
-        p1.dshift = 6;  // log2(Q)
+        p1.kind = KIND_HOT_SPLIT;
+        p1.R = (uint32_t)(SPLIT_HOT_CAP + S);
+        p1.dshift = (uint32_t)__builtin_ctz((unsigned)R);  // the full partition id's bits
+        p1.dir = stream_of;
         p1.mbits = (uint32_t)geo1.mbits;
-        HIP_TRY(launch_scatter(in, c.split_tmp.p, n, rb, chunk, G, p1, offs1, geo1, err, st, gate, 1u));
+        HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, p1, cur1, geo1, err, st, nullptr, 0u, c.split_tmp.p,
+                               (uint32_t)SPLIT_HOT_CAP));
         SGX_TRY(debug_sync(e, st, "K4 split level 1"));
         PartParams p2 = spp;
         p2.kind = KIND_HASH_POW2;
         p2.R = (uint32_t)Q;
         p2.mbits = (uint32_t)geo2.mbits;
-        const int grid = (int)(S + (n + target - 1) / target + 1);
-        HIP_TRY(launch_scatter16_seg(c.split_tmp.p, out, n, p2, (const uint32_t *)c.offs.p, G, desc, npieces + 1, grid,
-                                     geo2, err, st, gate, 1u));
+        const int grid = (int)(S + pieces + 1);  // >= the pieces: one per super + every cut
+        HIP_TRY(launch_scatter16_seg(c.split_tmp.p, out, n, p2, (const uint32_t *)c.offs.p, G, desc, npieces + 1,
+                                     part_off1 + S, grid, geo2, err, st));
         SGX_TRY(debug_sync(e, st, "K4 split level 2"));
-        PartParams po = spp;
-        po.mbits = (uint32_t)geo_ord.mbits;
-        HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, po, (const uint32_t *)c.offs.p, geo_ord, err, st, gate, 0u));
-        SGX_TRY(debug_sync(e, st, "K4 single pass (skewed map)"));
     } else {
         HIP_TRY(hipEventRecord(c1, st));
         if (n > 0) HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, lpp, (const uint32_t *)c.offs.p, geo, err, st));

@@ -200,14 +200,16 @@ def test_write_combining_carry_pressure(sgx_lib, oracle_lib, R, group):
 
 
 @pytest.mark.parametrize("R", [2048, 4096, 8192])
-@pytest.mark.parametrize("shape", ["uniform", "one_super", "hot_partition", "tiny", "empty"])
+@pytest.mark.parametrize("shape", ["uniform", "one_super", "hot_partition", "many_hot", "all_hot", "zipf", "tiny", "empty"])
 def test_two_level_split_scatter(sgx_lib, oracle_lib, R, shape):
     """The two-level split K4 (hash, power-of-two R > 1024: S = R/64 super-partitions written
     whole-line, then 64 sub-partitions inside each, over pieces of whole (super, chunk)
-    blocks): bit-exact against the oracle, and byte-identical to the single lane-ordered pass
+    blocks; the hybrid level 1 writes partitions with >= 2x the mean count straight to the
+    output): bit-exact against the oracle, and byte-identical to the single lane-ordered pass
     (SGX_FLAG_NO_SPLIT_SCATTER), for uniform keys, every key in ONE super-partition (one piece
-    per chunk, all other supers empty), one hot partition holding most records, a map smaller
-    than one tile, and an empty map; 1, 5 and the default number of chunks."""
+    per chunk, all other supers empty), one hot partition holding most records, more hot
+    partitions than the hybrid's 192 hot streams, every record hot (level 2 empty), Zipf(1.1),
+    a map smaller than one tile, and an empty map; 1, 5 and the default number of chunks."""
     n = {"tiny": 1000, "empty": 0}.get(shape, 400_003)
     recs = oracle_lib.gen_uniform16(max(n, 1), 0x5B1 + R)[:n]
     rng = np.random.default_rng(R)
@@ -217,6 +219,14 @@ def test_two_level_split_scatter(sgx_lib, oracle_lib, R, shape):
     elif shape == "hot_partition":
         pid = np.where(rng.random(n) < 0.8, 5, rng.integers(0, R, n))
         recs[:, :8] = (pid + R * rng.integers(0, 1 << 20, n)).astype(np.int64).view(np.uint8).reshape(-1, 8)
+    elif shape == "many_hot":  # the hybrid's hot streams: more qualifying partitions than SPLIT_HOT_CAP (192)
+        pid = np.where(rng.random(n) < 0.7, rng.integers(0, 300, n) * (R // 300), rng.integers(0, R, n))
+        recs[:, :8] = (pid + R * rng.integers(0, 1 << 20, n)).astype(np.int64).view(np.uint8).reshape(-1, 8)
+    elif shape == "all_hot":  # every record in a hot partition: level 2 gets no records
+        pid = rng.integers(0, 8, n) * 37 % R
+        recs[:, :8] = (pid + R * rng.integers(0, 1 << 20, n)).astype(np.int64).view(np.uint8).reshape(-1, 8)
+    elif shape == "zipf":
+        recs = oracle_lib.gen_zipf16(n, 0x5B1 + R, oracle_lib.zipf_cdf(1.1, 2**24))
     for chunks in (0, 1, 5):
         for flags in (0, sgx_lib.FLAG_NO_SPLIT_SCATTER):  # both bit-exact: byte-identical to each other
             with sgx_lib.ShuffleEngine(device=0, num_chunks=chunks, flags=flags) as e:
