@@ -109,7 +109,6 @@ hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint
                        hipStream_t stream);
 int64_t scan_tiles(int64_t len);
 // Two-level split scatter (hash partitioner, power-of-two R > 1024, 16 B records):
-// csum[s][g] = sum over the Q sub-partitions q of counts[(s*Q + q)][g]   (S*G entries);
 // desc: the level-2 pieces cut from the level-1 offsets (offs1[S][G], u32) -- each piece a
 // run of whole (super, chunk) blocks inside one super-partition, about `target` records --
 // as {begin, -, super, first chunk} int64 quadruples (a piece ends at the next one's begin;
@@ -118,18 +117,13 @@ int64_t scan_tiles(int64_t len);
 // work area of scan_tiles(S*G) tiles);
 // launch_scatter16_seg: level 2, write-combining K4 with R = Q over the pieces, cursors
 // offs[(super*Q + q)][chunk] of the single-level scan.
-hipError_t launch_super_counts(const uint32_t *counts, uint32_t *csum, int S, int Q, int G, hipStream_t stream);
 hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, const uint32_t *total, int64_t pieces, int64_t *desc,
                            uint32_t *flags, uint32_t *idx, uint64_t *status, uint32_t *ticket, uint32_t *err,
                            uint32_t *npieces, hipStream_t stream);
 // seg_end: device count of the level-1 records the pieces cover (the last piece's end)
 hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
                                 int G, const int64_t *desc, const uint32_t *ndesc, const uint32_t *seg_end, int grid,
-                                const ScatterGeom &geo, uint32_t *err, hipStream_t stream,
-                                const uint32_t *gate = nullptr, uint32_t gate_want = 0);
-// *gate = 1 when no partition holds more than 1/50 of the records (the split's kernels run),
-// 0 otherwise (the single lane-ordered pass runs): both are launched, gated on the flag.
-hipError_t launch_split_choice(const uint32_t *part_off, int R, uint32_t *gate, hipStream_t stream);
+                                const ScatterGeom &geo, uint32_t *err, hipStream_t stream);
 // Hybrid split: from the partition offsets, stream_of[p] = hot index for
 // about the SPLIT_HOT_CAP largest partitions (a coarse count histogram picks the cut; the hot
 // ones numbered in id order), else SPLIT_HOT_CAP + p / Q; hot_part[h] = the partition of hot
@@ -156,8 +150,7 @@ hipError_t launch_lds_order_probe(uint32_t *bad, hipStream_t stream);
 // out2 / hot_cap: KIND_HOT_SPLIT only -- streams >= hot_cap go to out2 (the split's scratch)
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes, int64_t chunk,
                           int G, const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
-                          uint32_t *err, hipStream_t stream, const uint32_t *gate = nullptr, uint32_t gate_want = 0,
-                          void *out2 = nullptr, uint32_t hot_cap = 0);
+                          uint32_t *err, hipStream_t stream, void *out2 = nullptr, uint32_t hot_cap = 0);
 // items: [n][3] int64 {src_off, dst_off, bytes}; all offsets/bytes multiples of `align`.
 // LZ4BlockOutputStream framing (sgx_lz4.hip)
 int lz4_lanes_per_workgroup();

@@ -963,10 +963,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_ord(const u32x4 *__
                                                                  u32x4 *__restrict__ out, int64_t n,
                                                                  int64_t chunk, PartParams pp,
                                                                  const uint32_t *__restrict__ offs,
-                                                                 int G, uint32_t *err,
-                                                                 const uint32_t *__restrict__ gate = nullptr,
-                                                                 uint32_t gate_want = 0) {
-    if (gate && *gate != gate_want) return;  // the other kernel choice of this map runs
+                                                                 int G, uint32_t *err) {
     constexpr int T = WAVES * 64;
     constexpr int TILE = WAVES * ITEMS * 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1113,8 +1110,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                                                                 int G, uint32_t *err,
                                                                 const int64_t *__restrict__ desc = nullptr,
                                                                 const uint32_t *__restrict__ ndesc = nullptr,
-                                                                const uint32_t *__restrict__ gate = nullptr,
-                                                                uint32_t gate_want = 0,
                                                                 u32x4 *__restrict__ out2 = nullptr,
                                                                 uint32_t hot_cap = 0,
                                                                 const uint32_t *__restrict__ seg_end = nullptr) {
@@ -1145,7 +1140,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     uint32_t *myrow32 = (uint32_t *)myrow;
     const uint32_t n32 = (uint32_t)n;  // n < 2^32 (sgx_write_map)
 
-    if (gate && *gate != gate_want) return;  // the other kernel choice of this map runs
     int g = blockIdx.x;
     int64_t begin = (int64_t)g * chunk, end = min(n, begin + chunk), obase = 0;
     if constexpr (SEG) {
@@ -1710,8 +1704,9 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 // per 4.3 GB of records (profiles/r02a_u4096_summary.md) -- and the write-combining kernel
 // cannot keep 4096 streams' incomplete lines on chip.  So the split runs two
 // write-combining passes of R <= 1024 each, both writing whole lines only:
-//   level 1: partition by the top log2(S) bits of the id (KIND_HASH_BITS, S super-partitions)
-//            into a scratch buffer, cursors from a scan of the per-chunk super counts;
+//   level 1: partition by the top log2(S) bits of the id (S super-partitions) into a scratch
+//            buffer, cursors from a scan of the per-chunk super counts -- the hybrid below
+//            (KIND_HOT_SPLIT) sends the largest partitions straight to the output instead;
 //   level 2: inside every super-partition, partition by the low log2(Q) bits (R = Q = 64),
 //            over pieces of whole (super, chunk) blocks: the level-1 output holds super s's
 //            records chunk after chunk in input order, so a piece starting at block (s, g)
@@ -1719,22 +1714,6 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 //            offs[(s*Q + q)][g] -- no second histogram, and the result is byte-identical to
 //            the single-pass scatter (both stable, same offsets).
 // ------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_super_counts(const uint32_t *__restrict__ counts, uint32_t *__restrict__ csum,
-                                                      int S, int Q, int G) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i >= (int64_t)S * G) return;
-    const int64_t sidx = i / G, g = i - sidx * G;
-    uint32_t acc = 0;
-    for (int q = 0; q < Q; ++q) acc += counts[(sidx * Q + q) * G + g];
-    csum[i] = acc;
-}
-
-hipError_t launch_super_counts(const uint32_t *counts, uint32_t *csum, int S, int Q, int G, hipStream_t stream) {
-    const int64_t n = (int64_t)S * G;
-    hipLaunchKernelGGL(k_super_counts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, counts, csum, S, Q, G);
-    return hipGetLastError();
-}
-
 // Level-2 pieces.  Block i = s*G + g (s-major, the level-1 layout) starts a piece when g == 0
 // or when it crosses a multiple of `target` records (k_seg_flags); an exclusive scan of the
 // flags (K3) numbers the pieces, and k_seg_desc writes piece k = {begin, -, super, chunk}.
@@ -1773,26 +1752,6 @@ hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, const uint32_t *
                        idx, nb, status, ticket, err, npieces, (int)nb, 1);
     hipLaunchKernelGGL(k_seg_desc, dim3(grid), dim3(256), 0, stream, offs1, (const uint32_t *)flags,
                        (const uint32_t *)idx, S, G, desc);
-    return hipGetLastError();
-}
-
-// The split is chosen per map, on the device (no host round trip): *gate = 1 (split) unless one
-// partition holds more than 1/50 of the records -- skewed keys (Zipf: the hottest of 4096
-// reducers holds ~11.5 %) whose hot sub-partition serialises the write-combining ranking
-// atomics -- where the single lane-ordered pass runs instead (measured).
-__global__ __launch_bounds__(256) void k_split_choice(const uint32_t *__restrict__ part_off, int R, uint32_t *gate) {
-    __shared__ uint32_t s_max;
-    if (threadIdx.x == 0) s_max = 0;
-    __syncthreads();
-    uint32_t mx = 0;
-    for (int p = (int)threadIdx.x; p < R; p += 256) mx = max(mx, part_off[p + 1] - part_off[p]);
-    atomicMax(&s_max, mx);
-    __syncthreads();
-    if (threadIdx.x == 0) *gate = (uint64_t)s_max * 50 <= (uint64_t)part_off[R] ? 1u : 0u;
-}
-
-hipError_t launch_split_choice(const uint32_t *part_off, int R, uint32_t *gate, hipStream_t stream) {
-    hipLaunchKernelGGL(k_split_choice, dim3(1), dim3(256), 0, stream, part_off, R, gate);
     return hipGetLastError();
 }
 
@@ -1919,8 +1878,7 @@ hipError_t launch_hot_cursors(const uint32_t *offs, const int32_t *hot_part, con
 
 hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
                                 int G, const int64_t *desc, const uint32_t *ndesc, const uint32_t *seg_end, int grid,
-                                const ScatterGeom &geo, uint32_t *err, hipStream_t stream, const uint32_t *gate,
-                                uint32_t gate_want) {
+                                const ScatterGeom &geo, uint32_t *err, hipStream_t stream) {
     if ((pp.R & (pp.R - 1)) != 0) return hipErrorInvalidValue;
 #define SGX_WCS(W, NI, SI)                                                                                   \
     do {                                                                                                     \
@@ -1928,7 +1886,7 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes);           \
         hipLaunchKernelGGL((k_scatter16_wc<KIND_HASH_POW2, W, NI, SI, true>), dim3(grid), dim3(W * 64),      \
                            geo.lds_bytes, stream, (const u32x4 *)in, (u32x4 *)out, n, (int64_t)0, pp, offs, G, \
-                           err, desc, ndesc, gate, gate_want, nullptr, 0u, seg_end);                         \
+                           err, desc, ndesc, nullptr, 0u, seg_end);                                         \
     } while (0)
     const int W = geo.waves - WC_GEOM_BASE;
     if (W == 8 && geo.mbits == 16 && geo.items == 12) SGX_WCS(8, 12, 16);
@@ -2200,8 +2158,7 @@ hipError_t launch_lds_order_probe(uint32_t *bad, hipStream_t stream) {
 
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t chunk, int G,
                           const PartParams &pp, const uint32_t *offs, const ScatterGeom &geo,
-                          uint32_t *err, hipStream_t stream, const uint32_t *gate, uint32_t gate_want,
-                          void *out2, uint32_t hot_cap) {
+                          uint32_t *err, hipStream_t stream, void *out2, uint32_t hot_cap) {
     const bool pow2 = (pp.R & (pp.R - 1)) == 0;
     if (rb == 16 && geo.waves >= WC_GEOM_BASE) {
         if ((pp.kind != SGX_PART_HASH && pp.kind != KIND_DIGIT && pp.kind != KIND_HASH_BITS &&
@@ -2214,7 +2171,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
         hipLaunchKernelGGL((k_scatter16_wc<K, W, NI, SI>), dim3(G), dim3(W * 64), geo.lds_bytes,  \
                            stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err,   \
-                           nullptr, nullptr, gate, gate_want, (u32x4 *)out2, hot_cap);           \
+                           nullptr, nullptr, (u32x4 *)out2, hot_cap);                            \
     } while (0)
         // geometries: 8 waves, NI 12 | 8, SI 16, one workgroup per CU
         const int W = geo.waves - WC_GEOM_BASE;
@@ -2252,8 +2209,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         (void)hipFuncSetAttribute((const void *)k_scatter16_ord<K, WV, I, P>,                   \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
         hipLaunchKernelGGL((k_scatter16_ord<K, WV, I, P>), dim3(G), dim3(WV * 64), geo.lds_bytes, \
-                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err,  \
-                           gate, gate_want);                                                     \
+                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err); \
     } while (0)
 #define SGX_ORD_K(K)                                                      \
     do {                                                                  \

@@ -150,7 +150,7 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     PartParams lpp = spp;
     lpp.mbits = (uint32_t)geo.mbits;
     if (split && n > 0) {
-        // per map, on the device: the hot partitions (>= twice the mean count) and the
+        // per map, on the device: the hot partitions (the SPLIT_HOT_CAP largest) and the
         // partition -> stream table; level-1 cursors (a hot stream: its final offsets; a cold
         // super: a scan of its cold partitions' per-chunk counts); level-2 pieces from those
         HIP_TRY(launch_hot_select(part_off_dev, R, Q, stream_of, hot_part, st));
@@ -169,7 +169,7 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
         p1.dshift = (uint32_t)__builtin_ctz((unsigned)R);  // the full partition id's bits
         p1.dir = stream_of;
         p1.mbits = (uint32_t)geo1.mbits;
-        HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, p1, cur1, geo1, err, st, nullptr, 0u, c.split_tmp.p,
+        HIP_TRY(launch_scatter(in, out, n, rb, chunk, G, p1, cur1, geo1, err, st, c.split_tmp.p,
                                (uint32_t)SPLIT_HOT_CAP));
         SGX_TRY(debug_sync(e, st, "K4 split level 1"));
         PartParams p2 = spp;

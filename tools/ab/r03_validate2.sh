@@ -17,4 +17,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/
   python3 bench.py --steps 10 --no-cpu-baseline > "$out/bench_kt.log" 2>&1
 bash tools/gpu_prof.sh $tag/prof_c1
 bash tools/gpu_prof.sh $tag/prof_ts --record-bytes 100 --records 42949672
+bash tools/gpu_prof.sh $tag/prof_c3 --partitions 4096 --dist zipf
 echo done > "$out/DONE"
