@@ -1037,23 +1037,33 @@ ScatterGeom scatter_geom16_ord(uint32_t R, int force_waves, int force_items) {
 // kernels above run at 2.9 ms, i.e. AT the unaligned floor.
 //
 // How: each (partition, chunk) output stream keeps its incomplete last line ON CHIP.
-// Per tile, partition p's stage segment is [deferred records of p][new records of p],
-// covering output positions [a_p, e_p) with a_p = c_p - dl_p (c_p = cursor of the first
-// new record, dl_p <= 7 deferred records).  The drain writes positions [a_p, LE_p) with
-// LE_p = max(e_p & ~7, a_p): every line it writes is complete (only a stream's first line
-// can be partial: its head belongs to the previous stream).  Records at [LE_p, e_p) stay
-// in the REGISTERS of the lane that drained them (slot k of the lane's SI drain items,
-// with their output position) and are staged again, ahead of the next tile's new records.
-// The chunk's last tile flushes everything; so does a tile whose deferred records would
-// not fit next to a full tile (sum dl > DCAP: rare, R <= 585 never), which only costs a
-// few partial lines.  The output is byte-identical to every other K4: positions come from
-// the same counts and the same stable ranks.
+// Per tile, partition p's records cover output positions [a_p, e_p): the ones it kept from
+// the previous tile, [a_p, c_p) (<= 7), then its new ones.  The drain writes positions
+// [a_p, LE_p) with LE_p = max(e_p & ~7, a_p): every line it writes is complete (only a
+// stream's first line can be partial: its head belongs to the previous stream).  Records at
+// [LE_p, e_p) stay in the REGISTERS of the lane that drained them (slot k of the lane's SI
+// drain items, with their output position) and are staged again next tile.  The chunk's
+// last tile flushes everything; so does a tile whose kept records would not fit next to a
+// full tile (sum > DCAP: rare, R <= 585 never), which only costs a few partial lines.  The
+// output is byte-identical to every other K4: positions come from the same counts and the
+// same stable ranks.
 //
-// Tile: NI new records per lane (TNEW = T*NI) + up to DCAP = T*SI - TNEW deferred ones.
-// LDS: stage[T*SI] 16 B | rows[W][RS] u16 | cur[RS] u32 | dlt[RS] u32 | lim[RS] u32
-// (RS = R rounded up to 8); a stream's deferred count is cur - lim (no array of its own:
-// the 2 KB it saved at R = 1024 let a histogram workgroup share the CU, 156 + 4 KB).  The merge's block-scan scratch borrows the stage
-// (free between B1 and B3: every wave has drained the previous tile before B1).
+// Stage layout (round 3): the records the tile keeps, all streams' [LE_p, e_p) back to
+// back, then the ones it writes, all streams' [a_p, LE_p) back to back -- so the drain's
+// first ~3.5 R slots need no store instruction and the rest are stores with every lane
+// active, most of them in the late group that issues during the next tile's ranking.
+// (Each stream's [a_p, e_p) in one segment left every drain round with both kinds: 16
+// store instructions per lane per tile, about half the lanes masked.  C1 K4 1.96 -> 1.85
+// ms, bench 1612 -> 1674 GB/s; writes-first measured between the two, and slower at
+// R = 4096: profiles/r03_wc_compact_ab.jsonl.)  A record at position x has s0 = x - dw_p:
+// it goes to slot s0 if s0 < wend_p (x < LE_p), else to s0 + shift_p in the kept region;
+// the drain inverts that per slot.
+//
+// Tile: NI new records per lane (TNEW = T*NI) + up to DCAP = T*SI - TNEW kept ones.
+// LDS: stage[T*SI] 16 B | rows[W][RS] u16 | e[RS] u32 | LE[RS] u32 | {dw, wend | shift << 16}[RS]
+// (RS = R rounded up to 8; 160 KB at R = 1024); a stream's kept count is e - LE.  The merge's
+// block-scan scratch borrows the stage (free between B1 and B3: every wave has drained the
+// previous tile before B1).
 // ------------------------------------------------------------------------------------
 #ifdef SGX_WC_STAMPS
 // Diagnostic build only (tools/build_variant.sh <tag> - -DSGX_WC_STAMPS, tools/wc_stamps.py):
@@ -1096,7 +1106,7 @@ extern "C" int sgx_diag_wc_stamps(unsigned long long *out16, int reset) {
 #endif
 
 __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
-    return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 12;  // cur 4 + dlim 8
+    return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 16;  // e, LE, {dw, dt}
 }
 
 // SEG (level 2 of the two-level split, launch_scatter16_seg): the workgroup's records are
@@ -1117,7 +1127,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     constexpr int TNEW = T * NI;
     constexpr int STAGE = T * SI;
     constexpr uint32_t DCAP = (uint32_t)(STAGE - TNEW);
-    static_assert(SI > NI && SI <= 32 && SI % 8 == 0, "deferred slots: 32-bit mask, drained 8 at a time");
+    static_assert(SI > NI && SI <= 32 && SI % 8 == 0, "kept slots: 32-bit mask, drained 8 at a time");
     // drain slots [LATE_K, SI) store during the next tile's ranking (SGX_WC_LATE groups of 8,
     // never the only group)
     constexpr int LATE_K = SI - 8 * (SGX_WC_LATE < SI / 8 - 1 ? SGX_WC_LATE : SI / 8 - 1);
@@ -1126,11 +1136,15 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     u32x4 *stage = (u32x4 *)smem;
     uint16_t *rows = (uint16_t *)(smem + (size_t)STAGE * 16);
-    uint32_t *cur = (uint32_t *)(rows + (size_t)WAVES * RS);
-    uint2 *dlim = (uint2 *)(cur + RS);          // {dlt_p, lim_p}: one ds_read_b64 per drained slot
+    // per stream p: pe = end of its records so far, ple = LE (written up to), pdw = {dw, wend |
+    // shift << 16}: a record at position x has s0 = x - dw; it is written from slot s0 if
+    // s0 < wend (x < LE), else kept in slot s0 + shift (shift: signed 16 bits)
+    uint32_t *pe = (uint32_t *)(rows + (size_t)WAVES * RS);
+    uint32_t *ple = pe + RS;
+    uint2 *pdw = (uint2 *)(ple + RS);
     uint32_t *scratch = (uint32_t *)smem;  // merge only (B1..B3)
-    // KIND_HOT_SPLIT: the map's partition -> stream table, staged after dlim
-    uint16_t *tbl = (uint16_t *)(dlim + RS);
+    // KIND_HOT_SPLIT: the map's partition -> stream table, staged after pdw
+    uint16_t *tbl = (uint16_t *)(pdw + RS);
     // a record's stream: the partition id, or (hybrid split) its partition's stream
     auto pidf = [&](const u32x4 &r) __attribute__((always_inline)) -> uint32_t {
         if constexpr (KIND == KIND_HOT_SPLIT) return tbl[(r.x ^ r.y) & ((1u << pp.dshift) - 1u)];
@@ -1155,8 +1169,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     const int64_t ntiles = (len + TNEW - 1) / TNEW;
     for (uint32_t p = tid; p < RS; p += T) {
         const uint32_t c0 = p < R ? offs[(obase + p) * G + g] : 0u;
-        cur[p] = c0;
-        dlim[p] = make_uint2(0u, c0);  // lim = cur: nothing deferred
+        pe[p] = c0;
+        ple[p] = c0;  // nothing kept
     }
     for (uint32_t i = tid; i < (uint32_t)WAVES * RS / 2; i += T) ((uint32_t *)rows)[i] = 0u;
     if constexpr (KIND == KIND_HOT_SPLIT)
@@ -1167,7 +1181,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     bool valid[NI];
     u32x4 dk[SI];
     uint32_t dpos[SI];
-    uint32_t dmask = 0;
+    uint32_t dmask = 0;  // drained records this lane keeps for the next tile
     uint32_t wmask = 0;  // drained records whose store waits for the next tile's rank (SGX_WC_LATE)
 #pragma unroll
     for (int k = 0; k < SI; ++k) { dk[k] = u32x4{0, 0, 0, 0}; dpos[k] = 0; }
@@ -1184,10 +1198,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     uint64_t st_last = wc_stamp();
 #endif
     uint32_t bad = 0;
-    // ---- drain: whole lines out, the rest stays in this lane's registers (dk/dpos).
+    // ---- drain: the stage's kept region [0, nkeep) into this lane's registers (dk/dpos), the
+    //      written region [nkeep, ntot) out as whole lines.
     //      (Draining tile t after tile t+1's ranking, so the wait for t+1's loads does not
     //      also wait for t's stores, measured slightly slower: 1.90-1.97 vs 1.86-1.95 ms.)
-    auto drain = [&](const uint32_t ntot) __attribute__((always_inline)) {
+    auto drain = [&](const uint32_t ntot, const uint32_t nkeep) __attribute__((always_inline)) {
         dmask = 0;
 #pragma unroll
         for (int k0 = 0; k0 < SI; k0 += 8) {
@@ -1196,20 +1211,23 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const uint32_t s = (uint32_t)((k0 + q) * T + tid);
-                dk[k0 + q] = stage[s];  // slots past `total` hold stale records: never used
+                dk[k0 + q] = stage[s];  // slots past `ntot` hold stale records: never used
             }
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 pq[q] = pidf(dk[k0 + q]);
-                dm[q] = dlim[pq[q]];
+                dm[q] = pdw[pq[q]];
             }
-            WC_STAMP(9);  // drain: stage + dlim reads
+            WC_STAMP(9);  // drain: stage + dw reads
 #pragma unroll
             for (int q = 0; q < 8; ++q) {
                 const uint32_t s = (uint32_t)((k0 + q) * T + tid);
                 const bool live = s < ntot;
-                const uint32_t pos = dm[q].x + s;
-                const bool wr = live && pos < dm[q].y;
+                const bool keep = s < nkeep;
+                const uint32_t pos = s + dm[q].x - (keep ? (uint32_t)((int32_t)dm[q].y >> 16) : 0u);
+                // every written position is below n by construction; a corrupt count (flagged
+                // in the merge) drops the record here instead of storing outside the output
+                const bool wr = live && !keep && pos < n32;
                 dpos[k0 + q] = pos;
                 // nontemporal: the map output is read back much later (exchange / fetch);
                 // streaming it past the caches keeps the input's lines in the Infinity
@@ -1224,7 +1242,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 }
                 if (k0 >= LATE_K) wmask |= wr ? 1u << (k0 + q) : 0u;
                 else if (wr) __builtin_nontemporal_store(dk[k0 + q], (u32x4 *)ob + pos);
-                dmask |= (live && !wr) ? 1u << (k0 + q) : 0u;
+                dmask |= (live && keep) ? 1u << (k0 + q) : 0u;
             }
             WC_STAMP(10);  // drain: global stores issued
         }
@@ -1266,11 +1284,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         lds_barrier();  // B1
         WC_STAMP(1);  // rank
 
-        // ---- merge: per partition pair (one pair per thread), both u16 halves at once
+        // ---- merge: per partition pair (one pair per thread).  Stream p's records this tile
+        //      cover positions [a, e): a = LE of the last tile (its kept records, dl = c - a of
+        //      them, then the new ones from c on); it writes [a, LE) and keeps [LE, e),
+        //      LE = max(e & ~7, a) -- everything when the tile flushes.
         const uint32_t j = tid;
-        uint32_t before[WAVES], tot = 0, dlp = 0, seg = 0, dnf_lo = 0, dnf_hi = 0;
-        uint2 c = make_uint2(0, 0);
-        uint32_t S = 0, D = 0;
+        uint32_t before[WAVES], tot = 0, S = 0, D = 0;
+        uint2 c = make_uint2(0, 0), a = make_uint2(0, 0), e = make_uint2(0, 0), kf = make_uint2(0, 0);
         if (j < NP) {
 #pragma unroll
             for (int v = 0; v < WAVES; ++v) {
@@ -1278,66 +1298,84 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 before[v] = tot;
                 tot += x;  // <= TNEW per half: no carry between halves
             }
-            c = ((const uint2 *)cur)[j];
-            const u32x4 pl = ((const u32x4 *)dlim)[j];  // previous tile's limits
-            dlp = ((c.x - pl.y) & 0xFFFFu) | ((c.y - pl.w) << 16);
-            seg = tot + dlp;
-            const uint32_t e0 = c.x + (tot & 0xFFFFu), e1 = c.y + (tot >> 16);
-            const uint32_t a0 = c.x - (dlp & 0xFFFFu), a1 = c.y - (dlp >> 16);
-            dnf_lo = e0 - max(e0 & ~7u, a0);
-            dnf_hi = e1 - max(e1 & ~7u, a1);
-            S = (seg & 0xFFFFu) + (seg >> 16);
-            D = dnf_lo + dnf_hi;
+            c = ((const uint2 *)pe)[j];
+            a = ((const uint2 *)ple)[j];
+            e = make_uint2(c.x + (tot & 0xFFFFu), c.y + (tot >> 16));
+            kf = make_uint2(e.x - max(e.x & ~7u, a.x), e.y - max(e.y & ~7u, a.y));  // kept if no flush
+            S = (e.x - a.x) + (e.y - a.y);
+            D = kf.x + kf.y;
         }
-        const uint32_t xs = wave_inclusive_scan(S | (D << 16), lane);  // S <= STAGE, D <= 7R
+        const uint32_t sd = S | (D << 16);  // S <= STAGE, D <= 7R
+        const uint32_t xs = wave_inclusive_scan(sd, lane);
         if (lane == 63) scratch[w] = xs;
         lds_barrier();  // B2
-        uint32_t base = (xs - (S | (D << 16))) & 0xFFFFu, total = 0, dsum = 0;
+        uint32_t base = (xs - sd) & 0xFFFFu, based = (xs - sd) >> 16, total = 0, dsum = 0;
 #pragma unroll
         for (int v = 0; v < WAVES; ++v) {
             const uint32_t y = scratch[v];
-            if (v < (int)w) base += y & 0xFFFFu;
+            if (v < (int)w) {
+                base += y & 0xFFFFu;
+                based += y >> 16;
+            }
             total += y & 0xFFFFu;
             dsum += y >> 16;
         }
         const bool flush = last || dsum > DCAP;
+        const uint32_t nkeep = flush ? 0u : dsum;
         if (j < NP) {
-            const uint32_t ls0 = base, ls1 = base + (seg & 0xFFFFu);
-            const uint32_t t0 = tot & 0xFFFFu, t1 = tot >> 16;
-            const uint32_t dl0 = dlp & 0xFFFFu, dl1 = dlp >> 16;
-            const uint32_t L = (ls0 + dl0) | ((ls1 + dl1) << 16);  // new records start after the deferred
+            if (flush) kf = make_uint2(0, 0), based = 0;
+            // stream 2j: written slots from wb0, kept slots from kb0; stream 2j+1 follows it
+            const uint32_t seg0 = e.x - a.x;
+            const uint32_t wb0 = nkeep + base - based, kb0 = based;
+            const uint32_t wb1 = wb0 + seg0 - kf.x, kb1 = kb0 + kf.x;
+            const uint32_t le0 = e.x - kf.x, le1 = e.y - kf.y;
+            const uint32_t dw0 = a.x - wb0, dw1 = a.y - wb1;
+            // a kept record's slot: kb + (x - LE) = (x - dw) + shift, shift = kb - wb - (LE - a)
+            const uint32_t sh0 = kb0 - wb0 - (le0 - a.x), sh1 = kb1 - wb1 - (le1 - a.y);
+            const uint32_t we0 = wb0 + (le0 - a.x), we1 = wb1 + (le1 - a.y);
+            // new records start after the kept ones in the written region (their slot is
+            // corrected into the kept region in the stage phase when past LE)
+            const uint32_t L = (wb0 + (c.x - a.x)) | ((wb1 + (c.y - a.y)) << 16);
 #pragma unroll
             for (int v = 0; v < WAVES; ++v) ((uint32_t *)(rows + (size_t)v * RS))[j] = before[v] + L;
-            const uint32_t e0 = c.x + t0, e1 = c.y + t1;
-            const uint32_t a0 = c.x - dl0, a1 = c.y - dl1;
-            const uint32_t le0 = flush ? e0 : e0 - dnf_lo, le1 = flush ? e1 : e1 - dnf_hi;
-            // every position this tile writes is below lim <= e <= n by construction; a
-            // corrupt count is reported and clamped here, never per record
-            bad |= (e0 > n32 || e1 > n32) ? 1u : 0u;
-            ((u32x4 *)dlim)[j] = u32x4{a0 - ls0, min(le0, n32), a1 - ls1, min(le1, n32)};
-            ((uint2 *)cur)[j] = make_uint2(e0, e1);
+            // every position this tile writes is below e <= n by construction; a corrupt count
+            // is reported here and its records are dropped at the store (pos < n)
+            bad |= (e.x > n32 || e.y > n32) ? 1u : 0u;
+            ((uint2 *)pe)[j] = e;
+            ((uint2 *)ple)[j] = make_uint2(le0, le1);
+            ((u32x4 *)pdw)[j] = u32x4{dw0, we0 | (sh0 << 16), dw1, we1 | (sh1 << 16)};
         }
         lds_barrier();  // B3
         WC_STAMP(2);  // merge
 
-        // ---- stage: deferred records first (their slots follow from their positions), then
-        //      the new ones.  LDS reads of a phase are issued together, one wait each.
+        // ---- stage: a record at position x of stream p goes to s0 = x - dw if x < LE (a
+        //      written slot), else to s0 + shift (a kept slot).  LDS reads of a phase are
+        //      issued together, one wait each (kept records in groups of 8: registers).
+        auto slot_of = [](uint32_t s0, uint32_t ws) __attribute__((always_inline)) -> uint32_t {
+            return s0 < (ws & 0xFFFFu) ? s0 : s0 + (uint32_t)((int32_t)ws >> 16);
+        };
+#pragma unroll
+        for (int k0 = 0; k0 < SI; k0 += 8) {
+            uint2 kd[8];
+#pragma unroll
+            for (int q = 0; q < 8; ++q) kd[q] = pdw[pidf(dk[k0 + q])];
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+                if ((dmask >> (k0 + q)) & 1u) stage[slot_of(dpos[k0 + q] - kd[q].x, kd[q].y)] = dk[k0 + q];
+        }
+        WC_STAMP(7);  // stage: kept-record reads + writes
         {
-            uint32_t dd[SI];
+            uint32_t rb[NI], nw[NI];
 #pragma unroll
-            for (int k = 0; k < SI; ++k) dd[k] = dlim[pidf(dk[k])].x;
-            uint32_t rb[NI];
-#pragma unroll
-            for (int k = 0; k < NI; ++k) rb[k] = myrow[pid[k]];
-            WC_STAMP(6);  // stage: dlt + row reads
-#pragma unroll
-            for (int k = 0; k < SI; ++k)
-                if ((dmask >> k) & 1u) stage[dpos[k] - dd[k]] = dk[k];
-            WC_STAMP(7);  // stage: deferred writes
+            for (int k = 0; k < NI; ++k) {
+                rb[k] = myrow[pid[k]];
+                nw[k] = ((const uint32_t *)pdw)[2 * pid[k] + 1];
+            }
+            WC_STAMP(6);  // stage: row + slot-map reads
 #pragma unroll
             for (int k = 0; k < NI; ++k) {
                 const uint32_t sh = (pid[k] & 1u) << 4;
-                if (valid[k]) stage[rb[k] + ((old[k] >> sh) & 0xFFFFu)] = rec[k];
+                if (valid[k]) stage[slot_of(rb[k] + ((old[k] >> sh) & 0xFFFFu), nw[k])] = rec[k];
             }
             WC_STAMP(8);  // stage: new writes
         }
@@ -1355,7 +1393,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         }
         lds_barrier();  // B4
         WC_STAMP(3);  // stage: zero rows, next loads, B4
-        drain(total);
+        drain(total, nkeep);
     }
     late_stores();
 #ifdef SGX_WC_STAMPS

@@ -52,6 +52,15 @@ __device__ __forceinline__ uint32_t g32(const uint8_t *p) {
     __builtin_memcpy(&v, p, 4);
     return v;
 }
+// The compressor's view of its block: bytes [0, n) read as one unaligned little-endian dword
+// (u32) or one byte (u8) through L1.  (Staging the whole block in LDS first -- 48 KiB per
+// block with the table, 3 blocks per CU instead of 10 -- measured 1.7x slower on C1's Kryo
+// stream: DESIGN §14.)
+struct GlobalSrc {
+    const uint8_t *p;
+    __device__ __forceinline__ uint32_t u32(int i) const { return g32(p + i); }
+    __device__ __forceinline__ uint32_t u8(int i) const { return p[i]; }
+};
 __device__ __forceinline__ uint32_t hash4(uint32_t seq) { return (seq * 2654435761u) >> (32 - kHashLog); }
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
 
@@ -144,7 +153,8 @@ __device__ __forceinline__ int lane_value(int v, int l) { return __builtin_amdgc
 // access and every decision stays in the serial order.
 // LZ4_count's end: the first a' >= a with src[a'] != src[a' + d0], or mlimit.  (d, full) is
 // the first round's comparison at a + 4 * lane, issued by the caller.
-__device__ __forceinline__ int lz4_count_end(const uint8_t *src, int a, int d0, int mlimit, uint32_t d, bool full) {
+template <typename Src>
+__device__ __forceinline__ int lz4_count_end(const Src &src, int a, int d0, int mlimit, uint32_t d, bool full) {
     const int lane = (int)(threadIdx.x & 63);
     for (;;) {
         const uint64_t dm = __ballot(d != 0);
@@ -155,30 +165,32 @@ __device__ __forceinline__ int lz4_count_end(const uint8_t *src, int a, int d0, 
         const int nfull = __popcll(__ballot(full));
         a += 4 * nfull;
         if (nfull < 64) {  // < 4 bytes before matchlimit: byte-wise
-            while (a < mlimit && src[a] == src[a + d0]) ++a;
+            while (a < mlimit && src.u8(a) == src.u8(a + d0)) ++a;
             return a;
         }
         const int al = a + 4 * lane;
         full = al + 4 <= mlimit;
-        d = full ? g32(src + al) ^ g32(src + al + d0) : 0u;
+        d = full ? src.u32(al) ^ src.u32(al + d0) : 0u;
     }
 }
 
 // The search's first batch of sequences from `start` (iteration lane); loaded ahead of the
 // table work that precedes the search, which they do not depend on.
-__device__ __forceinline__ uint32_t search_seq(const uint8_t *src, int start, int it, int n) {
+template <typename Src>
+__device__ __forceinline__ uint32_t search_seq(const Src &src, int start, int it, int n) {
     const int lane = (int)(threadIdx.x & 63);
-    return g32(src + min(start + skip_dist(it + lane), n - 4));  // (invalid lanes: any bytes)
+    return src.u32(min(start + skip_dist(it + lane), n - 4));  // (invalid lanes: any bytes)
 }
 
-__device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uint8_t *out, int cap) {
+template <typename Src>
+__device__ __forceinline__ int lz4_compress_wave(const Src &src, int n, uint16_t *table, uint8_t *out, int cap) {
     const int lane = (int)(threadIdx.x & 63);
     const uint64_t below = (1ull << lane) - 1ull;
     int anchor = 0, op = 0;
     if (n >= kMfLimit + 1) {
         const int lim = n - kMfLimit + 1;      // mflimit_plus_one
         const int mlimit = n - kLastLiterals;  // matchlimit
-        if (lane == 0) table[hash4(g32(src))] = 0;
+        if (lane == 0) table[hash4(src.u32(0))] = 0;
         int ip = 1;
         uint32_t seq0 = search_seq(src, ip, 0, n);
         for (;;) {
@@ -211,7 +223,7 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
                 const uint64_t lower = peers & below;
                 if (lower) cand = start + skip_dist(it + 63 - (int)__builtin_clzll(lower));
                 // (a valid lane's candidate is in the block: a lower peer of a valid lane is valid)
-                const bool hit = g32(src + min(cand, n - 4)) == seq && valid;
+                const bool hit = src.u32(min(cand, n - 4)) == seq && valid;
                 const uint64_t vm = __ballot(valid), hm = __ballot(hit);
                 const int kinv = first_clear(vm);
                 const int khit = hm ? (int)__builtin_ctzll(hm) : 64;
@@ -239,10 +251,10 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
                 const int d0 = match - ip, a0 = ip + kMinMatch;
                 const int al = a0 + 4 * lane;
                 const bool full = al + 4 <= mlimit;
-                const uint32_t d = full ? g32(src + al) ^ g32(src + al + d0) : 0u;
+                const uint32_t d = full ? src.u32(al) ^ src.u32(al + d0) : 0u;
                 for (;;) {
                     const int a = ip - 1 - lane, b = match - 1 - lane;
-                    const bool eq = (src[max(a, 0)] == src[max(b, 0)]) && a >= anchor && b >= 0;  // (loads unconditional)
+                    const bool eq = (src.u8(max(a, 0)) == src.u8(max(b, 0))) && a >= anchor && b >= 0;  // (loads unconditional)
                     const int back = first_clear(__ballot(eq));
                     ip -= back;
                     match -= back;
@@ -253,6 +265,10 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
             // ---- literals
             const int lit = ip - anchor;
             if (op + 1 + lit / 255 + 1 + lit + 2 + 1 > cap) return -1;
+            // the output only grows: once token + literals + offset reach n the block is RAW
+            // (lz4-java keeps a block whose compressed size is >= its length uncompressed), and
+            // its payload is never read (k_lz4_gather copies RAW blocks from the stream)
+            if (op + 1 + lit + 2 >= n) return n;
             int token = op++;
             uint32_t tk;
             if (lit >= 15) {
@@ -263,7 +279,7 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
             } else {
                 tk = (uint32_t)lit << 4;
             }
-            for (int j = lane; j < lit; j += 64) out[op + j] = src[anchor + j];
+            for (int j = lane; j < lit; j += 64) out[op + j] = (uint8_t)src.u8(anchor + j);
             op += lit;
             for (;;) {  // _next_match
                 const uint32_t off = (uint32_t)(ip - match);
@@ -291,7 +307,7 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
                 if (ip >= lim) goto last_literals;
                 // the next search's first sequences load with this test's (unused on a hit)
                 seq0 = search_seq(src, ip + 1, 0, n);
-                const uint32_t s2 = g32(src + ip - 2), s0 = g32(src + ip);
+                const uint32_t s2 = src.u32(ip - 2), s0 = src.u32(ip);
                 if (lane == 0) table[hash4(s2)] = (uint16_t)(ip - 2);
                 __builtin_amdgcn_wave_barrier();  // the write above, then the read below
                 const uint32_t h = hash4(s0);
@@ -301,8 +317,8 @@ __device__ int lz4_compress_wave(const uint8_t *src, int n, uint16_t *table, uin
                 // a candidate's LZ4_count round loads with its test (m2 < ip: in bounds)
                 const int d0 = m2 - ip, al = ip + kMinMatch + 4 * lane;
                 const bool full = al + 4 <= mlimit;
-                const uint32_t d = full ? g32(src + al) ^ g32(src + al + d0) : 0u;
-                if (g32(src + m2) != s0) break;
+                const uint32_t d = full ? src.u32(al) ^ src.u32(al + d0) : 0u;
+                if (src.u32(m2) != s0) break;
                 match = m2;
                 token = op++;
                 tk = 0;
@@ -315,6 +331,8 @@ last_literals:
     {
         const int last = n - anchor;
         if (op + 1 + last / 255 + 1 + last > cap) return -1;
+        const int fin = op + 1 + (last >= 15 ? (last - 15) / 255 + 1 : 0) + last;
+        if (fin >= n) return fin;  // RAW: nothing to write (see the literal run above)
         if (last >= 15) {
             const int nrun = (last - 15) / 255;
             if (lane == 0) out[op] = 15u << 4;
@@ -324,7 +342,7 @@ last_literals:
             if (lane == 0) out[op] = (uint8_t)(last << 4);
             ++op;
         }
-        for (int j = lane; j < last; j += 64) out[op + j] = src[anchor + j];
+        for (int j = lane; j < last; j += 64) out[op + j] = (uint8_t)src.u8(anchor + j);
         op += last;
     }
     return op;
@@ -368,10 +386,10 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
         return;
     }
     for (int i = lane; i < kTable / 8; i += 64) ((uint4 *)s_tab)[i] = make_uint4(0u, 0u, 0u, 0u);
-    __syncthreads();
     const int n = (int)blen;
-    const uint8_t *src = stream + boff;
     uint8_t *slot = slots + b * slot_bytes;
+    __syncthreads();
+    const GlobalSrc src{stream + boff};
     const int sc = lz4_compress_wave(src, n, s_tab, slot + kHeader, (int)(slot_bytes - kHeader));
     if (sc < 0) {
         if (lane == 0) {
