@@ -1520,7 +1520,10 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
     constexpr int NCH = TR * RB / 16;                              // 16 B chunks per full tile
     constexpr int LD = (NCH + T - 1) / T;
     constexpr int PC = (RB + 15) / 16;                             // drain pieces per record
-    constexpr int TAILW = (RB % 16) ? (RB % 16) / 4 : 4;           // dwords in the last piece
+    // every piece is 16 B: the last one of a record whose size is not a multiple of 16 ends
+    // at the record's end and overlaps the one before it (the same bytes written twice), so
+    // the drain's stores are one dwordx4 per lane with every lane active
+    auto piece_dw = [](uint32_t pc) -> uint32_t { return pc + 1 < (uint32_t)PC ? 4 * pc : (uint32_t)DW - 4; };
     constexpr int DRB = 7;                                         // pieces per lane per batch
     static_assert(RB % 16 == 4 || RB % 16 == 8 || RB % 16 == 12 || RB % 16 == 0, "RB multiple of 4");
     static_assert((TR * RB) % 16 == 0, "tiles start 16 B aligned");
@@ -1585,14 +1588,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
     uint64_t st_last = wc_stamp();
 #endif
     auto store_piece = [&](const u32x4 &v, uint32_t dst, uint32_t pc) {
-        uint32_t *d = out + (uint64_t)dst * DW + 4 * pc;
-        if (TAILW == 4 || pc + 1 < PC) {
-            *(u32x4 *)d = v;
-        } else {
-            d[0] = v.x;
-            if (TAILW > 1) d[1] = v.y;
-            if (TAILW > 2) d[2] = v.z;
-        }
+        *(u32x4 *)(out + (uint64_t)dst * DW + piece_dw(pc)) = v;
     };
     for (int t = 0; t < ntiles; ++t) {
         const int nrec = t + 1 < ntiles ? TR : lastn;
@@ -1679,8 +1675,9 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
         for (uint32_t i = lane; i < RS / 8; i += 64) ((u32x4 *)myrow)[i] = u32x4{0, 0, 0, 0};
         lds_barrier();
         WC_STAMP(6);  // sorted index + barrier
-        // ---- drain: the sorted tile in 16 B pieces, PC per record (RB = 100: six of 16 B and
-        //      one of 4 B), consecutive lanes -> consecutive pieces, so a partition run still
+        // ---- drain: the sorted tile in 16 B pieces, PC per record (RB = 100: bytes 0-95 in six
+        //      and 84-99 in the seventh, piece_dw), consecutive lanes -> consecutive pieces, so a
+        //      partition run still
         //      leaves the CU as consecutive lanes, with a quarter of the store instructions and
         //      LDS lookups of a dword stream.  Records are 4 B-aligned in the stage and in the
         //      output: the pieces are read as dwords (ds_read2_b32 pairs) and stored as one
@@ -1698,12 +1695,8 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
                 const uint32_t s = uu / PC;
                 pc[q] = uu - s * PC;
                 const uint32_t e = idx[s];
-                const uint32_t *sp = stage + (e & 0xFFFFu) * DW + 4 * pc[q];
-                if (TAILW == 4 || pc[q] + 1 < PC) {
-                    v[q] = u32x4{sp[0], sp[1], sp[2], sp[3]};
-                } else {
-                    v[q] = u32x4{sp[0], TAILW > 1 ? sp[1] : 0u, TAILW > 2 ? sp[2] : 0u, 0u};
-                }
+                const uint32_t *sp = stage + (e & 0xFFFFu) * DW + piece_dw(pc[q]);
+                v[q] = u32x4{sp[0], sp[1], sp[2], sp[3]};
                 dst[q] = dlt[e >> 16] + s;
             }
             WC_STAMP(7);  // drain: LDS reads
