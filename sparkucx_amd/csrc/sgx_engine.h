@@ -257,7 +257,7 @@ struct Ctx {
     DevBuf input_stage;
     const uint32_t *last_off_dev = nullptr;  // device (R+1) record offsets of the last partition pass
     // reduce side and map-side combine
-    DevBuf kryo_in, kryo_work, sort_buf[2], sort_err, grp_flags, grp_offs, grp_status, grp_out, grp_prefix;
+    DevBuf kryo_in, kryo_work, sort_buf[2], sort_err, grp_status, grp_out;
     DevBuf digit_hist, items_dev, gather_stage, fetch_tmp, comb_buf;
     HostPinned gather_items;
     HostPinned seg_host;  // (partition, spill) segment offsets of an UnsafeShuffleWriter commit

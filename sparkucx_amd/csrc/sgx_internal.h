@@ -178,12 +178,12 @@ hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, i
 hipError_t launch_gather_items(const int64_t *items, int64_t n_items, int align, hipStream_t stream);
 // Reduce side (sgx_reduce.hip), key-sorted (Long, Long) records
 hipError_t launch_digit_hist(const void *rec, int64_t n, int rb, uint32_t *hist, int num_cus, hipStream_t st);
-hipError_t launch_group_flags(const void *rec, int64_t n, uint32_t *flags, hipStream_t st);
-hipError_t launch_group_emit(const void *rec, int64_t n, const uint32_t *flags, const uint32_t *offs,
-                             int64_t *keys, int64_t *starts, int64_t *values, hipStream_t st);
-int64_t prefix64_blocks(int64_t n);
-hipError_t launch_group_sums(const void *rec, int64_t n, const int64_t *starts, int64_t ngroups,
-                             uint64_t *bsum, uint64_t *P, int64_t *sums, hipStream_t st);
+// groupByKey / reduceByKey(_ + _) over key-sorted (Long, Long) records in one pass
+// (sgx_reduce.hip, k_group_fused): keys[g], starts[g] (may be NULL), vals = every value (GROUP)
+// or the group sums (SUM), *ngroups.  status: 2 * group_tiles(n) u64, ticket/err: zeroed.
+int64_t group_tiles(int64_t n);
+hipError_t launch_group_fused(const void *rec, int64_t n, bool sum, uint64_t *status, uint32_t *ticket, uint32_t *err,
+                              int64_t *keys, int64_t *starts, int64_t *vals, int64_t *ngroups, hipStream_t st);
 // keys[i], vals[i] -> 16 B records {key, value} (map-side combine output)
 hipError_t launch_pack_pairs(const int64_t *keys, const int64_t *vals, int64_t n, void *out, hipStream_t st);
 // RangePartitioner.sketch (sgx_sample.hip): reservoir of k keys of n records, XORShiftRandom

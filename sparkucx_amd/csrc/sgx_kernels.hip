@@ -1939,6 +1939,9 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
 // of the 7-9 LSD digit passes that remain below the window.
 // ------------------------------------------------------------------------------------
 constexpr int BS_THREADS = 512;
+#ifndef BS_UNROLL
+#define BS_UNROLL 8  // keys compared per step of the rank loop (independent LDS loads; 8 vs 4: sorted 1 GiB 3.67 -> 3.62 ms, profiles/r03_bucket_unroll_ab.jsonl)
+#endif
 
 // the order key of a staged record: 16 B -> the signed Long sign-flipped (hi), lo = 0;
 // 100 B -> the first 8 key bytes big-endian (hi) and the last 2 (lo)
@@ -2066,16 +2069,16 @@ __global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__re
         const uint64_t kh = khi[j];
         const uint32_t kl = LO ? klo[j] : 0u;
         int rank = 0, i = s0;
-        for (; i + 4 <= e0; i += 4) {
-            uint64_t h[4];
-            uint32_t l[4];
+        for (; i + BS_UNROLL <= e0; i += BS_UNROLL) {
+            uint64_t h[BS_UNROLL];
+            uint32_t l[BS_UNROLL];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < BS_UNROLL; ++q) {
                 h[q] = khi[i + q];
                 l[q] = LO ? klo[i + q] : 0u;
             }
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
+            for (int q = 0; q < BS_UNROLL; ++q) {
                 const bool lt = LO ? (h[q] < kh || (h[q] == kh && l[q] < kl)) : h[q] < kh;
                 const bool eq = LO ? (h[q] == kh && l[q] == kl) : h[q] == kh;
                 rank += (lt || (i + q < j && eq)) ? 1 : 0;

@@ -387,41 +387,28 @@ int sgx::group_records(sgx_engine *e, Ctx &c, const void *sorted, int64_t n, int
                        int64_t **keys, int64_t **starts, int64_t **vals) {
     hipStream_t st = c.st;
     *ngroups = 0;
-    // group ids: flags of key changes, exclusive scan (K3 with one partition: offs[i] is the
-    // group of record i minus its flag; part_off[1] the group count)
-    const int64_t tiles = scan_tiles(n);
-    SGX_TRY(c.grp_flags.ensure((size_t)std::max<int64_t>(n, 1) * 4));
-    SGX_TRY(c.grp_offs.ensure((size_t)std::max<int64_t>(n, 1) * 4));
-    SGX_TRY(c.grp_status.ensure((size_t)(16 + tiles * 8 + 16)));
+    // one pass (k_group_fused): outputs sized for the worst case (every record its own group)
+    if (n >= (int64_t)1 << 31) return fail_msg(SGX_ERR_UNSUPPORTED, "grouping %lld records (limit 2^31 - 1)", (long long)n);
+    const int64_t tiles = group_tiles(n);
+    SGX_TRY(c.grp_out.ensure((size_t)std::max<int64_t>(n, 1) * 24));
+    int64_t *dkeys = (int64_t *)c.grp_out.p, *dstarts = dkeys + std::max<int64_t>(n, 1),
+            *dvals = dstarts + std::max<int64_t>(n, 1);
+    // [ticket, err | ngroups | two status words per tile]
+    SGX_TRY(c.grp_status.ensure((size_t)(16 + tiles * 16)));
     uint32_t *ticket_err = (uint32_t *)c.grp_status.p;
-    uint32_t *gcount = (uint32_t *)((char *)c.grp_status.p + 16 + tiles * 8);  // [0, total]
+    int64_t *dng = (int64_t *)((char *)c.grp_status.p + 8);
     hipEvent_t t0 = e->ev(), t1 = e->ev();
     HIP_TRY(hipEventRecord(t0, st));
     int64_t ng = 0;
     if (n > 0) {
-        HIP_TRY(hipMemsetAsync(c.grp_status.p, 0, (size_t)(16 + tiles * 8 + 16), st));
-        HIP_TRY(launch_group_flags(sorted, n, (uint32_t *)c.grp_flags.p, st));
-        HIP_TRY(launch_scan((const uint32_t *)c.grp_flags.p, (uint32_t *)c.grp_offs.p, n,
-                            (uint64_t *)((char *)c.grp_status.p + 16), ticket_err, ticket_err + 1, gcount, (int)n, 1,
-                            st));
-        uint32_t h[2] = {0, 0}, terr[2] = {0, 0};
-        HIP_TRY(hipMemcpyAsync(h, gcount, 8, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipMemsetAsync(c.grp_status.p, 0, (size_t)(16 + tiles * 16), st));
+        HIP_TRY(launch_group_fused(sorted, n, agg == SGX_AGG_SUM, (uint64_t *)((char *)c.grp_status.p + 16), ticket_err,
+                                   ticket_err + 1, dkeys, starts ? dstarts : nullptr, dvals, dng, st));
+        uint32_t terr[2] = {0, 0};
+        HIP_TRY(hipMemcpyAsync(&ng, dng, 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipMemcpyAsync(terr, ticket_err, 8, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         if (terr[1] & 1u) return fail_msg(SGX_ERR_TIMEOUT, "group scan look-back spin gave up");
-        ng = h[1];
-    }
-    const int64_t nvals = agg == SGX_AGG_GROUP ? n : ng;
-    SGX_TRY(c.grp_out.ensure((size_t)std::max<int64_t>(ng * 16 + nvals * 8, 16)));
-    int64_t *dkeys = (int64_t *)c.grp_out.p, *dstarts = dkeys + ng, *dvals = dstarts + ng;
-    if (n > 0) {
-        HIP_TRY(launch_group_emit(sorted, n, (const uint32_t *)c.grp_flags.p, (const uint32_t *)c.grp_offs.p, dkeys,
-                                  dstarts, agg == SGX_AGG_GROUP ? dvals : nullptr, st));
-        if (agg == SGX_AGG_SUM) {
-            SGX_TRY(c.grp_prefix.ensure((size_t)(n + prefix64_blocks(n)) * 8));
-            uint64_t *P = (uint64_t *)c.grp_prefix.p, *bsum = P + n;
-            HIP_TRY(launch_group_sums(sorted, n, dstarts, ng, bsum, P, dvals, st));
-        }
     }
     HIP_TRY(hipEventRecord(t1, st));
     e->record_stage(SGX_STAGE_GROUP, t0, t1);

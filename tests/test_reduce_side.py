@@ -170,6 +170,27 @@ def test_grouped(sgx_lib, oracle_lib, agg, R):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("agg", ["group", "sum"])
+@pytest.mark.parametrize("shape", ["spanning", "tile_aligned", "unique", "one"])
+def test_grouped_tile_shapes(sgx_lib, oracle_lib, agg, shape):
+    """The one-pass grouping (k_group_fused: 4096-record tiles, a look-back over tiles) on
+    group sizes that stress its tile boundaries: groups spanning several tiles (the sum is
+    carried), groups starting exactly on tile boundaries, every key unique, one record.
+    Values near +-2^63, so the Long sums wrap."""
+    T = 4096
+    sizes = {"spanning": [1, T - 1, 3 * T + 17, 5, 2 * T, T + 1, 2, 7 * T - 3, 1],
+             "tile_aligned": [T, T, 1, T - 1, 2 * T, T],
+             "unique": [1] * (2 * T + 1),
+             "one": [1]}[shape]
+    rng = np.random.default_rng(len(sizes))
+    keys = np.repeat(np.arange(len(sizes), dtype=np.int64) * 7 - 10, sizes)
+    vals = rng.integers(2**62, 2**63 - 1, size=len(keys), dtype=np.int64) * rng.choice([-1, 1], size=len(keys))
+    perm = rng.permutation(len(keys))
+    recs = _records16(keys[perm], vals[perm])
+    _run(sgx_lib, oracle_lib, [recs[: len(recs) // 2], recs[len(recs) // 2:]], 1, agg=agg)
+
+
+@pytest.mark.gpu
 def test_grouped_empty_range(sgx_lib, oracle_lib):
     maps = [oracle_lib.gen_uniform16(1000, 1)]
     _run(sgx_lib, oracle_lib, maps, 16, rng_part=(5, 5), agg="group")
