@@ -1051,7 +1051,7 @@ ScatterGeom scatter_geom16_ord(uint32_t R, int force_waves, int force_items) {
 // Stage layout (round 3): the records the tile keeps, all streams' [LE_p, e_p) back to
 // back, then the ones it writes, all streams' [a_p, LE_p) back to back -- so the drain's
 // first ~3.5 R slots need no store instruction and the rest are stores with every lane
-// active, most of them in the late group that issues during the next tile's ranking.
+// active.
 // (Each stream's [a_p, e_p) in one segment left every drain round with both kinds: 16
 // store instructions per lane per tile, about half the lanes masked.  C1 K4 1.96 -> 1.85
 // ms, bench 1612 -> 1674 GB/s; writes-first measured between the two, and slower at
@@ -1099,10 +1099,12 @@ extern "C" int sgx_diag_wc_stamps(unsigned long long *out16, int reset) {
 #endif
 
 // Drain groups (of 8 slots) whose stores are held back and issued during the next tile's
-// ranking atomics, so the CU's memory queue is not idle through the LDS-only phases
-// (C1 K4 ~1 % faster, profiles/r03_wc_late_stores_ab.jsonl).
+// ranking atomics, so the CU's memory queue is not idle through the LDS-only phases.  With
+// each stream's records in one stage segment that bought ~1 % (profiles/r03_wc_late_stores_ab.jsonl);
+// with the kept-first layout (below) the held group is nearly all stores and holding it
+// back costs ~1.5 % instead (C1 K4 1.78 -> 1.75 ms without it, r03_wc_late0_ab.jsonl): off.
 #ifndef SGX_WC_LATE
-#define SGX_WC_LATE 1
+#define SGX_WC_LATE 0
 #endif
 
 __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
