@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--num-chunks", type=int, default=0)
     ap.add_argument("--no-split", action="store_true",
                     help="R > 1024: one lane-ordered K4 pass instead of the two-level split (A/B measurement)")
+    ap.add_argument("--no-padded", action="store_true",
+                    help="hash maps take the two-pass map side (histogram + scan + scatter) instead of the "
+                         "single-pass padded write (A/B measurement, DESIGN.md §7)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=16.0,
                     help="budget of the CPU baseline's timed legs (plus ~5 s of C0 and setup)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -213,7 +216,8 @@ def main():
 
     n, R, rb = args.records, args.partitions, args.record_bytes
     eng = sgx.ShuffleEngine(device=device, num_chunks=args.num_chunks,
-                            flags=sgx.FLAG_NO_SPLIT_SCATTER if args.no_split else 0)
+                            flags=(sgx.FLAG_NO_SPLIT_SCATTER if args.no_split else 0) |
+                            (sgx.FLAG_NO_PADDED_MAP if args.no_padded else 0))
     self_x = args.self_exchange and world == 1
     if world > 1 and args.comm == "host":
         eng.comm_init_host(world, rank)
@@ -289,6 +293,7 @@ def main():
 
     verified = None
     lens = eng.map_lengths(sid, rank, R)
+    layout = eng.map_layout(sid, last["mid"])
     if not args.no_verify:
         verified = bool(lens.sum() == rb * n) if args.serializer == "fixed" else bool(lens.sum() >= 4 * n)
     xgmi = None
@@ -331,6 +336,7 @@ def main():
         k4_pmc, side_pmc = pmc.get("scatter") or {}, pmc.get("map_side") or {}
         side_ms = (st.ms["hist"] + st.ms["scan"] + st.ms["scatter"]) / max(1, st.count["scatter"])
         side_ach = algo * n / (side_ms * 1e-3) / 1e9
+        padded = layout == sgx.LAYOUT_PADDED
         out = {
             "metric": METRIC, "value": round(value, 2), "unit": "GB/s", "n_gpus": world,
             "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms_per_step, 4),
@@ -340,6 +346,8 @@ def main():
                      f"{len(bounds)} bounds sampled from rank 0's batch"),
             "config": {"workload": _workload_name(args, n, R, world, self_x),
                        "records_per_gpu": n, "partitions": R, "record_bytes": rb,
+                       "map_layout": "padded (single pass: sampled histogram, K4 into sub-bins, K3 over the "
+                                     "streams' counts)" if padded else "contiguous (two-pass: K1+K2 histogram, K3, K4)",
                        "parallelism": f"dp{world} (map shards per GPU, reducers owned "
                                       + ("floor(r*P/R))" if args.placement == "even" else "in byte-balanced ranges)"),
                        "exchange": ("RCCL ncclAllToAllv, 1 rank (rehearsal)" if self_x else None) if world == 1 else (
@@ -357,10 +365,13 @@ def main():
                                   "traffic": side_pmc.get("hbm_bytes_per_write"),
                                   "traffic_over_algorithmic": side_pmc.get("ratio")},
             "stages_ms_per_step": {k: round(v / max(1, st.count[k]), 4) for k, v in st.ms.items() if st.count[k]},
-            # the two-pass map side must move 3 x record bytes (hist reads the record
-            # for its 8 B key; K4 reads 16 + writes 16): its HBM stream rate against 8 TB/s
-            "map_side_two_pass_hbm": {"bytes_per_record": 3 * rb, "achieved": round(3.0 * rb * n / side_ms / 1e6, 1),
-                                      "frac": round(3.0 * rb * n / side_ms / 1e6 / HBM_PEAK_GBS, 4)},
+            # the HBM bytes the map side's design must move per record -- two-pass: 3 x record
+            # bytes (the histogram reads the whole record for its 8 B key; K4 reads + writes it);
+            # padded: 2 x record bytes + the sampled lines (one 128 B line in 128) -- as a
+            # stream rate against 8 TB/s
+            "map_side_design_hbm": (lambda bpr: {"bytes_per_record": bpr, "achieved": round(bpr * n / side_ms / 1e6, 1),
+                                                 "frac": round(bpr * n / side_ms / 1e6 / HBM_PEAK_GBS, 4)})(
+                (2 * rb + rb / 128.0) if padded else 3 * rb),
             "verified_lengths_sum": verified,
         }
         if xgmi is not None:
@@ -393,6 +404,20 @@ def main():
                 if args.compress:
                     out["lz4"]["decompress_ms"] = round(st2.ms["decompress"] / max(1, st2.count["decompress"]), 4)
                 dst.free()
+        if world == 1 and args.serializer == "fixed" and rb == 16:
+            # the consumer side of the layout: every block of the last map gathered reducer by
+            # reducer into HBM (sgx_fetch_blocks; a padded map's blocks come from its
+            # fragments, a contiguous map's from one range each)
+            dst = eng.alloc(n * rb)
+            eng.stats_reset()
+            for _ in range(3):
+                eng.fetch_blocks(sid, [last["mid"]] * R, list(range(R)), dst=dst)
+            st2 = eng.stats()
+            g_ms = st2.ms["regroup"] / max(1, st2.count["regroup"])
+            out["fetch_all_blocks"] = {"kernel": "k_gather_frags" if padded else "k_gather_items", "ms": round(g_ms, 4),
+                                       "achieved_GBs": round(algo * n / (g_ms * 1e-3) / 1e9, 1),
+                                       "note": "R blocks of one map into device memory, read + write per record"}
+            dst.free()
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(args)
         elif world == 1:

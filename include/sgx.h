@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SGX_ABI_VERSION 5
+#define SGX_ABI_VERSION 6
 
 enum sgx_status {
     SGX_OK = 0,
@@ -72,8 +72,13 @@ enum sgx_flags {
                                          of the two-level write-combining split               */
     SGX_FLAG_NO_BUCKET_SORT = 64,     /* sorted reads / map-side combine: LSD digit passes only
                                          (no key-window buckets sorted on chip)               */
-    SGX_FLAG_ASSUME_LDS_DISORDER = 128 /* testing: act as if the engine-start LDS ordering
+    SGX_FLAG_ASSUME_LDS_DISORDER = 128, /* testing: act as if the engine-start LDS ordering
                                           check had failed (see sgx_lds_order_ok)             */
+    SGX_FLAG_NO_PADDED_MAP = 256,     /* hash maps always take the two-pass map side (histogram
+                                         + scan + scatter) instead of the single-pass padded
+                                         write (sgx_map_layout)                                */
+    SGX_FLAG_PAD_ANY_SIZE = 512       /* testing: write maps of any size padded (default: from
+                                         2^20 records up)                                      */
 };
 
 typedef struct sgx_config {
@@ -240,9 +245,24 @@ int sgx_map_begin(sgx_engine *e, int32_t shuffle_id, int64_t map_id);
 int sgx_map_append(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records, int64_t nrecords,
                    int32_t record_bytes, int32_t mem_kind);
 int sgx_map_commit(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *out_partition_lengths);
-/* Device pointer + byte size of a map output (partition-contiguous data). */
+/* Device pointer + byte size of a map output (partition-contiguous data; a padded map's
+ * contiguous copy is built on the first call, see sgx_map_layout). */
 int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, void **out_dev_ptr,
                  int64_t *out_bytes);
+/* How the engine holds a written map (waits for its kernels).  A fixed-codec HashPartitioner
+ * map of 16 B records with R <= 1024, written by sgx_write_map on an engine without a
+ * multi-rank communicator, is written in ONE pass over its records: a sampled
+ * histogram sizes a line-aligned sub-bin per (partition, chunk) stream, the stable scatter
+ * writes every stream into its sub-bin, and a scan of the streams' true counts gives the
+ * partition lengths and index offsets -- the same lengths, offsets and per-block bytes as the
+ * two-pass write, with gaps between the streams in HBM (SGX_LAYOUT_PADDED).  Block fetches
+ * gather the streams directly; exchange sends, sgx_map_data and index files use a contiguous
+ * copy built once on first use.  A stream longer than its sub-bin (keys not spread like the
+ * sample) makes the write redo the map with the two-pass kernels on the device
+ * (SGX_LAYOUT_CONTIGUOUS), and the shuffle's later maps skip the padded attempt.  Maps of
+ * other shuffles are always SGX_LAYOUT_CONTIGUOUS. */
+enum sgx_layout { SGX_LAYOUT_CONTIGUOUS = 0, SGX_LAYOUT_PADDED = 1 };
+int sgx_map_layout(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int32_t *out_layout);
 
 /* ---- IndexShuffleBlockResolver.writeIndexFileAndCommit (IndexShuffleBlockResolver.scala:
  *      161-217): writes the map output as data file + index file ((R+1) big-endian int64
@@ -306,6 +326,13 @@ int sgx_exchange(sgx_engine *e, int32_t shuffle_id);
 /* The same collective with exactly the listed local maps (n >= 0; 0 = this rank contributes
  * nothing this round): a pipelined writer exchanges map k while it writes map k + 1. */
 int sgx_exchange_maps(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t n);
+/* A rank that cannot take part in an exchange round of a shuffle with num_partitions
+ * reducers (it failed before sgx_exchange: e.g. registering the shuffle) joins the round's
+ * first all-gather anyway, marked failed with `code` (< 0), so every rank's sgx_exchange of
+ * that round fails at once with SGX_ERR_STATE instead of waiting in the collective for it
+ * until the timeout.  A rank whose own sgx_exchange fails locally (an open map, a failed
+ * write) marks the round the same way by itself.  Returns `code`. */
+int sgx_exchange_fail(sgx_engine *e, int32_t num_partitions, int32_t code);
 
 /* ---- ShuffleTransport.fetchBlocksByBlockIds (ucx/ShuffleTransport.scala:154-156) /
  *      BlockStoreClient.fetchBlocks (spark_3_0/UcxShuffleClient.scala:49-91): copy blocks
@@ -321,6 +348,22 @@ int sgx_fetch_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids,
  * all submitted work is complete, 0 while some is in flight. sgx_sync blocks until done. */
 int sgx_progress(sgx_engine *e);
 int sgx_sync(sgx_engine *e);
+
+/* ---- blocks fetched from elsewhere: a reduce task Spark placed on an executor that does not
+ *      own its reducers (the reference's reader takes any block from anywhere,
+ *      spark_3_0/UcxShuffleReader.scala:74-103) fetches their raw blocks from the owners and
+ *      imports them into its own engine; sgx_read_records / _sorted / _grouped and
+ *      sgx_fetch_blocks then run over them on this GPU as over exchanged blocks.  data: the
+ *      blocks (map_ids[j], r) for r in [start, end), j in [0, nmaps), back to back in the
+ *      canonical order -- reducer-major, then map (what sgx_fetch_blocks returns for that
+ *      list) -- in host or device memory (mem_kind); lengths[(r - start) * nmaps + j] their
+ *      bytes (published bytes: fixed records, or Kryo / LZ4 frames).  Copied: the caller's
+ *      buffer may be freed on return.  *out_import_id names the import for
+ *      sgx_release_import, which frees its HBM (the read's results stay valid). ---- */
+int sgx_import_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
+                      int32_t start_partition, int32_t end_partition, const void *data, int32_t mem_kind,
+                      const int64_t *lengths, int64_t *out_import_id);
+int sgx_release_import(sgx_engine *e, int32_t shuffle_id, int64_t import_id);
 
 /* ---- reduce side after the fetch: UcxShuffleReader.read (spark_3_0/UcxShuffleReader.scala:
  *      137-191).  Input = the blocks (map_ids[0..nmaps) x reducers [start, end)) this engine

@@ -331,6 +331,13 @@ JNIEXPORT void JNICALL JNI_FN(exchangeMaps)(JNIEnv *env, jclass c, jlong e, jint
     check(env, rc);
 }
 
+/* a round this executor cannot take part in (it failed before the exchange): join its first
+ * all-gather marked failed, so every rank fails the round together (sgx_exchange_fail) */
+JNIEXPORT void JNICALL JNI_FN(exchangeFail)(JNIEnv *env, jclass c, jlong e, jint numPartitions) {
+    (void)c;
+    check(env, sgx_exchange_fail(E(e), numPartitions, SGX_ERR_STATE));
+}
+
 /* the executor's reducers [r0, r1) of the shuffle (fixed by its first exchange): int[2] */
 JNIEXPORT jintArray JNICALL JNI_FN(shuffleReducers)(JNIEnv *env, jclass c, jlong e, jint sid) {
     (void)c;
@@ -384,6 +391,39 @@ JNIEXPORT jlongArray JNICALL JNI_FN(fetchBlocks)(JNIEnv *env, jclass c, jlong e,
     free(r);
     free(len);
     return out;
+}
+
+/* blocks fetched from the reducers' owners (reducer-major, map-minor in `data`, a direct
+ * buffer; lengths in the same order) handed to this executor's engine: the reads then run
+ * over them on this GPU (sgx_import_blocks).  Returns the import id for releaseImport. */
+JNIEXPORT jlong JNICALL JNI_FN(importBlocks)(JNIEnv *env, jclass c, jlong e, jint sid, jlongArray mapIds, jint r0,
+                                             jint r1, jobject data, jlongArray lengths) {
+    (void)c;
+    jsize n, nl;
+    void *p;
+    int64_t cap;
+    if (direct(env, data, &p, &cap)) return 0;
+    int64_t *m = map_list(env, mapIds, &n);
+    int64_t *len = map_list(env, lengths, &nl);
+    int64_t id = 0;
+    if (m && len) {
+        if ((int64_t)nl != (int64_t)n * (r1 - r0)) {
+            throw_arg(env, "one length per (reducer, map) block");
+        } else {
+            int64_t total = 0;
+            for (jsize i = 0; i < nl; ++i) total += len[i];
+            if (total > cap) throw_arg(env, "lengths exceed the data buffer");
+            else check(env, sgx_import_blocks(E(e), sid, m, n, r0, r1, p, SGX_MEM_HOST, len, &id));
+        }
+    }
+    free(m);
+    free(len);
+    return (jlong)id;
+}
+
+JNIEXPORT void JNICALL JNI_FN(releaseImport)(JNIEnv *env, jclass c, jlong e, jint sid, jlong importId) {
+    (void)c;
+    check(env, sgx_release_import(E(e), sid, importId));
 }
 
 JNIEXPORT jint JNICALL JNI_FN(progress)(JNIEnv *env, jclass c, jlong e) {

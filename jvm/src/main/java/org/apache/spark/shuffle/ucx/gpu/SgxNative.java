@@ -77,6 +77,13 @@ public final class SgxNative {
   // exchangeMaps: exactly these local maps (the pipelined form)
   public static native void exchange(long e, int shuffleId);
   public static native void exchangeMaps(long e, int shuffleId, long[] mapIds);
+  // a round this executor cannot take part in: join it marked failed (every rank fails it)
+  public static native void exchangeFail(long e, int numPartitions);
+  // blocks of reducers [r0, r1) x mapIds fetched from their owners (reducer-major, map-minor
+  // in a direct buffer): the reads then run over them on this GPU; returns the import id
+  public static native long importBlocks(long e, int shuffleId, long[] mapIds, int r0, int r1, ByteBuffer data,
+                                         long[] lengths);
+  public static native void releaseImport(long e, int shuffleId, long importId);
 
   // fetchBlocksByBlockIds: blocks back to back in dst; returns their lengths (dst null = sizes)
   public static native long[] fetchBlocks(long e, int shuffleId, long[] mapIds, int[] reduceIds,

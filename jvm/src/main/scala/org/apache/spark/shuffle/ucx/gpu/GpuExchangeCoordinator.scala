@@ -17,14 +17,20 @@
  *     runs SgxNative.commInit -- all on the executor's one "comm" thread, so nothing else
  *     reaches the communicator before it exists.
  *  2. Exchange: the first reduce task of a shuffle on any executor (GpuShuffleReader.read)
- *     sends GpuExchangeRequest(shuffleId, digest of the map ids the MapOutputTracker lists)
- *     to the driver and waits.  A reduce task only starts once its map stage has completed,
- *     so every executor's maps of those ids are committed by then.  The driver de-duplicates
- *     (one exchange per shuffle and map set: a re-run map stage has new map ids and gets a
- *     new round with just the new maps) and sends GpuRunExchange to EVERY executor, in one
- *     global sequence (the driver endpoint is single-threaded; Spark RPC keeps a sender's
- *     messages to one receiver in order).  Each executor runs SgxNative.exchange +
+ *     sends GpuExchangeRequest(shuffleId, the shuffle's full map id set as the
+ *     MapOutputTracker lists it over ALL partitions, the shuffle's GpuShuffleSpec) to the
+ *     driver and waits.  A reduce task only starts once its map stage has completed, so every
+ *     executor's maps of those ids are committed by then, and every reduce task of the stage
+ *     computes the same key (not its own range's non-empty blocks).  The driver
+ *     de-duplicates (one exchange per shuffle and map set: a re-run map stage has new map ids
+ *     and gets a new round with just the new maps) and sends GpuRunExchange to EVERY
+ *     executor, in one global sequence (the driver endpoint is single-threaded; Spark RPC
+ *     keeps a sender's messages to one receiver in order).  Each executor registers the
+ *     shuffle from the spec if no task of it ran there yet, then runs SgxNative.exchange +
  *     SgxNative.sync on its comm thread, in that order, and completes the waiting readers.
+ *     A rank that fails locally still joins the collective's first all-gather with an error
+ *     mark (sgx_exchange), so all ranks fail the round together; each reports
+ *     GpuExchangeFailed and the driver forgets the round, so a retried task starts a new one.
  *  3. Reads outside this executor's reducers (Spark placed the reduce task elsewhere):
  *     GpuShuffleReader asks the owners for the raw blocks over RPC (GpuFetchRemote, served
  *     from their HBM by SgxNative.fetchBlocks) and reads them on the CPU with Spark's own
@@ -52,10 +58,14 @@ object GpuRpcMessages {
   /** executor -> driver (ask): join the exchange world; reply GpuRankAssigned. */
   case class GpuExecutorJoin(executorId: String, host: String, endpoint: RpcEndpointRef)
   case class GpuRankAssigned(rank: Int, nranks: Int, rootHost: String)
-  /** executor -> driver (send): a reader needs shuffleId over the maps with this digest. */
-  case class GpuExchangeRequest(shuffleId: Int, mapsDigest: Long)
-  /** driver -> every executor (send), one global sequence: run the exchange now. */
-  case class GpuRunExchange(shuffleId: Int, mapsDigest: Long)
+  /** executor -> driver (send): a reader needs shuffleId exchanged over this full map set. */
+  case class GpuExchangeRequest(shuffleId: Int, maps: Seq[Long], spec: GpuShuffleSpec)
+  /** driver -> every executor (send), one global sequence: run attempt `attempt` of the
+   *  exchange now. */
+  case class GpuRunExchange(shuffleId: Int, maps: Seq[Long], spec: GpuShuffleSpec, attempt: Int)
+  /** executor -> driver (send): that attempt failed here; a new request starts a new round
+   *  (a late report of an older attempt never cancels a newer one). */
+  case class GpuExchangeFailed(shuffleId: Int, maps: Seq[Long], attempt: Int)
   /** executor -> driver (ask): every rank's endpoint; reply GpuPeers. */
   case object GpuPeersRequest
   case class GpuPeers(endpoints: Map[Int, RpcEndpointRef])
@@ -72,7 +82,8 @@ import GpuRpcMessages._
 class GpuDriverEndpoint(override val rpcEnv: RpcEnv, nranks: Int) extends ThreadSafeRpcEndpoint with Logging {
   private val ranks = mutable.LinkedHashMap.empty[String, (Int, RpcEndpointRef)]
   private var rootHost: String = _
-  private val done = mutable.HashSet.empty[(Int, Long)]
+  private val done = mutable.HashMap.empty[(Int, Seq[Long]), Int]      // key -> attempt broadcast
+  private val attempts = mutable.HashMap.empty[(Int, Seq[Long]), Int]
 
   override def receiveAndReply(context: RpcCallContext): PartialFunction[Any, Unit] = {
     case GpuExecutorJoin(execId, host, ep) =>
@@ -89,12 +100,18 @@ class GpuDriverEndpoint(override val rpcEnv: RpcEnv, nranks: Int) extends Thread
   }
 
   override def receive: PartialFunction[Any, Unit] = {
-    case GpuExchangeRequest(shuffleId, digest) =>
-      if (done.add((shuffleId, digest))) {
-        logInfo(s"exchange of shuffle $shuffleId (maps $digest) on ${ranks.size} executors")
+    case GpuExchangeRequest(shuffleId, maps, spec) =>
+      val key = (shuffleId, maps)
+      if (!done.contains(key)) {
+        val a = attempts.getOrElse(key, 0) + 1
+        attempts(key) = a
+        done(key) = a
+        logInfo(s"exchange of shuffle $shuffleId (${maps.size} maps, attempt $a) on ${ranks.size} executors")
         // every rank, the same order: ranks in rank order, requests in arrival order
-        ranks.values.toSeq.sortBy(_._1).foreach { case (_, ep) => ep.send(GpuRunExchange(shuffleId, digest)) }
+        ranks.values.toSeq.sortBy(_._1).foreach { case (_, ep) => ep.send(GpuRunExchange(shuffleId, maps, spec, a)) }
       }
+    case GpuExchangeFailed(shuffleId, maps, attempt) =>
+      if (done.get((shuffleId, maps)).contains(attempt)) done.remove((shuffleId, maps))
   }
 }
 
@@ -102,7 +119,7 @@ class GpuDriverEndpoint(override val rpcEnv: RpcEnv, nranks: Int) extends Thread
 class GpuExecutorEndpoint(override val rpcEnv: RpcEnv, engine: Long, coordinator: GpuExchangeCoordinator)
     extends ThreadSafeRpcEndpoint with Logging {
   override def receive: PartialFunction[Any, Unit] = {
-    case GpuRunExchange(shuffleId, digest) => coordinator.runExchange(shuffleId, digest)
+    case GpuRunExchange(shuffleId, maps, spec, attempt) => coordinator.runExchange(shuffleId, maps, spec, attempt)
   }
 
   override def receiveAndReply(context: RpcCallContext): PartialFunction[Any, Unit] = {
@@ -121,14 +138,15 @@ class GpuExecutorEndpoint(override val rpcEnv: RpcEnv, engine: Long, coordinator
   }
 }
 
-class GpuExchangeCoordinator(conf: SparkConf, isDriver: Boolean, engine: () => Long) extends Logging {
+class GpuExchangeCoordinator(conf: SparkConf, isDriver: Boolean, engine: () => Long,
+                             register: GpuShuffleSpec => Unit) extends Logging {
   private val driverName = "SgxGpuShuffle_driver"
   private val nranks = conf.getInt("spark.shuffle.ucx.gpu.numExecutors", conf.getInt("spark.executor.instances", 1))
   private val port = conf.getInt("spark.shuffle.ucx.gpu.bootstrapPort", 13380)
   private val timeoutMs = conf.getInt("spark.shuffle.ucx.gpu.commTimeoutMs", 300000)
   // one thread runs commInit and every exchange, in message order
   private val comm = ThreadUtils.newDaemonSingleThreadExecutor("sgx-comm")
-  private val exchanges = new ConcurrentHashMap[(Int, Long), Promise[Unit]]()
+  private val exchanges = new ConcurrentHashMap[(Int, Seq[Long]), Promise[Unit]]()
   @volatile private var driverRef: RpcEndpointRef = _
   @volatile private var peers: Map[Int, RpcEndpointRef] = Map.empty
   private val ranges = new ConcurrentHashMap[(Int, Int), Array[Int]]()
@@ -170,33 +188,46 @@ class GpuExchangeCoordinator(conf: SparkConf, isDriver: Boolean, engine: () => L
     }
   })
 
-  private def promise(key: (Int, Long)): Promise[Unit] = {
+  private def promise(key: (Int, Seq[Long])): Promise[Unit] = {
     val p = Promise[Unit]()
     val prev = exchanges.putIfAbsent(key, p)
     if (prev == null) p else prev
   }
 
   /** Called by GpuExecutorEndpoint for GpuRunExchange: queue the collective on the comm thread. */
-  private[gpu] def runExchange(shuffleId: Int, digest: Long): Unit = {
-    val p = promise((shuffleId, digest))
+  private[gpu] def runExchange(shuffleId: Int, maps: Seq[Long], spec: GpuShuffleSpec, attempt: Int): Unit = {
+    val key = (shuffleId, maps)
+    val p = promise(key)
     comm.submit(new Runnable {
       override def run(): Unit = try {
+        try register(spec)  // an executor that ran no task of the shuffle still takes part
+        catch {
+          case t: Throwable =>
+            // the round's collective still needs this executor: join its first all-gather
+            // marked failed, so every rank fails the round now (sgx_exchange_fail)
+            try SgxNative.exchangeFail(engine(), spec.numPartitions) catch { case _: Throwable => }
+            throw t
+        }
         SgxNative.exchange(engine(), shuffleId)
         SgxNative.sync(engine())
         p.trySuccess(())
       } catch {
-        case t: Throwable => p.tryFailure(t)
+        case t: Throwable =>
+          exchanges.remove(key, p)  // a later task may ask again
+          p.tryFailure(t)
+          driverRef.send(GpuExchangeFailed(shuffleId, maps, attempt))
       }
     })
   }
 
-  /** A reader's barrier: the shuffle's exchange over `maps` has completed on this executor. */
-  def awaitExchange(shuffleId: Int, maps: Array[Long]): Unit = {
+  /** A reader's barrier: the shuffle's exchange over its full map set `allMaps` (sorted) has
+   *  completed on this executor. */
+  def awaitExchange(shuffleId: Int, allMaps: Array[Long], spec: GpuShuffleSpec): Unit = {
     Await.result(setup.future, Duration(timeoutMs, TimeUnit.MILLISECONDS))
-    val digest = java.util.Arrays.hashCode(maps).toLong << 32 | (maps.length.toLong & 0xffffffffL)
-    val key = (shuffleId, digest)
+    val maps: Seq[Long] = allMaps.toVector
+    val key = (shuffleId, maps)
     val p = promise(key)
-    if (!p.isCompleted) driverRef.send(GpuExchangeRequest(shuffleId, digest))
+    if (!p.isCompleted) driverRef.send(GpuExchangeRequest(shuffleId, maps, spec))
     try Await.result(p.future, Duration(timeoutMs, TimeUnit.MILLISECONDS))
     catch {
       case t: Throwable =>

@@ -1,7 +1,8 @@
 /*
  * GpuShuffleClient — BlockStoreClient.fetchBlocks over the engine's HBM-resident blocks.
- * Replaces spark_3_0/UcxShuffleClient.scala:17-91: same signature, same recursive split at
- * spark.shuffle.ucx.maxBlocksPerRequest (:53-58), same "shuffle_<s>_<m>_<r>" parsing (:64).
+ * Replaces spark_3_0/UcxShuffleClient.scala:17-91: same signature, same recursive split in
+ * halves (splitAt(length / 2)) above spark.shuffle.ucx.maxBlocksPerRequest (:53-58), same
+ * "shuffle_<s>_<m>_<r>" parsing (:64).
  * Differences, by design:
  *   - one SgxNative.fetchBlocks per request (one gather launch on the GPU) instead of one
  *     synchronous UCX round trip per block with a progress() spin (:17-47);
@@ -25,9 +26,10 @@ class GpuShuffleClient(engine: Long, conf: SparkConf) extends BlockStoreClient {
                            listener: BlockFetchingListener,
                            downloadFileManager: DownloadFileManager): Unit = {
     if (blockIds.length > maxBlocksPerRequest) {
-      blockIds.grouped(maxBlocksPerRequest).foreach { ids =>
-        fetchBlocks(host, port, execId, ids, listener, downloadFileManager)
-      }
+      // the reference's split (UcxShuffleClient.scala:53-58): halve, recurse on both halves
+      val (b1, b2) = blockIds.splitAt(blockIds.length / 2)
+      fetchBlocks(host, port, execId, b1, listener, downloadFileManager)
+      fetchBlocks(host, port, execId, b2, listener, downloadFileManager)
       return
     }
     val parsed = blockIds.map(id => BlockId(id).asInstanceOf[ShuffleBlockId])

@@ -12,35 +12,42 @@
  *      declared "group" aggregator (groupByKey)                      -> readGrouped(AGG_GROUP)
  *      keyOrdering (sortByKey, :166-181)                             -> readSorted
  *      neither (deserializeStream, :137-145)                         -> readRecords
- * 3. Otherwise (Spark placed the task on another executor) the raw blocks of the reducers
- *    this executor does not hold come from their owners over RPC (coordinator.fetchRemote),
- *    and the read runs on the CPU with Spark's own serializer stream, the dependency's real
- *    aggregator and an ExternalSorter -- what BlockStoreShuffleReader does, so the results
- *    are Spark's.
+ * 3. Otherwise (Spark placed the task on another executor) the raw blocks of the range come
+ *    from their owners over RPC (coordinator.fetchRemote), are imported into this executor's
+ *    engine (SgxNative.importBlocks) and read on this GPU by the same calls as 2.
  */
 package org.apache.spark.shuffle.ucx.gpu
 
-import java.io.ByteArrayInputStream
 import java.nio.{ByteBuffer, ByteOrder}
 
 import org.apache.spark.{SparkEnv, TaskContext}
-import org.apache.spark.serializer.KryoSerializer
-import org.apache.spark.shuffle.{BaseShuffleHandle, ShuffleReader}
+import org.apache.spark.shuffle.ShuffleReader
 import org.apache.spark.storage.ShuffleBlockId
-import org.apache.spark.util.CompletionIterator
-import org.apache.spark.util.collection.{CompactBuffer, ExternalSorter}
+import org.apache.spark.util.collection.CompactBuffer
 
 class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], startPartition: Int,
                              endPartition: Int, context: TaskContext,
-                             coordinator: Option[GpuExchangeCoordinator]) extends ShuffleReader[K, C] {
+                             coordinator: Option[GpuExchangeCoordinator],
+                             mapRange: Option[(Int, Int)] = None) extends ShuffleReader[K, C] {
   private val dep = handle.dependency
   private val shuffleId = handle.shuffleId
 
-  private def mapIds: Array[Long] =
-    SparkEnv.get.mapOutputTracker
-      .getMapSizesByExecutorId(shuffleId, startPartition, endPartition)
-      .flatMap(_._2.map(_._1.asInstanceOf[ShuffleBlockId].mapId))
-      .toArray.distinct.sorted
+  private def ids(blocks: Iterator[(_, Seq[(org.apache.spark.storage.BlockId, Long, Int)])]): Array[Long] =
+    blocks.flatMap(_._2.map(_._1.asInstanceOf[ShuffleBlockId].mapId)).toArray.distinct.sorted
+
+  /** The maps this read covers: those the MapOutputTracker lists for the partition range (and,
+   *  for the AQE local reader, getReaderForRange's map index range). */
+  private def mapIds: Array[Long] = mapRange match {
+    case Some((m0, m1)) =>
+      ids(SparkEnv.get.mapOutputTracker.getMapSizesByRange(shuffleId, m0, m1, startPartition, endPartition))
+    case None =>
+      ids(SparkEnv.get.mapOutputTracker.getMapSizesByExecutorId(shuffleId, startPartition, endPartition))
+  }
+
+  /** The shuffle's full map set (every partition): the exchange key every reduce task of the
+   *  stage agrees on, whatever its own range. */
+  private def allMapIds: Array[Long] =
+    ids(SparkEnv.get.mapOutputTracker.getMapSizesByExecutorId(shuffleId, 0, dep.partitioner.numPartitions))
 
   /** A little-endian direct buffer of n bytes (a clear error past 2 GiB, no silent wrap). */
   private def le(n: Long): ByteBuffer = {
@@ -52,7 +59,7 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
 
   override def read(): Iterator[Product2[K, C]] = {
     val maps = mapIds
-    coordinator.foreach(_.awaitExchange(shuffleId, maps))
+    coordinator.foreach(_.awaitExchange(shuffleId, allMapIds, handle.spec))
     val local = coordinator.isEmpty || {
       val Array(r0, r1) = SgxNative.shuffleReducers(engine, shuffleId)
       r0 <= startPartition && endPartition <= r1
@@ -92,48 +99,36 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
     }
   }
 
-  /** Blocks (map, r) of the range from their owners, deserialized and aggregated on the CPU. */
+  /** Reducers this executor does not hold (Spark placed the task here): their raw blocks come
+   *  from the owners over RPC -- one request per owner, its reducers of the range x every map,
+   *  reducer-major (coordinator.fetchRemote, served from the owner's HBM) -- and are imported
+   *  into this executor's engine (SgxNative.importBlocks), so the read runs on this GPU exactly
+   *  as an owner's does: Kryo / LZ4 decode, sort, group, sum.  The reference's "any block from
+   *  anywhere" (spark_3_0/UcxShuffleReader.scala:74-103), without Spark's CPU reader. */
   private def readRemote(maps: Array[Long], coord: GpuExchangeCoordinator): Iterator[Product2[K, C]] = {
-    val owners = coord.rankRanges(shuffleId)
-    val kryo = dep.serializer.isInstanceOf[KryoSerializer]
-    val blocks = (startPartition until endPartition).iterator.flatMap { r =>
-      val rank = owners.collectFirst { case (k, Array(a, b)) if a <= r && r < b => k }
-        .getOrElse(throw new SgxFetchException(s"no executor holds reducer $r of shuffle $shuffleId"))
-      val got = coord.fetchRemote(shuffleId, rank, maps, Array.fill(maps.length)(r))
-      var off = 0
-      maps.indices.iterator.map { i =>
-        val len = got.lengths(i).toInt
-        val block = (ShuffleBlockId(shuffleId, maps(i), r), got.bytes, off, len)
-        off += len
-        block
+    val owners = coord.rankRanges(shuffleId).toSeq.sortBy(_._2(0))
+    val nm = maps.length
+    val lengths = new Array[Long]((endPartition - startPartition) * nm)
+    val pieces = owners.flatMap { case (rank, Array(a, b)) =>
+      val lo = math.max(a, startPartition)
+      val hi = math.min(b, endPartition)
+      if (lo >= hi || nm == 0) None
+      else {
+        val rs = (lo until hi).toArray
+        val got = coord.fetchRemote(shuffleId, rank, rs.flatMap(_ => maps), rs.flatMap(r => Array.fill(nm)(r)))
+        System.arraycopy(got.lengths, 0, lengths, (lo - startPartition) * nm, got.lengths.length)
+        Some(got.bytes)
       }
     }
-    // empty blocks are never opened (Spark's fetcher drops zero-size blocks)
-    val records: Iterator[Product2[Any, Any]] = blocks.filter(_._4 > 0).flatMap { case (id, bytes, off, len) =>
-      if (kryo) {
-        // Spark's own stream: LZ4 (spark.shuffle.compress) then the Kryo deserializer
-        val wrapped = SparkEnv.get.serializerManager.wrapStream(id, new ByteArrayInputStream(bytes, off, len))
-        dep.serializer.newInstance().deserializeStream(wrapped).asKeyValueIterator
-      } else {
-        // the engine's fixed 16 B codec: {key LE, value LE}
-        val b = ByteBuffer.wrap(bytes, off, len).order(ByteOrder.LITTLE_ENDIAN)
-        Iterator.fill(len / 16)((b.getLong, b.getLong))
-      }
-    }
-    val aggregated: Iterator[Product2[K, C]] = dep.aggregator match {
-      case Some(agg) if dep.mapSideCombine =>
-        agg.combineCombinersByKey(records.asInstanceOf[Iterator[Product2[K, C]]], context)
-      case Some(agg) =>
-        agg.asInstanceOf[org.apache.spark.Aggregator[K, Any, C]]
-          .combineValuesByKey(records.asInstanceOf[Iterator[Product2[K, Any]]], context)
-      case None => records.asInstanceOf[Iterator[Product2[K, C]]]
-    }
-    dep.keyOrdering match {
-      case Some(ord: Ordering[K @unchecked]) =>
-        val sorter = new ExternalSorter[K, C, C](context, ordering = Some(ord), serializer = dep.serializer)
-        sorter.insertAll(aggregated)
-        CompletionIterator[Product2[K, C], Iterator[Product2[K, C]]](sorter.iterator, sorter.stop())
-      case None => aggregated
-    }
+    val covered = owners.map { case (_, Array(a, b)) => math.max(0, math.min(b, endPartition) - math.max(a, startPartition)) }.sum
+    if (covered != endPartition - startPartition)
+      throw new SgxFetchException(s"the executors' reducer ranges do not cover [$startPartition, $endPartition) " +
+                                  s"of shuffle $shuffleId")
+    val buf = le(lengths.sum)
+    pieces.foreach(p => buf.put(p))
+    buf.flip()
+    val id = SgxNative.importBlocks(engine, shuffleId, maps, startPartition, endPartition, buf, lengths)
+    // the read copies its results out of HBM before returning: the import can go right after
+    try readOnGpu(maps) finally SgxNative.releaseImport(engine, shuffleId, id)
   }
 }

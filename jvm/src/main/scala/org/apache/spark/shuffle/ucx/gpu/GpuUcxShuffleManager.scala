@@ -15,11 +15,14 @@
  *     combineByKey(...) -- stays on the CPU path instead of being guessed.
  * Everything else falls back to SortShuffleManager's own writer and reader.
  *
+ *   - a compressed Kryo shuffle only with spark.io.compression.codec = lz4 (the GPU frames
+ *     lz4-java's LZ4BlockOutputStream; Spark's own readers unwrap with the configured codec).
+ *
  * registerShuffle runs on the DRIVER (the ShuffleDependency constructor calls it): it only
- * decides, and marks the decision in the handle's type (GpuShuffleHandle).  Each executor
- * registers the shuffle with its own engine on first use (getWriter / getReader), so the
- * engine -- one per executor = per GPU, spark.shuffle.ucx.gpu.device -- never exists on the
- * driver.  The exchange world (RCCL communicator, the collective per shuffle) is set up and
+ * decides, and puts the decision and the engine registration (GpuShuffleSpec) in the handle.
+ * Each executor registers the shuffle with its own engine on first use (getWriter / getReader,
+ * or the shuffle's GpuRunExchange on an executor that runs none of its tasks), so the engine
+ * -- one per executor = per GPU, spark.shuffle.ucx.gpu.device -- never exists on the driver.  The exchange world (RCCL communicator, the collective per shuffle) is set up and
  * driven by GpuExchangeCoordinator.
  */
 package org.apache.spark.shuffle.ucx.gpu
@@ -27,12 +30,23 @@ package org.apache.spark.shuffle.ucx.gpu
 import java.nio.{ByteBuffer, ByteOrder}
 
 import org.apache.spark.{HashPartitioner, Partitioner, RangePartitioner, ShuffleDependency, SparkConf, TaskContext}
+import org.apache.spark.io.CompressionCodec
 import org.apache.spark.serializer.KryoSerializer
 import org.apache.spark.shuffle._
 import org.apache.spark.shuffle.sort.{SortShuffleManager, SortShuffleWriter}
 
-/** A shuffle the GPU runs: same fields as BaseShuffleHandle, plus the declared aggregation. */
-class GpuShuffleHandle[K, V, C](shuffleId: Int, dependency: ShuffleDependency[K, V, C], val agg: Int)
+/** Everything an executor's engine needs to register a GPU shuffle (sgx_register_shuffle and
+ *  the dependency properties), decided once on the driver.  It travels in the handle and in
+ *  every GpuRunExchange, so an executor that never ran a task of the shuffle registers it
+ *  before joining the shuffle's collective (instead of failing it). */
+case class GpuShuffleSpec(shuffleId: Int, numPartitions: Int, kind: Int, bounds: Array[Long], ascending: Boolean,
+                          kryo: Boolean, lz4Block: Int, combineSum: Boolean, writerUnsafe: Boolean,
+                          placementBytes: Boolean)
+
+/** A shuffle the GPU runs: same fields as BaseShuffleHandle, plus the declared aggregation and
+ *  the engine registration. */
+class GpuShuffleHandle[K, V, C](shuffleId: Int, dependency: ShuffleDependency[K, V, C], val agg: Int,
+                                val spec: GpuShuffleSpec)
   extends BaseShuffleHandle[K, V, C](shuffleId, dependency)
 
 object GpuUcxShuffleManager {
@@ -60,7 +74,7 @@ class GpuUcxShuffleManager(conf: SparkConf, isDriver: Boolean) extends SortShuff
     engineCreated = true
     e
   }
-  private[gpu] lazy val coordinator = new GpuExchangeCoordinator(conf, isDriver, () => engine)
+  private[gpu] lazy val coordinator = new GpuExchangeCoordinator(conf, isDriver, () => engine, ensureRegistered)
   if (conf.getInt("spark.shuffle.ucx.gpu.numExecutors", conf.getInt("spark.executor.instances", 1)) > 1)
     coordinator  // start the world's setup (driver endpoint / executor join) right away
   private val registered = new java.util.concurrent.ConcurrentHashMap[Int, java.lang.Boolean]()
@@ -80,54 +94,77 @@ class GpuUcxShuffleManager(conf: SparkConf, isDriver: Boolean) extends SortShuff
     case _ => false
   }
 
+  /** A compressed Kryo shuffle is framed with lz4-java's LZ4BlockOutputStream on the GPU, and
+   *  Spark's own readers (remote reads, SortShuffleManager fallbacks) unwrap blocks with
+   *  spark.io.compression.codec: the GPU path needs that codec to be lz4. */
+  private def codecIsLz4: Boolean =
+    CompressionCodec.getShortName(conf.get("spark.io.compression.codec", CompressionCodec.DEFAULT_COMPRESSION_CODEC)) ==
+      "lz4"
+
   override def registerShuffle[K, V, C](shuffleId: Int, dependency: ShuffleDependency[K, V, C]): ShuffleHandle = {
     val longs = LONG_CLASSES(dependency.keyClassName) && LONG_CLASSES(dependency.valueClassName)
-    val agg = if (longs && gpuPartitioner(dependency.partitioner, dependency)) gpuAgg(shuffleId, dependency) else None
+    val kryo = dependency.serializer.isInstanceOf[KryoSerializer]
+    val codecOk = !kryo || !conf.getBoolean("spark.shuffle.compress", true) || codecIsLz4
+    val agg = if (longs && codecOk && gpuPartitioner(dependency.partitioner, dependency)) gpuAgg(shuffleId, dependency)
+              else None
     agg match {
-      case Some(a) => new GpuShuffleHandle(shuffleId, dependency, a)
+      case Some(a) => new GpuShuffleHandle(shuffleId, dependency, a, specOf(shuffleId, dependency, a))
       case None => super.registerShuffle(shuffleId, dependency)
     }
   }
 
-  /** Executor side, once per shuffle: the shuffle's partitioner, serializer, codec, combine and
-   *  reducer placement in this executor's engine. */
-  private def ensureRegistered(h: GpuShuffleHandle[_, _, _]): Unit = {
-    if (registered.containsKey(h.shuffleId)) return
-    registered.synchronized {  // handles are per-task copies: lock the executor's table
-      if (registered.containsKey(h.shuffleId)) return
-      val dep = h.dependency
-      dep.partitioner match {
-        case p: HashPartitioner =>
-          SgxNative.registerShuffle(engine, h.shuffleId, p.numPartitions, SgxNative.PART_HASH, null, 0, true, 16)
-        case p: RangePartitioner[_, _] =>
-          val bounds = rangeField[Array[_]](p, "rangeBounds").map(_.asInstanceOf[Long])
-          val b = ByteBuffer.allocateDirect(math.max(8, bounds.length * 8)).order(ByteOrder.LITTLE_ENDIAN)
-          bounds.foreach(b.putLong)
-          SgxNative.registerShuffle(engine, h.shuffleId, p.numPartitions, SgxNative.PART_RANGE_I64, b, bounds.length,
-                                    rangeField[Boolean](p, "ascending"), 16)
-      }
-      if (dep.serializer.isInstanceOf[KryoSerializer]) {
-        SgxNative.setSerializer(engine, h.shuffleId, SgxNative.SER_KRYO)
-        if (conf.getBoolean("spark.shuffle.compress", true))
-          SgxNative.setCompression(engine, h.shuffleId, SgxNative.CODEC_LZ4,
-                                   conf.getSizeAsBytes("spark.io.compression.lz4.blockSize", "32k").toInt)
-      }
-      if (dep.mapSideCombine && h.agg == SgxNative.AGG_SUM)
-        SgxNative.setMapSideCombine(engine, h.shuffleId, SgxNative.AGG_SUM)
+  /** Driver side: the engine registration of a GPU shuffle. */
+  private def specOf(shuffleId: Int, dep: ShuffleDependency[_, _, _], agg: Int): GpuShuffleSpec = {
+    val kryo = dep.serializer.isInstanceOf[KryoSerializer]
+    val (kind, bounds, asc) = dep.partitioner match {
+      case _: HashPartitioner => (SgxNative.PART_HASH, Array.empty[Long], true)
+      case p: RangePartitioner[_, _] =>
+        (SgxNative.PART_RANGE_I64, rangeField[Array[_]](p, "rangeBounds").map(_.asInstanceOf[Long]),
+         rangeField[Boolean](p, "ascending"))
+    }
+    GpuShuffleSpec(
+      shuffleId, dep.partitioner.numPartitions, kind, bounds, asc, kryo,
+      if (kryo && conf.getBoolean("spark.shuffle.compress", true))
+        conf.getSizeAsBytes("spark.io.compression.lz4.blockSize", "32k").toInt
+      else 0,
+      dep.mapSideCombine && agg == SgxNative.AGG_SUM,
       // the writer Spark's own handle would run (SortShuffleManager.registerShuffle; the
       // reference's getWriter, spark_3_0/UcxShuffleManager.scala:32-53): UnsafeShuffleWriter for
       // a SerializedShuffleHandle, whose fast spill merge keeps each spill's partition segment
       // as its own LZ4 stream (the batches GpuShuffleWriter appends are its spills)
-      if (!SortShuffleWriter.shouldBypassMergeSort(conf, dep) && SortShuffleManager.canUseSerializedShuffle(dep) &&
-          conf.getBoolean("spark.shuffle.unsafe.fastMergeEnabled", true))
-        SgxNative.setMapWriter(engine, h.shuffleId, SgxNative.WRITER_UNSAFE)
+      !SortShuffleWriter.shouldBypassMergeSort(conf, dep) && SortShuffleManager.canUseSerializedShuffle(dep) &&
+        conf.getBoolean("spark.shuffle.unsafe.fastMergeEnabled", true),
       // reducer placement, fixed by the shuffle's first exchange: "even" (floor(r*P/R)) or
       // "bytes" (ranges balanced on the lengths, for skewed keys)
-      if (conf.get("spark.shuffle.ucx.gpu.reducerPlacement", "even") == "bytes")
-        SgxNative.setReducerPlacement(engine, h.shuffleId, SgxNative.PLACE_BYTES)
-      registered.put(h.shuffleId, true)
+      conf.get("spark.shuffle.ucx.gpu.reducerPlacement", "even") == "bytes")
+  }
+
+  /** Executor side, once per shuffle: the shuffle's partitioner, serializer, codec, combine,
+   *  map writer and reducer placement in this executor's engine -- from a task's handle, or
+   *  from a GpuRunExchange on an executor that has not run a task of the shuffle yet. */
+  private[gpu] def ensureRegistered(sp: GpuShuffleSpec): Unit = {
+    if (registered.containsKey(sp.shuffleId)) return
+    registered.synchronized {  // handles are per-task copies: lock the executor's table
+      if (registered.containsKey(sp.shuffleId)) return
+      if (sp.kind == SgxNative.PART_HASH) {
+        SgxNative.registerShuffle(engine, sp.shuffleId, sp.numPartitions, SgxNative.PART_HASH, null, 0, true, 16)
+      } else {
+        val b = ByteBuffer.allocateDirect(math.max(8, sp.bounds.length * 8)).order(ByteOrder.LITTLE_ENDIAN)
+        sp.bounds.foreach(b.putLong)
+        SgxNative.registerShuffle(engine, sp.shuffleId, sp.numPartitions, sp.kind, b, sp.bounds.length, sp.ascending, 16)
+      }
+      if (sp.kryo) {
+        SgxNative.setSerializer(engine, sp.shuffleId, SgxNative.SER_KRYO)
+        if (sp.lz4Block > 0) SgxNative.setCompression(engine, sp.shuffleId, SgxNative.CODEC_LZ4, sp.lz4Block)
+      }
+      if (sp.combineSum) SgxNative.setMapSideCombine(engine, sp.shuffleId, SgxNative.AGG_SUM)
+      if (sp.writerUnsafe) SgxNative.setMapWriter(engine, sp.shuffleId, SgxNative.WRITER_UNSAFE)
+      if (sp.placementBytes) SgxNative.setReducerPlacement(engine, sp.shuffleId, SgxNative.PLACE_BYTES)
+      registered.put(sp.shuffleId, true)
     }
   }
+
+  private def ensureRegistered(h: GpuShuffleHandle[_, _, _]): Unit = ensureRegistered(h.spec)
 
   override def getWriter[K, V](handle: ShuffleHandle, mapId: Long, context: TaskContext,
                                metrics: ShuffleWriteMetricsReporter): ShuffleWriter[K, V] = handle match {
@@ -145,6 +182,23 @@ class GpuUcxShuffleManager(conf: SparkConf, isDriver: Boolean) extends SortShuff
         new GpuShuffleReader[K, C](engine, h, startPartition, endPartition, context,
                                    if (isWorld) Some(coordinator) else None)
       case _ => super.getReader(handle, startPartition, endPartition, context, metrics)
+    }
+
+  /** Spark 3.0's AQE local shuffle reader reads a map range (startMapIndex, endMapIndex) of a
+   *  partition range.  The reference does not override it, so its local reads bypass UCX
+   *  (SURVEY §8(b)); here a GPU shuffle's map outputs live in HBM (index files only with
+   *  spark.shuffle.ucx.gpu.writeIndexFiles), so the range read goes through the same GPU reader
+   *  restricted to those maps. */
+  override def getReaderForRange[K, C](handle: ShuffleHandle, startMapIndex: Int, endMapIndex: Int,
+                                       startPartition: Int, endPartition: Int, context: TaskContext,
+                                       metrics: ShuffleReadMetricsReporter): ShuffleReader[K, C] =
+    handle match {
+      case h: GpuShuffleHandle[K @unchecked, _, C @unchecked] =>
+        ensureRegistered(h)
+        new GpuShuffleReader[K, C](engine, h, startPartition, endPartition, context,
+                                   if (isWorld) Some(coordinator) else None, Some((startMapIndex, endMapIndex)))
+      case _ => super.getReaderForRange(handle, startMapIndex, endMapIndex, startPartition, endPartition, context,
+                                        metrics)
     }
 
   private def isWorld: Boolean =

@@ -31,9 +31,12 @@ FLAG_LZ4_LANE_DECODE = 16
 FLAG_NO_SPLIT_SCATTER = 32
 FLAG_NO_BUCKET_SORT = 64
 FLAG_ASSUME_LDS_DISORDER = 128
+FLAG_NO_PADDED_MAP = 256
+FLAG_PAD_ANY_SIZE = 512
+LAYOUT_CONTIGUOUS, LAYOUT_PADDED = 0, 1
 PLACE_EVEN, PLACE_BYTES = 0, 1
 WRITER_SORT, WRITER_UNSAFE = 0, 1
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 
 class ShuffleError(RuntimeError):
@@ -116,6 +119,7 @@ SIGNATURES = {
     "sgx_write_map": (ctypes.c_int, [_vp, _i32, _i64, _vp, _i64, _i32, _i32, _vp]),
     "sgx_map_lengths": (ctypes.c_int, [_vp, _i32, _i64, _vp]),
     "sgx_map_data": (ctypes.c_int, [_vp, _i32, _i64, ctypes.POINTER(_vp), _P64]),
+    "sgx_map_layout": (ctypes.c_int, [_vp, _i32, _i64, _P32]),
     "sgx_write_index": (ctypes.c_int, [_vp, _i32, _i64, _cp, _cp, _vp]),
     "sgx_check_index_and_data": (ctypes.c_int, [_cp, _cp, _i32, _vp]),
     "sgx_index_block_range": (ctypes.c_int, [_cp, _i32, _i32, _P64, _P64]),
@@ -124,6 +128,9 @@ SIGNATURES = {
     "sgx_comm_size": (ctypes.c_int, [_vp, _P32, _P32]),
     "sgx_exchange": (ctypes.c_int, [_vp, _i32]),
     "sgx_exchange_maps": (ctypes.c_int, [_vp, _i32, _vp, _i64]),
+    "sgx_exchange_fail": (ctypes.c_int, [_vp, _i32, _i32]),
+    "sgx_import_blocks": (ctypes.c_int, [_vp, _i32, _vp, _i64, _i32, _i32, _vp, _i32, _vp, _P64]),
+    "sgx_release_import": (ctypes.c_int, [_vp, _i32, _i64]),
     "sgx_shuffle_reducers": (ctypes.c_int, [_vp, _i32, _vp, _vp]),
     "sgx_plan_exchange_maps": (ctypes.c_int, [_vp, _vp, _i32, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp]),
     "sgx_fetch_blocks": (ctypes.c_int, [_vp, _i32, _vp, _vp, _i64, _vp, _i64, _i32, _vp]),

@@ -176,7 +176,23 @@ struct MapOut {
     // streaming writes (sgx_map_begin / _append / _commit): the batches so far
     bool open = false;
     std::vector<std::unique_ptr<Spill>> spills;
-    const void *view() const { return comp_valid ? comp.p : (ser.p && ser_valid ? ser.p : data.p); }
+    // Single-pass padded output (sgx_map.cpp padded_pass): `data` holds one
+    // line-aligned sub-bin per (partition, chunk) stream with unwritten gaps between them;
+    // frag = device [fstart][foff][cnt] u32 x R*G: a stream's first record in `data`, its
+    // position in the contiguous layout, its record count.  pad_try: this write ran the
+    // padded kernels (the layout is decided when its lengths land: padded, or -- a sub-bin
+    // overflowed -- rewritten contiguous by the fallback).  Consumers that need contiguous
+    // bytes (view(): exchange sends, map data, index files) use `dense`, built once by
+    // materialize(); fetches gather the fragments directly.
+    bool pad_try = false;
+    bool padded = false;       // valid once `ready`
+    int32_t frag_G = 0;
+    DevBuf frag;
+    DevBuf dense;
+    bool dense_valid = false;
+    const void *view() const {
+        return comp_valid ? comp.p : (ser.p && ser_valid ? ser.p : (padded ? (dense_valid ? dense.p : nullptr) : data.p));
+    }
     bool ser_valid = false;    // `ser` holds this write's Kryo stream
     bool exchanged = false;    // an exchange round carried this write (sgx_exchange skips it)
     ~MapOut() {
@@ -200,6 +216,8 @@ struct Round {
     DevBuf data;                          // receive buffer
     // P == 1 without a communicator: the map outputs themselves ([M], block_off inside each)
     std::vector<std::shared_ptr<MapOut>> alias;
+    // sgx_import_blocks: blocks a reader fetched from elsewhere (0 = an exchange round)
+    int64_t import_id = 0;
     Event done;
     const char *block_ptr(size_t j, int32_t r) const {
         const size_t nmine = (size_t)(r1 - r0);
@@ -227,6 +245,10 @@ struct Shuffle {
     PartParams pp{};
     std::map<int64_t, std::shared_ptr<MapOut>> maps;
     std::vector<std::shared_ptr<Round>> rounds;
+    int64_t next_import = 1;      // sgx_import_blocks ids
+    // a padded write of this shuffle overflowed its sub-bins (keys not spread like the
+    // sample): its later maps take the two-pass path directly
+    std::atomic<bool> pad_failed{false};
     bool configurable() {  // serializer / codec / combine may change until the first write
         std::lock_guard<std::mutex> lk(mu);
         return maps.empty();
@@ -297,6 +319,7 @@ struct sgx_engine {
     int rank_mode = 0;               // sgx_config.rank_mode
     int flags = 0;                   // sgx_config.flags
     bool lds_order_ok = true;        // engine-start check (sgx_create; sgx_lds_order_ok)
+    int64_t pad_min = 1 << 20;       // smallest map written padded (SGX_FLAG_PAD_ANY_SIZE: 1)
     int64_t comm_timeout_ms = 300000;
 
     std::mutex reg_mu;
@@ -344,6 +367,9 @@ int partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_t n, 
                    int32_t R, int32_t kind, uint32_t *host_off, uint32_t *err_slot, bool stats);
 // Lengths / published bytes of a written map (waits for its kernels).  Caller holds m.mu.
 int finish_lengths(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m);
+// A padded map's contiguous copy (m.dense, once; m.done is recorded behind it), so that
+// view() is valid.  No-op for other maps.  Caller holds m.mu and ran finish_lengths.
+int materialize(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m);
 // Look up a map output (shared pointer: stays alive while used).
 int find_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, std::shared_ptr<Shuffle> *ps,
              std::shared_ptr<MapOut> *pm);

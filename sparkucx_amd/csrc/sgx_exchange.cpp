@@ -146,18 +146,31 @@ struct LocalMap {
 // outputs, which are already destination-grouped -- no pack step -- into the receive layout
 // [source rank][its maps][my reducers]; host backend: the same bytes through the caller's
 // all-to-all).
-static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> &s, std::vector<LocalMap> mine) {
-    std::lock_guard<std::mutex> clk(e->comm_mu);
+// Caller holds comm_mu (taken before the maps were selected, so two concurrent exchanges of
+// one shuffle cannot both carry a map).  A rank whose maps fail locally (still open, a
+// failed write) still joins the first all-gather, with an error mark, so every rank fails
+// the round together instead of waiting in a collective for it.
+static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> &s, std::vector<LocalMap> mine,
+                          int local_rc = SGX_OK, std::string local_msg = std::string()) {
     const int32_t P = e->nranks, R = s->R;
     for (auto &lm : mine) {
+        if (local_rc != SGX_OK) break;
         std::lock_guard<std::mutex> lk(lm.m->mu);
-        if (lm.m->open) return fail_msg(SGX_ERR_STATE, "map %lld is still open", (long long)lm.id);
-        SGX_TRY(finish_lengths(e, *c, *s, *lm.m));
+        int rc = lm.m->open ? fail_msg(SGX_ERR_STATE, "map %lld is still open", (long long)lm.id) : SGX_OK;
+        // a padded map is sent from its contiguous copy (sends are contiguous byte ranges)
+        if (rc == SGX_OK) rc = finish_lengths(e, *c, *s, *lm.m);
+        if (rc == SGX_OK) rc = materialize(e, *c, *s, *lm.m);
+        if (rc != SGX_OK) {
+            local_rc = rc;
+            local_msg = sgx_last_error();
+            break;
+        }
         lm.lens = lm.m->lengths;
         lm.bytes = lm.m->out_bytes;
     }
     if (e->comm_broken) return fail_msg(SGX_ERR_STATE, "the communicator was aborted after an exchange failure");
     const bool collective = e->comm || e->host_comm;
+    if (local_rc != SGX_OK && !collective) return fail_msg(local_rc, "%s", local_msg.c_str());
     if (P > 1 && !collective) return fail_msg(SGX_ERR_STATE, "sgx_comm_init was not called (world of %d ranks)", P);
     hipStream_t st = collective ? e->s_comm : c->st;
     hipEvent_t a0 = e->ev(), a1 = e->ev(), a2 = e->ev(), a3 = e->ev();
@@ -177,7 +190,8 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
     } else {
         // first all-gather: [map count | the first map's {id, lengths}] per rank -- the whole
         // round when every rank holds at most one map (the pipelined exchange_maps step)
-        const int64_t nloc = (int64_t)mine.size();
+        // a local failure travels as a negative map count: -1 - (the error code's magnitude)
+        const int64_t nloc = local_rc != SGX_OK ? -1 + (int64_t)local_rc : (int64_t)mine.size();
         std::vector<int64_t> first(1 + row, 0), firsts((1 + row) * (size_t)P, 0);
         first[0] = nloc;
         if (nloc > 0) {
@@ -188,6 +202,11 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
         int64_t mmax = 0;
         for (int32_t j = 0; j < P; ++j) {
             counts[(size_t)j] = firsts[(size_t)j * (1 + row)];
+            if (counts[(size_t)j] < 0) {
+                if (j == e->rank) return fail_msg(local_rc, "%s (every rank fails this exchange)", local_msg.c_str());
+                return fail_msg(SGX_ERR_STATE, "exchange of shuffle %d failed on rank %d (code %lld): every rank fails it",
+                                s->id, j, (long long)(-1 - counts[(size_t)j]));
+            }
             mmax = std::max(mmax, counts[(size_t)j]);
         }
         if (mmax <= 1) {
@@ -265,7 +284,7 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
     {
         std::lock_guard<std::mutex> sl(s->mu);
         for (auto it = s->rounds.begin(); it != s->rounds.end(); ++it) {
-            if ((*it)->map_ids == rd->map_ids) {
+            if ((*it)->import_id == 0 && (*it)->map_ids == rd->map_ids) {
                 if (it->use_count() == 1 && (*it)->alias.empty()) {
                     HIP_TRY((*it)->done.wait_host());
                     rd->data.swap((*it)->data);
@@ -370,7 +389,9 @@ extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id) {
     Ctx *c = e->ctx();
     if (!c) return SGX_ERR_HIP;
     // every committed map output no earlier round carried, in map id order (snapshot now:
-    // the call's place in the caller's program order decides what it carries)
+    // the call's place in the caller's program order decides what it carries), selected under
+    // comm_mu: the round marks them exchanged before another exchange can select
+    std::lock_guard<std::mutex> clk(e->comm_mu);
     std::vector<LocalMap> mine;
     {
         std::lock_guard<std::mutex> sl(s->mu);
@@ -394,13 +415,120 @@ extern "C" int sgx_exchange_maps(sgx_engine *e, int32_t shuffle_id, const int64_
     Ctx *c = e->ctx();
     if (!c) return SGX_ERR_HIP;
     std::vector<LocalMap> mine;
-    for (int64_t i = 0; i < n; ++i) {
+    int rc = SGX_OK;
+    std::string msg;
+    for (int64_t i = 0; i < n && rc == SGX_OK; ++i) {
         std::shared_ptr<Shuffle> s2;
         std::shared_ptr<MapOut> m;
-        SGX_TRY(find_map(e, shuffle_id, map_ids[i], &s2, &m));
-        mine.push_back(LocalMap{map_ids[i], m, {}, 0});
+        rc = find_map(e, shuffle_id, map_ids[i], &s2, &m);
+        if (rc == SGX_OK) mine.push_back(LocalMap{map_ids[i], m, {}, 0});
+        else msg = sgx_last_error();
     }
-    return exchange_round(e, c, s, std::move(mine));
+    // an unknown map still joins the round's first all-gather, marked failed
+    std::lock_guard<std::mutex> clk(e->comm_mu);
+    return exchange_round(e, c, s, std::move(mine), rc, msg);
+}
+
+extern "C" int sgx_exchange_fail(sgx_engine *e, int32_t num_partitions, int32_t code) {
+    sgx::TraceRange trace_("sgx_exchange_fail");
+    if (!e || num_partitions < 1 || code >= 0) return fail_msg(SGX_ERR_INVALID, "sgx_exchange_fail: bad arguments");
+    HIP_TRY(hipSetDevice(e->device));
+    std::lock_guard<std::mutex> clk(e->comm_mu);
+    if (e->comm_broken) return fail_msg(SGX_ERR_STATE, "the communicator was aborted after an exchange failure");
+    if (!(e->comm || e->host_comm)) return fail_msg(code, "this rank failed the exchange before it began");
+    // the round's first all-gather, exactly as exchange_round sizes it ([count | first map's
+    // {id, R lengths}]), with the failure mark a local error puts in the count
+    std::vector<int64_t> first((size_t)num_partitions + 2, 0), all(first.size() * (size_t)e->nranks, 0);
+    first[0] = -1 + (int64_t)code;
+    SGX_TRY(allgather_i64(e, first.data(), first.size(), all.data()));
+    return fail_msg(code, "this rank failed the exchange before it began (every rank fails it)");
+}
+
+// ------------------------------------------------------------------------------------
+// blocks fetched from elsewhere (a reduce task Spark placed off the reducers' owner)
+// ------------------------------------------------------------------------------------
+// The reference's reader takes any block from anywhere (spark_3_0/UcxShuffleReader.scala:
+// 74-103); here a reduce task on an executor that does not own its reducers fetches their
+// raw blocks from the owners (over Spark RPC) and hands them to its own engine, which then
+// runs the reads (sgx_read_records / _sorted / _grouped, sgx_fetch_blocks) over them on the
+// GPU exactly as over exchanged blocks: the import is a round of its own.
+extern "C" int sgx_import_blocks(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, int64_t nmaps,
+                                 int32_t start_partition, int32_t end_partition, const void *data,
+                                 int32_t mem_kind, const int64_t *lengths, int64_t *out_import_id) {
+    sgx::TraceRange trace_("sgx_import_blocks");
+    if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
+    if (!e || !out_import_id || nmaps < 0 || (nmaps > 0 && !map_ids))
+        return fail_msg(SGX_ERR_INVALID, "sgx_import_blocks: bad arguments");
+    if (mem_kind != SGX_MEM_HOST && mem_kind != SGX_MEM_DEVICE)
+        return fail_msg(SGX_ERR_INVALID, "unknown mem_kind %d", mem_kind);
+    std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
+    if (!s) return SGX_ERR_STATE;
+    const int32_t R = s->R;
+    if (start_partition < 0 || end_partition > R || start_partition > end_partition)
+        return fail_msg(SGX_ERR_INVALID, "partition range [%d, %d) outside [0, %d)", start_partition, end_partition, R);
+    const int32_t nmine = end_partition - start_partition;
+    const int64_t nblk = (int64_t)nmine * nmaps;
+    if (nblk > 0 && !lengths) return fail_msg(SGX_ERR_INVALID, "lengths is NULL");
+    {
+        std::vector<int64_t> ids(map_ids, map_ids + nmaps);
+        std::sort(ids.begin(), ids.end());
+        if (std::adjacent_find(ids.begin(), ids.end()) != ids.end())
+            return fail_msg(SGX_ERR_INVALID, "an import lists a map id twice");
+    }
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    auto rd = std::make_shared<Round>();
+    rd->map_ids.assign(map_ids, map_ids + nmaps);
+    rd->src.assign((size_t)nmaps, -1);
+    rd->r0 = start_partition;
+    rd->r1 = end_partition;
+    rd->lens.assign((size_t)nmaps * (size_t)R, 0);
+    rd->block_off.assign((size_t)nblk, 0);
+    // `data` holds the blocks in the canonical order: reducer-major, then map (what
+    // sgx_fetch_blocks returns for the same list)
+    int64_t off = 0;
+    for (int32_t r = 0; r < nmine; ++r)
+        for (int64_t j = 0; j < nmaps; ++j) {
+            const int64_t L = lengths[(size_t)r * nmaps + j];
+            if (L < 0) return fail_msg(SGX_ERR_INVALID, "negative block length");
+            if (s->ser == SGX_SER_FIXED && L % s->rb)
+                return fail_msg(SGX_ERR_INVALID, "block of %lld bytes is not whole %d B records", (long long)L, s->rb);
+            rd->lens[(size_t)j * R + (size_t)(start_partition + r)] = L;
+            rd->block_off[(size_t)j * nmine + (size_t)r] = off;
+            off += L;
+        }
+    if (off > 0 && !data) return fail_msg(SGX_ERR_INVALID, "data is NULL");
+    SGX_TRY(rd->data.ensure((size_t)std::max<int64_t>(off, 16) + 64));  // readers may read 32 B past
+    if (off > 0)
+        HIP_TRY(hipMemcpyAsync(rd->data.p, data, (size_t)off,
+                               mem_kind == SGX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, c->st));
+    HIP_TRY(rd->done.record(c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));  // the caller's buffer may go once this returns
+    std::lock_guard<std::mutex> sl(s->mu);
+    rd->import_id = s->next_import++;
+    *out_import_id = rd->import_id;
+    s->rounds.push_back(std::move(rd));
+    return SGX_OK;
+}
+
+extern "C" int sgx_release_import(sgx_engine *e, int32_t shuffle_id, int64_t import_id) {
+    if (e) e->mutated();
+    if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
+    std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
+    if (!s) return SGX_ERR_STATE;
+    std::shared_ptr<Round> gone;  // freed outside the lock (its destructor waits for readers)
+    {
+        std::lock_guard<std::mutex> sl(s->mu);
+        for (auto it = s->rounds.begin(); it != s->rounds.end(); ++it)
+            if ((*it)->import_id == import_id && import_id != 0) {
+                gone = *it;
+                s->rounds.erase(it);
+                break;
+            }
+    }
+    if (!gone) return fail_msg(SGX_ERR_NOT_FOUND, "shuffle %d has no import %lld", shuffle_id, (long long)import_id);
+    return SGX_OK;
 }
 
 extern "C" int sgx_copy_items(sgx_engine *e, const void *src, void *dst, const int64_t *items, int64_t n_items,
@@ -427,7 +555,7 @@ extern "C" int sgx_round_reducers(sgx_engine *e, int32_t shuffle_id, int64_t map
     if (!s) return SGX_ERR_STATE;
     std::lock_guard<std::mutex> sl(s->mu);
     for (auto it = s->rounds.rbegin(); it != s->rounds.rend(); ++it)
-        for (int64_t m : (*it)->map_ids)
+        for (int64_t m : (*it)->import_id ? std::vector<int64_t>() : (*it)->map_ids)
             if (m == map_id) {
                 *r0 = (*it)->r0;
                 *r1 = (*it)->r1;

@@ -27,7 +27,27 @@ struct PartParams {
     // [2^RDIR_BITS + 1]: dir[j] = first bound whose top bits are >= j), or null when the bounds
     // need the JDK binary search's exact path (duplicates with more than 128 bounds)
     const uint16_t *dir;
+    // ---- single-pass padded map output (sgx_map.cpp padded_pass) ----
+    // guard: non-null -> the kernel (k_hist, k_scatter16_wc) runs only when *guard holds
+    // PAD_OVERFLOW, i.e. it is the two-pass fallback of a padded write whose bins overflowed
+    const uint32_t *guard;
+    // K4 output capacity in records (0 = n): the padded output is larger than the input
+    uint32_t olim;
+    // K4 padded: final record count of every (partition, chunk) stream out [R][G], checked
+    // against pad_cap[p] (the sub-bin capacity of partition p); an overflow sets PAD_OVERFLOW
+    uint32_t *pad_cnt;
+    const uint32_t *pad_cap;
 };
+// Error-word bits shared by the map-side kernels and the engine.
+constexpr uint32_t ERR_SPIN = 1u;          // a look-back spin gave up
+constexpr uint32_t ERR_SCATTER_OOB = 2u;   // a scatter destination was out of range
+constexpr uint32_t PAD_OVERFLOW = 0x100u;  // a padded sub-bin overflowed: the two-pass fallback ran
+// Padded map output: one line in PAD_SAMPLE_STRIDE_MAX (128 B = 8 records) at most is read by
+// the sampled histogram; sub-bin capacity = mu + PAD_SIGMAS * sqrt(a * mu + 16) + 8, rounded up
+// to a whole line (a = 1 + chunk / sampled records: the chunk's own Poisson spread plus the
+// sample's estimation error).
+constexpr int PAD_SAMPLE_STRIDE_MAX = 128;
+constexpr double PAD_SIGMAS = 6.5;
 constexpr int RDIR_BITS = 10;
 constexpr int RDIR_N = (1 << RDIR_BITS) + 1;
 constexpr size_t RDIR_BYTES = ((size_t)RDIR_N * 2 + 15) & ~(size_t)15;
@@ -103,11 +123,30 @@ constexpr int HIST_ATOMIC = 0, HIST_BALLOT = 1;
 hipError_t launch_hist(const void *in, int64_t n, int record_bytes, int64_t chunk, int G,
                        const PartParams &pp, uint32_t *counts, hipStream_t stream, int mode = 0,
                        bool zeroed = false);
-// ticket: zeroed dispatch-order counter; err: sticky error word (bit 0: look-back gave up)
+// ticket: zeroed dispatch-order counter; err: sticky error word (bit 0: look-back gave up);
+// guard: as PartParams::guard
 hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint64_t *status,
                        uint32_t *ticket, uint32_t *err, uint32_t *part_off, int G, int R,
-                       hipStream_t stream);
+                       hipStream_t stream, const uint32_t *guard = nullptr);
 int64_t scan_tiles(int64_t len);
+// Padded map output.  launch_pad_sample: est[p] += records of partition p among
+// every `stride`-th 128 B line (est zeroed by the caller; hash partitioner, 16 B records).
+hipError_t launch_pad_sample(const void *in, int64_t n, int stride, const PartParams &pp, uint32_t *est,
+                             hipStream_t stream);
+// The number of records launch_pad_sample reads (the estimate's denominator).
+int64_t pad_sampled_records(int64_t n, int stride);
+// Sub-bin capacities pcap[p] (records, a multiple of 8) from the sampled counts, and the
+// stream starts fstart[p][g] = pbase[p] + g * pcap[p] (pbase: exclusive scan of G * pcap);
+// a total above olim sets PAD_OVERFLOW in *err_pad.  R <= 1024.
+hipError_t launch_pad_caps(const uint32_t *est, int R, int64_t sampled, int64_t chunk, int G, uint32_t olim,
+                           uint32_t *pcap, uint32_t *fstart, uint32_t *err_pad, hipStream_t stream);
+// Host bound of the padded output's records for any sample (>= every total launch_pad_caps
+// can produce), or -1 when it does not fit 32-bit record offsets.
+int64_t pad_capacity_bound(int64_t n, int R, int64_t chunk, int G, int64_t sampled);
+// Gather of padded fragments: for each block b, fragments g in [0, G) of partition part[b]
+// of a padded map -- src + 16 * fstart[p*G+g], 16 * cnt[p*G+g] bytes -- to
+// dst[b] + 16 * (foff[p*G+g] - foff[p*G]).  desc[b] = {src, fstart, foff, cnt, dst, p | G << 32}.
+hipError_t launch_gather_frags(const int64_t *desc, int64_t nblocks, int G, hipStream_t stream);
 // Two-level split scatter (hash partitioner, power-of-two R > 1024, 16 B records):
 // desc: the level-2 pieces cut from the level-1 offsets (offs1[S][G], u32) -- each piece a
 // run of whole (super, chunk) blocks inside one super-partition, about `target` records --

@@ -296,10 +296,14 @@ __device__ __forceinline__ void hist_body(const char *__restrict__ in, int64_t n
     }
 }
 
-template <int KIND, bool REC16, bool AGG = false, bool LB = true>
+// FB: the histogram of a padded write's two-pass fallback (a no-op unless the padded K4
+// flagged PAD_OVERFLOW in *pp.guard); its own instantiation, so profiles tell it apart
+template <int KIND, bool REC16, bool AGG = false, bool LB = true, bool FB = false>
 __global__ __launch_bounds__(HIST_THREADS) void k_hist(const char *__restrict__ in, int64_t n, int rb,
                                                        int64_t chunk, PartParams pp,
                                                        uint32_t *__restrict__ counts, int G) {
+    if constexpr (FB)
+        if (!(*pp.guard & PAD_OVERFLOW)) return;
     hist_body<KIND, REC16, HIST_UNROLL, HIST_SPLIT, AGG, LB>(in, n, rb, chunk, pp, counts, G);
 }
 
@@ -318,6 +322,16 @@ hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
     }
     const bool r16 = (rb == 16);
     const dim3 grid(G * HIST_SPLIT), block(HIST_THREADS);
+    if (pp.guard) {  // a padded write's fallback: hash partitioner, 16 B records only
+        if (!r16 || pp.kind != SGX_PART_HASH) return hipErrorInvalidValue;
+        if ((pp.R & (pp.R - 1)) == 0)
+            hipLaunchKernelGGL((k_hist<KIND_HASH_POW2, true, false, true, true>), grid, block, lds, stream, p, n, rb,
+                               chunk, pp, counts, G);
+        else
+            hipLaunchKernelGGL((k_hist<SGX_PART_HASH, true, false, true, true>), grid, block, lds, stream, p, n, rb,
+                               chunk, pp, counts, G);
+        return hipGetLastError();
+    }
     if (mode == HIST_BALLOT && r16 && pp.kind == SGX_PART_HASH) {  // wave-aggregated counting
         if ((pp.R & (pp.R - 1)) == 0)
             hipLaunchKernelGGL((k_hist<KIND_HASH_POW2, true, true>), grid, block, lds, stream, p, n, rb, chunk, pp,
@@ -375,11 +389,14 @@ constexpr uint64_t ST_AGG = 1ull << 62, ST_PRE = 2ull << 62, ST_VAL = (1ull << 6
 
 int64_t scan_tiles(int64_t len) { return (len + SCAN_TILE - 1) / SCAN_TILE; }
 
+template <bool FB = false>  // FB: a padded write's fallback scan, a no-op unless *guard has PAD_OVERFLOW
 __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const uint32_t *__restrict__ in,
                                                        uint32_t *__restrict__ out, int64_t len,
                                                        uint64_t *status, uint32_t *ticket, uint32_t *err,
                                                        uint32_t *__restrict__ part_off, int G,
-                                                       int R) {
+                                                       int R, const uint32_t *guard) {
+    if constexpr (FB)
+        if (!(*guard & PAD_OVERFLOW)) return;  // the whole workgroup, before its ticket
     __shared__ uint32_t s_tile, s_prefix_lo;
     __shared__ uint32_t s_wsum[SCAN_THREADS / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -443,10 +460,15 @@ __global__ __launch_bounds__(SCAN_THREADS) void k_scan(const uint32_t *__restric
 }
 
 hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint64_t *status,
-                       uint32_t *ticket, uint32_t *err, uint32_t *part_off, int G, int R, hipStream_t stream) {
+                       uint32_t *ticket, uint32_t *err, uint32_t *part_off, int G, int R, hipStream_t stream,
+                       const uint32_t *guard) {
     const int64_t tiles = scan_tiles(len);
-    hipLaunchKernelGGL(k_scan, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, stream, counts, offs,
-                       len, status, ticket, err, part_off, G, R);
+    if (guard)
+        hipLaunchKernelGGL(k_scan<true>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, stream, counts, offs,
+                           len, status, ticket, err, part_off, G, R, guard);
+    else
+        hipLaunchKernelGGL(k_scan<false>, dim3((unsigned)tiles), dim3(SCAN_THREADS), 0, stream, counts, offs,
+                           len, status, ticket, err, part_off, G, R, guard);
     return hipGetLastError();
 }
 
@@ -1114,7 +1136,12 @@ __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
 // SEG (level 2 of the two-level split, launch_scatter16_seg): the workgroup's records are
 // piece desc[blockIdx.x] = {begin, -, super s, chunk g}, up to the next piece's begin,
 // instead of chunk blockIdx.x, and its R streams start at offs[(s * R + p) * G + g].
-template <int KIND, int WAVES, int NI, int SI, bool SEG = false>
+// MODE (single-pass padded write): 0 the two-pass K4; WC_PADDED the padded K4
+// (streams start at their sub-bins, output capacity pp.olim, final counts to pp.pad_cnt
+// checked against pp.pad_cap); WC_FALLBACK the fallback's K4, a no-op unless *pp.guard holds
+// PAD_OVERFLOW.  Three instantiations, so profiles tell them apart.
+constexpr int WC_PADDED = 1, WC_FALLBACK = 2;
+template <int KIND, int WAVES, int NI, int SI, bool SEG = false, int MODE = 0>
 __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__restrict__ in,
                                                                 u32x4 *__restrict__ out, int64_t n,
                                                                 int64_t chunk, PartParams pp,
@@ -1154,7 +1181,10 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     };
     uint16_t *myrow = rows + (size_t)w * RS;
     uint32_t *myrow32 = (uint32_t *)myrow;
-    const uint32_t n32 = (uint32_t)n;  // n < 2^32 (sgx_write_map)
+    // output capacity in records: n, or the padded output's (every position stays below it)
+    const uint32_t n32 = MODE == WC_PADDED ? pp.olim : (uint32_t)n;  // n < 2^32 (sgx_write_map)
+    if constexpr (MODE == WC_FALLBACK)
+        if (!(*pp.guard & PAD_OVERFLOW)) return;  // the whole workgroup, before any barrier
 
     int g = blockIdx.x;
     int64_t begin = (int64_t)g * chunk, end = min(n, begin + chunk), obase = 0;
@@ -1405,6 +1435,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         atomicAdd(&g_wc_stamps[15], 1ull);
     }
 #endif
+    // padded output: every stream's final count, and whether it stayed inside its sub-bin
+    // (pe is final: every thread passed the last tile's B4, or the prologue's barrier)
+    if constexpr (MODE == WC_PADDED) {
+        bool ovf = false;
+        for (uint32_t p = tid; p < R; p += T) {
+            const int64_t i = (obase + p) * G + g;
+            const uint32_t cnt = pe[p] - offs[i];
+            pp.pad_cnt[i] = cnt;
+            ovf |= cnt > pp.pad_cap[p];
+        }
+        if (ovf) atomicOr(err, PAD_OVERFLOW);
+    }
     if (bad) atomicOr(err, SCATTER_OOB);
 }
 
@@ -1781,8 +1823,8 @@ hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, const uint32_t *
     const unsigned grid = (unsigned)((nb + 255) / 256);
     hipLaunchKernelGGL(k_seg_flags, dim3(grid), dim3(256), 0, stream, offs1, S, G, pieces, total, flags);
     // one "partition" over all blocks: idx = exclusive prefix of the flags, npieces[1] = total
-    hipLaunchKernelGGL(k_scan, dim3((unsigned)scan_tiles(nb)), dim3(SCAN_THREADS), 0, stream, (const uint32_t *)flags,
-                       idx, nb, status, ticket, err, npieces, (int)nb, 1);
+    hipLaunchKernelGGL(k_scan<false>, dim3((unsigned)scan_tiles(nb)), dim3(SCAN_THREADS), 0, stream, (const uint32_t *)flags,
+                       idx, nb, status, ticket, err, npieces, (int)nb, 1, nullptr);
     hipLaunchKernelGGL(k_seg_desc, dim3(grid), dim3(256), 0, stream, offs1, (const uint32_t *)flags,
                        (const uint32_t *)idx, S, G, desc);
     return hipGetLastError();
@@ -2201,14 +2243,15 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
              pp.kind != KIND_KEY_BITS && pp.kind != KIND_HOT_SPLIT) ||
             geo.waves < WC_GEOM_BASE)
             return hipErrorInvalidValue;
-#define SGX_WC_SI(K, W, NI, SI)                                                                  \
+#define SGX_WC_SIM(K, W, NI, SI, M)                                                              \
     do {                                                                                         \
-        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, W, NI, SI>,                   \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, W, NI, SI, false, M>,         \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
-        hipLaunchKernelGGL((k_scatter16_wc<K, W, NI, SI>), dim3(G), dim3(W * 64), geo.lds_bytes,  \
-                           stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, offs, G, err,   \
-                           nullptr, nullptr, (u32x4 *)out2, hot_cap);                            \
+        hipLaunchKernelGGL((k_scatter16_wc<K, W, NI, SI, false, M>), dim3(G), dim3(W * 64),      \
+                           geo.lds_bytes, stream, (const u32x4 *)in, (u32x4 *)out, n, chunk, pp, \
+                           offs, G, err, nullptr, nullptr, (u32x4 *)out2, hot_cap);              \
     } while (0)
+#define SGX_WC_SI(K, W, NI, SI) SGX_WC_SIM(K, W, NI, SI, 0)
         // geometries: 8 waves, NI 12 | 8, SI 16, one workgroup per CU
         const int W = geo.waves - WC_GEOM_BASE;
 #define SGX_WC(K)                                                                                \
@@ -2217,7 +2260,26 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         else if (W == 8 && geo.mbits == 16 && geo.items == 8) SGX_WC_SI(K, 8, 8, 16);            \
         else return hipErrorInvalidValue;                                                        \
     } while (0)
-        if (pp.kind == KIND_DIGIT) {
+        // a padded write's K4 and its fallback's (hash partitioner only)
+        const int mode = pp.pad_cnt ? WC_PADDED : pp.guard ? WC_FALLBACK : 0;
+        if (mode && (pp.kind != SGX_PART_HASH || !(W == 8 && geo.mbits == 16 && (geo.items == 12 || geo.items == 8)) ||
+                     (mode == WC_PADDED && (!pp.pad_cap || !pp.olim))))
+            return hipErrorInvalidValue;
+#define SGX_WC_PAD(K)                                                                            \
+    do {                                                                                         \
+        if (mode == WC_PADDED) {                                                                 \
+            if (geo.items == 12) SGX_WC_SIM(K, 8, 12, 16, WC_PADDED);                           \
+            else SGX_WC_SIM(K, 8, 8, 16, WC_PADDED);                                            \
+        } else {                                                                                 \
+            if (geo.items == 12) SGX_WC_SIM(K, 8, 12, 16, WC_FALLBACK);                         \
+            else SGX_WC_SIM(K, 8, 8, 16, WC_FALLBACK);                                          \
+        }                                                                                        \
+    } while (0)
+        if (mode) {
+            if (pow2) SGX_WC_PAD(KIND_HASH_POW2);
+            else SGX_WC_PAD(SGX_PART_HASH);
+#undef SGX_WC_PAD
+        } else if (pp.kind == KIND_DIGIT) {
             if (pp.R != DIGIT_R) return hipErrorInvalidValue;
             SGX_WC(KIND_DIGIT);
         } else if (pp.kind == KIND_KEY_BITS) {
@@ -2236,6 +2298,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         }
 #undef SGX_WC
 #undef SGX_WC_SI
+#undef SGX_WC_SIM
         return hipGetLastError();
     }
     if (rb == 16 && geo.waves >= ORD_GEOM_BASE) {
@@ -2428,6 +2491,169 @@ hipError_t launch_gather_items(const int64_t *items, int64_t n_items, int align,
         hipLaunchKernelGGL(k_gather_items<4>, dim3((unsigned)n_items), dim3(256), 0, stream, items);
     else
         hipLaunchKernelGGL(k_gather_items<1>, dim3((unsigned)n_items), dim3(256), 0, stream, items);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// Single-pass padded map output.  The two-pass map side reads every record
+// twice (K1+K2's histogram, then K4): 48 B of HBM per 16 B record instead of 32.  The
+// padded write skips the full histogram.  A sampled histogram (one line in `stride`) sizes
+// a sub-bin per (partition, chunk) stream with a Poisson margin; K4 writes every stream from
+// the start of its sub-bin (line-aligned) and reports the streams' true counts; K3 then
+// scans those counts into the index offsets and each stream's place in the contiguous
+// layout.  The output keeps every partition's streams in chunk order, i.e. in input order,
+// with unwritten gaps between them, and is read through the fragment tables
+// (k_gather_frags).  A stream longer than its sub-bin sets PAD_OVERFLOW and the map is
+// redone by the two-pass kernels guarded on that bit, on the same stream.
+// ------------------------------------------------------------------------------------
+constexpr int PAD_SAMPLE_THREADS = 256;
+constexpr int PAD_SAMPLE_UNROLL = 8;
+// few workgroups, many loads each: every workgroup ends with up to R global atomics into the
+// same R counters (2048 workgroups of 4 loads per lane measured 63 µs at C1, mostly that)
+constexpr int PAD_SAMPLE_GRID = 512;
+
+int64_t pad_sampled_records(int64_t n, int stride) {
+    if (n <= 0) return 0;
+    const int64_t nlines = (n + 7) / 8, ns = (nlines + stride - 1) / stride;
+    const int64_t last = (ns - 1) * stride * 8;  // the last sampled line's first record
+    return (ns - 1) * 8 + (n - last < 8 ? n - last : 8);
+}
+
+__global__ __launch_bounds__(PAD_SAMPLE_THREADS) void k_pad_sample(const uint4 *__restrict__ in, int64_t n,
+                                                                   int stride, PartParams pp,
+                                                                   uint32_t *__restrict__ est) {
+    __shared__ uint32_t h[1024];
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t p = tid; p < pp.R; p += PAD_SAMPLE_THREADS) h[p] = 0;
+    __syncthreads();
+    const int64_t nlines = (n + 7) / 8, ns = (nlines + stride - 1) / stride, nt = ns * 8;
+    const int64_t step = (int64_t)gridDim.x * PAD_SAMPLE_THREADS;
+    // sampled slot t = record t & 7 of line (t >> 3) * stride: 8 lanes read one 128 B line
+    for (int64_t t0 = (int64_t)blockIdx.x * PAD_SAMPLE_THREADS + tid; t0 < nt; t0 += step * PAD_SAMPLE_UNROLL) {
+        uint4 r[PAD_SAMPLE_UNROLL];
+        bool ok[PAD_SAMPLE_UNROLL];
+#pragma unroll
+        for (int u = 0; u < PAD_SAMPLE_UNROLL; ++u) {
+            const int64_t t = t0 + u * step;
+            const int64_t i = (t >> 3) * stride * 8 + (t & 7);
+            ok[u] = t < nt && i < n;
+            r[u] = ok[u] ? in[i] : uint4{0, 0, 0, 0};
+        }
+#pragma unroll
+        for (int u = 0; u < PAD_SAMPLE_UNROLL; ++u)
+            if (ok[u]) atomicAdd(&h[hash_pid(r[u].x, r[u].y, pp)], 1u);
+    }
+    __syncthreads();
+    for (uint32_t p = tid; p < pp.R; p += PAD_SAMPLE_THREADS)
+        if (h[p]) atomicAdd(&est[p], h[p]);
+}
+
+hipError_t launch_pad_sample(const void *in, int64_t n, int stride, const PartParams &pp, uint32_t *est,
+                             hipStream_t stream) {
+    if (pp.R > 1024 || stride < 1) return hipErrorInvalidValue;
+    if (n <= 0) return hipSuccess;
+    const int64_t nt = pad_sampled_records(n, stride) + 8;
+    const int64_t per = (int64_t)PAD_SAMPLE_THREADS * PAD_SAMPLE_UNROLL;
+    const int64_t want = (nt + per - 1) / per;
+    const int grid = (int)(want < 1 ? 1 : want > PAD_SAMPLE_GRID ? PAD_SAMPLE_GRID : want);
+    hipLaunchKernelGGL(k_pad_sample, dim3(grid), dim3(PAD_SAMPLE_THREADS), 0, stream, (const uint4 *)in, n, stride,
+                       pp, est);
+    return hipGetLastError();
+}
+
+constexpr int PAD_CAPS_THREADS = 1024;
+
+__global__ __launch_bounds__(PAD_CAPS_THREADS) void k_pad_caps(const uint32_t *__restrict__ est, int R, double scale,
+                                                               double a, int G, uint32_t olim,
+                                                               uint32_t *__restrict__ pcap,
+                                                               uint32_t *__restrict__ fstart, uint32_t *err_pad) {
+    __shared__ uint64_t s_x[PAD_CAPS_THREADS];
+    __shared__ uint32_t s_cap[PAD_CAPS_THREADS];
+    const int tid = (int)threadIdx.x;
+    uint32_t cap = 0;
+    if (tid < R) {
+        const double mu = (double)est[tid] * scale;
+        const double c = mu + PAD_SIGMAS * sqrt(a * mu + 16.0) + 8.0;
+        cap = ((uint32_t)ceil(c) + 7u) & ~7u;
+    }
+    s_cap[tid] = cap;
+    s_x[tid] = (uint64_t)cap * (uint64_t)G;
+    __syncthreads();
+    // inclusive scan (Hillis-Steele over R <= 1024 entries, 64-bit: a total above olim is
+    // detected, not wrapped)
+    for (int d = 1; d < PAD_CAPS_THREADS; d <<= 1) {
+        const uint64_t y = tid >= d ? s_x[tid - d] : 0ull;
+        __syncthreads();
+        s_x[tid] += y;
+        __syncthreads();
+    }
+    if (blockIdx.x == 0) {
+        if (tid < R) pcap[tid] = cap;
+        if (tid == 0 && s_x[R - 1] > (uint64_t)olim) atomicOr(err_pad, PAD_OVERFLOW);
+    }
+    // this workgroup's partitions [p0, p1): fstart[p*G + g] = base[p] + g * cap[p] (coalesced)
+    const int per = (R + (int)gridDim.x - 1) / (int)gridDim.x;
+    const int p0 = min(R, (int)blockIdx.x * per), p1 = min(R, p0 + per);
+    for (int64_t i = (int64_t)p0 * G + tid; i < (int64_t)p1 * G; i += PAD_CAPS_THREADS) {
+        const int p = (int)(i / G), g = (int)(i - (int64_t)p * G);
+        const uint64_t base = s_x[p] - (uint64_t)s_cap[p] * (uint64_t)G;
+        fstart[i] = (uint32_t)min<uint64_t>(base + (uint64_t)g * s_cap[p], (uint64_t)olim);
+    }
+}
+
+hipError_t launch_pad_caps(const uint32_t *est, int R, int64_t sampled, int64_t chunk, int G, uint32_t olim,
+                           uint32_t *pcap, uint32_t *fstart, uint32_t *err_pad, hipStream_t stream) {
+    if (R < 1 || R > PAD_CAPS_THREADS || sampled < 1 || G < 1) return hipErrorInvalidValue;
+    const double scale = (double)chunk / (double)sampled, a = 1.0 + scale;
+    const int grid = min(R, 64);
+    hipLaunchKernelGGL(k_pad_caps, dim3(grid), dim3(PAD_CAPS_THREADS), 0, stream, est, R, scale, a, G, olim, pcap,
+                       fstart, err_pad);
+    return hipGetLastError();
+}
+
+int64_t pad_capacity_bound(int64_t n, int R, int64_t chunk, int G, int64_t sampled) {
+    if (n <= 0 || sampled < 1) return -1;
+    // cap[p] <= mu[p] + k sqrt(a mu[p] + 16) + 16, sum mu = chunk, and by Cauchy-Schwarz
+    // sum sqrt(a mu + 16) <= sqrt(R (a chunk + 16 R))
+    const double a = 1.0 + (double)chunk / (double)sampled;
+    const double per = (double)chunk + PAD_SIGMAS * sqrt((double)R * (a * (double)chunk + 16.0 * R)) + 16.0 * R;
+    const double total = (double)G * per + 1024.0;
+    if (total >= 4294967040.0) return -1;
+    return (int64_t)total;
+}
+
+constexpr int FRAG_THREADS = 256;
+
+__global__ __launch_bounds__(FRAG_THREADS) void k_gather_frags(const int64_t *__restrict__ desc, int64_t nblocks) {
+    const uint32_t g = blockIdx.x, tid = threadIdx.x;
+    for (int64_t b = blockIdx.y; b < nblocks; b += gridDim.y) {
+        const int64_t *d = desc + 6 * b;
+        const uint64_t pg = (uint64_t)d[5];
+        const uint32_t p = (uint32_t)pg, G = (uint32_t)(pg >> 32);
+        if (g >= G) continue;
+        const uint32_t *fstart = (const uint32_t *)(uintptr_t)d[1];
+        const uint32_t *foff = (const uint32_t *)(uintptr_t)d[2];
+        const uint32_t *cnt = (const uint32_t *)(uintptr_t)d[3];
+        const int64_t i = (int64_t)p * G + g;
+        const uint32_t c = cnt[i];
+        const uint4 *s = (const uint4 *)(uintptr_t)d[0] + fstart[i];
+        uint4 *o = (uint4 *)(uintptr_t)d[4] + (foff[i] - foff[(int64_t)p * G]);
+        uint32_t k = tid;
+        for (; k + 3 * FRAG_THREADS < c; k += 4 * FRAG_THREADS) {
+            const uint4 v0 = s[k], v1 = s[k + FRAG_THREADS], v2 = s[k + 2 * FRAG_THREADS], v3 = s[k + 3 * FRAG_THREADS];
+            o[k] = v0;
+            o[k + FRAG_THREADS] = v1;
+            o[k + 2 * FRAG_THREADS] = v2;
+            o[k + 3 * FRAG_THREADS] = v3;
+        }
+        for (; k < c; k += FRAG_THREADS) o[k] = s[k];
+    }
+}
+
+hipError_t launch_gather_frags(const int64_t *desc, int64_t nblocks, int G, hipStream_t stream) {
+    if (nblocks <= 0 || G <= 0) return hipSuccess;
+    const dim3 grid((unsigned)G, (unsigned)(nblocks < 65535 ? nblocks : 65535));
+    hipLaunchKernelGGL(k_gather_frags, grid, dim3(FRAG_THREADS), 0, stream, desc, nblocks);
     return hipGetLastError();
 }
 

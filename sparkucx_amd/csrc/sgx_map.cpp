@@ -199,6 +199,145 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     return SGX_OK;
 }
 
+// ------------------------------------------------------------------------------------
+// single-pass padded write
+// ------------------------------------------------------------------------------------
+// Whether the map is written padded: hash partitioner, 16 B fixed-codec records, R within the
+// write-combining K4 (<= 1024), the default kernels, no multi-rank communicator (an exchange
+// sends contiguous bytes: a padded map would need its contiguous copy first), big enough for
+// the skipped histogram to matter, and no earlier overflow in this shuffle.
+static bool use_padded(sgx_engine *e, const Shuffle &s, int64_t n) {
+    if (s.rb != 16 || s.kind != SGX_PART_HASH || s.R < 2 || s.ser != SGX_SER_FIXED || s.combine != -1) return false;
+    if (e->flags & (SGX_FLAG_NO_PADDED_MAP | SGX_FLAG_NO_WRITE_COMBINING)) return false;
+    if (e->rank_mode != SGX_RANK_ORDERED || !e->lds_order_ok || e->sc_waves || e->sc_items) return false;
+    if (e->nranks > 1 || n < e->pad_min || s.pad_failed.load()) return false;
+    return scatter_geom16_wc((uint32_t)s.R).items != 0;
+}
+
+// The map's geometry: chunk / G exactly as partition_pass cuts them (the fallback's kernels
+// and the padded kernels share it), the sample stride and the output capacity.
+struct PadGeom {
+    ScatterGeom geo;
+    int64_t chunk = 0, sampled = 0, olim = -1;
+    int G = 0, stride = 1;
+};
+
+static PadGeom pad_geom(sgx_engine *e, int32_t R, int64_t n) {
+    PadGeom pg;
+    pg.geo = scatter_geom16_wc((uint32_t)R);
+    const int tile = pg.geo.tile;
+    int64_t chunk = n > 0 ? (n + e->G - 1) / e->G : 1;
+    pg.chunk = (chunk + tile - 1) / tile * tile;
+    pg.G = n > 0 ? (int)((n + pg.chunk - 1) / pg.chunk) : 1;
+    // about 2^16 sampled lines or more, one line in PAD_SAMPLE_STRIDE_MAX at most (C1: one
+    // 128 B line in 128, 34 MB of the 4.3 GB map)
+    pg.stride = (int)std::min<int64_t>(PAD_SAMPLE_STRIDE_MAX, std::max<int64_t>(1, ((n + 7) / 8) >> 16));
+    pg.sampled = pad_sampled_records(n, pg.stride);
+    pg.olim = pad_capacity_bound(n, R, pg.chunk, pg.G, pg.sampled);
+    return pg;
+}
+
+// sample -> sub-bin capacities -> K4 into the sub-bins (final counts out) -> K3 over the
+// counts (contiguous positions + index offsets), then the two-pass K1+K2 -> K3 -> K4 into the
+// same buffer, every kernel of it guarded on the padded K4's overflow bit (a no-op launch
+// otherwise).  Asynchronous on the context's stream; (R+1) offsets, the error word and the
+// padded K4's flag word land in m.part_off.
+static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n,
+                       const PadGeom &pg) {
+    hipStream_t st = c.st;
+    const int32_t R = s.R;
+    const int G = pg.G;
+    const int64_t len = (int64_t)R * G, tiles = scan_tiles(len);
+    const uint32_t olim = (uint32_t)pg.olim;
+    SGX_TRY(m.data.ensure((size_t)olim * 16));
+    SGX_TRY(m.frag.ensure((size_t)len * 12 + 16));
+    uint32_t *fstart = (uint32_t *)m.frag.p, *foff = fstart + len, *cnt = foff + len;
+    SGX_TRY(c.offs.ensure((size_t)len * 4));
+    // one work block, one memset: [fallback counts R*G][fallback ticket | status]
+    // [offsets R+1 | error | padded flags][padded scan ticket | status][est R][pcap R]
+    const size_t counts_bytes = ((size_t)len * 4 + 15) & ~(size_t)15;
+    const size_t status_bytes = ((size_t)(16 + tiles * 8) + 15) & ~(size_t)15;
+    const size_t off_bytes = ((size_t)(R + 3) * 4 + 15) & ~(size_t)15;
+    const size_t rbytes = ((size_t)R * 4 + 15) & ~(size_t)15;
+    const size_t work_bytes = counts_bytes + 2 * status_bytes + off_bytes + 2 * rbytes;
+    SGX_TRY(c.work.ensure(work_bytes));
+    char *w = (char *)c.work.p;
+    uint32_t *counts_fb = (uint32_t *)w;
+    uint32_t *ticket_fb = (uint32_t *)(w + counts_bytes);
+    uint64_t *status_fb = (uint64_t *)((char *)ticket_fb + 16);
+    uint32_t *part_off_dev = (uint32_t *)(w + counts_bytes + status_bytes);
+    uint32_t *err = part_off_dev + R + 1, *err_pad = part_off_dev + R + 2;
+    uint32_t *ticket_pad = (uint32_t *)((char *)part_off_dev + off_bytes);
+    uint64_t *status_pad = (uint64_t *)((char *)ticket_pad + 16);
+    uint32_t *est = (uint32_t *)((char *)ticket_pad + status_bytes);
+    uint32_t *pcap = (uint32_t *)((char *)est + rbytes);
+    c.last_off_dev = part_off_dev;
+    HIP_TRY(hipMemsetAsync(c.work.p, 0, work_bytes, st));
+    hipEvent_t h0 = e->ev(), h1 = e->ev(), c1 = e->ev(), x1 = e->ev();
+    HIP_TRY(hipEventRecord(h0, st));
+    HIP_TRY(launch_pad_sample(in, n, pg.stride, s.pp, est, st));
+    HIP_TRY(launch_pad_caps(est, R, pg.sampled, pg.chunk, G, olim, pcap, fstart, err_pad, st));
+    SGX_TRY(debug_sync(e, st, "padded sample / capacities"));
+    HIP_TRY(hipEventRecord(h1, st));
+    PartParams kp = s.pp;
+    kp.mbits = (uint32_t)pg.geo.mbits;
+    kp.olim = olim;
+    kp.pad_cnt = cnt;
+    kp.pad_cap = pcap;
+    HIP_TRY(launch_scatter(in, m.data.p, n, 16, pg.chunk, G, kp, fstart, pg.geo, err_pad, st));
+    SGX_TRY(debug_sync(e, st, "K4 padded scatter"));
+    HIP_TRY(hipEventRecord(c1, st));
+    HIP_TRY(launch_scan(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, st));
+    // the two-pass fallback, each kernel a no-op unless *err_pad has PAD_OVERFLOW
+    PartParams fp = s.pp;
+    fp.guard = err_pad;
+    HIP_TRY(launch_hist(in, n, 16, pg.chunk, G, fp, counts_fb, st, e->hist_mode, true));
+    HIP_TRY(launch_scan(counts_fb, (uint32_t *)c.offs.p, len, status_fb, ticket_fb, err, part_off_dev, G, R, st,
+                        err_pad));
+    fp.mbits = (uint32_t)pg.geo.mbits;
+    HIP_TRY(launch_scatter(in, m.data.p, n, 16, pg.chunk, G, fp, (const uint32_t *)c.offs.p, pg.geo, err, st));
+    SGX_TRY(debug_sync(e, st, "padded scan / fallback"));
+    HIP_TRY(hipEventRecord(x1, st));
+    HIP_TRY(hipMemcpyAsync(m.part_off.p, part_off_dev, (size_t)(R + 3) * 4, hipMemcpyDeviceToHost, st));
+    // stages: the sampled histogram stands where K1+K2 do, the scans (and the no-op fallback
+    // launches) where K3 does
+    e->record_stage(SGX_STAGE_HIST, h0, h1);
+    e->record_stage(SGX_STAGE_SCATTER, h1, c1);
+    e->record_stage(SGX_STAGE_SCAN, c1, x1);
+    m.pad_try = true;
+    m.frag_G = G;
+    return SGX_OK;
+}
+
+int sgx::materialize(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
+    if (!m.padded || m.dense_valid) return SGX_OK;
+    const int32_t R = s.R;
+    const int G = m.frag_G;
+    const uint32_t *po = (const uint32_t *)m.part_off.p;
+    SGX_TRY(m.dense.ensure((size_t)std::max<int64_t>(m.nrec * 16, 16)));
+    std::vector<int64_t> desc((size_t)R * 6);
+    const int64_t len = (int64_t)R * G;
+    const uint32_t *fstart = (const uint32_t *)m.frag.p;
+    for (int32_t p = 0; p < R; ++p) {
+        int64_t *d = &desc[(size_t)p * 6];
+        d[0] = (int64_t)(uintptr_t)m.data.p;
+        d[1] = (int64_t)(uintptr_t)fstart;
+        d[2] = (int64_t)(uintptr_t)(fstart + len);
+        d[3] = (int64_t)(uintptr_t)(fstart + 2 * len);
+        d[4] = (int64_t)(uintptr_t)((char *)m.dense.p + (size_t)po[p] * 16);
+        d[5] = (int64_t)(((uint64_t)(uint32_t)G << 32) | (uint32_t)p);
+    }
+    SGX_TRY(c.items_dev.ensure(desc.size() * 8));
+    HIP_TRY(hipStreamWaitEvent(c.st, m.done.ev, 0));
+    HIP_TRY(hipMemcpyAsync(c.items_dev.p, desc.data(), desc.size() * 8, hipMemcpyHostToDevice, c.st));
+    HIP_TRY(launch_gather_frags((const int64_t *)c.items_dev.p, R, G, c.st));
+    SGX_TRY(debug_sync(e, c.st, "k_gather_frags (contiguous copy)"));
+    HIP_TRY(m.done.record(c.st));
+    HIP_TRY(hipStreamSynchronize(c.st));  // the descriptors are host memory of this frame
+    m.dense_valid = true;
+    return SGX_OK;
+}
+
 // Kryo framing of the partition-contiguous 16 B records just written (sgx_serde.hip), on
 // the context's stream behind the scatter; byte offsets land in m.ser_off (pinned).
 // rec_off_dev: device (R+1) u32 record offsets of m.data.
@@ -266,9 +405,16 @@ static int run_map_pipeline(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const 
     m.ready = false;
     m.ser_valid = false;
     m.comp_valid = false;
+    m.pad_try = m.padded = m.dense_valid = false;
     const uint32_t *rec_off_dev = part_dev;
+    PadGeom pg;
+    if (!partitioned && use_padded(e, s, n)) pg = pad_geom(e, s.R, n);
     if (s.combine == SGX_AGG_SUM) {
         SGX_TRY(combine_sum(e, c, s, m, partitioned ? m.data.p : in, n));
+        rec_off_dev = c.last_off_dev;
+    } else if (!partitioned && pg.olim >= n) {
+        m.nrec = n;
+        SGX_TRY(padded_pass(e, c, s, m, in, n, pg));
         rec_off_dev = c.last_off_dev;
     } else if (!partitioned) {
         m.nrec = n;
@@ -293,6 +439,16 @@ int sgx::finish_lengths(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
     if (!m.written) return fail_msg(SGX_ERR_STATE, "map output was not committed");
     HIP_TRY(m.done.wait_host());
     const uint32_t *po = (const uint32_t *)m.part_off.p;
+    if (m.pad_try) {
+        // the padded write's own flag word: an overflow means the guarded two-pass fallback
+        // rewrote the map contiguous (its errors are in the main word, checked below)
+        const uint32_t fl = po[s.R + 2];
+        const bool ovf = (fl & PAD_OVERFLOW) != 0;
+        if (!ovf && fl) return fail_msg(SGX_ERR_HIP, "internal error: padded scatter flag %#x", fl);
+        m.padded = !ovf;
+        if (ovf) s.pad_failed.store(true);
+        m.pad_try = false;
+    }
     if (po[s.R + 1] & 1u)
         return fail_msg(SGX_ERR_TIMEOUT, "scan look-back spin gave up (device flag %u)", po[s.R + 1]);
     if (po[s.R + 1] & 2u)
@@ -415,7 +571,7 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
     m->open = false;
     m->spills.clear();
     m->seg_spills = 1;
-    SGX_TRY(m->part_off.ensure((size_t)(s->R + 2) * 4));
+    SGX_TRY(m->part_off.ensure((size_t)(s->R + 3) * 4));
     const void *in = nullptr;
     int rc = device_input(*c, records, n * rb, mem_kind, &in);
     if (rc == SGX_OK) rc = run_map_pipeline(e, *c, *s, *m, in, n, false, nullptr);
@@ -472,7 +628,7 @@ extern "C" int sgx_map_append(sgx_engine *e, int32_t shuffle_id, int64_t map_id,
     const void *in = nullptr;
     SGX_TRY(device_input(*c, records, n * rb, mem_kind, &in));
     SGX_TRY(sp->data.ensure((size_t)std::max<int64_t>(n * rb, 16)));
-    SGX_TRY(m->part_off.ensure((size_t)(s->R + 2) * 4));
+    SGX_TRY(m->part_off.ensure((size_t)(s->R + 3) * 4));
     uint32_t *po = (uint32_t *)m->part_off.p;
     SGX_TRY(partition_pass(e, *c, in, sp->data.p, n, rb, s->pp, s->R, s->kind, po, nullptr, true));
     HIP_TRY(hipStreamSynchronize(c->st));
@@ -503,7 +659,7 @@ extern "C" int sgx_map_commit(sgx_engine *e, int32_t shuffle_id, int64_t map_id,
     if (total >= (int64_t)UINT32_MAX)
         return fail_msg(SGX_ERR_INVALID, "map %lld holds %lld records (>= 2^32)", (long long)map_id, (long long)total);
     // merged partition offsets (records): partition-major, batches in append order
-    SGX_TRY(m->part_off.ensure((size_t)(R + 2) * 4));
+    SGX_TRY(m->part_off.ensure((size_t)(R + 3) * 4));
     uint32_t *po = (uint32_t *)m->part_off.p;
     std::vector<int64_t> items;
     int64_t off = 0;
@@ -595,8 +751,23 @@ extern "C" int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, v
     if (!c) return SGX_ERR_HIP;
     std::lock_guard<std::mutex> lk(m->mu);
     SGX_TRY(finish_lengths(e, *c, *s, *m));
+    SGX_TRY(materialize(e, *c, *s, *m));
     *ptr = const_cast<void *>(m->view());
     *bytes = m->out_bytes;
+    return SGX_OK;
+}
+
+extern "C" int sgx_map_layout(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int32_t *out_layout) {
+    if (!e || !out_layout) return fail_msg(SGX_ERR_INVALID, "NULL argument");
+    std::shared_ptr<Shuffle> s;
+    std::shared_ptr<MapOut> m;
+    SGX_TRY(find_map(e, shuffle_id, map_id, &s, &m));
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    std::lock_guard<std::mutex> lk(m->mu);
+    SGX_TRY(finish_lengths(e, *c, *s, *m));
+    *out_layout = m->padded ? SGX_LAYOUT_PADDED : SGX_LAYOUT_CONTIGUOUS;
     return SGX_OK;
 }
 
@@ -615,6 +786,7 @@ extern "C" int sgx_write_index(sgx_engine *e, int32_t shuffle_id, int64_t map_id
     if (!c) return SGX_ERR_HIP;
     std::lock_guard<std::mutex> lk(m->mu);
     SGX_TRY(finish_lengths(e, *c, *s, *m));
+    SGX_TRY(materialize(e, *c, *s, *m));
     std::vector<uint8_t> host((size_t)m->out_bytes);
     if (m->out_bytes) HIP_TRY(hipMemcpy(host.data(), m->view(), (size_t)m->out_bytes, hipMemcpyDeviceToHost));
     return commit_index_files(index_path, data_path, s->R, m->lengths.data(), host.data(), m->out_bytes, out_lengths);

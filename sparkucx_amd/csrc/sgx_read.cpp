@@ -22,6 +22,8 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
         const void *p;
         int64_t len;
         hipEvent_t ready;
+        const MapOut *pad = nullptr;  // a padded map's block: gathered from its fragments
+        int32_t part = 0;
     };
     // snapshot the shuffle's rounds and the maps asked for (references keep them alive)
     std::vector<std::shared_ptr<Round>> rounds;
@@ -35,7 +37,11 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
         }
     }
     std::map<int64_t, std::vector<int64_t>> map_off;  // per local map: partition byte offsets
+    std::map<int64_t, bool> map_pad;                  // per local map: read through its fragments
     std::vector<Src> srcs((size_t)n);
+    // a padded map's fragments are copied 16 B at a time: a destination that is not 16-byte
+    // aligned reads the map's contiguous copy instead
+    const bool dst_al16 = ((uintptr_t)dst & 15) == 0 || dst_mem_kind != SGX_MEM_DEVICE;
     int64_t total = 0;
     for (int64_t i = 0; i < n; ++i) {
         const int64_t mid = map_ids[i];
@@ -62,12 +68,18 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
                     std::lock_guard<std::mutex> lk(m.mu);
                     if (m.open) return fail_msg(SGX_ERR_STATE, "map %lld is still open", (long long)mid);
                     SGX_TRY(finish_lengths(e, c, s, m));
+                    // (only a fill needs the contiguous copy; a size query reads lengths)
+                    if (m.padded && !dst_al16 && dst) SGX_TRY(materialize(e, c, s, m));
                     std::vector<int64_t> o((size_t)s.R + 1, 0);
                     for (int32_t q = 0; q < s.R; ++q) o[(size_t)q + 1] = o[(size_t)q] + m.lengths[(size_t)q];
                     ot = map_off.emplace(mid, std::move(o)).first;
+                    map_pad[mid] = m.padded && !m.dense_valid;
                 }
-                srcs[(size_t)i] = Src{(const char *)m.view() + ot->second[(size_t)r],
-                                      ot->second[(size_t)r + 1] - ot->second[(size_t)r], m.done.ev};
+                const int64_t bl = ot->second[(size_t)r + 1] - ot->second[(size_t)r];
+                if (map_pad[mid])
+                    srcs[(size_t)i] = Src{nullptr, bl, m.done.ev, &m, r};
+                else
+                    srcs[(size_t)i] = Src{(const char *)m.view() + ot->second[(size_t)r], bl, m.done.ev};
                 found = true;
             }
         }
@@ -98,15 +110,39 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
         SGX_TRY(c.gather_stage.ensure((size_t)total));
         gdst = (char *)c.gather_stage.p;
     }
-    int64_t npieces = 0;
-    for (int64_t i = 0; i < n; ++i) npieces += (srcs[(size_t)i].len + ITEM_BYTES - 1) / ITEM_BYTES;
-    SGX_TRY(c.gather_items.ensure((size_t)npieces * 24));
-    SGX_TRY(c.items_dev.ensure((size_t)npieces * 24));
+    int64_t npieces = 0, nfrag = 0;
+    int maxG = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        if (srcs[(size_t)i].pad) {
+            ++nfrag;
+            maxG = std::max(maxG, (int)srcs[(size_t)i].pad->frag_G);
+        } else {
+            npieces += (srcs[(size_t)i].len + ITEM_BYTES - 1) / ITEM_BYTES;
+        }
+    }
+    // [pieces x 3][fragment descriptors x 6], one host-to-device copy
+    const int64_t nwords = npieces * 3 + nfrag * 6;
+    SGX_TRY(c.gather_items.ensure((size_t)nwords * 8));
+    SGX_TRY(c.items_dev.ensure((size_t)nwords * 8));
     // the pinned item list is rewritten only after the previous gather's copy has landed
     HIP_TRY(hipStreamSynchronize(st));
     int64_t *gi = (int64_t *)c.gather_items.p, k = 0, off = 0;
+    int64_t *fd = gi + npieces * 3, nf = 0;
     bool al16 = ((uintptr_t)gdst & 15) == 0, al4 = ((uintptr_t)gdst & 3) == 0;
     for (int64_t i = 0; i < n; ++i) {
+        if (const MapOut *pm = srcs[(size_t)i].pad) {
+            const int64_t len = (int64_t)s.R * pm->frag_G;
+            const uint32_t *fstart = (const uint32_t *)pm->frag.p;
+            int64_t *d = fd + 6 * nf++;
+            d[0] = (int64_t)(uintptr_t)pm->data.p;
+            d[1] = (int64_t)(uintptr_t)fstart;
+            d[2] = (int64_t)(uintptr_t)(fstart + len);
+            d[3] = (int64_t)(uintptr_t)(fstart + 2 * len);
+            d[4] = (int64_t)(uintptr_t)(gdst + off);
+            d[5] = (int64_t)(((uint64_t)(uint32_t)pm->frag_G << 32) | (uint32_t)srcs[(size_t)i].part);
+            off += srcs[(size_t)i].len;
+            continue;
+        }
         const char *sp = (const char *)srcs[(size_t)i].p;
         for (int64_t done = 0; done < srcs[(size_t)i].len; done += ITEM_BYTES, ++k) {
             const int64_t b = std::min<int64_t>(ITEM_BYTES, srcs[(size_t)i].len - done);
@@ -121,9 +157,11 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
     }
     hipEvent_t g0 = e->ev(), g1 = e->ev();
     HIP_TRY(hipEventRecord(g0, st));
-    HIP_TRY(hipMemcpyAsync(c.items_dev.p, gi, (size_t)npieces * 24, hipMemcpyHostToDevice, st));
+    HIP_TRY(hipMemcpyAsync(c.items_dev.p, gi, (size_t)nwords * 8, hipMemcpyHostToDevice, st));
     HIP_TRY(launch_gather_items((const int64_t *)c.items_dev.p, npieces, al16 ? 16 : al4 ? 4 : 1, st));
     SGX_TRY(debug_sync(e, st, "k_gather_items"));
+    HIP_TRY(launch_gather_frags((const int64_t *)c.items_dev.p + npieces * 3, nfrag, maxG, st));
+    SGX_TRY(debug_sync(e, st, "k_gather_frags"));
     HIP_TRY(hipEventRecord(g1, st));
     e->record_stage(SGX_STAGE_REGROUP, g0, g1);
     if (!dev_dst) HIP_TRY(hipMemcpyAsync(dst, gdst, (size_t)total, hipMemcpyDeviceToHost, st));

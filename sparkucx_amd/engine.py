@@ -238,6 +238,13 @@ class ShuffleEngine:
         check(lib().sgx_map_data(self.handle, shuffle_id, map_id, ctypes.byref(p), ctypes.byref(n)), "map_data")
         return int(p.value or 0), int(n.value)
 
+    def map_layout(self, shuffle_id: int, map_id: int) -> int:
+        """LAYOUT_PADDED if the map was written in one pass into padded sub-bins, else
+        LAYOUT_CONTIGUOUS (two-pass write, or the padded write's overflow fallback)."""
+        v = ctypes.c_int32()
+        check(lib().sgx_map_layout(self.handle, shuffle_id, map_id, ctypes.byref(v)), "map_layout")
+        return int(v.value)
+
     def map_output_bytes(self, shuffle_id: int, map_id: int) -> np.ndarray:
         ptr, n = self.map_data(shuffle_id, map_id)
         out = np.empty(n, dtype=np.uint8)
@@ -343,6 +350,11 @@ class ShuffleEngine:
         check(lib().sgx_exchange_maps(self.handle, shuffle_id, m.ctypes.data if len(m) else None, len(m)),
               "exchange")
 
+    def exchange_fail(self, num_partitions: int, code: int = _lib.SGX_ERR_STATE):
+        """Join an exchange round this rank cannot take part in, marked failed (sgx_exchange_fail):
+        every rank's exchange of the round fails together.  Always raises."""
+        check(lib().sgx_exchange_fail(self.handle, num_partitions, code), "exchange_fail")
+
     def fetch_blocks(self, shuffle_id: int, map_ids: Sequence[int], reduce_ids: Sequence[int], dst=None,
                      dst_cap: Optional[int] = None):
         """Copy blocks back to back into ``dst`` (host ndarray, DeviceBuffer or device tensor).
@@ -363,6 +375,28 @@ class ShuffleEngine:
         check(lib().sgx_fetch_blocks(self.handle, shuffle_id, m.ctypes.data, r.ctypes.data, len(m),
                                      ptr if cap else None, cap, kind, lens.ctypes.data), "fetchBlocks")
         return dst, lens
+
+    def import_blocks(self, shuffle_id: int, map_ids: Sequence[int], start_partition: int, end_partition: int,
+                      data, lengths) -> int:
+        """Hand blocks fetched from another executor to this engine (sgx_import_blocks): the
+        blocks (map_ids[j], r), r in [start, end), reducer-major then map, back to back in
+        ``data`` (host ndarray, DeviceBuffer or device tensor), ``lengths`` in the same order.
+        The reads then run over them on this GPU.  Returns the import id (release_import)."""
+        m = np.ascontiguousarray([int(x) for x in map_ids], dtype=np.int64)
+        lens = np.ascontiguousarray(lengths, dtype=np.int64)
+        if len(lens) != len(m) * (end_partition - start_partition):
+            raise _lib.IllegalArgumentException("one length per (reducer, map) block")
+        ptr, nbytes, kind = buffer_arg(data)
+        if int(lens.sum()) > nbytes:
+            raise _lib.IllegalArgumentException("lengths exceed the data buffer")
+        out = ctypes.c_int64(0)
+        check(lib().sgx_import_blocks(self.handle, shuffle_id, m.ctypes.data if len(m) else None, len(m),
+                                      start_partition, end_partition, ptr if nbytes else None, kind,
+                                      lens.ctypes.data if len(lens) else None, ctypes.byref(out)), "import_blocks")
+        return int(out.value)
+
+    def release_import(self, shuffle_id: int, import_id: int):
+        check(lib().sgx_release_import(self.handle, shuffle_id, import_id), "release_import")
 
     def read_sorted(self, shuffle_id: int, map_ids: Sequence[int], start_partition: int, end_partition: int,
                     dst=None) -> np.ndarray:

@@ -331,8 +331,9 @@ class BlockFetchingListener:
 class UcxShuffleClient:
     """BlockStoreClient.fetchBlocks over the engine's HBM-resident blocks
     (spark_3_0/UcxShuffleClient.scala:17-91; Scala edition in jvm/.../GpuShuffleClient.scala).
-    Same signature, same recursive split at spark.shuffle.ucx.maxBlocksPerRequest (default
-    50, :53-58), same "shuffle_<s>_<m>_<r>" ids (:64).  One engine fetch (one gather launch)
+    Same signature, same recursive split in halves (``splitAt(length / 2)``) while a request
+    holds more than spark.shuffle.ucx.maxBlocksPerRequest ids (default 50, :53-58), same
+    "shuffle_<s>_<m>_<r>" ids (:64).  One engine fetch (one gather launch)
     per request instead of one synchronous round trip per block (:17-47); a failed request
     reports onBlockFetchFailure for each of its blocks, which the reference never does
     (:36-40), so Spark's FetchFailed / stage retry runs."""
@@ -341,14 +342,16 @@ class UcxShuffleClient:
         self.transport = transport
         self.maxBlocksPerRequest = int((conf or {}).get("spark.shuffle.ucx.maxBlocksPerRequest", 50))
         self.requests = 0  # engine fetches issued (tests check the split)
+        self.request_sizes: List[int] = []  # block ids per engine fetch, in issue order
 
     def fetchBlocks(self, host: str, port: int, execId: str, blockIds: Sequence[str],
                     listener: BlockFetchingListener, downloadFileManager=None) -> None:
         blockIds = list(blockIds)
         if len(blockIds) > self.maxBlocksPerRequest:
-            for i in range(0, len(blockIds), self.maxBlocksPerRequest):
-                self.fetchBlocks(host, port, execId, blockIds[i:i + self.maxBlocksPerRequest], listener,
-                                 downloadFileManager)
+            # the reference's split (UcxShuffleClient.scala:53-58): halve, recurse on both halves
+            half = len(blockIds) // 2
+            self.fetchBlocks(host, port, execId, blockIds[:half], listener, downloadFileManager)
+            self.fetchBlocks(host, port, execId, blockIds[half:], listener, downloadFileManager)
             return
         if not blockIds:
             return
@@ -358,6 +361,7 @@ class UcxShuffleClient:
             if len(sids) != 1:
                 raise IllegalArgumentException("blocks of one request belong to one shuffle")
             self.requests += 1
+            self.request_sizes.append(len(blockIds))
             data, lens = self.transport.engine.fetch_blocks(sids.pop(), [m for _, m, _ in parsed],
                                                             [r for _, _, r in parsed])
         except _lib.ShuffleError as ex:

@@ -116,6 +116,9 @@ void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchange(JNIEnv *, jclass, 
 void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchangeMaps(JNIEnv *, jclass, jlong, jint, jlongArray);
 void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_setMapWriter(JNIEnv *, jclass, jlong, jint, jint);
 jintArray Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_shuffleReducers(JNIEnv *, jclass, jlong, jint);
+jlong Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_importBlocks(JNIEnv *, jclass, jlong, jint, jlongArray, jint, jint,
+                                                                   jobject, jlongArray);
+void Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchangeFail(JNIEnv *, jclass, jlong, jint);
 
 static obj *jstr(const char *s) {
     obj *o = (obj *)calloc(1, sizeof(obj));
@@ -160,6 +163,24 @@ int fake_fetch_mismatched(int64_t engine) {
     obj *m = new_obj(K_LONGS, 3, 8), *r = new_obj(K_INTS, 2, 4);
     obj *res = (obj *)Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_fetchBlocks(&g_env, NULL, engine, 1, m, r, NULL);
     return res ? res->n : -1;
+}
+
+/* importBlocks of 2 maps x reducers [0, r1) with nlen lengths of 16 B each over a direct
+ * buffer of cap bytes: the import id, or -1 (an exception is pending) */
+int64_t fake_import_blocks(int64_t engine, void *data, int64_t cap, int r1, int nlen) {
+    obj buf = {K_DIRECT, 0, data, cap};
+    obj *m = new_obj(K_LONGS, 2, 8), *l = new_obj(K_LONGS, nlen, 8);
+    ((int64_t *)m->data)[0] = 1;
+    ((int64_t *)m->data)[1] = 2;
+    for (int i = 0; i < nlen; ++i) ((int64_t *)l->data)[i] = 16;
+    const jlong id = Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_importBlocks(&g_env, NULL, engine, 1, m, 0, r1,
+                                                                                   &buf, l);
+    return g_exc_class[0] ? -1 : id;
+}
+
+int fake_exchange_fail(int64_t engine, int R) {
+    Java_org_apache_spark_shuffle_ucx_gpu_SgxNative_exchangeFail(&g_env, NULL, engine, R);
+    return 0;
 }
 
 int fake_exchange(int64_t engine) {

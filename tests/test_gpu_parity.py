@@ -713,7 +713,8 @@ def test_shuffle_client_fetch_blocks_split_and_listener(sgx_lib, oracle_lib):
         lst = Listener()
         client = mgr.shuffleClient
         client.fetchBlocks("localhost", 1338, "1", ids, lst)
-        assert client.requests == 3 and not lst.failed
+        # the reference's recursive halving: 130 -> 65 + 65 -> 32 + 33 + 32 + 33
+        assert client.requests == 4 and client.request_sizes == [32, 33, 32, 33] and not lst.failed
         for b in ids:
             _, m, r = sgx_lib.parse_block_id(b)
             out, counts = outs[m]

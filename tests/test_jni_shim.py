@@ -34,6 +34,9 @@ def shim(sgx_lib, tmp_path_factory):
     L.fake_write_map.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int]
     L.fake_fetch_mismatched.argtypes = [ctypes.c_int64]
     L.fake_exchange.argtypes = [ctypes.c_int64]
+    L.fake_import_blocks.argtypes = [ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+    L.fake_import_blocks.restype = ctypes.c_int64
+    L.fake_exchange_fail.argtypes = [ctypes.c_int64, ctypes.c_int]
     L.fake_exchange_maps.argtypes = [ctypes.c_int64, ctypes.c_int]
     L.fake_set_map_writer.argtypes = [ctypes.c_int64, ctypes.c_int]
     L.fake_shuffle_reducers.argtypes = [ctypes.c_int64, ctypes.c_void_p]
@@ -91,6 +94,23 @@ def test_argument_errors_become_illegal_argument(shim):
     shim.fake_clear()
     r = np.zeros(2, np.int32)
     assert shim.fake_shuffle_reducers(0, r.ctypes.data) == -1
+    assert exc(shim)[0] == "java/lang/IllegalArgumentException"
+    # blocks fetched from the owners (GpuShuffleReader.readRemote): one length per (reducer,
+    # map) block, lengths within the buffer, then the engine's own checks
+    buf = np.zeros(64, np.uint8)
+    for r1, nlen, cap in ((2, 3, 64), (2, 4, 32), (2, 4, 64)):
+        shim.fake_clear()
+        assert shim.fake_import_blocks(0, buf.ctypes.data, cap, r1, nlen) == -1
+        cls, m = exc(shim)
+        assert cls == "java/lang/IllegalArgumentException", (r1, nlen, cap)
+        if (nlen, cap) == (3, 64):
+            assert "one length per" in m
+        elif cap == 32:
+            assert "exceed" in m
+        else:
+            assert "bad arguments" in m  # NULL engine, reported by sgx_import_blocks
+    shim.fake_clear()
+    shim.fake_exchange_fail(0, 8)
     assert exc(shim)[0] == "java/lang/IllegalArgumentException"
     # the handle's map writer (GpuUcxShuffleManager: UnsafeShuffleWriter for a SerializedShuffleHandle)
     for w in (0, 1):
