@@ -336,6 +336,9 @@ struct sgx_engine {
     int32_t nranks = 1, rank = 0;
     sgx::DevBuf ag_send, ag_recv;
     sgx::HostPinned ag_host, x_send, x_recv;
+    // RCCL exchange of a rank holding many small maps: its pieces packed per destination
+    sgx::DevBuf x_pack, x_items_dev;
+    sgx::HostPinned x_items;
     sgx::DevBuf jump_dev;  // XORShiftRandom jump table (built once, read-only after)
     std::mutex jump_mu;
     std::shared_ptr<sgx::PoolState> pool;  // MemoryPool (sgx_pool.cpp), created on first use

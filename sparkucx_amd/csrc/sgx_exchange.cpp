@@ -129,6 +129,17 @@ static int allgather_i64(sgx_engine *e, const int64_t *send, size_t n, int64_t *
     return SGX_OK;
 }
 
+// A source rank holding several maps whose (map, destination) pieces average below this sends
+// ONE packed piece per destination (its pieces gathered on the device first) instead of one
+// RCCL send per (map, destination): Spark executors hold hundreds of map outputs per shuffle,
+// and every point-to-point operation has a fixed cost.  Every rank decides it for every
+// source from the all-gathered lengths, so receivers post matching receives.
+static constexpr int64_t PACK_PIECE_BYTES = 4ll << 20;
+
+static bool packs_sends(int64_t nmaps, int64_t bytes, int32_t P) {
+    return nmaps > 1 && bytes < PACK_PIECE_BYTES * nmaps * (int64_t)P;
+}
+
 namespace {
 struct LocalMap {
     int64_t id;
@@ -321,18 +332,77 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
         for (auto &lm : mine) HIP_TRY(hipStreamWaitEvent(st, lm.m->done.ev, 0));
         HIP_TRY(hipEventRecord(a2, st));
         if (e->comm) {
-            // grouped point-to-point: my sends to d go map after map, and d posts its receives
-            // from me in the same order (it knows my map count and lengths from (1))
+            // every source rank's choice: packed (one piece per destination) or per map
+            std::vector<char> packed((size_t)P, 0);
+            {
+                size_t m = 0;
+                for (int32_t j = 0; j < P; ++j) {
+                    int64_t bytes = 0;
+                    for (int64_t k = 0; k < counts[(size_t)j]; ++k, ++m)
+                        for (int32_t r = 0; r < R; ++r) bytes += lens[m * R + r];
+                    packed[(size_t)j] = packs_sends(counts[(size_t)j], bytes, P) ? 1 : 0;
+                }
+            }
+            const bool pack_mine = packed[(size_t)e->rank] != 0;
+            if (pack_mine && out_total > 0) {
+                // my pieces, [destination][map] at the plan's send displacements, in one gather
+                // launch on the exchange stream (ahead of the sends in stream order)
+                std::vector<int64_t> items;
+                bool al16 = true, al4 = true;
+                SGX_TRY(e->x_pack.ensure((size_t)out_total));
+                for (int32_t d = 0; d < P; ++d) {
+                    int64_t pos = sd[(size_t)d];
+                    for (size_t k = 0; k < mine.size(); ++k) {
+                        int64_t o, l;
+                        piece(k, d, &o, &l);
+                        for (int64_t done = 0; done < l; done += 65536) {
+                            const int64_t b = std::min<int64_t>(65536, l - done);
+                            const uintptr_t src = (uintptr_t)mine[k].m->view() + (uintptr_t)(o + done);
+                            const uintptr_t dst = (uintptr_t)e->x_pack.p + (uintptr_t)(pos + done);
+                            items.push_back((int64_t)src);
+                            items.push_back((int64_t)dst);
+                            items.push_back(b);
+                            al16 = al16 && ((src | dst | (uintptr_t)b) & 15) == 0;
+                            al4 = al4 && ((src | dst | (uintptr_t)b) & 3) == 0;
+                        }
+                        pos += l;
+                    }
+                }
+                const int64_t ni = (int64_t)items.size() / 3;
+                SGX_TRY(e->x_items.ensure(items.size() * 8));
+                SGX_TRY(e->x_items_dev.ensure(items.size() * 8));
+                std::memcpy(e->x_items.p, items.data(), items.size() * 8);
+                HIP_TRY(hipMemcpyAsync(e->x_items_dev.p, e->x_items.p, items.size() * 8, hipMemcpyHostToDevice, st));
+                HIP_TRY(launch_gather_items((const int64_t *)e->x_items_dev.p, ni, al16 ? 16 : al4 ? 4 : 1, st));
+                SGX_TRY(debug_sync(e, st, "exchange send pack"));
+            }
+            // grouped point-to-point: my sends to d go map after map (or as one packed piece),
+            // and d posts its receives from me the same way (it knows my map count and lengths
+            // from (1))
             NCCL_TRY(ncclGroupStart());
-            for (int32_t d = 0; d < P; ++d)
+            for (int32_t d = 0; d < P; ++d) {
+                if (pack_mine) {
+                    if (sc[(size_t)d] > 0)
+                        NCCL_TRY(ncclSend((const char *)e->x_pack.p + sd[(size_t)d], (size_t)sc[(size_t)d], ncclUint8,
+                                          d, e->comm, st));
+                    continue;
+                }
                 for (size_t k = 0; k < mine.size(); ++k) {
                     int64_t o, l;
                     piece(k, d, &o, &l);
                     if (l > 0)
                         NCCL_TRY(ncclSend((const char *)mine[k].m->view() + o, (size_t)l, ncclUint8, d, e->comm, st));
                 }
+            }
             size_t m = 0;
             for (int32_t j = 0; j < P; ++j) {
+                if (packed[(size_t)j]) {
+                    if (rc[(size_t)j] > 0)
+                        NCCL_TRY(ncclRecv((char *)rd->data.p + rdp[(size_t)j], (size_t)rc[(size_t)j], ncclUint8, j,
+                                          e->comm, st));
+                    m += (size_t)counts[(size_t)j];
+                    continue;
+                }
                 int64_t off = rdp[(size_t)j];
                 for (int64_t k = 0; k < counts[(size_t)j]; ++k, ++m) {
                     int64_t l = 0;

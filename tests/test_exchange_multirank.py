@@ -211,6 +211,12 @@ def test_exchange_per_shuffle_uneven_maps(sgx_lib, oracle_lib, tmp_path, codec, 
     run_world(tmp_path, 3, "host", codec, R, n, counts_by_round=[[0, 1, 4], [2, 0, 1]])
 
 
+def test_exchange_spark_map_counts_host_backend(sgx_lib, oracle_lib, tmp_path):
+    """Spark's map counts per executor: 64 maps on one rank, none and 3 on the others, then
+    a second round with 0 / 40 / 1, host backend (three executors sharing the GPU)."""
+    run_world(tmp_path, 3, "host", "fixed", 256, 2_000, counts_by_round=[[64, 0, 3], [0, 40, 1]])
+
+
 def test_exchange_per_shuffle_rank_without_maps_in_every_round(sgx_lib, oracle_lib, tmp_path):
     """A rank that never holds a map still takes part in every round and reads its reducers;
     a round where nobody holds a map is a no-op collective."""
@@ -277,6 +283,9 @@ def test_exchange_rccl_one_gpu_per_rank(sgx_lib, oracle_lib, tmp_path, world):
     uneven = [[k % 3 for k in range(world)], [1] + [0] * (world - 1)]
     run_world(tmp_path, world, "rccl", "kryo+lz4", 200, 50_000, counts_by_round=uneven)
     run_world(tmp_path, world, "rccl", "fixed", 1024, 20_000, counts_by_round=uneven, rb=100)
+    # Spark's map counts: many small maps on some ranks (packed sends), few large on others
+    many = [[64 if k == 0 else (3 if k % 2 else 0) for k in range(world)], [1] * world]
+    run_world(tmp_path, world, "rccl", "kryo+lz4", 200, 3_000, counts_by_round=many)
 
 
 def test_bench_multi_rank_path_rehearsal(tmp_path):

@@ -573,6 +573,34 @@ def test_exchange_single_rank_over_rccl(sgx_lib, oracle_lib):
         assert st.count["alltoall"] >= 1 and st.count["regroup"] >= 1
 
 
+@pytest.mark.parametrize("nmaps,n", [(64, 3_000), (96, 20_001), (3, 600_000)])
+def test_exchange_many_maps_one_rank_over_rccl(sgx_lib, oracle_lib, nmaps, n):
+    """Spark's map counts: one executor holding many map outputs of a shuffle.  Small pieces
+    (64 / 96 maps) go out packed -- one RCCL send per destination, gathered on the device --
+    large ones (3 maps of 600 K records) one send per (map, destination); both land in the
+    same receive layout and every block equals the oracle's, in the canonical order."""
+    R = 512
+    with sgx_lib.ShuffleEngine(device=0) as e:
+        e.comm_init(1, 0, sgx_lib.get_unique_id())
+        e.register_shuffle(1, R)
+        outs = []
+        for m in range(nmaps):
+            recs = oracle_lib.gen_uniform16(n + 37 * m, 500 + m, value_base=m << 32)
+            e.write_map(1, m, recs, len(recs), 16)
+            outs.append(oracle_lib.map_write(recs, R))
+        e.exchange(1)
+        e.sync()
+        seqs = oracle_lib.canonical_reducer_sequences(outs, R, 16)
+        for r0, r1 in ((0, 3), (250, 251), (R - 2, R)):
+            mids = [m for r in range(r0, r1) for m in range(nmaps)]
+            rids = [r for r in range(r0, r1) for _ in range(nmaps)]
+            data, _ = e.fetch_blocks(1, mids, rids)
+            assert np.array_equal(data.reshape(-1, 16), np.concatenate(seqs[r0:r1]))
+        got = e.read_records(1, list(range(nmaps)), 0, R).reshape(-1, 16)
+        assert np.array_equal(got, np.concatenate(seqs))
+        assert e.stats().count["alltoall"] == 1
+
+
 @pytest.mark.parametrize("P", [2, 4, 8])
 def test_regroup_kernel_multi_rank_plan(sgx_lib, oracle_lib, engine, P):
     """Simulate the receive side of a P-rank exchange on one GPU: build each source rank's
