@@ -130,22 +130,25 @@ hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint
                        hipStream_t stream, const uint32_t *guard = nullptr);
 int64_t scan_tiles(int64_t len);
 // Padded map output.  launch_pad_sample: est[p] += records of partition p among
-// every `stride`-th 128 B line (est zeroed by the caller; hash partitioner, 16 B records).
-hipError_t launch_pad_sample(const void *in, int64_t n, int stride, const PartParams &pp, uint32_t *est,
+// every `stride`-th group of 8 records (est zeroed by the caller; hash partitioner over 16 B
+// records, or RangePartitioner over 100 B TeraSort records; R <= 4096).
+hipError_t launch_pad_sample(const void *in, int64_t n, int rb, int stride, const PartParams &pp, uint32_t *est,
                              hipStream_t stream);
 // The number of records launch_pad_sample reads (the estimate's denominator).
 int64_t pad_sampled_records(int64_t n, int stride);
 // Sub-bin capacities pcap[p] (records, a multiple of 8) from the sampled counts, and the
 // stream starts fstart[p][g] = pbase[p] + g * pcap[p] (pbase: exclusive scan of G * pcap);
-// a total above olim sets PAD_OVERFLOW in *err_pad.  R <= 1024.
+// a total above olim sets PAD_OVERFLOW in *err_pad.  R <= 4096.
 hipError_t launch_pad_caps(const uint32_t *est, int R, int64_t sampled, int64_t chunk, int G, uint32_t olim,
                            uint32_t *pcap, uint32_t *fstart, uint32_t *err_pad, hipStream_t stream);
 // Host bound of the padded output's records for any sample (>= every total launch_pad_caps
 // can produce), or -1 when it does not fit 32-bit record offsets.
 int64_t pad_capacity_bound(int64_t n, int R, int64_t chunk, int G, int64_t sampled);
-// Gather of padded fragments: for each block b, fragments g in [0, G) of partition part[b]
-// of a padded map -- src + 16 * fstart[p*G+g], 16 * cnt[p*G+g] bytes -- to
-// dst[b] + 16 * (foff[p*G+g] - foff[p*G]).  desc[b] = {src, fstart, foff, cnt, dst, p | G << 32}.
+// Gather of padded fragments: for each block b, fragments g in [0, G_b) of partition p_b of a
+// padded map of rb-byte records -- src + rb * fstart[p*G+g], rb * cnt[p*G+g] bytes -- to
+// dst + rb * (foff[p*G+g] - foff[p*G]).  desc[b] = {src, fstart, foff, cnt, dst, p, G_b, rb};
+// G = the largest G_b.
+constexpr int FRAG_DESC_WORDS = 8;
 hipError_t launch_gather_frags(const int64_t *desc, int64_t nblocks, int G, hipStream_t stream);
 // Two-level split scatter (hash partitioner, power-of-two R > 1024, 16 B records):
 // desc: the level-2 pieces cut from the level-1 offsets (offs1[S][G], u32) -- each piece a
@@ -160,6 +163,9 @@ hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, const uint32_t *
                            uint32_t *flags, uint32_t *idx, uint64_t *status, uint32_t *ticket, uint32_t *err,
                            uint32_t *npieces, hipStream_t stream);
 // seg_end: device count of the level-1 records the pieces cover (the last piece's end)
+// With pp.pad_cnt (the padded split): one workgroup walks fragments blockIdx.x, + grid, ... of
+// desc ({begin, end, super, chunk} each, *ndesc of them), every fragment's 64 streams starting
+// at offs[(super*Q + q)][chunk] (their sub-bins) and their final counts going to pad_cnt.
 hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
                                 int G, const int64_t *desc, const uint32_t *ndesc, const uint32_t *seg_end, int grid,
                                 const ScatterGeom &geo, uint32_t *err, hipStream_t stream);
@@ -170,12 +176,23 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
 // csum[s][g] = the cold partitions' counts summed per super-partition s and chunk g;
 // cur1[(SPLIT_HOT_CAP + S) x G] = level-1 cursors: a hot stream's final offsets
 // offs[p][g], a cold super's scratch offsets offs1[s][g].
+// counts (optional): per-partition counts to select from instead of the offsets' differences
 hipError_t launch_hot_select(const uint32_t *part_off, int R, int Q, uint16_t *stream_of, int32_t *hot_part,
-                             hipStream_t stream);
+                             hipStream_t stream, const uint32_t *counts = nullptr);
 hipError_t launch_super_counts_cold(const uint32_t *counts, const uint16_t *stream_of, uint32_t *csum, int S, int Q,
                                     int G, hipStream_t stream);
+// pcap / cap1 / capS: the padded split's sub-bin capacities (capS[stream] written when given)
 hipError_t launch_hot_cursors(const uint32_t *offs, const int32_t *hot_part, const uint32_t *offs1, uint32_t *cur1,
-                              int S, int G, hipStream_t stream);
+                              int S, int G, hipStream_t stream, const uint32_t *pcap = nullptr,
+                              const uint32_t *cap1 = nullptr, uint32_t *capS = nullptr);
+// The padded split: est1[s] = cold partitions' sampled counts per super; level 2's
+// fragment list desc[s*G+g] = {begin, end, s, g} of the level-1 scratch sub-bins (cnt1: the
+// level-1 streams' counts, [HOT + S][G]); the hot partitions' final counts from level 1.
+hipError_t launch_cold_super_est(const uint32_t *est, const uint16_t *stream_of, int S, int Q, uint32_t *est1,
+                                 hipStream_t stream);
+hipError_t launch_frag_desc(const uint32_t *fstart1, const uint32_t *cnt1, int S, int G, int64_t *desc,
+                            uint32_t *ndesc, hipStream_t stream);
+hipError_t launch_hot_counts(const uint32_t *cnt1, const int32_t *hot_part, int G, uint32_t *cnt, hipStream_t stream);
 // The sorted read's last step: `in` is ordered by bucket = (P(key) << kbits) | key window
 // bits [kshift, kshift + kbits) (P the shuffle's hash partitioner when use_p, else 0); every
 // bucket is sorted stably by the full key on chip (16 B: signed Long; 100 B: 10-byte

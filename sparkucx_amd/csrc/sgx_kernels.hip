@@ -322,7 +322,20 @@ hipError_t launch_hist(const void *in, int64_t n, int rb, int64_t chunk, int G,
     }
     const bool r16 = (rb == 16);
     const dim3 grid(G * HIST_SPLIT), block(HIST_THREADS);
-    if (pp.guard) {  // a padded write's fallback: hash partitioner, 16 B records only
+    if (pp.guard) {  // a padded write's fallback: hash / 16 B, or TeraSort's range / 100 B
+        if (pp.kind == SGX_PART_RANGE_BYTES10 && !r16) {
+            if (lb) {
+                if (lds > 65536)
+                    (void)hipFuncSetAttribute((const void *)k_hist<SGX_PART_RANGE_BYTES10, false, false, true, true>,
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+                hipLaunchKernelGGL((k_hist<SGX_PART_RANGE_BYTES10, false, false, true, true>), grid, block, lds, stream,
+                                   p, n, rb, chunk, pp, counts, G);
+            } else {
+                hipLaunchKernelGGL((k_hist<SGX_PART_RANGE_BYTES10, false, false, false, true>), grid, block, lds,
+                                   stream, p, n, rb, chunk, pp, counts, G);
+            }
+            return hipGetLastError();
+        }
         if (!r16 || pp.kind != SGX_PART_HASH) return hipErrorInvalidValue;
         if ((pp.R & (pp.R - 1)) == 0)
             hipLaunchKernelGGL((k_hist<KIND_HASH_POW2, true, false, true, true>), grid, block, lds, stream, p, n, rb,
@@ -986,6 +999,9 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_ord(const u32x4 *__
                                                                  int64_t chunk, PartParams pp,
                                                                  const uint32_t *__restrict__ offs,
                                                                  int G, uint32_t *err) {
+    // the two-pass fallback of a padded split write (R > 1024) runs this single pass, a no-op
+    // unless the padded kernels flagged PAD_OVERFLOW
+    if (pp.guard && !(*pp.guard & PAD_OVERFLOW)) return;
     constexpr int T = WAVES * 64;
     constexpr int TILE = WAVES * ITEMS * 64;
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1185,10 +1201,24 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     const uint32_t n32 = MODE == WC_PADDED ? pp.olim : (uint32_t)n;  // n < 2^32 (sgx_write_map)
     if constexpr (MODE == WC_FALLBACK)
         if (!(*pp.guard & PAD_OVERFLOW)) return;  // the whole workgroup, before any barrier
+    uint32_t bad = 0;
 
+    // FRAGS (level 2 of the padded split): the workgroup walks fragments blockIdx.x, +
+    // gridDim.x, ... -- desc[f] = {begin, end, super, chunk} -- every one with fresh streams
+    // at their sub-bins and the last tile flushing; otherwise one chunk / piece
+    constexpr bool FRAGS = SEG && MODE == WC_PADDED;
+    const int64_t nfrag = FRAGS ? (int64_t)*ndesc : 1;
+    for (int64_t frag = FRAGS ? (int64_t)blockIdx.x : 0; frag < nfrag; frag += FRAGS ? (int64_t)gridDim.x : 1) {
+    if (FRAGS && frag != (int64_t)blockIdx.x) __syncthreads();  // the last fragment's drain read the stream state
     int g = blockIdx.x;
     int64_t begin = (int64_t)g * chunk, end = min(n, begin + chunk), obase = 0;
-    if constexpr (SEG) {
+    if constexpr (FRAGS) {
+        const int64_t *d = desc + 4 * frag;
+        begin = d[0];
+        end = d[1];
+        obase = d[2] * (int64_t)R;
+        g = (int)d[3];
+    } else if constexpr (SEG) {
         if (blockIdx.x >= *ndesc) return;  // the whole workgroup, before any barrier
         const int64_t *d = desc + 4 * (int64_t)blockIdx.x;
         begin = d[0];
@@ -1229,7 +1259,6 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     uint64_t st_acc[12] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t st_last = wc_stamp();
 #endif
-    uint32_t bad = 0;
     // ---- drain: the stage's kept region [0, nkeep) into this lane's registers (dk/dpos), the
     //      written region [nkeep, ntot) out as whole lines.
     //      (Draining tile t after tile t+1's ranking, so the wait for t+1's loads does not
@@ -1443,10 +1472,11 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             const int64_t i = (obase + p) * G + g;
             const uint32_t cnt = pe[p] - offs[i];
             pp.pad_cnt[i] = cnt;
-            ovf |= cnt > pp.pad_cap[p];
+            ovf |= cnt > pp.pad_cap[obase + p];
         }
         if (ovf) atomicOr(err, PAD_OVERFLOW);
     }
+    }  // fragments
     if (bad) atomicOr(err, SCATTER_OOB);
 }
 
@@ -1554,11 +1584,18 @@ __host__ __device__ size_t scatter_wide2_lds(uint32_t R, int rb, int kind, int n
            (size_t)8 * rs8(R) * 2 + (size_t)rs8(R) * 8 + (size_t)WIDE2_TR * 4 + 64 * 4;
 }
 
-template <int KIND, int RB>
+// MODE: as k_scatter16_wc's (0, WC_PADDED: streams start at their sub-bins, final counts to
+// pp.pad_cnt checked against pp.pad_cap; WC_FALLBACK: a no-op unless *pp.guard has
+// PAD_OVERFLOW), so TeraSort maps are written in one pass too.
+template <int KIND, int RB, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restrict__ in, uint32_t *__restrict__ out,
                                                           int64_t n, int64_t chunk, PartParams pp,
                                                           const uint32_t *__restrict__ offs, int G,
                                                           uint32_t *err) {
+    if constexpr (MODE == WC_FALLBACK)
+        if (!(*pp.guard & PAD_OVERFLOW)) return;  // the whole workgroup, before any barrier
+    // output capacity in records: n, or the padded output's
+    const uint32_t olim = MODE == WC_PADDED ? pp.olim : (uint32_t)n;
     constexpr int T = 512, W = 8, TR = WIDE2_TR, ITEMS = TR / T;  // 2 records per lane
     constexpr int DW = RB / 4;                                     // dwords per record
     constexpr int NCH = TR * RB / 16;                              // 16 B chunks per full tile
@@ -1704,7 +1741,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
                 const uint2 c = ((const uint2 *)cur)[j];
                 ((uint2 *)dlt)[j] = make_uint2(c.x - lo, c.y - hi);
                 ((uint2 *)cur)[j] = make_uint2(c.x + (tot[i] & 0xFFFFu), c.y + (tot[i] >> 16));
-                bad |= (c.x + (tot[i] & 0xFFFFu) > (uint32_t)n || c.y + (tot[i] >> 16) > (uint32_t)n) ? 1u : 0u;
+                bad |= (c.x + (tot[i] & 0xFFFFu) > olim || c.y + (tot[i] >> 16) > olim) ? 1u : 0u;
             }
         }
         lds_barrier();
@@ -1748,7 +1785,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
             // kernel does, measured slower here: DESIGN.md §6.4)
 #pragma unroll
             for (int q = 0; q < DRB; ++q)
-                if (live[q] && dst[q] < (uint32_t)n) store_piece(v[q], dst[q], pc[q]);
+                if (live[q] && dst[q] < olim) store_piece(v[q], dst[q], pc[q]);
             WC_STAMP(8);  // drain: global stores
         }
         __syncthreads();  // stage / idx reused by the next tile
@@ -1761,6 +1798,16 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
         atomicAdd(&g_wc_stamps[15], 1ull);
     }
 #endif
+    if constexpr (MODE == WC_PADDED) {  // every stream's final count against its sub-bin
+        bool ovf = false;
+        for (uint32_t p = tid; p < R; p += T) {
+            const int64_t i = (int64_t)p * G + g;
+            const uint32_t cnt = cur[p] - offs[i];  // cur[p]: written by this thread or before a barrier
+            pp.pad_cnt[i] = cnt;
+            ovf |= cnt > pp.pad_cap[p];
+        }
+        if (ovf) atomicOr(err, PAD_OVERFLOW);
+    }
     if (bad) atomicOr(err, SCATTER_OOB);
 }
 
@@ -1841,7 +1888,10 @@ hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, const uint32_t *
 // >= SPLIT_HOT_CAP partitions, then the first SPLIT_HOT_CAP of those in id order.
 // One workgroup; R <= 4 * 1024.
 constexpr int HS_THREADS = 1024, HS_PER = 4;
-__global__ __launch_bounds__(HS_THREADS) void k_hot_select(const uint32_t *__restrict__ part_off, int R, int Q,
+// counts: per-partition counts (the padded split's sampled estimate), or null to take them from
+// the partition offsets
+__global__ __launch_bounds__(HS_THREADS) void k_hot_select(const uint32_t *__restrict__ part_off,
+                                                           const uint32_t *__restrict__ counts, int R, int Q,
                                                            uint16_t *__restrict__ stream_of,
                                                            int32_t *__restrict__ hot_part) {
     __shared__ uint32_t s_w[HS_THREADS / 64];
@@ -1852,7 +1902,7 @@ __global__ __launch_bounds__(HS_THREADS) void k_hot_select(const uint32_t *__res
 #pragma unroll
     for (int i = 0; i < HS_PER; ++i) {
         const int p = (int)tid * HS_PER + i;
-        cnt[i] = p < R ? part_off[p + 1] - part_off[p] : 0u;
+        cnt[i] = p < R ? (counts ? counts[p] : part_off[p + 1] - part_off[p]) : 0u;
         mx = max(mx, cnt[i]);
     }
     if (tid < 256) s_hist[tid] = 0;
@@ -1902,9 +1952,73 @@ __global__ __launch_bounds__(HS_THREADS) void k_hot_select(const uint32_t *__res
 }
 
 hipError_t launch_hot_select(const uint32_t *part_off, int R, int Q, uint16_t *stream_of, int32_t *hot_part,
-                             hipStream_t stream) {
+                             hipStream_t stream, const uint32_t *counts) {
     if (R > HS_THREADS * HS_PER) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_hot_select, dim3(1), dim3(HS_THREADS), 0, stream, part_off, R, Q, stream_of, hot_part);
+    hipLaunchKernelGGL(k_hot_select, dim3(1), dim3(HS_THREADS), 0, stream, part_off, counts, R, Q, stream_of,
+                       hot_part);
+    return hipGetLastError();
+}
+
+// ---- the padded split: level 1 into sub-bins (hot partitions: their final
+// sub-bins; cold super-partitions: sub-bins of a scratch buffer), level 2 one (super, chunk)
+// fragment at a time into the cold partitions' final sub-bins.
+// est1[s] = the cold partitions' sampled counts summed per super-partition.
+__global__ __launch_bounds__(256) void k_cold_super_est(const uint32_t *__restrict__ est,
+                                                        const uint16_t *__restrict__ stream_of, int S, int Q,
+                                                        uint32_t *__restrict__ est1) {
+    const int sidx = (int)(blockIdx.x * 256 + threadIdx.x);
+    if (sidx >= S) return;
+    uint32_t acc = 0;
+    for (int q = 0; q < Q; ++q)
+        if (stream_of[sidx * Q + q] >= SPLIT_HOT_CAP) acc += est[sidx * Q + q];
+    est1[sidx] = acc;
+}
+
+hipError_t launch_cold_super_est(const uint32_t *est, const uint16_t *stream_of, int S, int Q, uint32_t *est1,
+                                 hipStream_t stream) {
+    hipLaunchKernelGGL(k_cold_super_est, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, stream, est, stream_of, S, Q,
+                       est1);
+    return hipGetLastError();
+}
+
+// Level 2's work list, one fragment per (super s, chunk g) of the level-1 scratch, s-major:
+// desc[s*G + g] = {begin, end, s, g} (end = begin + the stream's level-1 count); *ndesc = S*G.
+__global__ __launch_bounds__(256) void k_frag_desc(const uint32_t *__restrict__ fstart1,
+                                                   const uint32_t *__restrict__ cnt1, int S, int G,
+                                                   int64_t *__restrict__ desc, uint32_t *__restrict__ ndesc) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i == 0) *ndesc = (uint32_t)((int64_t)S * G);
+    if (i >= (int64_t)S * G) return;
+    const int64_t b = fstart1[i];
+    int64_t *d = desc + 4 * i;
+    d[0] = b;
+    d[1] = b + cnt1[(int64_t)SPLIT_HOT_CAP * G + i];
+    d[2] = i / G;
+    d[3] = i % G;
+}
+
+hipError_t launch_frag_desc(const uint32_t *fstart1, const uint32_t *cnt1, int S, int G, int64_t *desc,
+                            uint32_t *ndesc, hipStream_t stream) {
+    const int64_t n = (int64_t)S * G;
+    hipLaunchKernelGGL(k_frag_desc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, fstart1, cnt1, S, G, desc,
+                       ndesc);
+    return hipGetLastError();
+}
+
+// The hot partitions' final counts, from their level-1 streams (level 2 wrote 0 for them).
+__global__ __launch_bounds__(256) void k_hot_counts(const uint32_t *__restrict__ cnt1,
+                                                    const int32_t *__restrict__ hot_part, int G,
+                                                    uint32_t *__restrict__ cnt) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= (int64_t)SPLIT_HOT_CAP * G) return;
+    const int64_t h = i / G, g = i - h * G;
+    const int32_t p = hot_part[h];
+    if (p >= 0) cnt[(int64_t)p * G + g] = cnt1[i];
+}
+
+hipError_t launch_hot_counts(const uint32_t *cnt1, const int32_t *hot_part, int G, uint32_t *cnt, hipStream_t stream) {
+    const int64_t n = (int64_t)SPLIT_HOT_CAP * G;
+    hipLaunchKernelGGL(k_hot_counts, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, cnt1, hot_part, G, cnt);
     return hipGetLastError();
 }
 
@@ -1928,26 +2042,32 @@ hipError_t launch_super_counts_cold(const uint32_t *counts, const uint16_t *stre
     return hipGetLastError();
 }
 
+// pcap / cap1 / capS (the padded split only): capS[stream] = its sub-bin capacity, a hot
+// stream's partition's (pcap) or a cold super's (cap1)
 __global__ __launch_bounds__(256) void k_hot_cursors(const uint32_t *__restrict__ offs,
                                                      const int32_t *__restrict__ hot_part,
                                                      const uint32_t *__restrict__ offs1, uint32_t *__restrict__ cur1,
-                                                     int S, int G) {
+                                                     int S, int G, const uint32_t *__restrict__ pcap,
+                                                     const uint32_t *__restrict__ cap1, uint32_t *__restrict__ capS) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= (int64_t)(SPLIT_HOT_CAP + S) * G) return;
     const int64_t st = i / G, g = i - st * G;
     if (st < SPLIT_HOT_CAP) {
         const int32_t p = hot_part[st];
         cur1[i] = p >= 0 ? offs[(int64_t)p * G + g] : 0u;
+        if (capS && g == 0) capS[st] = p >= 0 ? pcap[p] : 0u;
     } else {
         cur1[i] = offs1[(st - SPLIT_HOT_CAP) * G + g];
+        if (capS && g == 0) capS[st] = cap1[st - SPLIT_HOT_CAP];
     }
 }
 
 hipError_t launch_hot_cursors(const uint32_t *offs, const int32_t *hot_part, const uint32_t *offs1, uint32_t *cur1,
-                              int S, int G, hipStream_t stream) {
+                              int S, int G, hipStream_t stream, const uint32_t *pcap, const uint32_t *cap1,
+                              uint32_t *capS) {
     const int64_t n = (int64_t)(SPLIT_HOT_CAP + S) * G;
     hipLaunchKernelGGL(k_hot_cursors, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, offs, hot_part, offs1,
-                       cur1, S, G);
+                       cur1, S, G, pcap, cap1, capS);
     return hipGetLastError();
 }
 
@@ -1955,18 +2075,24 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
                                 int G, const int64_t *desc, const uint32_t *ndesc, const uint32_t *seg_end, int grid,
                                 const ScatterGeom &geo, uint32_t *err, hipStream_t stream) {
     if ((pp.R & (pp.R - 1)) != 0) return hipErrorInvalidValue;
-#define SGX_WCS(W, NI, SI)                                                                                   \
+    if (pp.pad_cnt && (!pp.pad_cap || !pp.olim)) return hipErrorInvalidValue;
+#define SGX_WCS(W, NI, SI, M)                                                                                \
     do {                                                                                                     \
-        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<KIND_HASH_POW2, W, NI, SI, true>,            \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<KIND_HASH_POW2, W, NI, SI, true, M>,         \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes);           \
-        hipLaunchKernelGGL((k_scatter16_wc<KIND_HASH_POW2, W, NI, SI, true>), dim3(grid), dim3(W * 64),      \
+        hipLaunchKernelGGL((k_scatter16_wc<KIND_HASH_POW2, W, NI, SI, true, M>), dim3(grid), dim3(W * 64),   \
                            geo.lds_bytes, stream, (const u32x4 *)in, (u32x4 *)out, n, (int64_t)0, pp, offs, G, \
                            err, desc, ndesc, nullptr, 0u, seg_end);                                         \
     } while (0)
     const int W = geo.waves - WC_GEOM_BASE;
-    if (W == 8 && geo.mbits == 16 && geo.items == 12) SGX_WCS(8, 12, 16);
-    else if (W == 8 && geo.mbits == 16 && geo.items == 8) SGX_WCS(8, 8, 16);
-    else return hipErrorInvalidValue;
+    const bool pad = pp.pad_cnt != nullptr;
+    if (W == 8 && geo.mbits == 16 && geo.items == 12) {
+        if (pad) SGX_WCS(8, 12, 16, WC_PADDED); else SGX_WCS(8, 12, 16, 0);
+    } else if (W == 8 && geo.mbits == 16 && geo.items == 8) {
+        if (pad) SGX_WCS(8, 8, 16, WC_PADDED); else SGX_WCS(8, 8, 16, 0);
+    } else {
+        return hipErrorInvalidValue;
+    }
 #undef SGX_WCS
     return hipGetLastError();
 }
@@ -2262,8 +2388,11 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
     } while (0)
         // a padded write's K4 and its fallback's (hash partitioner only)
         const int mode = pp.pad_cnt ? WC_PADDED : pp.guard ? WC_FALLBACK : 0;
-        if (mode && (pp.kind != SGX_PART_HASH || !(W == 8 && geo.mbits == 16 && (geo.items == 12 || geo.items == 8)) ||
-                     (mode == WC_PADDED && (!pp.pad_cap || !pp.olim))))
+        const bool hot_split = pp.kind == KIND_HOT_SPLIT;  // level 1 of the padded split
+        if (mode && ((pp.kind != SGX_PART_HASH && !(hot_split && mode == WC_PADDED)) ||
+                     !(W == 8 && geo.mbits == 16 && (geo.items == 12 || geo.items == 8)) ||
+                     (mode == WC_PADDED && (!pp.pad_cap || !pp.olim)) ||
+                     (hot_split && (!pp.dir || !out2 || pp.dshift > 13))))
             return hipErrorInvalidValue;
 #define SGX_WC_PAD(K)                                                                            \
     do {                                                                                         \
@@ -2276,8 +2405,14 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         }                                                                                        \
     } while (0)
         if (mode) {
-            if (pow2) SGX_WC_PAD(KIND_HASH_POW2);
-            else SGX_WC_PAD(SGX_PART_HASH);
+            if (hot_split) {
+                if (geo.items == 12) SGX_WC_SIM(KIND_HOT_SPLIT, 8, 12, 16, WC_PADDED);
+                else SGX_WC_SIM(KIND_HOT_SPLIT, 8, 8, 16, WC_PADDED);
+            } else if (pow2) {
+                SGX_WC_PAD(KIND_HASH_POW2);
+            } else {
+                SGX_WC_PAD(SGX_PART_HASH);
+            }
 #undef SGX_WC_PAD
         } else if (pp.kind == KIND_DIGIT) {
             if (pp.R != DIGIT_R) return hipErrorInvalidValue;
@@ -2369,13 +2504,23 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
 #undef SGX_SC16
     } else if (rb == 100 && geo.waves == WIDE2_GEOM_TAG) {
         if (((uintptr_t)in & 15) != 0) return hipErrorInvalidValue;
-#define SGX_W2(K)                                                                                \
+#define SGX_W2M(K, M)                                                                            \
     do {                                                                                         \
-        (void)hipFuncSetAttribute((const void *)k_scatter_wide2<K, 100>,                        \
+        (void)hipFuncSetAttribute((const void *)k_scatter_wide2<K, 100, M>,                     \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes); \
-        hipLaunchKernelGGL((k_scatter_wide2<K, 100>), dim3(G), dim3(512), geo.lds_bytes, stream,  \
+        hipLaunchKernelGGL((k_scatter_wide2<K, 100, M>), dim3(G), dim3(512), geo.lds_bytes, stream, \
                            (const u32x4 *)in, (uint32_t *)out, n, chunk, pp, offs, G, err);     \
     } while (0)
+#define SGX_W2(K) SGX_W2M(K, 0)
+        // a padded write's K4 and its fallback's (RangePartitioner over 10-byte keys)
+        const int mode = pp.pad_cnt ? WC_PADDED : pp.guard ? WC_FALLBACK : 0;
+        if (mode) {
+            if (pp.kind != SGX_PART_RANGE_BYTES10 || (mode == WC_PADDED && (!pp.pad_cap || !pp.olim)))
+                return hipErrorInvalidValue;
+            if (mode == WC_PADDED) SGX_W2M(SGX_PART_RANGE_BYTES10, WC_PADDED);
+            else SGX_W2M(SGX_PART_RANGE_BYTES10, WC_FALLBACK);
+            return hipGetLastError();
+        }
         switch (pp.kind) {
         case SGX_PART_HASH:
             if (pow2) SGX_W2(KIND_HASH_POW2); else SGX_W2(SGX_PART_HASH);
@@ -2387,6 +2532,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         default: return hipErrorInvalidValue;
         }
 #undef SGX_W2
+#undef SGX_W2M
     } else {
         if (geo.items == 0 || (rb & 3) != 0 || rb < 12) return hipErrorInvalidValue;
         const char *ic = (const char *)in;
@@ -2511,6 +2657,7 @@ constexpr int PAD_SAMPLE_UNROLL = 8;
 // few workgroups, many loads each: every workgroup ends with up to R global atomics into the
 // same R counters (2048 workgroups of 4 loads per lane measured 63 µs at C1, mostly that)
 constexpr int PAD_SAMPLE_GRID = 512;
+constexpr int PAD_SAMPLE_MAX_R = 4096;
 
 int64_t pad_sampled_records(int64_t n, int stride) {
     if (n <= 0) return 0;
@@ -2519,67 +2666,99 @@ int64_t pad_sampled_records(int64_t n, int stride) {
     return (ns - 1) * 8 + (n - last < 8 ? n - last : 8);
 }
 
-__global__ __launch_bounds__(PAD_SAMPLE_THREADS) void k_pad_sample(const uint4 *__restrict__ in, int64_t n,
+template <int KIND, int RB>
+__global__ __launch_bounds__(PAD_SAMPLE_THREADS) void k_pad_sample(const char *__restrict__ in, int64_t n,
                                                                    int stride, PartParams pp,
                                                                    uint32_t *__restrict__ est) {
-    __shared__ uint32_t h[1024];
+    __shared__ uint32_t h[PAD_SAMPLE_MAX_R];
     const uint32_t tid = threadIdx.x;
     for (uint32_t p = tid; p < pp.R; p += PAD_SAMPLE_THREADS) h[p] = 0;
     __syncthreads();
     const int64_t nlines = (n + 7) / 8, ns = (nlines + stride - 1) / stride, nt = ns * 8;
     const int64_t step = (int64_t)gridDim.x * PAD_SAMPLE_THREADS;
-    // sampled slot t = record t & 7 of line (t >> 3) * stride: 8 lanes read one 128 B line
+    // sampled slot t = record t & 7 of group (t >> 3) * stride of 8 records: 8 lanes read one
+    // 128 B line (16 B records) or 800 B (100 B records)
     for (int64_t t0 = (int64_t)blockIdx.x * PAD_SAMPLE_THREADS + tid; t0 < nt; t0 += step * PAD_SAMPLE_UNROLL) {
-        uint4 r[PAD_SAMPLE_UNROLL];
+        uint32_t x[PAD_SAMPLE_UNROLL], y[PAD_SAMPLE_UNROLL], z[PAD_SAMPLE_UNROLL];
         bool ok[PAD_SAMPLE_UNROLL];
 #pragma unroll
         for (int u = 0; u < PAD_SAMPLE_UNROLL; ++u) {
             const int64_t t = t0 + u * step;
             const int64_t i = (t >> 3) * stride * 8 + (t & 7);
             ok[u] = t < nt && i < n;
-            r[u] = ok[u] ? in[i] : uint4{0, 0, 0, 0};
+            x[u] = y[u] = z[u] = 0;
+            if (ok[u]) {
+                if constexpr (RB == 16) {
+                    const uint4 r = ((const uint4 *)in)[i];
+                    x[u] = r.x;
+                    y[u] = r.y;
+                    z[u] = r.z;
+                } else {
+                    const uint32_t *q = (const uint32_t *)(in + i * RB);
+                    x[u] = q[0];
+                    y[u] = q[1];
+                    z[u] = q[2];
+                }
+            }
         }
 #pragma unroll
         for (int u = 0; u < PAD_SAMPLE_UNROLL; ++u)
-            if (ok[u]) atomicAdd(&h[hash_pid(r[u].x, r[u].y, pp)], 1u);
+            if (ok[u]) atomicAdd(&h[pid_of<KIND>(x[u], y[u], z[u], pp)], 1u);
     }
     __syncthreads();
     for (uint32_t p = tid; p < pp.R; p += PAD_SAMPLE_THREADS)
         if (h[p]) atomicAdd(&est[p], h[p]);
 }
 
-hipError_t launch_pad_sample(const void *in, int64_t n, int stride, const PartParams &pp, uint32_t *est,
+hipError_t launch_pad_sample(const void *in, int64_t n, int rb, int stride, const PartParams &pp, uint32_t *est,
                              hipStream_t stream) {
-    if (pp.R > 1024 || stride < 1) return hipErrorInvalidValue;
+    if (pp.R > (uint32_t)PAD_SAMPLE_MAX_R || stride < 1) return hipErrorInvalidValue;
     if (n <= 0) return hipSuccess;
     const int64_t nt = pad_sampled_records(n, stride) + 8;
     const int64_t per = (int64_t)PAD_SAMPLE_THREADS * PAD_SAMPLE_UNROLL;
     const int64_t want = (nt + per - 1) / per;
     const int grid = (int)(want < 1 ? 1 : want > PAD_SAMPLE_GRID ? PAD_SAMPLE_GRID : want);
-    hipLaunchKernelGGL(k_pad_sample, dim3(grid), dim3(PAD_SAMPLE_THREADS), 0, stream, (const uint4 *)in, n, stride,
-                       pp, est);
+    const char *c = (const char *)in;
+    if (rb == 16 && pp.kind == SGX_PART_HASH)
+        hipLaunchKernelGGL((k_pad_sample<SGX_PART_HASH, 16>), dim3(grid), dim3(PAD_SAMPLE_THREADS), 0, stream, c, n,
+                           stride, pp, est);
+    else if (rb == 100 && pp.kind == SGX_PART_RANGE_BYTES10)
+        hipLaunchKernelGGL((k_pad_sample<SGX_PART_RANGE_BYTES10, 100>), dim3(grid), dim3(PAD_SAMPLE_THREADS), 0, stream,
+                           c, n, stride, pp, est);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
 constexpr int PAD_CAPS_THREADS = 1024;
+
+constexpr int PAD_CAPS_PER = 4;  // partitions per thread: R <= 4096
 
 __global__ __launch_bounds__(PAD_CAPS_THREADS) void k_pad_caps(const uint32_t *__restrict__ est, int R, double scale,
                                                                double a, int G, uint32_t olim,
                                                                uint32_t *__restrict__ pcap,
                                                                uint32_t *__restrict__ fstart, uint32_t *err_pad) {
     __shared__ uint64_t s_x[PAD_CAPS_THREADS];
-    __shared__ uint32_t s_cap[PAD_CAPS_THREADS];
+    __shared__ uint32_t s_cap[PAD_CAPS_THREADS * PAD_CAPS_PER];
+    __shared__ uint64_t s_base[PAD_CAPS_THREADS * PAD_CAPS_PER];
     const int tid = (int)threadIdx.x;
-    uint32_t cap = 0;
-    if (tid < R) {
-        const double mu = (double)est[tid] * scale;
-        const double c = mu + PAD_SIGMAS * sqrt(a * mu + 16.0) + 8.0;
-        cap = ((uint32_t)ceil(c) + 7u) & ~7u;
+    uint32_t cap[PAD_CAPS_PER];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < PAD_CAPS_PER; ++k) {
+        const int p = tid * PAD_CAPS_PER + k;
+        cap[k] = 0;
+        if (p < R) {
+            const double mu = (double)est[p] * scale;
+            const double c = mu + PAD_SIGMAS * sqrt(a * mu + 16.0) + 8.0;
+            cap[k] = ((uint32_t)ceil(c) + 7u) & ~7u;
+        }
+        s_cap[tid * PAD_CAPS_PER + k] = cap[k];
+        sum += (uint64_t)cap[k] * (uint64_t)G;
     }
-    s_cap[tid] = cap;
-    s_x[tid] = (uint64_t)cap * (uint64_t)G;
+    s_x[tid] = sum;
     __syncthreads();
-    // inclusive scan (Hillis-Steele over R <= 1024 entries, 64-bit: a total above olim is
+    // inclusive scan of the per-thread sums (Hillis-Steele, 64-bit: a total above olim is
     // detected, not wrapped)
     for (int d = 1; d < PAD_CAPS_THREADS; d <<= 1) {
         const uint64_t y = tid >= d ? s_x[tid - d] : 0ull;
@@ -2587,23 +2766,32 @@ __global__ __launch_bounds__(PAD_CAPS_THREADS) void k_pad_caps(const uint32_t *_
         s_x[tid] += y;
         __syncthreads();
     }
+    uint64_t run = s_x[tid] - sum;
+#pragma unroll
+    for (int k = 0; k < PAD_CAPS_PER; ++k) {
+        s_base[tid * PAD_CAPS_PER + k] = run;
+        run += (uint64_t)cap[k] * (uint64_t)G;
+    }
+    __syncthreads();
     if (blockIdx.x == 0) {
-        if (tid < R) pcap[tid] = cap;
-        if (tid == 0 && s_x[R - 1] > (uint64_t)olim) atomicOr(err_pad, PAD_OVERFLOW);
+#pragma unroll
+        for (int k = 0; k < PAD_CAPS_PER; ++k)
+            if (tid * PAD_CAPS_PER + k < R) pcap[tid * PAD_CAPS_PER + k] = cap[k];
+        if (tid == 0 && s_x[PAD_CAPS_THREADS - 1] > (uint64_t)olim) atomicOr(err_pad, PAD_OVERFLOW);
     }
     // this workgroup's partitions [p0, p1): fstart[p*G + g] = base[p] + g * cap[p] (coalesced)
     const int per = (R + (int)gridDim.x - 1) / (int)gridDim.x;
     const int p0 = min(R, (int)blockIdx.x * per), p1 = min(R, p0 + per);
     for (int64_t i = (int64_t)p0 * G + tid; i < (int64_t)p1 * G; i += PAD_CAPS_THREADS) {
         const int p = (int)(i / G), g = (int)(i - (int64_t)p * G);
-        const uint64_t base = s_x[p] - (uint64_t)s_cap[p] * (uint64_t)G;
+        const uint64_t base = s_base[p];
         fstart[i] = (uint32_t)min<uint64_t>(base + (uint64_t)g * s_cap[p], (uint64_t)olim);
     }
 }
 
 hipError_t launch_pad_caps(const uint32_t *est, int R, int64_t sampled, int64_t chunk, int G, uint32_t olim,
                            uint32_t *pcap, uint32_t *fstart, uint32_t *err_pad, hipStream_t stream) {
-    if (R < 1 || R > PAD_CAPS_THREADS || sampled < 1 || G < 1) return hipErrorInvalidValue;
+    if (R < 1 || R > PAD_CAPS_THREADS * PAD_CAPS_PER || sampled < 1 || G < 1) return hipErrorInvalidValue;
     const double scale = (double)chunk / (double)sampled, a = 1.0 + scale;
     const int grid = min(R, 64);
     hipLaunchKernelGGL(k_pad_caps, dim3(grid), dim3(PAD_CAPS_THREADS), 0, stream, est, R, scale, a, G, olim, pcap,
@@ -2624,29 +2812,53 @@ int64_t pad_capacity_bound(int64_t n, int R, int64_t chunk, int G, int64_t sampl
 
 constexpr int FRAG_THREADS = 256;
 
+// Copy `bytes` from s to d by one workgroup: 16 B units when both ends and the size are
+// 16 B-aligned, else dwords (fixed-width records are whole dwords).
+__device__ __forceinline__ void frag_copy(const char *s, char *d, uint64_t bytes, uint32_t tid) {
+    if ((((uintptr_t)s | (uintptr_t)d | bytes) & 15) == 0) {
+        const uint4 *s4 = (const uint4 *)s;
+        uint4 *d4 = (uint4 *)d;
+        const uint64_t c = bytes >> 4;
+        uint64_t k = tid;
+        for (; k + 3 * FRAG_THREADS < c; k += 4 * FRAG_THREADS) {
+            const uint4 v0 = s4[k], v1 = s4[k + FRAG_THREADS], v2 = s4[k + 2 * FRAG_THREADS],
+                        v3 = s4[k + 3 * FRAG_THREADS];
+            d4[k] = v0;
+            d4[k + FRAG_THREADS] = v1;
+            d4[k + 2 * FRAG_THREADS] = v2;
+            d4[k + 3 * FRAG_THREADS] = v3;
+        }
+        for (; k < c; k += FRAG_THREADS) d4[k] = s4[k];
+    } else {
+        const uint32_t *s1 = (const uint32_t *)s;
+        uint32_t *d1 = (uint32_t *)d;
+        const uint64_t c = bytes >> 2;
+        uint64_t k = tid;
+        for (; k + 3 * FRAG_THREADS < c; k += 4 * FRAG_THREADS) {
+            const uint32_t v0 = s1[k], v1 = s1[k + FRAG_THREADS], v2 = s1[k + 2 * FRAG_THREADS],
+                           v3 = s1[k + 3 * FRAG_THREADS];
+            d1[k] = v0;
+            d1[k + FRAG_THREADS] = v1;
+            d1[k + 2 * FRAG_THREADS] = v2;
+            d1[k + 3 * FRAG_THREADS] = v3;
+        }
+        for (; k < c; k += FRAG_THREADS) d1[k] = s1[k];
+    }
+}
+
 __global__ __launch_bounds__(FRAG_THREADS) void k_gather_frags(const int64_t *__restrict__ desc, int64_t nblocks) {
     const uint32_t g = blockIdx.x, tid = threadIdx.x;
     for (int64_t b = blockIdx.y; b < nblocks; b += gridDim.y) {
-        const int64_t *d = desc + 6 * b;
-        const uint64_t pg = (uint64_t)d[5];
-        const uint32_t p = (uint32_t)pg, G = (uint32_t)(pg >> 32);
+        const int64_t *d = desc + FRAG_DESC_WORDS * b;
+        const uint32_t p = (uint32_t)d[5], G = (uint32_t)d[6];
+        const uint64_t rb = (uint64_t)d[7];
         if (g >= G) continue;
         const uint32_t *fstart = (const uint32_t *)(uintptr_t)d[1];
         const uint32_t *foff = (const uint32_t *)(uintptr_t)d[2];
         const uint32_t *cnt = (const uint32_t *)(uintptr_t)d[3];
         const int64_t i = (int64_t)p * G + g;
-        const uint32_t c = cnt[i];
-        const uint4 *s = (const uint4 *)(uintptr_t)d[0] + fstart[i];
-        uint4 *o = (uint4 *)(uintptr_t)d[4] + (foff[i] - foff[(int64_t)p * G]);
-        uint32_t k = tid;
-        for (; k + 3 * FRAG_THREADS < c; k += 4 * FRAG_THREADS) {
-            const uint4 v0 = s[k], v1 = s[k + FRAG_THREADS], v2 = s[k + 2 * FRAG_THREADS], v3 = s[k + 3 * FRAG_THREADS];
-            o[k] = v0;
-            o[k + FRAG_THREADS] = v1;
-            o[k + 2 * FRAG_THREADS] = v2;
-            o[k + 3 * FRAG_THREADS] = v3;
-        }
-        for (; k < c; k += FRAG_THREADS) o[k] = s[k];
+        frag_copy((const char *)(uintptr_t)d[0] + (uint64_t)fstart[i] * rb,
+                  (char *)(uintptr_t)d[4] + (uint64_t)(foff[i] - foff[(int64_t)p * G]) * rb, (uint64_t)cnt[i] * rb, tid);
     }
 }
 

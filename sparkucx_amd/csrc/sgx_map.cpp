@@ -206,12 +206,27 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
 // write-combining K4 (<= 1024), the default kernels, no multi-rank communicator (an exchange
 // sends contiguous bytes: a padded map would need its contiguous copy first), big enough for
 // the skipped histogram to matter, and no earlier overflow in this shuffle.
-static bool use_padded(sgx_engine *e, const Shuffle &s, int64_t n) {
-    if (s.rb != 16 || s.kind != SGX_PART_HASH || s.R < 2 || s.ser != SGX_SER_FIXED || s.combine != -1) return false;
-    if (e->flags & (SGX_FLAG_NO_PADDED_MAP | SGX_FLAG_NO_WRITE_COMBINING)) return false;
+// R in (1024, 4096], a power of two: the hybrid two-level split of partition_pass, padded.
+static bool split_ok(sgx_engine *e, int32_t R) {
+    return R > 1024 && R <= 4096 && (R & (R - 1)) == 0 &&
+           !(e->flags & (SGX_FLAG_NO_WRITE_COMBINING | SGX_FLAG_NO_SPLIT_SCATTER));
+}
+
+// TeraSort's 100 B records under a RangePartitioner over 10-byte keys take the same path with the
+// LDS-staged wide-record K4 (its input 16 B-aligned, as that kernel needs).
+static bool use_padded(sgx_engine *e, const Shuffle &s, const void *in, int64_t n) {
+    if (s.R < 2 || s.ser != SGX_SER_FIXED || s.combine != -1) return false;
+    if (e->flags & SGX_FLAG_NO_PADDED_MAP) return false;
     if (e->rank_mode != SGX_RANK_ORDERED || !e->lds_order_ok || e->sc_waves || e->sc_items) return false;
     if (e->nranks > 1 || n < e->pad_min || s.pad_failed.load()) return false;
-    return scatter_geom16_wc((uint32_t)s.R).items != 0;
+    if (s.rb == 16 && s.kind == SGX_PART_HASH && s.R > 1024)  // the padded two-level split
+        return split_ok(e, s.R);
+    if (s.rb == 16 && s.kind == SGX_PART_HASH)
+        return !(e->flags & SGX_FLAG_NO_WRITE_COMBINING) && scatter_geom16_wc((uint32_t)s.R).items != 0;
+    if (s.rb == 100 && s.kind == SGX_PART_RANGE_BYTES10)
+        return !(e->flags & SGX_FLAG_NO_WIDE_STAGED) && ((uintptr_t)in & 15) == 0 &&
+               scatter_geom_wide2((uint32_t)s.R, 100, s.kind, s.nb).items != 0;
+    return false;
 }
 
 // The map's geometry: chunk / G exactly as partition_pass cuts them (the fallback's kernels
@@ -222,19 +237,156 @@ struct PadGeom {
     int G = 0, stride = 1;
 };
 
-static PadGeom pad_geom(sgx_engine *e, int32_t R, int64_t n) {
+static PadGeom pad_geom(sgx_engine *e, const Shuffle &s, int64_t n) {
     PadGeom pg;
-    pg.geo = scatter_geom16_wc((uint32_t)R);
+    const int32_t R = s.R;
+    if (s.rb == 16 && R > 1024) {  // the split's level 1 (its tile decides the chunks)
+        pg.geo = scatter_geom16_wc((uint32_t)(SPLIT_HOT_CAP + R / 64));
+        pg.geo.lds_bytes += ((size_t)R * 2 + 15) & ~(size_t)15;  // the partition -> stream table
+        pg.geo.items = 8;
+        pg.geo.tile = 8 * 512;
+    } else {
+        pg.geo = s.rb == 16 ? scatter_geom16_wc((uint32_t)R) : scatter_geom_wide2((uint32_t)R, s.rb, s.kind, s.nb);
+    }
     const int tile = pg.geo.tile;
     int64_t chunk = n > 0 ? (n + e->G - 1) / e->G : 1;
     pg.chunk = (chunk + tile - 1) / tile * tile;
     pg.G = n > 0 ? (int)((n + pg.chunk - 1) / pg.chunk) : 1;
-    // about 2^16 sampled lines or more, one line in PAD_SAMPLE_STRIDE_MAX at most (C1: one
-    // 128 B line in 128, 34 MB of the 4.3 GB map)
+    // about 2^16 sampled groups of 8 records or more, one group in PAD_SAMPLE_STRIDE_MAX at most
+    // (C1: one 128 B line in 128, 34 MB of the 4.3 GB map)
     pg.stride = (int)std::min<int64_t>(PAD_SAMPLE_STRIDE_MAX, std::max<int64_t>(1, ((n + 7) / 8) >> 16));
     pg.sampled = pad_sampled_records(n, pg.stride);
     pg.olim = pad_capacity_bound(n, R, pg.chunk, pg.G, pg.sampled);
+    if (s.rb == 16 && R > 1024 && pg.olim >= 0) {
+        // the level-1 scratch (cold super-partitions' sub-bins) and the output share one bound
+        const int64_t o1 = pad_capacity_bound(n, R / 64, pg.chunk, pg.G, pg.sampled);
+        pg.olim = o1 < 0 ? -1 : std::max(pg.olim, o1);
+    }
     return pg;
+}
+
+// The hybrid two-level split (partition_pass), padded: the hot partitions --
+// chosen from the sampled counts -- stream from level 1 into their final sub-bins, the others
+// into sub-bins of their super-partition in a scratch buffer; level 2 walks the scratch one
+// (super, chunk) fragment at a time and writes each cold partition's records into ITS final
+// sub-bin of that chunk.  Then, as in padded_pass: K3 over the final counts, and a guarded
+// two-pass fallback (K1+K2, K3, the single lane-ordered K4).
+static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n,
+                             const PadGeom &pg) {
+    hipStream_t st = c.st;
+    const int32_t R = s.R;
+    constexpr int32_t Q = 64;
+    const int32_t S = R / Q;
+    constexpr int32_t HOT = SPLIT_HOT_CAP;
+    const int G = pg.G;
+    const int64_t len = (int64_t)R * G, tiles = scan_tiles(len);
+    const uint32_t olim = (uint32_t)pg.olim;
+    // the fallback's own geometry (the single lane-ordered K4)
+    const ScatterGeom gfb = scatter_geom16_ord((uint32_t)R);
+    if (gfb.items == 0) return fail_msg(SGX_ERR_UNSUPPORTED, "no single-pass geometry for R=%d", R);
+    int64_t chunk_fb = (n + e->G - 1) / e->G;
+    chunk_fb = (chunk_fb + gfb.tile - 1) / gfb.tile * gfb.tile;
+    const int G_fb = (int)((n + chunk_fb - 1) / chunk_fb);
+    const int64_t len_fb = (int64_t)R * G_fb, tiles_fb = scan_tiles(len_fb);
+    SGX_TRY(m.data.ensure((size_t)olim * 16));
+    SGX_TRY(m.frag.ensure((size_t)len * 12 + 16));
+    uint32_t *fstart = (uint32_t *)m.frag.p, *foff = fstart + len, *cnt = foff + len;
+    SGX_TRY(c.offs.ensure((size_t)len_fb * 4));
+    SGX_TRY(c.split_tmp.ensure((size_t)olim * 16));
+    // [fallback counts][fallback ticket | status][offsets R+1 | error | padded flags]
+    // [padded scan ticket | status][est R][pcap R], one memset
+    auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    const size_t counts_bytes = al((size_t)len_fb * 4);
+    const size_t status_fb_bytes = al((size_t)(16 + tiles_fb * 8));
+    const size_t off_bytes = al((size_t)(R + 3) * 4);
+    const size_t status_bytes = al((size_t)(16 + tiles * 8));
+    const size_t rbytes = al((size_t)R * 4);
+    const size_t work_bytes = counts_bytes + status_fb_bytes + off_bytes + status_bytes + 2 * rbytes;
+    SGX_TRY(c.work.ensure(work_bytes));
+    char *w = (char *)c.work.p;
+    uint32_t *counts_fb = (uint32_t *)w;
+    uint32_t *ticket_fb = (uint32_t *)(w + counts_bytes);
+    uint64_t *status_fb = (uint64_t *)((char *)ticket_fb + 16);
+    uint32_t *part_off_dev = (uint32_t *)(w + counts_bytes + status_fb_bytes);
+    uint32_t *err = part_off_dev + R + 1, *err_pad = part_off_dev + R + 2;
+    uint32_t *ticket_pad = (uint32_t *)((char *)part_off_dev + off_bytes);
+    uint64_t *status_pad = (uint64_t *)((char *)ticket_pad + 16);
+    uint32_t *est = (uint32_t *)((char *)ticket_pad + status_bytes);
+    uint32_t *pcap = (uint32_t *)((char *)est + rbytes);
+    c.last_off_dev = part_off_dev;
+    // the split's scratch: [stream_of u16 R][hot_part i32 HOT][est1 S][cap1 S][fstart1 S*G]
+    // [cnt1 (HOT+S)*G][cur1 (HOT+S)*G][capS HOT+S][ndesc | pad][desc i64 4*S*G]
+    const int64_t ns = (int64_t)(HOT + S);
+    const size_t b_so = al((size_t)R * 2), b_hp = al((size_t)HOT * 4), b_s = al((size_t)S * 4);
+    const size_t b_sg = al((size_t)S * G * 4), b_st = al((size_t)ns * G * 4), b_cs = al((size_t)ns * 4);
+    SGX_TRY(c.split_work.ensure(b_so + b_hp + 2 * b_s + b_sg + 2 * b_st + b_cs + 16 + (size_t)S * G * 32));
+    char *x = (char *)c.split_work.p;
+    uint16_t *stream_of = (uint16_t *)x;
+    int32_t *hot_part = (int32_t *)(x += b_so);
+    uint32_t *est1 = (uint32_t *)(x += b_hp);
+    uint32_t *cap1 = (uint32_t *)(x += b_s);
+    uint32_t *fstart1 = (uint32_t *)(x += b_s);
+    uint32_t *cnt1 = (uint32_t *)(x += b_sg);
+    uint32_t *cur1 = (uint32_t *)(x += b_st);
+    uint32_t *capS = (uint32_t *)(x += b_st);
+    uint32_t *ndesc = (uint32_t *)(x += b_cs);
+    int64_t *desc = (int64_t *)(x + 16);
+    HIP_TRY(hipMemsetAsync(c.work.p, 0, work_bytes, st));
+    hipEvent_t h0 = e->ev(), h1 = e->ev(), c1 = e->ev(), x1 = e->ev();
+    HIP_TRY(hipEventRecord(h0, st));
+    HIP_TRY(launch_pad_sample(in, n, 16, pg.stride, s.pp, est, st));
+    HIP_TRY(launch_hot_select(nullptr, R, Q, stream_of, hot_part, st, est));
+    HIP_TRY(launch_pad_caps(est, R, pg.sampled, pg.chunk, G, olim, pcap, fstart, err_pad, st));
+    HIP_TRY(launch_cold_super_est(est, stream_of, S, Q, est1, st));
+    HIP_TRY(launch_pad_caps(est1, S, pg.sampled, pg.chunk, G, olim, cap1, fstart1, err_pad, st));
+    HIP_TRY(launch_hot_cursors(fstart, hot_part, fstart1, cur1, S, G, st, pcap, cap1, capS));
+    SGX_TRY(debug_sync(e, st, "padded split: sample / selection / capacities"));
+    HIP_TRY(hipEventRecord(h1, st));
+    PartParams p1 = s.pp;
+    p1.kind = KIND_HOT_SPLIT;
+    p1.R = (uint32_t)(HOT + S);
+    p1.dshift = (uint32_t)__builtin_ctz((unsigned)R);
+    p1.dir = stream_of;
+    p1.mbits = (uint32_t)pg.geo.mbits;
+    p1.olim = olim;
+    p1.pad_cnt = cnt1;
+    p1.pad_cap = capS;
+    HIP_TRY(launch_scatter(in, m.data.p, n, 16, pg.chunk, G, p1, cur1, pg.geo, err_pad, st, c.split_tmp.p,
+                           (uint32_t)HOT));
+    SGX_TRY(debug_sync(e, st, "K4 padded split level 1"));
+    HIP_TRY(launch_frag_desc(fstart1, cnt1, S, G, desc, ndesc, st));
+    const ScatterGeom geo2 = scatter_geom16_wc((uint32_t)Q);
+    PartParams p2 = s.pp;
+    p2.kind = KIND_HASH_POW2;
+    p2.R = (uint32_t)Q;
+    p2.mbits = (uint32_t)geo2.mbits;
+    p2.olim = olim;
+    p2.pad_cnt = cnt;
+    p2.pad_cap = pcap;
+    const int grid2 = (int)std::min<int64_t>((int64_t)S * G, (int64_t)e->num_cus);
+    HIP_TRY(launch_scatter16_seg(c.split_tmp.p, m.data.p, n, p2, fstart, G, desc, ndesc, nullptr, grid2, geo2, err_pad,
+                                 st));
+    SGX_TRY(debug_sync(e, st, "K4 padded split level 2"));
+    HIP_TRY(launch_hot_counts(cnt1, hot_part, G, cnt, st));
+    HIP_TRY(hipEventRecord(c1, st));
+    HIP_TRY(launch_scan(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, st));
+    // the two-pass fallback, each kernel a no-op unless *err_pad has PAD_OVERFLOW
+    PartParams fp = s.pp;
+    fp.guard = err_pad;
+    HIP_TRY(launch_hist(in, n, 16, chunk_fb, G_fb, fp, counts_fb, st, e->hist_mode, true));
+    HIP_TRY(launch_scan(counts_fb, (uint32_t *)c.offs.p, len_fb, status_fb, ticket_fb, err, part_off_dev, G_fb, R, st,
+                        err_pad));
+    fp.mbits = (uint32_t)gfb.mbits;
+    HIP_TRY(launch_scatter(in, m.data.p, n, 16, chunk_fb, G_fb, fp, (const uint32_t *)c.offs.p, gfb, err, st));
+    SGX_TRY(debug_sync(e, st, "padded split scan / fallback"));
+    HIP_TRY(hipEventRecord(x1, st));
+    HIP_TRY(hipMemcpyAsync(m.part_off.p, part_off_dev, (size_t)(R + 3) * 4, hipMemcpyDeviceToHost, st));
+    e->record_stage(SGX_STAGE_HIST, h0, h1);
+    e->record_stage(SGX_STAGE_SCATTER, h1, c1);
+    e->record_stage(SGX_STAGE_SCAN, c1, x1);
+    m.pad_try = true;
+    m.frag_G = G;
+    return SGX_OK;
 }
 
 // sample -> sub-bin capacities -> K4 into the sub-bins (final counts out) -> K3 over the
@@ -249,7 +401,8 @@ static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void 
     const int G = pg.G;
     const int64_t len = (int64_t)R * G, tiles = scan_tiles(len);
     const uint32_t olim = (uint32_t)pg.olim;
-    SGX_TRY(m.data.ensure((size_t)olim * 16));
+    const int rb = s.rb;
+    SGX_TRY(m.data.ensure((size_t)olim * (size_t)rb));
     SGX_TRY(m.frag.ensure((size_t)len * 12 + 16));
     uint32_t *fstart = (uint32_t *)m.frag.p, *foff = fstart + len, *cnt = foff + len;
     SGX_TRY(c.offs.ensure((size_t)len * 4));
@@ -275,7 +428,7 @@ static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void 
     HIP_TRY(hipMemsetAsync(c.work.p, 0, work_bytes, st));
     hipEvent_t h0 = e->ev(), h1 = e->ev(), c1 = e->ev(), x1 = e->ev();
     HIP_TRY(hipEventRecord(h0, st));
-    HIP_TRY(launch_pad_sample(in, n, pg.stride, s.pp, est, st));
+    HIP_TRY(launch_pad_sample(in, n, rb, pg.stride, s.pp, est, st));
     HIP_TRY(launch_pad_caps(est, R, pg.sampled, pg.chunk, G, olim, pcap, fstart, err_pad, st));
     SGX_TRY(debug_sync(e, st, "padded sample / capacities"));
     HIP_TRY(hipEventRecord(h1, st));
@@ -284,18 +437,18 @@ static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void 
     kp.olim = olim;
     kp.pad_cnt = cnt;
     kp.pad_cap = pcap;
-    HIP_TRY(launch_scatter(in, m.data.p, n, 16, pg.chunk, G, kp, fstart, pg.geo, err_pad, st));
+    HIP_TRY(launch_scatter(in, m.data.p, n, rb, pg.chunk, G, kp, fstart, pg.geo, err_pad, st));
     SGX_TRY(debug_sync(e, st, "K4 padded scatter"));
     HIP_TRY(hipEventRecord(c1, st));
     HIP_TRY(launch_scan(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, st));
     // the two-pass fallback, each kernel a no-op unless *err_pad has PAD_OVERFLOW
     PartParams fp = s.pp;
     fp.guard = err_pad;
-    HIP_TRY(launch_hist(in, n, 16, pg.chunk, G, fp, counts_fb, st, e->hist_mode, true));
+    HIP_TRY(launch_hist(in, n, rb, pg.chunk, G, fp, counts_fb, st, e->hist_mode, true));
     HIP_TRY(launch_scan(counts_fb, (uint32_t *)c.offs.p, len, status_fb, ticket_fb, err, part_off_dev, G, R, st,
                         err_pad));
     fp.mbits = (uint32_t)pg.geo.mbits;
-    HIP_TRY(launch_scatter(in, m.data.p, n, 16, pg.chunk, G, fp, (const uint32_t *)c.offs.p, pg.geo, err, st));
+    HIP_TRY(launch_scatter(in, m.data.p, n, rb, pg.chunk, G, fp, (const uint32_t *)c.offs.p, pg.geo, err, st));
     SGX_TRY(debug_sync(e, st, "padded scan / fallback"));
     HIP_TRY(hipEventRecord(x1, st));
     HIP_TRY(hipMemcpyAsync(m.part_off.p, part_off_dev, (size_t)(R + 3) * 4, hipMemcpyDeviceToHost, st));
@@ -314,18 +467,20 @@ int sgx::materialize(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
     const int32_t R = s.R;
     const int G = m.frag_G;
     const uint32_t *po = (const uint32_t *)m.part_off.p;
-    SGX_TRY(m.dense.ensure((size_t)std::max<int64_t>(m.nrec * 16, 16)));
-    std::vector<int64_t> desc((size_t)R * 6);
+    SGX_TRY(m.dense.ensure((size_t)std::max<int64_t>(m.nrec * s.rb, 16)));
+    std::vector<int64_t> desc((size_t)R * FRAG_DESC_WORDS);
     const int64_t len = (int64_t)R * G;
     const uint32_t *fstart = (const uint32_t *)m.frag.p;
     for (int32_t p = 0; p < R; ++p) {
-        int64_t *d = &desc[(size_t)p * 6];
+        int64_t *d = &desc[(size_t)p * FRAG_DESC_WORDS];
         d[0] = (int64_t)(uintptr_t)m.data.p;
         d[1] = (int64_t)(uintptr_t)fstart;
         d[2] = (int64_t)(uintptr_t)(fstart + len);
         d[3] = (int64_t)(uintptr_t)(fstart + 2 * len);
-        d[4] = (int64_t)(uintptr_t)((char *)m.dense.p + (size_t)po[p] * 16);
-        d[5] = (int64_t)(((uint64_t)(uint32_t)G << 32) | (uint32_t)p);
+        d[4] = (int64_t)(uintptr_t)((char *)m.dense.p + (size_t)po[p] * (size_t)s.rb);
+        d[5] = p;
+        d[6] = G;
+        d[7] = s.rb;
     }
     SGX_TRY(c.items_dev.ensure(desc.size() * 8));
     HIP_TRY(hipStreamWaitEvent(c.st, m.done.ev, 0));
@@ -408,13 +563,14 @@ static int run_map_pipeline(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const 
     m.pad_try = m.padded = m.dense_valid = false;
     const uint32_t *rec_off_dev = part_dev;
     PadGeom pg;
-    if (!partitioned && use_padded(e, s, n)) pg = pad_geom(e, s.R, n);
+    if (!partitioned && use_padded(e, s, in, n)) pg = pad_geom(e, s, n);
     if (s.combine == SGX_AGG_SUM) {
         SGX_TRY(combine_sum(e, c, s, m, partitioned ? m.data.p : in, n));
         rec_off_dev = c.last_off_dev;
     } else if (!partitioned && pg.olim >= n) {
         m.nrec = n;
-        SGX_TRY(padded_pass(e, c, s, m, in, n, pg));
+        if (s.rb == 16 && s.R > 1024) SGX_TRY(padded_split_pass(e, c, s, m, in, n, pg));
+        else SGX_TRY(padded_pass(e, c, s, m, in, n, pg));
         rec_off_dev = c.last_off_dev;
     } else if (!partitioned) {
         m.nrec = n;

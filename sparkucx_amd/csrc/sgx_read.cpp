@@ -39,9 +39,9 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
     std::map<int64_t, std::vector<int64_t>> map_off;  // per local map: partition byte offsets
     std::map<int64_t, bool> map_pad;                  // per local map: read through its fragments
     std::vector<Src> srcs((size_t)n);
-    // a padded map's fragments are copied 16 B at a time: a destination that is not 16-byte
-    // aligned reads the map's contiguous copy instead
-    const bool dst_al16 = ((uintptr_t)dst & 15) == 0 || dst_mem_kind != SGX_MEM_DEVICE;
+    // a padded map's fragments are copied a dword at a time at least: a destination that is
+    // not 4-byte aligned reads the map's contiguous copy instead
+    const bool dst_al4 = ((uintptr_t)dst & 3) == 0 || dst_mem_kind != SGX_MEM_DEVICE;
     int64_t total = 0;
     for (int64_t i = 0; i < n; ++i) {
         const int64_t mid = map_ids[i];
@@ -69,7 +69,7 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
                     if (m.open) return fail_msg(SGX_ERR_STATE, "map %lld is still open", (long long)mid);
                     SGX_TRY(finish_lengths(e, c, s, m));
                     // (only a fill needs the contiguous copy; a size query reads lengths)
-                    if (m.padded && !dst_al16 && dst) SGX_TRY(materialize(e, c, s, m));
+                    if (m.padded && !dst_al4 && dst) SGX_TRY(materialize(e, c, s, m));
                     std::vector<int64_t> o((size_t)s.R + 1, 0);
                     for (int32_t q = 0; q < s.R; ++q) o[(size_t)q + 1] = o[(size_t)q] + m.lengths[(size_t)q];
                     ot = map_off.emplace(mid, std::move(o)).first;
@@ -120,8 +120,8 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
             npieces += (srcs[(size_t)i].len + ITEM_BYTES - 1) / ITEM_BYTES;
         }
     }
-    // [pieces x 3][fragment descriptors x 6], one host-to-device copy
-    const int64_t nwords = npieces * 3 + nfrag * 6;
+    // [pieces x 3][fragment descriptors], one host-to-device copy
+    const int64_t nwords = npieces * 3 + nfrag * FRAG_DESC_WORDS;
     SGX_TRY(c.gather_items.ensure((size_t)nwords * 8));
     SGX_TRY(c.items_dev.ensure((size_t)nwords * 8));
     // the pinned item list is rewritten only after the previous gather's copy has landed
@@ -133,13 +133,15 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
         if (const MapOut *pm = srcs[(size_t)i].pad) {
             const int64_t len = (int64_t)s.R * pm->frag_G;
             const uint32_t *fstart = (const uint32_t *)pm->frag.p;
-            int64_t *d = fd + 6 * nf++;
+            int64_t *d = fd + FRAG_DESC_WORDS * nf++;
             d[0] = (int64_t)(uintptr_t)pm->data.p;
             d[1] = (int64_t)(uintptr_t)fstart;
             d[2] = (int64_t)(uintptr_t)(fstart + len);
             d[3] = (int64_t)(uintptr_t)(fstart + 2 * len);
             d[4] = (int64_t)(uintptr_t)(gdst + off);
-            d[5] = (int64_t)(((uint64_t)(uint32_t)pm->frag_G << 32) | (uint32_t)srcs[(size_t)i].part);
+            d[5] = srcs[(size_t)i].part;
+            d[6] = pm->frag_G;
+            d[7] = s.rb;
             off += srcs[(size_t)i].len;
             continue;
         }

@@ -34,21 +34,20 @@ def all_blocks(engine, sid, mid, R, dst=None):
     return data, lens
 
 
-def check_map(engine, oracle_lib, recs, R, sid, mid, want_layout):
-    import sparkucx_amd as sgx
-
-    want, counts = oracle_lib.map_write(recs, R, nthreads=8)
+def check_map(engine, oracle_lib, recs, R, sid, mid, want_layout, kind=0, bounds=None):
+    rb = recs.shape[1]
+    want, counts = oracle_lib.map_write(recs, R, kind, bounds, nthreads=8)
     lengths = engine.map_lengths(sid, mid, R)
-    assert np.array_equal(lengths, counts * 16), "partition lengths / index offsets differ"
+    assert np.array_equal(lengths, counts * rb), "partition lengths / index offsets differ"
     assert engine.map_layout(sid, mid) == want_layout
     # block fetches, reducer by reducer, straight from the fragments
     data, lens = all_blocks(engine, sid, mid, R)
-    assert np.array_equal(lens, counts * 16)
-    assert np.array_equal(data.reshape(-1, 16), want)
+    assert np.array_equal(lens, counts * rb)
+    assert np.array_equal(data.reshape(-1, rb), want)
     # a random subset of blocks, repeated and out of order, into device memory
     rng = np.random.default_rng(R)
     rids = rng.integers(0, R, 97)
-    o = oracle_lib.offsets(counts) * 16
+    o = oracle_lib.offsets(counts) * rb
     flat = want.reshape(-1)
     sub = np.concatenate([flat[o[r]:o[r + 1]] for r in rids])
     dev = engine.alloc(max(int(sub.size), 16))
@@ -56,9 +55,8 @@ def check_map(engine, oracle_lib, recs, R, sid, mid, want_layout):
     assert np.array_equal(dev.to_numpy(sub.size), sub)
     dev.free()
     # the contiguous bytes (built once), and the layout query is unchanged by them
-    assert np.array_equal(engine.map_output_bytes(sid, mid).reshape(-1, 16), want)
+    assert np.array_equal(engine.map_output_bytes(sid, mid).reshape(-1, rb), want)
     assert engine.map_layout(sid, mid) == want_layout
-    _ = sgx
 
 
 @pytest.mark.parametrize("R", [2, 3, 7, 200, 1000, 1024])
@@ -136,6 +134,87 @@ def test_padded_overflow_falls_back_bit_exact(sgx_lib, pad_engine, oracle_lib, s
         again = oracle_lib.gen_uniform16(n, 78)
         pad_engine.write_map(sid, 1, again, n, 16, R)
         check_map(pad_engine, oracle_lib, again, R, sid, 1, sgx_lib.LAYOUT_CONTIGUOUS)
+    finally:
+        pad_engine.unregister_shuffle(sid)
+
+
+@pytest.mark.parametrize("R", [2048, 4096])
+@pytest.mark.parametrize("shape", ["uniform", "zipf", "one_super", "hot_partition", "few_keys", "tiny"])
+def test_padded_split_r_over_1024(sgx_lib, pad_engine, oracle_lib, R, shape):
+    """R > 1024 (config C3's 4096): the padded two-level split -- hot partitions chosen from
+    the sample stream from level 1 into their final sub-bins, the rest through their
+    super-partition's scratch sub-bins and level 2's (super, chunk) fragments."""
+    n = 2_000_003 if shape != "tiny" else 777
+    if shape == "zipf":
+        recs = oracle_lib.gen_zipf16(n, 5, oracle_lib.zipf_cdf(1.1, 1 << 20))
+    else:
+        recs = oracle_lib.gen_uniform16(n, 6 + R)
+        k = recs[:, :8].copy().view("<i8").reshape(-1)
+        if shape == "one_super":  # every key in super-partition 3 (64 partitions)
+            k = 3 * 64 + (k & 63)
+        elif shape == "hot_partition":  # one partition holds ~40 % of the records
+            k = np.where(np.arange(n) % 5 < 2, 17, k)
+        elif shape == "few_keys":
+            k = k % 7
+        recs[:, :8] = k.astype(np.int64).view(np.uint8).reshape(-1, 8)
+    sid = next_sid()
+    pad_engine.register_shuffle(sid, R)
+    try:
+        pad_engine.write_map(sid, 0, recs, n, 16, R)
+        check_map(pad_engine, oracle_lib, recs, R, sid, 0, sgx_lib.LAYOUT_PADDED)
+    finally:
+        pad_engine.unregister_shuffle(sid)
+
+
+def test_padded_split_sorted_input_falls_back(sgx_lib, pad_engine, oracle_lib):
+    """Sorted keys at R = 4096: sub-bins overflow, the single-pass lane-ordered fallback runs."""
+    R, n = 4096, 1_000_000
+    recs = oracle_lib.gen_uniform16(n, 8)
+    recs[:, :8] = (np.arange(n) * R // n).astype(np.int64).view(np.uint8).reshape(-1, 8)
+    sid = next_sid()
+    pad_engine.register_shuffle(sid, R)
+    try:
+        pad_engine.write_map(sid, 0, recs, n, 16, R)
+        check_map(pad_engine, oracle_lib, recs, R, sid, 0, sgx_lib.LAYOUT_CONTIGUOUS)
+    finally:
+        pad_engine.unregister_shuffle(sid)
+
+
+def terasort_bounds(oracle_lib, R, seed=0xC4):
+    sample = oracle_lib.gen_terasort100(20 * R, seed)[:, :10]
+    sample = sample[np.lexsort(sample.T[::-1])]
+    return np.ascontiguousarray(sample[[int(len(sample) / R * (i + 1)) for i in range(R - 1)]])
+
+
+@pytest.mark.parametrize("R", [2, 64, 1024])
+@pytest.mark.parametrize("n", [1, 999, 50_001, 600_003])
+def test_padded_terasort_records(sgx_lib, pad_engine, oracle_lib, R, n):
+    """TeraSort's 100 B records under a RangePartitioner over 10-byte keys (config C4): the
+    sampled histogram searches the bounds, the LDS-staged wide-record K4 writes the sub-bins."""
+    recs = oracle_lib.gen_terasort100(n, 0x7E + n + R)
+    bounds = terasort_bounds(oracle_lib, R)
+    sid = next_sid()
+    pad_engine.register_shuffle(sid, R, sgx_lib.PART_RANGE_BYTES10, bounds, True, 100)
+    try:
+        pad_engine.write_map(sid, 0, recs, n, 100, R)
+        check_map(pad_engine, oracle_lib, recs, R, sid, 0, sgx_lib.LAYOUT_PADDED, sgx_lib.PART_RANGE_BYTES10, bounds)
+    finally:
+        pad_engine.unregister_shuffle(sid)
+
+
+def test_padded_terasort_sorted_input_falls_back(sgx_lib, pad_engine, oracle_lib):
+    """Records already sorted by key: each chunk holds a few partitions, every sub-bin of them
+    overflows and the wide-record two-pass fallback rewrites the map on the device."""
+    R, n = 256, 400_000
+    recs = oracle_lib.gen_terasort100(n, 31)
+    recs = np.ascontiguousarray(recs[np.lexsort(recs[:, :10].T[::-1])])
+    bounds = terasort_bounds(oracle_lib, R)
+    sid = next_sid()
+    pad_engine.register_shuffle(sid, R, sgx_lib.PART_RANGE_BYTES10, bounds, True, 100)
+    try:
+        pad_engine.write_map(sid, 0, recs, n, 100, R)
+        check_map(pad_engine, oracle_lib, recs, R, sid, 0, sgx_lib.LAYOUT_CONTIGUOUS, sgx_lib.PART_RANGE_BYTES10,
+                  bounds)
     finally:
         pad_engine.unregister_shuffle(sid)
 
