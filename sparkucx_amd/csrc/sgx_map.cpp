@@ -203,8 +203,9 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
 // single-pass padded write
 // ------------------------------------------------------------------------------------
 // Whether the map is written padded: hash partitioner, 16 B fixed-codec records, R within the
-// write-combining K4 (<= 1024), the default kernels, no multi-rank communicator (an exchange
-// sends contiguous bytes: a padded map would need its contiguous copy first), big enough for
+// write-combining K4 (<= 1024), the default kernels, no communicator at all (an exchange sends
+// contiguous bytes, so a padded map would need its contiguous copy first; a one-rank
+// communicator is the self-exchange stand-in for the multi-rank path and keeps its layout), big enough for
 // the skipped histogram to matter, and no earlier overflow in this shuffle.
 // R in (1024, 4096], a power of two: the hybrid two-level split of partition_pass, padded.
 static bool split_ok(sgx_engine *e, int32_t R) {
@@ -218,7 +219,7 @@ static bool use_padded(sgx_engine *e, const Shuffle &s, const void *in, int64_t 
     if (s.R < 2 || s.ser != SGX_SER_FIXED || s.combine != -1) return false;
     if (e->flags & SGX_FLAG_NO_PADDED_MAP) return false;
     if (e->rank_mode != SGX_RANK_ORDERED || !e->lds_order_ok || e->sc_waves || e->sc_items) return false;
-    if (e->nranks > 1 || n < e->pad_min || s.pad_failed.load()) return false;
+    if (e->nranks > 1 || e->comm || e->host_comm || n < e->pad_min || s.pad_failed.load()) return false;
     if (s.rb == 16 && s.kind == SGX_PART_HASH && s.R > 1024)  // the padded two-level split
         return split_ok(e, s.R);
     if (s.rb == 16 && s.kind == SGX_PART_HASH)

@@ -305,20 +305,26 @@ def test_padded_fetch_into_unaligned_device_memory(sgx_lib, pad_engine, oracle_l
 
 
 def test_padded_exchange_one_rank(sgx_lib, oracle_lib):
-    """A one-rank RCCL communicator keeps the padded write (nranks == 1); the exchange sends
-    the map's contiguous copy and the received blocks equal the oracle's."""
+    """A communicator (even a one-rank one, the self-exchange stand-in for the multi-rank path)
+    keeps maps written after it contiguous; a map written padded before the communicator
+    existed is exchanged through its contiguous copy.  Both exchange to the oracle's blocks."""
     R = 1024
     with sgx_lib.ShuffleEngine(device=0, flags=sgx_lib.FLAG_PAD_ANY_SIZE) as e:
-        e.comm_init(1, 0, sgx_lib.get_unique_id())
         e.register_shuffle(1, R)
+        early = oracle_lib.gen_uniform16(300_000, 22)
+        e.write_map(1, 5, early, len(early), 16, R)
+        assert e.map_layout(1, 5) == sgx_lib.LAYOUT_PADDED
+        e.comm_init(1, 0, sgx_lib.get_unique_id())
         recs = oracle_lib.gen_uniform16(400_000, 23)
         e.write_map(1, 6, recs, len(recs), 16, R)
-        assert e.map_layout(1, 6) == sgx_lib.LAYOUT_PADDED
+        assert e.map_layout(1, 6) == sgx_lib.LAYOUT_CONTIGUOUS
         e.exchange(1)
         e.sync()
-        data, lens = e.fetch_blocks(1, [6] * R, list(range(R)))
-        out, counts = oracle_lib.map_write(recs, R)
-        assert np.array_equal(data.reshape(-1, 16), out)
+        for mid, src in ((5, early), (6, recs)):
+            data, lens = e.fetch_blocks(1, [mid] * R, list(range(R)))
+            out, counts = oracle_lib.map_write(src, R)
+            assert np.array_equal(data.reshape(-1, 16), out)
+            assert np.array_equal(np.asarray(lens), counts * 16)
 
 
 def test_padded_concurrent_writers(sgx_lib, pad_engine, oracle_lib):
