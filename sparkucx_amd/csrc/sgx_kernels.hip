@@ -1577,6 +1577,10 @@ __global__ __launch_bounds__(WIDE_THREADS, 1) void k_scatter_wide(const char *__
 // LDS: stage[TR * RB] | bounds[nb] | rows[W][RS] u16 | cur[RS] u32 | dlt[RS] u32 | idx[TR] u32
 // ------------------------------------------------------------------------------------
 constexpr int WIDE2_TR = 1024;
+// A/B probe: nontemporal drain stores (tools/build_variant.sh <tag> - -DSGX_WIDE_NT=1)
+#ifndef SGX_WIDE_NT
+#define SGX_WIDE_NT 0
+#endif
 
 __host__ __device__ size_t scatter_wide2_lds(uint32_t R, int rb, int kind, int nb) {
     const size_t bsz = kind == SGX_PART_RANGE_BYTES10 ? sizeof(Key10) : 8;
@@ -1669,7 +1673,11 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
     uint64_t st_last = wc_stamp();
 #endif
     auto store_piece = [&](const u32x4 &v, uint32_t dst, uint32_t pc) {
+#if SGX_WIDE_NT
+        __builtin_nontemporal_store(v, (u32x4 *)(out + (uint64_t)dst * DW + piece_dw(pc)));
+#else
         *(u32x4 *)(out + (uint64_t)dst * DW + piece_dw(pc)) = v;
+#endif
     };
     for (int t = 0; t < ntiles; ++t) {
         const int nrec = t + 1 < ntiles ? TR : lastn;

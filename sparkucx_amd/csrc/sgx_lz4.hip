@@ -60,6 +60,9 @@ struct GlobalSrc {
     const uint8_t *p;
     __device__ __forceinline__ uint32_t u32(int i) const { return g32(p + i); }
     __device__ __forceinline__ uint32_t u8(int i) const { return p[i]; }
+    // bytes [i, i + 4 * N) as N little-endian dwords: one unaligned global_load_dwordxN
+    template <int N>
+    __device__ __forceinline__ void words(int i, uint32_t (&w)[N]) const { __builtin_memcpy(w, p + i, 4 * N); }
 };
 __device__ __forceinline__ uint32_t hash4(uint32_t seq) { return (seq * 2654435761u) >> (32 - kHashLog); }
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
@@ -174,12 +177,30 @@ __device__ __forceinline__ int lz4_count_end(const Src &src, int a, int d0, int 
     }
 }
 
-// The search's first batch of sequences from `start` (iteration lane); loaded ahead of the
-// table work that precedes the search, which they do not depend on.
+// A search lane's bytes: s0, s4, s8 = the dwords at pos, pos + 4, pos + 8 and pb = the byte
+// at pos - 1 -- the sequence it hashes, plus what a hit needs to settle the common match
+// without another round trip: the first LZ4_count comparison (s4 against the candidate's
+// second dword), the first catch-up comparison (pb against the byte before the candidate) and
+// the next position's sequences (_next_match's ip - 2 and ip, inside bytes [pos + 2, pos + 11)
+// when the match ends in that first dword).  Valid lanes have pos + 12 <= n (pos < mflimit).
+struct Probe {
+    uint32_t s0, s4, s8, pb;
+};
 template <typename Src>
-__device__ __forceinline__ uint32_t search_seq(const Src &src, int start, int it, int n) {
+__device__ __forceinline__ Probe search_probe(const Src &src, int start, int it, int n) {
     const int lane = (int)(threadIdx.x & 63);
-    return src.u32(min(start + skip_dist(it + lane), n - 4));  // (invalid lanes: any bytes)
+    const int pos = min(start + skip_dist(it + lane), n - 12);  // (invalid lanes: any bytes)
+    Probe pr;
+    if (start >= 4) {  // uniform: bytes [pos - 4, pos + 12) in one load
+        uint32_t w[4];
+        src.words(pos - 4, w);
+        pr = Probe{w[1], w[2], w[3], w[0] >> 24};
+    } else {  // the block's first positions
+        uint32_t w[3];
+        src.words(pos, w);
+        pr = Probe{w[0], w[1], w[2], src.u8(max(pos - 1, 0))};
+    }
+    return pr;
 }
 
 template <typename Src>
@@ -192,23 +213,37 @@ __device__ __forceinline__ int lz4_compress_wave(const Src &src, int n, uint16_t
         const int mlimit = n - kLastLiterals;  // matchlimit
         if (lane == 0) table[hash4(src.u32(0))] = 0;
         int ip = 1;
-        uint32_t seq0 = search_seq(src, ip, 0, n);
+        Probe pr0 = search_probe(src, ip, 0, n);
+        // _next_match's two sequences when the search's match settled inside its probe bytes
+        bool have_next = false;
+        uint32_t nx_s2 = 0, nx_s0 = 0;
         for (;;) {
             // ---- match search from ip (step 1, search counter 64)
             const int start = ip;
             int it = 0, match = 0;
             bool found = false;
-            uint32_t seq = seq0;
+            Probe pr = pr0;
+            // the hit lane's bytes (Probe) and its candidate's: dword at match + 4, the byte
+            // before match (cbok: read; a candidate below 4 leaves the catch-up to the loop)
+            uint32_t hs0 = 0, hs4 = 0, hs8 = 0, hpb = 0, hc4 = 0, hcb = 0;
+            bool hcbok = false;
             for (;;) {
                 const int pos = start + skip_dist(it + lane);
                 const int nxt = pos + max((it + lane + 63) >> 6, 1);  // the position after this one
                 const bool valid = nxt <= lim;
                 // past the first batch a search tends to run on: the next batch's sequences
                 // load with this one's
-                uint32_t seqn = 0;
-                if (it > 0) seqn = search_seq(src, start, it + 64, n);
+                Probe prn{0, 0, 0, 0};
+                if (it > 0) prn = search_probe(src, start, it + 64, n);
+                const uint32_t seq = pr.s0;
                 const uint32_t h = hash4(seq);
-                int cand = table[h];
+                const int tcand = table[h];
+                // the table candidate's bytes [cand - 4, cand + 8) load as soon as the entry
+                // arrives (tcand < pos <= n - 12 for a valid lane), before the ballots below
+                // resolve: a lane with a lower peer takes the peer's probe bytes instead
+                const int tc = min(tcand, n - 12), tb0 = max(tc - 4, 0), tsh = tc - tb0;
+                uint32_t cw[3];
+                src.words(tb0, cw);
                 // lanes probing the same hash: those whose ballot bits agree with ours on all
                 // hash bits (diff: the lanes that differ on some bit)
                 uint32_t diff_lo = 0, diff_hi = 0;
@@ -221,9 +256,18 @@ __device__ __forceinline__ int lz4_compress_wave(const Src &src, int n, uint16_t
                 }
                 const uint64_t peers = ~(((uint64_t)diff_hi << 32) | diff_lo);
                 const uint64_t lower = peers & below;
-                if (lower) cand = start + skip_dist(it + 63 - (int)__builtin_clzll(lower));
+                // the latest lower lane with our hash: its position is the entry the serial code
+                // would read, and its probe holds that position's bytes
                 // (a valid lane's candidate is in the block: a lower peer of a valid lane is valid)
-                const bool hit = src.u32(min(cand, n - 4)) == seq && valid;
+                const int peer = lower ? 63 - (int)__builtin_clzll(lower) : lane;
+                const uint32_t ps0 = (uint32_t)__shfl((int)pr.s0, peer), ps4 = (uint32_t)__shfl((int)pr.s4, peer),
+                               ppb = (uint32_t)__shfl((int)pr.pb, peer);
+                const int cand = lower ? start + skip_dist(it + peer) : tcand;
+                const uint32_t c0 = lower ? ps0 : tsh == 4 ? cw[1] : __builtin_amdgcn_alignbyte(cw[1], cw[0], (uint32_t)tsh);
+                const uint32_t c4 = lower ? ps4 : tsh == 4 ? cw[2] : __builtin_amdgcn_alignbyte(cw[2], cw[1], (uint32_t)tsh);
+                const uint32_t cbyte = lower ? ppb : cw[0] >> 24;
+                const bool cbok = lower || tsh == 4;  // the byte before the candidate was read
+                const bool hit = c0 == seq && valid;
                 const uint64_t vm = __ballot(valid), hm = __ballot(hit);
                 const int kinv = first_clear(vm);
                 const int khit = hm ? (int)__builtin_ctzll(hm) : 64;
@@ -237,30 +281,54 @@ __device__ __forceinline__ int lz4_compress_wave(const Src &src, int n, uint16_t
                     found = true;
                     ip = start + skip_dist(it + khit);
                     match = lane_value(cand, khit);
+                    hs0 = (uint32_t)lane_value((int)pr.s0, khit);
+                    hs4 = (uint32_t)lane_value((int)pr.s4, khit);
+                    hs8 = (uint32_t)lane_value((int)pr.s8, khit);
+                    hpb = (uint32_t)lane_value((int)pr.pb, khit);
+                    hc4 = (uint32_t)lane_value((int)c4, khit);
+                    hcb = (uint32_t)lane_value((int)cbyte, khit);
+                    hcbok = (__ballot(cbok) >> khit) & 1ull;
                     break;
                 }
                 if (kinv < 64) break;  // next position past mflimit: no match in this block
-                seq = it == 0 ? search_seq(src, start, 64, n) : seqn;
+                pr = it == 0 ? search_probe(src, start, 64, n) : prn;
                 it += 64;
             }
             if (!found) break;
-            // ---- catch up backwards, and LZ4_count from ip + 4 in the same round trip: the
-            // bytes the catch-up adds before ip match, so the match end does not move
+            // ---- catch up backwards, and LZ4_count from ip + 4.  The common match settles from
+            // the probe bytes: no catch-up (the bytes before ip and match differ, or ip is the
+            // anchor) and an end inside the first counted dword; then _next_match's sequences
+            // at the end come from the same bytes.  Otherwise the catch-up and the count's
+            // first round load together (the bytes the catch-up adds before ip match, so the
+            // match end does not move).
             int aend;
             {
                 const int d0 = match - ip, a0 = ip + kMinMatch;
-                const int al = a0 + 4 * lane;
-                const bool full = al + 4 <= mlimit;
-                const uint32_t d = full ? src.u32(al) ^ src.u32(al + d0) : 0u;
-                for (;;) {
-                    const int a = ip - 1 - lane, b = match - 1 - lane;
-                    const bool eq = (src.u8(max(a, 0)) == src.u8(max(b, 0))) && a >= anchor && b >= 0;  // (loads unconditional)
-                    const int back = first_clear(__ballot(eq));
-                    ip -= back;
-                    match -= back;
-                    if (back < 64) break;
+                const bool no_back = ip - 1 < anchor || match < 1 || (hcbok && hpb != hcb);
+                const bool short_end = a0 + 4 <= mlimit && hs4 != hc4;
+                if (no_back && short_end) {
+                    aend = a0 + ((int)__builtin_ctz(hs4 ^ hc4) >> 3);
+                    const uint32_t k = (uint32_t)(aend - ip);  // 4..7: ip + 2 .. ip + 10 are probe bytes
+                    nx_s0 = k == 4 ? hs4 : __builtin_amdgcn_alignbyte(hs8, hs4, k - 4);
+                    nx_s2 = k - 2 < 4 ? __builtin_amdgcn_alignbyte(hs4, hs0, k - 2)
+                                      : __builtin_amdgcn_alignbyte(hs8, hs4, k - 6);
+                    have_next = true;
+                } else {
+                    const int al = a0 + 4 * lane;
+                    const bool full = al + 4 <= mlimit;
+                    const uint32_t d = full ? src.u32(al) ^ src.u32(al + d0) : 0u;
+                    if (!no_back) {
+                        for (;;) {
+                            const int a = ip - 1 - lane, b = match - 1 - lane;
+                            const bool eq = (src.u8(max(a, 0)) == src.u8(max(b, 0))) && a >= anchor && b >= 0;  // (loads unconditional)
+                            const int back = first_clear(__ballot(eq));
+                            ip -= back;
+                            match -= back;
+                            if (back < 64) break;
+                        }
+                    }
+                    aend = lz4_count_end(src, a0, d0, mlimit, d, full);
                 }
-                aend = lz4_count_end(src, a0, d0, mlimit, d, full);
             }
             // ---- literals
             const int lit = ip - anchor;
@@ -306,8 +374,16 @@ __device__ __forceinline__ int lz4_compress_wave(const Src &src, int n, uint16_t
                 anchor = ip;
                 if (ip >= lim) goto last_literals;
                 // the next search's first sequences load with this test's (unused on a hit)
-                seq0 = search_seq(src, ip + 1, 0, n);
-                const uint32_t s2 = src.u32(ip - 2), s0 = src.u32(ip);
+                pr0 = search_probe(src, ip + 1, 0, n);
+                uint32_t s2, s0;
+                if (have_next) {
+                    s2 = nx_s2;
+                    s0 = nx_s0;
+                    have_next = false;
+                } else {
+                    s2 = src.u32(ip - 2);
+                    s0 = src.u32(ip);
+                }
                 if (lane == 0) table[hash4(s2)] = (uint16_t)(ip - 2);
                 __builtin_amdgcn_wave_barrier();  // the write above, then the read below
                 const uint32_t h = hash4(s0);

@@ -737,7 +737,7 @@ def test_shuffle_client_fetch_blocks_split_and_listener(sgx_lib, oracle_lib):
             def onBlockFetchFailure(self, blockId, exception):
                 self.failed[blockId] = exception
 
-        ids = [f"shuffle_3_{m}_{r}" for r in range(R) for m in (0, 1)][:130]
+        ids = [f"shuffle_3_{m}_{r}" for r in range(R) for m in (0, 1, 2)][:130]
         lst = Listener()
         client = mgr.shuffleClient
         client.fetchBlocks("localhost", 1338, "1", ids, lst)

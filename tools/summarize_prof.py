@@ -11,7 +11,9 @@ HBM traffic per MI355X_MICROARCH.md §HBM: FETCH_SIZE (KiB) reads exactly half o
 coalesced stream on gfx950, so it is doubled; WRITE_SIZE (KiB) is taken as is.  The map side
 is every kernel of the write except the input generator, per write (calls / iters).
 
-usage: summarize_prof.py <tag> <out_dir of gpu_prof.sh> <records> <R> <dist> [record_bytes]
+usage: summarize_prof.py <tag> <out_dir of gpu_prof.sh> <records> <R> <dist> [record_bytes] [layout]
+layout: padded (the default map write) or twopass (--flags 256); pmc_map.json keys
+a two-pass profile with the suffix "_twopass" (bench.py --no-padded reads that one).
 """
 import csv
 import json
@@ -41,6 +43,8 @@ def pmc(d, counter):
 def main():
     tag, d, n, R, dist = sys.argv[1:6]
     rb = int(sys.argv[6]) if len(sys.argv) > 6 else 16
+    layout = sys.argv[7] if len(sys.argv) > 7 else "padded"
+    assert layout in ("padded", "twopass"), layout
     n, R = int(n), int(R)
     prof = os.path.join(ROOT, "profiles")
     shutil.copy(os.path.join(d, "kt", "run_kernel_stats.csv"), os.path.join(prof, f"{tag}_kernel_stats.csv"))
@@ -51,7 +55,7 @@ def main():
     fetch, write = pmc(os.path.join(d, "fetch"), "FETCH_SIZE"), pmc(os.path.join(d, "write"), "WRITE_SIZE")
     iters_kt, iters_pmc = 5, 2
     algo = 2 * rb * n
-    lines = [f"# rocprofv3 summary `{tag}` — map-side write, {n} x {rb} B records ({dist}), R = {R}", "",
+    lines = [f"# rocprofv3 summary `{tag}` — map-side write ({layout}), {n} x {rb} B records ({dist}), R = {R}", "",
              "| kernel | calls/write | mean µs | HBM read GB/launch (FETCH×2) | HBM write GB/launch | traffic GB/s |",
              "|---|---|---|---|---|---|"]
     side = {"read_bytes": 0.0, "write_bytes": 0.0, "us": 0.0}
@@ -88,10 +92,10 @@ def main():
         f.write("\n".join(lines) + "\n")
     path = os.path.join(prof, "pmc_map.json")
     cur = json.load(open(path)) if os.path.exists(path) else {}
-    cur[f"{dist}_n{n}_R{R}_rb{rb}"] = {"scatter": k4, "map_side": {
+    cur[f"{dist}_n{n}_R{R}_rb{rb}" + ("_twopass" if layout == "twopass" else "")] = {"scatter": k4, "map_side": {
         "hbm_bytes_per_write": int(tot), "read_bytes": int(side["read_bytes"]),
         "write_bytes": int(side["write_bytes"]), "kernel_us": round(side["us"], 1),
-        "algorithmic_bytes": algo, "ratio": round(tot / algo, 4)}, "source": tag}
+        "algorithmic_bytes": algo, "ratio": round(tot / algo, 4)}, "source": tag, "layout": layout}
     json.dump(cur, open(path, "w"), indent=1, sort_keys=True)
     print("\n".join(lines))
 
