@@ -1581,6 +1581,11 @@ constexpr int WIDE2_TR = 1024;
 #ifndef SGX_WIDE_NT
 #define SGX_WIDE_NT 0
 #endif
+// A/B probe: nontemporal tile loads, so the input stream does not evict the streams' open
+// output lines from L2 (-DSGX_WIDE_NTLOAD=1)
+#ifndef SGX_WIDE_NTLOAD
+#define SGX_WIDE_NTLOAD 0
+#endif
 
 __host__ __device__ size_t scatter_wide2_lds(uint32_t R, int rb, int kind, int nb) {
     const size_t bsz = kind == SGX_PART_RANGE_BYTES10 ? sizeof(Key10) : 8;
@@ -1663,7 +1668,11 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
 #pragma unroll
         for (int i = 0; i < LD; ++i) {
             const int c = i * T + tid;
+#if SGX_WIDE_NTLOAD
+            ld[i] = c < nch ? __builtin_nontemporal_load(tb + c) : u32x4{0, 0, 0, 0};
+#else
             ld[i] = c < nch ? tb[c] : u32x4{0, 0, 0, 0};
+#endif
         }
     };
     if (ntiles > 0) issue(0);

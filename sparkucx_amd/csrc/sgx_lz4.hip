@@ -35,6 +35,16 @@ constexpr int kMaxBlock = 32768;                   // largest block (lz4-java's 
 constexpr int kLanes = 1;                          // one block per workgroup (one wave):
                                                    // 16 KiB LDS -> 10 workgroups per CU
 constexpr int kHeader = 21;
+// A/B switch: the search's table candidate loads before the same-hash ballots resolve, a
+// lower peer's bytes then come from its probe by lane shuffle (1), or the candidate loads
+// after them (0)
+#ifndef SGX_LZ4_PEER_SHFL
+#define SGX_LZ4_PEER_SHFL 1
+#endif
+// lz4_compress_batch (several sequences per batch, 1) or lz4_compress_wave (0)
+#ifndef SGX_LZ4_BATCH
+#define SGX_LZ4_BATCH 1
+#endif
 
 // unaligned little-endian 32-bit read from the LDS staging buffer: the two aligned dwords
 // around it + one v_alignbyte (instead of four ds_read_u8); the buffer is padded by 8 bytes
@@ -237,6 +247,7 @@ __device__ __forceinline__ int lz4_compress_wave(const Src &src, int n, uint16_t
                 if (it > 0) prn = search_probe(src, start, it + 64, n);
                 const uint32_t seq = pr.s0;
                 const uint32_t h = hash4(seq);
+#if SGX_LZ4_PEER_SHFL
                 const int tcand = table[h];
                 // the table candidate's bytes [cand - 4, cand + 8) load as soon as the entry
                 // arrives (tcand < pos <= n - 12 for a valid lane), before the ballots below
@@ -267,6 +278,27 @@ __device__ __forceinline__ int lz4_compress_wave(const Src &src, int n, uint16_t
                 const uint32_t c4 = lower ? ps4 : tsh == 4 ? cw[2] : __builtin_amdgcn_alignbyte(cw[2], cw[1], (uint32_t)tsh);
                 const uint32_t cbyte = lower ? ppb : cw[0] >> 24;
                 const bool cbok = lower || tsh == 4;  // the byte before the candidate was read
+#else
+                int cand = table[h];
+                uint32_t diff_lo = 0, diff_hi = 0;
+#pragma unroll
+                for (int bt = 0; bt < kHashLog; ++bt) {
+                    const uint32_t sx = (uint32_t)((int32_t)(h << (31 - bt)) >> 31);  // 0 or ~0
+                    const uint64_t m = __ballot(sx != 0);
+                    diff_lo |= (uint32_t)m ^ sx;
+                    diff_hi |= (uint32_t)(m >> 32) ^ sx;
+                }
+                const uint64_t peers = ~(((uint64_t)diff_hi << 32) | diff_lo);
+                const uint64_t lower = peers & below;
+                if (lower) cand = start + skip_dist(it + 63 - (int)__builtin_clzll(lower));
+                const int tc = min(cand, n - 12), tb0 = max(tc - 4, 0), tsh = tc - tb0;
+                uint32_t cw[3];
+                src.words(tb0, cw);
+                const uint32_t c0 = tsh == 4 ? cw[1] : __builtin_amdgcn_alignbyte(cw[1], cw[0], (uint32_t)tsh);
+                const uint32_t c4 = tsh == 4 ? cw[2] : __builtin_amdgcn_alignbyte(cw[2], cw[1], (uint32_t)tsh);
+                const uint32_t cbyte = cw[0] >> 24;
+                const bool cbok = tsh == 4;
+#endif
                 const bool hit = c0 == seq && valid;
                 const uint64_t vm = __ballot(valid), hm = __ballot(hit);
                 const int kinv = first_clear(vm);
@@ -424,6 +456,289 @@ last_literals:
     return op;
 }
 
+// LZ4_compress_default of src[0, n) again, with several sequences per batch (round 4,
+// SGX_LZ4_BATCH).  A batch whose lanes probe consecutive positions (the first 64 iterations
+// of a search: step 1) keeps going after a match that ends inside it: the match's end ip,
+// `_next_match`'s ip - 2 and ip, and the next search's positions ip + 1, ip + 2, ... are all
+// lanes of the same batch, already loaded and hashed.  The serial table state a lane must see
+// follows from a mask W of the batch's lanes whose positions the serial code has inserted so
+// far (every insertion is at a higher position than the last, so "the latest inserted lane
+// below me with my hash" is the entry it would read; no such lane: the batch-start entry);
+// the table receives W's last writer per hash when the batch ends.  A candidate that is
+// another lane comes with that lane's probe bytes (shuffle / readlane); one from the table
+// with the bytes the lane loaded at the batch start.  So a C1 Kryo block's short sequences
+// cost a few wave instructions each instead of a batch plus one to three memory round trips.
+// Matches that end past the batch, and batches of a search's later iterations (steps > 1),
+// go the way of lz4_compress_wave.  Same iterations, same table, same bytes.
+template <typename Src>
+__device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_t *table, uint8_t *out, int cap) {
+    const int lane = (int)(threadIdx.x & 63);
+    const uint64_t below = (1ull << lane) - 1ull;
+    int anchor = 0, op = 0;
+    if (n >= kMfLimit + 1) {
+        const int lim = n - kMfLimit + 1;      // mflimit_plus_one
+        const int mlimit = n - kLastLiterals;  // matchlimit
+        if (lane == 0) table[hash4(src.u32(0))] = 0;
+        int start = 1, it = 0;  // the running search: its first position, iterations done
+        Probe pr0 = search_probe(src, start, 0, n);
+        bool have_next = false;  // _next_match's sequences from a settled match's probe bytes
+        uint32_t nx_s2 = 0, nx_s0 = 0;
+        for (;;) {  // ---- one batch: iterations [it, it + 64) of the search from `start`
+            const int pos = start + skip_dist(it + lane);
+            const int nxt = pos + max((it + lane + 63) >> 6, 1);  // the position after this one
+            const bool valid = nxt <= lim;
+            const Probe pr = pr0;
+            Probe prn{0, 0, 0, 0};
+            if (it > 0) prn = search_probe(src, start, it + 64, n);  // a search past its first batch runs on
+            const uint32_t h = hash4(pr.s0);
+            const int tcand = table[h];
+            // the batch-start entry's bytes [tcand - 4, tcand + 8) (tcand < pos <= n - 12 for a valid lane)
+            const int tc = min(tcand, n - 12), tb0 = max(tc - 4, 0), tsh = tc - tb0;
+            uint32_t cw[3];
+            src.words(tb0, cw);
+            uint32_t diff_lo = 0, diff_hi = 0;
+#pragma unroll
+            for (int bt = 0; bt < kHashLog; ++bt) {
+                const uint32_t sx = (uint32_t)((int32_t)(h << (31 - bt)) >> 31);  // 0 or ~0
+                const uint64_t m = __ballot(sx != 0);
+                diff_lo |= (uint32_t)m ^ sx;
+                diff_hi |= (uint32_t)(m >> 32) ^ sx;
+            }
+            const uint64_t peers = ~(((uint64_t)diff_hi << 32) | diff_lo);  // lanes with our hash
+            const uint32_t tc0 = tsh == 4 ? cw[1] : __builtin_amdgcn_alignbyte(cw[1], cw[0], (uint32_t)tsh);
+            const uint32_t tc4 = tsh == 4 ? cw[2] : __builtin_amdgcn_alignbyte(cw[2], cw[1], (uint32_t)tsh);
+            const bool consec = it == 0;  // lane j probes start + j
+            uint64_t W = 0;               // lanes whose positions the serial code inserted so far
+            int lo = 0;                   // the running search's first lane
+            bool ended = false;           // no more matches: last literals
+            bool fresh = false;           // pr0 already holds the next batch's probe
+            int next_start = 0, next_it = 0;
+            for (;;) {  // ---- one search inside the batch: lanes [lo, 64)
+                const uint64_t run = ~0ull << lo;
+                const uint64_t elig = peers & below & (W | run);
+                const int pj = elig ? 63 - (int)__builtin_clzll(elig) : lane;
+                const uint32_t ps0 = (uint32_t)__shfl((int)pr.s0, pj), ps4 = (uint32_t)__shfl((int)pr.s4, pj),
+                               ppb = (uint32_t)__shfl((int)pr.pb, pj);
+                const int cand = elig ? start + skip_dist(it + pj) : tcand;
+                const uint32_t c0 = elig ? ps0 : tc0, c4 = elig ? ps4 : tc4, cbyte = elig ? ppb : cw[0] >> 24;
+                const bool cbok = elig || tsh == 4;  // the byte before the candidate was read
+                const bool hit = ((run >> lane) & 1ull) && valid && c0 == pr.s0;
+                const uint64_t hm = __ballot(hit), inv = ~__ballot(valid) & run;
+                const int kinv = inv ? (int)__builtin_ctzll(inv) : 64;
+                const int khit = hm ? (int)__builtin_ctzll(hm) : 64;
+                const int kend = khit < kinv ? khit + 1 : kinv;  // iterations [lo, kend) ran
+                W |= (kend >= 64 ? ~0ull : (1ull << kend) - 1ull) & run;
+                if (khit >= kinv) {
+                    if (kinv < 64) {  // the next position passes mflimit: no match in this block
+                        ended = true;
+                    } else {          // the search runs on in the next batch
+                        next_start = lo == 0 ? start : start + lo;  // (lo > 0: a consecutive batch)
+                        next_it = lo == 0 ? it + 64 : 64 - lo;
+                    }
+                    break;
+                }
+                // ---- a match at lane khit
+                int ip = lane_value(pos, khit);
+                int match = lane_value(cand, khit);
+                const uint32_t hs0 = (uint32_t)lane_value((int)pr.s0, khit), hs4 = (uint32_t)lane_value((int)pr.s4, khit),
+                               hs8 = (uint32_t)lane_value((int)pr.s8, khit), hpb = (uint32_t)lane_value((int)pr.pb, khit),
+                               hc4 = (uint32_t)lane_value((int)c4, khit), hcb = (uint32_t)lane_value((int)cbyte, khit);
+                const bool hcbok = (__ballot(cbok) >> khit) & 1ull;
+                int aend;
+                {  // catch-up and LZ4_count from ip + 4, settled from the probe bytes when possible
+                    const int d0 = match - ip, a0 = ip + kMinMatch;
+                    const bool no_back = ip - 1 < anchor || match < 1 || (hcbok && hpb != hcb);
+                    const bool short_end = a0 + 4 <= mlimit && hs4 != hc4;
+                    if (no_back && short_end) {
+                        aend = a0 + ((int)__builtin_ctz(hs4 ^ hc4) >> 3);
+                        const uint32_t k = (uint32_t)(aend - ip);  // 4..7: ip + 2 .. ip + 10 are probe bytes
+                        nx_s0 = k == 4 ? hs4 : __builtin_amdgcn_alignbyte(hs8, hs4, k - 4);
+                        nx_s2 = k - 2 < 4 ? __builtin_amdgcn_alignbyte(hs4, hs0, k - 2)
+                                          : __builtin_amdgcn_alignbyte(hs8, hs4, k - 6);
+                        have_next = true;
+                    } else {
+                        have_next = false;
+                        const int al = a0 + 4 * lane;
+                        const bool full = al + 4 <= mlimit;
+                        const uint32_t d = full ? src.u32(al) ^ src.u32(al + d0) : 0u;
+                        if (!no_back) {
+                            for (;;) {
+                                const int a = ip - 1 - lane, b = match - 1 - lane;
+                                const bool eq = (src.u8(max(a, 0)) == src.u8(max(b, 0))) && a >= anchor && b >= 0;
+                                const int back = first_clear(__ballot(eq));
+                                ip -= back;
+                                match -= back;
+                                if (back < 64) break;
+                            }
+                        }
+                        aend = lz4_count_end(src, a0, d0, mlimit, d, full);
+                    }
+                }
+                // ---- literals
+                const int lit = ip - anchor;
+                if (op + 1 + lit / 255 + 1 + lit + 2 + 1 > cap) return -1;
+                if (op + 1 + lit + 2 >= n) return n;  // RAW (see lz4_compress_wave)
+                int token = op++;
+                uint32_t tk;
+                if (lit >= 15) {
+                    const int nrun = (lit - 15) / 255;
+                    for (int j = lane; j <= nrun; j += 64) out[op + j] = j < nrun ? (uint8_t)255 : (uint8_t)((lit - 15) % 255);
+                    op += nrun + 1;
+                    tk = 15u << 4;
+                } else {
+                    tk = (uint32_t)lit << 4;
+                }
+                if (consec && anchor >= start - 1) {
+                    // the literals [anchor, ip) are this batch's positions (and lane 0's byte
+                    // before them): their bytes come from the probes, not from memory
+                    const int sl = anchor + lane - start;
+                    const uint32_t v0 = (uint32_t)__shfl((int)pr.s0, max(sl, 0)), vb = (uint32_t)__shfl((int)pr.pb, 0);
+                    if (lane < lit) out[op + lane] = (uint8_t)(sl < 0 ? vb : v0);
+                } else {
+                    for (int j = lane; j < lit; j += 64) out[op + j] = (uint8_t)src.u8(anchor + j);
+                }
+                op += lit;
+                bool cont = false;  // the next search continues inside this batch from lane lo
+                for (;;) {          // ---- _next_match
+                    const uint32_t off = (uint32_t)(ip - match);
+                    if (lane == 0) {
+                        out[op] = (uint8_t)off;
+                        out[op + 1] = (uint8_t)(off >> 8);
+                    }
+                    op += 2;
+                    uint32_t mc = (uint32_t)(aend - (ip + kMinMatch));
+                    if (op + (int)(mc / 255) + 1 + 3 > cap) return -1;
+                    ip = aend;
+                    if (mc >= 15) {
+                        tk += 15;
+                        mc -= 15;
+                        const int nrun = (int)(mc / 255);
+                        for (int j = lane; j <= nrun; j += 64) out[op + j] = j < nrun ? (uint8_t)255 : (uint8_t)(mc % 255);
+                        op += nrun + 1;
+                    } else {
+                        tk += mc;
+                    }
+                    if (lane == 0) out[token] = (uint8_t)tk;
+                    anchor = ip;
+                    if (ip >= lim) {
+                        ended = true;
+                        break;
+                    }
+                    const int a0 = ip - start;  // ip's lane in a consecutive batch
+                    if (consec && a0 < 64) {
+                        // insert ip - 2; the entry for ip's hash (the latest inserted lane below
+                        // a0 with it, else a0's batch-start entry); insert ip
+                        have_next = false;
+                        W |= 1ull << (a0 - 2);
+                        const uint64_t e = peers & below & W;
+                        const uint64_t ea = ((uint64_t)(uint32_t)lane_value((int)(uint32_t)(e >> 32), a0) << 32) |
+                                            (uint32_t)lane_value((int)(uint32_t)e, a0);
+                        int m2;
+                        uint32_t m0, m4;
+                        if (ea) {
+                            const int pl = 63 - (int)__builtin_clzll(ea);
+                            m2 = start + pl;
+                            m0 = (uint32_t)lane_value((int)pr.s0, pl);
+                            m4 = (uint32_t)lane_value((int)pr.s4, pl);
+                        } else {
+                            m2 = lane_value(tcand, a0);
+                            m0 = (uint32_t)lane_value((int)tc0, a0);
+                            m4 = (uint32_t)lane_value((int)tc4, a0);
+                        }
+                        W |= 1ull << a0;
+                        const uint32_t s0 = (uint32_t)lane_value((int)pr.s0, a0), s4 = (uint32_t)lane_value((int)pr.s4, a0);
+                        if (m0 != s0) {  // no match at ip: the next search starts at ip + 1
+                            lo = a0 + 1;
+                            cont = lo < 64;
+                            if (!cont) {
+                                next_start = ip + 1;
+                                next_it = 0;
+                            }
+                            break;
+                        }
+                        match = m2;
+                        token = op++;
+                        tk = 0;
+                        const int a = ip + kMinMatch;
+                        if (a + 4 <= mlimit && s4 != m4) {
+                            aend = a + ((int)__builtin_ctz(s4 ^ m4) >> 3);
+                        } else {
+                            const int d0 = m2 - ip, al = a + 4 * lane;
+                            const bool full = al + 4 <= mlimit;
+                            const uint32_t d = full ? src.u32(al) ^ src.u32(al + d0) : 0u;
+                            aend = lz4_count_end(src, a, d0, mlimit, d, full);
+                        }
+                        continue;
+                    }
+                    // past the batch: its insertions go to the table first, then the serial test
+                    if ((W >> lane) & 1ull) {
+                        if (((peers & W) >> lane) == 1ull) table[h] = (uint16_t)pos;
+                    }
+                    W = 0;
+                    __builtin_amdgcn_wave_barrier();
+                    pr0 = search_probe(src, ip + 1, 0, n);  // the next search's first batch
+                    fresh = true;
+                    uint32_t s2, s0;
+                    if (have_next) {
+                        s2 = nx_s2;
+                        s0 = nx_s0;
+                        have_next = false;
+                    } else {
+                        s2 = src.u32(ip - 2);
+                        s0 = src.u32(ip);
+                    }
+                    if (lane == 0) table[hash4(s2)] = (uint16_t)(ip - 2);
+                    __builtin_amdgcn_wave_barrier();
+                    const uint32_t hh = hash4(s0);
+                    const int m2 = table[hh];
+                    __builtin_amdgcn_wave_barrier();
+                    if (lane == 0) table[hh] = (uint16_t)ip;
+                    const int d0 = m2 - ip, al = ip + kMinMatch + 4 * lane;
+                    const bool full = al + 4 <= mlimit;
+                    const uint32_t d = full ? src.u32(al) ^ src.u32(al + d0) : 0u;
+                    if (src.u32(m2) != s0) {
+                        next_start = ip + 1;
+                        next_it = 0;
+                        break;
+                    }
+                    match = m2;
+                    token = op++;
+                    tk = 0;
+                    aend = lz4_count_end(src, ip + kMinMatch, d0, mlimit, d, full);
+                }
+                if (ended || !cont) break;
+            }
+            // ---- the batch's insertions: per hash, its last inserted lane
+            if ((W >> lane) & 1ull) {
+                if (((peers & W) >> lane) == 1ull) table[h] = (uint16_t)pos;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (ended) break;
+            if (!fresh) pr0 = (it > 0 && next_start == start && next_it == it + 64) ? prn : search_probe(src, next_start, next_it, n);
+            start = next_start;
+            it = next_it;
+        }
+    }
+    {  // last literals
+        const int last = n - anchor;
+        if (op + 1 + last / 255 + 1 + last > cap) return -1;
+        const int fin = op + 1 + (last >= 15 ? (last - 15) / 255 + 1 : 0) + last;
+        if (fin >= n) return fin;  // RAW: nothing to write
+        if (last >= 15) {
+            const int nrun = (last - 15) / 255;
+            if (lane == 0) out[op] = 15u << 4;
+            for (int j = lane; j <= nrun; j += 64) out[op + 1 + j] = j < nrun ? (uint8_t)255 : (uint8_t)((last - 15) % 255);
+            op += nrun + 2;
+        } else {
+            if (lane == 0) out[op] = (uint8_t)(last << 4);
+            ++op;
+        }
+        for (int j = lane; j < last; j += 64) out[op + j] = (uint8_t)src.u8(anchor + j);
+        op += last;
+    }
+    return op;
+}
+
 __device__ __forceinline__ void st32le(uint8_t *p, uint32_t v) {
     p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
 }
@@ -466,7 +781,11 @@ __global__ __launch_bounds__(64) void k_lz4_blocks(const uint8_t *__restrict__ s
     uint8_t *slot = slots + b * slot_bytes;
     __syncthreads();
     const GlobalSrc src{stream + boff};
+#if SGX_LZ4_BATCH
+    const int sc = lz4_compress_batch(src, n, s_tab, slot + kHeader, (int)(slot_bytes - kHeader));
+#else
     const int sc = lz4_compress_wave(src, n, s_tab, slot + kHeader, (int)(slot_bytes - kHeader));
+#endif
     if (sc < 0) {
         if (lane == 0) {
             err[1] = b;
