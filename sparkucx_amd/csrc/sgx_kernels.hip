@@ -1144,6 +1144,11 @@ extern "C" int sgx_diag_wc_stamps(unsigned long long *out16, int reset) {
 #ifndef SGX_WC_LATE
 #define SGX_WC_LATE 0
 #endif
+// Records per written unit of the write-combining K4: 8 (a 128 B L2 line); an A/B probe of
+// 64 B units (-DSGX_WC_LINE_RECS=4) asks whether half lines leave HBM as cheaply.
+#ifndef SGX_WC_LINE_RECS
+#define SGX_WC_LINE_RECS 8
+#endif
 
 __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
     return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 16;  // e, LE, {dw, dt}
@@ -1362,7 +1367,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             c = ((const uint2 *)pe)[j];
             a = ((const uint2 *)ple)[j];
             e = make_uint2(c.x + (tot & 0xFFFFu), c.y + (tot >> 16));
-            kf = make_uint2(e.x - max(e.x & ~7u, a.x), e.y - max(e.y & ~7u, a.y));  // kept if no flush
+            kf = make_uint2(e.x - max(e.x & ~(SGX_WC_LINE_RECS - 1u), a.x),
+                            e.y - max(e.y & ~(SGX_WC_LINE_RECS - 1u), a.y));  // kept if no flush
             S = (e.x - a.x) + (e.y - a.y);
             D = kf.x + kf.y;
         }
