@@ -55,6 +55,9 @@ def parse():
     ap.add_argument("--cpu-baseline-seconds", type=float, default=16.0,
                     help="budget of the CPU baseline's timed legs (plus ~5 s of C0 and setup)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-live-pmc", action="store_true",
+                    help="N=1: skip the two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) that measure this "
+                         "run's HBM bytes per launch (roofline.traffic); the committed profiles/pmc_map.json is used")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--comm", choices=["rccl", "host"], default="rccl",
                     help="N > 1 exchange backend: RCCL over xGMI (the product path) or host collectives "
@@ -180,6 +183,77 @@ def load_pmc(dist, n, R, rb=16, padded=True):
         return None
 
 
+def live_pmc(args):
+    """HBM bytes of this workload's map side, measured now: two rocprofv3 --pmc passes
+    (FETCH_SIZE, then WRITE_SIZE: one counter per pass, nothing else traced) over
+    tools/prof_map.py writing the same records, partitions and layout twice, run as child
+    processes before this process touches the GPU.  Per kernel: the median launch's counter
+    x launches per write; reads are FETCH_SIZE x 2 KiB (gfx950 counts half of a wide stream,
+    MI355X_MICROARCH.md), writes WRITE_SIZE x 1 KiB.  Returns the pmc_map.json shape, or None."""
+    import csv
+    import glob
+    import shutil
+    import subprocess
+    import tempfile
+
+    exe = shutil.which("rocprofv3")
+    if exe is None:
+        return None
+    flags = 256 if args.no_padded else 0
+    if args.no_split:
+        flags |= 32  # FLAG_NO_SPLIT_SCATTER (sparkucx_amd is not imported yet)
+    cmd_tail = ["--", sys.executable, os.path.join(ROOT, "tools", "prof_map.py"), "--iters", "2",
+                "--records", str(args.records), "--partitions", str(args.partitions), "--dist", args.dist,
+                "--record-bytes", str(args.record_bytes), "--flags", str(flags), "--num-chunks", str(args.num_chunks)]
+    per = {}
+    tmp = tempfile.mkdtemp(prefix="sgx_pmc_")
+    try:
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(tmp, counter)
+            r = subprocess.run([exe, "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run"] + cmd_tail,
+                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL, timeout=180)
+            files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
+            if r.returncode != 0 or not files:
+                return None
+            vals = {}
+            for f in files:
+                with open(f) as fh:
+                    for row in csv.DictReader(fh):
+                        if row["Counter_Name"] == counter:
+                            k = row["Kernel_Name"].split("(")[0].replace("void ", "").strip()
+                            vals.setdefault(k, []).append(float(row["Counter_Value"]))
+            per[counter] = vals
+    except (OSError, subprocess.SubprocessError):
+        return None
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    import statistics
+
+    algo = 2 * args.record_bytes * args.records
+    side = {"read": 0.0, "write": 0.0}
+    k4 = {"kernel": None, "hbm_bytes_per_launch": 0, "read_bytes": 0, "write_bytes": 0, "algorithmic_bytes": algo}
+    names = set(per["FETCH_SIZE"]) | set(per["WRITE_SIZE"])
+    for k in sorted(names):
+        if k.replace("sgx::", "").startswith(("k_gen", "k_lds_order_probe")):
+            continue  # the input generator; the engine-start LDS ordering check
+        f, w = per["FETCH_SIZE"].get(k, []), per["WRITE_SIZE"].get(k, [])
+        calls = max(len(f), len(w)) / 2.0  # launches per write (two writes)
+        rd = statistics.median(f) * 2 * 1024 if f else 0.0
+        wr = statistics.median(w) * 1024 if w else 0.0
+        side["read"] += rd * calls
+        side["write"] += wr * calls
+        if k.replace("sgx::", "").startswith("k_scatter") and rd + wr > 1e6:  # (not the guarded fallback's no-op)
+            k4["kernel"] = k if k4["kernel"] is None else k4["kernel"] + " + " + k
+            k4["hbm_bytes_per_launch"] += int((rd + wr) * calls)
+            k4["read_bytes"] += int(rd * calls)
+            k4["write_bytes"] += int(wr * calls)
+    tot = side["read"] + side["write"]
+    return {"scatter": k4, "map_side": {"hbm_bytes_per_write": int(tot), "read_bytes": int(side["read"]),
+                                        "write_bytes": int(side["write"]), "algorithmic_bytes": algo,
+                                        "ratio": round(tot / algo, 4)},
+            "source": "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/prof_map.py in this bench run"}
+
+
 def _workload_name(args, n, R, world, self_x):
     x = ("RCCL alltoallv" if args.comm == "rccl" else "host all-to-all (rehearsal)") if world > 1 else (
         "exchange through a 1-rank RCCL communicator (rehearsal)" if self_x else None)
@@ -202,6 +276,10 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    # this run's HBM bytes first, in child processes, before this one touches the GPU
+    live = None
+    if world == 1 and not args.no_live_pmc and args.serializer == "fixed" and not args.self_exchange:
+        live = live_pmc(args)
     import numpy as np
     import torch
 
@@ -334,7 +412,7 @@ def main():
         algo = 2 * rb  # the record read once and written once
         achieved = algo * n / (sc_ms * 1e-3) / 1e9
         padded = layout == sgx.LAYOUT_PADDED
-        pmc = load_pmc(args.dist if rb == 16 else "terasort", n, R, rb, padded) or {}
+        pmc = live or load_pmc(args.dist if rb == 16 else "terasort", n, R, rb, padded) or {}
         k4_pmc, side_pmc = pmc.get("scatter") or {}, pmc.get("map_side") or {}
         side_ms = (st.ms["hist"] + st.ms["scan"] + st.ms["scatter"]) / max(1, st.count["scatter"])
         side_ach = algo * n / (side_ms * 1e-3) / 1e9
