@@ -466,7 +466,7 @@ def main():
                 c_ms = st.ms["compress"] / max(1, st.count["compress"])
                 out["lz4"] = {"kernel": "k_lz4_blocks", "ms": round(c_ms, 4), "framed_bytes": kbytes,
                               "note": "k_lz4_blocks + k_xxh32_blocks: one wave per 32 KiB block, LZ4_compress_default's "
-                                      "search 64 iterations per step (DESIGN.md §14)"}
+                                      "search 64 positions per batch, several sequences per batch (DESIGN.md §14)"}
             if world == 1:
                 # reduce side of the same shuffle: every block of the last map, decoded on the GPU
                 dst = eng.alloc(n * 16)

@@ -16,6 +16,7 @@ import pytest
 from conftest import GOLDEN
 
 FIXTURES = sorted(glob.glob(os.path.join(GOLDEN, "lz4_*.npz")))
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _liblz4():
@@ -597,3 +598,50 @@ def test_gpu_serializer_cannot_leave_kryo_while_compressed(sgx_lib):
             e.set_serializer(1, sgx_lib.SER_FIXED)
         e.set_compression(1, "none")
         e.set_serializer(1, sgx_lib.SER_FIXED)  # allowed once compression is off
+
+
+def _batch_shapes(oracle_lib, size):
+    """Block shapes for the multi-sequence batch compressor (sgx_lz4.hip lz4_compress_batch):
+    C1's Kryo stream (short matches every ~16 bytes: several sequences per 64-position batch),
+    a low-entropy stream (matches that end inside the batch and hit again at `_next_match`),
+    byte runs over three symbols (long matches past the batch, catch-ups), a period of 10,
+    uniform bytes (no matches: the search's later, wider steps) and a stream of 8-byte
+    repeats at batch-straddling offsets."""
+    rng = np.random.default_rng(23)
+    recs = oracle_lib.gen_uniform16(size // 8, 7, value_base=3 << 32)
+    kryo = oracle_lib.kryo_serialize(recs).tobytes()
+    low = b"".join(int(i % 4096).to_bytes(8, "little") + int(i).to_bytes(8, "little") for i in range(size // 16))
+    rep = b"".join(bytes(rng.integers(0, 256, 8, dtype=np.uint8)) * int(rng.integers(1, 4)) + bytes(rng.integers(0, 256, int(rng.integers(1, 70)), dtype=np.uint8))
+                   for _ in range(size // 40))
+    return [kryo[:size], low[:size], bytes(rng.integers(0, 3, size, dtype=np.uint8)), (b"abcdefghij" * (size // 10 + 1))[:size],
+            bytes(rng.integers(0, 256, size, dtype=np.uint8)), rep[:size]]
+
+
+def test_batch_model_matches_oracle(oracle_lib):
+    """The host model of the batch compressor's table state (tools/lz4_batch_model.py) against
+    the oracle, on 4 KiB blocks of every shape (the GPU test below runs the kernel)."""
+    import importlib.util
+
+    spec = importlib.util.spec_from_file_location("lz4_batch_model", os.path.join(ROOT, "tools", "lz4_batch_model.py"))
+    model = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(model)
+    for blk in _batch_shapes(oracle_lib, 4096):
+        assert model.compress(blk) == oracle_lib.lz4_compress_block(blk)
+
+
+@pytest.mark.gpu
+def test_gpu_batch_compressor_shapes(engine, oracle_lib):
+    """Every batch-compressor shape as 32 KiB blocks (and ragged tails) through the GPU
+    framing, byte-identical to the oracle."""
+    cases = [c[:n] for c in _batch_shapes(oracle_lib, 65536) for n in (65536, 40001)]
+    stream = b"".join(cases)
+    offs = np.zeros(len(cases) + 1, dtype=np.int64)
+    np.cumsum([len(c) for c in cases], out=offs[1:])
+    buf = _to_device(engine, stream)
+    try:
+        framed, lens = engine.lz4_frame(buf.ptr, offs, 32768)
+    finally:
+        buf.free()
+    want, wlens = oracle_lib.lz4_frame_partitions(np.frombuffer(stream, np.uint8), offs, 32768)
+    assert np.array_equal(lens, wlens)
+    assert framed.tobytes() == want.tobytes()
