@@ -41,6 +41,37 @@ constexpr int kHeader = 21;
 #ifndef SGX_LZ4_PEER_SHFL
 #define SGX_LZ4_PEER_SHFL 1
 #endif
+// Diagnostic build only (-DSGX_LZ4_STAMPS, tools/lz4_stamps.py): per-phase s_memtime sums of
+// lz4_compress_batch, read through sgx_diag_lz4_stamps.  Never in libsgx.so; the stamps' waits
+// (lgkmcnt(0), and vmcnt(0) where a phase is a memory wait) change the run: read the SHARES.
+#ifdef SGX_LZ4_STAMPS
+__device__ unsigned long long g_lz4_stamps[16];
+__device__ __forceinline__ uint64_t lz4_stamp_now() {
+    uint64_t t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return t;
+}
+#define LZ4_STAMP(i)                          \
+    do {                                      \
+        const uint64_t t_ = lz4_stamp_now();  \
+        st_acc[i] += t_ - st_last;            \
+        st_last = t_;                         \
+    } while (0)
+#define LZ4_STAMP_VM(i)                                           \
+    do {                                                          \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");          \
+        LZ4_STAMP(i);                                             \
+    } while (0)
+#else
+#define LZ4_STAMP(i) \
+    do {             \
+    } while (0)
+#define LZ4_STAMP_VM(i) \
+    do {                \
+    } while (0)
+#endif
 // lz4_compress_batch (several sequences per batch, 1) or lz4_compress_wave (0)
 #ifndef SGX_LZ4_BATCH
 #define SGX_LZ4_BATCH 1
@@ -475,6 +506,10 @@ __device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_
     const int lane = (int)(threadIdx.x & 63);
     const uint64_t below = (1ull << lane) - 1ull;
     int anchor = 0, op = 0;
+#ifdef SGX_LZ4_STAMPS
+    uint64_t st_acc[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_last = lz4_stamp_now();
+#endif
     if (n >= kMfLimit + 1) {
         const int lim = n - kMfLimit + 1;      // mflimit_plus_one
         const int mlimit = n - kLastLiterals;  // matchlimit
@@ -487,6 +522,7 @@ __device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_
             const int pos = start + skip_dist(it + lane);
             const int nxt = pos + max((it + lane + 63) >> 6, 1);  // the position after this one
             const bool valid = nxt <= lim;
+            LZ4_STAMP_VM(0);  // 0: the batch's probe bytes (loaded at the last batch's end or earlier)
             const Probe pr = pr0;
             Probe prn{0, 0, 0, 0};
             if (it > 0) prn = search_probe(src, start, it + 64, n);  // a search past its first batch runs on
@@ -496,6 +532,7 @@ __device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_
             const int tc = min(tcand, n - 12), tb0 = max(tc - 4, 0), tsh = tc - tb0;
             uint32_t cw[3];
             src.words(tb0, cw);
+            LZ4_STAMP(1);  // 1: hash, table read
             uint32_t diff_lo = 0, diff_hi = 0;
 #pragma unroll
             for (int bt = 0; bt < kHashLog; ++bt) {
@@ -505,8 +542,10 @@ __device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_
                 diff_hi |= (uint32_t)(m >> 32) ^ sx;
             }
             const uint64_t peers = ~(((uint64_t)diff_hi << 32) | diff_lo);  // lanes with our hash
+            LZ4_STAMP(2);  // 2: the 13 same-hash ballots
             const uint32_t tc0 = tsh == 4 ? cw[1] : __builtin_amdgcn_alignbyte(cw[1], cw[0], (uint32_t)tsh);
             const uint32_t tc4 = tsh == 4 ? cw[2] : __builtin_amdgcn_alignbyte(cw[2], cw[1], (uint32_t)tsh);
+            LZ4_STAMP_VM(3);  // 3: the table candidates' bytes
             const bool consec = it == 0;  // lane j probes start + j
             uint64_t W = 0;               // lanes whose positions the serial code inserted so far
             int lo = 0;                   // the running search's first lane
@@ -527,6 +566,7 @@ __device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_
                 const int kinv = inv ? (int)__builtin_ctzll(inv) : 64;
                 const int khit = hm ? (int)__builtin_ctzll(hm) : 64;
                 const int kend = khit < kinv ? khit + 1 : kinv;  // iterations [lo, kend) ran
+                LZ4_STAMP(4);  // 4: a search in the batch (candidates, shuffles, hit ballots)
                 W |= (kend >= 64 ? ~0ull : (1ull << kend) - 1ull) & run;
                 if (khit >= kinv) {
                     if (kinv < 64) {  // the next position passes mflimit: no match in this block
@@ -574,6 +614,7 @@ __device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_
                         aend = lz4_count_end(src, a0, d0, mlimit, d, full);
                     }
                 }
+                LZ4_STAMP_VM(5);  // 5: the hit's catch-up and count (fast: readlanes; slow: loads)
                 // ---- literals
                 const int lit = ip - anchor;
                 if (op + 1 + lit / 255 + 1 + lit + 2 + 1 > cap) return -1;
@@ -619,6 +660,7 @@ __device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_
                         tk += mc;
                     }
                     if (lane == 0) out[token] = (uint8_t)tk;
+                    LZ4_STAMP(6);  // 6: the sequence's output bytes (stores issued)
                     anchor = ip;
                     if (ip >= lim) {
                         ended = true;
@@ -647,6 +689,7 @@ __device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_
                         }
                         W |= 1ull << a0;
                         const uint32_t s0 = (uint32_t)lane_value((int)pr.s0, a0), s4 = (uint32_t)lane_value((int)pr.s4, a0);
+                        LZ4_STAMP(7);  // 7: _next_match's test inside the batch
                         if (m0 != s0) {  // no match at ip: the next search starts at ip + 1
                             lo = a0 + 1;
                             cont = lo < 64;
@@ -696,6 +739,7 @@ __device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_
                     const int d0 = m2 - ip, al = ip + kMinMatch + 4 * lane;
                     const bool full = al + 4 <= mlimit;
                     const uint32_t d = full ? src.u32(al) ^ src.u32(al + d0) : 0u;
+                    LZ4_STAMP_VM(8);  // 8: _next_match's test past the batch (table, loads)
                     if (src.u32(m2) != s0) {
                         next_start = ip + 1;
                         next_it = 0;
@@ -708,6 +752,7 @@ __device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_
                 }
                 if (ended || !cont) break;
             }
+            LZ4_STAMP(9);  // 9: (the batch's last search / exits)
             // ---- the batch's insertions: per hash, its last inserted lane
             if ((W >> lane) & 1ull) {
                 if (((peers & W) >> lane) == 1ull) table[h] = (uint16_t)pos;
@@ -719,6 +764,12 @@ __device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_
             it = next_it;
         }
     }
+#ifdef SGX_LZ4_STAMPS
+    if (lane == 0) {
+        for (int i = 0; i < 10; ++i) atomicAdd(&g_lz4_stamps[i], (unsigned long long)st_acc[i]);
+        atomicAdd(&g_lz4_stamps[15], 1ull);
+    }
+#endif
     {  // last literals
         const int last = n - anchor;
         if (op + 1 + last / 255 + 1 + last > cap) return -1;
@@ -739,6 +790,21 @@ __device__ __forceinline__ int lz4_compress_batch(const Src &src, int n, uint16_
     return op;
 }
 
+#ifdef SGX_LZ4_STAMPS
+}  // namespace
+}  // namespace sgx
+extern "C" int sgx_diag_lz4_stamps(unsigned long long *out16, int reset) {
+    if (hipDeviceSynchronize() != hipSuccess) return -1;
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(sgx::g_lz4_stamps), 16 * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(sgx::g_lz4_stamps), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+namespace sgx {
+namespace {
+#endif
 __device__ __forceinline__ void st32le(uint8_t *p, uint32_t v) {
     p[0] = (uint8_t)v; p[1] = (uint8_t)(v >> 8); p[2] = (uint8_t)(v >> 16); p[3] = (uint8_t)(v >> 24);
 }
