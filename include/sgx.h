@@ -77,8 +77,11 @@ enum sgx_flags {
     SGX_FLAG_NO_PADDED_MAP = 256,     /* hash maps always take the two-pass map side (histogram
                                          + scan + scatter) instead of the single-pass padded
                                          write (sgx_map_layout)                                */
-    SGX_FLAG_PAD_ANY_SIZE = 512       /* testing: write maps of any size padded (default: from
+    SGX_FLAG_PAD_ANY_SIZE = 512,      /* testing: write maps of any size padded (default: from
                                          2^20 records up)                                      */
+    SGX_FLAG_NO_SEG_WINDOW = 1024     /* sorted reads of several partitions: the key window and
+                                         the partitioner in two LSD passes instead of one
+                                         segmented pass per partition                          */
 };
 
 typedef struct sgx_config {

@@ -33,6 +33,7 @@ FLAG_NO_BUCKET_SORT = 64
 FLAG_ASSUME_LDS_DISORDER = 128
 FLAG_NO_PADDED_MAP = 256
 FLAG_PAD_ANY_SIZE = 512
+FLAG_NO_SEG_WINDOW = 1024
 LAYOUT_CONTIGUOUS, LAYOUT_PADDED = 0, 1
 PLACE_EVEN, PLACE_BYTES = 0, 1
 WRITER_SORT, WRITER_UNSAFE = 0, 1

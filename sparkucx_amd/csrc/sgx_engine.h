@@ -281,6 +281,11 @@ struct Ctx {
     // reduce side and map-side combine
     DevBuf kryo_in, kryo_work, sort_buf[2], sort_err, grp_status, grp_out;
     DevBuf digit_hist, items_dev, gather_stage, fetch_tmp, comb_buf;
+    // records of each partition in c.sort_buf[0] after the last fixed-codec gather (canonical
+    // reducer-major order: the partitions are contiguous), empty when unknown (Kryo reads)
+    std::vector<int64_t> gather_part_recs;
+    DevBuf seg_work;  // the segmented window pass: [desc][ndesc | seg_end][counts][offsets]
+    HostPinned seg_desc_host;
     HostPinned gather_items;
     HostPinned seg_host;  // (partition, spill) segment offsets of an UnsafeShuffleWriter commit
     // LZ4 framing / unframing scratch (grow-only)

@@ -2099,13 +2099,22 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
                                 const ScatterGeom &geo, uint32_t *err, hipStream_t stream) {
     if ((pp.R & (pp.R - 1)) != 0) return hipErrorInvalidValue;
     if (pp.pad_cnt && (!pp.pad_cap || !pp.olim)) return hipErrorInvalidValue;
-#define SGX_WCS(W, NI, SI, M)                                                                                \
+    // the map side's split level 2 (hash bits), or the sorted read's segmented window pass
+    // (key bits, never padded)
+    const bool key_bits = pp.kind == KIND_KEY_BITS;
+    if (key_bits && pp.pad_cnt) return hipErrorInvalidValue;
+#define SGX_WCS_K(K, W, NI, SI, M)                                                                           \
     do {                                                                                                     \
-        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<KIND_HASH_POW2, W, NI, SI, true, M>,         \
+        (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, W, NI, SI, true, M>,                      \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)geo.lds_bytes);           \
-        hipLaunchKernelGGL((k_scatter16_wc<KIND_HASH_POW2, W, NI, SI, true, M>), dim3(grid), dim3(W * 64),   \
+        hipLaunchKernelGGL((k_scatter16_wc<K, W, NI, SI, true, M>), dim3(grid), dim3(W * 64),                \
                            geo.lds_bytes, stream, (const u32x4 *)in, (u32x4 *)out, n, (int64_t)0, pp, offs, G, \
                            err, desc, ndesc, nullptr, 0u, seg_end);                                         \
+    } while (0)
+#define SGX_WCS(W, NI, SI, M)                                         \
+    do {                                                              \
+        if (key_bits) SGX_WCS_K(KIND_KEY_BITS, W, NI, SI, 0);         \
+        else SGX_WCS_K(KIND_HASH_POW2, W, NI, SI, M);                 \
     } while (0)
     const int W = geo.waves - WC_GEOM_BASE;
     const bool pad = pp.pad_cnt != nullptr;
@@ -2117,6 +2126,84 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
         return hipErrorInvalidValue;
     }
 #undef SGX_WCS
+#undef SGX_WCS_K
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// The sorted read's segmented window pass.  After the gather the records of
+// each partition are contiguous (canonical reducer-major order), so sorting by (partition,
+// window bits) needs no pass by the partitioner: one stable write-combining pass by the
+// window bits inside every partition's segment -- K4's SEG mode over pieces of the segments,
+// each piece's streams starting at offsets from a per-piece histogram -- replaces the
+// window pass + partitioner pass (two histograms, two scatters) of the LSD form.
+// ------------------------------------------------------------------------------------
+constexpr int PH_THREADS = 1024;
+__global__ __launch_bounds__(PH_THREADS) void k_piece_hist(const u32x4 *__restrict__ in, int64_t n,
+                                                           const int64_t *__restrict__ desc, int64_t npieces,
+                                                           PartParams pp, int Gmax, uint32_t *__restrict__ cnt) {
+    __shared__ uint32_t h[1024];
+    const uint32_t Q = pp.R, tid = threadIdx.x;
+    for (uint32_t i = tid; i < Q; i += PH_THREADS) h[i] = 0;
+    __syncthreads();
+    const int64_t k = blockIdx.x;
+    const int64_t b = desc[4 * k], e = k + 1 < npieces ? desc[4 * (k + 1)] : n;
+    constexpr int U = 4;  // loads in flight per thread
+    int64_t i = b + tid;
+    for (; i + (U - 1) * PH_THREADS < e; i += U * PH_THREADS) {
+        u32x4 r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[u] = in[i + u * PH_THREADS];
+#pragma unroll
+        for (int u = 0; u < U; ++u) atomicAdd(&h[pid_of<KIND_KEY_BITS>(r[u].x, r[u].y, r[u].z, pp)], 1u);
+    }
+    for (; i < e; i += PH_THREADS) {
+        const u32x4 r = in[i];
+        atomicAdd(&h[pid_of<KIND_KEY_BITS>(r.x, r.y, r.z, pp)], 1u);
+    }
+    __syncthreads();
+    const int64_t sg = desc[4 * k + 2], g = desc[4 * k + 3];
+    for (uint32_t q = tid; q < Q; q += PH_THREADS) cnt[((int64_t)sg * Q + q) * Gmax + g] = h[q];
+}
+
+hipError_t launch_piece_hist(const void *in, int64_t n, const int64_t *desc, int64_t npieces, const PartParams &pp,
+                             int Gmax, uint32_t *cnt, hipStream_t st) {
+    if (npieces <= 0) return hipSuccess;
+    if (pp.kind != KIND_KEY_BITS || pp.R > 1024) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_piece_hist, dim3((unsigned)npieces), dim3(PH_THREADS), 0, st, (const u32x4 *)in, n, desc,
+                       npieces, pp, Gmax, cnt);
+    return hipGetLastError();
+}
+
+// one workgroup per segment: offs over (q, g), q-major, from the segment's first record
+constexpr int SO_THREADS = 256;
+__global__ __launch_bounds__(SO_THREADS) void k_seg_offsets(const uint32_t *__restrict__ cnt,
+                                                            const int64_t *__restrict__ seg_base, uint32_t Q, int Gmax,
+                                                            uint32_t *__restrict__ offs) {
+    __shared__ uint32_t s_w[SO_THREADS / 64];
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int64_t sg = blockIdx.x;
+    const uint32_t m = Q * (uint32_t)Gmax;  // entries of the segment
+    const uint32_t per = (m + SO_THREADS - 1) / SO_THREADS, j0 = min(m, tid * per), j1 = min(m, j0 + per);
+    const uint32_t *c = cnt + (int64_t)sg * m;
+    uint32_t sum = 0;
+    for (uint32_t j = j0; j < j1; ++j) sum += c[j];
+    const uint32_t x = wave_inclusive_scan(sum, lane);
+    if (lane == 63) s_w[w] = x;
+    __syncthreads();
+    uint32_t base = (uint32_t)seg_base[sg] + x - sum;
+    for (uint32_t v = 0; v < w; ++v) base += s_w[v];
+    uint32_t *o = offs + (int64_t)sg * m;
+    for (uint32_t j = j0; j < j1; ++j) {
+        o[j] = base;
+        base += c[j];
+    }
+}
+
+hipError_t launch_seg_offsets(const uint32_t *cnt, const int64_t *seg_base, int64_t nseg, uint32_t Q, int Gmax,
+                              uint32_t *offs, hipStream_t st) {
+    if (nseg <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_seg_offsets, dim3((unsigned)nseg), dim3(SO_THREADS), 0, st, cnt, seg_base, Q, Gmax, offs);
     return hipGetLastError();
 }
 

@@ -225,6 +225,13 @@ static int records_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_id
     int64_t total = 0;
     for (int64_t L : lens) total += L;
     hipStream_t st = c.st;
+    // records per partition, in the gather's (reducer-major) order, for the sorted read's
+    // segmented window pass; unknown for a Kryo stream until it is decoded
+    c.gather_part_recs.clear();
+    if (s.ser != SGX_SER_KRYO && nmaps > 0) {
+        c.gather_part_recs.assign((size_t)(r1 - r0), 0);
+        for (int64_t i = 0; i < nreq; ++i) c.gather_part_recs[(size_t)(i / nmaps)] += lens[(size_t)i] / rb;
+    }
     if (s.ser == SGX_SER_KRYO) {
         // the fetched Kryo stream (blocks back to back are one valid stream) -> records
         *nrec = 0;
@@ -320,7 +327,8 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
     // partitioner, then every bucket sorted on chip (launch_bucket_sort) -- 2-4 passes instead
     // of up to 8-10 digit passes + 1.  Skewed keys (the top varying byte's largest value
     // holding > 1/16 of the records) keep the digit passes, whose trivial digits are skipped.
-    const bool use_p = by_partition && !range_asc && s.R > 1;
+    // (a read of one partition needs no pass by the partitioner: every record has the same one)
+    const bool use_p = by_partition && !range_asc && s.R > 1 && nparts != 1;
     if (skip && !(e->flags & SGX_FLAG_NO_BUCKET_SORT) && (use_p ? s.kind == SGX_PART_HASH : true)) {
         int top_byte = -1;  // most significant varying key byte, as a bit position of the window
         uint32_t maxbin = 0;
@@ -343,7 +351,83 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
                               (double)n / (rp * (double)(1ull << kbits)) <= 256.0;
         if (eligible) {
             const int lo = top - kbits;
-            for (int b0 = lo; b0 < top; b0 += 10) {  // least significant window chunk first
+            // Segmented form: the gather left every partition's records
+            // contiguous, so one stable pass by the window bits inside each partition's segment
+            // replaces the window pass + the pass by the partitioner.  Pieces of <= SEG_PIECE
+            // records; a segment longer than SEG_PIECE_MAX pieces (skew) keeps the LSD form.
+            constexpr int64_t SEG_PIECE = 1 << 17;
+            constexpr int SEG_PIECE_MAX = 8;
+            bool seg_done = false;
+            const std::vector<int64_t> &pr = c.gather_part_recs;
+            int64_t pr_sum = 0, pr_max = 0;
+            for (int64_t x : pr) {
+                pr_sum += x;
+                pr_max = std::max(pr_max, x);
+            }
+            if (use_p && rb == 16 && kbits >= 1 && kbits <= 10 && !(e->flags & SGX_FLAG_NO_SEG_WINDOW) &&
+                (int64_t)pr.size() == (int64_t)(nparts > 0 ? nparts : 0) && pr_sum == n &&
+                (pr_max + SEG_PIECE - 1) / SEG_PIECE <= SEG_PIECE_MAX &&
+                scatter_geom16_wc(1u << kbits).items != 0) {
+                const int64_t nseg = (int64_t)pr.size();
+                const uint32_t Q = 1u << kbits;
+                int Gmax = 1;
+                int64_t npieces = 0;
+                for (int64_t x : pr) {
+                    const int64_t g = std::max<int64_t>(1, (x + SEG_PIECE - 1) / SEG_PIECE);
+                    Gmax = std::max(Gmax, (int)g);
+                    npieces += x > 0 ? g : 0;
+                }
+                // [desc 4 x npieces int64][seg_base nseg int64][ndesc | seg_end u32][cnt][offs]
+                auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+                const size_t b_desc = al((size_t)npieces * 32), b_base = al((size_t)nseg * 8), b_sc = 256;
+                const size_t b_cnt = al((size_t)nseg * Q * Gmax * 4);
+                SGX_TRY(c.seg_work.ensure(b_desc + b_base + b_sc + 2 * b_cnt));
+                SGX_TRY(c.seg_desc_host.ensure(b_desc + b_base + b_sc));
+                char *hw = (char *)c.seg_desc_host.p;
+                int64_t *hd = (int64_t *)hw, *hb = (int64_t *)(hw + b_desc);
+                uint32_t *hsc = (uint32_t *)(hw + b_desc + b_base);
+                int64_t k = 0, pos = 0;
+                for (int64_t sg = 0; sg < nseg; ++sg) {
+                    hb[sg] = pos;
+                    const int64_t x = pr[(size_t)sg];
+                    for (int64_t g = 0, b = 0; b < x; ++g, b += SEG_PIECE, ++k) {
+                        hd[4 * k] = pos + b;
+                        hd[4 * k + 1] = 0;
+                        hd[4 * k + 2] = sg;
+                        hd[4 * k + 3] = g;
+                    }
+                    pos += x;
+                }
+                hsc[0] = (uint32_t)npieces;
+                hsc[1] = (uint32_t)n;
+                char *dw = (char *)c.seg_work.p;
+                const int64_t *ddesc = (const int64_t *)dw;
+                const int64_t *dbase = (const int64_t *)(dw + b_desc);
+                const uint32_t *dnd = (const uint32_t *)(dw + b_desc + b_base);
+                uint32_t *dcnt = (uint32_t *)(dw + b_desc + b_base + b_sc);
+                uint32_t *doffs = (uint32_t *)((char *)dcnt + b_cnt);
+                HIP_TRY(hipMemcpyAsync(dw, hw, b_desc + b_base + b_sc, hipMemcpyHostToDevice, st));
+                HIP_TRY(hipMemsetAsync(dcnt, 0, b_cnt, st));  // pieces a short segment lacks count 0
+                PartParams kp{};
+                kp.kind = KIND_KEY_BITS;
+                kp.R = Q;
+                kp.nbits = (uint32_t)kbits;
+                kp.dshift = (uint32_t)lo;
+                kp.dflip = 1u;
+                const ScatterGeom geo = scatter_geom16_wc(Q);
+                kp.mbits = (uint32_t)geo.mbits;
+                HIP_TRY(launch_piece_hist(c.sort_buf[cur].p, n, ddesc, npieces, kp, Gmax, dcnt, st));
+                HIP_TRY(launch_seg_offsets(dcnt, dbase, nseg, Q, Gmax, doffs, st));
+                HIP_TRY(launch_scatter16_seg(c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, kp, doffs, Gmax, ddesc, dnd,
+                                             dnd + 1, (int)npieces, geo, errs + np, st));
+                SGX_TRY(debug_sync(e, st, "segmented window pass"));
+                // the pinned descriptors are rewritten by the next sort only after this one's
+                // host-side check below has synchronised the stream
+                cur ^= 1;
+                ++np;
+                seg_done = true;
+            }
+            for (int b0 = lo; b0 < top && !seg_done; b0 += 10) {  // least significant window chunk first
                 const int cb = std::min(10, top - b0);
                 PartParams kp{};
                 kp.kind = KIND_KEY_BITS;
@@ -356,7 +440,7 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
                 cur ^= 1;
                 ++np;
             }
-            if (use_p) {
+            if (use_p && !seg_done) {
                 SGX_TRY(partition_pass(e, c, c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, s.pp, s.R, s.kind,
                                        nullptr, errs + np, false));
                 cur ^= 1;

@@ -402,3 +402,34 @@ def test_sorted_bucket_path(sgx_lib, oracle_lib, flags, case):
         recs = oracle_lib.gen_uniform16(300_000, 900)
         recs[10_000:13_000, :8] = recs[9_999, :8]
         _run(sgx_lib, oracle_lib, [recs], 256, flags=flags)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [0, 1024])
+@pytest.mark.parametrize("case", ["pieces", "subrange", "skew_fallback", "grouped_sum", "empty_partitions"])
+def test_sorted_segmented_window(sgx_lib, oracle_lib, flags, case):
+    """The sorted read's segmented window pass (one stable pass by the key window inside every
+    partition's segment of the gathered records) against the oracle, and the
+    LSD form it replaces (SGX_FLAG_NO_SEG_WINDOW = 1024): partitions of several 2^17-record
+    pieces, a sub-range of reducers, a partition too long for the segmented form (it keeps the
+    LSD passes), reduceByKey sums, and empty partitions between full ones."""
+    if case == "pieces":  # 4 reducers x ~200 K records: two pieces each
+        maps = [oracle_lib.gen_uniform16(n, 1000 + i, value_base=i << 32) for i, n in enumerate((500_001, 300_000))]
+        _run(sgx_lib, oracle_lib, maps, 4, flags=flags)
+    elif case == "subrange":
+        maps = [oracle_lib.gen_uniform16(n, 1100 + i, value_base=i << 32) for i, n in enumerate((400_000, 123_457))]
+        _run(sgx_lib, oracle_lib, maps, 64, rng_part=(5, 41), flags=flags)
+    elif case == "skew_fallback":  # 2 reducers x 1.25 M records: > 8 pieces each
+        maps = [oracle_lib.gen_uniform16(2_500_000, 1200)]
+        _run(sgx_lib, oracle_lib, maps, 2, flags=flags)
+    elif case == "grouped_sum":
+        rng = np.random.default_rng(1300)
+        keys = rng.integers(0, 1 << 40, size=600_000, dtype=np.int64)
+        keys[::3] = keys[1::3][: len(keys[::3])]
+        maps = [_records16(keys, rng.integers(-(2**40), 2**40, size=len(keys), dtype=np.int64))]
+        _run(sgx_lib, oracle_lib, maps, 32, agg="sum", flags=flags)
+    else:  # keys that hash to 3 of 16 reducers only: 13 empty segments
+        rng = np.random.default_rng(1400)
+        keys = rng.choice(np.array([1, 2, 3], dtype=np.int64), size=400_000) + 16 * rng.integers(0, 1 << 26, size=400_000)
+        maps = [_records16(keys, np.arange(len(keys), dtype=np.int64))]
+        _run(sgx_lib, oracle_lib, maps, 16, flags=flags)
