@@ -365,7 +365,7 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
                 pr_max = std::max(pr_max, x);
             }
             if (use_p && rb == 16 && kbits >= 1 && kbits <= 10 && !(e->flags & SGX_FLAG_NO_SEG_WINDOW) &&
-                (int64_t)pr.size() == (int64_t)(nparts > 0 ? nparts : 0) && pr_sum == n &&
+                nparts > 0 && (int64_t)pr.size() == (int64_t)nparts && pr_sum == n &&
                 (pr_max + SEG_PIECE - 1) / SEG_PIECE <= SEG_PIECE_MAX &&
                 scatter_geom16_wc(1u << kbits).items != 0) {
                 const int64_t nseg = (int64_t)pr.size();
