@@ -234,13 +234,14 @@ hipError_t launch_copy_items(const void *src, void *dst, const int64_t *items, i
 hipError_t launch_gather_items(const int64_t *items, int64_t n_items, int align, hipStream_t stream);
 // Reduce side (sgx_reduce.hip), key-sorted (Long, Long) records
 hipError_t launch_digit_hist(const void *rec, int64_t n, int rb, uint32_t *hist, int num_cus, hipStream_t st);
-// The sorted read's segmented window pass (records already contiguous by partition): piece k =
-// desc[4k..] = {begin, -, segment s, piece g} up to the next piece's begin (the last: n);
-// cnt[(s * Q + q) * Gmax + g] = piece (s, g)'s records in window bucket q (KIND_KEY_BITS, Q =
-// pp.R <= 1024); then offs = per-segment exclusive scan over (q, g) + seg_base[s].
+// The sorted read's segmented passes (records already contiguous by partition): piece k =
+// desc[4k..] = {begin, -, k, 0} up to the next piece's begin (the last: n), pieces of segment
+// s = [pk[s], pk[s+1]); cnt[k * Q + q] = piece k's records in bucket q (KIND_KEY_BITS or
+// KIND_DIGIT, Q = pp.R <= 1024); offs = per-segment exclusive scan, bucket-major,
+// piece-minor, from seg_base[s] -- K4's SEG mode then runs with G = 1.
 hipError_t launch_piece_hist(const void *in, int64_t n, const int64_t *desc, int64_t npieces, const PartParams &pp,
-                             int Gmax, uint32_t *cnt, hipStream_t st);
-hipError_t launch_seg_offsets(const uint32_t *cnt, const int64_t *seg_base, int64_t nseg, uint32_t Q, int Gmax,
+                             uint32_t *cnt, hipStream_t st);
+hipError_t launch_seg_offsets(const uint32_t *cnt, const int64_t *seg_base, const int32_t *pk, int64_t nseg, uint32_t Q,
                               uint32_t *offs, hipStream_t st);
 // groupByKey / reduceByKey(_ + _) over key-sorted (Long, Long) records in one pass
 // (sgx_reduce.hip, k_group_fused): keys[g], starts[g] (may be NULL), vals = every value (GROUP)

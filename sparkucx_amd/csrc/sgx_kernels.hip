@@ -2101,8 +2101,8 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
     if (pp.pad_cnt && (!pp.pad_cap || !pp.olim)) return hipErrorInvalidValue;
     // the map side's split level 2 (hash bits), or the sorted read's segmented window pass
     // (key bits, never padded)
-    const bool key_bits = pp.kind == KIND_KEY_BITS;
-    if (key_bits && pp.pad_cnt) return hipErrorInvalidValue;
+    const bool key_bits = pp.kind == KIND_KEY_BITS, digit = pp.kind == KIND_DIGIT;
+    if ((key_bits || digit) && pp.pad_cnt) return hipErrorInvalidValue;
 #define SGX_WCS_K(K, W, NI, SI, M)                                                                           \
     do {                                                                                                     \
         (void)hipFuncSetAttribute((const void *)k_scatter16_wc<K, W, NI, SI, true, M>,                      \
@@ -2114,6 +2114,7 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
 #define SGX_WCS(W, NI, SI, M)                                         \
     do {                                                              \
         if (key_bits) SGX_WCS_K(KIND_KEY_BITS, W, NI, SI, 0);         \
+        else if (digit) SGX_WCS_K(KIND_DIGIT, W, NI, SI, 0);          \
         else SGX_WCS_K(KIND_HASH_POW2, W, NI, SI, M);                 \
     } while (0)
     const int W = geo.waves - WC_GEOM_BASE;
@@ -2139,9 +2140,10 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
 // window pass + partitioner pass (two histograms, two scatters) of the LSD form.
 // ------------------------------------------------------------------------------------
 constexpr int PH_THREADS = 1024;
+template <int KIND>
 __global__ __launch_bounds__(PH_THREADS) void k_piece_hist(const u32x4 *__restrict__ in, int64_t n,
                                                            const int64_t *__restrict__ desc, int64_t npieces,
-                                                           PartParams pp, int Gmax, uint32_t *__restrict__ cnt) {
+                                                           PartParams pp, uint32_t *__restrict__ cnt) {
     __shared__ uint32_t h[1024];
     const uint32_t Q = pp.R, tid = threadIdx.x;
     for (uint32_t i = tid; i < Q; i += PH_THREADS) h[i] = 0;
@@ -2155,55 +2157,63 @@ __global__ __launch_bounds__(PH_THREADS) void k_piece_hist(const u32x4 *__restri
 #pragma unroll
         for (int u = 0; u < U; ++u) r[u] = in[i + u * PH_THREADS];
 #pragma unroll
-        for (int u = 0; u < U; ++u) atomicAdd(&h[pid_of<KIND_KEY_BITS>(r[u].x, r[u].y, r[u].z, pp)], 1u);
+        for (int u = 0; u < U; ++u) atomicAdd(&h[pid_of<KIND>(r[u].x, r[u].y, r[u].z, pp)], 1u);
     }
     for (; i < e; i += PH_THREADS) {
         const u32x4 r = in[i];
-        atomicAdd(&h[pid_of<KIND_KEY_BITS>(r.x, r.y, r.z, pp)], 1u);
+        atomicAdd(&h[pid_of<KIND>(r.x, r.y, r.z, pp)], 1u);
     }
     __syncthreads();
-    const int64_t sg = desc[4 * k + 2], g = desc[4 * k + 3];
-    for (uint32_t q = tid; q < Q; q += PH_THREADS) cnt[((int64_t)sg * Q + q) * Gmax + g] = h[q];
+    for (uint32_t q = tid; q < Q; q += PH_THREADS) cnt[k * Q + q] = h[q];
 }
 
 hipError_t launch_piece_hist(const void *in, int64_t n, const int64_t *desc, int64_t npieces, const PartParams &pp,
-                             int Gmax, uint32_t *cnt, hipStream_t st) {
+                             uint32_t *cnt, hipStream_t st) {
     if (npieces <= 0) return hipSuccess;
-    if (pp.kind != KIND_KEY_BITS || pp.R > 1024) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_piece_hist, dim3((unsigned)npieces), dim3(PH_THREADS), 0, st, (const u32x4 *)in, n, desc,
-                       npieces, pp, Gmax, cnt);
+    if (pp.R > 1024) return hipErrorInvalidValue;
+    if (pp.kind == KIND_KEY_BITS)
+        hipLaunchKernelGGL(k_piece_hist<KIND_KEY_BITS>, dim3((unsigned)npieces), dim3(PH_THREADS), 0, st,
+                           (const u32x4 *)in, n, desc, npieces, pp, cnt);
+    else if (pp.kind == KIND_DIGIT)
+        hipLaunchKernelGGL(k_piece_hist<KIND_DIGIT>, dim3((unsigned)npieces), dim3(PH_THREADS), 0, st,
+                           (const u32x4 *)in, n, desc, npieces, pp, cnt);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 
-// one workgroup per segment: offs over (q, g), q-major, from the segment's first record
+// one workgroup per segment s, whose pieces are [pk[s], pk[s+1]): offs[k * Q + q] = the first
+// record of segment s + every count before (q, k) in bucket-major, piece-minor order
 constexpr int SO_THREADS = 256;
 __global__ __launch_bounds__(SO_THREADS) void k_seg_offsets(const uint32_t *__restrict__ cnt,
-                                                            const int64_t *__restrict__ seg_base, uint32_t Q, int Gmax,
+                                                            const int64_t *__restrict__ seg_base,
+                                                            const int32_t *__restrict__ pk, uint32_t Q,
                                                             uint32_t *__restrict__ offs) {
     __shared__ uint32_t s_w[SO_THREADS / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t sg = blockIdx.x;
-    const uint32_t m = Q * (uint32_t)Gmax;  // entries of the segment
+    const uint32_t k0 = (uint32_t)pk[sg], np = (uint32_t)pk[sg + 1] - k0;
+    const uint32_t m = Q * np;  // entries of the segment: j = q * np + (k - k0)
     const uint32_t per = (m + SO_THREADS - 1) / SO_THREADS, j0 = min(m, tid * per), j1 = min(m, j0 + per);
-    const uint32_t *c = cnt + (int64_t)sg * m;
+    auto at = [&](uint32_t j) -> int64_t { return (int64_t)(k0 + j % np) * Q + j / np; };
     uint32_t sum = 0;
-    for (uint32_t j = j0; j < j1; ++j) sum += c[j];
+    for (uint32_t j = j0; j < j1; ++j) sum += cnt[at(j)];
     const uint32_t x = wave_inclusive_scan(sum, lane);
     if (lane == 63) s_w[w] = x;
     __syncthreads();
     uint32_t base = (uint32_t)seg_base[sg] + x - sum;
     for (uint32_t v = 0; v < w; ++v) base += s_w[v];
-    uint32_t *o = offs + (int64_t)sg * m;
     for (uint32_t j = j0; j < j1; ++j) {
-        o[j] = base;
-        base += c[j];
+        const int64_t a = at(j);
+        offs[a] = base;
+        base += cnt[a];
     }
 }
 
-hipError_t launch_seg_offsets(const uint32_t *cnt, const int64_t *seg_base, int64_t nseg, uint32_t Q, int Gmax,
+hipError_t launch_seg_offsets(const uint32_t *cnt, const int64_t *seg_base, const int32_t *pk, int64_t nseg, uint32_t Q,
                               uint32_t *offs, hipStream_t st) {
     if (nseg <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_seg_offsets, dim3((unsigned)nseg), dim3(SO_THREADS), 0, st, cnt, seg_base, Q, Gmax, offs);
+    hipLaunchKernelGGL(k_seg_offsets, dim3((unsigned)nseg), dim3(SO_THREADS), 0, st, cnt, seg_base, pk, Q, offs);
     return hipGetLastError();
 }
 

@@ -329,6 +329,81 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
     // holding > 1/16 of the records) keep the digit passes, whose trivial digits are skipped.
     // (a read of one partition needs no pass by the partitioner: every record has the same one)
     const bool use_p = by_partition && !range_asc && s.R > 1 && nparts != 1;
+    // Segmented passes: the gather of a fixed-codec read left partition p's records
+    // contiguous (c.gather_part_recs), so every LSD pass can run inside each partition's segment
+    // -- pieces of <= SEG_PIECE records, K4's SEG mode from per-piece offsets -- and the final
+    // pass by the partitioner disappears.
+    constexpr int64_t SEG_PIECE = 1 << 17;
+    const std::vector<int64_t> &gpr = c.gather_part_recs;
+    int64_t gpr_sum = 0;
+    for (int64_t x : gpr) gpr_sum += x;
+    const bool seg_ok = use_p && rb == 16 && !(e->flags & SGX_FLAG_NO_SEG_WINDOW) && nparts > 0 &&
+                        (int64_t)gpr.size() == (int64_t)nparts && gpr_sum == n;
+    bool seg_planned = false;
+    int64_t seg_npieces = 0;
+    const int64_t *seg_desc = nullptr;
+    const uint32_t *seg_nd = nullptr;
+    uint32_t *seg_cnt = nullptr, *seg_offs = nullptr;
+    const int64_t *seg_base = nullptr;
+    const int32_t *seg_pk = nullptr;
+    auto seg_plan = [&]() -> int {
+        if (seg_planned) return SGX_OK;
+        const int64_t nseg = (int64_t)gpr.size();
+        int64_t npieces = 0;
+        for (int64_t x : gpr) npieces += (x + SEG_PIECE - 1) / SEG_PIECE;
+        // [desc 4 x npieces i64][seg_base nseg i64][pk nseg+1 i32][ndesc | seg_end u32][cnt][offs]
+        auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        const size_t b_desc = al((size_t)std::max<int64_t>(npieces, 1) * 32), b_base = al((size_t)nseg * 8);
+        const size_t b_pk = al((size_t)(nseg + 1) * 4), b_sc = 256;
+        const size_t b_cnt = al((size_t)std::max<int64_t>(npieces, 1) * 1024 * 4);
+        const size_t host = b_desc + b_base + b_pk + b_sc;
+        SGX_TRY(c.seg_work.ensure(host + 2 * b_cnt));
+        SGX_TRY(c.seg_desc_host.ensure(host));
+        char *hw = (char *)c.seg_desc_host.p;
+        int64_t *hd = (int64_t *)hw, *hb = (int64_t *)(hw + b_desc);
+        int32_t *hpk = (int32_t *)(hw + b_desc + b_base);
+        uint32_t *hsc = (uint32_t *)(hw + b_desc + b_base + b_pk);
+        int64_t k = 0, pos = 0;
+        for (int64_t sg = 0; sg < nseg; ++sg) {
+            hb[sg] = pos;
+            hpk[sg] = (int32_t)k;
+            const int64_t x = gpr[(size_t)sg];
+            for (int64_t b = 0; b < x; b += SEG_PIECE, ++k) {
+                hd[4 * k] = pos + b;
+                hd[4 * k + 1] = 0;
+                hd[4 * k + 2] = k;  // K4's "segment" index: this piece's own offsets (G = 1)
+                hd[4 * k + 3] = 0;
+            }
+            pos += x;
+        }
+        hpk[nseg] = (int32_t)k;
+        hsc[0] = (uint32_t)npieces;
+        hsc[1] = (uint32_t)n;
+        char *dw = (char *)c.seg_work.p;
+        HIP_TRY(hipMemcpyAsync(dw, hw, host, hipMemcpyHostToDevice, st));
+        seg_desc = (const int64_t *)dw;
+        seg_base = (const int64_t *)(dw + b_desc);
+        seg_pk = (const int32_t *)(dw + b_desc + b_base);
+        seg_nd = (const uint32_t *)(dw + b_desc + b_base + b_pk);
+        seg_cnt = (uint32_t *)(dw + host);
+        seg_offs = (uint32_t *)(dw + host + b_cnt);
+        seg_npieces = npieces;
+        seg_planned = true;
+        return SGX_OK;
+    };
+    // one segmented pass c.sort_buf[cur] -> c.sort_buf[cur ^ 1] by kp (KIND_KEY_BITS / KIND_DIGIT)
+    auto seg_pass = [&](PartParams kp, uint32_t *err) -> int {
+        SGX_TRY(seg_plan());
+        if (seg_npieces == 0) return SGX_OK;
+        const ScatterGeom geo = scatter_geom16_wc(kp.R);
+        if (geo.items == 0) return fail_msg(SGX_ERR_HIP, "internal error: no write-combining geometry for %u", kp.R);
+        kp.mbits = (uint32_t)geo.mbits;
+        HIP_TRY(launch_piece_hist(c.sort_buf[cur].p, n, seg_desc, seg_npieces, kp, seg_cnt, st));
+        HIP_TRY(launch_seg_offsets(seg_cnt, seg_base, seg_pk, (int64_t)gpr.size(), kp.R, seg_offs, st));
+        HIP_TRY(launch_scatter16_seg(c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, kp, seg_offs, 1, seg_desc, seg_nd,
+                                     seg_nd + 1, (int)seg_npieces, geo, err, st));
+        return debug_sync(e, st, "segmented sort pass");
+    };
     if (skip && !(e->flags & SGX_FLAG_NO_BUCKET_SORT) && (use_p ? s.kind == SGX_PART_HASH : true)) {
         int top_byte = -1;  // most significant varying key byte, as a bit position of the window
         uint32_t maxbin = 0;
@@ -353,76 +428,16 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
             const int lo = top - kbits;
             // Segmented form: the gather left every partition's records
             // contiguous, so one stable pass by the window bits inside each partition's segment
-            // replaces the window pass + the pass by the partitioner.  Pieces of <= SEG_PIECE
-            // records; a segment longer than SEG_PIECE_MAX pieces (skew) keeps the LSD form.
-            constexpr int64_t SEG_PIECE = 1 << 17;
-            constexpr int SEG_PIECE_MAX = 8;
+            // replaces the window pass + the pass by the partitioner.
             bool seg_done = false;
-            const std::vector<int64_t> &pr = c.gather_part_recs;
-            int64_t pr_sum = 0, pr_max = 0;
-            for (int64_t x : pr) {
-                pr_sum += x;
-                pr_max = std::max(pr_max, x);
-            }
-            if (use_p && rb == 16 && kbits >= 1 && kbits <= 10 && !(e->flags & SGX_FLAG_NO_SEG_WINDOW) &&
-                nparts > 0 && (int64_t)pr.size() == (int64_t)nparts && pr_sum == n &&
-                (pr_max + SEG_PIECE - 1) / SEG_PIECE <= SEG_PIECE_MAX &&
-                scatter_geom16_wc(1u << kbits).items != 0) {
-                const int64_t nseg = (int64_t)pr.size();
-                const uint32_t Q = 1u << kbits;
-                int Gmax = 1;
-                int64_t npieces = 0;
-                for (int64_t x : pr) {
-                    const int64_t g = std::max<int64_t>(1, (x + SEG_PIECE - 1) / SEG_PIECE);
-                    Gmax = std::max(Gmax, (int)g);
-                    npieces += x > 0 ? g : 0;
-                }
-                // [desc 4 x npieces int64][seg_base nseg int64][ndesc | seg_end u32][cnt][offs]
-                auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-                const size_t b_desc = al((size_t)npieces * 32), b_base = al((size_t)nseg * 8), b_sc = 256;
-                const size_t b_cnt = al((size_t)nseg * Q * Gmax * 4);
-                SGX_TRY(c.seg_work.ensure(b_desc + b_base + b_sc + 2 * b_cnt));
-                SGX_TRY(c.seg_desc_host.ensure(b_desc + b_base + b_sc));
-                char *hw = (char *)c.seg_desc_host.p;
-                int64_t *hd = (int64_t *)hw, *hb = (int64_t *)(hw + b_desc);
-                uint32_t *hsc = (uint32_t *)(hw + b_desc + b_base);
-                int64_t k = 0, pos = 0;
-                for (int64_t sg = 0; sg < nseg; ++sg) {
-                    hb[sg] = pos;
-                    const int64_t x = pr[(size_t)sg];
-                    for (int64_t g = 0, b = 0; b < x; ++g, b += SEG_PIECE, ++k) {
-                        hd[4 * k] = pos + b;
-                        hd[4 * k + 1] = 0;
-                        hd[4 * k + 2] = sg;
-                        hd[4 * k + 3] = g;
-                    }
-                    pos += x;
-                }
-                hsc[0] = (uint32_t)npieces;
-                hsc[1] = (uint32_t)n;
-                char *dw = (char *)c.seg_work.p;
-                const int64_t *ddesc = (const int64_t *)dw;
-                const int64_t *dbase = (const int64_t *)(dw + b_desc);
-                const uint32_t *dnd = (const uint32_t *)(dw + b_desc + b_base);
-                uint32_t *dcnt = (uint32_t *)(dw + b_desc + b_base + b_sc);
-                uint32_t *doffs = (uint32_t *)((char *)dcnt + b_cnt);
-                HIP_TRY(hipMemcpyAsync(dw, hw, b_desc + b_base + b_sc, hipMemcpyHostToDevice, st));
-                HIP_TRY(hipMemsetAsync(dcnt, 0, b_cnt, st));  // pieces a short segment lacks count 0
+            if (seg_ok && kbits >= 1 && kbits <= 10) {
                 PartParams kp{};
                 kp.kind = KIND_KEY_BITS;
-                kp.R = Q;
+                kp.R = 1u << kbits;
                 kp.nbits = (uint32_t)kbits;
                 kp.dshift = (uint32_t)lo;
                 kp.dflip = 1u;
-                const ScatterGeom geo = scatter_geom16_wc(Q);
-                kp.mbits = (uint32_t)geo.mbits;
-                HIP_TRY(launch_piece_hist(c.sort_buf[cur].p, n, ddesc, npieces, kp, Gmax, dcnt, st));
-                HIP_TRY(launch_seg_offsets(dcnt, dbase, nseg, Q, Gmax, doffs, st));
-                HIP_TRY(launch_scatter16_seg(c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, kp, doffs, Gmax, ddesc, dnd,
-                                             dnd + 1, (int)npieces, geo, errs + np, st));
-                SGX_TRY(debug_sync(e, st, "segmented window pass"));
-                // the pinned descriptors are rewritten by the next sort only after this one's
-                // host-side check below has synchronised the stream
+                SGX_TRY(seg_pass(kp, errs + np));
                 cur ^= 1;
                 ++np;
                 seg_done = true;
@@ -484,11 +499,14 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
         dp.nbits = 8;
         dp.dshift = rb == 16 ? 8u * (uint32_t)d : 8u * (uint32_t)(9 - d);
         dp.dflip = (rb == 16 && d == 7) ? 0x80u : 0u;
-        SGX_TRY(partition_pass(e, c, c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, dp, (int32_t)DIGIT_R, KIND_DIGIT,
-                               nullptr, errs + np - 1, false));
+        if (seg_ok)
+            SGX_TRY(seg_pass(dp, errs + np - 1));
+        else
+            SGX_TRY(partition_pass(e, c, c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, dp, (int32_t)DIGIT_R,
+                                   KIND_DIGIT, nullptr, errs + np - 1, false));
         cur ^= 1;
     }
-    if (by_partition && !range_asc && s.R > 1) {
+    if (use_p && !seg_ok) {
         SGX_TRY(partition_pass(e, c, c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, s.pp, s.R, s.kind, nullptr,
                                errs + np, false));
         cur ^= 1;
