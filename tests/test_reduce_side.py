@@ -406,20 +406,20 @@ def test_sorted_bucket_path(sgx_lib, oracle_lib, flags, case):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("flags", [0, 1024])
-@pytest.mark.parametrize("case", ["pieces", "subrange", "skew_fallback", "grouped_sum", "empty_partitions"])
+@pytest.mark.parametrize("case", ["pieces", "subrange", "many_pieces", "grouped_sum", "empty_partitions"])
 def test_sorted_segmented_window(sgx_lib, oracle_lib, flags, case):
     """The sorted read's segmented window pass (one stable pass by the key window inside every
     partition's segment of the gathered records) against the oracle, and the
     LSD form it replaces (SGX_FLAG_NO_SEG_WINDOW = 1024): partitions of several 2^17-record
-    pieces, a sub-range of reducers, a partition too long for the segmented form (it keeps the
-    LSD passes), reduceByKey sums, and empty partitions between full ones."""
+    pieces, a sub-range of reducers, two partitions of ten pieces each, reduceByKey sums, and
+    empty partitions between full ones."""
     if case == "pieces":  # 4 reducers x ~200 K records: two pieces each
         maps = [oracle_lib.gen_uniform16(n, 1000 + i, value_base=i << 32) for i, n in enumerate((500_001, 300_000))]
         _run(sgx_lib, oracle_lib, maps, 4, flags=flags)
     elif case == "subrange":
         maps = [oracle_lib.gen_uniform16(n, 1100 + i, value_base=i << 32) for i, n in enumerate((400_000, 123_457))]
         _run(sgx_lib, oracle_lib, maps, 64, rng_part=(5, 41), flags=flags)
-    elif case == "skew_fallback":  # 2 reducers x 1.25 M records: > 8 pieces each
+    elif case == "many_pieces":  # 2 reducers x 1.25 M records: 10 pieces each
         maps = [oracle_lib.gen_uniform16(2_500_000, 1200)]
         _run(sgx_lib, oracle_lib, maps, 2, flags=flags)
     elif case == "grouped_sum":
