@@ -341,6 +341,11 @@ def main():
     def step(k):
         mid = (k & 1) * world + rank  # two alternating map slots per rank
         eng.write_map(sid, mid, buf, n, rb)
+        if args.compress:
+            # the map task commits: its partition lengths, i.e. the LZ4 framing of its Kryo
+            # streams, which the engine does when the lengths are first needed -- inside the step,
+            # as Spark's map task does before it ends
+            eng.map_lengths(sid, mid, R)
         if world > 1 or self_x:
             # this step's map through the shuffle's exchange (sgx_exchange_maps: the pipelined
             # form -- the all-to-all of map k runs on the exchange stream while map k+1 is
