@@ -46,7 +46,10 @@ constexpr uint32_t PAD_OVERFLOW = 0x100u;  // a padded sub-bin overflowed: the t
 // the sampled histogram; sub-bin capacity = mu + PAD_SIGMAS * sqrt(a * mu + 16) + 8, rounded up
 // to a whole line (a = 1 + chunk / sampled records: the chunk's own Poisson spread plus the
 // sample's estimation error).
-constexpr int PAD_SAMPLE_STRIDE_MAX = 128;
+#ifndef SGX_PAD_SAMPLE_STRIDE_MAX  // (A/B builds: -DSGX_PAD_SAMPLE_STRIDE_MAX=512)
+#define SGX_PAD_SAMPLE_STRIDE_MAX 128
+#endif
+constexpr int PAD_SAMPLE_STRIDE_MAX = SGX_PAD_SAMPLE_STRIDE_MAX;
 constexpr double PAD_SIGMAS = 6.5;
 constexpr int RDIR_BITS = 10;
 constexpr int RDIR_N = (1 << RDIR_BITS) + 1;
