@@ -267,12 +267,15 @@ hipError_t launch_gather_keys(const void *recs, int rb, int key_bytes, const int
                               void *out_keys, hipStream_t st);
 // Kryo (Long, Long) framing (sgx_serde.hip): n partition-contiguous 16 B records -> their
 // KryoSerializationStream bytes in `out` (capacity 20 n), partition byte offsets ser_off[R+1]
-// from the record offsets rec_off[R+1].  Workspace `work` / `status`: kryo_work_bytes(tiles)
+// from the record offsets rec_off[R+1].  A padded map's records come through its fragment
+// table `frag` ([fstart | foff | cnt] x nfrag) unless *ovf has PAD_OVERFLOW (the fallback
+// rewrote them contiguously).  Workspace `work` / `status`: kryo_work_bytes(tiles)
 // bytes (tiles = kryo_ser16_tiles(n) / kryo_deser16_tiles(bytes)), no zeroing needed.
 int64_t kryo_ser16_tiles(int64_t n);
 int64_t kryo_work_bytes(int64_t tiles);  // the `status` workspace of either launcher
 hipError_t launch_kryo_ser16(const void *in, int64_t n, void *out, const uint32_t *rec_off, int R, int64_t *ser_off,
-                             uint64_t *work, hipStream_t st);
+                             uint64_t *work, hipStream_t st,
+                             const uint32_t *frag = nullptr, int64_t nfrag = 0, const uint32_t *ovf = nullptr);
 // Kryo (Long, Long) stream of `bytes` bytes (16 B-aligned, readable to bytes + 32) -> 16 B
 // records (at most out_cap); *count_out = records; ticket_err[1] bit 1 = malformed stream.
 int64_t kryo_deser16_tiles(int64_t bytes);

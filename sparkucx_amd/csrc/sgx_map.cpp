@@ -216,7 +216,10 @@ static bool split_ok(sgx_engine *e, int32_t R) {
 // TeraSort's 100 B records under a RangePartitioner over 10-byte keys take the same path with the
 // LDS-staged wide-record K4 (its input 16 B-aligned, as that kernel needs).
 static bool use_padded(sgx_engine *e, const Shuffle &s, const void *in, int64_t n) {
-    if (s.R < 2 || s.ser != SGX_SER_FIXED || s.combine != -1) return false;
+    // a Kryo shuffle's 16 B records too: the serializer reads them through the fragment table
+    // and publishes its contiguous stream (the map itself is then contiguous to every consumer)
+    const bool kryo16 = s.ser == SGX_SER_KRYO && s.rb == 16 && s.kind == SGX_PART_HASH;
+    if (s.R < 2 || (s.ser != SGX_SER_FIXED && !kryo16) || s.combine != -1) return false;
     if (e->flags & SGX_FLAG_NO_PADDED_MAP) return false;
     if (e->rank_mode != SGX_RANK_ORDERED || !e->lds_order_ok || e->sc_waves || e->sc_items) return false;
     if (e->nranks > 1 || e->comm || e->host_comm || n < e->pad_min || s.pad_failed.load()) return false;
@@ -499,7 +502,8 @@ int sgx::materialize(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
 // rec_off_dev: device (R+1) u32 record offsets of m.data.
 // rec_off_dev: (nseg+1) u32 record offsets of the stream's segments (the R partitions, or
 // the (partition, spill) segments of SGX_WRITER_UNSAFE).
-static int serialize_kryo(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const uint32_t *rec_off_dev, int32_t nseg) {
+static int serialize_kryo(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const uint32_t *rec_off_dev, int32_t nseg,
+                          bool padded = false) {
     hipStream_t st = c.st;
     const int64_t n = m.nrec;
     const int64_t tiles = kryo_ser16_tiles(n);
@@ -512,7 +516,12 @@ static int serialize_kryo(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const ui
     if (n == 0) HIP_TRY(hipMemsetAsync(off_dev, 0, offb, st));  // no tile writes them
     hipEvent_t k0 = e->ev(), k1 = e->ev();
     HIP_TRY(hipEventRecord(k0, st));
-    HIP_TRY(launch_kryo_ser16(m.data.p, n, m.ser.p, rec_off_dev, nseg, off_dev, work, st));
+    // a padded write's records through its fragment table, unless its fallback ran (the flag
+    // word behind the partition offsets: padded_pass / padded_split_pass)
+    const int64_t nfrag = padded ? (int64_t)s.R * m.frag_G : 0;
+    HIP_TRY(launch_kryo_ser16(m.data.p, n, m.ser.p, rec_off_dev, nseg, off_dev, work, st,
+                              padded ? (const uint32_t *)m.frag.p : nullptr, nfrag,
+                              padded ? rec_off_dev + s.R + 2 : nullptr));
     SGX_TRY(debug_sync(e, st, "Kryo serializer"));
     HIP_TRY(hipEventRecord(k1, st));
     e->record_stage(SGX_STAGE_SERIALIZE, k0, k1);
@@ -584,7 +593,7 @@ static int run_map_pipeline(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const 
         if (m.seg_spills > 1)  // (partition, spill) segments, SGX_WRITER_UNSAFE
             SGX_TRY(serialize_kryo(e, c, s, m, (const uint32_t *)m.seg_off.p, s.R * m.seg_spills));
         else
-            SGX_TRY(serialize_kryo(e, c, s, m, rec_off_dev, s.R));
+            SGX_TRY(serialize_kryo(e, c, s, m, rec_off_dev, s.R, m.pad_try));
     }
     HIP_TRY(m.done.record(c.st));
     m.written = true;
@@ -602,7 +611,8 @@ int sgx::finish_lengths(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
         const uint32_t fl = po[s.R + 2];
         const bool ovf = (fl & PAD_OVERFLOW) != 0;
         if (!ovf && fl) return fail_msg(SGX_ERR_HIP, "internal error: padded scatter flag %#x", fl);
-        m.padded = !ovf;
+        // (a Kryo map publishes its serialized stream: contiguous whatever its records were)
+        m.padded = !ovf && s.ser == SGX_SER_FIXED;
         if (ovf) s.pad_failed.store(true);
         m.pad_try = false;
     }

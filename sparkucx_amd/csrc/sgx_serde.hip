@@ -139,18 +139,98 @@ __device__ __forceinline__ uint64_t tile_base(const uint64_t *excl, const uint64
     return v + excl[tile];
 }
 
-__global__ __launch_bounds__(KS_THREADS) void k_kryo_len16(const uint4 *__restrict__ in, int64_t n,
-                                                           uint32_t *__restrict__ agg) {
+// The map's partitioned records: contiguous, or (a padded map) the fragments
+// (p, g) = [fstart, + cnt) of the padded buffer in (p, g) order, foff their contiguous
+// positions -- unless the padded write overflowed (*ovf & PAD_OVERFLOW: its fallback rewrote
+// the map contiguously).  k_tile_frags first stores every tile's first fragment (one pass over
+// the fragment table); a tile then stages the fragments covering its records in LDS (a tile of
+// 1024 records meets a few dozen) and every record finds its own by a binary search there --
+// no dependent global loads per record or per tile.  A tile that meets more (a run of empty
+// fragments) searches the global table over the same range.
+constexpr int KS_FRAGS = 256;
+struct RecSrc {
+    const uint4 *in;
+    const uint32_t *fstart = nullptr, *foff = nullptr, *cnt = nullptr;  // padded map: R * G fragments
+    int64_t nf = 0;
+    const uint32_t *ovf = nullptr;
+    const uint32_t *tile_f0 = nullptr;  // [tiles + 1]: the fragment holding each tile's first record
+};
+struct TileFrags {  // LDS
+    uint32_t foff[KS_FRAGS], fstart[KS_FRAGS];
+    int64_t f0;  // first fragment of the tile (-1: contiguous records)
+    int nfr;     // fragments [f0, f0 + nfr) cover the tile
+};
+
+// tile_f0[t] = the nonempty fragment holding record t * KS_TILE (exactly one writer per
+// tile), tile_f0[tiles] = nf - 1.  A no-op when the padded write overflowed.
+__global__ __launch_bounds__(256) void k_tile_frags(RecSrc rs, int64_t tiles, uint32_t *__restrict__ tile_f0) {
+    if (*rs.ovf & PAD_OVERFLOW) return;
+    const int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (f == 0) tile_f0[tiles] = (uint32_t)(rs.nf - 1);
+    if (f >= rs.nf) return;
+    const int64_t c = rs.cnt[f];
+    if (c == 0) return;
+    const int64_t a = rs.foff[f];
+    for (int64_t t = (a + KS_TILE - 1) / KS_TILE; t <= (a + c - 1) / KS_TILE && t < tiles; ++t)
+        tile_f0[t] = (uint32_t)f;
+}
+
+// whole block; a no-op (no barrier) for a contiguous source
+__device__ __forceinline__ void stage_frags(const RecSrc &rs, int64_t tile, uint32_t tid, TileFrags &tf) {
+    if (!rs.foff) return;
+    if (tid == 0) {
+        if (*rs.ovf & PAD_OVERFLOW) {
+            tf.f0 = -1;
+        } else {
+            const uint32_t f0 = rs.tile_f0[tile], f1 = rs.tile_f0[tile + 1];
+            tf.f0 = f0;
+            tf.nfr = (int)(f1 - f0) + 1;
+        }
+    }
+    __syncthreads();
+    const int nfr = tf.nfr;
+    if (tf.f0 >= 0 && nfr <= KS_FRAGS) {
+        for (int j = (int)tid; j < nfr; j += KS_THREADS) {
+            tf.foff[j] = rs.foff[tf.f0 + j];
+            tf.fstart[j] = rs.fstart[tf.f0 + j];
+        }
+        __syncthreads();
+    }
+}
+__device__ __forceinline__ uint4 load_rec(const RecSrc &rs, const TileFrags &tf, int64_t i) {
+    if (!rs.foff || tf.f0 < 0) return rs.in[i];
+    const uint32_t x = (uint32_t)i;
+    int lo = 0, hi = tf.nfr;  // last j with foff[j] <= x (foff[0] <= t0 <= x)
+    if (hi <= KS_FRAGS) {
+        while (hi - lo > 1) {
+            const int mid = (lo + hi) >> 1;
+            if (tf.foff[mid] <= x) lo = mid;
+            else hi = mid;
+        }
+        return rs.in[(int64_t)tf.fstart[lo] + (int64_t)(x - tf.foff[lo])];
+    }
+    const uint32_t *fo = rs.foff + tf.f0;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        if (fo[mid] <= x) lo = mid;
+        else hi = mid;
+    }
+    return rs.in[(int64_t)rs.fstart[tf.f0 + lo] + (int64_t)(x - fo[lo])];
+}
+
+__global__ __launch_bounds__(KS_THREADS) void k_kryo_len16(RecSrc rs, int64_t n, uint32_t *__restrict__ agg) {
     __shared__ uint32_t s_w[KS_THREADS / 64];
+    __shared__ TileFrags s_tf;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t t0 = (int64_t)blockIdx.x * KS_TILE;
     const int64_t tn = min((int64_t)KS_TILE, n - t0);
+    stage_frags(rs, blockIdx.x, tid, s_tf);
     uint32_t sum = 0;
 #pragma unroll
     for (int k = 0; k < KS_ITEMS; ++k) {
         const int64_t i = (int64_t)k * KS_THREADS + tid;
         if (i < tn) {
-            const uint4 r = in[t0 + i];
+            const uint4 r = load_rec(rs, s_tf, t0 + i);
             sum += 2u + varlong_len(zigzag((uint64_t)r.x | ((uint64_t)r.y << 32))) +
                    varlong_len(zigzag((uint64_t)r.z | ((uint64_t)r.w << 32)));
         }
@@ -166,7 +246,7 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_len16(const uint4 *__restri
     }
 }
 
-__global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(const uint4 *__restrict__ in, int64_t n,
+__global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(RecSrc rs, int64_t n,
                                                            uint8_t *__restrict__ out,
                                                            const uint32_t *__restrict__ rec_off, int R,
                                                            int64_t *__restrict__ ser_off, const uint64_t *status,
@@ -177,6 +257,7 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(const uint4 *__restri
     __shared__ uint32_t s_wsum[KS_THREADS / 64];
     __shared__ uint64_t s_base;
     __shared__ int s_p0;
+    __shared__ TileFrags s_tf;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const int64_t t0 = (int64_t)tile * KS_TILE;
@@ -184,12 +265,13 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(const uint4 *__restri
 
     for (uint32_t z = tid; z < (KS_TILE * KS_MAXREC + 16) / 16; z += KS_THREADS)
         ((uint4 *)s_out)[z] = make_uint4(0, 0, 0, 0);
+    stage_frags(rs, blockIdx.x, tid, s_tf);
     // lengths, coalesced loads (record t0 + k*256 + tid)
     uint4 rec[KS_ITEMS];
 #pragma unroll
     for (int k = 0; k < KS_ITEMS; ++k) {
         const int64_t i = (int64_t)k * KS_THREADS + tid;
-        rec[k] = i < tn ? in[t0 + i] : make_uint4(0, 0, 0, 0);
+        rec[k] = i < tn ? load_rec(rs, s_tf, t0 + i) : make_uint4(0, 0, 0, 0);
         const uint64_t key = (uint64_t)rec[k].x | ((uint64_t)rec[k].y << 32);
         const uint64_t val = (uint64_t)rec[k].z | ((uint64_t)rec[k].w << 32);
         s_len[i] = i < tn ? (uint8_t)(2u + varlong_len(zigzag(key)) + varlong_len(zigzag(val))) : (uint8_t)0;
@@ -491,10 +573,11 @@ __global__ __launch_bounds__(KD_THREADS) void k_kryo_deser16(const uint8_t *__re
 int64_t kryo_deser16_tiles(int64_t bytes) { return (bytes + KD_TILE - 1) / KD_TILE; }
 
 int64_t kryo_work_bytes(int64_t tiles) {
-    return (tiles + (tiles + TS_BLOCK - 1) / TS_BLOCK + 1) * 8 + tiles * 4;
+    return (tiles + (tiles + TS_BLOCK - 1) / TS_BLOCK + 1) * 8 + tiles * 4 + (tiles + 1) * 4;
 }
 
-// workspace: excl[tiles] u64 | btot[nblk] u64 | agg[tiles] u32
+// workspace: excl[tiles] u64 | btot[nblk] u64 | agg[tiles] u32 | tile_f0[tiles + 1] u32 (the
+// serializer of a padded map)
 static void work_split(uint64_t *ws, int64_t tiles, uint64_t **excl, uint64_t **btot, uint32_t **agg,
                        int64_t *nblk) {
     *nblk = (tiles + TS_BLOCK - 1) / TS_BLOCK;
@@ -522,18 +605,32 @@ hipError_t launch_kryo_deser16(const void *in, int64_t bytes, void *out, int64_t
 int64_t kryo_ser16_tiles(int64_t n) { return (n + KS_TILE - 1) / KS_TILE; }
 
 hipError_t launch_kryo_ser16(const void *in, int64_t n, void *out, const uint32_t *rec_off, int R, int64_t *ser_off,
-                             uint64_t *work, hipStream_t st) {
+                             uint64_t *work, hipStream_t st, const uint32_t *frag, int64_t nfrag,
+                             const uint32_t *ovf) {
     if (n <= 0) return hipSuccess;
+    if (frag && (nfrag <= 0 || nfrag >= (int64_t)INT32_MAX || !ovf)) return hipErrorInvalidValue;
     const int64_t tiles = kryo_ser16_tiles(n);
     uint64_t *excl, *btot;
     uint32_t *agg;
     int64_t nblk;
     work_split(work, tiles, &excl, &btot, &agg, &nblk);
-    hipLaunchKernelGGL(k_kryo_len16, dim3((unsigned)tiles), dim3(KS_THREADS), 0, st, (const uint4 *)in, n, agg);
+    RecSrc rs;
+    rs.in = (const uint4 *)in;
+    if (frag) {  // [fstart nfrag][foff nfrag][cnt nfrag]
+        rs.fstart = frag;
+        rs.foff = frag + nfrag;
+        rs.cnt = frag + 2 * nfrag;
+        rs.nf = nfrag;
+        rs.ovf = ovf;
+        rs.tile_f0 = agg + tiles;
+        hipLaunchKernelGGL(k_tile_frags, dim3((unsigned)((nfrag + 255) / 256)), dim3(256), 0, st, rs, tiles,
+                           agg + tiles);
+    }
+    hipLaunchKernelGGL(k_kryo_len16, dim3((unsigned)tiles), dim3(KS_THREADS), 0, st, rs, n, agg);
     hipLaunchKernelGGL(k_tile_scan64, dim3((unsigned)nblk), dim3(TS_THREADS), 0, st, (const uint32_t *)agg, tiles,
                        excl, btot);
-    hipLaunchKernelGGL(k_kryo_ser16, dim3((unsigned)tiles), dim3(KS_THREADS), 0, st, (const uint4 *)in, n,
-                       (uint8_t *)out, rec_off, R, ser_off, (const uint64_t *)excl, (const uint64_t *)btot);
+    hipLaunchKernelGGL(k_kryo_ser16, dim3((unsigned)tiles), dim3(KS_THREADS), 0, st, rs, n, (uint8_t *)out, rec_off, R,
+                       ser_off, (const uint64_t *)excl, (const uint64_t *)btot);
     return hipGetLastError();
 }
 

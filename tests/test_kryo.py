@@ -296,3 +296,44 @@ def test_varlong_pinned_to_protobuf_sint64():
     want = b"".join(b"\x09" + pb._VarintBytes(wf.ZigZagEncode(int(k))) + b"\x09" + pb._VarintBytes(wf.ZigZagEncode(int(x)))
                     for k, x in recs)
     assert stream == want
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("R,shape", [(1024, "uniform"), (200, "uniform"), (4096, "uniform"), (1024, "sorted"),
+                                     (64, "lz4")])
+def test_gpu_kryo_padded_write(sgx_lib, oracle_lib, R, shape):
+    """A Kryo shuffle's map written padded: the serializer reads the records
+    through the fragment table and publishes the same stream, lengths, blocks and LZ4 frames
+    as the two-pass write; sorted keys overflow every sub-bin and the serializer reads the
+    fallback's contiguous records; R = 4096 goes through the padded split."""
+    import sparkucx_amd as sgx
+
+    n = 300_001
+    recs = oracle_lib.gen_uniform16(n, 0xAB + R)
+    if shape == "sorted":
+        recs = recs[np.argsort(recs[:, :8].copy().view("<i8").reshape(-1) % R, kind="stable")]
+    out, counts = oracle_lib.map_write(recs, R, nthreads=8)
+    want = oracle_lib.kryo_serialize(out)
+    off = oracle_lib.kryo_partition_offsets(out, counts)
+    with sgx_lib.ShuffleEngine(device=0, flags=sgx.FLAG_PAD_ANY_SIZE) as e:
+        sid = _next_sid()
+        e.register_shuffle(sid, R, serializer=sgx.SER_KRYO)
+        if shape == "lz4":
+            e.set_compression(sid, "lz4")
+        lengths = e.write_map(sid, 0, np.ascontiguousarray(recs), n, 16, R)
+        assert e.map_layout(sid, 0) == sgx.LAYOUT_CONTIGUOUS  # the published stream
+        if shape == "lz4":
+            framed, wl = oracle_lib.lz4_frame_partitions(want, off)
+            assert np.array_equal(lengths, wl)
+            assert np.array_equal(e.map_output_bytes(sid, 0), framed)
+            o = oracle_lib.offsets(counts)
+            assert e.read_records(sid, [0], 3, 40).tobytes() == out[o[3]:o[40]].tobytes()
+        else:
+            assert np.array_equal(lengths, np.diff(off))
+            assert np.array_equal(e.map_output_bytes(sid, 0), want)
+            rids = [R - 1, 0, R // 2, 1]
+            data, lens = e.fetch_blocks(sid, [0] * len(rids), rids)
+            pos = 0
+            for r, L in zip(rids, lens):
+                assert np.array_equal(data[pos:pos + L], want[off[r]:off[r + 1]])
+                pos += L
