@@ -416,7 +416,7 @@ def main():
         sc_ms = st.ms["scatter"] / max(1, st.count["scatter"])
         algo = 2 * rb  # the record read once and written once
         achieved = algo * n / (sc_ms * 1e-3) / 1e9
-        padded = layout == sgx.LAYOUT_PADDED
+        padded = layout in (sgx.LAYOUT_PADDED, sgx.LAYOUT_SERIALIZED_PADDED)
         pmc = live or load_pmc(args.dist if rb == 16 else "terasort", n, R, rb, padded) or {}
         k4_pmc, side_pmc = pmc.get("scatter") or {}, pmc.get("map_side") or {}
         side_ms = (st.ms["hist"] + st.ms["scan"] + st.ms["scatter"]) / max(1, st.count["scatter"])

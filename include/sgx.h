@@ -253,7 +253,8 @@ int sgx_map_commit(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *o
 int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, void **out_dev_ptr,
                  int64_t *out_bytes);
 /* How the engine holds a written map (waits for its kernels).  A fixed-codec HashPartitioner
- * map of 16 B records with R <= 1024, written by sgx_write_map on an engine without a
+ * map of 16 B records (R > 1024 through the two-level split), or a 100 B TeraSort map under
+ * its RangePartitioner, written by sgx_write_map on an engine without a
  * multi-rank communicator, is written in ONE pass over its records: a sampled
  * histogram sizes a line-aligned sub-bin per (partition, chunk) stream, the stable scatter
  * writes every stream into its sub-bin, and a scan of the streams' true counts gives the
@@ -262,9 +263,12 @@ int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, void **out_d
  * gather the streams directly; exchange sends, sgx_map_data and index files use a contiguous
  * copy built once on first use.  A stream longer than its sub-bin (keys not spread like the
  * sample) makes the write redo the map with the two-pass kernels on the device
- * (SGX_LAYOUT_CONTIGUOUS), and the shuffle's later maps skip the padded attempt.  Maps of
- * other shuffles are always SGX_LAYOUT_CONTIGUOUS. */
-enum sgx_layout { SGX_LAYOUT_CONTIGUOUS = 0, SGX_LAYOUT_PADDED = 1 };
+ * (SGX_LAYOUT_CONTIGUOUS), and the shuffle's later maps skip the padded attempt.  A Kryo
+ * shuffle's (Long, Long) map under a HashPartitioner is written the same way and its serializer
+ * reads the records from the sub-bins: what it publishes (the Kryo stream) is contiguous, and
+ * SGX_LAYOUT_SERIALIZED_PADDED says only how the records got there.  Maps of other shuffles
+ * are always SGX_LAYOUT_CONTIGUOUS. */
+enum sgx_layout { SGX_LAYOUT_CONTIGUOUS = 0, SGX_LAYOUT_PADDED = 1, SGX_LAYOUT_SERIALIZED_PADDED = 2 };
 int sgx_map_layout(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int32_t *out_layout);
 
 /* ---- IndexShuffleBlockResolver.writeIndexFileAndCommit (IndexShuffleBlockResolver.scala:

@@ -34,7 +34,7 @@ FLAG_ASSUME_LDS_DISORDER = 128
 FLAG_NO_PADDED_MAP = 256
 FLAG_PAD_ANY_SIZE = 512
 FLAG_NO_SEG_WINDOW = 1024
-LAYOUT_CONTIGUOUS, LAYOUT_PADDED = 0, 1
+LAYOUT_CONTIGUOUS, LAYOUT_PADDED, LAYOUT_SERIALIZED_PADDED = 0, 1, 2
 PLACE_EVEN, PLACE_BYTES = 0, 1
 WRITER_SORT, WRITER_UNSAFE = 0, 1
 ABI_VERSION = 6

@@ -186,6 +186,7 @@ struct MapOut {
     // materialize(); fetches gather the fragments directly.
     bool pad_try = false;
     bool padded = false;       // valid once `ready`
+    bool rec_padded = false;   // the records were written padded (a Kryo map: SGX_LAYOUT_SERIALIZED_PADDED)
     int32_t frag_G = 0;
     DevBuf frag;
     DevBuf dense;

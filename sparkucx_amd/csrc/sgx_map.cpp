@@ -570,7 +570,7 @@ static int run_map_pipeline(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const 
     m.ready = false;
     m.ser_valid = false;
     m.comp_valid = false;
-    m.pad_try = m.padded = m.dense_valid = false;
+    m.pad_try = m.padded = m.rec_padded = m.dense_valid = false;
     const uint32_t *rec_off_dev = part_dev;
     PadGeom pg;
     if (!partitioned && use_padded(e, s, in, n)) pg = pad_geom(e, s, n);
@@ -613,6 +613,7 @@ int sgx::finish_lengths(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
         if (!ovf && fl) return fail_msg(SGX_ERR_HIP, "internal error: padded scatter flag %#x", fl);
         // (a Kryo map publishes its serialized stream: contiguous whatever its records were)
         m.padded = !ovf && s.ser == SGX_SER_FIXED;
+        m.rec_padded = !ovf;
         if (ovf) s.pad_failed.store(true);
         m.pad_try = false;
     }
@@ -934,7 +935,9 @@ extern "C" int sgx_map_layout(sgx_engine *e, int32_t shuffle_id, int64_t map_id,
     if (!c) return SGX_ERR_HIP;
     std::lock_guard<std::mutex> lk(m->mu);
     SGX_TRY(finish_lengths(e, *c, *s, *m));
-    *out_layout = m->padded ? SGX_LAYOUT_PADDED : SGX_LAYOUT_CONTIGUOUS;
+    *out_layout = m->padded       ? SGX_LAYOUT_PADDED
+                  : m->rec_padded ? SGX_LAYOUT_SERIALIZED_PADDED
+                                  : SGX_LAYOUT_CONTIGUOUS;
     return SGX_OK;
 }
 

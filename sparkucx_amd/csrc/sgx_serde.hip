@@ -155,12 +155,13 @@ struct RecSrc {
     const uint32_t *ovf = nullptr;
     const uint32_t *tile_f0 = nullptr;  // [tiles + 1]: the fragment holding each tile's first record
 };
-struct TileFrags {  // LDS
-    uint32_t foff[KS_FRAGS], fstart[KS_FRAGS];
-    int64_t f0;  // first fragment of the tile (-1: contiguous records)
-    int nfr;     // fragments [f0, f0 + nfr) cover the tile
+// a tile's fragments [f0, f0 + nfr) (registers: tile-uniform scalar loads) and their
+// foff / fstart staged in LDS (2 x KS_FRAGS words the caller provides)
+struct TileFrags {
+    int64_t f0 = -1;  // -1: contiguous records
+    int nfr = 0;
+    uint32_t *s_foff = nullptr, *s_fstart = nullptr;
 };
-
 // tile_f0[t] = the nonempty fragment holding record t * KS_TILE (exactly one writer per
 // tile), tile_f0[tiles] = nf - 1.  A no-op when the padded write overflowed.
 __global__ __launch_bounds__(256) void k_tile_frags(RecSrc rs, int64_t tiles, uint32_t *__restrict__ tile_f0) {
@@ -175,39 +176,36 @@ __global__ __launch_bounds__(256) void k_tile_frags(RecSrc rs, int64_t tiles, ui
         tile_f0[t] = (uint32_t)f;
 }
 
-// whole block; a no-op (no barrier) for a contiguous source
-__device__ __forceinline__ void stage_frags(const RecSrc &rs, int64_t tile, uint32_t tid, TileFrags &tf) {
-    if (!rs.foff) return;
-    if (tid == 0) {
-        if (*rs.ovf & PAD_OVERFLOW) {
-            tf.f0 = -1;
-        } else {
-            const uint32_t f0 = rs.tile_f0[tile], f1 = rs.tile_f0[tile + 1];
-            tf.f0 = f0;
-            tf.nfr = (int)(f1 - f0) + 1;
-        }
-    }
-    __syncthreads();
-    const int nfr = tf.nfr;
-    if (tf.f0 >= 0 && nfr <= KS_FRAGS) {
-        for (int j = (int)tid; j < nfr; j += KS_THREADS) {
-            tf.foff[j] = rs.foff[tf.f0 + j];
-            tf.fstart[j] = rs.fstart[tf.f0 + j];
-        }
-        __syncthreads();
+// the tile's fragment range (every thread; no LDS yet)
+__device__ __forceinline__ TileFrags tile_frags(const RecSrc &rs, int64_t tile, uint32_t *lds) {
+    TileFrags tf;
+    if (!rs.foff || (*rs.ovf & PAD_OVERFLOW)) return tf;
+    const uint32_t f0 = rs.tile_f0[tile], f1 = rs.tile_f0[tile + 1];
+    tf.f0 = f0;
+    tf.nfr = (int)(f1 - f0) + 1;
+    tf.s_foff = lds;
+    tf.s_fstart = lds + KS_FRAGS;
+    return tf;
+}
+// whole block: stage the range in LDS; the caller's barrier publishes it
+__device__ __forceinline__ void stage_frags(const RecSrc &rs, const TileFrags &tf, uint32_t tid) {
+    if (tf.f0 < 0 || tf.nfr > KS_FRAGS) return;
+    for (int j = (int)tid; j < tf.nfr; j += KS_THREADS) {
+        tf.s_foff[j] = rs.foff[tf.f0 + j];
+        tf.s_fstart[j] = rs.fstart[tf.f0 + j];
     }
 }
 __device__ __forceinline__ uint4 load_rec(const RecSrc &rs, const TileFrags &tf, int64_t i) {
-    if (!rs.foff || tf.f0 < 0) return rs.in[i];
+    if (tf.f0 < 0) return rs.in[i];
     const uint32_t x = (uint32_t)i;
     int lo = 0, hi = tf.nfr;  // last j with foff[j] <= x (foff[0] <= t0 <= x)
     if (hi <= KS_FRAGS) {
         while (hi - lo > 1) {
             const int mid = (lo + hi) >> 1;
-            if (tf.foff[mid] <= x) lo = mid;
+            if (tf.s_foff[mid] <= x) lo = mid;
             else hi = mid;
         }
-        return rs.in[(int64_t)tf.fstart[lo] + (int64_t)(x - tf.foff[lo])];
+        return rs.in[(int64_t)tf.s_fstart[lo] + (int64_t)(x - tf.s_foff[lo])];
     }
     const uint32_t *fo = rs.foff + tf.f0;
     while (hi - lo > 1) {
@@ -220,17 +218,21 @@ __device__ __forceinline__ uint4 load_rec(const RecSrc &rs, const TileFrags &tf,
 
 __global__ __launch_bounds__(KS_THREADS) void k_kryo_len16(RecSrc rs, int64_t n, uint32_t *__restrict__ agg) {
     __shared__ uint32_t s_w[KS_THREADS / 64];
-    __shared__ TileFrags s_tf;
+    __shared__ uint32_t s_frag[2 * KS_FRAGS];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t t0 = (int64_t)blockIdx.x * KS_TILE;
     const int64_t tn = min((int64_t)KS_TILE, n - t0);
-    stage_frags(rs, blockIdx.x, tid, s_tf);
+    const TileFrags tf = tile_frags(rs, blockIdx.x, s_frag);
+    if (tf.f0 >= 0) {
+        stage_frags(rs, tf, tid);
+        __syncthreads();
+    }
     uint32_t sum = 0;
 #pragma unroll
     for (int k = 0; k < KS_ITEMS; ++k) {
         const int64_t i = (int64_t)k * KS_THREADS + tid;
         if (i < tn) {
-            const uint4 r = load_rec(rs, s_tf, t0 + i);
+            const uint4 r = load_rec(rs, tf, t0 + i);
             sum += 2u + varlong_len(zigzag((uint64_t)r.x | ((uint64_t)r.y << 32))) +
                    varlong_len(zigzag((uint64_t)r.z | ((uint64_t)r.w << 32)));
         }
@@ -257,21 +259,24 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(RecSrc rs, int64_t n,
     __shared__ uint32_t s_wsum[KS_THREADS / 64];
     __shared__ uint64_t s_base;
     __shared__ int s_p0;
-    __shared__ TileFrags s_tf;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const int64_t t0 = (int64_t)tile * KS_TILE;
     const int64_t tn = min((int64_t)KS_TILE, n - t0);
 
+    // a padded map's fragment range, staged in s_off (free until the offsets scan below)
+    static_assert(2 * KS_FRAGS <= KS_TILE, "fragment staging fits s_off");
+    const TileFrags tf = tile_frags(rs, tile, s_off);
+    stage_frags(rs, tf, tid);
     for (uint32_t z = tid; z < (KS_TILE * KS_MAXREC + 16) / 16; z += KS_THREADS)
         ((uint4 *)s_out)[z] = make_uint4(0, 0, 0, 0);
-    stage_frags(rs, blockIdx.x, tid, s_tf);
+    if (tf.f0 >= 0) __syncthreads();
     // lengths, coalesced loads (record t0 + k*256 + tid)
     uint4 rec[KS_ITEMS];
 #pragma unroll
     for (int k = 0; k < KS_ITEMS; ++k) {
         const int64_t i = (int64_t)k * KS_THREADS + tid;
-        rec[k] = i < tn ? load_rec(rs, s_tf, t0 + i) : make_uint4(0, 0, 0, 0);
+        rec[k] = i < tn ? load_rec(rs, tf, t0 + i) : make_uint4(0, 0, 0, 0);
         const uint64_t key = (uint64_t)rec[k].x | ((uint64_t)rec[k].y << 32);
         const uint64_t val = (uint64_t)rec[k].z | ((uint64_t)rec[k].w << 32);
         s_len[i] = i < tn ? (uint8_t)(2u + varlong_len(zigzag(key)) + varlong_len(zigzag(val))) : (uint8_t)0;

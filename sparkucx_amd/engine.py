@@ -240,7 +240,9 @@ class ShuffleEngine:
 
     def map_layout(self, shuffle_id: int, map_id: int) -> int:
         """LAYOUT_PADDED if the map was written in one pass into padded sub-bins, else
-        LAYOUT_CONTIGUOUS (two-pass write, or the padded write's overflow fallback)."""
+        LAYOUT_CONTIGUOUS (two-pass write, or the padded write's overflow fallback);
+        LAYOUT_SERIALIZED_PADDED: a Kryo map whose records were written padded (its published
+        Kryo stream is contiguous)."""
         v = ctypes.c_int32()
         check(lib().sgx_map_layout(self.handle, shuffle_id, map_id, ctypes.byref(v)), "map_layout")
         return int(v.value)

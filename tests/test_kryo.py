@@ -299,19 +299,23 @@ def test_varlong_pinned_to_protobuf_sint64():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("R,shape", [(1024, "uniform"), (200, "uniform"), (4096, "uniform"), (1024, "sorted"),
+@pytest.mark.parametrize("R,shape", [(1024, "uniform"), (200, "uniform"), (4096, "uniform"), (1024, "overflow"),
                                      (64, "lz4")])
 def test_gpu_kryo_padded_write(sgx_lib, oracle_lib, R, shape):
     """A Kryo shuffle's map written padded: the serializer reads the records
     through the fragment table and publishes the same stream, lengths, blocks and LZ4 frames
-    as the two-pass write; sorted keys overflow every sub-bin and the serializer reads the
-    fallback's contiguous records; R = 4096 goes through the padded split."""
+    as the two-pass write; keys the sample misses ("overflow") overflow a sub-bin and the
+    serializer reads the fallback's contiguous records; R = 4096 goes through the padded split."""
     import sparkucx_amd as sgx
 
-    n = 300_001
+    n = 300_001 if shape != "overflow" else 1_500_000
     recs = oracle_lib.gen_uniform16(n, 0xAB + R)
-    if shape == "sorted":
-        recs = recs[np.argsort(recs[:, :8].copy().view("<i8").reshape(-1) % R, kind="stable")]
+    if shape == "overflow":
+        # one partition dense in every line the sample skips (stride 2 at this size,
+        # test_padded.py::test_padded_overflow_falls_back_bit_exact): its sub-bins overflow
+        line = np.arange(n) // 8
+        k = np.where(line % 2 == 1, 5, np.arange(n) % 1024).astype(np.int64)
+        recs[:, :8] = k.view(np.uint8).reshape(-1, 8)
     out, counts = oracle_lib.map_write(recs, R, nthreads=8)
     want = oracle_lib.kryo_serialize(out)
     off = oracle_lib.kryo_partition_offsets(out, counts)
@@ -321,7 +325,9 @@ def test_gpu_kryo_padded_write(sgx_lib, oracle_lib, R, shape):
         if shape == "lz4":
             e.set_compression(sid, "lz4")
         lengths = e.write_map(sid, 0, np.ascontiguousarray(recs), n, 16, R)
-        assert e.map_layout(sid, 0) == sgx.LAYOUT_CONTIGUOUS  # the published stream
+        # the records went through the sub-bins unless sorted keys overflowed them
+        want_layout = sgx.LAYOUT_CONTIGUOUS if shape == "overflow" else sgx.LAYOUT_SERIALIZED_PADDED
+        assert e.map_layout(sid, 0) == want_layout
         if shape == "lz4":
             framed, wl = oracle_lib.lz4_frame_partitions(want, off)
             assert np.array_equal(lengths, wl)
