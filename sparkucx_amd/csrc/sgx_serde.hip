@@ -392,12 +392,18 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(RecSrc rs, int64_t n,
 constexpr int KD_THREADS = 256, KD_BYTES = 64, KD_TILE = KD_THREADS * KD_BYTES;
 constexpr int KD_STAGE = 16 + KD_TILE + 64;  // bytes [t0 - 16, t0 + KD_TILE + 64) of the stream
 
+// The stage holds one pad dword after every 16 (64 bytes): a thread's bytes start 64 bytes
+// after its neighbour's, so unpadded its window reads hit the same few banks as every
+// other lane's; padded, lane t's dwords sit 17 t apart (distinct banks).
+constexpr int KD_STAGE_DW = KD_STAGE / 4 + KD_STAGE / 64 + 8;
+__device__ __forceinline__ uint32_t kd_pad(uint32_t dw) { return dw + (dw >> 4); }
+
 // 24 bytes of the LDS stage from byte offset q (q + 28 <= KD_STAGE) as 3 little-endian u64
 __device__ __forceinline__ void lds_window(const uint32_t *s32, uint32_t q, uint64_t W[3]) {
     const uint32_t b = q >> 2, sh = 8u * (q & 3u);
     uint32_t d[7];
 #pragma unroll
-    for (int i = 0; i < 7; ++i) d[i] = s32[b + i];
+    for (int i = 0; i < 7; ++i) d[i] = s32[kd_pad(b + i)];
     uint32_t x[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) x[i] = sh ? (d[i] >> sh) | (d[i + 1] << (32u - sh)) : d[i];
@@ -510,23 +516,33 @@ __global__ __launch_bounds__(KD_THREADS) void k_kryo_deser16(const uint8_t *__re
                                                              uint4 *__restrict__ out, int64_t out_cap,
                                                              const uint64_t *status, const uint64_t *btot,
                                                              uint32_t *ticket_err, int64_t *count_out) {
-    __shared__ __attribute__((aligned(16))) uint8_t s_in[KD_STAGE];
+    __shared__ uint32_t s32[KD_STAGE_DW];
     __shared__ uint32_t s_wsum[KD_THREADS / 64];
     __shared__ uint64_t s_base;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    const uint32_t *s32 = (const uint32_t *)s_in;
     const uint32_t tile = blockIdx.x;
     const int64_t t0 = (int64_t)tile * KD_TILE;
-    // stage [t0 - 16, t0 + KD_TILE + 64): the buffer is readable to B + 64 (16 B-aligned)
+    const int64_t p0 = t0 + (int64_t)tid * KD_BYTES;
+    // stage [t0 - 16, t0 + KD_TILE + 64), padded (kd_pad): the buffer is readable to B + 64
+    // (16 B-aligned); a 16 B chunk stays inside one 64 B group, so its dwords stay adjacent
     for (uint32_t i = tid; i < KD_STAGE / 16; i += KD_THREADS) {
         const int64_t g = t0 - 16 + 16 * (int64_t)i;
-        ((uint4 *)s_in)[i] = (g >= 0 && g + 16 <= B + 64) ? *(const uint4 *)(in + g) : make_uint4(0, 0, 0, 0);
+        const uint4 v = (g >= 0 && g + 16 <= B + 64) ? *(const uint4 *)(in + g) : make_uint4(0, 0, 0, 0);
+        uint32_t *d = s32 + kd_pad(4 * i);
+        d[0] = v.x;
+        d[1] = v.y;
+        d[2] = v.z;
+        d[3] = v.w;
     }
     __syncthreads();
-    const int64_t p0 = t0 + (int64_t)tid * KD_BYTES;
+    // this thread's token ends from its own bytes [p0 - 16, p0 + 64): stage dwords 16 t ..
+    // 16 t + 19, at padded addresses 17 t + ... (distinct banks across the wave)
     uint4 q5[5];
 #pragma unroll
-    for (int v = 0; v < 5; ++v) q5[v] = ((const uint4 *)s_in)[(KD_BYTES / 16) * tid + v];
+    for (int v = 0; v < 5; ++v) {
+        const uint32_t b = 16u * tid + 4u * v;
+        q5[v] = make_uint4(s32[kd_pad(b)], s32[kd_pad(b + 1)], s32[kd_pad(b + 2)], s32[kd_pad(b + 3)]);
+    }
     const uint64_t tok = tok_mask64(q5, p0, B);
     const uint32_t cnt = (uint32_t)__popcll(tok);
     const uint32_t incl = ks_wave_scan(cnt, lane);
