@@ -75,8 +75,8 @@ __device__ __forceinline__ void or_shifted(uint64_t w[3], uint64_t lo, uint64_t 
 // latency, not by HBM.
 constexpr int TS_THREADS = 1024, TS_PER = 4, TS_BLOCK = TS_THREADS * TS_PER;
 // Workspace after the tile sums: excl[tiles] (exclusive prefix within a block of TS_BLOCK
-// tiles) | btot[ceil(tiles / TS_BLOCK)] (block totals).  tile_base() adds the totals of the
-// blocks before the tile's: at most a few hundred values, one wave, coalesced.
+// tiles) | btot[ceil(tiles / TS_BLOCK)] (block totals).  k_ser_tile_info adds the totals of
+// the blocks before each tile's (at most a few hundred values).
 __global__ __launch_bounds__(TS_THREADS) void k_tile_scan64(const uint32_t *__restrict__ agg, int64_t ntiles,
                                                             uint64_t *__restrict__ excl, uint64_t *__restrict__ btot) {
     __shared__ uint64_t s_w[TS_THREADS / 64];
@@ -109,34 +109,6 @@ __global__ __launch_bounds__(TS_THREADS) void k_tile_scan64(const uint32_t *__re
         run += v[i];
     }
     if (tid == 0) btot[blockIdx.x] = tot;
-}
-
-// first index p in [0, n) with a[p] >= x (n if none) of a nondecreasing array, by one
-// whole wave: 64 probes per round trip instead of log2(n) dependent loads per thread
-__device__ __forceinline__ int wave_lower_bound(const uint32_t *a, int n, int64_t x, uint32_t lane) {
-    int lo = 0, hi = n;  // the answer is in [lo, hi]
-    while (hi - lo > 64) {
-        const int step = (hi - lo + 63) / 64;
-        const int idx = lo + (int)lane * step;
-        const uint64_t m = __ballot(idx < hi && (int64_t)a[idx] < x);  // a prefix of the probes
-        const int c = __popcll(m);
-        const int nlo = c ? lo + (c - 1) * step + 1 : lo;
-        hi = min(hi, lo + c * step);
-        lo = nlo;
-    }
-    const int idx = lo + (int)lane;
-    return lo + __popcll(__ballot(idx < hi && (int64_t)a[idx] < x));
-}
-
-// prefix of `tile` (call from a whole wave; every lane gets it)
-__device__ __forceinline__ uint64_t tile_base(const uint64_t *excl, const uint64_t *btot, uint32_t tile,
-                                              uint32_t lane) {
-    const uint32_t nb = tile / TS_BLOCK;
-    uint64_t v = 0;
-    for (uint32_t i = lane; i < nb; i += 64) v += btot[i];
-#pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
-    return v + excl[tile];
 }
 
 // The map's partitioned records: contiguous, or (a padded map) the fragments
@@ -248,22 +220,49 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_len16(RecSrc rs, int64_t n,
     }
 }
 
+// Per serializer (decoder) tile: its 64-bit byte (token) prefix (the scan's in-block prefix + the totals of the
+// blocks before) and the first segment whose first record is at or after the tile's start
+// (lower bound of t0 in rec_off[0..R]), one thread per tile.  The serializer then needs two
+// scalar loads instead of a wave's dependent search after its records land.
+__global__ __launch_bounds__(256) void k_ser_tile_info(const uint64_t *__restrict__ excl,
+                                                       const uint64_t *__restrict__ btot, int64_t tiles,
+                                                       const uint32_t *__restrict__ rec_off, int R,
+                                                       uint64_t *__restrict__ tbase, uint32_t *__restrict__ tp0) {
+    const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= tiles) return;
+    uint64_t b = excl[t];
+    for (int64_t i = 0; i < t / TS_BLOCK; ++i) b += btot[i];
+    tbase[t] = b;
+    if (!rec_off) return;  // the decoder's tiles: the prefix only
+    const int64_t t0 = t * KS_TILE;
+    int lo = 0, hi = R + 1;  // first p with rec_off[p] >= t0
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((int64_t)rec_off[mid] < t0) lo = mid + 1;
+        else hi = mid;
+    }
+    tp0[t] = (uint32_t)lo;
+}
+
 __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(RecSrc rs, int64_t n,
                                                            uint8_t *__restrict__ out,
                                                            const uint32_t *__restrict__ rec_off, int R,
-                                                           int64_t *__restrict__ ser_off, const uint64_t *status,
-                                                           const uint64_t *btot) {
+                                                           int64_t *__restrict__ ser_off,
+                                                           const uint64_t *__restrict__ tbase,
+                                                           const uint32_t *__restrict__ tp0) {
     __shared__ __attribute__((aligned(16))) uint8_t s_len[KS_TILE];
     __shared__ __attribute__((aligned(16))) uint32_t s_off[KS_TILE];
     __shared__ __attribute__((aligned(16))) uint8_t s_out[KS_TILE * KS_MAXREC + 16];
     __shared__ uint32_t s_wsum[KS_THREADS / 64];
-    __shared__ uint64_t s_base;
-    __shared__ int s_p0;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const int64_t t0 = (int64_t)tile * KS_TILE;
     const int64_t tn = min((int64_t)KS_TILE, n - t0);
 
+    // the tile's byte prefix and the first partition that starts in it (k_ser_tile_info):
+    // two tile-uniform scalar loads, in flight with the record loads
+    const uint64_t B = tbase[tile];
+    const int P0 = (int)tp0[tile];
     // a padded map's fragment range, staged in s_off (free until the offsets scan below)
     static_assert(2 * KS_FRAGS <= KS_TILE, "fragment staging fits s_off");
     const TileFrags tf = tile_frags(rs, tile, s_off);
@@ -302,18 +301,7 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(RecSrc rs, int64_t n,
 #pragma unroll
         for (int j = 0; j < KS_ITEMS; ++j) { s_off[tid * KS_ITEMS + j] = run; run += lv[j]; }
     }
-    // the tile's byte prefix from the reduce-then-scan pre-pass; the first partition that
-    // starts in this tile
-    if (w == 0) {
-        const uint64_t b0 = tile_base(status, btot, tile, lane);
-        const int p0 = wave_lower_bound(rec_off, R + 1, t0, lane);
-        if (lane == 0) {
-            s_base = b0;
-            s_p0 = p0;
-        }
-    }
     __syncthreads();
-    const uint64_t B = s_base;
     const uint32_t head = (uint32_t)(B & 15u);
 
     // encode into LDS at the output's 16 B phase: each record's <= 20 bytes are assembled
@@ -364,7 +352,7 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(RecSrc rs, int64_t n,
     // writes those that start at n: the total)
     const int64_t t1 = t0 + tn;
     const bool last = t1 >= n;
-    for (int p = s_p0 + (int)tid; p <= R; p += KS_THREADS) {
+    for (int p = P0 + (int)tid; p <= R; p += KS_THREADS) {
         const int64_t ro = (int64_t)rec_off[p];
         if (ro < t1) ser_off[p] = (int64_t)(B + s_off[ro - t0]);
         else if (last && ro == n) ser_off[p] = (int64_t)(B + agg);
@@ -514,11 +502,10 @@ __global__ __launch_bounds__(KD_THREADS) void k_kryo_tok(const uint8_t *__restri
 
 __global__ __launch_bounds__(KD_THREADS) void k_kryo_deser16(const uint8_t *__restrict__ in, int64_t B,
                                                              uint4 *__restrict__ out, int64_t out_cap,
-                                                             const uint64_t *status, const uint64_t *btot,
+                                                             const uint64_t *__restrict__ tbase,
                                                              uint32_t *ticket_err, int64_t *count_out) {
     __shared__ uint32_t s32[KD_STAGE_DW];
     __shared__ uint32_t s_wsum[KD_THREADS / 64];
-    __shared__ uint64_t s_base;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t tile = blockIdx.x;
     const int64_t t0 = (int64_t)tile * KD_TILE;
@@ -547,16 +534,12 @@ __global__ __launch_bounds__(KD_THREADS) void k_kryo_deser16(const uint8_t *__re
     const uint32_t cnt = (uint32_t)__popcll(tok);
     const uint32_t incl = ks_wave_scan(cnt, lane);
     if (lane == 63) s_wsum[w] = incl;
-    if (w == 0) {
-        const uint64_t b0 = tile_base(status, btot, tile, lane);
-        if (lane == 0) s_base = b0;
-    }
     __syncthreads();
     uint32_t texcl = incl - cnt;
 #pragma unroll
     for (uint32_t qq = 0; qq < KD_THREADS / 64; ++qq)
         if (qq < w) texcl += s_wsum[qq];
-    const uint64_t c0 = s_base + texcl;  // global index of this thread's first token end
+    const uint64_t c0 = tbase[tile] + texcl;  // global index of this thread's first token end
     bool bad = false;
     if (p0 == 0 && B > 0) {
         uint64_t kv[2];
@@ -594,17 +577,23 @@ __global__ __launch_bounds__(KD_THREADS) void k_kryo_deser16(const uint8_t *__re
 int64_t kryo_deser16_tiles(int64_t bytes) { return (bytes + KD_TILE - 1) / KD_TILE; }
 
 int64_t kryo_work_bytes(int64_t tiles) {
-    return (tiles + (tiles + TS_BLOCK - 1) / TS_BLOCK + 1) * 8 + tiles * 4 + (tiles + 1) * 4;
+    return (tiles + (tiles + TS_BLOCK - 1) / TS_BLOCK + 1) * 8 + tiles * 4 + (tiles + 1) * 4 + 8 + tiles * 12;
 }
 
 // workspace: excl[tiles] u64 | btot[nblk] u64 | agg[tiles] u32 | tile_f0[tiles + 1] u32 (the
-// serializer of a padded map)
+// serializer of a padded map) | (8 B aligned) tbase[tiles] u64 | tp0[tiles] u32 (serializer)
 static void work_split(uint64_t *ws, int64_t tiles, uint64_t **excl, uint64_t **btot, uint32_t **agg,
                        int64_t *nblk) {
     *nblk = (tiles + TS_BLOCK - 1) / TS_BLOCK;
     *excl = ws;
     *btot = ws + tiles;
     *agg = (uint32_t *)(ws + tiles + *nblk + 1);
+}
+
+// the tile-info arrays behind agg[tiles] | tile_f0[tiles + 1]
+static void tile_info_split(uint32_t *agg, int64_t tiles, uint64_t **tbase, uint32_t **tp0) {
+    *tbase = (uint64_t *)(((uintptr_t)(agg + 2 * tiles + 1) + 7) & ~(uintptr_t)7);
+    *tp0 = (uint32_t *)(*tbase + tiles);
 }
 
 hipError_t launch_kryo_deser16(const void *in, int64_t bytes, void *out, int64_t out_cap, uint64_t *status,
@@ -618,8 +607,13 @@ hipError_t launch_kryo_deser16(const void *in, int64_t bytes, void *out, int64_t
     hipLaunchKernelGGL(k_kryo_tok, dim3((unsigned)tiles), dim3(KD_THREADS), 0, st, (const uint8_t *)in, bytes, agg);
     hipLaunchKernelGGL(k_tile_scan64, dim3((unsigned)nblk), dim3(TS_THREADS), 0, st, (const uint32_t *)agg, tiles,
                        excl, btot);
+    uint64_t *tbase;
+    uint32_t *tp0;
+    tile_info_split(agg, tiles, &tbase, &tp0);
+    hipLaunchKernelGGL(k_ser_tile_info, dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, st,
+                       (const uint64_t *)excl, (const uint64_t *)btot, tiles, nullptr, 0, tbase, tp0);
     hipLaunchKernelGGL(k_kryo_deser16, dim3((unsigned)tiles), dim3(KD_THREADS), 0, st, (const uint8_t *)in, bytes,
-                       (uint4 *)out, out_cap, (const uint64_t *)excl, (const uint64_t *)btot, ticket_err, count_out);
+                       (uint4 *)out, out_cap, (const uint64_t *)tbase, ticket_err, count_out);
     return hipGetLastError();
 }
 
@@ -650,8 +644,13 @@ hipError_t launch_kryo_ser16(const void *in, int64_t n, void *out, const uint32_
     hipLaunchKernelGGL(k_kryo_len16, dim3((unsigned)tiles), dim3(KS_THREADS), 0, st, rs, n, agg);
     hipLaunchKernelGGL(k_tile_scan64, dim3((unsigned)nblk), dim3(TS_THREADS), 0, st, (const uint32_t *)agg, tiles,
                        excl, btot);
+    uint64_t *tbase;
+    uint32_t *tp0;
+    tile_info_split(agg, tiles, &tbase, &tp0);
+    hipLaunchKernelGGL(k_ser_tile_info, dim3((unsigned)((tiles + 255) / 256)), dim3(256), 0, st,
+                       (const uint64_t *)excl, (const uint64_t *)btot, tiles, rec_off, R, tbase, tp0);
     hipLaunchKernelGGL(k_kryo_ser16, dim3((unsigned)tiles), dim3(KS_THREADS), 0, st, rs, n, (uint8_t *)out, rec_off, R,
-                       ser_off, (const uint64_t *)excl, (const uint64_t *)btot);
+                       ser_off, (const uint64_t *)tbase, (const uint32_t *)tp0);
     return hipGetLastError();
 }
 
