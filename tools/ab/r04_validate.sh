@@ -24,6 +24,7 @@ step 300 bench_c3.log python -u bench.py --workload c3 --no-cpu-baseline
 step 300 bench_c3_twopass.log python -u bench.py --workload c3 --no-padded --no-cpu-baseline
 step 300 bench_c4.log python -u bench.py --workload c4 --no-cpu-baseline
 step 300 bench_c4_twopass.log python -u bench.py --workload c4 --no-padded --no-cpu-baseline
+step 300 bench_kryo.log python -u bench.py --serializer kryo --no-cpu-baseline
 step 300 bench_kryo_lz4.log python -u bench.py --serializer kryo --compress --steps 5 --warmup 2 --no-cpu-baseline
 for f in bench bench_twopass bench_c3 bench_c3_twopass bench_c4 bench_c4_twopass; do
   grep '^{' "$out/$f.log" | python3 -c "import json,sys; j=json.loads(sys.stdin.read()); print('$f', j['value'], j['roofline']['frac'], j['roofline_map_side']['frac'], j['roofline_map_side']['ms'], j['stages_ms_per_step'])" || true
