@@ -40,6 +40,10 @@ Ctx *sgx_engine::ctx() {
     return slot.get();
 }
 
+#ifndef SGX_STAGE_EVENT_FENCE
+#define SGX_STAGE_EVENT_FENCE 0
+#endif
+
 hipEvent_t sgx_engine::ev() {
     {
         std::lock_guard<std::mutex> lk(stats_mu);
@@ -50,7 +54,15 @@ hipEvent_t sgx_engine::ev() {
         }
     }
     hipEvent_t e = nullptr;
+    // stage events only time the kernels between them (resolve_stats; nothing waits on them
+    // for ordering), so they skip the system-scope fence a default event's record performs:
+    // that fence idles the GPU ~6 µs per record between a map write's kernels (kernel trace,
+    // DESIGN.md §9).  A/B: -DSGX_STAGE_EVENT_FENCE=1 restores the default.
+#if SGX_STAGE_EVENT_FENCE
     (void)hipEventCreate(&e);
+#else
+    (void)hipEventCreateWithFlags(&e, hipEventDisableSystemFence);
+#endif
     return e;
 }
 
