@@ -71,6 +71,10 @@ def parse():
                          "with the all-to-all of map k on one GPU (a rehearsal, never the default line)")
     ap.add_argument("--compress", action="store_true",
                     help="with --serializer kryo: spark.shuffle.compress=true (LZ4 frames, Spark's default)")
+    ap.add_argument("--map-tasks", type=int, default=1,
+                    help="N=1 without an exchange: map writes issued by this many concurrent threads "
+                         "(Spark runs one map task per executor core; each thread gets its own engine "
+                         "stream, so one map's small kernels overlap another's scatter)")
     ap.add_argument("--serializer", choices=["fixed", "kryo"], default="fixed",
                     help="kryo: also frame each map output as Spark's Kryo stream (SURVEY §8(f) row 2)")
     a = ap.parse_args()
@@ -337,9 +341,13 @@ def main():
         eng.set_compression(sid, "lz4")
 
     last = {"mid": None}  # the map the last step wrote (read back by the Kryo leg below)
+    # concurrent map tasks (N = 1, no exchange): task j writes steps j, j + T, ... into its own
+    # map slot on its own thread, i.e. its own engine stream
+    tasks = args.map_tasks if (world == 1 and not self_x) else 1
+    slots = max(2, tasks)
 
     def step(k):
-        mid = (k & 1) * world + rank  # two alternating map slots per rank
+        mid = (k % slots) * world + rank  # alternating map slots per rank (one per task)
         eng.write_map(sid, mid, buf, n, rb)
         if args.compress:
             # the map task commits: its partition lengths, i.e. the LZ4 framing of its Kryo
@@ -359,14 +367,29 @@ def main():
         eng.sync()
         torch.cuda.synchronize()
 
-    for k in range(args.warmup):
-        step(k)
+    pool = None
+    if tasks > 1:
+        import concurrent.futures as cf
+
+        pool = cf.ThreadPoolExecutor(max_workers=tasks)
+
+    def run(nsteps):
+        if pool is None:
+            for k in range(nsteps):
+                step(k)
+            return
+        # one job per task: its steps in order, all in its own slot; a job the pool runs on an
+        # already-busy thread just serializes (the barriers separate the phases' slot reuse)
+        jobs = [pool.submit(lambda j=j: [step(k) for k in range(j, nsteps, tasks)]) for j in range(tasks)]
+        for f in jobs:
+            f.result()
+
+    run(max(args.warmup, tasks))
     barrier()
     eng.stats_reset()
     barrier()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
+    run(args.steps)
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
@@ -428,7 +451,10 @@ def main():
             "data": (f"synthetic {args.dist} (Long,Long) 16 B records, splitmix64 seed {args.seed:#x}+rank"
                      if rb == 16 else f"synthetic TeraSort 100 B records (10 random key bytes), seed {args.seed:#x}+rank, "
                      f"{len(bounds)} bounds sampled from rank 0's batch"),
-            "config": {"workload": _workload_name(args, n, R, world, self_x),
+            "config": {"workload": _workload_name(args, n, R, world, self_x), "map_tasks": tasks,
+                       "map_tasks_note": None if tasks == 1 else (
+                           "concurrent map tasks: stage event times include the other tasks' kernels, "
+                           "so the roofline fields are not per-kernel figures (DESIGN.md §9)"),
                        "records_per_gpu": n, "partitions": R, "record_bytes": rb,
                        "map_layout": "padded (single pass: sampled histogram, K4 into sub-bins, K3 over the "
                                      "streams' counts)" if padded else "contiguous (two-pass: K1+K2 histogram, K3, K4)",
