@@ -186,3 +186,21 @@ def test_check_index_accepts_decreasing_offsets_like_spark(sgx_lib, oracle_lib, 
     dat.write_bytes(b"\1" * 80)
     assert sgx_lib.lib().sgx_check_index_and_data(str(idx).encode(), str(dat).encode(), 4, out.ctypes.data) != 0
     assert S.check_index_and_data(idxb, 80, 4) is None
+
+
+def test_header_enum_and_flag_values_match_the_bindings(sgx_lib):
+    """Every `SGX_<NAME> = value` of include/sgx.h's enums that the Python bindings also
+    define (as <NAME>) carries the same value, e.g. the map layouts and engine flags."""
+    import sparkucx_amd._lib as L
+
+    txt = open(os.path.join(ROOT, "include", "sgx.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    pairs = re.findall(r"\bSGX_([A-Z0-9_]+)\s*=\s*(-?\d+)\b", txt)
+    assert pairs, "no enum values parsed from include/sgx.h"
+    checked = 0
+    for name, val in pairs:
+        if hasattr(L, name):
+            assert getattr(L, name) == int(val), f"SGX_{name} = {val} in sgx.h, {getattr(L, name)} in _lib"
+            checked += 1
+    assert checked >= 10
+    assert L.LAYOUT_SERIALIZED_PADDED == 2
