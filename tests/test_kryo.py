@@ -300,7 +300,7 @@ def test_varlong_pinned_to_protobuf_sint64():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("R,shape", [(1024, "uniform"), (200, "uniform"), (4096, "uniform"), (1024, "overflow"),
-                                     (64, "lz4")])
+                                     (64, "lz4"), (2, "uniform"), (1024, "tiny"), (1024, "zipf"), (4096, "zipf")])
 def test_gpu_kryo_padded_write(sgx_lib, oracle_lib, R, shape):
     """A Kryo shuffle's map written padded: the serializer reads the records
     through the fragment table and publishes the same stream, lengths, blocks and LZ4 frames
@@ -308,8 +308,12 @@ def test_gpu_kryo_padded_write(sgx_lib, oracle_lib, R, shape):
     serializer reads the fallback's contiguous records; R = 4096 goes through the padded split."""
     import sparkucx_amd as sgx
 
-    n = 300_001 if shape != "overflow" else 1_500_000
+    n = {"overflow": 1_500_000, "tiny": 7}.get(shape, 300_001)
     recs = oracle_lib.gen_uniform16(n, 0xAB + R)
+    if shape == "zipf":
+        ranks = np.arange(1, (1 << 16) + 1, dtype=np.float64)
+        cdf = np.cumsum(ranks ** -1.1)
+        recs = oracle_lib.gen_zipf16(n, 0xAB + R, cdf / cdf[-1])
     if shape == "overflow":
         # one partition dense in every line the sample skips (stride 2 at this size,
         # test_padded.py::test_padded_overflow_falls_back_bit_exact): its sub-bins overflow
@@ -326,8 +330,9 @@ def test_gpu_kryo_padded_write(sgx_lib, oracle_lib, R, shape):
             e.set_compression(sid, "lz4")
         lengths = e.write_map(sid, 0, np.ascontiguousarray(recs), n, 16, R)
         # the records went through the sub-bins unless sorted keys overflowed them
-        want_layout = sgx.LAYOUT_CONTIGUOUS if shape == "overflow" else sgx.LAYOUT_SERIALIZED_PADDED
-        assert e.map_layout(sid, 0) == want_layout
+        if shape != "zipf":  # (skewed keys may or may not fit the sampled sub-bins)
+            want_layout = sgx.LAYOUT_CONTIGUOUS if shape == "overflow" else sgx.LAYOUT_SERIALIZED_PADDED
+            assert e.map_layout(sid, 0) == want_layout
         if shape == "lz4":
             framed, wl = oracle_lib.lz4_frame_partitions(want, off)
             assert np.array_equal(lengths, wl)
@@ -343,3 +348,9 @@ def test_gpu_kryo_padded_write(sgx_lib, oracle_lib, R, shape):
             for r, L in zip(rids, lens):
                 assert np.array_equal(data[pos:pos + L], want[off[r]:off[r + 1]])
                 pos += L
+            # the reduce side decodes the published stream: sorted and grouped reads
+            seqs = oracle_lib.canonical_reducer_sequences([(out, counts)], R, 16)
+            assert e.read_sorted(sid, [0], 0, R).tobytes() == oracle_lib.reduce_sorted(seqs).tobytes()
+            ks, ss = e.read_grouped(sid, [0], 0, R, sgx.AGG_SUM)
+            wk, wsum = oracle_lib.reduce_grouped(seqs, "sum")
+            assert np.array_equal(ks, wk) and np.array_equal(ss, wsum)
