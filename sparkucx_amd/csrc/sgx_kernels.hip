@@ -1842,6 +1842,304 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 }
 
 // ------------------------------------------------------------------------------------
+// Write-combining K4 for 100 B records (TeraSort under its RangePartitioner, R <= 1024;
+// DESIGN.md §6.4).  k_scatter_wide2 writes each record as it comes; at R = 1024 a tile holds
+// ~1 record per stream, so every record leaves as partial 128 B lines that the L2 merges only
+// while the line stays resident (1.18x the record bytes written).  Here every stream keeps
+// its incomplete 64 B unit on chip (a carry of <= 60 bytes in LDS, 64 KB at R = 1024) and
+// the drain stores whole units only: 4 lanes x 16 B, 64 B-aligned in the output.  A unit's
+// bytes come from the stream's carry (its head) and from the tile's records (staged in LDS,
+// found through the partition-sorted index).  The stream's first unit (bytes before the
+// stream's start belong to its neighbour) and its last (the chunk's end) are written dword by
+// dword.  Tiles of 512 records (51 KB staged) leave room for the carries, the ranking rows
+// and the bounds (12 B each).
+// LDS: stage[TR*100] | bounds (12 B) | rdir | carry[RS][16] u32 (15 data dwords + the stream's
+// first record) | rows[W][RS] u16 (ranking; then ps[RS+1] u32 + umap u16 for the drain) |
+// cur[RS] u32 | idx[TR] u16 | scratch
+// ------------------------------------------------------------------------------------
+#ifndef SGX_WIDE_WC
+#define SGX_WIDE_WC 1
+#endif
+#ifndef SGX_WWC_LAND_SYNC
+#define SGX_WWC_LAND_SYNC 1
+#endif
+// the two-pass TeraSort K4 (streams start at the scan's offsets) on the write-combining kernel
+#ifndef SGX_WIDE_WC_TWOPASS
+#define SGX_WIDE_WC_TWOPASS 0
+#endif
+#ifndef SGX_WWC_DRAIN_UNROLL
+#define SGX_WWC_DRAIN_UNROLL 1
+#endif
+constexpr int WWC_TR = 512;
+constexpr int WWC_UMAX = (WWC_TR * 100 + 1024 * 60) / 64 + 1;  // units per tile (R <= 1024)
+
+// range bounds packed 12 B each in LDS: {hi lo32, hi hi32, lo}
+struct Bounds12 {
+    const uint32_t *w;
+    __device__ __forceinline__ Key10 operator[](int i) const {
+        Key10 k;
+        k.hi = (uint64_t)w[3 * i] | ((uint64_t)w[3 * i + 1] << 32);
+        k.lo = w[3 * i + 2];
+        k.pad = 0;
+        return k;
+    }
+};
+
+__host__ __device__ size_t scatter_wide_wc_lds(uint32_t R, int nb) {
+    return al16((size_t)WWC_TR * 100) + al16((size_t)nb * 12) + RDIR_BYTES + (size_t)rs8(R) * 64 +
+           (size_t)8 * rs8(R) * 2 + al16((size_t)WWC_UMAX * 4) + (size_t)rs8(R) * 4 + al16((size_t)WWC_TR * 2) +
+           64 * 4;
+}
+
+template <int KIND, int MODE>
+__global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restrict__ in, uint32_t *__restrict__ out,
+                                                            int64_t n, int64_t chunk, PartParams pp,
+                                                            const uint32_t *__restrict__ offs, int G,
+                                                            uint32_t *err) {
+    constexpr int T = 512, W = 8, TR = WWC_TR, RB = 100, DW = RB / 4;
+    constexpr int NCH = TR * RB / 16;  // 16 B chunks per full tile
+    constexpr int LD = (NCH + T - 1) / T;
+    static_assert((TR * RB) % 16 == 0 && TR == T, "one record per thread, tiles 16 B aligned");
+    const uint32_t olim = MODE == WC_PADDED ? pp.olim : (uint32_t)n;
+    const uint64_t capB = (uint64_t)olim * RB;  // output bytes
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const uint32_t R = pp.R, RS = rs8(R), NP = RS / 2;
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    char *sp = smem;
+    uint32_t *stage = (uint32_t *)sp;
+    sp += al16((size_t)TR * RB);
+    uint32_t *b12 = (uint32_t *)sp;
+    if constexpr (KIND == SGX_PART_RANGE_BYTES10) {
+        const Key10 *gb = (const Key10 *)pp.bounds;
+        for (int i = tid; i < pp.nb; i += T) {
+            const Key10 k = gb[i];
+            b12[3 * i] = (uint32_t)k.hi;
+            b12[3 * i + 1] = (uint32_t)(k.hi >> 32);
+            b12[3 * i + 2] = k.lo;
+        }
+    } else if constexpr (KIND == SGX_PART_RANGE_I64) {
+        for (int i = tid; i < pp.nb; i += T) ((int64_t *)sp)[i] = ((const int64_t *)pp.bounds)[i];
+    }
+    sp += al16((size_t)pp.nb * 12);
+    const uint16_t *bdir = nullptr;
+    if (pp.dir) {
+        for (int i = tid; i < RDIR_N; i += T) ((uint16_t *)sp)[i] = pp.dir[i];
+        bdir = (const uint16_t *)sp;
+    }
+    sp += RDIR_BYTES;
+    uint32_t *carry = (uint32_t *)sp;  // [p][0..14] the open unit's bytes, [p][15] the stream's first record
+    sp += (size_t)RS * 64;
+    uint16_t *rows = (uint16_t *)sp;
+    sp += (size_t)8 * RS * 2;
+    uint32_t *desc = (uint32_t *)sp;  // whole units of the tile: p | slot base << 10 | unit of p << 20
+    sp += al16((size_t)WWC_UMAX * 4);
+    uint32_t *cur = (uint32_t *)sp;
+    sp += (size_t)RS * 4;
+    uint16_t *idx = (uint16_t *)sp;
+    sp += al16((size_t)TR * 2);
+    uint32_t *scratch = (uint32_t *)sp;
+    uint16_t *myrow = rows + (size_t)w * RS;
+    uint32_t *myrow32 = (uint32_t *)myrow;
+    const Bounds12 bk{b12};
+    const int64_t *bi64 = (const int64_t *)b12;
+
+    const int g = blockIdx.x;
+    const int64_t begin = (int64_t)g * chunk;
+    const int64_t end = min(n, begin + chunk);
+    const int64_t len = end > begin ? end - begin : 0;
+    const int ntiles = (int)((len + TR - 1) / TR);
+    const int lastn = ntiles > 0 ? (int)(len - (int64_t)(ntiles - 1) * TR) : 0;
+    for (uint32_t p = tid; p < RS; p += T) {
+        const uint32_t c0 = p < R ? offs[(int64_t)p * G + g] : 0u;
+        cur[p] = c0;
+        carry[16 * p + 15] = c0;  // the stream's first record: bytes before it are not ours
+    }
+
+    u32x4 ld[LD];
+    auto issue = [&](int t) {
+        const u32x4 *tb = (const u32x4 *)((const char *)in + (begin + (int64_t)t * TR) * RB);
+        const int nch = (t + 1 < ntiles ? TR : lastn) == TR ? NCH : 0;  // partial tiles: dword-wise
+#pragma unroll
+        for (int i = 0; i < LD; ++i) {
+            const int c = i * T + tid;
+            ld[i] = c < nch ? tb[c] : u32x4{0, 0, 0, 0};
+        }
+    };
+    if (ntiles > 0) issue(0);
+    uint32_t bad = 0;
+    // the owner thread's streams 2 tid, 2 tid + 1: their next cursor and carry, taken from the
+    // tile's last record of the stream during the drain, stored at the next tile's start
+    // (after the barrier that ends every drain's reads of the old ones)
+    uint32_t ncur[2] = {0, 0}, ncnt[2] = {0, 0}, creg[2][15];
+    bool upd[2] = {false, false};
+    auto writeback = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!upd[h]) continue;
+            const uint32_t p = 2 * tid + h;
+#pragma unroll
+            for (int i = 0; i < 15; ++i)
+                if ((uint32_t)i < ncnt[h]) carry[16 * p + i] = creg[h][i];
+            cur[p] = ncur[h];
+            upd[h] = false;
+        }
+    };
+    for (int t = 0; t < ntiles; ++t) {
+        const int nrec = t + 1 < ntiles ? TR : lastn;
+        writeback();
+        // ---- land the tile; clear the ranking rows
+        if (nrec == TR) {
+#pragma unroll
+            for (int i = 0; i < LD; ++i) {
+                const int c = i * T + tid;
+                if (c < NCH) ((u32x4 *)stage)[c] = ld[i];
+            }
+        } else {
+            const uint32_t *tb = (const uint32_t *)((const char *)in + (begin + (int64_t)t * TR) * RB);
+            for (int d = tid; d < nrec * DW; d += T) stage[d] = tb[d];
+        }
+        for (uint32_t i = tid; i < (uint32_t)W * RS / 2; i += T) ((uint32_t *)rows)[i] = 0u;
+        // SGX_WWC_LAND_SYNC=0: an LDS-only barrier, so the last drain's global stores stay in
+        // flight through this tile's ranking (the tile's loads are waited for where their
+        // registers are used)
+#if SGX_WWC_LAND_SYNC
+        __syncthreads();
+#else
+        lds_barrier();
+#endif
+        if (t + 1 < ntiles) issue(t + 1);
+        // ---- partition id + rank (record tid: input order = thread order)
+        const bool valid = tid < (uint32_t)nrec;
+        uint32_t pid = 0, old;
+        if (valid) {
+            const uint32_t *rp = stage + tid * DW;
+            pid = pid_of_b<KIND>(rp[0], rp[1], rp[2], pp, bi64, bk, bdir);
+        }
+        old = __hip_atomic_fetch_add(myrow32 + (pid >> 1), valid ? 1u << ((pid & 1u) << 4) : 0u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+        lds_barrier();
+        // ---- merge: per partition pair j = tid, prefix over the wave rows; block scan of
+        //      {records, whole units} packed 16 | 16
+        const uint32_t j = tid;
+        uint32_t before[W], tot = 0, val = 0, k[2] = {0, 0}, nu[2] = {0, 0};
+        if (j < NP) {
+#pragma unroll
+            for (int v = 0; v < W; ++v) {
+                before[v] = tot;
+                tot += ((const uint32_t *)(rows + (size_t)v * RS))[j];
+            }
+            k[0] = tot & 0xFFFFu;
+            k[1] = tot >> 16;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                nu[h] = ((uint32_t)(((uint64_t)cur[2 * j + h] * RB) & 63u) + RB * k[h]) >> 6;
+            val = (k[0] + k[1]) | ((nu[0] + nu[1]) << 16);
+        }
+        const uint32_t xs = wave_inclusive_scan(val, lane);
+        if (lane == 63) scratch[w] = xs;
+        lds_barrier();
+        uint32_t base = xs - val, total = 0;
+#pragma unroll
+        for (int v = 0; v < W; ++v) {
+            const uint32_t y = scratch[v];
+            if (v < (int)w) base += y;
+            total += y;
+        }
+        const uint32_t sb[2] = {base & 0xFFFFu, (base & 0xFFFFu) + k[0]};
+        const uint32_t ubs[2] = {base >> 16, (base >> 16) + nu[0]};
+        if (j < NP) {
+            const uint32_t L = sb[0] | (sb[1] << 16);
+#pragma unroll
+            for (int v = 0; v < W; ++v) ((uint32_t *)(rows + (size_t)v * RS))[j] = before[v] + L;
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                for (uint32_t i = 0; i < nu[h]; ++i) desc[ubs[h] + i] = (2 * j + h) | (sb[h] << 10) | (i << 20);
+        }
+        lds_barrier();
+        // ---- partition-sorted index of the tile
+        if (valid) idx[myrow[pid] + ((old >> ((pid & 1u) << 4)) & 0xFFFFu)] = (uint16_t)tid;
+        lds_barrier();
+        // ---- drain: whole 64 B units, 16 B per lane, 4 lanes per unit.  Unit byte x of
+        //      stream p: its carry below cb (the open unit's bytes), else byte x - cb of the
+        //      stream's records in sorted order
+        const uint32_t npieces = (total >> 16) * 4u;
+#if SGX_WWC_DRAIN_UNROLL > 1
+#pragma unroll SGX_WWC_DRAIN_UNROLL
+#endif
+        for (uint32_t q = tid; q < npieces; q += T) {
+            const uint32_t D = desc[q >> 2];
+            const uint32_t p = D & 1023u, plo = (D >> 10) & 1023u;
+            const uint32_t rel = (D >> 20) * 64u + (q & 3u) * 16u;
+            const uint64_t cB = (uint64_t)cur[p] * RB;
+            const uint64_t startB = (uint64_t)carry[16 * p + 15] * RB;
+            const uint64_t u0B = cB & ~(uint64_t)63;
+            const uint32_t cb = (uint32_t)(cB - u0B);
+            uint32_t vv[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const uint32_t x = rel + 4u * d;
+                if (x < cb) {
+                    vv[d] = carry[16 * p + (x >> 2)];
+                } else {
+                    const uint32_t o = x - cb, r = o / 100u;
+                    vv[d] = stage[(uint32_t)idx[plo + r] * DW + ((o - r * 100u) >> 2)];
+                }
+            }
+            const uint64_t b0 = u0B + rel;
+            if (b0 >= startB && b0 + 16 <= capB) {
+                *(u32x4 *)((char *)out + b0) = u32x4{vv[0], vv[1], vv[2], vv[3]};
+            } else {  // the stream's first unit: only its own dwords
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const uint64_t b = b0 + 4u * d;
+                    if (b >= startB && b + 4 <= capB) *(uint32_t *)((char *)out + b) = vv[d];
+                }
+            }
+        }
+        // the owner's streams: next cursor, and the new open unit = the tail of the tile's last
+        // record of the stream (a record is longer than a unit, so it always closes the old one)
+        if (j < NP) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (k[h] == 0) continue;
+                const uint32_t p = 2 * j + h;
+                const uint64_t cB = (uint64_t)cur[p] * RB, cnB = cB + (uint64_t)RB * k[h];
+                const uint64_t u1B = cnB & ~(uint64_t)63;
+                const uint32_t o = (uint32_t)(u1B - cB) - RB * (k[h] - 1);  // byte of the last record
+                const uint32_t s0 = (uint32_t)idx[sb[h] + k[h] - 1] * DW + (o >> 2);
+                ncnt[h] = (uint32_t)(cnB - u1B) >> 2;
+#pragma unroll
+                for (int i = 0; i < 15; ++i) creg[h][i] = stage[min(s0 + i, (uint32_t)(TR * DW - 1))];
+                ncur[h] = cur[p] + k[h];
+                upd[h] = true;
+                bad |= ncur[h] > olim ? 1u : 0u;
+            }
+        }
+        lds_barrier();
+    }
+    writeback();
+    __syncthreads();
+    // ---- the chunk's end: every stream's open unit (its own dwords)
+    for (uint32_t p = tid; p < R; p += T) {
+        const uint64_t cB = (uint64_t)cur[p] * RB, u0B = cB & ~(uint64_t)63;
+        const uint64_t startB = (uint64_t)carry[16 * p + 15] * RB;
+        for (uint64_t b = u0B > startB ? u0B : startB; b < cB; b += 4)
+            if (b + 4 <= capB) *(uint32_t *)((char *)out + b) = carry[16 * p + (uint32_t)((b - u0B) >> 2)];
+    }
+    if constexpr (MODE == WC_PADDED) {
+        bool ovf = false;
+        for (uint32_t p = tid; p < R; p += T) {
+            const int64_t i = (int64_t)p * G + g;
+            const uint32_t cnt = cur[p] - offs[i];
+            pp.pad_cnt[i] = cnt;
+            ovf |= cnt > pp.pad_cap[p];
+        }
+        if (ovf) atomicOr(err, PAD_OVERFLOW);
+    }
+    if (bad) atomicOr(err, SCATTER_OOB);
+}
+
+// ------------------------------------------------------------------------------------
 // Two-level split scatter for R > 1024 (hash partitioner, power-of-two R, 16 B records).
 //
 // A single pass at R = 4096 (k_scatter16_ord) gives every partition ~1 record per 4 K-record
@@ -2637,6 +2935,15 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         if (mode) {
             if (pp.kind != SGX_PART_RANGE_BYTES10 || (mode == WC_PADDED && (!pp.pad_cap || !pp.olim)))
                 return hipErrorInvalidValue;
+            // the padded K4 write-combines whole 64 B units when its LDS fits (R <= 1024)
+            const size_t wlds = scatter_wide_wc_lds(pp.R, pp.nb);
+            if (SGX_WIDE_WC && mode == WC_PADDED && pp.R <= 1024 && wlds <= LDS_MAX && chunk % WWC_TR == 0) {
+                (void)hipFuncSetAttribute((const void *)k_scatter_wide_wc<SGX_PART_RANGE_BYTES10, WC_PADDED>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)wlds);
+                hipLaunchKernelGGL((k_scatter_wide_wc<SGX_PART_RANGE_BYTES10, WC_PADDED>), dim3(G), dim3(512), wlds,
+                                   stream, (const u32x4 *)in, (uint32_t *)out, n, chunk, pp, offs, G, err);
+                return hipGetLastError();
+            }
             if (mode == WC_PADDED) SGX_W2M(SGX_PART_RANGE_BYTES10, WC_PADDED);
             else SGX_W2M(SGX_PART_RANGE_BYTES10, WC_FALLBACK);
             return hipGetLastError();
@@ -2648,7 +2955,19 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         case KIND_DIGIT: SGX_W2(KIND_DIGIT); break;
         case KIND_KEY_BITS: SGX_W2(KIND_KEY_BITS); break;
         case SGX_PART_RANGE_I64: SGX_W2(SGX_PART_RANGE_I64); break;
-        case SGX_PART_RANGE_BYTES10: SGX_W2(SGX_PART_RANGE_BYTES10); break;
+        case SGX_PART_RANGE_BYTES10: {
+            // the two-pass TeraSort K4 write-combines too (streams start at their offsets)
+            const size_t wlds = scatter_wide_wc_lds(pp.R, pp.nb);
+            if (SGX_WIDE_WC && SGX_WIDE_WC_TWOPASS && pp.R <= 1024 && wlds <= LDS_MAX && chunk % WWC_TR == 0) {
+                (void)hipFuncSetAttribute((const void *)k_scatter_wide_wc<SGX_PART_RANGE_BYTES10, 0>,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)wlds);
+                hipLaunchKernelGGL((k_scatter_wide_wc<SGX_PART_RANGE_BYTES10, 0>), dim3(G), dim3(512), wlds, stream,
+                                   (const u32x4 *)in, (uint32_t *)out, n, chunk, pp, offs, G, err);
+            } else {
+                SGX_W2(SGX_PART_RANGE_BYTES10);
+            }
+            break;
+        }
         default: return hipErrorInvalidValue;
         }
 #undef SGX_W2
