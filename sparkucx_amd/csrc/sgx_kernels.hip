@@ -1865,10 +1865,10 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 #endif
 // the two-pass TeraSort K4 (streams start at the scan's offsets) on the write-combining kernel
 #ifndef SGX_WIDE_WC_TWOPASS
-#define SGX_WIDE_WC_TWOPASS 0
+#define SGX_WIDE_WC_TWOPASS 1
 #endif
 #ifndef SGX_WWC_DRAIN_UNROLL
-#define SGX_WWC_DRAIN_UNROLL 1
+#define SGX_WWC_DRAIN_UNROLL 2
 #endif
 constexpr int WWC_TR = 512;
 constexpr int WWC_UMAX = (WWC_TR * 100 + 1024 * 60) / 64 + 1;  // units per tile (R <= 1024)
