@@ -1864,6 +1864,10 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 #define SGX_WWC_LAND_SYNC 1
 #endif
 // the two-pass TeraSort K4 (streams start at the scan's offsets) on the write-combining kernel
+// ... and the reduce side's digit / key-window passes
+#ifndef SGX_WIDE_WC_REDUCE
+#define SGX_WIDE_WC_REDUCE 0
+#endif
 #ifndef SGX_WIDE_WC_TWOPASS
 #define SGX_WIDE_WC_TWOPASS 1
 #endif
@@ -2952,8 +2956,22 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         case SGX_PART_HASH:
             if (pow2) SGX_W2(KIND_HASH_POW2); else SGX_W2(SGX_PART_HASH);
             break;
-        case KIND_DIGIT: SGX_W2(KIND_DIGIT); break;
-        case KIND_KEY_BITS: SGX_W2(KIND_KEY_BITS); break;
+#define SGX_WWC_OR_W2(K)                                                                                      \
+    do {                                                                                                      \
+        const size_t wlds = scatter_wide_wc_lds(pp.R, pp.nb);                                                 \
+        if (SGX_WIDE_WC && SGX_WIDE_WC_REDUCE && pp.R <= 1024 && wlds <= LDS_MAX && chunk % WWC_TR == 0) {    \
+            (void)hipFuncSetAttribute((const void *)k_scatter_wide_wc<K, 0>,                                  \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)wlds);                 \
+            hipLaunchKernelGGL((k_scatter_wide_wc<K, 0>), dim3(G), dim3(512), wlds, stream, (const u32x4 *)in, \
+                               (uint32_t *)out, n, chunk, pp, offs, G, err);                                  \
+        } else {                                                                                              \
+            SGX_W2(K);                                                                                        \
+        }                                                                                                     \
+    } while (0)
+        // the reduce side's digit / key-window passes over 100 B records
+        case KIND_DIGIT: SGX_WWC_OR_W2(KIND_DIGIT); break;
+        case KIND_KEY_BITS: SGX_WWC_OR_W2(KIND_KEY_BITS); break;
+#undef SGX_WWC_OR_W2
         case SGX_PART_RANGE_I64: SGX_W2(SGX_PART_RANGE_I64); break;
         case SGX_PART_RANGE_BYTES10: {
             // the two-pass TeraSort K4 write-combines too (streams start at their offsets)
