@@ -150,6 +150,7 @@ class GpuExchangeCoordinator(conf: SparkConf, isDriver: Boolean, engine: () => L
   @volatile private var driverRef: RpcEndpointRef = _
   @volatile private var peers: Map[Int, RpcEndpointRef] = Map.empty
   private val ranges = new ConcurrentHashMap[(Int, Int), Array[Int]]()
+  private val mapSets = new ConcurrentHashMap[Int, (Long, Array[Long])]()
   private val setup = Promise[Unit]()
 
   comm.submit(new Runnable {
@@ -213,9 +214,13 @@ class GpuExchangeCoordinator(conf: SparkConf, isDriver: Boolean, engine: () => L
         p.trySuccess(())
       } catch {
         case t: Throwable =>
+          // the report goes out BEFORE the promise is dropped: a reader of this executor that
+          // asks again only finds no promise after the driver has the failure (Spark RPC keeps
+          // one sender's messages to one receiver in order), so its GpuExchangeRequest starts
+          // a new round instead of being dropped as a duplicate of the failed one
+          driverRef.send(GpuExchangeFailed(shuffleId, maps, attempt))
           exchanges.remove(key, p)  // a later task may ask again
           p.tryFailure(t)
-          driverRef.send(GpuExchangeFailed(shuffleId, maps, attempt))
       }
     })
   }
@@ -228,11 +233,27 @@ class GpuExchangeCoordinator(conf: SparkConf, isDriver: Boolean, engine: () => L
     val key = (shuffleId, maps)
     val p = promise(key)
     if (!p.isCompleted) driverRef.send(GpuExchangeRequest(shuffleId, maps, spec))
+    // A failed round has already dropped its promise (runExchange).  A timeout keeps it: the
+    // round may only be slow (queued behind another exchange on the comm thread), and the
+    // driver holds the key as broadcast, so a fresh promise would never be completed; the
+    // next reader waits on this one, which the comm thread still completes.
     try Await.result(p.future, Duration(timeoutMs, TimeUnit.MILLISECONDS))
     catch {
       case t: Throwable =>
-        exchanges.remove(key, p)  // a later task may ask again
         throw new SgxFetchException(s"exchange of shuffle $shuffleId failed: ${t.getMessage}")
+    }
+  }
+
+  /** The shuffle's full map id set for one map-output epoch, computed by the first reduce task
+   *  of the executor that asks and reused by the others (listing every partition's blocks
+   *  costs M x R tuples per call).  A new epoch (a map stage re-ran) recomputes it. */
+  def allMapIds(shuffleId: Int, epoch: Long, compute: => Array[Long]): Array[Long] = {
+    val cached = mapSets.get(shuffleId)
+    if (cached != null && cached._1 == epoch) cached._2
+    else {
+      val ids = compute
+      mapSets.put(shuffleId, (epoch, ids))
+      ids
     }
   }
 

@@ -15,19 +15,33 @@
  * 3. Otherwise (Spark placed the task on another executor) the raw blocks of the range come
  *    from their owners over RPC (coordinator.fetchRemote), are imported into this executor's
  *    engine (SgxNative.importBlocks) and read on this GPU by the same calls as 2.
+ *
+ * Task metrics and cancellation follow the reference's reader (spark_3_0/UcxShuffleReader.scala):
+ *   - incFetchWaitTime: the time blocked on the exchange barrier and on remote fetches (the
+ *     reference times its progress() spin, :116-123);
+ *   - incLocalBlocksFetched / incLocalBytesRead for blocks read from this executor's HBM,
+ *     incRemoteBlocksFetched / incRemoteBytesRead for blocks fetched from their owners;
+ *   - incRecordsRead per record handed to the task, merged into the task's metrics when the
+ *     iterator completes (CompletionIterator + mergeShuffleReadMetrics, :148-153);
+ *   - the result is an InterruptibleIterator (:155-156, :193-199), so a killed task stops at
+ *     its next record, and a task killed while it waits for the exchange stops before the read.
  */
 package org.apache.spark.shuffle.ucx.gpu
 
 import java.nio.{ByteBuffer, ByteOrder}
 
-import org.apache.spark.{SparkEnv, TaskContext}
-import org.apache.spark.shuffle.ShuffleReader
+import java.util.concurrent.TimeUnit
+
+import org.apache.spark.{InterruptibleIterator, SparkEnv, TaskContext}
+import org.apache.spark.shuffle.{ShuffleReadMetricsReporter, ShuffleReader}
 import org.apache.spark.storage.ShuffleBlockId
+import org.apache.spark.util.CompletionIterator
 import org.apache.spark.util.collection.CompactBuffer
 
 class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], startPartition: Int,
                              endPartition: Int, context: TaskContext,
                              coordinator: Option[GpuExchangeCoordinator],
+                             readMetrics: ShuffleReadMetricsReporter,
                              mapRange: Option[(Int, Int)] = None) extends ShuffleReader[K, C] {
   private val dep = handle.dependency
   private val shuffleId = handle.shuffleId
@@ -45,9 +59,12 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
   }
 
   /** The shuffle's full map set (every partition): the exchange key every reduce task of the
-   *  stage agrees on, whatever its own range. */
-  private def allMapIds: Array[Long] =
-    ids(SparkEnv.get.mapOutputTracker.getMapSizesByExecutorId(shuffleId, 0, dep.partitioner.numPartitions))
+   *  stage agrees on, whatever its own range.  Built once per map-output epoch on the executor
+   *  (GpuExchangeCoordinator.allMapIds), not by every reduce task: listing every block of every
+   *  partition costs M x R tuples. */
+  private def allMapIds(coord: GpuExchangeCoordinator): Array[Long] =
+    coord.allMapIds(shuffleId, SparkEnv.get.mapOutputTracker.getEpoch,
+      ids(SparkEnv.get.mapOutputTracker.getMapSizesByExecutorId(shuffleId, 0, dep.partitioner.numPartitions)))
 
   /** A little-endian direct buffer of n bytes (a clear error past 2 GiB, no silent wrap). */
   private def le(n: Long): ByteBuffer = {
@@ -57,14 +74,38 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
     ByteBuffer.allocateDirect(math.max(8L, n).toInt).order(ByteOrder.LITTLE_ENDIAN)
   }
 
+  /** Blocks (map, reducer) of the range that hold bytes, and their bytes (the engine's lengths). */
+  private def blockStats(maps: Array[Long]): (Long, Long) = {
+    val nm = maps.length
+    if (nm == 0 || endPartition <= startPartition) return (0L, 0L)
+    val rs = (startPartition until endPartition).toArray
+    val sizes = SgxNative.fetchBlocks(engine, shuffleId, rs.flatMap(_ => maps), rs.flatMap(r => Array.fill(nm)(r)), null)
+    (sizes.count(_ > 0).toLong, sizes.sum)
+  }
+
+  private def timedWait[T](f: => T): T = {
+    val t0 = System.nanoTime()
+    try f finally readMetrics.incFetchWaitTime(TimeUnit.NANOSECONDS.toMillis(System.nanoTime() - t0))
+  }
+
   override def read(): Iterator[Product2[K, C]] = {
     val maps = mapIds
-    coordinator.foreach(_.awaitExchange(shuffleId, allMapIds, handle.spec))
+    coordinator.foreach(c => timedWait(c.awaitExchange(shuffleId, allMapIds(c), handle.spec)))
+    context.killTaskIfInterrupted()  // killed while it waited for the collective
     val local = coordinator.isEmpty || {
       val Array(r0, r1) = SgxNative.shuffleReducers(engine, shuffleId)
       r0 <= startPartition && endPartition <= r1
     }
-    if (local) readOnGpu(maps) else readRemote(maps, coordinator.get)
+    val records = if (local) {
+      val (blocks, bytes) = blockStats(maps)
+      readMetrics.incLocalBlocksFetched(blocks)
+      readMetrics.incLocalBytesRead(bytes)
+      readOnGpu(maps)
+    } else readRemote(maps, coordinator.get)
+    val counted = CompletionIterator[Product2[K, C], Iterator[Product2[K, C]]](
+      records.map { r => readMetrics.incRecordsRead(1); r },
+      context.taskMetrics().mergeShuffleReadMetrics())
+    new InterruptibleIterator[Product2[K, C]](context, counted)
   }
 
   private def readOnGpu(maps: Array[Long]): Iterator[Product2[K, C]] = {
@@ -115,8 +156,10 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
       if (lo >= hi || nm == 0) None
       else {
         val rs = (lo until hi).toArray
-        val got = coord.fetchRemote(shuffleId, rank, rs.flatMap(_ => maps), rs.flatMap(r => Array.fill(nm)(r)))
+        val got = timedWait(coord.fetchRemote(shuffleId, rank, rs.flatMap(_ => maps), rs.flatMap(r => Array.fill(nm)(r))))
         System.arraycopy(got.lengths, 0, lengths, (lo - startPartition) * nm, got.lengths.length)
+        readMetrics.incRemoteBlocksFetched(got.lengths.count(_ > 0).toLong)
+        readMetrics.incRemoteBytesRead(got.bytes.length.toLong)
         Some(got.bytes)
       }
     }

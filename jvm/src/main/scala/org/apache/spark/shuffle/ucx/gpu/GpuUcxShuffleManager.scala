@@ -180,7 +180,7 @@ class GpuUcxShuffleManager(conf: SparkConf, isDriver: Boolean) extends SortShuff
       case h: GpuShuffleHandle[K @unchecked, _, C @unchecked] =>
         ensureRegistered(h)
         new GpuShuffleReader[K, C](engine, h, startPartition, endPartition, context,
-                                   if (isWorld) Some(coordinator) else None)
+                                   if (isWorld) Some(coordinator) else None, metrics)
       case _ => super.getReader(handle, startPartition, endPartition, context, metrics)
     }
 
@@ -196,7 +196,8 @@ class GpuUcxShuffleManager(conf: SparkConf, isDriver: Boolean) extends SortShuff
       case h: GpuShuffleHandle[K @unchecked, _, C @unchecked] =>
         ensureRegistered(h)
         new GpuShuffleReader[K, C](engine, h, startPartition, endPartition, context,
-                                   if (isWorld) Some(coordinator) else None, Some((startMapIndex, endMapIndex)))
+                                   if (isWorld) Some(coordinator) else None, metrics,
+                                   Some((startMapIndex, endMapIndex)))
       case _ => super.getReaderForRange(handle, startMapIndex, endMapIndex, startPartition, endPartition, context,
                                         metrics)
     }

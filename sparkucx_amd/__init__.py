@@ -20,8 +20,8 @@ from .engine import (  # noqa: F401
 )
 from .shuffle import (  # noqa: F401
     Aggregator, BaseShuffleHandle, BlockFetchingListener, BypassMergeSortShuffleHandle, SerializedShuffleHandle, GpuShuffleMapOutputWriter, GpuShuffleTransport, GpuShuffleWriter,
-    HashPartitioner, MapStatus, MemoryBlock, MemoryPool, OperationResult, OperationStatus, RangePartitioner,
-    ShuffleDependency, UcxShuffleBlockId, UcxShuffleBlockResolver, UcxShuffleManager,
+    HashPartitioner, InterruptibleIterator, MapStatus, MemoryBlock, MemoryPool, OperationResult, OperationStatus,
+    RangePartitioner, ShuffleDependency, ShuffleReadMetricsReporter, TaskContext, TaskKilledException, UcxShuffleBlockId, UcxShuffleBlockResolver, UcxShuffleManager,
     UcxShuffleClient, UcxShuffleReader, byte_string, parse_block_id,
 )
 

@@ -166,11 +166,15 @@ class ExchangeCoordinator:
                 self.engine.sync()
                 self.ran.append((key, attempt))
             except BaseException as ex:  # noqa: BLE001 - handed to the waiting readers
+                # report first, then drop the promise: a reader that asks again only finds no
+                # promise once the driver's inbox holds the failure ahead of its new request
+                # (one sender's messages stay in order), so the request starts a new round
+                # instead of being dropped as a duplicate of the failed one
+                self.driver.put(("failed", sid, tuple(maps), attempt))
                 with self._lock:
                     if self._promises.get(key) is p:
                         del self._promises[key]  # a later task may ask again
                 p.error = ex
-                self.driver.put(("failed", sid, tuple(maps), attempt))
             p.event.set()
 
     def await_exchange(self, spec: ShuffleSpec, all_maps: Sequence[int]) -> None:
@@ -181,6 +185,8 @@ class ExchangeCoordinator:
         if not p.event.is_set():
             self.driver.put(("request", key[0], key[1], spec))
         if not p.event.wait(self.timeout_s):
+            # the promise stays: the round may only be slow, and the driver keeps the key as
+            # broadcast, so the next reader waits on this one (the comm thread completes it)
             raise _lib.DeviceTimeout(f"exchange of shuffle {spec.shuffle_id} did not complete")
         if p.error is not None:
             raise _lib.IllegalStateException(f"exchange of shuffle {spec.shuffle_id} failed: {p.error}")

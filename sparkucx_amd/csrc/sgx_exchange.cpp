@@ -185,7 +185,15 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
     if (P > 1 && !collective) return fail_msg(SGX_ERR_STATE, "sgx_comm_init was not called (world of %d ranks)", P);
     hipStream_t st = collective ? e->s_comm : c->st;
     hipEvent_t a0 = e->ev(), a1 = e->ev(), a2 = e->ev(), a3 = e->ev();
-    HIP_TRY(hipEventRecord(a0, st));
+    if (local_rc == SGX_OK) {
+        // a failing record is a local error like any other: it still joins the all-gather
+        const hipError_t he = hipEventRecord(a0, st);
+        if (he != hipSuccess) {
+            if (!collective) return fail_msg(SGX_ERR_HIP, "hipEventRecord: %s", hipGetErrorString(he));
+            local_rc = SGX_ERR_HIP;
+            local_msg = std::string("hipEventRecord: ") + hipGetErrorString(he);
+        }
+    }
     // (1) who holds which maps, and their lengths
     std::vector<int64_t> counts((size_t)P, 0);
     std::vector<int64_t> ids, lens;  // [M], [M][R], source-rank-major
@@ -449,15 +457,42 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
     return SGX_OK;
 }
 
+// The round's first all-gather ([count | the first map's {id, R lengths}], as exchange_round
+// sizes it) joined with a failure mark: every rank then fails the round together instead of
+// waiting in the collective.  Caller holds comm_mu.
+static int join_failed(sgx_engine *e, int32_t R, int code, const std::string &why) {
+    if (e->comm_broken) return fail_msg(SGX_ERR_STATE, "the communicator was aborted after an exchange failure");
+    if (!(e->comm || e->host_comm)) return fail_msg(code, "%s", why.c_str());
+    std::vector<int64_t> first((size_t)R + 2, 0), all(first.size() * (size_t)e->nranks, 0);
+    first[0] = -1 + (int64_t)code;
+    SGX_TRY(allgather_i64(e, first.data(), first.size(), all.data()));
+    return fail_msg(code, "%s (every rank fails this exchange)", why.c_str());
+}
+
+// hipSetDevice + the calling thread's context; a failure on a collective engine joins the
+// round marked failed (the shuffle is known, so is the all-gather's size)
+static Ctx *exchange_ctx(sgx_engine *e, const Shuffle &s, int *rc) {
+    const hipError_t he = hipSetDevice(e->device);
+    Ctx *c = he == hipSuccess ? e->ctx() : nullptr;
+    if (c) return c;
+    const std::string why = he != hipSuccess ? std::string("hipSetDevice: ") + hipGetErrorString(he)
+                                             : std::string(sgx_last_error());
+    std::lock_guard<std::mutex> clk(e->comm_mu);
+    *rc = join_failed(e, s.R, SGX_ERR_HIP, why);
+    return nullptr;
+}
+
 extern "C" int sgx_exchange(sgx_engine *e, int32_t shuffle_id) {
     sgx::TraceRange trace_("sgx_exchange");
     if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
+    // an unknown shuffle cannot size the round's all-gather: a collective caller that failed
+    // to register it joins the round through sgx_exchange_fail(e, R, code) instead
     std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
     if (!s) return SGX_ERR_STATE;
-    HIP_TRY(hipSetDevice(e->device));
-    Ctx *c = e->ctx();
-    if (!c) return SGX_ERR_HIP;
+    int rc = SGX_OK;
+    Ctx *c = exchange_ctx(e, *s, &rc);
+    if (!c) return rc;
     // every committed map output no earlier round carried, in map id order (snapshot now:
     // the call's place in the caller's program order decides what it carries), selected under
     // comm_mu: the round marks them exchanged before another exchange can select
@@ -481,11 +516,10 @@ extern "C" int sgx_exchange_maps(sgx_engine *e, int32_t shuffle_id, const int64_
     if (!e || n < 0 || (n > 0 && !map_ids)) return fail_msg(SGX_ERR_INVALID, "bad arguments");
     std::shared_ptr<Shuffle> s = e->find_shuffle(shuffle_id);
     if (!s) return SGX_ERR_STATE;
-    HIP_TRY(hipSetDevice(e->device));
-    Ctx *c = e->ctx();
-    if (!c) return SGX_ERR_HIP;
-    std::vector<LocalMap> mine;
     int rc = SGX_OK;
+    Ctx *c = exchange_ctx(e, *s, &rc);
+    if (!c) return rc;
+    std::vector<LocalMap> mine;
     std::string msg;
     for (int64_t i = 0; i < n && rc == SGX_OK; ++i) {
         std::shared_ptr<Shuffle> s2;
@@ -504,14 +538,7 @@ extern "C" int sgx_exchange_fail(sgx_engine *e, int32_t num_partitions, int32_t 
     if (!e || num_partitions < 1 || code >= 0) return fail_msg(SGX_ERR_INVALID, "sgx_exchange_fail: bad arguments");
     HIP_TRY(hipSetDevice(e->device));
     std::lock_guard<std::mutex> clk(e->comm_mu);
-    if (e->comm_broken) return fail_msg(SGX_ERR_STATE, "the communicator was aborted after an exchange failure");
-    if (!(e->comm || e->host_comm)) return fail_msg(code, "this rank failed the exchange before it began");
-    // the round's first all-gather, exactly as exchange_round sizes it ([count | first map's
-    // {id, R lengths}]), with the failure mark a local error puts in the count
-    std::vector<int64_t> first((size_t)num_partitions + 2, 0), all(first.size() * (size_t)e->nranks, 0);
-    first[0] = -1 + (int64_t)code;
-    SGX_TRY(allgather_i64(e, first.data(), first.size(), all.data()));
-    return fail_msg(code, "this rank failed the exchange before it began (every rank fails it)");
+    return join_failed(e, num_partitions, code, "this rank failed the exchange before it began");
 }
 
 // ------------------------------------------------------------------------------------

@@ -378,6 +378,19 @@ class ShuffleEngine:
                                      ptr if cap else None, cap, kind, lens.ctypes.data), "fetchBlocks")
         return dst, lens
 
+    def block_lengths(self, shuffle_id: int, map_ids: Sequence[int], reduce_ids: Sequence[int]) -> np.ndarray:
+        """Byte length of every block (map_ids[j], reduce_ids[j]) (sgx_fetch_blocks' size query:
+        no destination, nothing copied)."""
+        m = np.ascontiguousarray(map_ids, dtype=np.int64)
+        r = np.ascontiguousarray(reduce_ids, dtype=np.int32)
+        lens = np.zeros(len(m), dtype=np.int64)
+        if len(m):
+            rc = lib().sgx_fetch_blocks(self.handle, shuffle_id, m.ctypes.data, r.ctypes.data, len(m), None, 0,
+                                        MEM_HOST, lens.ctypes.data)
+            if rc not in (0, _lib.SGX_ERR_INVALID):
+                check(rc, "fetchBlocks")
+        return lens
+
     def import_blocks(self, shuffle_id: int, map_ids: Sequence[int], start_partition: int, end_partition: int,
                       data, lengths) -> int:
         """Hand blocks fetched from another executor to this engine (sgx_import_blocks): the

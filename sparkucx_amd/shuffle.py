@@ -543,6 +543,92 @@ class UcxShuffleBlockResolver:
 # ---------------------------------------------------------------------------------------
 
 
+class TaskKilledException(_lib.ShuffleError):
+    """org.apache.spark.TaskKilledException: the task was cancelled."""
+
+
+class TaskContext:
+    """The part of Spark's TaskContext a shuffle read uses: cancellation (``markInterrupted``
+    by the executor, ``killTaskIfInterrupted`` by the task) and the task's read metrics
+    (``taskMetrics().mergeShuffleReadMetrics()`` folds a reader's temporary metrics in)."""
+
+    def __init__(self):
+        self._reason: Optional[str] = None
+        self.shuffleReadMetrics = ShuffleReadMetricsReporter()
+        self._temps: List["ShuffleReadMetricsReporter"] = []
+
+    def markInterrupted(self, reason: str = "killed") -> None:
+        self._reason = reason
+
+    def isInterrupted(self) -> bool:
+        return self._reason is not None
+
+    def killTaskIfInterrupted(self) -> None:
+        if self._reason is not None:
+            raise TaskKilledException(self._reason)
+
+    def createTempShuffleReadMetrics(self) -> "ShuffleReadMetricsReporter":
+        m = ShuffleReadMetricsReporter()
+        self._temps.append(m)
+        return m
+
+    def mergeShuffleReadMetrics(self) -> None:
+        t = ShuffleReadMetricsReporter()
+        for m in self._temps:
+            for k, v in vars(m).items():
+                setattr(t, k, getattr(t, k) + v)
+        self.shuffleReadMetrics = t
+
+
+class ShuffleReadMetricsReporter:
+    """Spark 3.0's ShuffleReadMetricsReporter (what getReader's ``metrics`` is): the counters the
+    reference's reader feeds (spark_3_0/UcxShuffleReader.scala:118-123 fetch wait, :148-153
+    records read) plus the block / byte counts Spark's fetcher iterator reports."""
+
+    def __init__(self):
+        self.remoteBlocksFetched = 0
+        self.localBlocksFetched = 0
+        self.remoteBytesRead = 0
+        self.localBytesRead = 0
+        self.fetchWaitTime = 0  # ms
+        self.recordsRead = 0
+
+    def incRemoteBlocksFetched(self, v: int) -> None:
+        self.remoteBlocksFetched += int(v)
+
+    def incLocalBlocksFetched(self, v: int) -> None:
+        self.localBlocksFetched += int(v)
+
+    def incRemoteBytesRead(self, v: int) -> None:
+        self.remoteBytesRead += int(v)
+
+    def incLocalBytesRead(self, v: int) -> None:
+        self.localBytesRead += int(v)
+
+    def incFetchWaitTime(self, ms: int) -> None:
+        self.fetchWaitTime += int(ms)
+
+    def incRecordsRead(self, v: int) -> None:
+        self.recordsRead += int(v)
+
+
+class InterruptibleIterator:
+    """org.apache.spark.InterruptibleIterator: checks the task's cancellation before every
+    element (the reference wraps its read in one, spark_3_0/UcxShuffleReader.scala:155-156,
+    193-199)."""
+
+    def __init__(self, context: TaskContext, delegate):
+        self.context = context
+        self.delegate = iter(delegate)
+
+    def __iter__(self):
+        return self
+
+    def __next__(self):
+        self.context.killTaskIfInterrupted()
+        return next(self.delegate)
+
+
 class UcxShuffleReader:
     """Reads reduce partitions [startPartition, endPartition) (UcxShuffleReader.scala:74-200).
     Blocks are fetched per (map, reduce) from HBM; the result is returned in the canonical
@@ -550,13 +636,24 @@ class UcxShuffleReader:
     each block (SURVEY.md §8(a) parity note)."""
 
     def __init__(self, manager: "UcxShuffleManager", handle: BaseShuffleHandle, startPartition: int,
-                 endPartition: int, mapIds: Optional[Sequence[int]] = None):
+                 endPartition: int, mapIds: Optional[Sequence[int]] = None, context: Optional[TaskContext] = None,
+                 readMetrics: Optional[ShuffleReadMetricsReporter] = None):
         R = handle.dependency.partitioner.numPartitions
         if not 0 <= startPartition <= endPartition <= R:
             raise IllegalArgumentException(f"bad partition range [{startPartition}, {endPartition})")
         self.manager, self.handle = manager, handle
         self.start, self.end = startPartition, endPartition
         self.mapIds = list(mapIds) if mapIds is not None else None
+        self.context = context or TaskContext()
+        self.readMetrics = readMetrics if readMetrics is not None else self.context.createTempShuffleReadMetrics()
+
+    def _count_blocks(self) -> None:
+        """Local blocks and bytes of the range (every block this engine holds for it)."""
+        maps = self._maps()
+        rids = [r for r in range(self.start, self.end) for _ in maps]
+        lens = self.manager.engine.block_lengths(self.handle.shuffleId, maps * (self.end - self.start), rids)
+        self.readMetrics.incLocalBlocksFetched(int(np.count_nonzero(lens)))
+        self.readMetrics.incLocalBytesRead(int(lens.sum()))
 
     def read_blocks(self):
         maps = self.mapIds if self.mapIds is not None else self.manager.known_maps(self.handle.shuffleId)
@@ -588,17 +685,73 @@ class UcxShuffleReader:
           key (ExternalSorter with an ordering, :166-181);
         * aggregator "group" (groupByKey, combineValuesByKey :155-164): (keys, group_starts,
           values) -- keys ascending per reducer, values in arrival order;
-        * aggregator "sum" (reduceByKey(_ + _)): (keys, sums)."""
+        * aggregator "sum" (reduceByKey(_ + _)): (keys, sums).
+        Metrics as the reference's reader reports them: the range's blocks and bytes, and
+        ``incRecordsRead`` with the records (or groups) handed to the task; a task killed
+        before the read raises TaskKilledException (``iterator()`` checks per record)."""
         dep = self.handle.dependency
         sid = self.handle.shuffleId
+        self.context.killTaskIfInterrupted()
+        self._count_blocks()
         if dep.aggregator is not None:
             if dep.recordBytes != 16:
                 raise UnsupportedOperationException("aggregation needs (Long, Long) 16 B records")
             agg = _lib.AGG_SUM if dep.aggregator.kind == "sum" else _lib.AGG_GROUP
-            return self.manager.engine.read_grouped(sid, self._maps(), self.start, self.end, agg)
+            out = self.manager.engine.read_grouped(sid, self._maps(), self.start, self.end, agg)
+            nrec = len(out[0])
+        elif dep.keyOrdering:
+            out = self.manager.engine.read_sorted(sid, self._maps(), self.start, self.end).reshape(-1, dep.recordBytes)
+            nrec = len(out)
+        elif _SERIALIZERS[dep.serializer] != _lib.SER_FIXED:  # the Kryo stream, decoded on the GPU
+            out = self.manager.engine.read_records(sid, self._maps(), self.start, self.end).reshape(-1, 16)
+            nrec = len(out)
+        else:
+            data, _, _, _ = self.read_blocks()
+            out = data.reshape(-1, dep.recordBytes)
+            nrec = len(out)
+        self.readMetrics.incRecordsRead(nrec)
+        self.context.mergeShuffleReadMetrics()
+        return out
+
+    def iterator(self) -> InterruptibleIterator:
+        """read() as Spark's task consumes it: (key, value) pairs of (Long, Long) records (or
+        (key, sum) / (key, values) after an aggregator), one at a time, in an
+        InterruptibleIterator that stops at the next record once the task is killed, with
+        ``incRecordsRead`` per record (spark_3_0/UcxShuffleReader.scala:148-156)."""
+        dep = self.handle.dependency
+        self.context.killTaskIfInterrupted()
+        self._count_blocks()
+        if dep.aggregator is not None:
+            if dep.recordBytes != 16:
+                raise UnsupportedOperationException("aggregation needs (Long, Long) 16 B records")
+            agg = _lib.AGG_SUM if dep.aggregator.kind == "sum" else _lib.AGG_GROUP
+            res = self.manager.engine.read_grouped(self.handle.shuffleId, self._maps(), self.start, self.end, agg)
+            if agg == _lib.AGG_SUM:
+                pairs = zip(res[0].tolist(), res[1].tolist())
+            else:
+                keys, starts, vals = res
+                ends = list(starts[1:].tolist()) + [len(vals)]
+                pairs = ((k, vals[s:e].tolist()) for k, s, e in zip(keys.tolist(), starts.tolist(), ends))
+        else:
+            out = self.read_raw()
+            kv = out.view("<i8").reshape(-1, dep.recordBytes // 8)[:, :2] if dep.recordBytes == 16 else None
+            pairs = ((int(a), int(b)) for a, b in kv) if kv is not None else (bytes(r) for r in out)
+
+        def counted():
+            for p in pairs:
+                self.readMetrics.incRecordsRead(1)
+                yield p
+            self.context.mergeShuffleReadMetrics()
+
+        return InterruptibleIterator(self.context, counted())
+
+    def read_raw(self) -> np.ndarray:
+        """The range's records (sorted when the dependency has a key ordering), no metrics."""
+        dep = self.handle.dependency
+        sid = self.handle.shuffleId
         if dep.keyOrdering:
             return self.manager.engine.read_sorted(sid, self._maps(), self.start, self.end).reshape(-1, dep.recordBytes)
-        if _SERIALIZERS[dep.serializer] != _lib.SER_FIXED:  # the Kryo stream, decoded on the GPU
+        if _SERIALIZERS[dep.serializer] != _lib.SER_FIXED:
             return self.manager.engine.read_records(sid, self._maps(), self.start, self.end).reshape(-1, 16)
         data, _, _, _ = self.read_blocks()
         return data.reshape(-1, dep.recordBytes)
@@ -707,7 +860,7 @@ class UcxShuffleManager:
 
     def getReader(self, handle: BaseShuffleHandle, startPartition: int, endPartition: int, context=None,
                   metrics=None, mapIds: Optional[Sequence[int]] = None) -> UcxShuffleReader:
-        return UcxShuffleReader(self, handle, startPartition, endPartition, mapIds)
+        return UcxShuffleReader(self, handle, startPartition, endPartition, mapIds, context, metrics)
 
     def exchange(self, handle: BaseShuffleHandle, mapId: int):
         """Push a local map output to the reducers' owners over RCCL (collective)."""

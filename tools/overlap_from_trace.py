@@ -37,6 +37,24 @@ def main():
     print(json.dumps(summ))
     for o in long[:12]:
         print(json.dumps(o))
+    # each map kernel's duration while an all-to-all runs beside it (HBM shared with the
+    # exchange) against its duration alone (the steps before the first / after the last one)
+    by = {}
+    for ms, me, _, name, _ in maps:
+        ov = sum(max(0, min(e, me) - max(s, ms)) for s, e, *_ in comms if e - s > 1e5)
+        frac = ov / max(1, me - ms)
+        key = "overlapped" if frac > 0.9 else "alone" if frac == 0 else None
+        if key:
+            by.setdefault(name, {}).setdefault(key, []).append((me - ms) / 1e6)
+    for name, d in by.items():
+        row = {"map_kernel": name}
+        for key in ("alone", "overlapped"):
+            v = d.get(key, [])
+            row[key + "_ms_mean"] = round(sum(v) / len(v), 4) if v else None
+            row[key + "_n"] = len(v)
+        if row["alone_ms_mean"] and row["overlapped_ms_mean"]:
+            row["stretch"] = round(row["overlapped_ms_mean"] / row["alone_ms_mean"], 3)
+        print(json.dumps(row))
 
 
 if __name__ == "__main__":
