@@ -77,6 +77,11 @@ def parse():
                          "stream, so one map's small kernels overlap another's scatter)")
     ap.add_argument("--serializer", choices=["fixed", "kryo"], default="fixed",
                     help="kryo: also frame each map output as Spark's Kryo stream (SURVEY §8(f) row 2)")
+    ap.add_argument("--batches", type=int, default=1,
+                    help="> 1: every map goes through the writer call sequence Spark drives "
+                         "(GpuShuffleWriter: sgx_map_begin, this many sgx_map_append batches -- 2^22 records "
+                         "each at C1 with 64 -- as retained device slices of the resident input, "
+                         "sgx_map_commit) instead of one sgx_write_map")
     a = ap.parse_args()
     a.record_bytes = 100 if a.workload == "c4" else 16
     a.records = a.records or (1 << 25 if a.workload == "c4" else 1 << 28)
@@ -208,7 +213,8 @@ def live_pmc(args):
         flags |= 32  # FLAG_NO_SPLIT_SCATTER (sparkucx_amd is not imported yet)
     cmd_tail = ["--", sys.executable, os.path.join(ROOT, "tools", "prof_map.py"), "--iters", "2",
                 "--records", str(args.records), "--partitions", str(args.partitions), "--dist", args.dist,
-                "--record-bytes", str(args.record_bytes), "--flags", str(flags), "--num-chunks", str(args.num_chunks)]
+                "--record-bytes", str(args.record_bytes), "--flags", str(flags), "--num-chunks", str(args.num_chunks),
+                "--batches", str(args.batches)]
     per = {}
     tmp = tempfile.mkdtemp(prefix="sgx_pmc_")
     try:
@@ -346,9 +352,20 @@ def main():
     tasks = args.map_tasks if (world == 1 and not self_x) else 1
     slots = max(2, tasks)
 
+    nbatch = max(1, args.batches)
+    cuts = [n * j // nbatch for j in range(nbatch + 1)]
+
     def step(k):
         mid = (k % slots) * world + rank  # alternating map slots per rank (one per task)
-        eng.write_map(sid, mid, buf, n, rb)
+        if nbatch == 1:
+            eng.write_map(sid, mid, buf, n, rb)
+        else:
+            # GpuShuffleWriter's sequence: begin, the batches (device slices the caller keeps
+            # until the commit), commit -- one pass over every batch at the commit
+            eng.map_begin(sid, mid)
+            for j in range(nbatch):
+                eng.map_append(sid, mid, buf, cuts[j + 1] - cuts[j], rb, offset=cuts[j] * rb, retained=True)
+            eng.map_commit(sid, mid)
         if args.compress:
             # the map task commits: its partition lengths, i.e. the LZ4 framing of its Kryo
             # streams, which the engine does when the lengths are first needed -- inside the step,
@@ -452,6 +469,9 @@ def main():
                      if rb == 16 else f"synthetic TeraSort 100 B records (10 random key bytes), seed {args.seed:#x}+rank, "
                      f"{len(bounds)} bounds sampled from rank 0's batch"),
             "config": {"workload": _workload_name(args, n, R, world, self_x), "map_tasks": tasks,
+                       "writer": "sgx_write_map (one batch)" if nbatch == 1 else (
+                           f"sgx_map_begin + {nbatch} x sgx_map_append (~{n // nbatch} records each, retained "
+                           f"device batches) + sgx_map_commit"),
                        "map_tasks_note": None if tasks == 1 else (
                            "concurrent map tasks: stage event times include the other tasks' kernels, "
                            "so the roofline fields are not per-kernel figures (DESIGN.md §9)"),

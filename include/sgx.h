@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define SGX_ABI_VERSION 6
+#define SGX_ABI_VERSION 7
 
 enum sgx_status {
     SGX_OK = 0,
@@ -49,8 +49,10 @@ enum sgx_partitioner {
     SGX_PART_RANGE_BYTES10 = 2  /* RangePartitioner over 10-byte unsigned keys (TeraSort)  */
 };
 
-/* Where a caller buffer lives. */
-enum sgx_mem_kind { SGX_MEM_HOST = 0, SGX_MEM_DEVICE = 1 };
+/* Where a caller buffer lives.  SGX_MEM_DEVICE_RETAINED (sgx_map_append only): device memory
+ * the caller keeps valid and unchanged until sgx_map_commit returns -- the commit reads the
+ * batch in place (no copy); elsewhere it means SGX_MEM_DEVICE. */
+enum sgx_mem_kind { SGX_MEM_HOST = 0, SGX_MEM_DEVICE = 1, SGX_MEM_DEVICE_RETAINED = 2 };
 
 typedef struct sgx_engine sgx_engine;
 
@@ -79,9 +81,12 @@ enum sgx_flags {
                                          write (sgx_map_layout)                                */
     SGX_FLAG_PAD_ANY_SIZE = 512,      /* testing: write maps of any size padded (default: from
                                          2^20 records up)                                      */
-    SGX_FLAG_NO_SEG_WINDOW = 1024     /* sorted reads of several partitions: the key window and
+    SGX_FLAG_NO_SEG_WINDOW = 1024,    /* sorted reads of several partitions: the key window and
                                          the partitioner in two LSD passes instead of one
                                          segmented pass per partition                          */
+    SGX_FLAG_NO_DEFERRED_APPEND = 2048 /* streaming maps: partition every sgx_map_append batch on
+                                         arrival and gather them at the commit (the round-4 form)
+                                         instead of one pass over all batches at the commit    */
 };
 
 typedef struct sgx_config {
@@ -238,12 +243,19 @@ int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void 
 int sgx_map_lengths(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *out_lengths);
 /* Streaming map output: the map task's records arrive as any number of batches (Spark's
  * writer sees unbounded partition streams and merges spills in spill order,
- * ucx/NvkvShuffleMapOutputWriter.scala:106-113,228-246).  sgx_map_begin opens the map;
- * every sgx_map_append partitions one batch on the GPU (K1-K4, Kryo framing) and keeps it in
- * HBM; sgx_map_commit concatenates, per partition, the batches in append order (one gather
- * launch) -- the result is byte-identical to sgx_write_map of all batches concatenated, then
- * LZ4 framing / map-side combine apply as for sgx_write_map.  out_lengths as sgx_write_map
- * (may be NULL).  Each batch holds < 2^32 records. */
+ * ucx/NvkvShuffleMapOutputWriter.scala:106-113,228-246).  sgx_map_begin opens the map.
+ * sgx_map_append hands over one batch: a host batch is copied into HBM, a SGX_MEM_DEVICE
+ * batch is copied within HBM, a SGX_MEM_DEVICE_RETAINED batch stays where it is (the caller
+ * keeps it until the commit returns).  sgx_map_commit then partitions ALL batches in one
+ * pass, exactly as sgx_write_map partitions one contiguous batch (the padded single-pass
+ * write when sgx_write_map would take it): every batch is cut into chunks of
+ * its own and a chunk table replaces the contiguous input.  The result is byte-identical to
+ * sgx_write_map of all batches concatenated; LZ4 framing applies as for sgx_write_map.
+ * Shuffles the one-pass commit does not cover (map-side combine, R > 1024 under a hash
+ * partitioner, 16 B records under a RangePartitioner, SGX_FLAG_NO_DEFERRED_APPEND, an engine
+ * whose lane-ordered ranking check failed) partition every batch on arrival and concatenate
+ * the batches per partition at the commit (one gather launch), with the same bytes.
+ * out_lengths as sgx_write_map (may be NULL).  A map holds < 2^32 records. */
 int sgx_map_begin(sgx_engine *e, int32_t shuffle_id, int64_t map_id);
 int sgx_map_append(sgx_engine *e, int32_t shuffle_id, int64_t map_id, const void *records, int64_t nrecords,
                    int32_t record_bytes, int32_t mem_kind);
@@ -254,8 +266,10 @@ int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, void **out_d
                  int64_t *out_bytes);
 /* How the engine holds a written map (waits for its kernels).  A fixed-codec HashPartitioner
  * map of 16 B records (R > 1024 through the two-level split), or a 100 B TeraSort map under
- * its RangePartitioner, written by sgx_write_map on an engine without a
- * multi-rank communicator, is written in ONE pass over its records: a sampled
+ * its RangePartitioner, written by sgx_write_map (or committed from sgx_map_append batches)
+ * on an engine with no communicator at all (none: a one-rank or host-collective communicator
+ * counts, so every multi-executor deployment takes the two-pass write), is written in ONE pass
+ * over its records: a sampled
  * histogram sizes a line-aligned sub-bin per (partition, chunk) stream, the stable scatter
  * writes every stream into its sub-bin, and a scan of the streams' true counts gives the
  * partition lengths and index offsets -- the same lengths, offsets and per-block bytes as the

@@ -19,7 +19,7 @@ SGX_OK = 0
 SGX_ERR_INVALID, SGX_ERR_STATE, SGX_ERR_HIP, SGX_ERR_COMM = -1, -2, -3, -4
 SGX_ERR_IO, SGX_ERR_NOMEM, SGX_ERR_NOT_FOUND, SGX_ERR_UNSUPPORTED, SGX_ERR_TIMEOUT = -5, -6, -7, -8, -9
 PART_HASH, PART_RANGE_I64, PART_RANGE_BYTES10 = 0, 1, 2
-MEM_HOST, MEM_DEVICE = 0, 1
+MEM_HOST, MEM_DEVICE, MEM_DEVICE_RETAINED = 0, 1, 2
 AGG_GROUP, AGG_SUM = 0, 1
 SER_FIXED, SER_KRYO = 0, 1
 STAGES = ("hist", "scan", "scatter", "allgather", "alltoall", "regroup", "sort", "group", "serialize",
@@ -34,10 +34,11 @@ FLAG_ASSUME_LDS_DISORDER = 128
 FLAG_NO_PADDED_MAP = 256
 FLAG_PAD_ANY_SIZE = 512
 FLAG_NO_SEG_WINDOW = 1024
+FLAG_NO_DEFERRED_APPEND = 2048
 LAYOUT_CONTIGUOUS, LAYOUT_PADDED, LAYOUT_SERIALIZED_PADDED = 0, 1, 2
 PLACE_EVEN, PLACE_BYTES = 0, 1
 WRITER_SORT, WRITER_UNSAFE = 0, 1
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 
 class ShuffleError(RuntimeError):

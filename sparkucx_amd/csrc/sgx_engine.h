@@ -148,8 +148,11 @@ struct Event {  // a lazily created, timing-disabled event
 // 106-113, 228-246; Spark merges spills in spill order).
 struct Spill {
     DevBuf data;                   // published bytes of this batch, partition-contiguous
+                                   // (deferred: the batch's records as appended, engine copy)
     std::vector<int64_t> lengths;  // [R] published bytes per partition
     int64_t nrec = 0;
+    const void *src = nullptr;     // deferred: the batch's records (data.p, or the caller's
+                                   // SGX_MEM_DEVICE_RETAINED buffer)
 };
 
 struct MapOut {
@@ -176,6 +179,11 @@ struct MapOut {
     // streaming writes (sgx_map_begin / _append / _commit): the batches so far
     bool open = false;
     std::vector<std::unique_ptr<Spill>> spills;
+    // deferred (sgx_map.cpp deferred_ok): the batches are kept as appended and the commit
+    // partitions all of them in one pass through a chunk table
+    bool deferred = false;
+    HostPinned chunk_host;     // [2G] i64 {byte offset from the first batch, records} | [S] i32 first chunk per batch
+    DevBuf chunk_dev;
     // Single-pass padded output (sgx_map.cpp padded_pass): `data` holds one
     // line-aligned sub-bin per (partition, chunk) stream with unwritten gaps between them;
     // frag = device [fstart][foff][cnt] u32 x R*G: a stream's first record in `data`, its
@@ -371,9 +379,20 @@ namespace sgx {
 // SGX_FLAG_DEBUG_SYNC: synchronise `st` and report a device error naming `what`.
 int debug_sync(sgx_engine *e, hipStream_t st, const char *what);
 PartParams make_part_params(const Shuffle &s);
-// One stable partition pass (K1+K2 hist -> K3 scan -> K4 scatter) on the context's stream.
+// A streaming map's batches as the map side's chunks (sgx_map_commit of deferred batches):
+// chunk g = chunks[2g+1] records at byte chunks[2g] from the pass's input pointer, every
+// chunk inside one batch, at most `chunk` records (a multiple of the K4 tile).
+struct ChunkTable {
+    const int64_t *dev = nullptr;
+    int64_t chunk = 0;
+    int G = 0;
+    std::vector<int64_t> len;  // host copy of the chunks' record counts
+};
+// One stable partition pass (K1+K2 hist -> K3 scan -> K4 scatter) on the context's stream;
+// with a chunk table its chunks replace the contiguous input's.
 int partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_t n, int rb, const PartParams &spp,
-                   int32_t R, int32_t kind, uint32_t *host_off, uint32_t *err_slot, bool stats);
+                   int32_t R, int32_t kind, uint32_t *host_off, uint32_t *err_slot, bool stats,
+                   const ChunkTable *ct = nullptr);
 // Lengths / published bytes of a written map (waits for its kernels).  Caller holds m.mu.
 int finish_lengths(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m);
 // A padded map's contiguous copy (m.dense, once; m.done is recorded behind it), so that

@@ -37,6 +37,11 @@ struct PartParams {
     // against pad_cap[p] (the sub-bin capacity of partition p); an overflow sets PAD_OVERFLOW
     uint32_t *pad_cnt;
     const uint32_t *pad_cap;
+    // ---- streaming map (sgx_map_append batches written in one pass at sgx_map_commit) ----
+    // chunk table: chunk g's records start at byte chunks[2g] from the kernel's input pointer
+    // and number chunks[2g+1] (every chunk inside one batch); null: chunk g = records
+    // [g * chunk, min(n, (g + 1) * chunk)) of one contiguous input
+    const int64_t *chunks;
 };
 // Error-word bits shared by the map-side kernels and the engine.
 constexpr uint32_t ERR_SPIN = 1u;          // a look-back spin gave up
@@ -134,9 +139,13 @@ hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint
 int64_t scan_tiles(int64_t len);
 // Padded map output.  launch_pad_sample: est[p] += records of partition p among
 // every `stride`-th group of 8 records (est zeroed by the caller; hash partitioner over 16 B
-// records, or RangePartitioner over 100 B TeraSort records; R <= 4096).
+// records, or RangePartitioner over 100 B TeraSort records; R <= 4096).  With a chunk table
+// (pp.chunks, a streaming map) each of the G chunks (<= `chunk` records) is sampled on its own.
 hipError_t launch_pad_sample(const void *in, int64_t n, int rb, int stride, const PartParams &pp, uint32_t *est,
-                             hipStream_t stream);
+                             hipStream_t stream, int64_t chunk = 0, int G = 0);
+// (partition, spill) segment offsets of a streaming map committed in one pass (k_spill_seg_offs).
+hipError_t launch_spill_seg_offs(const uint32_t *offs, const uint32_t *part_off, int R, int G, int S,
+                                 const int32_t *g0, uint32_t *out, hipStream_t stream);
 // The number of records launch_pad_sample reads (the estimate's denominator).
 int64_t pad_sampled_records(int64_t n, int stride);
 // Sub-bin capacities pcap[p] (records, a multiple of 8) from the sampled counts, and the

@@ -255,7 +255,11 @@ __device__ __forceinline__ void hist_body(const char *__restrict__ in, int64_t n
     __syncthreads();
     const int g = blockIdx.x / SPLIT, sub = blockIdx.x % SPLIT;
     const int64_t cbeg = (int64_t)g * chunk;
-    const int64_t cend = min(n, cbeg + chunk);
+    int64_t cend = min(n, cbeg + chunk);
+    if (pp.chunks) {  // a streaming map's chunk: its batch's bytes, indexed from cbeg as usual
+        in += pp.chunks[2 * g] - cbeg * (REC16 ? 16 : rb);
+        cend = cbeg + pp.chunks[2 * g + 1];
+    }
     const int64_t slice = (int64_t)T * UNROLL, step = slice * SPLIT;
     const int64_t nsteps = cend > cbeg ? (cend - cbeg + step - 1) / step : 0;
     for (int64_t st = nsteps - 1; st >= 0; --st) {
@@ -1232,6 +1236,13 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         obase = d[2] * (int64_t)R;
         g = (int)d[3];
     }
+    // the chunk's records (a streaming map's chunk: its batch's bytes, chunk table)
+    const u32x4 *cin = in + begin;
+    if constexpr (!SEG)
+        if (pp.chunks) {
+            cin = (const u32x4 *)((const char *)in + pp.chunks[2 * g]);
+            end = begin + pp.chunks[2 * g + 1];
+        }
     const int64_t len = end > begin ? end - begin : 0;
     const int64_t ntiles = (len + TNEW - 1) / TNEW;
     for (uint32_t p = tid; p < RS; p += T) {
@@ -1243,7 +1254,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     if constexpr (KIND == KIND_HOT_SPLIT)
         for (uint32_t i = tid; i < (1u << pp.dshift); i += T) tbl[i] = pp.dir[i];
 
-    const u32x4 *src = in + begin + (int64_t)w * NI * 64 + lane;
+    const u32x4 *src = cin + (int64_t)w * NI * 64 + lane;
     u32x4 rec[NI];
     bool valid[NI];
     u32x4 dk[SI];
@@ -1449,7 +1460,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         for (uint32_t i = lane; i < RS / 8; i += 64) ((u32x4 *)myrow)[i] = u32x4{0, 0, 0, 0};
         if (!last) {
             const int64_t nb = (t + 1) * TNEW;
-            const u32x4 *cb = in + begin;
+            const u32x4 *cb = cin;
 #pragma unroll
             for (int k = 0; k < NI; ++k) {
                 const int64_t i = nb + (int64_t)w * NI * 64 + k * 64 + lane;
@@ -1657,7 +1668,9 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
     const int g = blockIdx.x;
     const int64_t begin = (int64_t)g * chunk;
     const int64_t end = min(n, begin + chunk);
-    const int64_t len = end > begin ? end - begin : 0;
+    // the chunk's bytes (a streaming map's chunk: its batch's, chunk table)
+    const char *cin = pp.chunks ? (const char *)in + pp.chunks[2 * g] : (const char *)in + begin * RB;
+    const int64_t len = pp.chunks ? pp.chunks[2 * g + 1] : end > begin ? end - begin : 0;
     // tile counts in 32 bits, the last tile's size computed once: a 64-bit min() of the
     // per-tile remainder was mis-selected by the compiler (s_cselect on a stale SCC)
     const int ntiles = (int)((len + TR - 1) / TR);
@@ -1668,7 +1681,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
     // tile loads: 16 B chunks of a full tile; the input's last (partial) tile goes dword-wise
     u32x4 ld[LD];
     auto issue = [&](int t) {
-        const u32x4 *tb = (const u32x4 *)((const char *)in + (begin + (int64_t)t * TR) * RB);
+        const u32x4 *tb = (const u32x4 *)(cin + (int64_t)t * TR * RB);
         const int nrec = t + 1 < ntiles ? TR : lastn;
         const int nch = nrec == TR ? NCH : 0;  // partial tiles are loaded dword-wise below
 #pragma unroll
@@ -1705,7 +1718,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
                 if (c < NCH) ((u32x4 *)stage)[c] = ld[i];
             }
         } else {
-            const uint32_t *tb = (const uint32_t *)((const char *)in + (begin + (int64_t)t * TR) * RB);
+            const uint32_t *tb = (const uint32_t *)(cin + (int64_t)t * TR * RB);
             for (int d = tid; d < nrec * DW; d += T) stage[d] = tb[d];
         }
         __syncthreads();
@@ -1874,6 +1887,14 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 #ifndef SGX_WWC_DRAIN_UNROLL
 #define SGX_WWC_DRAIN_UNROLL 2
 #endif
+// the drain in dword arithmetic, one division per piece (A/B: -DSGX_WWC_DRAIN_V2=0)
+#ifndef SGX_WWC_DRAIN_V2
+#define SGX_WWC_DRAIN_V2 1
+#endif
+// XOR-swizzled carry rows (A/B: -DSGX_WWC_SWIZZLE=0)
+#ifndef SGX_WWC_SWIZZLE
+#define SGX_WWC_SWIZZLE 1
+#endif
 constexpr int WWC_TR = 512;
 constexpr int WWC_UMAX = (WWC_TR * 100 + 1024 * 60) / 64 + 1;  // units per tile (R <= 1024)
 
@@ -1946,22 +1967,31 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
     uint32_t *myrow32 = (uint32_t *)myrow;
     const Bounds12 bk{b12};
     const int64_t *bi64 = (const int64_t *)b12;
+    // dword i of stream p's carry row, XOR-swizzled by the stream's p / 4: a row is 16 dwords,
+    // so unswizzled the rows of streams p, p + 4, ... share their banks -- the owners' carry
+    // writes (lanes j -> streams 2j + h) were 32-way bank conflicts (SQ counters,
+    // profiles/r05a_terasort_k4_sq_counters.txt: conflicts 56 % of the LDS cycles)
+    auto cx = [](uint32_t p, uint32_t i) __attribute__((always_inline)) -> uint32_t {
+        return 16u * p + (i ^ (SGX_WWC_SWIZZLE ? (p >> 2) & 15u : 0u));
+    };
 
     const int g = blockIdx.x;
     const int64_t begin = (int64_t)g * chunk;
     const int64_t end = min(n, begin + chunk);
-    const int64_t len = end > begin ? end - begin : 0;
+    // the chunk's bytes (a streaming map's chunk: its batch's, chunk table)
+    const char *cin = pp.chunks ? (const char *)in + pp.chunks[2 * g] : (const char *)in + begin * RB;
+    const int64_t len = pp.chunks ? pp.chunks[2 * g + 1] : end > begin ? end - begin : 0;
     const int ntiles = (int)((len + TR - 1) / TR);
     const int lastn = ntiles > 0 ? (int)(len - (int64_t)(ntiles - 1) * TR) : 0;
     for (uint32_t p = tid; p < RS; p += T) {
         const uint32_t c0 = p < R ? offs[(int64_t)p * G + g] : 0u;
         cur[p] = c0;
-        carry[16 * p + 15] = c0;  // the stream's first record: bytes before it are not ours
+        carry[cx(p, 15)] = c0;  // the stream's first record: bytes before it are not ours
     }
 
     u32x4 ld[LD];
     auto issue = [&](int t) {
-        const u32x4 *tb = (const u32x4 *)((const char *)in + (begin + (int64_t)t * TR) * RB);
+        const u32x4 *tb = (const u32x4 *)(cin + (int64_t)t * TR * RB);
         const int nch = (t + 1 < ntiles ? TR : lastn) == TR ? NCH : 0;  // partial tiles: dword-wise
 #pragma unroll
         for (int i = 0; i < LD; ++i) {
@@ -1983,7 +2013,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             const uint32_t p = 2 * tid + h;
 #pragma unroll
             for (int i = 0; i < 15; ++i)
-                if ((uint32_t)i < ncnt[h]) carry[16 * p + i] = creg[h][i];
+                if ((uint32_t)i < ncnt[h]) carry[cx(p, i)] = creg[h][i];
             cur[p] = ncur[h];
             upd[h] = false;
         }
@@ -1999,7 +2029,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
                 if (c < NCH) ((u32x4 *)stage)[c] = ld[i];
             }
         } else {
-            const uint32_t *tb = (const uint32_t *)((const char *)in + (begin + (int64_t)t * TR) * RB);
+            const uint32_t *tb = (const uint32_t *)(cin + (int64_t)t * TR * RB);
             for (int d = tid; d < nrec * DW; d += T) stage[d] = tb[d];
         }
         for (uint32_t i = tid; i < (uint32_t)W * RS / 2; i += T) ((uint32_t *)rows)[i] = 0u;
@@ -2071,11 +2101,49 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
 #pragma unroll SGX_WWC_DRAIN_UNROLL
 #endif
         for (uint32_t q = tid; q < npieces; q += T) {
+#if SGX_WWC_DRAIN_V2
+            // dword arithmetic: a piece's 4 dwords are y0..y0+3 of the unit space that starts at
+            // the stream's open unit (u0D); below cbD they are the carry's, else dword od of the
+            // stream's new records in sorted order -- record r = od / 25, dword w = od % 25, one
+            // division per piece (a piece crosses at most one record boundary)
+            const uint32_t D = desc[q >> 2];
+            const uint32_t p = D & 1023u, plo = (D >> 10) & 1023u;
+            const uint32_t y0 = (D >> 20) * 16u + (q & 3u) * 4u;
+            const uint64_t cD = (uint64_t)cur[p] * DW;
+            const uint64_t u0D = cD & ~(uint64_t)15;
+            const uint32_t cbD = (uint32_t)(cD - u0D);
+            const int32_t od0 = (int32_t)y0 - (int32_t)cbD;
+            uint32_t r = od0 > 0 ? (uint32_t)od0 / (uint32_t)DW : 0u;
+            uint32_t wd = od0 > 0 ? (uint32_t)od0 - r * DW : 0u;
+            uint32_t sbase = (uint32_t)idx[plo + r] * DW;
+            uint32_t vv[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                if (od0 + d < 0) {
+                    vv[d] = carry[cx(p, y0 + d)];
+                } else {
+                    vv[d] = stage[sbase + wd];
+                    if (++wd == (uint32_t)DW && d < 3) {
+                        wd = 0;
+                        sbase = (uint32_t)idx[plo + ++r] * DW;
+                    }
+                }
+            }
+            const uint64_t bD = u0D + y0;
+            const uint64_t startD = (uint64_t)carry[cx(p, 15)] * DW, capD = (uint64_t)olim * DW;
+            if (bD >= startD && bD + 4 <= capD) {
+                *(u32x4 *)(out + bD) = u32x4{vv[0], vv[1], vv[2], vv[3]};
+            } else {  // the stream's first unit: only its own dwords
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                    if (bD + d >= startD && bD + d < capD) out[bD + d] = vv[d];
+            }
+#else
             const uint32_t D = desc[q >> 2];
             const uint32_t p = D & 1023u, plo = (D >> 10) & 1023u;
             const uint32_t rel = (D >> 20) * 64u + (q & 3u) * 16u;
             const uint64_t cB = (uint64_t)cur[p] * RB;
-            const uint64_t startB = (uint64_t)carry[16 * p + 15] * RB;
+            const uint64_t startB = (uint64_t)carry[cx(p, 15)] * RB;
             const uint64_t u0B = cB & ~(uint64_t)63;
             const uint32_t cb = (uint32_t)(cB - u0B);
             uint32_t vv[4];
@@ -2083,7 +2151,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             for (int d = 0; d < 4; ++d) {
                 const uint32_t x = rel + 4u * d;
                 if (x < cb) {
-                    vv[d] = carry[16 * p + (x >> 2)];
+                    vv[d] = carry[cx(p, x >> 2)];
                 } else {
                     const uint32_t o = x - cb, r = o / 100u;
                     vv[d] = stage[(uint32_t)idx[plo + r] * DW + ((o - r * 100u) >> 2)];
@@ -2099,6 +2167,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
                     if (b >= startB && b + 4 <= capB) *(uint32_t *)((char *)out + b) = vv[d];
                 }
             }
+#endif
         }
         // the owner's streams: next cursor, and the new open unit = the tail of the tile's last
         // record of the stream (a record is longer than a unit, so it always closes the old one)
@@ -2126,9 +2195,9 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
     // ---- the chunk's end: every stream's open unit (its own dwords)
     for (uint32_t p = tid; p < R; p += T) {
         const uint64_t cB = (uint64_t)cur[p] * RB, u0B = cB & ~(uint64_t)63;
-        const uint64_t startB = (uint64_t)carry[16 * p + 15] * RB;
+        const uint64_t startB = (uint64_t)carry[cx(p, 15)] * RB;
         for (uint64_t b = u0B > startB ? u0B : startB; b < cB; b += 4)
-            if (b + 4 <= capB) *(uint32_t *)((char *)out + b) = carry[16 * p + (uint32_t)((b - u0B) >> 2)];
+            if (b + 4 <= capB) *(uint32_t *)((char *)out + b) = carry[cx(p, (uint32_t)((b - u0B) >> 2))];
     }
     if constexpr (MODE == WC_PADDED) {
         bool ovf = false;
@@ -3123,35 +3192,52 @@ int64_t pad_sampled_records(int64_t n, int stride) {
     return (ns - 1) * 8 + (n - last < 8 ? n - last : 8);
 }
 
+// sample slots per chunk of a streaming map (chunk table): every chunk is sampled on its own,
+// one group of 8 records in `stride`, like a whole map
+__host__ __device__ inline int64_t pad_chunk_slots(int64_t chunk, int stride) {
+    return ((chunk + 7) / 8 + stride - 1) / stride * 8;
+}
+
 template <int KIND, int RB>
 __global__ __launch_bounds__(PAD_SAMPLE_THREADS) void k_pad_sample(const char *__restrict__ in, int64_t n,
                                                                    int stride, PartParams pp,
-                                                                   uint32_t *__restrict__ est) {
+                                                                   uint32_t *__restrict__ est, int64_t chunk,
+                                                                   int G) {
     __shared__ uint32_t h[PAD_SAMPLE_MAX_R];
     const uint32_t tid = threadIdx.x;
     for (uint32_t p = tid; p < pp.R; p += PAD_SAMPLE_THREADS) h[p] = 0;
     __syncthreads();
-    const int64_t nlines = (n + 7) / 8, ns = (nlines + stride - 1) / stride, nt = ns * 8;
+    const int64_t nlines = (n + 7) / 8, ns = (nlines + stride - 1) / stride;
+    const int64_t per = pp.chunks ? pad_chunk_slots(chunk, stride) : 0;
+    const int64_t nt = pp.chunks ? per * G : ns * 8;
     const int64_t step = (int64_t)gridDim.x * PAD_SAMPLE_THREADS;
     // sampled slot t = record t & 7 of group (t >> 3) * stride of 8 records: 8 lanes read one
-    // 128 B line (16 B records) or 800 B (100 B records)
+    // 128 B line (16 B records) or 800 B (100 B records); a streaming map's slot t is slot
+    // t % per of chunk t / per
     for (int64_t t0 = (int64_t)blockIdx.x * PAD_SAMPLE_THREADS + tid; t0 < nt; t0 += step * PAD_SAMPLE_UNROLL) {
         uint32_t x[PAD_SAMPLE_UNROLL], y[PAD_SAMPLE_UNROLL], z[PAD_SAMPLE_UNROLL];
         bool ok[PAD_SAMPLE_UNROLL];
 #pragma unroll
         for (int u = 0; u < PAD_SAMPLE_UNROLL; ++u) {
-            const int64_t t = t0 + u * step;
+            int64_t t = t0 + u * step, lim = n;
+            const char *base = in;
+            if (pp.chunks && t < nt) {
+                const int64_t g = t / per;
+                t -= g * per;
+                base = in + pp.chunks[2 * g];
+                lim = pp.chunks[2 * g + 1];
+            }
             const int64_t i = (t >> 3) * stride * 8 + (t & 7);
-            ok[u] = t < nt && i < n;
+            ok[u] = t0 + u * step < nt && i < lim;
             x[u] = y[u] = z[u] = 0;
             if (ok[u]) {
                 if constexpr (RB == 16) {
-                    const uint4 r = ((const uint4 *)in)[i];
+                    const uint4 r = ((const uint4 *)base)[i];
                     x[u] = r.x;
                     y[u] = r.y;
                     z[u] = r.z;
                 } else {
-                    const uint32_t *q = (const uint32_t *)(in + i * RB);
+                    const uint32_t *q = (const uint32_t *)(base + i * RB);
                     x[u] = q[0];
                     y[u] = q[1];
                     z[u] = q[2];
@@ -3168,20 +3254,20 @@ __global__ __launch_bounds__(PAD_SAMPLE_THREADS) void k_pad_sample(const char *_
 }
 
 hipError_t launch_pad_sample(const void *in, int64_t n, int rb, int stride, const PartParams &pp, uint32_t *est,
-                             hipStream_t stream) {
+                             hipStream_t stream, int64_t chunk, int G) {
     if (pp.R > (uint32_t)PAD_SAMPLE_MAX_R || stride < 1) return hipErrorInvalidValue;
     if (n <= 0) return hipSuccess;
-    const int64_t nt = pad_sampled_records(n, stride) + 8;
+    const int64_t nt = pp.chunks ? pad_chunk_slots(chunk, stride) * G : pad_sampled_records(n, stride) + 8;
     const int64_t per = (int64_t)PAD_SAMPLE_THREADS * PAD_SAMPLE_UNROLL;
     const int64_t want = (nt + per - 1) / per;
     const int grid = (int)(want < 1 ? 1 : want > PAD_SAMPLE_GRID ? PAD_SAMPLE_GRID : want);
     const char *c = (const char *)in;
     if (rb == 16 && pp.kind == SGX_PART_HASH)
         hipLaunchKernelGGL((k_pad_sample<SGX_PART_HASH, 16>), dim3(grid), dim3(PAD_SAMPLE_THREADS), 0, stream, c, n,
-                           stride, pp, est);
+                           stride, pp, est, chunk, G);
     else if (rb == 100 && pp.kind == SGX_PART_RANGE_BYTES10)
         hipLaunchKernelGGL((k_pad_sample<SGX_PART_RANGE_BYTES10, 100>), dim3(grid), dim3(PAD_SAMPLE_THREADS), 0, stream,
-                           c, n, stride, pp, est);
+                           c, n, stride, pp, est, chunk, G);
     else
         return hipErrorInvalidValue;
     return hipGetLastError();
@@ -3323,6 +3409,36 @@ hipError_t launch_gather_frags(const int64_t *desc, int64_t nblocks, int G, hipS
     if (nblocks <= 0 || G <= 0) return hipSuccess;
     const dim3 grid((unsigned)G, (unsigned)(nblocks < 65535 ? nblocks : 65535));
     hipLaunchKernelGGL(k_gather_frags, grid, dim3(FRAG_THREADS), 0, stream, desc, nblocks);
+    return hipGetLastError();
+}
+
+// ------------------------------------------------------------------------------------
+// A streaming map committed in one pass (sgx_map_commit, deferred batches) and framed by
+// UnsafeShuffleWriter's fast merge: every (partition p, spill b) segment's first record in the
+// contiguous output = the pass's offset of stream (p, the batch's first chunk g0[b]) -- the
+// batch's chunks follow each other in every partition -- or, past the last chunk, the
+// partition's end.  out[R*S] = the record count.
+// ------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_spill_seg_offs(const uint32_t *__restrict__ offs,
+                                                         const uint32_t *__restrict__ part_off, int R, int G, int S,
+                                                         const int32_t *__restrict__ g0, uint32_t *__restrict__ out) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const int64_t nseg = (int64_t)R * S;
+    if (i > nseg) return;
+    if (i == nseg) {
+        out[i] = part_off[R];
+        return;
+    }
+    const int p = (int)(i / S), b = (int)(i - (int64_t)p * S);
+    const int g = g0[b];
+    out[i] = g < G ? offs[(int64_t)p * G + g] : part_off[p + 1];
+}
+
+hipError_t launch_spill_seg_offs(const uint32_t *offs, const uint32_t *part_off, int R, int G, int S,
+                                 const int32_t *g0, uint32_t *out, hipStream_t stream) {
+    const int64_t m = (int64_t)R * S + 1;
+    hipLaunchKernelGGL(k_spill_seg_offs, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, offs, part_off, R, G,
+                       S, g0, out);
     return hipGetLastError();
 }
 

@@ -25,8 +25,11 @@ using namespace sgx;
 // stream.  The (R+1) record offsets and the device error word land in `host_off` (R+2 u32,
 // pinned) when given; the error word alone in `err_slot` (device) when given; the device
 // offsets stay in c.last_off_dev until the context's next pass.
-int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_t n, int rb, const PartParams &spp,
-                        int32_t R, int32_t kind, uint32_t *host_off, uint32_t *err_slot, bool stats) {
+int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_t n, int rb, const PartParams &spp0,
+                        int32_t R, int32_t kind, uint32_t *host_off, uint32_t *err_slot, bool stats,
+                        const ChunkTable *ct) {
+    PartParams spp = spp0;
+    spp.chunks = ct ? ct->dev : nullptr;
     hipStream_t st = c.st;
     // K4 choice (every choice is byte-identical):
     //   hash, 16 B, R <= 1024   write-combining staged kernel (whole 128 B lines only)
@@ -84,7 +87,14 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     const int tile = geo.tile;
     int64_t chunk = n > 0 ? (n + e->G - 1) / e->G : 1;
     chunk = (chunk + tile - 1) / tile * tile;
-    const int G = n > 0 ? (int)((n + chunk - 1) / chunk) : 1;
+    int G = n > 0 ? (int)((n + chunk - 1) / chunk) : 1;
+    if (ct && n > 0) {  // a streaming map's chunks (cut by the commit on this geometry's tile)
+        if (split || ct->chunk % tile != 0)
+            return fail_msg(SGX_ERR_HIP, "internal error: chunk table of %lld records on a tile of %d",
+                            (long long)ct->chunk, tile);
+        chunk = ct->chunk;
+        G = ct->G;
+    }
     const int64_t len = (int64_t)R * G;
     const int64_t tiles = scan_tiles(len);
     const int64_t len1 = (int64_t)S * G;
@@ -241,7 +251,7 @@ struct PadGeom {
     int G = 0, stride = 1;
 };
 
-static PadGeom pad_geom(sgx_engine *e, const Shuffle &s, int64_t n) {
+static PadGeom pad_geom(sgx_engine *e, const Shuffle &s, int64_t n, const ChunkTable *ct = nullptr) {
     PadGeom pg;
     const int32_t R = s.R;
     if (s.rb == 16 && R > 1024) {  // the split's level 1 (its tile decides the chunks)
@@ -260,6 +270,13 @@ static PadGeom pad_geom(sgx_engine *e, const Shuffle &s, int64_t n) {
     // (C1: one 128 B line in 128, 34 MB of the 4.3 GB map)
     pg.stride = (int)std::min<int64_t>(PAD_SAMPLE_STRIDE_MAX, std::max<int64_t>(1, ((n + 7) / 8) >> 16));
     pg.sampled = pad_sampled_records(n, pg.stride);
+    if (ct) {  // a streaming map: its chunks, each sampled on its own (k_pad_sample)
+        if (ct->chunk % tile != 0) return PadGeom{};
+        pg.chunk = ct->chunk;
+        pg.G = ct->G;
+        pg.sampled = 0;
+        for (int64_t l : ct->len) pg.sampled += pad_sampled_records(l, pg.stride);
+    }
     pg.olim = pad_capacity_bound(n, R, pg.chunk, pg.G, pg.sampled);
     if (s.rb == 16 && R > 1024 && pg.olim >= 0) {
         // the level-1 scratch (cold super-partitions' sub-bins) and the output share one bound
@@ -399,7 +416,7 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
 // otherwise).  Asynchronous on the context's stream; (R+1) offsets, the error word and the
 // padded K4's flag word land in m.part_off.
 static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n,
-                       const PadGeom &pg) {
+                       const PadGeom &pg, const ChunkTable *ct = nullptr) {
     hipStream_t st = c.st;
     const int32_t R = s.R;
     const int G = pg.G;
@@ -432,11 +449,13 @@ static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void 
     HIP_TRY(hipMemsetAsync(c.work.p, 0, work_bytes, st));
     hipEvent_t h0 = e->ev(), h1 = e->ev(), c1 = e->ev(), x1 = e->ev();
     HIP_TRY(hipEventRecord(h0, st));
-    HIP_TRY(launch_pad_sample(in, n, rb, pg.stride, s.pp, est, st));
+    PartParams bp = s.pp;  // the shuffle's partitioner over this map's input (chunk table or not)
+    bp.chunks = ct ? ct->dev : nullptr;
+    HIP_TRY(launch_pad_sample(in, n, rb, pg.stride, bp, est, st, pg.chunk, G));
     HIP_TRY(launch_pad_caps(est, R, pg.sampled, pg.chunk, G, olim, pcap, fstart, err_pad, st));
     SGX_TRY(debug_sync(e, st, "padded sample / capacities"));
     HIP_TRY(hipEventRecord(h1, st));
-    PartParams kp = s.pp;
+    PartParams kp = bp;
     kp.mbits = (uint32_t)pg.geo.mbits;
     kp.olim = olim;
     kp.pad_cnt = cnt;
@@ -446,7 +465,7 @@ static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void 
     HIP_TRY(hipEventRecord(c1, st));
     HIP_TRY(launch_scan(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, st));
     // the two-pass fallback, each kernel a no-op unless *err_pad has PAD_OVERFLOW
-    PartParams fp = s.pp;
+    PartParams fp = bp;
     fp.guard = err_pad;
     HIP_TRY(launch_hist(in, n, rb, pg.chunk, G, fp, counts_fb, st, e->hist_mode, true));
     HIP_TRY(launch_scan(counts_fb, (uint32_t *)c.offs.p, len, status_fb, ticket_fb, err, part_off_dev, G, R, st,
@@ -565,29 +584,39 @@ static int combine_sum(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void 
 // After the records of a map are known (device `in`, n records, or already partitioned in
 // m.data when `partitioned`): partition / combine, then frame.  Asynchronous except for the
 // combine.  m.done is recorded behind the last kernel.
+// ct: a streaming map's batches (deferred commit) as the input's chunks; the padded write
+// then needs no_pad false, and a Kryo map framed per (partition, spill) segment (seg_spills > 1)
+// gets its segment offsets from the pass's per-(partition, chunk) offsets (g0: each batch's
+// first chunk, device).
 static int run_map_pipeline(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n,
-                            bool partitioned, const uint32_t *part_dev) {
+                            bool partitioned, const uint32_t *part_dev, const ChunkTable *ct = nullptr,
+                            bool no_pad = false, const int32_t *g0_dev = nullptr) {
     m.ready = false;
     m.ser_valid = false;
     m.comp_valid = false;
     m.pad_try = m.padded = m.rec_padded = m.dense_valid = false;
     const uint32_t *rec_off_dev = part_dev;
     PadGeom pg;
-    if (!partitioned && use_padded(e, s, in, n)) pg = pad_geom(e, s, n);
+    if (!partitioned && !no_pad && use_padded(e, s, in, n)) pg = pad_geom(e, s, n, ct);
     if (s.combine == SGX_AGG_SUM) {
         SGX_TRY(combine_sum(e, c, s, m, partitioned ? m.data.p : in, n));
         rec_off_dev = c.last_off_dev;
     } else if (!partitioned && pg.olim >= n) {
         m.nrec = n;
-        if (s.rb == 16 && s.R > 1024) SGX_TRY(padded_split_pass(e, c, s, m, in, n, pg));
-        else SGX_TRY(padded_pass(e, c, s, m, in, n, pg));
+        if (s.rb == 16 && s.R > 1024 && !ct) SGX_TRY(padded_split_pass(e, c, s, m, in, n, pg));
+        else SGX_TRY(padded_pass(e, c, s, m, in, n, pg, ct));
         rec_off_dev = c.last_off_dev;
     } else if (!partitioned) {
         m.nrec = n;
         SGX_TRY(m.data.ensure((size_t)std::max<int64_t>(n * s.rb, 16)));
         SGX_TRY(partition_pass(e, c, in, m.data.p, n, s.rb, s.pp, s.R, s.kind, (uint32_t *)m.part_off.p, nullptr,
-                               true));
+                               true, ct));
         rec_off_dev = c.last_off_dev;
+        if (ct && m.seg_spills > 1) {  // (partition, spill) segments from the (partition, chunk) offsets
+            SGX_TRY(m.seg_off.ensure((size_t)((int64_t)s.R * m.seg_spills + 1) * 4));
+            HIP_TRY(launch_spill_seg_offs((const uint32_t *)c.offs.p, rec_off_dev, s.R, n > 0 ? ct->G : 0,
+                                          m.seg_spills, g0_dev, (uint32_t *)m.seg_off.p, c.st));
+        }
     }
     if (s.ser == SGX_SER_KRYO) {
         if (m.seg_spills > 1)  // (partition, spill) segments, SGX_WRITER_UNSAFE
@@ -604,6 +633,7 @@ int sgx::finish_lengths(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
     if (m.ready) return SGX_OK;
     if (!m.written) return fail_msg(SGX_ERR_STATE, "map output was not committed");
     HIP_TRY(m.done.wait_host());
+    if (m.deferred) m.spills.clear();  // the commit's pass has read the batches
     const uint32_t *po = (const uint32_t *)m.part_off.p;
     if (m.pad_try) {
         // the padded write's own flag word: an overflow means the guarded two-pass fallback
@@ -701,7 +731,7 @@ static int check_batch(const Shuffle &s, const void *records, int64_t n, int32_t
     if (rb != s.rb) return fail_msg(SGX_ERR_INVALID, "record_bytes %d != registered %d", rb, s.rb);
     if (n < 0 || n >= (int64_t)UINT32_MAX) return fail_msg(SGX_ERR_INVALID, "nrecords %lld out of range", (long long)n);
     if (n > 0 && !records) return fail_msg(SGX_ERR_INVALID, "records is NULL");
-    if (mem_kind != SGX_MEM_HOST && mem_kind != SGX_MEM_DEVICE)
+    if (mem_kind != SGX_MEM_HOST && mem_kind != SGX_MEM_DEVICE && mem_kind != SGX_MEM_DEVICE_RETAINED)
         return fail_msg(SGX_ERR_INVALID, "unknown mem_kind %d", mem_kind);
     return SGX_OK;
 }
@@ -737,6 +767,7 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
     m->written = false;
     m->exchanged = false;
     m->open = false;
+    m->deferred = false;
     m->spills.clear();
     m->seg_spills = 1;
     SGX_TRY(m->part_off.ensure((size_t)(s->R + 3) * 4));
@@ -757,6 +788,84 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
 // ------------------------------------------------------------------------------------
 // streaming map outputs
 // ------------------------------------------------------------------------------------
+// Deferred batches: sgx_map_append only lands the batch in HBM (a host batch
+// through PCIe, a device batch copied, a retained device batch not at all) and the commit
+// partitions every batch in ONE pass, with a chunk table in place of a contiguous input --
+// the padded single-pass write where sgx_write_map would take it, else the two-pass one.  The
+// map-side kernels that take a chunk table: the write-combining 16 B K4 (hash, R <= 1024) and
+// the wide-record K4s (TeraSort), with their histogram and sample.
+static bool deferred_ok(sgx_engine *e, const Shuffle &s) {
+    if ((e->flags & SGX_FLAG_NO_DEFERRED_APPEND) || s.combine != -1) return false;
+    if (e->rank_mode != SGX_RANK_ORDERED || !e->lds_order_ok || e->sc_waves || e->sc_items) return false;
+    if (s.rb == 16 && s.kind == SGX_PART_HASH && s.R <= 1024)
+        return !(e->flags & SGX_FLAG_NO_WRITE_COMBINING) && scatter_geom16_wc((uint32_t)s.R).items != 0;
+    if (s.rb == 100 && s.kind == SGX_PART_RANGE_BYTES10)
+        return !(e->flags & SGX_FLAG_NO_WIDE_STAGED) && scatter_geom_wide2((uint32_t)s.R, 100, s.kind, s.nb).items != 0;
+    return false;
+}
+
+// the K4 tile the deferred commit cuts its chunks on (partition_pass / pad_geom pick the same
+// geometry for these shuffles)
+static int deferred_tile(const Shuffle &s) {
+    return s.rb == 16 ? scatter_geom16_wc((uint32_t)s.R).tile : scatter_geom_wide2((uint32_t)s.R, 100, s.kind, s.nb).tile;
+}
+
+// The commit of deferred batches: chunks of at most `chunk` records (the map cut like one
+// contiguous batch: about one per CU, a multiple of the tile), every batch into chunks of
+// its own, the last one partial; byte offsets from the first non-empty batch.  The table
+// ([2G] i64, then [S] i32 first chunk of every batch) goes to the device on the context's
+// stream from the map's pinned buffer.
+static int commit_deferred(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, int64_t total) {
+    const int rb = s.rb;
+    const int32_t S = (int32_t)m.spills.size();
+    const void *base = nullptr;
+    for (auto &sp : m.spills)
+        if (sp->nrec > 0) {
+            base = sp->src;
+            break;
+        }
+    m.seg_spills = (s.writer == SGX_WRITER_UNSAFE && s.ser == SGX_SER_KRYO && s.lz4_block > 0 && S > 1) ? S : 1;
+    if (total == 0) {
+        m.open = false;
+        if (m.seg_spills > 1) {  // every (partition, spill) segment is empty
+            const size_t sb = (size_t)((int64_t)s.R * m.seg_spills + 1) * 4;
+            SGX_TRY(m.seg_off.ensure(sb));
+            HIP_TRY(hipMemsetAsync(m.seg_off.p, 0, sb, c.st));
+        }
+        return run_map_pipeline(e, c, s, m, nullptr, 0, false, nullptr);
+    }
+    const int tile = deferred_tile(s);
+    int64_t chunk = (total + e->G - 1) / e->G;
+    chunk = (chunk + tile - 1) / tile * tile;
+    ChunkTable ct;
+    ct.chunk = chunk;
+    std::vector<int64_t> tab;
+    std::vector<int32_t> g0((size_t)S, 0);
+    for (int32_t b = 0; b < S; ++b) {
+        const Spill &sp = *m.spills[(size_t)b];
+        g0[(size_t)b] = (int32_t)ct.len.size();
+        for (int64_t j = 0; j < sp.nrec; j += chunk) {
+            tab.push_back((int64_t)((const char *)sp.src - (const char *)base) + j * rb);
+            tab.push_back(std::min<int64_t>(chunk, sp.nrec - j));
+            ct.len.push_back(tab.back());
+        }
+    }
+    ct.G = (int)ct.len.size();
+    const size_t tb = tab.size() * 8, bytes = tb + (size_t)S * 4;
+    SGX_TRY(m.chunk_host.ensure(bytes));
+    SGX_TRY(m.chunk_dev.ensure(bytes));
+    std::memcpy(m.chunk_host.p, tab.data(), tb);
+    std::memcpy((char *)m.chunk_host.p + tb, g0.data(), (size_t)S * 4);
+    HIP_TRY(hipMemcpyAsync(m.chunk_dev.p, m.chunk_host.p, bytes, hipMemcpyHostToDevice, c.st));
+    ct.dev = (const int64_t *)m.chunk_dev.p;
+    m.open = false;
+    // UnsafeShuffleWriter's per-(partition, spill) LZ4 streams need contiguous records (the
+    // serializer's segment offsets come from the two-pass scan)
+    SGX_TRY(run_map_pipeline(e, c, s, m, base, total, false, nullptr, &ct, m.seg_spills > 1,
+                             (const int32_t *)((const char *)m.chunk_dev.p + tb)));
+    return SGX_OK;
+}
+
 extern "C" int sgx_map_begin(sgx_engine *e, int32_t shuffle_id, int64_t map_id) {
     if (e) e->mutated();  // invalidates cached reduce-side results (sgx_read_*)
     if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
@@ -772,6 +881,8 @@ extern "C" int sgx_map_begin(sgx_engine *e, int32_t shuffle_id, int64_t map_id) 
     m->exchanged = false;
     m->ready = false;
     m->open = true;
+    m->deferred = false;
+    m->seg_spills = 1;
     m->spills.clear();
     return SGX_OK;
 }
@@ -791,8 +902,23 @@ extern "C" int sgx_map_append(sgx_engine *e, int32_t shuffle_id, int64_t map_id,
     std::lock_guard<std::mutex> lk(m->mu);
     if (!m->open) return fail_msg(SGX_ERR_STATE, "map %lld of shuffle %d is not open (sgx_map_begin)",
                                   (long long)map_id, shuffle_id);
+    if (m->spills.empty()) m->deferred = deferred_ok(e, *s);
     std::unique_ptr<Spill> sp(new Spill());
     sp->nrec = n;
+    if (m->deferred) {  // land the batch; the commit partitions every batch in one pass
+        const int64_t bytes = n * rb;
+        if (mem_kind == SGX_MEM_DEVICE_RETAINED && ((uintptr_t)records & 15) == 0) {
+            sp->src = records;  // read in place at the commit
+        } else if (bytes > 0) {
+            SGX_TRY(sp->data.ensure((size_t)bytes));
+            HIP_TRY(hipMemcpyAsync(sp->data.p, records, (size_t)bytes,
+                                   mem_kind == SGX_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, c->st));
+            HIP_TRY(hipStreamSynchronize(c->st));  // the caller's buffer is free again on return
+            sp->src = sp->data.p;
+        }
+        m->spills.push_back(std::move(sp));
+        return SGX_OK;
+    }
     const void *in = nullptr;
     SGX_TRY(device_input(*c, records, n * rb, mem_kind, &in));
     SGX_TRY(sp->data.ensure((size_t)std::max<int64_t>(n * rb, 16)));
@@ -826,6 +952,15 @@ extern "C" int sgx_map_commit(sgx_engine *e, int32_t shuffle_id, int64_t map_id,
     for (auto &sp : m->spills) total += sp->nrec;
     if (total >= (int64_t)UINT32_MAX)
         return fail_msg(SGX_ERR_INVALID, "map %lld holds %lld records (>= 2^32)", (long long)map_id, (long long)total);
+    if (m->deferred) {
+        SGX_TRY(m->part_off.ensure((size_t)(R + 3) * 4));
+        SGX_TRY(commit_deferred(e, *c, *s, *m, total));
+        if (out_lengths) {  // (finish_lengths frees the batches once the pass is done)
+            SGX_TRY(finish_lengths(e, *c, *s, *m));
+            std::memcpy(out_lengths, m->lengths.data(), sizeof(int64_t) * (size_t)R);
+        }
+        return SGX_OK;
+    }
     // merged partition offsets (records): partition-major, batches in append order
     SGX_TRY(m->part_off.ensure((size_t)(R + 3) * 4));
     uint32_t *po = (uint32_t *)m->part_off.p;

@@ -212,12 +212,21 @@ class ShuffleEngine:
         """Open a streaming map output (batches appended with map_append, merged by map_commit)."""
         check(lib().sgx_map_begin(self.handle, shuffle_id, map_id), "map_begin")
 
-    def map_append(self, shuffle_id: int, map_id: int, records, nrecords: int, record_bytes: int):
+    def map_append(self, shuffle_id: int, map_id: int, records, nrecords: int, record_bytes: int,
+                   offset: int = 0, retained: bool = False):
+        """Append one batch: ``nrecords`` records from byte ``offset`` of ``records``.  A device
+        batch with ``retained`` stays where it is until map_commit returns (the commit reads it
+        in place: SGX_MEM_DEVICE_RETAINED); otherwise the engine copies it before returning."""
         ptr, nbytes, kind = buffer_arg(records)
-        if nrecords * record_bytes > nbytes:
+        if offset < 0 or offset + nrecords * record_bytes > nbytes:
             raise _lib.IllegalArgumentException(
-                f"{nrecords} records of {record_bytes} B exceed the {nbytes} B buffer")
-        check(lib().sgx_map_append(self.handle, shuffle_id, map_id, ptr, nrecords, record_bytes, kind), "map_append")
+                f"{nrecords} records of {record_bytes} B at offset {offset} exceed the {nbytes} B buffer")
+        if retained:
+            if kind != MEM_DEVICE:
+                raise _lib.IllegalArgumentException("only device batches can be retained")
+            kind = _lib.MEM_DEVICE_RETAINED
+        check(lib().sgx_map_append(self.handle, shuffle_id, map_id, ptr + offset, nrecords, record_bytes, kind),
+              "map_append")
 
     def map_commit(self, shuffle_id: int, map_id: int, num_partitions: Optional[int] = None) -> Optional[np.ndarray]:
         out = None

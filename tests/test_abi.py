@@ -26,7 +26,7 @@ def test_every_declared_symbol_is_exported_and_bound(sgx_lib):
         assert hasattr(lib, n), f"{n} declared in include/sgx.h but not exported"
         assert n in sgx_lib._lib.SIGNATURES, f"{n} has no ctypes signature"
     assert set(sgx_lib._lib.SIGNATURES) == set(names)
-    assert lib.sgx_abi_version() == sgx_lib._lib.ABI_VERSION == 6
+    assert lib.sgx_abi_version() == sgx_lib._lib.ABI_VERSION == 7
 
 
 def test_library_is_gfx950_code_object():

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--dist", default="uniform")
     ap.add_argument("--flags", type=int, default=0, help="sgx_config.flags (FLAG_*)")
     ap.add_argument("--record-bytes", type=int, default=16, choices=[16, 100])
+    ap.add_argument("--batches", type=int, default=1, help="> 1: map_begin / append (retained slices) / commit")
     a = ap.parse_args()
     import numpy as np
 
@@ -45,8 +46,16 @@ def main():
         e.register_shuffle(1, a.partitions, kind=sgx.PART_RANGE_BYTES10, bounds=bounds, record_bytes=100)
     else:
         e.register_shuffle(1, a.partitions)
+    cuts = [a.records * j // a.batches for j in range(a.batches + 1)]
     for i in range(a.iters):
-        e.write_map(1, i & 1, buf, a.records, a.record_bytes)
+        if a.batches <= 1:
+            e.write_map(1, i & 1, buf, a.records, a.record_bytes)
+            continue
+        e.map_begin(1, i & 1)
+        for j in range(a.batches):
+            e.map_append(1, i & 1, buf, cuts[j + 1] - cuts[j], a.record_bytes, offset=cuts[j] * a.record_bytes,
+                         retained=True)
+        e.map_commit(1, i & 1)
     e.sync()
     st = e.stats()
     print({k: round(v / max(1, st.count[k]), 4) for k, v in st.ms.items() if st.count[k]})
