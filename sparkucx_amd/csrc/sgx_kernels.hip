@@ -2113,21 +2113,23 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             const uint64_t u0D = cD & ~(uint64_t)15;
             const uint32_t cbD = (uint32_t)(cD - u0D);
             const int32_t od0 = (int32_t)y0 - (int32_t)cbD;
-            uint32_t r = od0 > 0 ? (uint32_t)od0 / (uint32_t)DW : 0u;
-            uint32_t wd = od0 > 0 ? (uint32_t)od0 - r * DW : 0u;
-            uint32_t sbase = (uint32_t)idx[plo + r] * DW;
+            const uint32_t r = od0 > 0 ? (uint32_t)od0 / (uint32_t)DW : 0u;
+            const uint32_t wd = od0 > 0 ? (uint32_t)od0 - r * DW : 0u;
+            // both records the piece can touch, read up front: every LDS read below has its
+            // address without waiting for another (the record after the last is never used:
+            // whole units end inside the stream's records; its index read stays in the tile)
+            const uint32_t sb0 = (uint32_t)idx[plo + r] * DW;
+            const uint32_t sb1 = (uint32_t)idx[min(plo + r + 1u, (uint32_t)TR - 1u)] * DW;
             uint32_t vv[4];
 #pragma unroll
             for (int d = 0; d < 4; ++d) {
-                if (od0 + d < 0) {
-                    vv[d] = carry[cx(p, y0 + d)];
-                } else {
-                    vv[d] = stage[sbase + wd];
-                    if (++wd == (uint32_t)DW && d < 3) {
-                        wd = 0;
-                        sbase = (uint32_t)idx[plo + ++r] * DW;
-                    }
-                }
+                // dword od0 + d: the carry's below 0, else record r (or r + 1 past its end)
+                const int32_t od = od0 + d;
+                const uint32_t w = (od0 > 0 ? wd : 0u) + (uint32_t)(od0 > 0 ? d : (od > 0 ? od : 0));
+                const uint32_t sa = w < (uint32_t)DW ? sb0 + w : sb1 + w - DW;
+                // (both reads stay in bounds, so either may be speculated: od < 0 only within the
+                // carry's first 15 dwords)
+                vv[d] = od < 0 ? carry[cx(p, (y0 + d) & 15u)] : stage[sa];
             }
             const uint64_t bD = u0D + y0;
             const uint64_t startD = (uint64_t)carry[cx(p, 15)] * DW, capD = (uint64_t)olim * DW;

@@ -21,6 +21,9 @@ for i in 1 2; do
 done
 timeout -k 10 300 python -u bench.py --batches 64 --no-cpu-baseline > "$out/bench_batches64.log" 2>&1 || fail "bench batches" "$out/bench_batches64.log"
 timeout -k 10 300 python -u bench.py --no-cpu-baseline > "$out/bench.log" 2>&1 || fail "bench" "$out/bench.log"
+for g in 512 1024; do
+  timeout -k 10 300 python -u bench.py --no-cpu-baseline --no-live-pmc --num-chunks $g > "$out/bench_g$g.log" 2>&1 || fail "bench g$g" "$out/bench_g$g.log"
+done
 python3 - "$out" <<'PY'
 import glob, json, sys
 for f in sorted(glob.glob(sys.argv[1] + "/*.log")):
@@ -31,6 +34,10 @@ for f in sorted(glob.glob(sys.argv[1] + "/*.log")):
     print(f.split("/")[-1], d["value"], d["ms_per_step"], d["roofline"]["frac"], d["roofline_map_side"]["frac"],
           d["roofline_map_side"]["traffic_over_algorithmic"], d["stages_ms_per_step"])
 PY
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$out/rec_c1" -o run -- \
+  python3 tools/prof_map.py --iters 8 --per-launch > "$out/rec_c1.log" 2>&1 || fail "reconcile c1" "$out/rec_c1.log"
+python3 tools/reconcile_trace.py "$out/rec_c1/run_kernel_trace.csv" "$out/rec_c1.log" > "$out/reconcile_c1.jsonl" || true
+tail -1 "$out/reconcile_c1.jsonl"
 bash tools/gpu_prof.sh $tag/prof_ts --record-bytes 100 --records 42949672 || exit 1
 bash tools/sq_counters.sh "$out/sq_ts" --record-bytes 100 --records 42949672 --iters 2 || exit 1
 echo done > "$out/DONE"

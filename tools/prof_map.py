@@ -21,6 +21,8 @@ def main():
     ap.add_argument("--flags", type=int, default=0, help="sgx_config.flags (FLAG_*)")
     ap.add_argument("--record-bytes", type=int, default=16, choices=[16, 100])
     ap.add_argument("--batches", type=int, default=1, help="> 1: map_begin / append (retained slices) / commit")
+    ap.add_argument("--per-launch", action="store_true",
+                    help="print every write's stage events (PER_LAUNCH json), each write alone on the GPU")
     a = ap.parse_args()
     import numpy as np
 
@@ -47,16 +49,29 @@ def main():
     else:
         e.register_shuffle(1, a.partitions)
     cuts = [a.records * j // a.batches for j in range(a.batches + 1)]
+    import json
+
+    per = []  # this launch's stage events (ms), for tools/reconcile_trace.py
     for i in range(a.iters):
+        if a.per_launch:
+            e.sync()
+            e.stats_reset()
         if a.batches <= 1:
             e.write_map(1, i & 1, buf, a.records, a.record_bytes)
-            continue
-        e.map_begin(1, i & 1)
-        for j in range(a.batches):
+        else:
+            e.map_begin(1, i & 1)
+        for j in range(a.batches if a.batches > 1 else 0):
             e.map_append(1, i & 1, buf, cuts[j + 1] - cuts[j], a.record_bytes, offset=cuts[j] * a.record_bytes,
                          retained=True)
-        e.map_commit(1, i & 1)
+        if a.batches > 1:
+            e.map_commit(1, i & 1)
+        if a.per_launch:
+            e.sync()
+            st = e.stats()
+            per.append({k: round(v, 4) for k, v in st.ms.items() if st.count[k]})
     e.sync()
+    if a.per_launch:
+        print("PER_LAUNCH " + json.dumps(per))
     st = e.stats()
     print({k: round(v / max(1, st.count[k]), 4) for k, v in st.ms.items() if st.count[k]})
     e.close()
