@@ -414,9 +414,11 @@ int group_records(sgx_engine *e, Ctx &c, const void *sorted, int64_t n, int32_t 
 // Stable sort of n 16 B / 100 B records in c.sort_buf[0] by key, then by the shuffle's
 // partitioner (when `by_partition`): *sorted = the buffer holding the result.
 // nparts: partitions present in the records (a read's reducer range; 0 = all R), which sizes
-// the bucket path's key window.
+// the bucket path's key window.  final_dst (device, n records, 16 B-aligned, not a sort buffer):
+// the bucket path's last pass writes there directly -- *sorted == final_dst tells the caller
+// no copy is left to do.
 int sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool by_partition, const void **sorted,
-                 int32_t nparts = 0);
+                 int32_t nparts = 0, void *final_dst = nullptr);
 // LZ4 framing / unframing on the context's stream (sgx_lz4_host.cpp).
 int lz4_frame_impl(sgx_engine *e, Ctx &c, const void *stream_dev, const int64_t *part_offsets, int32_t R,
                    int32_t block_size, DevBuf *alloc_dst, void *dst_dev, int64_t dst_cap, int64_t *out_lengths);

@@ -2602,6 +2602,10 @@ hipError_t launch_seg_offsets(const uint32_t *cnt, const int64_t *seg_base, cons
 // of the 7-9 LSD digit passes that remain below the window.
 // ------------------------------------------------------------------------------------
 constexpr int BS_THREADS = 512;
+// sub-bins inside each bucket before the rank (A/B: -DSGX_BS_SUBBIN=0, the whole-bucket rank)
+#ifndef SGX_BS_SUBBIN
+#define SGX_BS_SUBBIN 1
+#endif
 #ifndef BS_UNROLL
 #define BS_UNROLL 8  // keys compared per step of the rank loop (independent LDS loads; 8 vs 4: sorted 1 GiB 3.67 -> 3.62 ms, profiles/r03_bucket_unroll_ab.jsonl)
 #endif
@@ -2633,7 +2637,8 @@ __global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__re
     uint16_t *bs = (uint16_t *)(klo + (LO ? CAP : 0));            // bucket start of each local position
     uint16_t *be = bs + CAP;                                      // bucket end
     uint16_t *inv = be + CAP;                                     // output slot -> local position
-    uint8_t *flag = (uint8_t *)(inv + CAP);                       // a bucket starts here
+    uint16_t *cnt = inv + CAP;                                    // sub-bin counts (SGX_BS_SUBBIN)
+    uint8_t *flag = (uint8_t *)(cnt + (SGX_BS_SUBBIN ? CAP : 0)); // a bucket starts here
     __shared__ uint32_t s_a, s_b, s_scr[BS_THREADS / 64];
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const int64_t t0 = (int64_t)blockIdx.x * TILE;
@@ -2643,6 +2648,8 @@ __global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__re
     const int m = (int)(L1 - L0);
     const uint64_t wmask = kbits >= 64 ? ~0ull : ((1ull << kbits) - 1ull);
     for (int u = (int)tid; u < m * DW; u += BS_THREADS) rec[u] = in[L0 * DW + u];
+    if constexpr (SGX_BS_SUBBIN)
+        for (int j = (int)tid; j < m; j += BS_THREADS) cnt[j] = 0;
     if (tid == 0) {
         s_a = 0xFFFFFFFFu;
         s_b = 0xFFFFFFFFu;
@@ -2725,6 +2732,89 @@ __global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__re
         }
     }
     __syncthreads();
+#if SGX_BS_SUBBIN
+    // Sub-bins (round 5): a bucket [s0, e0) of m records owns the m positions s0 .. e0 - 1 as
+    // bins, and record j goes to bin s0 + floor(x_j * m / 2^32), x_j = the 32 key bits right
+    // below the window -- monotone in the key, so equal keys share a bin and every key of a
+    // lower bin is smaller.  Bins are counted, scanned over [a, b) into output slots, their
+    // members listed, and a record is ranked among its bin's members only (about two on
+    // uniform keys) instead of among its whole bucket (~64): the rank loop was the kernel's
+    // VALU time.  Stable: equal keys rank by position.
+    {
+        constexpr int PER = (CAP + BS_THREADS - 1) / BS_THREADS;
+        const uint32_t kl_sh = kshift;  // the window's low bit
+        // S1: bins (kept in be[j] from here on), counts
+        for (int j = (int)a + (int)tid; j < (int)b; j += BS_THREADS) {
+            const uint32_t s0 = bs[j], mm = (uint32_t)be[j] - s0;
+            const uint64_t kh = khi[j];
+            const uint64_t below = kl_sh == 0 ? 0ull : (kl_sh >= 32 ? (kh >> (kl_sh - 32)) : (kh << (32 - kl_sh)));
+            const uint32_t x = (uint32_t)below;
+            const uint32_t bin = s0 + (uint32_t)(((uint64_t)x * mm) >> 32);
+            be[j] = (uint16_t)bin;
+            atomicAdd((uint32_t *)((uintptr_t)(cnt + (bin & ~1u))), 1u << ((bin & 1u) << 4));
+        }
+        __syncthreads();
+        // S2: exclusive scan of the counts over [a, b) -> bs[bin] = the bin's first output slot
+        // (relative to a); one contiguous run of positions per thread
+        {
+            const int lenb = (int)(b - a);
+            const int per = (lenb + BS_THREADS - 1) / BS_THREADS;
+            const int q0 = (int)a + min(lenb, (int)tid * per), q1 = (int)a + min(lenb, ((int)tid + 1) * per);
+            uint32_t sum = 0;
+            for (int q = q0; q < q1; ++q) sum += cnt[q];
+            const uint32_t x = wave_inclusive_scan(sum, lane);
+            if (lane == 63) s_scr[w] = x;
+            __syncthreads();
+            uint32_t base = x - sum;
+            for (uint32_t v = 0; v < w; ++v) base += s_scr[v];
+            for (int q = q0; q < q1; ++q) {
+                bs[q] = (uint16_t)base;
+                base += cnt[q];
+            }
+        }
+        __syncthreads();
+        // S3: list every bin's members in its slots (inv[a + slot], any order: the count runs
+        // down)
+        for (int j = (int)a + (int)tid; j < (int)b; j += BS_THREADS) {
+            const uint32_t bin = be[j];
+            const uint32_t sh = (bin & 1u) << 4;
+            const uint32_t old = atomicSub((uint32_t *)((uintptr_t)(cnt + (bin & ~1u))), 1u << sh);
+            const uint32_t k = ((old >> sh) & 0xFFFFu) - 1u;
+            inv[a + bs[bin] + k] = (uint16_t)j;
+        }
+        __syncthreads();
+        // S4: rank among the bin's members (key, then position), slot kept in registers until
+        // every member list has been read, then written over be[] as the output permutation
+        int myslot[PER], myj[PER];
+#pragma unroll
+        for (int t = 0; t < PER; ++t) {
+            const int j = (int)a + (int)tid + t * BS_THREADS;
+            myj[t] = -1;
+            if (j >= (int)b) continue;
+            const uint32_t bin = be[j];
+            const uint32_t st0 = bs[bin], st1 = bin + 1 < b ? bs[bin + 1] : (uint32_t)(b - a);
+            const uint64_t kh = khi[j];
+            const uint32_t kl = LO ? klo[j] : 0u;
+            uint32_t rank = 0;
+            for (uint32_t u = st0; u < st1; ++u) {
+                const int i = inv[a + u];
+                const uint64_t h = khi[i];
+                const uint32_t l = LO ? klo[i] : 0u;
+                const bool lt = LO ? (h < kh || (h == kh && l < kl)) : h < kh;
+                const bool eq = LO ? (h == kh && l == kl) : h == kh;
+                rank += (lt || (i < j && eq)) ? 1u : 0u;
+            }
+            myslot[t] = (int)(a + st0 + rank);
+            myj[t] = j;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < PER; ++t)
+            if (myj[t] >= 0) be[myslot[t]] = (uint16_t)myj[t];
+        __syncthreads();
+    }
+    const uint16_t *perm = be;
+#else
     // stable rank inside the bucket: keys below, plus equal keys at earlier positions.  Keys
     // come from the compact key array four at a time (independent LDS loads, one wait).
     for (int j = (int)a + (int)tid; j < (int)b; j += BS_THREADS) {
@@ -2757,14 +2847,16 @@ __global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__re
         inv[s0 + rank] = (uint16_t)j;
     }
     __syncthreads();
-    // the bucket region, coalesced: output position L0 + p takes local record inv[p]
+    const uint16_t *perm = inv;
+#endif
+    // the bucket region, coalesced: output position L0 + p takes local record perm[p]
     if constexpr (RB == 16) {
         for (int p = (int)a + (int)tid; p < (int)b; p += BS_THREADS)
-            ((u32x4 *)out)[L0 + p] = ((const u32x4 *)rec)[inv[p]];
+            ((u32x4 *)out)[L0 + p] = ((const u32x4 *)rec)[perm[p]];
     } else {
         for (int u = (int)tid; u < len * DW; u += BS_THREADS) {
             const int p = (int)a + u / DW, q = u % DW;
-            out[(L0 + p) * DW + q] = rec[(size_t)inv[p] * DW + q];
+            out[(L0 + p) * DW + q] = rec[(size_t)perm[p] * DW + q];
         }
     }
 }
@@ -2772,14 +2864,16 @@ __global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__re
 template <int RB, int TILE, int HALO>
 static size_t bucket_sort_lds() {
     constexpr int CAP = TILE + HALO + 1;
-    return (size_t)CAP * RB + (size_t)CAP * 8 + (RB != 16 ? (size_t)CAP * 4 : 0) + (size_t)CAP * 6 + (size_t)CAP + 16;
+    return (size_t)CAP * RB + (size_t)CAP * 8 + (RB != 16 ? (size_t)CAP * 4 : 0) + (size_t)CAP * (SGX_BS_SUBBIN ? 8 : 6) +
+           (size_t)CAP + 16;
 }
 
 hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, const PartParams &pp, int use_p,
                               uint32_t kshift, uint32_t kbits, uint32_t *err, hipStream_t stream) {
     if (n <= 0) return hipSuccess;
     if (rb == 16) {
-        constexpr int T = 2048, H = 511;  // CAP = 2560: the key array stays 8-byte aligned
+        // CAP = 2560 (sub-bins: 2304, two workgroups per CU): the key array stays 8-byte aligned
+        constexpr int T = 2048, H = SGX_BS_SUBBIN ? 255 : 511;
         const size_t lds = bucket_sort_lds<16, T, H>();
         (void)hipFuncSetAttribute((const void *)k_bucket_sort<16, T, H>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);

@@ -299,7 +299,7 @@ static int records_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_id
 // of the keys histograms every digit; a digit with a single non-empty bucket is the identity
 // permutation and is skipped (unless SGX_FLAG_SORT_ALL_DIGITS).
 int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool by_partition, const void **sorted,
-                      int32_t nparts) {
+                      int32_t nparts, void *final_dst) {
     const int rb = s.rb;
     if (rb != 16 && rb != 100)
         return fail_msg(SGX_ERR_UNSUPPORTED, "sorted read needs 16 B (Long, Long) or 100 B TeraSort records, not %d B",
@@ -461,7 +461,10 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
                 cur ^= 1;
                 ++np;
             }
-            HIP_TRY(launch_bucket_sort(c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, rb, s.pp, use_p ? 1 : 0,
+            // the last pass straight into the caller's device buffer when it has one (a sorted read
+            // into HBM: no copy of the result afterwards)
+            void *bout = final_dst ? final_dst : c.sort_buf[cur ^ 1].p;
+            HIP_TRY(launch_bucket_sort(c.sort_buf[cur].p, bout, n, rb, s.pp, use_p ? 1 : 0,
                                        (uint32_t)lo, (uint32_t)kbits, errs + np, st));
             SGX_TRY(debug_sync(e, st, "bucket sort"));
             ++np;
@@ -475,7 +478,7 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
             if (!(herr[np - 1] & 4u)) {
                 HIP_TRY(hipEventRecord(t1, st));
                 e->record_stage(SGX_STAGE_SORT, t0, t1);
-                *sorted = c.sort_buf[cur ^ 1].p;
+                *sorted = bout;
                 return SGX_OK;
             }
             // a bucket too long for the chip: the digit passes below finish from the bucket
@@ -653,14 +656,20 @@ extern "C" int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t 
         sorted = c->rc.sorted;
     } else {
         SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
-        SGX_TRY(sort_records(e, *c, *s, n, true, &sorted, end_partition - start_partition));
+        if (n * rb > dst_cap)
+            return fail_msg(SGX_ERR_INVALID, "destination capacity %lld < %lld bytes", (long long)dst_cap,
+                            (long long)(n * rb));
+        // a device destination takes the sort's last pass directly
+        const bool direct = dst && dst_mem_kind == SGX_MEM_DEVICE && ((uintptr_t)dst & 15) == 0 &&
+                            dst != c->sort_buf[0].p && dst != c->sort_buf[1].p;
+        SGX_TRY(sort_records(e, *c, *s, n, true, &sorted, end_partition - start_partition, direct ? dst : nullptr));
     }
     *out_bytes = n * rb;
     if (n * rb > dst_cap)
         return fail_msg(SGX_ERR_INVALID, "destination capacity %lld < %lld bytes", (long long)dst_cap,
                         (long long)(n * rb));
     if (n > 0 && !dst) return fail_msg(SGX_ERR_INVALID, "dst is NULL");
-    SGX_TRY(copy_out(*c, dst, sorted, n * rb, dst_mem_kind));
+    if (sorted != dst) SGX_TRY(copy_out(*c, dst, sorted, n * rb, dst_mem_kind));
     HIP_TRY(hipStreamSynchronize(c->st));
     return SGX_OK;
 }

@@ -267,11 +267,20 @@ __global__ __launch_bounds__(RT) void k_digit_hist(const uint8_t *__restrict__ r
         w[0] = *(const uint32_t *)r;
         w[1] = *(const uint32_t *)(r + 4);
         w[2] = ND > 8 ? *(const uint32_t *)(r + 8) : 0u;
+        const uint64_t act = __ballot(1);
 #pragma unroll
         for (int d = 0; d < ND; ++d) {
             uint32_t b = (w[d >> 2] >> ((d & 3) * 8)) & 0xFFu;
             if (RB == 16 && d == 7) b ^= 0x80u;
-            atomicAdd(&h[d * 256 + b], 1u);
+            // a byte the whole wave shares (the high bytes of small keys: Zipf ranks < 2^24 leave
+            // five of eight constant) is one atomic of the wave's count, not 64 on one counter
+            const uint32_t b0 = __builtin_amdgcn_readfirstlane(b);
+            if (__ballot(b == b0) == act) {
+                if ((uint64_t)__lane_id() == (uint64_t)(__ffsll((unsigned long long)act) - 1))
+                    atomicAdd(&h[d * 256 + b0], (uint32_t)__popcll(act));
+            } else {
+                atomicAdd(&h[d * 256 + b], 1u);
+            }
         }
     }
     __syncthreads();
