@@ -29,7 +29,8 @@ Ctx *sgx_engine::ctx() {
     auto &slot = ctxs[std::this_thread::get_id()];
     if (!slot) {
         std::unique_ptr<Ctx> c(new Ctx());
-        if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
+        if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
+            hipStreamCreateWithFlags(&c->st_tail, hipStreamNonBlocking) != hipSuccess) {
             ctxs.erase(std::this_thread::get_id());
             fail_msg(SGX_ERR_HIP, "hipStreamCreate failed for a new calling thread");
             return nullptr;
@@ -433,7 +434,10 @@ extern "C" int sgx_progress(sgx_engine *e) {
     std::vector<hipStream_t> streams;
     {
         std::lock_guard<std::mutex> lk(e->reg_mu);
-        for (auto &kv : e->ctxs) streams.push_back(kv.second->st);
+        for (auto &kv : e->ctxs) {
+            streams.push_back(kv.second->st);
+            streams.push_back(kv.second->st_tail);
+        }
     }
     streams.push_back(e->s_comm);
     bool done = true;
@@ -455,7 +459,10 @@ extern "C" int sgx_sync(sgx_engine *e) {
     std::vector<std::shared_ptr<Shuffle>> all;
     {
         std::lock_guard<std::mutex> lk(e->reg_mu);
-        for (auto &kv : e->ctxs) streams.push_back(kv.second->st);
+        for (auto &kv : e->ctxs) {
+            streams.push_back(kv.second->st);
+            streams.push_back(kv.second->st_tail);
+        }
         for (auto &kv : e->shuffles) all.push_back(kv.second);
     }
     for (hipStream_t st : streams) HIP_TRY(hipStreamSynchronize(st));

@@ -287,6 +287,14 @@ struct Ctx {
     DevBuf split_work, split_tmp;  // R > 1024: the two-level split scatter's scratch and level-1 output
     DevBuf input_stage;
     const uint32_t *last_off_dev = nullptr;  // device (R+1) record offsets of the last partition pass
+    // The padded write's tail (its scan, the guarded two-pass fallback, the offsets' copy to the
+    // host) runs on a second stream so that the next write's kernels do not queue behind it;
+    // its work block and offsets alternate between two slots, a slot reused only once the tail
+    // that last read it has run (pad_done)
+    hipStream_t st_tail = nullptr;
+    DevBuf pad_work[2], pad_offs[2];
+    Event pad_done[2];
+    int pad_slot = 0, tail_slot = -1;
     // reduce side and map-side combine
     DevBuf kryo_in, kryo_work, sort_buf[2], sort_err, grp_status, grp_out;
     DevBuf digit_hist, items_dev, gather_stage, fetch_tmp, comb_buf;
@@ -306,6 +314,10 @@ struct Ctx {
         if (st) {
             (void)hipStreamSynchronize(st);
             (void)hipStreamDestroy(st);
+        }
+        if (st_tail) {
+            (void)hipStreamSynchronize(st_tail);
+            (void)hipStreamDestroy(st_tail);
         }
     }
 };

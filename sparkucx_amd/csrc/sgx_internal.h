@@ -251,6 +251,10 @@ hipError_t launch_digit_hist(const void *rec, int64_t n, int rb, uint32_t *hist,
 // s = [pk[s], pk[s+1]); cnt[k * Q + q] = piece k's records in bucket q (KIND_KEY_BITS or
 // KIND_DIGIT, Q = pp.R <= 1024); offs = per-segment exclusive scan, bucket-major,
 // piece-minor, from seg_base[s] -- K4's SEG mode then runs with G = 1.
+// The window histogram of every piece (KIND_KEY_BITS) and the 8 digit histograms of 16 B records
+// in one pass (dhist zeroed here).
+hipError_t launch_piece_digit_hist(const void *in, int64_t n, const int64_t *desc, int64_t npieces,
+                                   const PartParams &pp, uint32_t *cnt, uint32_t *dhist, hipStream_t st);
 hipError_t launch_piece_hist(const void *in, int64_t n, const int64_t *desc, int64_t npieces, const PartParams &pp,
                              uint32_t *cnt, hipStream_t st);
 hipError_t launch_seg_offsets(const uint32_t *cnt, const int64_t *seg_base, const int32_t *pk, int64_t nseg, uint32_t Q,

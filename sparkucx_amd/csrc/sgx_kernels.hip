@@ -2540,6 +2540,73 @@ __global__ __launch_bounds__(PH_THREADS) void k_piece_hist(const u32x4 *__restri
     for (uint32_t q = tid; q < Q; q += PH_THREADS) cnt[k * Q + q] = h[q];
 }
 
+// A sorted read's first look at its keys in ONE pass (round 5): every piece's window histogram
+// for the window the bucket path takes when the keys' top byte varies (the common case: the
+// caller checks that guess against the digit histograms and recounts if it was wrong) plus the
+// eight digit histograms the skip / window decisions need (k_digit_hist's, with its
+// wave-uniform shortcut).  16 B records, KIND_KEY_BITS.
+__global__ __launch_bounds__(PH_THREADS) void k_piece_digit_hist(const u32x4 *__restrict__ in, int64_t n,
+                                                                 const int64_t *__restrict__ desc, int64_t npieces,
+                                                                 PartParams pp, uint32_t *__restrict__ cnt,
+                                                                 uint32_t *__restrict__ dhist) {
+    __shared__ uint32_t h[1024];
+    __shared__ uint32_t dh[8 * 256];
+    const uint32_t Q = pp.R, tid = threadIdx.x, lane = tid & 63u;
+    for (uint32_t i = tid; i < Q; i += PH_THREADS) h[i] = 0;
+    for (uint32_t i = tid; i < 8 * 256; i += PH_THREADS) dh[i] = 0;
+    __syncthreads();
+    const int64_t k = blockIdx.x;
+    const int64_t b = desc[4 * k], e = k + 1 < npieces ? desc[4 * (k + 1)] : n;
+    auto count = [&](const u32x4 &r) __attribute__((always_inline)) {
+        const uint64_t act = __ballot(1);
+        const uint32_t first = (uint32_t)__ffsll((unsigned long long)act) - 1u;
+        // (the guessed window of skewed keys -- small keys share their top bits -- is one bin
+        // for the whole wave: one atomic, as for the constant digits below)
+        const uint32_t q = pid_of<KIND_KEY_BITS>(r.x, r.y, r.z, pp);
+        const uint32_t q0 = __builtin_amdgcn_readfirstlane(q);
+        if (__ballot(q == q0) == act) {
+            if (lane == first) atomicAdd(&h[q0], (uint32_t)__popcll(act));
+        } else {
+            atomicAdd(&h[q], 1u);
+        }
+#pragma unroll
+        for (int d = 0; d < 8; ++d) {
+            uint32_t v = ((d < 4 ? r.x : r.y) >> ((d & 3) * 8)) & 0xFFu;
+            if (d == 7) v ^= 0x80u;
+            const uint32_t v0 = __builtin_amdgcn_readfirstlane(v);
+            if (__ballot(v == v0) == act) {
+                if (lane == first) atomicAdd(&dh[d * 256 + v0], (uint32_t)__popcll(act));
+            } else {
+                atomicAdd(&dh[d * 256 + v], 1u);
+            }
+        }
+    };
+    constexpr int U = 4;  // loads in flight per thread
+    int64_t i = b + tid;
+    for (; i + (U - 1) * PH_THREADS < e; i += U * PH_THREADS) {
+        u32x4 r[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[u] = in[i + u * PH_THREADS];
+#pragma unroll
+        for (int u = 0; u < U; ++u) count(r[u]);
+    }
+    for (; i < e; i += PH_THREADS) count(in[i]);
+    __syncthreads();
+    for (uint32_t q = tid; q < Q; q += PH_THREADS) cnt[k * Q + q] = h[q];
+    for (uint32_t j = tid; j < 8 * 256; j += PH_THREADS)
+        if (dh[j]) atomicAdd(&dhist[j], dh[j]);
+}
+
+hipError_t launch_piece_digit_hist(const void *in, int64_t n, const int64_t *desc, int64_t npieces,
+                                   const PartParams &pp, uint32_t *cnt, uint32_t *dhist, hipStream_t st) {
+    hipError_t err = hipMemsetAsync(dhist, 0, 8 * 256 * 4, st);
+    if (err != hipSuccess || npieces <= 0) return err;
+    if (pp.R > 1024 || pp.kind != KIND_KEY_BITS) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_piece_digit_hist, dim3((unsigned)npieces), dim3(PH_THREADS), 0, st, (const u32x4 *)in, n, desc,
+                       npieces, pp, cnt, dhist);
+    return hipGetLastError();
+}
+
 hipError_t launch_piece_hist(const void *in, int64_t n, const int64_t *desc, int64_t npieces, const PartParams &pp,
                              uint32_t *cnt, hipStream_t st) {
     if (npieces <= 0) return hipSuccess;

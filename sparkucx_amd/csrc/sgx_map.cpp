@@ -423,10 +423,14 @@ static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void 
     const int64_t len = (int64_t)R * G, tiles = scan_tiles(len);
     const uint32_t olim = (uint32_t)pg.olim;
     const int rb = s.rb;
+    // this write's work slot: the tail that last read it (two writes ago) must have run
+    const int slot = c.pad_slot;
+    c.pad_slot ^= 1;
+    if (c.pad_done[slot].ev) HIP_TRY(hipStreamWaitEvent(st, c.pad_done[slot].ev, 0));
     SGX_TRY(m.data.ensure((size_t)olim * (size_t)rb));
     SGX_TRY(m.frag.ensure((size_t)len * 12 + 16));
     uint32_t *fstart = (uint32_t *)m.frag.p, *foff = fstart + len, *cnt = foff + len;
-    SGX_TRY(c.offs.ensure((size_t)len * 4));
+    SGX_TRY(c.pad_offs[slot].ensure((size_t)len * 4));
     // one work block, one memset: [fallback counts R*G][fallback ticket | status]
     // [offsets R+1 | error | padded flags][padded scan ticket | status][est R][pcap R]
     const size_t counts_bytes = ((size_t)len * 4 + 15) & ~(size_t)15;
@@ -434,8 +438,8 @@ static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void 
     const size_t off_bytes = ((size_t)(R + 3) * 4 + 15) & ~(size_t)15;
     const size_t rbytes = ((size_t)R * 4 + 15) & ~(size_t)15;
     const size_t work_bytes = counts_bytes + 2 * status_bytes + off_bytes + 2 * rbytes;
-    SGX_TRY(c.work.ensure(work_bytes));
-    char *w = (char *)c.work.p;
+    SGX_TRY(c.pad_work[slot].ensure(work_bytes));
+    char *w = (char *)c.pad_work[slot].p;
     uint32_t *counts_fb = (uint32_t *)w;
     uint32_t *ticket_fb = (uint32_t *)(w + counts_bytes);
     uint64_t *status_fb = (uint64_t *)((char *)ticket_fb + 16);
@@ -445,8 +449,9 @@ static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void 
     uint64_t *status_pad = (uint64_t *)((char *)ticket_pad + 16);
     uint32_t *est = (uint32_t *)((char *)ticket_pad + status_bytes);
     uint32_t *pcap = (uint32_t *)((char *)est + rbytes);
+    uint32_t *offs_fb = (uint32_t *)c.pad_offs[slot].p;
     c.last_off_dev = part_off_dev;
-    HIP_TRY(hipMemsetAsync(c.work.p, 0, work_bytes, st));
+    HIP_TRY(hipMemsetAsync(w, 0, work_bytes, st));
     hipEvent_t h0 = e->ev(), h1 = e->ev(), c1 = e->ev(), x1 = e->ev();
     HIP_TRY(hipEventRecord(h0, st));
     PartParams bp = s.pp;  // the shuffle's partitioner over this map's input (chunk table or not)
@@ -463,18 +468,22 @@ static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void 
     HIP_TRY(launch_scatter(in, m.data.p, n, rb, pg.chunk, G, kp, fstart, pg.geo, err_pad, st));
     SGX_TRY(debug_sync(e, st, "K4 padded scatter"));
     HIP_TRY(hipEventRecord(c1, st));
-    HIP_TRY(launch_scan(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, st));
-    // the two-pass fallback, each kernel a no-op unless *err_pad has PAD_OVERFLOW
+    // the tail on the second stream, behind K4: K3 over the counts, then the two-pass
+    // fallback, each kernel a no-op unless *err_pad has PAD_OVERFLOW, and the offsets to the host
+    hipStream_t tl = c.st_tail;
+    HIP_TRY(hipStreamWaitEvent(tl, c1, 0));
+    HIP_TRY(launch_scan(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, tl));
     PartParams fp = bp;
     fp.guard = err_pad;
-    HIP_TRY(launch_hist(in, n, rb, pg.chunk, G, fp, counts_fb, st, e->hist_mode, true));
-    HIP_TRY(launch_scan(counts_fb, (uint32_t *)c.offs.p, len, status_fb, ticket_fb, err, part_off_dev, G, R, st,
-                        err_pad));
+    HIP_TRY(launch_hist(in, n, rb, pg.chunk, G, fp, counts_fb, tl, e->hist_mode, true));
+    HIP_TRY(launch_scan(counts_fb, offs_fb, len, status_fb, ticket_fb, err, part_off_dev, G, R, tl, err_pad));
     fp.mbits = (uint32_t)pg.geo.mbits;
-    HIP_TRY(launch_scatter(in, m.data.p, n, rb, pg.chunk, G, fp, (const uint32_t *)c.offs.p, pg.geo, err, st));
-    SGX_TRY(debug_sync(e, st, "padded scan / fallback"));
-    HIP_TRY(hipEventRecord(x1, st));
-    HIP_TRY(hipMemcpyAsync(m.part_off.p, part_off_dev, (size_t)(R + 3) * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(launch_scatter(in, m.data.p, n, rb, pg.chunk, G, fp, offs_fb, pg.geo, err, tl));
+    SGX_TRY(debug_sync(e, tl, "padded scan / fallback"));
+    HIP_TRY(hipEventRecord(x1, tl));
+    HIP_TRY(hipMemcpyAsync(m.part_off.p, part_off_dev, (size_t)(R + 3) * 4, hipMemcpyDeviceToHost, tl));
+    HIP_TRY(c.pad_done[slot].record(tl));
+    c.tail_slot = slot;
     // stages: the sampled histogram stands where K1+K2 do, the scans (and the no-op fallback
     // launches) where K3 does
     e->record_stage(SGX_STAGE_HIST, h0, h1);
@@ -596,6 +605,7 @@ static int run_map_pipeline(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const 
     m.comp_valid = false;
     m.pad_try = m.padded = m.rec_padded = m.dense_valid = false;
     const uint32_t *rec_off_dev = part_dev;
+    int tail = -1;  // the padded write left its tail on c.st_tail (this slot's pad_done)
     PadGeom pg;
     if (!partitioned && !no_pad && use_padded(e, s, in, n)) pg = pad_geom(e, s, n, ct);
     if (s.combine == SGX_AGG_SUM) {
@@ -603,8 +613,12 @@ static int run_map_pipeline(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const 
         rec_off_dev = c.last_off_dev;
     } else if (!partitioned && pg.olim >= n) {
         m.nrec = n;
-        if (s.rb == 16 && s.R > 1024 && !ct) SGX_TRY(padded_split_pass(e, c, s, m, in, n, pg));
-        else SGX_TRY(padded_pass(e, c, s, m, in, n, pg, ct));
+        if (s.rb == 16 && s.R > 1024 && !ct) {
+            SGX_TRY(padded_split_pass(e, c, s, m, in, n, pg));
+        } else {
+            SGX_TRY(padded_pass(e, c, s, m, in, n, pg, ct));
+            tail = c.tail_slot;
+        }
         rec_off_dev = c.last_off_dev;
     } else if (!partitioned) {
         m.nrec = n;
@@ -618,13 +632,18 @@ static int run_map_pipeline(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const 
                                           m.seg_spills, g0_dev, (uint32_t *)m.seg_off.p, c.st));
         }
     }
+    if (s.ser == SGX_SER_KRYO && tail >= 0) {  // the serializer reads the tail's final bytes / offsets
+        HIP_TRY(hipStreamWaitEvent(c.st, c.pad_done[tail].ev, 0));
+        tail = -1;
+    }
     if (s.ser == SGX_SER_KRYO) {
         if (m.seg_spills > 1)  // (partition, spill) segments, SGX_WRITER_UNSAFE
             SGX_TRY(serialize_kryo(e, c, s, m, (const uint32_t *)m.seg_off.p, s.R * m.seg_spills));
         else
             SGX_TRY(serialize_kryo(e, c, s, m, rec_off_dev, s.R, m.pad_try));
     }
-    HIP_TRY(m.done.record(c.st));
+    // the map is complete behind its last kernel: the tail's, when nothing followed it
+    HIP_TRY(m.done.record(tail >= 0 ? c.st_tail : c.st));
     m.written = true;
     return SGX_OK;
 }

@@ -315,10 +315,6 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
     HIP_TRY(hipEventRecord(t0, st));
     const int ndig = rb == 16 ? 8 : 10;
     SGX_TRY(c.digit_hist.ensure((size_t)ndig * 256 * 4));
-    HIP_TRY(launch_digit_hist(c.sort_buf[0].p, n, rb, (uint32_t *)c.digit_hist.p, e->num_cus, st));
-    std::vector<uint32_t> dh((size_t)ndig * 256);
-    HIP_TRY(hipMemcpyAsync(dh.data(), c.digit_hist.p, dh.size() * 4, hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
     const bool skip = !(e->flags & SGX_FLAG_SORT_ALL_DIGITS);
     int cur = 0, np = 0;
     const bool range_asc = s.kind != SGX_PART_HASH && s.asc;
@@ -391,6 +387,33 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
         seg_planned = true;
         return SGX_OK;
     };
+    // The keys' first read: the digit histograms (which bytes vary, skew), and -- when the
+    // segmented bucket path is possible -- in the same pass every piece's histogram of the
+    // window that path takes if the keys' top byte varies (k_piece_digit_hist); the window pass
+    // below uses those counts when the guess holds instead of counting again.
+    const double rp = use_p ? (double)(nparts > 0 ? std::min(nparts, s.R) : s.R) : 1.0;
+    int kbits0 = 0;  // the window width the bucket path takes (before the top byte's cap)
+    while (kbits0 < 30 && (double)n / (rp * (double)(1ull << kbits0)) > 64.0) ++kbits0;
+    PartParams spec{};
+    bool spec_counted = false;
+    if (seg_ok && skip && !(e->flags & SGX_FLAG_NO_BUCKET_SORT) && s.kind == SGX_PART_HASH && kbits0 >= 1 &&
+        kbits0 <= 10) {
+        SGX_TRY(seg_plan());
+        if (seg_npieces > 0) {
+            spec.kind = KIND_KEY_BITS;
+            spec.R = 1u << kbits0;
+            spec.nbits = (uint32_t)kbits0;
+            spec.dshift = (uint32_t)(64 - kbits0);
+            spec.dflip = 1u;
+            HIP_TRY(launch_piece_digit_hist(c.sort_buf[0].p, n, seg_desc, seg_npieces, spec, seg_cnt,
+                                            (uint32_t *)c.digit_hist.p, st));
+            spec_counted = true;
+        }
+    }
+    if (!spec_counted) HIP_TRY(launch_digit_hist(c.sort_buf[0].p, n, rb, (uint32_t *)c.digit_hist.p, e->num_cus, st));
+    std::vector<uint32_t> dh((size_t)ndig * 256);
+    HIP_TRY(hipMemcpyAsync(dh.data(), c.digit_hist.p, dh.size() * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
     // one segmented pass c.sort_buf[cur] -> c.sort_buf[cur ^ 1] by kp (KIND_KEY_BITS / KIND_DIGIT)
     auto seg_pass = [&](PartParams kp, uint32_t *err) -> int {
         SGX_TRY(seg_plan());
@@ -398,7 +421,11 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
         const ScatterGeom geo = scatter_geom16_wc(kp.R);
         if (geo.items == 0) return fail_msg(SGX_ERR_HIP, "internal error: no write-combining geometry for %u", kp.R);
         kp.mbits = (uint32_t)geo.mbits;
-        HIP_TRY(launch_piece_hist(c.sort_buf[cur].p, n, seg_desc, seg_npieces, kp, seg_cnt, st));
+        // the counts of the first read, when this is the guessed window over the unsorted buffer
+        const bool have = spec_counted && cur == 0 && kp.kind == KIND_KEY_BITS && kp.R == spec.R &&
+                          kp.dshift == spec.dshift && kp.dflip == spec.dflip;
+        spec_counted = false;
+        if (!have) HIP_TRY(launch_piece_hist(c.sort_buf[cur].p, n, seg_desc, seg_npieces, kp, seg_cnt, st));
         HIP_TRY(launch_seg_offsets(seg_cnt, seg_base, seg_pk, (int64_t)gpr.size(), kp.R, seg_offs, st));
         HIP_TRY(launch_scatter16_seg(c.sort_buf[cur].p, c.sort_buf[cur ^ 1].p, n, kp, seg_offs, 1, seg_desc, seg_nd,
                                      seg_nd + 1, (int)seg_npieces, geo, err, st));
@@ -418,10 +445,7 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
         // window top bit: 16 B -> 8 * (byte + 1) of the sign-flipped Long; 100 B -> the first 8
         // key bytes big-endian, byte j ends at bit 64 - 8 j (bytes 8, 9 are outside the window)
         const int top = top_byte < 0 ? 64 : (rb == 16 ? 8 * (top_byte + 1) : (top_byte < 8 ? 64 - 8 * top_byte : -1));
-        const double rp = use_p ? (double)(nparts > 0 ? std::min(nparts, s.R) : s.R) : 1.0;
-        int kbits = 0;
-        while (kbits < 30 && (double)n / (rp * (double)(1ull << kbits)) > 64.0) ++kbits;
-        kbits = std::min(kbits, std::max(top, 0));
+        const int kbits = std::min(kbits0, std::max(top, 0));
         const bool eligible = top_byte >= 0 && top > 0 && (uint64_t)maxbin * 16 <= (uint64_t)n &&
                               (double)n / (rp * (double)(1ull << kbits)) <= 256.0;
         if (eligible) {
