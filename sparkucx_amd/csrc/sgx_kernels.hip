@@ -2947,7 +2947,9 @@ hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, cons
         hipLaunchKernelGGL((k_bucket_sort<16, T, H>), dim3((unsigned)((n + T - 1) / T)), dim3(BS_THREADS), lds, stream,
                            (const uint32_t *)in, (uint32_t *)out, n, pp, use_p, kshift, kbits, err);
     } else if (rb == 100) {
-        constexpr int T = 384, H = 253;  // CAP = 638 (even: 100 B records keep the key array 8-aligned)
+        // CAP = 640 (even: 100 B records keep the key array 8-aligned); with sub-bins a halo of 127
+        // (buckets average ~64 records) reads 1.25x the tile instead of 1.66x
+        constexpr int T = SGX_BS_SUBBIN ? 512 : 384, H = SGX_BS_SUBBIN ? 127 : 253;
         const size_t lds = bucket_sort_lds<100, T, H>();
         (void)hipFuncSetAttribute((const void *)k_bucket_sort<100, T, H>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);

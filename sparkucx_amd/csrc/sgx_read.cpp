@@ -446,8 +446,10 @@ int sgx::sort_records(sgx_engine *e, Ctx &c, const Shuffle &s, int64_t n, bool b
         // key bytes big-endian, byte j ends at bit 64 - 8 j (bytes 8, 9 are outside the window)
         const int top = top_byte < 0 ? 64 : (rb == 16 ? 8 * (top_byte + 1) : (top_byte < 8 ? 64 - 8 * top_byte : -1));
         const int kbits = std::min(kbits0, std::max(top, 0));
+        // (buckets must fit the bucket sort's halo: 255 records for 16 B, 127 for 100 B)
+        const double max_avg = rb == 16 ? 128.0 : 64.0;
         const bool eligible = top_byte >= 0 && top > 0 && (uint64_t)maxbin * 16 <= (uint64_t)n &&
-                              (double)n / (rp * (double)(1ull << kbits)) <= 256.0;
+                              (double)n / (rp * (double)(1ull << kbits)) <= max_avg;
         if (eligible) {
             const int lo = top - kbits;
             // Segmented form: the gather left every partition's records
