@@ -70,8 +70,36 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
   private def le(n: Long): ByteBuffer = {
     if (n > Int.MaxValue - 8)
       throw new UnsupportedOperationException(
-        s"a read of $n bytes exceeds one direct buffer: split the reduce task's partition range")
+        s"a read of $n bytes of ONE partition exceeds one direct buffer (2 GiB)")
     ByteBuffer.allocateDirect(math.max(8L, n).toInt).order(ByteOrder.LITTLE_ENDIAN)
+  }
+
+  /** The largest result one engine call hands over (a direct buffer holds < 2 GiB). */
+  private val maxChunkBytes: Long = SparkEnv.get.conf.getSizeAsBytes("spark.shuffle.ucx.gpu.readChunkBytes",
+    (1L << 30).toString)
+
+  /** The engine's size of a read of [a, b): what readGrouped / readSorted / readRecords would
+   *  hand over (groups and values for an aggregation, bytes otherwise). */
+  private def readSize(maps: Array[Long], a: Int, b: Int): Long =
+    if (handle.agg != GpuUcxShuffleManager.NO_AGG) {
+      val Array(groups, values) = SgxNative.readGrouped(engine, shuffleId, maps, a, b, handle.agg, null, null, null)
+      8 * math.max(groups, values)
+    } else if (dep.keyOrdering.isDefined) SgxNative.readSorted(engine, shuffleId, maps, a, b, null)
+    else SgxNative.readRecords(engine, shuffleId, maps, a, b, null)
+
+  /** [start, end) cut into partition sub-ranges whose results fit maxChunkBytes, read one after
+   *  the other as the task consumes them: a range's sorted / grouped / plain result is the
+   *  concatenation of its partitions' (a key lives in one partition; sortByKey's reader
+   *  orders by partition, then key), so a large reduce task streams instead of failing on one
+   *  2 GiB buffer.  A sub-range too large is halved; a single partition too large fails. */
+  private def chunked(maps: Array[Long]): Iterator[Product2[K, C]] = {
+    def ranges(a: Int, b: Int): Iterator[(Int, Int)] =
+      if (b - a <= 1 || readSize(maps, a, b) <= maxChunkBytes) Iterator.single((a, b))
+      else {
+        val m = a + (b - a) / 2
+        ranges(a, m) ++ ranges(m, b)
+      }
+    ranges(startPartition, endPartition).flatMap { case (a, b) => readOnGpu(maps, a, b) }
   }
 
   /** Blocks (map, reducer) of the range that hold bytes, and their bytes (the engine's lengths). */
@@ -100,7 +128,7 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
       val (blocks, bytes) = blockStats(maps)
       readMetrics.incLocalBlocksFetched(blocks)
       readMetrics.incLocalBytesRead(bytes)
-      readOnGpu(maps)
+      chunked(maps)
     } else readRemote(maps, coordinator.get)
     val counted = CompletionIterator[Product2[K, C], Iterator[Product2[K, C]]](
       records.map { r => readMetrics.incRecordsRead(1); r },
@@ -108,13 +136,12 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
     new InterruptibleIterator[Product2[K, C]](context, counted)
   }
 
-  private def readOnGpu(maps: Array[Long]): Iterator[Product2[K, C]] = {
+  private def readOnGpu(maps: Array[Long], a: Int, b: Int): Iterator[Product2[K, C]] = {
     if (handle.agg != GpuUcxShuffleManager.NO_AGG) {
       val sum = handle.agg == SgxNative.AGG_SUM
-      val Array(groups, values) = SgxNative.readGrouped(engine, shuffleId, maps, startPartition, endPartition,
-                                                        handle.agg, null, null, null)
+      val Array(groups, values) = SgxNative.readGrouped(engine, shuffleId, maps, a, b, handle.agg, null, null, null)
       val keys = le(groups * 8); val starts = le(groups * 8); val vals = le(values * 8)
-      SgxNative.readGrouped(engine, shuffleId, maps, startPartition, endPartition, handle.agg, keys, starts, vals)
+      SgxNative.readGrouped(engine, shuffleId, maps, a, b, handle.agg, keys, starts, vals)
       val k = keys.asLongBuffer(); val s = starts.asLongBuffer(); val v = vals.asLongBuffer()
       if (sum) {
         Iterator.tabulate(groups.toInt)(g => (k.get(g), v.get(g)).asInstanceOf[Product2[K, C]])
@@ -130,11 +157,11 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
       }
     } else {
       val sorted = dep.keyOrdering.isDefined
-      val bytes = if (sorted) SgxNative.readSorted(engine, shuffleId, maps, startPartition, endPartition, null)
-                  else SgxNative.readRecords(engine, shuffleId, maps, startPartition, endPartition, null)
+      val bytes = if (sorted) SgxNative.readSorted(engine, shuffleId, maps, a, b, null)
+                  else SgxNative.readRecords(engine, shuffleId, maps, a, b, null)
       val dst = le(bytes)
-      if (sorted) SgxNative.readSorted(engine, shuffleId, maps, startPartition, endPartition, dst)
-      else SgxNative.readRecords(engine, shuffleId, maps, startPartition, endPartition, dst)
+      if (sorted) SgxNative.readSorted(engine, shuffleId, maps, a, b, dst)
+      else SgxNative.readRecords(engine, shuffleId, maps, a, b, dst)
       val recs = dst.asLongBuffer()
       Iterator.tabulate((bytes / 16).toInt)(i => (recs.get(2 * i), recs.get(2 * i + 1)).asInstanceOf[Product2[K, C]])
     }
@@ -171,7 +198,14 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
     pieces.foreach(p => buf.put(p))
     buf.flip()
     val id = SgxNative.importBlocks(engine, shuffleId, maps, startPartition, endPartition, buf, lengths)
-    // the read copies its results out of HBM before returning: the import can go right after
-    try readOnGpu(maps) finally SgxNative.releaseImport(engine, shuffleId, id)
+    // every read copies its results out of HBM before returning: the import goes once the
+    // last sub-range has been read (the iterator drains the chunks in order)
+    var released = false
+    def release(): Unit = if (!released) {
+      released = true
+      SgxNative.releaseImport(engine, shuffleId, id)
+    }
+    context.addTaskCompletionListener[Unit](_ => release())  // a killed task drops it too
+    CompletionIterator[Product2[K, C], Iterator[Product2[K, C]]](chunked(maps), release())
   }
 }
