@@ -1891,6 +1891,15 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 #ifndef SGX_WWC_DRAIN_V2
 #define SGX_WWC_DRAIN_V2 1
 #endif
+// the drain's units carry their first record slot and dword (no cursor read, no division on
+// the piece's path), two pieces in flight per thread (A/B: -DSGX_WWC_DRAIN_V3=0)
+#ifndef SGX_WWC_DRAIN_V3
+#define SGX_WWC_DRAIN_V3 1
+#endif
+// tiles of loads in flight per workgroup (A/B: -DSGX_WWC_PREFETCH=1)
+#ifndef SGX_WWC_PREFETCH
+#define SGX_WWC_PREFETCH 1
+#endif
 // XOR-swizzled carry rows (A/B: -DSGX_WWC_SWIZZLE=0)
 #ifndef SGX_WWC_SWIZZLE
 #define SGX_WWC_SWIZZLE 1
@@ -1989,8 +1998,10 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
         carry[cx(p, 15)] = c0;  // the stream's first record: bytes before it are not ours
     }
 
-    u32x4 ld[LD];
-    auto issue = [&](int t) {
+    // the tile loads in registers, SGX_WWC_PREFETCH tiles ahead (2: two buffers, the tile loop
+    // unrolled by two so that each buffer is named statically)
+    u32x4 ld0[LD], ld1[LD];
+    auto issue = [&](int t, u32x4(&ld)[LD]) __attribute__((always_inline)) {
         const u32x4 *tb = (const u32x4 *)(cin + (int64_t)t * TR * RB);
         const int nch = (t + 1 < ntiles ? TR : lastn) == TR ? NCH : 0;  // partial tiles: dword-wise
 #pragma unroll
@@ -1999,8 +2010,15 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             ld[i] = c < nch ? tb[c] : u32x4{0, 0, 0, 0};
         }
     };
-    if (ntiles > 0) issue(0);
+    if (ntiles > 0) issue(0, ld0);
+#if SGX_WWC_PREFETCH > 1
+    if (ntiles > 1) issue(1, ld1);
+#endif
     uint32_t bad = 0;
+#ifdef SGX_WC_STAMPS
+    uint64_t st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+    uint64_t st_last = wc_stamp();
+#endif
     // the owner thread's streams 2 tid, 2 tid + 1: their next cursor and carry, taken from the
     // tile's last record of the stream during the drain, stored at the next tile's start
     // (after the barrier that ends every drain's reads of the old ones)
@@ -2018,9 +2036,11 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             upd[h] = false;
         }
     };
-    for (int t = 0; t < ntiles; ++t) {
+    auto tile = [&](const int t, u32x4(&ld)[LD], u32x4(&ldn)[LD]) __attribute__((always_inline)) {
         const int nrec = t + 1 < ntiles ? TR : lastn;
+        WC_STAMP(0);  // loop top
         writeback();
+        WC_STAMP(1);  // owners' carry writeback
         // ---- land the tile; clear the ranking rows
         if (nrec == TR) {
 #pragma unroll
@@ -2041,7 +2061,13 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
 #else
         lds_barrier();
 #endif
-        if (t + 1 < ntiles) issue(t + 1);
+        WC_STAMP(2);  // land the tile (its loads' wait) + barrier
+#if SGX_WWC_PREFETCH > 1
+        if (t + 2 < ntiles) issue(t + 2, ld);
+#else
+        if (t + 1 < ntiles) issue(t + 1, ldn);
+#endif
+        WC_STAMP(3);  // issue the next tile's loads
         // ---- partition id + rank (record tid: input order = thread order)
         const bool valid = tid < (uint32_t)nrec;
         uint32_t pid = 0, old;
@@ -2052,10 +2078,11 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
         old = __hip_atomic_fetch_add(myrow32 + (pid >> 1), valid ? 1u << ((pid & 1u) << 4) : 0u, __ATOMIC_RELAXED,
                                      __HIP_MEMORY_SCOPE_WORKGROUP);
         lds_barrier();
+        WC_STAMP(4);  // partition ids + ranking atomics + barrier
         // ---- merge: per partition pair j = tid, prefix over the wave rows; block scan of
         //      {records, whole units} packed 16 | 16
         const uint32_t j = tid;
-        uint32_t before[W], tot = 0, val = 0, k[2] = {0, 0}, nu[2] = {0, 0};
+        uint32_t before[W], tot = 0, val = 0, k[2] = {0, 0}, nu[2] = {0, 0}, cc[2] = {0, 0};
         if (j < NP) {
 #pragma unroll
             for (int v = 0; v < W; ++v) {
@@ -2065,13 +2092,17 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             k[0] = tot & 0xFFFFu;
             k[1] = tot >> 16;
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
-                nu[h] = ((uint32_t)(((uint64_t)cur[2 * j + h] * RB) & 63u) + RB * k[h]) >> 6;
+            for (int h = 0; h < 2; ++h) {
+                cc[h] = cur[2 * j + h];  // the owner's cursors (cur[] is the drain's view below)
+                nu[h] = ((uint32_t)(((uint64_t)cc[h] * RB) & 63u) + RB * k[h]) >> 6;
+            }
             val = (k[0] + k[1]) | ((nu[0] + nu[1]) << 16);
         }
+        WC_STAMP(5);  // merge: rank rows read
         const uint32_t xs = wave_inclusive_scan(val, lane);
         if (lane == 63) scratch[w] = xs;
         lds_barrier();
+        WC_STAMP(10);  // merge: scan + barrier
         uint32_t base = xs - val, total = 0;
 #pragma unroll
         for (int v = 0; v < W; ++v) {
@@ -2079,24 +2110,118 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             if (v < (int)w) base += y;
             total += y;
         }
+        WC_STAMP(11);  // merge: wave totals read
         const uint32_t sb[2] = {base & 0xFFFFu, (base & 0xFFFFu) + k[0]};
         const uint32_t ubs[2] = {base >> 16, (base >> 16) + nu[0]};
         if (j < NP) {
             const uint32_t L = sb[0] | (sb[1] << 16);
 #pragma unroll
             for (int v = 0; v < W; ++v) ((uint32_t *)(rows + (size_t)v * RS))[j] = before[v] + L;
+#if SGX_WWC_DRAIN_V3
+            // unit i of stream p starts at dword 16 i - cbD of the stream's new records: below 0
+            // (unit 0 only) its first cneg dwords are the carry's, else record slot sb + r, dword
+            // w.  desc = p | slot << 10 | w << 19 | cneg << 24 | slow << 28, slow: the unit holds
+            // dwords before the stream's first record or past the output's end.  cur[p] becomes
+            // the drain's view cur - sb (the unit's output dword = 25 (view + slot) + w - cneg);
+            // the owner's writeback restores it (a stream without records keeps its cursor)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                if (k[h] == 0) continue;
+                const uint32_t p = 2 * j + h;
+                const uint64_t cD = (uint64_t)cc[h] * DW, u0D = cD & ~(uint64_t)15;
+                const uint64_t startD = (uint64_t)carry[cx(p, 15)] * DW, capD = (uint64_t)olim * DW;
+                int32_t base = -(int32_t)(cD - u0D);
+                uint32_t r = 0, wv = 0;
+                for (uint32_t i = 0; i < nu[h]; ++i) {
+                    const uint32_t cneg = base < 0 ? (uint32_t)-base : 0u;
+                    const uint32_t slow = ((i == 0 && u0D < startD) || u0D + 16u * (i + 1) > capD) ? 1u : 0u;
+                    desc[ubs[h] + i] = p | ((sb[h] + r) << 10) | (wv << 19) | (cneg << 24) | (slow << 28);
+                    const int32_t nb = base + 16;
+                    if (base < 0) {
+                        wv = nb > 0 ? (uint32_t)nb : 0u;
+                    } else {
+                        wv += 16u;
+                        if (wv >= (uint32_t)DW) wv -= DW, ++r;
+                    }
+                    base = nb;
+                }
+                cur[p] = cc[h] - sb[h];
+            }
+#else
 #pragma unroll
             for (int h = 0; h < 2; ++h)
                 for (uint32_t i = 0; i < nu[h]; ++i) desc[ubs[h] + i] = (2 * j + h) | (sb[h] << 10) | (i << 20);
+#endif
         }
+        WC_STAMP(12);  // merge: rows + unit words written
         lds_barrier();
+        WC_STAMP(13);  // merge: barrier
         // ---- partition-sorted index of the tile
         if (valid) idx[myrow[pid] + ((old >> ((pid & 1u) << 4)) & 0xFFFFu)] = (uint16_t)tid;
         lds_barrier();
+        WC_STAMP(6);  // sorted index + barrier
         // ---- drain: whole 64 B units, 16 B per lane, 4 lanes per unit.  Unit byte x of
         //      stream p: its carry below cb (the open unit's bytes), else byte x - cb of the
         //      stream's records in sorted order
         const uint32_t npieces = (total >> 16) * 4u;
+#if SGX_WWC_DRAIN_V3
+        // two pieces per step, each phase issued for both before its results are used: the
+        // unit word; then the two index slots (and carry dwords); then the 4 data dwords
+        const uint32_t coff = (uint32_t)(carry - stage);
+        for (uint32_t q0 = tid; q0 < npieces; q0 += 2 * T) {
+            uint32_t Dw[2], o4[2], s0[2], s1[2], vw[2][4];
+            bool live[2];
+            // both words at once (one ds_read2: the second is T / 4 words on, inside the LDS
+            // block even past the desc array; a dead piece's word is zeroed)
+            Dw[0] = desc[q0 >> 2];
+            Dw[1] = desc[(q0 >> 2) + T / 4];
+            live[0] = true;
+            live[1] = q0 + T < npieces;
+            Dw[1] = live[1] ? Dw[1] : 0u;
+            uint32_t vx[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint32_t D = Dw[u], p = D & 1023u, slot = (D >> 10) & 511u;
+                o4[u] = ((D >> 19) & 31u) + ((q0 + (uint32_t)u * T) & 3u) * 4u;  // + cneg
+                s0[u] = idx[slot];
+                s1[u] = idx[min(slot + 1u, (uint32_t)TR - 1u)];
+                vx[u] = cur[p];
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const uint32_t D = Dw[u], p = D & 1023u, cneg = (D >> 24) & 15u;
+                const uint32_t b0 = s0[u] * DW, b1 = s1[u] * DW - DW;
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    // dword od = o4 + d - cneg of the unit's records: the carry's below 0 (its
+                    // dword o4 + d), else record slot (slot + 1 from dword 25; od < 50).  The
+                    // choices as masks, so the four reads issue back to back without branches
+                    // (the carry rows addressed from the stage's base)
+                    const uint32_t e = o4[u] + d;
+                    const uint32_t w = e - cneg;
+                    const uint32_t m1 = 0u - (uint32_t)(w >= (uint32_t)DW);
+                    const uint32_t sa = w + (b0 ^ ((b0 ^ b1) & m1));
+                    const uint32_t ca = coff + cx(p, e & 15u);
+                    const uint32_t m2 = 0u - (uint32_t)(e < cneg);
+                    vw[u][d] = stage[sa ^ ((sa ^ ca) & m2)];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                if (!live[u]) continue;
+                const uint32_t D = Dw[u], p = D & 1023u, slot = (D >> 10) & 511u, cneg = (D >> 24) & 15u;
+                const uint64_t bD = (uint64_t)(vx[u] + slot) * DW + o4[u] - cneg;
+                if (!(D >> 28)) {
+                    *(u32x4 *)(out + bD) = u32x4{vw[u][0], vw[u][1], vw[u][2], vw[u][3]};
+                } else {  // the stream's first unit, or the output's end: only the dwords that are ours
+                    const uint64_t startD = (uint64_t)carry[cx(p, 15)] * DW, capD = (uint64_t)olim * DW;
+#pragma unroll
+                    for (int d = 0; d < 4; ++d)
+                        if (bD + d >= startD && bD + d < capD) out[bD + d] = vw[u][d];
+                }
+            }
+        }
+#else
 #if SGX_WWC_DRAIN_UNROLL > 1
 #pragma unroll SGX_WWC_DRAIN_UNROLL
 #endif
@@ -2171,27 +2296,41 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             }
 #endif
         }
+#endif
+        WC_STAMP(7);  // drain
         // the owner's streams: next cursor, and the new open unit = the tail of the tile's last
         // record of the stream (a record is longer than a unit, so it always closes the old one)
         if (j < NP) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 if (k[h] == 0) continue;
-                const uint32_t p = 2 * j + h;
-                const uint64_t cB = (uint64_t)cur[p] * RB, cnB = cB + (uint64_t)RB * k[h];
+                const uint64_t cB = (uint64_t)cc[h] * RB, cnB = cB + (uint64_t)RB * k[h];
                 const uint64_t u1B = cnB & ~(uint64_t)63;
                 const uint32_t o = (uint32_t)(u1B - cB) - RB * (k[h] - 1);  // byte of the last record
                 const uint32_t s0 = (uint32_t)idx[sb[h] + k[h] - 1] * DW + (o >> 2);
                 ncnt[h] = (uint32_t)(cnB - u1B) >> 2;
 #pragma unroll
                 for (int i = 0; i < 15; ++i) creg[h][i] = stage[min(s0 + i, (uint32_t)(TR * DW - 1))];
-                ncur[h] = cur[p] + k[h];
+                ncur[h] = cc[h] + k[h];
                 upd[h] = true;
                 bad |= ncur[h] > olim ? 1u : 0u;
             }
         }
+        WC_STAMP(8);  // owners' next carries
         lds_barrier();
+        WC_STAMP(9);  // final barrier
+    };
+    for (int t = 0; t < ntiles; t += 2) {
+        tile(t, ld0, ld1);
+        if (t + 1 < ntiles) tile(t + 1, ld1, ld0);
     }
+#ifdef SGX_WC_STAMPS
+    if (lane == 0) {
+        for (int i = 0; i < 14; ++i) atomicAdd(&g_wc_stamps[i], (unsigned long long)st_acc[i]);
+        atomicAdd(&g_wc_stamps[14], (unsigned long long)ntiles);
+        atomicAdd(&g_wc_stamps[15], 1ull);
+    }
+#endif
     writeback();
     __syncthreads();
     // ---- the chunk's end: every stream's open unit (its own dwords)

@@ -17,6 +17,10 @@ PHASES = ["wait_loads", "rank", "merge", "stage_zero_loads_B4", "unused", "loop"
 # k_scatter_wide2 (TeraSort 100 B records, --record-bytes 100)
 PHASES_WIDE2 = ["loop_top", "land_stage_writes_barrier", "issue_next_loads", "partition_ids", "rank_barrier",
                 "merge", "sorted_index", "drain_lds_reads", "drain_stores", "final_barrier", "unused", "unused2"]
+# k_scatter_wide_wc (the padded TeraSort K4, --record-bytes 100 --wide-wc)
+PHASES_WIDE_WC = ["loop_top", "carry_writeback", "land_barrier", "issue_next_loads", "partition_ids_rank_barrier",
+                  "merge_rows_read", "sorted_index_barrier", "drain", "owner_next_carries", "final_barrier",
+                  "merge_scan_barrier", "merge_totals_read", "merge_rows_units_written", "merge_barrier"]
 
 
 def main():
@@ -26,6 +30,7 @@ def main():
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--dist", default="uniform")
     ap.add_argument("--record-bytes", type=int, default=16, choices=[16, 100])
+    ap.add_argument("--wide-wc", action="store_true", help="100 B records on the padded write (k_scatter_wide_wc)")
     a = ap.parse_args()
     import numpy as np
 
@@ -65,8 +70,10 @@ def main():
     assert fn(out, 1) == 0
     v = list(out)
     waves_tiles = v[14]  # every wave adds its workgroup's tile count
-    tot = sum(v[:12])
-    names = PHASES_WIDE2 if rb == 100 else PHASES
+    nph = 14 if a.wide_wc else 12
+    tot = sum(v[:nph])
+    names = PHASES_WIDE_WC if a.wide_wc else PHASES_WIDE2 if rb == 100 else PHASES
+    names = names[:nph]
     res = {"partitions": a.partitions, "dist": a.dist if rb == 16 else "terasort", "workgroups": v[15] // 8, "tile_waves": v[14],
            "cycles_per_tile_wave": {p: round(v[i] / max(1, waves_tiles), 1) for i, p in enumerate(names)},
            "share": {p: round(v[i] / max(1, tot), 4) for i, p in enumerate(names)}}
