@@ -1884,18 +1884,33 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 #ifndef SGX_WIDE_WC_TWOPASS
 #define SGX_WIDE_WC_TWOPASS 1
 #endif
-// diagnostic probe only (tools/build_variant.sh <tag> - -DSGX_WWC_NOSTORE=1): the drain and the
-// head units compute their stores but do not issue them -- the kernel's time without its writes
+#ifndef SGX_WWC_DRAIN_UNROLL
+#define SGX_WWC_DRAIN_UNROLL 2
+#endif
+// the drain in dword arithmetic, one division per piece (A/B: -DSGX_WWC_DRAIN_V2=0)
+#ifndef SGX_WWC_DRAIN_V2
+#define SGX_WWC_DRAIN_V2 1
+#endif
+// the drain's units carry their first record slot and dword (no cursor read, no division on
+// the piece's path), two pieces in flight per thread (A/B: -DSGX_WWC_DRAIN_V3=0)
+#ifndef SGX_WWC_DRAIN_V3
+#define SGX_WWC_DRAIN_V3 1
+#endif
+// tiles of loads in flight per workgroup (A/B: -DSGX_WWC_PREFETCH=1)
+#ifndef SGX_WWC_PREFETCH
+#define SGX_WWC_PREFETCH 1
+#endif
+// XOR-swizzled carry rows (A/B: -DSGX_WWC_SWIZZLE=0)
+#ifndef SGX_WWC_SWIZZLE
+#define SGX_WWC_SWIZZLE 1
+#endif
+// diagnostic probe only (tools/build_variant.sh <tag> - -DSGX_WWC_NOSTORE=1): the drain computes
+// its stores but does not issue them -- the kernel's time without its writes
 #ifndef SGX_WWC_NOSTORE
 #define SGX_WWC_NOSTORE 0
 #endif
-// the write-combining unit in dwords: 32 = whole 128 B lines (A/B: -DSGX_WWC_UNIT_DW=16)
-#ifndef SGX_WWC_UNIT_DW
-#define SGX_WWC_UNIT_DW 32
-#endif
-constexpr int WWC_TR = 1024;
-// closed units per tile (R <= 1024): every record's dwords plus every stream's carry
-constexpr int WWC_UMAX = (WWC_TR * 100 + 1024 * (SGX_WWC_UNIT_DW - 1) * 4) / (SGX_WWC_UNIT_DW * 4) + 1;
+constexpr int WWC_TR = 512;
+constexpr int WWC_UMAX = (WWC_TR * 100 + 1024 * 60) / 64 + 1;  // units per tile (R <= 1024)
 
 // range bounds packed 12 B each in LDS: {hi lo32, hi hi32, lo}
 struct Bounds12 {
@@ -1910,33 +1925,22 @@ struct Bounds12 {
 };
 
 __host__ __device__ size_t scatter_wide_wc_lds(uint32_t R, int nb) {
-    return al16((size_t)WWC_TR * 100) + al16((size_t)nb * 12) + RDIR_BYTES + (size_t)8 * rs8(R) * 2 +
-           al16((size_t)WWC_UMAX * 4) + (size_t)rs8(R) * 4 + al16((size_t)WWC_TR * 2) + 64 * 4;
+    return al16((size_t)WWC_TR * 100) + al16((size_t)nb * 12) + RDIR_BYTES + (size_t)rs8(R) * 64 +
+           (size_t)8 * rs8(R) * 2 + al16((size_t)WWC_UMAX * 4) + (size_t)rs8(R) * 4 + al16((size_t)WWC_TR * 2) +
+           64 * 4;
 }
 
-// The tile loop.  Round 5 measured the 512-record form's phases (s_memtime stamps,
-// profiles/r05l_terasort_wc_stamps.jsonl): the merge over all R streams, the carry write-back
-// and the barriers -- work per tile, not per record -- took ~45 % of the cycles, and the carry
-// rows (64 KB of LDS at R = 1024) were what kept the tile at 512 records and the unit at 64 B.
-// So the carries live in the owner threads' registers (thread j owns streams 2j, 2j + 1), the
-// freed LDS holds a 1024-record tile, and the unit is UD dwords (SGX_WWC_UNIT_DW: 32 = whole
-// 128 B lines, a carry of <= 31 dwords per stream).  A unit that closes this tile is drained
-// in 16 B pieces, except the pieces of the stream's open unit that hold carried dwords: those
-// the owner writes from its registers (with <= 3 dwords of the tile's first record of the
-// stream).  A unit spans up to three records, a piece up to two.
 template <int KIND, int MODE>
 __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restrict__ in, uint32_t *__restrict__ out,
                                                             int64_t n, int64_t chunk, PartParams pp,
                                                             const uint32_t *__restrict__ offs, int G,
                                                             uint32_t *err) {
     constexpr int T = 512, W = 8, TR = WWC_TR, RB = 100, DW = RB / 4;
-    constexpr int UD = SGX_WWC_UNIT_DW, PU = UD / 4, CW = UD - 1;  // unit dwords, pieces, carry dwords
     constexpr int NCH = TR * RB / 16;  // 16 B chunks per full tile
     constexpr int LD = (NCH + T - 1) / T;
-    static_assert((TR * RB) % 16 == 0 && TR == 2 * T, "two records per thread, tiles 16 B aligned");
-    static_assert(UD == 16 || UD == 32, "64 B or 128 B units");
+    static_assert((TR * RB) % 16 == 0 && TR == T, "one record per thread, tiles 16 B aligned");
     const uint32_t olim = MODE == WC_PADDED ? pp.olim : (uint32_t)n;
-    const uint64_t capD = (uint64_t)olim * DW;  // output dwords
+    const uint64_t capB = (uint64_t)olim * RB;  // output bytes
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const uint32_t R = pp.R, RS = rs8(R), NP = RS / 2;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -1962,13 +1966,13 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
         bdir = (const uint16_t *)sp;
     }
     sp += RDIR_BYTES;
+    uint32_t *carry = (uint32_t *)sp;  // [p][0..14] the open unit's bytes, [p][15] the stream's first record
+    sp += (size_t)RS * 64;
     uint16_t *rows = (uint16_t *)sp;
     sp += (size_t)8 * RS * 2;
-    // the tile's closed units: p | first record slot << 10 | (first dword + 32) << 20 | past the
-    // output's end << 26 (the first dword is negative when the unit starts in the carry)
-    uint32_t *desc = (uint32_t *)sp;
+    uint32_t *desc = (uint32_t *)sp;  // whole units of the tile: p | slot base << 10 | unit of p << 20
     sp += al16((size_t)WWC_UMAX * 4);
-    uint32_t *cur = (uint32_t *)sp;  // the drain's view of stream p: its cursor - its first slot
+    uint32_t *cur = (uint32_t *)sp;
     sp += (size_t)RS * 4;
     uint16_t *idx = (uint16_t *)sp;
     sp += al16((size_t)TR * 2);
@@ -1977,6 +1981,13 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
     uint32_t *myrow32 = (uint32_t *)myrow;
     const Bounds12 bk{b12};
     const int64_t *bi64 = (const int64_t *)b12;
+    // dword i of stream p's carry row, XOR-swizzled by the stream's p / 4: a row is 16 dwords,
+    // so unswizzled the rows of streams p, p + 4, ... share their banks -- the owners' carry
+    // writes (lanes j -> streams 2j + h) were 32-way bank conflicts (SQ counters,
+    // profiles/r05a_terasort_k4_sq_counters.txt: conflicts 56 % of the LDS cycles)
+    auto cx = [](uint32_t p, uint32_t i) __attribute__((always_inline)) -> uint32_t {
+        return 16u * p + (i ^ (SGX_WWC_SWIZZLE ? (p >> 2) & 15u : 0u));
+    };
 
     const int g = blockIdx.x;
     const int64_t begin = (int64_t)g * chunk;
@@ -1986,20 +1997,16 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
     const int64_t len = pp.chunks ? pp.chunks[2 * g + 1] : end > begin ? end - begin : 0;
     const int ntiles = (int)((len + TR - 1) / TR);
     const int lastn = ntiles > 0 ? (int)(len - (int64_t)(ntiles - 1) * TR) : 0;
-    // the owner's streams 2j + h: cursor, first record, and the carry -- dword d of the open
-    // unit at (oc * 25) & ~(UD - 1), valid below (oc * 25) & (UD - 1)
-    const uint32_t j = tid;
-    uint32_t oc[2] = {0, 0}, ost[2] = {0, 0}, creg[2][CW];
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const uint32_t p = 2 * j + h;
-        oc[h] = ost[h] = j < NP && p < R ? offs[(int64_t)p * G + g] : 0u;
-#pragma unroll
-        for (int i = 0; i < CW; ++i) creg[h][i] = 0u;
+    for (uint32_t p = tid; p < RS; p += T) {
+        const uint32_t c0 = p < R ? offs[(int64_t)p * G + g] : 0u;
+        cur[p] = c0;
+        carry[cx(p, 15)] = c0;  // the stream's first record: bytes before it are not ours
     }
 
-    u32x4 ld[LD];
-    auto issue = [&](int t) __attribute__((always_inline)) {
+    // the tile loads in registers, SGX_WWC_PREFETCH tiles ahead (2: two buffers, the tile loop
+    // unrolled by two so that each buffer is named statically)
+    u32x4 ld0[LD], ld1[LD];
+    auto issue = [&](int t, u32x4(&ld)[LD]) __attribute__((always_inline)) {
         const u32x4 *tb = (const u32x4 *)(cin + (int64_t)t * TR * RB);
         const int nch = (t + 1 < ntiles ? TR : lastn) == TR ? NCH : 0;  // partial tiles: dword-wise
 #pragma unroll
@@ -2008,15 +2015,37 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             ld[i] = c < nch ? tb[c] : u32x4{0, 0, 0, 0};
         }
     };
-    if (ntiles > 0) issue(0);
+    if (ntiles > 0) issue(0, ld0);
+#if SGX_WWC_PREFETCH > 1
+    if (ntiles > 1) issue(1, ld1);
+#endif
     uint32_t bad = 0;
 #ifdef SGX_WC_STAMPS
     uint64_t st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t st_last = wc_stamp();
 #endif
-    for (int t = 0; t < ntiles; ++t) {
+    // the owner thread's streams 2 tid, 2 tid + 1: their next cursor and carry, taken from the
+    // tile's last record of the stream during the drain, stored at the next tile's start
+    // (after the barrier that ends every drain's reads of the old ones)
+    uint32_t ncur[2] = {0, 0}, ncnt[2] = {0, 0}, creg[2][15];
+    bool upd[2] = {false, false};
+    auto writeback = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (!upd[h]) continue;
+            const uint32_t p = 2 * tid + h;
+#pragma unroll
+            for (int i = 0; i < 15; ++i)
+                if ((uint32_t)i < ncnt[h]) carry[cx(p, i)] = creg[h][i];
+            cur[p] = ncur[h];
+            upd[h] = false;
+        }
+    };
+    auto tile = [&](const int t, u32x4(&ld)[LD], u32x4(&ldn)[LD]) __attribute__((always_inline)) {
         const int nrec = t + 1 < ntiles ? TR : lastn;
         WC_STAMP(0);  // loop top
+        writeback();
+        WC_STAMP(1);  // owners' carry writeback
         // ---- land the tile; clear the ranking rows
         if (nrec == TR) {
 #pragma unroll
@@ -2029,37 +2058,36 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             for (int d = tid; d < nrec * DW; d += T) stage[d] = tb[d];
         }
         for (uint32_t i = tid; i < (uint32_t)W * RS / 2; i += T) ((uint32_t *)rows)[i] = 0u;
+        // SGX_WWC_LAND_SYNC=0: an LDS-only barrier, so the last drain's global stores stay in
+        // flight through this tile's ranking (the tile's loads are waited for where their
+        // registers are used)
 #if SGX_WWC_LAND_SYNC
         __syncthreads();
 #else
         lds_barrier();
 #endif
         WC_STAMP(2);  // land the tile (its loads' wait) + barrier
-        if (t + 1 < ntiles) issue(t + 1);
+#if SGX_WWC_PREFETCH > 1
+        if (t + 2 < ntiles) issue(t + 2, ld);
+#else
+        if (t + 1 < ntiles) issue(t + 1, ldn);
+#endif
         WC_STAMP(3);  // issue the next tile's loads
-        // ---- partition ids + ranks: wave w takes records [128 w, 128 w + 128), the first 64
-        //      with one atomic, then the next 64 -- input order within the wave's row
-        uint32_t pid[2], old[2];
-        bool valid[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const uint32_t rec = 128u * w + 64u * r + lane;
-            valid[r] = rec < (uint32_t)nrec;
-            pid[r] = 0;
-            if (valid[r]) {
-                const uint32_t *rp = stage + rec * DW;
-                pid[r] = pid_of_b<KIND>(rp[0], rp[1], rp[2], pp, bi64, bk, bdir);
-            }
+        // ---- partition id + rank (record tid: input order = thread order)
+        const bool valid = tid < (uint32_t)nrec;
+        uint32_t pid = 0, old;
+        if (valid) {
+            const uint32_t *rp = stage + tid * DW;
+            pid = pid_of_b<KIND>(rp[0], rp[1], rp[2], pp, bi64, bk, bdir);
         }
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-            old[r] = __hip_atomic_fetch_add(myrow32 + (pid[r] >> 1), valid[r] ? 1u << ((pid[r] & 1u) << 4) : 0u,
-                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        old = __hip_atomic_fetch_add(myrow32 + (pid >> 1), valid ? 1u << ((pid & 1u) << 4) : 0u, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
         lds_barrier();
         WC_STAMP(4);  // partition ids + ranking atomics + barrier
-        // ---- merge: per partition pair j, prefix over the wave rows; block scan of
-        //      {records, closed units} packed 16 | 16
-        uint32_t before[W], tot = 0, val = 0, k[2] = {0, 0}, nu[2] = {0, 0};
+        // ---- merge: per partition pair j = tid, prefix over the wave rows; block scan of
+        //      {records, whole units} packed 16 | 16
+        const uint32_t j = tid;
+        uint32_t before[W], tot = 0, val = 0, k[2] = {0, 0}, nu[2] = {0, 0}, cc[2] = {0, 0};
         if (j < NP) {
 #pragma unroll
             for (int v = 0; v < W; ++v) {
@@ -2069,7 +2097,10 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             k[0] = tot & 0xFFFFu;
             k[1] = tot >> 16;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) nu[h] = (((oc[h] * (uint32_t)DW) & (UD - 1u)) + DW * k[h]) / UD;
+            for (int h = 0; h < 2; ++h) {
+                cc[h] = cur[2 * j + h];  // the owner's cursors (cur[] is the drain's view below)
+                nu[h] = ((uint32_t)(((uint64_t)cc[h] * RB) & 63u) + RB * k[h]) >> 6;
+            }
             val = (k[0] + k[1]) | ((nu[0] + nu[1]) << 16);
         }
         WC_STAMP(5);  // merge: rank rows read
@@ -2091,148 +2122,213 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             const uint32_t L = sb[0] | (sb[1] << 16);
 #pragma unroll
             for (int v = 0; v < W; ++v) ((uint32_t *)(rows + (size_t)v * RS))[j] = before[v] + L;
-            // closed unit i starts at dword o = UD i - cb of the stream's new records: record
-            // slot sb + r, dword o - 25 r (o < 0: unit 0 starts in the carry, r = 0)
+#if SGX_WWC_DRAIN_V3
+            // unit i of stream p starts at dword 16 i - cbD of the stream's new records: below 0
+            // (unit 0 only) its first cneg dwords are the carry's, else record slot sb + r, dword
+            // w.  desc = p | slot << 10 | w << 19 | cneg << 24 | slow << 28, slow: the unit holds
+            // dwords before the stream's first record or past the output's end.  cur[p] becomes
+            // the drain's view cur - sb (the unit's output dword = 25 (view + slot) + w - cneg);
+            // the owner's writeback restores it (a stream without records keeps its cursor)
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 if (k[h] == 0) continue;
                 const uint32_t p = 2 * j + h;
-                const uint64_t cD = (uint64_t)oc[h] * DW, u0D = cD & ~(uint64_t)(UD - 1);
-                const uint64_t room = capD > u0D ? (capD - u0D) / UD : 0;  // whole units before the end
-                const uint32_t ncap = room > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)room;
-                int32_t o = -(int32_t)(cD - u0D);
-                uint32_t r = 0;
+                const uint64_t cD = (uint64_t)cc[h] * DW, u0D = cD & ~(uint64_t)15;
+                const uint64_t startD = (uint64_t)carry[cx(p, 15)] * DW, capD = (uint64_t)olim * DW;
+                int32_t base = -(int32_t)(cD - u0D);
+                uint32_t r = 0, wv = 0;
                 for (uint32_t i = 0; i < nu[h]; ++i) {
-                    desc[ubs[h] + i] =
-                        p | ((sb[h] + r) << 10) | ((uint32_t)(o + 32) << 20) | ((i >= ncap ? 1u : 0u) << 26);
-                    o += UD;
-                    if (o >= DW) o -= DW, ++r;
-                    if (o >= DW) o -= DW, ++r;
+                    const uint32_t cneg = base < 0 ? (uint32_t)-base : 0u;
+                    const uint32_t slow = ((i == 0 && u0D < startD) || u0D + 16u * (i + 1) > capD) ? 1u : 0u;
+                    desc[ubs[h] + i] = p | ((sb[h] + r) << 10) | (wv << 19) | (cneg << 24) | (slow << 28);
+                    const int32_t nb = base + 16;
+                    if (base < 0) {
+                        wv = nb > 0 ? (uint32_t)nb : 0u;
+                    } else {
+                        wv += 16u;
+                        if (wv >= (uint32_t)DW) wv -= DW, ++r;
+                    }
+                    base = nb;
                 }
-                cur[p] = oc[h] - sb[h];
+                cur[p] = cc[h] - sb[h];
             }
+#else
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                for (uint32_t i = 0; i < nu[h]; ++i) desc[ubs[h] + i] = (2 * j + h) | (sb[h] << 10) | (i << 20);
+#endif
         }
         WC_STAMP(12);  // merge: rows + unit words written
         lds_barrier();
         WC_STAMP(13);  // merge: barrier
         // ---- partition-sorted index of the tile
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-            if (valid[r])
-                idx[myrow[pid[r]] + ((old[r] >> ((pid[r] & 1u) << 4)) & 0xFFFFu)] = (uint16_t)(128u * w + 64u * r + lane);
+        if (valid) idx[myrow[pid] + ((old >> ((pid & 1u) << 4)) & 0xFFFFu)] = (uint16_t)tid;
         lds_barrier();
         WC_STAMP(6);  // sorted index + barrier
-        // ---- drain: the closed units in 16 B pieces, PU lanes per unit, two pieces per step,
-        //      each phase issued for both before its results are used (the unit words; the
-        //      two index slots and the cursor view; the 4 data dwords).  A piece that starts in
-        //      the carry is the owner's.
-        const uint32_t npieces = (total >> 16) * PU;
+        // ---- drain: whole 64 B units, 16 B per lane, 4 lanes per unit.  Unit byte x of
+        //      stream p: its carry below cb (the open unit's bytes), else byte x - cb of the
+        //      stream's records in sorted order
+        const uint32_t npieces = (total >> 16) * 4u;
+#if SGX_WWC_DRAIN_V3
+        // two pieces per step, each phase issued for both before its results are used: the
+        // unit word; then the two index slots (and carry dwords); then the 4 data dwords
+        const uint32_t coff = (uint32_t)(carry - stage);
         for (uint32_t q0 = tid; q0 < npieces; q0 += 2 * T) {
-            uint32_t Dw[2], s0[2], s1[2], vx[2], vw[2][4];
-            int32_t e0[2];
-            // both words at once (one ds_read2: the second is T / PU words on, inside the LDS
+            uint32_t Dw[2], o4[2], s0[2], s1[2], vw[2][4];
+            bool live[2];
+            // both words at once (one ds_read2: the second is T / 4 words on, inside the LDS
             // block even past the desc array; a dead piece's word is zeroed)
-            Dw[0] = desc[q0 / PU];
-            Dw[1] = desc[q0 / PU + T / PU];
-            const bool live1 = q0 + T < npieces;
-            Dw[1] = live1 ? Dw[1] : (32u << 20);
+            Dw[0] = desc[q0 >> 2];
+            Dw[1] = desc[(q0 >> 2) + T / 4];
+            live[0] = true;
+            live[1] = q0 + T < npieces;
+            Dw[1] = live[1] ? Dw[1] : 0u;
+            uint32_t vx[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                const uint32_t D = Dw[u], slot = (D >> 10) & 1023u;
-                e0[u] = (int32_t)((D >> 20) & 63u) - 32 + (int32_t)(q0 % PU) * 4;  // (q0 + T) % PU == q0 % PU
-                const uint32_t rr = e0[u] >= 2 * DW ? 2u : e0[u] >= DW ? 1u : 0u;
-                s0[u] = idx[min(slot + rr, (uint32_t)TR - 1u)];
-                s1[u] = idx[min(slot + rr + 1u, (uint32_t)TR - 1u)];
-                vx[u] = cur[D & 1023u];
-                e0[u] -= (int32_t)(rr * DW);  // the dword within record slot + rr
+                const uint32_t D = Dw[u], p = D & 1023u, slot = (D >> 10) & 511u;
+                o4[u] = ((D >> 19) & 31u) + ((q0 + (uint32_t)u * T) & 3u) * 4u;  // + cneg
+                s0[u] = idx[slot];
+                s1[u] = idx[min(slot + 1u, (uint32_t)TR - 1u)];
+                vx[u] = cur[p];
             }
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
+                const uint32_t D = Dw[u], p = D & 1023u, cneg = (D >> 24) & 15u;
                 const uint32_t b0 = s0[u] * DW, b1 = s1[u] * DW - DW;
 #pragma unroll
                 for (int d = 0; d < 4; ++d) {
-                    const uint32_t e = (uint32_t)max(e0[u] + d, 0);  // (< 0: the owner's piece, not stored)
-                    vw[u][d] = stage[e + (e < (uint32_t)DW ? b0 : b1)];
+                    // dword od = o4 + d - cneg of the unit's records: the carry's below 0 (its
+                    // dword o4 + d), else record slot (slot + 1 from dword 25; od < 50).  The
+                    // choices as masks, so the four reads issue back to back without branches
+                    // (the carry rows addressed from the stage's base)
+                    const uint32_t e = o4[u] + d;
+                    const uint32_t w = e - cneg;
+                    const uint32_t m1 = 0u - (uint32_t)(w >= (uint32_t)DW);
+                    const uint32_t sa = w + (b0 ^ ((b0 ^ b1) & m1));
+                    const uint32_t ca = coff + cx(p, e & 15u);
+                    const uint32_t m2 = 0u - (uint32_t)(e < cneg);
+                    vw[u][d] = stage[sa ^ ((sa ^ ca) & m2)];
                 }
             }
-            // every read of both pieces issued before either store (the stores are predicated,
-            // and the compiler would otherwise sink the second piece's reads behind the first's)
-            asm volatile("" ::"v"(vw[0][0]), "v"(vw[0][1]), "v"(vw[0][2]), "v"(vw[0][3]), "v"(vw[1][0]), "v"(vw[1][1]),
-                         "v"(vw[1][2]), "v"(vw[1][3]), "v"(vx[0]), "v"(vx[1]));
 #pragma unroll
             for (int u = 0; u < 2; ++u) {
-                const uint32_t D = Dw[u], slot = (D >> 10) & 1023u;
-                const int32_t o = (int32_t)((D >> 20) & 63u) - 32 + (int32_t)(q0 % PU) * 4;
-                if (o < 0 || (u == 1 && !live1)) continue;
-                const uint64_t bD = (uint64_t)(vx[u] + slot) * DW + (uint32_t)o;
+                if (!live[u]) continue;
+                const uint32_t D = Dw[u], p = D & 1023u, slot = (D >> 10) & 511u, cneg = (D >> 24) & 15u;
+                const uint64_t bD = (uint64_t)(vx[u] + slot) * DW + o4[u] - cneg;
                 if (SGX_WWC_NOSTORE && bD != ~0ull) {
-                } else if (!((D >> 26) & 1u)) {
+                } else if (!(D >> 28)) {
                     *(u32x4 *)(out + bD) = u32x4{vw[u][0], vw[u][1], vw[u][2], vw[u][3]};
-                } else {  // the output's end (a corrupt count): only the dwords inside it
+                } else {  // the stream's first unit, or the output's end: only the dwords that are ours
+                    const uint64_t startD = (uint64_t)carry[cx(p, 15)] * DW, capD = (uint64_t)olim * DW;
 #pragma unroll
                     for (int d = 0; d < 4; ++d)
-                        if (bD + d < capD) out[bD + d] = vw[u][d];
+                        if (bD + d >= startD && bD + d < capD) out[bD + d] = vw[u][d];
                 }
             }
         }
+#else
+#if SGX_WWC_DRAIN_UNROLL > 1
+#pragma unroll SGX_WWC_DRAIN_UNROLL
+#endif
+        for (uint32_t q = tid; q < npieces; q += T) {
+#if SGX_WWC_DRAIN_V2
+            // dword arithmetic: a piece's 4 dwords are y0..y0+3 of the unit space that starts at
+            // the stream's open unit (u0D); below cbD they are the carry's, else dword od of the
+            // stream's new records in sorted order -- record r = od / 25, dword w = od % 25, one
+            // division per piece (a piece crosses at most one record boundary)
+            const uint32_t D = desc[q >> 2];
+            const uint32_t p = D & 1023u, plo = (D >> 10) & 1023u;
+            const uint32_t y0 = (D >> 20) * 16u + (q & 3u) * 4u;
+            const uint64_t cD = (uint64_t)cur[p] * DW;
+            const uint64_t u0D = cD & ~(uint64_t)15;
+            const uint32_t cbD = (uint32_t)(cD - u0D);
+            const int32_t od0 = (int32_t)y0 - (int32_t)cbD;
+            const uint32_t r = od0 > 0 ? (uint32_t)od0 / (uint32_t)DW : 0u;
+            const uint32_t wd = od0 > 0 ? (uint32_t)od0 - r * DW : 0u;
+            // both records the piece can touch, read up front: every LDS read below has its
+            // address without waiting for another (the record after the last is never used:
+            // whole units end inside the stream's records; its index read stays in the tile)
+            const uint32_t sb0 = (uint32_t)idx[plo + r] * DW;
+            const uint32_t sb1 = (uint32_t)idx[min(plo + r + 1u, (uint32_t)TR - 1u)] * DW;
+            uint32_t vv[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                // dword od0 + d: the carry's below 0, else record r (or r + 1 past its end)
+                const int32_t od = od0 + d;
+                const uint32_t w = (od0 > 0 ? wd : 0u) + (uint32_t)(od0 > 0 ? d : (od > 0 ? od : 0));
+                const uint32_t sa = w < (uint32_t)DW ? sb0 + w : sb1 + w - DW;
+                // (both reads stay in bounds, so either may be speculated: od < 0 only within the
+                // carry's first 15 dwords)
+                vv[d] = od < 0 ? carry[cx(p, (y0 + d) & 15u)] : stage[sa];
+            }
+            const uint64_t bD = u0D + y0;
+            const uint64_t startD = (uint64_t)carry[cx(p, 15)] * DW, capD = (uint64_t)olim * DW;
+            if (bD >= startD && bD + 4 <= capD) {
+                *(u32x4 *)(out + bD) = u32x4{vv[0], vv[1], vv[2], vv[3]};
+            } else {  // the stream's first unit: only its own dwords
+#pragma unroll
+                for (int d = 0; d < 4; ++d)
+                    if (bD + d >= startD && bD + d < capD) out[bD + d] = vv[d];
+            }
+#else
+            const uint32_t D = desc[q >> 2];
+            const uint32_t p = D & 1023u, plo = (D >> 10) & 1023u;
+            const uint32_t rel = (D >> 20) * 64u + (q & 3u) * 16u;
+            const uint64_t cB = (uint64_t)cur[p] * RB;
+            const uint64_t startB = (uint64_t)carry[cx(p, 15)] * RB;
+            const uint64_t u0B = cB & ~(uint64_t)63;
+            const uint32_t cb = (uint32_t)(cB - u0B);
+            uint32_t vv[4];
+#pragma unroll
+            for (int d = 0; d < 4; ++d) {
+                const uint32_t x = rel + 4u * d;
+                if (x < cb) {
+                    vv[d] = carry[cx(p, x >> 2)];
+                } else {
+                    const uint32_t o = x - cb, r = o / 100u;
+                    vv[d] = stage[(uint32_t)idx[plo + r] * DW + ((o - r * 100u) >> 2)];
+                }
+            }
+            const uint64_t b0 = u0B + rel;
+            if (b0 >= startB && b0 + 16 <= capB) {
+                *(u32x4 *)((char *)out + b0) = u32x4{vv[0], vv[1], vv[2], vv[3]};
+            } else {  // the stream's first unit: only its own dwords
+#pragma unroll
+                for (int d = 0; d < 4; ++d) {
+                    const uint64_t b = b0 + 4u * d;
+                    if (b >= startB && b + 4 <= capB) *(uint32_t *)((char *)out + b) = vv[d];
+                }
+            }
+#endif
+        }
+#endif
         WC_STAMP(7);  // drain
-        // ---- the owners: the carried pieces of each closing open unit (on the stream's first
-        //      unit the dwords before its first record are not ours), then the next carry = the
-        //      stream's dwords from the new open unit's start (the last <= 2 records of the
-        //      tile, or, when no unit closed, the old carry and the tile's one record)
+        // the owner's streams: next cursor, and the new open unit = the tail of the tile's last
+        // record of the stream (a record is longer than a unit, so it always closes the old one)
         if (j < NP) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 if (k[h] == 0) continue;
-                const uint64_t cD = (uint64_t)oc[h] * DW, u0D = cD & ~(uint64_t)(UD - 1);
-                const uint32_t cb = (uint32_t)(cD - u0D);
-                if (nu[h] > 0 && cb > 0) {
-                    // the boundary piece's record dwords are the first record's dwords 0..2
-                    const uint32_t s = (uint32_t)idx[sb[h]] * DW;
-                    const uint32_t f0 = stage[s], f1 = stage[s + 1], f2 = stage[s + 2];
-                    const uint64_t startD = (uint64_t)ost[h] * DW;
-                    const bool whole = u0D >= startD && u0D + UD <= capD;
+                const uint64_t cB = (uint64_t)cc[h] * RB, cnB = cB + (uint64_t)RB * k[h];
+                const uint64_t u1B = cnB & ~(uint64_t)63;
+                const uint32_t o = (uint32_t)(u1B - cB) - RB * (k[h] - 1);  // byte of the last record
+                const uint32_t s0 = (uint32_t)idx[sb[h] + k[h] - 1] * DW + (o >> 2);
+                ncnt[h] = (uint32_t)(cnB - u1B) >> 2;
 #pragma unroll
-                    for (int pc = 0; pc < PU; ++pc) {
-                        uint32_t v[4];
-#pragma unroll
-                        for (int d = 0; d < 4; ++d) {
-                            const int dd = 4 * pc + d;
-                            const uint32_t rd = (uint32_t)dd - cb;  // record dword (0..2 in this piece)
-                            const uint32_t fr = rd == 0 ? f0 : rd == 1 ? f1 : f2;
-                            v[d] = dd < CW && (uint32_t)dd < cb ? creg[h][dd < CW ? dd : 0] : fr;
-                        }
-                        const uint64_t b = u0D + 4 * pc;
-                        if ((uint32_t)(4 * pc) >= cb || (SGX_WWC_NOSTORE && b != ~0ull)) {
-                        } else if (whole) {
-                            *(u32x4 *)(out + b) = u32x4{v[0], v[1], v[2], v[3]};
-                        } else {
-#pragma unroll
-                            for (int d = 0; d < 4; ++d)
-                                if (b + d >= startD && b + d < capD) out[b + d] = v[d];
-                        }
-                    }
-                }
-                const uint64_t cnD = cD + (uint64_t)DW * k[h], u1D = cnD & ~(uint64_t)(UD - 1);
-                const uint32_t ncnt = (uint32_t)(cnD - u1D);
-                const int32_t xb = (int32_t)(u1D - cD);  // < 0 only when no unit closed (u1D == u0D)
-                const int32_t lastb = DW * (int32_t)(k[h] - 1);
-                const uint32_t rl = (uint32_t)idx[sb[h] + k[h] - 1] * DW;
-                const uint32_t rp = (uint32_t)idx[sb[h] + (k[h] >= 2 ? k[h] - 2 : 0)] * DW;
-#pragma unroll
-                for (int i = 0; i < CW; ++i) {
-                    const int32_t x = xb + i;  // dword of the stream's new records
-                    const uint32_t a = x >= lastb ? rl + (uint32_t)(x - lastb) : rp + (uint32_t)(x - lastb + DW);
-                    const uint32_t nv = stage[min(a, (uint32_t)(TR * DW - 1))];  // (branch-free)
-                    creg[h][i] = x >= 0 && (uint32_t)i < ncnt ? nv : creg[h][i];
-                }
-                oc[h] += k[h];
-                bad |= oc[h] > olim ? 1u : 0u;
+                for (int i = 0; i < 15; ++i) creg[h][i] = stage[min(s0 + i, (uint32_t)(TR * DW - 1))];
+                ncur[h] = cc[h] + k[h];
+                upd[h] = true;
+                bad |= ncur[h] > olim ? 1u : 0u;
             }
         }
-        WC_STAMP(8);  // owners: carried pieces + next carries
+        WC_STAMP(8);  // owners' next carries
         lds_barrier();
         WC_STAMP(9);  // final barrier
+    };
+    for (int t = 0; t < ntiles; t += 2) {
+        tile(t, ld0, ld1);
+        if (t + 1 < ntiles) tile(t + 1, ld1, ld0);
     }
 #ifdef SGX_WC_STAMPS
     if (lane == 0) {
@@ -2241,26 +2337,22 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
         atomicAdd(&g_wc_stamps[15], 1ull);
     }
 #endif
-    // ---- the chunk's end: every stream's open unit (its own dwords), from the owner
-    if (j < NP) {
+    writeback();
+    __syncthreads();
+    // ---- the chunk's end: every stream's open unit (its own dwords)
+    for (uint32_t p = tid; p < R; p += T) {
+        const uint64_t cB = (uint64_t)cur[p] * RB, u0B = cB & ~(uint64_t)63;
+        const uint64_t startB = (uint64_t)carry[cx(p, 15)] * RB;
+        for (uint64_t b = u0B > startB ? u0B : startB; b < cB; b += 4)
+            if (b + 4 <= capB) *(uint32_t *)((char *)out + b) = carry[cx(p, (uint32_t)((b - u0B) >> 2))];
+    }
+    if constexpr (MODE == WC_PADDED) {
         bool ovf = false;
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            const uint32_t p = 2 * j + h;
-            if (p >= R) continue;
-            const uint64_t cD = (uint64_t)oc[h] * DW, u0D = cD & ~(uint64_t)(UD - 1);
-            const uint64_t startD = (uint64_t)ost[h] * DW;
-#pragma unroll
-            for (int d = 0; d < CW; ++d) {
-                const uint64_t b = u0D + d;
-                if (b < cD && b >= startD && b < capD) out[b] = creg[h][d];
-            }
-            if constexpr (MODE == WC_PADDED) {
-                const int64_t i = (int64_t)p * G + g;
-                const uint32_t cnt = oc[h] - ost[h];
-                pp.pad_cnt[i] = cnt;
-                ovf |= cnt > pp.pad_cap[p];
-            }
+        for (uint32_t p = tid; p < R; p += T) {
+            const int64_t i = (int64_t)p * G + g;
+            const uint32_t cnt = cur[p] - offs[i];
+            pp.pad_cnt[i] = cnt;
+            ovf |= cnt > pp.pad_cap[p];
         }
         if (ovf) atomicOr(err, PAD_OVERFLOW);
     }
