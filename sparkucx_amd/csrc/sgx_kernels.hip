@@ -2135,20 +2135,16 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
                 const uint32_t p = 2 * j + h;
                 const uint64_t cD = (uint64_t)cc[h] * DW, u0D = cD & ~(uint64_t)15;
                 const uint64_t startD = (uint64_t)carry[cx(p, 15)] * DW, capD = (uint64_t)olim * DW;
-                int32_t base = -(int32_t)(cD - u0D);
-                uint32_t r = 0, wv = 0;
-                for (uint32_t i = 0; i < nu[h]; ++i) {
-                    const uint32_t cneg = base < 0 ? (uint32_t)-base : 0u;
-                    const uint32_t slow = ((i == 0 && u0D < startD) || u0D + 16u * (i + 1) > capD) ? 1u : 0u;
-                    desc[ubs[h] + i] = p | ((sb[h] + r) << 10) | (wv << 19) | (cneg << 24) | (slow << 28);
-                    const int32_t nb = base + 16;
-                    if (base < 0) {
-                        wv = nb > 0 ? (uint32_t)nb : 0u;
-                    } else {
-                        wv += 16u;
-                        if (wv >= (uint32_t)DW) wv -= DW, ++r;
-                    }
-                    base = nb;
+                const uint64_t room = capD > u0D ? (capD - u0D) >> 4 : 0;  // whole units before the end
+                const uint32_t ncap = room > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)room;
+                const uint32_t cb = (uint32_t)(cD - u0D), w0 = p | (sb[h] << 10);
+                // unit 0: its first cb dwords are the carry's; units 1.. start in the records
+                desc[ubs[h]] = w0 | (cb << 24) | ((u0D < startD || ncap == 0 ? 1u : 0u) << 28);
+                uint32_t r = 0, wv = 16u - cb;
+                for (uint32_t i = 1; i < nu[h]; ++i) {
+                    desc[ubs[h] + i] = (w0 + (r << 10)) | (wv << 19) | ((i >= ncap ? 1u : 0u) << 28);
+                    wv += 16u;
+                    if (wv >= (uint32_t)DW) wv -= DW, ++r;
                 }
                 cur[p] = cc[h] - sb[h];
             }
