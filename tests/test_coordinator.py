@@ -137,6 +137,9 @@ def executor(rank, world, port, driver_q, my_q, result_dir):
         # sees the failure when it was waiting for that round; one that asks after the failed
         # round has already run (and been forgotten) starts the retry instead, so at least
         # the executor whose request started the round sees it, not necessarily every one.
+        # Which readers see it is pinned deterministically (every reader waiting on the round
+        # when it fails, and the retry is one round) in
+        # test_coordinator_protocol.py::test_every_waiting_reader_sees_the_failed_round_and_the_retry_is_one_round.
         first_error = None
         for attempt in range(3):
             try:
