@@ -1906,6 +1906,13 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 #endif
 // diagnostic probe only (tools/build_variant.sh <tag> - -DSGX_WWC_NOSTORE=1): the drain computes
 // its stores but does not issue them -- the kernel's time without its writes
+// nontemporal unit stores in the drain, as the 16 B kernel's (A/B: -DSGX_WWC_NT=0): whole 64 B
+// units need no L2 merging, and the output streamed past the caches leaves the next map's
+// sample and scan their lines (K4 1.826 -> 1.775 ms, sample 0.038 -> 0.030 ms,
+// profiles/r05w_terasort_nt_ab.jsonl)
+#ifndef SGX_WWC_NT
+#define SGX_WWC_NT 1
+#endif
 #ifndef SGX_WWC_NOSTORE
 #define SGX_WWC_NOSTORE 0
 #endif
@@ -2214,7 +2221,11 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
                 const uint64_t bD = (uint64_t)(vx[u] + slot) * DW + o4[u] - cneg;
                 if (SGX_WWC_NOSTORE && bD != ~0ull) {
                 } else if (!(D >> 28)) {
+#if SGX_WWC_NT
+                    __builtin_nontemporal_store(u32x4{vw[u][0], vw[u][1], vw[u][2], vw[u][3]}, (u32x4 *)(out + bD));
+#else
                     *(u32x4 *)(out + bD) = u32x4{vw[u][0], vw[u][1], vw[u][2], vw[u][3]};
+#endif
                 } else {  // the stream's first unit, or the output's end: only the dwords that are ours
                     const uint64_t startD = (uint64_t)carry[cx(p, 15)] * DW, capD = (uint64_t)olim * DW;
 #pragma unroll
