@@ -244,6 +244,11 @@ __global__ __launch_bounds__(256) void k_ser_tile_info(const uint64_t *__restric
     tp0[t] = (uint32_t)lo;
 }
 
+// nontemporal stream stores, as the map's K4 (A/B: -DSGX_KRYO_NT=0): serialize 2.54 -> 2.51 ms
+// at C1 (profiles/r05x_kryo_nt_ab.jsonl)
+#ifndef SGX_KRYO_NT
+#define SGX_KRYO_NT 1
+#endif
 __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(RecSrc rs, int64_t n,
                                                            uint8_t *__restrict__ out,
                                                            const uint32_t *__restrict__ rec_off, int R,
@@ -342,7 +347,12 @@ __global__ __launch_bounds__(KS_THREADS) void k_kryo_ser16(RecSrc rs, int64_t n,
     for (uint32_t wd = tid; wd < nwords; wd += KS_THREADS) {
         const uint32_t lo = wd * 16u;
         if (lo >= head && lo + 16u <= span) {
+#if SGX_KRYO_NT
+            typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+            __builtin_nontemporal_store(((const v4u *)s_out)[wd], (v4u *)(gbase + lo));
+#else
             *(uint4 *)(gbase + lo) = ((const uint4 *)s_out)[wd];
+#endif
         } else {
             for (uint32_t b = max(lo, head); b < min(lo + 16u, span); ++b) gbase[b] = s_out[b];
         }
