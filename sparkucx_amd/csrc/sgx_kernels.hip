@@ -1153,6 +1153,13 @@ extern "C" int sgx_diag_wc_stamps(unsigned long long *out16, int reset) {
 #ifndef SGX_WC_LINE_RECS
 #define SGX_WC_LINE_RECS 8
 #endif
+// nontemporal tile loads in the 16 B write-combining K4 (A/B: -DSGX_WC_NTLOAD=0): each record
+// is read once, so its lines need not displace the streams' or the next map's in the caches
+// (C1 K4 1.815 -> 1.776 ms, C3 2.461 -> 2.413, 64 batches 1.814 -> 1.787; same box,
+// alternating: profiles/r05yz_ntload_ab.jsonl)
+#ifndef SGX_WC_NTLOAD
+#define SGX_WC_NTLOAD 1
+#endif
 
 __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
     return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 16;  // e, LE, {dw, dt}
@@ -1267,7 +1274,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
             valid[k] = (int64_t)w * NI * 64 + k * 64 + lane < len;
-            rec[k] = valid[k] ? src[k * 64] : u32x4{0, 0, 0, 0};
+            rec[k] = valid[k] ? (SGX_WC_NTLOAD ? __builtin_nontemporal_load(src + k * 64) : src[k * 64]) : u32x4{0, 0, 0, 0};
         }
     }
     __syncthreads();
@@ -1466,7 +1473,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 const int64_t i = nb + (int64_t)w * NI * 64 + k * 64 + lane;
                 valid[k] = i < len;
                 // branch-free: an invalid item re-reads the chunk head
-                rec[k] = cb[valid[k] ? i : 0];
+                rec[k] = SGX_WC_NTLOAD ? __builtin_nontemporal_load(cb + (valid[k] ? i : 0)) : cb[valid[k] ? i : 0];
             }
         }
         lds_barrier();  // B4
@@ -1913,6 +1920,11 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 #ifndef SGX_WWC_NT
 #define SGX_WWC_NT 1
 #endif
+// nontemporal tile loads in the TeraSort K4 (A/B: -DSGX_WWC_NTLOAD=0): K4 1.782 -> 1.775 ms
+// (profiles/r05yz_ntload_ab.jsonl)
+#ifndef SGX_WWC_NTLOAD
+#define SGX_WWC_NTLOAD 1
+#endif
 #ifndef SGX_WWC_NOSTORE
 #define SGX_WWC_NOSTORE 0
 #endif
@@ -2019,7 +2031,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
 #pragma unroll
         for (int i = 0; i < LD; ++i) {
             const int c = i * T + tid;
-            ld[i] = c < nch ? tb[c] : u32x4{0, 0, 0, 0};
+            ld[i] = c < nch ? (SGX_WWC_NTLOAD ? __builtin_nontemporal_load(tb + c) : tb[c]) : u32x4{0, 0, 0, 0};
         }
     };
     if (ntiles > 0) issue(0, ld0);
