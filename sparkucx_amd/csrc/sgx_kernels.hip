@@ -2475,10 +2475,21 @@ __global__ __launch_bounds__(HS_THREADS) void k_hot_select(const uint32_t *__res
     for (int i = 0; i < HS_PER; ++i)
         if ((int)tid * HS_PER + i < R && cnt[i]) atomicAdd(&s_hist[(uint32_t)((uint64_t)cnt[i] * 256 / span)], 1u);
     __syncthreads();
-    if (tid == 0) {  // the lowest bin whose bins above hold >= SPLIT_HOT_CAP partitions
-        uint32_t b = 256, cum = 0;
-        while (b > 0 && cum < (uint32_t)SPLIT_HOT_CAP) cum += s_hist[--b];
-        s_bin = b;
+    // the lowest bin whose bins above hold >= SPLIT_HOT_CAP partitions: the highest bin b whose
+    // suffix sum (bins b..255) reaches the cap, else 0 -- a suffix scan over the 256 bins by the
+    // first four waves (a serial walk of the bins by one thread was most of this kernel)
+    if (tid == 0) s_bin = 0;
+    __syncthreads();
+    if (tid < 256) {
+        const uint32_t hb = s_hist[255 - tid];  // reversed: an inclusive prefix = a suffix sum
+        const uint32_t incl = wave_inclusive_scan(hb, lane);
+        if (lane == 63) s_w[w] = incl;
+        __syncthreads();
+        uint32_t suf = incl;
+        for (uint32_t v = 0; v < w; ++v) suf += s_w[v];
+        if (suf >= (uint32_t)SPLIT_HOT_CAP) atomicMax(&s_bin, 255u - tid);
+    } else {
+        __syncthreads();
     }
     __syncthreads();
     const uint32_t bmin = s_bin;
@@ -2523,21 +2534,25 @@ hipError_t launch_hot_select(const uint32_t *part_off, int R, int Q, uint16_t *s
 // sub-bins; cold super-partitions: sub-bins of a scratch buffer), level 2 one (super, chunk)
 // fragment at a time into the cold partitions' final sub-bins.
 // est1[s] = the cold partitions' sampled counts summed per super-partition.
-__global__ __launch_bounds__(256) void k_cold_super_est(const uint32_t *__restrict__ est,
-                                                        const uint16_t *__restrict__ stream_of, int S, int Q,
-                                                        uint32_t *__restrict__ est1) {
-    const int sidx = (int)(blockIdx.x * 256 + threadIdx.x);
-    if (sidx >= S) return;
+__global__ __launch_bounds__(64) void k_cold_super_est(const uint32_t *__restrict__ est,
+                                                       const uint16_t *__restrict__ stream_of, int S, int Q,
+                                                       uint32_t *__restrict__ est1) {
+    // one wave per super, its Q partitions across the lanes (a serial walk of them per thread
+    // was a chain of dependent loads)
+    const int sidx = (int)blockIdx.x;
+    const uint32_t lane = threadIdx.x;
     uint32_t acc = 0;
-    for (int q = 0; q < Q; ++q)
-        if (stream_of[sidx * Q + q] >= SPLIT_HOT_CAP) acc += est[sidx * Q + q];
-    est1[sidx] = acc;
+    for (int q = (int)lane; q < Q; q += 64)
+        if (stream_of[(int64_t)sidx * Q + q] >= SPLIT_HOT_CAP) acc += est[(int64_t)sidx * Q + q];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) acc += __shfl_xor(acc, d, 64);
+    if (lane == 0) est1[sidx] = acc;
 }
 
 hipError_t launch_cold_super_est(const uint32_t *est, const uint16_t *stream_of, int S, int Q, uint32_t *est1,
                                  hipStream_t stream) {
-    hipLaunchKernelGGL(k_cold_super_est, dim3((unsigned)((S + 255) / 256)), dim3(256), 0, stream, est, stream_of, S, Q,
-                       est1);
+    if (S <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_cold_super_est, dim3((unsigned)S), dim3(64), 0, stream, est, stream_of, S, Q, est1);
     return hipGetLastError();
 }
 
