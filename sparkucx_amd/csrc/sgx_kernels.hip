@@ -2852,6 +2852,10 @@ constexpr int BS_THREADS = 512;
 #ifndef SGX_BS_SUBBIN
 #define SGX_BS_SUBBIN 1
 #endif
+// the bucket region stored nontemporal (A/B: -DSGX_BS_NT=0)
+#ifndef SGX_BS_NT
+#define SGX_BS_NT 1
+#endif
 #ifndef BS_UNROLL
 #define BS_UNROLL 8  // keys compared per step of the rank loop (independent LDS loads; 8 vs 4: sorted 1 GiB 3.67 -> 3.62 ms, profiles/r03_bucket_unroll_ab.jsonl)
 #endif
@@ -3097,8 +3101,10 @@ __global__ __launch_bounds__(BS_THREADS) void k_bucket_sort(const uint32_t *__re
 #endif
     // the bucket region, coalesced: output position L0 + p takes local record perm[p]
     if constexpr (RB == 16) {
-        for (int p = (int)a + (int)tid; p < (int)b; p += BS_THREADS)
-            ((u32x4 *)out)[L0 + p] = ((const u32x4 *)rec)[perm[p]];
+        for (int p = (int)a + (int)tid; p < (int)b; p += BS_THREADS) {
+            if (SGX_BS_NT) __builtin_nontemporal_store(((const u32x4 *)rec)[perm[p]], (u32x4 *)out + L0 + p);
+            else ((u32x4 *)out)[L0 + p] = ((const u32x4 *)rec)[perm[p]];
+        }
     } else {
         for (int u = (int)tid; u < len * DW; u += BS_THREADS) {
             const int p = (int)a + u / DW, q = u % DW;

@@ -35,6 +35,15 @@ constexpr int RT = 256;  // threads per workgroup
 // gather): one read of the records and the outputs' writes.
 // ------------------------------------------------------------------------------------
 constexpr int GT = 256, GI = 16, GTILE = GT * GI;
+// the group outputs (keys, starts, values: the caller's arrays, read after the call) stored
+// nontemporal (A/B: -DSGX_GROUP_NT=0)
+#ifndef SGX_GROUP_NT
+#define SGX_GROUP_NT 1
+#endif
+__device__ __forceinline__ void gst(int64_t *p, int64_t v) {
+    if (SGX_GROUP_NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 // LDS slot of tile record j: one pad element per GI, so a thread's contiguous run (stride
 // GI + 1 elements between lanes) does not put every lane on the same banks
 __device__ __forceinline__ int gslot(int j) { return j + j / GI; }
@@ -90,7 +99,7 @@ __global__ __launch_bounds__(GT) void k_group_fused(const ulonglong2 *__restrict
             const ulonglong2 r = rec[i];
             s_key[gslot(k * GT + tid)] = r.x;
             if constexpr (SUM) s_val[gslot(k * GT + tid)] = r.y;
-            else vals[i] = (int64_t)r.y;
+            else gst(vals + i, (int64_t)r.y);
         }
     }
     if (tid == 0) s_prev = t0 > 0 ? rec[t0 - 1].x : 0ull;
@@ -226,10 +235,10 @@ __global__ __launch_bounds__(GT) void k_group_fused(const ulonglong2 *__restrict
     __syncthreads();
     const uint32_t ngt = (uint32_t)tagg.c;
     for (uint32_t q = tid; q < ngt; q += GT) {
-        keys[gt0 + q] = (int64_t)s_gkey[q];
-        if (starts) starts[gt0 + q] = t0 + s_st[q];
+        gst(keys + gt0 + q, (int64_t)s_gkey[q]);
+        if (starts) gst(starts + gt0 + q, t0 + (int64_t)s_st[q]);
         if constexpr (SUM)
-            if (q + 1 < ngt) vals[gt0 + q] = (int64_t)s_gsum[q];  // (the tile's last group is still open)
+            if (q + 1 < ngt) gst(vals + gt0 + q, (int64_t)s_gsum[q]);  // (the tile's last group is still open)
     }
 }
 
