@@ -1891,28 +1891,10 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 #ifndef SGX_WIDE_WC_TWOPASS
 #define SGX_WIDE_WC_TWOPASS 1
 #endif
-#ifndef SGX_WWC_DRAIN_UNROLL
-#define SGX_WWC_DRAIN_UNROLL 2
-#endif
-// the drain in dword arithmetic, one division per piece (A/B: -DSGX_WWC_DRAIN_V2=0)
-#ifndef SGX_WWC_DRAIN_V2
-#define SGX_WWC_DRAIN_V2 1
-#endif
-// the drain's units carry their first record slot and dword (no cursor read, no division on
-// the piece's path), two pieces in flight per thread (A/B: -DSGX_WWC_DRAIN_V3=0)
-#ifndef SGX_WWC_DRAIN_V3
-#define SGX_WWC_DRAIN_V3 1
-#endif
-// tiles of loads in flight per workgroup (A/B: -DSGX_WWC_PREFETCH=1)
-#ifndef SGX_WWC_PREFETCH
-#define SGX_WWC_PREFETCH 1
-#endif
 // XOR-swizzled carry rows (A/B: -DSGX_WWC_SWIZZLE=0)
 #ifndef SGX_WWC_SWIZZLE
 #define SGX_WWC_SWIZZLE 1
 #endif
-// diagnostic probe only (tools/build_variant.sh <tag> - -DSGX_WWC_NOSTORE=1): the drain computes
-// its stores but does not issue them -- the kernel's time without its writes
 // nontemporal unit stores in the drain, as the 16 B kernel's (A/B: -DSGX_WWC_NT=0): whole 64 B
 // units need no L2 merging, and the output streamed past the caches leaves the next map's
 // sample and scan their lines (K4 1.826 -> 1.775 ms, sample 0.038 -> 0.030 ms,
@@ -1925,6 +1907,8 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 #ifndef SGX_WWC_NTLOAD
 #define SGX_WWC_NTLOAD 1
 #endif
+// diagnostic probe only (tools/build_variant.sh <tag> - -DSGX_WWC_NOSTORE=1): the drain computes
+// its stores but does not issue them -- the kernel's time without its writes
 #ifndef SGX_WWC_NOSTORE
 #define SGX_WWC_NOSTORE 0
 #endif
@@ -2022,8 +2006,9 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
         carry[cx(p, 15)] = c0;  // the stream's first record: bytes before it are not ours
     }
 
-    // the tile loads in registers, SGX_WWC_PREFETCH tiles ahead (2: two buffers, the tile loop
-    // unrolled by two so that each buffer is named statically)
+    // the next tile's loads in registers, two named buffers taking turns (the tile loop is
+    // unrolled by two; a second tile in flight made hipcc wait vmcnt(0) at every landing, behind
+    // the drain's stores, and bought nothing)
     u32x4 ld0[LD], ld1[LD];
     auto issue = [&](int t, u32x4(&ld)[LD]) __attribute__((always_inline)) {
         const u32x4 *tb = (const u32x4 *)(cin + (int64_t)t * TR * RB);
@@ -2035,9 +2020,6 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
         }
     };
     if (ntiles > 0) issue(0, ld0);
-#if SGX_WWC_PREFETCH > 1
-    if (ntiles > 1) issue(1, ld1);
-#endif
     uint32_t bad = 0;
 #ifdef SGX_WC_STAMPS
     uint64_t st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
@@ -2086,11 +2068,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
         lds_barrier();
 #endif
         WC_STAMP(2);  // land the tile (its loads' wait) + barrier
-#if SGX_WWC_PREFETCH > 1
-        if (t + 2 < ntiles) issue(t + 2, ld);
-#else
         if (t + 1 < ntiles) issue(t + 1, ldn);
-#endif
         WC_STAMP(3);  // issue the next tile's loads
         // ---- partition id + rank (record tid: input order = thread order)
         const bool valid = tid < (uint32_t)nrec;
@@ -2141,7 +2119,6 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             const uint32_t L = sb[0] | (sb[1] << 16);
 #pragma unroll
             for (int v = 0; v < W; ++v) ((uint32_t *)(rows + (size_t)v * RS))[j] = before[v] + L;
-#if SGX_WWC_DRAIN_V3
             // unit i of stream p starts at dword 16 i - cbD of the stream's new records: below 0
             // (unit 0 only) its first cneg dwords are the carry's, else record slot sb + r, dword
             // w.  desc = p | slot << 10 | w << 19 | cneg << 24 | slow << 28, slow: the unit holds
@@ -2167,11 +2144,6 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
                 }
                 cur[p] = cc[h] - sb[h];
             }
-#else
-#pragma unroll
-            for (int h = 0; h < 2; ++h)
-                for (uint32_t i = 0; i < nu[h]; ++i) desc[ubs[h] + i] = (2 * j + h) | (sb[h] << 10) | (i << 20);
-#endif
         }
         WC_STAMP(12);  // merge: rows + unit words written
         lds_barrier();
@@ -2184,7 +2156,6 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
         //      stream p: its carry below cb (the open unit's bytes), else byte x - cb of the
         //      stream's records in sorted order
         const uint32_t npieces = (total >> 16) * 4u;
-#if SGX_WWC_DRAIN_V3
         // two pieces per step, each phase issued for both before its results are used: the
         // unit word; then the two index slots (and carry dwords); then the 4 data dwords
         const uint32_t coff = (uint32_t)(carry - stage);
@@ -2246,82 +2217,6 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
                 }
             }
         }
-#else
-#if SGX_WWC_DRAIN_UNROLL > 1
-#pragma unroll SGX_WWC_DRAIN_UNROLL
-#endif
-        for (uint32_t q = tid; q < npieces; q += T) {
-#if SGX_WWC_DRAIN_V2
-            // dword arithmetic: a piece's 4 dwords are y0..y0+3 of the unit space that starts at
-            // the stream's open unit (u0D); below cbD they are the carry's, else dword od of the
-            // stream's new records in sorted order -- record r = od / 25, dword w = od % 25, one
-            // division per piece (a piece crosses at most one record boundary)
-            const uint32_t D = desc[q >> 2];
-            const uint32_t p = D & 1023u, plo = (D >> 10) & 1023u;
-            const uint32_t y0 = (D >> 20) * 16u + (q & 3u) * 4u;
-            const uint64_t cD = (uint64_t)cur[p] * DW;
-            const uint64_t u0D = cD & ~(uint64_t)15;
-            const uint32_t cbD = (uint32_t)(cD - u0D);
-            const int32_t od0 = (int32_t)y0 - (int32_t)cbD;
-            const uint32_t r = od0 > 0 ? (uint32_t)od0 / (uint32_t)DW : 0u;
-            const uint32_t wd = od0 > 0 ? (uint32_t)od0 - r * DW : 0u;
-            // both records the piece can touch, read up front: every LDS read below has its
-            // address without waiting for another (the record after the last is never used:
-            // whole units end inside the stream's records; its index read stays in the tile)
-            const uint32_t sb0 = (uint32_t)idx[plo + r] * DW;
-            const uint32_t sb1 = (uint32_t)idx[min(plo + r + 1u, (uint32_t)TR - 1u)] * DW;
-            uint32_t vv[4];
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                // dword od0 + d: the carry's below 0, else record r (or r + 1 past its end)
-                const int32_t od = od0 + d;
-                const uint32_t w = (od0 > 0 ? wd : 0u) + (uint32_t)(od0 > 0 ? d : (od > 0 ? od : 0));
-                const uint32_t sa = w < (uint32_t)DW ? sb0 + w : sb1 + w - DW;
-                // (both reads stay in bounds, so either may be speculated: od < 0 only within the
-                // carry's first 15 dwords)
-                vv[d] = od < 0 ? carry[cx(p, (y0 + d) & 15u)] : stage[sa];
-            }
-            const uint64_t bD = u0D + y0;
-            const uint64_t startD = (uint64_t)carry[cx(p, 15)] * DW, capD = (uint64_t)olim * DW;
-            if (bD >= startD && bD + 4 <= capD) {
-                *(u32x4 *)(out + bD) = u32x4{vv[0], vv[1], vv[2], vv[3]};
-            } else {  // the stream's first unit: only its own dwords
-#pragma unroll
-                for (int d = 0; d < 4; ++d)
-                    if (bD + d >= startD && bD + d < capD) out[bD + d] = vv[d];
-            }
-#else
-            const uint32_t D = desc[q >> 2];
-            const uint32_t p = D & 1023u, plo = (D >> 10) & 1023u;
-            const uint32_t rel = (D >> 20) * 64u + (q & 3u) * 16u;
-            const uint64_t cB = (uint64_t)cur[p] * RB;
-            const uint64_t startB = (uint64_t)carry[cx(p, 15)] * RB;
-            const uint64_t u0B = cB & ~(uint64_t)63;
-            const uint32_t cb = (uint32_t)(cB - u0B);
-            uint32_t vv[4];
-#pragma unroll
-            for (int d = 0; d < 4; ++d) {
-                const uint32_t x = rel + 4u * d;
-                if (x < cb) {
-                    vv[d] = carry[cx(p, x >> 2)];
-                } else {
-                    const uint32_t o = x - cb, r = o / 100u;
-                    vv[d] = stage[(uint32_t)idx[plo + r] * DW + ((o - r * 100u) >> 2)];
-                }
-            }
-            const uint64_t b0 = u0B + rel;
-            if (b0 >= startB && b0 + 16 <= capB) {
-                *(u32x4 *)((char *)out + b0) = u32x4{vv[0], vv[1], vv[2], vv[3]};
-            } else {  // the stream's first unit: only its own dwords
-#pragma unroll
-                for (int d = 0; d < 4; ++d) {
-                    const uint64_t b = b0 + 4u * d;
-                    if (b >= startB && b + 4 <= capB) *(uint32_t *)((char *)out + b) = vv[d];
-                }
-            }
-#endif
-        }
-#endif
         WC_STAMP(7);  // drain
         // the owner's streams: next cursor, and the new open unit = the tail of the tile's last
         // record of the stream (a record is longer than a unit, so it always closes the old one)
