@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--flags", type=int, default=0, help="sgx_config.flags (FLAG_*)")
     ap.add_argument("--record-bytes", type=int, default=16, choices=[16, 100])
     ap.add_argument("--batches", type=int, default=1, help="> 1: map_begin / append (retained slices) / commit")
+    ap.add_argument("--slots", type=int, default=2, help="map ids the writes cycle through (bench.py: 2)")
     ap.add_argument("--per-launch", action="store_true",
                     help="print every write's stage events (PER_LAUNCH json), each write alone on the GPU")
     a = ap.parse_args()
@@ -57,14 +58,14 @@ def main():
             e.sync()
             e.stats_reset()
         if a.batches <= 1:
-            e.write_map(1, i & 1, buf, a.records, a.record_bytes)
+            e.write_map(1, i % a.slots, buf, a.records, a.record_bytes)
         else:
-            e.map_begin(1, i & 1)
+            e.map_begin(1, i % a.slots)
         for j in range(a.batches if a.batches > 1 else 0):
-            e.map_append(1, i & 1, buf, cuts[j + 1] - cuts[j], a.record_bytes, offset=cuts[j] * a.record_bytes,
+            e.map_append(1, i % a.slots, buf, cuts[j + 1] - cuts[j], a.record_bytes, offset=cuts[j] * a.record_bytes,
                          retained=True)
         if a.batches > 1:
-            e.map_commit(1, i & 1)
+            e.map_commit(1, i % a.slots)
         if a.per_launch:
             e.sync()
             st = e.stats()
