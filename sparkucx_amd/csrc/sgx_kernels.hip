@@ -2058,7 +2058,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             const uint32_t *tb = (const uint32_t *)(cin + (int64_t)t * TR * RB);
             for (int d = tid; d < nrec * DW; d += T) stage[d] = tb[d];
         }
-        for (uint32_t i = tid; i < (uint32_t)W * RS / 2; i += T) ((uint32_t *)rows)[i] = 0u;
+        for (uint32_t i = tid; i < (uint32_t)W * RS / 8; i += T) ((u32x4 *)rows)[i] = u32x4{0, 0, 0, 0};
         // SGX_WWC_LAND_SYNC=0: an LDS-only barrier, so the last drain's global stores stay in
         // flight through this tile's ranking (the tile's loads are waited for where their
         // registers are used)
