@@ -50,8 +50,10 @@ enum sgx_partitioner {
 };
 
 /* Where a caller buffer lives.  SGX_MEM_DEVICE_RETAINED (sgx_map_append only): device memory
- * the caller keeps valid and unchanged until sgx_map_commit returns -- the commit reads the
- * batch in place (no copy); elsewhere it means SGX_MEM_DEVICE. */
+ * the caller keeps valid and unchanged until the map's partition lengths are known -- an
+ * sgx_map_commit given out_partition_lengths has returned, or sgx_map_lengths / sgx_sync has
+ * returned after an asynchronous commit -- because the commit's kernels read the batch in place
+ * (no copy); elsewhere it means SGX_MEM_DEVICE. */
 enum sgx_mem_kind { SGX_MEM_HOST = 0, SGX_MEM_DEVICE = 1, SGX_MEM_DEVICE_RETAINED = 2 };
 
 typedef struct sgx_engine sgx_engine;
@@ -246,7 +248,7 @@ int sgx_map_lengths(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *
  * ucx/NvkvShuffleMapOutputWriter.scala:106-113,228-246).  sgx_map_begin opens the map.
  * sgx_map_append hands over one batch: a host batch is copied into HBM, a SGX_MEM_DEVICE
  * batch is copied within HBM, a SGX_MEM_DEVICE_RETAINED batch stays where it is (the caller
- * keeps it until the commit returns).  sgx_map_commit then partitions ALL batches in one
+ * keeps it until the map's lengths are known: see sgx_mem_kind).  sgx_map_commit then partitions ALL batches in one
  * pass, exactly as sgx_write_map partitions one contiguous batch (the padded single-pass
  * write when sgx_write_map would take it): every batch is cut into chunks of
  * its own and a chunk table replaces the contiguous input.  The result is byte-identical to
@@ -428,6 +430,11 @@ int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t *map_ids, 
                      int32_t start_partition, int32_t end_partition, int32_t agg, int64_t *keys,
                      int64_t *group_starts, int64_t *values, int64_t cap_groups, int64_t cap_values,
                      int32_t mem_kind, int64_t *out_groups, int64_t *out_values);
+/* The records the calling thread's last sgx_read_records / _sorted / _grouped consumed, before
+ * any aggregation: the reference's reader counts incRecordsRead once per shuffled record ahead
+ * of combineValuesByKey / combineCombinersByKey (spark_3_0/UcxShuffleReader.scala:148-162), so
+ * an aggregated read reports these, not its groups. */
+int sgx_last_read_records(sgx_engine *e, int64_t *out_records);
 
 /* ---- RangePartitioner's bounds from the data (Spark 3.0.1 RangePartitioner: the
  *      rangeBounds initialiser, RangePartitioner.sketch and RangePartitioner.determineBounds;

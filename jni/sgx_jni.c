@@ -258,7 +258,7 @@ JNIEXPORT jlongArray JNICALL JNI_FN(checkIndexAndData)(JNIEnv *env, jclass c, js
 JNIEXPORT jlongArray JNICALL JNI_FN(indexBlockRange)(JNIEnv *env, jclass c, jstring index, jint start, jint end) {
     (void)c;
     const char *ip = (*env)->GetStringUTFChars(env, index, NULL);
-    int64_t r[2] = {0, 0};
+    int64_t r[3] = {0, 0, 0};
     jlongArray out = NULL;
     if (ip && !check(env, sgx_index_block_range(ip, start, end, &r[0], &r[1]))) out = long_array(env, r, 2);
     if (ip) (*env)->ReleaseStringUTFChars(env, index, ip);
@@ -469,8 +469,9 @@ JNIEXPORT jlong JNICALL JNI_FN(readSorted)(JNIEnv *env, jclass c, jlong e, jint 
     return check(env, rc) ? -1 : bytes;
 }
 
-/* readGrouped: {groups, values}; agg 0 = groupByKey (keys, groupStarts, values), 1 = sum
- * (keys, sums in values).  Null buffers with their capacities 0 = size query. */
+/* readGrouped: {groups, values, records}; agg 0 = groupByKey (keys, groupStarts, values), 1 = sum
+ * (keys, sums in values); records = the shuffled records the aggregation consumed (the reader's
+ * incRecordsRead).  Null buffers with their capacities 0 = size query. */
 JNIEXPORT jlongArray JNICALL JNI_FN(readGrouped)(JNIEnv *env, jclass c, jlong e, jint sid, jlongArray maps,
                                                  jint start, jint end, jint agg, jobject keys, jobject starts,
                                                  jobject values) {
@@ -481,12 +482,12 @@ JNIEXPORT jlongArray JNICALL JNI_FN(readGrouped)(JNIEnv *env, jclass c, jlong e,
     jsize n;
     int64_t *m = map_list(env, maps, &n);
     if (!m) return NULL;
-    int64_t r[2] = {0, 0};
+    int64_t r[3] = {0, 0, 0};
     /* group_starts receives as many entries as keys: the smaller buffer bounds both */
     const int64_t cap_groups = kp ? (sp && sc < kc ? sc : kc) / 8 : 0, cap_values = vp ? vc / 8 : 0;
     const int rc = sgx_read_grouped(E(e), sid, m, n, start, end, agg, (int64_t *)kp, (int64_t *)sp, (int64_t *)vp,
                                     cap_groups, cap_values, SGX_MEM_HOST, &r[0], &r[1]);
     free(m);
-    if (check(env, rc)) return NULL;
-    return long_array(env, r, 2);
+    if (check(env, rc) || check(env, sgx_last_read_records(E(e), &r[2]))) return NULL;
+    return long_array(env, r, 3);
 }

@@ -82,7 +82,7 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
    *  hand over (groups and values for an aggregation, bytes otherwise). */
   private def readSize(maps: Array[Long], a: Int, b: Int): Long =
     if (handle.agg != GpuUcxShuffleManager.NO_AGG) {
-      val Array(groups, values) = SgxNative.readGrouped(engine, shuffleId, maps, a, b, handle.agg, null, null, null)
+      val Array(groups, values, _) = SgxNative.readGrouped(engine, shuffleId, maps, a, b, handle.agg, null, null, null)
       8 * math.max(groups, values)
     } else if (dep.keyOrdering.isDefined) SgxNative.readSorted(engine, shuffleId, maps, a, b, null)
     else SgxNative.readRecords(engine, shuffleId, maps, a, b, null)
@@ -130,8 +130,10 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
       readMetrics.incLocalBytesRead(bytes)
       chunked(maps)
     } else readRemote(maps, coordinator.get)
+    // one per shuffled record; behind an aggregator readOnGpu counts the records it consumed
+    val aggregated = handle.agg != GpuUcxShuffleManager.NO_AGG
     val counted = CompletionIterator[Product2[K, C], Iterator[Product2[K, C]]](
-      records.map { r => readMetrics.incRecordsRead(1); r },
+      if (aggregated) records else records.map { r => readMetrics.incRecordsRead(1); r },
       context.taskMetrics().mergeShuffleReadMetrics())
     new InterruptibleIterator[Product2[K, C]](context, counted)
   }
@@ -139,9 +141,12 @@ class GpuShuffleReader[K, C](engine: Long, handle: GpuShuffleHandle[K, _, C], st
   private def readOnGpu(maps: Array[Long], a: Int, b: Int): Iterator[Product2[K, C]] = {
     if (handle.agg != GpuUcxShuffleManager.NO_AGG) {
       val sum = handle.agg == SgxNative.AGG_SUM
-      val Array(groups, values) = SgxNative.readGrouped(engine, shuffleId, maps, a, b, handle.agg, null, null, null)
+      val Array(groups, values, _) = SgxNative.readGrouped(engine, shuffleId, maps, a, b, handle.agg, null, null, null)
       val keys = le(groups * 8); val starts = le(groups * 8); val vals = le(values * 8)
-      SgxNative.readGrouped(engine, shuffleId, maps, a, b, handle.agg, keys, starts, vals)
+      val Array(_, _, consumed) = SgxNative.readGrouped(engine, shuffleId, maps, a, b, handle.agg, keys, starts, vals)
+      // the reference counts every shuffled record ahead of the aggregator, not its groups
+      // (spark_3_0/UcxShuffleReader.scala:148-162)
+      readMetrics.incRecordsRead(consumed)
       val k = keys.asLongBuffer(); val s = starts.asLongBuffer(); val v = vals.asLongBuffer()
       if (sum) {
         Iterator.tabulate(groups.toInt)(g => (k.get(g), v.get(g)).asInstanceOf[Product2[K, C]])

@@ -143,6 +143,7 @@ SIGNATURES = {
     "sgx_bootstrap_join": (ctypes.c_int, [ctypes.c_char_p, _i32, _i32, _i32, _vp, _vp]),
     "sgx_read_grouped": (ctypes.c_int, [_vp, _i32, _vp, _i64, _i32, _i32, _i32, _vp, _vp, _vp, _i64, _i64, _i32,
                                         _vp, _vp]),
+    "sgx_last_read_records": (ctypes.c_int, [_vp, _vp]),
     "sgx_progress": (ctypes.c_int, [_vp]),
     "sgx_sync": (ctypes.c_int, [_vp]),
     "sgx_stats_reset": (ctypes.c_int, [_vp]),
@@ -164,6 +165,10 @@ SIGNATURES = {
 }
 
 
+# tools/ab_run.py only: bind what an older engine build exports (its missing calls are unused)
+ALLOW_MISSING = False
+
+
 def lib() -> ctypes.CDLL:
     """Load the in-tree libsgx.so (raises if it was not built: no CPU fallback)."""
     global _lib
@@ -179,6 +184,8 @@ def lib() -> ctypes.CDLL:
             if L.sgx_abi_version() != ABI_VERSION:
                 raise ImportError(f"{LIB_PATH} has ABI {L.sgx_abi_version()}, the bindings expect {ABI_VERSION}: rebuild")
             for name, (res, args) in SIGNATURES.items():
+                if ALLOW_MISSING and not hasattr(L, name):
+                    continue  # an older build under A/B measurement (tools/ab_run.py)
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args

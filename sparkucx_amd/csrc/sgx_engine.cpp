@@ -24,13 +24,21 @@ using namespace sgx;
 // ------------------------------------------------------------------------------------
 // contexts, events, stats
 // ------------------------------------------------------------------------------------
+#ifndef SGX_TAIL_LOW_PRIORITY
+#define SGX_TAIL_LOW_PRIORITY 0
+#endif
+
 Ctx *sgx_engine::ctx() {
     std::lock_guard<std::mutex> lk(reg_mu);
     auto &slot = ctxs[std::this_thread::get_id()];
     if (!slot) {
         std::unique_ptr<Ctx> c(new Ctx());
-        if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess ||
-            hipStreamCreateWithFlags(&c->st_tail, hipStreamNonBlocking) != hipSuccess) {
+        // (A/B: -DSGX_TAIL_LOW_PRIORITY=1 puts the padded write's tail on a low-priority
+        // stream, so the next write's sample and K4 are dispatched ahead of it)
+        int lo = 0, hi = 0;
+        if (!SGX_TAIL_LOW_PRIORITY || hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) lo = hi = 0;
+        if (hipStreamCreateWithPriority(&c->st, hipStreamNonBlocking, hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&c->st_tail, hipStreamNonBlocking, lo) != hipSuccess) {
             ctxs.erase(std::this_thread::get_id());
             fail_msg(SGX_ERR_HIP, "hipStreamCreate failed for a new calling thread");
             return nullptr;

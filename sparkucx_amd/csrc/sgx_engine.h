@@ -286,6 +286,8 @@ struct Ctx {
     DevBuf offs, work;
     DevBuf split_work, split_tmp;  // R > 1024: the two-level split scatter's scratch and level-1 output
     DevBuf input_stage;
+    // pre-aggregation records of the last read on this thread (sgx_last_read_records)
+    int64_t last_read_records = 0;
     const uint32_t *last_off_dev = nullptr;  // device (R+1) record offsets of the last partition pass
     // The padded write's tail (its scan, the guarded two-pass fallback, the offsets' copy to the
     // host) runs on a second stream so that the next write's kernels do not queue behind it;
@@ -293,8 +295,26 @@ struct Ctx {
     // that last read it has run (pad_done)
     hipStream_t st_tail = nullptr;
     DevBuf pad_work[2], pad_offs[2];
+    // 16 B padded writes: the sample's block per slot ([est][K4 flags][layout]), how many of its
+    // leading bytes the slot's last tail left zeroed (its next sample needs them zero), and the
+    // event behind that reset (the next write on the slot waits for it, not for the whole tail)
+    DevBuf pad_crit[2];
+    size_t pad_crit_zeroed[2] = {0, 0};
+    Event pad_free[2];
     Event pad_done[2];
     int pad_slot = 0, tail_slot = -1;
+    // Host records into input_stage on stream `s`, behind the last padded-write tail: its
+    // guarded fallback still reads its map's input, which may be this buffer (a growth waits
+    // for that tail on the host, since the old allocation is freed).
+    int stage_input(const void *src, size_t bytes, hipStream_t s, const void **out) {
+        const hipEvent_t tail = tail_slot >= 0 ? pad_done[tail_slot].ev : nullptr;
+        if (tail && bytes > input_stage.cap) HIP_TRY(hipEventSynchronize(tail));
+        SGX_TRY(input_stage.ensure(bytes));
+        if (tail) HIP_TRY(hipStreamWaitEvent(s, tail, 0));
+        HIP_TRY(hipMemcpyAsync(input_stage.p, src, bytes, hipMemcpyHostToDevice, s));
+        *out = input_stage.p;
+        return SGX_OK;
+    }
     // reduce side and map-side combine
     DevBuf kryo_in, kryo_work, sort_buf[2], sort_err, grp_status, grp_out;
     DevBuf digit_hist, items_dev, gather_stage, fetch_tmp, comb_buf;

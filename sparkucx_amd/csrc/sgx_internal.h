@@ -37,6 +37,15 @@ struct PartParams {
     // against pad_cap[p] (the sub-bin capacity of partition p); an overflow sets PAD_OVERFLOW
     uint32_t *pad_cnt;
     const uint32_t *pad_cap;
+    // K4 padded, sub-bins laid out by K4 itself (pad_est non-null, 16 B write-combining K4):
+    // every workgroup turns the sampled counts est[R] into capacities cap[p] (mu = est * scale,
+    // cap = mu + PAD_SIGMAS * sqrt(a * mu + 16) + 8, a whole line) and bases pbase[p] =
+    // sum_{q<p} G cap[q]; stream (p, g) starts at min(pbase[p] + g cap[p], olim); workgroup 0
+    // publishes {cap[R], pbase[R]} in pad_layout; the epilogue writes every stream's END
+    // position to pad_cnt (k_pad_finish turns them into counts and checks the capacities)
+    const uint32_t *pad_est;
+    uint32_t *pad_layout;
+    double pad_scale, pad_a;
     // ---- streaming map (sgx_map_append batches written in one pass at sgx_map_commit) ----
     // chunk table: chunk g's records start at byte chunks[2g] from the kernel's input pointer
     // and number chunks[2g+1] (every chunk inside one batch); null: chunk g = records
@@ -143,6 +152,22 @@ int64_t scan_tiles(int64_t len);
 // (pp.chunks, a streaming map) each of the G chunks (<= `chunk` records) is sampled on its own.
 hipError_t launch_pad_sample(const void *in, int64_t n, int rb, int stride, const PartParams &pp, uint32_t *est,
                              hipStream_t stream, int64_t chunk = 0, int G = 0);
+// The tail of a padded write whose K4 laid its sub-bins out itself (PartParams.pad_est):
+// fstart[i] = min(pbase[p] + g cap[p], olim) from the published layout ([R] caps, [R] bases),
+// cnt[i] = the end position K4 left there - fstart[i]; a count above its capacity sets
+// PAD_OVERFLOW in *flags.  Also zeroes `zero` (nzero u32: the scan's ticket / status, its
+// error word) for the kernels that follow on the stream.
+hipError_t launch_pad_finish(const uint32_t *layout, int R, int G, uint32_t olim, uint32_t *fstart, uint32_t *cnt,
+                             uint32_t *flags, uint32_t *zero, int64_t nzero, hipStream_t stream);
+// *flags_out = *flags; then est[R], *flags = 0 (the slot's next sample and K4 start from zero).
+hipError_t launch_pad_reset(uint32_t *flags, uint32_t *flags_out, uint32_t *est, int R, hipStream_t stream);
+// The padded 16 B write's overflow fallback (a no-op unless *guard has PAD_OVERFLOW): the
+// map's records into the contiguous layout, stream (p, g) from foff[p*G+g] on, stably, one
+// wave per chunk and no LDS -- so its no-op launch takes no CU away from the next map's K4.
+// cur: R*G u32 of scratch (the streams' cursors).
+hipError_t launch_scatter16_fallback(const void *in, void *out, int64_t n, int64_t chunk, int G, const PartParams &pp,
+                                     const uint32_t *foff, uint32_t *cur, const uint32_t *guard, uint32_t *err,
+                                     hipStream_t stream);
 // (partition, spill) segment offsets of a streaming map committed in one pass (k_spill_seg_offs).
 hipError_t launch_spill_seg_offs(const uint32_t *offs, const uint32_t *part_off, int R, int G, int S,
                                  const int32_t *g0, uint32_t *out, hipStream_t stream);

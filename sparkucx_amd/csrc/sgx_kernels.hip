@@ -1161,6 +1161,71 @@ extern "C" int sgx_diag_wc_stamps(unsigned long long *out16, int reset) {
 #define SGX_WC_NTLOAD 1
 #endif
 
+// Sub-bin capacity of a partition from its sampled count: mu = est * chunk / sampled records
+// expected per chunk, cap = mu + PAD_SIGMAS * sqrt(a * mu + 16) + 8 (a = 1 + chunk / sampled:
+// the chunk's Poisson spread plus the estimate's), rounded up to a whole 128 B line.
+__device__ __forceinline__ uint32_t pad_cap_of(uint32_t est, double scale, double a) {
+    const double mu = (double)est * scale;
+    const double c = mu + PAD_SIGMAS * sqrt(a * mu + 16.0) + 8.0;
+    return ((uint32_t)ceil(c) + 7u) & ~7u;
+}
+
+__device__ __forceinline__ uint64_t shfl_up64(uint64_t x, int d) {
+    const uint32_t lo = __shfl_up((uint32_t)x, d, 64), hi = __shfl_up((uint32_t)(x >> 32), d, 64);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+// A padded write's sub-bin layout, computed by each workgroup of its K4 from the sampled counts
+// (PartParams.pad_est; the same numbers k_pad_caps computes for the split): stream (p, g) of
+// this workgroup's chunk g starts at min(pbase[p] + g cap[p], olim) -> pe[p], ple[p] (p < RS,
+// 0 past R).  Workgroup 0 publishes {cap[R], pbase[R]} (pp.pad_layout) for the write's tail
+// and flags a layout larger than olim.  RS <= 2 T.  scratch: T / 64 u64 of LDS.  Ends with a
+// barrier.
+template <int T>
+__device__ void pad_layout_starts(const PartParams &pp, uint32_t R, uint32_t RS, int g, int G, uint32_t *pe,
+                                  uint32_t *ple, uint64_t *scratch, uint32_t *err) {
+    const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    uint32_t cap[2];
+    uint64_t sum = 0;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t p = 2 * tid + k;
+        cap[k] = p < R ? pad_cap_of(pp.pad_est[p], pp.pad_scale, pp.pad_a) : 0u;
+        sum += (uint64_t)cap[k] * (uint64_t)G;
+    }
+    uint64_t x = sum;  // inclusive scan over the wave, then over the waves' totals
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t y = shfl_up64(x, d);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    if (lane == 63) scratch[w] = x;
+    __syncthreads();
+    uint64_t run = x - sum, total = 0;
+#pragma unroll
+    for (int v = 0; v < T / 64; ++v) {
+        const uint64_t y = scratch[v];
+        if (v < (int)w) run += y;
+        total += y;
+    }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const uint32_t p = 2 * tid + k;
+        if (p < RS) {
+            const uint32_t c0 = p < R ? (uint32_t)min<uint64_t>(run + (uint64_t)g * cap[k], (uint64_t)pp.olim) : 0u;
+            pe[p] = c0;
+            ple[p] = c0;
+            if (g == 0 && p < R) {
+                pp.pad_layout[p] = cap[k];
+                pp.pad_layout[R + p] = (uint32_t)min<uint64_t>(run, (uint64_t)pp.olim);
+            }
+        }
+        run += (uint64_t)cap[k] * (uint64_t)G;
+    }
+    if (g == 0 && tid == 0 && total > (uint64_t)pp.olim) atomicOr(err, PAD_OVERFLOW);
+    __syncthreads();
+}
+
 __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
     return (size_t)waves * 64 * si * 16 + (size_t)waves * rs8(R) * 2 + (size_t)rs8(R) * 16;  // e, LE, {dw, dt}
 }
@@ -1252,10 +1317,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         }
     const int64_t len = end > begin ? end - begin : 0;
     const int64_t ntiles = (len + TNEW - 1) / TNEW;
-    for (uint32_t p = tid; p < RS; p += T) {
-        const uint32_t c0 = p < R ? offs[(obase + p) * G + g] : 0u;
-        pe[p] = c0;
-        ple[p] = c0;  // nothing kept
+    if (MODE == WC_PADDED && !SEG && pp.pad_est) {
+        pad_layout_starts<T>(pp, R, RS, g, G, pe, ple, (uint64_t *)smem, err);  // scratch: the stage
+    } else {
+        for (uint32_t p = tid; p < RS; p += T) {
+            const uint32_t c0 = p < R ? offs[(obase + p) * G + g] : 0u;
+            pe[p] = c0;
+            ple[p] = c0;  // nothing kept
+        }
     }
     for (uint32_t i = tid; i < (uint32_t)WAVES * RS / 2; i += T) ((uint32_t *)rows)[i] = 0u;
     if constexpr (KIND == KIND_HOT_SPLIT)
@@ -1491,14 +1560,18 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     // padded output: every stream's final count, and whether it stayed inside its sub-bin
     // (pe is final: every thread passed the last tile's B4, or the prologue's barrier)
     if constexpr (MODE == WC_PADDED) {
-        bool ovf = false;
-        for (uint32_t p = tid; p < R; p += T) {
-            const int64_t i = (obase + p) * G + g;
-            const uint32_t cnt = pe[p] - offs[i];
-            pp.pad_cnt[i] = cnt;
-            ovf |= cnt > pp.pad_cap[obase + p];
+        if (!SEG && pp.pad_est) {  // the end positions: k_pad_finish makes them counts
+            for (uint32_t p = tid; p < R; p += T) pp.pad_cnt[(int64_t)p * G + g] = pe[p];
+        } else {
+            bool ovf = false;
+            for (uint32_t p = tid; p < R; p += T) {
+                const int64_t i = (obase + p) * G + g;
+                const uint32_t cnt = pe[p] - offs[i];
+                pp.pad_cnt[i] = cnt;
+                ovf |= cnt > pp.pad_cap[obase + p];
+            }
+            if (ovf) atomicOr(err, PAD_OVERFLOW);
         }
-        if (ovf) atomicOr(err, PAD_OVERFLOW);
     }
     }  // fragments
     if (bad) atomicOr(err, SCATTER_OOB);
@@ -3127,7 +3200,7 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         const bool hot_split = pp.kind == KIND_HOT_SPLIT;  // level 1 of the padded split
         if (mode && ((pp.kind != SGX_PART_HASH && !(hot_split && mode == WC_PADDED)) ||
                      !(W == 8 && geo.mbits == 16 && (geo.items == 12 || geo.items == 8)) ||
-                     (mode == WC_PADDED && (!pp.pad_cap || !pp.olim)) ||
+                     (mode == WC_PADDED && ((!pp.pad_cap && !(pp.pad_est && pp.pad_layout)) || !pp.olim)) ||
                      (hot_split && (!pp.dir || !out2 || pp.dshift > 13))))
             return hipErrorInvalidValue;
 #define SGX_WC_PAD(K)                                                                            \
@@ -3423,11 +3496,20 @@ hipError_t launch_gather_items(const int64_t *items, int64_t n_items, int align,
 // (k_gather_frags).  A stream longer than its sub-bin sets PAD_OVERFLOW and the map is
 // redone by the two-pass kernels guarded on that bit, on the same stream.
 // ------------------------------------------------------------------------------------
-constexpr int PAD_SAMPLE_THREADS = 256;
-constexpr int PAD_SAMPLE_UNROLL = 8;
+#ifndef SGX_PAD_SAMPLE_THREADS  // (A/B builds: -DSGX_PAD_SAMPLE_THREADS / _GRID / _UNROLL)
+#define SGX_PAD_SAMPLE_THREADS 256
+#endif
+#ifndef SGX_PAD_SAMPLE_GRID
+#define SGX_PAD_SAMPLE_GRID 512
+#endif
+#ifndef SGX_PAD_SAMPLE_UNROLL
+#define SGX_PAD_SAMPLE_UNROLL 8
+#endif
+constexpr int PAD_SAMPLE_THREADS = SGX_PAD_SAMPLE_THREADS;
+constexpr int PAD_SAMPLE_UNROLL = SGX_PAD_SAMPLE_UNROLL;
 // few workgroups, many loads each: every workgroup ends with up to R global atomics into the
 // same R counters (2048 workgroups of 4 loads per lane measured 63 µs at C1, mostly that)
-constexpr int PAD_SAMPLE_GRID = 512;
+constexpr int PAD_SAMPLE_GRID = SGX_PAD_SAMPLE_GRID;
 constexpr int PAD_SAMPLE_MAX_R = 4096;
 
 int64_t pad_sampled_records(int64_t n, int stride) {
@@ -3518,6 +3600,103 @@ hipError_t launch_pad_sample(const void *in, int64_t n, int rb, int stride, cons
     return hipGetLastError();
 }
 
+// The tail of a padded write whose K4 laid the sub-bins out (launch_pad_finish in sgx_internal.h).
+__global__ __launch_bounds__(256) void k_pad_finish(const uint32_t *__restrict__ layout, int R, int G, uint32_t olim,
+                                                    uint32_t *__restrict__ fstart, uint32_t *__restrict__ cnt,
+                                                    uint32_t *flags, uint32_t *__restrict__ zero, int64_t nzero) {
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i < nzero) zero[i] = 0u;
+    bool ovf = false;
+    if (i < (int64_t)R * G) {
+        const int p = (int)(i / G), g = (int)(i - (int64_t)p * G);
+        const uint32_t cap = layout[p];
+        const uint32_t f = (uint32_t)min<uint64_t>((uint64_t)layout[R + p] + (uint64_t)g * cap, (uint64_t)olim);
+        const uint32_t c = cnt[i] - f;  // K4 left the stream's end position
+        fstart[i] = f;
+        cnt[i] = c;
+        ovf = c > cap;
+    }
+    const uint64_t any = __ballot(ovf);
+    if (any && __lane_id() == (uint32_t)__ffsll((unsigned long long)any) - 1) atomicOr(flags, PAD_OVERFLOW);
+}
+
+hipError_t launch_pad_finish(const uint32_t *layout, int R, int G, uint32_t olim, uint32_t *fstart, uint32_t *cnt,
+                             uint32_t *flags, uint32_t *zero, int64_t nzero, hipStream_t stream) {
+    int64_t m = (int64_t)R * G;
+    if (nzero > m) m = nzero;
+    if (m < 1) m = 1;
+    hipLaunchKernelGGL(k_pad_finish, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, stream, layout, R, G, olim,
+                       fstart, cnt, flags, zero, nzero);
+    return hipGetLastError();
+}
+
+__global__ __launch_bounds__(256) void k_pad_reset(uint32_t *flags, uint32_t *flags_out, uint32_t *est, int R) {
+    if (threadIdx.x == 0) {
+        *flags_out = *flags;
+        *flags = 0u;
+    }
+    for (int p = threadIdx.x; p < R; p += 256) est[p] = 0u;
+}
+
+hipError_t launch_pad_reset(uint32_t *flags, uint32_t *flags_out, uint32_t *est, int R, hipStream_t stream) {
+    hipLaunchKernelGGL(k_pad_reset, dim3(1), dim3(256), 0, stream, flags, flags_out, est, R);
+    return hipGetLastError();
+}
+
+// The padded 16 B write's overflow fallback (launch_scatter16_fallback): one wave per chunk
+// walks its records in order, 64 at a time; a record's rank among the wave's records of its
+// partition comes from ballot matching, the stream's cursor from one global atomic per
+// partition present.  Slow (a global round trip per 64 records) and only ever run when a
+// sub-bin overflowed.
+template <int KIND>
+__global__ __launch_bounds__(64) void k_scatter16_fb(const uint4 *__restrict__ in, uint4 *__restrict__ out, int64_t n,
+                                                     int64_t chunk, PartParams pp, const uint32_t *__restrict__ foff,
+                                                     uint32_t *cur, int G, const uint32_t *guard, uint32_t *err) {
+    if (!(*guard & PAD_OVERFLOW)) return;
+    const int g = blockIdx.x;
+    const uint32_t lane = threadIdx.x, R = pp.R;
+    for (uint32_t p = lane; p < R; p += 64)
+        __hip_atomic_store(&cur[(int64_t)p * G + g], foff[(int64_t)p * G + g], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+    __syncthreads();
+    const int64_t begin = (int64_t)g * chunk;
+    const uint4 *cin = in + begin;
+    int64_t len = min(n, begin + chunk) - begin;
+    if (pp.chunks) {
+        cin = (const uint4 *)((const char *)in + pp.chunks[2 * g]);
+        len = pp.chunks[2 * g + 1];
+    }
+    bool bad = false;
+    for (int64_t i0 = 0; i0 < len; i0 += 64) {
+        const int64_t i = i0 + lane;
+        const bool valid = i < len;
+        const uint4 r = valid ? cin[i] : make_uint4(0, 0, 0, 0);
+        const uint32_t p = valid ? pid_of<KIND>(r.x, r.y, r.z, pp) : 0u;
+        const uint64_t peers = match_peers(p, __ballot(valid), pp.nbits);
+        const uint32_t leader = peers ? (uint32_t)__ffsll((unsigned long long)peers) - 1 : 0u;
+        uint32_t b = 0;
+        if (valid && lane == leader) b = atomicAdd(&cur[(int64_t)p * G + g], (uint32_t)__popcll(peers));
+        b = __shfl(b, (int)leader, 64);
+        const uint64_t pos = (uint64_t)b + (uint64_t)__popcll(peers & ((1ull << lane) - 1ull));
+        if (valid) {
+            if (pos < (uint64_t)n) out[pos] = r;
+            else bad = true;
+        }
+    }
+    if (bad) atomicOr(err, ERR_SCATTER_OOB);
+}
+
+hipError_t launch_scatter16_fallback(const void *in, void *out, int64_t n, int64_t chunk, int G, const PartParams &pp,
+                                     const uint32_t *foff, uint32_t *cur, const uint32_t *guard, uint32_t *err,
+                                     hipStream_t stream) {
+    if (n <= 0 || G <= 0) return hipSuccess;
+    if (pp.kind != SGX_PART_HASH) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_scatter16_fb<SGX_PART_HASH>, dim3(G), dim3(64), 0, stream, (const uint4 *)in, (uint4 *)out, n,
+                       chunk, pp, foff, cur, G, guard, err);
+    return hipGetLastError();
+}
+
 constexpr int PAD_CAPS_THREADS = 1024;
 
 constexpr int PAD_CAPS_PER = 4;  // partitions per thread: R <= 4096
@@ -3536,11 +3715,7 @@ __global__ __launch_bounds__(PAD_CAPS_THREADS) void k_pad_caps(const uint32_t *_
     for (int k = 0; k < PAD_CAPS_PER; ++k) {
         const int p = tid * PAD_CAPS_PER + k;
         cap[k] = 0;
-        if (p < R) {
-            const double mu = (double)est[p] * scale;
-            const double c = mu + PAD_SIGMAS * sqrt(a * mu + 16.0) + 8.0;
-            cap[k] = ((uint32_t)ceil(c) + 7u) & ~7u;
-        }
+        if (p < R) cap[k] = pad_cap_of(est[p], scale, a);
         s_cap[tid * PAD_CAPS_PER + k] = cap[k];
         sum += (uint64_t)cap[k] * (uint64_t)G;
     }

@@ -410,13 +410,13 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
     return SGX_OK;
 }
 
-// sample -> sub-bin capacities -> K4 into the sub-bins (final counts out) -> K3 over the
+// 100 B TeraSort records: sample -> sub-bin capacities -> K4 into the sub-bins (final counts out) -> K3 over the
 // counts (contiguous positions + index offsets), then the two-pass K1+K2 -> K3 -> K4 into the
 // same buffer, every kernel of it guarded on the padded K4's overflow bit (a no-op launch
 // otherwise).  Asynchronous on the context's stream; (R+1) offsets, the error word and the
 // padded K4's flag word land in m.part_off.
-static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n,
-                       const PadGeom &pg, const ChunkTable *ct = nullptr) {
+static int padded_pass_wide(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n,
+                            const PadGeom &pg, const ChunkTable *ct) {
     hipStream_t st = c.st;
     const int32_t R = s.R;
     const int G = pg.G;
@@ -492,6 +492,98 @@ static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void 
     m.pad_try = true;
     m.frag_G = G;
     return SGX_OK;
+}
+
+// 16 B records (the write-combining K4): sample -> K4, which lays the sub-bins out itself from
+// the sampled counts and writes every stream into its sub-bin (end positions out), on the
+// context's stream -- nothing else runs ahead of the next write's K4.  Then, on the tail
+// stream behind K4: the fragment table and the streams' counts (k_pad_finish, which also
+// checks them against their capacities), K3 over the counts (contiguous positions + index
+// offsets), the slot's reset for its next sample, and the overflow fallback (a no-op launch
+// that takes no LDS unless a sub-bin overflowed).  Asynchronous; (R+1) offsets, the error
+// word and the padded flag word land in m.part_off.
+static int padded_pass16(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n, const PadGeom &pg,
+                         const ChunkTable *ct) {
+    hipStream_t st = c.st;
+    const int32_t R = s.R;
+    const int G = pg.G;
+    const int64_t len = (int64_t)R * G, tiles = scan_tiles(len);
+    const uint32_t olim = (uint32_t)pg.olim;
+    auto al = [](size_t b) { return (b + 15) & ~(size_t)15; };
+    // this write's slot: its sample block is free once the tail two writes ago reset it; the
+    // rest of the slot is the tail stream's own (in order)
+    const int slot = c.pad_slot;
+    c.pad_slot ^= 1;
+    if (c.pad_free[slot].ev) HIP_TRY(hipStreamWaitEvent(st, c.pad_free[slot].ev, 0));
+    SGX_TRY(m.data.ensure((size_t)olim * 16));
+    SGX_TRY(m.frag.ensure((size_t)len * 12 + 16));
+    uint32_t *fstart = (uint32_t *)m.frag.p, *foff = fstart + len, *cnt = foff + len;
+    SGX_TRY(c.pad_offs[slot].ensure((size_t)len * 4));
+    // the sample's block: [est R][flags | pad][layout: caps R, bases R]; est and flags are zero
+    // when the sample starts (the slot's last tail reset them)
+    const size_t rbytes = al((size_t)R * 4), zero_bytes = rbytes + 16;
+    if (c.pad_crit[slot].cap < zero_bytes + 2 * rbytes) c.pad_crit_zeroed[slot] = 0;
+    SGX_TRY(c.pad_crit[slot].ensure(zero_bytes + 2 * rbytes));
+    char *cb = (char *)c.pad_crit[slot].p;
+    uint32_t *est = (uint32_t *)cb, *flags = (uint32_t *)(cb + rbytes), *layout = (uint32_t *)(cb + zero_bytes);
+    if (c.pad_crit_zeroed[slot] < zero_bytes) HIP_TRY(hipMemsetAsync(cb, 0, zero_bytes, st));
+    c.pad_crit_zeroed[slot] = 0;  // until this write's tail has reset it
+    // the tail's block: [offsets R+1 | error | flags copy][scan ticket | status]; k_pad_finish
+    // zeroes what the scan needs zero: everything from the error word on
+    const size_t off_bytes = al((size_t)(R + 3) * 4);
+    const size_t status_bytes = al((size_t)(16 + tiles * 8));
+    SGX_TRY(c.pad_work[slot].ensure(off_bytes + status_bytes));
+    char *w = (char *)c.pad_work[slot].p;
+    uint32_t *part_off_dev = (uint32_t *)w;
+    uint32_t *err = part_off_dev + R + 1, *flags_copy = part_off_dev + R + 2;
+    uint32_t *ticket_pad = (uint32_t *)(w + off_bytes);
+    uint64_t *status_pad = (uint64_t *)((char *)ticket_pad + 16);
+    c.last_off_dev = part_off_dev;
+    hipEvent_t h0 = e->ev(), h1 = e->ev(), c1 = e->ev(), x1 = e->ev();
+    HIP_TRY(hipEventRecord(h0, st));
+    PartParams bp = s.pp;  // the shuffle's partitioner over this map's input (chunk table or not)
+    bp.chunks = ct ? ct->dev : nullptr;
+    HIP_TRY(launch_pad_sample(in, n, 16, pg.stride, bp, est, st, pg.chunk, G));
+    SGX_TRY(debug_sync(e, st, "padded sample"));
+    HIP_TRY(hipEventRecord(h1, st));
+    PartParams kp = bp;
+    kp.mbits = (uint32_t)pg.geo.mbits;
+    kp.olim = olim;
+    kp.pad_cnt = cnt;
+    kp.pad_est = est;
+    kp.pad_layout = layout;
+    kp.pad_scale = (double)pg.chunk / (double)pg.sampled;
+    kp.pad_a = 1.0 + kp.pad_scale;
+    HIP_TRY(launch_scatter(in, m.data.p, n, 16, pg.chunk, G, kp, nullptr, pg.geo, flags, st));
+    SGX_TRY(debug_sync(e, st, "K4 padded scatter"));
+    HIP_TRY(hipEventRecord(c1, st));
+    hipStream_t tl = c.st_tail;
+    HIP_TRY(hipStreamWaitEvent(tl, c1, 0));
+    HIP_TRY(launch_pad_finish(layout, R, G, olim, fstart, cnt, flags, err,
+                              (int64_t)((off_bytes + status_bytes) / 4) - (R + 1), tl));
+    HIP_TRY(launch_scan(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, tl));
+    HIP_TRY(launch_pad_reset(flags, flags_copy, est, R, tl));
+    HIP_TRY(c.pad_free[slot].record(tl));
+    c.pad_crit_zeroed[slot] = zero_bytes;
+    HIP_TRY(launch_scatter16_fallback(in, m.data.p, n, pg.chunk, G, bp, foff, (uint32_t *)c.pad_offs[slot].p,
+                                      flags_copy, err, tl));
+    SGX_TRY(debug_sync(e, tl, "padded tail"));
+    HIP_TRY(hipEventRecord(x1, tl));
+    HIP_TRY(hipMemcpyAsync(m.part_off.p, part_off_dev, (size_t)(R + 3) * 4, hipMemcpyDeviceToHost, tl));
+    HIP_TRY(c.pad_done[slot].record(tl));
+    c.tail_slot = slot;
+    // stages: the sampled histogram stands where K1+K2 do, the tail where K3 does
+    e->record_stage(SGX_STAGE_HIST, h0, h1);
+    e->record_stage(SGX_STAGE_SCATTER, h1, c1);
+    e->record_stage(SGX_STAGE_SCAN, c1, x1);
+    m.pad_try = true;
+    m.frag_G = G;
+    return SGX_OK;
+}
+
+static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n, const PadGeom &pg,
+                       const ChunkTable *ct = nullptr) {
+    return s.rb == 16 ? padded_pass16(e, c, s, m, in, n, pg, ct) : padded_pass_wide(e, c, s, m, in, n, pg, ct);
 }
 
 int sgx::materialize(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
@@ -758,11 +850,7 @@ static int check_batch(const Shuffle &s, const void *records, int64_t n, int32_t
 // device pointer of a batch (host batches are staged through the context's buffer)
 static int device_input(Ctx &c, const void *records, int64_t bytes, int32_t mem_kind, const void **in) {
     *in = records;
-    if (mem_kind == SGX_MEM_HOST && bytes > 0) {
-        SGX_TRY(c.input_stage.ensure((size_t)bytes));
-        HIP_TRY(hipMemcpyAsync(c.input_stage.p, records, (size_t)bytes, hipMemcpyHostToDevice, c.st));
-        *in = c.input_stage.p;
-    }
+    if (mem_kind == SGX_MEM_HOST && bytes > 0) SGX_TRY(c.stage_input(records, (size_t)bytes, c.st, in));
     return SGX_OK;
 }
 

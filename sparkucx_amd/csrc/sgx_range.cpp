@@ -178,9 +178,7 @@ extern "C" int sgx_range_bounds(sgx_engine *e, const void *const *batches, const
         if (kk == 0) continue;
         const void *src = batches[i];
         if (mem_kind == SGX_MEM_HOST) {
-            SGX_TRY(c->input_stage.ensure((size_t)(n * rb)));
-            HIP_TRY(hipMemcpyAsync(c->input_stage.p, src, (size_t)(n * rb), hipMemcpyHostToDevice, st));
-            src = c->input_stage.p;
+            SGX_TRY(c->stage_input(src, (size_t)(n * rb), st, &src));
         }
         const int32_t seed = byteswap32((int32_t)((uint32_t)i ^ ((uint32_t)rdd_id << 16)));
         const uint64_t s0 = xorshift_hash_seed((int64_t)seed);  // Int seed widened to Long
@@ -252,9 +250,7 @@ extern "C" int sgx_range_bounds(sgx_engine *e, const void *const *batches, const
             if (idx.empty()) continue;
             const void *src = batches[i];
             if (mem_kind == SGX_MEM_HOST) {
-                SGX_TRY(c->input_stage.ensure((size_t)(n * rb)));
-                HIP_TRY(hipMemcpyAsync(c->input_stage.p, src, (size_t)(n * rb), hipMemcpyHostToDevice, st));
-                src = c->input_stage.p;
+                SGX_TRY(c->stage_input(src, (size_t)(n * rb), st, &src));
             }
             const int64_t m = (int64_t)idx.size();
             SGX_TRY(c->sample_winner.ensure((size_t)m * 8));

@@ -691,6 +691,7 @@ extern "C" int sgx_read_sorted(sgx_engine *e, int32_t shuffle_id, const int64_t 
         SGX_TRY(sort_records(e, *c, *s, n, true, &sorted, end_partition - start_partition, direct ? dst : nullptr));
     }
     *out_bytes = n * rb;
+    c->last_read_records = n;
     if (n * rb > dst_cap)
         return fail_msg(SGX_ERR_INVALID, "destination capacity %lld < %lld bytes", (long long)dst_cap,
                         (long long)(n * rb));
@@ -716,6 +717,7 @@ extern "C" int sgx_read_records(sgx_engine *e, int32_t shuffle_id, const int64_t
     else
         SGX_TRY(records_impl(e, *c, *s, map_ids, nmaps, start_partition, end_partition, &n));
     *out_bytes = n * rb;
+    c->last_read_records = n;
     if (!dst && dst_cap == 0) {  // size query
         rc_store(*c, epoch, RC_RECORDS, 0, shuffle_id, map_ids, nmaps, start_partition, end_partition, n, 0,
                  c->sort_buf[0].p, nullptr, nullptr, nullptr);
@@ -762,6 +764,7 @@ extern "C" int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t
         SGX_TRY(group_records(e, *c, sorted, n, agg, &ng, &dkeys, &dstarts, &dvals));
     }
     const int64_t nvals = agg == SGX_AGG_GROUP ? n : ng;
+    c->last_read_records = n;  // the shuffled records the aggregation consumed
     *out_groups = ng;
     *out_values = nvals;
     if (!keys && cap_groups == 0 && cap_values == 0) {  // size query
@@ -778,5 +781,17 @@ extern "C" int sgx_read_grouped(sgx_engine *e, int32_t shuffle_id, const int64_t
     if (group_starts) SGX_TRY(copy_out(*c, group_starts, dstarts, ng * 8, mem_kind));
     SGX_TRY(copy_out(*c, values, dvals, nvals * 8, mem_kind));
     HIP_TRY(hipStreamSynchronize(c->st));
+    return SGX_OK;
+}
+
+// The records (before any aggregation) the calling thread's last sgx_read_records / _sorted /
+// _grouped consumed: what the reference's reader counts with incRecordsRead, one per shuffled
+// record ahead of the aggregator (spark_3_0/UcxShuffleReader.scala:148-162).
+extern "C" int sgx_last_read_records(sgx_engine *e, int64_t *out) {
+    if (!e || !out) return fail_msg(SGX_ERR_INVALID, "NULL argument");
+    HIP_TRY(hipSetDevice(e->device));
+    Ctx *c = e->ctx();
+    if (!c) return SGX_ERR_HIP;
+    *out = c->last_read_records;
     return SGX_OK;
 }

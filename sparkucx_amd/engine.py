@@ -215,8 +215,10 @@ class ShuffleEngine:
     def map_append(self, shuffle_id: int, map_id: int, records, nrecords: int, record_bytes: int,
                    offset: int = 0, retained: bool = False):
         """Append one batch: ``nrecords`` records from byte ``offset`` of ``records``.  A device
-        batch with ``retained`` stays where it is until map_commit returns (the commit reads it
-        in place: SGX_MEM_DEVICE_RETAINED); otherwise the engine copies it before returning."""
+        batch with ``retained`` stays where it is (SGX_MEM_DEVICE_RETAINED): the caller keeps it
+        unchanged until the map's lengths are known -- map_commit with ``num_partitions`` has
+        returned, or map_lengths / sync after an asynchronous commit -- since the commit's
+        kernels read it in place; otherwise the engine copies it before returning."""
         ptr, nbytes, kind = buffer_arg(records)
         if offset < 0 or offset + nrecords * record_bytes > nbytes:
             raise _lib.IllegalArgumentException(
@@ -489,6 +491,14 @@ class ShuffleEngine:
         if group:
             return keys, starts, vals
         return keys, vals
+
+    def last_read_records(self) -> int:
+        """Records (before any aggregation) the calling thread's last read_records / read_sorted
+        / read_grouped consumed -- what the reference's reader counts with incRecordsRead
+        (spark_3_0/UcxShuffleReader.scala:148-162)."""
+        n = ctypes.c_int64(0)
+        check(lib().sgx_last_read_records(self.handle, ctypes.byref(n)), "lastReadRecords")
+        return int(n.value)
 
     def range_bounds(self, batches: Sequence, nrecords: Sequence[int], record_bytes: int, num_partitions: int,
                      rdd_id: int = 0, sample_points_per_partition: int = 20,

@@ -687,8 +687,9 @@ class UcxShuffleReader:
           values) -- keys ascending per reducer, values in arrival order;
         * aggregator "sum" (reduceByKey(_ + _)): (keys, sums).
         Metrics as the reference's reader reports them: the range's blocks and bytes, and
-        ``incRecordsRead`` with the records (or groups) handed to the task; a task killed
-        before the read raises TaskKilledException (``iterator()`` checks per record)."""
+        ``incRecordsRead`` with the shuffled records read (for an aggregator: the records it
+        consumed, not its groups); a task killed before the read raises TaskKilledException
+        (``iterator()`` checks per record)."""
         dep = self.handle.dependency
         sid = self.handle.shuffleId
         self.context.killTaskIfInterrupted()
@@ -698,7 +699,9 @@ class UcxShuffleReader:
                 raise UnsupportedOperationException("aggregation needs (Long, Long) 16 B records")
             agg = _lib.AGG_SUM if dep.aggregator.kind == "sum" else _lib.AGG_GROUP
             out = self.manager.engine.read_grouped(sid, self._maps(), self.start, self.end, agg)
-            nrec = len(out[0])
+            # the shuffled records the aggregator consumed, not its groups (the reference counts
+            # ahead of combineValuesByKey / combineCombinersByKey, UcxShuffleReader.scala:148-162)
+            nrec = self.manager.engine.last_read_records()
         elif dep.keyOrdering:
             out = self.manager.engine.read_sorted(sid, self._maps(), self.start, self.end).reshape(-1, dep.recordBytes)
             nrec = len(out)
@@ -717,7 +720,8 @@ class UcxShuffleReader:
         """read() as Spark's task consumes it: (key, value) pairs of (Long, Long) records (or
         (key, sum) / (key, values) after an aggregator), one at a time, in an
         InterruptibleIterator that stops at the next record once the task is killed, with
-        ``incRecordsRead`` per record (spark_3_0/UcxShuffleReader.scala:148-156)."""
+        ``incRecordsRead`` per record (spark_3_0/UcxShuffleReader.scala:148-156); behind an
+        aggregator, every record it consumed, counted when its first group is handed over."""
         dep = self.handle.dependency
         self.context.killTaskIfInterrupted()
         self._count_blocks()
@@ -726,6 +730,8 @@ class UcxShuffleReader:
                 raise UnsupportedOperationException("aggregation needs (Long, Long) 16 B records")
             agg = _lib.AGG_SUM if dep.aggregator.kind == "sum" else _lib.AGG_GROUP
             res = self.manager.engine.read_grouped(self.handle.shuffleId, self._maps(), self.start, self.end, agg)
+            # the aggregator consumed every shuffled record before its first group comes out
+            consumed = self.manager.engine.last_read_records()
             if agg == _lib.AGG_SUM:
                 pairs = zip(res[0].tolist(), res[1].tolist())
             else:
@@ -738,8 +744,11 @@ class UcxShuffleReader:
             pairs = ((int(a), int(b)) for a, b in kv) if kv is not None else (bytes(r) for r in out)
 
         def counted():
+            if dep.aggregator is not None:
+                self.readMetrics.incRecordsRead(consumed)
             for p in pairs:
-                self.readMetrics.incRecordsRead(1)
+                if dep.aggregator is None:
+                    self.readMetrics.incRecordsRead(1)
                 yield p
             self.context.mergeShuffleReadMetrics()
 

@@ -138,6 +138,29 @@ def test_padded_overflow_falls_back_bit_exact(sgx_lib, pad_engine, oracle_lib, s
         pad_engine.unregister_shuffle(sid)
 
 
+def test_async_host_writes_behind_an_overflowing_map(sgx_lib, pad_engine, oracle_lib):
+    """Two asynchronous writes of host batches on one thread, the first overflowing its
+    sub-bins: its guarded fallback runs on the tail stream and reads the staged input, which
+    the second write stages its own records into -- the second copy must wait for that tail
+    (ADVICE r05: Ctx::stage_input).  Both maps must equal the oracle's."""
+    R, n = 1024, 1_500_000
+    first = oracle_lib.gen_uniform16(n, 91)
+    first[:, :8] = (np.arange(n) * 300 // n).astype(np.int64).view(np.uint8).reshape(-1, 8)
+    second = oracle_lib.gen_uniform16(n, 92)
+    sid1, sid2 = next_sid(), next_sid()  # two shuffles: the second's maps still try padded
+    pad_engine.register_shuffle(sid1, R)
+    pad_engine.register_shuffle(sid2, R)
+    try:
+        for _ in range(2):
+            pad_engine.write_map(sid1, 0, first, n, 16)   # asynchronous (no lengths asked)
+            pad_engine.write_map(sid2, 0, second, n, 16)
+            check_map(pad_engine, oracle_lib, first, R, sid1, 0, sgx_lib.LAYOUT_CONTIGUOUS)
+            check_map(pad_engine, oracle_lib, second, R, sid2, 0, sgx_lib.LAYOUT_PADDED)
+    finally:
+        pad_engine.unregister_shuffle(sid1)
+        pad_engine.unregister_shuffle(sid2)
+
+
 @pytest.mark.parametrize("R", [2048, 4096])
 @pytest.mark.parametrize("shape", ["uniform", "zipf", "one_super", "hot_partition", "few_keys", "tiny"])
 def test_padded_split_r_over_1024(sgx_lib, pad_engine, oracle_lib, R, shape):

@@ -74,6 +74,25 @@ def test_commit_is_one_padded_pass(sgx_lib, engine, oracle_lib, R, modes):
         engine.unregister_shuffle(sid)
 
 
+def test_async_commit_retained_until_lengths(sgx_lib, engine, oracle_lib):
+    """An asynchronous commit (no lengths asked) only enqueues its pass, which reads the
+    retained batches in place: the caller keeps them until the map's lengths are known
+    (sgx_map_lengths here; sgx.h, SGX_MEM_DEVICE_RETAINED) and may then overwrite them."""
+    R, n = 1024, 1_200_000
+    recs = oracle_lib.gen_uniform16(n, 0x77)
+    sid = next_sid()
+    engine.register_shuffle(sid, R)
+    try:
+        dev = append_batches(engine, sid, 0, recs, sizes_for(n, 4, 5), ("retained",))
+        assert engine.map_commit(sid, 0) is None
+        engine.map_lengths(sid, 0, R)
+        engine.gen_uniform16(dev, n, 0x78)  # the caller reuses its buffer
+        dev.free()
+        check_map(engine, oracle_lib, recs, R, sid, 0, sgx_lib.LAYOUT_PADDED)
+    finally:
+        engine.unregister_shuffle(sid)
+
+
 @pytest.mark.parametrize("R", [2, 7, 1000])
 @pytest.mark.parametrize("n,k", [(1, 1), (5, 3), (70_001, 5), (300_000, 300)])
 def test_commit_padded_any_size_and_many_batches(sgx_lib, oracle_lib, R, n, k):

@@ -16,6 +16,7 @@ def main():
     import sparkucx_amd._lib as L
 
     L.LIB_PATH = os.path.abspath(lib)
+    L.ALLOW_MISSING = True
     sys.argv = [tool + ".py"] + rest
     importlib.import_module(tool).main()
 
