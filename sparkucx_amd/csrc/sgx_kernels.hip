@@ -489,6 +489,71 @@ hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint
     return hipGetLastError();
 }
 
+// One wave per tile of SCAN_TILE counts (64 per lane), no LDS: the ticket and the look-back
+// prefix are broadcast by lane shuffles (launch_scan_wave in sgx_internal.h).
+__global__ __launch_bounds__(64) void k_scan_wave(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                  int64_t len, uint64_t *status, uint32_t *ticket, uint32_t *err,
+                                                  uint32_t *__restrict__ part_off, int G, int R) {
+    constexpr int ITEMS = SCAN_TILE / 64;
+    const uint32_t lane = threadIdx.x;
+    uint32_t tile = lane == 0 ? atomicAdd(ticket, 1u) : 0u;
+    tile = __shfl(tile, 0, 64);
+    const int64_t base = (int64_t)tile * SCAN_TILE + (int64_t)lane * ITEMS;
+    // the lane's counts are read twice (the second time from the cache) instead of held: few
+    // VGPRs, so the waves fit beside a running K4's
+    uint32_t sum = 0;
+    for (int j = 0; j < ITEMS; ++j) {
+        const int64_t i = base + j;
+        sum += i < len ? in[i] : 0u;
+    }
+    const uint32_t incl = wave_inclusive_scan(sum, lane);
+    const uint64_t agg = __shfl(incl, 63, 64);
+    uint32_t prefix = 0;
+    if (lane == 0) {
+        uint64_t excl = 0;
+        if (tile == 0) {
+            __hip_atomic_store(&status[0], ST_PRE | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            __hip_atomic_store(&status[tile], ST_AGG | agg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            int64_t j = (int64_t)tile - 1;
+            uint32_t spins = 0;
+            while (j >= 0) {
+                const uint64_t s = __hip_atomic_load(&status[j], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const uint64_t flag = s & ~ST_VAL;
+                if (flag == 0) {
+                    if (++spins > (1u << 26)) { atomicOr(err, 1u); break; }
+                    __builtin_amdgcn_s_sleep(1);
+                    continue;
+                }
+                excl += s & ST_VAL;
+                if (flag == ST_PRE) break;
+                --j;
+            }
+            __hip_atomic_store(&status[tile], ST_PRE | (excl + agg), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        prefix = (uint32_t)excl;
+    }
+    uint32_t run = __shfl(prefix, 0, 64) + incl - sum;  // offsets fit 32 bits (records per map < 2^32)
+    for (int j = 0; j < ITEMS; ++j) {
+        const int64_t i = base + j;
+        if (i < len) {
+            const uint32_t v = in[i];
+            out[i] = run;
+            if (i % G == 0) part_off[i / G] = run;
+            if (i == len - 1) part_off[R] = run + v;
+            run += v;
+        }
+    }
+}
+
+hipError_t launch_scan_wave(const uint32_t *counts, uint32_t *offs, int64_t len, uint64_t *status, uint32_t *ticket,
+                            uint32_t *err, uint32_t *part_off, int G, int R, hipStream_t stream) {
+    const int64_t tiles = scan_tiles(len);
+    hipLaunchKernelGGL(k_scan_wave, dim3((unsigned)tiles), dim3(64), 0, stream, counts, offs, len, status, ticket, err,
+                       part_off, G, R);
+    return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------
 // K4: stable scatter.
 //
@@ -3496,11 +3561,13 @@ hipError_t launch_gather_items(const int64_t *items, int64_t n_items, int align,
 // (k_gather_frags).  A stream longer than its sub-bin sets PAD_OVERFLOW and the map is
 // redone by the two-pass kernels guarded on that bit, on the same stream.
 // ------------------------------------------------------------------------------------
+// 128 workgroups of 1024 threads, 8 loads in flight per lane: 13 µs at C1 against 23-25 µs for
+// 512 x 256 (fewer workgroups end with fewer global atomics into est; profiles/r06e_*.log)
 #ifndef SGX_PAD_SAMPLE_THREADS  // (A/B builds: -DSGX_PAD_SAMPLE_THREADS / _GRID / _UNROLL)
-#define SGX_PAD_SAMPLE_THREADS 256
+#define SGX_PAD_SAMPLE_THREADS 1024
 #endif
 #ifndef SGX_PAD_SAMPLE_GRID
-#define SGX_PAD_SAMPLE_GRID 512
+#define SGX_PAD_SAMPLE_GRID 128
 #endif
 #ifndef SGX_PAD_SAMPLE_UNROLL
 #define SGX_PAD_SAMPLE_UNROLL 8

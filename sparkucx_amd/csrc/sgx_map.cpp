@@ -561,7 +561,7 @@ static int padded_pass16(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const voi
     HIP_TRY(hipStreamWaitEvent(tl, c1, 0));
     HIP_TRY(launch_pad_finish(layout, R, G, olim, fstart, cnt, flags, err,
                               (int64_t)((off_bytes + status_bytes) / 4) - (R + 1), tl));
-    HIP_TRY(launch_scan(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, tl));
+    HIP_TRY(launch_scan_wave(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, tl));
     HIP_TRY(launch_pad_reset(flags, flags_copy, est, R, tl));
     HIP_TRY(c.pad_free[slot].record(tl));
     c.pad_crit_zeroed[slot] = zero_bytes;

@@ -25,6 +25,17 @@ class _Engine:
         self.calls.append("lengths")
         return np.array([len(self._block(m, r)) for m, r in zip(mids, rids)], dtype=np.int64)
 
+    def read_grouped(self, sid, maps, r0, r1, agg):
+        """The aggregation of the same blocks: one group per distinct key, summed values."""
+        self.calls.append("grouped")
+        recs = np.concatenate([self._block(m, r) for r in range(r0, r1) for m in maps]).view("<i8").reshape(-1, 2)
+        self._consumed = len(recs)
+        keys, inv = np.unique(recs[:, 0], return_inverse=True)
+        return keys, np.bincount(inv, weights=recs[:, 1]).astype(np.int64)
+
+    def last_read_records(self):
+        return self._consumed
+
     def fetch_blocks(self, sid, mids, rids):
         self.calls.append("fetch")
         parts = [self._block(m, r) for m, r in zip(mids, rids)]
@@ -44,10 +55,10 @@ class _Manager:
         return False
 
 
-def _reader(maps, r0, r1, context=None, metrics=None):
+def _reader(maps, r0, r1, context=None, metrics=None, aggregator=None):
     import sparkucx_amd as sgx
 
-    dep = sgx.ShuffleDependency(sgx.HashPartitioner(8), 16)
+    dep = sgx.ShuffleDependency(sgx.HashPartitioner(8), 16, aggregator=aggregator)
     h = sgx.BaseShuffleHandle(3, dep)
     return sgx.UcxShuffleReader(_Manager(maps), h, r0, r1, None, context, metrics)
 
@@ -69,6 +80,23 @@ def test_read_reports_blocks_bytes_and_records():
     # merged into the task's metrics on completion (mergeShuffleReadMetrics)
     assert ctx.shuffleReadMetrics.recordsRead == len(out)
     assert ctx.shuffleReadMetrics.localBytesRead == m.localBytesRead
+
+
+def test_aggregated_read_counts_the_shuffled_records():
+    """Behind an aggregator the reference counts every shuffled record it consumed, not the
+    groups it emits (spark_3_0/UcxShuffleReader.scala:148-162)."""
+    import sparkucx_amd as sgx
+
+    want = 2 * sum((r + 1) % 4 for r in range(8))
+    rd = _reader([5, 9], 0, 8, sgx.TaskContext(), aggregator=sgx.Aggregator("sum"))
+    keys, sums = rd.read()
+    assert len(keys) < want
+    assert rd.readMetrics.recordsRead == want
+    ctx = sgx.TaskContext()
+    it = _reader([5, 9], 0, 8, ctx, aggregator=sgx.Aggregator("sum")).iterator()
+    groups = list(it)
+    assert len(groups) == len(keys)
+    assert ctx.shuffleReadMetrics.recordsRead == want
 
 
 def test_iterator_counts_per_record_and_merges_at_the_end():
@@ -148,6 +176,17 @@ def test_read_metrics_on_the_gpu(sgx_lib, oracle_lib, tmp_path):
         assert rd.readMetrics.localBlocksFetched == sum(int(np.count_nonzero(c[10:30])) for c in counts)
         assert rd.readMetrics.localBytesRead == 16 * len(want)
         assert ctx.shuffleReadMetrics.recordsRead == len(want)
+        # groupByKey / reduceByKey over the same blocks: the shuffled records, not the groups
+        for kind in ("group", "sum"):
+            hg = mgr.registerShuffle(1 if kind == "group" else 2, sgx.ShuffleDependency(
+                sgx.HashPartitioner(R), 16, aggregator=sgx.Aggregator(kind)))
+            for mid, recs in zip((3, 7, 11), [oracle.gen_uniform16(5000 + 113 * m, 0xAB + m, value_base=m << 32)
+                                              for m in (3, 7, 11)]):
+                mgr.getWriter(hg, mid).write(recs)
+            ctxg = sgx.TaskContext()
+            res = mgr.getReader(hg, 10, 30, ctxg).read()
+            assert len(res[0]) <= len(want)
+            assert ctxg.shuffleReadMetrics.recordsRead == len(want)
         # per record, with cancellation
         ctx2 = sgx.TaskContext()
         it = mgr.getReader(h, 0, R, ctx2).iterator()
