@@ -82,6 +82,10 @@ def parse():
                          "(GpuShuffleWriter: sgx_map_begin, this many sgx_map_append batches -- 2^22 records "
                          "each at C1 with 64 -- as retained device slices of the resident input, "
                          "sgx_map_commit) instead of one sgx_write_map")
+    ap.add_argument("--no-p2p", action="store_true",
+                    help="N > 1 / --self-exchange: move the exchange's bytes by RCCL send / recv (or the host "
+                         "all-to-all) over contiguous map outputs, with two-pass map writes, instead of the "
+                         "direct peer gather out of single-pass padded maps (A/B, DESIGN.md §8)")
     a = ap.parse_args()
     a.record_bytes = 100 if a.workload == "c4" else 16
     a.records = a.records or (1 << 25 if a.workload == "c4" else 1 << 28)
@@ -264,9 +268,20 @@ def live_pmc(args):
             "source": "live: rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes over tools/prof_map.py in this bench run"}
 
 
+def _exchange_name(args, world, self_x):
+    if world == 1 and not self_x:
+        return None
+    ctl = "RCCL" if args.comm == "rccl" or self_x else "host collectives (gloo)"
+    if args.no_p2p:
+        data = "RCCL grouped send/recv" if ctl == "RCCL" else "host all-to-all"
+    else:
+        data = "direct peer gather (IPC-mapped receive buffers)"
+    return f"{data}, {ctl} control" + (", 1 rank (rehearsal)" if self_x else
+                                       " (rehearsal: ranks share one GPU)" if args.comm == "host" else "")
+
+
 def _workload_name(args, n, R, world, self_x):
-    x = ("RCCL alltoallv" if args.comm == "rccl" else "host all-to-all (rehearsal)") if world > 1 else (
-        "exchange through a 1-rank RCCL communicator (rehearsal)" if self_x else None)
+    x = _exchange_name(args, world, self_x)
     if args.workload == "c4":
         w = f"C4: {n} x 100 B TeraSort records per GPU, RangePartitioner R={R} (sampled bounds), partition+scatter"
     elif args.workload == "c3":
@@ -306,7 +321,8 @@ def main():
     n, R, rb = args.records, args.partitions, args.record_bytes
     eng = sgx.ShuffleEngine(device=device, num_chunks=args.num_chunks,
                             flags=(sgx.FLAG_NO_SPLIT_SCATTER if args.no_split else 0) |
-                            (sgx.FLAG_NO_PADDED_MAP if args.no_padded else 0))
+                            (sgx.FLAG_NO_PADDED_MAP if args.no_padded else 0) |
+                            (sgx.FLAG_NO_P2P_EXCHANGE if args.no_p2p else 0))
     self_x = args.self_exchange and world == 1
     if world > 1 and args.comm == "host":
         eng.comm_init_host(world, rank)
@@ -421,6 +437,17 @@ def main():
     if not args.no_verify:
         verified = bool(lens.sum() == rb * n) if args.serializer == "fixed" else bool(lens.sum() >= 4 * n)
     xgmi = None
+    xbytes = None
+    if world > 1 or self_x:
+        # what the exchange moved against the blocks' lengths: the peer gather sends a padded
+        # map's blocks from its fragments, so exactly the lengths (no sub-bin slack)
+        xb = eng.exchange_bytes()
+        t = torch.tensor([xb["sent"], xb["kept"], float(lens.sum()) * args.steps], dtype=torch.float64)
+        if dist is not None:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        xbytes = {"sent_to_peers": float(t[0]), "kept_local": float(t[1]), "published": float(t[2]),
+                  "moved_over_published": round(float((t[0] + t[1]) / max(t[2], 1.0)), 6),
+                  "rounds_per_rank": xb["rounds"]}
     if world > 1:
         # bytes this rank's map sends over xGMI (reducer r lives on rank floor(r*P/R))
         r0, r1 = eng.shuffle_reducers(sid)  # this rank's reducers (fixed by the shuffle's first round)
@@ -461,6 +488,11 @@ def main():
         k4_pmc, side_pmc = pmc.get("scatter") or {}, pmc.get("map_side") or {}
         side_ms = (st.ms["hist"] + st.ms["scan"] + st.ms["scatter"]) / max(1, st.count["scatter"])
         side_src = "stage events (K1+K2 / sample, K3, K4)"
+        if layout == sgx.LAYOUT_PADDED:
+            # the padded write's K3 runs on its tail stream beside the next write (its stage
+            # interval spans the next map's kernels): the write is the sample and K4
+            side_ms = (st.ms["hist"] + st.ms["scatter"]) / max(1, st.count["scatter"])
+            side_src = "stage events (sample, K4; the tail's K3 overlaps the next write)"
         if world == 1 and not self_x and tasks == 1 and not args.compress and args.serializer == "fixed":
             # a step is exactly one map write: its wall time is the map side as a map task sees
             # it, host calls included -- the padded write's tail (K3 + the guarded fallback) runs
@@ -487,8 +519,7 @@ def main():
                                      "streams' counts)" if padded else "contiguous (two-pass: K1+K2 histogram, K3, K4)",
                        "parallelism": f"dp{world} (map shards per GPU, reducers owned "
                                       + ("floor(r*P/R))" if args.placement == "even" else "in byte-balanced ranges)"),
-                       "exchange": ("RCCL ncclAllToAllv, 1 rank (rehearsal)" if self_x else None) if world == 1 else (
-                           "RCCL ncclAllToAllv" if args.comm == "rccl" else "host collectives (gloo), rehearsal")},
+                       "exchange": _exchange_name(args, world, self_x)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": k4_pmc.get("hbm_bytes_per_launch"),
@@ -513,6 +544,8 @@ def main():
         }
         if xgmi is not None:
             out["xgmi_roofline"] = xgmi
+        if xbytes is not None:
+            out["exchange_bytes"] = xbytes
         if args.serializer == "kryo":
             ser_ms = st.ms["serialize"] / max(1, st.count["serialize"])
             kbytes = float(lens.sum())

@@ -86,9 +86,14 @@ enum sgx_flags {
     SGX_FLAG_NO_SEG_WINDOW = 1024,    /* sorted reads of several partitions: the key window and
                                          the partitioner in two LSD passes instead of one
                                          segmented pass per partition                          */
-    SGX_FLAG_NO_DEFERRED_APPEND = 2048 /* streaming maps: partition every sgx_map_append batch on
+    SGX_FLAG_NO_DEFERRED_APPEND = 2048, /* streaming maps: partition every sgx_map_append batch on
                                          arrival and gather them at the commit (the round-4 form)
                                          instead of one pass over all batches at the commit    */
+    SGX_FLAG_NO_P2P_EXCHANGE = 4096   /* exchange rounds move their bytes by grouped
+                                         ncclSend / ncclRecv (RCCL) or the host all-to-all over
+                                         contiguous map outputs, and a communicator keeps the
+                                         map side two-pass; default: the direct peer gather
+                                         (sgx_exchange) out of single-pass padded maps         */
 };
 
 typedef struct sgx_config {
@@ -488,6 +493,10 @@ enum sgx_stage { SGX_STAGE_HIST = 0, SGX_STAGE_SCAN = 1, SGX_STAGE_SCATTER = 2,
 int sgx_stats_reset(sgx_engine *e);
 /* out_ms[SGX_NUM_STAGES] summed milliseconds, out_count[SGX_NUM_STAGES] launches. */
 int sgx_stats_get(sgx_engine *e, double *out_ms, int64_t *out_count);
+/* Bytes the exchange rounds moved since sgx_stats_reset: out[0] to other ranks, out[1] kept
+ * by this rank (its own reducers' blocks), out[2] rounds -- the blocks' lengths exactly, with
+ * no sub-bin slack, whether a map was written padded or contiguous. */
+int sgx_exchange_bytes(sgx_engine *e, int64_t out[3]);
 
 /* ---- pure-host exchange planning (exported for tests of the multi-GPU logic) ----
  * lengths_all: [P][R] per-rank partition lengths in bytes.  Writes, for `rank`:

@@ -500,6 +500,14 @@ extern "C" int sgx_stats_reset(sgx_engine *e) {
         e->stage_ms[i] = 0;
         e->stage_n[i] = 0;
     }
+    for (int64_t &b : e->x_bytes) b = 0;
+    return SGX_OK;
+}
+
+extern "C" int sgx_exchange_bytes(sgx_engine *e, int64_t out[3]) {
+    if (!e || !out) return fail_msg(SGX_ERR_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lk(e->stats_mu);
+    for (int i = 0; i < 3; ++i) out[i] = e->x_bytes[i];
     return SGX_OK;
 }
 

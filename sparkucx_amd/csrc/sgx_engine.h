@@ -395,6 +395,8 @@ struct sgx_engine {
     std::vector<sgx::PendingStage> pending;
     double stage_ms[SGX_NUM_STAGES] = {0};
     int64_t stage_n[SGX_NUM_STAGES] = {0};
+    // exchange bytes: [0] sent to other ranks, [1] kept by this rank, [2] rounds (sgx_exchange_bytes)
+    int64_t x_bytes[3] = {0, 0, 0};
 
     // the calling thread's context (created on first use); nullptr + last_error on failure
     sgx::Ctx *ctx();

@@ -149,6 +149,158 @@ struct LocalMap {
 };
 }  // namespace
 
+// Direct peer gather: rank `me` writes the blocks of its maps that rank d owns
+// straight into d's receive buffer, at the place d's plan gives them -- a padded map's blocks
+// from their fragments (one workgroup per fragment), a contiguous map's as byte ranges -- in
+// one gather launch per kind on the exchange stream.  Peers' buffers are mapped into this
+// process through IPC handles all-gathered by the backend (the image's dmabuf IPC; this rank's
+// own buffer directly); a second all-gather after every rank's gather has finished is the
+// completion barrier, and carries each rank's status so a failed gather fails the round on
+// every rank.  No pack step and no contiguous copy of a padded map: each map's published bytes
+// leave it exactly once, sent bytes = the blocks' lengths.
+static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<LocalMap> &mine,
+                    const std::vector<int32_t> &bounds, const std::vector<int64_t> &lens,
+                    const std::vector<int32_t> &srcs, hipStream_t st) {
+    const int32_t P = e->nranks, me = e->rank, R = s.R;
+    const size_t M = srcs.size();
+    // (a) every rank's receive buffer, as an IPC handle (P > 1); a failure travels as a status
+    constexpr size_t HW = (sizeof(hipIpcMemHandle_t) + 7) / 8;
+    std::vector<int64_t> mine_h(HW + 1, 0), all_h((HW + 1) * (size_t)P, 0);
+    int local_rc = SGX_OK;
+    std::string local_msg;
+    if (P > 1) {
+        hipIpcMemHandle_t h;
+        const hipError_t he = hipIpcGetMemHandle(&h, rd.data.p);
+        if (he != hipSuccess) {
+            local_rc = SGX_ERR_HIP;
+            local_msg = std::string("hipIpcGetMemHandle: ") + hipGetErrorString(he);
+        } else {
+            std::memcpy(mine_h.data(), &h, sizeof(h));
+        }
+        mine_h[HW] = local_rc;
+        SGX_TRY(allgather_i64(e, mine_h.data(), HW + 1, all_h.data()));
+        for (int32_t j = 0; j < P; ++j)
+            if (all_h[(size_t)j * (HW + 1) + HW] != SGX_OK) {
+                if (j == me) return fail_msg(local_rc, "%s (every rank fails this exchange)", local_msg.c_str());
+                return fail_msg(SGX_ERR_STATE, "exchange of shuffle %d failed on rank %d: every rank fails it", s.id, j);
+            }
+    }
+    // (b) where my contribution starts in every rank's receive buffer: [source][its maps][d's
+    //     reducers], i.e. after the blocks of d's reducers of every map of lower ranks
+    std::vector<int64_t> at((size_t)P, 0), piece_end((size_t)P, 0);
+    for (int32_t d = 0; d < P; ++d) {
+        int64_t o = 0;
+        for (size_t m = 0; m < M && srcs[m] < me; ++m)
+            for (int32_t r = bounds[(size_t)d]; r < bounds[(size_t)d + 1]; ++r) o += lens[m * R + r];
+        at[(size_t)d] = o;
+    }
+    // (c) the destinations: mine directly, the peers' through their handles
+    std::vector<void *> peer((size_t)P, nullptr);
+    std::vector<int64_t> to((size_t)P, 0);  // bytes I send to each rank
+    for (auto &lm : mine)
+        for (int32_t d = 0; d < P; ++d)
+            for (int32_t r = bounds[(size_t)d]; r < bounds[(size_t)d + 1]; ++r) to[(size_t)d] += lm.lens[(size_t)r];
+    auto close_all = [&]() {
+        for (int32_t d = 0; d < P; ++d)
+            if (peer[(size_t)d] && d != me) (void)hipIpcCloseMemHandle(peer[(size_t)d]);
+    };
+    peer[(size_t)me] = rd.data.p;
+    for (int32_t d = 0; d < P && local_rc == SGX_OK; ++d) {
+        if (d == me || to[(size_t)d] == 0) continue;
+        hipIpcMemHandle_t h;
+        std::memcpy(&h, &all_h[(size_t)d * (HW + 1)], sizeof(h));
+        const hipError_t he = hipIpcOpenMemHandle(&peer[(size_t)d], h, hipIpcMemLazyEnablePeerAccess);
+        if (he != hipSuccess) {
+            peer[(size_t)d] = nullptr;
+            local_rc = SGX_ERR_HIP;
+            local_msg = std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(he);
+        }
+    }
+    // (d) the gathers: padded maps by fragment table (one descriptor per block), contiguous
+    //     maps by byte ranges (64 KiB items)
+    std::vector<int64_t> frag, items;
+    int Gmax = 0;
+    bool al16 = true, al4 = true;
+    int64_t sent = 0, kept = 0;
+    std::vector<int64_t> off_in((size_t)P, 0);  // bytes of my earlier maps' pieces to each rank
+    for (size_t k = 0; k < mine.size() && local_rc == SGX_OK; ++k) {
+        MapOut &m = *mine[k].m;
+        const uint32_t *po = (const uint32_t *)m.part_off.p;  // record offsets (fixed codec)
+        for (int32_t d = 0; d < P; ++d) {
+            const int32_t b0 = bounds[(size_t)d], b1 = bounds[(size_t)d + 1];
+            int64_t l = 0, o = 0;
+            for (int32_t r = 0; r < b0; ++r) o += mine[k].lens[(size_t)r];
+            for (int32_t r = b0; r < b1; ++r) l += mine[k].lens[(size_t)r];
+            char *dst = (char *)peer[(size_t)d] + at[(size_t)d] + off_in[(size_t)d];
+            off_in[(size_t)d] += l;
+            (d == me ? kept : sent) += l;
+            if (l == 0) continue;
+            if (m.padded) {
+                const int G = m.frag_G;
+                Gmax = std::max(Gmax, G);
+                const uint32_t *fs = (const uint32_t *)m.frag.p;
+                const int64_t len = (int64_t)R * G;
+                for (int32_t p = b0; p < b1; ++p) {
+                    if (mine[k].lens[(size_t)p] == 0) continue;
+                    frag.insert(frag.end(), {(int64_t)(uintptr_t)m.data.p, (int64_t)(uintptr_t)fs,
+                                             (int64_t)(uintptr_t)(fs + len), (int64_t)(uintptr_t)(fs + 2 * len),
+                                             (int64_t)(uintptr_t)(dst + (int64_t)(po[p] - po[b0]) * s.rb), p, G, s.rb});
+                }
+            } else {
+                const char *src = (const char *)m.view() + o;
+                for (int64_t done = 0; done < l; done += 65536) {
+                    const int64_t b = std::min<int64_t>(65536, l - done);
+                    items.insert(items.end(), {(int64_t)(uintptr_t)(src + done), (int64_t)(uintptr_t)(dst + done), b});
+                    const uintptr_t u = (uintptr_t)(src + done) | (uintptr_t)(dst + done) | (uintptr_t)b;
+                    al16 = al16 && (u & 15) == 0;
+                    al4 = al4 && (u & 3) == 0;
+                }
+            }
+        }
+    }
+    auto launch = [&]() -> int {
+        for (auto &lm : mine) HIP_TRY(hipStreamWaitEvent(st, lm.m->done.ev, 0));
+        const size_t fb = frag.size() * 8, ib = items.size() * 8;
+        if (fb + ib == 0) return SGX_OK;
+        SGX_TRY(e->x_items.ensure(fb + ib));
+        SGX_TRY(e->x_items_dev.ensure(fb + ib));
+        std::memcpy(e->x_items.p, frag.data(), fb);
+        std::memcpy((char *)e->x_items.p + fb, items.data(), ib);
+        HIP_TRY(hipMemcpyAsync(e->x_items_dev.p, e->x_items.p, fb + ib, hipMemcpyHostToDevice, st));
+        if (!frag.empty())
+            HIP_TRY(launch_gather_frags((const int64_t *)e->x_items_dev.p, (int64_t)(frag.size() / FRAG_DESC_WORDS),
+                                        Gmax, st));
+        if (!items.empty())
+            HIP_TRY(launch_gather_items((const int64_t *)((char *)e->x_items_dev.p + fb), (int64_t)(items.size() / 3),
+                                        al16 ? 16 : al4 ? 4 : 1, st));
+        SGX_TRY(debug_sync(e, st, "exchange peer gather"));
+        return comm_wait(e);  // every byte has landed before the barrier says so
+    };
+    if (local_rc == SGX_OK) {
+        local_rc = launch();
+        if (local_rc != SGX_OK) local_msg = sgx_last_error();
+    }
+    // (e) the barrier: every rank's gather is complete (or failed) once this returns
+    if (P > 1) {
+        std::vector<int64_t> st_mine(1, local_rc), st_all((size_t)P, 0);
+        const int brc = allgather_i64(e, st_mine.data(), 1, st_all.data());
+        close_all();
+        if (brc != SGX_OK) return brc;
+        for (int32_t j = 0; j < P; ++j)
+            if (st_all[(size_t)j] != SGX_OK) {
+                if (j == me) return fail_msg(local_rc, "%s (every rank fails this exchange)", local_msg.c_str());
+                return fail_msg(SGX_ERR_STATE, "exchange of shuffle %d failed on rank %d: every rank fails it", s.id, j);
+            }
+    } else if (local_rc != SGX_OK) {
+        return fail_msg(local_rc, "%s", local_msg.c_str());
+    }
+    std::lock_guard<std::mutex> lk(e->stats_mu);
+    e->x_bytes[0] += sent;
+    e->x_bytes[1] += kept;
+    e->x_bytes[2] += 1;
+    return SGX_OK;
+}
+
 // One exchange round of shuffle s with this rank's maps `mine` (any number, the same call
 // order on every rank).  (1) all-gather of every rank's map count, then of {map id, R
 // lengths} per map; (2) the shuffle's reducer ranges -- fixed by its first round, so every
@@ -164,13 +316,15 @@ struct LocalMap {
 static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> &s, std::vector<LocalMap> mine,
                           int local_rc = SGX_OK, std::string local_msg = std::string()) {
     const int32_t P = e->nranks, R = s->R;
+    // the direct peer gather moves the blocks (a padded map's from its fragments); RCCL's
+    // send / recv and the host all-to-all move contiguous byte ranges
+    const bool p2p = (e->comm || e->host_comm) && !(e->flags & SGX_FLAG_NO_P2P_EXCHANGE);
     for (auto &lm : mine) {
         if (local_rc != SGX_OK) break;
         std::lock_guard<std::mutex> lk(lm.m->mu);
         int rc = lm.m->open ? fail_msg(SGX_ERR_STATE, "map %lld is still open", (long long)lm.id) : SGX_OK;
-        // a padded map is sent from its contiguous copy (sends are contiguous byte ranges)
         if (rc == SGX_OK) rc = finish_lengths(e, *c, *s, *lm.m);
-        if (rc == SGX_OK) rc = materialize(e, *c, *s, *lm.m);
+        if (rc == SGX_OK && !p2p) rc = materialize(e, *c, *s, *lm.m);
         if (rc != SGX_OK) {
             local_rc = rc;
             local_msg = sgx_last_error();
@@ -335,6 +489,12 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
             }
         }
         HIP_TRY(hipEventRecord(a2, st));
+    } else if (p2p) {
+        // a fresh receive buffer: peers write into it through its IPC handle
+        rd->data.release();
+        SGX_TRY(rd->data.ensure((size_t)std::max<int64_t>(total_recv, 16)));
+        HIP_TRY(hipEventRecord(a2, st));
+        SGX_TRY(p2p_data(e, *s, *rd, mine, bounds, lens, srcs, st));
     } else {
         SGX_TRY(rd->data.ensure((size_t)std::max<int64_t>(total_recv, 16)));
         for (auto &lm : mine) HIP_TRY(hipStreamWaitEvent(st, lm.m->done.ev, 0));
@@ -387,27 +547,33 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
             // grouped point-to-point: my sends to d go map after map (or as one packed piece),
             // and d posts its receives from me the same way (it knows my map count and lengths
             // from (1))
-            NCCL_TRY(ncclGroupStart());
-            for (int32_t d = 0; d < P; ++d) {
+            // every ncclSend / ncclRecv of the group, then ncclGroupEnd even when one of them
+            // failed (an open group would poison the communicator's next call)
+            ncclResult_t gr = ncclGroupStart();
+            if (gr != ncclSuccess) return fail_msg(SGX_ERR_COMM, "ncclGroupStart failed: %s", ncclGetErrorString(gr));
+            ncclResult_t first = ncclSuccess;
+            auto note = [&](ncclResult_t r) {
+                if (r != ncclSuccess && first == ncclSuccess) first = r;
+            };
+            for (int32_t d = 0; d < P && first == ncclSuccess; ++d) {
                 if (pack_mine) {
                     if (sc[(size_t)d] > 0)
-                        NCCL_TRY(ncclSend((const char *)e->x_pack.p + sd[(size_t)d], (size_t)sc[(size_t)d], ncclUint8,
-                                          d, e->comm, st));
+                        note(ncclSend((const char *)e->x_pack.p + sd[(size_t)d], (size_t)sc[(size_t)d], ncclUint8, d,
+                                      e->comm, st));
                     continue;
                 }
-                for (size_t k = 0; k < mine.size(); ++k) {
+                for (size_t k = 0; k < mine.size() && first == ncclSuccess; ++k) {
                     int64_t o, l;
                     piece(k, d, &o, &l);
-                    if (l > 0)
-                        NCCL_TRY(ncclSend((const char *)mine[k].m->view() + o, (size_t)l, ncclUint8, d, e->comm, st));
+                    if (l > 0) note(ncclSend((const char *)mine[k].m->view() + o, (size_t)l, ncclUint8, d, e->comm, st));
                 }
             }
             size_t m = 0;
-            for (int32_t j = 0; j < P; ++j) {
+            for (int32_t j = 0; j < P && first == ncclSuccess; ++j) {
                 if (packed[(size_t)j]) {
                     if (rc[(size_t)j] > 0)
-                        NCCL_TRY(ncclRecv((char *)rd->data.p + rdp[(size_t)j], (size_t)rc[(size_t)j], ncclUint8, j,
-                                          e->comm, st));
+                        note(ncclRecv((char *)rd->data.p + rdp[(size_t)j], (size_t)rc[(size_t)j], ncclUint8, j,
+                                      e->comm, st));
                     m += (size_t)counts[(size_t)j];
                     continue;
                 }
@@ -415,11 +581,13 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
                 for (int64_t k = 0; k < counts[(size_t)j]; ++k, ++m) {
                     int64_t l = 0;
                     for (int32_t r = rd->r0; r < rd->r1; ++r) l += lens[m * R + r];
-                    if (l > 0) NCCL_TRY(ncclRecv((char *)rd->data.p + off, (size_t)l, ncclUint8, j, e->comm, st));
+                    if (l > 0) note(ncclRecv((char *)rd->data.p + off, (size_t)l, ncclUint8, j, e->comm, st));
                     off += l;
                 }
             }
-            NCCL_TRY(ncclGroupEnd());
+            note(ncclGroupEnd());
+            if (first != ncclSuccess)
+                return fail_msg(SGX_ERR_COMM, "grouped ncclSend / ncclRecv failed: %s", ncclGetErrorString(first));
         } else {
             // host backend: stage my pieces out packed [destination][map], exchange on the
             // host, stage the received bytes in
@@ -442,6 +610,12 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
                 HIP_TRY(hipMemcpyAsync(rd->data.p, e->x_recv.p, (size_t)total_recv, hipMemcpyHostToDevice, st));
             HIP_TRY(hipStreamSynchronize(st));  // the pinned staging buffers are reused next round
         }
+    }
+    if (collective && !p2p) {  // RCCL send / recv or the host all-to-all: contiguous pieces
+        std::lock_guard<std::mutex> lk(e->stats_mu);
+        e->x_bytes[0] += out_total - sc[(size_t)e->rank];
+        e->x_bytes[1] += sc[(size_t)e->rank];
+        e->x_bytes[2] += 1;
     }
     HIP_TRY(hipEventRecord(a3, st));
     HIP_TRY(rd->done.record(st));

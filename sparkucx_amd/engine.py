@@ -537,6 +537,12 @@ class ShuffleEngine:
               "copy_items")
 
     # -- measurement ----------------------------------------------------------------------
+    def exchange_bytes(self) -> dict:
+        """Bytes the exchange rounds moved since stats_reset: to other ranks, kept, rounds."""
+        out = (ctypes.c_int64 * 3)()
+        check(lib().sgx_exchange_bytes(self.handle, out), "exchangeBytes")
+        return {"sent": int(out[0]), "kept": int(out[1]), "rounds": int(out[2])}
+
     def stats_reset(self):
         check(lib().sgx_stats_reset(self.handle), "stats_reset")
 

@@ -72,7 +72,7 @@ def all_maps(world, counts_by_round, upto):
     return sorted(out, key=lambda x: map_id(*x))
 
 
-def worker(rank, world, port, backend, codec, R, n, result_dir, placement, keys, counts_by_round, rb):
+def worker(rank, world, port, backend, codec, R, n, result_dir, placement, keys, counts_by_round, rb, flags=0):
     import torch.distributed as dist
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -82,7 +82,7 @@ def worker(rank, world, port, backend, codec, R, n, result_dir, placement, keys,
         import oracle
         import sparkucx_amd as sgx
 
-        e = sgx.ShuffleEngine(device=rank if backend == "rccl" else 0, comm_timeout_ms=60_000)
+        e = sgx.ShuffleEngine(device=rank if backend == "rccl" else 0, comm_timeout_ms=60_000, flags=flags)
         if backend == "rccl":
             uid = [sgx.get_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
@@ -101,10 +101,15 @@ def worker(rank, world, port, backend, codec, R, n, result_dir, placement, keys,
         if placement == "bytes":
             e.set_reducer_placement(sid, "bytes")
         outs = {}  # (t, j, k) -> oracle map output
+        published = 0  # bytes of my maps: what the exchange rounds must move, no more
         for t, counts in enumerate(counts_by_round):
             for k in range(counts[rank]):
                 recs = batch(oracle, t, rank, k, n, keys, rb)
-                e.write_map(sid, map_id(t, rank, k), recs, len(recs), rb)
+                lens_k = e.write_map(sid, map_id(t, rank, k), recs, len(recs), rb, R)
+                published += int(lens_k.sum())
+                if flags & sgx.FLAG_PAD_ANY_SIZE and codec == "fixed" and not flags & sgx.FLAG_NO_P2P_EXCHANGE:
+                    if e.map_layout(sid, map_id(t, rank, k)) != sgx.LAYOUT_PADDED:
+                        raise AssertionError("a map under a communicator was not written in one pass")
             e.exchange(sid)  # every rank, whatever it holds (maybe nothing)
             e.sync()
             for key in all_maps(world, counts_by_round, t):
@@ -180,6 +185,9 @@ def worker(rank, world, port, backend, codec, R, n, result_dir, placement, keys,
         st = e.stats()
         if msg == "ok" and st.count["alltoall"] < len(counts_by_round):
             msg = f"only {st.count['alltoall']} exchange rounds recorded"
+        xb = e.exchange_bytes()
+        if msg == "ok" and xb["sent"] + xb["kept"] != published:
+            msg = f"the exchange moved {xb['sent']} + {xb['kept']} bytes for {published} published"
         e.close()
     except Exception:  # noqa: BLE001 - reported through the result file
         msg = traceback.format_exc()
@@ -190,12 +198,12 @@ def worker(rank, world, port, backend, codec, R, n, result_dir, placement, keys,
 
 
 def run_world(tmp_path, world, backend, codec, R, n, placement="even", keys="uniform", counts_by_round=None,
-              rb=16):
+              rb=16, flags=0):
     import torch.multiprocessing as mp
 
     counts_by_round = counts_by_round or [[1] * world] * 3
     mp.start_processes(worker, args=(world, free_port(), backend, codec, R, n, str(tmp_path), placement, keys,
-                                     counts_by_round, rb),
+                                     counts_by_round, rb, flags),
                        nprocs=world, start_method="spawn", join=True)
     msgs = {r: (tmp_path / f"rank{r}").read_text() for r in range(world)}
     bad = {r: m for r, m in msgs.items() if m != "ok"}
@@ -271,6 +279,43 @@ def test_exchange_terasort_c4(sgx_lib, oracle_lib, tmp_path, world, R):
     # keys sorted globally; records equal as a multiset in key order (ties: stable per reducer)
     assert np.array_equal(got[:, :10], want[:, :10])
     assert np.array_equal(np.sort(got.view("V100").reshape(-1)), np.sort(want.view("V100").reshape(-1)))
+
+
+@pytest.mark.parametrize("world,R,keys", [(2, 1024, "uniform"), (4, 200, "uniform"), (8, 1024, "uniform"),
+                                          (3, 4096, "zipf")])
+def test_exchange_p2p_from_padded_maps(sgx_lib, oracle_lib, tmp_path, world, R, keys):
+    """The direct peer gather: under a communicator every map is written in ONE
+    pass (padded, SGX_FLAG_PAD_ANY_SIZE so the test's maps qualify) and each rank writes the
+    blocks other ranks own straight from the map's fragments into their receive buffers,
+    mapped through IPC handles (separate processes sharing cuda:0).  Blocks and reads as the
+    oracle's; the bytes moved equal the published lengths (no sub-bin slack)."""
+    import sparkucx_amd as sgx
+
+    run_world(tmp_path, world, "host", "fixed", R, 150_000, keys=keys,
+              placement="bytes" if keys == "zipf" else "even",
+              counts_by_round=[[1] * world, [2] + [0] * (world - 2) + [1]], flags=sgx.FLAG_PAD_ANY_SIZE)
+
+
+def test_exchange_p2p_terasort_padded(sgx_lib, oracle_lib, tmp_path):
+    """C4's exchange over the peer gather from padded 100 B TeraSort maps (RangePartitioner)."""
+    import oracle
+    import sparkucx_amd as sgx
+
+    counts = [[1, 1, 1], [2, 0, 0]]
+    run_world(tmp_path, 3, "host", "fixed", 1024, 30_000, counts_by_round=counts, rb=100, flags=sgx.FLAG_PAD_ANY_SIZE)
+    got = np.concatenate([np.load(tmp_path / f"sorted{r}.npy") for r in range(3)])
+    allrecs = np.concatenate([batch(oracle, *x, 30_000, "uniform", 100) for x in all_maps(3, counts, 1)])
+    assert np.array_equal(got[:, :10], allrecs[np.lexsort(allrecs[:, :10].T[::-1])][:, :10])
+
+
+@pytest.mark.parametrize("codec", ["fixed", "kryo+lz4"])
+def test_exchange_staged_all_to_all_no_p2p(sgx_lib, oracle_lib, tmp_path, codec):
+    """SGX_FLAG_NO_P2P_EXCHANGE: the host all-to-all of contiguous map outputs (two-pass
+    writes under a communicator), uneven maps."""
+    import sparkucx_amd as sgx
+
+    run_world(tmp_path, 3, "host", codec, 200, 30_000, counts_by_round=[[0, 1, 4], [2, 0, 1]],
+              flags=sgx.FLAG_NO_P2P_EXCHANGE)
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])

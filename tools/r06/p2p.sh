@@ -1,0 +1,44 @@
+#!/bin/bash
+# Round 6: the direct peer gather exchange (single-pass maps under a communicator): multirank
+# parity (ranks share cuda:0, IPC-mapped receive buffers), the self-exchange and 8-rank host
+# rehearsal bench lines (P2P vs --no-p2p), then C1 A/B of engine builds.
+# usage: bash tools/r06/p2p.sh <tag> [lib...]
+tag=$1; shift
+out=$GRAFT_REPO_ROOT/gpurun_out/$tag
+mkdir -p "$out"
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+step() {  # step <timeout> <log> <cmd...>: test failures (rc 1) reported, anything else stops the run
+  local t=$1 log=$2; shift 2
+  timeout -k 10 "$t" "$@" > "$out/$log" 2>&1
+  local rc=$?
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "step $log: rc $rc"; tail -30 "$out/$log"; exit $rc; fi
+  [ $rc -eq 1 ] && { echo "step $log: rc 1"; tail -40 "$out/$log"; }
+  return 0
+}
+line() { grep '^{' "$out/$1" | python3 -c "
+import json,sys
+j=json.loads(sys.stdin.read())
+print('$1', j['value'], j['ms_per_step'], j['roofline']['frac'], j['roofline_map_side']['frac'], j['config'].get('map_layout','')[:8], j.get('exchange_bytes'), j.get('xgmi_roofline',{}).get('alltoall_ms_max_rank'))" || true; }
+step 900 pytest_x.log python -u -m pytest tests/test_exchange_multirank.py -v -x --timeout 300 --timeout-method thread -p no:cacheprovider
+tail -3 "$out/pytest_x.log"
+step 600 pytest_p.log python -u -m pytest tests/test_padded.py tests/test_streaming_commit.py tests/test_read_metrics.py -q -x --timeout 300 --timeout-method thread -p no:cacheprovider
+tail -2 "$out/pytest_p.log"
+step 300 bench_selfx.log python -u bench.py --self-exchange --no-cpu-baseline --steps 20
+line bench_selfx.log
+step 300 bench_selfx_nop2p.log python -u bench.py --self-exchange --no-p2p --no-cpu-baseline --steps 20
+line bench_selfx_nop2p.log
+step 600 bench_host8.log python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 8 --comm host --records 67108864 --steps 6 --warmup 2 --no-cpu-baseline
+line bench_host8.log
+step 600 bench_host8_nop2p.log python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 --master-addr 127.0.0.1 --master-port 29534 bench.py --gpus 8 --comm host --records 67108864 --steps 6 --warmup 2 --no-cpu-baseline --no-p2p
+line bench_host8_nop2p.log
+for rep in 1 2; do
+  for lib in "$@"; do
+    if [ "$lib" = tree ]; then
+      step 200 bench_${lib}_$rep.log python -u bench.py --no-cpu-baseline --no-live-pmc --steps 40
+    else
+      step 200 bench_${lib}_$rep.log python -u tools/ab_run.py tools/ab/libsgx_$lib.so bench --no-cpu-baseline --no-live-pmc --steps 40
+    fi
+    line bench_${lib}_$rep.log
+  done
+done
+echo done > "$out/DONE"
