@@ -184,7 +184,7 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     if (dev < 0 || dev >= ndev) return fail_msg(SGX_ERR_INVALID, "sgx_create: device %d of %d", dev, ndev);
     if (cfg && (cfg->hist_mode < SGX_HIST_ATOMIC || cfg->hist_mode > SGX_HIST_BALLOT ||
                 cfg->rank_mode < SGX_RANK_ORDERED || cfg->rank_mode > SGX_RANK_MATCH || cfg->flags < 0 ||
-                cfg->flags > 4095 || cfg->comm_timeout_ms < 0 || cfg->num_chunks < 0))
+                cfg->flags > 8191 || cfg->comm_timeout_ms < 0 || cfg->num_chunks < 0))
         return fail_msg(SGX_ERR_INVALID, "sgx_create: bad configuration");
     HIP_TRY(hipSetDevice(dev));
     hipDeviceProp_t prop;
@@ -218,6 +218,11 @@ extern "C" void sgx_destroy(sgx_engine *e) {
     e->resolve_stats();
     e->shuffles.clear();  // map outputs and rounds free their HBM
     e->ctxs.clear();
+    for (auto &pm : e->p2p_mapped) {  // peers' receive buffers the last rounds mapped
+        for (void *q : pm.ptrs) (void)hipIpcCloseMemHandle(q);
+        if (pm.done) (void)hipEventDestroy(pm.done);
+    }
+    e->p2p_mapped.clear();
     for (hipEvent_t ev : e->ev_free) (void)hipEventDestroy(ev);
     if (e->comm) {
         if (e->comm_broken) (void)ncclCommAbort(e->comm);

@@ -385,6 +385,16 @@ struct sgx_engine {
     // RCCL exchange of a rank holding many small maps: its pieces packed per destination
     sgx::DevBuf x_pack, x_items_dev;
     sgx::HostPinned x_items;
+    // the direct peer gather: its descriptors' upload (reused by the next round once done),
+    // peers' receive buffers still mapped by a round whose gather may be running (closed once
+    // the round's event has passed), and the RCCL completion barrier's word
+    sgx::Event x_items_up;
+    struct PeerMaps {
+        std::vector<void *> ptrs;
+        hipEvent_t done = nullptr;
+    };
+    std::vector<PeerMaps> p2p_mapped;
+    sgx::DevBuf p2p_word;
     sgx::DevBuf jump_dev;  // XORShiftRandom jump table (built once, read-only after)
     std::mutex jump_mu;
     std::shared_ptr<sgx::PoolState> pool;  // MemoryPool (sgx_pool.cpp), created on first use

@@ -149,71 +149,104 @@ struct LocalMap {
 };
 }  // namespace
 
+// Unmap peers' receive buffers of earlier rounds whose gathers have finished (all of them
+// with `wait`).  Caller holds comm_mu.
+static void p2p_release(sgx_engine *e, bool wait) {
+    auto &v = e->p2p_mapped;
+    for (auto it = v.begin(); it != v.end();) {
+        if (!wait && it->done && hipEventQuery(it->done) == hipErrorNotReady) {
+            ++it;
+            continue;
+        }
+        if (it->done) (void)hipEventSynchronize(it->done);
+        for (void *q : it->ptrs) (void)hipIpcCloseMemHandle(q);
+        if (it->done) (void)hipEventDestroy(it->done);
+        it = v.erase(it);
+    }
+}
+
 // Direct peer gather: rank `me` writes the blocks of its maps that rank d owns
 // straight into d's receive buffer, at the place d's plan gives them -- a padded map's blocks
 // from their fragments (one workgroup per fragment), a contiguous map's as byte ranges -- in
 // one gather launch per kind on the exchange stream.  Peers' buffers are mapped into this
 // process through IPC handles all-gathered by the backend (the image's dmabuf IPC; this rank's
-// own buffer directly); a second all-gather after every rank's gather has finished is the
-// completion barrier, and carries each rank's status so a failed gather fails the round on
-// every rank.  No pack step and no contiguous copy of a padded map: each map's published bytes
-// leave it exactly once, sent bytes = the blocks' lengths.
+// own buffer directly), and a second all-gather says every rank has mapped its peers (or
+// fails the round on every rank).  Completion: with RCCL a one-word ncclAllReduce on the
+// exchange stream behind the gather (the round stays asynchronous; readers wait for the
+// round's event), with host collectives a host barrier after the gather.  No pack step and no
+// contiguous copy of a padded map: each map's published bytes leave it exactly once, sent
+// bytes = the blocks' lengths.
 static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<LocalMap> &mine,
                     const std::vector<int32_t> &bounds, const std::vector<int64_t> &lens,
                     const std::vector<int32_t> &srcs, hipStream_t st) {
     const int32_t P = e->nranks, me = e->rank, R = s.R;
     const size_t M = srcs.size();
-    // (a) every rank's receive buffer, as an IPC handle (P > 1); a failure travels as a status
+    p2p_release(e, false);
+    // any rank's failure before the gather fails the round on every rank (status all-gather)
+    auto agree = [&](int rc, const std::string &msg, const int64_t *extra, size_t nextra,
+                     std::vector<int64_t> *all) -> int {
+        std::vector<int64_t> mine_w(nextra + 1, 0);
+        mine_w[0] = rc;
+        for (size_t i = 0; i < nextra; ++i) mine_w[i + 1] = extra[i];
+        std::vector<int64_t> tmp((nextra + 1) * (size_t)P, 0);
+        SGX_TRY(allgather_i64(e, mine_w.data(), nextra + 1, tmp.data()));
+        for (int32_t j = 0; j < P; ++j)
+            if (tmp[(size_t)j * (nextra + 1)] != SGX_OK) {
+                if (j == me) return fail_msg(rc, "%s (every rank fails this exchange)", msg.c_str());
+                return fail_msg(SGX_ERR_STATE, "exchange of shuffle %d failed on rank %d: every rank fails it", s.id, j);
+            }
+        if (all) *all = std::move(tmp);
+        return SGX_OK;
+    };
+    // (a) every rank's receive buffer as an IPC handle
     constexpr size_t HW = (sizeof(hipIpcMemHandle_t) + 7) / 8;
-    std::vector<int64_t> mine_h(HW + 1, 0), all_h((HW + 1) * (size_t)P, 0);
+    std::vector<int64_t> all_h;
     int local_rc = SGX_OK;
     std::string local_msg;
     if (P > 1) {
+        int64_t hw[HW] = {0};
         hipIpcMemHandle_t h;
         const hipError_t he = hipIpcGetMemHandle(&h, rd.data.p);
         if (he != hipSuccess) {
             local_rc = SGX_ERR_HIP;
-            local_msg = std::string("hipIpcGetMemHandle: ") + hipGetErrorString(he);
+            hipPointerAttribute_t pa{};
+            const hipError_t ae = hipPointerGetAttributes(&pa, rd.data.p);
+            char buf[256];
+            std::snprintf(buf, sizeof buf, "hipIpcGetMemHandle(%p, %zu B): %s (pointer attributes: %s, type %d, device %d)",
+                          rd.data.p, rd.data.cap, hipGetErrorString(he), hipGetErrorString(ae), (int)pa.type, pa.device);
+            local_msg = buf;
         } else {
-            std::memcpy(mine_h.data(), &h, sizeof(h));
+            std::memcpy(hw, &h, sizeof(h));
         }
-        mine_h[HW] = local_rc;
-        SGX_TRY(allgather_i64(e, mine_h.data(), HW + 1, all_h.data()));
-        for (int32_t j = 0; j < P; ++j)
-            if (all_h[(size_t)j * (HW + 1) + HW] != SGX_OK) {
-                if (j == me) return fail_msg(local_rc, "%s (every rank fails this exchange)", local_msg.c_str());
-                return fail_msg(SGX_ERR_STATE, "exchange of shuffle %d failed on rank %d: every rank fails it", s.id, j);
-            }
+        SGX_TRY(agree(local_rc, local_msg, hw, HW, &all_h));
     }
     // (b) where my contribution starts in every rank's receive buffer: [source][its maps][d's
     //     reducers], i.e. after the blocks of d's reducers of every map of lower ranks
-    std::vector<int64_t> at((size_t)P, 0), piece_end((size_t)P, 0);
+    std::vector<int64_t> at((size_t)P, 0), to((size_t)P, 0);
     for (int32_t d = 0; d < P; ++d) {
         int64_t o = 0;
         for (size_t m = 0; m < M && srcs[m] < me; ++m)
             for (int32_t r = bounds[(size_t)d]; r < bounds[(size_t)d + 1]; ++r) o += lens[m * R + r];
         at[(size_t)d] = o;
     }
-    // (c) the destinations: mine directly, the peers' through their handles
-    std::vector<void *> peer((size_t)P, nullptr);
-    std::vector<int64_t> to((size_t)P, 0);  // bytes I send to each rank
     for (auto &lm : mine)
         for (int32_t d = 0; d < P; ++d)
             for (int32_t r = bounds[(size_t)d]; r < bounds[(size_t)d + 1]; ++r) to[(size_t)d] += lm.lens[(size_t)r];
-    auto close_all = [&]() {
-        for (int32_t d = 0; d < P; ++d)
-            if (peer[(size_t)d] && d != me) (void)hipIpcCloseMemHandle(peer[(size_t)d]);
-    };
+    // (c) the destinations: mine directly, the peers' through their handles
+    std::vector<void *> peer((size_t)P, nullptr);
     peer[(size_t)me] = rd.data.p;
+    sgx_engine::PeerMaps mapped;
     for (int32_t d = 0; d < P && local_rc == SGX_OK; ++d) {
         if (d == me || to[(size_t)d] == 0) continue;
         hipIpcMemHandle_t h;
-        std::memcpy(&h, &all_h[(size_t)d * (HW + 1)], sizeof(h));
+        std::memcpy(&h, &all_h[(size_t)d * (HW + 1) + 1], sizeof(h));
         const hipError_t he = hipIpcOpenMemHandle(&peer[(size_t)d], h, hipIpcMemLazyEnablePeerAccess);
         if (he != hipSuccess) {
             peer[(size_t)d] = nullptr;
             local_rc = SGX_ERR_HIP;
             local_msg = std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(he);
+        } else {
+            mapped.ptrs.push_back(peer[(size_t)d]);
         }
     }
     // (d) the gathers: padded maps by fragment table (one descriptor per block), contiguous
@@ -258,41 +291,65 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
             }
         }
     }
+    auto unmap_now = [&]() {
+        for (void *q : mapped.ptrs) (void)hipIpcCloseMemHandle(q);
+        mapped.ptrs.clear();
+    };
+    if (P > 1) {  // every rank has mapped the buffers it writes to (or the round fails everywhere)
+        const int arc = agree(local_rc, local_msg, nullptr, 0, nullptr);
+        if (arc != SGX_OK) {
+            unmap_now();
+            return arc;
+        }
+    }
     auto launch = [&]() -> int {
         for (auto &lm : mine) HIP_TRY(hipStreamWaitEvent(st, lm.m->done.ev, 0));
         const size_t fb = frag.size() * 8, ib = items.size() * 8;
         if (fb + ib == 0) return SGX_OK;
+        HIP_TRY(e->x_items_up.wait_host());  // the last round's descriptors have been uploaded
         SGX_TRY(e->x_items.ensure(fb + ib));
         SGX_TRY(e->x_items_dev.ensure(fb + ib));
         std::memcpy(e->x_items.p, frag.data(), fb);
         std::memcpy((char *)e->x_items.p + fb, items.data(), ib);
         HIP_TRY(hipMemcpyAsync(e->x_items_dev.p, e->x_items.p, fb + ib, hipMemcpyHostToDevice, st));
+        HIP_TRY(e->x_items_up.record(st));
         if (!frag.empty())
             HIP_TRY(launch_gather_frags((const int64_t *)e->x_items_dev.p, (int64_t)(frag.size() / FRAG_DESC_WORDS),
                                         Gmax, st));
         if (!items.empty())
             HIP_TRY(launch_gather_items((const int64_t *)((char *)e->x_items_dev.p + fb), (int64_t)(items.size() / 3),
                                         al16 ? 16 : al4 ? 4 : 1, st));
-        SGX_TRY(debug_sync(e, st, "exchange peer gather"));
-        return comm_wait(e);  // every byte has landed before the barrier says so
+        return debug_sync(e, st, "exchange peer gather");
     };
-    if (local_rc == SGX_OK) {
-        local_rc = launch();
-        if (local_rc != SGX_OK) local_msg = sgx_last_error();
-    }
-    // (e) the barrier: every rank's gather is complete (or failed) once this returns
-    if (P > 1) {
-        std::vector<int64_t> st_mine(1, local_rc), st_all((size_t)P, 0);
-        const int brc = allgather_i64(e, st_mine.data(), 1, st_all.data());
-        close_all();
+    int rc = launch();
+    if (P > 1 && e->comm) {
+        // completion barrier on the stream: a peer's allreduce runs after its gather, so once
+        // this one completes every block of my reducers has landed (a rank whose launch failed
+        // still joins it, then fails)
+        SGX_TRY(e->p2p_word.ensure(16));
+        const ncclResult_t nr = ncclAllReduce(e->p2p_word.p, (char *)e->p2p_word.p + 8, 1, ncclInt64, ncclSum,
+                                              e->comm, st);
+        if (nr != ncclSuccess && rc == SGX_OK)
+            rc = fail_msg(SGX_ERR_COMM, "ncclAllReduce (peer gather barrier) failed: %s", ncclGetErrorString(nr));
+        hipEvent_t ev = nullptr;
+        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess && hipEventRecord(ev, st) == hipSuccess) {
+            mapped.done = ev;
+            e->p2p_mapped.push_back(std::move(mapped));
+        } else {
+            if (ev) (void)hipEventDestroy(ev);
+            (void)hipStreamSynchronize(st);
+            unmap_now();
+        }
+        if (rc != SGX_OK) return rc;
+    } else if (P > 1) {
+        // host collectives: the gather has finished on every rank once the barrier returns
+        if (rc == SGX_OK) rc = comm_wait(e);
+        const std::string msg = rc == SGX_OK ? std::string() : std::string(sgx_last_error());
+        const int brc = agree(rc, msg, nullptr, 0, nullptr);
+        unmap_now();
         if (brc != SGX_OK) return brc;
-        for (int32_t j = 0; j < P; ++j)
-            if (st_all[(size_t)j] != SGX_OK) {
-                if (j == me) return fail_msg(local_rc, "%s (every rank fails this exchange)", local_msg.c_str());
-                return fail_msg(SGX_ERR_STATE, "exchange of shuffle %d failed on rank %d: every rank fails it", s.id, j);
-            }
-    } else if (local_rc != SGX_OK) {
-        return fail_msg(local_rc, "%s", local_msg.c_str());
+    } else if (rc != SGX_OK) {
+        return rc;
     }
     std::lock_guard<std::mutex> lk(e->stats_mu);
     e->x_bytes[0] += sent;

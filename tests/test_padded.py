@@ -327,12 +327,17 @@ def test_padded_fetch_into_unaligned_device_memory(sgx_lib, pad_engine, oracle_l
         pad_engine.unregister_shuffle(sid)
 
 
-def test_padded_exchange_one_rank(sgx_lib, oracle_lib):
-    """A communicator (even a one-rank one, the self-exchange stand-in for the multi-rank path)
-    keeps maps written after it contiguous; a map written padded before the communicator
-    existed is exchanged through its contiguous copy.  Both exchange to the oracle's blocks."""
+@pytest.mark.parametrize("p2p", [True, False])
+def test_padded_exchange_one_rank(sgx_lib, oracle_lib, p2p):
+    """A one-rank communicator (the self-exchange stand-in for the multi-rank path).  With the
+    direct peer gather (the default) maps written after it stay single-pass (padded) and the
+    exchange gathers their blocks from the fragments; with SGX_FLAG_NO_P2P_EXCHANGE they are
+    written contiguous for RCCL's send / recv, and a map written padded before the
+    communicator existed is exchanged through its contiguous copy.  Every way gives the
+    oracle's blocks, and the exchange moves exactly the published bytes."""
     R = 1024
-    with sgx_lib.ShuffleEngine(device=0, flags=sgx_lib.FLAG_PAD_ANY_SIZE) as e:
+    flags = sgx_lib.FLAG_PAD_ANY_SIZE | (0 if p2p else sgx_lib.FLAG_NO_P2P_EXCHANGE)
+    with sgx_lib.ShuffleEngine(device=0, flags=flags) as e:
         e.register_shuffle(1, R)
         early = oracle_lib.gen_uniform16(300_000, 22)
         e.write_map(1, 5, early, len(early), 16, R)
@@ -340,9 +345,11 @@ def test_padded_exchange_one_rank(sgx_lib, oracle_lib):
         e.comm_init(1, 0, sgx_lib.get_unique_id())
         recs = oracle_lib.gen_uniform16(400_000, 23)
         e.write_map(1, 6, recs, len(recs), 16, R)
-        assert e.map_layout(1, 6) == sgx_lib.LAYOUT_CONTIGUOUS
+        assert e.map_layout(1, 6) == (sgx_lib.LAYOUT_PADDED if p2p else sgx_lib.LAYOUT_CONTIGUOUS)
+        e.stats_reset()
         e.exchange(1)
         e.sync()
+        assert e.exchange_bytes() == {"sent": 0, "kept": 16 * (len(early) + len(recs)), "rounds": 1}
         for mid, src in ((5, early), (6, recs)):
             data, lens = e.fetch_blocks(1, [mid] * R, list(range(R)))
             out, counts = oracle_lib.map_write(src, R)
