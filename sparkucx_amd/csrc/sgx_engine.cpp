@@ -218,11 +218,11 @@ extern "C" void sgx_destroy(sgx_engine *e) {
     e->resolve_stats();
     e->shuffles.clear();  // map outputs and rounds free their HBM
     e->ctxs.clear();
-    for (auto &pm : e->p2p_mapped) {  // peers' receive buffers the last rounds mapped
-        for (void *q : pm.ptrs) (void)hipIpcCloseMemHandle(q);
-        if (pm.done) (void)hipEventDestroy(pm.done);
+    for (auto &kv : e->p2p_cache) {  // peers' receive buffers the exchange mapped
+        (void)hipIpcCloseMemHandle(kv.second.ptr);
+        if (kv.second.done) (void)hipEventDestroy(kv.second.done);
     }
-    e->p2p_mapped.clear();
+    e->p2p_cache.clear();
     for (hipEvent_t ev : e->ev_free) (void)hipEventDestroy(ev);
     if (e->comm) {
         if (e->comm_broken) (void)ncclCommAbort(e->comm);

@@ -223,6 +223,11 @@ struct Round {
     std::vector<int64_t> block_off;      // [M][nmine] byte offset in `data` (or in alias[j])
     int32_t r0 = 0, r1 = 0;              // my reducers [r0, r1)
     DevBuf data;                          // receive buffer
+    // the receive buffer's IPC handle (the direct peer gather), taken once per allocation: it
+    // moves with `data` when a re-run round reuses the buffer, so peers keep their mapping
+    hipIpcMemHandle_t ipc{};
+    bool ipc_valid = false;
+    uint64_t ipc_gen = 0;  // this rank's serial of the allocation: peers key their mappings on it
     // P == 1 without a communicator: the map outputs themselves ([M], block_off inside each)
     std::vector<std::shared_ptr<MapOut>> alias;
     // sgx_import_blocks: blocks a reader fetched from elsewhere (0 = an exchange round)
@@ -389,11 +394,16 @@ struct sgx_engine {
     // peers' receive buffers still mapped by a round whose gather may be running (closed once
     // the round's event has passed), and the RCCL completion barrier's word
     sgx::Event x_items_up;
-    struct PeerMaps {
-        std::vector<void *> ptrs;
-        hipEvent_t done = nullptr;
+    // peers' receive buffers mapped by the direct peer gather, by handle: kept open across
+    // rounds (a re-run round reuses its buffer, so its handle comes back); closed once unused
+    // for a few rounds and the last gather into it has finished
+    struct PeerMap {
+        void *ptr = nullptr;
+        uint64_t last_round = 0;
+        hipEvent_t done = nullptr;  // behind the last round's gather that wrote into it
     };
-    std::vector<PeerMaps> p2p_mapped;
+    std::map<std::string, PeerMap> p2p_cache;  // key: rank, allocation serial, handle bytes
+    uint64_t p2p_rounds = 0, p2p_gen = 0;
     sgx::DevBuf p2p_word;
     sgx::DevBuf jump_dev;  // XORShiftRandom jump table (built once, read-only after)
     std::mutex jump_mu;

@@ -149,19 +149,23 @@ struct LocalMap {
 };
 }  // namespace
 
-// Unmap peers' receive buffers of earlier rounds whose gathers have finished (all of them
-// with `wait`).  Caller holds comm_mu.
-static void p2p_release(sgx_engine *e, bool wait) {
-    auto &v = e->p2p_mapped;
-    for (auto it = v.begin(); it != v.end();) {
-        if (!wait && it->done && hipEventQuery(it->done) == hipErrorNotReady) {
+// Unmap peers' receive buffers no round used in the last few (their last gather finished; all
+// with `all`, after waiting).  Caller holds comm_mu.
+static void p2p_release(sgx_engine *e, bool all) {
+    constexpr uint64_t KEEP_ROUNDS = 4;
+    for (auto it = e->p2p_cache.begin(); it != e->p2p_cache.end();) {
+        sgx_engine::PeerMap &pm = it->second;
+        const bool stale = all || e->p2p_rounds - pm.last_round > KEEP_ROUNDS;
+        if (!stale || (!all && pm.done && hipEventQuery(pm.done) == hipErrorNotReady)) {
             ++it;
             continue;
         }
-        if (it->done) (void)hipEventSynchronize(it->done);
-        for (void *q : it->ptrs) (void)hipIpcCloseMemHandle(q);
-        if (it->done) (void)hipEventDestroy(it->done);
-        it = v.erase(it);
+        if (pm.done) {
+            (void)hipEventSynchronize(pm.done);
+            (void)hipEventDestroy(pm.done);
+        }
+        (void)hipIpcCloseMemHandle(pm.ptr);
+        it = e->p2p_cache.erase(it);
     }
 }
 
@@ -181,6 +185,7 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
                     const std::vector<int32_t> &srcs, hipStream_t st) {
     const int32_t P = e->nranks, me = e->rank, R = s.R;
     const size_t M = srcs.size();
+    ++e->p2p_rounds;
     p2p_release(e, false);
     // any rank's failure before the gather fails the round on every rank (status all-gather)
     auto agree = [&](int rc, const std::string &msg, const int64_t *extra, size_t nextra,
@@ -199,14 +204,15 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
         return SGX_OK;
     };
     // (a) every rank's receive buffer as an IPC handle
-    constexpr size_t HW = (sizeof(hipIpcMemHandle_t) + 7) / 8;
+    constexpr size_t HW = (sizeof(hipIpcMemHandle_t) + 7) / 8 + 1;  // the handle, then its serial
     std::vector<int64_t> all_h;
     int local_rc = SGX_OK;
     std::string local_msg;
     if (P > 1) {
         int64_t hw[HW] = {0};
-        hipIpcMemHandle_t h;
-        const hipError_t he = hipIpcGetMemHandle(&h, rd.data.p);
+        const hipError_t he = rd.ipc_valid ? hipSuccess : hipIpcGetMemHandle(&rd.ipc, rd.data.p);
+        if (he == hipSuccess && !rd.ipc_valid) rd.ipc_gen = ++e->p2p_gen;
+        rd.ipc_valid = he == hipSuccess;
         if (he != hipSuccess) {
             local_rc = SGX_ERR_HIP;
             hipPointerAttribute_t pa{};
@@ -216,7 +222,8 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
                           rd.data.p, rd.data.cap, hipGetErrorString(he), hipGetErrorString(ae), (int)pa.type, pa.device);
             local_msg = buf;
         } else {
-            std::memcpy(hw, &h, sizeof(h));
+            std::memcpy(hw, &rd.ipc, sizeof(rd.ipc));
+            hw[HW - 1] = (int64_t)rd.ipc_gen;
         }
         SGX_TRY(agree(local_rc, local_msg, hw, HW, &all_h));
     }
@@ -234,20 +241,29 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
             for (int32_t r = bounds[(size_t)d]; r < bounds[(size_t)d + 1]; ++r) to[(size_t)d] += lm.lens[(size_t)r];
     // (c) the destinations: mine directly, the peers' through their handles
     std::vector<void *> peer((size_t)P, nullptr);
+    std::vector<sgx_engine::PeerMap *> used;
     peer[(size_t)me] = rd.data.p;
-    sgx_engine::PeerMaps mapped;
     for (int32_t d = 0; d < P && local_rc == SGX_OK; ++d) {
         if (d == me || to[(size_t)d] == 0) continue;
         hipIpcMemHandle_t h;
-        std::memcpy(&h, &all_h[(size_t)d * (HW + 1) + 1], sizeof(h));
-        const hipError_t he = hipIpcOpenMemHandle(&peer[(size_t)d], h, hipIpcMemLazyEnablePeerAccess);
-        if (he != hipSuccess) {
-            peer[(size_t)d] = nullptr;
-            local_rc = SGX_ERR_HIP;
-            local_msg = std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(he);
-        } else {
-            mapped.ptrs.push_back(peer[(size_t)d]);
+        const int64_t *w = &all_h[(size_t)d * (HW + 1) + 1];
+        std::memcpy(&h, w, sizeof(h));
+        const int64_t tag[2] = {d, w[HW - 1]};
+        const std::string key = std::string((const char *)tag, sizeof(tag)) + std::string((const char *)&h, sizeof(h));
+        auto it = e->p2p_cache.find(key);
+        if (it == e->p2p_cache.end()) {
+            void *q = nullptr;
+            const hipError_t he = hipIpcOpenMemHandle(&q, h, hipIpcMemLazyEnablePeerAccess);
+            if (he != hipSuccess) {
+                local_rc = SGX_ERR_HIP;
+                local_msg = std::string("hipIpcOpenMemHandle: ") + hipGetErrorString(he);
+                break;
+            }
+            it = e->p2p_cache.emplace(key, sgx_engine::PeerMap{q, 0, nullptr}).first;
         }
+        it->second.last_round = e->p2p_rounds;
+        peer[(size_t)d] = it->second.ptr;
+        used.push_back(&it->second);
     }
     // (d) the gathers: padded maps by fragment table (one descriptor per block), contiguous
     //     maps by byte ranges (64 KiB items)
@@ -291,16 +307,17 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
             }
         }
     }
-    auto unmap_now = [&]() {
-        for (void *q : mapped.ptrs) (void)hipIpcCloseMemHandle(q);
-        mapped.ptrs.clear();
+    // the mappings this round writes through stay open until its gather has finished
+    auto mark_used = [&]() -> int {
+        for (sgx_engine::PeerMap *pm : used) {
+            if (!pm->done) HIP_TRY(hipEventCreateWithFlags(&pm->done, hipEventDisableTiming));
+            HIP_TRY(hipEventRecord(pm->done, st));
+        }
+        return SGX_OK;
     };
     if (P > 1) {  // every rank has mapped the buffers it writes to (or the round fails everywhere)
         const int arc = agree(local_rc, local_msg, nullptr, 0, nullptr);
-        if (arc != SGX_OK) {
-            unmap_now();
-            return arc;
-        }
+        if (arc != SGX_OK) return arc;
     }
     auto launch = [&]() -> int {
         for (auto &lm : mine) HIP_TRY(hipStreamWaitEvent(st, lm.m->done.ev, 0));
@@ -314,8 +331,10 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
         HIP_TRY(hipMemcpyAsync(e->x_items_dev.p, e->x_items.p, fb + ib, hipMemcpyHostToDevice, st));
         HIP_TRY(e->x_items_up.record(st));
         if (!frag.empty())
+            // a few workgroups per CU, each looping over blocks: the next map's sample and K4
+            // share the CUs with the gather instead of queueing behind ~R x G workgroups
             HIP_TRY(launch_gather_frags((const int64_t *)e->x_items_dev.p, (int64_t)(frag.size() / FRAG_DESC_WORDS),
-                                        Gmax, st));
+                                        Gmax, st, std::max(1, 4 * e->num_cus / std::max(1, Gmax))));
         if (!items.empty())
             HIP_TRY(launch_gather_items((const int64_t *)((char *)e->x_items_dev.p + fb), (int64_t)(items.size() / 3),
                                         al16 ? 16 : al4 ? 4 : 1, st));
@@ -331,23 +350,16 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
                                               e->comm, st);
         if (nr != ncclSuccess && rc == SGX_OK)
             rc = fail_msg(SGX_ERR_COMM, "ncclAllReduce (peer gather barrier) failed: %s", ncclGetErrorString(nr));
-        hipEvent_t ev = nullptr;
-        if (hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess && hipEventRecord(ev, st) == hipSuccess) {
-            mapped.done = ev;
-            e->p2p_mapped.push_back(std::move(mapped));
-        } else {
-            if (ev) (void)hipEventDestroy(ev);
-            (void)hipStreamSynchronize(st);
-            unmap_now();
-        }
+        const int mrc = mark_used();
         if (rc != SGX_OK) return rc;
+        SGX_TRY(mrc);
     } else if (P > 1) {
         // host collectives: the gather has finished on every rank once the barrier returns
         if (rc == SGX_OK) rc = comm_wait(e);
         const std::string msg = rc == SGX_OK ? std::string() : std::string(sgx_last_error());
         const int brc = agree(rc, msg, nullptr, 0, nullptr);
-        unmap_now();
         if (brc != SGX_OK) return brc;
+        SGX_TRY(mark_used());
     } else if (rc != SGX_OK) {
         return rc;
     }
@@ -518,6 +530,9 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
                 if (it->use_count() == 1 && (*it)->alias.empty()) {
                     HIP_TRY((*it)->done.wait_host());
                     rd->data.swap((*it)->data);
+                    std::swap(rd->ipc, (*it)->ipc);
+                    std::swap(rd->ipc_valid, (*it)->ipc_valid);
+                    std::swap(rd->ipc_gen, (*it)->ipc_gen);
                 }
                 s->rounds.erase(it);
                 break;
@@ -547,9 +562,11 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
         }
         HIP_TRY(hipEventRecord(a2, st));
     } else if (p2p) {
-        // a fresh receive buffer: peers write into it through its IPC handle
-        rd->data.release();
+        // peers write into the receive buffer through its IPC handle (a new allocation gets a
+        // new handle)
+        const void *was = rd->data.p;
         SGX_TRY(rd->data.ensure((size_t)std::max<int64_t>(total_recv, 16)));
+        if (rd->data.p != was) rd->ipc_valid = false;
         HIP_TRY(hipEventRecord(a2, st));
         SGX_TRY(p2p_data(e, *s, *rd, mine, bounds, lens, srcs, st));
     } else {

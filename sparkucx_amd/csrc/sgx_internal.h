@@ -191,7 +191,8 @@ int64_t pad_capacity_bound(int64_t n, int R, int64_t chunk, int G, int64_t sampl
 // dst + rb * (foff[p*G+g] - foff[p*G]).  desc[b] = {src, fstart, foff, cnt, dst, p, G_b, rb};
 // G = the largest G_b.
 constexpr int FRAG_DESC_WORDS = 8;
-hipError_t launch_gather_frags(const int64_t *desc, int64_t nblocks, int G, hipStream_t stream);
+hipError_t launch_gather_frags(const int64_t *desc, int64_t nblocks, int G, hipStream_t stream,
+                               int max_rows = 65535);  // max_rows: workgroups per fragment column
 // Two-level split scatter (hash partitioner, power-of-two R > 1024, 16 B records):
 // desc: the level-2 pieces cut from the level-1 offsets (offs1[S][G], u32) -- each piece a
 // run of whole (super, chunk) blocks inside one super-partition, about `target` records --

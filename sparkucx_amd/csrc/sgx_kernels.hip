@@ -3892,9 +3892,10 @@ __global__ __launch_bounds__(FRAG_THREADS) void k_gather_frags(const int64_t *__
     }
 }
 
-hipError_t launch_gather_frags(const int64_t *desc, int64_t nblocks, int G, hipStream_t stream) {
+hipError_t launch_gather_frags(const int64_t *desc, int64_t nblocks, int G, hipStream_t stream, int max_rows) {
     if (nblocks <= 0 || G <= 0) return hipSuccess;
-    const dim3 grid((unsigned)G, (unsigned)(nblocks < 65535 ? nblocks : 65535));
+    const int64_t rows = max_rows < 1 ? 1 : max_rows > 65535 ? 65535 : max_rows;
+    const dim3 grid((unsigned)G, (unsigned)(nblocks < rows ? nblocks : rows));
     hipLaunchKernelGGL(k_gather_frags, grid, dim3(FRAG_THREADS), 0, stream, desc, nblocks);
     return hipGetLastError();
 }
