@@ -82,6 +82,9 @@ def parse():
                          "(GpuShuffleWriter: sgx_map_begin, this many sgx_map_append batches -- 2^22 records "
                          "each at C1 with 64 -- as retained device slices of the resident input, "
                          "sgx_map_commit) instead of one sgx_write_map")
+    ap.add_argument("--host-batches", action="store_true",
+                    help="with --batches: the batches come from pageable host memory (a copy of the input), as "
+                         "the JVM writer hands them (SGX_MEM_HOST, staged through the engine's pinned buffers)")
     ap.add_argument("--no-p2p", action="store_true",
                     help="N > 1 / --self-exchange: move the exchange's bytes by RCCL send / recv (or the host "
                          "all-to-all) over contiguous map outputs, with two-pass map writes, instead of the "
@@ -370,6 +373,11 @@ def main():
 
     nbatch = max(1, args.batches)
     cuts = [n * j // nbatch for j in range(nbatch + 1)]
+    host = None
+    if args.host_batches:
+        if nbatch == 1:
+            raise SystemExit("--host-batches needs --batches > 1")
+        host = buf.to_numpy(n * rb)  # pageable host copy of the input (not timed)
 
     def step(k):
         mid = (k % slots) * world + rank  # alternating map slots per rank (one per task)
@@ -380,7 +388,10 @@ def main():
             # until the commit), commit -- one pass over every batch at the commit
             eng.map_begin(sid, mid)
             for j in range(nbatch):
-                eng.map_append(sid, mid, buf, cuts[j + 1] - cuts[j], rb, offset=cuts[j] * rb, retained=True)
+                if host is not None:
+                    eng.map_append(sid, mid, host[cuts[j] * rb:cuts[j + 1] * rb], cuts[j + 1] - cuts[j], rb)
+                else:
+                    eng.map_append(sid, mid, buf, cuts[j + 1] - cuts[j], rb, offset=cuts[j] * rb, retained=True)
             eng.map_commit(sid, mid)
         if args.compress:
             # the map task commits: its partition lengths, i.e. the LZ4 framing of its Kryo
@@ -493,7 +504,7 @@ def main():
             # interval spans the next map's kernels): the write is the sample and K4
             side_ms = (st.ms["hist"] + st.ms["scatter"]) / max(1, st.count["scatter"])
             side_src = "stage events (sample, K4; the tail's K3 overlaps the next write)"
-        if world == 1 and not self_x and tasks == 1 and not args.compress and args.serializer == "fixed":
+        if world == 1 and not self_x and tasks == 1 and not args.compress and args.serializer == "fixed" and host is None:
             # a step is exactly one map write: its wall time is the map side as a map task sees
             # it, host calls included -- the padded write's tail (K3 + the guarded fallback) runs
             # on a second stream behind K4 and overlaps the next write, so its stage interval
@@ -509,8 +520,9 @@ def main():
                      f"{len(bounds)} bounds sampled from rank 0's batch"),
             "config": {"workload": _workload_name(args, n, R, world, self_x), "map_tasks": tasks,
                        "writer": "sgx_write_map (one batch)" if nbatch == 1 else (
-                           f"sgx_map_begin + {nbatch} x sgx_map_append (~{n // nbatch} records each, retained "
-                           f"device batches) + sgx_map_commit"),
+                           f"sgx_map_begin + {nbatch} x sgx_map_append (~{n // nbatch} records each, " +
+                           ("pageable host batches" if host is not None else "retained device batches") +
+                           ") + sgx_map_commit"),
                        "map_tasks_note": None if tasks == 1 else (
                            "concurrent map tasks: stage event times include the other tasks' kernels, "
                            "so the roofline fields are not per-kernel figures (DESIGN.md §9)"),
@@ -546,6 +558,12 @@ def main():
             out["xgmi_roofline"] = xgmi
         if xbytes is not None:
             out["exchange_bytes"] = xbytes
+        if host is not None:
+            # the whole step is the writer's ingest: host batches -> pinned -> HBM, then the
+            # commit's one pass; the map side alone is in roofline_map_side's stage figures
+            out["host_ingest"] = {"GBs": round(rb * n / (ms_per_step * 1e-3) / 1e9, 2), "bytes_per_step": rb * n,
+                                  "note": "pageable host batches through two pinned staging buffers (64 MiB pieces), "
+                                          "H2D overlapping the next batch's staging copy"}
         if args.serializer == "kryo":
             ser_ms = st.ms["serialize"] / max(1, st.count["serialize"])
             kbytes = float(lens.sum())

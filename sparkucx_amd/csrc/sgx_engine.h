@@ -151,8 +151,9 @@ struct Spill {
                                    // (deferred: the batch's records as appended, engine copy)
     std::vector<int64_t> lengths;  // [R] published bytes per partition
     int64_t nrec = 0;
-    const void *src = nullptr;     // deferred: the batch's records (data.p, or the caller's
-                                   // SGX_MEM_DEVICE_RETAINED buffer)
+    const void *src = nullptr;     // deferred: the batch's records (in the map's landing
+                                   // area, or the caller's SGX_MEM_DEVICE_RETAINED buffer)
+    bool landed = false;           // deferred: copied into the map's landing area
 };
 
 struct MapOut {
@@ -184,6 +185,11 @@ struct MapOut {
     bool deferred = false;
     HostPinned chunk_host;     // [2G] i64 {byte offset from the first batch, records} | [S] i32 first chunk per batch
     DevBuf chunk_dev;
+    // deferred: the landing area of copied batches, packed back to back in append order into
+    // large segments, so a run of batches is one region of the commit's chunk table (the
+    // chunk count stays ~one per CU whatever the number of batches)
+    std::vector<std::unique_ptr<DevBuf>> landing;
+    size_t land_used = 0;      // bytes used in landing.back()
     // Single-pass padded output (sgx_map.cpp padded_pass): `data` holds one
     // line-aligned sub-bin per (partition, chunk) stream with unwritten gaps between them;
     // frag = device [fstart][foff][cnt] u32 x R*G: a stream's first record in `data`, its
@@ -291,6 +297,11 @@ struct Ctx {
     DevBuf offs, work;
     DevBuf split_work, split_tmp;  // R > 1024: the two-level split scatter's scratch and level-1 output
     DevBuf input_stage;
+    // host batches of a streaming map: two pinned staging buffers, each reused once its last
+    // copy to HBM has run (the caller's buffer is free as soon as it is copied into one)
+    HostPinned host_stage[2];
+    Event host_up[2];
+    int host_slot = 0;
     // pre-aggregation records of the last read on this thread (sgx_last_read_records)
     int64_t last_read_records = 0;
     const uint32_t *last_off_dev = nullptr;  // device (R+1) record offsets of the last partition pass

@@ -748,7 +748,11 @@ int sgx::finish_lengths(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
     if (m.ready) return SGX_OK;
     if (!m.written) return fail_msg(SGX_ERR_STATE, "map output was not committed");
     HIP_TRY(m.done.wait_host());
-    if (m.deferred) m.spills.clear();  // the commit's pass has read the batches
+    if (m.deferred) {  // the commit's pass has read the batches
+        m.spills.clear();
+        m.landing.clear();
+        m.land_used = 0;
+    }
     const uint32_t *po = (const uint32_t *)m.part_off.p;
     if (m.pad_try) {
         // the padded write's own flag word: an overflow means the guarded two-pass fallback
@@ -915,6 +919,10 @@ static bool deferred_ok(sgx_engine *e, const Shuffle &s) {
     return false;
 }
 
+// the deferred commit's landing segments, and the pinned staging pieces of host batches
+constexpr size_t LANDING_SEGMENT_BYTES = 512ull << 20;
+constexpr int64_t HOST_STAGE_BYTES = 64ll << 20;
+
 // the K4 tile the deferred commit cuts its chunks on (partition_pass / pad_geom pick the same
 // geometry for these shuffles)
 static int deferred_tile(const Shuffle &s) {
@@ -952,15 +960,43 @@ static int commit_deferred(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, int64_t
     ct.chunk = chunk;
     std::vector<int64_t> tab;
     std::vector<int32_t> g0((size_t)S, 0);
+    // regions: a batch, or a run of landed batches back to back in one landing segment (one
+    // region, chunked as if one batch) -- except for per-(partition, spill) framing, which
+    // needs every batch's first chunk
+    struct Region {
+        const char *src;
+        int64_t nrec;
+    };
+    std::vector<Region> regions;
     for (int32_t b = 0; b < S; ++b) {
         const Spill &sp = *m.spills[(size_t)b];
+        if (sp.nrec == 0) continue;
+        const char *src = (const char *)sp.src;
+        if (m.seg_spills == 1 && sp.landed && b > 0 && m.spills[(size_t)b - 1]->landed && !regions.empty() &&
+            regions.back().src + regions.back().nrec * rb == src) {
+            regions.back().nrec += sp.nrec;
+            continue;
+        }
+        regions.push_back(Region{src, sp.nrec});
+    }
+    for (int32_t b = 0, r = 0; b < S; ++b) {  // first chunk of every batch (per-batch regions)
         g0[(size_t)b] = (int32_t)ct.len.size();
-        for (int64_t j = 0; j < sp.nrec; j += chunk) {
-            tab.push_back((int64_t)((const char *)sp.src - (const char *)base) + j * rb);
-            tab.push_back(std::min<int64_t>(chunk, sp.nrec - j));
-            ct.len.push_back(tab.back());
+        if (m.seg_spills > 1 && m.spills[(size_t)b]->nrec > 0) {
+            const Region &rg = regions[(size_t)r++];
+            for (int64_t j = 0; j < rg.nrec; j += chunk) {
+                tab.push_back((int64_t)(rg.src - (const char *)base) + j * rb);
+                tab.push_back(std::min<int64_t>(chunk, rg.nrec - j));
+                ct.len.push_back(tab.back());
+            }
         }
     }
+    if (m.seg_spills == 1)
+        for (const Region &rg : regions)
+            for (int64_t j = 0; j < rg.nrec; j += chunk) {
+                tab.push_back((int64_t)(rg.src - (const char *)base) + j * rb);
+                tab.push_back(std::min<int64_t>(chunk, rg.nrec - j));
+                ct.len.push_back(tab.back());
+            }
     ct.G = (int)ct.len.size();
     const size_t tb = tab.size() * 8, bytes = tb + (size_t)S * 4;
     SGX_TRY(m.chunk_host.ensure(bytes));
@@ -995,6 +1031,8 @@ extern "C" int sgx_map_begin(sgx_engine *e, int32_t shuffle_id, int64_t map_id) 
     m->deferred = false;
     m->seg_spills = 1;
     m->spills.clear();
+    m->landing.clear();
+    m->land_used = 0;
     return SGX_OK;
 }
 
@@ -1021,11 +1059,34 @@ extern "C" int sgx_map_append(sgx_engine *e, int32_t shuffle_id, int64_t map_id,
         if (mem_kind == SGX_MEM_DEVICE_RETAINED && ((uintptr_t)records & 15) == 0) {
             sp->src = records;  // read in place at the commit
         } else if (bytes > 0) {
-            SGX_TRY(sp->data.ensure((size_t)bytes));
-            HIP_TRY(hipMemcpyAsync(sp->data.p, records, (size_t)bytes,
-                                   mem_kind == SGX_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice, c->st));
-            HIP_TRY(hipStreamSynchronize(c->st));  // the caller's buffer is free again on return
-            sp->src = sp->data.p;
+            // into the landing area, right behind the last landed batch (16 B-aligned starts)
+            if (m->landing.empty() || m->landing.back()->cap < m->land_used + (size_t)bytes) {
+                std::unique_ptr<DevBuf> seg(new DevBuf());
+                SGX_TRY(seg->ensure(std::max<size_t>((size_t)bytes, LANDING_SEGMENT_BYTES)));
+                m->landing.push_back(std::move(seg));
+                m->land_used = 0;
+            }
+            char *dst = (char *)m->landing.back()->p + m->land_used;
+            m->land_used += ((size_t)bytes + 15) & ~(size_t)15;
+            if (mem_kind == SGX_MEM_HOST) {
+                // through the two pinned buffers: the copy to HBM runs while the caller fills
+                // its next batch (the caller's buffer is free once it is in pinned memory)
+                for (int64_t off = 0; off < bytes; off += HOST_STAGE_BYTES) {
+                    const size_t piece = (size_t)std::min<int64_t>(HOST_STAGE_BYTES, bytes - off);
+                    const int slot = c->host_slot;
+                    c->host_slot ^= 1;
+                    HIP_TRY(c->host_up[slot].wait_host());
+                    SGX_TRY(c->host_stage[slot].ensure(piece));
+                    std::memcpy(c->host_stage[slot].p, (const char *)records + off, piece);
+                    HIP_TRY(hipMemcpyAsync(dst + off, c->host_stage[slot].p, piece, hipMemcpyHostToDevice, c->st));
+                    HIP_TRY(c->host_up[slot].record(c->st));
+                }
+            } else {
+                HIP_TRY(hipMemcpyAsync(dst, records, (size_t)bytes, hipMemcpyDeviceToDevice, c->st));
+                HIP_TRY(hipStreamSynchronize(c->st));  // the caller's device buffer is free again on return
+            }
+            sp->src = dst;
+            sp->landed = true;
         }
         m->spills.push_back(std::move(sp));
         return SGX_OK;

@@ -107,6 +107,27 @@ def test_commit_padded_any_size_and_many_batches(sgx_lib, oracle_lib, R, n, k):
         check_map(e, oracle_lib, recs, R, sid, 0, sgx_lib.LAYOUT_PADDED)
 
 
+def test_host_batches_land_packed(sgx_lib, engine, oracle_lib):
+    """The writer Spark drives: pageable host batches, staged through the engine's two pinned
+    buffers (a batch above one 64 MiB piece goes in several) and landed back to back, so 400
+    batches still commit as one pass over ~one chunk per CU.  Bytes as one write's."""
+    R = 1024
+    sizes = [5_000_000] + [3_000] * 400 + [1, 0, 777_777]
+    n = sum(sizes)
+    recs = oracle_lib.gen_uniform16(n, 0x5A)
+    sid = next_sid()
+    engine.register_shuffle(sid, R)
+    try:
+        dev = append_batches(engine, sid, 0, recs, sizes, ("host",))
+        dev.free()
+        lengths = engine.map_commit(sid, 0, R)
+        check_map(engine, oracle_lib, recs, R, sid, 0, sgx_lib.LAYOUT_PADDED)
+        engine.write_map(sid, 1, recs, n, 16, R)
+        assert np.array_equal(lengths, engine.map_lengths(sid, 1, R))
+    finally:
+        engine.unregister_shuffle(sid)
+
+
 @pytest.mark.parametrize("shape", ["sorted_by_chunk", "one_partition_late"])
 def test_commit_overflow_falls_back_bit_exact(sgx_lib, engine, oracle_lib, shape):
     """Keys the per-chunk sample cannot see coming: the guarded two-pass kernels rewrite the map
