@@ -2051,7 +2051,9 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 #define SGX_WWC_NOSTORE 0
 #endif
 constexpr int WWC_TR = 512;
-constexpr int WWC_UMAX = (WWC_TR * 100 + 1024 * 60) / 64 + 1;  // units per tile (R <= 1024)
+// whole units per tile: a stream with k new records closes <= (63 + 100 k) / 64 units, and at
+// most WWC_TR streams have records in a tile
+constexpr int WWC_UMAX = (WWC_TR * 100 + WWC_TR * 63) / 64 + 1;
 
 // range bounds packed 12 B each in LDS: {hi lo32, hi hi32, lo}
 struct Bounds12 {
@@ -2068,7 +2070,7 @@ struct Bounds12 {
 __host__ __device__ size_t scatter_wide_wc_lds(uint32_t R, int nb) {
     return al16((size_t)WWC_TR * 100) + al16((size_t)nb * 12) + RDIR_BYTES + (size_t)rs8(R) * 64 +
            (size_t)8 * rs8(R) * 2 + al16((size_t)WWC_UMAX * 4) + (size_t)rs8(R) * 4 + al16((size_t)WWC_TR * 2) +
-           64 * 4;
+           al16((size_t)(WWC_TR + 1) * 4) + 64 * 4;
 }
 
 template <int KIND, int MODE>
@@ -2117,6 +2119,11 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
     sp += (size_t)RS * 4;
     uint16_t *idx = (uint16_t *)sp;
     sp += al16((size_t)TR * 2);
+    // the tile's active streams (those with records), in stream order: p | first slot << 10 |
+    // first unit << 20, then a sentinel {records, units} -- the per-stream work of the tile runs
+    // one active stream per thread instead of two streams of every pair per thread
+    uint32_t *act = (uint32_t *)sp;
+    sp += al16((size_t)(TR + 1) * 4);
     uint32_t *scratch = (uint32_t *)sp;
     uint16_t *myrow = rows + (size_t)w * RS;
     uint32_t *myrow32 = (uint32_t *)myrow;
@@ -2163,22 +2170,18 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
     uint64_t st_acc[14] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     uint64_t st_last = wc_stamp();
 #endif
-    // the owner thread's streams 2 tid, 2 tid + 1: their next cursor and carry, taken from the
-    // tile's last record of the stream during the drain, stored at the next tile's start
-    // (after the barrier that ends every drain's reads of the old ones)
-    uint32_t ncur[2] = {0, 0}, ncnt[2] = {0, 0}, creg[2][15];
-    bool upd[2] = {false, false};
+    // the thread's active stream of the last tile (act[tid]): its next cursor and carry, taken
+    // from the tile's last record of the stream after the drain, stored at the next tile's
+    // start (after the barrier that ends every drain's reads of the old ones)
+    uint32_t ap = 0, ak = 0, acc = 0, asb = 0, ncur = 0, ncnt = 0, creg[15];
+    bool upd = false;
     auto writeback = [&]() __attribute__((always_inline)) {
+        if (!upd) return;
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (!upd[h]) continue;
-            const uint32_t p = 2 * tid + h;
-#pragma unroll
-            for (int i = 0; i < 15; ++i)
-                if ((uint32_t)i < ncnt[h]) carry[cx(p, i)] = creg[h][i];
-            cur[p] = ncur[h];
-            upd[h] = false;
-        }
+        for (int i = 0; i < 15; ++i)
+            if ((uint32_t)i < ncnt) carry[cx(ap, i)] = creg[i];
+        cur[ap] = ncur;
+        upd = false;
     };
     auto tile = [&](const int t, u32x4(&ld)[LD], u32x4(&ldn)[LD]) __attribute__((always_inline)) {
         const int nrec = t + 1 < ntiles ? TR : lastn;
@@ -2220,7 +2223,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
         lds_barrier();
         WC_STAMP(4);  // partition ids + ranking atomics + barrier
         // ---- merge: per partition pair j = tid, prefix over the wave rows; block scan of
-        //      {records, whole units} packed 16 | 16
+        //      {records, whole units, active streams} packed 10 | 11 | 11 (<= 512, 1304, 512)
         const uint32_t j = tid;
         uint32_t before[W], tot = 0, val = 0, k[2] = {0, 0}, nu[2] = {0, 0}, cc[2] = {0, 0};
         if (j < NP) {
@@ -2233,10 +2236,10 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             k[1] = tot >> 16;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                cc[h] = cur[2 * j + h];  // the owner's cursors (cur[] is the drain's view below)
+                cc[h] = cur[2 * j + h];  // the cursors (cur[] becomes the drain's view below)
                 nu[h] = ((uint32_t)(((uint64_t)cc[h] * RB) & 63u) + RB * k[h]) >> 6;
             }
-            val = (k[0] + k[1]) | ((nu[0] + nu[1]) << 16);
+            val = (k[0] + k[1]) | ((nu[0] + nu[1]) << 10) | (((k[0] ? 1u : 0u) + (k[1] ? 1u : 0u)) << 21);
         }
         WC_STAMP(5);  // merge: rank rows read
         const uint32_t xs = wave_inclusive_scan(val, lane);
@@ -2251,49 +2254,61 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             total += y;
         }
         WC_STAMP(11);  // merge: wave totals read
-        const uint32_t sb[2] = {base & 0xFFFFu, (base & 0xFFFFu) + k[0]};
-        const uint32_t ubs[2] = {base >> 16, (base >> 16) + nu[0]};
+        const uint32_t sb[2] = {base & 1023u, (base & 1023u) + k[0]};
+        const uint32_t ubs[2] = {(base >> 10) & 2047u, ((base >> 10) & 2047u) + nu[0]};
         if (j < NP) {
             const uint32_t L = sb[0] | (sb[1] << 16);
 #pragma unroll
             for (int v = 0; v < W; ++v) ((uint32_t *)(rows + (size_t)v * RS))[j] = before[v] + L;
-            // unit i of stream p starts at dword 16 i - cbD of the stream's new records: below 0
-            // (unit 0 only) its first cneg dwords are the carry's, else record slot sb + r, dword
-            // w.  desc = p | slot << 10 | w << 19 | cneg << 24 | slow << 28, slow: the unit holds
-            // dwords before the stream's first record or past the output's end.  cur[p] becomes
-            // the drain's view cur - sb (the unit's output dword = 25 (view + slot) + w - cneg);
-            // the owner's writeback restores it (a stream without records keeps its cursor)
+            // the pair's active streams into the list; cur[p] becomes the drain's view cur - sb
+            // (the unit's output dword = 25 (view + slot) + w - cneg); the next writeback
+            // restores it (a stream without records keeps its cursor)
+            uint32_t a = base >> 21;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 if (k[h] == 0) continue;
-                const uint32_t p = 2 * j + h;
-                const uint64_t cD = (uint64_t)cc[h] * DW, u0D = cD & ~(uint64_t)15;
-                const uint64_t startD = (uint64_t)carry[cx(p, 15)] * DW, capD = (uint64_t)olim * DW;
-                const uint64_t room = capD > u0D ? (capD - u0D) >> 4 : 0;  // whole units before the end
-                const uint32_t ncap = room > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)room;
-                const uint32_t cb = (uint32_t)(cD - u0D), w0 = p | (sb[h] << 10);
-                // unit 0: its first cb dwords are the carry's; units 1.. start in the records
-                desc[ubs[h]] = w0 | (cb << 24) | ((u0D < startD || ncap == 0 ? 1u : 0u) << 28);
-                uint32_t r = 0, wv = 16u - cb;
-                for (uint32_t i = 1; i < nu[h]; ++i) {
-                    desc[ubs[h] + i] = (w0 + (r << 10)) | (wv << 19) | ((i >= ncap ? 1u : 0u) << 28);
-                    wv += 16u;
-                    if (wv >= (uint32_t)DW) wv -= DW, ++r;
-                }
-                cur[p] = cc[h] - sb[h];
+                act[a++] = (2 * j + h) | (sb[h] << 10) | (ubs[h] << 20);
+                cur[2 * j + h] = cc[h] - sb[h];
             }
         }
-        WC_STAMP(12);  // merge: rows + unit words written
+        if (tid == 0) act[total >> 21] = ((total & 1023u) << 10) | (((total >> 10) & 2047u) << 20);  // sentinel
+        WC_STAMP(12);  // merge: rows + active list written
         lds_barrier();
         WC_STAMP(13);  // merge: barrier
-        // ---- partition-sorted index of the tile
+        // ---- partition-sorted index of the tile; the unit words, one active stream per thread:
+        //      unit i of stream p starts at dword 16 i - cbD of the stream's new records: below 0
+        //      (unit 0 only) its first cneg dwords are the carry's, else record slot sb + r, dword
+        //      w.  desc = p | slot << 10 | w << 19 | cneg << 24 | slow << 28, slow: the unit holds
+        //      dwords before the stream's first record or past the output's end
         if (valid) idx[myrow[pid] + ((old >> ((pid & 1u) << 4)) & 0xFFFFu)] = (uint16_t)tid;
+        const uint32_t nact = total >> 21;
+        if (tid < nact) {
+            const uint32_t e0 = act[tid], e1 = act[tid + 1];
+            ap = e0 & 1023u;
+            asb = (e0 >> 10) & 1023u;
+            ak = ((e1 >> 10) & 1023u) - asb;
+            const uint32_t ub = e0 >> 20, nun = (e1 >> 20) - ub;
+            acc = cur[ap] + asb;  // the cursor (cur[] holds the drain's view)
+            const uint64_t cD = (uint64_t)acc * DW, u0D = cD & ~(uint64_t)15;
+            const uint64_t startD = (uint64_t)carry[cx(ap, 15)] * DW, capD = (uint64_t)olim * DW;
+            const uint64_t room = capD > u0D ? (capD - u0D) >> 4 : 0;  // whole units before the end
+            const uint32_t ncap = room > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)room;
+            const uint32_t cb = (uint32_t)(cD - u0D), w0 = ap | (asb << 10);
+            // unit 0: its first cb dwords are the carry's; units 1.. start in the records
+            desc[ub] = w0 | (cb << 24) | ((u0D < startD || ncap == 0 ? 1u : 0u) << 28);
+            uint32_t r = 0, wv = 16u - cb;
+            for (uint32_t i = 1; i < nun; ++i) {
+                desc[ub + i] = (w0 + (r << 10)) | (wv << 19) | ((i >= ncap ? 1u : 0u) << 28);
+                wv += 16u;
+                if (wv >= (uint32_t)DW) wv -= DW, ++r;
+            }
+        }
         lds_barrier();
-        WC_STAMP(6);  // sorted index + barrier
+        WC_STAMP(6);  // sorted index + unit words + barrier
         // ---- drain: whole 64 B units, 16 B per lane, 4 lanes per unit.  Unit byte x of
         //      stream p: its carry below cb (the open unit's bytes), else byte x - cb of the
         //      stream's records in sorted order
-        const uint32_t npieces = (total >> 16) * 4u;
+        const uint32_t npieces = ((total >> 10) & 2047u) * 4u;
         // two pieces per step, each phase issued for both before its results are used: the
         // unit word; then the two index slots (and carry dwords); then the 4 data dwords
         const uint32_t coff = (uint32_t)(carry - stage);
@@ -2356,23 +2371,20 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             }
         }
         WC_STAMP(7);  // drain
-        // the owner's streams: next cursor, and the new open unit = the tail of the tile's last
-        // record of the stream (a record is longer than a unit, so it always closes the old one)
-        if (j < NP) {
+        // the thread's active stream: next cursor, and the new open unit = the tail of the
+        // tile's last record of the stream (a record is longer than a unit, so it always closes
+        // the old one)
+        if (tid < nact) {
+            const uint64_t cB = (uint64_t)acc * RB, cnB = cB + (uint64_t)RB * ak;
+            const uint64_t u1B = cnB & ~(uint64_t)63;
+            const uint32_t o = (uint32_t)(u1B - cB) - RB * (ak - 1);  // byte of the last record
+            const uint32_t s0 = (uint32_t)idx[asb + ak - 1] * DW + (o >> 2);
+            ncnt = (uint32_t)(cnB - u1B) >> 2;
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                if (k[h] == 0) continue;
-                const uint64_t cB = (uint64_t)cc[h] * RB, cnB = cB + (uint64_t)RB * k[h];
-                const uint64_t u1B = cnB & ~(uint64_t)63;
-                const uint32_t o = (uint32_t)(u1B - cB) - RB * (k[h] - 1);  // byte of the last record
-                const uint32_t s0 = (uint32_t)idx[sb[h] + k[h] - 1] * DW + (o >> 2);
-                ncnt[h] = (uint32_t)(cnB - u1B) >> 2;
-#pragma unroll
-                for (int i = 0; i < 15; ++i) creg[h][i] = stage[min(s0 + i, (uint32_t)(TR * DW - 1))];
-                ncur[h] = cc[h] + k[h];
-                upd[h] = true;
-                bad |= ncur[h] > olim ? 1u : 0u;
-            }
+            for (int i = 0; i < 15; ++i) creg[i] = stage[min(s0 + i, (uint32_t)(TR * DW - 1))];
+            ncur = acc + ak;
+            upd = true;
+            bad |= ncur > olim ? 1u : 0u;
         }
         WC_STAMP(8);  // owners' next carries
         lds_barrier();

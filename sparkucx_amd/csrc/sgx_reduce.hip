@@ -34,7 +34,13 @@ constexpr int RT = 256;  // threads per workgroup
 // Replaces four passes (flags, a scan, emit, and for SUM three prefix-sum kernels plus a
 // gather): one read of the records and the outputs' writes.
 // ------------------------------------------------------------------------------------
-constexpr int GT = 256, GI = 16, GTILE = GT * GI;
+#ifndef SGX_GROUP_GT  // (A/B builds: -DSGX_GROUP_GT / -DSGX_GROUP_GI)
+#define SGX_GROUP_GT 256
+#endif
+#ifndef SGX_GROUP_GI
+#define SGX_GROUP_GI 16
+#endif
+constexpr int GT = SGX_GROUP_GT, GI = SGX_GROUP_GI, GTILE = GT * GI;
 // the group outputs (keys, starts, values: the caller's arrays, read after the call) stored
 // nontemporal (A/B: -DSGX_GROUP_NT=0)
 #ifndef SGX_GROUP_NT
