@@ -172,7 +172,10 @@ hipError_t launch_pad_reset(uint32_t *flags, uint32_t *flags_out, uint32_t *est,
 // cur: R*G u32 of scratch (the streams' cursors).
 hipError_t launch_scatter16_fallback(const void *in, void *out, int64_t n, int64_t chunk, int G, const PartParams &pp,
                                      const uint32_t *foff, uint32_t *cur, const uint32_t *guard, uint32_t *err,
-                                     hipStream_t stream);
+                                     hipStream_t stream, int rb = 16);  // rb 16 (hash) or 100 (TeraSort range)
+// Whether a padded TeraSort map's K4 is the write-combining kernel (the one that lays its
+// sub-bins out itself): R <= 1024, its LDS fits, chunks a multiple of its tile.
+bool wide_wc_padded_ok(uint32_t R, int nb, int64_t chunk);
 // (partition, spill) segment offsets of a streaming map committed in one pass (k_spill_seg_offs).
 hipError_t launch_spill_seg_offs(const uint32_t *offs, const uint32_t *part_off, int R, int G, int S,
                                  const int32_t *g0, uint32_t *out, hipStream_t stream);

@@ -2067,6 +2067,11 @@ struct Bounds12 {
     }
 };
 
+__host__ __device__ size_t scatter_wide_wc_lds(uint32_t R, int nb);
+bool wide_wc_padded_ok(uint32_t R, int nb, int64_t chunk) {
+    return SGX_WIDE_WC && R <= 1024 && scatter_wide_wc_lds(R, nb) <= LDS_MAX && chunk % WWC_TR == 0;
+}
+
 __host__ __device__ size_t scatter_wide_wc_lds(uint32_t R, int nb) {
     return al16((size_t)WWC_TR * 100) + al16((size_t)nb * 12) + RDIR_BYTES + (size_t)rs8(R) * 64 +
            (size_t)8 * rs8(R) * 2 + al16((size_t)WWC_UMAX * 4) + (size_t)rs8(R) * 4 + al16((size_t)WWC_TR * 2) +
@@ -2145,10 +2150,15 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
     const int64_t len = pp.chunks ? pp.chunks[2 * g + 1] : end > begin ? end - begin : 0;
     const int ntiles = (int)((len + TR - 1) / TR);
     const int lastn = ntiles > 0 ? (int)(len - (int64_t)(ntiles - 1) * TR) : 0;
-    for (uint32_t p = tid; p < RS; p += T) {
-        const uint32_t c0 = p < R ? offs[(int64_t)p * G + g] : 0u;
-        cur[p] = c0;
-        carry[cx(p, 15)] = c0;  // the stream's first record: bytes before it are not ours
+    if (MODE == WC_PADDED && pp.pad_est) {  // the sub-bins laid out here (PartParams.pad_est)
+        pad_layout_starts<T>(pp, R, RS, g, G, cur, cur, (uint64_t *)scratch, err);
+        for (uint32_t p = tid; p < RS; p += T) carry[cx(p, 15)] = cur[p];
+    } else {
+        for (uint32_t p = tid; p < RS; p += T) {
+            const uint32_t c0 = p < R ? offs[(int64_t)p * G + g] : 0u;
+            cur[p] = c0;
+            carry[cx(p, 15)] = c0;  // the stream's first record: bytes before it are not ours
+        }
     }
 
     // the next tile's loads in registers, two named buffers taking turns (the tile loop is
@@ -2411,14 +2421,18 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide_wc(const u32x4 *__restr
             if (b + 4 <= capB) *(uint32_t *)((char *)out + b) = carry[cx(p, (uint32_t)((b - u0B) >> 2))];
     }
     if constexpr (MODE == WC_PADDED) {
-        bool ovf = false;
-        for (uint32_t p = tid; p < R; p += T) {
-            const int64_t i = (int64_t)p * G + g;
-            const uint32_t cnt = cur[p] - offs[i];
-            pp.pad_cnt[i] = cnt;
-            ovf |= cnt > pp.pad_cap[p];
+        if (pp.pad_est) {  // the end positions: k_pad_finish makes them counts
+            for (uint32_t p = tid; p < R; p += T) pp.pad_cnt[(int64_t)p * G + g] = cur[p];
+        } else {
+            bool ovf = false;
+            for (uint32_t p = tid; p < R; p += T) {
+                const int64_t i = (int64_t)p * G + g;
+                const uint32_t cnt = cur[p] - offs[i];
+                pp.pad_cnt[i] = cnt;
+                ovf |= cnt > pp.pad_cap[p];
+            }
+            if (ovf) atomicOr(err, PAD_OVERFLOW);
         }
-        if (ovf) atomicOr(err, PAD_OVERFLOW);
     }
     if (bad) atomicOr(err, SCATTER_OOB);
 }
@@ -3401,11 +3415,15 @@ hipError_t launch_scatter(const void *in, void *out, int64_t n, int rb, int64_t 
         // a padded write's K4 and its fallback's (RangePartitioner over 10-byte keys)
         const int mode = pp.pad_cnt ? WC_PADDED : pp.guard ? WC_FALLBACK : 0;
         if (mode) {
-            if (pp.kind != SGX_PART_RANGE_BYTES10 || (mode == WC_PADDED && (!pp.pad_cap || !pp.olim)))
+            if (pp.kind != SGX_PART_RANGE_BYTES10 ||
+                (mode == WC_PADDED && ((!pp.pad_cap && !(pp.pad_est && pp.pad_layout)) || !pp.olim)))
                 return hipErrorInvalidValue;
-            // the padded K4 write-combines whole 64 B units when its LDS fits (R <= 1024)
-            const size_t wlds = scatter_wide_wc_lds(pp.R, pp.nb);
-            if (SGX_WIDE_WC && mode == WC_PADDED && pp.R <= 1024 && wlds <= LDS_MAX && chunk % WWC_TR == 0) {
+            // the padded K4 write-combines whole 64 B units when its LDS fits (R <= 1024); only
+            // that kernel lays its sub-bins out itself
+            const bool wwc = wide_wc_padded_ok(pp.R, pp.nb, chunk);
+            if (mode == WC_PADDED && pp.pad_est && !wwc) return hipErrorInvalidValue;
+            if (mode == WC_PADDED && wwc) {
+                const size_t wlds = scatter_wide_wc_lds(pp.R, pp.nb);
                 (void)hipFuncSetAttribute((const void *)k_scatter_wide_wc<SGX_PART_RANGE_BYTES10, WC_PADDED>,
                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)wlds);
                 hipLaunchKernelGGL((k_scatter_wide_wc<SGX_PART_RANGE_BYTES10, WC_PADDED>), dim3(G), dim3(512), wlds,
@@ -3766,13 +3784,63 @@ __global__ __launch_bounds__(64) void k_scatter16_fb(const uint4 *__restrict__ i
     if (bad) atomicOr(err, ERR_SCATTER_OOB);
 }
 
+// The same for 100 B TeraSort records under their RangePartitioner: a record's lane copies its
+// 25 dwords (the bounds searched in global memory).
+template <int KIND>
+__global__ __launch_bounds__(64) void k_scatter_wide_fb(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
+                                                        int64_t n, int64_t chunk, PartParams pp,
+                                                        const uint32_t *__restrict__ foff, uint32_t *cur, int G,
+                                                        const uint32_t *guard, uint32_t *err) {
+    constexpr int DW = 25;
+    if (!(*guard & PAD_OVERFLOW)) return;
+    const int g = blockIdx.x;
+    const uint32_t lane = threadIdx.x, R = pp.R;
+    for (uint32_t p = lane; p < R; p += 64)
+        __hip_atomic_store(&cur[(int64_t)p * G + g], foff[(int64_t)p * G + g], __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    __threadfence();
+    __syncthreads();
+    const int64_t begin = (int64_t)g * chunk;
+    const uint32_t *cin = in + begin * DW;
+    int64_t len = min(n, begin + chunk) - begin;
+    if (pp.chunks) {
+        cin = (const uint32_t *)((const char *)in + pp.chunks[2 * g]);
+        len = pp.chunks[2 * g + 1];
+    }
+    bool bad = false;
+    for (int64_t i0 = 0; i0 < len; i0 += 64) {
+        const int64_t i = i0 + lane;
+        const bool valid = i < len;
+        const uint32_t *r = cin + (valid ? i : 0) * DW;
+        const uint32_t p = valid ? pid_of<KIND>(r[0], r[1], r[2], pp) : 0u;
+        const uint64_t peers = match_peers(p, __ballot(valid), pp.nbits);
+        const uint32_t leader = peers ? (uint32_t)__ffsll((unsigned long long)peers) - 1 : 0u;
+        uint32_t b = 0;
+        if (valid && lane == leader) b = atomicAdd(&cur[(int64_t)p * G + g], (uint32_t)__popcll(peers));
+        b = __shfl(b, (int)leader, 64);
+        const uint64_t pos = (uint64_t)b + (uint64_t)__popcll(peers & ((1ull << lane) - 1ull));
+        if (valid) {
+            if (pos < (uint64_t)n)
+                for (int d = 0; d < DW; ++d) out[pos * DW + d] = r[d];
+            else
+                bad = true;
+        }
+    }
+    if (bad) atomicOr(err, ERR_SCATTER_OOB);
+}
+
 hipError_t launch_scatter16_fallback(const void *in, void *out, int64_t n, int64_t chunk, int G, const PartParams &pp,
                                      const uint32_t *foff, uint32_t *cur, const uint32_t *guard, uint32_t *err,
-                                     hipStream_t stream) {
+                                     hipStream_t stream, int rb) {
     if (n <= 0 || G <= 0) return hipSuccess;
-    if (pp.kind != SGX_PART_HASH) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_scatter16_fb<SGX_PART_HASH>, dim3(G), dim3(64), 0, stream, (const uint4 *)in, (uint4 *)out, n,
-                       chunk, pp, foff, cur, G, guard, err);
+    if (rb == 16 && pp.kind == SGX_PART_HASH)
+        hipLaunchKernelGGL(k_scatter16_fb<SGX_PART_HASH>, dim3(G), dim3(64), 0, stream, (const uint4 *)in, (uint4 *)out,
+                           n, chunk, pp, foff, cur, G, guard, err);
+    else if (rb == 100 && pp.kind == SGX_PART_RANGE_BYTES10)
+        hipLaunchKernelGGL(k_scatter_wide_fb<SGX_PART_RANGE_BYTES10>, dim3(G), dim3(64), 0, stream,
+                           (const uint32_t *)in, (uint32_t *)out, n, chunk, pp, foff, cur, G, guard, err);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

@@ -509,6 +509,7 @@ static int padded_pass_wide(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const 
 static int padded_pass16(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n, const PadGeom &pg,
                          const ChunkTable *ct) {
     hipStream_t st = c.st;
+    const int rb = s.rb;  // 16, or 100 (TeraSort's write-combining K4: wide_wc_padded_ok)
     const int32_t R = s.R;
     const int G = pg.G;
     const int64_t len = (int64_t)R * G, tiles = scan_tiles(len);
@@ -519,7 +520,7 @@ static int padded_pass16(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const voi
     const int slot = c.pad_slot;
     c.pad_slot ^= 1;
     if (c.pad_free[slot].ev) HIP_TRY(hipStreamWaitEvent(st, c.pad_free[slot].ev, 0));
-    SGX_TRY(m.data.ensure((size_t)olim * 16));
+    SGX_TRY(m.data.ensure((size_t)olim * (size_t)rb));
     SGX_TRY(m.frag.ensure((size_t)len * 12 + 16));
     uint32_t *fstart = (uint32_t *)m.frag.p, *foff = fstart + len, *cnt = foff + len;
     SGX_TRY(c.pad_offs[slot].ensure((size_t)len * 4));
@@ -547,7 +548,7 @@ static int padded_pass16(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const voi
     HIP_TRY(hipEventRecord(h0, st));
     PartParams bp = s.pp;  // the shuffle's partitioner over this map's input (chunk table or not)
     bp.chunks = ct ? ct->dev : nullptr;
-    HIP_TRY(launch_pad_sample(in, n, 16, pg.stride, bp, est, st, pg.chunk, G));
+    HIP_TRY(launch_pad_sample(in, n, rb, pg.stride, bp, est, st, pg.chunk, G));
     SGX_TRY(debug_sync(e, st, "padded sample"));
     HIP_TRY(hipEventRecord(h1, st));
     PartParams kp = bp;
@@ -558,7 +559,7 @@ static int padded_pass16(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const voi
     kp.pad_layout = layout;
     kp.pad_scale = (double)pg.chunk / (double)pg.sampled;
     kp.pad_a = 1.0 + kp.pad_scale;
-    HIP_TRY(launch_scatter(in, m.data.p, n, 16, pg.chunk, G, kp, nullptr, pg.geo, flags, st));
+    HIP_TRY(launch_scatter(in, m.data.p, n, rb, pg.chunk, G, kp, nullptr, pg.geo, flags, st));
     SGX_TRY(debug_sync(e, st, "K4 padded scatter"));
     HIP_TRY(hipEventRecord(c1, st));
     hipStream_t tl = c.st_tail;
@@ -570,7 +571,7 @@ static int padded_pass16(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const voi
     HIP_TRY(c.pad_free[slot].record(tl));
     c.pad_crit_zeroed[slot] = zero_bytes;
     HIP_TRY(launch_scatter16_fallback(in, m.data.p, n, pg.chunk, G, bp, foff, (uint32_t *)c.pad_offs[slot].p,
-                                      flags_copy, err, tl));
+                                      flags_copy, err, tl, rb));
     SGX_TRY(debug_sync(e, tl, "padded tail"));
     HIP_TRY(hipEventRecord(x1, tl));
     HIP_TRY(hipMemcpyAsync(m.part_off.p, part_off_dev, (size_t)(R + 3) * 4, hipMemcpyDeviceToHost, tl));
@@ -587,7 +588,8 @@ static int padded_pass16(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const voi
 
 static int padded_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n, const PadGeom &pg,
                        const ChunkTable *ct = nullptr) {
-    return s.rb == 16 ? padded_pass16(e, c, s, m, in, n, pg, ct) : padded_pass_wide(e, c, s, m, in, n, pg, ct);
+    const bool own_layout = s.rb == 16 || wide_wc_padded_ok((uint32_t)s.R, s.nb, pg.chunk);
+    return own_layout ? padded_pass16(e, c, s, m, in, n, pg, ct) : padded_pass_wide(e, c, s, m, in, n, pg, ct);
 }
 
 int sgx::materialize(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m) {
