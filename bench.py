@@ -558,6 +558,16 @@ def main():
             out["xgmi_roofline"] = xgmi
         if xbytes is not None:
             out["exchange_bytes"] = xbytes
+            # the whole step against HBM: the map side's design bytes plus the exchange reading
+            # every published byte once and writing it once into a reducer's buffer (per GPU,
+            # over the timed step: on one GPU the gather shares HBM with the next map's K4, so
+            # the map side's own stage figure is stretched and this is the step's roofline)
+            bpr = (2 * rb + rb / 128.0) if padded else 3 * rb
+            per_gpu = bpr * n + 2.0 * xbytes["published"] / args.steps / world
+            ach = per_gpu / (ms_per_step * 1e-3) / 1e9
+            out["step_design_hbm"] = {"bytes_per_gpu_step": per_gpu, "achieved": round(ach, 1),
+                                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+                                      "note": "map side design bytes + 2 x published bytes, per GPU, / ms_per_step"}
         if host is not None:
             # the whole step is the writer's ingest: host batches -> pinned -> HBM, then the
             # commit's one pass; the map side alone is in roofline_map_side's stage figures

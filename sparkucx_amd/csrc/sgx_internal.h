@@ -51,7 +51,14 @@ struct PartParams {
     // and number chunks[2g+1] (every chunk inside one batch); null: chunk g = records
     // [g * chunk, min(n, (g + 1) * chunk)) of one contiguous input
     const int64_t *chunks;
+    // ---- the padded split's level 2 (k_scatter16_wc SEG + WC_PADDED): workgroup b = k G + g
+    // reads the level-1 fragments of supers k pack .. k pack + pack - 1 in chunk g -- fragment
+    // (s, g) = frag_cnt[s G + g] records from frag_start[s G + g] -- as one sequence; its R =
+    // 64 pack streams are the partitions k R .. k R + R - 1 (pack <= SPLIT_PACK_MAX)
+    const uint32_t *frag_start, *frag_cnt;
+    uint32_t pack;
 };
+constexpr uint32_t SPLIT_PACK_MAX = 16;
 // Error-word bits shared by the map-side kernels and the engine.
 constexpr uint32_t ERR_SPIN = 1u;          // a look-back spin gave up
 constexpr uint32_t ERR_SCATTER_OOB = 2u;   // a scatter destination was out of range
@@ -236,8 +243,6 @@ hipError_t launch_hot_cursors(const uint32_t *offs, const int32_t *hot_part, con
 // level-1 streams' counts, [HOT + S][G]); the hot partitions' final counts from level 1.
 hipError_t launch_cold_super_est(const uint32_t *est, const uint16_t *stream_of, int S, int Q, uint32_t *est1,
                                  hipStream_t stream);
-hipError_t launch_frag_desc(const uint32_t *fstart1, const uint32_t *cnt1, int S, int G, int64_t *desc,
-                            uint32_t *ndesc, hipStream_t stream);
 hipError_t launch_hot_counts(const uint32_t *cnt1, const int32_t *hot_part, int G, uint32_t *cnt, hipStream_t stream);
 // The sorted read's last step: `in` is ordered by bucket = (P(key) << kbits) | key window
 // bits [kshift, kshift + kbits) (P the shuffle's hash partitioner when use_p, else 0); every

@@ -1349,21 +1349,33 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         if (!(*pp.guard & PAD_OVERFLOW)) return;  // the whole workgroup, before any barrier
     uint32_t bad = 0;
 
-    // FRAGS (level 2 of the padded split): the workgroup walks fragments blockIdx.x, +
-    // gridDim.x, ... -- desc[f] = {begin, end, super, chunk} -- every one with fresh streams
-    // at their sub-bins and the last tile flushing; otherwise one chunk / piece
+    // FRAGS (level 2 of the padded split): workgroup k G + g reads the level-1 fragments (s,
+    // g) of supers s = k pack + f, f < pack, back to back as one sequence -- item i of it is
+    // record i + fdl[f] of the scratch for the last f with fpre[f] <= i -- into the R = 64 pack
+    // streams of partitions k R + p.  (One 64-stream fragment per workgroup pass left each
+    // pass under a third of a tile: 0.71 ms for C3's 2.9 GB.)  Otherwise one chunk / piece.
+    // The fragment table lives in lane f of two registers of every wave (fpre: prefix, or ~0
+    // past the group; fdl: scratch start - prefix): a 4-step search by lane shuffles per item
+    // (16 compares, or the table in scalar registers, spilled)
     constexpr bool FRAGS = SEG && MODE == WC_PADDED;
-    const int64_t nfrag = FRAGS ? (int64_t)*ndesc : 1;
-    for (int64_t frag = FRAGS ? (int64_t)blockIdx.x : 0; frag < nfrag; frag += FRAGS ? (int64_t)gridDim.x : 1) {
-    if (FRAGS && frag != (int64_t)blockIdx.x) __syncthreads();  // the last fragment's drain read the stream state
+    uint32_t fpre = 0xFFFFFFFFu, fdl = 0;
+    {
     int g = blockIdx.x;
     int64_t begin = (int64_t)g * chunk, end = min(n, begin + chunk), obase = 0;
     if constexpr (FRAGS) {
-        const int64_t *d = desc + 4 * frag;
-        begin = d[0];
-        end = d[1];
-        obase = d[2] * (int64_t)R;
-        g = (int)d[3];
+        const int kg = (int)blockIdx.x / G;
+        g = (int)blockIdx.x - kg * G;
+        obase = (int64_t)kg * R;
+        const bool on = lane < pp.pack;
+        const int64_t i1 = ((int64_t)kg * pp.pack + lane) * G + g;
+        const uint32_t b = on ? pp.frag_start[i1] : 0u, c = on ? pp.frag_cnt[i1] : 0u;
+        const uint32_t incl = wave_inclusive_scan(c, lane);
+        if (on) {
+            fpre = incl - c;
+            fdl = b - fpre;
+        }
+        begin = 0;
+        end = (uint32_t)__shfl((int)incl, 63, 64);
     } else if constexpr (SEG) {
         if (blockIdx.x >= *ndesc) return;  // the whole workgroup, before any barrier
         const int64_t *d = desc + 4 * (int64_t)blockIdx.x;
@@ -1396,6 +1408,14 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
         for (uint32_t i = tid; i < (1u << pp.dshift); i += T) tbl[i] = pp.dir[i];
 
     const u32x4 *src = cin + (int64_t)w * NI * 64 + lane;
+    // FRAGS: the scratch record behind item i of the workgroup's sequence
+    auto fidx = [&](uint32_t i) __attribute__((always_inline)) -> uint32_t {
+        uint32_t f = 0;  // the last fragment whose prefix is <= i (fragment 0's is 0)
+#pragma unroll
+        for (uint32_t st = SPLIT_PACK_MAX / 2; st >= 1; st >>= 1)
+            f = i >= (uint32_t)__shfl((int)fpre, (int)(f + st), 64) ? f + st : f;
+        return i + (uint32_t)__shfl((int)fdl, (int)f, 64);
+    };
     u32x4 rec[NI];
     bool valid[NI];
     u32x4 dk[SI];
@@ -1408,7 +1428,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
 #pragma unroll
         for (int k = 0; k < NI; ++k) {
             valid[k] = (int64_t)w * NI * 64 + k * 64 + lane < len;
-            rec[k] = valid[k] ? (SGX_WC_NTLOAD ? __builtin_nontemporal_load(src + k * 64) : src[k * 64]) : u32x4{0, 0, 0, 0};
+            const u32x4 *a = FRAGS ? cin + fidx((uint32_t)(w * NI * 64 + k * 64 + lane)) : src + k * 64;
+            rec[k] = valid[k] ? (SGX_WC_NTLOAD ? __builtin_nontemporal_load(a) : *a) : u32x4{0, 0, 0, 0};
         }
     }
     __syncthreads();
@@ -1607,7 +1628,8 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 const int64_t i = nb + (int64_t)w * NI * 64 + k * 64 + lane;
                 valid[k] = i < len;
                 // branch-free: an invalid item re-reads the chunk head
-                rec[k] = SGX_WC_NTLOAD ? __builtin_nontemporal_load(cb + (valid[k] ? i : 0)) : cb[valid[k] ? i : 0];
+                const int64_t ia = FRAGS ? (int64_t)fidx(valid[k] ? (uint32_t)i : 0u) : (valid[k] ? i : 0);
+                rec[k] = SGX_WC_NTLOAD ? __builtin_nontemporal_load(cb + ia) : cb[ia];
             }
         }
         lds_barrier();  // B4
@@ -1638,7 +1660,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
             if (ovf) atomicOr(err, PAD_OVERFLOW);
         }
     }
-    }  // fragments
+    }
     if (bad) atomicOr(err, SCATTER_OOB);
 }
 
@@ -2503,8 +2525,9 @@ hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, const uint32_t *
 // only the others go through their super-partition to level 2 -- fewer records for level 2
 // on any keys.  Any choice of hot set gives the same bytes: a hot stream's cursors are the
 // single-pass offsets, and level 2 sees every cold partition's records of a chunk in input
-// order.  The cut: a 256-bin histogram of the counts over [0, max], the highest bins holding
-// >= SPLIT_HOT_CAP partitions, then the first SPLIT_HOT_CAP of those in id order.
+// order.  The cut: a 256-bin log-scale histogram of the counts; every partition of the bins
+// above bmin -- the highest bin whose suffix holds >= SPLIT_HOT_CAP partitions -- then bin
+// bmin's in id order up to SPLIT_HOT_CAP.
 // One workgroup; R <= 4 * 1024.
 constexpr int HS_THREADS = 1024, HS_PER = 4;
 // counts: per-partition counts (the padded split's sampled estimate), or null to take them from
@@ -2513,26 +2536,41 @@ __global__ __launch_bounds__(HS_THREADS) void k_hot_select(const uint32_t *__res
                                                            const uint32_t *__restrict__ counts, int R, int Q,
                                                            uint16_t *__restrict__ stream_of,
                                                            int32_t *__restrict__ hot_part) {
-    __shared__ uint32_t s_w[HS_THREADS / 64];
+    __shared__ uint32_t s_w[HS_THREADS / 64], s_w2[HS_THREADS / 64];
     __shared__ uint32_t s_hist[256];
-    __shared__ uint32_t s_max, s_bin;
+    __shared__ uint32_t s_bin;
     const uint32_t tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    uint32_t cnt[HS_PER], mx = 0;
+    // bins on a log scale, 8 per octave (a bin's counts within 9% of each other): linear bins
+    // over [0, max] put every partition but a few under a Zipf head in bin 0, and the cut then
+    // took the first partitions by id
+    auto hbin = [](uint32_t c) -> uint32_t {
+        const uint32_t l = 31u - (uint32_t)__clz(c | 1u);
+        const uint32_t m = (l >= 3 ? c >> (l - 3) : c << (3 - l)) & 7u;
+        return l * 8u + m;
+    };
+    uint32_t cnt[HS_PER];
 #pragma unroll
     for (int i = 0; i < HS_PER; ++i) {
         const int p = (int)tid * HS_PER + i;
         cnt[i] = p < R ? (counts ? counts[p] : part_off[p + 1] - part_off[p]) : 0u;
-        mx = max(mx, cnt[i]);
     }
     if (tid < 256) s_hist[tid] = 0;
-    if (tid == 0) s_max = 0;
     __syncthreads();
-    atomicMax(&s_max, mx);
-    __syncthreads();
-    const uint64_t span = (uint64_t)s_max + 1;
+    // one LDS atomic per distinct bin of a wave (the lanes of a bin counted by a ballot): equal
+    // counts -- most partitions of a skewed map -- made every lane's atomic hit one address
 #pragma unroll
-    for (int i = 0; i < HS_PER; ++i)
-        if ((int)tid * HS_PER + i < R && cnt[i]) atomicAdd(&s_hist[(uint32_t)((uint64_t)cnt[i] * 256 / span)], 1u);
+    for (int i = 0; i < HS_PER; ++i) {
+        const uint32_t b = hbin(cnt[i]);
+        bool todo = cnt[i] != 0;
+        while (__ballot(todo)) {
+            const uint32_t lead = (uint32_t)__ffsll((unsigned long long)__ballot(todo)) - 1u;
+            const uint32_t lb = (uint32_t)__shfl((int)b, (int)lead, 64);
+            const bool mine = todo && b == lb;
+            const uint32_t k = (uint32_t)__popcll(__ballot(mine));
+            if (lane == lead) atomicAdd(&s_hist[lb], k);
+            todo = todo && !mine;
+        }
+    }
     __syncthreads();
     // the lowest bin whose bins above hold >= SPLIT_HOT_CAP partitions: the highest bin b whose
     // suffix sum (bins b..255) reaches the cap, else 0 -- a suffix scan over the 256 bins by the
@@ -2551,13 +2589,40 @@ __global__ __launch_bounds__(HS_THREADS) void k_hot_select(const uint32_t *__res
         __syncthreads();
     }
     __syncthreads();
+    // hot: every partition of a bin above bmin (fewer than the cap), then bin bmin's in id
+    // order up to the cap
     const uint32_t bmin = s_bin;
-    uint32_t hot[HS_PER], c = 0;
+    uint32_t hot[HS_PER], eq = 0, ca = 0, ce = 0;
 #pragma unroll
     for (int i = 0; i < HS_PER; ++i) {
-        hot[i] = (cnt[i] > 0 && (uint32_t)((uint64_t)cnt[i] * 256 / span) >= bmin) ? 1u : 0u;
-        c += hot[i];
+        const uint32_t hb = hbin(cnt[i]);
+        hot[i] = (cnt[i] > 0 && hb > bmin) ? 1u : 0u;
+        eq |= (cnt[i] > 0 && hb == bmin) ? 1u << i : 0u;
+        ca += hot[i];
+        ce += (eq >> i) & 1u;
     }
+    {
+        const uint32_t x = ca | (ce << 16);  // both <= R <= 4096
+        const uint32_t xi = wave_inclusive_scan(x, lane);
+        if (lane == 63) s_w2[w] = xi;
+        __syncthreads();
+        uint32_t eb = (xi - x) >> 16, above = 0;
+        for (uint32_t v = 0; v < HS_THREADS / 64; ++v) {
+            if (v < w) eb += s_w2[v] >> 16;
+            above += s_w2[v] & 0xFFFFu;
+        }
+        const uint32_t room = (uint32_t)SPLIT_HOT_CAP - min(above, (uint32_t)SPLIT_HOT_CAP);
+#pragma unroll
+        for (int i = 0; i < HS_PER; ++i) {
+            if ((eq >> i) & 1u) {
+                hot[i] = eb < room ? 1u : 0u;
+                ++eb;
+            }
+        }
+    }
+    uint32_t c = 0;
+#pragma unroll
+    for (int i = 0; i < HS_PER; ++i) c += hot[i];
     const uint32_t incl = wave_inclusive_scan(c, lane);
     if (lane == 63) s_w[w] = incl;
     __syncthreads();
@@ -2612,30 +2677,6 @@ hipError_t launch_cold_super_est(const uint32_t *est, const uint16_t *stream_of,
                                  hipStream_t stream) {
     if (S <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_cold_super_est, dim3((unsigned)S), dim3(64), 0, stream, est, stream_of, S, Q, est1);
-    return hipGetLastError();
-}
-
-// Level 2's work list, one fragment per (super s, chunk g) of the level-1 scratch, s-major:
-// desc[s*G + g] = {begin, end, s, g} (end = begin + the stream's level-1 count); *ndesc = S*G.
-__global__ __launch_bounds__(256) void k_frag_desc(const uint32_t *__restrict__ fstart1,
-                                                   const uint32_t *__restrict__ cnt1, int S, int G,
-                                                   int64_t *__restrict__ desc, uint32_t *__restrict__ ndesc) {
-    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    if (i == 0) *ndesc = (uint32_t)((int64_t)S * G);
-    if (i >= (int64_t)S * G) return;
-    const int64_t b = fstart1[i];
-    int64_t *d = desc + 4 * i;
-    d[0] = b;
-    d[1] = b + cnt1[(int64_t)SPLIT_HOT_CAP * G + i];
-    d[2] = i / G;
-    d[3] = i % G;
-}
-
-hipError_t launch_frag_desc(const uint32_t *fstart1, const uint32_t *cnt1, int S, int G, int64_t *desc,
-                            uint32_t *ndesc, hipStream_t stream) {
-    const int64_t n = (int64_t)S * G;
-    hipLaunchKernelGGL(k_frag_desc, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, stream, fstart1, cnt1, S, G, desc,
-                       ndesc);
     return hipGetLastError();
 }
 
@@ -2710,6 +2751,10 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
                                 const ScatterGeom &geo, uint32_t *err, hipStream_t stream) {
     if ((pp.R & (pp.R - 1)) != 0) return hipErrorInvalidValue;
     if (pp.pad_cnt && (!pp.pad_cap || !pp.olim)) return hipErrorInvalidValue;
+    // the padded split's level 2: packed fragments, a workgroup per (super group, chunk)
+    if (pp.pad_cnt && (!pp.frag_start || !pp.frag_cnt || pp.pack < 1 || pp.pack > SPLIT_PACK_MAX ||
+                       pp.R != 64u * pp.pack || grid % G != 0))
+        return hipErrorInvalidValue;
     // the map side's split level 2 (hash bits), or the sorted read's segmented window pass
     // (key bits, never padded)
     const bool key_bits = pp.kind == KIND_KEY_BITS, digit = pp.kind == KIND_DIGIT;

@@ -292,9 +292,9 @@ static PadGeom pad_geom(sgx_engine *e, const Shuffle &s, int64_t n, const ChunkT
 
 // The hybrid two-level split (partition_pass), padded: the hot partitions --
 // chosen from the sampled counts -- stream from level 1 into their final sub-bins, the others
-// into sub-bins of their super-partition in a scratch buffer; level 2 walks the scratch one
-// (super, chunk) fragment at a time and writes each cold partition's records into ITS final
-// sub-bin of that chunk.  Then, as in padded_pass: K3 over the final counts, and a guarded
+// into sub-bins of their super-partition in a scratch buffer; level 2 reads the scratch's
+// (super, chunk) fragments of 16 supers and one chunk per workgroup and writes each cold
+// partition's records into ITS final sub-bin of that chunk.  Then, as in padded_pass: K3 over the final counts, and a guarded
 // two-pass fallback (K1+K2, K3, the single lane-ordered K4).
 static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n,
                              const PadGeom &pg) {
@@ -340,11 +340,11 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
     uint32_t *pcap = (uint32_t *)((char *)est + rbytes);
     c.last_off_dev = part_off_dev;
     // the split's scratch: [stream_of u16 R][hot_part i32 HOT][est1 S][cap1 S][fstart1 S*G]
-    // [cnt1 (HOT+S)*G][cur1 (HOT+S)*G][capS HOT+S][ndesc | pad][desc i64 4*S*G]
+    // [cnt1 (HOT+S)*G][cur1 (HOT+S)*G][capS HOT+S]
     const int64_t ns = (int64_t)(HOT + S);
     const size_t b_so = al((size_t)R * 2), b_hp = al((size_t)HOT * 4), b_s = al((size_t)S * 4);
     const size_t b_sg = al((size_t)S * G * 4), b_st = al((size_t)ns * G * 4), b_cs = al((size_t)ns * 4);
-    SGX_TRY(c.split_work.ensure(b_so + b_hp + 2 * b_s + b_sg + 2 * b_st + b_cs + 16 + (size_t)S * G * 32));
+    SGX_TRY(c.split_work.ensure(b_so + b_hp + 2 * b_s + b_sg + 2 * b_st + b_cs));
     char *x = (char *)c.split_work.p;
     uint16_t *stream_of = (uint16_t *)x;
     int32_t *hot_part = (int32_t *)(x += b_so);
@@ -354,8 +354,6 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
     uint32_t *cnt1 = (uint32_t *)(x += b_sg);
     uint32_t *cur1 = (uint32_t *)(x += b_st);
     uint32_t *capS = (uint32_t *)(x += b_st);
-    uint32_t *ndesc = (uint32_t *)(x += b_cs);
-    int64_t *desc = (int64_t *)(x + 16);
     HIP_TRY(hipMemsetAsync(c.work.p, 0, work_bytes, st));
     hipEvent_t h0 = e->ev(), h1 = e->ev(), c1 = e->ev(), x1 = e->ev();
     HIP_TRY(hipEventRecord(h0, st));
@@ -379,18 +377,24 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
     HIP_TRY(launch_scatter(in, m.data.p, n, 16, pg.chunk, G, p1, cur1, pg.geo, err_pad, st, c.split_tmp.p,
                            (uint32_t)HOT));
     SGX_TRY(debug_sync(e, st, "K4 padded split level 1"));
-    HIP_TRY(launch_frag_desc(fstart1, cnt1, S, G, desc, ndesc, st));
-    const ScatterGeom geo2 = scatter_geom16_wc((uint32_t)Q);
+    // level 2: a workgroup per (group of `pack` supers, chunk), its 64 pack streams the
+    // group's partitions (pid & (64 pack - 1)), the group's fragments of that chunk read back to
+    // back
+    const int pack = std::min<int>(S, (int)SPLIT_PACK_MAX);
+    const ScatterGeom geo2 = scatter_geom16_wc((uint32_t)(Q * pack));
     PartParams p2 = s.pp;
     p2.kind = KIND_HASH_POW2;
-    p2.R = (uint32_t)Q;
+    p2.R = (uint32_t)(Q * pack);
     p2.mbits = (uint32_t)geo2.mbits;
     p2.olim = olim;
     p2.pad_cnt = cnt;
     p2.pad_cap = pcap;
-    const int grid2 = (int)std::min<int64_t>((int64_t)S * G, (int64_t)e->num_cus);
-    HIP_TRY(launch_scatter16_seg(c.split_tmp.p, m.data.p, n, p2, fstart, G, desc, ndesc, nullptr, grid2, geo2, err_pad,
-                                 st));
+    p2.frag_start = fstart1;
+    p2.frag_cnt = cnt1 + (int64_t)HOT * G;
+    p2.pack = (uint32_t)pack;
+    const int grid2 = (S / pack) * G;
+    HIP_TRY(launch_scatter16_seg(c.split_tmp.p, m.data.p, n, p2, fstart, G, nullptr, nullptr, nullptr, grid2, geo2,
+                                 err_pad, st));
     SGX_TRY(debug_sync(e, st, "K4 padded split level 2"));
     HIP_TRY(launch_hot_counts(cnt1, hot_part, G, cnt, st));
     HIP_TRY(hipEventRecord(c1, st));
