@@ -5,10 +5,12 @@
   python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...
 
 A step is one pass of the hot path over one batch: every rank partitions its own batch of
-16 B records resident in HBM (K1+K2 histogram, K3 decoupled-look-back scan, K4 stable
-scatter) and, for N > 1, pushes it to the reducer owners (counts all-gather +
-ncclAllToAllv over xGMI + K5 regroup).  Weak scaling: 2^28 records per GPU (config C1 at
-N=1; config C2's 2^31 total at N=8).  value = 16 B x records of all ranks / max-rank time.
+records resident in HBM (the single-pass padded write: sampled histogram, K4 stable
+write-combining scatter into sub-bins, the scan of the true counts on a second stream) and,
+for N > 1, pushes it to the reducer owners (lengths all-gather + the direct peer gather into
+their IPC-mapped receive buffers over xGMI).  Weak scaling: 2^28 records per GPU (config C1
+at N=1; config C2's 2^31 total at N=8).  value = record bytes x records of all ranks /
+max-rank time.
 
 Also reported (rank 0): the roofline of the dominant kernel (K4 scatter) from HIP events
 on the engine's compute stream over the timed region, the stage breakdown, and the CPU
@@ -51,7 +53,7 @@ def parse():
                     help="R > 1024: one lane-ordered K4 pass instead of the two-level split (A/B measurement)")
     ap.add_argument("--no-padded", action="store_true",
                     help="hash maps take the two-pass map side (histogram + scan + scatter) instead of the "
-                         "single-pass padded write (A/B measurement, DESIGN.md §7)")
+                         "single-pass padded write (A/B measurement, DESIGN.md §6.1)")
     ap.add_argument("--cpu-baseline-seconds", type=float, default=16.0,
                     help="budget of the CPU baseline's timed legs (plus ~5 s of C0 and setup)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -67,8 +69,9 @@ def parse():
                          "ranges balancing each rank's received bytes; the default for c3's skewed keys)")
     ap.add_argument("--self-exchange", action="store_true",
                     help="N=1 only: run every step's exchange through a one-rank RCCL communicator "
-                         "(counts all-gather + ncclAllToAllv to itself), to measure the overlap of map k+1 "
-                         "with the all-to-all of map k on one GPU (a rehearsal, never the default line)")
+                         "(lengths all-gather + the peer gather into its own receive buffer), to measure the "
+                         "overlap of map k+1 with the exchange of map k on one GPU (a rehearsal, never the "
+                         "default line)")
     ap.add_argument("--compress", action="store_true",
                     help="with --serializer kryo: spark.shuffle.compress=true (LZ4 frames, Spark's default)")
     ap.add_argument("--map-tasks", type=int, default=1,
@@ -585,7 +588,7 @@ def main():
                 c_ms = st.ms["compress"] / max(1, st.count["compress"])
                 out["lz4"] = {"kernel": "k_lz4_blocks", "ms": round(c_ms, 4), "framed_bytes": kbytes,
                               "note": "k_lz4_blocks + k_xxh32_blocks: one wave per 32 KiB block, LZ4_compress_default's "
-                                      "search 64 positions per batch, several sequences per batch (DESIGN.md §14)"}
+                                      "search 64 positions per batch, several sequences per batch (DESIGN.md §13)"}
             if world == 1:
                 # reduce side of the same shuffle: every block of the last map, decoded on the GPU
                 dst = eng.alloc(n * 16)

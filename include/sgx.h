@@ -255,7 +255,7 @@ int sgx_map_lengths(sgx_engine *e, int32_t shuffle_id, int64_t map_id, int64_t *
  * batch is copied within HBM, a SGX_MEM_DEVICE_RETAINED batch stays where it is (the caller
  * keeps it until the map's lengths are known: see sgx_mem_kind).  sgx_map_commit then partitions ALL batches in one
  * pass, exactly as sgx_write_map partitions one contiguous batch (the padded single-pass
- * write when sgx_write_map would take it, DESIGN.md §16): every batch is cut into chunks of
+ * write when sgx_write_map would take it, DESIGN.md §7): every batch is cut into chunks of
  * its own and a chunk table replaces the contiguous input.  The result is byte-identical to
  * sgx_write_map of all batches concatenated; LZ4 framing applies as for sgx_write_map.
  * Shuffles the one-pass commit does not cover (map-side combine, R > 1024 under a hash
@@ -276,7 +276,7 @@ int sgx_map_data(sgx_engine *e, int32_t shuffle_id, int64_t map_id, void **out_d
  * its RangePartitioner, written by sgx_write_map (or committed from sgx_map_append batches)
  * on an engine with no communicator at all (none: a one-rank or host-collective communicator
  * counts, so every multi-executor deployment takes the two-pass write), is written in ONE pass
- * over its records (DESIGN.md §7): a sampled
+ * over its records (DESIGN.md §6.1): a sampled
  * histogram sizes a line-aligned sub-bin per (partition, chunk) stream, the stable scatter
  * writes every stream into its sub-bin, and a scan of the streams' true counts gives the
  * partition lengths and index offsets -- the same lengths, offsets and per-block bytes as the

@@ -262,7 +262,7 @@ def reducer_owner(reduce_id: int, num_partitions: int, world: int) -> int:
 # RangePartitioner.sketch, SamplingUtils.reservoirSampleAndCount, XORShiftRandom (+ its
 # hashSeed over scala.util.hashing.MurmurHash3.bytesHash) and RangePartitioner.determineBounds,
 # restated sequentially.  Parity of this row is UNPINNED: no Spark runs here and the reference
-# holds no fixture for it (DESIGN.md §10).
+# holds no fixture for it (DESIGN.md §16).
 M32 = 0xFFFFFFFF
 M64 = 0xFFFFFFFFFFFFFFFF
 

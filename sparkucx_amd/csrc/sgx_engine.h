@@ -96,6 +96,9 @@ struct DevBuf {
     }
 };
 
+// memcpy over a few threads (sgx_engine.cpp)
+void host_copy_parallel(char *dst, const char *src, size_t bytes);
+
 struct HostPinned {
     void *p = nullptr;
     size_t cap = 0;
@@ -181,7 +184,7 @@ struct MapOut {
     bool open = false;
     std::vector<std::unique_ptr<Spill>> spills;
     // deferred (sgx_map.cpp deferred_ok): the batches are kept as appended and the commit
-    // partitions all of them in one pass through a chunk table (DESIGN.md §16)
+    // partitions all of them in one pass through a chunk table (DESIGN.md §7)
     bool deferred = false;
     HostPinned chunk_host;     // [2G] i64 {byte offset from the first batch, records} | [S] i32 first chunk per batch
     DevBuf chunk_dev;
@@ -190,7 +193,7 @@ struct MapOut {
     // chunk count stays ~one per CU whatever the number of batches)
     std::vector<std::unique_ptr<DevBuf>> landing;
     size_t land_used = 0;      // bytes used in landing.back()
-    // Single-pass padded output (sgx_map.cpp padded_pass, DESIGN.md §7): `data` holds one
+    // Single-pass padded output (sgx_map.cpp padded_pass, DESIGN.md §6.1): `data` holds one
     // line-aligned sub-bin per (partition, chunk) stream with unwritten gaps between them;
     // frag = device [fstart][foff][cnt] u32 x R*G: a stream's first record in `data`, its
     // position in the contiguous layout, its record count.  pad_try: this write ran the
@@ -302,6 +305,10 @@ struct Ctx {
     HostPinned host_stage[2];
     Event host_up[2];
     int host_slot = 0;
+    // reads into pageable host memory: two pinned pieces, the DMA of one overlapping the host
+    // copy of the other (copy_to_host, sgx_read.cpp)
+    HostPinned read_stage[2];
+    Event read_ev[2];
     // pre-aggregation records of the last read on this thread (sgx_last_read_records)
     int64_t last_read_records = 0;
     const uint32_t *last_off_dev = nullptr;  // device (R+1) record offsets of the last partition pass
@@ -311,6 +318,12 @@ struct Ctx {
     // that last read it has run (pad_done)
     hipStream_t st_tail = nullptr;
     DevBuf pad_work[2], pad_offs[2];
+    // The padded split's front (sample, hot cut, capacities, cursors) runs on a third stream:
+    // it reads only its own map's input, so it overlaps the previous write's level 2; its
+    // scratch alternates with the slots (split_pad[slot]), and level 1 waits for pre_done[slot]
+    hipStream_t st_pre = nullptr;
+    DevBuf split_pad[2];
+    Event pre_done[2], pre_in;
     // 16 B padded writes: the sample's block per slot ([est][K4 flags][layout]), how many of its
     // leading bytes the slot's last tail left zeroed (its next sample needs them zero), and the
     // event behind that reset (the next write on the slot waits for it, not for the whole tail)
@@ -354,6 +367,10 @@ struct Ctx {
         if (st_tail) {
             (void)hipStreamSynchronize(st_tail);
             (void)hipStreamDestroy(st_tail);
+        }
+        if (st_pre) {
+            (void)hipStreamSynchronize(st_pre);
+            (void)hipStreamDestroy(st_pre);
         }
     }
 };

@@ -341,6 +341,11 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
         return debug_sync(e, st, "exchange peer gather");
     };
     int rc = launch();
+    // peers' buffers are written through this GPU's L2s: write them back before the barrier
+    if (rc == SGX_OK && P > 1 && sent > 0) {
+        const hipError_t fe = launch_l2_fence(true, st);
+        if (fe != hipSuccess) rc = fail_msg(SGX_ERR_HIP, "peer gather release: %s", hipGetErrorString(fe));
+    }
     if (P > 1 && e->comm) {
         // completion barrier on the stream: a peer's allreduce runs after its gather, so once
         // this one completes every block of my reducers has landed (a rank whose launch failed
@@ -353,6 +358,8 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
         const int mrc = mark_used();
         if (rc != SGX_OK) return rc;
         SGX_TRY(mrc);
+        // the peers' stores into my buffer are in HBM now: drop my L2s' older lines of it
+        HIP_TRY(launch_l2_fence(false, st));
     } else if (P > 1) {
         // host collectives: the gather has finished on every rank once the barrier returns
         if (rc == SGX_OK) rc = comm_wait(e);
@@ -360,6 +367,7 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
         const int brc = agree(rc, msg, nullptr, 0, nullptr);
         if (brc != SGX_OK) return brc;
         SGX_TRY(mark_used());
+        HIP_TRY(launch_l2_fence(false, st));
     } else if (rc != SGX_OK) {
         return rc;
     }

@@ -27,7 +27,7 @@ struct PartParams {
     // [2^RDIR_BITS + 1]: dir[j] = first bound whose top bits are >= j), or null when the bounds
     // need the JDK binary search's exact path (duplicates with more than 128 bounds)
     const uint16_t *dir;
-    // ---- single-pass padded map output (DESIGN.md §7, sgx_map.cpp padded_pass) ----
+    // ---- single-pass padded map output (DESIGN.md §6.1, sgx_map.cpp padded_pass) ----
     // guard: non-null -> the kernel (k_hist, k_scatter16_wc) runs only when *guard holds
     // PAD_OVERFLOW, i.e. it is the two-pass fallback of a padded write whose bins overflowed
     const uint32_t *guard;
@@ -158,7 +158,7 @@ int64_t scan_tiles(int64_t len);
 // share CUs with that K4 instead of holding back some of its workgroups.
 hipError_t launch_scan_wave(const uint32_t *counts, uint32_t *offs, int64_t len, uint64_t *status, uint32_t *ticket,
                             uint32_t *err, uint32_t *part_off, int G, int R, hipStream_t stream);
-// Padded map output (DESIGN.md §7).  launch_pad_sample: est[p] += records of partition p among
+// Padded map output (DESIGN.md §6.1).  launch_pad_sample: est[p] += records of partition p among
 // every `stride`-th group of 8 records (est zeroed by the caller; hash partitioner over 16 B
 // records, or RangePartitioner over 100 B TeraSort records; R <= 4096).  With a chunk table
 // (pp.chunks, a streaming map) each of the G chunks (<= `chunk` records) is sampled on its own.
@@ -201,6 +201,8 @@ int64_t pad_capacity_bound(int64_t n, int R, int64_t chunk, int G, int64_t sampl
 // dst + rb * (foff[p*G+g] - foff[p*G]).  desc[b] = {src, fstart, foff, cnt, dst, p, G_b, rb};
 // G = the largest G_b.
 constexpr int FRAG_DESC_WORDS = 8;
+// the peer gather's system-scope L2 write-back (release) / invalidate (acquire) on every XCD
+hipError_t launch_l2_fence(bool release, hipStream_t stream);
 hipError_t launch_gather_frags(const int64_t *desc, int64_t nblocks, int G, hipStream_t stream,
                                int max_rows = 65535);  // max_rows: workgroups per fragment column
 // Two-level split scatter (hash partitioner, power-of-two R > 1024, 16 B records):
@@ -222,7 +224,7 @@ hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, const uint32_t *
 hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const PartParams &pp, const uint32_t *offs,
                                 int G, const int64_t *desc, const uint32_t *ndesc, const uint32_t *seg_end, int grid,
                                 const ScatterGeom &geo, uint32_t *err, hipStream_t stream);
-// Hybrid split (DESIGN.md §6.3): from the partition offsets, stream_of[p] = hot index for
+// Hybrid split (DESIGN.md §6.2): from the partition offsets, stream_of[p] = hot index for
 // about the SPLIT_HOT_CAP largest partitions (a coarse count histogram picks the cut; the hot
 // ones numbered in id order), else SPLIT_HOT_CAP + p / Q; hot_part[h] = the partition of hot
 // stream h (-1: unused).
@@ -238,7 +240,7 @@ hipError_t launch_super_counts_cold(const uint32_t *counts, const uint16_t *stre
 hipError_t launch_hot_cursors(const uint32_t *offs, const int32_t *hot_part, const uint32_t *offs1, uint32_t *cur1,
                               int S, int G, hipStream_t stream, const uint32_t *pcap = nullptr,
                               const uint32_t *cap1 = nullptr, uint32_t *capS = nullptr);
-// The padded split (DESIGN.md §7): est1[s] = cold partitions' sampled counts per super; level 2's
+// The padded split (DESIGN.md §6.1): est1[s] = cold partitions' sampled counts per super; level 2's
 // fragment list desc[s*G+g] = {begin, end, s, g} of the level-1 scratch sub-bins (cnt1: the
 // level-1 streams' counts, [HOT + S][G]); the hot partitions' final counts from level 1.
 hipError_t launch_cold_super_est(const uint32_t *est, const uint16_t *stream_of, int S, int Q, uint32_t *est1,
@@ -252,7 +254,7 @@ hipError_t launch_hot_counts(const uint32_t *cnt1, const int32_t *hot_part, int 
 hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, const PartParams &pp, int use_p,
                               uint32_t kshift, uint32_t kbits, uint32_t *err, hipStream_t stream);
 // Engine-start self-check of the lane-ordered LDS atomics the ordered ranking relies on:
-// *bad |= 1 on any violation (sgx_create; DESIGN.md §6.2).
+// *bad |= 1 on any violation (sgx_create; DESIGN.md §6.1).
 hipError_t launch_lds_order_probe(uint32_t *bad, hipStream_t stream);
 // out2 / hot_cap: KIND_HOT_SPLIT only -- streams >= hot_cap go to out2 (the split's scratch)
 hipError_t launch_scatter(const void *in, void *out, int64_t n, int record_bytes, int64_t chunk,

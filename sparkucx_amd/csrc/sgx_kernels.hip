@@ -1298,7 +1298,7 @@ __host__ __device__ size_t scatter16_wc_lds(uint32_t R, int waves, int si) {
 // SEG (level 2 of the two-level split, launch_scatter16_seg): the workgroup's records are
 // piece desc[blockIdx.x] = {begin, -, super s, chunk g}, up to the next piece's begin,
 // instead of chunk blockIdx.x, and its R streams start at offs[(s * R + p) * G + g].
-// MODE (single-pass padded write, DESIGN.md §7): 0 the two-pass K4; WC_PADDED the padded K4
+// MODE (single-pass padded write, DESIGN.md §6.1): 0 the two-pass K4; WC_PADDED the padded K4
 // (streams start at their sub-bins, output capacity pp.olim, final counts to pp.pad_cnt
 // checked against pp.pad_cap); WC_FALLBACK the fallback's K4, a no-op unless *pp.guard holds
 // PAD_OVERFLOW.  Three instantiations, so profiles tell them apart.
@@ -1779,7 +1779,7 @@ __host__ __device__ size_t scatter_wide2_lds(uint32_t R, int rb, int kind, int n
 
 // MODE: as k_scatter16_wc's (0, WC_PADDED: streams start at their sub-bins, final counts to
 // pp.pad_cnt checked against pp.pad_cap; WC_FALLBACK: a no-op unless *pp.guard has
-// PAD_OVERFLOW), so TeraSort maps are written in one pass too (DESIGN.md §7).
+// PAD_OVERFLOW), so TeraSort maps are written in one pass too (DESIGN.md §6.1).
 template <int KIND, int RB, int MODE = 0>
 __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restrict__ in, uint32_t *__restrict__ out,
                                                           int64_t n, int64_t chunk, PartParams pp,
@@ -1985,7 +1985,7 @@ __global__ __launch_bounds__(512, 1) void k_scatter_wide2(const u32x4 *__restric
             }
             WC_STAMP(7);  // drain: LDS reads
             // (holding the last batch's pieces back for the next tile's ranking, as the 16 B
-            // kernel does, measured slower here: DESIGN.md §6.4)
+            // kernel does, measured slower here: DESIGN.md §6.3)
 #pragma unroll
             for (int q = 0; q < DRB; ++q)
                 if (live[q] && dst[q] < olim) store_piece(v[q], dst[q], pc[q]);
@@ -2023,7 +2023,7 @@ ScatterGeom scatter_geom_wide2(uint32_t R, int rb, int kind, int nb) {
 
 // ------------------------------------------------------------------------------------
 // Write-combining K4 for 100 B records (TeraSort under its RangePartitioner, R <= 1024;
-// DESIGN.md §6.4).  k_scatter_wide2 writes each record as it comes; at R = 1024 a tile holds
+// DESIGN.md §6.3).  k_scatter_wide2 writes each record as it comes; at R = 1024 a tile holds
 // ~1 record per stream, so every record leaves as partial 128 B lines that the L2 merges only
 // while the line stays resident (1.18x the record bytes written).  Here every stream keeps
 // its incomplete 64 B unit on chip (a carry of <= 60 bytes in LDS, 64 KB at R = 1024) and
@@ -2518,7 +2518,7 @@ hipError_t launch_seg_desc(const uint32_t *offs1, int S, int G, const uint32_t *
     return hipGetLastError();
 }
 
-// Hybrid split (DESIGN.md §6.3).  Moving a hot partition's records twice is what made the
+// Hybrid split (DESIGN.md §6.2).  Moving a hot partition's records twice is what made the
 // plain split lose on skewed keys, so level 1 writes about the SPLIT_HOT_CAP largest
 // partitions straight to the final output through streams of their own (write-combined like
 // every stream: a write-combining pass costs about the same at 768 streams as at 64), and
@@ -2654,7 +2654,7 @@ hipError_t launch_hot_select(const uint32_t *part_off, int R, int Q, uint16_t *s
     return hipGetLastError();
 }
 
-// ---- the padded split (DESIGN.md §7): level 1 into sub-bins (hot partitions: their final
+// ---- the padded split (DESIGN.md §6.1): level 1 into sub-bins (hot partitions: their final
 // sub-bins; cold super-partitions: sub-bins of a scratch buffer), level 2 one (super, chunk)
 // fragment at a time into the cold partitions' final sub-bins.
 // est1[s] = the cold partitions' sampled counts summed per super-partition.
@@ -2788,7 +2788,7 @@ hipError_t launch_scatter16_seg(const void *in, void *out, int64_t n, const Part
 }
 
 // ------------------------------------------------------------------------------------
-// The sorted read's segmented window pass (DESIGN.md §11).  After the gather the records of
+// The sorted read's segmented window pass (DESIGN.md §10).  After the gather the records of
 // each partition are contiguous (canonical reducer-major order), so sorting by (partition,
 // window bits) needs no pass by the partitioner: one stable write-combining pass by the
 // window bits inside every partition's segment -- K4's SEG mode over pieces of the segments,
@@ -3257,7 +3257,7 @@ hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, cons
 // (issue order, then lane order).  Probed once per engine with the ranking's exact
 // instruction pattern (packed u16 counters, relaxed workgroup-scope fetch-add, one wait):
 // every (item k, lane l) must receive exactly the number of earlier (k' < k, or k' == k and
-// l' < l) increments of its counter.  A violation sets *bad (DESIGN.md §6.2).
+// l' < l) increments of its counter.  A violation sets *bad (DESIGN.md §6.1).
 // ------------------------------------------------------------------------------------
 constexpr int PROBE_NI = 8, PROBE_ROUNDS = 96;
 __global__ __launch_bounds__(512) void k_lds_order_probe(uint32_t *bad) {
@@ -3625,7 +3625,7 @@ hipError_t launch_gather_items(const int64_t *items, int64_t n_items, int align,
 }
 
 // ------------------------------------------------------------------------------------
-// Single-pass padded map output (DESIGN.md §7).  The two-pass map side reads every record
+// Single-pass padded map output (DESIGN.md §6.1).  The two-pass map side reads every record
 // twice (K1+K2's histogram, then K4): 48 B of HBM per 16 B record instead of 32.  The
 // padded write skips the full histogram.  A sampled histogram (one line in `stride`) sizes
 // a sub-bin per (partition, chunk) stream with a Poisson margin; K4 writes every stream from
@@ -4015,6 +4015,31 @@ __global__ __launch_bounds__(FRAG_THREADS) void k_gather_frags(const int64_t *__
         frag_copy((const char *)(uintptr_t)d[0] + (uint64_t)fstart[i] * rb,
                   (char *)(uintptr_t)d[4] + (uint64_t)(foff[i] - foff[(int64_t)p * G]) * rb, (uint64_t)cnt[i] * rb, tid);
     }
+}
+
+// Cross-GPU visibility of the peer gather.  A peer's receive buffer is ordinary
+// device memory mapped over xGMI, so the gather's stores may sit dirty in this GPU's L2s, and the
+// owner's L2s may hold lines of the buffer from an earlier round.  k_l2_release writes back every
+// XCD's L2 (a system-scope release) behind the gather, before the round's barrier;
+// k_l2_acquire drops every XCD's non-coherent lines (a system-scope acquire) behind the barrier,
+// before any read of the round.  Workgroups are dispatched round-robin over the XCDs: 64 of
+// them reach all eight.
+__global__ __launch_bounds__(64) void k_l2_release(uint32_t *sink) {
+    __threadfence_system();
+    __builtin_amdgcn_s_waitcnt(0);  // the write-back has completed before the wave ends
+    if (sink && threadIdx.x == 0 && blockIdx.x == 0) sink[0] = 0u;
+}
+__global__ __launch_bounds__(64) void k_l2_acquire(uint32_t *sink) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    if (sink && threadIdx.x == 0 && blockIdx.x == 0) sink[0] = 0u;
+}
+
+hipError_t launch_l2_fence(bool release, hipStream_t stream) {
+    if (release)
+        hipLaunchKernelGGL(k_l2_release, dim3(64), dim3(64), 0, stream, (uint32_t *)nullptr);
+    else
+        hipLaunchKernelGGL(k_l2_acquire, dim3(64), dim3(64), 0, stream, (uint32_t *)nullptr);
+    return hipGetLastError();
 }
 
 hipError_t launch_gather_frags(const int64_t *desc, int64_t nblocks, int G, hipStream_t stream, int max_rows) {

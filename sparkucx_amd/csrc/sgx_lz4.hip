@@ -3,7 +3,7 @@
 // Spark 3.0.1 defaults; SerializerManager.wrapStream per partition in
 // ShufflePartitionPairsWriter.open).  Byte-identical to liblz4 1.9.x LZ4_compress_default
 // per 32 KiB block + XXH32 (seed 0x9747b28c, masked to 28 bits) + the 21-byte block headers and
-// the end mark; see oracle/lz4_oracle.c for the restated algorithm and DESIGN.md §14.
+// the end mark; see oracle/lz4_oracle.c for the restated algorithm and DESIGN.md §13.
 //
 // Three kernels:
 //   k_lz4_blocks    one WAVE per block: the block's 8192-entry u16 hash table lives in LDS
@@ -96,7 +96,7 @@ __device__ __forceinline__ uint32_t g32(const uint8_t *p) {
 // The compressor's view of its block: bytes [0, n) read as one unaligned little-endian dword
 // (u32) or one byte (u8) through L1.  (Staging the whole block in LDS first -- 48 KiB per
 // block with the table, 3 blocks per CU instead of 10 -- measured 1.7x slower on C1's Kryo
-// stream: DESIGN §14.)
+// stream: DESIGN §13.)
 struct GlobalSrc {
     const uint8_t *p;
     __device__ __forceinline__ uint32_t u32(int i) const { return g32(p + i); }
@@ -189,11 +189,11 @@ __device__ __forceinline__ int lane_value(int v, int l) { return __builtin_amdgc
 //  * LZ4_count: 64 4-byte comparisons per round, the first differing byte from a ballot.
 //  * the backward catch-up: 64 byte comparisons per round.
 //  * literal and length-run bytes: lane-parallel stores.
-// The wave is latency-bound (DESIGN §14), so loads whose addresses are known early go out
+// The wave is latency-bound (DESIGN §13), so loads whose addresses are known early go out
 // together: the catch-up's and LZ4_count's first rounds (the catch-up never moves the match
 // end), a _next_match candidate's 4-byte test and its first count round, and the next
 // search's first 64 sequences with the _next_match test.  (Loading each search batch's
-// successor with the batch measured 2-3% slower: DESIGN §14.)  Only loads move; every table
+// successor with the batch measured 2-3% slower: DESIGN §13.)  Only loads move; every table
 // access and every decision stays in the serial order.
 // LZ4_count's end: the first a' >= a with src[a'] != src[a' + d0], or mlimit.  (d, full) is
 // the first round's comparison at a + 4 * lane, issued by the caller.

@@ -1,5 +1,5 @@
 // sgx_lz4_host.cpp — host side of the LZ4 codec (spark.shuffle.compress=true with
-// spark.io.compression.codec=lz4, Spark 3.0.1's defaults; DESIGN.md §12): lz4-java's
+// spark.io.compression.codec=lz4, Spark 3.0.1's defaults; DESIGN.md §11): lz4-java's
 // LZ4BlockOutputStream framing of partition streams and LZ4BlockInputStream on fetched
 // blocks, both on the GPU (sgx_lz4.hip) with grow-only per-thread scratch.
 #include "sgx_engine.h"

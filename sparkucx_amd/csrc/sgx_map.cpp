@@ -64,7 +64,7 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
     // hot partitions straight to the output and the cold ones into S = R / 64
     // super-partitions, level 2 splits each super into Q = 64; both write-combining, whole
     // lines only, instead of one pass whose runs leave L2 as partial lines (sgx_kernels.hip,
-    // "Two-level split scatter", "Hybrid split"; DESIGN.md §6.3)
+    // "Two-level split scatter", "Hybrid split"; DESIGN.md §6.2)
     const bool split = rb == 16 && kind == SGX_PART_HASH && R > 1024 && (R & (R - 1)) == 0 && R <= 4096 &&
                        e->rank_mode == SGX_RANK_ORDERED && e->sc_waves == 0 && e->sc_items == 0 &&
                        !(e->flags & (SGX_FLAG_NO_WRITE_COMBINING | SGX_FLAG_NO_SPLIT_SCATTER));
@@ -210,7 +210,7 @@ int sgx::partition_pass(sgx_engine *e, Ctx &c, const void *in, void *out, int64_
 }
 
 // ------------------------------------------------------------------------------------
-// single-pass padded write (DESIGN.md §7)
+// single-pass padded write (DESIGN.md §6.1)
 // ------------------------------------------------------------------------------------
 // Whether the map is written padded: hash partitioner, 16 B fixed-codec records, R within the
 // write-combining K4 (<= 1024), the default kernels, no communicator at all (an exchange sends
@@ -290,12 +290,15 @@ static PadGeom pad_geom(sgx_engine *e, const Shuffle &s, int64_t n, const ChunkT
     return pg;
 }
 
-// The hybrid two-level split (partition_pass, DESIGN.md §6.3), padded: the hot partitions --
+// The hybrid two-level split (partition_pass, DESIGN.md §6.2), padded: the hot partitions --
 // chosen from the sampled counts -- stream from level 1 into their final sub-bins, the others
 // into sub-bins of their super-partition in a scratch buffer; level 2 reads the scratch's
 // (super, chunk) fragments of 16 supers and one chunk per workgroup and writes each cold
 // partition's records into ITS final sub-bin of that chunk.  Then, as in padded_pass: K3 over the final counts, and a guarded
 // two-pass fallback (K1+K2, K3, the single lane-ordered K4).
+#ifndef SGX_SPLIT_PRE_STREAM  // (A/B builds: 0 runs the split's front on the main stream)
+#define SGX_SPLIT_PRE_STREAM 1
+#endif
 static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n,
                              const PadGeom &pg) {
     hipStream_t st = c.st;
@@ -306,6 +309,18 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
     const int G = pg.G;
     const int64_t len = (int64_t)R * G, tiles = scan_tiles(len);
     const uint32_t olim = (uint32_t)pg.olim;
+    // this write's work slot: the tail that last read it (two writes ago) must have run.  The
+    // front (sample, cut, capacities, cursors) runs on the pre stream, which waits for that
+    // tail only -- not for the previous write's level 2 on the main stream -- and for the
+    // input when the engine staged it on the main stream
+    const int slot = c.pad_slot;
+    c.pad_slot ^= 1;
+    hipStream_t pre = SGX_SPLIT_PRE_STREAM ? c.st_pre : st;
+    if (c.pad_done[slot].ev) HIP_TRY(hipStreamWaitEvent(pre, c.pad_done[slot].ev, 0));
+    if (in == c.input_stage.p) {
+        HIP_TRY(c.pre_in.record(st));
+        HIP_TRY(hipStreamWaitEvent(pre, c.pre_in.ev, 0));
+    }
     // the fallback's own geometry (the single lane-ordered K4)
     const ScatterGeom gfb = scatter_geom16_ord((uint32_t)R);
     if (gfb.items == 0) return fail_msg(SGX_ERR_UNSUPPORTED, "no single-pass geometry for R=%d", R);
@@ -316,7 +331,7 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
     SGX_TRY(m.data.ensure((size_t)olim * 16));
     SGX_TRY(m.frag.ensure((size_t)len * 12 + 16));
     uint32_t *fstart = (uint32_t *)m.frag.p, *foff = fstart + len, *cnt = foff + len;
-    SGX_TRY(c.offs.ensure((size_t)len_fb * 4));
+    SGX_TRY(c.pad_offs[slot].ensure((size_t)len_fb * 4));
     SGX_TRY(c.split_tmp.ensure((size_t)olim * 16));
     // [fallback counts][fallback ticket | status][offsets R+1 | error | padded flags]
     // [padded scan ticket | status][est R][pcap R], one memset
@@ -327,8 +342,8 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
     const size_t status_bytes = al((size_t)(16 + tiles * 8));
     const size_t rbytes = al((size_t)R * 4);
     const size_t work_bytes = counts_bytes + status_fb_bytes + off_bytes + status_bytes + 2 * rbytes;
-    SGX_TRY(c.work.ensure(work_bytes));
-    char *w = (char *)c.work.p;
+    SGX_TRY(c.pad_work[slot].ensure(work_bytes));
+    char *w = (char *)c.pad_work[slot].p;
     uint32_t *counts_fb = (uint32_t *)w;
     uint32_t *ticket_fb = (uint32_t *)(w + counts_bytes);
     uint64_t *status_fb = (uint64_t *)((char *)ticket_fb + 16);
@@ -344,8 +359,8 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
     const int64_t ns = (int64_t)(HOT + S);
     const size_t b_so = al((size_t)R * 2), b_hp = al((size_t)HOT * 4), b_s = al((size_t)S * 4);
     const size_t b_sg = al((size_t)S * G * 4), b_st = al((size_t)ns * G * 4), b_cs = al((size_t)ns * 4);
-    SGX_TRY(c.split_work.ensure(b_so + b_hp + 2 * b_s + b_sg + 2 * b_st + b_cs));
-    char *x = (char *)c.split_work.p;
+    SGX_TRY(c.split_pad[slot].ensure(b_so + b_hp + 2 * b_s + b_sg + 2 * b_st + b_cs));
+    char *x = (char *)c.split_pad[slot].p;
     uint16_t *stream_of = (uint16_t *)x;
     int32_t *hot_part = (int32_t *)(x += b_so);
     uint32_t *est1 = (uint32_t *)(x += b_hp);
@@ -354,17 +369,20 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
     uint32_t *cnt1 = (uint32_t *)(x += b_sg);
     uint32_t *cur1 = (uint32_t *)(x += b_st);
     uint32_t *capS = (uint32_t *)(x += b_st);
-    HIP_TRY(hipMemsetAsync(c.work.p, 0, work_bytes, st));
-    hipEvent_t h0 = e->ev(), h1 = e->ev(), c1 = e->ev(), x1 = e->ev();
-    HIP_TRY(hipEventRecord(h0, st));
-    HIP_TRY(launch_pad_sample(in, n, 16, pg.stride, s.pp, est, st));
-    HIP_TRY(launch_hot_select(nullptr, R, Q, stream_of, hot_part, st, est));
-    HIP_TRY(launch_pad_caps(est, R, pg.sampled, pg.chunk, G, olim, pcap, fstart, err_pad, st));
-    HIP_TRY(launch_cold_super_est(est, stream_of, S, Q, est1, st));
-    HIP_TRY(launch_pad_caps(est1, S, pg.sampled, pg.chunk, G, olim, cap1, fstart1, err_pad, st));
-    HIP_TRY(launch_hot_cursors(fstart, hot_part, fstart1, cur1, S, G, st, pcap, cap1, capS));
-    SGX_TRY(debug_sync(e, st, "padded split: sample / selection / capacities"));
-    HIP_TRY(hipEventRecord(h1, st));
+    hipEvent_t h0 = e->ev(), h1 = e->ev(), l0 = e->ev(), c1 = e->ev(), x1 = e->ev();
+    HIP_TRY(hipEventRecord(h0, pre));
+    HIP_TRY(hipMemsetAsync(w, 0, work_bytes, pre));
+    HIP_TRY(launch_pad_sample(in, n, 16, pg.stride, s.pp, est, pre));
+    HIP_TRY(launch_hot_select(nullptr, R, Q, stream_of, hot_part, pre, est));
+    HIP_TRY(launch_pad_caps(est, R, pg.sampled, pg.chunk, G, olim, pcap, fstart, err_pad, pre));
+    HIP_TRY(launch_cold_super_est(est, stream_of, S, Q, est1, pre));
+    HIP_TRY(launch_pad_caps(est1, S, pg.sampled, pg.chunk, G, olim, cap1, fstart1, err_pad, pre));
+    HIP_TRY(launch_hot_cursors(fstart, hot_part, fstart1, cur1, S, G, pre, pcap, cap1, capS));
+    SGX_TRY(debug_sync(e, pre, "padded split: sample / selection / capacities"));
+    HIP_TRY(hipEventRecord(h1, pre));
+    HIP_TRY(c.pre_done[slot].record(pre));
+    HIP_TRY(hipStreamWaitEvent(st, c.pre_done[slot].ev, 0));
+    HIP_TRY(hipEventRecord(l0, st));
     PartParams p1 = s.pp;
     p1.kind = KIND_HOT_SPLIT;
     p1.R = (uint32_t)(HOT + S);
@@ -379,7 +397,7 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
     SGX_TRY(debug_sync(e, st, "K4 padded split level 1"));
     // level 2: a workgroup per (group of `pack` supers, chunk), its 64 pack streams the
     // group's partitions (pid & (64 pack - 1)), the group's fragments of that chunk read back to
-    // back (DESIGN.md §6.3)
+    // back (DESIGN.md §6.2)
     const int pack = std::min<int>(S, (int)SPLIT_PACK_MAX);
     const ScatterGeom geo2 = scatter_geom16_wc((uint32_t)(Q * pack));
     PartParams p2 = s.pp;
@@ -398,20 +416,26 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
     SGX_TRY(debug_sync(e, st, "K4 padded split level 2"));
     HIP_TRY(launch_hot_counts(cnt1, hot_part, G, cnt, st));
     HIP_TRY(hipEventRecord(c1, st));
-    HIP_TRY(launch_scan(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, st));
-    // the two-pass fallback, each kernel a no-op unless *err_pad has PAD_OVERFLOW
+    // the tail on the second stream, behind level 2 (it runs beside the next write's sample and
+    // cut): K3 over the final counts, then the two-pass fallback, each kernel a no-op unless
+    // *err_pad has PAD_OVERFLOW, and the offsets to the host
+    hipStream_t tl = c.st_tail;
+    HIP_TRY(hipStreamWaitEvent(tl, c1, 0));
+    HIP_TRY(launch_scan(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, tl));
     PartParams fp = s.pp;
     fp.guard = err_pad;
-    HIP_TRY(launch_hist(in, n, 16, chunk_fb, G_fb, fp, counts_fb, st, e->hist_mode, true));
-    HIP_TRY(launch_scan(counts_fb, (uint32_t *)c.offs.p, len_fb, status_fb, ticket_fb, err, part_off_dev, G_fb, R, st,
-                        err_pad));
+    uint32_t *offs_fb = (uint32_t *)c.pad_offs[slot].p;
+    HIP_TRY(launch_hist(in, n, 16, chunk_fb, G_fb, fp, counts_fb, tl, e->hist_mode, true));
+    HIP_TRY(launch_scan(counts_fb, offs_fb, len_fb, status_fb, ticket_fb, err, part_off_dev, G_fb, R, tl, err_pad));
     fp.mbits = (uint32_t)gfb.mbits;
-    HIP_TRY(launch_scatter(in, m.data.p, n, 16, chunk_fb, G_fb, fp, (const uint32_t *)c.offs.p, gfb, err, st));
-    SGX_TRY(debug_sync(e, st, "padded split scan / fallback"));
-    HIP_TRY(hipEventRecord(x1, st));
-    HIP_TRY(hipMemcpyAsync(m.part_off.p, part_off_dev, (size_t)(R + 3) * 4, hipMemcpyDeviceToHost, st));
+    HIP_TRY(launch_scatter(in, m.data.p, n, 16, chunk_fb, G_fb, fp, offs_fb, gfb, err, tl));
+    SGX_TRY(debug_sync(e, tl, "padded split scan / fallback"));
+    HIP_TRY(hipEventRecord(x1, tl));
+    HIP_TRY(hipMemcpyAsync(m.part_off.p, part_off_dev, (size_t)(R + 3) * 4, hipMemcpyDeviceToHost, tl));
+    HIP_TRY(c.pad_done[slot].record(tl));
+    c.tail_slot = slot;
     e->record_stage(SGX_STAGE_HIST, h0, h1);
-    e->record_stage(SGX_STAGE_SCATTER, h1, c1);
+    e->record_stage(SGX_STAGE_SCATTER, l0, c1);
     e->record_stage(SGX_STAGE_SCAN, c1, x1);
     m.pad_try = true;
     m.frag_G = G;
@@ -719,8 +743,8 @@ static int run_map_pipeline(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const 
             SGX_TRY(padded_split_pass(e, c, s, m, in, n, pg));
         } else {
             SGX_TRY(padded_pass(e, c, s, m, in, n, pg, ct));
-            tail = c.tail_slot;
         }
+        tail = c.tail_slot;
         rec_off_dev = c.last_off_dev;
     } else if (!partitioned) {
         m.nrec = n;
@@ -909,7 +933,7 @@ extern "C" int sgx_write_map(sgx_engine *e, int32_t shuffle_id, int64_t map_id, 
 // ------------------------------------------------------------------------------------
 // streaming map outputs
 // ------------------------------------------------------------------------------------
-// Deferred batches (DESIGN.md §16): sgx_map_append only lands the batch in HBM (a host batch
+// Deferred batches (DESIGN.md §7): sgx_map_append only lands the batch in HBM (a host batch
 // through PCIe, a device batch copied, a retained device batch not at all) and the commit
 // partitions every batch in ONE pass, with a chunk table in place of a contiguous input --
 // the padded single-pass write where sgx_write_map would take it, else the two-pass one.  The
@@ -1083,7 +1107,7 @@ extern "C" int sgx_map_append(sgx_engine *e, int32_t shuffle_id, int64_t map_id,
                     c->host_slot ^= 1;
                     HIP_TRY(c->host_up[slot].wait_host());
                     SGX_TRY(c->host_stage[slot].ensure(piece));
-                    std::memcpy(c->host_stage[slot].p, (const char *)records + off, piece);
+                    host_copy_parallel((char *)c->host_stage[slot].p, (const char *)records + off, piece);
                     HIP_TRY(hipMemcpyAsync(dst + off, c->host_stage[slot].p, piece, hipMemcpyHostToDevice, c->st));
                     HIP_TRY(c->host_up[slot].record(c->st));
                 }

@@ -1,6 +1,6 @@
 // sgx_range.cpp — RangePartitioner's bounds from the data (Spark 3.0.1 RangePartitioner:
 // the rangeBounds initialiser, sketch and determineBounds; restated, see include/sgx.h and
-// DESIGN.md §10): GPU reservoir sampling with Spark's seeds + determineBounds on the host.
+// DESIGN.md §16): GPU reservoir sampling with Spark's seeds + determineBounds on the host.
 #include "sgx_engine.h"
 
 #include <algorithm>

@@ -111,7 +111,7 @@ __global__ __launch_bounds__(TS_THREADS) void k_tile_scan64(const uint32_t *__re
     if (tid == 0) btot[blockIdx.x] = tot;
 }
 
-// The map's partitioned records: contiguous, or (a padded map, DESIGN.md §7) the fragments
+// The map's partitioned records: contiguous, or (a padded map, DESIGN.md §6.1) the fragments
 // (p, g) = [fstart, + cnt) of the padded buffer in (p, g) order, foff their contiguous
 // positions -- unless the padded write overflowed (*ovf & PAD_OVERFLOW: its fallback rewrote
 // the map contiguously).  k_tile_frags first stores every tile's first fragment (one pass over

@@ -457,12 +457,15 @@ class ShuffleEngine:
         return dst
 
     def read_grouped(self, shuffle_id: int, map_ids: Sequence[int], start_partition: int, end_partition: int,
-                     agg: int = _lib.AGG_GROUP, device: bool = False):
+                     agg: int = _lib.AGG_GROUP, device: bool = False, out=None):
         """UcxShuffleReader.read with an aggregator on (Long, Long) records.  AGG_GROUP ->
         (keys, group_starts, values); AGG_SUM -> (keys, sums).  Keys ascending per reducer,
         values in canonical arrival order.  Host int64 arrays, or DeviceBuffers of int64 left
-        in HBM with ``device=True`` (the caller frees them).  The size query computes the
-        result and the filling call reuses it (one fetch + sort + group per read)."""
+        in HBM with ``device=True`` (the caller frees them).  ``out``: host int64 arrays
+        (keys, group_starts or None, values) to fill instead of fresh ones -- as the JVM reader
+        reuses its direct buffers -- at least as long as the result; the returned arrays are
+        views of them.  The size query computes the result and the filling call reuses it (one
+        fetch + sort + group per read)."""
         m = np.ascontiguousarray(map_ids, dtype=np.int64)
         ng, nv = ctypes.c_int64(0), ctypes.c_int64(0)
         check(lib().sgx_read_grouped(self.handle, shuffle_id, m.ctypes.data, len(m), start_partition, end_partition,
@@ -474,6 +477,15 @@ class ShuffleEngine:
             keys, vals = self.alloc(max(G, 1) * 8), self.alloc(max(V, 1) * 8)
             starts = self.alloc(max(G, 1) * 8) if group else None
             ptrs, kind = (keys.ptr, starts.ptr if group else None, vals.ptr), MEM_DEVICE
+        elif out is not None:
+            keys, vals = out[0][:G], out[2][:V]
+            starts = out[1][:G] if group else None
+            for a in (keys, starts, vals):
+                if a is not None and (a.dtype != np.int64 or not a.flags["C_CONTIGUOUS"]):
+                    raise ValueError("out arrays must be C-contiguous int64")
+            if len(keys) < G or len(vals) < V or (group and len(starts) < G):
+                raise ValueError("out arrays are shorter than the result")
+            ptrs, kind = (keys.ctypes.data, starts.ctypes.data if group else None, vals.ctypes.data), MEM_HOST
         else:
             keys, vals = np.empty(G, dtype=np.int64), np.empty(V, dtype=np.int64)
             starts = np.empty(G, dtype=np.int64) if group else None

@@ -265,7 +265,7 @@ def test_large_r_shapes(sgx_lib, oracle_lib, R, shape):
     partition (every chunk sees a different narrow band of partitions); only the first and
     last partitions; one hot partition holding half the records -- over several chunk
     counts and a ragged size, bit-exact against the oracle.  (These shapes were written
-    for the split write-combining K4 that was measured and rejected, DESIGN.md §6.3; they
+    for the split write-combining K4 that was measured and rejected, DESIGN.md §6.2; they
     run the lane-ordered kernel.)"""
     n = 700_001
     recs = oracle_lib.gen_uniform16(n, 0x5917 + R)

@@ -6,7 +6,7 @@ answers and to each other.  GPU tests compare the HIP path, through the C ABI, w
 oracle and the golden fixtures byte for byte: partition lengths (= index offsets), the
 partition-contiguous Kryo stream, the index and data files, fetched blocks, and the
 decoded records / sorted / grouped reads of a Kryo shuffle against the fixed-codec ones.
-Parity against a JVM is unpinned (no JVM here; DESIGN.md §11)."""
+Parity against a JVM is unpinned (no JVM here; DESIGN.md §10)."""
 import glob
 import json
 import os
@@ -302,7 +302,7 @@ def test_varlong_pinned_to_protobuf_sint64():
 @pytest.mark.parametrize("R,shape", [(1024, "uniform"), (200, "uniform"), (4096, "uniform"), (1024, "overflow"),
                                      (64, "lz4"), (2, "uniform"), (1024, "tiny"), (1024, "zipf"), (4096, "zipf")])
 def test_gpu_kryo_padded_write(sgx_lib, oracle_lib, R, shape):
-    """A Kryo shuffle's map written padded (DESIGN.md §7): the serializer reads the records
+    """A Kryo shuffle's map written padded (DESIGN.md §6.1): the serializer reads the records
     through the fragment table and publishes the same stream, lengths, blocks and LZ4 frames
     as the two-pass write; keys the sample misses ("overflow") overflow a sub-bin and the
     serializer reads the fallback's contiguous records; R = 4096 goes through the padded split."""

@@ -1,4 +1,4 @@
-"""GPU parity of the single-pass padded map write (DESIGN.md §7, sgx_map_layout).
+"""GPU parity of the single-pass padded map write (DESIGN.md §6.1, sgx_map_layout).
 
 The padded write replaces the map side's full histogram by a sampled one: every
 (partition, chunk) stream is written into a sub-bin sized from the sample, and the streams'

@@ -409,7 +409,7 @@ def test_sorted_bucket_path(sgx_lib, oracle_lib, flags, case):
 @pytest.mark.parametrize("case", ["pieces", "subrange", "many_pieces", "grouped_sum", "empty_partitions"])
 def test_sorted_segmented_window(sgx_lib, oracle_lib, flags, case):
     """The sorted read's segmented window pass (one stable pass by the key window inside every
-    partition's segment of the gathered records, DESIGN.md §11) against the oracle, and the
+    partition's segment of the gathered records, DESIGN.md §10) against the oracle, and the
     LSD form it replaces (SGX_FLAG_NO_SEG_WINDOW = 1024): partitions of several 2^17-record
     pieces, a sub-range of reducers, two partitions of ten pieces each, reduceByKey sums, and
     empty partitions between full ones."""

@@ -1,4 +1,4 @@
-"""GPU parity of the one-pass streaming commit (DESIGN.md §16): sgx_map_append only lands each
+"""GPU parity of the one-pass streaming commit (DESIGN.md §7): sgx_map_append only lands each
 batch in HBM (host batches through PCIe, device batches copied, SGX_MEM_DEVICE_RETAINED batches
 read in place) and sgx_map_commit partitions every batch in one pass through a chunk table --
 the padded single-pass write when sgx_write_map would take it, else the two-pass write.  The

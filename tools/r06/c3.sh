@@ -13,7 +13,7 @@ step() {
   if [ $rc -ne 0 ]; then echo "step $log: rc $rc"; tail -40 "$out/$log"; exit $rc; fi
   return 0
 }
-step 600 pytest_split.log python -u -m pytest tests/test_padded.py tests/test_gpu_parity.py -q -x --timeout 120 --timeout-method thread -p no:cacheprovider -k "4096 or 2048 or zipf or split or 8192 or 6144 or padded"
+step 600 pytest_split.log python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread -p no:cacheprovider -k "4096 or 2048 or zipf or split or 8192 or 6144 or padded"
 tail -2 "$out/pytest_split.log"
 step 300 bench_c3.log python -u bench.py --workload c3 --no-cpu-baseline --no-live-pmc --steps 20
 grep '^{' "$out/bench_c3.log" | python3 -c "

@@ -12,7 +12,7 @@ coalesced stream on gfx950, so it is doubled; WRITE_SIZE (KiB) is taken as is.  
 is every kernel of the write except the input generator, per write (calls / iters).
 
 usage: summarize_prof.py <tag> <out_dir of gpu_prof.sh> <records> <R> <dist> [record_bytes] [layout]
-layout: padded (the default map write, DESIGN §7) or twopass (--flags 256); pmc_map.json keys
+layout: padded (the default map write, DESIGN §6.1) or twopass (--flags 256); pmc_map.json keys
 a two-pass profile with the suffix "_twopass" (bench.py --no-padded reads that one).
 """
 import csv
