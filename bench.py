@@ -92,6 +92,10 @@ def parse():
                     help="N > 1 / --self-exchange: move the exchange's bytes by RCCL send / recv (or the host "
                          "all-to-all) over contiguous map outputs, with two-pass map writes, instead of the "
                          "direct peer gather out of single-pass padded maps (A/B, DESIGN.md §8)")
+    ap.add_argument("--overlap-writes", action="store_true",
+                    help="SGX_FLAG_OVERLAP_WRITES: consecutive map writes on two alternating streams, so one "
+                         "write's K4 starts on the CUs the previous one's last workgroups free (more map "
+                         "throughput; the K4 roofline's per-launch interval then includes that overlap)")
     a = ap.parse_args()
     a.record_bytes = 100 if a.workload == "c4" else 16
     a.records = a.records or (1 << 25 if a.workload == "c4" else 1 << 28)
@@ -328,7 +332,8 @@ def main():
     eng = sgx.ShuffleEngine(device=device, num_chunks=args.num_chunks,
                             flags=(sgx.FLAG_NO_SPLIT_SCATTER if args.no_split else 0) |
                             (sgx.FLAG_NO_PADDED_MAP if args.no_padded else 0) |
-                            (sgx.FLAG_NO_P2P_EXCHANGE if args.no_p2p else 0))
+                            (sgx.FLAG_NO_P2P_EXCHANGE if args.no_p2p else 0) |
+                            (sgx.FLAG_OVERLAP_WRITES if args.overlap_writes else 0))
     self_x = args.self_exchange and world == 1
     if world > 1 and args.comm == "host":
         eng.comm_init_host(world, rank)
@@ -534,7 +539,8 @@ def main():
                                      "streams' counts)" if padded else "contiguous (two-pass: K1+K2 histogram, K3, K4)",
                        "parallelism": f"dp{world} (map shards per GPU, reducers owned "
                                       + ("floor(r*P/R))" if args.placement == "even" else "in byte-balanced ranges)"),
-                       "exchange": _exchange_name(args, world, self_x)},
+                       "exchange": _exchange_name(args, world, self_x),
+                       "overlap_writes": bool(args.overlap_writes)},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": k4_pmc.get("hbm_bytes_per_launch"),

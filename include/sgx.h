@@ -89,11 +89,17 @@ enum sgx_flags {
     SGX_FLAG_NO_DEFERRED_APPEND = 2048, /* streaming maps: partition every sgx_map_append batch on
                                          arrival and gather them at the commit (the round-4 form)
                                          instead of one pass over all batches at the commit    */
-    SGX_FLAG_NO_P2P_EXCHANGE = 4096   /* exchange rounds move their bytes by grouped
+    SGX_FLAG_NO_P2P_EXCHANGE = 4096,  /* exchange rounds move their bytes by grouped
                                          ncclSend / ncclRecv (RCCL) or the host all-to-all over
                                          contiguous map outputs, and a communicator keeps the
                                          map side two-pass; default: the direct peer gather
                                          (sgx_exchange) out of single-pass padded maps         */
+    SGX_FLAG_OVERLAP_WRITES = 8192    /* consecutive padded writes of a calling thread run on two
+                                         alternating streams, so a write's sample and K4 start
+                                         on the CUs the previous write's last K4 workgroups
+                                         free (+1.3-1.8 % map throughput at C1 / C4); per-kernel
+                                         durations then include that overlap, so the default
+                                         keeps writes on one stream                            */
 };
 
 typedef struct sgx_config {

@@ -536,7 +536,6 @@ static int padded_pass_wide(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const 
 // word and the padded flag word land in m.part_off.
 static int padded_pass16(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const void *in, int64_t n, const PadGeom &pg,
                          const ChunkTable *ct) {
-    hipStream_t st = c.st;
     const int rb = s.rb;  // 16, or 100 (TeraSort's write-combining K4: wide_wc_padded_ok)
     const int32_t R = s.R;
     const int G = pg.G;
@@ -547,6 +546,23 @@ static int padded_pass16(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const voi
     // rest of the slot is the tail stream's own (in order)
     const int slot = c.pad_slot;
     c.pad_slot ^= 1;
+    // SGX_FLAG_OVERLAP_WRITES: consecutive writes alternate between two streams (slot 1 on the
+    // pre stream, which the R > 1024 split uses for its front), so a write's sample and K4 start
+    // on the CUs the previous write's last K4 workgroups leave, instead of behind its whole
+    // grid (C1 1.794 -> 1.772 ms per write, C4 1.663 -> 1.634, profiles/r06/r06w_*; kernel
+    // traces then time a K4 from its dispatch, waiting included: r06x).  A write on the pre
+    // stream waits for what the call put on the main stream for it: the input's staging copy
+    // and the all-to-all still reading the map's old bytes (a streaming commit's landing
+    // copies: the whole main stream).
+    hipStream_t st = c.st;
+    if ((e->flags & SGX_FLAG_OVERLAP_WRITES) && slot == 1) {
+        st = c.st_pre;
+        if (ct || in == c.input_stage.p) {
+            HIP_TRY(c.pre_in.record(c.st));
+            HIP_TRY(hipStreamWaitEvent(st, c.pre_in.ev, 0));
+        }
+        if (m.read_done.ev) HIP_TRY(hipStreamWaitEvent(st, m.read_done.ev, 0));
+    }
     if (c.pad_free[slot].ev) HIP_TRY(hipStreamWaitEvent(st, c.pad_free[slot].ev, 0));
     SGX_TRY(m.data.ensure((size_t)olim * (size_t)rb));
     SGX_TRY(m.frag.ensure((size_t)len * 12 + 16));

@@ -410,3 +410,40 @@ def test_full_c1_padded_fetch_bit_exact(sgx_lib, engine, oracle_lib):
     del recs
     assert np.array_equal(lengths, counts * 16)
     assert np.array_equal(got, want.reshape(-1))
+
+
+@pytest.mark.parametrize("overlap", [False, True])
+@pytest.mark.parametrize("R", [1024, 4096])
+def test_back_to_back_async_writes(sgx_lib, oracle_lib, R, overlap):
+    """Asynchronous writes issued back to back from one thread (the
+    tail on a second stream, the split's front on a third; with SGX_FLAG_OVERLAP_WRITES
+    consecutive writes also alternate between two streams): host and device inputs mixed, a
+    map id written twice (the second attempt wins), every map checked after one sync."""
+    n = 300_007
+    sid = next_sid()
+    pad_engine = sgx_lib.ShuffleEngine(
+        device=0, flags=sgx_lib.FLAG_PAD_ANY_SIZE | (sgx_lib.FLAG_OVERLAP_WRITES if overlap else 0))
+    pad_engine.register_shuffle(sid, R)
+    bufs = []
+    try:
+        want = {}
+        plan = [(0, "host"), (1, "dev"), (2, "host"), (0, "dev"), (3, "dev"), (4, "host")]
+        for k, (mid, kind) in enumerate(plan):
+            recs = oracle_lib.gen_zipf16(n, 0x7A0 + k, oracle_lib.zipf_cdf(1.1, 1 << 16)) if k % 2 else \
+                oracle_lib.gen_uniform16(n, 0x7A0 + k)
+            if kind == "dev":
+                b = pad_engine.alloc(recs.nbytes)
+                b.copy_from(recs)
+                bufs.append(b)  # kept alive until the writes have run
+                pad_engine.write_map(sid, mid, b, n, 16)
+            else:
+                pad_engine.write_map(sid, mid, recs, n, 16)
+            want[mid] = recs
+        pad_engine.sync()
+        for mid, recs in want.items():
+            check_map(pad_engine, oracle_lib, recs, R, sid, mid, sgx_lib.LAYOUT_PADDED)
+    finally:
+        pad_engine.unregister_shuffle(sid)
+        for b in bufs:
+            b.free()
+        pad_engine.close()
