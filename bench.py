@@ -92,10 +92,13 @@ def parse():
                     help="N > 1 / --self-exchange: move the exchange's bytes by RCCL send / recv (or the host "
                          "all-to-all) over contiguous map outputs, with two-pass map writes, instead of the "
                          "direct peer gather out of single-pass padded maps (A/B, DESIGN.md §8)")
-    ap.add_argument("--overlap-writes", action="store_true",
-                    help="SGX_FLAG_OVERLAP_WRITES: consecutive map writes on two alternating streams, so one "
-                         "write's K4 starts on the CUs the previous one's last workgroups free (more map "
-                         "throughput; the K4 roofline's per-launch interval then includes that overlap)")
+    ap.add_argument("--no-overlap-writes", action="store_true",
+                    help="SGX_FLAG_NO_OVERLAP_WRITES: every map write on one stream (default: consecutive "
+                         "writes alternate between two streams, so one write's K4 starts on the CUs the "
+                         "previous one's last workgroups free)")
+    ap.add_argument("--roofline-steps", type=int, default=5,
+                    help="with overlapping writes: K4 launches timed after the timed region with overlap off, "
+                         "for the roofline object (an overlapped launch's interval includes its wait for CUs)")
     a = ap.parse_args()
     a.record_bytes = 100 if a.workload == "c4" else 16
     a.records = a.records or (1 << 25 if a.workload == "c4" else 1 << 28)
@@ -333,7 +336,7 @@ def main():
                             flags=(sgx.FLAG_NO_SPLIT_SCATTER if args.no_split else 0) |
                             (sgx.FLAG_NO_PADDED_MAP if args.no_padded else 0) |
                             (sgx.FLAG_NO_P2P_EXCHANGE if args.no_p2p else 0) |
-                            (sgx.FLAG_OVERLAP_WRITES if args.overlap_writes else 0))
+                            (sgx.FLAG_NO_OVERLAP_WRITES if args.no_overlap_writes else 0))
     self_x = args.self_exchange and world == 1
     if world > 1 and args.comm == "host":
         eng.comm_init_host(world, rank)
@@ -449,6 +452,22 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     st = eng.stats()
+    # The K4 roofline from launches that do not overlap.  With overlapping writes
+    # (the engine's default) a K4 is dispatched while the previous one's last workgroups still
+    # run, so its HIP-event interval -- and its rocprofv3 duration -- include the wait for their
+    # CUs: the timed region gives the throughput, these launches the kernel's own time.
+    k4_alone = None
+    if (not args.no_overlap_writes and world == 1 and not self_x and tasks == 1 and args.roofline_steps > 0
+            and args.serializer == "fixed"):
+        eng.set_overlap_writes(False)
+        run(2)
+        barrier()
+        eng.stats_reset()
+        run(args.roofline_steps)
+        barrier()
+        st_alone = eng.stats()
+        eng.set_overlap_writes(True)
+        k4_alone = st_alone.ms["scatter"] / max(1, st_alone.count["scatter"])
 
     verified = None
     lens = eng.map_lengths(sid, rank, R)
@@ -499,7 +518,8 @@ def main():
         ms_per_step = dt * 1e3 / args.steps
         total_bytes = float(rb) * n * world * args.steps
         value = total_bytes / dt / 1e9
-        sc_ms = st.ms["scatter"] / max(1, st.count["scatter"])
+        sc_ms_timed = st.ms["scatter"] / max(1, st.count["scatter"])
+        sc_ms = k4_alone if k4_alone is not None else sc_ms_timed
         algo = 2 * rb  # the record read once and written once
         achieved = algo * n / (sc_ms * 1e-3) / 1e9
         padded = layout in (sgx.LAYOUT_PADDED, sgx.LAYOUT_SERIALIZED_PADDED)
@@ -540,12 +560,17 @@ def main():
                        "parallelism": f"dp{world} (map shards per GPU, reducers owned "
                                       + ("floor(r*P/R))" if args.placement == "even" else "in byte-balanced ranges)"),
                        "exchange": _exchange_name(args, world, self_x),
-                       "overlap_writes": bool(args.overlap_writes)},
+                       "overlap_writes": not args.no_overlap_writes},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": k4_pmc.get("hbm_bytes_per_launch"),
                          "kernel": k4_pmc.get("kernel", "K4 scatter"), "algo_bytes_per_record": algo,
-                         "traffic_source": pmc.get("source")},
+                         "traffic_source": pmc.get("source"),
+                         "launch_ms": round(sc_ms, 4),
+                         "launch_ms_source": (f"{args.roofline_steps} K4 launches right after the timed region, "
+                                              "overlapping writes off (HIP events on K4's stream)")
+                         if k4_alone is not None else "the timed region's K4 launches (HIP events on K4's stream)",
+                         "timed_region_k4_interval_ms": round(sc_ms_timed, 4)},
             # the whole map side (K1+K2 histogram, K3 scan, K4 scatter, their memsets) against
             # the same 32 B/record: what north_star's partition+scatter target is quoted on
             "roofline_map_side": {"bound": "hbm", "achieved": round(side_ach, 1), "peak": HBM_PEAK_GBS,

@@ -94,12 +94,11 @@ enum sgx_flags {
                                          contiguous map outputs, and a communicator keeps the
                                          map side two-pass; default: the direct peer gather
                                          (sgx_exchange) out of single-pass padded maps         */
-    SGX_FLAG_OVERLAP_WRITES = 8192    /* consecutive padded writes of a calling thread run on two
-                                         alternating streams, so a write's sample and K4 start
-                                         on the CUs the previous write's last K4 workgroups
-                                         free (+1.3-1.8 % map throughput at C1 / C4); per-kernel
-                                         durations then include that overlap, so the default
-                                         keeps writes on one stream                            */
+    SGX_FLAG_NO_OVERLAP_WRITES = 8192 /* keep every padded write of a calling thread on one
+                                         stream; default: consecutive writes alternate between
+                                         two streams, so a write's sample and K4 start on the
+                                         CUs the previous write's last K4 workgroups free (see
+                                         sgx_set_overlap_writes)                              */
 };
 
 typedef struct sgx_config {
@@ -114,6 +113,14 @@ typedef struct sgx_config {
                                 aborts the communicator and fails with SGX_ERR_TIMEOUT
                                 instead of spinning forever (UcxShuffleClient.scala:44-46) */
 } sgx_config;
+
+/* Overlapping consecutive map writes (default on; SGX_FLAG_NO_OVERLAP_WRITES at creation, or
+ * this call at any time, from the next write on): a calling thread's padded writes alternate
+ * between two streams, so the next write's sample and K4 fill the CUs the previous K4's last
+ * workgroups leave idle (map throughput +1.3 % to +8 % at C1, by box).  With
+ * it on, a K4's HIP-event interval or traced duration starts at its dispatch and includes the
+ * wait for those CUs, so kernel-alone timings are taken with it off (bench.py's roofline). */
+int sgx_set_overlap_writes(sgx_engine *e, int32_t on);
 
 /* ---- engine lifetime: replaces CommonUcxShuffleManager.startUcxTransport
  *      (shuffle/ucx/CommonUcxShuffleManager.scala:67-100) and stop() (:111-124) ---- */

@@ -36,7 +36,7 @@ FLAG_PAD_ANY_SIZE = 512
 FLAG_NO_SEG_WINDOW = 1024
 FLAG_NO_DEFERRED_APPEND = 2048
 FLAG_NO_P2P_EXCHANGE = 4096
-FLAG_OVERLAP_WRITES = 8192
+FLAG_NO_OVERLAP_WRITES = 8192
 LAYOUT_CONTIGUOUS, LAYOUT_PADDED, LAYOUT_SERIALIZED_PADDED = 0, 1, 2
 PLACE_EVEN, PLACE_BYTES = 0, 1
 WRITER_SORT, WRITER_UNSAFE = 0, 1
@@ -151,6 +151,7 @@ SIGNATURES = {
     "sgx_stats_reset": (ctypes.c_int, [_vp]),
     "sgx_stats_get": (ctypes.c_int, [_vp, _vp, _vp]),
     "sgx_exchange_bytes": (ctypes.c_int, [_vp, _vp]),
+    "sgx_set_overlap_writes": (ctypes.c_int, [_vp, ctypes.c_int32]),
     "sgx_plan_exchange": (ctypes.c_int, [_vp, _i32, _i32, _i32, _i64, _vp, _vp, _vp, _vp, _vp, _P64]),
     "sgx_copy_items": (ctypes.c_int, [_vp, _vp, _vp, _vp, _i64, _i32]),
     "sgx_reducer_owner": (_i32, [_i32, _i32, _i32]),

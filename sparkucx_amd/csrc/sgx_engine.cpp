@@ -220,6 +220,7 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
         e->rank_mode = cfg->rank_mode;
         e->flags = cfg->flags;
         if (cfg->flags & SGX_FLAG_PAD_ANY_SIZE) e->pad_min = 1;
+        if (cfg->flags & SGX_FLAG_NO_OVERLAP_WRITES) e->overlap_writes = false;
         if (cfg->comm_timeout_ms > 0) e->comm_timeout_ms = cfg->comm_timeout_ms;
     }
     HIP_TRY(hipStreamCreateWithFlags(&e->s_comm, hipStreamNonBlocking));
@@ -455,6 +456,12 @@ extern "C" int sgx_set_reducer_placement(sgx_engine *e, int32_t shuffle_id, int3
     if (!s->place_bounds.empty())  // a reducer's blocks must all land on one rank
         return fail_msg(SGX_ERR_STATE, "shuffle %d was already exchanged: its reducer ranges are fixed", shuffle_id);
     s->placement.store(placement);
+    return SGX_OK;
+}
+
+extern "C" int sgx_set_overlap_writes(sgx_engine *e, int32_t on) {
+    if (!e) return fail_msg(SGX_ERR_INVALID, "engine is NULL");
+    e->overlap_writes = on != 0;
     return SGX_OK;
 }
 

@@ -393,6 +393,8 @@ struct sgx_engine {
     int hist_mode = 0;               // sgx_config.hist_mode
     int rank_mode = 0;               // sgx_config.rank_mode
     int flags = 0;                   // sgx_config.flags
+    // consecutive padded writes of a thread alternate between two streams (sgx_set_overlap_writes)
+    std::atomic<bool> overlap_writes{true};
     bool lds_order_ok = true;        // engine-start check (sgx_create; sgx_lds_order_ok)
     int64_t pad_min = 1 << 20;       // smallest map written padded (SGX_FLAG_PAD_ANY_SIZE: 1)
     int64_t comm_timeout_ms = 300000;

@@ -546,7 +546,8 @@ static int padded_pass16(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const voi
     // rest of the slot is the tail stream's own (in order)
     const int slot = c.pad_slot;
     c.pad_slot ^= 1;
-    // SGX_FLAG_OVERLAP_WRITES: consecutive writes alternate between two streams (slot 1 on the
+    // Overlapping writes (the default; sgx_set_overlap_writes): consecutive writes alternate
+    // between two streams (slot 1 on the
     // pre stream, which the R > 1024 split uses for its front), so a write's sample and K4 start
     // on the CUs the previous write's last K4 workgroups leave, instead of behind its whole
     // grid (C1 1.794 -> 1.772 ms per write, C4 1.663 -> 1.634, profiles/r06/r06w_*; kernel
@@ -555,7 +556,7 @@ static int padded_pass16(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const voi
     // and the all-to-all still reading the map's old bytes (a streaming commit's landing
     // copies: the whole main stream).
     hipStream_t st = c.st;
-    if ((e->flags & SGX_FLAG_OVERLAP_WRITES) && slot == 1) {
+    if (e->overlap_writes.load() && slot == 1) {
         st = c.st_pre;
         if (ct || in == c.input_stage.p) {
             HIP_TRY(c.pre_in.record(c.st));

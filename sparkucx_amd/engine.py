@@ -504,6 +504,11 @@ class ShuffleEngine:
             return keys, starts, vals
         return keys, vals
 
+    def set_overlap_writes(self, on: bool):
+        """sgx_set_overlap_writes: consecutive padded writes of a thread on two alternating
+        streams (the default) or on one (kernel-alone timings)."""
+        check(lib().sgx_set_overlap_writes(self.handle, 1 if on else 0), "set_overlap_writes")
+
     def last_read_records(self) -> int:
         """Records (before any aggregation) the calling thread's last read_records / read_sorted
         / read_grouped consumed -- what the reference's reader counts with incRecordsRead

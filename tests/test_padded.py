@@ -416,13 +416,13 @@ def test_full_c1_padded_fetch_bit_exact(sgx_lib, engine, oracle_lib):
 @pytest.mark.parametrize("R", [1024, 4096])
 def test_back_to_back_async_writes(sgx_lib, oracle_lib, R, overlap):
     """Asynchronous writes issued back to back from one thread (the
-    tail on a second stream, the split's front on a third; with SGX_FLAG_OVERLAP_WRITES
-    consecutive writes also alternate between two streams): host and device inputs mixed, a
+    tail on a second stream, the split's front on a third; by default consecutive writes also
+    alternate between two streams, SGX_FLAG_NO_OVERLAP_WRITES keeps them on one): host and device inputs mixed, a
     map id written twice (the second attempt wins), every map checked after one sync."""
     n = 300_007
     sid = next_sid()
     pad_engine = sgx_lib.ShuffleEngine(
-        device=0, flags=sgx_lib.FLAG_PAD_ANY_SIZE | (sgx_lib.FLAG_OVERLAP_WRITES if overlap else 0))
+        device=0, flags=sgx_lib.FLAG_PAD_ANY_SIZE | (0 if overlap else sgx_lib.FLAG_NO_OVERLAP_WRITES))
     pad_engine.register_shuffle(sid, R)
     bufs = []
     try:
