@@ -29,7 +29,9 @@ def main():
 
     import sparkucx_amd as sgx
 
-    e = sgx.ShuffleEngine(0, a.num_chunks, flags=a.flags)
+    # kernel profiles are of kernels alone: consecutive writes on one stream (overlapping writes
+    # make a K4's traced duration include its wait for the previous K4's CUs)
+    e = sgx.ShuffleEngine(0, a.num_chunks, flags=a.flags | sgx.FLAG_NO_OVERLAP_WRITES)
     buf = e.alloc(a.records * a.record_bytes)
     if a.record_bytes == 100:
         e.gen_terasort100(buf, a.records, 0x5EEDC0DE)
