@@ -1,7 +1,9 @@
 #!/bin/bash
-# Round-6 validation, part B: rocprofv3 kernel trace of the default bench (and its steady-state
-# map side, tools/trace_steady.py), of the C3 and C4 lines, and the PMC passes
-# (tools/gpu_prof.sh: FETCH_SIZE and WRITE_SIZE in separate runs) for C1, TeraSort and C3.
+# Round-6 validation, part C: rocprofv3 kernel traces of the default bench (overlapping writes:
+# its timed K4s include their wait for CUs, its roofline phase does not), of the same without
+# overlap (and its steady-state map side, tools/trace_steady.py), of the C3 and C4 lines, and
+# the PMC passes (tools/gpu_prof.sh over tools/prof_map.py, writes on one stream: FETCH_SIZE and
+# WRITE_SIZE in separate runs) for C1, TeraSort and C3.
 tag=${1:-r06v}
 out=$GRAFT_REPO_ROOT/gpurun_out/$tag
 mkdir -p "$out"
@@ -14,6 +16,8 @@ step() {
   return 0
 }
 step 300 bench_kt.log rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt" -o run -- python3 bench.py --steps 10 --no-cpu-baseline --no-live-pmc
+step 300 bench_kt_noov.log rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt_noov" -o run -- python3 bench.py --steps 10 --no-cpu-baseline --no-live-pmc --no-overlap-writes
+python3 tools/trace_steady.py "$out/kt_noov/run_kernel_trace.csv" --warmup 3 --out "$out/trace_steady_noov.json"
 step 300 bench_kt_c3.log rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt_c3" -o run -- python3 bench.py --workload c3 --steps 10 --no-cpu-baseline --no-live-pmc
 step 300 bench_kt_c4.log rocprofv3 --kernel-trace --stats --output-format csv -d "$out/kt_c4" -o run -- python3 bench.py --workload c4 --steps 10 --no-cpu-baseline --no-live-pmc
 bash tools/gpu_prof.sh $tag/prof_c1 || exit 1
