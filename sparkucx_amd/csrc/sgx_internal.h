@@ -157,7 +157,12 @@ int64_t scan_tiles(int64_t len);
 // padded write's tail runs it while the next map's K4 holds every CU's LDS, so its workgroups
 // share CUs with that K4 instead of holding back some of its workgroups.
 hipError_t launch_scan_wave(const uint32_t *counts, uint32_t *offs, int64_t len, uint64_t *status, uint32_t *ticket,
-                            uint32_t *err, uint32_t *part_off, int G, int R, hipStream_t stream);
+                            uint32_t *err, uint32_t *part_off, int G, int R, hipStream_t stream,
+                            const uint32_t *guard = nullptr);
+// the padded split's overflow fallback histogram: [R][G] counts of a contiguous 16 B input
+// (hash partitioner), no LDS; a no-op unless *guard has PAD_OVERFLOW
+hipError_t launch_hist16_fallback(const void *in, int64_t n, int64_t chunk, int G, const PartParams &pp,
+                                  uint32_t *counts, const uint32_t *guard, hipStream_t stream);
 // Padded map output.  launch_pad_sample: est[p] += records of partition p among
 // every `stride`-th group of 8 records (est zeroed by the caller; hash partitioner over 16 B
 // records, or RangePartitioner over 100 B TeraSort records; R <= 4096).  With a chunk table

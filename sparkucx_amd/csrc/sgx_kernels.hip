@@ -491,9 +491,12 @@ hipError_t launch_scan(const uint32_t *counts, uint32_t *offs, int64_t len, uint
 
 // One wave per tile of SCAN_TILE counts (64 per lane), no LDS: the ticket and the look-back
 // prefix are broadcast by lane shuffles (launch_scan_wave in sgx_internal.h).
+// guard (nullable): a padded write's fallback scan, a no-op unless *guard has PAD_OVERFLOW.
 __global__ __launch_bounds__(64) void k_scan_wave(const uint32_t *__restrict__ in, uint32_t *__restrict__ out,
                                                   int64_t len, uint64_t *status, uint32_t *ticket, uint32_t *err,
-                                                  uint32_t *__restrict__ part_off, int G, int R) {
+                                                  uint32_t *__restrict__ part_off, int G, int R,
+                                                  const uint32_t *guard) {
+    if (guard && !(*guard & PAD_OVERFLOW)) return;  // the whole wave, before its ticket
     constexpr int ITEMS = SCAN_TILE / 64;
     const uint32_t lane = threadIdx.x;
     uint32_t tile = lane == 0 ? atomicAdd(ticket, 1u) : 0u;
@@ -547,10 +550,10 @@ __global__ __launch_bounds__(64) void k_scan_wave(const uint32_t *__restrict__ i
 }
 
 hipError_t launch_scan_wave(const uint32_t *counts, uint32_t *offs, int64_t len, uint64_t *status, uint32_t *ticket,
-                            uint32_t *err, uint32_t *part_off, int G, int R, hipStream_t stream) {
+                            uint32_t *err, uint32_t *part_off, int G, int R, hipStream_t stream, const uint32_t *guard) {
     const int64_t tiles = scan_tiles(len);
     hipLaunchKernelGGL(k_scan_wave, dim3((unsigned)tiles), dim3(64), 0, stream, counts, offs, len, status, ticket, err,
-                       part_off, G, R);
+                       part_off, G, R, guard);
     return hipGetLastError();
 }
 
@@ -3782,6 +3785,40 @@ __global__ __launch_bounds__(256) void k_pad_reset(uint32_t *flags, uint32_t *fl
 
 hipError_t launch_pad_reset(uint32_t *flags, uint32_t *flags_out, uint32_t *est, int R, hipStream_t stream) {
     hipLaunchKernelGGL(k_pad_reset, dim3(1), dim3(256), 0, stream, flags, flags_out, est, R);
+    return hipGetLastError();
+}
+
+// The padded split's overflow fallback histogram (launch_hist16_fallback): the per-(partition,
+// chunk) counts of the map, [R][G], one wave per chunk, ballot-matched partitions and one
+// global atomic per partition present in each 64 records.  No LDS, so like the rest of the
+// split's tail it runs beside the next write's K4s; a no-op unless *guard has PAD_OVERFLOW.
+// (The split cannot take its counts from the padded write as the 16 B path does: an
+// overflowing level-1 sub-bin corrupts the scratch level 2 partitions.)  counts: zeroed.
+template <int KIND>
+__global__ __launch_bounds__(64) void k_hist16_fb(const uint4 *__restrict__ in, int64_t n, int64_t chunk,
+                                                  PartParams pp, uint32_t *counts, int G, const uint32_t *guard) {
+    if (!(*guard & PAD_OVERFLOW)) return;
+    const int g = blockIdx.x;
+    const uint32_t lane = threadIdx.x;
+    const int64_t begin = (int64_t)g * chunk;
+    const int64_t len = min(n, begin + chunk) - begin;
+    for (int64_t i0 = 0; i0 < len; i0 += 64) {
+        const int64_t i = i0 + lane;
+        const bool valid = i < len;
+        const uint4 r = valid ? in[begin + i] : make_uint4(0, 0, 0, 0);
+        const uint32_t p = valid ? pid_of<KIND>(r.x, r.y, r.z, pp) : 0u;
+        const uint64_t peers = match_peers(p, __ballot(valid), pp.nbits);
+        const uint32_t leader = peers ? (uint32_t)__ffsll((unsigned long long)peers) - 1 : 0u;
+        if (valid && lane == leader) atomicAdd(&counts[(int64_t)p * G + g], (uint32_t)__popcll(peers));
+    }
+}
+
+hipError_t launch_hist16_fallback(const void *in, int64_t n, int64_t chunk, int G, const PartParams &pp,
+                                  uint32_t *counts, const uint32_t *guard, hipStream_t stream) {
+    if (n <= 0 || G <= 0) return hipSuccess;
+    if (pp.kind != SGX_PART_HASH || pp.chunks) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_hist16_fb<SGX_PART_HASH>, dim3(G), dim3(64), 0, stream, (const uint4 *)in, n, chunk, pp, counts,
+                       G, guard);
     return hipGetLastError();
 }
 

@@ -321,17 +321,14 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
         HIP_TRY(c.pre_in.record(st));
         HIP_TRY(hipStreamWaitEvent(pre, c.pre_in.ev, 0));
     }
-    // the fallback's own geometry (the single lane-ordered K4)
-    const ScatterGeom gfb = scatter_geom16_ord((uint32_t)R);
-    if (gfb.items == 0) return fail_msg(SGX_ERR_UNSUPPORTED, "no single-pass geometry for R=%d", R);
-    int64_t chunk_fb = (n + e->G - 1) / e->G;
-    chunk_fb = (chunk_fb + gfb.tile - 1) / gfb.tile * gfb.tile;
+    // the fallback's chunks (one wave each: the zero-LDS histogram and scatter)
+    const int64_t chunk_fb = std::max<int64_t>(1, (n + e->G - 1) / e->G);
     const int G_fb = (int)((n + chunk_fb - 1) / chunk_fb);
     const int64_t len_fb = (int64_t)R * G_fb, tiles_fb = scan_tiles(len_fb);
     SGX_TRY(m.data.ensure((size_t)olim * 16));
     SGX_TRY(m.frag.ensure((size_t)len * 12 + 16));
     uint32_t *fstart = (uint32_t *)m.frag.p, *foff = fstart + len, *cnt = foff + len;
-    SGX_TRY(c.pad_offs[slot].ensure((size_t)len_fb * 4));
+    SGX_TRY(c.pad_offs[slot].ensure((size_t)len_fb * 8));  // the fallback's offsets, then its cursors
     SGX_TRY(c.split_tmp.ensure((size_t)olim * 16));
     // [fallback counts][fallback ticket | status][offsets R+1 | error | padded flags]
     // [padded scan ticket | status][est R][pcap R], one memset
@@ -416,19 +413,18 @@ static int padded_split_pass(sgx_engine *e, Ctx &c, Shuffle &s, MapOut &m, const
     SGX_TRY(debug_sync(e, st, "K4 padded split level 2"));
     HIP_TRY(launch_hot_counts(cnt1, hot_part, G, cnt, st));
     HIP_TRY(hipEventRecord(c1, st));
-    // the tail on the second stream, behind level 2 (it runs beside the next write's sample and
-    // cut): K3 over the final counts, then the two-pass fallback, each kernel a no-op unless
-    // *err_pad has PAD_OVERFLOW, and the offsets to the host
+    // the tail on the second stream, behind level 2: K3 over the final counts (one wave per
+    // tile), then the two-pass fallback -- a histogram, a scan, a scatter, each a no-op unless
+    // *err_pad has PAD_OVERFLOW -- and the offsets to the host.  Every kernel of it is LDS-free,
+    // so it runs beside the next write's level 1 instead of waiting for its CUs
     hipStream_t tl = c.st_tail;
     HIP_TRY(hipStreamWaitEvent(tl, c1, 0));
-    HIP_TRY(launch_scan(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, tl));
-    PartParams fp = s.pp;
-    fp.guard = err_pad;
-    uint32_t *offs_fb = (uint32_t *)c.pad_offs[slot].p;
-    HIP_TRY(launch_hist(in, n, 16, chunk_fb, G_fb, fp, counts_fb, tl, e->hist_mode, true));
-    HIP_TRY(launch_scan(counts_fb, offs_fb, len_fb, status_fb, ticket_fb, err, part_off_dev, G_fb, R, tl, err_pad));
-    fp.mbits = (uint32_t)gfb.mbits;
-    HIP_TRY(launch_scatter(in, m.data.p, n, 16, chunk_fb, G_fb, fp, offs_fb, gfb, err, tl));
+    HIP_TRY(launch_scan_wave(cnt, foff, len, status_pad, ticket_pad, err, part_off_dev, G, R, tl));
+    uint32_t *offs_fb = (uint32_t *)c.pad_offs[slot].p, *cur_fb = offs_fb + len_fb;
+    HIP_TRY(launch_hist16_fallback(in, n, chunk_fb, G_fb, s.pp, counts_fb, err_pad, tl));
+    HIP_TRY(launch_scan_wave(counts_fb, offs_fb, len_fb, status_fb, ticket_fb, err, part_off_dev, G_fb, R, tl,
+                             err_pad));
+    HIP_TRY(launch_scatter16_fallback(in, m.data.p, n, chunk_fb, G_fb, s.pp, offs_fb, cur_fb, err_pad, err, tl, 16));
     SGX_TRY(debug_sync(e, tl, "padded split scan / fallback"));
     HIP_TRY(hipEventRecord(x1, tl));
     HIP_TRY(hipMemcpyAsync(m.part_off.p, part_off_dev, (size_t)(R + 3) * 4, hipMemcpyDeviceToHost, tl));
