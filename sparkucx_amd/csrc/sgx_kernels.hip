@@ -1243,6 +1243,9 @@ __device__ __forceinline__ uint64_t shfl_up64(uint64_t x, int d) {
     return ((uint64_t)hi << 32) | lo;
 }
 
+#ifndef SGX_PAD_CHUNK_MAJOR  // (A/B builds: 0 lays a padded write's sub-bins out partition-major)
+#define SGX_PAD_CHUNK_MAJOR 1
+#endif
 // A padded write's sub-bin layout, computed by each workgroup of its K4 from the sampled counts
 // (PartParams.pad_est; the same numbers k_pad_caps computes for the split): stream (p, g) of
 // this workgroup's chunk g starts at min(pbase[p] + g cap[p], olim) -> pe[p], ple[p] (p < RS,
@@ -1259,7 +1262,7 @@ __device__ void pad_layout_starts(const PartParams &pp, uint32_t R, uint32_t RS,
     for (int k = 0; k < 2; ++k) {
         const uint32_t p = 2 * tid + k;
         cap[k] = p < R ? pad_cap_of(pp.pad_est[p], pp.pad_scale, pp.pad_a) : 0u;
-        sum += (uint64_t)cap[k] * (uint64_t)G;
+        sum += SGX_PAD_CHUNK_MAJOR ? (uint64_t)cap[k] : (uint64_t)cap[k] * (uint64_t)G;
     }
     uint64_t x = sum;  // inclusive scan over the wave, then over the waves' totals
 #pragma unroll
@@ -1276,11 +1279,15 @@ __device__ void pad_layout_starts(const PartParams &pp, uint32_t R, uint32_t RS,
         if (v < (int)w) run += y;
         total += y;
     }
+    // chunk-major (SGX_PAD_CHUNK_MAJOR): chunk g's sub-bins are one region, [g total, (g + 1)
+    // total), partition p's at run_p inside it -- a workgroup's 1024 streams span ~olim / G
+    // records instead of the whole output; partition-major: stream (p, g) at run_p + g cap_p
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
         const uint32_t p = 2 * tid + k;
         if (p < RS) {
-            const uint32_t c0 = p < R ? (uint32_t)min<uint64_t>(run + (uint64_t)g * cap[k], (uint64_t)pp.olim) : 0u;
+            const uint64_t at = SGX_PAD_CHUNK_MAJOR ? (uint64_t)g * total + run : run + (uint64_t)g * cap[k];
+            const uint32_t c0 = p < R ? (uint32_t)min<uint64_t>(at, (uint64_t)pp.olim) : 0u;
             pe[p] = c0;
             ple[p] = c0;
             if (g == 0 && p < R) {
@@ -1288,9 +1295,10 @@ __device__ void pad_layout_starts(const PartParams &pp, uint32_t R, uint32_t RS,
                 pp.pad_layout[R + p] = (uint32_t)min<uint64_t>(run, (uint64_t)pp.olim);
             }
         }
-        run += (uint64_t)cap[k] * (uint64_t)G;
+        run += SGX_PAD_CHUNK_MAJOR ? (uint64_t)cap[k] : (uint64_t)cap[k] * (uint64_t)G;
     }
-    if (g == 0 && tid == 0 && total > (uint64_t)pp.olim) atomicOr(err, PAD_OVERFLOW);
+    const uint64_t whole = SGX_PAD_CHUNK_MAJOR ? total * (uint64_t)G : total;
+    if (g == 0 && tid == 0 && whole > (uint64_t)pp.olim) atomicOr(err, PAD_OVERFLOW);
     __syncthreads();
 }
 
@@ -3755,7 +3763,11 @@ __global__ __launch_bounds__(256) void k_pad_finish(const uint32_t *__restrict__
     if (i < (int64_t)R * G) {
         const int p = (int)(i / G), g = (int)(i - (int64_t)p * G);
         const uint32_t cap = layout[p];
-        const uint32_t f = (uint32_t)min<uint64_t>((uint64_t)layout[R + p] + (uint64_t)g * cap, (uint64_t)olim);
+        // (pad_layout_starts' layout: chunk-major, a chunk's region = the sum of the capacities)
+        const uint64_t total = (uint64_t)layout[R + R - 1] + layout[R - 1];
+        const uint64_t at = SGX_PAD_CHUNK_MAJOR ? (uint64_t)g * total + layout[R + p]
+                                                : (uint64_t)layout[R + p] + (uint64_t)g * cap;
+        const uint32_t f = (uint32_t)min<uint64_t>(at, (uint64_t)olim);
         const uint32_t c = cnt[i] - f;  // K4 left the stream's end position
         fstart[i] = f;
         cnt[i] = c;
