@@ -3958,7 +3958,7 @@ __global__ __launch_bounds__(PAD_CAPS_THREADS) void k_pad_caps(const uint32_t *_
         cap[k] = 0;
         if (p < R) cap[k] = pad_cap_of(est[p], scale, a);
         s_cap[tid * PAD_CAPS_PER + k] = cap[k];
-        sum += (uint64_t)cap[k] * (uint64_t)G;
+        sum += SGX_PAD_CHUNK_MAJOR ? (uint64_t)cap[k] : (uint64_t)cap[k] * (uint64_t)G;
     }
     s_x[tid] = sum;
     __syncthreads();
@@ -3974,22 +3974,26 @@ __global__ __launch_bounds__(PAD_CAPS_THREADS) void k_pad_caps(const uint32_t *_
 #pragma unroll
     for (int k = 0; k < PAD_CAPS_PER; ++k) {
         s_base[tid * PAD_CAPS_PER + k] = run;
-        run += (uint64_t)cap[k] * (uint64_t)G;
+        run += SGX_PAD_CHUNK_MAJOR ? (uint64_t)cap[k] : (uint64_t)cap[k] * (uint64_t)G;
     }
     __syncthreads();
     if (blockIdx.x == 0) {
 #pragma unroll
         for (int k = 0; k < PAD_CAPS_PER; ++k)
             if (tid * PAD_CAPS_PER + k < R) pcap[tid * PAD_CAPS_PER + k] = cap[k];
-        if (tid == 0 && s_x[PAD_CAPS_THREADS - 1] > (uint64_t)olim) atomicOr(err_pad, PAD_OVERFLOW);
+        const uint64_t whole = SGX_PAD_CHUNK_MAJOR ? s_x[PAD_CAPS_THREADS - 1] * (uint64_t)G : s_x[PAD_CAPS_THREADS - 1];
+        if (tid == 0 && whole > (uint64_t)olim) atomicOr(err_pad, PAD_OVERFLOW);
     }
-    // this workgroup's partitions [p0, p1): fstart[p*G + g] = base[p] + g * cap[p] (coalesced)
+    // this workgroup's partitions [p0, p1): fstart[p*G + g] (coalesced) -- chunk-major
+    // (pad_layout_starts): g * total + base[p]; partition-major: base[p] + g * cap[p]
+    const uint64_t total = s_x[PAD_CAPS_THREADS - 1];
     const int per = (R + (int)gridDim.x - 1) / (int)gridDim.x;
     const int p0 = min(R, (int)blockIdx.x * per), p1 = min(R, p0 + per);
     for (int64_t i = (int64_t)p0 * G + tid; i < (int64_t)p1 * G; i += PAD_CAPS_THREADS) {
         const int p = (int)(i / G), g = (int)(i - (int64_t)p * G);
         const uint64_t base = s_base[p];
-        fstart[i] = (uint32_t)min<uint64_t>(base + (uint64_t)g * s_cap[p], (uint64_t)olim);
+        const uint64_t at = SGX_PAD_CHUNK_MAJOR ? (uint64_t)g * total + base : base + (uint64_t)g * s_cap[p];
+        fstart[i] = (uint32_t)min<uint64_t>(at, (uint64_t)olim);
     }
 }
 
