@@ -1228,6 +1228,14 @@ extern "C" int sgx_diag_wc_stamps(unsigned long long *out16, int reset) {
 #ifndef SGX_WC_NTLOAD
 #define SGX_WC_NTLOAD 1
 #endif
+// nontemporal line stores in the 16 B write-combining K4's drain (A/B: -DSGX_WC_NTSTORE=0)
+#ifndef SGX_WC_NTSTORE
+#define SGX_WC_NTSTORE 1
+#endif
+__device__ __forceinline__ void wc_store(const u32x4 &v, u32x4 *p) {
+    if constexpr (SGX_WC_NTSTORE) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
 
 // Sub-bin capacity of a partition from its sampled count: mu = est * chunk / sampled records
 // expected per chunk, cap = mu + PAD_SIGMAS * sqrt(a * mu + 16) + 8 (a = 1 + chunk / sampled:
@@ -1491,7 +1499,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                     ob = o2 ? (uint64_t)out2 : ob;
                 }
                 if (k0 >= LATE_K) wmask |= wr ? 1u << (k0 + q) : 0u;
-                else if (wr) __builtin_nontemporal_store(dk[k0 + q], (u32x4 *)ob + pos);
+                else if (wr) wc_store(dk[k0 + q], (u32x4 *)ob + pos);
                 dmask |= (live && keep) ? 1u << (k0 + q) : 0u;
             }
             WC_STAMP(10);  // drain: global stores issued
@@ -1506,7 +1514,7 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
                 // hipcc move dk[] to scratch memory)
                 uint64_t ob = (uint64_t)out;
                 if constexpr (KIND == KIND_HOT_SPLIT) ob = pidf(dk[k]) >= hot_cap ? (uint64_t)out2 : ob;
-                if ((wmask >> k) & 1u) __builtin_nontemporal_store(dk[k], (u32x4 *)ob + dpos[k]);
+                if ((wmask >> k) & 1u) wc_store(dk[k], (u32x4 *)ob + dpos[k]);
             }
             wmask = 0;
         }
