@@ -94,11 +94,14 @@ enum sgx_flags {
                                          contiguous map outputs, and a communicator keeps the
                                          map side two-pass; default: the direct peer gather
                                          (sgx_exchange) out of single-pass padded maps         */
-    SGX_FLAG_NO_OVERLAP_WRITES = 8192 /* keep every padded write of a calling thread on one
+    SGX_FLAG_NO_OVERLAP_WRITES = 8192, /* keep every padded write of a calling thread on one
                                          stream; default: consecutive writes alternate between
                                          two streams, so a write's sample and K4 start on the
                                          CUs the previous write's last K4 workgroups free (see
                                          sgx_set_overlap_writes)                              */
+    SGX_FLAG_TEST_P2P_UNAVAILABLE = 16384 /* testing: this rank reports the direct peer gather's
+                                         IPC mapping as unavailable; the exchange then falls
+                                         back on every rank (see sgx_exchange)               */
 };
 
 typedef struct sgx_config {

@@ -37,6 +37,7 @@ FLAG_NO_SEG_WINDOW = 1024
 FLAG_NO_DEFERRED_APPEND = 2048
 FLAG_NO_P2P_EXCHANGE = 4096
 FLAG_NO_OVERLAP_WRITES = 8192
+FLAG_TEST_P2P_UNAVAILABLE = 16384
 LAYOUT_CONTIGUOUS, LAYOUT_PADDED, LAYOUT_SERIALIZED_PADDED = 0, 1, 2
 PLACE_EVEN, PLACE_BYTES = 0, 1
 WRITER_SORT, WRITER_UNSAFE = 0, 1

@@ -203,7 +203,7 @@ extern "C" int sgx_create(const sgx_config *cfg, sgx_engine **out) {
     if (dev < 0 || dev >= ndev) return fail_msg(SGX_ERR_INVALID, "sgx_create: device %d of %d", dev, ndev);
     if (cfg && (cfg->hist_mode < SGX_HIST_ATOMIC || cfg->hist_mode > SGX_HIST_BALLOT ||
                 cfg->rank_mode < SGX_RANK_ORDERED || cfg->rank_mode > SGX_RANK_MATCH || cfg->flags < 0 ||
-                cfg->flags > 16383 || cfg->comm_timeout_ms < 0 || cfg->num_chunks < 0))
+                cfg->flags > 32767 || cfg->comm_timeout_ms < 0 || cfg->num_chunks < 0))
         return fail_msg(SGX_ERR_INVALID, "sgx_create: bad configuration");
     HIP_TRY(hipSetDevice(dev));
     hipDeviceProp_t prop;

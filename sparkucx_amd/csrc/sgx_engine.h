@@ -430,6 +430,9 @@ struct sgx_engine {
     };
     std::map<std::string, PeerMap> p2p_cache;  // key: rank, allocation serial, handle bytes
     uint64_t p2p_rounds = 0, p2p_gen = 0;
+    // the direct peer gather failed to map a peer's buffer on some rank: every later round
+    // moves contiguous pieces (RCCL send / recv, host all-to-all) and maps are written two-pass
+    std::atomic<bool> p2p_off{false};
     sgx::DevBuf p2p_word;
     sgx::DevBuf jump_dev;  // XORShiftRandom jump table (built once, read-only after)
     std::mutex jump_mu;

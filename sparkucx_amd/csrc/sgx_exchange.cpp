@@ -180,6 +180,11 @@ static void p2p_release(sgx_engine *e, bool all) {
 // round's event), with host collectives a host barrier after the gather.  No pack step and no
 // contiguous copy of a padded map: each map's published bytes leave it exactly once, sent
 // bytes = the blocks' lengths.
+// p2p_data's answer when some rank could not get or map a receive buffer's IPC handle: every
+// rank learns it from the same all-gather before anything was written, so every rank falls
+// back together (exchange_round)
+constexpr int P2P_UNAVAILABLE = 1 << 20;
+
 static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<LocalMap> &mine,
                     const std::vector<int32_t> &bounds, const std::vector<int64_t> &lens,
                     const std::vector<int32_t> &srcs, hipStream_t st) {
@@ -187,7 +192,9 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
     const size_t M = srcs.size();
     ++e->p2p_rounds;
     p2p_release(e, false);
-    // any rank's failure before the gather fails the round on every rank (status all-gather)
+    // any rank's failure before the gather fails the round on every rank (status all-gather);
+    // `refused` notes that the all-gather itself worked and some rank reported a failure
+    bool refused = false;
     auto agree = [&](int rc, const std::string &msg, const int64_t *extra, size_t nextra,
                      std::vector<int64_t> *all) -> int {
         std::vector<int64_t> mine_w(nextra + 1, 0);
@@ -197,6 +204,7 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
         SGX_TRY(allgather_i64(e, mine_w.data(), nextra + 1, tmp.data()));
         for (int32_t j = 0; j < P; ++j)
             if (tmp[(size_t)j * (nextra + 1)] != SGX_OK) {
+                refused = true;
                 if (j == me) return fail_msg(rc, "%s (every rank fails this exchange)", msg.c_str());
                 return fail_msg(SGX_ERR_STATE, "exchange of shuffle %d failed on rank %d: every rank fails it", s.id, j);
             }
@@ -210,7 +218,9 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
     std::string local_msg;
     if (P > 1) {
         int64_t hw[HW] = {0};
-        const hipError_t he = rd.ipc_valid ? hipSuccess : hipIpcGetMemHandle(&rd.ipc, rd.data.p);
+        const hipError_t he = (e->flags & SGX_FLAG_TEST_P2P_UNAVAILABLE) ? hipErrorNotSupported
+                              : rd.ipc_valid                             ? hipSuccess
+                                                                         : hipIpcGetMemHandle(&rd.ipc, rd.data.p);
         if (he == hipSuccess && !rd.ipc_valid) rd.ipc_gen = ++e->p2p_gen;
         rd.ipc_valid = he == hipSuccess;
         if (he != hipSuccess) {
@@ -225,7 +235,8 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
             std::memcpy(hw, &rd.ipc, sizeof(rd.ipc));
             hw[HW - 1] = (int64_t)rd.ipc_gen;
         }
-        SGX_TRY(agree(local_rc, local_msg, hw, HW, &all_h));
+        const int arc = agree(local_rc, local_msg, hw, HW, &all_h);
+        if (arc != SGX_OK) return refused ? P2P_UNAVAILABLE : arc;
     }
     // (b) where my contribution starts in every rank's receive buffer: [source][its maps][d's
     //     reducers], i.e. after the blocks of d's reducers of every map of lower ranks
@@ -317,7 +328,7 @@ static int p2p_data(sgx_engine *e, Shuffle &s, Round &rd, const std::vector<Loca
     };
     if (P > 1) {  // every rank has mapped the buffers it writes to (or the round fails everywhere)
         const int arc = agree(local_rc, local_msg, nullptr, 0, nullptr);
-        if (arc != SGX_OK) return arc;
+        if (arc != SGX_OK) return refused ? P2P_UNAVAILABLE : arc;
     }
     auto launch = [&]() -> int {
         for (auto &lm : mine) HIP_TRY(hipStreamWaitEvent(st, lm.m->done.ev, 0));
@@ -395,7 +406,7 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
     const int32_t P = e->nranks, R = s->R;
     // the direct peer gather moves the blocks (a padded map's from its fragments); RCCL's
     // send / recv and the host all-to-all move contiguous byte ranges
-    const bool p2p = (e->comm || e->host_comm) && !(e->flags & SGX_FLAG_NO_P2P_EXCHANGE);
+    const bool p2p = (e->comm || e->host_comm) && !(e->flags & SGX_FLAG_NO_P2P_EXCHANGE) && !e->p2p_off.load();
     for (auto &lm : mine) {
         if (local_rc != SGX_OK) break;
         std::lock_guard<std::mutex> lk(lm.m->mu);
@@ -576,7 +587,17 @@ static int exchange_round(sgx_engine *e, Ctx *c, const std::shared_ptr<Shuffle> 
         SGX_TRY(rd->data.ensure((size_t)std::max<int64_t>(total_recv, 16)));
         if (rd->data.p != was) rd->ipc_valid = false;
         HIP_TRY(hipEventRecord(a2, st));
-        SGX_TRY(p2p_data(e, *s, *rd, mine, bounds, lens, srcs, st));
+        const int prc = p2p_data(e, *s, *rd, mine, bounds, lens, srcs, st);
+        if (prc == P2P_UNAVAILABLE) {
+            // nothing has moved on any rank: the round again over contiguous pieces, and the
+            // engine's later maps two-pass (use_padded)
+            if (!e->p2p_off.exchange(true))
+                std::fprintf(stderr, "sgx: rank %d: direct peer gather unavailable (%s); exchanging contiguous pieces\n",
+                             e->rank, sgx_last_error());
+            e->release_events({a0, a1, a2, a3});
+            return exchange_round(e, c, s, std::move(mine));
+        }
+        SGX_TRY(prc);
     } else {
         SGX_TRY(rd->data.ensure((size_t)std::max<int64_t>(total_recv, 16)));
         for (auto &lm : mine) HIP_TRY(hipStreamWaitEvent(st, lm.m->done.ev, 0));

@@ -233,10 +233,11 @@ static bool use_padded(sgx_engine *e, const Shuffle &s, const void *in, int64_t 
     if (e->flags & SGX_FLAG_NO_PADDED_MAP) return false;
     if (e->rank_mode != SGX_RANK_ORDERED || !e->lds_order_ok || e->sc_waves || e->sc_items) return false;
     // a communicator sends padded maps by the direct peer gather, straight from their fragments
-    // (sgx_exchange.cpp p2p_data); without it (SGX_FLAG_NO_P2P_EXCHANGE) sends are contiguous
-    // byte ranges and the write stays two-pass
+    // (sgx_exchange.cpp p2p_data); without it (SGX_FLAG_NO_P2P_EXCHANGE, or after the peer
+    // gather could not map a peer's buffer) sends are contiguous byte ranges and the write
+    // stays two-pass
     const bool comm = e->nranks > 1 || e->comm || e->host_comm;
-    if ((comm && (e->flags & SGX_FLAG_NO_P2P_EXCHANGE)) || n < e->pad_min || s.pad_failed.load()) return false;
+    if ((comm && ((e->flags & SGX_FLAG_NO_P2P_EXCHANGE) || e->p2p_off.load())) || n < e->pad_min || s.pad_failed.load()) return false;
     if (s.rb == 16 && s.kind == SGX_PART_HASH && s.R > 1024)  // the padded two-level split
         return split_ok(e, s.R);
     if (s.rb == 16 && s.kind == SGX_PART_HASH)
