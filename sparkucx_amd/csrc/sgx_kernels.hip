@@ -2979,6 +2979,10 @@ constexpr int BS_THREADS = 512;
 #ifndef SGX_BS_NT
 #define SGX_BS_NT 1
 #endif
+// 16 B records per bucket-sort tile (A/B builds: -DSGX_BS_TILE16=1280, three workgroups per CU)
+#ifndef SGX_BS_TILE16
+#define SGX_BS_TILE16 2048
+#endif
 #ifndef BS_UNROLL
 #define BS_UNROLL 8  // keys compared per step of the rank loop (independent LDS loads; 8 vs 4: sorted 1 GiB 3.67 -> 3.62 ms, profiles/r03_bucket_unroll_ab.jsonl)
 #endif
@@ -3248,7 +3252,7 @@ hipError_t launch_bucket_sort(const void *in, void *out, int64_t n, int rb, cons
     if (n <= 0) return hipSuccess;
     if (rb == 16) {
         // CAP = 2560 (sub-bins: 2304, two workgroups per CU): the key array stays 8-byte aligned
-        constexpr int T = 2048, H = SGX_BS_SUBBIN ? 255 : 511;
+        constexpr int T = SGX_BS_TILE16, H = SGX_BS_SUBBIN ? 255 : 511;
         const size_t lds = bucket_sort_lds<16, T, H>();
         (void)hipFuncSetAttribute((const void *)k_bucket_sort<16, T, H>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                   (int)lds);
