@@ -579,6 +579,10 @@ def main():
                                   "traffic": side_pmc.get("hbm_bytes_per_write"),
                                   "traffic_over_algorithmic": side_pmc.get("ratio")},
             "stages_ms_per_step": {k: round(v / max(1, st.count[k]), 4) for k, v in st.ms.items() if st.count[k]},
+            "stages_note": ("HIP-event intervals per stage on the stage's own stream; with overlapping writes a "
+                            "stage's interval includes its wait for the CUs the previous write's K4 holds (hist = the "
+                            "pad sample), so they do not add up to ms_per_step (DESIGN.md §6.1)")
+            if padded and not args.no_overlap_writes else "HIP-event intervals per stage",
             # the HBM bytes the map side's design must move per record -- two-pass: 3 x record
             # bytes (the histogram reads the whole record for its 8 B key; K4 reads + writes it);
             # padded: 2 x record bytes + the sampled lines (one 128 B line in 128) -- as a
