@@ -1228,6 +1228,11 @@ extern "C" int sgx_diag_wc_stamps(unsigned long long *out16, int reset) {
 #ifndef SGX_WC_NTLOAD
 #define SGX_WC_NTLOAD 1
 #endif
+// chunk <- workgroup mapping of the 16 B write-combining K4 (A/B: -DSGX_WC_XCD_REMAP=1, one
+// contiguous run of chunks per XCD)
+#ifndef SGX_WC_XCD_REMAP
+#define SGX_WC_XCD_REMAP 0
+#endif
 // nontemporal line stores in the 16 B write-combining K4's drain (A/B: -DSGX_WC_NTSTORE=0)
 #ifndef SGX_WC_NTSTORE
 #define SGX_WC_NTSTORE 1
@@ -1380,6 +1385,12 @@ __global__ __launch_bounds__(WAVES * 64, 1) void k_scatter16_wc(const u32x4 *__r
     uint32_t fpre = 0xFFFFFFFFu, fdl = 0;
     {
     int g = blockIdx.x;
+#if SGX_WC_XCD_REMAP
+    // workgroup b runs on XCD b % 8: give each XCD a contiguous run of chunks (and, chunk-major,
+    // of output regions)
+    if constexpr (!SEG)
+        if ((G & 7) == 0 && (int)gridDim.x == G) g = (int)(blockIdx.x & 7u) * (G >> 3) + (int)(blockIdx.x >> 3);
+#endif
     int64_t begin = (int64_t)g * chunk, end = min(n, begin + chunk), obase = 0;
     if constexpr (FRAGS) {
         const int kg = (int)blockIdx.x / G;
